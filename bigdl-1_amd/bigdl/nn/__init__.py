@@ -1,0 +1,9 @@
+"""bigdl.nn — Torch-style modules with explicit forward/backward (``DL/nn``)."""
+from .abstractnn import (AbstractModule, TensorModule, AutogradModule, AbstractCriterion, AutogradCriterion,
+                         Activity, LayerException, FlatParameters)
+from .containers import Container, Sequential, Concat, ConcatTable, ParallelTable, MapTable, Bottle
+from .graph import Graph, StaticGraph, Model, Input, ModuleNode, to_graph
+from .layers import *  # noqa: F401,F403
+from .criterion import *  # noqa: F401,F403
+from .initialization_method import *  # noqa: F401,F403
+Module = AbstractModule

@@ -1,0 +1,11 @@
+"""Layer library, grouped by family (see each module's docstring for the reference citations)."""
+from .conv import *  # noqa: F401,F403
+from .normalization import *  # noqa: F401,F403
+from .activation import *  # noqa: F401,F403
+from .linear import *  # noqa: F401,F403
+from .pooling import *  # noqa: F401,F403
+from .shape import *  # noqa: F401,F403
+from .table_ops import *  # noqa: F401,F403
+from .math_ops import *  # noqa: F401,F403
+from .dropout import *  # noqa: F401,F403
+from .embedding import *  # noqa: F401,F403

@@ -1,0 +1,497 @@
+"""Convolution family.
+
+* ``SpatialConvolution`` — ``DL/nn/SpatialConvolution.scala`` (weight 5-D
+  ``(nGroup, out/g, in/g, kH, kW)`` at 93-98; ``padW=padH=-1`` = TensorFlow SAME padding via
+  ``Utils.getSAMEOutSizeAndPadding``; default init U(±1/√(kW·kH·nIn)) at 150-154).
+  The reference runs im2col + MKL GEMM per sample; here the whole batch is one NHWC implicit-GEMM
+  launch on MFMA (``bigdl/ops/csrc/conv_igemm.hip``).  The weight is stored physically as
+  ``(g, out/g, kH, kW, in/g)`` = KRSC so the kernel's B operand is K-contiguous; the logical
+  tensor the user sees keeps BigDL's shape.
+* ``SpatialShareConvolution`` (``:312``) — buffer sharing is the allocator's job on HIP; kept as a
+  class for API/serialization compatibility.
+* Dilated / Full(transposed) / Separable / ConvolutionMap / Temporal / Volumetric / LocallyConnected.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ...utils.engine import Engine
+from ..abstractnn import TensorModule, AutogradModule
+from ..initialization_method import RandomUniform, Zeros, VariableFormats
+
+
+def same_padding(in_h, in_w, stride_h, stride_w, k_h, k_w, dil_h=1, dil_w=1):
+    """``Utils.getSAMEOutSizeAndPadding``: returns (padTop, padBottom, padLeft, padRight, outH, outW)."""
+    out_h = math.ceil(in_h / stride_h)
+    out_w = math.ceil(in_w / stride_w)
+    ekh = (k_h - 1) * dil_h + 1
+    ekw = (k_w - 1) * dil_w + 1
+    ph = max((out_h - 1) * stride_h + ekh - in_h, 0)
+    pw = max((out_w - 1) * stride_w + ekw - in_w, 0)
+    return ph // 2, ph - ph // 2, pw // 2, pw - pw // 2, out_h, out_w
+
+
+def to_device_layout(x: torch.Tensor) -> torch.Tensor:
+    """Device activations are NHWC (channels_last) in the compute dtype."""
+    if x.is_cuda and x.dim() == 4:
+        dt = Engine.compute_dtype()
+        if x.dtype != dt and x.is_floating_point():
+            x = x.to(dt)
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+    return x
+
+
+class SpatialConvolution(TensorModule):
+    def __init__(self, n_input_plane, n_output_plane, kernel_w, kernel_h, stride_w=1, stride_h=1, pad_w=0,
+                 pad_h=0, n_group=1, propagate_back=True, wRegularizer=None, bRegularizer=None, init_weight=None,
+                 init_bias=None, init_grad_weight=None, init_grad_bias=None, with_bias=True, data_format="NCHW",
+                 bigdl_type="float"):
+        super().__init__()
+        if n_output_plane % n_group != 0 or n_input_plane % n_group != 0:
+            raise ValueError(f"channels must be multiples of group: in {n_input_plane} out {n_output_plane} g {n_group}")
+        if not ((pad_w >= 0 and pad_h >= 0) or (pad_w == -1 and pad_h == -1)):
+            raise ValueError(f"Illegal padding configuration (padW: {pad_w}, padH: {pad_h})")
+        self.nInputPlane, self.nOutputPlane = n_input_plane, n_output_plane
+        self.kernelW, self.kernelH = kernel_w, kernel_h
+        self.strideW, self.strideH = stride_w, stride_h
+        self.padW, self.padH = pad_w, pad_h
+        self.nGroup = n_group
+        self.propagateBack = propagate_back
+        self.withBias = with_bias
+        self.format = data_format
+        self.dilationW = self.dilationH = 1
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        g = n_group
+        shape5 = (g, n_output_plane // g, n_input_plane // g, kernel_h, kernel_w)
+        phys = (g, n_output_plane // g, kernel_h, kernel_w, n_input_plane // g)
+        w = init_weight if init_weight is not None else torch.zeros(shape5)
+        self.register_parameter("weight", torch.as_tensor(w, dtype=torch.float32).reshape(shape5), "gradWeight",
+                                layout=(phys, (0, 1, 4, 2, 3)))
+        if with_bias:
+            b = init_bias if init_bias is not None else torch.zeros(n_output_plane)
+            self.register_parameter("bias", torch.as_tensor(b, dtype=torch.float32).reshape(n_output_plane), "gradBias")
+        else:
+            self.bias = None
+            self.gradBias = None
+        self._has_init_w = init_weight is not None
+        self._has_init_b = init_bias is not None
+        stdv = 1.0 / math.sqrt(kernel_w * kernel_h * n_input_plane)
+        self._init_weight_method = RandomUniform(-stdv, stdv)
+        self._init_bias_method = RandomUniform(-stdv, stdv) if with_bias else Zeros()
+        self.reset()
+
+    def reset(self):
+        if not self._has_init_w:
+            self._init_weight_method.init(self.weight, VariableFormats.GP_OUT_IN_KW_KH)
+        if self.withBias and not self._has_init_b:
+            self._init_bias_method.init(self.bias, VariableFormats.ONE_D)
+        self.zeroGradParameters()
+        return self
+
+    # -- geometry ----------------------------------------------------------------------------
+    def _pads(self, x):
+        H, W = x.shape[-2], x.shape[-1]
+        if self.padW == -1 and self.padH == -1:
+            pt, pb, pl, pr, _, _ = same_padding(H, W, self.strideH, self.strideW, self.kernelH, self.kernelW,
+                                                self.dilationH, self.dilationW)
+            return pt, pb, pl, pr
+        return self.padH, self.padH, self.padW, self.padW
+
+    def _w4(self, w):
+        """(O, I/g, kH, kW) view of a logical 5-D weight without copying when it is KRSC."""
+        g, og, ig, kh, kw = w.shape
+        krsc = w.permute(0, 1, 3, 4, 2)
+        if krsc.is_contiguous():
+            return krsc.reshape(g * og, kh, kw, ig).permute(0, 3, 1, 2)
+        return w.reshape(g * og, ig, kh, kw)
+
+    def _prep(self, input):
+        x = input
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        if self.format == "NHWC":
+            x = x.permute(0, 3, 1, 2)
+        x = to_device_layout(x)
+        pt, pb, pl, pr = self._pads(x)
+        if pt != pb or pl != pr:
+            x = F.pad(x, (pl, pr, pt, pb))
+            pad = (0, 0)
+        else:
+            pad = (pt, pl)
+        return x, pad, batched, (pt, pb, pl, pr)
+
+    def updateOutput(self, input):
+        x, pad, batched, _ = self._prep(input)
+        w4 = self._w4(self.cw("weight"))
+        b = self.cw("bias") if self.withBias else None
+        y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
+                               self.nGroup)
+        if self.format == "NHWC":
+            y = y.permute(0, 2, 3, 1)
+        return y if batched else y.squeeze(0)
+
+    def _backward(self, input, gradOutput, need_input, acc):
+        x, pad, batched, pads = self._prep(input)
+        gy = gradOutput if batched else gradOutput.unsqueeze(0)
+        if self.format == "NHWC":
+            gy = gy.permute(0, 3, 1, 2)
+        gy = to_device_layout(gy)
+        w4 = self._w4(self.cw("weight"))
+        gw = self._w4(self.gradWeight) if acc else None
+        same_scale = self.scale_b == self.scale_w
+        gb = self.gradBias if (acc and self.withBias and same_scale) else None
+        gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
+                                 self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0)
+        if acc and self.withBias and not same_scale and self.scale_b != 0:
+            self.gradBias.add_(gy.float().sum((0, 2, 3)), alpha=self.scale_b)
+        if need_input and gi is not None:
+            pt, pb, pl, pr = pads
+            if pt != pb or pl != pr:
+                gi = gi[:, :, pt:gi.shape[2] - pb, pl:gi.shape[3] - pr]
+            if self.format == "NHWC":
+                gi = gi.permute(0, 2, 3, 1)
+            if not batched:
+                gi = gi.squeeze(0)
+        return gi
+
+    def updateGradInput(self, input, gradOutput):
+        if not self.propagateBack:
+            self._gi_done = False
+            return torch.zeros_like(input) if isinstance(input, torch.Tensor) else None
+        # compute gradInput and (fused) parameter gradients in one pass; accGradParameters then
+        # only applies regularisers
+        gi = self._backward(input, gradOutput, True, True)
+        self._gi_done = True
+        return gi
+
+    def accGradParameters(self, input, gradOutput):
+        if not getattr(self, "_gi_done", False):
+            self._backward(input, gradOutput, False, True)
+        self._gi_done = False
+        if self.wRegularizer is not None and self.scale_w != 0:
+            self.wRegularizer.accRegularization(self.weight, self.gradWeight, self.scale_w)
+        if self.withBias and self.bRegularizer is not None and self.scale_b != 0:
+            self.bRegularizer.accRegularization(self.bias, self.gradBias, self.scale_b)
+
+    def backward(self, input, gradOutput):
+        return super().backward(input, gradOutput)
+
+    def __repr__(self):
+        return (f"SpatialConvolution[{self.get_name()}]({self.nInputPlane} -> {self.nOutputPlane}, "
+                f"{self.kernelW} x {self.kernelH}, {self.strideW}, {self.strideH}, {self.padW}, {self.padH})")
+
+
+class SpatialShareConvolution(SpatialConvolution):
+    """Same math as SpatialConvolution; the reference shares im2col buffers between layers
+    (``SpatialShareConvolution.scala:312``) — implicit GEMM needs no im2col buffer at all."""
+
+
+class SpatialDilatedConvolution(SpatialConvolution):
+    def __init__(self, n_input_plane, n_output_plane, kw, kh, dw=1, dh=1, pad_w=0, pad_h=0, dilation_w=1,
+                 dilation_h=1, wRegularizer=None, bRegularizer=None, bigdl_type="float"):
+        super().__init__(n_input_plane, n_output_plane, kw, kh, dw, dh, pad_w, pad_h, 1, True, wRegularizer,
+                         bRegularizer)
+        self.dilationW, self.dilationH = dilation_w, dilation_h
+
+
+class SpatialFullConvolution(AutogradModule):
+    """Transposed convolution (``SpatialFullConvolution.scala``); weight (g, in/g, out/g, kH, kW)."""
+
+    def __init__(self, n_input_plane, n_output_plane, kw, kh, dw=1, dh=1, pad_w=0, pad_h=0, adj_w=0, adj_h=0,
+                 n_group=1, no_bias=False, wRegularizer=None, bRegularizer=None, bigdl_type="float"):
+        super().__init__()
+        self.nInputPlane, self.nOutputPlane = n_input_plane, n_output_plane
+        self.kW, self.kH, self.dW, self.dH = kw, kh, dw, dh
+        self.padW, self.padH, self.adjW, self.adjH = pad_w, pad_h, adj_w, adj_h
+        self.nGroup, self.noBias = n_group, no_bias
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.register_parameter("weight", torch.zeros(n_group, n_input_plane // n_group, n_output_plane // n_group, kh, kw))
+        if not no_bias:
+            self.register_parameter("bias", torch.zeros(n_output_plane))
+        stdv = 1.0 / math.sqrt(kw * kh * n_input_plane)
+        self._init_weight_method = RandomUniform(-stdv, stdv)
+        self._init_bias_method = RandomUniform(-stdv, stdv)
+        self.reset()
+
+    def reset(self):
+        self._init_weight_method.init(self.weight, VariableFormats.GP_IN_OUT_KW_KH)
+        if not self.noBias:
+            self._init_bias_method.init(self.bias, VariableFormats.ONE_D)
+        return self
+
+    def _forward(self, x):
+        if isinstance(x, torch.Tensor):
+            inp = x
+            adj = (self.adjH, self.adjW)
+        else:  # Table(input, sizeTensor) variant
+            inp = x[1]
+            target = x[2]
+            oh = (inp.shape[-2] - 1) * self.dH - 2 * self.padH + self.kH
+            ow = (inp.shape[-1] - 1) * self.dW - 2 * self.padW + self.kW
+            adj = (target.shape[-2] - oh, target.shape[-1] - ow)
+        batched = inp.dim() == 4
+        if not batched:
+            inp = inp.unsqueeze(0)
+        w = self.P("weight")
+        g = self.nGroup
+        w4 = w.reshape(g * w.shape[1], w.shape[2], self.kH, self.kW)
+        b = self.P("bias") if not self.noBias else None
+        y = F.conv_transpose2d(inp, w4.to(inp.dtype), None if b is None else b.to(inp.dtype), (self.dH, self.dW),
+                               (self.padH, self.padW), adj, g)
+        return y if batched else y.squeeze(0)
+
+
+class SpatialSeparableConvolution(AutogradModule):
+    """Depthwise (multiplier) + pointwise conv (``SpatialSeparableConvolution.scala``)."""
+
+    def __init__(self, n_input_channel, n_output_channel, depth_multiplier, kernel_w, kernel_h, stride_w=1,
+                 stride_h=1, pad_w=0, pad_h=0, with_bias=True, data_format="NCHW", w_regularizer=None,
+                 b_regularizer=None, p_regularizer=None, bigdl_type="float"):
+        super().__init__()
+        self.nIn, self.nOut, self.mult = n_input_channel, n_output_channel, depth_multiplier
+        self.kW, self.kH, self.sW, self.sH, self.pW, self.pH = kernel_w, kernel_h, stride_w, stride_h, pad_w, pad_h
+        self.withBias, self.format = with_bias, data_format
+        self.register_parameter("depthWeight", torch.zeros(n_input_channel * depth_multiplier, 1, kernel_h, kernel_w),
+                                "depthGradWeight")
+        self.register_parameter("pointWeight", torch.zeros(n_output_channel, n_input_channel * depth_multiplier, 1, 1),
+                                "pointGradWeight")
+        if with_bias:
+            self.register_parameter("bias", torch.zeros(n_output_channel))
+        self.reset()
+
+    def reset(self):
+        RandomUniform().init(self.depthWeight, VariableFormats.OUT_IN_KW_KH)
+        RandomUniform().init(self.pointWeight, VariableFormats.OUT_IN_KW_KH)
+        if self.withBias:
+            Zeros().init(self.bias)
+        return self
+
+    def _forward(self, x):
+        nhwc = self.format == "NHWC"
+        if nhwc:
+            x = x.permute(0, 3, 1, 2)
+        pad = (self.pH, self.pW)
+        if self.pW == -1:
+            pt, pb, pl, pr, _, _ = same_padding(x.shape[2], x.shape[3], self.sH, self.sW, self.kH, self.kW)
+            x = F.pad(x, (pl, pr, pt, pb))
+            pad = (0, 0)
+        y = F.conv2d(x, self.P("depthWeight").to(x.dtype), None, (self.sH, self.sW), pad, 1, self.nIn)
+        y = F.conv2d(y, self.P("pointWeight").to(x.dtype), self.P("bias").to(x.dtype) if self.withBias else None)
+        return y.permute(0, 2, 3, 1) if nhwc else y
+
+
+class SpatialConvolutionMap(AutogradModule):
+    """Convolution with an explicit input→output connection table (``SpatialConvolutionMap.scala``)."""
+
+    def __init__(self, conn_table, kw, kh, dw=1, dh=1, pad_w=0, pad_h=0, wRegularizer=None, bRegularizer=None,
+                 bigdl_type="float"):
+        super().__init__()
+        ct = torch.as_tensor(conn_table).long()
+        self.connTable = ct
+        self.kW, self.kH, self.dW, self.dH, self.padW, self.padH = kw, kh, dw, dh, pad_w, pad_h
+        self.nInputPlane = int(ct[:, 0].max())
+        self.nOutputPlane = int(ct[:, 1].max())
+        self.register_parameter("weight", torch.zeros(ct.shape[0], kh, kw))
+        self.register_parameter("bias", torch.zeros(self.nOutputPlane))
+        self.reset()
+
+    @staticmethod
+    def full(nin, nout):
+        return torch.tensor([[i + 1, o + 1] for o in range(nout) for i in range(nin)])
+
+    @staticmethod
+    def oneToOne(n):
+        return torch.tensor([[i + 1, i + 1] for i in range(n)])
+
+    @staticmethod
+    def random(nin, nout, nto):
+        rows = []
+        for o in range(nout):
+            perm = torch.randperm(nin)[:nto]
+            rows += [[int(i) + 1, o + 1] for i in perm]
+        return torch.tensor(rows)
+
+    def reset(self):
+        ninp = {}
+        for i, o in self.connTable.tolist():
+            ninp[o] = ninp.get(o, 0) + 1
+        stdv = 1.0 / math.sqrt(self.kW * self.kH * max(ninp.values()))
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+        return self
+
+    def _forward(self, x):
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        dense = torch.zeros(self.nOutputPlane, self.nInputPlane, self.kH, self.kW, dtype=x.dtype, device=x.device)
+        w = self.P("weight").to(x.dtype)
+        idx_o = self.connTable[:, 1].to(x.device) - 1
+        idx_i = self.connTable[:, 0].to(x.device) - 1
+        dense = dense.index_put((idx_o, idx_i), w, accumulate=True)
+        y = F.conv2d(x, dense, self.P("bias").to(x.dtype), (self.dH, self.dW), (self.padH, self.padW))
+        return y if batched else y.squeeze(0)
+
+
+class TemporalConvolution(AutogradModule):
+    """1-D conv over (batch, frames, features) (``TemporalConvolution.scala``): weight (out, in·kW)."""
+
+    def __init__(self, input_frame_size, output_frame_size, kernel_w, stride_w=1, propagate_back=True,
+                 weight_regularizer=None, bias_regularizer=None, init_weight=None, init_bias=None,
+                 init_grad_weight=None, init_grad_bias=None, bigdl_type="float"):
+        super().__init__()
+        self.inputFrameSize, self.outputFrameSize = input_frame_size, output_frame_size
+        self.kernelW, self.strideW = kernel_w, stride_w
+        self.wRegularizer, self.bRegularizer = weight_regularizer, bias_regularizer
+        self.register_parameter("weight", torch.zeros(output_frame_size, input_frame_size * kernel_w))
+        self.register_parameter("bias", torch.zeros(output_frame_size))
+        stdv = 1.0 / math.sqrt(kernel_w * input_frame_size)
+        if init_weight is not None:
+            self.weight.copy_(torch.as_tensor(init_weight).reshape(self.weight.shape))
+        else:
+            RandomUniform(-stdv, stdv).init(self.weight)
+        if init_bias is not None:
+            self.bias.copy_(torch.as_tensor(init_bias).reshape(self.bias.shape))
+        else:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def _forward(self, x):
+        batched = x.dim() == 3
+        if not batched:
+            x = x.unsqueeze(0)
+        w = self.P("weight").to(x.dtype).view(self.outputFrameSize, self.kernelW, self.inputFrameSize).permute(0, 2, 1)
+        y = F.conv1d(x.transpose(1, 2), w, self.P("bias").to(x.dtype), self.strideW).transpose(1, 2)
+        return y if batched else y.squeeze(0)
+
+
+class VolumetricConvolution(AutogradModule):
+    """3-D conv (``VolumetricConvolution.scala``): weight (out, in, kT, kH, kW)."""
+
+    def __init__(self, n_input_plane, n_output_plane, k_t, k_w, k_h, d_t=1, d_w=1, d_h=1, pad_t=0, pad_w=0,
+                 pad_h=0, with_bias=True, wRegularizer=None, bRegularizer=None, bigdl_type="float"):
+        super().__init__()
+        self.nInputPlane, self.nOutputPlane = n_input_plane, n_output_plane
+        self.k = (k_t, k_h, k_w)
+        self.d = (d_t, d_h, d_w)
+        self.p = (pad_t, pad_h, pad_w)
+        self.withBias = with_bias
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.register_parameter("weight", torch.zeros(n_output_plane, n_input_plane, k_t, k_h, k_w))
+        if with_bias:
+            self.register_parameter("bias", torch.zeros(n_output_plane))
+        stdv = 1.0 / math.sqrt(k_t * k_w * k_h * n_input_plane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if with_bias:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def _forward(self, x):
+        batched = x.dim() == 5
+        if not batched:
+            x = x.unsqueeze(0)
+        pad = self.p
+        if self.p[1] == -1:
+            pads = []
+            for dim, k, s in zip(x.shape[2:], self.k, self.d):
+                o = math.ceil(dim / s)
+                tot = max((o - 1) * s + k - dim, 0)
+                pads.append((tot // 2, tot - tot // 2))
+            x = F.pad(x, (pads[2][0], pads[2][1], pads[1][0], pads[1][1], pads[0][0], pads[0][1]))
+            pad = (0, 0, 0)
+        y = F.conv3d(x, self.P("weight").to(x.dtype), self.P("bias").to(x.dtype) if self.withBias else None, self.d,
+                     pad)
+        return y if batched else y.squeeze(0)
+
+
+class VolumetricFullConvolution(AutogradModule):
+    def __init__(self, n_input_plane, n_output_plane, kt, kw, kh, dt=1, dw=1, dh=1, pad_t=0, pad_w=0, pad_h=0,
+                 adj_t=0, adj_w=0, adj_h=0, n_group=1, no_bias=False, wRegularizer=None, bRegularizer=None,
+                 bigdl_type="float"):
+        super().__init__()
+        self.k, self.d, self.p, self.adj = (kt, kh, kw), (dt, dh, dw), (pad_t, pad_h, pad_w), (adj_t, adj_h, adj_w)
+        self.nGroup, self.noBias = n_group, no_bias
+        self.register_parameter("weight", torch.zeros(n_group, n_input_plane // n_group, n_output_plane // n_group,
+                                                      kt, kh, kw))
+        if not no_bias:
+            self.register_parameter("bias", torch.zeros(n_output_plane))
+        stdv = 1.0 / math.sqrt(kt * kw * kh * n_input_plane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if not no_bias:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def _forward(self, x):
+        batched = x.dim() == 5
+        if not batched:
+            x = x.unsqueeze(0)
+        w = self.P("weight")
+        w5 = w.reshape(w.shape[0] * w.shape[1], w.shape[2], *self.k)
+        y = F.conv_transpose3d(x, w5.to(x.dtype), None if self.noBias else self.P("bias").to(x.dtype), self.d,
+                               self.p, self.adj, self.nGroup)
+        return y if batched else y.squeeze(0)
+
+
+class LocallyConnected2D(AutogradModule):
+    """Unshared-weight 2-D conv (``LocallyConnected2D.scala``)."""
+
+    def __init__(self, n_input_plane, input_width, input_height, n_output_plane, kernel_w, kernel_h, stride_w=1,
+                 stride_h=1, pad_w=0, pad_h=0, propagate_back=True, wRegularizer=None, bRegularizer=None,
+                 init_weight=None, init_bias=None, init_grad_weight=None, init_grad_bias=None, with_bias=True,
+                 data_format="NCHW", bigdl_type="float"):
+        super().__init__()
+        self.nIn, self.nOut = n_input_plane, n_output_plane
+        self.kW, self.kH, self.sW, self.sH, self.pW, self.pH = kernel_w, kernel_h, stride_w, stride_h, pad_w, pad_h
+        self.oH = (input_height + 2 * pad_h - kernel_h) // stride_h + 1
+        self.oW = (input_width + 2 * pad_w - kernel_w) // stride_w + 1
+        self.withBias, self.format = with_bias, data_format
+        L = self.oH * self.oW
+        self.register_parameter("weight", torch.zeros(L, n_output_plane, n_input_plane * kernel_h * kernel_w))
+        if with_bias:
+            self.register_parameter("bias", torch.zeros(L, n_output_plane))
+        stdv = 1.0 / math.sqrt(kernel_w * kernel_h * n_input_plane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if with_bias:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def _forward(self, x):
+        nhwc = self.format == "NHWC"
+        if nhwc:
+            x = x.permute(0, 3, 1, 2)
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        cols = F.unfold(x, (self.kH, self.kW), padding=(self.pH, self.pW), stride=(self.sH, self.sW))  # N, CKK, L
+        y = torch.einsum("ncl,loc->nol", cols, self.P("weight").to(x.dtype))
+        if self.withBias:
+            y = y + self.P("bias").to(x.dtype).t().unsqueeze(0)
+        y = y.reshape(x.shape[0], self.nOut, self.oH, self.oW)
+        if not batched:
+            y = y.squeeze(0)
+        return y.permute(0, 2, 3, 1) if nhwc else y
+
+
+class LocallyConnected1D(AutogradModule):
+    def __init__(self, n_input_frame, input_frame_size, output_frame_size, kernel_w, stride_w=1,
+                 propagate_back=True, weight_regularizer=None, bias_regularizer=None, init_weight=None,
+                 init_bias=None, init_grad_weight=None, init_grad_bias=None, bigdl_type="float"):
+        super().__init__()
+        self.nFrame, self.inSize, self.outSize, self.kW, self.sW = n_input_frame, input_frame_size, output_frame_size, kernel_w, stride_w
+        self.nOutFrame = (n_input_frame - kernel_w) // stride_w + 1
+        self.register_parameter("weight", torch.zeros(self.nOutFrame, output_frame_size, input_frame_size * kernel_w))
+        self.register_parameter("bias", torch.zeros(self.nOutFrame, output_frame_size))
+        stdv = 1.0 / math.sqrt(kernel_w * input_frame_size)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+
+    def _forward(self, x):
+        batched = x.dim() == 3
+        if not batched:
+            x = x.unsqueeze(0)
+        win = x.unfold(1, self.kW, self.sW)  # N, L, F, kW
+        win = win.permute(0, 1, 3, 2).reshape(x.shape[0], self.nOutFrame, -1)
+        y = torch.einsum("nlc,loc->nlo", win, self.P("weight").to(x.dtype)) + self.P("bias").to(x.dtype)
+        return y if batched else y.squeeze(0)

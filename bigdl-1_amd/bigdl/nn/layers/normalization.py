@@ -1,0 +1,396 @@
+"""Normalisation layers.
+
+* ``BatchNormalization`` / ``SpatialBatchNormalization`` — ``DL/nn/BatchNormalization.scala``
+  (eps 1e-5, momentum 0.1, running stats ``runningMean``/``runningVar`` (variance, unbiased),
+  saved ``saveMean``/``saveStd`` (=1/√(var+eps)); default init γ~U(0,1), β=0 (:107-109)) and
+  ``SpatialBatchNormalization.scala`` (NCHW/NHWC; cross-replica sync via ``setParallism``).
+  Device path: NHWC two-stage Welford/one-pass statistics + apply kernels with optional fused
+  ReLU / residual add (K5/K7/K8/K9).
+* ``SpatialCrossMapLRN`` (``SpatialCrossMapLRN.scala:96-200``), ``SpatialWithinChannelLRN``,
+  ``LayerNormalization``, ``Normalize``, ``NormalizeScale``, ``SpatialSubtractive/Divisive/
+  ContrastiveNormalization``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ..abstractnn import TensorModule, AutogradModule
+from ..initialization_method import RandomUniform, Zeros, Ones, VariableFormats
+from .conv import to_device_layout
+
+
+class BatchNormalization(TensorModule):
+    def __init__(self, n_output, eps=1e-5, momentum=0.1, affine=True, init_weight=None, init_bias=None,
+                 init_grad_weight=None, init_grad_bias=None, bigdl_type="float"):
+        super().__init__()
+        if n_output <= 0:
+            raise ValueError("output feature map number must be greater than zero")
+        self.nOutput = n_output
+        self.eps = eps
+        self.momentum = momentum
+        self.affine = affine
+        self.register_buffer("runningMean", torch.zeros(n_output))
+        self.register_buffer("runningVar", torch.ones(n_output))
+        self.saveMean = torch.zeros(n_output)
+        self.saveStd = torch.zeros(n_output)
+        if affine:
+            self.register_parameter("weight", torch.zeros(n_output) if init_weight is None else
+                                    torch.as_tensor(init_weight, dtype=torch.float32).reshape(n_output))
+            self.register_parameter("bias", torch.zeros(n_output) if init_bias is None else
+                                    torch.as_tensor(init_bias, dtype=torch.float32).reshape(n_output))
+        else:
+            self.weight = self.bias = self.gradWeight = self.gradBias = None
+        self._has_init_w = init_weight is not None
+        self._has_init_b = init_bias is not None
+        self._init_weight_method = RandomUniform(0, 1)
+        self._init_bias_method = Zeros()
+        self._fused_relu = False
+        self._sync_group = None
+        self._sync = False
+        self.reset()
+
+    def reset(self):
+        if self.affine:
+            if not self._has_init_w:
+                self._init_weight_method.init(self.weight, VariableFormats.ONE_D)
+            if not self._has_init_b:
+                self._init_bias_method.init(self.bias, VariableFormats.ONE_D)
+        self.runningMean.zero_()
+        self.runningVar.fill_(1.0)
+        self.zeroGradParameters()
+        return self
+
+    # --- SyncBN (P6 / X11): reference setParallism registers cross-replica sums -------------
+    def setParallism(self, parallism: int):
+        """Compat: in the reference this syncs ``parallism`` replica threads; on HIP it enables
+        cross-rank SyncBN over the default process group."""
+        self._sync = parallism is not None and parallism > 1
+        return self
+
+    def set_sync_group(self, group=None, enabled: bool = True):
+        self._sync = enabled
+        self._sync_group = group
+        return self
+
+    def _to_nchw_like(self, x):
+        return x
+
+    def _shape_in(self, input):
+        """BN over dim 1 of (N, C) or (N, C, ...)."""
+        return input
+
+    def _sync_stats(self, x):
+        import torch.distributed as dist
+        C = x.shape[1]
+        dims = [d for d in range(x.dim()) if d != 1]
+        xf = x.float()
+        n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
+        s = torch.cat([xf.sum(dims), (xf * xf).sum(dims), n])
+        dist.all_reduce(s, group=self._sync_group)
+        cnt = s[-1]
+        mean = s[:C] / cnt
+        var = s[C:2 * C] / cnt - mean * mean
+        return mean, var.clamp_min(0), cnt
+
+    def updateOutput(self, input):
+        x = input
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        x = to_device_layout(x) if x.dim() == 4 else x
+        g = self.cw("weight", torch.float32) if self.affine else None
+        b = self.cw("bias", torch.float32) if self.affine else None
+        if self.train:
+            if self._sync and _dist_ready():
+                y, mean, invstd = self._sync_forward(x, g, b)
+            else:
+                y, mean, invstd = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
+                                                              self.momentum, self.eps, relu=self._fused_relu)
+            self.saveMean, self.saveStd = mean, invstd
+        else:
+            y = ops.batchnorm_forward_infer(x, g, b, self.runningMean, self.runningVar, self.eps,
+                                            relu=self._fused_relu)
+        return y.reshape(input.shape) if input.dim() == 1 else y
+
+    def _sync_forward(self, x, g, b):
+        mean, var, cnt = self._sync_stats(x)
+        invstd = torch.rsqrt(var + self.eps)
+        with torch.no_grad():
+            self.runningMean.mul_(1 - self.momentum).add_(mean, alpha=self.momentum)
+            self.runningVar.mul_(1 - self.momentum).add_(var * (cnt / (cnt - 1).clamp_min(1)), alpha=self.momentum)
+        shape = [1, x.shape[1]] + [1] * (x.dim() - 2)
+        y = (x.float() - mean.view(shape)) * invstd.view(shape)
+        if g is not None:
+            y = y * g.view(shape) + b.view(shape)
+        if self._fused_relu:
+            y = torch.relu(y)
+        return y.to(x.dtype), mean, invstd
+
+    def _bwd(self, input, gradOutput, need_input, acc):
+        x = input if input.dim() > 1 else input.unsqueeze(0)
+        gy = gradOutput if gradOutput.dim() > 1 else gradOutput.unsqueeze(0)
+        if x.dim() == 4:
+            x = to_device_layout(x)
+            gy = to_device_layout(gy)
+        y = self.output if self._fused_relu else None
+        if y is not None and y.dim() == 1:
+            y = y.unsqueeze(0)
+        g = self.cw("weight", torch.float32) if self.affine else None
+        if self._sync and _dist_ready() and self.train:
+            gi = self._sync_backward(x, gy, g, y, need_input, acc)
+        else:
+            same = self.scale_w == self.scale_b
+            gi = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=self._fused_relu,
+                                        need_input=need_input,
+                                        gg_acc=self.gradWeight if (acc and self.affine) else None,
+                                        gb_acc=self.gradBias if (acc and self.affine and same) else None,
+                                        scale=self.scale_w if acc else 0.0)
+            if acc and self.affine and not same and self.scale_b != 0:
+                gf = gy.float() * ((y > 0).float() if self._fused_relu else 1.0)
+                dims = [d for d in range(gf.dim()) if d != 1]
+                self.gradBias.add_(gf.sum(dims), alpha=self.scale_b)
+        if gi is not None and input.dim() == 1:
+            gi = gi.reshape(input.shape)
+        return gi
+
+    def _sync_backward(self, x, gy, g, y, need_input, acc):
+        import torch.distributed as dist
+        C = x.shape[1]
+        dims = [d for d in range(x.dim()) if d != 1]
+        shape = [1, C] + [1] * (x.dim() - 2)
+        gf = gy.float()
+        if self._fused_relu:
+            gf = gf * (y > 0).float()
+        xhat = (x.float() - self.saveMean.view(shape)) * self.saveStd.view(shape)
+        n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
+        s = torch.cat([gf.sum(dims), (gf * xhat).sum(dims), n])
+        local_db, local_dg = s[:C].clone(), s[C:2 * C].clone()
+        dist.all_reduce(s, group=self._sync_group)
+        db, dg, cnt = s[:C], s[C:2 * C], s[-1]
+        if acc and self.affine:
+            self.gradWeight.add_(local_dg, alpha=self.scale_w)
+            self.gradBias.add_(local_db, alpha=self.scale_b)
+        if not need_input:
+            return None
+        gam = g.view(shape) if g is not None else 1.0
+        gi = (gam * self.saveStd.view(shape) / cnt) * (cnt * gf - db.view(shape) - xhat * dg.view(shape))
+        return gi.to(x.dtype)
+
+    def updateGradInput(self, input, gradOutput):
+        gi = self._bwd(input, gradOutput, True, True)
+        self._gi_done = True
+        return gi
+
+    def accGradParameters(self, input, gradOutput):
+        if not getattr(self, "_gi_done", False):
+            self._bwd(input, gradOutput, False, True)
+        self._gi_done = False
+
+    def set_running_mean(self, v):
+        self.runningMean.copy_(torch.as_tensor(v))
+        return self
+
+    def set_running_std(self, v):
+        self.runningVar.copy_(torch.as_tensor(v))
+        return self
+
+    def __repr__(self):
+        return f"{type(self).__name__}[{self.get_name()}]({self.nOutput}, {self.eps}, {self.momentum}, {self.affine})"
+
+
+class SpatialBatchNormalization(BatchNormalization):
+    def __init__(self, n_output, eps=1e-5, momentum=0.1, affine=True, init_weight=None, init_bias=None,
+                 init_grad_weight=None, init_grad_bias=None, data_format="NCHW", bigdl_type="float"):
+        super().__init__(n_output, eps, momentum, affine, init_weight, init_bias, init_grad_weight, init_grad_bias)
+        self.dataFormat = data_format
+
+    def updateOutput(self, input):
+        if self.dataFormat == "NHWC":
+            y = super().updateOutput(input.permute(0, 3, 1, 2))
+            return y.permute(0, 2, 3, 1)
+        return super().updateOutput(input)
+
+    def updateGradInput(self, input, gradOutput):
+        if self.dataFormat == "NHWC":
+            saved = self.output
+            self.output = saved.permute(0, 3, 1, 2)
+            gi = super().updateGradInput(input.permute(0, 3, 1, 2), gradOutput.permute(0, 3, 1, 2))
+            self.output = saved
+            return gi.permute(0, 2, 3, 1)
+        return super().updateGradInput(input, gradOutput)
+
+    def accGradParameters(self, input, gradOutput):
+        if self.dataFormat == "NHWC":
+            if not getattr(self, "_gi_done", False):
+                saved = self.output
+                self.output = saved.permute(0, 3, 1, 2)
+                self._bwd(input.permute(0, 3, 1, 2), gradOutput.permute(0, 3, 1, 2), False, True)
+                self.output = saved
+            self._gi_done = False
+            return
+        super().accGradParameters(input, gradOutput)
+
+
+def _dist_ready():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+class SpatialCrossMapLRN(TensorModule):
+    """Cross-channel LRN: y = x / (k + α/size·Σ x²)^β (``SpatialCrossMapLRN.scala:96-200``)."""
+
+    def __init__(self, size=5, alpha=1.0, beta=0.75, k=1.0, data_format="NCHW", bigdl_type="float"):
+        super().__init__()
+        self.size, self.alpha, self.beta, self.k = size, alpha, beta, k
+        self.format = data_format
+
+    def _f(self, x):
+        nhwc = self.format == "NHWC"
+        if nhwc:
+            x = x.permute(0, 3, 1, 2)
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        y = ops.lrn_forward(x, self.size, self.alpha, self.beta, self.k)
+        if not batched:
+            y = y.squeeze(0)
+        return y.permute(0, 2, 3, 1) if nhwc else y
+
+    def updateOutput(self, input):
+        return self._f(input)
+
+    def updateGradInput(self, input, gradOutput):
+        x = input.detach().requires_grad_(True)
+        with torch.enable_grad():
+            y = F.local_response_norm(x if x.dim() == 4 else x.unsqueeze(0), self.size, self.alpha, self.beta, self.k) \
+                if self.format != "NHWC" else self._f(x)
+            if self.format != "NHWC" and input.dim() == 3:
+                y = y.squeeze(0)
+        return torch.autograd.grad(y, x, gradOutput.to(y.dtype))[0]
+
+
+class SpatialWithinChannelLRN(AutogradModule):
+    """LRN inside each channel over a size×size spatial window (``SpatialWithinChannelLRN.scala``)."""
+
+    def __init__(self, size=5, alpha=1.0, beta=0.75, bigdl_type="float"):
+        super().__init__()
+        self.size, self.alpha, self.beta = size, alpha, beta
+
+    def _forward(self, x):
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        p = (self.size - 1) // 2
+        sq = F.avg_pool2d(x * x, self.size, 1, p, count_include_pad=True)
+        y = x * torch.pow(1 + self.alpha * sq, -self.beta)
+        return y if batched else y.squeeze(0)
+
+
+class LayerNormalization(AutogradModule):
+    """Transformer layer norm (``LayerNormalization.scala``): weight init 1, bias 0, eps 1e-6."""
+
+    def __init__(self, hidden_size, bigdl_type="float"):
+        super().__init__()
+        self.hiddenSize = hidden_size
+        self.register_parameter("weight", torch.ones(hidden_size))
+        self.register_parameter("bias", torch.zeros(hidden_size))
+
+    def _forward(self, x):
+        mean = x.mean(-1, keepdim=True)
+        var = ((x - mean) ** 2).mean(-1, keepdim=True)
+        return (x - mean) * torch.rsqrt(var + 1e-6) * self.P("weight").to(x.dtype) + self.P("bias").to(x.dtype)
+
+
+class Normalize(AutogradModule):
+    """Lp-normalise along the feature dim (``Normalize.scala``)."""
+
+    def __init__(self, p, eps=1e-10, bigdl_type="float"):
+        super().__init__()
+        self.p, self.eps = p, eps
+
+    def _forward(self, x):
+        dim = 1 if x.dim() > 1 else 0
+        if math.isinf(self.p):
+            n = x.abs().amax(dim, keepdim=True)
+        else:
+            n = (x.abs().pow(self.p).sum(dim, keepdim=True) + self.eps).pow(1.0 / self.p)
+        return x / n
+
+
+class NormalizeScale(AutogradModule):
+    """L2-normalise then per-channel scale (SSD, ``NormalizeScale.scala``)."""
+
+    def __init__(self, p, scale, size, w_regularizer=None, eps=1e-10, bigdl_type="float"):
+        super().__init__()
+        self.p, self.eps = p, eps
+        self.register_parameter("weight", torch.full(tuple(size), float(scale)))
+
+    def _forward(self, x):
+        n = (x.abs().pow(self.p).sum(1, keepdim=True) + self.eps).pow(1.0 / self.p)
+        return x / n * self.P("weight").to(x.dtype)
+
+
+def _gauss_kernel(size):
+    if isinstance(size, torch.Tensor):
+        return size.float()
+    k = torch.ones(size, size)
+    return k
+
+
+class SpatialSubtractiveNormalization(AutogradModule):
+    """x − weighted local mean (``SpatialSubtractiveNormalization.scala``)."""
+
+    def __init__(self, n_input_plane=1, kernel=None, bigdl_type="float"):
+        super().__init__()
+        self.nInputPlane = n_input_plane
+        k = torch.ones(9, 9) if kernel is None else torch.as_tensor(kernel, dtype=torch.float32)
+        if k.dim() == 1:
+            k = torch.outer(k, k)
+        self.kernel = k / (k.sum() * n_input_plane)
+
+    def _mean(self, x):
+        kh, kw = self.kernel.shape
+        w = self.kernel.to(x.device, x.dtype).expand(1, self.nInputPlane, kh, kw)
+        pad = (kw // 2, (kw - 1) // 2, kh // 2, (kh - 1) // 2)
+        xp = F.pad(x, pad)
+        m = F.conv2d(xp, w)
+        ones = torch.ones(1, self.nInputPlane, x.shape[2], x.shape[3], device=x.device, dtype=x.dtype)
+        coef = F.conv2d(F.pad(ones, pad), w)
+        return m / coef
+
+    def _forward(self, x):
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        y = x - self._mean(x)
+        return y if batched else y.squeeze(0)
+
+
+class SpatialDivisiveNormalization(SpatialSubtractiveNormalization):
+    def __init__(self, n_input_plane=1, kernel=None, threshold=1e-4, thresval=1e-4, bigdl_type="float"):
+        super().__init__(n_input_plane, kernel)
+        self.threshold, self.thresval = threshold, thresval
+
+    def _forward(self, x):
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        std = torch.sqrt(self._mean(x * x))
+        mean_std = std.mean(dim=(1, 2, 3), keepdim=True)
+        div = torch.maximum(std, mean_std)
+        div = torch.where(div > self.threshold, div, torch.full_like(div, self.thresval))
+        y = x / div
+        return y if batched else y.squeeze(0)
+
+
+class SpatialContrastiveNormalization(AutogradModule):
+    def __init__(self, n_input_plane=1, kernel=None, threshold=1e-4, thresval=1e-4, bigdl_type="float"):
+        super().__init__()
+        self.sub = SpatialSubtractiveNormalization(n_input_plane, kernel)
+        self.div = SpatialDivisiveNormalization(n_input_plane, kernel, threshold, thresval)
+
+    def _forward(self, x):
+        return self.div._forward(self.sub._forward(x))

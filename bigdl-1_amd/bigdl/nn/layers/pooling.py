@@ -1,0 +1,314 @@
+"""Pooling and resampling.
+
+``SpatialMaxPooling`` (``DL/nn/SpatialMaxPooling.scala:91-246`` via ``NNPrimitive.maxPooling*``;
+``ceil()`` = Caffe ceil mode), ``SpatialAveragePooling`` (``SpatialAveragePooling.scala:115-700``:
+count_include_pad, ceil, global pooling, ``divide``).  Device path: NHWC vectorised kernels that
+save the argmax offset within the window.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ..abstractnn import TensorModule, AutogradModule
+from .conv import to_device_layout, same_padding
+
+
+def _pool_pad(x, kh, kw, dh, dw, ph, pw):
+    if ph == -1 and pw == -1:
+        pt, pb, pl, pr, _, _ = same_padding(x.shape[-2], x.shape[-1], dh, dw, kh, kw)
+        return pt, pb, pl, pr
+    return ph, ph, pw, pw
+
+
+class SpatialMaxPooling(TensorModule):
+    def __init__(self, kw, kh, dw=None, dh=None, pad_w=0, pad_h=0, to_ceil=False, format="NCHW",
+                 bigdl_type="float"):
+        super().__init__()
+        self.kW, self.kH = kw, kh
+        self.dW = dw if dw is not None else kw
+        self.dH = dh if dh is not None else kh
+        self.padW, self.padH = pad_w, pad_h
+        self.ceilMode = to_ceil
+        self.format = format
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def floor(self):
+        self.ceilMode = False
+        return self
+
+    def _prep(self, input):
+        x = input
+        if self.format == "NHWC":
+            x = x.permute(0, 3, 1, 2) if x.dim() == 4 else x.permute(2, 0, 1)
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        x = to_device_layout(x)
+        pt, pb, pl, pr = _pool_pad(x, self.kH, self.kW, self.dH, self.dW, self.padH, self.padW)
+        if pt != pb or pl != pr:
+            x = F.pad(x, (pl, pr, pt, pb), value=float("-inf"))
+            pad = (0, 0)
+        else:
+            pad = (pt, pl)
+        return x, pad, batched, (pt, pb, pl, pr)
+
+    def _post(self, y, batched):
+        if not batched:
+            y = y.squeeze(0)
+        if self.format == "NHWC":
+            y = y.permute(0, 2, 3, 1) if y.dim() == 4 else y.permute(1, 2, 0)
+        return y
+
+    def updateOutput(self, input):
+        x, pad, batched, _ = self._prep(input)
+        y, idx = ops.maxpool2d_forward(x, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode)
+        self._indices = idx
+        return self._post(y, batched)
+
+    def updateGradInput(self, input, gradOutput):
+        x, pad, batched, pads = self._prep(input)
+        gy = gradOutput
+        if self.format == "NHWC":
+            gy = gy.permute(0, 3, 1, 2) if gy.dim() == 4 else gy.permute(2, 0, 1)
+        if not batched:
+            gy = gy.unsqueeze(0)
+        gy = to_device_layout(gy)
+        gi = ops.maxpool2d_backward(gy, x, self._indices, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode)
+        pt, pb, pl, pr = pads
+        if pt != pb or pl != pr:
+            gi = gi[:, :, pt:gi.shape[2] - pb, pl:gi.shape[3] - pr]
+        return self._post(gi, batched)
+
+    def __repr__(self):
+        return f"SpatialMaxPooling[{self.get_name()}]({self.kW}, {self.kH}, {self.dW}, {self.dH}, {self.padW}, {self.padH})"
+
+
+class SpatialAveragePooling(TensorModule):
+    def __init__(self, kw, kh, dw=1, dh=1, pad_w=0, pad_h=0, global_pooling=False, ceil_mode=False,
+                 count_include_pad=True, divide=True, format="NCHW", bigdl_type="float"):
+        super().__init__()
+        self.kW, self.kH, self.dW, self.dH = kw, kh, dw, dh
+        self.padW, self.padH = pad_w, pad_h
+        self.globalPooling = global_pooling
+        self.ceilMode = ceil_mode
+        self.countIncludePad = count_include_pad
+        self.divide = divide
+        self.format = format
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def floor(self):
+        self.ceilMode = False
+        return self
+
+    def _geom(self, x):
+        if self.globalPooling:
+            return (x.shape[-2], x.shape[-1]), (1, 1), (0, 0)
+        return (self.kH, self.kW), (self.dH, self.dW), None
+
+    def _prep(self, input):
+        x = input
+        if self.format == "NHWC":
+            x = x.permute(0, 3, 1, 2) if x.dim() == 4 else x.permute(2, 0, 1)
+        batched = x.dim() == 4
+        if not batched:
+            x = x.unsqueeze(0)
+        x = to_device_layout(x)
+        k, s, p = self._geom(x)
+        pads = (0, 0, 0, 0)
+        if p is None:
+            pt, pb, pl, pr = _pool_pad(x, k[0], k[1], s[0], s[1], self.padH, self.padW)
+            pads = (pt, pb, pl, pr)
+            if pt != pb or pl != pr:
+                x = F.pad(x, (pl, pr, pt, pb))
+                p = (0, 0)
+            else:
+                p = (pt, pl)
+        divisor = None if self.divide else 1
+        return x, k, s, p, batched, pads, divisor
+
+    def _post(self, y, batched):
+        if not batched:
+            y = y.squeeze(0)
+        if self.format == "NHWC":
+            y = y.permute(0, 2, 3, 1) if y.dim() == 4 else y.permute(1, 2, 0)
+        return y
+
+    def updateOutput(self, input):
+        x, k, s, p, batched, _, divisor = self._prep(input)
+        y = ops.avgpool2d_forward(x, k, s, p, self.ceilMode, self.countIncludePad, divisor)
+        return self._post(y, batched)
+
+    def updateGradInput(self, input, gradOutput):
+        x, k, s, p, batched, pads, divisor = self._prep(input)
+        gy = gradOutput
+        if self.format == "NHWC":
+            gy = gy.permute(0, 3, 1, 2) if gy.dim() == 4 else gy.permute(2, 0, 1)
+        if not batched:
+            gy = gy.unsqueeze(0)
+        gy = to_device_layout(gy)
+        gi = ops.avgpool2d_backward(gy, x, k, s, p, self.ceilMode, self.countIncludePad, divisor)
+        pt, pb, pl, pr = pads
+        if pt != pb or pl != pr:
+            gi = gi[:, :, pt:gi.shape[2] - pb, pl:gi.shape[3] - pr]
+        return self._post(gi, batched)
+
+
+class TemporalMaxPooling(AutogradModule):
+    def __init__(self, k_w, d_w=-1, bigdl_type="float"):
+        super().__init__()
+        self.kW, self.dW = k_w, (d_w if d_w != -1 else k_w)
+
+    def _forward(self, x):
+        batched = x.dim() == 3
+        if not batched:
+            x = x.unsqueeze(0)
+        y = F.max_pool1d(x.transpose(1, 2), self.kW, self.dW).transpose(1, 2)
+        return y if batched else y.squeeze(0)
+
+
+class VolumetricMaxPooling(AutogradModule):
+    def __init__(self, k_t, k_w, k_h, d_t, d_w, d_h, pad_t=0, pad_w=0, pad_h=0, bigdl_type="float"):
+        super().__init__()
+        self.k, self.d, self.p = (k_t, k_h, k_w), (d_t, d_h, d_w), (pad_t, pad_h, pad_w)
+        self.ceilMode = False
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def _forward(self, x):
+        batched = x.dim() == 5
+        if not batched:
+            x = x.unsqueeze(0)
+        y = F.max_pool3d(x, self.k, self.d, self.p, ceil_mode=self.ceilMode)
+        return y if batched else y.squeeze(0)
+
+
+class VolumetricAveragePooling(AutogradModule):
+    def __init__(self, k_t, k_w, k_h, d_t, d_w, d_h, pad_t=0, pad_w=0, pad_h=0, count_include_pad=True,
+                 ceil_mode=False, bigdl_type="float"):
+        super().__init__()
+        self.k, self.d, self.p = (k_t, k_h, k_w), (d_t, d_h, d_w), (pad_t, pad_h, pad_w)
+        self.countIncludePad, self.ceilMode = count_include_pad, ceil_mode
+
+    def _forward(self, x):
+        batched = x.dim() == 5
+        if not batched:
+            x = x.unsqueeze(0)
+        y = F.avg_pool3d(x, self.k, self.d, self.p, self.ceilMode, self.countIncludePad)
+        return y if batched else y.squeeze(0)
+
+
+class RoiPooling(AutogradModule):
+    """Max-pool each ROI (batch_idx, x1, y1, x2, y2) to (pooledH, pooledW) (``RoiPooling.scala``)."""
+
+    def __init__(self, pooled_w, pooled_h, spatial_scale, bigdl_type="float"):
+        super().__init__()
+        self.pooledW, self.pooledH, self.spatialScale = pooled_w, pooled_h, spatial_scale
+
+    def _forward(self, x):
+        data, rois = x[1], x[2]
+        outs = []
+        H, W = data.shape[2], data.shape[3]
+        for r in rois.tolist():
+            b = int(r[0])
+            x1, y1, x2, y2 = [int(round(v * self.spatialScale)) for v in r[1:5]]
+            rh = max(y2 - y1 + 1, 1)
+            rw = max(x2 - x1 + 1, 1)
+            bh, bw = rh / self.pooledH, rw / self.pooledW
+            cells = []
+            for ph in range(self.pooledH):
+                hs = min(max(int(math.floor(ph * bh)) + y1, 0), H)
+                he = min(max(int(math.ceil((ph + 1) * bh)) + y1, 0), H)
+                row = []
+                for pw in range(self.pooledW):
+                    ws = min(max(int(math.floor(pw * bw)) + x1, 0), W)
+                    we = min(max(int(math.ceil((pw + 1) * bw)) + x1, 0), W)
+                    if he <= hs or we <= ws:
+                        row.append(torch.zeros(data.shape[1], dtype=data.dtype, device=data.device))
+                    else:
+                        row.append(data[b, :, hs:he, ws:we].amax(dim=(1, 2)))
+                cells.append(torch.stack(row, -1))
+            outs.append(torch.stack(cells, -2))
+        return torch.stack(outs, 0)
+
+
+class RoiAlign(AutogradModule):
+    """Bilinear ROI align (``RoiAlign.scala``): rois (K, 4) with batch index from a second input."""
+
+    def __init__(self, spatial_scale, sampling_ratio, pooled_h, pooled_w, mode="avg", aligned=True,
+                 bigdl_type="float"):
+        super().__init__()
+        self.spatialScale, self.samplingRatio = spatial_scale, sampling_ratio
+        self.pooledH, self.pooledW, self.aligned = pooled_h, pooled_w, aligned
+
+    def _forward(self, x):
+        data, rois = x[1], x[2]
+        if rois.shape[-1] == 4:
+            rois = torch.cat([torch.zeros(rois.shape[0], 1, dtype=rois.dtype, device=rois.device), rois], 1)
+        off = 0.5 if self.aligned else 0.0
+        outs = []
+        sr = max(self.samplingRatio, 1)
+        for r in rois:
+            b = int(r[0])
+            x1, y1, x2, y2 = [float(v) * self.spatialScale - off for v in r[1:5]]
+            rw, rh = max(x2 - x1, 1e-6 if self.aligned else 1.0), max(y2 - y1, 1e-6 if self.aligned else 1.0)
+            ys = y1 + (torch.arange(self.pooledH * sr, device=data.device, dtype=torch.float32) + 0.5) * rh / (self.pooledH * sr)
+            xs = x1 + (torch.arange(self.pooledW * sr, device=data.device, dtype=torch.float32) + 0.5) * rw / (self.pooledW * sr)
+            gy, gx = torch.meshgrid(ys, xs, indexing="ij")
+            H, W = data.shape[2], data.shape[3]
+            grid = torch.stack([(gx + 0.5) / W * 2 - 1, (gy + 0.5) / H * 2 - 1], -1).unsqueeze(0)
+            samp = F.grid_sample(data[b:b + 1].float(), grid, mode="bilinear", align_corners=False)
+            outs.append(F.avg_pool2d(samp, sr)[0])
+        return torch.stack(outs, 0).to(data.dtype)
+
+
+class UpSampling1D(AutogradModule):
+    def __init__(self, length, bigdl_type="float"):
+        super().__init__()
+        self.length = length
+
+    def _forward(self, x):
+        return x.repeat_interleave(self.length, dim=-2)
+
+
+class UpSampling2D(AutogradModule):
+    def __init__(self, size, data_format="nchw", bigdl_type="float"):
+        super().__init__()
+        self.size, self.format = list(size), data_format.lower()
+
+    def _forward(self, x):
+        hd, wd = (2, 3) if self.format == "nchw" else (1, 2)
+        return x.repeat_interleave(self.size[0], dim=hd).repeat_interleave(self.size[1], dim=wd)
+
+
+class UpSampling3D(AutogradModule):
+    def __init__(self, size, bigdl_type="float"):
+        super().__init__()
+        self.size = list(size)
+
+    def _forward(self, x):
+        return x.repeat_interleave(self.size[0], 2).repeat_interleave(self.size[1], 3).repeat_interleave(self.size[2], 4)
+
+
+class ResizeBilinear(AutogradModule):
+    def __init__(self, output_height, output_width, align_corner=False, data_format="NCHW", bigdl_type="float"):
+        super().__init__()
+        self.oh, self.ow, self.alignCorners, self.format = output_height, output_width, align_corner, data_format
+
+    def _forward(self, x):
+        nhwc = self.format == "NHWC"
+        if nhwc:
+            x = x.permute(0, 3, 1, 2)
+        y = F.interpolate(x, size=(self.oh, self.ow), mode="bilinear", align_corners=self.alignCorners)
+        return y.permute(0, 2, 3, 1) if nhwc else y

@@ -1,0 +1,294 @@
+"""Table layers (``DL/nn/{CAddTable,CSubTable,CMulTable,CDivTable,CMaxTable,CMinTable,CAveTable,
+JoinTable,SplitTable,SelectTable,NarrowTable,FlattenTable,MixtureTable,BifurcateSplitTable,
+TableOperation}.scala``).  ``CAddTable`` is on the ResNet hot path (residual add) and
+``JoinTable`` on Inception's (channel concat, K19)."""
+from __future__ import annotations
+
+import torch
+
+from ..abstractnn import TensorModule, AutogradModule
+from ...utils.table import Table
+
+
+class CAddTable(TensorModule):
+    def __init__(self, inplace=False, bigdl_type="float"):
+        super().__init__()
+        self.inplace = inplace
+
+    def updateOutput(self, input):
+        ts = list(input)
+        out = ts[0]  # ``inplace`` is honoured as a hint only (see Threshold)
+        for t in ts[1:]:
+            out = out + t
+        return out
+
+    def updateGradInput(self, input, gradOutput):
+        gi = Table()
+        for i, t in enumerate(list(input)):
+            if t.shape == gradOutput.shape:
+                gi[i + 1] = gradOutput
+            else:  # broadcast input: reduce
+                g = gradOutput
+                while g.dim() > t.dim():
+                    g = g.sum(0)
+                for d in range(t.dim()):
+                    if t.shape[d] == 1 and g.shape[d] != 1:
+                        g = g.sum(d, keepdim=True)
+                gi[i + 1] = g
+        return gi
+
+
+class CSubTable(TensorModule):
+    def updateOutput(self, input):
+        return input[1] - input[2]
+
+    def updateGradInput(self, input, gradOutput):
+        return Table(gradOutput, -gradOutput)
+
+
+class CMulTable(TensorModule):
+    def updateOutput(self, input):
+        out = input[1]
+        for t in list(input)[1:]:
+            out = out * t
+        return out
+
+    def updateGradInput(self, input, gradOutput):
+        ts = list(input)
+        gi = Table()
+        for i in range(len(ts)):
+            g = gradOutput
+            for j, t in enumerate(ts):
+                if j != i:
+                    g = g * t
+            gi[i + 1] = g
+        return gi
+
+
+class CDivTable(TensorModule):
+    def updateOutput(self, input):
+        return input[1] / input[2]
+
+    def updateGradInput(self, input, gradOutput):
+        a, b = input[1], input[2]
+        return Table(gradOutput / b, -gradOutput * a / (b * b))
+
+
+class CMaxTable(AutogradModule):
+    def _forward(self, x):
+        ts = list(x)
+        out = ts[0]
+        for t in ts[1:]:
+            out = torch.maximum(out, t)
+        return out
+
+
+class CMinTable(AutogradModule):
+    def _forward(self, x):
+        ts = list(x)
+        out = ts[0]
+        for t in ts[1:]:
+            out = torch.minimum(out, t)
+        return out
+
+
+class CAveTable(AutogradModule):
+    def __init__(self, inplace=False, bigdl_type="float"):
+        super().__init__()
+
+    def _forward(self, x):
+        ts = list(x)
+        return sum(ts) / len(ts)
+
+
+class JoinTable(TensorModule):
+    """Concatenate table entries along ``dimension`` (1-based, batch-shifted by nInputDims)."""
+
+    def __init__(self, dimension, n_input_dims=0, bigdl_type="float"):
+        super().__init__()
+        self.dimension, self.nInputDims = dimension, n_input_dims
+
+    def _d(self, x):
+        d = self.dimension - 1 if self.dimension > 0 else x.dim() + self.dimension
+        if self.nInputDims > 0 and x.dim() > self.nInputDims and self.dimension > 0:
+            d += x.dim() - self.nInputDims
+        return d
+
+    def updateOutput(self, input):
+        ts = list(input)
+        d = self._d(ts[0])
+        self._sizes = [t.shape[d] for t in ts]
+        if ts[0].is_cuda and ts[0].dim() == 4 and d == 1:
+            return torch.cat(ts, d).contiguous(memory_format=torch.channels_last)
+        return torch.cat(ts, d)
+
+    def updateGradInput(self, input, gradOutput):
+        ts = list(input)
+        d = self._d(ts[0])
+        parts = torch.split(gradOutput, self._sizes, dim=d)
+        gi = Table()
+        for i, p in enumerate(parts):
+            if p.is_cuda and p.dim() == 4:
+                gi[i + 1] = p.contiguous(memory_format=torch.channels_last)
+            else:
+                gi[i + 1] = p.contiguous()
+        return gi
+
+
+class SplitTable(TensorModule):
+    def __init__(self, dimension, n_input_dims=-1, bigdl_type="float"):
+        super().__init__()
+        self.dimension, self.nInputDims = dimension, n_input_dims
+
+    def _d(self, x):
+        d = self.dimension - 1 if self.dimension > 0 else x.dim() + self.dimension
+        if self.nInputDims > 0 and x.dim() > self.nInputDims and self.dimension > 0:
+            d += x.dim() - self.nInputDims
+        return d
+
+    def updateOutput(self, input):
+        d = self._d(input)
+        return Table(*[t for t in torch.unbind(input, d)])
+
+    def updateGradInput(self, input, gradOutput):
+        d = self._d(input)
+        return torch.stack(list(gradOutput), d)
+
+
+class BifurcateSplitTable(TensorModule):
+    def __init__(self, dimension, bigdl_type="float"):
+        super().__init__()
+        self.dimension = dimension
+
+    def updateOutput(self, input):
+        d = self.dimension - 1
+        n = input.shape[d] // 2
+        return Table(input.narrow(d, 0, n), input.narrow(d, n, input.shape[d] - n))
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.cat([gradOutput[1], gradOutput[2]], self.dimension - 1)
+
+
+class SelectTable(TensorModule):
+    def __init__(self, index, bigdl_type="float"):
+        super().__init__()
+        self.index = index
+
+    def _i(self, input):
+        return self.index if self.index > 0 else input.length() + self.index + 1
+
+    def updateOutput(self, input):
+        return input[self._i(input)]
+
+    def updateGradInput(self, input, gradOutput):
+        gi = Table()
+        idx = self._i(input)
+        for k in range(1, input.length() + 1):
+            if k == idx:
+                gi[k] = gradOutput
+            else:
+                v = input[k]
+                gi[k] = torch.zeros_like(v) if isinstance(v, torch.Tensor) else _zeros_like_table(v)
+        return gi
+
+
+def _zeros_like_table(t):
+    out = Table()
+    for k, v in t.items():
+        out[k] = torch.zeros_like(v) if isinstance(v, torch.Tensor) else _zeros_like_table(v)
+    return out
+
+
+class NarrowTable(TensorModule):
+    def __init__(self, offset, length=1, bigdl_type="float"):
+        super().__init__()
+        self.offset, self.length = offset, length
+
+    def _range(self, input):
+        n = input.length()
+        ln = self.length if self.length > 0 else n - self.offset + 2 + self.length
+        return self.offset, ln
+
+    def updateOutput(self, input):
+        off, ln = self._range(input)
+        return Table(*[input[off + i] for i in range(ln)])
+
+    def updateGradInput(self, input, gradOutput):
+        off, ln = self._range(input)
+        gi = Table()
+        for k in range(1, input.length() + 1):
+            if off <= k < off + ln:
+                gi[k] = gradOutput[k - off + 1]
+            else:
+                gi[k] = torch.zeros_like(input[k])
+        return gi
+
+
+class FlattenTable(TensorModule):
+    def updateOutput(self, input):
+        return input.flatten()
+
+    def updateGradInput(self, input, gradOutput):
+        flat = list(gradOutput)
+        pos = [0]
+
+        def rebuild(t):
+            out = Table()
+            for k in range(1, t.length() + 1):
+                v = t[k]
+                if isinstance(v, Table):
+                    out[k] = rebuild(v)
+                else:
+                    out[k] = flat[pos[0]]
+                    pos[0] += 1
+            return out
+        return rebuild(input)
+
+
+class MixtureTable(AutogradModule):
+    """Mixture of experts: Table(gater (N,E), experts Table or tensor) (``MixtureTable.scala``)."""
+
+    def __init__(self, dim=INT_MAX if False else 2147483647, bigdl_type="float"):
+        super().__init__()
+        self.dim = dim
+
+    def _forward(self, x):
+        gater, experts = x[1], x[2]
+        if isinstance(experts, Table):
+            ex = torch.stack(list(experts), 1)
+        else:
+            ex = experts
+        g = gater
+        while g.dim() < ex.dim():
+            g = g.unsqueeze(-1)
+        return (g * ex).sum(1)
+
+
+class TableOperation(AutogradModule):
+    """Apply a 2-input table op, broadcasting the smaller operand (``TableOperation.scala``)."""
+
+    def __init__(self, operation_layer, bigdl_type="float"):
+        super().__init__()
+        self.operation = operation_layer
+
+    def _forward(self, x):
+        a, b = x[1], x[2]
+        if a.numel() < b.numel():
+            a = a.expand_as(b)
+        elif b.numel() < a.numel():
+            b = b.expand_as(a)
+        op = self.operation
+        name = type(op).__name__
+        if name == "CAddTable":
+            return a + b
+        if name == "CMulTable":
+            return a * b
+        if name == "CSubTable":
+            return a - b
+        if name == "CDivTable":
+            return a / b
+        if name == "CMaxTable":
+            return torch.maximum(a, b)
+        if name == "CMinTable":
+            return torch.minimum(a, b)
+        return op.forward(Table(a, b))

@@ -1,0 +1,380 @@
+// NHWC BatchNormalization for training and inference (K5/K6/K7 + fused K8/K9 epilogues).
+//
+// Reference semantics: DL/nn/SpatialBatchNormalization.scala (updateOutputNCHWTrainFloat :1211,
+// updateGradInputNCHWTrainFloat :1048, accGradientNCHWFloat :1970): normalise with the biased batch
+// variance, update runningVar with the UNBIASED variance, momentum m: r = (1-m) r + m v.
+//
+// Layout: x is [M = N·H·W rows][C channels] bf16 (NHWC contiguous), C % 8 == 0.
+// A thread owns one group of 8 channels (one 16-B load per row) and strides over rows; a block covers
+// all channels of a contiguous row range and writes per-block partial sums; a small finalize kernel
+// combines the G partials per channel in double precision.  Statistics use the SHIFTED sums
+// Σ(x−K), Σ(x−K)² with K = x[row 0] per channel, so no catastrophic cancellation when |mean| ≫ std.
+//
+// Forward (train) = stats (read x) + finalize + apply (read x [+res], write y): 3 passes of HBM
+// traffic — the minimum for a non-fused BN.  Backward = reduce (read gy, x [, y]) + finalize + apply
+// (read gy, x [, y], write gx [, g_res]).
+#include "common.h"
+
+struct BnGeom {
+  int C, CG, RPI, tpr;  // channels, channel groups of 8, rows per iteration, active threads
+};
+
+__device__ __forceinline__ BnGeom bn_geom(int C) {
+  BnGeom g;
+  g.C = C;
+  g.CG = C >> 3;
+  int cg_eff = g.CG < 256 ? g.CG : 256;
+  g.RPI = 256 / cg_eff;
+  g.tpr = cg_eff;
+  return g;
+}
+
+// ------------------------------------------------------------------------------------------------ stats
+// partial[b][c] = Σ_{rows of block b} (x − K_c),  partial[G + b][c] = Σ (x − K_c)²
+__global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, long long M, int C,
+                                                  long long rows_per_block, float* __restrict__ partial, int G) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  long long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float* s_sum = smem;                 // [RPI][C]
+  float* s_sq = smem + g.RPI * C;      // [RPI][C]
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    float K[8], s[8], q[8];
+    load8(x + (size_t)cg * 8, K);  // row 0
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+    if (r_off < g.RPI) {
+      for (long long r = r0 + r_off; r < r1; r += g.RPI) {
+        float v[8];
+        load8(x + (size_t)r * C + (size_t)cg * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float d = v[k] - K[k];
+          s[k] += d;
+          q[k] = fmaf(d, d, q[k]);
+        }
+      }
+      #pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s_sum[r_off * C + cg * 8 + k] = s[k];
+        s_sq[r_off * C + cg * 8 + k] = q[k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float s = 0.f, q = 0.f;
+    for (int i = 0; i < g.RPI; ++i) {
+      s += s_sum[i * C + c];
+      q += s_sq[i * C + c];
+    }
+    partial[(size_t)blockIdx.x * C + c] = s;
+    partial[(size_t)(G + blockIdx.x) * C + c] = q;
+  }
+}
+
+// Combine partials; write save_mean/save_invstd, apply coefficients scale/shift, update running stats.
+__global__ void k_bn_finalize(const bf16_t* __restrict__ x, const float* __restrict__ partial, int G, long long M,
+                              int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                              float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float eps,
+                              float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                              float* __restrict__ scale, float* __restrict__ shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < G; ++b) {
+    s += (double)partial[(size_t)b * C + c];
+    q += (double)partial[(size_t)(G + b) * C + c];
+  }
+  double K = (double)bf2f(x[c]);
+  double dm = s / (double)M;
+  double var = q / (double)M - dm * dm;
+  if (var < 0) var = 0;
+  double mean = K + dm;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  float gm = gamma ? gamma[c] : 1.f;
+  float bt = beta ? beta[c] : 0.f;
+  float sc = gm * invstd;
+  scale[c] = sc;
+  shift[c] = bt - (float)mean * sc;
+  if (run_mean) {
+    double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+}
+
+// inference coefficients from running stats
+__global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                const float* __restrict__ run_mean, const float* __restrict__ run_var, float eps,
+                                float* __restrict__ scale, float* __restrict__ shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float invstd = rsqrtf(run_var[c] + eps);
+  float sc = (gamma ? gamma[c] : 1.f) * invstd;
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - run_mean[c] * sc;
+}
+
+// ------------------------------------------------------------------------------------------------ apply
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                  bf16_t* __restrict__ y, long long M, int C,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift) {
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  if (r_off >= g.RPI) return;
+  const long long rstride = (long long)gridDim.x * g.RPI;
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    float sc[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = scale[cg * 8 + k];
+      sh[k] = shift[cg * 8 + k];
+    }
+    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
+      size_t off = (size_t)r * C + (size_t)cg * 8;
+      float v[8];
+      load8(x + off, v);
+      float rv[8];
+      if (RES) load8(res + off, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = fmaf(v[k], sc[k], sh[k]);
+        if (RES) o += rv[k];
+        if (RELU) o = fmaxf(o, 0.f);
+        v[k] = o;
+      }
+      store8(y + off, v);
+    }
+  }
+}
+
+static int apply_grid(long long M, int C) {
+  int CG = C / 8;
+  int tpr = CG < 256 ? CG : 256;
+  int rpi = 256 / tpr;
+  long long blocks = (M + rpi - 1) / rpi;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+// number of partial blocks used by the stats / backward-reduce kernels (mirrored in Python)
+BIGDL_EXPORT int bigdl_bn_num_partials(long long M, int C) {
+  int CG = C / 8;
+  int tpr = CG < 256 ? CG : 256;
+  int rpi = 256 / tpr;
+  long long target_rows = (long long)rpi * 16;  // ≥16 rows per thread per block
+  long long G = (M + target_rows - 1) / target_rows;
+  if (G > 1024) G = 1024;
+  if (G < 1) G = 1;
+  return (int)G;
+}
+
+static size_t stats_smem(int C) {
+  int CG = C / 8;
+  int tpr = CG < 256 ? CG : 256;
+  int rpi = 256 / tpr;
+  return (size_t)rpi * C * 2 * sizeof(float);
+}
+
+// Training forward.  ws: partial buffer of 2·G·C floats; coef: 2·C floats (scale, shift).
+BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                                    const float* beta, float* run_mean, float* run_var, float momentum, float eps,
+                                    float* save_mean, float* save_invstd, float* ws, float* coef, int relu,
+                                    hipStream_t s) {
+  if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
+  int G = bigdl_bn_num_partials(M, C);
+  long long rpb = (M + G - 1) / G;
+  size_t sm = stats_smem(C);
+  if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, ws, G, M, C, gamma,
+                     beta, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
+  int grid = apply_grid(M, C);
+  const bf16_t* xr = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  bf16_t* yr = (bf16_t*)y;
+  if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_bn_fwd_infer(const void* x, void* y, long long M, int C, const float* gamma, const float* beta,
+                                    const float* run_mean, const float* run_var, float eps, float* coef, int relu,
+                                    hipStream_t s) {
+  if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_infer_coef, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, run_mean, run_var, eps,
+                     coef, coef + C);
+  int grid = apply_grid(M, C);
+  if (relu)
+    hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, nullptr, (bf16_t*)y,
+                       M, C, coef, coef + C);
+  else
+    hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, nullptr,
+                       (bf16_t*)y, M, C, coef, coef + C);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------ backward
+// partial[b][c] = Σ g',  partial[G+b][c] = Σ g'·(x − mean),  g' = gy · [y > 0 if RELU]
+template <bool RELU>
+__global__ void __launch_bounds__(256) k_bn_bwd_reduce(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ y, long long M, int C,
+                                                       long long rows_per_block, const float* __restrict__ mean,
+                                                       float* __restrict__ partial, int G) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  long long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float* s_a = smem;
+  float* s_b = smem + g.RPI * C;
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    if (r_off >= g.RPI) break;
+    float mu[8], a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { mu[k] = mean[cg * 8 + k]; a[k] = 0.f; b[k] = 0.f; }
+    for (long long r = r0 + r_off; r < r1; r += g.RPI) {
+      size_t off = (size_t)r * C + (size_t)cg * 8;
+      float gv[8], xv[8];
+      load8(gy + off, gv);
+      load8(x + off, xv);
+      if (RELU) {
+        float yv[8];
+        load8(y + off, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a[k] += gv[k];
+        b[k] = fmaf(gv[k], xv[k] - mu[k], b[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s_a[r_off * C + cg * 8 + k] = a[k];
+      s_b[r_off * C + cg * 8 + k] = b[k];
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < g.RPI; ++i) {
+      a += s_a[i * C + c];
+      b += s_b[i * C + c];
+    }
+    partial[(size_t)blockIdx.x * C + c] = a;
+    partial[(size_t)(G + blockIdx.x) * C + c] = b;
+  }
+}
+
+// dβ = Σg', dγ = invstd·Σg'(x−μ); accumulate scale·dγ, scale·dβ into the fp32 grad arena;
+// coefficients for gx = A·g' + B·x + Cc
+__global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int G, long long M, int C,
+                                  const float* __restrict__ gamma, const float* __restrict__ mean,
+                                  const float* __restrict__ invstd, float* __restrict__ ggamma,
+                                  float* __restrict__ gbeta, float gscale, float* __restrict__ coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int i = 0; i < G; ++i) {
+    a += (double)partial[(size_t)i * C + c];
+    b += (double)partial[(size_t)(G + i) * C + c];
+  }
+  float is = invstd[c];
+  float dbeta = (float)a;
+  float dgamma = (float)(b * (double)is);
+  if (ggamma) ggamma[c] += gscale * dgamma;
+  if (gbeta) gbeta[c] += gscale * dbeta;
+  float gm = gamma ? gamma[c] : 1.f;
+  float A = gm * is;
+  float B = -gm * is * is * dgamma / (float)M;
+  float Cc = -gm * is * dbeta / (float)M - B * mean[c];
+  coef[c] = A;
+  coef[C + c] = B;
+  coef[2 * C + c] = Cc;
+}
+
+template <bool RELU, bool GRES>
+__global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ y, bf16_t* __restrict__ gx,
+                                                      bf16_t* __restrict__ gres, long long M, int C,
+                                                      const float* __restrict__ coef) {
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  if (r_off >= g.RPI) return;
+  const long long rstride = (long long)gridDim.x * g.RPI;
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    float A[8], B[8], Cc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      A[k] = coef[cg * 8 + k];
+      B[k] = coef[C + cg * 8 + k];
+      Cc[k] = coef[2 * C + cg * 8 + k];
+    }
+    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
+      size_t off = (size_t)r * C + (size_t)cg * 8;
+      float gv[8], xv[8];
+      load8(gy + off, gv);
+      load8(x + off, xv);
+      if (RELU) {
+        float yv[8];
+        load8(y + off, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+      }
+      if (GRES) store8(gres + off, gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xv[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
+      store8(gx + off, xv);
+    }
+  }
+}
+
+// Backward.  ws: 2·G·C floats; coef: 3·C floats.  gx may be null (no input gradient needed).
+// gres (optional): receives g' (the masked upstream gradient) for a fused residual branch.
+BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void* gx, void* gres, long long M, int C,
+                              const float* gamma, const float* mean, const float* invstd, float* ggamma,
+                              float* gbeta, float gscale, float* ws, float* coef, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
+  int G = bigdl_bn_num_partials(M, C);
+  long long rpb = (M + G - 1) / G;
+  size_t sm = stats_smem(C);
+  if (relu)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
+                       (const bf16_t*)y, M, C, rpb, mean, ws, G);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
+                       (const bf16_t*)y, M, C, rpb, mean, ws, G);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, s, ws, G, M, C, gamma, mean, invstd,
+                     ggamma, gbeta, gscale, coef);
+  if (gx) {
+    int grid = apply_grid(M, C);
+    const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;
+    bf16_t *gx_ = (bf16_t*)gx, *gr_ = (bf16_t*)gres;
+    if (relu && gres) hipLaunchKernelGGL((k_bn_bwd_apply<true, true>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+    else if (relu) hipLaunchKernelGGL((k_bn_bwd_apply<true, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+    else if (gres) hipLaunchKernelGGL((k_bn_bwd_apply<false, true>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+    else hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

@@ -1,0 +1,222 @@
+// Elementwise kernels: dtype casts, ReLU/Threshold fwd+bwd (K8), fused optimizer updates (K22).
+// All are HBM-bound streaming kernels: 16 B per lane per access, grid-stride, grid capped at
+// 2048 blocks of 256 (cdna_hip_programming.md Guideline 11).
+#include "common.h"
+
+// ------------------------------------------------------------------------------------------------
+// casts
+// ------------------------------------------------------------------------------------------------
+__global__ void k_f32_to_bf16(const float* __restrict__ src, bf16_t* __restrict__ dst, long long n) {
+  long long n8 = n >> 3;
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float4 a = reinterpret_cast<const float4*>(src)[2 * i];
+    float4 b = reinterpret_cast<const float4*>(src)[2 * i + 1];
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    store8(dst + 8 * i, v);
+  }
+  for (long long i = (n8 << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = f2bf(src[i]);
+}
+
+__global__ void k_bf16_to_f32(const bf16_t* __restrict__ src, float* __restrict__ dst, long long n) {
+  long long n8 = n >> 3;
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float v[8];
+    load8(src + 8 * i, v);
+    reinterpret_cast<float4*>(dst)[2 * i] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(dst)[2 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  for (long long i = (n8 << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = bf2f(src[i]);
+}
+
+// mode 0: f32->bf16, 1: bf16->f32.  Pointers must be 16-B aligned (checked on the host).
+BIGDL_EXPORT int bigdl_cast(const void* src, void* dst, long long n, int mode, hipStream_t s) {
+  if (n <= 0) return 0;
+  int grid = bigdl_grid((n + 7) / 8, 256);
+  if (mode == 0)
+    hipLaunchKernelGGL(k_f32_to_bf16, dim3(grid), dim3(256), 0, s, (const float*)src, (bf16_t*)dst, n);
+  else
+    hipLaunchKernelGGL(k_bf16_to_f32, dim3(grid), dim3(256), 0, s, (const bf16_t*)src, (float*)dst, n);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// ReLU / Threshold (bf16): y = x > th ? x : v ; backward gx = gy * (ref > th)
+// ------------------------------------------------------------------------------------------------
+__global__ void k_threshold_fwd_bf16(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8, float th,
+                                     float val) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float v[8];
+    load8(x + 8 * i, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > th ? v[k] : val;
+    store8(y + 8 * i, v);
+  }
+}
+
+__global__ void k_threshold_bwd_bf16(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ ref,
+                                     bf16_t* __restrict__ gx, long long n8, float th) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float g[8], r[8];
+    load8(gy + 8 * i, g);
+    load8(ref + 8 * i, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = r[k] > th ? g[k] : 0.f;
+    store8(gx + 8 * i, g);
+  }
+}
+
+BIGDL_EXPORT int bigdl_threshold_fwd_bf16(const void* x, void* y, long long n, float th, float val, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 8) return (int)hipErrorInvalidValue;
+  long long n8 = n / 8;
+  hipLaunchKernelGGL(k_threshold_fwd_bf16, dim3(bigdl_grid(n8, 256)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+                     n8, th, val);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_threshold_bwd_bf16(const void* gy, const void* ref, void* gx, long long n, float th,
+                                          hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 8) return (int)hipErrorInvalidValue;
+  long long n8 = n / 8;
+  hipLaunchKernelGGL(k_threshold_bwd_bf16, dim3(bigdl_grid(n8, 256)), dim3(256), 0, s, (const bf16_t*)gy,
+                     (const bf16_t*)ref, (bf16_t*)gx, n8, th);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused SGD (DL/optim/SGD.scala:61-124) over a flat fp32 buffer:
+//   g' = g*scale (+ wd * wds * w) ; v = first ? g' : mom*v + (1-damp)*g' ;
+//   d = nesterov ? g' + mom*v : v (or g' when mom == 0) ; w -= lr * (lrs ? lrs*d : d) ;
+//   shadow = bf16(w)
+// ------------------------------------------------------------------------------------------------
+template <bool MOM, bool NEST, bool FIRST, bool SHADOW, bool PERELEM>
+__global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ buf,
+                      bf16_t* __restrict__ shadow, const float* __restrict__ lrs, const float* __restrict__ wds,
+                      long long n4, float lr, float mom, float damp, float wd, float scale) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 W = reinterpret_cast<float4*>(w)[i];
+    float4 G = reinterpret_cast<const float4*>(g)[i];
+    float wv[4] = {W.x, W.y, W.z, W.w};
+    float gv[4] = {G.x, G.y, G.z, G.w};
+    float wdv[4] = {1.f, 1.f, 1.f, 1.f};
+    float lrv[4] = {1.f, 1.f, 1.f, 1.f};
+    if (PERELEM) {
+      if (wds) {
+        float4 t = reinterpret_cast<const float4*>(wds)[i];
+        wdv[0] = t.x; wdv[1] = t.y; wdv[2] = t.z; wdv[3] = t.w;
+      }
+      if (lrs) {
+        float4 t = reinterpret_cast<const float4*>(lrs)[i];
+        lrv[0] = t.x; lrv[1] = t.y; lrv[2] = t.z; lrv[3] = t.w;
+      }
+    }
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (MOM && !FIRST) {
+      float4 B = reinterpret_cast<float4*>(buf)[i];
+      bv[0] = B.x; bv[1] = B.y; bv[2] = B.z; bv[3] = B.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = gv[k] * scale + wd * wdv[k] * wv[k];
+      float d = gg;
+      if (MOM) {
+        bv[k] = FIRST ? gg : mom * bv[k] + (1.f - damp) * gg;
+        d = NEST ? gg + mom * bv[k] : bv[k];
+      }
+      wv[k] -= lr * lrv[k] * d;
+    }
+    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    if (MOM) reinterpret_cast<float4*>(buf)[i] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+    if (SHADOW) {
+      uint32_t lo = (uint32_t)f2bf(wv[0]) | ((uint32_t)f2bf(wv[1]) << 16);
+      uint32_t hi = (uint32_t)f2bf(wv[2]) | ((uint32_t)f2bf(wv[3]) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
+    }
+  }
+}
+
+#define SGD_LAUNCH(M, NS, F, SH, PE)                                                                    \
+  hipLaunchKernelGGL((k_sgd<M, NS, F, SH, PE>), dim3(grid), dim3(256), 0, s, w, g, buf, shadow, lrs, wds, n4, lr, \
+                     mom, damp, wd, scale)
+
+// n must be a multiple of 4 and all pointers 16-B aligned (host-checked).
+BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
+                           long long n, float lr, float mom, float damp, float wd, int nesterov, int first,
+                           float scale, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 4) return (int)hipErrorInvalidValue;
+  long long n4 = n / 4;
+  int grid = bigdl_grid(n4, 256);
+  bool M = mom != 0.f, NS = nesterov != 0, F = first != 0, SH = shadow != nullptr, PE = (lrs || wds);
+  // dispatch the common combinations without per-element branches
+  if (!PE) {
+    if (M && NS && !F && SH) SGD_LAUNCH(true, true, false, true, false);
+    else if (M && NS && !F && !SH) SGD_LAUNCH(true, true, false, false, false);
+    else if (M && !NS && !F && SH) SGD_LAUNCH(true, false, false, true, false);
+    else if (M && !NS && !F && !SH) SGD_LAUNCH(true, false, false, false, false);
+    else if (M && NS && F && SH) SGD_LAUNCH(true, true, true, true, false);
+    else if (M && NS && F && !SH) SGD_LAUNCH(true, true, true, false, false);
+    else if (M && !NS && F && SH) SGD_LAUNCH(true, false, true, true, false);
+    else if (M && !NS && F && !SH) SGD_LAUNCH(true, false, true, false, false);
+    else if (!M && SH) SGD_LAUNCH(false, false, false, true, false);
+    else SGD_LAUNCH(false, false, false, false, false);
+  } else {
+    if (M && NS && F) SGD_LAUNCH(true, true, true, true, true);
+    else if (M && NS) SGD_LAUNCH(true, true, false, true, true);
+    else if (M && F) SGD_LAUNCH(true, false, true, true, true);
+    else if (M) SGD_LAUNCH(true, false, false, true, true);
+    else SGD_LAUNCH(false, false, false, true, true);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused Adam (DL/optim/Adam.scala): m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g² ;
+// w -= step_size * m / (sqrt(v) + eps), step_size = lr * sqrt(1-b2^t) / (1-b1^t)
+// ------------------------------------------------------------------------------------------------
+__global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, bf16_t* __restrict__ shadow, long long n4, float step_size, float b1,
+                       float b2, float eps, float wd, float scale) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 W = reinterpret_cast<float4*>(w)[i];
+    float4 G = reinterpret_cast<const float4*>(g)[i];
+    float4 M = reinterpret_cast<float4*>(m)[i];
+    float4 V = reinterpret_cast<float4*>(v)[i];
+    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w};
+    float mv[4] = {M.x, M.y, M.z, M.w}, vv[4] = {V.x, V.y, V.z, V.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = gv[k] * scale + wd * wv[k];
+      mv[k] = b1 * mv[k] + (1.f - b1) * gg;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gg * gg;
+      wv[k] -= step_size * mv[k] / (sqrtf(vv[k]) + eps);
+    }
+    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (shadow) {
+      uint32_t lo = (uint32_t)f2bf(wv[0]) | ((uint32_t)f2bf(wv[1]) << 16);
+      uint32_t hi = (uint32_t)f2bf(wv[2]) | ((uint32_t)f2bf(wv[3]) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
+    }
+  }
+}
+
+BIGDL_EXPORT int bigdl_adam(float* w, const float* g, float* m, float* v, bf16_t* shadow, long long n,
+                            float step_size, float b1, float b2, float eps, float wd, float scale, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 4) return (int)hipErrorInvalidValue;
+  long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adam, dim3(bigdl_grid(n4, 256)), dim3(256), 0, s, w, g, m, v, shadow, n4, step_size, b1, b2,
+                     eps, wd, scale);
+  BIGDL_CHECK_LAUNCH();
+}

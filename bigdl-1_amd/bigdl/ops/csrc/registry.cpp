@@ -1,0 +1,18 @@
+// Names of the native ops compiled into libbigdl_kernels.so (reported by bigdl.ops.native_status()).
+#include <hip/hip_runtime.h>
+
+static const char* kOps[] = {
+    "cast", "threshold_fwd_bf16", "threshold_bwd_bf16", "sgd", "adam", "bn_fwd_train", "bn_fwd_infer", "bn_bwd",
+    "cross_entropy", "logsoftmax",
+};
+
+extern "C" __attribute__((visibility("default"))) int bigdl_num_ops() {
+  return (int)(sizeof(kOps) / sizeof(kOps[0]));
+}
+
+extern "C" __attribute__((visibility("default"))) const char* bigdl_op_name(int i) {
+  int n = bigdl_num_ops();
+  return (i >= 0 && i < n) ? kOps[i] : "";
+}
+
+extern "C" __attribute__((visibility("default"))) int bigdl_device_sync() { return (int)hipDeviceSynchronize(); }

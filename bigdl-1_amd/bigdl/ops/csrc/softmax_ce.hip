@@ -1,0 +1,161 @@
+// Fused LogSoftMax + ClassNLL (CrossEntropyCriterion, K12+K13) and row-wise (log-)softmax.
+//
+// Reference: DL/nn/CrossEntropyCriterion.scala (LogSoftMax + ClassNLLCriterion), ClassNLLCriterion
+// .scala:89-230 — targets are 1-BASED class indices, a target equal to paddingValue contributes
+// nothing, optional per-class weights, sizeAverage divides by Σ weights (or the valid count).
+// One block (256 threads = 4 waves) per row; the row is read twice (max/sum pass, then gradient).
+#include "common.h"
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p, long long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, long long i) { return bf2f(p[i]); }
+
+template <typename T>
+__device__ __forceinline__ void st(T* p, long long i, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, long long i, float v) { p[i] = v; }
+template <>
+__device__ __forceinline__ void st<bf16_t>(bf16_t* p, long long i, float v) { p[i] = f2bf(v); }
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  __syncthreads();
+  return r;
+}
+
+// per row: lse, row loss (weighted), row weight
+template <typename T>
+__global__ void __launch_bounds__(256) k_ce_rows(const T* __restrict__ x, const int* __restrict__ tgt,
+                                                 const float* __restrict__ cw, int K, int padding,
+                                                 float* __restrict__ lse, float* __restrict__ rloss,
+                                                 float* __restrict__ rw) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  const T* xr = x + row * K;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) m = fmaxf(m, ld(xr, i));
+  m = block_reduce(m, red, true);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) s += __expf(ld(xr, i) - m);
+  s = block_reduce(s, red, false);
+  if (threadIdx.x == 0) {
+    float l = m + __logf(s);
+    lse[row] = l;
+    int t = tgt[row];
+    bool valid = t != padding && t >= 1 && t <= K;
+    float w = valid ? (cw ? cw[t - 1] : 1.f) : 0.f;
+    rw[row] = w;
+    rloss[row] = valid ? -(ld(xr, t - 1) - l) * w : 0.f;
+  }
+}
+
+// total loss and denominator (single block, deterministic order)
+__global__ void k_ce_total(const float* __restrict__ rloss, const float* __restrict__ rw, long long B, int size_avg,
+                           float* __restrict__ out) {
+  __shared__ float red[8];
+  float a = 0.f, b = 0.f;
+  for (long long i = threadIdx.x; i < B; i += blockDim.x) {
+    a += rloss[i];
+    b += rw[i];
+  }
+  a = block_reduce(a, red, false);
+  b = block_reduce(b, red, false);
+  if (threadIdx.x == 0) {
+    float denom = size_avg ? fmaxf(b, 1e-12f) : 1.f;
+    out[0] = a / denom;
+    out[1] = denom;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_ce_grad(const T* __restrict__ x, const int* __restrict__ tgt,
+                                                 const float* __restrict__ lse, const float* __restrict__ rw,
+                                                 const float* __restrict__ tot, int K, T* __restrict__ gx) {
+  const long long row = blockIdx.x;
+  const T* xr = x + row * K;
+  T* gr = gx + row * K;
+  const float scale = rw[row] / tot[1];
+  const float l = lse[row];
+  const int t = tgt[row] - 1;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) {
+    float p = __expf(ld(xr, i) - l);
+    st(gr, i, scale * (p - (i == t ? 1.f : 0.f)));
+  }
+}
+
+// dtype: 0 fp32, 1 bf16.  ws: 3·B floats; out: 2 floats (loss, denom).
+BIGDL_EXPORT int bigdl_cross_entropy(const void* x, const int* tgt, const float* cw, void* gx, long long B, int K,
+                                     int padding, int size_avg, int dtype, float* ws, float* out, hipStream_t s) {
+  if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  float *lse = ws, *rl = ws + B, *rw = ws + 2 * B;
+  if (dtype == 1) {
+    hipLaunchKernelGGL(k_ce_rows<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, cw, K, padding, lse, rl, rw);
+  } else {
+    hipLaunchKernelGGL(k_ce_rows<float>, dim3(B), dim3(256), 0, s, (const float*)x, tgt, cw, K, padding, lse, rl, rw);
+  }
+  hipLaunchKernelGGL(k_ce_total, dim3(1), dim3(256), 0, s, rl, rw, B, size_avg, out);
+  if (gx) {
+    if (dtype == 1)
+      hipLaunchKernelGGL(k_ce_grad<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, lse, rw, out, K,
+                         (bf16_t*)gx);
+    else
+      hipLaunchKernelGGL(k_ce_grad<float>, dim3(B), dim3(256), 0, s, (const float*)x, tgt, lse, rw, out, K,
+                         (float*)gx);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// row-wise log-softmax forward / backward (LogSoftMax.scala:49-130) over the last dim
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) k_logsoftmax_fwd(const T* __restrict__ x, T* __restrict__ y, int K) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  const T* xr = x + row * K;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) m = fmaxf(m, ld(xr, i));
+  m = block_reduce(m, red, true);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) s += __expf(ld(xr, i) - m);
+  s = block_reduce(s, red, false);
+  float l = m + __logf(s);
+  for (int i = threadIdx.x; i < K; i += blockDim.x) st(y + row * K, i, ld(xr, i) - l);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_logsoftmax_bwd(const T* __restrict__ gy, const T* __restrict__ y,
+                                                        T* __restrict__ gx, int K) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) s += ld(gy + row * K, i);
+  s = block_reduce(s, red, false);
+  for (int i = threadIdx.x; i < K; i += blockDim.x)
+    st(gx + row * K, i, ld(gy + row * K, i) - __expf(ld(y + row * K, i)) * s);
+}
+
+BIGDL_EXPORT int bigdl_logsoftmax(const void* a, const void* b, void* out, long long rows, int K, int backward,
+                                  int dtype, hipStream_t s) {
+  if (rows <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (!backward) {
+    if (dtype == 1) hipLaunchKernelGGL(k_logsoftmax_fwd<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)a, (bf16_t*)out, K);
+    else hipLaunchKernelGGL(k_logsoftmax_fwd<float>, dim3(rows), dim3(256), 0, s, (const float*)a, (float*)out, K);
+  } else {
+    if (dtype == 1)
+      hipLaunchKernelGGL(k_logsoftmax_bwd<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
+                         (bf16_t*)out, K);
+    else
+      hipLaunchKernelGGL(k_logsoftmax_bwd<float>, dim3(rows), dim3(256), 0, s, (const float*)a, (const float*)b,
+                         (float*)out, K);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

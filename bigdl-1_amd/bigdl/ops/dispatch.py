@@ -1,0 +1,55 @@
+"""Device dispatch for the hot ops: native HIP kernels for GPU tensors, reference otherwise."""
+from __future__ import annotations
+
+import torch
+
+from . import reference as R
+from . import native as N
+
+__all__ = [
+    "cast_copy", "relu_forward", "relu_backward",
+    "conv2d_forward", "conv2d_backward", "conv_transpose2d_forward",
+    "batchnorm_forward_train", "batchnorm_forward_infer", "batchnorm_backward",
+    "maxpool2d_forward", "maxpool2d_backward", "avgpool2d_forward", "avgpool2d_backward",
+    "linear_forward", "linear_backward",
+    "log_softmax_forward", "log_softmax_backward", "softmax_forward", "softmax_backward",
+    "class_nll_forward", "class_nll_backward", "cross_entropy_fused",
+    "sgd_step", "adam_step", "lstm_cell_forward", "lstm_cell_backward",
+    "embedding_forward", "embedding_backward", "dropout_forward", "dropout_backward", "lrn_forward",
+]
+
+
+def native_status() -> dict:
+    return N.status()
+
+
+def _nat(t: torch.Tensor, opname: str) -> bool:
+    """True → use the native kernel for this op on this tensor."""
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        return False
+    return N.has(opname)
+
+
+def _g(opname):
+    nat = getattr(N, opname, None)
+    ref = getattr(R, opname)
+
+    def f(*args, **kwargs):
+        t = None
+        for a in args:
+            if isinstance(a, torch.Tensor):
+                t = a
+                break
+        if nat is not None and t is not None and _nat(t, opname):
+            r = nat(*args, **kwargs)
+            if r is not NotImplemented:
+                return r
+        return ref(*args, **kwargs)
+
+    f.__name__ = opname
+    f.__doc__ = ref.__doc__
+    return f
+
+
+for _name in __all__:
+    globals()[_name] = _g(_name)

@@ -1,0 +1,105 @@
+"""ctypes bindings to ``libbigdl_kernels.so`` (hand-written HIP/CDNA4 kernels, gfx950).
+
+The library is built in-tree by ``bigdl/ops/build.py`` (``hipcc --offload-arch=gfx950``) into
+``bigdl/ops/lib/``.  Kernels take raw device pointers plus the current HIP stream of the torch
+caching allocator, so they interleave with torch ops and are capturable in HIP graphs.
+
+Each Python wrapper validates shapes/strides on the host BEFORE launching (a mis-shaped launch
+must never reach the GPU), and returns ``NotImplemented`` for a configuration the kernel does not
+cover so the dispatcher can fall back explicitly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+from ..utils import config
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbigdl_kernels.so")
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+_ops_available: set = set()
+
+
+def _load():
+    global _lib, _load_error
+    if _lib is not None or _load_error is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"{LIB_PATH} not built (run python -m bigdl.ops.build)"
+        return None
+    try:
+        _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - depends on box
+        _load_error = str(e)
+        return None
+    _declare(_lib)
+    return _lib
+
+
+def _declare(lib):
+    # every exported symbol returns int (hipError_t) and takes void*/int64/float args
+    names = []
+    try:
+        lib.bigdl_op_name.restype = ctypes.c_char_p
+        n = lib.bigdl_num_ops()
+        for i in range(n):
+            names.append(lib.bigdl_op_name(i).decode())
+    except AttributeError:
+        pass
+    _ops_available.update(names)
+
+
+def status() -> dict:
+    _load()
+    return {"library": LIB_PATH, "loaded": _lib is not None, "error": _load_error,
+            "ops": sorted(_ops_available)}
+
+
+def lib():
+    l = _load()
+    if l is None and torch.cuda.is_available() and config.get_property("bigdl.native.require"):
+        raise RuntimeError(f"bigdl native HIP kernels are required on a GPU but not loaded: {_load_error}")
+    return l
+
+
+def has(opname: str) -> bool:
+    l = _load()
+    if l is None:
+        if torch.cuda.is_available() and config.get_property("bigdl.native.require"):
+            raise RuntimeError(f"bigdl native HIP kernels are required on a GPU but not loaded: {_load_error}")
+        return False
+    return opname in _PY_OPS
+
+
+# Python-level op wrappers registered below (populated by kernels.py once written)
+_PY_OPS: dict = {}
+
+
+def register(name):
+    def deco(fn):
+        _PY_OPS[name] = fn
+        globals()[name] = fn
+        return fn
+    return deco
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"bigdl HIP kernel {what} failed with hipError {rc}")
+
+
+from . import native_ops  # noqa: E402,F401  (registers wrappers)

@@ -1,0 +1,353 @@
+"""Reference implementations of every hot op, on plain torch.
+
+These are (a) the CPU execution path (config 1 — LeNet LocalOptimizer — runs without a GPU) and
+(b) the fp32 ORACLES that the native HIP kernels in ``bigdl/ops/csrc`` are tested against.
+Semantics follow the reference layers cited per function.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+aten = torch.ops.aten
+
+
+# ------------------------------------------------------------------------- casts / elementwise
+def cast_copy(dst: torch.Tensor, src: torch.Tensor):
+    dst.copy_(src.reshape(dst.shape) if src.shape != dst.shape else src)
+    return dst
+
+
+def relu_forward(x: torch.Tensor, threshold: float = 0.0, value: float = 0.0, inplace=False):
+    """``Threshold.updateOutput`` (``DL/nn/Threshold.scala:46``): y = x > th ? x : value."""
+    if threshold == 0.0 and value == 0.0:
+        return torch.relu_(x) if inplace else torch.relu(x)
+    y = torch.where(x > threshold, x, torch.full_like(x, value))
+    if inplace:
+        x.copy_(y)
+        return x
+    return y
+
+
+def relu_backward(gy: torch.Tensor, y_or_x: torch.Tensor, threshold: float = 0.0):
+    return gy * (y_or_x > threshold).to(gy.dtype)
+
+
+# ------------------------------------------------------------------------- convolution
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+    """``SpatialConvolution.updateOutput`` (``DL/nn/SpatialConvolution.scala:253-362``).
+
+    ``w4`` is (O, I/g, kH, kW); ``pad`` is (padH, padW) after SAME resolution.
+    """
+    return F.conv2d(x, w4.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dilation, groups)
+
+
+def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
+                    gb_acc=None, scale=1.0):
+    """``SpatialConvolution.updateGradInput`` + ``accGradParameters`` (``:364-505``).
+
+    Returns gradInput (or None); ACCUMULATES ``scale·dW`` into ``gw_acc`` (O, I/g, kH, kW view,
+    fp32) and ``scale·db`` into ``gb_acc``."""
+    gy = gy.to(x.dtype)
+    need_w = gw_acc is not None and scale != 0
+    need_b = gb_acc is not None and scale != 0
+    gi, gw, gb = aten.convolution_backward(gy, x, w4.to(x.dtype), [w4.shape[0]] if need_b else None,
+                                           list(stride), list(pad), list(dilation), False, [0, 0], groups,
+                                           [need_input, need_w, need_b])
+    if need_w:
+        gw_acc.add_(gw.float(), alpha=scale)
+    if need_b:
+        gb_acc.add_(gb.float(), alpha=scale)
+    return gi
+
+
+def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups=1):
+    return F.conv_transpose2d(x, w4.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, adj, groups,
+                              dilation)
+
+
+# ------------------------------------------------------------------------- batch norm
+def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None):
+    """Training BN (``SpatialBatchNormalization.updateOutputNCHWTrainFloat``, ``:1211``).
+
+    Normalises with the biased variance, updates ``runningVar`` with the UNBIASED variance and
+    momentum 0.1 by default (``DL/nn/BatchNormalization.scala:53-54, 85-88``).
+    Returns (y, save_mean, save_invstd).  Optional fused residual add and ReLU (K9).
+    """
+    C = x.shape[1]
+    dims = [d for d in range(x.dim()) if d != 1]
+    xf = x.float()
+    n = x.numel() // C
+    mean = xf.mean(dim=dims)
+    var = xf.var(dim=dims, unbiased=False)
+    invstd = torch.rsqrt(var + eps)
+    if running_mean is not None:
+        with torch.no_grad():
+            unbiased = var * (n / max(n - 1, 1))
+            running_mean.mul_(1 - momentum).add_(mean, alpha=momentum)
+            running_var.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+    shape = [1, C] + [1] * (x.dim() - 2)
+    g = gamma.float().view(shape) if gamma is not None else 1.0
+    bb = beta.float().view(shape) if beta is not None else 0.0
+    y = (xf - mean.view(shape)) * invstd.view(shape) * g + bb
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype), mean, invstd
+
+
+def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False):
+    C = x.shape[1]
+    shape = [1, C] + [1] * (x.dim() - 2)
+    invstd = torch.rsqrt(running_var.float() + eps)
+    scale = invstd * (gamma.float() if gamma is not None else 1.0)
+    shift = (beta.float() if beta is not None else 0.0) - running_mean.float() * scale
+    y = x.float() * scale.view(shape) + shift.view(shape)
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, need_input=True, gg_acc=None,
+                       gb_acc=None, scale=1.0):
+    """Returns (gradInput, gradGamma, gradBeta) — ``updateGradInputNCHWTrainFloat`` (:1048) and
+    ``accGradientNCHWFloat`` (:1970).  With ``relu`` the ReLU mask is taken from ``y`` (the BN+ReLU
+    output) and fused in (K7/K8)."""
+    C = x.shape[1]
+    dims = [d for d in range(x.dim()) if d != 1]
+    shape = [1, C] + [1] * (x.dim() - 2)
+    g = gy.float()
+    if relu:
+        g = g * (y > 0).float()
+    xhat = (x.float() - save_mean.view(shape)) * save_invstd.view(shape)
+    dbeta = g.sum(dim=dims)
+    dgamma = (g * xhat).sum(dim=dims)
+    gi = None
+    if need_input:
+        n = x.numel() // C
+        gam = gamma.float().view(shape) if gamma is not None else 1.0
+        gi = (gam * save_invstd.view(shape) / n) * (n * g - dbeta.view(shape) - xhat * dgamma.view(shape))
+        gi = gi.to(x.dtype)
+    if gg_acc is not None and scale != 0:
+        gg_acc.add_(dgamma, alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(dbeta, alpha=scale)
+    return gi
+
+
+# ------------------------------------------------------------------------- pooling
+def maxpool2d_forward(x, k, s, p, ceil_mode):
+    y, idx = F.max_pool2d(x, k, s, p, 1, ceil_mode, return_indices=True)
+    return y, idx
+
+
+def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
+    return aten.max_pool2d_with_indices_backward(gy, x, list(k), list(s), list(p), [1, 1], ceil_mode, idx)
+
+
+def avgpool2d_forward(x, k, s, p, ceil_mode, count_include_pad, divisor=None):
+    return F.avg_pool2d(x, k, s, p, ceil_mode, count_include_pad, divisor)
+
+
+def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=None):
+    return aten.avg_pool2d_backward(gy, x, list(k), list(s), list(p), ceil_mode, count_include_pad, divisor)
+
+
+# ------------------------------------------------------------------------- linear
+def linear_forward(x, w, b):
+    """``Linear.updateOutput`` (``DL/nn/Linear.scala:108-109``): y = x Wᵀ + b."""
+    y = x @ w.to(x.dtype).t()
+    if b is not None:
+        y = y + b.to(y.dtype)
+    return y
+
+
+def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1.0):
+    """``Linear.scala:128-158``: gradInput = gy·W; gradWeight += scale·gyᵀx; gradBias += scale·Σgy."""
+    gi = gy @ w.to(gy.dtype) if need_input else None
+    if gw_acc is not None and scale != 0:
+        gw_acc.add_(gy.float().t() @ x.float(), alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.float().sum(0), alpha=scale)
+    return gi
+
+
+# ------------------------------------------------------------------------- softmax / criteria
+def log_softmax_forward(x):
+    """Row-wise log-softmax over the last dim (``DL/nn/LogSoftMax.scala:49-130``)."""
+    return torch.log_softmax(x.float(), dim=-1).to(x.dtype)
+
+
+def log_softmax_backward(gy, y):
+    gyf = gy.float()
+    return (gyf - torch.exp(y.float()) * gyf.sum(-1, keepdim=True)).to(y.dtype)
+
+
+def softmax_forward(x):
+    return torch.softmax(x.float(), dim=-1).to(x.dtype)
+
+
+def softmax_backward(gy, y):
+    gyf, yf = gy.float(), y.float()
+    return (yf * (gyf - (gyf * yf).sum(-1, keepdim=True))).to(y.dtype)
+
+
+def class_nll_forward(logp, target_1b, weights=None, size_average=True, padding_value=-1):
+    """``ClassNLLCriterion.updateOutput`` (``DL/nn/ClassNLLCriterion.scala:89-170``): 1-based
+    targets, targets equal to ``paddingValue`` contribute nothing."""
+    if logp.dim() == 1:
+        logp = logp.unsqueeze(0)
+        target_1b = target_1b.reshape(1)
+    t = target_1b.long().reshape(-1)
+    valid = t != padding_value
+    idx = torch.where(valid, t - 1, torch.zeros_like(t))
+    picked = logp.float().gather(1, idx.unsqueeze(1)).squeeze(1)
+    w = weights.float()[idx] if weights is not None else torch.ones_like(picked)
+    w = w * valid.float()
+    total = -(picked * w).sum()
+    if size_average:
+        denom = w.sum()
+        total = total / torch.clamp(denom, min=1e-12) if weights is not None else total / torch.clamp(valid.float().sum(), min=1)
+    return total
+
+
+def class_nll_backward(logp, target_1b, weights=None, size_average=True, padding_value=-1):
+    squeeze = logp.dim() == 1
+    lp = logp.unsqueeze(0) if squeeze else logp
+    t = target_1b.long().reshape(-1)
+    valid = t != padding_value
+    idx = torch.where(valid, t - 1, torch.zeros_like(t))
+    w = weights.float()[idx] if weights is not None else torch.ones(t.shape[0], device=lp.device)
+    w = w * valid.float()
+    if size_average:
+        denom = w.sum() if weights is not None else valid.float().sum()
+        w = w / torch.clamp(denom, min=1e-12 if weights is not None else 1)
+    g = torch.zeros(lp.shape, dtype=torch.float32, device=lp.device)
+    g.scatter_(1, idx.unsqueeze(1), (-w).unsqueeze(1))
+    g = g.to(logp.dtype)
+    return g.squeeze(0) if squeeze else g
+
+
+def cross_entropy_fused(x, target_1b, weights=None, size_average=True, padding_value=-1):
+    """Fused LogSoftMax + ClassNLL (K12+K13): returns (loss, grad_x)."""
+    logp = torch.log_softmax(x.float(), dim=-1)
+    loss = class_nll_forward(logp, target_1b, weights, size_average, padding_value)
+    gl = class_nll_backward(logp, target_1b, weights, size_average, padding_value).float()
+    gx = gl - torch.exp(logp) * gl.sum(-1, keepdim=True)
+    return loss, gx.to(x.dtype)
+
+
+# ------------------------------------------------------------------------- optimizer
+def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale=1.0,
+             shadow=None, lrs=None, wds=None):
+    """Fused SGD (``DL/optim/SGD.scala:61-124``): g += wd·x; v = μv + (1-d)g; nesterov; x -= lr·v.
+
+    ``grad_scale`` folds the 1/N gradient averaging in; ``lrs``/``wds`` are per-element
+    learning-rate / weight-decay multipliers (``learningRates``/``weightDecays``)."""
+    gg = g * grad_scale if grad_scale != 1.0 else g.clone()
+    if weight_decay != 0:
+        gg.add_(w * (wds if wds is not None else 1.0), alpha=weight_decay)
+    if momentum != 0:
+        if first_step:
+            buf.copy_(gg)
+        else:
+            buf.mul_(momentum).add_(gg, alpha=1 - dampening)
+        if nesterov:
+            gg = gg.add(buf, alpha=momentum)
+        else:
+            gg = buf
+    if lrs is not None:
+        w.add_(gg * lrs, alpha=-lr)
+    else:
+        w.add_(gg, alpha=-lr)
+    if shadow is not None:
+        shadow.copy_(w)
+    return w
+
+
+def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0, shadow=None):
+    """``DL/optim/Adam.scala``: bias-corrected Adam."""
+    gg = g * grad_scale
+    if weight_decay != 0:
+        gg = gg + weight_decay * w
+    m.mul_(beta1).add_(gg, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(gg, gg, value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    step_size = lr * math.sqrt(bc2) / bc1
+    w.addcdiv_(m, v.sqrt().add_(eps), value=-step_size)
+    if shadow is not None:
+        shadow.copy_(w)
+    return w
+
+
+# ------------------------------------------------------------------------- recurrent
+def lstm_cell_forward(gates, c_prev):
+    """Pointwise LSTM cell (``DL/nn/LSTM.scala:124-187``), gate order (i, g, f, o) along the
+    last dim in blocks of H: i=σ, g=tanh, f=σ, o=σ; c' = i·g + f·c; h' = o·tanh(c')."""
+    H = c_prev.shape[-1]
+    gf = gates.float()
+    i = torch.sigmoid(gf[..., 0:H])
+    g = torch.tanh(gf[..., H:2 * H])
+    f = torch.sigmoid(gf[..., 2 * H:3 * H])
+    o = torch.sigmoid(gf[..., 3 * H:4 * H])
+    c = i * g + f * c_prev.float()
+    tc = torch.tanh(c)
+    h = o * tc
+    act = torch.cat([i, g, f, o], dim=-1)
+    return h.to(gates.dtype), c, act, tc
+
+
+def lstm_cell_backward(gh, gc_next, act, tc, c_prev):
+    H = c_prev.shape[-1]
+    i, g, f, o = act[..., 0:H], act[..., H:2 * H], act[..., 2 * H:3 * H], act[..., 3 * H:]
+    gh = gh.float()
+    dc = gh * o * (1 - tc * tc) + (gc_next.float() if gc_next is not None else 0.0)
+    do = gh * tc
+    di = dc * g
+    dg = dc * i
+    df = dc * c_prev.float()
+    dc_prev = dc * f
+    dgates = torch.cat([di * i * (1 - i), dg * (1 - g * g), df * f * (1 - f), do * o * (1 - o)], dim=-1)
+    return dgates, dc_prev
+
+
+# ------------------------------------------------------------------------- embedding / dropout / lrn
+def embedding_forward(weight, idx_1b, padding_value=0):
+    idx = idx_1b.long() - 1
+    return weight[idx.clamp(min=0)]
+
+
+def embedding_backward(grad_weight, idx_1b, gy, scale=1.0, padding_value=0):
+    idx = (idx_1b.long() - 1).reshape(-1)
+    g = gy.reshape(idx.numel(), -1).float() * scale
+    if padding_value != 0:
+        keep = (idx_1b.reshape(-1).long() != padding_value)
+        idx = idx[keep]
+        g = g[keep]
+    grad_weight.index_add_(0, idx, g.to(grad_weight.dtype))
+
+
+def dropout_forward(x, p, generator=None):
+    """``DL/nn/Dropout.scala:64-150``: drop with probability p, scale kept values by 1/(1-p)."""
+    if p <= 0:
+        return x.clone(), None
+    mask = (torch.rand(x.shape, device=x.device, generator=generator) >= p)
+    scale = 1.0 / (1.0 - p)
+    return x * mask.to(x.dtype) * scale, mask
+
+
+def dropout_backward(gy, mask, p):
+    if mask is None:
+        return gy.clone()
+    return gy * mask.to(gy.dtype) * (1.0 / (1.0 - p))
+
+
+def lrn_forward(x, size, alpha, beta, k):
+    """``SpatialCrossMapLRN`` (``DL/nn/SpatialCrossMapLRN.scala:96-200``):
+    y = x / (k + α/size · Σ_{window} x²)^β."""
+    return F.local_response_norm(x, size, alpha, beta, k)

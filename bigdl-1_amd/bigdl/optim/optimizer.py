@@ -1,0 +1,553 @@
+"""Training drivers: ``Optimizer`` builder, ``LocalOptimizer``.
+
+Reference: ``DL/optim/Optimizer.scala:47-699`` (builder setters 93-470; ``apply`` 602-681),
+``AbstractOptimizer.scala:30-286`` (summary 47-91, validate 93-191, checkpoint 205-231),
+``LocalOptimizer.scala:45-295`` and the retry loop of ``DistriOptimizer.scala:881-963``.
+
+Loop per iteration (one device, or one rank of :class:`bigdl.parallel.DistriOptimizer`)::
+
+    zero grads (one memset of the flat grad arena)
+    forward → criterion forward/backward → backward       (explicit Module contract)
+    gradient hooks: bucketed reduce-scatter (distributed only, overlapped with backward)
+    clipping (constant / global L2 norm, X9)
+    OptimMethod update(s) on the flat arena or this rank's shard (fused HIP kernel, K22)
+    all-gather of updated weights (distributed only; waited for lazily by the next forward)
+
+The hot loop never synchronises the host with the device: the loss stays on the GPU and is read
+back one iteration late through a pinned buffer, so the host enqueues step i+1 while step i runs.
+The canonical log line (``DistriOptimizer.scala:411-416``) is kept.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from ..dataset.core import (AbstractDataSet, DataSet, DevicePrefetcher, MiniBatch, SampleToMiniBatch,
+                            TransformedDataSet)
+from ..nn.abstractnn import AbstractModule, AbstractCriterion, to_torch
+from ..utils import config
+from ..utils.engine import Engine
+from ..utils.logger import get_logger, iteration_line
+from ..utils.table import Table
+from .metrics import Metrics
+from .optim_method import OptimMethod, SGD
+from .trigger import Trigger, MaxEpoch
+from .validation import ValidationMethod, allreduce_results
+
+log = get_logger("bigdl.optim")
+
+
+class _LazyScalar:
+    """Device scalar read back asynchronously (pinned host copy + event)."""
+
+    def __init__(self, t: torch.Tensor):
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            self.host = torch.empty((), dtype=torch.float32, pin_memory=True)
+            self.host.copy_(t.detach().float(), non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+            self.v = None
+        else:
+            self.ev = None
+            self.v = float(t)
+
+    def ready(self) -> bool:
+        return self.ev is None or self.ev.query()
+
+    def value(self) -> float:
+        if self.v is None:
+            self.ev.synchronize()
+            self.v = float(self.host)
+        return self.v
+
+
+class BaseOptimizer:
+    """Builder + loop shared by the local and distributed drivers."""
+
+    def __init__(self, model: AbstractModule, dataset, criterion: AbstractCriterion, batch_size: int = 32):
+        self.model = model
+        self.criterion = criterion
+        self.batch_size = batch_size
+        self.dataset = self._as_dataset(dataset, batch_size)
+        self.optim_methods: Dict[str, OptimMethod] = {model.get_name(): SGD()}
+        self.end_when: Trigger = MaxEpoch(1)
+        self.state = {"epoch": 1, "neval": 1, "recordsProcessedThisEpoch": 0, "Loss": float("nan"),
+                      "score": 0.0}
+        self.validation_trigger = None
+        self.validation_set = None
+        self.validation_methods: List[ValidationMethod] = []
+        self.checkpoint_trigger = None
+        self.checkpoint_path = None
+        self.is_overwrite = False
+        self.train_summary = None
+        self.validation_summary = None
+        self.constant_clip = None
+        self.l2_clip = None
+        self.drop_percentage = 0.0
+        self.reserve_optim_state = False
+        self.metrics = Metrics()
+        self.log_interval = 1
+        self.device = Engine.device()
+        self.compute_dtype = Engine.compute_dtype()
+        self._pending_loss: Optional[_LazyScalar] = None
+
+    # ------------------------------------------------------------------------------ data helpers
+    @staticmethod
+    def _as_dataset(ds, batch_size):
+        if ds is None:
+            return None
+        if isinstance(ds, AbstractDataSet):
+            return ds
+        if isinstance(ds, (list, tuple)):
+            items = list(ds)
+            if items and isinstance(items[0], MiniBatch):
+                return DataSet.array(items)
+            return DataSet.array(items).transform(SampleToMiniBatch(batch_size))
+        raise TypeError(f"unsupported training data {type(ds)}")
+
+    # ------------------------------------------------------------------------------ builder setters
+    def setValidation(self, trigger, dataset, vmethods, batch_size=None):
+        self.validation_trigger = trigger
+        self.validation_set = self._as_dataset(dataset, batch_size or self.batch_size)
+        self.validation_methods = list(vmethods)
+        return self
+
+    set_validation = setValidation
+
+    def setCheckpoint(self, path, trigger, is_overwrite=False):
+        stamp = time.strftime("%Y%m%d_%H%M%S")
+        self.checkpoint_path = os.path.join(path, stamp) if not os.environ.get("BIGDL_CKPT_FLAT") else path
+        self.checkpoint_trigger = trigger
+        self.is_overwrite = is_overwrite
+        if Engine.rank() == 0:
+            os.makedirs(self.checkpoint_path, exist_ok=True)
+        return self
+
+    def set_checkpoint(self, checkpoint_trigger, checkpoint_path, isOverWrite=True):
+        return self.setCheckpoint(checkpoint_path, checkpoint_trigger, isOverWrite)
+
+    def overWriteCheckpoint(self):
+        self.is_overwrite = True
+        return self
+
+    def setTrainSummary(self, summary):
+        self.train_summary = summary
+        return self
+
+    set_train_summary = setTrainSummary
+
+    def setValidationSummary(self, summary):
+        self.validation_summary = summary
+        return self
+
+    set_val_summary = setValidationSummary
+
+    def setModel(self, model):
+        self.model = model
+        return self
+
+    def setTrainData(self, dataset, batch_size=None):
+        self.dataset = self._as_dataset(dataset, batch_size or self.batch_size)
+        return self
+
+    set_traindata = setTrainData
+
+    def setCriterion(self, criterion):
+        self.criterion = criterion
+        return self
+
+    set_criterion = setCriterion
+
+    def setState(self, state):
+        self.state.update(dict(state.items()) if isinstance(state, Table) else dict(state))
+        return self
+
+    def setOptimMethod(self, method: OptimMethod):
+        self.optim_methods = {self.model.get_name(): method}
+        return self
+
+    def setOptimMethods(self, methods: Dict[str, OptimMethod]):
+        self.optim_methods = dict(methods)
+        return self
+
+    def setModelAndOptimMethods(self, model, methods):
+        self.model = model
+        return self.setOptimMethods(methods)
+
+    def setEndWhen(self, trigger: Trigger):
+        self.end_when = trigger
+        return self
+
+    set_end_when = setEndWhen
+
+    def setDropModuleProperty(self, drop_percentage, max_drop_percentage, batchsize=100, warmup_iteration=200):
+        """Straggler dropping (P5).  One GPU per rank rarely straggles; the knob is accepted and
+        a per-rank step-time watchdog logs slow ranks instead of cancelling work."""
+        self.drop_percentage = drop_percentage
+        return self
+
+    def disableGradientClipping(self):
+        self.constant_clip = None
+        self.l2_clip = None
+        return self
+
+    disable_gradient_clipping = disableGradientClipping
+
+    def setConstantGradientClipping(self, min_value, max_value):
+        self.constant_clip = (min_value, max_value)
+        return self
+
+    set_gradclip_const = setConstantGradientClipping
+
+    def setGradientClippingByl2Norm(self, clip_norm):
+        self.l2_clip = clip_norm
+        return self
+
+    set_gradclip_l2norm = setGradientClippingByl2Norm
+
+    def reserveOptim(self, reserve: bool):
+        self.reserve_optim_state = reserve
+        return self
+
+    def prepareInput(self):
+        return self
+
+    # ------------------------------------------------------------------------------ setup
+    def _setup_model(self):
+        m = self.model
+        m.to(self.device)
+        m.training()
+        flat_w, flat_g = m.getParameters()
+        self.flat = m.flat_parameters()
+        if self.flat is not None and self.device.type == "cuda" and self.compute_dtype != torch.float32:
+            self.flat.enable_shadow(self.compute_dtype)
+        self._method_slices = self._compute_method_slices()
+        for name, meth in self.optim_methods.items():
+            for k in ("epoch", "neval"):
+                meth.state.setdefault(k, self.state[k])
+
+    def _compute_method_slices(self):
+        """Map each OptimMethod to the (offset, length) of its sub-module's parameters in the
+        flat arena (``Optimizer.scala:492-522`` checkSubModules)."""
+        if self.flat is None:
+            return {}
+        slices = {}
+        root = self.model.get_name()
+        for name in self.optim_methods:
+            if name == root:
+                slices[name] = (0, self.flat.numel)
+                continue
+            sub = [m for m in self.model.flattened_modules() if m.get_name() == name]
+            if not sub:
+                raise ValueError(f"optimMethod names a sub-module '{name}' that does not exist")
+            ents = sub[0]._param_entries()
+            offs = [o for (m, w, g, o, n, s) in self.flat.slices for (mm, ww, gg) in ents if m is mm and w == ww]
+            lens = [n for (m, w, g, o, n, s) in self.flat.slices for (mm, ww, gg) in ents if m is mm and w == ww]
+            lo = min(offs)
+            hi = max(o + n for o, n in zip(offs, lens))
+            slices[name] = (lo, hi - lo)
+        covered = sum(l for _, l in slices.values())
+        if covered != self.flat.numel:
+            raise ValueError("optimMethods must cover every trainable parameter exactly once")
+        return slices
+
+    # ------------------------------------------------------------------------------ per-iteration hooks
+    def _before_backward(self):
+        pass
+
+    def _sync_and_update(self, loss_t: torch.Tensor, batch_size: int):
+        """Gradient aggregation + clipping + optimizer update (local: no aggregation)."""
+        self._clip(self.flat.grad, self.flat.grad)
+        for name, meth in self.optim_methods.items():
+            off, n = self._method_slices[name]
+            w = self.flat.weight[off:off + n]
+            g = self.flat.grad[off:off + n]
+            meth.shadow = self.flat.shadow[off:off + n] if self.flat.shadow is not None else None
+            meth.optimize(lambda _x, g=g: (loss_t, g), w)
+        if self.flat.shadow is not None:
+            self.flat.mark_shadow_fresh()
+
+    def _clip(self, grad: torch.Tensor, local_shard: torch.Tensor):
+        if self.constant_clip is not None:
+            grad.clamp_(self.constant_clip[0], self.constant_clip[1])
+        if self.l2_clip is not None:
+            sq = (local_shard.float() ** 2).sum()
+            sq = self._global_sum(sq)
+            norm = torch.sqrt(sq)
+            scale = torch.clamp(self.l2_clip / (norm + 1e-6), max=1.0)
+            grad.mul_(scale)
+
+    def _global_sum(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def _reduce_scalar(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    # ------------------------------------------------------------------------------ main loop
+    def optimize(self) -> AbstractModule:
+        retry = int(config.get_property("bigdl.failure.retryTimes"))
+        interval = float(config.get_property("bigdl.failure.retryTimeInterval"))
+        failures: List[float] = []
+        self._setup_model()
+        while True:
+            try:
+                self._train_loop()
+                break
+            except (ValueError, KeyboardInterrupt):
+                raise
+            except Exception as e:  # noqa: BLE001 - retry loop (DistriOptimizer.scala:881-963)
+                now = time.time()
+                failures = [t for t in failures if now - t < retry * interval] + [now]
+                if self.checkpoint_path is None or len(failures) > retry:
+                    raise
+                log.warning(f"training failed ({e!r}); retry {len(failures)}/{retry} from the latest checkpoint")
+                self._restore_latest()
+        self._finish()
+        return self.model
+
+    def _global_epoch_size(self, local_epoch_size: int) -> int:
+        """Records per epoch across all ranks: a rank-sharded dataset reports the local shard."""
+        if hasattr(self.dataset, "local_size") and Engine.world_size() > 1:
+            return local_epoch_size * Engine.world_size()
+        return local_epoch_size
+
+    def _finish(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        self.metrics.resolve()
+
+    def _batches(self):
+        it = self.dataset.data(train=True)
+        if self.device.type == "cuda":
+            return DevicePrefetcher(it, self.device)
+        return it
+
+    def _epoch_size(self) -> int:
+        ds = self.dataset
+        n = getattr(ds, "local_size", None)
+        n = n() if callable(n) else ds.size()
+        return max(1, n)
+
+    def _train_loop(self):
+        m, crit = self.model, self.criterion
+        epoch_size = self._epoch_size()
+        batches = self._batches()
+        wall0 = time.perf_counter()
+        for meth in self.optim_methods.values():
+            meth.state["epoch"] = self.state["epoch"]
+            meth.state["neval"] = self.state["neval"]
+        while not self.end_when(self.state):
+            t0 = time.perf_counter()
+            batch = next(batches)
+            bs = batch.size()
+            loss_t = self.train_step(batch)
+            # bookkeeping (no device sync: the loss is read one iteration late)
+            prev = self._pending_loss
+            self._pending_loss = _LazyScalar(loss_t)
+            if prev is not None:
+                self.state["Loss"] = prev.value() if (prev.ready() or self._needs_loss()) else self.state["Loss"]
+            it = self.state["neval"]
+            global_bs = bs * Engine.world_size()
+            self.state["recordsProcessedThisEpoch"] += global_bs
+            dt = time.perf_counter() - t0
+            self.metrics.add("computing time", dt)
+            if it % self.log_interval == 0 and Engine.rank() == 0:
+                log.info(iteration_line(self.state["epoch"], self.state["recordsProcessedThisEpoch"],
+                                        self._global_epoch_size(epoch_size), it, time.perf_counter() - wall0,
+                                        global_bs, dt, self.state["Loss"], self._hyper_str()))
+            self.state["neval"] = it + 1
+            if self.state["recordsProcessedThisEpoch"] >= self._global_epoch_size(epoch_size):
+                self.state["epoch"] += 1
+                self.state["recordsProcessedThisEpoch"] = 0
+                self.dataset.shuffle()
+            for meth in self.optim_methods.values():
+                meth.state["epoch"] = self.state["epoch"]
+                meth.state["neval"] = self.state["neval"]
+            self._save_summary(global_bs, dt)
+            self._maybe_validate()
+            self._maybe_checkpoint()
+        if self._pending_loss is not None:
+            self.state["Loss"] = self._pending_loss.value()
+
+    def prepare(self):
+        """Set the model up for stepping without running the loop (used by bench/smoke)."""
+        self._setup_model()
+        return self
+
+    def train_step(self, batch: MiniBatch) -> torch.Tensor:
+        """One synchronous-SGD iteration on ``batch``; returns the (rank-averaged) loss as a
+        device scalar without synchronising the host."""
+        m, crit = self.model, self.criterion
+        x, y = batch.getInput(), batch.getTarget()
+        self._before_forward()
+        m.zeroGradParameters()
+        out = m.forward(x)
+        loss = crit.forward(out, y)
+        gout = crit.backward(out, y)
+        self._before_backward()
+        m.backward(x, gout)
+        loss_t = loss if isinstance(loss, torch.Tensor) else torch.tensor(float(loss))
+        loss_t = self._reduce_scalar(loss_t.detach().float().reshape(()))
+        self._sync_and_update(loss_t, batch.size())
+        return loss_t
+
+    def _needs_loss(self) -> bool:
+        from .trigger import MinLoss, TriggerAnd, TriggerOr
+
+        def uses(t):
+            if isinstance(t, MinLoss):
+                return True
+            if isinstance(t, (TriggerAnd, TriggerOr)):
+                return any(uses(s) for s in t.triggers)
+            return False
+        return uses(self.end_when) or self.train_summary is not None
+
+    def _hyper_str(self):
+        return "".join(m.getHyperParameter() for m in self.optim_methods.values())
+
+    def _before_forward(self):
+        pass
+
+    # ------------------------------------------------------------------------------ summary / validation / checkpoint
+    def _save_summary(self, batch, dt):
+        s = self.train_summary
+        if s is None or Engine.rank() != 0:
+            return
+        it = self.state["neval"] - 1
+        if s.should_write("Loss", self.state):
+            s.add_scalar("Loss", float(self.state["Loss"]), it)
+        if s.should_write("Throughput", self.state):
+            s.add_scalar("Throughput", batch / dt if dt > 0 else 0.0, it)
+        if s.should_write("LearningRate", self.state):
+            lr = list(self.optim_methods.values())[0].getLearningRate()
+            s.add_scalar("LearningRate", -lr if lr < 0 else lr, it)
+        if s.should_write("Parameters", self.state):
+            for mod in self.model.flattened_modules():
+                p = mod.parameters() if not mod.children() else None
+                if p:
+                    for (w, g), wt, gt in zip(mod._param_slots, p[0], p[1]):
+                        s.add_histogram(f"{mod.get_name()}/{w}", wt, it)
+                        s.add_histogram(f"{mod.get_name()}/{g}", gt, it)
+
+    def _maybe_validate(self):
+        if self.validation_trigger is None or self.validation_set is None:
+            return
+        if not self.validation_trigger(self.state):
+            return
+        results = self.validate()
+        if results:
+            self.state["score"] = results[0][1].result()[0]
+            for meth in self.optim_methods.values():
+                meth.state["score"] = self.state["score"]
+                for vm, r in results:
+                    meth.state[vm.format()] = r.result()[0]
+
+    def validate(self):
+        self._flush_weights()
+        m = self.model
+        m.evaluate()
+        results = None
+        it = self.validation_set.data(train=False)
+        with torch.no_grad():
+            for b in it:
+                b = b.to(self.device) if self.device.type == "cuda" else b
+                out = m.forward(b.getInput())
+                rs = [vm(out, b.getTarget()) for vm in self.validation_methods]
+                results = rs if results is None else [a + r for a, r in zip(results, rs)]
+        m.training()
+        if results is None:
+            return []
+        results = allreduce_results(results)
+        pairs = list(zip(self.validation_methods, results))
+        if Engine.rank() == 0:
+            for vm, r in pairs:
+                log.info(f"{vm.format()} is {r}")
+            if self.validation_summary is not None:
+                for vm, r in pairs:
+                    self.validation_summary.add_scalar(vm.format(), r.result()[0], self.state["neval"] - 1)
+        return pairs
+
+    def _flush_weights(self):
+        """Make sure the fp32 weights in the arena are current (distributed overrides)."""
+
+    def _maybe_checkpoint(self):
+        if self.checkpoint_trigger is None or self.checkpoint_path is None:
+            return
+        if not self.checkpoint_trigger(self.state):
+            return
+        self.checkpoint()
+
+    def checkpoint(self):
+        from ..serialization.checkpoint import save_checkpoint
+        self._flush_weights()
+        if Engine.rank() == 0:
+            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite)
+
+    def _restore_latest(self):
+        from ..serialization.checkpoint import load_latest_checkpoint
+        model, methods, state = load_latest_checkpoint(self.checkpoint_path)
+        if model is not None:
+            p_dst = self.model.parameters()
+            p_src = model.parameters()
+            if p_dst is not None and p_src is not None:
+                for a, b in zip(p_dst[0], p_src[0]):
+                    a.copy_(b.to(a.device))
+            ex_dst, ex_src = self.model.getExtraParameter(), model.getExtraParameter()
+            if ex_dst and ex_src:
+                for a, b in zip(ex_dst, ex_src):
+                    a.copy_(b.to(a.device))
+        if methods:
+            for k, v in methods.items():
+                if k in self.optim_methods:
+                    for sk, sv in v.state.items():
+                        v.state[sk] = sv.to(self.device) if isinstance(sv, torch.Tensor) else sv
+                    self.optim_methods[k] = v
+        if state:
+            self.state.update(state)
+        if self.flat is not None and self.flat.shadow is not None:
+            self.flat.refresh_shadow()
+        self._on_restore()
+
+    def _on_restore(self):
+        pass
+
+
+class LocalOptimizer(BaseOptimizer):
+    """Single-device trainer (``LocalOptimizer.scala:45-295``).  The reference clones one replica
+    per core and sums their gradients; a GPU is one replica, so the loop is direct."""
+
+    def __init__(self, model, training_set, criterion, optim_method=None, end_trigger=None, batch_size=32,
+                 bigdl_type="float"):
+        super().__init__(model, training_set, criterion, batch_size)
+        if optim_method is not None:
+            if isinstance(optim_method, dict):
+                self.setOptimMethods(optim_method)
+            else:
+                self.setOptimMethod(optim_method)
+        if end_trigger is not None:
+            self.setEndWhen(end_trigger)
+
+
+class Optimizer:
+    """Factory mirroring ``object Optimizer`` and pyspark ``Optimizer.create``."""
+
+    def __new__(cls, model, training_rdd=None, criterion=None, end_trigger=None, batch_size=32, optim_method=None,
+                bigdl_type="float", **kw):
+        return Optimizer.create(model, training_rdd, criterion, end_trigger, batch_size, optim_method)
+
+    @staticmethod
+    def create(model, training_set, criterion, end_trigger=None, batch_size=32, optim_method=None,
+               cores=None, bigdl_type="float", distributed: Optional[bool] = None):
+        if distributed is None:
+            distributed = Engine.is_distributed() or (
+                hasattr(training_set, "world") and getattr(training_set, "world", 1) > 1)
+        if distributed:
+            from ..parallel.distri_optimizer import DistriOptimizer
+            opt = DistriOptimizer(model, training_set, criterion, optim_method, end_trigger, batch_size)
+        else:
+            opt = LocalOptimizer(model, training_set, criterion, optim_method, end_trigger, batch_size)
+        return opt

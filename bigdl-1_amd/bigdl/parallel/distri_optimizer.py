@@ -1,0 +1,334 @@
+"""DistriOptimizer: synchronous data-parallel SGD, one process per GPU, RCCL over xGMI.
+
+Reference semantics (``DL/optim/DistriOptimizer.scala:97-517``, ``ParallelOptimizer.scala``):
+  job 1 — every replica pulls weights, runs fwd/bwd on its slice of the global batch, pushes its
+  gradient split into N chunks (bf16);  job 2 — each partition sums its chunk from all replicas
+  (``aggregateGradientPartition``), runs the OptimMethod on ITS 1/N of the parameters (ZeRO-1
+  style, one optimizer state per shard) and publishes the updated weight shard.
+  ParallelOptimizer additionally pushes each layer group's gradient as soon as its backward is
+  done (≈10 buckets, reverse execution order) and applies updates lazily before the next forward.
+
+MI355X mapping (``bigdl.comm.*`` config keys):
+  * the flat parameter arena is re-laid out into contiguous buckets of ``bucketMB`` (default 32 MB
+    — large enough for RCCL's bandwidth plateau on the 7 xGMI links, few enough to overlap)
+    padded to a multiple of 64·world so every bucket is directly a collective buffer;
+  * module grad-ready hooks launch ``reduce_scatter_tensor`` for a bucket the moment its last
+    parameter gradient is written — these run on RCCL's internal stream concurrently with the rest
+    of backward;
+  * after backward each bucket's shard is updated by the fused optimizer kernel (``grad_scale=1/N``
+    folds the average in) and ``all_gather_into_tensor`` publishes it back into the arena;
+  * the next forward waits for a bucket's all-gather only when the first layer owning parameters
+    in it runs (pre-forward hook) — the reference's lazy ``updateParameter`` at forward;
+  * ``comm.dtype = bf16`` reduces bf16 gradients and gathers the bf16 compute shadow directly
+    (half the bytes; fp32 masters live only on the owning rank until :meth:`_flush_weights`);
+    ``bf16_truncate`` reproduces the reference's truncating wire format exactly.
+  * Non-sliceable methods (LBFGS, Ftrl, …) or several OptimMethods with non-SGD/Adam members fall
+    back to "replicated" mode: all-reduce of the full gradient, full update on every rank.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..optim.optimizer import BaseOptimizer
+from ..utils import config
+from ..utils.engine import Engine
+from ..utils.logger import get_logger
+from . import comm
+
+log = get_logger("bigdl.parallel")
+
+
+class _Bucket:
+    __slots__ = ("idx", "lo", "hi", "slo", "shi", "pending", "expected", "rs_work", "ag_work", "ready",
+                 "modules", "needs_shadow")
+
+    def __init__(self, idx, lo, hi, slo, shi):
+        self.idx, self.lo, self.hi, self.slo, self.shi = idx, lo, hi, slo, shi
+        self.pending = 0
+        self.expected = 0
+        self.rs_work = None
+        self.ag_work = None
+        self.ready = False
+        self.modules = []
+        self.needs_shadow = False
+
+
+class DistriOptimizer(BaseOptimizer):
+    def __init__(self, model, training_set, criterion, optim_method=None, end_trigger=None, batch_size=32,
+                 bigdl_type="float"):
+        super().__init__(model, training_set, criterion, batch_size)
+        if optim_method is not None:
+            if isinstance(optim_method, dict):
+                self.setOptimMethods(optim_method)
+            else:
+                self.setOptimMethod(optim_method)
+        if end_trigger is not None:
+            self.setEndWhen(end_trigger)
+        self.world = comm.world()
+        self.rank = comm.rank()
+        self.comm_dtype = str(config.get_property("bigdl.comm.dtype"))
+        self.bucket_bytes = int(float(config.get_property("bigdl.comm.bucketMB")) * 2 ** 20)
+        self.overlap = bool(config.get_property("bigdl.comm.overlap"))
+        self.sharded = bool(config.get_property("bigdl.comm.sharded"))
+        self._hook_counts: Dict[int, int] = {}
+        self._overlap_active = False
+        self._first_iter = True
+
+    # ------------------------------------------------------------------------------ setup
+    def _setup_model(self):
+        m = self.model
+        m.to(self.device)
+        m.training()
+        W = self.world
+        self.flat = m.compactParametersBucketed(self.bucket_bytes, 64 * W)
+        if self.flat is None:
+            raise ValueError("DistriOptimizer needs a model with trainable parameters")
+        comm.broadcast_module(m, 0)  # X1: identical initial replicas
+        if self.device.type == "cuda" and self.compute_dtype != torch.float32:
+            self.flat.enable_shadow(self.compute_dtype)
+        self._method_slices = self._compute_method_slices()
+        if self.sharded and not all(meth.supports_slices for meth in self.optim_methods.values()):
+            log.info("OptimMethod without slice support: using replicated (all-reduce) mode")
+            self.sharded = False
+        # buckets + shard space
+        self.buckets: List[_Bucket] = []
+        soff = 0
+        for i, (lo, hi) in enumerate(self.flat.buckets):
+            per = (hi - lo) // W
+            self.buckets.append(_Bucket(i, lo, hi, soff, soff + per))
+            soff += per
+        dev = self.flat.weight.device
+        if self.sharded:
+            self.shard_w = torch.empty(soff, dtype=torch.float32, device=dev)
+            self.shard_g = torch.zeros(soff, dtype=torch.float32, device=dev)
+            for b in self.buckets:
+                per = b.shi - b.slo
+                self.shard_w[b.slo:b.shi].copy_(self.flat.weight[b.lo + self.rank * per:b.lo + (self.rank + 1) * per])
+            self.shard_shadow = None
+            if self.flat.shadow is not None:
+                self.shard_shadow = torch.empty(soff, dtype=self.flat.shadow.dtype, device=dev)
+            self.grad_wire = None
+            if self.comm_dtype.startswith("bf16"):
+                self.grad_wire = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=dev)
+                self.shard_g_wire = torch.empty(soff, dtype=torch.bfloat16, device=dev)
+        # shard ranges per OptimMethod: intersection of its arena range with each bucket's shard
+        self._method_shard_ranges = {name: [] for name in self.optim_methods}
+        for name, (off, n) in self._method_slices.items():
+            for b in self.buckets:
+                per = b.shi - b.slo
+                own_lo = b.lo + self.rank * per
+                own_hi = own_lo + per
+                lo, hi = max(off, own_lo), min(off + n, own_hi)
+                if lo < hi:
+                    self._method_shard_ranges[name].append((b, b.slo + (lo - own_lo), b.slo + (hi - own_lo)))
+        for meth in self.optim_methods.values():
+            meth.grad_scale = 1.0 / W
+            for k in ("epoch", "neval"):
+                meth.state.setdefault(k, self.state[k])
+        # module → buckets map, hooks
+        self._mod_buckets = {}
+        for (mod, w, g, off, n, shape) in self.flat.slices:
+            for b in self.buckets:
+                if b.lo <= off < b.hi:
+                    self._mod_buckets.setdefault(id(mod), set()).add(b.idx)
+                    if mod not in b.modules:
+                        b.modules.append(mod)
+        for b in self.buckets:
+            b.expected = len(b.modules)
+        self._install_hooks()
+        log.info(f"DistriOptimizer: world={W} params={self.flat.numel} buckets={len(self.buckets)} "
+                 f"mode={'sharded' if self.sharded else 'replicated'} comm={self.comm_dtype} overlap={self.overlap}")
+
+    def _install_hooks(self):
+        seen = set()
+        for (mod, *_rest) in self.flat.slices:
+            if id(mod) in seen:
+                continue
+            seen.add(id(mod))
+            mod._grad_ready_hooks.append(self._on_grad_ready)
+            mod._pre_forward_hooks.append(self._on_pre_forward)
+
+    # ------------------------------------------------------------------------------ hooks
+    def _on_grad_ready(self, mod):
+        k = id(mod)
+        self._hook_counts[k] = self._hook_counts.get(k, 0) + 1
+        if not self._overlap_active:
+            return
+        for bi in self._mod_buckets.get(k, ()):
+            b = self.buckets[bi]
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch_reduce(b)
+
+    def _on_pre_forward(self, mod):
+        for bi in self._mod_buckets.get(id(mod), ()):
+            b = self.buckets[bi]
+            if b.ag_work is not None:
+                b.ag_work.wait()
+                b.ag_work = None
+                self._after_gather(b)
+
+    # ------------------------------------------------------------------------------ collectives
+    def _launch_reduce(self, b: _Bucket):
+        g = self.flat.grad[b.lo:b.hi]
+        if self.sharded:
+            if self.grad_wire is not None:
+                wire = self.grad_wire[b.lo:b.hi]
+                if self.comm_dtype == "bf16_truncate":
+                    wire.copy_(comm.bf16_truncate(g))
+                else:
+                    wire.copy_(g)
+                b.rs_work = dist.reduce_scatter_tensor(self.shard_g_wire[b.slo:b.shi], wire, async_op=True)
+            else:
+                b.rs_work = dist.reduce_scatter_tensor(self.shard_g[b.slo:b.shi], g, async_op=True)
+        else:
+            b.rs_work = dist.all_reduce(g, async_op=True)
+
+    def _finish_reduce(self, b: _Bucket):
+        if b.rs_work is None:
+            return
+        b.rs_work.wait()
+        b.rs_work = None
+        if self.sharded and self.grad_wire is not None:
+            self.shard_g[b.slo:b.shi].copy_(self.shard_g_wire[b.slo:b.shi])
+
+    def _bf16_gather(self) -> bool:
+        return self.comm_dtype.startswith("bf16") and self.flat.shadow is not None
+
+    def _launch_gather(self, b: _Bucket):
+        if not self.sharded:
+            return
+        if self._bf16_gather():
+            # reference wire format: replicas compute with the bf16 copy of the weights
+            b.ag_work = dist.all_gather_into_tensor(self.flat.shadow[b.lo:b.hi], self.shard_shadow[b.slo:b.shi],
+                                                    async_op=True)
+        else:
+            b.ag_work = dist.all_gather_into_tensor(self.flat.weight[b.lo:b.hi], self.shard_w[b.slo:b.shi],
+                                                    async_op=True)
+        b.needs_shadow = True
+
+    def _after_gather(self, b: _Bucket):
+        if not b.needs_shadow:
+            return
+        from .. import ops
+        if self._bf16_gather():
+            # fp32 view of the gathered bf16 weights for layers that read fp32 params (BN γ/β);
+            # exact fp32 masters stay in this rank's shard
+            ops.cast_copy(self.flat.weight[b.lo:b.hi], self.flat.shadow[b.lo:b.hi])
+        elif self.flat.shadow is not None:
+            ops.cast_copy(self.flat.shadow[b.lo:b.hi], self.flat.weight[b.lo:b.hi])
+        b.needs_shadow = False
+
+    # ------------------------------------------------------------------------------ iteration
+    def _before_forward(self):
+        for b in self.buckets:
+            b.pending = b.expected
+        self._overlap_active = self.overlap and not self._first_iter and self._overlap_ok
+        self._hook_counts = {}
+
+    @property
+    def _overlap_ok(self):
+        return getattr(self, "_overlap_checked", False)
+
+    def _reduce_scalar(self, t):
+        return comm.allreduce_scalar(t, average=True)
+
+    def _global_sum(self, t):
+        if comm.is_dist():
+            t = t.clone()
+            dist.all_reduce(t)
+        return t
+
+    def _sync_and_update(self, loss_t, batch_size):
+        if self._first_iter:
+            # enable overlap only if every parameterised module ran backward exactly once
+            ok = all(self._hook_counts.get(id(m), 0) == 1 for b in self.buckets for m in b.modules)
+            self._overlap_checked = ok
+            if not ok and self.overlap:
+                log.info("gradient/backward overlap disabled: shared or directly-driven parameter modules")
+        # launch any bucket not launched during backward
+        for b in reversed(self.buckets):
+            if b.rs_work is None:
+                self._launch_reduce(b)
+        if not self.sharded:
+            for b in self.buckets:
+                self._finish_reduce(b)
+            self.flat.grad.mul_(1.0 / self.world)
+            for meth in self.optim_methods.values():
+                meth.grad_scale = 1.0
+            BaseOptimizer._sync_and_update(self, loss_t, batch_size)
+            self._first_iter = False
+            return
+        # sharded: clipping needs the global gradient norm before any update
+        if self.constant_clip is not None or self.l2_clip is not None:
+            for b in self.buckets:
+                self._finish_reduce(b)
+            self.shard_g.mul_(1.0 / self.world)
+            for meth in self.optim_methods.values():
+                meth.grad_scale = 1.0
+            self._clip(self.shard_g, self.shard_g)
+        for meth in self.optim_methods.values():
+            meth.begin_iteration(self.shard_w)
+        done = set()
+        for b in reversed(self.buckets):  # in readiness order
+            self._finish_reduce(b)
+            for name, meth in self.optim_methods.items():
+                for (bb, lo, hi) in self._method_shard_ranges[name]:
+                    if bb is b:
+                        sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
+                                                          self.comm_dtype.startswith("bf16")) else None
+                        meth.apply_update(self.shard_w, self.shard_g, lo, hi, shadow=sh)
+            self._launch_gather(b)
+            done.add(b.idx)
+        if self.constant_clip is not None or self.l2_clip is not None:
+            for meth in self.optim_methods.values():
+                meth.grad_scale = 1.0 / self.world
+        self.flat.mark_shadow_fresh()
+        self._first_iter = False
+
+    def _wait_all_gathers(self):
+        for b in self.buckets:
+            if b.ag_work is not None:
+                b.ag_work.wait()
+                b.ag_work = None
+                self._after_gather(b)
+        self.flat.mark_shadow_fresh()
+
+    def _flush_weights(self):
+        """Bring every rank's fp32 arena up to date (needed before validation/checkpoint when
+        the bf16 wire format gathered only the compute shadow)."""
+        self._wait_all_gathers()
+        if self.sharded and self.comm_dtype.startswith("bf16"):
+            for b in self.buckets:
+                dist.all_gather_into_tensor(self.flat.weight[b.lo:b.hi], self.shard_w[b.slo:b.shi])
+            self.flat.mark_shadow_fresh()
+
+    def _finish(self):
+        self._wait_all_gathers()
+        self._flush_weights()
+        super()._finish()
+
+    def _on_restore(self):
+        comm.broadcast_module(self.model, 0)
+        if self.sharded:
+            W, r = self.world, self.rank
+            for b in self.buckets:
+                per = b.shi - b.slo
+                self.shard_w[b.slo:b.shi].copy_(self.flat.weight[b.lo + r * per:b.lo + (r + 1) * per])
+        if self.flat.shadow is not None:
+            self.flat.refresh_shadow()
+
+    def checkpoint(self):
+        """Gather the shards (X14) then rank 0 writes ``model.<neval>`` / ``optimMethod-*``.
+        Optimizer state is per shard: each rank writes its own state file next to it."""
+        from ..serialization.checkpoint import save_checkpoint, save_shard_state
+        self._flush_weights()
+        if Engine.rank() == 0:
+            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite)
+        if self.sharded:
+            save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite)
+        comm.barrier()

@@ -1,0 +1,3 @@
+from .tensor import Tensor
+from .sparse import SparseTensor
+from .quantized import QuantizedTensor

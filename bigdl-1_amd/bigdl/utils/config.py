@@ -1,0 +1,93 @@
+"""Typed configuration registry.
+
+The reference reads ~30 ``-Dbigdl.*`` JVM system properties ad hoc (e.g.
+``DL/utils/Engine.scala:45-46,191-252``, ``DL/optim/DistriOptimizer.scala:882-883``,
+``DL/optim/ParallelOptimizer.scala:404``).  Here every key is declared once with a type and a
+default; the environment variable ``BIGDL_<KEY with . → _ upper-cased>`` overrides it, and
+``set_property`` overrides both at runtime.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+_lock = threading.Lock()
+
+# key -> (type, default, doc)
+_REGISTRY = {
+    # engine / topology
+    "bigdl.localMode": (bool, False, "run without a process group"),
+    "bigdl.coreNumber": (int, 0, "host threads for CPU ops (0 = auto)"),
+    "bigdl.engineType": (str, "hip", "kept for compatibility: 'mklblas'/'mkldnn' map to the native engine"),
+    "bigdl.multiModels": (bool, False, "compat flag (one replica per GPU here)"),
+    "bigdl.utils.Engine.defaultPoolSize": (int, 0, "host pool size"),
+    "bigdl.check.singleton": (bool, False, "compat"),
+    # failure handling
+    "bigdl.failure.retryTimes": (int, 5, "optimizer retry budget"),
+    "bigdl.failure.retryTimeInterval": (int, 120, "retry window seconds"),
+    # parameter sync
+    "bigdl.Parameter.syncPoolSize": (int, 4, "compat"),
+    "bigdl.Parameter.computePoolSize": (int, 0, "compat"),
+    "bigdl.parallelOptimizer.parameterBlocks": (int, 10, "number of gradient buckets for overlap mode"),
+    # device / precision (new)
+    "bigdl.compute.dtype": (str, "fp32", "fp32 | bf16 activations/weights for device compute"),
+    "bigdl.comm.dtype": (str, "fp32", "fp32 | bf16 | bf16_truncate wire format for gradient reduction"),
+    "bigdl.comm.bucketMB": (float, 32.0, "gradient bucket size for RCCL collectives"),
+    "bigdl.comm.overlap": (bool, True, "overlap gradient reduce-scatter with backward"),
+    "bigdl.comm.sharded": (bool, True, "reduce-scatter + sharded update + all-gather (ZeRO-1)"),
+    "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
+    "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
+    # fusion flags (bigdl.mkldnn.fusion.* equivalents, nn/mkldnn/Fusion.scala:34)
+    "bigdl.fusion": (bool, True, "enable layer fusion"),
+    "bigdl.fusion.convbn": (bool, True, "fold BN into conv for inference"),
+    "bigdl.fusion.bnrelu": (bool, True, "fuse BN + ReLU"),
+    "bigdl.fusion.convrelu": (bool, True, "fuse conv + ReLU"),
+    "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
+    # logging
+    "bigdl.utils.LoggerFilter.disable": (bool, False, "disable log redirect"),
+    "bigdl.utils.LoggerFilter.logFile": (str, "bigdl.log", "log file"),
+    "bigdl.utils.LoggerFilter.enableSparkLog": (bool, True, "compat"),
+}
+
+_overrides: dict = {}
+
+
+def _env_name(key: str) -> str:
+    return "BIGDL_" + key.replace("bigdl.", "", 1).replace(".", "_").upper()
+
+
+def _coerce(typ, v):
+    if typ is bool:
+        if isinstance(v, bool):
+            return v
+        return str(v).strip().lower() in ("1", "true", "yes", "on")
+    return typ(v)
+
+
+def get_property(key: str, default=None):
+    with _lock:
+        if key in _overrides:
+            return _overrides[key]
+    typ, dflt, _ = _REGISTRY.get(key, (str, default, ""))
+    env = os.environ.get(_env_name(key))
+    if env is not None:
+        return _coerce(typ, env)
+    sysprop = os.environ.get(key)  # allow literal "bigdl.x.y" names too
+    if sysprop is not None:
+        return _coerce(typ, sysprop)
+    return dflt if default is None else default
+
+
+def set_property(key: str, value):
+    typ = _REGISTRY.get(key, (type(value), None, ""))[0]
+    with _lock:
+        _overrides[key] = _coerce(typ, value)
+
+
+def clear_property(key: str):
+    with _lock:
+        _overrides.pop(key, None)
+
+
+def describe() -> dict:
+    return {k: get_property(k) for k in _REGISTRY}

@@ -1,0 +1,176 @@
+"""Numerics of the native HIP kernels vs the fp32 reference ops (bigdl/ops/reference.py).
+
+Each test asserts the native library is loaded and the op actually dispatched natively (so a
+silent fallback to the reference path fails the test)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _native():
+    from bigdl.ops import native, native_status
+    st = native_status()
+    assert st["loaded"], st
+    return native
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def test_native_loaded_and_ops_registered():
+    N = _native()
+    for op in ["cast_copy", "relu_forward", "batchnorm_forward_train", "batchnorm_backward", "cross_entropy_fused",
+               "sgd_step"]:
+        assert N.has(op), op
+
+
+@pytest.mark.parametrize("n", [8, 1000, 4099, 1 << 20])
+def test_cast(n):
+    N = _native()
+    x = torch.randn(n, device=dev)
+    b = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    assert N.cast_copy(b, x) is not NotImplemented
+    torch.testing.assert_close(b, x.to(torch.bfloat16), rtol=0, atol=0)
+    f = torch.empty(n, device=dev)
+    N.cast_copy(f, b)
+    torch.testing.assert_close(f, b.float(), rtol=0, atol=0)
+
+
+def test_relu_fwd_bwd():
+    N = _native()
+    x = _cl(torch.randn(4, 64, 7, 7, device=dev).bfloat16())
+    y = N.relu_forward(x)
+    torch.testing.assert_close(y, torch.relu(x))
+    gy = _cl(torch.randn_like(x))
+    gx = N.relu_backward(gy, y)
+    torch.testing.assert_close(gx, gy * (x > 0).to(gy.dtype))
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 7, 7), (3, 24, 5, 5), (64, 512)])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_bn_forward_backward(shape, relu, res):
+    N = _native()
+    from bigdl.ops import reference as R
+    C = shape[1]
+    x = torch.randn(*shape, device=dev) * 3 + 1.5
+    x = (_cl(x) if len(shape) == 4 else x).bfloat16()
+    if len(shape) == 4:
+        x = _cl(x)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm.clone(), rv.clone()
+    r = None
+    if res:
+        r = torch.randn(*shape, device=dev).bfloat16()
+        r = _cl(r) if len(shape) == 4 else r
+    out = N.batchnorm_forward_train(x, gamma, beta, rm, rv, 0.1, 1e-5, relu=relu, residual=r)
+    assert out is not NotImplemented
+    y, mean, invstd = out
+    yr, meanr, invr = R.batchnorm_forward_train(x.float(), gamma, beta, rm2, rv2, 0.1, 1e-5, relu=relu,
+                                                residual=None if r is None else r.float())
+    torch.testing.assert_close(mean, meanr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(invstd, invr, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=3e-2)
+    # backward
+    gy = torch.randn(*shape, device=dev).bfloat16()
+    gy = _cl(gy) if len(shape) == 4 else gy
+    gg, gb = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    gg2, gb2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    gx = N.batchnorm_backward(gy, x, gamma, mean, invstd, y=y, relu=relu, gg_acc=gg, gb_acc=gb, scale=0.5)
+    assert gx is not NotImplemented
+    gxr = R.batchnorm_backward(gy.float(), x.float(), gamma, mean, invstd, y=y.float(), relu=relu, gg_acc=gg2,
+                               gb_acc=gb2, scale=0.5)
+    torch.testing.assert_close(gg, gg2, rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(gb, gb2, rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(gx.float(), gxr.float(), rtol=3e-2, atol=3e-2)
+
+
+def test_bn_infer():
+    N = _native()
+    from bigdl.ops import reference as R
+    x = _cl(torch.randn(4, 128, 9, 9, device=dev).bfloat16())
+    C = 128
+    g, b, m, v = torch.rand(C, device=dev), torch.randn(C, device=dev), torch.randn(C, device=dev), torch.rand(C, device=dev) + .5
+    y = N.batchnorm_forward_infer(x, g, b, m, v, 1e-5, relu=True)
+    yr = R.batchnorm_forward_infer(x.float(), g, b, m, v, 1e-5, relu=True)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("weights", [False, True])
+def test_cross_entropy(dtype, weights):
+    N = _native()
+    from bigdl.ops import reference as R
+    B, K = 37, 1000
+    x = (torch.randn(B, K, device=dev) * 4).to(dtype)
+    t = torch.randint(1, K + 1, (B,), device=dev).float()
+    t[3] = -1  # padding value -> skipped
+    w = torch.rand(K, device=dev) if weights else None
+    loss, g = N.cross_entropy_fused(x, t, w, True, -1)
+    lr, gr = R.cross_entropy_fused(x.float(), t, w, True, -1)
+    torch.testing.assert_close(loss, lr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(g.float(), gr.float(), rtol=2e-2, atol=2e-4 if dtype == torch.float32 else 2e-3)
+
+
+def test_logsoftmax():
+    N = _native()
+    from bigdl.ops import reference as R
+    x = torch.randn(33, 100, device=dev)
+    y = N.log_softmax_forward(x)
+    torch.testing.assert_close(y, R.log_softmax_forward(x), rtol=1e-5, atol=1e-5)
+    gy = torch.randn_like(x)
+    torch.testing.assert_close(N.log_softmax_backward(gy, y), R.log_softmax_backward(gy, y), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("nesterov,first", [(True, True), (True, False), (False, False)])
+def test_sgd(nesterov, first):
+    N = _native()
+    from bigdl.ops import reference as R
+    n = 4096 + 64
+    w = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    buf = torch.randn(n, device=dev)
+    w2, buf2 = w.clone(), buf.clone()
+    sh = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    damp = 0.0 if nesterov else 0.1
+    N.sgd_step(w, g, buf, 0.1, 0.9, damp, 1e-4, nesterov, first, 0.5, sh)
+    R.sgd_step(w2, g, buf2, 0.1, 0.9, damp, 1e-4, nesterov, first, 0.5)
+    torch.testing.assert_close(w, w2, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(buf, buf2, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(sh, w.bfloat16(), rtol=0, atol=0)
+
+
+def test_adam():
+    N = _native()
+    from bigdl.ops import reference as R
+    n = 1024
+    w, g = torch.randn(n, device=dev), torch.randn(n, device=dev)
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    w2, m2, v2 = w.clone(), m.clone(), v.clone()
+    for step in (1, 2, 3):
+        N.adam_step(w, g, m, v, 1e-3, 0.9, 0.999, 1e-8, step)
+        R.adam_step(w2, g, m2, v2, 1e-3, 0.9, 0.999, 1e-8, step)
+    torch.testing.assert_close(w, w2, rtol=1e-5, atol=1e-6)
+
+
+def test_layers_use_native_path():
+    """Spatial BN + ReLU layers on bf16 NHWC activations go through the native kernels."""
+    _native()
+    from bigdl.nn import SpatialBatchNormalization, ReLU, Sequential
+    from bigdl.utils.engine import Engine
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    m = Sequential().add(SpatialBatchNormalization(64)).add(ReLU(True)).cuda()
+    x = _cl(torch.randn(2, 64, 8, 8, device=dev).bfloat16())
+    y = m.forward(x)
+    g = m.backward(x, torch.ones_like(y))
+    assert y.dtype == torch.bfloat16 and g.dtype == torch.bfloat16
+    assert torch.isfinite(g.float()).all()
