@@ -197,25 +197,64 @@ class Concat(Container):
 
 
 class ConcatTable(Container):
-    """Apply each member to the same input; output is a Table (``ConcatTable.scala``)."""
+    """Apply each member to the same input; output is a Table (``ConcatTable.scala``).
+
+    With ``_residual`` set by :mod:`bigdl.nn.fusion` (ResNet block tail) the shortcut runs first and
+    the main branch's last BN emits ReLU(BN(·) + shortcut) directly; the following CAddTable/ReLU
+    are pass-throughs."""
+
+    _residual = None
 
     def updateOutput(self, input):
+        if self._residual is not None:
+            return self._fused_forward(input)
         return Table(*[m.forward(input) for m in self.modules])
 
+    def _fused_forward(self, input):
+        br, bn, shortcut, relu = self._residual
+        r = shortcut.forward(input)
+        h = input
+        for m in br.modules[:-1]:
+            h = m.forward(h)
+        self._bn_in = h
+        y = bn.forward_residual(h, r, relu)
+        br.output = y
+        return Table(y, r)
+
+    def _fused_backward(self, input, gradOutput):
+        br, bn, shortcut, relu = self._residual
+        g = gradOutput[1] if isinstance(gradOutput, Table) else gradOutput
+        gb, gres = bn.backward_residual(self._bn_in, g)
+        for i in range(len(br.modules) - 2, -1, -1):
+            prev = br.modules[i - 1].output if i > 0 else input
+            gb = br.modules[i].backward(prev, gb)
+        br.gradInput = gb
+        gs = shortcut.backward(input, gres)
+        return _add_act(gb, gs)
+
     def updateGradInput(self, input, gradOutput):
+        if self._residual is not None:
+            self._fused_done = True
+            return self._fused_backward(input, gradOutput)
         gi = None
         for i, m in enumerate(self.modules):
             gi = _add_act(gi, m.updateGradInput(input, gradOutput[i + 1]))
         return gi
 
     def accGradParameters(self, input, gradOutput):
+        if self._residual is not None and getattr(self, "_fused_done", False):
+            self._fused_done = False
+            return
         for i, m in enumerate(self.modules):
             m.accGradParameters(input, gradOutput[i + 1])
 
     def backward(self, input, gradOutput):
-        gi = None
-        for i, m in enumerate(self.modules):
-            gi = _add_act(gi, m.backward(input, gradOutput[i + 1]))
+        if self._residual is not None:
+            gi = self._fused_backward(input, gradOutput)
+        else:
+            gi = None
+            for i, m in enumerate(self.modules):
+                gi = _add_act(gi, m.backward(input, gradOutput[i + 1]))
         self.gradInput = gi
         for h in self._grad_ready_hooks:
             h(self)

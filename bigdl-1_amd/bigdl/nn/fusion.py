@@ -1,0 +1,90 @@
+"""Graph-level fusion for the device path (the reference's MKL-DNN fusion,
+``DL/nn/mkldnn/Fusion.scala:32-332`` and ``mkldnn/Sequential.scala:195-267``; flags
+``bigdl.fusion[.convbn|.bnrelu|.convsum]``).
+
+The module tree is NOT rewritten (serialisation, ``parameters()`` order and user-visible structure
+stay identical); matched modules get execution flags instead:
+
+* conv → BN (``convbn``): the conv skips its bias add and the BN folds the bias in (batch
+  normalisation is shift-invariant, so only the running mean sees it); the conv-bias gradient
+  Σ_rows gx is produced by the BN backward's finalize kernel from its closed form.
+* BN → ReLU (``bnrelu``): the ReLU becomes a pass-through; BN applies it in its apply kernel and
+  masks the gradient in its backward apply kernel.
+* ResNet block tail ``ConcatTable(branch…BN, shortcut) → CAddTable → ReLU`` (``convsum``): the
+  shortcut runs first and the branch's last BN computes ReLU(BN(x) + shortcut) in one pass; in
+  backward the same kernel emits both the branch gradient and the masked gradient for the shortcut.
+
+Each fusion removes one full read+write pass over an activation tensor from HBM.
+"""
+from __future__ import annotations
+
+from ..utils import config
+from .containers import Sequential, ConcatTable
+from .layers.activation import Threshold
+from .layers.conv import SpatialConvolution
+from .layers.normalization import BatchNormalization, SpatialBatchNormalization
+from .layers.table_ops import CAddTable
+
+
+def _is_relu(m):
+    return isinstance(m, Threshold) and m.threshold == 0.0 and m.value == 0.0
+
+
+def _is_nchw_bn(m):
+    return isinstance(m, BatchNormalization) and getattr(m, "dataFormat", "NCHW") == "NCHW"
+
+
+def fuse(model, convbn=None, bnrelu=None, convsum=None):
+    if not config.get_property("bigdl.fusion"):
+        return model
+    convbn = config.get_property("bigdl.fusion.convbn") if convbn is None else convbn
+    bnrelu = config.get_property("bigdl.fusion.bnrelu") if bnrelu is None else bnrelu
+    convsum = config.get_property("bigdl.fusion.convsum") if convsum is None else convsum
+    for s in model.flattened_modules():
+        if not isinstance(s, Sequential):
+            continue
+        mods = s.modules
+        for i in range(len(mods) - 1):
+            a, b = mods[i], mods[i + 1]
+            if convbn and isinstance(a, SpatialConvolution) and type(a) in (SpatialConvolution,) + tuple(
+                    SpatialConvolution.__subclasses__()) and a.format == "NCHW" and a.withBias and _is_nchw_bn(b) \
+                    and b._bias_producer is None:
+                a._bias_folded_into = b
+                b._bias_producer = a
+            if bnrelu and _is_nchw_bn(a) and _is_relu(b):
+                a._fused_relu = True
+                b._passthrough = True
+        if not convsum:
+            continue
+        for i in range(len(mods) - 1):
+            ct, add = mods[i], mods[i + 1]
+            if not (isinstance(ct, ConcatTable) and len(ct.modules) == 2 and isinstance(add, CAddTable)):
+                continue
+            br = ct.modules[0]
+            if not (isinstance(br, Sequential) and br.modules and _is_nchw_bn(br.modules[-1])):
+                continue
+            bn = br.modules[-1]
+            if bn._fused_relu:
+                continue
+            relu = mods[i + 2] if i + 2 < len(mods) and _is_relu(mods[i + 2]) else None
+            ct._residual = (br, bn, ct.modules[1], relu is not None)
+            add._passthrough = True
+            if relu is not None:
+                relu._passthrough = True
+    return model
+
+
+def unfuse(model):
+    for m in model.flattened_modules():
+        if isinstance(m, SpatialConvolution):
+            m._bias_folded_into = None
+        if isinstance(m, BatchNormalization):
+            m._bias_producer = None
+            m._fused_relu = False
+        if isinstance(m, Threshold):
+            m._passthrough = False
+        if isinstance(m, ConcatTable):
+            m._residual = None
+        if isinstance(m, CAddTable):
+            m._passthrough = False
+    return model

@@ -126,10 +126,14 @@ class SpatialConvolution(TensorModule):
             pad = (pt, pl)
         return x, pad, batched, (pt, pb, pl, pr)
 
+    #: BN this conv's bias is folded into (set by bigdl.nn.fusion); the BN adds it implicitly and
+    #: accumulates its gradient, so the conv skips both
+    _bias_folded_into = None
+
     def updateOutput(self, input):
         x, pad, batched, _ = self._prep(input)
         w4 = self._w4(self.cw("weight"))
-        b = self.cw("bias") if self.withBias else None
+        b = self.cw("bias") if (self.withBias and self._bias_folded_into is None) else None
         y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                self.nGroup)
         if self.format == "NHWC":
@@ -145,10 +149,11 @@ class SpatialConvolution(TensorModule):
         w4 = self._w4(self.cw("weight"))
         gw = self._w4(self.gradWeight) if acc else None
         same_scale = self.scale_b == self.scale_w
-        gb = self.gradBias if (acc and self.withBias and same_scale) else None
+        own_bias = self.withBias and self._bias_folded_into is None
+        gb = self.gradBias if (acc and own_bias and same_scale) else None
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                  self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0)
-        if acc and self.withBias and not same_scale and self.scale_b != 0:
+        if acc and own_bias and not same_scale and self.scale_b != 0:
             self.gradBias.add_(gy.float().sum((0, 2, 3)), alpha=self.scale_b)
         if need_input and gi is not None:
             pt, pb, pl, pr = pads

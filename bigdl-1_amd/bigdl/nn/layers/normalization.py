@@ -96,73 +96,129 @@ class BatchNormalization(TensorModule):
         var = s[C:2 * C] / cnt - mean * mean
         return mean, var.clamp_min(0), cnt
 
+    # --- fusion hooks (set by bigdl.nn.fusion) ---------------------------------------------
+    #: conv whose bias was folded into this BN (its output excludes the bias)
+    _bias_producer = None
+
+    def _in_bias(self):
+        p = self._bias_producer
+        if p is None or not getattr(p, "withBias", False):
+            return None
+        return p.cw("bias", torch.float32)
+
+    def forward_residual(self, x, residual, relu):
+        """y = [relu](BN(x) + residual) — the fused ResNet block tail (K9)."""
+        self._residual_mode = True
+        self._res_relu = relu
+        try:
+            self.output = self._forward_impl(x, residual, relu)
+        finally:
+            self._residual_mode = False
+        return self.output
+
     def updateOutput(self, input):
+        return self._forward_impl(input, None, self._fused_relu)
+
+    def _forward_impl(self, input, residual, relu):
         x = input
         if x.dim() == 1:
             x = x.unsqueeze(0)
         x = to_device_layout(x) if x.dim() == 4 else x
+        if residual is not None and residual.dim() == 4:
+            residual = to_device_layout(residual)
         g = self.cw("weight", torch.float32) if self.affine else None
         b = self.cw("bias", torch.float32) if self.affine else None
+        ib = self._in_bias()
+        self._last_relu = relu
         if self.train:
             if self._sync and _dist_ready():
-                y, mean, invstd = self._sync_forward(x, g, b)
+                y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib)
             else:
                 y, mean, invstd = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
-                                                              self.momentum, self.eps, relu=self._fused_relu)
+                                                              self.momentum, self.eps, relu=relu, residual=residual,
+                                                              in_bias=ib)
             self.saveMean, self.saveStd = mean, invstd
         else:
-            y = ops.batchnorm_forward_infer(x, g, b, self.runningMean, self.runningVar, self.eps,
-                                            relu=self._fused_relu)
+            y = ops.batchnorm_forward_infer(x, g, b, self.runningMean, self.runningVar, self.eps, relu=False,
+                                            in_bias=ib)
+            if residual is not None:
+                y = y + residual
+            if relu:
+                y = torch.relu(y)
         return y.reshape(input.shape) if input.dim() == 1 else y
 
-    def _sync_forward(self, x, g, b):
+    def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None):
         mean, var, cnt = self._sync_stats(x)
         invstd = torch.rsqrt(var + self.eps)
         with torch.no_grad():
-            self.runningMean.mul_(1 - self.momentum).add_(mean, alpha=self.momentum)
+            tm = mean if in_bias is None else mean + in_bias
+            self.runningMean.mul_(1 - self.momentum).add_(tm, alpha=self.momentum)
             self.runningVar.mul_(1 - self.momentum).add_(var * (cnt / (cnt - 1).clamp_min(1)), alpha=self.momentum)
         shape = [1, x.shape[1]] + [1] * (x.dim() - 2)
         y = (x.float() - mean.view(shape)) * invstd.view(shape)
         if g is not None:
             y = y * g.view(shape) + b.view(shape)
-        if self._fused_relu:
+        if residual is not None:
+            y = y + residual.float()
+        if relu:
             y = torch.relu(y)
         return y.to(x.dtype), mean, invstd
 
-    def _bwd(self, input, gradOutput, need_input, acc):
+    def _bwd(self, input, gradOutput, need_input, acc, want_gres=False):
         x = input if input.dim() > 1 else input.unsqueeze(0)
         gy = gradOutput if gradOutput.dim() > 1 else gradOutput.unsqueeze(0)
         if x.dim() == 4:
             x = to_device_layout(x)
             gy = to_device_layout(gy)
-        y = self.output if self._fused_relu else None
+        relu = getattr(self, "_last_relu", self._fused_relu)
+        y = self.output if relu else None
         if y is not None and y.dim() == 1:
             y = y.unsqueeze(0)
         g = self.cw("weight", torch.float32) if self.affine else None
+        prod = self._bias_producer
+        cb = prod.gradBias if (acc and prod is not None and getattr(prod, "withBias", False)) else None
+        cbs = prod.scale_b if prod is not None else 0.0
+        gres = None
         if self._sync and _dist_ready() and self.train:
-            gi = self._sync_backward(x, gy, g, y, need_input, acc)
+            gi = self._sync_backward(x, gy, g, y, need_input, acc, relu)
+            if cb is not None and gi is not None:
+                cb.add_(gi.float().sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
+            if want_gres:
+                gres = gy * (y > 0).to(gy.dtype) if relu else gy
         else:
             same = self.scale_w == self.scale_b
-            gi = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=self._fused_relu,
-                                        need_input=need_input,
-                                        gg_acc=self.gradWeight if (acc and self.affine) else None,
-                                        gb_acc=self.gradBias if (acc and self.affine and same) else None,
-                                        scale=self.scale_w if acc else 0.0)
+            gi, gres = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=relu,
+                                              need_input=need_input,
+                                              gg_acc=self.gradWeight if (acc and self.affine) else None,
+                                              gb_acc=self.gradBias if (acc and self.affine and same) else None,
+                                              scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs,
+                                              want_gres=want_gres)
             if acc and self.affine and not same and self.scale_b != 0:
-                gf = gy.float() * ((y > 0).float() if self._fused_relu else 1.0)
+                gf = gy.float() * ((y > 0).float() if relu else 1.0)
                 dims = [d for d in range(gf.dim()) if d != 1]
                 self.gradBias.add_(gf.sum(dims), alpha=self.scale_b)
         if gi is not None and input.dim() == 1:
             gi = gi.reshape(input.shape)
+        if want_gres:
+            return gi, gres
         return gi
 
-    def _sync_backward(self, x, gy, g, y, need_input, acc):
+    def backward_residual(self, input, gradOutput):
+        """Backward of :meth:`forward_residual`: returns (gradInput, gradient for the residual)."""
+        gi, gres = self._bwd(input, gradOutput, True, True, want_gres=True)
+        self.gradInput = gi
+        for h in self._grad_ready_hooks:
+            h(self)
+        return gi, gres
+
+    def _sync_backward(self, x, gy, g, y, need_input, acc, relu=None):
+        relu = self._fused_relu if relu is None else relu
         import torch.distributed as dist
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
         shape = [1, C] + [1] * (x.dim() - 2)
         gf = gy.float()
-        if self._fused_relu:
+        if relu:
             gf = gf * (y > 0).float()
         xhat = (x.float() - self.saveMean.view(shape)) * self.saveStd.view(shape)
         n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)

@@ -15,7 +15,12 @@ class CAddTable(TensorModule):
         super().__init__()
         self.inplace = inplace
 
+    #: set by bigdl.nn.fusion when the preceding ConcatTable already produced the sum
+    _passthrough = False
+
     def updateOutput(self, input):
+        if self._passthrough:
+            return input[1]
         ts = list(input)
         out = ts[0]  # ``inplace`` is honoured as a hint only (see Threshold)
         for t in ts[1:]:
@@ -23,6 +28,8 @@ class CAddTable(TensorModule):
         return out
 
     def updateGradInput(self, input, gradOutput):
+        if self._passthrough:
+            return Table(gradOutput, gradOutput)
         gi = Table()
         for i, t in enumerate(list(input)):
             if t.shape == gradOutput.shape:

@@ -78,49 +78,83 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
   }
 }
 
-// Combine partials; write save_mean/save_invstd, apply coefficients scale/shift, update running stats.
-__global__ void k_bn_finalize(const bf16_t* __restrict__ x, const float* __restrict__ partial, int G, long long M,
-                              int C, const float* __restrict__ gamma, const float* __restrict__ beta,
-                              float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float eps,
-                              float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                              float* __restrict__ scale, float* __restrict__ shift) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < G; ++b) {
-    s += (double)partial[(size_t)b * C + c];
-    q += (double)partial[(size_t)(G + b) * C + c];
+// Parallel reduction of the G per-block partials: a 1024-thread block owns 32 channels; its 32 row
+// groups each sum G/32 partials with coalesced 128-B loads (8 in flight per thread), then a LDS tree.
+// Results: red[0][c] = Σ partial[0..G), red[1][c] = Σ partial[G..2G) for the block's 32 channels.
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ partial, int G, int C, int c0,
+                                                float (*lds)[2][33], float& outA, float& outB) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = c0 + tx;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    int i = ty;
+#pragma unroll 8
+    for (; i < G; i += 32) {
+      a += partial[(size_t)i * C + c];
+      b += partial[(size_t)(G + i) * C + c];
+    }
   }
-  double K = (double)bf2f(x[c]);
-  double dm = s / (double)M;
-  double var = q / (double)M - dm * dm;
-  if (var < 0) var = 0;
-  double mean = K + dm;
-  float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  save_mean[c] = (float)mean;
+  lds[ty][0][tx] = a;
+  lds[ty][1][tx] = b;
+  __syncthreads();
+  for (int s = 16; s > 0; s >>= 1) {
+    if (ty < s) {
+      lds[ty][0][tx] += lds[ty + s][0][tx];
+      lds[ty][1][tx] += lds[ty + s][1][tx];
+    }
+    __syncthreads();
+  }
+  outA = lds[0][0][tx];
+  outB = lds[0][1][tx];
+}
+
+// Combine partials; write save_mean/save_invstd, apply coefficients scale/shift, update running stats.
+// ``in_bias`` (optional) is a per-channel constant the producer did NOT add to x (a conv bias folded
+// into this BN): normalisation is shift-invariant, so only the running mean sees it.
+__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const float* __restrict__ partial,
+                                                      int G, long long M, int C, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      const float* __restrict__ in_bias,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                      float momentum, float eps, float* __restrict__ save_mean,
+                                                      float* __restrict__ save_invstd, float* __restrict__ scale,
+                                                      float* __restrict__ shift) {
+  __shared__ float lds[32][2][33];
+  float s, q;
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  if ((threadIdx.x >> 5) != 0 || c >= C) return;
+  float K = bf2f(x[c]);
+  float dm = s / (float)M;
+  float var = fmaxf(q / (float)M - dm * dm, 0.f);
+  float mean = K + dm;
+  float invstd = rsqrtf(var + eps);
+  save_mean[c] = mean;
   save_invstd[c] = invstd;
   float gm = gamma ? gamma[c] : 1.f;
   float bt = beta ? beta[c] : 0.f;
   float sc = gm * invstd;
   scale[c] = sc;
-  shift[c] = bt - (float)mean * sc;
+  shift[c] = bt - mean * sc;
   if (run_mean) {
-    double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    float true_mean = mean + (in_bias ? in_bias[c] : 0.f);
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * true_mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
   }
 }
 
-// inference coefficients from running stats
+// inference coefficients from running stats (x excludes an optional folded producer bias)
 __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                const float* __restrict__ run_mean, const float* __restrict__ run_var, float eps,
-                                float* __restrict__ scale, float* __restrict__ shift) {
+                                const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                                const float* __restrict__ in_bias, float eps, float* __restrict__ scale,
+                                float* __restrict__ shift) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float invstd = rsqrtf(run_var[c] + eps);
   float sc = (gamma ? gamma[c] : 1.f) * invstd;
   scale[c] = sc;
-  shift[c] = (beta ? beta[c] : 0.f) - run_mean[c] * sc;
+  shift[c] = (beta ? beta[c] : 0.f) - (run_mean[c] - (in_bias ? in_bias[c] : 0.f)) * sc;
 }
 
 // ------------------------------------------------------------------------------------------------ apply
@@ -174,9 +208,9 @@ BIGDL_EXPORT int bigdl_bn_num_partials(long long M, int C) {
   int CG = C / 8;
   int tpr = CG < 256 ? CG : 256;
   int rpi = 256 / tpr;
-  long long target_rows = (long long)rpi * 16;  // ≥16 rows per thread per block
+  long long target_rows = (long long)rpi * 32;  // ≥32 rows per thread per block
   long long G = (M + target_rows - 1) / target_rows;
-  if (G > 1024) G = 1024;
+  if (G > 512) G = 512;
   if (G < 1) G = 1;
   return (int)G;
 }
@@ -190,17 +224,17 @@ static size_t stats_smem(int C) {
 
 // Training forward.  ws: partial buffer of 2·G·C floats; coef: 2·C floats (scale, shift).
 BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
-                                    const float* beta, float* run_mean, float* run_var, float momentum, float eps,
-                                    float* save_mean, float* save_invstd, float* ws, float* coef, int relu,
-                                    hipStream_t s) {
+                                    const float* beta, const float* in_bias, float* run_mean, float* run_var,
+                                    float momentum, float eps, float* save_mean, float* save_invstd, float* ws,
+                                    float* coef, int relu, hipStream_t s) {
   if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
   int G = bigdl_bn_num_partials(M, C);
   long long rpb = (M + G - 1) / G;
   size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, ws, G, M, C, gamma,
-                     beta, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, ws, G, M, C, gamma,
+                     beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;
@@ -213,11 +247,11 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
 }
 
 BIGDL_EXPORT int bigdl_bn_fwd_infer(const void* x, void* y, long long M, int C, const float* gamma, const float* beta,
-                                    const float* run_mean, const float* run_var, float eps, float* coef, int relu,
-                                    hipStream_t s) {
+                                    const float* run_mean, const float* run_var, const float* in_bias, float eps,
+                                    float* coef, int relu, hipStream_t s) {
   if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bn_infer_coef, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, run_mean, run_var, eps,
-                     coef, coef + C);
+  hipLaunchKernelGGL(k_bn_infer_coef, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, run_mean, run_var,
+                     in_bias, eps, coef, coef + C);
   int grid = apply_grid(M, C);
   if (relu)
     hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, nullptr, (bf16_t*)y,
@@ -287,20 +321,23 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const bf16_t* __restrict_
 
 // dβ = Σg', dγ = invstd·Σg'(x−μ); accumulate scale·dγ, scale·dβ into the fp32 grad arena;
 // coefficients for gx = A·g' + B·x + Cc
-__global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int G, long long M, int C,
-                                  const float* __restrict__ gamma, const float* __restrict__ mean,
-                                  const float* __restrict__ invstd, float* __restrict__ ggamma,
-                                  float* __restrict__ gbeta, float gscale, float* __restrict__ coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int i = 0; i < G; ++i) {
-    a += (double)partial[(size_t)i * C + c];
-    b += (double)partial[(size_t)(G + i) * C + c];
-  }
+// ``cbias`` (optional): gradient of a producer bias folded into this BN = Σ_rows gx, evaluated from
+// the closed form A·Σg' + B·Σx + M·Cc (Σx = M·mean) and accumulated with ``cbscale``.
+__global__ void __launch_bounds__(1024) k_bn_bwd_finalize(const float* __restrict__ partial, int G, long long M,
+                                                          int C, const float* __restrict__ gamma,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          float* __restrict__ ggamma, float* __restrict__ gbeta,
+                                                          float gscale, float* __restrict__ cbias, float cbscale,
+                                                          float* __restrict__ coef) {
+  __shared__ float lds[32][2][33];
+  float a, b;
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  if ((threadIdx.x >> 5) != 0 || c >= C) return;
   float is = invstd[c];
-  float dbeta = (float)a;
-  float dgamma = (float)(b * (double)is);
+  float dbeta = a;
+  float dgamma = b * is;
   if (ggamma) ggamma[c] += gscale * dgamma;
   if (gbeta) gbeta[c] += gscale * dbeta;
   float gm = gamma ? gamma[c] : 1.f;
@@ -310,6 +347,7 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int G, long
   coef[c] = A;
   coef[C + c] = B;
   coef[2 * C + c] = Cc;
+  if (cbias) cbias[c] += cbscale * (A * dbeta + B * (float)M * mean[c] + (float)M * Cc);
 }
 
 template <bool RELU, bool GRES>
@@ -354,7 +392,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
 // gres (optional): receives g' (the masked upstream gradient) for a fused residual branch.
 BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void* gx, void* gres, long long M, int C,
                               const float* gamma, const float* mean, const float* invstd, float* ggamma,
-                              float* gbeta, float gscale, float* ws, float* coef, int relu, hipStream_t s) {
+                              float* gbeta, float gscale, float* cbias, float cbscale, float* ws, float* coef,
+                              int relu, hipStream_t s) {
   if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
   int G = bigdl_bn_num_partials(M, C);
   long long rpb = (M + G - 1) / G;
@@ -365,8 +404,8 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
                        (const bf16_t*)y, M, C, rpb, mean, ws, G);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, s, ws, G, M, C, gamma, mean, invstd,
-                     ggamma, gbeta, gscale, coef);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, ws, G, M, C, gamma, mean, invstd,
+                     ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
     const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;

@@ -107,12 +107,13 @@ def _f32vec(t, C_):
 
 
 @register("batchnorm_forward_train")
-def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None):
+def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
+                            in_bias=None):
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
-    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var)):
+    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
                                  residual.dtype != _bf16 or not _al16(residual)):
@@ -125,31 +126,32 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
     check(lib.bigdl_bn_fwd_train(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
-                                 ptr(running_mean), ptr(running_var), _f(momentum), _f(eps), ptr(mean), ptr(invstd),
-                                 ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()), "bn_fwd_train")
+                                 ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum), _f(eps), ptr(mean),
+                                 ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()), "bn_fwd_train")
     return y, mean, invstd
 
 
 @register("batchnorm_forward_infer")
-def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False):
+def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False, in_bias=None):
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
-    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var)):
+    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
     check(_lib().bigdl_bn_fwd_infer(ptr(x), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta), ptr(running_mean),
-                                    ptr(running_var), _f(eps), ptr(coef), C.c_int(1 if relu else 0), _s()),
-          "bn_fwd_infer")
+                                    ptr(running_var), ptr(in_bias), _f(eps), ptr(coef), C.c_int(1 if relu else 0),
+                                    _s()), "bn_fwd_infer")
     return y
 
 
-def bn_backward_ex(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, need_input=True, gg_acc=None,
-                   gb_acc=None, scale=1.0, want_gres=False):
-    """Native BN backward; with ``want_gres`` also returns g' (masked upstream grad) for a fused
-    residual branch.  Returns NotImplemented if unsupported."""
+@register("batchnorm_backward")
+def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, need_input=True, gg_acc=None,
+                       gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, want_gres=False):
+    """Returns (gradInput or None, g' or None).  g' is the masked upstream gradient for a fused
+    residual branch (``want_gres``); ``cbias_acc`` receives the gradient of a folded producer bias."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -158,7 +160,7 @@ def bn_backward_ex(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, nee
         return NotImplemented
     if relu and (y is None or y.dtype != _bf16 or y.stride() != x.stride() or not _al16(y)):
         return NotImplemented
-    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc)):
+    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc)):
         return NotImplemented
     lib = _lib()
     G = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
@@ -168,17 +170,9 @@ def bn_backward_ex(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, nee
     gres = torch.empty_like(x) if want_gres else None
     check(lib.bigdl_bn_bwd(ptr(gy), ptr(x), ptr(y if relu else None), ptr(gx), ptr(gres), _ll(M), C.c_int(C_),
                            ptr(gamma), ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
-                           ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()), "bn_bwd")
+                           ptr(cbias_acc), _f(cbias_scale), ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()),
+          "bn_bwd")
     return gx, gres
-
-
-@register("batchnorm_backward")
-def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, need_input=True, gg_acc=None,
-                       gb_acc=None, scale=1.0):
-    r = bn_backward_ex(gy, x, gamma, save_mean, save_invstd, y, relu, need_input, gg_acc, gb_acc, scale)
-    if r is NotImplemented:
-        return r
-    return r[0]
 
 
 # ------------------------------------------------------------------------------------------------ softmax / CE

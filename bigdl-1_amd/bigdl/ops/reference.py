@@ -70,7 +70,8 @@ def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups
 
 
 # ------------------------------------------------------------------------- batch norm
-def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None):
+def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
+                            in_bias=None):
     """Training BN (``SpatialBatchNormalization.updateOutputNCHWTrainFloat``, ``:1211``).
 
     Normalises with the biased variance, updates ``runningVar`` with the UNBIASED variance and
@@ -87,7 +88,8 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     if running_mean is not None:
         with torch.no_grad():
             unbiased = var * (n / max(n - 1, 1))
-            running_mean.mul_(1 - momentum).add_(mean, alpha=momentum)
+            true_mean = mean if in_bias is None else mean + in_bias.float()
+            running_mean.mul_(1 - momentum).add_(true_mean, alpha=momentum)
             running_var.mul_(1 - momentum).add_(unbiased, alpha=momentum)
     shape = [1, C] + [1] * (x.dim() - 2)
     g = gamma.float().view(shape) if gamma is not None else 1.0
@@ -100,12 +102,14 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     return y.to(x.dtype), mean, invstd
 
 
-def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False):
+def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False, in_bias=None):
+    """Inference BN; ``in_bias`` is a per-channel producer bias folded into this BN (x excludes it)."""
     C = x.shape[1]
     shape = [1, C] + [1] * (x.dim() - 2)
     invstd = torch.rsqrt(running_var.float() + eps)
     scale = invstd * (gamma.float() if gamma is not None else 1.0)
-    shift = (beta.float() if beta is not None else 0.0) - running_mean.float() * scale
+    rm = running_mean.float() - (in_bias.float() if in_bias is not None else 0.0)
+    shift = (beta.float() if beta is not None else 0.0) - rm * scale
     y = x.float() * scale.view(shape) + shift.view(shape)
     if relu:
         y = torch.relu(y)
@@ -113,7 +117,7 @@ def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu
 
 
 def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False, need_input=True, gg_acc=None,
-                       gb_acc=None, scale=1.0):
+                       gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, want_gres=False):
     """Returns (gradInput, gradGamma, gradBeta) — ``updateGradInputNCHWTrainFloat`` (:1048) and
     ``accGradientNCHWFloat`` (:1970).  With ``relu`` the ReLU mask is taken from ``y`` (the BN+ReLU
     output) and fused in (K7/K8)."""
@@ -127,16 +131,18 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
     dbeta = g.sum(dim=dims)
     dgamma = (g * xhat).sum(dim=dims)
     gi = None
-    if need_input:
+    if need_input or cbias_acc is not None:
         n = x.numel() // C
         gam = gamma.float().view(shape) if gamma is not None else 1.0
-        gi = (gam * save_invstd.view(shape) / n) * (n * g - dbeta.view(shape) - xhat * dgamma.view(shape))
-        gi = gi.to(x.dtype)
+        gif = (gam * save_invstd.view(shape) / n) * (n * g - dbeta.view(shape) - xhat * dgamma.view(shape))
+        if cbias_acc is not None and cbias_scale != 0:
+            cbias_acc.add_(gif.sum(dim=dims), alpha=cbias_scale)
+        gi = gif.to(x.dtype) if need_input else None
     if gg_acc is not None and scale != 0:
         gg_acc.add_(dgamma, alpha=scale)
     if gb_acc is not None and scale != 0:
         gb_acc.add_(dbeta, alpha=scale)
-    return gi
+    return gi, (g.to(gy.dtype) if want_gres else None)
 
 
 # ------------------------------------------------------------------------- pooling

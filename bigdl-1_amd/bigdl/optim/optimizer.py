@@ -218,9 +218,11 @@ class BaseOptimizer:
 
     # ------------------------------------------------------------------------------ setup
     def _setup_model(self):
+        from ..nn.fusion import fuse
         m = self.model
         m.to(self.device)
         m.training()
+        fuse(m)
         flat_w, flat_g = m.getParameters()
         self.flat = m.flat_parameters()
         if self.flat is not None and self.device.type == "cuda" and self.compute_dtype != torch.float32:

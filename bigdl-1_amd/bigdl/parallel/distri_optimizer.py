@@ -80,9 +80,11 @@ class DistriOptimizer(BaseOptimizer):
 
     # ------------------------------------------------------------------------------ setup
     def _setup_model(self):
+        from ..nn.fusion import fuse
         m = self.model
         m.to(self.device)
         m.training()
+        fuse(m)
         W = self.world
         self.flat = m.compactParametersBucketed(self.bucket_bytes, 64 * W)
         if self.flat is None:

@@ -83,10 +83,16 @@ def test_bn_forward_backward(shape, relu, res):
     gy = _cl(gy) if len(shape) == 4 else gy
     gg, gb = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     gg2, gb2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-    gx = N.batchnorm_backward(gy, x, gamma, mean, invstd, y=y, relu=relu, gg_acc=gg, gb_acc=gb, scale=0.5)
-    assert gx is not NotImplemented
-    gxr = R.batchnorm_backward(gy.float(), x.float(), gamma, mean, invstd, y=y.float(), relu=relu, gg_acc=gg2,
-                               gb_acc=gb2, scale=0.5)
+    cb, cb2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    out = N.batchnorm_backward(gy, x, gamma, mean, invstd, y=y, relu=relu, gg_acc=gg, gb_acc=gb, scale=0.5,
+                               cbias_acc=cb, cbias_scale=1.0, want_gres=res)
+    assert out is not NotImplemented
+    gx, gres = out
+    gxr, gresr = R.batchnorm_backward(gy.float(), x.float(), gamma, mean, invstd, y=y.float(), relu=relu,
+                                      gg_acc=gg2, gb_acc=gb2, scale=0.5, cbias_acc=cb2, want_gres=res)
+    torch.testing.assert_close(cb, cb2, rtol=0, atol=5e-2)
+    if res:
+        torch.testing.assert_close(gres.float(), gresr.float())
     torch.testing.assert_close(gg, gg2, rtol=2e-3, atol=2e-2)
     torch.testing.assert_close(gb, gb2, rtol=2e-3, atol=2e-2)
     torch.testing.assert_close(gx.float(), gxr.float(), rtol=3e-2, atol=3e-2)
