@@ -1,0 +1,175 @@
+"""Checkpoint / resume.
+
+Reference: on trigger ``getModel`` gathers shards and saves ``model.<neval>`` plus one
+``optimMethod-<name>.<neval>`` per OptimMethod (``DL/optim/AbstractOptimizer.scala:205-231``,
+``Optimizer.scala:548-586``), overwriting fixed names with ``overWriteCheckpoint``; resume takes the
+latest files by mtime (``DistriOptimizer.scala:986-1003``).  The reference writes those with Java
+serialisation, which is not reproducible outside a JVM, so here:
+
+* ``model.<neval>`` is a ``.bigdl`` protobuf (loadable with ``Module.loadModule``);
+* ``optimMethod-<name>.<neval>`` is a BigDLModule-schema protobuf whose ``moduleType`` is the
+  OptimMethod's Scala class name, hyper-parameters are attrs and every state tensor / scalar
+  (momentum buffer, ``epoch``, ``neval``, ``evalCounter`` …) lives under the ``state`` attr;
+* with sharded (ZeRO-1) optimiser state each rank also writes ``….rank<r>`` with its shard's state.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import bigdl_pb as pb
+from .module_serializer import _SerCtx, _DeCtx, _set_attr, _get_attr, _storage_from_pb, save_module, load_module
+
+_SKIP = {"state", "shadow", "grad_scale", "slices", "_first", "_clr", "_t"}
+
+
+def optim_to_pb(method) -> pb.BigDLModule:
+    ctx = _SerCtx()
+    mp = pb.BigDLModule()
+    mp.moduleType = method.scala_class_name()
+    mp.name = type(method).__name__
+    for k, v in vars(method).items():
+        if k in _SKIP or k.startswith("_"):
+            continue
+        if isinstance(v, (int, float, bool, str)) or v is None:
+            _set_attr(ctx, mp.attr[k], v)
+        elif isinstance(v, torch.Tensor):
+            _set_attr(ctx, mp.attr[k], v)
+        else:
+            # schedules etc.: store their simple fields
+            try:
+                _set_attr(ctx, mp.attr[k], json.dumps({"type": type(v).__name__, **{a: b for a, b in vars(v).items()
+                                                                                     if isinstance(b, (int, float, str, bool, list))}}))
+            except TypeError:
+                pass
+    st = mp.attr["state"]
+    st.dataType = pb.DataType["NAME_ATTR_LIST"]
+    st.nameAttrListValue.name = "state"
+    for k, v in method.state.items():
+        if isinstance(v, (torch.Tensor, int, float, bool, str)):
+            _set_attr(ctx, st.nameAttrListValue.attr[k], v)
+    # storages inline (optimizer state is never shared with a model)
+    g = mp.attr["global_storage"]
+    g.dataType = pb.DataType["NAME_ATTR_LIST"]
+    g.nameAttrListValue.name = "global_storage"
+    for tid, tp in ctx.storages.items():
+        av = g.nameAttrListValue.attr[str(tid)]
+        av.dataType = pb.DataType["TENSOR"]
+        av.tensorValue.CopyFrom(tp)
+    return mp
+
+
+def optim_from_pb(mp):
+    from .. import optim as O
+    name = mp.moduleType.rsplit(".", 1)[-1]
+    cls = getattr(O, name)
+    storages = {}
+    if "global_storage" in mp.attr:
+        for _, av in mp.attr["global_storage"].nameAttrListValue.attr.items():
+            sp = av.tensorValue.storage
+            flat = _storage_from_pb(sp)
+            if flat is not None:
+                storages[sp.id] = flat
+    ctx = _DeCtx(storages)
+    m = cls.__new__(cls)
+    O.OptimMethod.__init__(m)
+    proto = cls()
+    m.__dict__.update(proto.__dict__)
+    for k, av in mp.attr.items():
+        if k in ("state", "global_storage"):
+            continue
+        v = _get_attr(ctx, av)
+        if isinstance(v, str) and v.startswith("{"):
+            try:
+                d = json.loads(v)
+                sched_cls = getattr(O, d.pop("type"), None)
+                if sched_cls is not None:
+                    obj = sched_cls.__new__(sched_cls)
+                    O.LearningRateSchedule.__init__(obj)
+                    obj.__dict__.update(d)
+                    v = obj
+            except (ValueError, TypeError):
+                pass
+        setattr(m, k, v)
+    m.state = {}
+    if "state" in mp.attr:
+        for k, av in mp.attr["state"].nameAttrListValue.attr.items():
+            v = _get_attr(ctx, av)
+            m.state[k] = v.clone() if isinstance(v, torch.Tensor) else v
+    return m
+
+
+def save_optim_method(method, path: str, over_write: bool = False):
+    if os.path.exists(path) and not over_write:
+        raise FileExistsError(path)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "wb") as f:
+        f.write(optim_to_pb(method).SerializeToString())
+
+
+def load_optim_method(path: str):
+    mp = pb.BigDLModule()
+    with open(path, "rb") as f:
+        mp.ParseFromString(f.read())
+    return optim_from_pb(mp)
+
+
+def _suffix(state, overwrite):
+    return "" if overwrite else f".{state['neval'] - 1}"
+
+
+def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: bool = False):
+    os.makedirs(path, exist_ok=True)
+    sfx = _suffix(state, overwrite)
+    save_module(model, os.path.join(path, "model" + sfx), over_write=True)
+    for name, m in methods.items():
+        m.state.update({k: state[k] for k in ("epoch", "neval", "recordsProcessedThisEpoch") if k in state})
+        save_optim_method(m, os.path.join(path, f"optimMethod-{name}" + sfx), over_write=True)
+    with open(os.path.join(path, "state" + sfx), "w") as f:
+        json.dump({k: (float(v) if isinstance(v, (int, float)) else v) for k, v in state.items()
+                   if isinstance(v, (int, float, str))}, f)
+
+
+def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False):
+    sfx = _suffix(state, overwrite)
+    for name, m in methods.items():
+        save_optim_method(m, os.path.join(path, f"optimMethod-{name}{sfx}.rank{rank}"), over_write=True)
+
+
+def _latest(pattern: str) -> Optional[str]:
+    files = [f for f in glob.glob(pattern) if ".rank" not in f]
+    if not files:
+        return None
+    return max(files, key=os.path.getmtime)
+
+
+def load_latest_checkpoint(path: str) -> Tuple[Optional[object], Dict, Dict]:
+    mfile = _latest(os.path.join(path, "model*"))
+    model = load_module(mfile) if mfile else None
+    methods = {}
+    for f in glob.glob(os.path.join(path, "optimMethod-*")):
+        if ".rank" in f:
+            continue
+        base = os.path.basename(f)[len("optimMethod-"):]
+        name = base.rsplit(".", 1)[0] if base.rsplit(".", 1)[-1].isdigit() else base
+        cur = methods.get(name)
+        if cur is None or os.path.getmtime(f) > cur[0]:
+            methods[name] = (os.path.getmtime(f), f)
+    loaded = {}
+    rank = int(os.environ.get("RANK", "0"))
+    for name, (_, f) in methods.items():
+        shard = f + f".rank{rank}"
+        loaded[name] = load_optim_method(shard if os.path.exists(shard) else f)
+    sfile = _latest(os.path.join(path, "state*"))
+    state = {}
+    if sfile:
+        with open(sfile) as fh:
+            state = json.load(fh)
+        for k in ("epoch", "neval", "recordsProcessedThisEpoch"):
+            if k in state:
+                state[k] = int(state[k])
+    return model, loaded, state
