@@ -1,0 +1,215 @@
+// Implicit-GEMM convolution on MFMA (K1 forward, K2 stride-1 backward-data), NHWC bf16 -> bf16,
+// fp32 accumulation.  Reference: SpatialConvolution.updateOutput (im2col + MKL sgemm per sample,
+// DL/nn/SpatialConvolution.scala:253-362, NNPrimitive.im2colFloat :108); here no im2col is ever
+// materialised — the A operand is gathered straight from the NHWC activation.
+//
+// GEMM view:   D[n = out channel][m = output pixel] = Σ_k W[n][k] · X̂[m][k],  k = (r, s, c)
+//   A operand (MFMA rows)  = weights, KRSC  → row n contiguous in k
+//   B operand (MFMA cols)  = im2col rows gathered on the fly, NHWC → 8 channels per 16-B chunk
+//   so each lane's accumulator holds 4 consecutive OUTPUT CHANNELS of one pixel (D layout of
+//   mfma_f32_16x16x32_bf16: row=(lane>>4)*4+j, col=lane&15) → 8-byte NHWC stores.
+//
+// Tiling: block 128 pixels × BN channels × BK=64, 256 threads = 4 waves (2 × 2), each wave
+// (BN/2) × 64 = (BN/32) × 4 MFMA 16×16×32 tiles.  Global→LDS through registers (the gather needs
+// per-row zero padding, so no global_load_lds), double-buffered LDS, one barrier per k-tile, the
+// next tile's loads issued before the current tile's MFMAs (T14 split).  LDS rows are 128 B with
+// a 16-B-chunk XOR swizzle (chunk ^ (row & 7)) so the ds_read_b128 fragment reads of 16 distinct
+// rows are conflict-free (cdna_hip_programming.md T2).  Blocks are remapped so each XCD gets a
+// contiguous range of tiles (T1; bijective for any grid size).
+#include "common.h"
+
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+struct ConvParams {
+  const bf16_t* x;     // [Nb][H][W][C]
+  const bf16_t* w;     // [K][R][S][C]
+  const float* bias;   // [K] or null
+  bf16_t* y;           // [Nb][P][Q][K]
+  int Nb, H, W, C, K, R, S, P, Q;
+  int sh, sw, ph, pw, dh, dw;
+  int M;               // Nb*P*Q
+  int Kg;              // R*S*C
+  int relu;
+  int tiles_n;
+};
+
+constexpr int BM = 128;
+constexpr int BK = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int BN>
+__global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
+  constexpr int ROWS = BM + BN;
+  constexpr int TN = BN / 32;  // MFMA tiles along channels per wave
+  constexpr int TM = 4;        // MFMA tiles along pixels per wave (64 pixels)
+  constexpr int A_CHUNKS = BM * BK / 8 / 256;  // activation chunks per thread (4)
+  constexpr int B_CHUNKS = BN * BK / 8 / 256;  // weight chunks per thread (4 or 2)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][ROWS * BK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wave_m = wid & 1, wave_n = wid >> 1;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int col8 = tid & 7;  // this thread's 16-B chunk column inside a 64-wide k tile
+
+  // per-row gather state for the activation rows this thread stages
+  int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    int m = m0 + (tid >> 3) + 32 * i;
+    if (m < p.M) {
+      int n = m / (p.P * p.Q);
+      int pq = m - n * p.P * p.Q;
+      int pp = pq / p.Q, qq = pq - pp * p.Q;
+      a_img[i] = n * p.H * p.W;
+      a_h[i] = pp * p.sh - p.ph;
+      a_w[i] = qq * p.sw - p.pw;
+    } else {
+      a_img[i] = -1;
+      a_h[i] = 0;
+      a_w[i] = 0;
+    }
+  }
+
+  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+  const int KT = (p.Kg + BK - 1) / BK;
+
+  auto load_tile = [&](int kt) {
+    const int k = kt * BK + col8 * 8;
+    int tap = 0, c = k, r = 0, s = 0;
+    const bool kin = k < p.Kg;
+    if (kin) {
+      tap = k / p.C;
+      c = k - tap * p.C;
+      r = tap / p.S;
+      s = tap - r * p.S;
+    }
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      int h = a_h[i] + r * p.dh, w = a_w[i] + s * p.dw;
+      bool ok = kin && a_img[i] >= 0 && h >= 0 && h < p.H && w >= 0 && w < p.W;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(p.x + ((size_t)(a_img[i] + h * p.W + w) * p.C + c))
+                 : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      int n = n0 + (tid >> 3) + 32 * i;
+      bool ok = kin && n < p.K;
+      rb[i] = ok ? *reinterpret_cast<const uint4*>(p.w + ((size_t)n * p.Kg + k)) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(&lds[buf][swz(row, col8)]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      int row = BM + (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(&lds[buf][swz(row, col8)]) = rb[i];
+    }
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tile(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        int row = BM + wave_n * (BN / 2) + i * 16 + fr;
+        af[i] = *reinterpret_cast<const v8s*>(&lds[buf][swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        int row = wave_m * 64 + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v8s*>(&lds[buf][swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: bias, relu, bf16, 8-byte stores of 4 consecutive channels
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
+    if (n >= p.K) continue;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b4[j] = (n + j < p.K) ? p.bias[n + j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wave_m * 64 + j * 16 + fr;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + b4[e];
+        if (p.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      bf16_t* dst = p.y + (size_t)m * p.K + n;
+      if (n + 4 <= p.K) {
+        uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+      } else {
+        for (int e = 0; e < 4 && n + e < p.K; ++e) dst[e] = f2bf(v[e]);
+      }
+    }
+  }
+}
+
+// Host launcher.  Requirements (checked): C % 8 == 0, K % 4 == 0, 16-B aligned x/w, 8-B aligned y.
+BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W, int C,
+                                int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                                int relu, hipStream_t s) {
+  if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
+  ConvParams p;
+  p.x = (const bf16_t*)x;
+  p.w = (const bf16_t*)w;
+  p.bias = bias;
+  p.y = (bf16_t*)y;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.M = Nb * P * Q;
+  p.Kg = R * S * C;
+  p.relu = relu;
+  const int BN = K <= 64 ? 64 : 128;
+  p.tiles_n = (K + BN - 1) / BN;
+  long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
+  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
+  if (BN == 64)
+    hipLaunchKernelGGL(k_conv_fwd<64>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_conv_fwd<128>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  BIGDL_CHECK_LAUNCH();
+}

@@ -1,0 +1,242 @@
+// Convolution weight gradient on MFMA (K3): dW[n][k] += scale · Σ_m dY[m][n] · X̂[m][k],
+// m = output pixel (N·P·Q), k = (r, s, c) — reference SpatialConvolution.accGradParameters
+// (DL/nn/SpatialConvolution.scala:435-505, a per-sample gemm into gradWeight).
+//
+// Both operands arrive pixel-major (NHWC rows).  Tiles are staged in LDS exactly as loaded
+// ([pixel][channel], 16-B chunks) and the MFMA fragments, which need 8 consecutive PIXELS per
+// lane, are read with gfx950's ds_read_b64_tr_b16 transposed read (cdna_hip_programming.md T10):
+// lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4×16 block and receives
+// column (lane) of the 4 rows.  The LDS image is XOR-swizzled on 32-B segments so each 32-lane half
+// (8 rows × 32 B) hits all 64 banks exactly once.
+// The reduction over pixels is split across blockIdx.y; partial tiles are added straight into the
+// fp32 gradient (KRSC, the arena's physical layout) with no-return float atomics (Guideline 12).
+#include "common.h"
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.d = d;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  f.s = l;
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t t = __umulhi(n, f.m);
+  return (t + n) >> f.s;
+}
+
+struct WgradParams {
+  const bf16_t* x;   // [Nb][H][W][C]
+  const bf16_t* dy;  // [Nb][P][Q][K]
+  float* dw;         // [K][R][S][C] fp32, accumulated
+  float scale;
+  int Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw_;
+  int M, Kg, tiles_k, tiles_n, m_per_split;
+  FastDiv fPQ, fQ;
+};
+
+constexpr int BP = 64;  // pixels per k-tile
+
+// byte offset inside a [BP rows][WIDTH bf16] tile for a 16-B chunk / 8-B quad
+template <int WIDTH>
+__device__ __forceinline__ int tr_swz_dword(int row, int dword) {
+  if constexpr (WIDTH == 128) {
+    int seg = (row & 3) | (((row >> 3) & 1) << 2);
+    return row * 64 + (dword ^ (seg << 3));
+  } else {
+    int seg = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    return row * 32 + (dword ^ (seg << 3));
+  }
+}
+
+template <int TILE_N, int TILE_K>
+__global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
+  constexpr int DY_CH = BP * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
+  constexpr int X_CH = BP * TILE_K / 8 / 256;   // for the X̂ tile
+  constexpr int TMN = TILE_N / 32;              // MFMA tiles per wave along n
+  constexpr int TMK = TILE_K / 32;              // along k
+  constexpr int DY_WORDS = BP * TILE_N / 2;     // dwords per tile
+  constexpr int X_WORDS = BP * TILE_K / 2;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[2][DY_WORDS + X_WORDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wave_n = wid & 1, wave_k = wid >> 1;
+  // tile mapping (XCD-contiguous ranges of the tile grid)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tnI = tile / p.tiles_k, tkI = tile - tnI * p.tiles_k;
+  const int n0 = tnI * TILE_N, k0 = tkI * TILE_K;
+  const int mbeg = blockIdx.y * p.m_per_split;
+  int mend = mbeg + p.m_per_split;
+  if (mend > p.M) mend = p.M;
+  if (mbeg >= mend) return;
+
+  // this thread's fixed chunk columns
+  constexpr int DY_CPR = TILE_N / 8;  // chunks per row
+  constexpr int X_CPR = TILE_K / 8;
+  const int dy_col = tid % DY_CPR, dy_row0 = tid / DY_CPR;
+  const int x_col = tid % X_CPR, x_row0 = tid / X_CPR;
+  constexpr int DY_RSTEP = 256 / DY_CPR, X_RSTEP = 256 / X_CPR;
+  // X̂ column → (tap, c) once
+  const int kx = k0 + x_col * 8;
+  const bool kx_ok = kx < p.Kg;
+  int tap = kx_ok ? kx / p.C : 0;
+  const int cx = kx - tap * p.C;
+  const int rx = tap / p.S, sx = tap - (tap / p.S) * p.S;
+  const int ndy = n0 + dy_col * 8;
+  const bool ndy_ok = ndy < p.K;
+
+  uint4 rdy[DY_CH], rx_[X_CH];
+  auto load = [&](int mt) {
+#pragma unroll
+    for (int i = 0; i < DY_CH; ++i) {
+      int m = mt + dy_row0 + i * DY_RSTEP;
+      bool ok = ndy_ok && m < mend;
+      rdy[i] = ok ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.K + ndy) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      int m = mt + x_row0 + i * X_RSTEP;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kx_ok && m < mend) {
+        uint32_t n = fdiv((uint32_t)m, p.fPQ);
+        uint32_t pq = (uint32_t)m - n * (uint32_t)(p.P * p.Q);
+        uint32_t pp = fdiv(pq, p.fQ);
+        uint32_t q = pq - pp * (uint32_t)p.Q;
+        int h = (int)pp * p.sh - p.ph + rx * p.dh;
+        int w = (int)q * p.sw - p.pw + sx * p.dw_;
+        if (h >= 0 && h < p.H && w >= 0 && w < p.W)
+          v = *reinterpret_cast<const uint4*>(p.x + ((size_t)((n * p.H + h) * p.W + w) * p.C + cx));
+      }
+      rx_[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < DY_CH; ++i) {
+      int row = dy_row0 + i * DY_RSTEP;
+      *reinterpret_cast<uint4*>(&lds[buf][tr_swz_dword<TILE_N>(row, dy_col * 4)]) = rdy[i];
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      int row = x_row0 + i * X_RSTEP;
+      *reinterpret_cast<uint4*>(&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = rx_[i];
+    }
+  };
+
+  v4f acc[TMN][TMK];
+#pragma unroll
+  for (int i = 0; i < TMN; ++i)
+#pragma unroll
+    for (int j = 0; j < TMK; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  load(mbeg);
+  store(0);
+  __syncthreads();
+
+  const int g = (lane >> 4) & 3;  // 16-lane group → pixels 8g..8g+7 of a 32-pixel k-step
+  const int t = lane & 15, q4 = t >> 2, p4 = t & 3;
+  int buf = 0;
+  for (int mt = mbeg; mt < mend; mt += BP) {
+    const bool more = mt + BP < mend;
+    if (more) load(mt + BP);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8s af[TMN], bfr[TMK];
+#pragma unroll
+      for (int i = 0; i < TMN; ++i) {
+        const int col = wave_n * (TILE_N / 2) + i * 16 + 4 * p4;  // channel of this lane's quad
+        const int r0 = kk * 32 + 8 * g + q4;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)&lds[buf][tr_swz_dword<TILE_N>(r0, col >> 1)]);
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)&lds[buf][tr_swz_dword<TILE_N>(r0 + 4, col >> 1)]);
+        af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TMK; ++j) {
+        const int col = wave_k * (TILE_K / 2) + j * 16 + 4 * p4;
+        const int r0 = kk * 32 + 8 * g + q4;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(r0, col >> 1)]);
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(r0 + 4, col >> 1)]);
+        bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TMN; ++i)
+#pragma unroll
+        for (int j = 0; j < TMK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // epilogue: D[row = n][col = k]; lane holds rows (lane>>4)*4 + e of column lane&15
+#pragma unroll
+  for (int i = 0; i < TMN; ++i) {
+#pragma unroll
+    for (int j = 0; j < TMK; ++j) {
+      const int k = k0 + wave_k * (TILE_K / 2) + j * 16 + (lane & 15);
+      if (k >= p.Kg) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wave_n * (TILE_N / 2) + i * 16 + (lane >> 4) * 4 + e;
+        if (n < p.K) atomicAdd(p.dw + (size_t)n * p.Kg + k, p.scale * acc[i][j][e]);
+      }
+    }
+  }
+}
+
+// dw += scale · wgrad.  Requirements (checked): C % 8 == 0, K % 8 == 0, 16-B aligned x/dy.
+BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C,
+                                  int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
+                                  int splits, hipStream_t s) {
+  if (C % 8 || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
+  WgradParams p;
+  p.x = (const bf16_t*)x;
+  p.dy = (const bf16_t*)dy;
+  p.dw = dw;
+  p.scale = scale;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw_ = dwd;
+  p.M = Nb * P * Q;
+  p.Kg = R * S * C;
+  p.fPQ = make_fastdiv((uint32_t)(P * Q));
+  p.fQ = make_fastdiv((uint32_t)Q);
+  const int TN = K <= 64 ? 64 : 128;
+  const int TK = p.Kg <= 64 ? 64 : 128;
+  p.tiles_n = (K + TN - 1) / TN;
+  p.tiles_k = (p.Kg + TK - 1) / TK;
+  const int tiles = p.tiles_n * p.tiles_k;
+  if (splits <= 0) {
+    // aim for ≈ 2048 blocks (8 per CU) but ≥ 8 k-tiles of pixels per block
+    long long want = (2048 + tiles - 1) / tiles;
+    long long max_by_work = (p.M + 8 * BP - 1) / (8 * BP);
+    splits = (int)(want < max_by_work ? want : max_by_work);
+    if (splits < 1) splits = 1;
+    if (splits > 65535) splits = 65535;
+  }
+  int mps = (p.M + splits - 1) / splits;
+  mps = (mps + BP - 1) / BP * BP;
+  p.m_per_split = mps;
+  splits = (p.M + mps - 1) / mps;
+  dim3 grid(tiles, splits);
+  if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64>), grid, dim3(256), 0, s, p);
+  else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128>), grid, dim3(256), 0, s, p);
+  else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((k_conv_wgrad<128, 128>), grid, dim3(256), 0, s, p);
+  BIGDL_CHECK_LAUNCH();
+}

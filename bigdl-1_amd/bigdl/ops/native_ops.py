@@ -230,6 +230,125 @@ def log_softmax_backward(gy, y):
     return gx
 
 
+# ------------------------------------------------------------------------------------------------ convolution
+def _krsc(w4):
+    """(O, I, kH, kW) view → contiguous (O, kH, kW, I) tensor (a view when already KRSC)."""
+    k = w4.permute(0, 2, 3, 1)
+    return k if k.is_contiguous() else k.contiguous()
+
+
+def _pad_channels(x_nhwc_4d, c_to):
+    """Zero-pad the channel dim of a channels-last NCHW-logical tensor to ``c_to``."""
+    n, c, h, w = x_nhwc_4d.shape
+    out = torch.zeros((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
+    out[..., :c] = x_nhwc_4d.permute(0, 2, 3, 1)
+    return out.permute(0, 3, 1, 2)
+
+
+def _conv_geom_ok(x, w4, groups, dilation):
+    return (groups == 1 and x.dim() == 4 and x.dtype == _bf16 and w4.dtype == _bf16 and
+            x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
+
+
+@register("conv2d_forward")
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+    if not _conv_geom_ok(x, w4, groups, dilation):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    K, Ci, R, S = w4.shape
+    if Ci != C_ or K % 4:
+        return NotImplemented
+    wk = _krsc(w4)
+    if C_ % 8:
+        cp = (C_ + 7) // 8 * 8
+        x = _pad_channels(x, cp)
+        wp = torch.zeros((K, R, S, cp), dtype=wk.dtype, device=wk.device)
+        wp[..., :C_] = wk
+        wk, C_ = wp, cp
+    P = (H + 2 * pad[0] - dilation[0] * (R - 1) - 1) // stride[0] + 1
+    Q = (W + 2 * pad[1] - dilation[1] * (S - 1) - 1) // stride[1] + 1
+    if P <= 0 or Q <= 0 or not _al16(wk):
+        return NotImplemented
+    y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    bias = b.float().contiguous() if b is not None else None
+    check(_lib().bigdl_conv_fwd(ptr(x), ptr(wk), ptr(bias), ptr(y), N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1],
+                                pad[0], pad[1], dilation[0], dilation[1], 0, _s()), "conv_fwd")
+    return y
+
+
+def _dgrad_s1(gy, w4, x_shape, pad, dilation):
+    """stride-1 backward-data as a forward conv of gy with the flipped, transposed kernel."""
+    N_, C_, H, W = x_shape
+    K, Ci, R, S = w4.shape
+    if C_ % 4 or K % 8:
+        return None
+    # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]
+    wt = w4.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    P, Q = gy.shape[2], gy.shape[3]
+    ph = dilation[0] * (R - 1) - pad[0]
+    pw = dilation[1] * (S - 1) - pad[1]
+    if ph < 0 or pw < 0:
+        return None
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_conv_fwd(ptr(gy), ptr(wt), ptr(None), ptr(gx), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw,
+                                dilation[0], dilation[1], 0, _s()), "conv_dgrad")
+    return gx
+
+
+def _dgrad_1x1_strided(gy, w4, x_shape, stride):
+    """1×1 stride-s backward-data: GEMM into the strided positions, zeros elsewhere."""
+    N_, C_, H, W = x_shape
+    K = w4.shape[0]
+    if C_ % 4 or K % 8:
+        return None
+    wt = w4.reshape(K, C_).t().contiguous()  # [C][K] = [C][1][1][K]
+    P, Q = gy.shape[2], gy.shape[3]
+    tmp = torch.empty((N_, C_, P, Q), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_conv_fwd(ptr(gy), ptr(wt), ptr(None), ptr(tmp), N_, P, Q, K, C_, 1, 1, P, Q, 1, 1, 0, 0, 1, 1,
+                                0, _s()), "conv_dgrad_1x1s")
+    gx = torch.zeros((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    gx[:, :, ::stride[0], ::stride[1]] = tmp
+    return gx
+
+
+@register("conv2d_backward")
+def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
+                    scale=1.0):
+    if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
+        return NotImplemented
+    if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    K, Ci, R, S = w4.shape
+    if K % 8:
+        return NotImplemented
+    from . import reference as R_
+    gi = None
+    if need_input:
+        if stride == (1, 1) or tuple(stride) == (1, 1):
+            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)
+        elif R == 1 and S == 1 and tuple(pad) == (0, 0):
+            gi = _dgrad_1x1_strided(gy, w4, x.shape, stride)
+        if gi is None:  # strided k>1 backward-data: library path until the sub-pixel kernel lands
+            gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
+    if gw_acc is not None and scale != 0:
+        xx, cc = x, C_
+        if C_ % 8:
+            cc = (C_ + 7) // 8 * 8
+            xx = _pad_channels(x, cc)
+        direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
+        target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
+        P, Q = gy.shape[2], gy.shape[3]
+        check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
+                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0,
+                                      _s()), "conv_wgrad")
+        if not direct:
+            gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
+    return gi
+
+
 # ------------------------------------------------------------------------------------------------ optimizers
 def _vec_ok(*ts, n):
     for t in ts:

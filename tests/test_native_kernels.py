@@ -180,3 +180,54 @@ def test_layers_use_native_path():
     g = m.backward(x, torch.ones_like(y))
     assert y.dtype == torch.bfloat16 and g.dtype == torch.bfloat16
     assert torch.isfinite(g.float()).all()
+
+
+# ---------------------------------------------------------------------------------------- conv
+CONV_CASES = [
+    # N, C, H, W, K, R, S, stride, pad
+    (2, 64, 14, 14, 256, 1, 1, 1, 0),     # 1x1 expand
+    (2, 256, 14, 14, 64, 1, 1, 1, 0),     # 1x1 reduce (K=64 tile)
+    (2, 64, 15, 13, 64, 3, 3, 1, 1),      # 3x3 s1, odd spatial
+    (2, 128, 16, 16, 128, 3, 3, 2, 1),    # 3x3 s2 (ResNet v1.5 downsample)
+    (2, 256, 14, 14, 512, 1, 1, 2, 0),    # 1x1 s2 projection shortcut
+    (2, 3, 32, 32, 64, 7, 7, 2, 3),       # stem (C=3 padded to 8)
+    (3, 24, 9, 9, 40, 5, 5, 1, 2),        # Inception-ish odd channels
+]
+
+
+def _conv_ref(x, w4, stride, pad):
+    return torch.nn.functional.conv2d(x.float(), w4.float(), None, stride, pad)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_forward(case):
+    N = _native()
+    n, c, h, w, k, r, s, st, pd = case
+    x = _cl(torch.randn(n, c, h, w, device=dev).bfloat16())
+    w4 = _cl(torch.randn(k, c, r, s, device=dev).bfloat16() * 0.1)
+    b = torch.randn(k, device=dev)
+    y = N.conv2d_forward(x, w4, b, (st, st), (pd, pd))
+    assert y is not NotImplemented
+    ref = _conv_ref(x, w4, (st, st), (pd, pd)) + b.view(1, -1, 1, 1)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_backward(case):
+    N = _native()
+    n, c, h, w, k, r, s, st, pd = case
+    if k % 8:
+        pytest.skip("K % 8")
+    x = _cl(torch.randn(n, c, h, w, device=dev).bfloat16())
+    w4 = _cl(torch.randn(k, c, r, s, device=dev).bfloat16() * 0.1)
+    xr = x.float().requires_grad_(True)
+    wr = w4.float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, (st, st), (pd, pd))
+    gy = _cl(torch.randn_like(yr).bfloat16())
+    yr.backward(gy.float())
+    gw = torch.zeros(k, r, s, c, device=dev).permute(0, 3, 1, 2)  # KRSC physical like the arena
+    gw.fill_(0.5)
+    gi = N.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (1, 1), 1, True, gw, None, 2.0)
+    assert gi is not NotImplemented
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(gw, 0.5 + 2.0 * wr.grad, rtol=2e-2, atol=5e-2)
