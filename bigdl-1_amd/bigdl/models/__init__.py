@@ -1,0 +1,5 @@
+"""Model zoo (``DL/models/**`` and the example models): same topology and initialisation."""
+from .lenet import LeNet5  # noqa: F401
+from .resnet import ResNet  # noqa: F401
+from .vgg import VggForCifar10, Vgg_16, Vgg_19  # noqa: F401
+from .rnn import PTBModel, SimpleRNN  # noqa: F401

@@ -9,3 +9,4 @@ from .table_ops import *  # noqa: F401,F403
 from .math_ops import *  # noqa: F401,F403
 from .dropout import *  # noqa: F401,F403
 from .embedding import *  # noqa: F401,F403
+from .recurrent import *  # noqa: F401,F403

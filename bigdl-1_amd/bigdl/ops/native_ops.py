@@ -306,7 +306,8 @@ def _dgrad_1x1_strided(gy, w4, x_shape, stride):
     tmp = torch.empty((N_, C_, P, Q), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
     check(_lib().bigdl_conv_fwd(ptr(gy), ptr(wt), ptr(None), ptr(tmp), N_, P, Q, K, C_, 1, 1, P, Q, 1, 1, 0, 0, 1, 1,
                                 0, _s()), "conv_dgrad_1x1s")
-    gx = torch.zeros((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    gx.zero_()
     gx[:, :, ::stride[0], ::stride[1]] = tmp
     return gx
 

@@ -292,33 +292,49 @@ def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_sc
 
 
 # ------------------------------------------------------------------------- recurrent
-def lstm_cell_forward(gates, c_prev):
+def lstm_cell_forward(xg, hg, c_prev, h_out=None, c_out=None, act_out=None, tc_out=None):
     """Pointwise LSTM cell (``DL/nn/LSTM.scala:124-187``), gate order (i, g, f, o) along the
-    last dim in blocks of H: i=σ, g=tanh, f=σ, o=σ; c' = i·g + f·c; h' = o·tanh(c')."""
+    last dim in blocks of H: i=σ, g=tanh, f=σ, o=σ; c' = i·g + f·c; h' = o·tanh(c').
+    ``xg`` is the input projection for this step (i2g, bias included), ``hg`` the recurrent
+    projection h·Uᵀ (or None); the gate sum is formed here in fp32.  Returns (h, c, act, tc):
+    h in xg's dtype (written into ``h_out`` when given), c/act/tc fp32 (saved for backward)."""
     H = c_prev.shape[-1]
-    gf = gates.float()
+    gf = xg.float() if hg is None else xg.float() + hg.float()
     i = torch.sigmoid(gf[..., 0:H])
     g = torch.tanh(gf[..., H:2 * H])
     f = torch.sigmoid(gf[..., 2 * H:3 * H])
     o = torch.sigmoid(gf[..., 3 * H:4 * H])
     c = i * g + f * c_prev.float()
     tc = torch.tanh(c)
-    h = o * tc
+    h = (o * tc).to(xg.dtype)
     act = torch.cat([i, g, f, o], dim=-1)
-    return h.to(gates.dtype), c, act, tc
+    res = []
+    for v, dst in ((h, h_out), (c, c_out), (act, act_out), (tc, tc_out)):
+        if dst is not None:
+            dst.copy_(v)
+            v = dst
+        res.append(v)
+    return tuple(res)
 
 
-def lstm_cell_backward(gh, gc_next, act, tc, c_prev):
+def lstm_cell_backward(gh, gh2, gc_next, act, tc, c_prev, dg_out=None):
+    """Backward of :func:`lstm_cell_forward`.  ``gh`` (+ ``gh2``, the recurrent gradient, when
+    not None) is dL/dh', ``gc_next`` dL/dc' from the next step (or None).  Returns
+    (d gates [compute dtype of gh], dc_prev fp32)."""
     H = c_prev.shape[-1]
     i, g, f, o = act[..., 0:H], act[..., H:2 * H], act[..., 2 * H:3 * H], act[..., 3 * H:]
-    gh = gh.float()
-    dc = gh * o * (1 - tc * tc) + (gc_next.float() if gc_next is not None else 0.0)
-    do = gh * tc
+    ghf = gh.float() if gh2 is None else gh.float() + gh2.float()
+    dc = ghf * o * (1 - tc * tc) + (gc_next.float() if gc_next is not None else 0.0)
+    do = ghf * tc
     di = dc * g
     dg = dc * i
     df = dc * c_prev.float()
     dc_prev = dc * f
     dgates = torch.cat([di * i * (1 - i), dg * (1 - g * g), df * f * (1 - f), do * o * (1 - o)], dim=-1)
+    dgates = dgates.to(gh.dtype)
+    if dg_out is not None:
+        dg_out.copy_(dgates)
+        dgates = dg_out
     return dgates, dc_prev
 
 
