@@ -389,3 +389,66 @@ def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_sc
     check(_lib().bigdl_adam(ptr(w), ptr(g), ptr(m), ptr(v), ptr(shadow), _ll(n), _f(step_size), _f(beta1), _f(beta2),
                             _f(eps), _f(weight_decay), _f(grad_scale), _s()), "adam")
     return w
+
+
+# ------------------------------------------------------------------------------------------------ LSTM
+def _row_view(t, rows, cols):
+    """(row stride) of a 2-D view with unit column stride, else None."""
+    if t is None:
+        return 0
+    if t.dim() != 2 or t.shape[0] != rows or t.shape[1] != cols or t.stride(1) != 1:
+        return None
+    return t.stride(0)
+
+
+def _f32c(t, n):
+    return t is None or (t.dtype == _f32 and t.is_contiguous() and t.numel() == n and t.is_cuda)
+
+
+@register("lstm_cell_forward")
+def lstm_cell_forward(xg, hg, c_prev, h_out=None, c_out=None, act_out=None, tc_out=None):
+    B, G = xg.shape
+    H = G // 4
+    dt = xg.dtype
+    if dt not in (_bf16, _f32) or G != 4 * H or (hg is not None and hg.dtype != dt):
+        return NotImplemented
+    if c_prev.dtype != _f32 or not c_prev.is_contiguous() or c_prev.shape != (B, H):
+        return NotImplemented
+    ldx, ldhg = _row_view(xg, B, G), _row_view(hg, B, G)
+    if ldx is None or ldhg is None:
+        return NotImplemented
+    h = h_out if h_out is not None else torch.empty(B, H, device=xg.device, dtype=dt)
+    ldh = _row_view(h, B, H)
+    if ldh is None or h.dtype != dt:
+        return NotImplemented
+    c = c_out if c_out is not None else torch.empty(B, H, device=xg.device, dtype=_f32)
+    act = act_out if act_out is not None else torch.empty(B, G, device=xg.device, dtype=_f32)
+    tc = tc_out if tc_out is not None else torch.empty(B, H, device=xg.device, dtype=_f32)
+    if not (_f32c(c, B * H) and _f32c(act, B * G) and _f32c(tc, B * H)):
+        return NotImplemented
+    check(_lib().bigdl_lstm_fwd(ptr(xg), C.c_long(ldx), ptr(hg), C.c_long(ldhg), ptr(c_prev), ptr(h), C.c_long(ldh),
+                                ptr(c), ptr(act), ptr(tc), B, H, 0 if dt == _bf16 else 1, _s()), "lstm_fwd")
+    return h, c, act, tc
+
+
+@register("lstm_cell_backward")
+def lstm_cell_backward(gh, gh2, gc_next, act, tc, c_prev, dg_out=None):
+    B, H = gh.shape
+    dt = gh.dtype
+    if dt not in (_bf16, _f32):
+        return NotImplemented
+    ldgh = _row_view(gh, B, H)
+    if ldgh is None:
+        return NotImplemented
+    if gh2 is not None and (gh2.dtype != dt or not gh2.is_contiguous() or gh2.shape != (B, H)):
+        return NotImplemented
+    if not (_f32c(gc_next, B * H) and _f32c(act, B * 4 * H) and _f32c(tc, B * H) and _f32c(c_prev, B * H)):
+        return NotImplemented
+    dg = dg_out if dg_out is not None else torch.empty(B, 4 * H, device=gh.device, dtype=dt)
+    lddg = _row_view(dg, B, 4 * H)
+    if lddg is None or dg.dtype != dt:
+        return NotImplemented
+    dc = torch.empty(B, H, device=gh.device, dtype=_f32)
+    check(_lib().bigdl_lstm_bwd(ptr(gh), C.c_long(ldgh), ptr(gh2), ptr(gc_next), ptr(act), ptr(tc), ptr(c_prev),
+                                ptr(dg), C.c_long(lddg), ptr(dc), B, H, 0 if dt == _bf16 else 1, _s()), "lstm_bwd")
+    return dg, dc

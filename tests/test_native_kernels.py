@@ -231,3 +231,50 @@ def test_conv_backward(case):
     assert gi is not NotImplemented
     torch.testing.assert_close(gi.float(), xr.grad, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(gw, 0.5 + 2.0 * wr.grad, rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_lstm_cell_kernels(dtype):
+    from bigdl.ops import reference as R
+    N = _native()
+    B, H, Tn = 5, 40, 3
+    seq = torch.randn(B, Tn, 4 * H, device=dev).to(dtype)
+    hg = torch.randn(B, 4 * H, device=dev).to(dtype)
+    c0 = torch.randn(B, H, device=dev)
+    out = torch.zeros(B, Tn, H, device=dev, dtype=dtype)
+    r = N.lstm_cell_forward(seq[:, 1], hg, c0, h_out=out[:, 1])
+    assert r is not NotImplemented
+    e = R.lstm_cell_forward(seq[:, 1], hg, c0)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    for a, b in zip(r, e):
+        torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
+    torch.testing.assert_close(out[:, 1].float(), e[0].float(), rtol=tol, atol=tol)
+    gy = torch.randn(B, Tn, H, device=dev).to(dtype)
+    gh2 = torch.randn(B, H, device=dev).to(dtype)
+    gc = torch.randn(B, H, device=dev)
+    dgs = torch.zeros(B, Tn, 4 * H, device=dev, dtype=dtype)
+    rb = N.lstm_cell_backward(gy[:, 2], gh2, gc, e[2], e[3], c0, dg_out=dgs[:, 2])
+    assert rb is not NotImplemented
+    eb = R.lstm_cell_backward(gy[:, 2], gh2, gc, e[2], e[3], c0)
+    for a, b in zip(rb, eb):
+        torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
+
+
+def test_recurrent_lstm_gpu_vs_cpu():
+    """Recurrent(LSTM) on the GPU (bf16 GEMMs + native cell) vs the CPU fp32 path."""
+    import copy
+    from bigdl.nn import Recurrent, LSTM
+    _native()
+    torch.manual_seed(0)
+    cpu = Recurrent().add(LSTM(32, 64))
+    gpu = copy.deepcopy(cpu).cuda()
+    x = torch.randn(8, 10, 32)
+    y = cpu.forward(x)
+    yg = gpu.forward(x.cuda())
+    torch.testing.assert_close(yg.float().cpu(), y, rtol=3e-2, atol=3e-2)
+    gy = torch.randn_like(y)
+    gi = cpu.backward(x, gy)
+    gig = gpu.backward(x.cuda(), gy.cuda())
+    torch.testing.assert_close(gig.float().cpu(), gi, rtol=5e-2, atol=5e-2)
+    for a, b in zip(gpu.parameters()[1], cpu.parameters()[1]):
+        torch.testing.assert_close(a.float().cpu(), b, rtol=5e-2, atol=5e-2 * float(b.abs().max()))
