@@ -10,3 +10,4 @@ from .math_ops import *  # noqa: F401,F403
 from .dropout import *  # noqa: F401,F403
 from .embedding import *  # noqa: F401,F403
 from .recurrent import *  # noqa: F401,F403
+from .attention import Attention, FeedForwardNetwork, Transformer, SequenceBeamSearch  # noqa: F401

@@ -1,0 +1,518 @@
+"""Attention / Transformer family: ``Attention``, ``FeedForwardNetwork``, ``Transformer``
+(LanguageModel and Translation), ``SequenceBeamSearch`` and the position/mask helpers.
+
+Reference: ``DL/nn/Attention.scala:30-111`` (dense q/k/v/out projections, split heads with
+q·depth^-0.5, QKᵀ + bias → softmax → dropout → ·V → combine heads, KV cache for inference at
+:114+), ``FeedForwardNetwork.scala``, ``TransformerOperation.scala`` (Xavier dense layers, the
+sinusoid position signal, padding / lower-triangle biases with −1e9), ``Transformer.scala``
+(pre-norm blocks: x + Dropout(Sublayer(LayerNorm(x))), final LayerNorm), ``SequenceBeamSearch.scala``.
+
+Reference quirks kept on purpose (parity): every Dropout in these layers is built as
+``Dropout(1 - rate)``, i.e. the configured rate is the KEEP probability; the beam-search length
+penalty is ``(5 + len/6)^alpha``; token ids produced by the search are 1-based.
+
+MI355X notes: the score/softmax/value product runs as one fused scaled-dot-product attention
+(flash kernel of the ROCm PyTorch build) whenever no attention-dropout mask is needed; the
+projections are bf16 GEMMs on the compute dtype with fp32 master weights.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ...utils.table import Table, T
+from ..abstractnn import AbstractModule, AutogradModule, TensorModule
+from ..initialization_method import Xavier, Zeros, VariableFormats
+
+_MASK = -1e9
+
+
+def _dense_param(mod, name, out_f, in_f, bias):
+    mod.register_parameter(f"{name}Weight", torch.zeros(out_f, in_f), f"{name}GradWeight")
+    Xavier().init(getattr(mod, f"{name}Weight"), VariableFormats.OUT_IN)
+    if bias:
+        mod.register_parameter(f"{name}Bias", torch.zeros(out_f), f"{name}GradBias")
+
+
+def _drop(x, keep_rate, train):
+    """``Dropout(initP = 1 - rate)`` of the reference: drop probability 1 - rate."""
+    p = 1.0 - keep_rate
+    if not train or p <= 0:
+        return x
+    if p >= 1:
+        return torch.zeros_like(x)
+    return F.dropout(x, p, True)
+
+
+def split_heads(x, n_heads):
+    B, L, Hd = x.shape
+    return x.reshape(B, L, n_heads, Hd // n_heads).transpose(1, 2)
+
+
+def combine_heads(x):
+    B, n, L, d = x.shape
+    return x.transpose(1, 2).reshape(B, L, n * d)
+
+
+class Attention(AutogradModule):
+    """Multi-head attention.  Input ``T(x, y, bias)``: queries from ``x`` (B, Lq, H), keys and
+    values from ``y`` (B, Lk, H), additive ``bias`` broadcastable to (B, heads, Lq, Lk).  For
+    cached incremental decoding pass ``T(x, y, T(bias, cache))`` (inference only); the cache
+    Table is updated with ``<name>_k`` / ``<name>_v``."""
+
+    def __init__(self, hidden_size, num_heads, attention_dropout, bigdl_type="float"):
+        super().__init__()
+        if hidden_size % num_heads:
+            raise ValueError("hidden_size must be a multiple of num_heads")
+        self.hiddenSize, self.numHeads, self.attentionDropout = hidden_size, num_heads, attention_dropout
+        for n in ("query", "key", "value", "output"):
+            _dense_param(self, n, hidden_size, hidden_size, False)
+
+    def _proj(self, x, name):
+        w = self.P(f"{name}Weight")
+        return F.linear(x.to(w.dtype), w)
+
+    def _attend(self, q, k, v, bias):
+        depth = self.hiddenSize // self.numHeads
+        q = split_heads(q, self.numHeads) * depth ** -0.5
+        k = split_heads(k, self.numHeads)
+        v = split_heads(v, self.numHeads)
+        bias = bias.to(q.dtype) if bias is not None else None
+        if not self.train or self.attentionDropout >= 1.0:
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=1.0)
+        else:
+            logits = q @ k.transpose(-1, -2)
+            if bias is not None:
+                logits = logits + bias
+            w = torch.softmax(logits.float(), -1).to(q.dtype)
+            o = _drop(w, self.attentionDropout, True) @ v
+        return self._proj(combine_heads(o), "output")
+
+    def _forward(self, input):
+        x, y, b = input[1], input[2], input[3]
+        if isinstance(b, Table):
+            return self._forward_cached(x, y, b[1], b[2])
+        return self._attend(self._proj(x, "query"), self._proj(y, "key"), self._proj(y, "value"), b)
+
+    def _forward_cached(self, x, y, bias, cache):
+        if self.train:
+            raise RuntimeError("Only support input cache for model inference")
+        q = self._proj(x, "query")
+        k = self._proj(y, "key")
+        v = self._proj(y, "value")
+        kn, vn = f"{self.get_name()}_k", f"{self.get_name()}_v"
+        if isinstance(cache, Table) and len(list(cache.keys())) > 0:
+            ck, cv = cache.get(kn), cache.get(vn)
+            if ck is not None and ck.numel() > 0:
+                k = torch.cat([k, ck.to(k.dtype)], 1)
+                v = torch.cat([v, cv.to(v.dtype)], 1)
+            cache[kn] = k
+            cache[vn] = v
+        return self._attend(q, k, v, bias)
+
+
+class FeedForwardNetwork(AutogradModule):
+    """dense(H→F, ReLU) → Dropout(1 - reluDropout) → dense(F→H) (``FeedForwardNetwork.scala``)."""
+
+    def __init__(self, hidden_size, filter_size, relu_dropout, bigdl_type="float"):
+        super().__init__()
+        self.hiddenSize, self.filterSize, self.reluDropout = hidden_size, filter_size, relu_dropout
+        _dense_param(self, "filter", filter_size, hidden_size, True)
+        _dense_param(self, "output", hidden_size, filter_size, True)
+
+    def _forward(self, x):
+        w1, b1 = self.P("filterWeight"), self.P("filterBias")
+        h = F.relu(F.linear(x.to(w1.dtype), w1, b1.to(w1.dtype)))
+        h = _drop(h, self.reluDropout, self.train)
+        w2, b2 = self.P("outputWeight"), self.P("outputBias")
+        return F.linear(h, w2, b2.to(w2.dtype))
+
+
+def position_signal(length, channels, min_timescale=1.0, max_timescale=1.0e4, device=None):
+    """``TransformerOperation.getPositionEncode``: [sin | cos] of position·inv_timescale."""
+    n = channels // 2
+    log_inc = math.log(max_timescale / min_timescale) / max(n - 1, 1)
+    inv = min_timescale * torch.exp(torch.arange(n, dtype=torch.float32, device=device) * -log_inc)
+    t = torch.arange(length, dtype=torch.float32, device=device).unsqueeze(1) * inv.unsqueeze(0)
+    out = torch.zeros(length, channels, device=device)
+    out[:, :n] = torch.sin(t)
+    out[:, n:2 * n] = torch.cos(t)
+    return out
+
+
+def lower_triangle_bias(length, device=None):
+    """(1, 1, L, L) with −1e9 above the diagonal (``attentionBiasLowerTriangle``)."""
+    m = torch.triu(torch.full((length, length), _MASK, device=device), diagonal=1)
+    return m.reshape(1, 1, length, length)
+
+
+class PositionEncode(TensorModule):
+    """Position signal (L, C) of a (B, L, C) input (no gradient to the input)."""
+
+    def updateOutput(self, input):
+        return position_signal(input.shape[1], input.shape[2], device=input.device).to(input.dtype)
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.zeros_like(input)
+
+
+class PositionEncodeWithShift(TensorModule):
+    """Shift the sequence right by one step, then add the position signal."""
+
+    def updateOutput(self, input):
+        out = torch.zeros_like(input)
+        out[:, 1:] = input[:, :-1]
+        return out + position_signal(input.shape[1], input.shape[2], device=input.device).to(input.dtype)
+
+    def updateGradInput(self, input, gradOutput):
+        g = torch.zeros_like(gradOutput)
+        g[:, :-1] = gradOutput[:, 1:]
+        return g
+
+
+class PaddingMask(TensorModule):
+    """(B, L) ids → (B, 1, 1, L) bias with −1e9 at padding (id == 0) positions."""
+
+    def updateOutput(self, input):
+        return ((input == 0).to(torch.float32) * _MASK).unsqueeze(1).unsqueeze(1)
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.zeros_like(input, dtype=torch.float32)
+
+
+class SelfAttentionMask(TensorModule):
+    """(B, L, ...) → (1, 1, L, L) causal bias."""
+
+    def updateOutput(self, input):
+        return lower_triangle_bias(input.shape[1], device=input.device)
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.zeros_like(input)
+
+
+class SplitTensor(TensorModule):
+    """Split dimension ``dim`` (1-based) into ``n`` equal chunks → Table."""
+
+    def __init__(self, dim, n, bigdl_type="float"):
+        super().__init__()
+        self.dim, self.n = dim, n
+
+    def updateOutput(self, input):
+        return T(*torch.chunk(input, self.n, self.dim - 1))
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.cat([gradOutput[i + 1] for i in range(self.n)], self.dim - 1)
+
+
+class Transformer(AbstractModule):
+    """``DL/nn/Transformer.scala``.  ``transformer_type`` "LanguageModel" (input ids (B, L) →
+    (B, L, H) hidden states) or "Translation" (training input T(src, tgt) → (B, Lt, H) or logits
+    with ``with_share_weights_linear``; inference input src ids → T(decoded ids, scores) via
+    ``beam_search``)."""
+
+    def __init__(self, vocab_size, hidden_size, num_heads, filter_size, num_hidden_layers, embedding_dropout,
+                 attention_dropout, ffn_dropout, padding_value=0.0, with_share_weights_linear=False,
+                 transformer_type="LanguageModel", beam_search=None, bigdl_type="float"):
+        super().__init__()
+        from ..containers import Sequential
+        from ..graph import Graph, Input
+        from .embedding import LookupTable
+        from .math_ops import MulConstant
+        from .linear import Linear
+        from .recurrent import TimeDistributed
+        self.vocabSize, self.hiddenSize, self.numHeads = vocab_size, hidden_size, num_heads
+        self.filterSize, self.numHiddenlayers = filter_size, num_hidden_layers
+        self.embeddingDropout, self.attentionDropout, self.ffnDropout = embedding_dropout, attention_dropout, ffn_dropout
+        self.paddingValue = padding_value
+        self.withShareWeightsLinear = with_share_weights_linear
+        self.transformerType = transformer_type
+        self.beamSearch = beam_search
+        self.embedding = LookupTable(vocab_size, hidden_size, padding_value=padding_value, mask_zero=True)
+        self.embedding.set_name("embedding")
+        emb_seq = Sequential().add(self.embedding).add(MulConstant(math.sqrt(hidden_size)))
+        self.linearSharedWeights = TimeDistributed(Linear(hidden_size, vocab_size, with_bias=False))
+        if transformer_type == "LanguageModel":
+            inp = Input()
+            e = emb_seq(inp)
+            dec_in = _Dropout(embedding_dropout)(PositionEncodeWithShift()(e))
+            bias = SelfAttentionMask()(e)
+            out = self._block(dec_in, bias, None, None, "decode")
+            self.model = Graph(inp, out)
+        elif transformer_type == "Translation":
+            self.encoderStack = self._stack(encoder=True)
+            self.decoderStack = self._stack(encoder=False)
+            src, tgt = Input(), Input()
+            from .table_ops import JoinTable, SelectTable, CAddTable
+            mask = PaddingMask()(src)
+            joined = JoinTable(1, -1)(src, tgt)
+            emb = emb_seq(joined)
+            split = SplitTensor(1, 2)(emb)
+            emb_in, emb_out = SelectTable(1)(split), SelectTable(2)(split)
+            enc_out = self._encode(emb_in, mask)
+            dec_in = _Dropout(embedding_dropout)(PositionEncodeWithShift()(emb_out))
+            dec_bias = SelfAttentionMask()(emb_out)
+            out = self.decoderStack(dec_in, dec_bias, enc_out, mask)
+            self.model = Graph([src, tgt], out)
+            self._emb_seq = emb_seq
+            if beam_search is not None:
+                beam_search.setLogitFn(self.symbols)
+        else:
+            raise ValueError(f"Only support LanguageModel and Translation transformer type, got {transformer_type}")
+
+    # -- construction helpers ------------------------------------------------------------
+    def _encode(self, emb, mask):
+        from .table_ops import CAddTable
+        pos = PositionEncode()(emb)
+        x = _Dropout(self.embeddingDropout)(CAddTable()(emb, pos))
+        return self.encoderStack(x, mask)
+
+    def _stack(self, encoder):
+        from ..graph import Graph, Input
+        if encoder:
+            x, b = Input(), Input()
+            return Graph([x, b], self._block(x, b, None, None, "encoder"))
+        x, b, eo, eb = Input(), Input(), Input(), Input()
+        return Graph([x, b, eo, eb], self._block(x, b, eo, eb, "decoder"))
+
+    def _sub(self, layer, x, inputs, name, suffix):
+        from .normalization import LayerNormalization
+        from .table_ops import CAddTable
+        norm = LayerNormalization(self.hiddenSize).set_name(name + "/norm")(x)
+        args = [norm if a is None else a for a in inputs]
+        y = layer.set_name(name + "/" + suffix)(*args)
+        return CAddTable()(x, _Dropout(self.embeddingDropout).set_name(name + "/dropout")(y))
+
+    def _block(self, x, self_bias, enc_out, enc_bias, kind):
+        from .normalization import LayerNormalization
+        for i in range(self.numHiddenlayers):
+            att = Attention(self.hiddenSize, self.numHeads, self.attentionDropout)
+            x = self._sub(att, x, [None, None, self_bias], f"{kind}_self_attention_{i}", "self_attention")
+            if enc_out is not None and enc_bias is not None:
+                att2 = Attention(self.hiddenSize, self.numHeads, self.attentionDropout)
+                x = self._sub(att2, x, [None, enc_out, enc_bias], f"{kind}_encdec_attention_{i}", "encdec_attention")
+            ffn = FeedForwardNetwork(self.hiddenSize, self.filterSize, self.ffnDropout)
+            x = self._sub(ffn, x, [None], f"{kind}_ffn_{i}", "ffn")
+        return LayerNormalization(self.hiddenSize)(x)
+
+    def children(self):
+        ch = [self.model]
+        if self.withShareWeightsLinear:
+            ch.append(self.linearSharedWeights)
+        return ch
+
+    def _param_entries(self):
+        return self.model._param_entries()
+
+    def parameters(self):
+        return self.model.parameters()
+
+    def _set_arena_recursive(self, arena):
+        self._arena = arena
+        self.model._set_arena_recursive(arena)
+
+    def zeroGradParameters(self):
+        self.model.zeroGradParameters()
+
+    def _share(self):
+        lin = self.linearSharedWeights.layer
+        with torch.no_grad():
+            lin.weight.copy_(self.embedding.weight)
+
+    # -- forward / backward --------------------------------------------------------------
+    def updateOutput(self, input):
+        if self.transformerType == "Translation" and isinstance(input, torch.Tensor):
+            if self.train:
+                raise RuntimeError("Input for Transformer should be tensor when doing translation prediction")
+            return self._translate(input)
+        out = self.model.forward(input)
+        if self.withShareWeightsLinear:
+            self._share()
+            out = self.linearSharedWeights.forward(out)
+        return out
+
+    def updateGradInput(self, input, gradOutput):
+        g = gradOutput
+        if self.withShareWeightsLinear:
+            g = self.linearSharedWeights.updateGradInput(self.model.output, gradOutput)
+        return self.model.updateGradInput(input, g)
+
+    def accGradParameters(self, input, gradOutput):
+        g = gradOutput
+        if self.withShareWeightsLinear:
+            g = self.linearSharedWeights.gradInput
+        self.model.accGradParameters(input, g)
+
+    def backward(self, input, gradOutput):
+        g = gradOutput
+        if self.withShareWeightsLinear:
+            g = self.linearSharedWeights.updateGradInput(self.model.output, gradOutput)
+        gi = self.model.backward(input, g)
+        self.gradInput = gi
+        for h in self._grad_ready_hooks:
+            h(self)
+        return gi
+
+    # -- translation inference -----------------------------------------------------------
+    def _translate(self, src):
+        if self.beamSearch is None:
+            raise RuntimeError("Translation inference needs a SequenceBeamSearch")
+        with torch.no_grad():
+            mask = PaddingMask().forward(src)
+            emb = self._emb_seq.forward(src)
+            x = emb + position_signal(emb.shape[1], emb.shape[2], device=emb.device).to(emb.dtype)
+            enc = self.encoderStack.forward(T(x, mask))
+            res = self.beamSearch.forward(T(enc, mask))
+        ids = res[1][:, 0]
+        scores = res[2][:, 0]
+        return T(ids[:, 1:], scores)
+
+    def symbols(self, ids, i, max_decode_length, encoder_outputs, enc_bias, cache_value):
+        """Logits for step ``i`` of incremental decoding (``Transformer.symbols``)."""
+        cache = Table()
+        for m in range(1, self.numHiddenlayers + 1):
+            if cache_value.contains(f"layer_{m}_k"):
+                cache[f"decoder_self_attention_{m - 1}/self_attention_k"] = cache_value[f"layer_{m}_k"]
+                cache[f"decoder_self_attention_{m - 1}/self_attention_v"] = cache_value[f"layer_{m}_v"]
+        sig = position_signal(max_decode_length + 1, self.hiddenSize, device=ids.device)
+        dec_in = self._emb_seq.forward(ids[:, i:i + 1])
+        dec_in = dec_in + sig[i].to(dec_in.dtype)
+        self_bias = lower_triangle_bias(max_decode_length, device=ids.device)[:, :, i:i + 1, :i + 1]
+        out = self.decoderStack.forward(T(dec_in, T(self_bias, cache), encoder_outputs, enc_bias))
+        self._share()
+        logits = self.linearSharedWeights.forward(out)
+        for m in range(1, self.numHiddenlayers + 1):
+            if cache_value.contains(f"layer_{m}_k"):
+                cache_value[f"layer_{m}_k"] = cache[f"decoder_self_attention_{m - 1}/self_attention_k"]
+                cache_value[f"layer_{m}_v"] = cache[f"decoder_self_attention_{m - 1}/self_attention_v"]
+        return logits.squeeze(1), cache_value
+
+
+class _Dropout(TensorModule):
+    """``Dropout(1 - rate)`` as built inside the reference transformer layers."""
+
+    def __init__(self, rate, bigdl_type="float"):
+        super().__init__()
+        self.rate = rate
+        self._mask = None
+
+    def updateOutput(self, input):
+        p = 1.0 - self.rate
+        if not self.train or p <= 0:
+            self._mask = None
+            return input
+        keep = 1.0 - p
+        self._mask = (torch.rand_like(input, dtype=torch.float32) < keep).to(input.dtype) / max(keep, 1e-12)
+        return input * self._mask
+
+    def updateGradInput(self, input, gradOutput):
+        return gradOutput if self._mask is None else gradOutput * self._mask
+
+
+class SequenceBeamSearch(AbstractModule):
+    """Beam search over a logit function (``SequenceBeamSearch.scala``), vectorised on device.
+
+    ``forward(T(encoder_outputs (B, L, H), attention_bias))`` → ``T(seq (B, beam, len+1),
+    scores (B, beam))``.  The logit function is ``fn(ids (B·beam, i+1), i, max_len, enc, bias,
+    cache Table) -> (logits (B·beam, V), cache)``."""
+
+    def __init__(self, vocab_size, beam_size, alpha, max_decode_length, eos_id, padding_value, num_hidden_layers,
+                 hidden_size, bigdl_type="float"):
+        super().__init__()
+        self.vocabSize, self.beamSize, self.alpha = vocab_size, beam_size, alpha
+        self.maxDecodeLength, self.eosID, self.paddingValue = max_decode_length, eos_id, padding_value
+        self.numHiddenLayers, self.hiddenSize = num_hidden_layers, hidden_size
+        self._fn = None
+
+    INF = -1e7
+
+    def setLogitFn(self, fn):
+        self._fn = fn
+        return self
+
+    def _len_norm(self, length):
+        return (5.0 + length / 6.0) ** self.alpha
+
+    @staticmethod
+    def _gather(t, idx):
+        """t (B, K, ...) gathered along dim 1 by idx (B, K')."""
+        shape = idx.shape + t.shape[2:]
+        ix = idx.reshape(idx.shape + (1,) * (t.dim() - 2)).expand(shape)
+        return torch.gather(t, 1, ix)
+
+    def _cache_map(self, cache, fn):
+        out = Table()
+        for k, v in cache.items():
+            out[k] = fn(v) if isinstance(v, torch.Tensor) and v.numel() > 0 else v
+        return out
+
+    def updateOutput(self, input):
+        if self._fn is None:
+            raise RuntimeError("SequenceBeamSearch: call setLogitFn first")
+        enc, bias = input[1], input[2]
+        B, K, V = enc.shape[0], self.beamSize, self.vocabSize
+        dev = enc.device
+        alive_seq = torch.full((B, K, 1), float(self.paddingValue), device=dev)
+        alive_lp = torch.full((B, K), self.INF, device=dev)
+        alive_lp[:, 0] = 0
+        enc_b = enc.unsqueeze(1).expand(B, K, *enc.shape[1:]).contiguous()
+        bias_b = bias.unsqueeze(1).expand(B, K, *bias.shape[1:]).contiguous()
+        cache = Table()
+        for j in range(1, self.numHiddenLayers + 1):
+            cache[f"layer_{j}_k"] = torch.empty(0, device=dev)
+            cache[f"layer_{j}_v"] = torch.empty(0, device=dev)
+        fin_seq = torch.zeros_like(alive_seq)
+        fin_scores = torch.full((B, K), self.INF, device=dev)
+        fin_flags = torch.zeros(B, K, dtype=torch.bool, device=dev)
+        flat = lambda t: t.reshape((B * t.shape[1],) + tuple(t.shape[2:]))  # noqa: E731
+        i = 0
+        while self._continue(i, alive_lp, fin_scores, fin_flags):
+            # grow alive
+            fcache = self._cache_map(cache, flat)
+            logits, ncache = self._fn(flat(alive_seq).long(), i, self.maxDecodeLength, flat(enc_b), flat(bias_b),
+                                      fcache)
+            logits = logits.float().reshape(B, K, V)
+            lp = torch.log_softmax(logits, -1) + alive_lp.unsqueeze(2)
+            top_lp, top_idx = lp.reshape(B, K * V).topk(2 * K, -1)
+            beam_idx = torch.div(top_idx, V, rounding_mode="floor")
+            top_ids = (top_idx % V + 1).float()
+            top_seq = torch.cat([self._gather(alive_seq, beam_idx), top_ids.unsqueeze(2)], 2)
+            ncache = self._cache_map(ncache, lambda v: self._gather(v.reshape((B, K) + tuple(v.shape[1:])), beam_idx))
+            enc2 = self._gather(enc_b, beam_idx)
+            bias2 = self._gather(bias_b, beam_idx)
+            finished_now = top_ids == self.eosID
+            # new alive state
+            nlp = top_lp + finished_now.float() * self.INF
+            _, keep = nlp.topk(K, -1)
+            alive_seq = self._gather(top_seq, keep)
+            alive_lp = self._gather(nlp, keep)
+            enc_b = self._gather(enc2, keep)
+            bias_b = self._gather(bias2, keep)
+            cache = self._cache_map(ncache, lambda v: self._gather(v, keep))
+            # new finished state
+            fin_seq = torch.cat([fin_seq, torch.full((B, K, 1), float(self.paddingValue), device=dev)], 2)
+            scores = top_lp / self._len_norm(i + 1) + (1.0 - finished_now.float()) * self.INF
+            all_seq = torch.cat([fin_seq, top_seq], 1)
+            all_scores = torch.cat([fin_scores, scores], 1)
+            all_flags = torch.cat([fin_flags, finished_now], 1)
+            _, keep = all_scores.topk(K, -1)
+            fin_seq = self._gather(all_seq, keep)
+            fin_scores = self._gather(all_scores, keep)
+            fin_flags = self._gather(all_flags, keep)
+            i += 1
+        any_fin = fin_flags.any(1)
+        seq = torch.where(any_fin.reshape(B, 1, 1), fin_seq, alive_seq)
+        scores = torch.where(any_fin.reshape(B, 1), fin_scores, alive_lp)
+        return T(seq, scores)
+
+    def _continue(self, i, alive_lp, fin_scores, fin_flags):
+        if i >= self.maxDecodeLength:
+            return False
+        best_alive = alive_lp[:, 0] / self._len_norm(self.maxDecodeLength)
+        lowest_fin = (fin_scores * fin_flags.float()).min(1).values
+        lowest_fin = lowest_fin + (1.0 - fin_flags.any(1).float()) * self.INF
+        return not bool(torch.all(lowest_fin > best_alive))
+
+    def updateGradInput(self, input, gradOutput):
+        raise RuntimeError("SequenceBeamSearch is inference only")

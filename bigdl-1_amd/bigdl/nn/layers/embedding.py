@@ -15,9 +15,10 @@ DOUBLEMAX = 1.7976931348623157e308
 
 class LookupTable(TensorModule):
     def __init__(self, n_index, n_output, padding_value=0.0, max_norm=DOUBLEMAX, norm_type=2.0,
-                 should_scale_grad_by_freq=False, wRegularizer=None, bigdl_type="float"):
+                 should_scale_grad_by_freq=False, wRegularizer=None, mask_zero=False, bigdl_type="float"):
         super().__init__()
         self.nIndex, self.nOutput = n_index, n_output
+        self.maskZero = mask_zero
         self.paddingValue = padding_value
         self.maxNorm, self.normType = max_norm, norm_type
         self.shouldScaleGradByFreq = should_scale_grad_by_freq
@@ -42,9 +43,15 @@ class LookupTable(TensorModule):
             self.weight[rows] = w * scale
 
     def updateOutput(self, input):
+        if self.maskZero and self.paddingValue != 0:
+            with torch.no_grad():
+                self.weight[int(self.paddingValue) - 1].zero_()
         self._renorm(input)
         w = self.cw("weight")
-        return ops.embedding_forward(w, input, self.paddingValue)
+        y = ops.embedding_forward(w, input, self.paddingValue)
+        if self.maskZero:
+            y = y * (input != self.paddingValue).unsqueeze(-1).to(y.dtype)
+        return y
 
     def updateGradInput(self, input, gradOutput):
         return torch.zeros_like(input, dtype=torch.float32)
