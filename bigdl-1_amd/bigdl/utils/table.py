@@ -88,6 +88,9 @@ class Table:
     def items(self):
         return list(self._state.items())
 
+    def __contains__(self, key) -> bool:
+        return key in self._state
+
     def __iter__(self) -> Iterator:
         for i in range(1, self.length() + 1):
             yield self._state[i]
