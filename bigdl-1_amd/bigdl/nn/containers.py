@@ -225,11 +225,20 @@ class ConcatTable(Container):
         br, bn, shortcut, relu = self._residual
         g = gradOutput[1] if isinstance(gradOutput, Table) else gradOutput
         gb, gres = bn.backward_residual(self._bn_in, g)
+        # shortcut first, so the branch's first conv can sum its gradient in the dgrad epilogue
+        gs = shortcut.backward(input, gres)
+        from .layers.conv import SpatialConvolution
+        first = br.modules[0]
+        fold = isinstance(first, SpatialConvolution) and isinstance(gs, torch.Tensor) and len(br.modules) > 1
+        if fold:
+            first._grad_residual = gs
         for i in range(len(br.modules) - 2, -1, -1):
             prev = br.modules[i - 1].output if i > 0 else input
             gb = br.modules[i].backward(prev, gb)
         br.gradInput = gb
-        gs = shortcut.backward(input, gres)
+        if fold:
+            first._grad_residual = None
+            return gb
         return _add_act(gb, gs)
 
     def updateGradInput(self, input, gradOutput):

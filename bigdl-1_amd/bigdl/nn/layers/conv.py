@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from ... import ops
 from ...utils.engine import Engine
+from ...utils import config
 from ..abstractnn import TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, VariableFormats
 
@@ -130,12 +131,35 @@ class SpatialConvolution(TensorModule):
     #: accumulates its gradient, so the conv skips both
     _bias_folded_into = None
 
+    #: gradient added to this conv's gradInput in the dgrad epilogue (set by a fused residual
+    #: ConcatTable for the first conv of a block: the branch/shortcut gradient sum)
+    _grad_residual = None
+
+    def _stats_consumer(self, x):
+        """The training BN that will consume this conv's output (fusion), if the epilogue can
+        produce its statistics."""
+        bn = self._bias_folded_into
+        if bn is None or not bn.train or getattr(bn, "_sync", False) or not x.is_cuda:
+            return None
+        if self.format != "NCHW" or not config.get_property("bigdl.fusion.convstats"):
+            return None
+        return bn
+
     def updateOutput(self, input):
         x, pad, batched, _ = self._prep(input)
         w4 = self._w4(self.cw("weight"))
         b = self.cw("bias") if (self.withBias and self._bias_folded_into is None) else None
-        y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
-                               self.nGroup)
+        bn = self._stats_consumer(x) if batched else None
+        y = NotImplemented
+        if bn is not None and ops.native_has("conv2d_forward"):
+            r = ops.native_ops.conv2d_forward_stats(x, w4, b, (self.strideH, self.strideW), pad,
+                                                (self.dilationH, self.dilationW), self.nGroup)
+            if r is not NotImplemented:
+                y, part, G = r
+                bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G)
+        if y is NotImplemented:
+            y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
+                                   self.nGroup)
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)
@@ -151,8 +175,13 @@ class SpatialConvolution(TensorModule):
         same_scale = self.scale_b == self.scale_w
         own_bias = self.withBias and self._bias_folded_into is None
         gb = self.gradBias if (acc and own_bias and same_scale) else None
+        res = self._grad_residual if need_input else None
+        self._grad_residual = None
+        pt, pb, pl, pr = pads
+        fuse_res = res is not None and pt == pb and pl == pr and self.format == "NCHW" and batched
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
-                                 self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0)
+                                 self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0,
+                                 residual=to_device_layout(res) if fuse_res else None)
         if acc and own_bias and not same_scale and self.scale_b != 0:
             self.gradBias.add_(gy.float().sum((0, 2, 3)), alpha=self.scale_b)
         if need_input and gi is not None:
@@ -163,11 +192,16 @@ class SpatialConvolution(TensorModule):
                 gi = gi.permute(0, 2, 3, 1)
             if not batched:
                 gi = gi.squeeze(0)
+            if res is not None and not fuse_res:
+                gi = gi + res
         return gi
 
     def updateGradInput(self, input, gradOutput):
         if not self.propagateBack:
             self._gi_done = False
+            res, self._grad_residual = self._grad_residual, None
+            if res is not None:
+                return res.clone()
             return torch.zeros_like(input) if isinstance(input, torch.Tensor) else None
         # compute gradInput and (fused) parameter gradients in one pass; accGradParameters then
         # only applies regularisers

@@ -99,6 +99,8 @@ class BatchNormalization(TensorModule):
     # --- fusion hooks (set by bigdl.nn.fusion) ---------------------------------------------
     #: conv whose bias was folded into this BN (its output excludes the bias)
     _bias_producer = None
+    #: (data_ptr, shape, partials, G) left by the producing conv's epilogue for the next forward
+    _pending_stats = None
 
     def _in_bias(self):
         p = self._bias_producer
@@ -134,9 +136,17 @@ class BatchNormalization(TensorModule):
             if self._sync and _dist_ready():
                 y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib)
             else:
-                y, mean, invstd = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
-                                                              self.momentum, self.eps, relu=relu, residual=residual,
-                                                              in_bias=ib)
+                r = NotImplemented
+                ps, self._pending_stats = self._pending_stats, None
+                if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
+                    r = ops.native_ops.batchnorm_forward_train_partials(
+                        x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
+                        relu=relu, residual=residual, in_bias=ib)
+                if r is NotImplemented:
+                    r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
+                                                    self.momentum, self.eps, relu=relu, residual=residual,
+                                                    in_bias=ib)
+                y, mean, invstd = r
             self.saveMean, self.saveStd = mean, invstd
         else:
             y = ops.batchnorm_forward_infer(x, g, b, self.runningMean, self.runningVar, self.eps, relu=False,

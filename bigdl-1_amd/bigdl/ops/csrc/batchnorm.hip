@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
-  float K = bf2f(x[c]);
+  float K = x ? bf2f(x[c]) : 0.f;  // x == null: partials are unshifted (conv-epilogue stats)
   float dm = s / (float)M;
   float var = fmaxf(q / (float)M - dm * dm, 0.f);
   float mean = K + dm;
@@ -235,6 +235,27 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, ws, G, M, C, gamma,
                      beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
+  int grid = apply_grid(M, C);
+  const bf16_t* xr = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  bf16_t* yr = (bf16_t*)y;
+  if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Training forward from precomputed partials (the producing conv's epilogue wrote Σy, Σy² per row
+// tile, unshifted): finalize + apply only — the stats pass over x is gone.
+BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, void* y, long long M, int C,
+                                             const float* gamma, const float* beta, const float* in_bias,
+                                             float* run_mean, float* run_var, float momentum, float eps,
+                                             float* save_mean, float* save_invstd, const float* partial, int G,
+                                             float* coef, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, partial, G, M, C,
+                     gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;

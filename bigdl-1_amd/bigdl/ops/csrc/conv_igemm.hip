@@ -32,6 +32,9 @@ struct ConvParams {
   int Kg;              // R*S*C
   int relu;
   int tiles_n;
+  const bf16_t* res;   // optional [M][K] tensor added before the ReLU (residual / gradient sum)
+  float* stats;        // optional BN partials: stats[tm][K] = Σ y, stats[G + tm][K] = Σ y² (G = #row tiles)
+  int tiles_m;
 };
 
 constexpr int BM = 128;
@@ -156,11 +159,18 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
     __syncthreads();
   }
 
-  // epilogue: bias, relu, bf16, 8-byte stores of 4 consecutive channels
+  // Epilogue, staged through LDS so every global access is a full 16-B chunk of a pixel row:
+  //  1. each lane parks its 4-channel fragments (+bias) as bf16 in a [BM][BN+8] tile (the +8 pad
+  //     spreads the 16 pixel rows a ds_write_b64 covers over distinct banks);
+  //  2. the block walks the tile row-major, 8 channels per thread: optional residual add (same
+  //     16-B chunk of `res`), ReLU, one global_store_dwordx4, and optional per-channel Σy / Σy²
+  //     partials for a following BatchNormalization (the conv then replaces the BN stats pass).
+  constexpr int LDR = BN + 8;
+  bf16_t* et = &lds[0][0];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
-    const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
-    if (n >= p.K) continue;
+    const int nl = wave_n * (BN / 2) + i * 16 + fq * 4;
+    const int n = n0 + nl;
     float b4[4] = {0.f, 0.f, 0.f, 0.f};
     if (p.bias) {
 #pragma unroll
@@ -168,48 +178,127 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
     }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wave_m * 64 + j * 16 + fr;
-      if (m >= p.M) continue;
-      float v[4];
+      const int ml = wave_m * 64 + j * 16 + fr;
+      uint32_t lo = (uint32_t)f2bf(acc[i][j][0] + b4[0]) | ((uint32_t)f2bf(acc[i][j][1] + b4[1]) << 16);
+      uint32_t hi = (uint32_t)f2bf(acc[i][j][2] + b4[2]) | ((uint32_t)f2bf(acc[i][j][3] + b4[3]) << 16);
+      *reinterpret_cast<uint2*>(&et[ml * LDR + nl]) = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;      // 16-B chunks per tile row
+  constexpr int RPP = 256 / CPR;   // rows per pass
+  const int cc = tid % CPR, rr = tid / CPR;
+  const int n = n0 + cc * 8;
+  float s8[8], q8[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] + b4[e];
-        if (p.relu) v[e] = fmaxf(v[e], 0.f);
+  for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
+  const bool full = n + 8 <= p.K;
+#pragma unroll 2
+  for (int r = rr; r < BM; r += RPP) {
+    const int m = m0 + r;
+    if (m >= p.M || n >= p.K) continue;
+    float v[8];
+    load8(&et[r * LDR + cc * 8], v);
+    const size_t off = (size_t)m * p.K + n;
+    if (full) {
+      if (p.res) {
+        float rv[8];
+        load8(p.res + off, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rv[e];
       }
-      bf16_t* dst = p.y + (size_t)m * p.K + n;
-      if (n + 4 <= p.K) {
-        uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
-      } else {
-        for (int e = 0; e < 4 && n + e < p.K; ++e) dst[e] = f2bf(v[e]);
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      store8(p.y + off, v);
+      if (p.stats) {
+        // statistics of the values as stored (bf16-rounded), which is what the BN reads
+        uint4 u = *reinterpret_cast<const uint4*>(p.y + off);
+        float w[8];
+        const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[2 * e] = __uint_as_float(uw[e] << 16);
+          w[2 * e + 1] = __uint_as_float(uw[e] & 0xFFFF0000u);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s8[e] += w[e]; q8[e] = fmaf(w[e], w[e], q8[e]); }
+      }
+    } else {
+      for (int e = 0; e < 8 && n + e < p.K; ++e) {
+        float t = v[e] + (p.res ? bf2f(p.res[off + e]) : 0.f);
+        if (p.relu) t = fmaxf(t, 0.f);
+        const bf16_t o = f2bf(t);
+        p.y[off + e] = o;
+        const float w = bf2f(o);
+        s8[e] += w;
+        q8[e] = fmaf(w, w, q8[e]);
+      }
+    }
+  }
+  if (p.stats) {
+    // reduce the RPP row groups of each channel chunk through LDS (after the tile reads retire)
+    float* red = reinterpret_cast<float*>(&et[BM * LDR]);  // [RPP][BN] Σ, then [RPP][BN] Σ²
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[rr * BN + cc * 8 + e] = s8[e];
+      red[RPP * BN + rr * BN + cc * 8 + e] = q8[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f, b = 0.f;
+#pragma unroll 4
+      for (int g = 0; g < RPP; ++g) {
+        a += red[g * BN + c];
+        b += red[RPP * BN + g * BN + c];
+      }
+      if (n0 + c < p.K) {
+        p.stats[(size_t)tm * p.K + n0 + c] = a;
+        p.stats[((size_t)p.tiles_m + tm) * p.K + n0 + c] = b;
       }
     }
   }
 }
 
-// Host launcher.  Requirements (checked): C % 8 == 0, K % 4 == 0, 16-B aligned x/w, 8-B aligned y.
-BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W, int C,
-                                int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
-                                int relu, hipStream_t s) {
+// Host launchers.  Requirements (checked): C % 8 == 0, K % 4 == 0, 16-B aligned x/w/y/res.
+// ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
+BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + BM - 1) / BM); }
+
+BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                   float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
+  if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   ConvParams p;
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)w;
   p.bias = bias;
   p.y = (bf16_t*)y;
+  p.res = (const bf16_t*)res;
+  p.stats = stats;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
-  p.M = Nb * P * Q;
+  long long Ml = (long long)Nb * P * Q;
+  if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  p.M = (int)Ml;
   p.Kg = R * S * C;
   p.relu = relu;
   const int BN = K <= 64 ? 64 : 128;
   p.tiles_n = (K + BN - 1) / BN;
-  long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  long long tiles = (long long)p.tiles_m * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   if (BN == 64)
     hipLaunchKernelGGL(k_conv_fwd<64>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL(k_conv_fwd<128>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W, int C,
+                                int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                                int relu, hipStream_t s) {
+  return bigdl_conv_fwd_ex(x, w, bias, nullptr, y, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu,
+                           s);
 }

@@ -23,6 +23,11 @@ def native_status() -> dict:
     return N.status()
 
 
+def native_has(opname: str) -> bool:
+    """True when device tensors of ``opname`` go to the HIP kernel (library loaded and enabled)."""
+    return N.has(opname)
+
+
 def _nat(t: torch.Tensor, opname: str) -> bool:
     """True → use the native kernel for this op on this tensor."""
     if not (isinstance(t, torch.Tensor) and t.is_cuda):

@@ -69,6 +69,8 @@ def lib():
 
 
 def has(opname: str) -> bool:
+    if not config.get_property("bigdl.native.enable"):
+        return False
     l = _load()
     if l is None:
         if torch.cuda.is_available() and config.get_property("bigdl.native.require"):

@@ -131,6 +131,33 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     return y, mean, invstd
 
 
+def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
+                                    relu=False, residual=None, in_bias=None):
+    """Training BN whose statistics were produced by the preceding conv's epilogue
+    (:func:`conv2d_forward_stats`): finalize + apply only."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
+        return NotImplemented
+    if partial is None or partial.numel() != 2 * G * C_ or partial.dtype != _f32:
+        return NotImplemented
+    if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
+                                 residual.dtype != _bf16 or not _al16(residual)):
+        return NotImplemented
+    coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
+    mean = torch.empty(C_, dtype=_f32, device=x.device)
+    invstd = torch.empty(C_, dtype=_f32, device=x.device)
+    y = torch.empty_like(x)
+    check(_lib().bigdl_bn_fwd_train_partials(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
+                                             ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
+                                             _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
+                                             C.c_int(G), ptr(coef), C.c_int(1 if relu else 0), _s()),
+          "bn_fwd_train_partials")
+    return y, mean, invstd
+
+
 @register("batchnorm_forward_infer")
 def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False, in_bias=None):
     rc = _rows_c(x)
@@ -250,13 +277,14 @@ def _conv_geom_ok(x, w4, groups, dilation):
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
 
 
-@register("conv2d_forward")
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False):
     if not _conv_geom_ok(x, w4, groups, dilation):
         return NotImplemented
     N_, C_, H, W = x.shape
     K, Ci, R, S = w4.shape
     if Ci != C_ or K % 4:
+        return NotImplemented
+    if (res is not None or stats) and K % 8:
         return NotImplemented
     wk = _krsc(w4)
     if C_ % 8:
@@ -269,15 +297,37 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
     Q = (W + 2 * pad[1] - dilation[1] * (S - 1) - 1) // stride[1] + 1
     if P <= 0 or Q <= 0 or not _al16(wk):
         return NotImplemented
+    if res is not None and not (res.shape == (N_, K, P, Q) and res.dtype == _bf16 and
+                                res.is_contiguous(memory_format=torch.channels_last) and _al16(res)):
+        return NotImplemented
     y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
     bias = b.float().contiguous() if b is not None else None
-    check(_lib().bigdl_conv_fwd(ptr(x), ptr(wk), ptr(bias), ptr(y), N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1],
-                                pad[0], pad[1], dilation[0], dilation[1], 0, _s()), "conv_fwd")
+    part, G = None, 0
+    if stats:
+        G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
+        part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
+    check(_lib().bigdl_conv_fwd_ex(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
+                                   P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0, _s()),
+          "conv_fwd")
+    if stats:
+        return y, part, G
     return y
 
 
-def _dgrad_s1(gy, w4, x_shape, pad, dilation):
-    """stride-1 backward-data as a forward conv of gy with the flipped, transposed kernel."""
+@register("conv2d_forward")
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups)
+
+
+def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+    """Forward conv whose epilogue also emits per-row-tile Σy/Σy² partials for a following BN.
+    Returns ``(y, partials, G)`` or NotImplemented."""
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True)
+
+
+def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None):
+    """stride-1 backward-data as a forward conv of gy with the flipped, transposed kernel; an optional
+    ``residual`` gradient (same shape as x) is summed in the epilogue."""
     N_, C_, H, W = x_shape
     K, Ci, R, S = w4.shape
     if C_ % 4 or K % 8:
@@ -289,9 +339,13 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation):
     pw = dilation[1] * (S - 1) - pad[1]
     if ph < 0 or pw < 0:
         return None
+    if residual is not None and not (C_ % 8 == 0 and residual.shape == (N_, C_, H, W) and residual.dtype == _bf16
+                                     and residual.is_contiguous(memory_format=torch.channels_last)
+                                     and _al16(residual)):
+        return None
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
-    check(_lib().bigdl_conv_fwd(ptr(gy), ptr(wt), ptr(None), ptr(gx), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw,
-                                dilation[0], dilation[1], 0, _s()), "conv_dgrad")
+    check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
+                                   S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, _s()), "conv_dgrad")
     return gx
 
 
@@ -314,7 +368,7 @@ def _dgrad_1x1_strided(gy, w4, x_shape, stride):
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                    scale=1.0):
+                    scale=1.0, residual=None):
     if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
         return NotImplemented
     if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):
@@ -326,12 +380,18 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     from . import reference as R_
     gi = None
     if need_input:
+        res_done = False
         if stride == (1, 1) or tuple(stride) == (1, 1):
-            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)
+            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation, residual)
+            res_done = gi is not None
+            if gi is None and residual is not None:
+                gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)
         elif R == 1 and S == 1 and tuple(pad) == (0, 0):
             gi = _dgrad_1x1_strided(gy, w4, x.shape, stride)
         if gi is None:  # strided k>1 backward-data: library path until the sub-pixel kernel lands
             gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
+        if residual is not None and not res_done:
+            gi = gi + residual
     if gw_acc is not None and scale != 0:
         xx, cc = x, C_
         if C_ % 8:

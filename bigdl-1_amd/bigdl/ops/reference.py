@@ -46,11 +46,11 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
 
 
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
-                    gb_acc=None, scale=1.0):
+                    gb_acc=None, scale=1.0, residual=None):
     """``SpatialConvolution.updateGradInput`` + ``accGradParameters`` (``:364-505``).
 
     Returns gradInput (or None); ACCUMULATES ``scale·dW`` into ``gw_acc`` (O, I/g, kH, kW view,
-    fp32) and ``scale·db`` into ``gb_acc``."""
+    fp32) and ``scale·db`` into ``gb_acc``.  ``residual`` (optional, x-shaped) is added to gradInput."""
     gy = gy.to(x.dtype)
     need_w = gw_acc is not None and scale != 0
     need_b = gb_acc is not None and scale != 0
@@ -61,6 +61,8 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         gw_acc.add_(gw.float(), alpha=scale)
     if need_b:
         gb_acc.add_(gb.float(), alpha=scale)
+    if residual is not None and gi is not None:
+        gi = gi + residual.to(gi.dtype)
     return gi
 
 

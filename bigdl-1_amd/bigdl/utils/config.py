@@ -36,6 +36,7 @@ _REGISTRY = {
     "bigdl.comm.overlap": (bool, True, "overlap gradient reduce-scatter with backward"),
     "bigdl.comm.sharded": (bool, True, "reduce-scatter + sharded update + all-gather (ZeRO-1)"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
+    "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
     # fusion flags (bigdl.mkldnn.fusion.* equivalents, nn/mkldnn/Fusion.scala:34)
     "bigdl.fusion": (bool, True, "enable layer fusion"),
@@ -43,6 +44,7 @@ _REGISTRY = {
     "bigdl.fusion.bnrelu": (bool, True, "fuse BN + ReLU"),
     "bigdl.fusion.convrelu": (bool, True, "fuse conv + ReLU"),
     "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
+    "bigdl.fusion.convstats": (bool, True, "conv epilogue emits the following training BN's statistics"),
     # logging
     "bigdl.utils.LoggerFilter.disable": (bool, False, "disable log redirect"),
     "bigdl.utils.LoggerFilter.logFile": (str, "bigdl.log", "log file"),

@@ -278,3 +278,56 @@ def test_recurrent_lstm_gpu_vs_cpu():
     torch.testing.assert_close(gig.float().cpu(), gi, rtol=5e-2, atol=5e-2)
     for a, b in zip(gpu.parameters()[1], cpu.parameters()[1]):
         torch.testing.assert_close(a.float().cpu(), b, rtol=5e-2, atol=5e-2 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[4] % 8 == 0])
+def test_conv_forward_residual_and_stats(case):
+    """Epilogue extras: residual add (used by the dgrad gradient-sum fold) and per-row-tile Σy/Σy²
+    partials that replace the following BN's statistics pass."""
+    N = _native()
+    from bigdl.ops import native_ops as NO
+    n, c, h, w, k, r, s, st, pd = case
+    x = _cl(torch.randn(n, c, h, w, device=dev).bfloat16())
+    w4 = _cl(torch.randn(k, c, r, s, device=dev).bfloat16() * 0.1)
+    y, part, G = NO.conv2d_forward_stats(x, w4, None, (st, st), (pd, pd))
+    ref = _conv_ref(x, w4, (st, st), (pd, pd))
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    yf = y.float()
+    s1 = part.view(2, G, k).sum(1)
+    torch.testing.assert_close(s1[0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(s1[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    res = _cl(torch.randn_like(ref).bfloat16())
+    y2 = NO._conv_fwd_impl(x, w4, None, (st, st), (pd, pd), res=res)
+    torch.testing.assert_close(y2.float(), ref + res.float(), rtol=2e-2, atol=3e-2)
+
+
+def test_bn_forward_from_conv_partials():
+    N = _native()
+    from bigdl.ops import native_ops as NO, reference as R
+    x = _cl(torch.randn(4, 64, 14, 14, device=dev).bfloat16())
+    w4 = _cl(torch.randn(128, 64, 3, 3, device=dev).bfloat16() * 0.05)
+    y, part, G = NO.conv2d_forward_stats(x, w4, None, (1, 1), (1, 1))
+    g = torch.rand(128, device=dev) + 0.5
+    b = torch.randn(128, device=dev)
+    rm1, rv1 = torch.zeros(128, device=dev), torch.ones(128, device=dev)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    ib = torch.randn(128, device=dev)
+    out, mean, invstd = NO.batchnorm_forward_train_partials(y, part, G, g, b, rm1, rv1, 0.1, 1e-3, relu=True,
+                                                            in_bias=ib)
+    ro, rmean, rinv = R.batchnorm_forward_train(y, g, b, rm2, rv2, 0.1, 1e-3, relu=True, in_bias=ib)
+    torch.testing.assert_close(mean, rmean, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(invstd, rinv, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rm1, rm2, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(out.float(), ro.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_dgrad_residual_fold():
+    N = _native()
+    x = _cl(torch.randn(2, 64, 14, 14, device=dev).bfloat16())
+    w4 = _cl(torch.randn(128, 64, 3, 3, device=dev).bfloat16() * 0.1)
+    gy = _cl(torch.randn(2, 128, 14, 14, device=dev).bfloat16())
+    res = _cl(torch.randn(2, 64, 14, 14, device=dev).bfloat16())
+    gi0 = N.conv2d_backward(gy, x, w4, (1, 1), (1, 1), (1, 1), 1, True, None, None, 0.0)
+    gi1 = N.conv2d_backward(gy, x, w4, (1, 1), (1, 1), (1, 1), 1, True, None, None, 0.0, residual=res)
+    torch.testing.assert_close(gi1.float(), gi0.float() + res.float(), rtol=2e-2, atol=3e-2)
