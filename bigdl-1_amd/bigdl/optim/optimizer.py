@@ -348,10 +348,15 @@ class BaseOptimizer:
             bs = batch.size()
             loss_t = self.train_step(batch)
             # bookkeeping (no device sync: the loss is read one iteration late)
-            prev = self._pending_loss
-            self._pending_loss = _LazyScalar(loss_t)
-            if prev is not None:
-                self.state["Loss"] = prev.value() if (prev.ready() or self._needs_loss()) else self.state["Loss"]
+            if not (isinstance(loss_t, torch.Tensor) and loss_t.is_cuda) or self._needs_loss():
+                # host tensor, or a consumer (summary / MinLoss trigger) needs this iteration's value
+                self._pending_loss = None
+                self.state["Loss"] = float(loss_t)
+            else:
+                prev = self._pending_loss
+                self._pending_loss = _LazyScalar(loss_t)
+                if prev is not None:
+                    self.state["Loss"] = prev.value() if prev.ready() else self.state["Loss"]
             it = self.state["neval"]
             global_bs = bs * Engine.world_size()
             self.state["recordsProcessedThisEpoch"] += global_bs

@@ -67,10 +67,10 @@ _EVENT = Msg("Event", [
     F("file_version", 3, "string", oneof="what"), F("graph_def", 4, "bytes", oneof="what"),
     F("summary", 5, "msg", type_name=".tensorflow.Summary", oneof="what")])
 
-_classes = build("bigdl_tf_event.proto", _PKG, [_HISTO, _SUMMARY, _EVENT], syntax="proto3")
-Event = _classes["Event"]
-Summary = _classes["Summary"]
-HistogramProto = _classes["HistogramProto"]
+_pool, _classes, _ = build("bigdl_tf_event.proto", _PKG, [_HISTO, _SUMMARY, _EVENT], syntax="proto3")
+Event = _classes["tensorflow.Event"]
+Summary = _classes["tensorflow.Summary"]
+HistogramProto = _classes["tensorflow.HistogramProto"]
 
 
 # ---------------------------------------------------------------------------------------- records
@@ -125,6 +125,7 @@ class EventWriter(threading.Thread):
         self._q: "queue.Queue" = queue.Queue()
         self._flush_secs = flush_secs
         self._closed = False
+        self._lock = threading.Lock()
         ev = Event(wall_time=time.time(), file_version="brain.Event:2")
         self._w.write(ev.SerializeToString())
         self._w.flush()
@@ -140,9 +141,12 @@ class EventWriter(threading.Thread):
             except queue.Empty:
                 ev = None
             if ev is _STOP:
+                self._q.task_done()
                 break
             if ev is not None:
-                self._w.write(ev.SerializeToString())
+                with self._lock:
+                    self._w.write(ev.SerializeToString())
+                self._q.task_done()
             if time.time() - last >= self._flush_secs:
                 self._w.flush()
                 last = time.time()
@@ -178,10 +182,10 @@ class FileWriter:
         return self
 
     def flush(self):
-        # synchronous: wait until the queue has drained
-        while not self._ew._q.empty():
-            time.sleep(0.005)
-        self._ew._w.flush()
+        # synchronous: wait until every queued event has been written
+        self._ew._q.join()
+        with self._ew._lock:
+            self._ew._w.flush()
 
     def close(self):
         self._ew.close()

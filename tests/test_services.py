@@ -1,0 +1,108 @@
+"""Observability + inference drivers: TrainSummary/ValidationSummary event files, LocalPredictor,
+Evaluator/Validator, PredictionService (bytes protocol of PredictionService.scala:184-281)."""
+import numpy as np
+import torch
+
+from bigdl.dataset import Sample
+from bigdl.nn import Sequential, Linear, LogSoftMax, ReLU, ClassNLLCriterion
+from bigdl.optim import SGD
+from bigdl.optim.evaluator import Evaluator, Validator
+from bigdl.optim.optimizer import LocalOptimizer
+from bigdl.optim.predictor import LocalPredictor, PredictionService, serialize_activity, deserialize_activity
+from bigdl.optim.trigger import MaxIteration, SeveralIteration, EveryEpoch
+from bigdl.optim.validation import Top1Accuracy, Loss
+from bigdl.utils.table import Table
+from bigdl.visualization import TrainSummary, ValidationSummary, crc32c, read_records
+
+
+def _data(n=64):
+    rng = np.random.RandomState(0)
+    xs = rng.randn(n, 4).astype(np.float32)
+    ys = (xs[:, 0] > 0).astype(np.float32) + 1
+    return [Sample(x, np.array([y], np.float32)) for x, y in zip(xs, ys)]
+
+
+def _model():
+    return Sequential().add(Linear(4, 8)).add(ReLU()).add(Linear(8, 2)).add(LogSoftMax())
+
+
+def test_crc32c_known_vector():
+    assert crc32c(b"123456789") == 0xE3069283
+
+
+def test_train_and_validation_summary(tmp_path):
+    data = _data()
+    opt = LocalOptimizer(_model(), data, ClassNLLCriterion(), SGD(learningrate=0.1), end_trigger=MaxIteration(6),
+                         batch_size=16)
+    ts = TrainSummary(str(tmp_path), "app")
+    ts.set_summary_trigger("Parameters", SeveralIteration(3))
+    vs = ValidationSummary(str(tmp_path), "app")
+    opt.setTrainSummary(ts)
+    opt.setValidationSummary(vs)
+    opt.setValidation(SeveralIteration(2), data, [Top1Accuracy()], 16)
+    opt.optimize()
+    loss = ts.read_scalar("Loss")
+    assert [s for s, _, _ in loss] == list(range(1, 7))
+    assert all(np.isfinite(v) for _, v, _ in loss)
+    assert len(ts.read_scalar("Throughput")) == 6
+    assert len(ts.read_scalar("LearningRate")) == 6
+    acc = vs.read_scalar("Top1Accuracy")
+    assert len(acc) == 3 and all(0 <= v <= 1 for _, v, _ in acc)
+    ts.close()
+    vs.close()
+    files = [p for p in (tmp_path / "app" / "train").iterdir()]
+    assert files and sum(1 for _ in read_records(str(files[0]))) > 6  # crc-checked read
+
+
+def test_local_predictor_and_evaluator():
+    m = _model()
+    data = _data(20)
+    out = LocalPredictor(m, batch_size=8).predict(data)
+    assert len(out) == 20 and out[0].shape == (2,)
+    cls = m.predict_class(data)
+    assert cls.shape == (20,) and set(cls.tolist()) <= {1, 2}
+    ref = m.forward(torch.stack([s.feature() for s in data])).argmax(1) + 1
+    assert cls.tolist() == ref.tolist()
+    res = Evaluator(m).test(data, [Top1Accuracy(), Loss()], 8)
+    assert res[0][0].result()[1] == 20
+    res2 = Validator(m, data).test([Top1Accuracy()])
+    assert res2[0][0].result()[0] == res[0][0].result()[0]
+    r3 = m.evaluate(data, [Top1Accuracy()], 5)
+    assert r3[0][0].result()[0] == res[0][0].result()[0]
+
+
+def test_prediction_service_bytes_and_errors():
+    m = _model()
+    ps = PredictionService(m, 3)
+    x = torch.randn(5, 4)
+    y = deserialize_activity(ps.predict(serialize_activity(x)))
+    torch.testing.assert_close(y, m.forward(x))
+    assert isinstance(ps.predict(torch.randn(2, 4)), torch.Tensor)
+    err = deserialize_activity(ps.predict(serialize_activity(torch.randn(2, 7))))
+    assert isinstance(err, str) and "running forward" in err
+    bad = deserialize_activity(ps.predict(b"\xff\xff\xff"))
+    assert isinstance(bad, str) and "DeSerialize" in bad
+    t = Table()
+    t[1] = torch.arange(6.0).reshape(2, 3)
+    t[2] = torch.tensor([1, 2, 3])
+    t2 = deserialize_activity(serialize_activity(t))
+    torch.testing.assert_close(t2[1], t[1])
+    assert t2[2].tolist() == [1, 2, 3]
+
+
+def test_prediction_service_concurrent():
+    import threading
+    m = _model()
+    ps = PredictionService(m, 2)
+    xs = [torch.randn(3, 4) for _ in range(8)]
+    outs = [None] * 8
+
+    def work(i):
+        outs[i] = ps.predict(xs[i])
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for x, o in zip(xs, outs):
+        torch.testing.assert_close(o, m.forward(x))
