@@ -1,0 +1,150 @@
+"""int8 inference layers (``DL/nn/quantized/{Linear,SpatialConvolution,SpatialDilatedConvolution}.scala``).
+
+Weights are quantised once, per output channel (``Quantization.quantize`` on the 2-D
+``(out, in·kh·kw)`` view).  At run time every GEMM row of the input — an FC input row, or a conv
+im2col window, BigQuant's "per-window" quantisation — gets its own scale; the product runs on the
+int8 MFMA GEMM (``ops.gemm_i8``) with the dequantisation (row scale × channel scale + bias) fused
+into its epilogue.  Backward is not supported (inference only), as in the reference.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ..abstractnn import TensorModule
+
+
+def _kp(k: int) -> int:
+    return (k + 63) // 64 * 64
+
+
+class _QuantizedBase(TensorModule):
+    SCALA_PACKAGE = "com.intel.analytics.bigdl.nn.quantized"
+
+    def _quantize_weight(self, w2d: torch.Tensor):
+        q, s = ops.reference.quant_rows(w2d.detach().float().cpu())
+        self.register_buffer("qweight", q)
+        self.register_buffer("weight_scale", s.float())
+
+    def _gemm(self, rows: torch.Tensor, out_dtype):
+        qa, sa = ops.quant_rows(rows.contiguous(), self.qweight.shape[1])
+        return ops.gemm_i8(qa, sa, self.qweight, self.weight_scale, self.bias_f, out_dtype=out_dtype)
+
+    def updateGradInput(self, input, gradOutput):
+        raise NotImplementedError(f"Doesn't updateGradInput for quantized model ({type(self).__name__})")
+
+    def accGradParameters(self, input, gradOutput):
+        pass
+
+    def parameters(self):
+        return None
+
+    @property
+    def bias_f(self):
+        return getattr(self, "qbias", None)
+
+
+class Linear(_QuantizedBase):
+    def __init__(self, input_size: int, output_size: int, with_bias: bool = True):
+        super().__init__()
+        self.inputSize, self.outputSize, self.withBias = input_size, output_size, with_bias
+        self.register_buffer("qweight", torch.zeros(output_size, _kp(input_size), dtype=torch.int8))
+        self.register_buffer("weight_scale", torch.zeros(output_size))
+        if with_bias:
+            self.register_buffer("qbias", torch.zeros(output_size))
+
+    @staticmethod
+    def from_float(m) -> "Linear":
+        q = Linear(m.inputSize, m.outputSize, m.bias is not None)
+        q._quantize_weight(m.weight)
+        if m.bias is not None:
+            q.qbias = m.bias.detach().float().clone().cpu()
+        q.set_name(m.get_name())
+        return q.to(m.weight.device)
+
+    def updateOutput(self, input):
+        x = input if input.dim() == 2 else input.reshape(1, -1)
+        out_dt = x.dtype if x.is_floating_point() and x.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        y = self._gemm(x, out_dt)
+        return y if input.dim() == 2 else y.reshape(-1)
+
+    def __repr__(self):
+        return f"quantized.Linear[{self.get_name()}]({self.inputSize} -> {self.outputSize})"
+
+
+class SpatialConvolution(_QuantizedBase):
+    def __init__(self, n_input_plane, n_output_plane, kernel_w, kernel_h, stride_w=1, stride_h=1, pad_w=0, pad_h=0,
+                 n_group=1, dilation_w=1, dilation_h=1, with_bias=True):
+        super().__init__()
+        self.nInputPlane, self.nOutputPlane = n_input_plane, n_output_plane
+        self.kernelW, self.kernelH, self.strideW, self.strideH = kernel_w, kernel_h, stride_w, stride_h
+        self.padW, self.padH, self.nGroup = pad_w, pad_h, n_group
+        self.dilationW, self.dilationH = dilation_w, dilation_h
+        self.withBias = with_bias
+        kg = n_input_plane // n_group * kernel_h * kernel_w
+        self.register_buffer("qweight", torch.zeros(n_output_plane, _kp(kg), dtype=torch.int8))
+        self.register_buffer("weight_scale", torch.zeros(n_output_plane))
+        if with_bias:
+            self.register_buffer("qbias", torch.zeros(n_output_plane))
+
+    @staticmethod
+    def from_float(m) -> "SpatialConvolution":
+        q = SpatialConvolution(m.nInputPlane, m.nOutputPlane, m.kernelW, m.kernelH, m.strideW, m.strideH, m.padW,
+                               m.padH, m.nGroup, getattr(m, "dilationW", 1), getattr(m, "dilationH", 1), m.withBias)
+        w = m.weight  # (g, out/g, in/g, kh, kw)
+        q._quantize_weight(w.reshape(m.nOutputPlane, -1))
+        if m.withBias:
+            q.qbias = m.bias.detach().float().clone().cpu()
+        q.format = getattr(m, "format", "NCHW")
+        q.set_name(m.get_name())
+        return q.to(w.device)
+
+    def _pads(self, x):
+        from ..layers.conv import same_padding
+        if self.padW == -1 and self.padH == -1:
+            return same_padding(x.shape[2], x.shape[3], self.strideH, self.strideW, self.kernelH, self.kernelW,
+                                self.dilationH, self.dilationW)
+        return self.padH, self.padH, self.padW, self.padW
+
+    def updateOutput(self, input):
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        if getattr(self, "format", "NCHW") == "NHWC":
+            x = x.permute(0, 3, 1, 2)
+        pt, pb, pl, pr = self._pads(x)
+        x = F.pad(x, (pl, pr, pt, pb)) if (pt or pb or pl or pr) else x
+        N, C, H, W = x.shape
+        kh, kw = self.kernelH, self.kernelW
+        P = (H - self.dilationH * (kh - 1) - 1) // self.strideH + 1
+        Q = (W - self.dilationW * (kw - 1) - 1) // self.strideW + 1
+        out_dt = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        g = self.nGroup
+        cg, kg = C // g, self.nOutputPlane // g
+        outs = []
+        for gi in range(g):
+            xs = x[:, gi * cg:(gi + 1) * cg]
+            cols = F.unfold(xs, (kh, kw), dilation=(self.dilationH, self.dilationW),
+                            stride=(self.strideH, self.strideW))  # [N, cg·kh·kw, L]
+            rows = cols.transpose(1, 2).reshape(N * P * Q, cg * kh * kw)
+            qa, sa = ops.quant_rows(rows.contiguous(), self.qweight.shape[1])
+            bias = self.bias_f[gi * kg:(gi + 1) * kg] if self.bias_f is not None else None
+            y = ops.gemm_i8(qa, sa, self.qweight[gi * kg:(gi + 1) * kg].contiguous(),
+                            self.weight_scale[gi * kg:(gi + 1) * kg].contiguous(), bias, out_dtype=out_dt)
+            outs.append(y.reshape(N, P, Q, kg))
+        y = torch.cat(outs, dim=3) if g > 1 else outs[0]
+        y = y.permute(0, 3, 1, 2)  # NCHW logical, channels-last memory
+        if getattr(self, "format", "NCHW") == "NHWC":
+            y = y.permute(0, 2, 3, 1)
+        return y if input.dim() == 4 else y.squeeze(0)
+
+    def __repr__(self):
+        return (f"quantized.SpatialConvolution[{self.get_name()}]({self.nInputPlane} -> {self.nOutputPlane}, "
+                f"{self.kernelW} x {self.kernelH}, {self.strideW}, {self.strideH}, {self.padW}, {self.padH})")
+
+
+class SpatialDilatedConvolution(SpatialConvolution):
+    @staticmethod
+    def from_float(m) -> "SpatialDilatedConvolution":
+        q = SpatialConvolution.from_float(m)
+        q.__class__ = SpatialDilatedConvolution
+        return q

@@ -512,3 +512,39 @@ def lstm_cell_backward(gh, gh2, gc_next, act, tc, c_prev, dg_out=None):
     check(_lib().bigdl_lstm_bwd(ptr(gh), C.c_long(ldgh), ptr(gh2), ptr(gc_next), ptr(act), ptr(tc), ptr(c_prev),
                                 ptr(dg), C.c_long(lddg), ptr(dc), B, H, 0 if dt == _bf16 else 1, _s()), "lstm_bwd")
     return dg, dc
+
+
+# ------------------------------------------------------------------------------------------------ int8 (K26)
+@register("quant_rows")
+def quant_rows(x2d, kp=None):
+    if x2d.dim() != 2 or x2d.dtype not in (_bf16, _f32) or x2d.stride(1) != 1:
+        return NotImplemented
+    M, K = x2d.shape
+    kp = kp or (K + 63) // 64 * 64
+    if kp % 16 or kp < K or M == 0 or K == 0:
+        return NotImplemented
+    q = torch.empty((M, kp), dtype=torch.int8, device=x2d.device)
+    sc = torch.empty(M, dtype=_f32, device=x2d.device)
+    check(_lib().bigdl_quant_rows(ptr(x2d), C.c_int(1 if x2d.dtype == _bf16 else 0), _ll(M), C.c_int(K),
+                                  _ll(x2d.stride(0)), ptr(q), C.c_int(kp), ptr(sc), _s()), "quant_rows")
+    return q, sc
+
+
+@register("gemm_i8")
+def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
+    if qa.dtype != torch.int8 or qb.dtype != torch.int8 or qa.shape[1] != qb.shape[1] or qa.shape[1] % 16:
+        return NotImplemented
+    if not (qa.is_contiguous() and qb.is_contiguous() and _al16(qa) and _al16(qb)):
+        return NotImplemented
+    if out_dtype not in (_f32, _bf16):
+        return NotImplemented
+    M, Kp = qa.shape
+    N = qb.shape[0]
+    sa = sa.float().contiguous()
+    sb = sb.float().contiguous()
+    b = bias.float().contiguous() if bias is not None else None
+    out = torch.empty((M, N), dtype=out_dtype, device=qa.device)
+    check(_lib().bigdl_gemm_i8(ptr(qa), ptr(qb), C.c_int(M), C.c_int(N), C.c_int(Kp), ptr(sa), ptr(sb), ptr(b),
+                               ptr(out), C.c_int(1 if out_dtype == _bf16 else 0), C.c_int(1 if relu else 0), _s()),
+          "gemm_i8")
+    return out

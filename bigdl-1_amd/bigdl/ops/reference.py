@@ -375,3 +375,30 @@ def lrn_forward(x, size, alpha, beta, k):
     """``SpatialCrossMapLRN`` (``DL/nn/SpatialCrossMapLRN.scala:96-200``):
     y = x / (k + α/size · Σ_{window} x²)^β."""
     return F.local_response_norm(x, size, alpha, beta, k)
+
+
+# ------------------------------------------------------------------------- int8 (K26)
+def quant_rows(x2d: torch.Tensor, kp: Optional[int] = None):
+    """Per-row symmetric int8 (``Quantization.quantize``: round-half-up(v / max|row| · 127)).
+    Returns (q [M][Kp] int8 zero-padded, scale [M] fp32 = max|row| / 127)."""
+    M, K = x2d.shape
+    kp = kp or (K + 63) // 64 * 64
+    xf = x2d.float()
+    amax = xf.abs().amax(dim=1) if K else torch.zeros(M, device=x2d.device)
+    inv = torch.where(amax > 0, 127.0 / amax, torch.zeros_like(amax))
+    q = torch.floor(xf * inv[:, None] + 0.5).clamp(-127, 127).to(torch.int8)
+    out = torch.zeros((M, kp), dtype=torch.int8, device=x2d.device)
+    out[:, :K] = q
+    return out, amax / 127.0
+
+
+def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
+    """C = (qa · qbᵀ) · sa[:, None] · sb[None, :] + bias, exact int32 accumulation."""
+    acc = (qa.to(torch.int32) @ qb.to(torch.int32).t()) if qa.device.type == "cpu" else \
+        (qa.double() @ qb.double().t())
+    y = acc.double() * sa.double()[:, None] * sb.double()[None, :]
+    if bias is not None:
+        y = y + bias.double()[None, :]
+    if relu:
+        y = torch.relu(y)
+    return y.to(out_dtype)
