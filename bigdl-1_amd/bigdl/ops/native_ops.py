@@ -548,3 +548,31 @@ def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
                                ptr(out), C.c_int(1 if out_dtype == _bf16 else 0), C.c_int(1 if relu else 0), _s()),
           "gemm_i8")
     return out
+
+
+# ------------------------------------------------------------------------------------------------ image (K25)
+@register("image_crop_flip_norm")
+def image_crop_flip_norm(src, oy, ox, flip, out_h, out_w, mean, std, to_rgb, out_dtype=torch.float32):
+    if src.dim() != 4 or src.dtype not in (torch.uint8, _f32) or not src.is_contiguous():
+        return NotImplemented
+    if out_dtype not in (_f32, _bf16):
+        return NotImplemented
+    B, H, W, Cc = src.shape
+    if Cc > 4:
+        return NotImplemented
+    oy_c, ox_c, fl_c = (torch.as_tensor(v).reshape(-1).cpu().int() for v in (oy, ox, flip))
+    if len(oy_c) != B or len(ox_c) != B or len(fl_c) != B:
+        return NotImplemented
+    if int(oy_c.max()) + out_h > H or int(ox_c.max()) + out_w > W or int(oy_c.min()) < 0 or int(ox_c.min()) < 0:
+        raise ValueError("crop window outside the image")
+    dev = src.device
+    oy_d, ox_d, fl_d = (t.to(dev, non_blocking=True) for t in (oy_c, ox_c, fl_c))
+    mean_f = (C.c_float * 4)(*[float(v) for v in list(mean)[:Cc]])
+    std_f = (C.c_float * 4)(*[float(v) for v in list(std)[:Cc]])
+    out = torch.empty((B, Cc, out_h, out_w), dtype=out_dtype, device=dev, memory_format=torch.channels_last)
+    check(_lib().bigdl_image_crop_flip_norm(ptr(src), C.c_int(1 if src.dtype == torch.uint8 else 0), C.c_int(B),
+                                            C.c_int(H), C.c_int(W), C.c_int(Cc), ptr(oy_d), ptr(ox_d), ptr(fl_d),
+                                            C.c_int(out_h), C.c_int(out_w), mean_f, std_f,
+                                            C.c_int(1 if to_rgb else 0), ptr(out),
+                                            C.c_int(1 if out_dtype == _bf16 else 0), _s()), "image_crop_flip_norm")
+    return out

@@ -402,3 +402,25 @@ def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
     if relu:
         y = torch.relu(y)
     return y.to(out_dtype)
+
+
+# ------------------------------------------------------------------------- image (K25)
+def image_crop_flip_norm(src, oy, ox, flip, out_h, out_w, mean, std, to_rgb, out_dtype=torch.float32):
+    """Batched crop + horizontal mirror + per-channel (x − mean)/std (+ BGR→RGB) of HWC images
+    ``src [B, H, W, C]`` (uint8 or float) → NCHW-logical channels-last tensor of ``out_dtype``.
+    ``mean``/``std`` are given in OUTPUT channel order."""
+    B, H, W, C = src.shape
+    outs = []
+    for i in range(B):
+        y, x = int(oy[i]), int(ox[i])
+        t = src[i, y:y + out_h, x:x + out_w].float()
+        if int(flip[i]):
+            t = t.flip(1)
+        if to_rgb and C == 3:
+            t = t.flip(2)
+        outs.append(t)
+    t = torch.stack(outs)
+    m = torch.tensor(list(mean)[:C], dtype=torch.float32, device=src.device)
+    s = torch.tensor(list(std)[:C], dtype=torch.float32, device=src.device)
+    t = (t - m) / s
+    return t.permute(0, 3, 1, 2).to(out_dtype)
