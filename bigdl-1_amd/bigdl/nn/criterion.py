@@ -601,3 +601,6 @@ class PGCriterion(AbstractCriterion):
     def updateGradInput(self, input, target):
         g = -target.float() / input.float().clamp_min(1e-12)
         return g / input.shape[0] if self.sizeAverage else g
+
+
+Criterion = AbstractCriterion  # pyspark ``bigdl.nn.criterion.Criterion``

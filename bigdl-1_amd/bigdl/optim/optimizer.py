@@ -116,7 +116,10 @@ class BaseOptimizer:
         self.validation_methods = list(vmethods)
         return self
 
-    set_validation = setValidation
+    def set_validation(self, batch_size, val_rdd, trigger, val_method=None):
+        """pyspark signature: ``set_validation(batch_size, val_rdd, trigger, val_method)``."""
+        from .validation import Top1Accuracy
+        return self.setValidation(trigger, val_rdd, val_method or [Top1Accuracy()], batch_size)
 
     def setCheckpoint(self, path, trigger, is_overwrite=False):
         stamp = time.strftime("%Y%m%d_%H%M%S")
@@ -183,6 +186,21 @@ class BaseOptimizer:
         return self
 
     set_end_when = setEndWhen
+
+    def set_gradclip_const(self, min_value, max_value):
+        return self.setConstantGradientClipping(min_value, max_value)
+
+    def set_gradclip_l2norm(self, clip_norm):
+        return self.setGradientClippingByl2Norm(clip_norm)
+
+    def disable_gradclip(self):
+        return self.disableGradientClipping()
+
+    def set_model(self, model):
+        return self.setModel(model)
+
+    def prepare_input(self):
+        return self.prepareInput()
 
     def setDropModuleProperty(self, drop_percentage, max_drop_percentage, batchsize=100, warmup_iteration=200):
         """Straggler dropping (P5).  One GPU per rank rarely straggles; the knob is accepted and
@@ -558,3 +576,20 @@ class Optimizer:
         else:
             opt = LocalOptimizer(model, training_set, criterion, optim_method, end_trigger, batch_size)
         return opt
+
+
+# ---- pyspark ``bigdl.optim.optimizer`` namespace: every optimizer-side class in one module ----
+from .optim_method import *  # noqa: E402,F401,F403
+from .trigger import *  # noqa: E402,F401,F403
+from .validation import *  # noqa: E402,F401,F403
+from .regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer  # noqa: E402,F401
+from ..visualization import TrainSummary, ValidationSummary  # noqa: E402,F401
+
+
+class ActivityRegularization(L1L2Regularizer):
+    """pyspark ``ActivityRegularization(l1, l2)`` — L1 and L2 together."""
+
+
+def DistriOptimizer(*args, **kwargs):  # noqa: N802 - pyspark class name
+    from ..parallel.distri_optimizer import DistriOptimizer as _D
+    return _D(*args, **kwargs)
