@@ -47,7 +47,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int BN>
+// FAST: C % 64 == 0 and R·S ≤ 64 — every k-tile lies inside one filter tap, so the tap / channel
+// position of a k-tile is wave-uniform (scalar registers, no per-lane division) and the padding test
+// of a staged row is one bit of a per-row tap-validity mask built once in the prologue.
+template <int BN, bool FAST>
 __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   constexpr int ROWS = BM + BN;
   constexpr int TN = BN / 32;  // MFMA tiles along channels per wave
@@ -63,6 +66,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int col8 = tid & 7;  // this thread's 16-B chunk column inside a 64-wide k tile
 
+  // Operand loads are raw buffer loads: the descriptor's num_records bounds-check returns zeros
+  // for an out-of-range offset, so conv padding, the M / K tails and the channel tail need no
+  // branches (a per-element "load or zero" select makes hipcc branch and drain vmcnt per load,
+  // cdna_hip_programming.md §5 item 4(c)).  OOB = an offset past the end of the tensor.
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C * 2);
+  const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.Kg * 2);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
+
   // per-row gather state for the activation rows this thread stages
   int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
 #pragma unroll
@@ -77,39 +90,89 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       a_w[i] = qq * p.sw - p.pw;
     } else {
       a_img[i] = -1;
-      a_h[i] = 0;
+      a_h[i] = -(1 << 28);
       a_w[i] = 0;
     }
   }
+  uint32_t b_row[B_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < B_CHUNKS; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    b_row[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 2u : 0x80000000u;  // + any k stays out of range
+  }
 
-  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
   const int KT = (p.Kg + BK - 1) / BK;
 
-  auto load_tile = [&](int kt) {
-    const int k = kt * BK + col8 * 8;
-    int tap = 0, c = k, r = 0, s = 0;
-    const bool kin = k < p.Kg;
-    if (kin) {
-      tap = k / p.C;
-      c = k - tap * p.C;
-      r = tap / p.S;
-      s = tap - r * p.S;
-    }
+  // FAST-path per-row state: base element offset of the (r=0, s=0) tap and its tap-validity mask
+  int rbase[A_CHUNKS];
+  uint64_t vmask[A_CHUNKS];
+  if constexpr (FAST) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      int h = a_h[i] + r * p.dh, w = a_w[i] + s * p.dw;
-      bool ok = kin && a_img[i] >= 0 && h >= 0 && h < p.H && w >= 0 && w < p.W;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(p.x + ((size_t)(a_img[i] + h * p.W + w) * p.C + c))
-                 : make_uint4(0, 0, 0, 0);
+      rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.C) + col8 * 8;
+      uint64_t msk = 0;
+      if (a_img[i] >= 0) {
+        for (int r = 0; r < p.R; ++r) {
+          const int h = a_h[i] + r * p.dh;
+          if ((unsigned)h >= (unsigned)p.H) continue;
+          for (int sx = 0; sx < p.S; ++sx) {
+            const int w = a_w[i] + sx * p.dw;
+            if ((unsigned)w < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
+          }
+        }
+      }
+      vmask[i] = msk;
     }
+  }
+
+  // ``live`` = false issues the same loads with out-of-range offsets (they return zeros and touch no
+  // memory): keeping every load unconditional keeps hipcc's vmcnt counting exact — a conditionally
+  // issued group makes it wait as if the group were absent, draining the pipeline every k-tile.
+  auto load_tile = [&](int kt, bool live, uint4 (&ra)[A_CHUNKS], uint4 (&rb)[B_CHUNKS]) {
+    const uint32_t dead = live ? 0u : 0x80000000u;
+    if constexpr (FAST) {
+      kt = live ? kt : 0;
+      const int kb = kt * BK;                 // wave-uniform
+      const int tap = kb / p.C;
+      const int c0 = kb - tap * p.C;
+      const int r = tap / p.S, sx = tap - (tap / p.S) * p.S;
+      const int tap_off = (r * p.dh * p.W + sx * p.dw) * p.C + c0;
 #pragma unroll
-    for (int i = 0; i < B_CHUNKS; ++i) {
-      int n = n0 + (tid >> 3) + 32 * i;
-      bool ok = kin && n < p.K;
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(p.w + ((size_t)n * p.Kg + k)) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const bool ok = (vmask[i] >> tap) & 1ull;
+        const uint32_t off = (ok ? (uint32_t)(rbase[i] + tap_off) * 2u : OOB) | dead;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < B_CHUNKS; ++i) {
+        const uint32_t off = (b_row[i] + (uint32_t)(kb + col8 * 8) * 2u) | dead;  // OOB rows stay out of range
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+      }
+    } else {
+      const int k = kt * BK + col8 * 8;
+      int tap = 0, c = k, r = 0, sx = 0;
+      const bool kin = live && k < p.Kg;
+      if (kin) {
+        tap = k / p.C;
+        c = k - tap * p.C;
+        r = tap / p.S;
+        sx = tap - r * p.S;
+      }
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const int h = a_h[i] + r * p.dh, w = a_w[i] + sx * p.dw;
+        const bool ok = kin && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+        const uint32_t off = ok ? (uint32_t)((a_img[i] + h * p.W + w) * p.C + c) * 2u : OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < B_CHUNKS; ++i) {
+        const uint32_t off = kin && b_row[i] != OOB ? b_row[i] + (uint32_t)k * 2u : OOB;
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+      }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[A_CHUNKS], const uint4 (&rb)[B_CHUNKS]) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
       int row = (tid >> 3) + 32 * i;
@@ -128,14 +191,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < KT) load_tile(kt + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -155,7 +212,31 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < KT) store_tile(buf ^ 1);
+  };
+
+  // Two register sets, loads issued two k-tiles ahead of their use: tile t+2 is requested while
+  // tile t is multiplied and is written to LDS only after tile t+1's MFMAs, so HBM / L2 latency
+  // hides under two compute phases (one barrier per k-tile; the loop is unrolled by two so both
+  // register sets stay statically indexed — runtime-indexed vectors would go to scratch).
+  uint4 ra0[A_CHUNKS], rb0[B_CHUNKS], ra1[A_CHUNKS], rb1[B_CHUNKS];
+  load_tile(0, true, ra0, rb0);
+  load_tile(1, KT > 1, ra1, rb1);
+  store_tile(0, ra0, rb0);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 2 <= KT; kt += 2) {
+    // lds[0] = tile kt; set 1 = tile kt+1 (in flight)
+    load_tile(kt + 2, kt + 2 < KT, ra0, rb0);
+    compute(0);
+    store_tile(1, ra1, rb1);
+    __syncthreads();
+    load_tile(kt + 3, kt + 3 < KT, ra1, rb1);
+    compute(1);
+    if (kt + 2 < KT) store_tile(0, ra0, rb0);
+    __syncthreads();
+  }
+  if (kt < KT) {  // odd KT: the last tile sits in lds[0]
+    compute(0);
     __syncthreads();
   }
 
@@ -165,7 +246,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   //  2. the block walks the tile row-major, 8 channels per thread: optional residual add (same
   //     16-B chunk of `res`), ReLU, one global_store_dwordx4, and optional per-channel Σy / Σy²
   //     partials for a following BatchNormalization (the conv then replaces the BN stats pass).
-  constexpr int LDR = BN + 8;
+  constexpr int LDR = BN + 16;  // 288/160-B rows: the b64 fragment writes of 16 rows hit distinct banks
   bf16_t* et = &lds[0][0];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
@@ -197,35 +278,43 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   for (int r = rr; r < BM; r += RPP) {
     const int m = m0 + r;
     if (m >= p.M || n >= p.K) continue;
-    float v[8];
-    load8(&et[r * LDR + cc * 8], v);
     const size_t off = (size_t)m * p.K + n;
     if (full) {
-      if (p.res) {
-        float rv[8];
-        load8(p.res + off, rv);
+      uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + cc * 8]);
+      if (p.res || p.relu) {
+        float v[8];
+        load8(&et[r * LDR + cc * 8], v);
+        if (p.res) {
+          float rv[8];
+          load8(p.res + off, rv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += rv[e];
-      }
-      if (p.relu) {
+          for (int e = 0; e < 8; ++e) v[e] += rv[e];
+        }
+        if (p.relu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+        u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
-      store8(p.y + off, v);
+      *reinterpret_cast<uint4*>(p.y + off) = u;
       if (p.stats) {
         // statistics of the values as stored (bf16-rounded), which is what the BN reads
-        uint4 u = *reinterpret_cast<const uint4*>(p.y + off);
-        float w[8];
         const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          w[2 * e] = __uint_as_float(uw[e] << 16);
-          w[2 * e + 1] = __uint_as_float(uw[e] & 0xFFFF0000u);
+          const float a = __uint_as_float(uw[e] << 16), b = __uint_as_float(uw[e] & 0xFFFF0000u);
+          s8[2 * e] += a;
+          q8[2 * e] = fmaf(a, a, q8[2 * e]);
+          s8[2 * e + 1] += b;
+          q8[2 * e + 1] = fmaf(b, b, q8[2 * e + 1]);
         }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { s8[e] += w[e]; q8[e] = fmaf(w[e], w[e], q8[e]); }
       }
     } else {
+      float v[8];
+      load8(&et[r * LDR + cc * 8], v);
       for (int e = 0; e < 8 && n + e < p.K; ++e) {
         float t = v[e] + (p.res ? bf2f(p.res[off + e]) : 0.f);
         if (p.relu) t = fmaxf(t, 0.f);
@@ -270,6 +359,9 @@ BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bi
                                    int sh, int sw, int ph, int pw, int dh, int dw, int relu, hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
+  // 32-bit buffer offsets: both operands must stay below 2 GiB
+  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * R * S * C * 2 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;
   ConvParams p;
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)w;
@@ -289,10 +381,15 @@ BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bi
   p.tiles_m = (p.M + BM - 1) / BM;
   long long tiles = (long long)p.tiles_m * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
-  if (BN == 64)
-    hipLaunchKernelGGL(k_conv_fwd<64>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  const bool fast = (C % 64 == 0) && R * S <= 64;
+  if (BN == 64 && fast)
+    hipLaunchKernelGGL((k_conv_fwd<64, true>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (BN == 64)
+    hipLaunchKernelGGL((k_conv_fwd<64, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (fast)
+    hipLaunchKernelGGL((k_conv_fwd<128, true>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL(k_conv_fwd<128>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((k_conv_fwd<128, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   BIGDL_CHECK_LAUNCH();
 }
 

@@ -222,8 +222,12 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   p.tiles_k = (p.Kg + TK - 1) / TK;
   const int tiles = p.tiles_n * p.tiles_k;
   if (splits <= 0) {
-    // aim for ≈ 2048 blocks (8 per CU) but ≥ 8 k-tiles of pixels per block
-    long long want = (2048 + tiles - 1) / tiles;
+    // splits <= 0: aim for -splits blocks in total (default 512 = two resident blocks per CU), but
+    // ≥ 8 k-tiles of pixels per block.  Every split adds its full K×Kg partial with fp32 atomics
+    // (≈1.3 TB/s chip-wide, MI355X_MICROARCH.md 'Global float atomics'), so fewer, longer splits win
+    // once the grid fills the chip.
+    const long long target = splits < 0 ? -(long long)splits : 512;
+    long long want = (target + tiles - 1) / tiles;
     long long max_by_work = (p.M + 8 * BP - 1) / (8 * BP);
     splits = (int)(want < max_by_work ? want : max_by_work);
     if (splits < 1) splits = 1;

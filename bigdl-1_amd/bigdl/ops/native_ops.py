@@ -366,6 +366,24 @@ def _dgrad_1x1_strided(gy, w4, x_shape, stride):
     return gx
 
 
+#: total blocks the wgrad kernel aims for (split-K over pixels); 0 = per-shape heuristic below.
+#: tools/bench_conv.py --wgrad-sweep A/Bs fixed values.
+_WGRAD_TARGET_BLOCKS = [int(__import__("os").environ.get("BIGDL_WGRAD_BLOCKS", "0"))]
+
+
+def _wgrad_blocks(M, C_, K):
+    """Split-K target measured on the ResNet-50 shapes (profiles/r1_wgrad_sweep.txt): 384 blocks
+    (1.5 per CU) minimises atomic traffic for most layers; the very tall, narrow 56² layers and the
+    C=3 stem need more blocks to fill the chip."""
+    if _WGRAD_TARGET_BLOCKS[0] > 0:
+        return _WGRAD_TARGET_BLOCKS[0]
+    if C_ <= 8:
+        return 2048
+    if M >= 400000 and (C_ <= 64 or K <= 64):
+        return 768
+    return 384
+
+
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
                     scale=1.0, residual=None):
@@ -401,8 +419,8 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
         P, Q = gy.shape[2], gy.shape[3]
         check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
-                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0,
-                                      _s()), "conv_wgrad")
+                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                      -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
         if not direct:
             gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
     if gb_acc is not None and scale != 0:

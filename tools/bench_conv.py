@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/bench_conv.json")
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--wgrad-sweep", default="", help="comma list of wgrad target block counts to A/B")
     args = ap.parse_args()
     import torch
     import torch.nn.functional as F
@@ -72,10 +73,18 @@ def main():
         t_f = timeit(lambda: NO.conv2d_forward(x, w, None, (s, s), (pad, pad)))
         t_d = timeit(lambda: NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=True)) if C != 3 else 0.0
         t_w = timeit(lambda: NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=False, gw_acc=gw))
+        sweep = {}
+        for tb in [int(v) for v in args.wgrad_sweep.split(",") if v]:
+            old = NO._WGRAD_TARGET_BLOCKS[0]
+            NO._WGRAD_TARGET_BLOCKS[0] = tb
+            sweep[tb] = timeit(lambda: NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=False, gw_acc=gw))
+            NO._WGRAD_TARGET_BLOCKS[0] = old
+            tot.setdefault(f"wgrad@{tb}", 0.0)
+            tot[f"wgrad@{tb}"] += sweep[tb] * mult
         row = {"C": C, "K": K, "R": R, "s": s, "H": H, "P": P, "mult": mult, "gflop": flops / 1e9,
                "fwd_ms": t_f, "dgrad_ms": t_d, "wgrad_ms": t_w,
                "fwd_tf": flops / t_f / 1e9, "dgrad_tf": flops / t_d / 1e9 if t_d else None,
-               "wgrad_tf": flops / t_w / 1e9}
+               "wgrad_tf": flops / t_w / 1e9, "wgrad_sweep_ms": sweep}
         if not args.no_miopen:
             xr = x.detach().clone().requires_grad_(True)
             wr = w.detach().clone().requires_grad_(True)
@@ -95,7 +104,7 @@ def main():
         print(f"C{C:5d} K{K:5d} R{R} s{s} H{H:3d} x{mult}  fwd {t_f:7.3f}ms {row['fwd_tf']:7.1f}TF  "
               f"dgrad {t_d:7.3f}ms {row['dgrad_tf'] or 0:7.1f}TF  wgrad {t_w:7.3f}ms {row['wgrad_tf']:7.1f}TF"
               + (f"  | miopen fwd {row['miopen_fwd_ms']:7.3f}ms bwd {row['miopen_bwd_ms']:7.3f}ms"
-                 if "miopen_fwd_ms" in row else ""), flush=True)
+                 if "miopen_fwd_ms" in row else "") + (f"  sweep {sweep}" if sweep else ""), flush=True)
     print("per-step totals (ms, weighted by multiplicity):", json.dumps({k: round(v, 3) for k, v in tot.items()}))
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:

@@ -1,0 +1,37 @@
+#!/usr/bin/env python
+"""Run one conv shape (fwd / dgrad / wgrad) N times — a target for rocprofv3 --pmc."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bigdl-1_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="256,256,3,1,14")  # C,K,R,stride,H
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
+    a = ap.parse_args()
+    import torch
+    from bigdl.ops import native_ops as NO
+    C, K, R, s, H = [int(v) for v in a.shape.split(",")]
+    pad = R // 2
+    x = torch.randn(a.batch, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).bfloat16()
+    y = NO.conv2d_forward(x, w, None, (s, s), (pad, pad))
+    gy = torch.randn_like(y)
+    gw = torch.zeros(K, C, R, R, device="cuda")
+    for _ in range(a.iters):
+        if a.op == "fwd":
+            NO.conv2d_forward(x, w, None, (s, s), (pad, pad))
+        elif a.op == "dgrad":
+            NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=True)
+        else:
+            NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=False, gw_acc=gw)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

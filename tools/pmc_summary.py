@@ -1,0 +1,32 @@
+"""Summarise rocprofv3 --pmc CSV passes (tools/pmc_conv.sh): per shape, per kernel, mean counter
+values over dispatches, plus derived MFMA utilisation."""
+import collections
+import csv
+import os
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+index = [l.split(" ", 2) for l in open(os.path.join(root, "index.txt")).read().splitlines()]
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for i, shape, grp in index:
+    path = os.path.join(root, f"p{i}", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        continue
+    for row in csv.DictReader(open(path)):
+        k = row["Kernel_Name"][:40]
+        if "k_conv" not in k:
+            continue
+        res[(shape, k)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+for (shape, k), cnt in sorted(res.items()):
+    m = {c: sum(v) / len(v) for c, v in cnt.items()}
+    print(f"== {shape}  {k}")
+    for c in sorted(m):
+        print(f"   {c:28s} {m[c]:16.1f}")
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
+        # MFMA busy is summed over SIMDs (256 CUs x 4)
+        print(f"   MFMA util ≈ {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] * 1024):.3f}"
+              f"  (busy / (gui_active x 1024 SIMDs))")
+    if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
+        print(f"   VALU per MFMA = {m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f}")
+    if "TCC_HIT_sum" in m:
+        print(f"   L2 hit = {m['TCC_HIT_sum'] / max(m['TCC_HIT_sum'] + m['TCC_MISS_sum'], 1):.3f}")
