@@ -97,32 +97,40 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
   const int ndy = n0 + dy_col * 8;
   const bool ndy_ok = ndy < p.K;
 
-  uint4 rdy[DY_CH], rx_[X_CH];
-  auto load = [&](int mt) {
+  // Raw buffer loads (OOB offsets → zeros, no branches) into two register sets; tile t+2 is
+  // requested while tile t is multiplied (loads always issued — beyond the range with a dead
+  // offset — so hipcc's vmcnt counts stay exact; see conv_igemm.hip).
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C * 2);
+  const uint32_t dy_bytes = (uint32_t)((size_t)p.M * p.K * 2);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)dy_bytes, 0x00020000);
+  constexpr uint32_t DEAD = 0x80000000u;
+
+  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH], uint4 (&rx_)[X_CH]) {
+    const uint32_t dead = live ? 0u : DEAD;
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
-      int m = mt + dy_row0 + i * DY_RSTEP;
-      bool ok = ndy_ok && m < mend;
-      rdy[i] = ok ? *reinterpret_cast<const uint4*>(p.dy + (size_t)m * p.K + ndy) : make_uint4(0, 0, 0, 0);
+      const int m = mt + dy_row0 + i * DY_RSTEP;
+      const bool ok = ndy_ok && m < mend;
+      const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.K + (uint32_t)ndy) * 2u : DEAD) | dead;
+      rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
-      int m = mt + x_row0 + i * X_RSTEP;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kx_ok && m < mend) {
-        uint32_t n = fdiv((uint32_t)m, p.fPQ);
-        uint32_t pq = (uint32_t)m - n * (uint32_t)(p.P * p.Q);
-        uint32_t pp = fdiv(pq, p.fQ);
-        uint32_t q = pq - pp * (uint32_t)p.Q;
-        int h = (int)pp * p.sh - p.ph + rx * p.dh;
-        int w = (int)q * p.sw - p.pw + sx * p.dw_;
-        if (h >= 0 && h < p.H && w >= 0 && w < p.W)
-          v = *reinterpret_cast<const uint4*>(p.x + ((size_t)((n * p.H + h) * p.W + w) * p.C + cx));
-      }
-      rx_[i] = v;
+      const int m = mt + x_row0 + i * X_RSTEP;
+      const uint32_t mm = (uint32_t)(m < mend ? m : mbeg);
+      const uint32_t n = fdiv(mm, p.fPQ);
+      const uint32_t pq = mm - n * (uint32_t)(p.P * p.Q);
+      const uint32_t pp = fdiv(pq, p.fQ);
+      const uint32_t q = pq - pp * (uint32_t)p.Q;
+      const int h = (int)pp * p.sh - p.ph + rx * p.dh;
+      const int w = (int)q * p.sw - p.pw + sx * p.dw_;
+      const bool ok = kx_ok && m < mend && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+      const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.C + (uint32_t)cx) * 2u : DEAD) | dead;
+      rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4 (&rdy)[DY_CH], const uint4 (&rx_)[X_CH]) {
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
       int row = dy_row0 + i * DY_RSTEP;
@@ -141,16 +149,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
 #pragma unroll
     for (int j = 0; j < TMK; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  load(mbeg);
-  store(0);
-  __syncthreads();
-
   const int g = (lane >> 4) & 3;  // 16-lane group → pixels 8g..8g+7 of a 32-pixel k-step
   const int t = lane & 15, q4 = t >> 2, p4 = t & 3;
-  int buf = 0;
-  for (int mt = mbeg; mt < mend; mt += BP) {
-    const bool more = mt + BP < mend;
-    if (more) load(mt + BP);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       v8s af[TMN], bfr[TMK];
@@ -179,9 +180,27 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
 #pragma unroll
         for (int j = 0; j < TMK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store(buf ^ 1);
+  };
+
+  uint4 dy0[DY_CH], x0[X_CH], dy1[DY_CH], x1[X_CH];
+  const int NT = (mend - mbeg + BP - 1) / BP;
+  load(mbeg, true, dy0, x0);
+  load(mbeg + BP, NT > 1, dy1, x1);
+  store(0, dy0, x0);
+  __syncthreads();
+  int it = 0;
+  for (; it + 2 <= NT; it += 2) {
+    load(mbeg + (it + 2) * BP, it + 2 < NT, dy0, x0);
+    compute(0);
+    store(1, dy1, x1);
     __syncthreads();
-    buf ^= 1;
+    load(mbeg + (it + 3) * BP, it + 3 < NT, dy1, x1);
+    compute(1);
+    if (it + 2 < NT) store(0, dy0, x0);
+    __syncthreads();
+  }
+  if (it < NT) {
+    compute(0);
   }
 
   // epilogue: D[row = n][col = k]; lane holds rows (lane>>4)*4 + e of column lane&15
@@ -205,6 +224,8 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
                                   int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
                                   int splits, hipStream_t s) {
   if (C % 8 || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)Nb * P * Q * K * 2 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   WgradParams p;
   p.x = (const bf16_t*)x;
   p.dy = (const bf16_t*)dy;
