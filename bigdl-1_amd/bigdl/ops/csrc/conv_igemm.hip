@@ -35,6 +35,9 @@ struct ConvParams {
   const bf16_t* res;   // optional [M][K] tensor added before the ReLU (residual / gradient sum)
   float* stats;        // optional BN partials: stats[tm][K] = Σ y, stats[G + tm][K] = Σ y² (G = #row tiles)
   int tiles_m;
+  // optional output scatter (sub-pixel strided dgrad): output pixel (n, p, q) is stored at pixel
+  // (n, p·osh + ooh, q·osw + oow) of a [Nb][oH][oW][K] tensor
+  int scatter, osh, osw, ooh, oow, oH, oW;
 };
 
 constexpr int BM = 128;
@@ -278,7 +281,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   for (int r = rr; r < BM; r += RPP) {
     const int m = m0 + r;
     if (m >= p.M || n >= p.K) continue;
-    const size_t off = (size_t)m * p.K + n;
+    size_t off = (size_t)m * p.K + n;
+    if (p.scatter) {
+      const int nimg = m / (p.P * p.Q);
+      const int pq = m - nimg * p.P * p.Q;
+      const int pp = pq / p.Q, qq = pq - pp * p.Q;
+      off = ((size_t)(nimg * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow) * p.K + n;
+    }
     if (full) {
       uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + cc * 8]);
       if (p.res || p.relu) {
@@ -354,9 +363,10 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 // ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
 BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + BM - 1) / BM); }
 
-BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,
-                                   float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
-                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, hipStream_t s) {
+BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                        float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P,
+                                        int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh,
+                                        int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
@@ -376,6 +386,9 @@ BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bi
   p.M = (int)Ml;
   p.Kg = R * S * C;
   p.relu = relu;
+  p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
+  p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
+  if (p.scatter && stats) return (int)hipErrorInvalidValue;
   const int BN = K <= 64 ? 64 : 128;
   p.tiles_n = (K + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
@@ -391,6 +404,13 @@ BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bi
   else
     hipLaunchKernelGGL((k_conv_fwd<128, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                   float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, hipStream_t s) {
+  return bigdl_conv_fwd_scatter(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, 1,
+                                1, 0, 0, P, Q, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W, int C,

@@ -349,6 +349,91 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None):
     return gx
 
 
+_SUBFILTER_IDX: dict = {}
+
+
+def _subfilters(w4, classes):
+    """All parity sub-filters of a strided dgrad in ONE gather: W'_ab[c][j'][i'][k] =
+    W[k][c][rs[Ra-1-j']][ss[Sb-1-i']], indexed straight from the weight's physical storage (KRSC
+    in the arena) with a cached index vector — one small kernel per layer per step."""
+    K, C_, R, S = w4.shape
+    krsc = w4.permute(0, 2, 3, 1)
+    phys = krsc if krsc.is_contiguous() else krsc.contiguous()
+    key = (K, C_, R, S, tuple((a, b, tuple(rs), tuple(ss)) for (a, b, rs, ss, *_r) in classes), w4.device)
+    ent = _SUBFILTER_IDX.get(key)
+    if ent is None:
+        parts, sizes = [], []
+        kk = torch.arange(K).view(1, 1, 1, K)
+        cc = torch.arange(C_).view(C_, 1, 1, 1)
+        for (a, b, rs, ss, *_r) in classes:
+            if not rs or not ss:
+                sizes.append(0)
+                continue
+            rr = torch.tensor(rs[::-1]).view(1, len(rs), 1, 1)
+            sv = torch.tensor(ss[::-1]).view(1, 1, len(ss), 1)
+            idx = ((kk * R + rr) * S + sv) * C_ + cc  # [C][Ra][Sb][K] → offset in (K, R, S, C)
+            parts.append(idx.reshape(-1))
+            sizes.append(idx.numel())
+        ent = (torch.cat(parts).to(w4.device), sizes)
+        _SUBFILTER_IDX[key] = ent
+    idx, sizes = ent
+    flat = phys.reshape(-1)[idx]
+    out, off = [], 0
+    for (a, b, rs, ss, *_r), n in zip(classes, sizes):
+        out.append(flat[off:off + n].view(C_, len(rs), len(ss), K) if n else None)
+        off += n
+    return out
+
+
+def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
+    """Strided backward-data by sub-pixel decomposition: the input-gradient pixels of parity
+    (a, b) = (h mod sh, w mod sw) receive only the filter taps r ≡ a + ph (mod sh), s ≡ b + pw
+    (mod sw), so each parity class is a STRIDE-1 convolution of gy with a flipped sub-filter whose
+    output is scattered to pixels (sh·ho + a, sw·wo + b) — sh·sw launches of the implicit-GEMM
+    kernel and no zero-stuffed FLOPs (reference: SpatialConvolution.updateGradInput's col2im,
+    DL/nn/SpatialConvolution.scala:656-735)."""
+    N_, C_, H, W = x_shape
+    K, Ci, R, S = w4.shape
+    sh, sw = stride
+    ph, pw = pad
+    if tuple(dilation) != (1, 1) or C_ % 8 or K % 8 or gy.shape[1] != K:
+        return None
+    if residual is not None and not (residual.shape == (N_, C_, H, W) and residual.dtype == _bf16 and
+                                     residual.is_contiguous(memory_format=torch.channels_last) and _al16(residual)):
+        return None
+    P, Q = gy.shape[2], gy.shape[3]
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    classes = []
+    for a in range(sh):
+        ra = (a + ph) % sh
+        rs = list(range(ra, R, sh))
+        for b in range(sw):
+            sb = (b + pw) % sw
+            ss = list(range(sb, S, sw))
+            ho = (H - a + sh - 1) // sh
+            wo = (W - b + sw - 1) // sw
+            if ho <= 0 or wo <= 0:
+                continue
+            classes.append((a, b, rs, ss, ho, wo, (a + ph - ra) // sh, (b + pw - sb) // sw))
+    if any(not rs or not ss for (_, _, rs, ss, *_r) in classes):
+        # some parity receives no tap (e.g. 1x1 stride 2): those pixels are exactly zero / the residual
+        if residual is not None:
+            gx.copy_(residual)
+        else:
+            gx.zero_()
+    subs = _subfilters(w4, classes)
+    for ci, (a, b, rs, ss, ho, wo, ea, eb) in enumerate(classes):
+        if not rs or not ss:
+            continue
+        wt = subs[ci]
+        Ra, Sb = len(rs), len(ss)
+        res_ok = residual is not None  # tap-less parities already hold the residual (copied above)
+        check(_lib().bigdl_conv_fwd_scatter(ptr(gy), ptr(wt), ptr(None), ptr(residual if res_ok else None), ptr(gx),
+                                            ptr(None), N_, P, Q, K, C_, Ra, Sb, ho, wo, 1, 1, Ra - 1 - ea,
+                                            Sb - 1 - eb, 1, 1, 0, sh, sw, a, b, H, W, _s()), "conv_dgrad_strided")
+    return gx
+
+
 def _dgrad_1x1_strided(gy, w4, x_shape, stride):
     """1×1 stride-s backward-data: GEMM into the strided positions, zeros elsewhere."""
     N_, C_, H, W = x_shape
@@ -404,9 +489,10 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             res_done = gi is not None
             if gi is None and residual is not None:
                 gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)
-        elif R == 1 and S == 1 and tuple(pad) == (0, 0):
-            gi = _dgrad_1x1_strided(gy, w4, x.shape, stride)
-        if gi is None:  # strided k>1 backward-data: library path until the sub-pixel kernel lands
+        else:
+            gi = _dgrad_strided(gy, w4, x.shape, tuple(stride), tuple(pad), dilation, residual)
+            res_done = gi is not None
+        if gi is None:  # dilated strided backward-data: library path
             gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
         if residual is not None and not res_done:
             gi = gi + residual

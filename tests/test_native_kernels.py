@@ -331,3 +331,23 @@ def test_dgrad_residual_fold():
     gi0 = N.conv2d_backward(gy, x, w4, (1, 1), (1, 1), (1, 1), 1, True, None, None, 0.0)
     gi1 = N.conv2d_backward(gy, x, w4, (1, 1), (1, 1), (1, 1), 1, True, None, None, 0.0, residual=res)
     torch.testing.assert_close(gi1.float(), gi0.float() + res.float(), rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 64, 15, 13, 128, 3, 3, 2, 1), (2, 64, 14, 14, 64, 1, 1, 2, 0),
+                                  (1, 32, 11, 12, 64, 5, 5, 2, 2), (2, 16, 9, 9, 32, 3, 3, 3, 1)])
+def test_strided_dgrad_subpixel(case):
+    """Sub-pixel strided backward-data (sh·sw stride-1 launches with output scatter) vs autograd,
+    with and without the fused residual-gradient sum."""
+    N = _native()
+    n, c, h, w, k, r, s, st, pd = case
+    x = _cl(torch.randn(n, c, h, w, device=dev).bfloat16())
+    w4 = _cl(torch.randn(k, c, r, s, device=dev).bfloat16() * 0.1)
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, w4.float(), None, (st, st), (pd, pd))
+    gy = _cl(torch.randn_like(yr).bfloat16())
+    yr.backward(gy.float())
+    gi = N.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (1, 1), 1, True, None, None, 0.0)
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=3e-2, atol=3e-2)
+    res = _cl(torch.randn_like(x))
+    gi2 = N.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (1, 1), 1, True, None, None, 0.0, residual=res)
+    torch.testing.assert_close(gi2.float(), xr.grad + res.float(), rtol=3e-2, atol=4e-2)
