@@ -34,12 +34,13 @@ def _is_nchw_bn(m):
     return isinstance(m, BatchNormalization) and getattr(m, "dataFormat", "NCHW") == "NCHW"
 
 
-def fuse(model, convbn=None, bnrelu=None, convsum=None):
+def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
     if not config.get_property("bigdl.fusion"):
         return model
     convbn = config.get_property("bigdl.fusion.convbn") if convbn is None else convbn
     bnrelu = config.get_property("bigdl.fusion.bnrelu") if bnrelu is None else bnrelu
     convsum = config.get_property("bigdl.fusion.convsum") if convsum is None else convsum
+    bnbwd = config.get_property("bigdl.fusion.bnbwd") if bnbwd is None else bnbwd
     for s in model.flattened_modules():
         if not isinstance(s, Sequential):
             continue
@@ -54,6 +55,9 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None):
             if bnrelu and _is_nchw_bn(a) and _is_relu(b):
                 a._fused_relu = True
                 b._passthrough = True
+                c = mods[i + 2] if i + 2 < len(mods) else None
+                if bnbwd and isinstance(c, SpatialConvolution) and c.format == "NCHW" and c.nGroup == 1:
+                    c._bn_bwd_target = a
         if not convsum:
             continue
         for i in range(len(mods) - 1):
@@ -78,9 +82,12 @@ def unfuse(model):
     for m in model.flattened_modules():
         if isinstance(m, SpatialConvolution):
             m._bias_folded_into = None
+            m._bn_bwd_target = None
         if isinstance(m, BatchNormalization):
             m._bias_producer = None
             m._fused_relu = False
+            m._pending_stats = None
+            m._pending_grad = None
         if isinstance(m, Threshold):
             m._passthrough = False
         if isinstance(m, ConcatTable):

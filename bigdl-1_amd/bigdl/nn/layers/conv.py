@@ -134,6 +134,9 @@ class SpatialConvolution(TensorModule):
     #: gradient added to this conv's gradInput in the dgrad epilogue (set by a fused residual
     #: ConcatTable for the first conv of a block: the branch/shortcut gradient sum)
     _grad_residual = None
+    #: BN (+fused ReLU) whose output this conv consumes: the dgrad epilogue applies its ReLU mask
+    #: and produces its backward reductions (set by bigdl.nn.fusion)
+    _bn_bwd_target = None
 
     def _stats_consumer(self, x):
         """The training BN that will consume this conv's output (fusion), if the epilogue can
@@ -179,9 +182,19 @@ class SpatialConvolution(TensorModule):
         self._grad_residual = None
         pt, pb, pl, pr = pads
         fuse_res = res is not None and pt == pb and pl == pr and self.format == "NCHW" and batched
+        bn = self._bn_bwd_target
+        bn_fuse = None
+        if (bn is not None and need_input and res is None and pt == pb and pl == pr and self.format == "NCHW"
+                and batched and gy.is_cuda and bn.train and bn._fused_relu and not getattr(bn, "_sync", False)
+                and bn._coef is not None and bn._last_input is not None
+                and config.get_property("bigdl.fusion.bnbwd")):
+            C_ = bn._coef.numel() // 2
+            bn_fuse = {"x": bn._last_input, "scale": bn._coef[:C_], "shift": bn._coef[C_:], "mean": bn.saveMean}
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                  self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0,
-                                 residual=to_device_layout(res) if fuse_res else None)
+                                 residual=to_device_layout(res) if fuse_res else None, bn_fuse=bn_fuse)
+        if bn_fuse is not None and "partial" in bn_fuse and gi is not None:
+            bn._pending_grad = (gi.data_ptr(), bn_fuse["partial"], bn_fuse["G"])
         if acc and own_bias and not same_scale and self.scale_b != 0:
             self.gradBias.add_(gy.float().sum((0, 2, 3)), alpha=self.scale_b)
         if need_input and gi is not None:

@@ -101,6 +101,11 @@ class BatchNormalization(TensorModule):
     _bias_producer = None
     #: (data_ptr, shape, partials, G) left by the producing conv's epilogue for the next forward
     _pending_stats = None
+    #: forward scale/shift (2C fp32) of the last training forward, and its input (device layout)
+    _coef = None
+    _last_input = None
+    #: (gm data_ptr, partials, G) left by the consuming conv's dgrad epilogue for this backward
+    _pending_grad = None
 
     def _in_bias(self):
         p = self._bias_producer
@@ -137,16 +142,21 @@ class BatchNormalization(TensorModule):
                 y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib)
             else:
                 r = NotImplemented
+                C_ = x.shape[1]
+                coef = self._coef
+                if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
+                    coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
                 ps, self._pending_stats = self._pending_stats, None
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
-                        relu=relu, residual=residual, in_bias=ib)
+                        relu=relu, residual=residual, in_bias=ib, coef_out=coef)
                 if r is NotImplemented:
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
                                                     self.momentum, self.eps, relu=relu, residual=residual,
-                                                    in_bias=ib)
+                                                    in_bias=ib, coef_out=coef)
                 y, mean, invstd = r
+                self._last_input = x
             self.saveMean, self.saveStd = mean, invstd
         else:
             y = ops.batchnorm_forward_infer(x, g, b, self.runningMean, self.runningVar, self.eps, relu=False,
@@ -197,6 +207,17 @@ class BatchNormalization(TensorModule):
                 gres = gy * (y > 0).to(gy.dtype) if relu else gy
         else:
             same = self.scale_w == self.scale_b
+            pg, self._pending_grad = self._pending_grad, None
+            if pg is not None and pg[0] == gy.data_ptr() and relu and not want_gres and same:
+                gi = ops.native_ops.batchnorm_backward_partials(
+                    gy, x, g, self.saveMean, self.saveStd, pg[1], pg[2], need_input=need_input,
+                    gg_acc=self.gradWeight if (acc and self.affine) else None,
+                    gb_acc=self.gradBias if (acc and self.affine) else None,
+                    scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
+                if gi is not NotImplemented:
+                    if gi is not None and input.dim() == 1:
+                        gi = gi.reshape(input.shape)
+                    return gi
             gi, gres = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=relu,
                                               need_input=need_input,
                                               gg_acc=self.gradWeight if (acc and self.affine) else None,

@@ -438,3 +438,21 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
   }
   BIGDL_CHECK_LAUNCH();
 }
+
+// Backward from partials produced by the consuming conv's dgrad epilogue (Σg, Σg·(x − mean) of
+// the already ReLU-masked gradient gm): finalize + apply only — the reduce pass over (gy, x, y)
+// is gone and the apply no longer reads y.
+BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
+                                       const float* mean, const float* invstd, float* ggamma, float* gbeta,
+                                       float gscale, float* cbias, float cbscale, const float* partial, int G,
+                                       float* coef, hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, M, C, gamma, mean, invstd,
+                     ggamma, gbeta, gscale, cbias, cbscale, coef);
+  if (gx) {
+    int grid = apply_grid(M, C);
+    hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,
+                       (const bf16_t*)x, (const bf16_t*)nullptr, (bf16_t*)gx, (bf16_t*)nullptr, M, C, coef);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

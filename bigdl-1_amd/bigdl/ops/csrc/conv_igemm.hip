@@ -38,6 +38,13 @@ struct ConvParams {
   // optional output scatter (sub-pixel strided dgrad): output pixel (n, p, q) is stored at pixel
   // (n, p·osh + ooh, q·osw + oow) of a [Nb][oH][oW][K] tensor
   int scatter, osh, osw, ooh, oow, oH, oW;
+  // optional fused BatchNorm-backward prologue for the BN (+ReLU) that produced this dgrad's
+  // input gradient target: g ← g · [bnx·sc + sh > 0] (the ReLU mask recomputed from the BN input
+  // and its forward coefficients), and per-row-tile partials Σg, Σg·(bnx − mean) into `stats`
+  const bf16_t* bnx;
+  const float* bn_sc;
+  const float* bn_sh;
+  const float* bn_mean;
 };
 
 constexpr int BM = 128;
@@ -277,6 +284,15 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
   const bool full = n + 8 <= p.K;
+  float bsc[8], bsh[8], bmu[8];
+  if (p.bnx && full) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = p.bn_sc[n + e];
+      bsh[e] = p.bn_sh[n + e];
+      bmu[e] = p.bn_mean[n + e];
+    }
+  }
 #pragma unroll 2
   for (int r = rr; r < BM; r += RPP) {
     const int m = m0 + r;
@@ -288,7 +304,28 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       const int pp = pq / p.Q, qq = pq - pp * p.Q;
       off = ((size_t)(nimg * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow) * p.K + n;
     }
-    if (full) {
+    if (full && p.bnx) {
+      float g[8], xv[8];
+      load8(&et[r * LDR + cc * 8], g);
+      load8(p.bnx + off, xv);
+      uint32_t w4[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool live = fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
+        g[e] = live ? g[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(g[2 * e]) | ((uint32_t)f2bf(g[2 * e + 1]) << 16);
+      *reinterpret_cast<uint4*>(p.y + off) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(w4[e] << 16), b = __uint_as_float(w4[e] & 0xFFFF0000u);
+        s8[2 * e] += a;
+        q8[2 * e] = fmaf(a, xv[2 * e] - bmu[2 * e], q8[2 * e]);
+        s8[2 * e + 1] += b;
+        q8[2 * e + 1] = fmaf(b, xv[2 * e + 1] - bmu[2 * e + 1], q8[2 * e + 1]);
+      }
+    } else if (full) {
       uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + cc * 8]);
       if (p.res || p.relu) {
         float v[8];
@@ -363,10 +400,11 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 // ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
 BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + BM - 1) / BM); }
 
-BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const float* bias, const void* res, void* y,
-                                        float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P,
-                                        int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh,
-                                        int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
+BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                     float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                     int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
+                                     int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
+                                     const float* bn_sh, const float* bn_mean, hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
@@ -389,6 +427,12 @@ BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const floa
   p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
   p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
   if (p.scatter && stats) return (int)hipErrorInvalidValue;
+  p.bnx = (const bf16_t*)bnx;
+  p.bn_sc = bn_sc;
+  p.bn_sh = bn_sh;
+  p.bn_mean = bn_mean;
+  if (bnx && (!stats || !bn_sc || !bn_sh || !bn_mean || res || relu || bias || p.scatter))
+    return (int)hipErrorInvalidValue;
   const int BN = K <= 64 ? 64 : 128;
   p.tiles_n = (K + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
@@ -404,6 +448,14 @@ BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const floa
   else
     hipLaunchKernelGGL((k_conv_fwd<128, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                        float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P,
+                                        int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh,
+                                        int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
+  return bigdl_conv_fwd_full(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
+                             osw, ooh, oow, oH, oW, nullptr, nullptr, nullptr, nullptr, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,

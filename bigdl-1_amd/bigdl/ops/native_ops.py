@@ -108,7 +108,7 @@ def _f32vec(t, C_):
 
 @register("batchnorm_forward_train")
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
-                            in_bias=None):
+                            in_bias=None, coef_out=None):
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -121,7 +121,7 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     lib = _lib()
     G = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
     ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
-    coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
+    coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
     mean = torch.empty(C_, dtype=_f32, device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
@@ -131,8 +131,12 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     return y, mean, invstd
 
 
+def _coef_ok(t, C_):
+    return t is not None and t.dtype == _f32 and t.is_contiguous() and t.numel() >= 2 * C_ and t.is_cuda
+
+
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
-                                    relu=False, residual=None, in_bias=None):
+                                    relu=False, residual=None, in_bias=None, coef_out=None):
     """Training BN whose statistics were produced by the preceding conv's epilogue
     (:func:`conv2d_forward_stats`): finalize + apply only."""
     rc = _rows_c(x)
@@ -146,7 +150,7 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
                                  residual.dtype != _bf16 or not _al16(residual)):
         return NotImplemented
-    coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
+    coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
     mean = torch.empty(C_, dtype=_f32, device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
@@ -156,6 +160,26 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
                                              C.c_int(G), ptr(coef), C.c_int(1 if relu else 0), _s()),
           "bn_fwd_train_partials")
     return y, mean, invstd
+
+
+def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G, need_input=True, gg_acc=None,
+                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0):
+    """BN backward whose reductions came from the consumer conv's dgrad epilogue; ``gm`` is the
+    already ReLU-masked gradient.  Returns gradInput (or None) / NotImplemented."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not _bn_ok(x, C_) or gm.dtype != _bf16 or gm.shape != x.shape or gm.stride() != x.stride() or not _al16(gm):
+        return NotImplemented
+    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc)):
+        return NotImplemented
+    coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
+    gx = torch.empty_like(x) if need_input else None
+    check(_lib().bigdl_bn_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
+                                       ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
+                                       _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef), _s()), "bn_bwd_partials")
+    return gx
 
 
 @register("batchnorm_forward_infer")
@@ -325,7 +349,7 @@ def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True)
 
 
-def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None):
+def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
     """stride-1 backward-data as a forward conv of gy with the flipped, transposed kernel; an optional
     ``residual`` gradient (same shape as x) is summed in the epilogue."""
     N_, C_, H, W = x_shape
@@ -344,6 +368,17 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None):
                                      and _al16(residual)):
         return None
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    if bn_fuse is not None and residual is None and C_ % 8 == 0:
+        bx, sc, sh, mu = bn_fuse["x"], bn_fuse["scale"], bn_fuse["shift"], bn_fuse["mean"]
+        if (bx.shape == (N_, C_, H, W) and bx.dtype == _bf16 and bx.is_contiguous(memory_format=torch.channels_last)
+                and _al16(bx) and all(_f32vec(t, C_) for t in (sc, sh, mu))):
+            G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
+            part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)
+            check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(None), ptr(gx), ptr(part), N_, P, Q, K,
+                                             C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, 1, 1, 0, 0,
+                                             H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), _s()), "conv_dgrad_bnbwd")
+            bn_fuse["partial"], bn_fuse["G"] = part, G
+            return gx
     check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
                                    S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, _s()), "conv_dgrad")
     return gx
@@ -471,7 +506,7 @@ def _wgrad_blocks(M, C_, K):
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                    scale=1.0, residual=None):
+                    scale=1.0, residual=None, bn_fuse=None):
     if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
         return NotImplemented
     if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):
@@ -485,7 +520,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     if need_input:
         res_done = False
         if stride == (1, 1) or tuple(stride) == (1, 1):
-            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation, residual)
+            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation, residual, bn_fuse)
             res_done = gi is not None
             if gi is None and residual is not None:
                 gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)

@@ -46,7 +46,7 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
 
 
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
-                    gb_acc=None, scale=1.0, residual=None):
+                    gb_acc=None, scale=1.0, residual=None, bn_fuse=None):
     """``SpatialConvolution.updateGradInput`` + ``accGradParameters`` (``:364-505``).
 
     Returns gradInput (or None); ACCUMULATES ``scale·dW`` into ``gw_acc`` (O, I/g, kH, kW view,
@@ -73,7 +73,7 @@ def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups
 
 # ------------------------------------------------------------------------- batch norm
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
-                            in_bias=None):
+                            in_bias=None, coef_out=None):
     """Training BN (``SpatialBatchNormalization.updateOutputNCHWTrainFloat``, ``:1211``).
 
     Normalises with the biased variance, updates ``runningVar`` with the UNBIASED variance and
@@ -96,6 +96,10 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     shape = [1, C] + [1] * (x.dim() - 2)
     g = gamma.float().view(shape) if gamma is not None else 1.0
     bb = beta.float().view(shape) if beta is not None else 0.0
+    if coef_out is not None:
+        sc = invstd * (gamma.float() if gamma is not None else 1.0)
+        coef_out[:C].copy_(sc)
+        coef_out[C:2 * C].copy_((beta.float() if beta is not None else 0.0) - mean * sc)
     y = (xf - mean.view(shape)) * invstd.view(shape) * g + bb
     if residual is not None:
         y = y + residual.float()

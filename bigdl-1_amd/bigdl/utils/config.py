@@ -45,6 +45,7 @@ _REGISTRY = {
     "bigdl.fusion.convrelu": (bool, True, "fuse conv + ReLU"),
     "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
     "bigdl.fusion.convstats": (bool, True, "conv epilogue emits the following training BN's statistics"),
+    "bigdl.fusion.bnbwd": (bool, True, "dgrad epilogue applies the producing BN's ReLU mask and its backward reductions"),
     # logging
     "bigdl.utils.LoggerFilter.disable": (bool, False, "disable log redirect"),
     "bigdl.utils.LoggerFilter.logFile": (str, "bigdl.log", "log file"),
