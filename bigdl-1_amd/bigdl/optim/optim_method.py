@@ -339,12 +339,40 @@ class SGD(OptimMethod):
         if self.momentum != 0:
             self._state_tensor("dfdx", x)
 
+    #: per-element vectors in the coordinate space of the ``x`` the optimizer passes (arena slice or
+    #: rank shard), installed by the optimizer: folded L2-regularizer decays, remapped user vectors
+    _reg_decay = None
+    _space_wds = None
+    _space_lrs = None
+
+    def _decays(self, dev, lo=None, hi=None):
+        def sl(t):
+            return t if (t is None or lo is None) else t[lo:hi]
+        wds = self._space_wds if self._space_wds is not None else (
+            self.weightDecays.to(dev) if self.weightDecays is not None else None)
+        lrs = self._space_lrs if self._space_lrs is not None else (
+            self.learningRates.to(dev) if self.learningRates is not None else None)
+        wds, lrs, reg = sl(wds), sl(lrs), sl(self._reg_decay)
+        # SGD.scala:79-93: a scalar weightDecay wins; the per-element weightDecays apply only when
+        # the scalar is 0
+        wd = self.weightDecay
+        if reg is not None:
+            key = (wd, lo, hi, None if wds is None else wds.data_ptr())
+            cache = getattr(self, "_eff_cache", None)
+            if cache is None or cache[0] != key:
+                eff = reg + (wd if wd != 0 else (wds if wds is not None else 0.0))
+                self._eff_cache = cache = (key, eff)
+            return lrs, 1.0, cache[1]
+        if wd != 0:
+            return lrs, wd, None
+        if wds is not None:
+            return lrs, 1.0, wds
+        return lrs, 0.0, None
+
     def apply_update(self, x, g, lo, hi, shadow=None):
         clr = self.learningRateSchedule.currentRate
         buf = self.state["dfdx"][lo:hi] if self.momentum != 0 else None
-        lrs = self.learningRates.to(x.device)[lo:hi] if self.learningRates is not None else None
-        wds = self.weightDecays.to(x.device)[lo:hi] if self.weightDecays is not None else None
-        wd = self.weightDecay if not (self.weightDecay == 0 and wds is not None) else 1.0
+        lrs, wd, wds = self._decays(x.device, lo, hi)
         ops.sgd_step(x[lo:hi], g[lo:hi], buf, -clr, self.momentum, self.dampening, wd, self.nesterov, self._first,
                      self.grad_scale, shadow, lrs, wds)
 
@@ -359,14 +387,16 @@ class SGD(OptimMethod):
         first = "dfdx" not in self.state or not isinstance(self.state.get("dfdx"), torch.Tensor) or \
             self.state["dfdx"].shape != x.shape
         buf = self._state_tensor("dfdx", x) if self.momentum != 0 else None
-        lrs = self.learningRates.to(x.device) if self.learningRates is not None else None
-        wds = self.weightDecays.to(x.device) if self.weightDecays is not None else None
-        wd = self.weightDecay
-        if wd == 0 and wds is not None:
-            wd = 1.0
+        lrs, wd, wds = self._decays(x.device)
         ops.sgd_step(x, dfdx, buf, -clr, self.momentum, self.dampening, wd, self.nesterov, first,
                      self.grad_scale, self.shadow, lrs, wds)
         return x, [fx]
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        for k in ("_reg_decay", "_space_wds", "_space_lrs", "_eff_cache"):
+            d.pop(k, None)
+        return d
 
 
 # ----------------------------------------------------------------------------------------- Adam family

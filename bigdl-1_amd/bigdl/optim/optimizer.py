@@ -249,6 +249,38 @@ class BaseOptimizer:
         for name, meth in self.optim_methods.items():
             for k in ("epoch", "neval"):
                 meth.state.setdefault(k, self.state[k])
+        reg = self._fold_regularizers()
+        if reg is not None:
+            for name, meth in self.optim_methods.items():
+                off, n = self._method_slices[name]
+                meth._reg_decay = reg[off:off + n]
+
+    def _fold_regularizers(self):
+        """Fold every pure-L2 ``wRegularizer``/``bRegularizer`` (``Regularizer.scala``: g += λ·w
+        inside accGradParameters) into a per-element decay vector over the arena, applied by the
+        fused SGD kernel — one elementwise pass per layer per step less.  Only when every
+        OptimMethod is SGD (the kernel that takes per-element decays).  Returns the vector or None."""
+        from .optim_method import SGD
+        from .regularizer import L1L2Regularizer
+        for mod in self.model.flattened_modules():  # undo a previous optimizer's folding
+            for r in (mod.wRegularizer, mod.bRegularizer):
+                if isinstance(r, L1L2Regularizer):
+                    r._folded = False
+        if self.flat is None or not config.get_property("bigdl.optim.foldRegularizers"):
+            return None
+        if not all(type(m) is SGD for m in self.optim_methods.values()):
+            return None
+        reg_full = None
+        for (m, wname, gname, off, n, shape) in self.flat.slices:
+            reg = m.wRegularizer if wname == "weight" else (m.bRegularizer if wname == "bias" else None)
+            if not (isinstance(reg, L1L2Regularizer) and reg.l1 == 0 and reg.isRegualrized):
+                continue
+            if reg_full is None:
+                reg_full = torch.zeros(self.flat.numel, dtype=torch.float32, device=self.flat.weight.device)
+            scale = m.scale_b if wname == "bias" else m.scale_w
+            reg_full[off:off + n] = reg.l2 * scale
+            reg._folded = True
+        return reg_full
 
     def _compute_method_slices(self):
         """Map each OptimMethod to the (offset, length) of its sub-module's parameters in the

@@ -27,8 +27,11 @@ class L1L2Regularizer(Regularizer):
         super().__init__()
         self.l1, self.l2 = l1, l2
 
+    #: set by an optimizer that folded this L2 term into its fused update kernel (per-element decay)
+    _folded = False
+
     def accRegularization(self, p, g, scale):
-        if not self.isRegualrized:
+        if not self.isRegualrized or self._folded:
             return
         with torch.no_grad():
             if self.l1 != 0:

@@ -131,6 +131,32 @@ class DistriOptimizer(BaseOptimizer):
             meth.grad_scale = 1.0 / W
             for k in ("epoch", "neval"):
                 meth.state.setdefault(k, self.state[k])
+        # per-element vectors (folded L2 regularizers, user lr/decay vectors) in the coordinate
+        # space the method's update sees: arena slices (replicated) or this rank's shard (sharded)
+        reg_full = self._fold_regularizers()
+        for name, meth in self.optim_methods.items():
+            off, n = self._method_slices[name]
+            user_w = getattr(meth, "weightDecays", None)
+            user_l = getattr(meth, "learningRates", None)
+            if not self.sharded:
+                if reg_full is not None:
+                    meth._reg_decay = reg_full[off:off + n]
+                continue
+            def to_shard(vec, base_off):
+                out = torch.zeros(soff, dtype=torch.float32, device=dev)
+                for b in self.buckets:
+                    per = b.shi - b.slo
+                    own_lo = b.lo + self.rank * per
+                    lo, hi = max(base_off, own_lo), min(base_off + vec.numel(), own_lo + per)
+                    if lo < hi:
+                        out[b.slo + (lo - own_lo):b.slo + (hi - own_lo)] = vec[lo - base_off:hi - base_off].to(dev)
+                return out
+            if reg_full is not None:
+                meth._reg_decay = to_shard(reg_full, 0)
+            if isinstance(user_w, torch.Tensor) and user_w.numel() == n:
+                meth._space_wds = to_shard(user_w.float(), off)
+            if isinstance(user_l, torch.Tensor) and user_l.numel() == n:
+                meth._space_lrs = to_shard(user_l.float(), off)
         # module → buckets map, hooks
         self._mod_buckets = {}
         for (mod, w, g, off, n, shape) in self.flat.slices:

@@ -38,6 +38,7 @@ _REGISTRY = {
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
+    "bigdl.optim.foldRegularizers": (bool, True, "apply pure-L2 layer regularizers inside the fused SGD update"),
     # fusion flags (bigdl.mkldnn.fusion.* equivalents, nn/mkldnn/Fusion.scala:34)
     "bigdl.fusion": (bool, True, "enable layer fusion"),
     "bigdl.fusion.convbn": (bool, True, "fold BN into conv for inference"),
