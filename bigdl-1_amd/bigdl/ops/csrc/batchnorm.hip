@@ -246,14 +246,61 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   BIGDL_CHECK_LAUNCH();
 }
 
+// Pre-fold of many per-row-tile partials (conv-epilogue statistics: G up to M/128) into S ≤ G/128
+// rows, so the per-channel finalize reads a short column instead of a latency-bound 6k-long one.
+// grid (ceil(C/64), S), 256 threads = 64 channels × 4 row groups; rows [sy·R, sy·R + R) per block.
+__global__ void __launch_bounds__(256) k_bn_fold_partials(const float* __restrict__ partial, int G, int C, int R,
+                                                          int S, float* __restrict__ out) {
+  __shared__ float red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int g0 = blockIdx.y * R;
+  int g1 = g0 + R;
+  if (g1 > G) g1 = G;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = g0 + ty; g < g1; g += 4) {
+      a += partial[(size_t)g * C + c];
+      b += partial[(size_t)(G + g) * C + c];
+    }
+  }
+  red[0][ty][tx] = a;
+  red[1][ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    out[(size_t)blockIdx.y * C + c] = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+    out[(size_t)(S + blockIdx.y) * C + c] = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+  }
+}
+
+static constexpr int kFoldRows = 128;
+
+// floats of scratch bigdl_bn_*_partials needs for G partials of C channels (0: no pre-fold)
+BIGDL_EXPORT long long bigdl_bn_fold_scratch(int G, int C) {
+  if (G <= 512) return 0;
+  const int S = (G + kFoldRows - 1) / kFoldRows;
+  return 2LL * S * C;
+}
+
+static const float* maybe_fold(const float* partial, int& G, int C, float* scratch, hipStream_t s) {
+  if (G <= 512 || !scratch) return partial;
+  const int S = (G + kFoldRows - 1) / kFoldRows;
+  hipLaunchKernelGGL(k_bn_fold_partials, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, G, C, kFoldRows, S,
+                     scratch);
+  G = S;
+  return scratch;
+}
+
 // Training forward from precomputed partials (the producing conv's epilogue wrote Σy, Σy² per row
 // tile, unshifted): finalize + apply only — the stats pass over x is gone.
 BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, void* y, long long M, int C,
                                              const float* gamma, const float* beta, const float* in_bias,
                                              float* run_mean, float* run_var, float momentum, float eps,
                                              float* save_mean, float* save_invstd, const float* partial, int G,
-                                             float* coef, int relu, hipStream_t s) {
+                                             float* coef, int relu, float* scratch, hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  partial = maybe_fold(partial, G, C, scratch, s);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, partial, G, M, C,
                      gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   int grid = apply_grid(M, C);
@@ -445,8 +492,9 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
 BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
                                        const float* mean, const float* invstd, float* ggamma, float* gbeta,
                                        float gscale, float* cbias, float cbscale, const float* partial, int G,
-                                       float* coef, hipStream_t s) {
+                                       float* coef, float* scratch, hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  partial = maybe_fold(partial, G, C, scratch, s);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, M, C, gamma, mean, invstd,
                      ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {

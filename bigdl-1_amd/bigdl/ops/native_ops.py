@@ -131,6 +131,13 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     return y, mean, invstd
 
 
+def _fold_scratch(G, C_, dev):
+    f = _lib().bigdl_bn_fold_scratch
+    f.restype = C.c_longlong
+    n = f(C.c_int(G), C.c_int(C_))
+    return torch.empty(n, dtype=_f32, device=dev) if n > 0 else None
+
+
 def _coef_ok(t, C_):
     return t is not None and t.dtype == _f32 and t.is_contiguous() and t.numel() >= 2 * C_ and t.is_cuda
 
@@ -157,7 +164,8 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     check(_lib().bigdl_bn_fwd_train_partials(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
                                              ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
                                              _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
-                                             C.c_int(G), ptr(coef), C.c_int(1 if relu else 0), _s()),
+                                             C.c_int(G), ptr(coef), C.c_int(1 if relu else 0),
+                                             ptr(_fold_scratch(G, C_, x.device)), _s()),
           "bn_fwd_train_partials")
     return y, mean, invstd
 
@@ -178,7 +186,8 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
     gx = torch.empty_like(x) if need_input else None
     check(_lib().bigdl_bn_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
                                        ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
-                                       _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef), _s()), "bn_bwd_partials")
+                                       _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
+                                       ptr(_fold_scratch(G, C_, x.device)), _s()), "bn_bwd_partials")
     return gx
 
 
@@ -715,3 +724,53 @@ def image_crop_flip_norm(src, oy, ox, flip, out_h, out_w, mean, std, to_rgb, out
                                             C.c_int(1 if to_rgb else 0), ptr(out),
                                             C.c_int(1 if out_dtype == _bf16 else 0), _s()), "image_crop_flip_norm")
     return out
+
+
+# ------------------------------------------------------------------------------------------------ pooling (K10)
+def _pool_out(size, k, s, p, ceil_mode):
+    if ceil_mode:
+        o = -(-(size + 2 * p - k) // s) + 1
+        if (o - 1) * s >= size + p:
+            o -= 1
+    else:
+        o = (size + 2 * p - k) // s + 1
+    return o
+
+
+class _Int8Idx:
+    """argmax offsets from the native max-pool forward (int8, NHWC) — only the native backward reads it."""
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+@register("maxpool2d_forward")
+def maxpool2d_forward(x, k, s, p, ceil_mode):
+    if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if C_ % 8 or k[0] * k[1] > 127 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
+        return NotImplemented
+    P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
+    Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
+    y = torch.empty((N_, C_, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    idx = torch.empty((N_, P, Q, C_), dtype=torch.int8, device=x.device)
+    check(_lib().bigdl_maxpool_fwd(ptr(x), ptr(y), ptr(idx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+                                   _s()), "maxpool_fwd")
+    return y, _Int8Idx(idx)
+
+
+@register("maxpool2d_backward")
+def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
+    if not isinstance(idx, _Int8Idx):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    P, Q = gy.shape[2], gy.shape[3]
+    if gy.dtype != _bf16:
+        gy = gy.to(_bf16)
+    gy = gy.contiguous(memory_format=torch.channels_last)
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_maxpool_bwd(ptr(gy), ptr(idx.t), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0],
+                                   p[1], _s()), "maxpool_bwd")
+    return gx

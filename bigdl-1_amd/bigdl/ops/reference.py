@@ -158,6 +158,8 @@ def maxpool2d_forward(x, k, s, p, ceil_mode):
 
 
 def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
+    if hasattr(idx, "t") and not isinstance(idx, torch.Tensor):  # native int8 argmax → recompute
+        _, idx = maxpool2d_forward(x, k, s, p, ceil_mode)
     return aten.max_pool2d_with_indices_backward(gy, x, list(k), list(s), list(p), [1, 1], ceil_mode, idx)
 
 

@@ -351,3 +351,19 @@ def test_strided_dgrad_subpixel(case):
     res = _cl(torch.randn_like(x))
     gi2 = N.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (1, 1), 1, True, None, None, 0.0, residual=res)
     torch.testing.assert_close(gi2.float(), xr.grad + res.float(), rtol=3e-2, atol=4e-2)
+
+
+@pytest.mark.parametrize("cfg", [((3, 3), (2, 2), (1, 1), False), ((2, 2), (2, 2), (0, 0), True),
+                                 ((3, 3), (2, 2), (0, 0), True), ((3, 3), (1, 1), (1, 1), False)])
+def test_maxpool_native(cfg):
+    N = _native()
+    from bigdl.ops import reference as R
+    k, s, p, ceil = cfg
+    x = _cl(torch.randn(2, 16, 13, 11, device=dev).bfloat16())
+    y, idx = N.maxpool2d_forward(x, k, s, p, ceil)
+    yr, idr = R.maxpool2d_forward(x.float(), k, s, p, ceil)
+    torch.testing.assert_close(y.float(), yr)
+    gy = _cl(torch.randn_like(yr).bfloat16())
+    gx = N.maxpool2d_backward(gy, x, idx, k, s, p, ceil)
+    gr = R.maxpool2d_backward(gy.float(), x.float(), idr, k, s, p, ceil)
+    torch.testing.assert_close(gx.float(), gr, rtol=1e-2, atol=1e-2)
