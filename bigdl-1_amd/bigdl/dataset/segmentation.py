@@ -103,15 +103,12 @@ class MaskUtils:
         m = torch.as_tensor(mask)
         h, w = m.shape
         flat = (m.t().reshape(-1) > 0).to(torch.int8).numpy()
-        counts = []
-        prev, run = 0, 0
-        for v in flat:
-            if v != prev:
-                counts.append(run)
-                run = 0
-                prev = v
-            run += 1
-        counts.append(run)
+        # run lengths from the change points (column-major, first run counts zeros)
+        edges = np.flatnonzero(np.diff(flat)) + 1
+        bounds = np.concatenate([[0], edges, [flat.size]])
+        counts = np.diff(bounds).tolist()
+        if flat.size and flat[0] == 1:
+            counts = [0] + counts
         return RLEMasks(counts, h, w)
 
     binaryToRLE = binary_to_rle

@@ -6,3 +6,4 @@ from .rnn import PTBModel, SimpleRNN  # noqa: F401
 from .inception import (Inception_Layer_v1, Inception_Layer_v2, Inception_v1, Inception_v1_NoAuxClassifier,  # noqa: F401
                         Inception_v2, Inception_v2_NoAuxClassifier)
 from .autoencoder import Autoencoder  # noqa: F401
+from .maskrcnn import MaskRCNN, MaskRCNNParams  # noqa: F401

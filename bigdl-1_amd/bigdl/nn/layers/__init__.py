@@ -11,3 +11,5 @@ from .dropout import *  # noqa: F401,F403
 from .embedding import *  # noqa: F401,F403
 from .recurrent import *  # noqa: F401,F403
 from .attention import Attention, FeedForwardNetwork, Transformer, SequenceBeamSearch  # noqa: F401
+from .detection import (Anchor, Nms, Proposal, RegionProposal, PriorBox, DetectionOutputSSD,  # noqa: F401
+                        DetectionOutputFrcnn, Pooler, FPN, BoxHead, MaskHead, nms, box_iou, roi_align)

@@ -243,10 +243,78 @@ class RoiPooling(AutogradModule):
         return torch.stack(outs, 0)
 
 
-class RoiAlign(AutogradModule):
-    """Bilinear ROI align (``RoiAlign.scala``): rois (K, 4) with batch index from a second input."""
+def roi_align(data: torch.Tensor, rois: torch.Tensor, spatial_scale: float, out_h: int, out_w: int,
+              sampling_ratio: int = 2, aligned: bool = True, chunk: int = 256) -> torch.Tensor:
+    """Bilinear ROI align over NCHW ``data`` for ``rois [K, 5]`` (batch index, x1, y1, x2, y2),
+    averaging ``sampling_ratio²`` samples per bin (``RoiAlign.scala``).  Gather-based and batched
+    over ROIs (chunks of ``chunk`` to bound the K·S·C sample tensor); differentiable via autograd."""
+    K = rois.shape[0]
+    N, C, H, W = data.shape
+    if K == 0:
+        return data.new_zeros((0, C, out_h, out_w))
+    off = 0.5 if aligned else 0.0
+    if sampling_ratio <= 0:
+        # adaptive grid: ceil(roi_size / bins) samples per bin, per ROI — group ROIs sharing a grid
+        r = rois.float()
+        rw = ((r[:, 3] - r[:, 1]) * spatial_scale).clamp_min(0.0 if aligned else 1.0)
+        rh = ((r[:, 4] - r[:, 2]) * spatial_scale).clamp_min(0.0 if aligned else 1.0)
+        gh = torch.ceil(rh / out_h).clamp_min(1).long()
+        gw = torch.ceil(rw / out_w).clamp_min(1).long()
+        out = data.new_zeros((K, C, out_h, out_w))
+        for key in torch.unique(torch.stack([gh, gw], 1), dim=0).tolist():
+            idx = torch.nonzero((gh == key[0]) & (gw == key[1])).flatten()
+            out[idx] = _roi_align_grid(data, rois[idx], spatial_scale, out_h, out_w, key[0], key[1], off,
+                                       aligned, chunk).to(data.dtype)
+        return out
+    sr = int(sampling_ratio)
+    return _roi_align_grid(data, rois, spatial_scale, out_h, out_w, sr, sr, off, aligned, chunk).to(data.dtype)
 
-    def __init__(self, spatial_scale, sampling_ratio, pooled_h, pooled_w, mode="avg", aligned=True,
+
+def _roi_align_grid(data, rois, spatial_scale, out_h, out_w, srh, srw, off, aligned, chunk):
+    K = rois.shape[0]
+    N, C, H, W = data.shape
+    d = data.permute(0, 2, 3, 1).float()  # N, H, W, C
+    gy = (torch.arange(out_h * srh, device=data.device, dtype=torch.float32) + 0.5) / srh
+    gx = (torch.arange(out_w * srw, device=data.device, dtype=torch.float32) + 0.5) / srw
+    outs = []
+    for s in range(0, K, chunk):
+        r = rois[s:s + chunk].float()
+        k = r.shape[0]
+        bi = r[:, 0].long()
+        x1 = r[:, 1] * spatial_scale - off
+        y1 = r[:, 2] * spatial_scale - off
+        x2 = r[:, 3] * spatial_scale - off
+        y2 = r[:, 4] * spatial_scale - off
+        rw = (x2 - x1) if aligned else (x2 - x1).clamp_min(1.0)
+        rh = (y2 - y1) if aligned else (y2 - y1).clamp_min(1.0)
+        ys = y1[:, None] + gy[None, :] * (rh / out_h)[:, None]  # k, oh·sr
+        xs = x1[:, None] + gx[None, :] * (rw / out_w)[:, None]
+        Y = ys[:, :, None].expand(k, out_h * srh, out_w * srw)
+        X = xs[:, None, :].expand(k, out_h * srh, out_w * srw)
+        valid = (Y >= -1.0) & (Y <= H) & (X >= -1.0) & (X <= W)
+        Y = Y.clamp(0, H - 1)
+        X = X.clamp(0, W - 1)
+        y0 = Y.floor().long()
+        x0 = X.floor().long()
+        y1i = (y0 + 1).clamp_max(H - 1)
+        x1i = (x0 + 1).clamp_max(W - 1)
+        ly, lx = Y - y0, X - x0
+        hy, hx = 1 - ly, 1 - lx
+        b = bi[:, None, None].expand_as(y0)
+        v = (d[b, y0, x0] * (hy * hx)[..., None] + d[b, y0, x1i] * (hy * lx)[..., None] +
+             d[b, y1i, x0] * (ly * hx)[..., None] + d[b, y1i, x1i] * (ly * lx)[..., None])
+        v = v * valid[..., None]
+        v = v.view(k, out_h, srh, out_w, srw, C).mean((2, 4))
+        outs.append(v.permute(0, 3, 1, 2))
+    return torch.cat(outs)
+
+
+class RoiAlign(AutogradModule):
+    """Bilinear ROI align (``RoiAlign.scala:45``): Table(data NCHW, rois (K, 4) on image 0 or (K, 5)
+    with a leading batch index); ``aligned=False`` is the reference's sampling (no half-pixel shift,
+    ROI sizes clamped to ≥1); ``samplingRatio ≤ 0`` picks ceil(roi/bin) samples per bin."""
+
+    def __init__(self, spatial_scale, sampling_ratio, pooled_h, pooled_w, mode="avg", aligned=False,
                  bigdl_type="float"):
         super().__init__()
         self.spatialScale, self.samplingRatio = spatial_scale, sampling_ratio
@@ -256,21 +324,7 @@ class RoiAlign(AutogradModule):
         data, rois = x[1], x[2]
         if rois.shape[-1] == 4:
             rois = torch.cat([torch.zeros(rois.shape[0], 1, dtype=rois.dtype, device=rois.device), rois], 1)
-        off = 0.5 if self.aligned else 0.0
-        outs = []
-        sr = max(self.samplingRatio, 1)
-        for r in rois:
-            b = int(r[0])
-            x1, y1, x2, y2 = [float(v) * self.spatialScale - off for v in r[1:5]]
-            rw, rh = max(x2 - x1, 1e-6 if self.aligned else 1.0), max(y2 - y1, 1e-6 if self.aligned else 1.0)
-            ys = y1 + (torch.arange(self.pooledH * sr, device=data.device, dtype=torch.float32) + 0.5) * rh / (self.pooledH * sr)
-            xs = x1 + (torch.arange(self.pooledW * sr, device=data.device, dtype=torch.float32) + 0.5) * rw / (self.pooledW * sr)
-            gy, gx = torch.meshgrid(ys, xs, indexing="ij")
-            H, W = data.shape[2], data.shape[3]
-            grid = torch.stack([(gx + 0.5) / W * 2 - 1, (gy + 0.5) / H * 2 - 1], -1).unsqueeze(0)
-            samp = F.grid_sample(data[b:b + 1].float(), grid, mode="bilinear", align_corners=False)
-            outs.append(F.avg_pool2d(samp, sr)[0])
-        return torch.stack(outs, 0).to(data.dtype)
+        return roi_align(data, rois, self.spatialScale, self.pooledH, self.pooledW, self.samplingRatio, self.aligned)
 
 
 class UpSampling1D(AutogradModule):
