@@ -13,6 +13,9 @@ stay identical); matched modules get execution flags instead:
 * ResNet block tail ``ConcatTable(branch…BN, shortcut) → CAddTable → ReLU`` (``convsum``): the
   shortcut runs first and the branch's last BN computes ReLU(BN(x) + shortcut) in one pass; in
   backward the same kernel emits both the branch gradient and the masked gradient for the shortcut.
+* block tail → next block (``bnbwd``): the next block's first conv computes, in its dgrad
+  epilogue, (dgrad + shortcut gradient) · [block output > 0] and the tail BN's Σg, Σg·(x − mean),
+  so the tail BN backward is a single apply pass and the masked gradient IS the shortcut gradient.
 
 Each fusion removes one full read+write pass over an activation tensor from HBM.
 """
@@ -41,6 +44,7 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
     bnrelu = config.get_property("bigdl.fusion.bnrelu") if bnrelu is None else bnrelu
     convsum = config.get_property("bigdl.fusion.convsum") if convsum is None else convsum
     bnbwd = config.get_property("bigdl.fusion.bnbwd") if bnbwd is None else bnbwd
+    tails, heads = [], []
     for s in model.flattened_modules():
         if not isinstance(s, Sequential):
             continue
@@ -75,6 +79,16 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
             add._passthrough = True
             if relu is not None:
                 relu._passthrough = True
+                tails.append(bn)
+            first = br.modules[0]
+            if isinstance(first, SpatialConvolution) and len(br.modules) > 1:
+                heads.append(first)
+    # block tail → next block: the first conv of a fused block (whose dgrad epilogue already sums
+    # the shortcut gradient) also applies the previous tail's ReLU mask and produces that BN's
+    # backward reductions; the match is made at backward time by tensor identity
+    if bnbwd and tails:
+        for h in heads:
+            h._tail_candidates = tails
     return model
 
 
@@ -83,6 +97,7 @@ def unfuse(model):
         if isinstance(m, SpatialConvolution):
             m._bias_folded_into = None
             m._bn_bwd_target = None
+            m._tail_candidates = None
         if isinstance(m, BatchNormalization):
             m._bias_producer = None
             m._fused_relu = False

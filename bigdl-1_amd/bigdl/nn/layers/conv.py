@@ -137,6 +137,18 @@ class SpatialConvolution(TensorModule):
     #: BN (+fused ReLU) whose output this conv consumes: the dgrad epilogue applies its ReLU mask
     #: and produces its backward reductions (set by bigdl.nn.fusion)
     _bn_bwd_target = None
+    #: fused block-tail BNs (ReLU(BN(x) + shortcut)) whose output may be this conv's input: the
+    #: dgrad epilogue then also applies that ReLU mask and produces the tail BN's reductions
+    _tail_candidates = None
+
+    def _tail_target(self, x):
+        for bn in self._tail_candidates or ():
+            y = bn.output
+            if (isinstance(y, torch.Tensor) and y.data_ptr() == x.data_ptr() and y.shape == x.shape and bn.train
+                    and getattr(bn, "_last_relu", False) and not getattr(bn, "_sync", False)
+                    and bn._last_input is not None and bn._last_input.shape == x.shape):
+                return bn
+        return None
 
     def _stats_consumer(self, x):
         """The training BN that will consume this conv's output (fusion), if the epilogue can
@@ -190,6 +202,10 @@ class SpatialConvolution(TensorModule):
                 and config.get_property("bigdl.fusion.bnbwd")):
             C_ = bn._coef.numel() // 2
             bn_fuse = {"x": bn._last_input, "scale": bn._coef[:C_], "shift": bn._coef[C_:], "mean": bn.saveMean}
+        elif (fuse_res and self._tail_candidates and gy.is_cuda and config.get_property("bigdl.fusion.bnbwd")):
+            bn = self._tail_target(x)
+            if bn is not None:
+                bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output}
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                  self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0,
                                  residual=to_device_layout(res) if fuse_res else None, bn_fuse=bn_fuse)

@@ -208,7 +208,9 @@ class BatchNormalization(TensorModule):
         else:
             same = self.scale_w == self.scale_b
             pg, self._pending_grad = self._pending_grad, None
-            if pg is not None and pg[0] == gy.data_ptr() and relu and not want_gres and same:
+            if pg is not None and pg[0] == gy.data_ptr() and relu and same:
+                # gy is already ReLU-masked (by the consumer conv's dgrad epilogue), which is also
+                # exactly the gradient a fused residual shortcut receives
                 gi = ops.native_ops.batchnorm_backward_partials(
                     gy, x, g, self.saveMean, self.saveStd, pg[1], pg[2], need_input=need_input,
                     gg_acc=self.gradWeight if (acc and self.affine) else None,
@@ -217,7 +219,7 @@ class BatchNormalization(TensorModule):
                 if gi is not NotImplemented:
                     if gi is not None and input.dim() == 1:
                         gi = gi.reshape(input.shape)
-                    return gi
+                    return (gi, gy) if want_gres else gi
             gi, gres = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=relu,
                                               need_input=need_input,
                                               gg_acc=self.gradWeight if (acc and self.affine) else None,

@@ -45,6 +45,9 @@ struct ConvParams {
   const float* bn_sc;
   const float* bn_sh;
   const float* bn_mean;
+  // optional explicit mask source for that mode (ResNet block tail: the block output, whose ReLU
+  // saw BN(bnx) + shortcut): g ← (g + res) · [bn_mask > 0] instead of the recomputed mask
+  const bf16_t* bn_mask;
 };
 
 constexpr int BM = 128;
@@ -288,8 +291,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   if (p.bnx && full) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      bsc[e] = p.bn_sc[n + e];
-      bsh[e] = p.bn_sh[n + e];
+      bsc[e] = p.bn_mask ? 0.f : p.bn_sc[n + e];
+      bsh[e] = p.bn_mask ? 0.f : p.bn_sh[n + e];
       bmu[e] = p.bn_mean[n + e];
     }
   }
@@ -309,10 +312,22 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       load8(&et[r * LDR + cc * 8], g);
       load8(p.bnx + off, xv);
       uint32_t w4[4];
+      if (p.bn_mask) {
+        float rv[8], mv[8];
+        load8(p.bn_mask + off, mv);
+        if (p.res) {
+          load8(p.res + off, rv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool live = fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
-        g[e] = live ? g[e] : 0.f;
+          for (int e = 0; e < 8; ++e) g[e] += rv[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = mv[e] > 0.f ? g[e] : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool live = fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
+          g[e] = live ? g[e] : 0.f;
+        }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(g[2 * e]) | ((uint32_t)f2bf(g[2 * e + 1]) << 16);
@@ -404,7 +419,8 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
                                      float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
                                      int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
                                      int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
-                                     const float* bn_sh, const float* bn_mean, hipStream_t s) {
+                                     const float* bn_sh, const float* bn_mean, const void* bn_mask,
+                                     hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
@@ -431,8 +447,10 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
   p.bn_sc = bn_sc;
   p.bn_sh = bn_sh;
   p.bn_mean = bn_mean;
-  if (bnx && (!stats || !bn_sc || !bn_sh || !bn_mean || res || relu || bias || p.scatter))
-    return (int)hipErrorInvalidValue;
+  p.bn_mask = (const bf16_t*)bn_mask;
+  if (bnx && (!stats || !bn_mean || relu || bias || p.scatter)) return (int)hipErrorInvalidValue;
+  if (bnx && !bn_mask && (!bn_sc || !bn_sh || res)) return (int)hipErrorInvalidValue;
+  if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
   const int BN = K <= 64 ? 64 : 128;
   p.tiles_n = (K + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
@@ -455,7 +473,7 @@ BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const floa
                                         int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh,
                                         int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
   return bigdl_conv_fwd_full(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
-                             osw, ooh, oow, oH, oW, nullptr, nullptr, nullptr, nullptr, s);
+                             osw, ooh, oow, oH, oW, nullptr, nullptr, nullptr, nullptr, nullptr, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,

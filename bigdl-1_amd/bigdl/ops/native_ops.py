@@ -377,15 +377,26 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
                                      and _al16(residual)):
         return None
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
-    if bn_fuse is not None and residual is None and C_ % 8 == 0:
-        bx, sc, sh, mu = bn_fuse["x"], bn_fuse["scale"], bn_fuse["shift"], bn_fuse["mean"]
-        if (bx.shape == (N_, C_, H, W) and bx.dtype == _bf16 and bx.is_contiguous(memory_format=torch.channels_last)
-                and _al16(bx) and all(_f32vec(t, C_) for t in (sc, sh, mu))):
+    if bn_fuse is not None and C_ % 8 == 0:
+        # BN-backward prologue in the epilogue: either the ReLU mask recomputed from the BN input
+        # (conv → BN+ReLU → this conv), or an explicit mask tensor with the residual gradient summed
+        # first (ResNet block tail: mask = block output)
+        bx, mu, mask = bn_fuse["x"], bn_fuse["mean"], bn_fuse.get("mask")
+        sc, sh = bn_fuse.get("scale"), bn_fuse.get("shift")
+
+        def _act_ok(t):
+            return (t.shape == (N_, C_, H, W) and t.dtype == _bf16
+                    and t.is_contiguous(memory_format=torch.channels_last) and _al16(t))
+        ok = _act_ok(bx) and mu is not None and _f32vec(mu, C_)
+        ok = ok and (_act_ok(mask) if mask is not None else (residual is None and sc is not None and sh is not None
+                                                             and _f32vec(sc, C_) and _f32vec(sh, C_)))
+        if ok:
             G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
             part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)
-            check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(None), ptr(gx), ptr(part), N_, P, Q, K,
-                                             C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, 1, 1, 0, 0,
-                                             H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), _s()), "conv_dgrad_bnbwd")
+            check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_, P,
+                                             Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, 1, 1,
+                                             0, 0, H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), _s()),
+                  "conv_dgrad_bnbwd")
             bn_fuse["partial"], bn_fuse["G"] = part, G
             return gx
     check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,

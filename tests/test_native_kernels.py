@@ -367,3 +367,59 @@ def test_maxpool_native(cfg):
     gx = N.maxpool2d_backward(gy, x, idx, k, s, p, ceil)
     gr = R.maxpool2d_backward(gy.float(), x.float(), idr, k, s, p, ceil)
     torch.testing.assert_close(gx.float(), gr, rtol=1e-2, atol=1e-2)
+
+
+def test_block_tail_bn_backward_fused_into_next_dgrad():
+    """Two ImageNet bottlenecks on bf16: the second block's first conv applies the first block's
+    tail ReLU mask and produces its BN reductions in the dgrad epilogue; gradients must match the
+    same fused model with that tail fusion switched off."""
+    _native()
+    import copy
+    from bigdl.models.resnet import Convolution, Sbn
+    from bigdl.nn import ConcatTable, Identity, Sequential, ReLU, CAddTable, SpatialConvolution, \
+        SpatialBatchNormalization
+    from bigdl.nn.fusion import fuse
+    from bigdl.utils.engine import Engine
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    torch.manual_seed(0)
+
+    def block(n_in, n, proj):
+        s = Sequential().add(Convolution(n_in, n, 1, 1)).add(Sbn(n)).add(ReLU(True))
+        s.add(Convolution(n, n, 3, 3, 1, 1, 1, 1)).add(Sbn(n)).add(ReLU(True))
+        s.add(Convolution(n, n * 4, 1, 1)).add(Sbn(n * 4))
+        sc = Sequential().add(Convolution(n_in, n * 4, 1, 1)).add(Sbn(n * 4)) if proj else Identity()
+        return Sequential().add(ConcatTable().add(s).add(sc)).add(CAddTable(True)).add(ReLU(True))
+    a = Sequential().add(block(64, 16, True)).add(block(64, 16, False)).add(block(64, 16, False))
+    for m in a.flattened_modules():
+        if isinstance(m, SpatialBatchNormalization):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    b = copy.deepcopy(a)
+    fuse(a)
+    fuse(b)
+    heads = [m for m in a.flattened_modules() if isinstance(m, SpatialConvolution) and m._tail_candidates]
+    assert len(heads) == 3
+    for m in b.flattened_modules():
+        if isinstance(m, SpatialConvolution):
+            m._tail_candidates = None
+    a.cuda()
+    b.cuda()
+    hits = []
+    orig = SpatialConvolution._tail_target
+    SpatialConvolution._tail_target = lambda self, x: (lambda r: (hits.append(r), r)[1])(orig(self, x))
+    try:
+        x = _cl(torch.randn(4, 64, 12, 12, device=dev).bfloat16())
+        gy = _cl(torch.randn(4, 64, 12, 12, device=dev).bfloat16())
+        for m in (a, b):
+            m.zeroGradParameters()
+        ya, yb = a.forward(x), b.forward(x)
+        ga, gb = a.backward(x, gy), b.backward(x, gy)
+    finally:
+        SpatialConvolution._tail_target = orig
+    assert sum(h is not None for h in hits) == 2  # blocks 2 and 3 consume a tail
+    torch.testing.assert_close(ya.float(), yb.float())
+    torch.testing.assert_close(ga.float(), gb.float(), rtol=5e-2, atol=5e-2)
+    for u, v in zip(a.parameters()[1], b.parameters()[1]):
+        torch.testing.assert_close(u.float(), v.float(), rtol=5e-2, atol=5e-2)
