@@ -3,6 +3,8 @@ from .abstractnn import (AbstractModule, TensorModule, AutogradModule, AbstractC
                          Activity, LayerException, FlatParameters)
 from .containers import Container, Sequential, Concat, ConcatTable, ParallelTable, MapTable, Bottle
 from .graph import Graph, StaticGraph, Model, Input, ModuleNode, to_graph
+from .dynamic_graph import (DynamicGraph, Scheduler, FrameManager, ControlNodes, SwitchControlNode,
+                            MergeControlNode)
 from .layers import *  # noqa: F401,F403
 from .criterion import *  # noqa: F401,F403
 from .initialization_method import *  # noqa: F401,F403

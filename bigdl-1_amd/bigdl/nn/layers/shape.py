@@ -33,14 +33,25 @@ class Identity(TensorModule):
 
 
 class Echo(Identity):
-    """Prints activation shapes (``Echo.scala``)."""
+    """Pass-through that reports activations (``Echo.scala``): ``feval(module, input)`` on forward
+    and ``bfeval(module, gradOutput)`` on backward; the default prints the shapes."""
+
+    def __init__(self, feval=None, bfeval=None, bigdl_type="float"):
+        super().__init__()
+        self.feval, self.bfeval = feval, bfeval
 
     def updateOutput(self, input):
-        print(f"{self.get_name()} : Activation size is {tuple(input.shape) if hasattr(input, 'shape') else input}")
+        if self.feval is not None:
+            self.feval(self, input)
+        else:
+            print(f"{self.get_name()} : Activation size is {tuple(input.shape) if hasattr(input, 'shape') else input}")
         return input
 
     def updateGradInput(self, input, gradOutput):
-        print(f"{self.get_name()} : Gradient size is {tuple(gradOutput.shape) if hasattr(gradOutput, 'shape') else gradOutput}")
+        if self.bfeval is not None:
+            self.bfeval(self, gradOutput)
+        else:
+            print(f"{self.get_name()} : Gradient size is {tuple(gradOutput.shape) if hasattr(gradOutput, 'shape') else gradOutput}")
         return gradOutput
 
 

@@ -481,6 +481,8 @@ ResizeBilinear = ResizeBilinearOps
 class RandomUniform(Operation):
     """``RandomUniform.scala``: shape tensor → U[minVal, maxVal)."""
 
+    is_random = True  # never memoised as a const node by the dynamic-graph scheduler
+
     def __init__(self, min_val=0.0, max_val=1.0, seed=None):
         super().__init__()
         self.minVal, self.maxVal, self.seed = min_val, max_val, seed
@@ -493,6 +495,8 @@ class RandomUniform(Operation):
 
 class TruncatedNormal(Operation):
     """``TruncatedNormal.scala``: normal(mean, stddev) re-drawn outside 2σ."""
+
+    is_random = True
 
     def __init__(self, mean=0.0, stddev=1.0, seed=None):
         super().__init__()

@@ -213,9 +213,22 @@ class SwitchOps(Operation):
 
 
 class MergeOps(Operation):
-    """First live (non-None) input."""
+    """Forwards one of its inputs: the one the scheduler selected with ``setSwitch`` (1-based,
+    ``ControlOps.scala`` MergeOps) or, when unset, the first live (non-None) input."""
+
+    def __init__(self, switch: int = 0):
+        super().__init__()
+        self.switch = switch
+
+    def setSwitch(self, s: int):
+        self.switch = s
+        return self
 
     def updateOutput(self, t):
+        if self.switch and isinstance(t, Table):
+            return t.get(self.switch)
+        if self.switch == 1 and not isinstance(t, Table):
+            return t
         vals = t.values() if isinstance(t, Table) else [t]
         for v in vals:
             if v is not None:
@@ -237,7 +250,11 @@ class Exit(Enter):
 
 
 class NextIteration(Enter):
-    pass
+    """Carries a loop variable to the next iteration; copies it, since the producing module may
+    overwrite its output buffer in that iteration."""
+
+    def updateOutput(self, x):
+        return x.clone() if isinstance(x, torch.Tensor) else x
 
 
 class LoopCondition(Operation):

@@ -7,9 +7,10 @@ constants only (``Const``, ``Identity`` of a const, shape arithmetic …) into v
 pattern-fuse the trainable layers (``MatMul`` + const weights [+ ``BiasAdd``/``Add`` const] →
 ``Linear``; ``Conv2D`` + const filter [+ bias] → NHWC ``SpatialConvolution``;
 ``FusedBatchNorm`` with const statistics → per-channel affine) → one module per remaining op,
-connected as a ``Graph``.  Control-flow loops (``Enter``/``Exit``/``NextIteration``) and queue/reader
-ops are not loaded (training-input pipelines are replaced by BigDL's own data layer, as in the
-reference's ``Session``).
+connected as a ``Graph``.  Graphs with control flow (``Switch``/``Merge`` conditionals and
+``Enter``/``Exit``/``NextIteration``/``LoopCond`` while loops) load as a forward-only
+``DynamicGraph`` run by the scheduler (``nn/dynamic_graph.py``).  Queue/reader ops are not loaded
+(training-input pipelines are replaced by BigDL's own data layer, as in the reference's ``Session``).
 """
 from __future__ import annotations
 
@@ -187,6 +188,12 @@ _OPS = {
     "Substr": lambda n: O.Substr(),
     "InvertPermutation": lambda n: T.InvertPermutation(), "ConcatOffset": lambda n: T.ConcatOffset(),
     "Switch": lambda n: T.SwitchOps(), "Merge": lambda n: T.MergeOps(),
+    "RefSwitch": lambda n: T.SwitchOps(), "RefMerge": lambda n: T.MergeOps(),
+    "Enter": lambda n: T.Enter(_attr(n, "frame_name", "") or ""),
+    "RefEnter": lambda n: T.Enter(_attr(n, "frame_name", "") or ""),
+    "Exit": lambda n: T.Exit(), "RefExit": lambda n: T.Exit(),
+    "NextIteration": lambda n: T.NextIteration(), "RefNextIteration": lambda n: T.NextIteration(),
+    "LoopCond": lambda n: T.LoopCondition(),
     "NoOp": lambda n: T.NoOp(), "Assert": lambda n: T.Assert(),
     "DecodeJpeg": lambda n: T.DecodeImage(int(_attr(n, "channels", 3) or 3)),
     "DecodePng": lambda n: T.DecodeImage(int(_attr(n, "channels", 3) or 3)),
@@ -231,7 +238,10 @@ def _depthwise(n):
     return O.DepthwiseConv2D(sw, sh, 0, 0, fmt)
 
 
-_NOT_LOADABLE = {"Enter", "Exit", "NextIteration", "LoopCond", "FIFOQueueV2", "QueueDequeueV2", "QueueDequeueManyV2",
+# data-dependent control flow: executed by a DynamicGraph scheduler, never constant-folded
+_CONTROL = {"Switch", "RefSwitch", "Merge", "RefMerge", "Enter", "RefEnter", "Exit", "RefExit", "NextIteration",
+            "RefNextIteration", "LoopCond"}
+_NOT_LOADABLE = {"FIFOQueueV2", "QueueDequeueV2", "QueueDequeueManyV2",
                  "QueueEnqueueV2", "QueueEnqueueManyV2", "TFRecordReaderV2", "ReaderReadV2", "RandomShuffleQueueV2"}
 _STATEFUL = {"RandomUniform", "TruncatedNormal", "RandomShuffle", "Placeholder", "PlaceholderWithDefault", "VariableV2"}
 
@@ -296,7 +306,7 @@ class _Builder:
             return self.consts[key]
         node = self.nodes[n]
         val = None
-        if n in self._fed_nodes or node.op in _STATEFUL or node.op in _NOT_LOADABLE:
+        if n in self._fed_nodes or node.op in _STATEFUL or node.op in _NOT_LOADABLE or node.op in _CONTROL:
             val = None
         elif node.op == "Const":
             val = tensor_to_torch(node.attr["value"].tensor, self.byte_order)
@@ -325,8 +335,13 @@ class _Builder:
                 self._feed_node[n] = node
             self._fed_nodes.add(n)
         self._made = {}
+        self._has_control = False
         out_nodes = [self._node_for(o) for o in outputs]
-        return Graph(ins, [o if not isinstance(o, tuple) else o[0] for o in out_nodes])
+        outs = [o if not isinstance(o, tuple) else o[0] for o in out_nodes]
+        if self._has_control:
+            from ...nn.dynamic_graph import DynamicGraph
+            return DynamicGraph(ins, outs, None, generate_backward=False)
+        return Graph(ins, outs)
 
     def _edge(self, name: str, pos: int):
         """Producer of the ``pos``-th data input of node ``name``."""
@@ -365,6 +380,18 @@ class _Builder:
             module = _OPS[node.op](node)
             edges = [(n, i) for i in range(len([x for x in node.input if not x.startswith("^")]))]
         module.set_name(n)
+        if node.op in _CONTROL:
+            from ...nn.dynamic_graph import MergeControlNode, SwitchControlNode
+            self._has_control = True
+            cls = (SwitchControlNode if node.op in ("Switch", "RefSwitch") else
+                   MergeControlNode if node.op in ("Merge", "RefMerge") else ModuleNode)
+            # register before resolving inputs: a loop's Merge is reached again through its
+            # NextIteration input (the graph has a cycle)
+            mn = cls(module)
+            self._made[n] = mn
+            prevs = [self._feed_node[n]] if n in self._feed_node else [self._edge(nm, pos) for nm, pos in edges]
+            mn(*prevs)
+            return (mn, idx + 1) if _num_outputs(node) > 1 else mn
         if n in self._feed_node:
             prevs = [self._feed_node[n]]
         else:

@@ -193,3 +193,52 @@ def test_feature_columns():
     assert ((h[2] >= 0) & (h[2] < 10)).all()
     kv = O.Kv2Tensor(fea_len=4).forward(["0:1.5,3:2", "1:1"])
     assert kv.tolist() == [[1.5, 0, 0, 2.0], [0, 1.0, 0, 0]]
+
+
+def _while_graphdef(path, limit=10.0):
+    """``i = x; while i < limit: i = i + 1`` as TF 1.x emits it (Enter/Merge/LoopCond/Switch/
+    Identity/NextIteration/Exit), written as a binary GraphDef."""
+    from bigdl.utils.tf.proto import graph_classes, torch_to_tensor
+    classes, _ = graph_classes()
+    gd = classes["tensorflow.GraphDef"]()
+
+    def node(name, op, inputs=(), **attrs):
+        n = gd.node.add()
+        n.name, n.op = name, op
+        n.input.extend(inputs)
+        for k, v in attrs.items():
+            if isinstance(v, torch.Tensor):
+                n.attr[k].tensor.CopyFrom(torch_to_tensor(v))
+            elif isinstance(v, str):
+                n.attr[k].s = v.encode()
+            elif isinstance(v, bool):
+                n.attr[k].b = v
+        return n
+    node("x", "Placeholder")
+    node("limit", "Const", value=torch.tensor(limit))
+    node("one", "Const", value=torch.tensor(1.0))
+    node("while/Enter", "Enter", ["x"], frame_name="while/ctx")
+    node("while/Merge", "Merge", ["while/Enter", "while/NextIteration"])
+    node("while/Less/y", "Enter", ["limit"], frame_name="while/ctx", is_constant=True)
+    node("while/Less", "Less", ["while/Merge", "while/Less/y"])
+    node("while/LoopCond", "LoopCond", ["while/Less"])
+    node("while/Switch", "Switch", ["while/Merge", "while/LoopCond"])
+    node("while/Identity", "Identity", ["while/Switch:1"])
+    node("while/add/y", "Enter", ["one"], frame_name="while/ctx", is_constant=True)
+    node("while/add", "Add", ["while/Identity", "while/add/y"])
+    node("while/NextIteration", "NextIteration", ["while/add"])
+    node("while/Exit", "Exit", ["while/Switch"])
+    node("out", "Mul", ["while/Exit", "one"])
+    with open(path, "wb") as f:
+        f.write(gd.SerializeToString())
+
+
+def test_load_while_loop_as_dynamic_graph(tmp_path):
+    from bigdl.nn import DynamicGraph
+    p = str(tmp_path / "while.pb")
+    _while_graphdef(p)
+    g = TensorflowLoader.load(p, ["x"], ["out"])
+    assert isinstance(g, DynamicGraph)
+    assert float(g.forward(torch.tensor(1.0))) == 10.0
+    assert float(g.forward(torch.tensor(-3.5))) == 10.5
+    assert float(g.forward(torch.tensor(12.0))) == 12.0  # zero trips

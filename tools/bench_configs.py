@@ -1,0 +1,245 @@
+#!/usr/bin/env python
+"""Benchmarks for the secondary BASELINE.json configs (the headline ResNet-50 one is ``bench.py``).
+
+    python tools/bench_configs.py --config lenet      # 1: LeNet-5 MNIST-shape, LocalOptimizer on CPU
+    python tools/bench_configs.py --config vgg        # 2: VggForCifar10 CIFAR-shape, 1 GPU bf16
+    python tools/bench_configs.py --config ptb        # 4: PTB 2-layer LSTM LM (N GPUs via torch.distributed.run)
+    python tools/bench_configs.py --config inception  # 5: Inception-v1 from Caffe files, batch inference
+    python tools/bench_configs.py --config all
+
+Every config builds the model exactly as the reference's example/model builder does, uses synthetic
+inputs of the reference shape and random-init weights (no datasets or checkpoints are available),
+times K full steps (forward + criterion + backward + optimizer, or one inference forward) between
+device synchronisations after W warmup steps, and prints one JSON line per config.
+
+Config 5 round-trips the model through the loaders: the random-init Inception-v1 is written as a
+Caffe prototxt + caffemodel (``CaffePersister``), loaded back with ``CaffeLoader``, saved as a
+``.bigdl`` protobuf and re-loaded from it — the timed model is the one that came out of the loaders.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(_HERE, "..", "bigdl-1_amd"))
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def _time_steps(fn, dev, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    _sync(dev)
+    t0 = time.perf_counter()
+    r = None
+    for _ in range(steps):
+        r = fn()
+    _sync(dev)
+    return time.perf_counter() - t0, r
+
+
+def bench_lenet(args):
+    """Config 1: LeNet-5 (``DL/models/lenet/LeNet5.scala:25``), MNIST shape 1×28×28, 10 classes,
+    ClassNLLCriterion, SGD lr 0.05 (``lenet/Train.scala``), LocalOptimizer on the CPU."""
+    import torch
+    from bigdl.utils.engine import Engine
+    Engine.init(device="cpu")
+    from bigdl.models.lenet import LeNet5
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    B = args.batch or 128
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, 1, 28, 28, generator=g)
+    y = (torch.randint(0, 10, (B,), generator=g) + 1).float()
+    batch = MiniBatch(x, y)
+    opt = LocalOptimizer(LeNet5(10), [batch], ClassNLLCriterion(), SGD(learningrate=0.05), batch_size=B)
+    opt.prepare()
+    dev = torch.device("cpu")
+    el, loss = _time_steps(lambda: opt.train_step(batch), dev, args.steps, args.warmup)
+    return {"metric": "records/sec LeNet-5 MNIST-shape LocalOptimizer (CPU)", "value": round(B * args.steps / el, 1),
+            "unit": "records/sec", "n_gpus": 0, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "fp32",
+            "data": "synthetic", "config": {"model": "LeNet-5", "global_batch": B, "device": "cpu",
+                                            "threads": torch.get_num_threads()},
+            "final_loss": float(loss)}
+
+
+def bench_vgg(args):
+    """Config 2: VggForCifar10 (``DL/models/vgg/VggForCifar10.scala:23-75``), 3×32×32, 10 classes,
+    ClassNLLCriterion, SGD(lr 0.01, wd 5e-4, momentum 0.9) as ``vgg/Train.scala``; bf16 compute."""
+    import torch
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.utils.engine import Engine
+    Engine.init()
+    dev = Engine.device()
+    from bigdl.models.vgg import VggForCifar10
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    B = args.batch or 128
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(B, 3, 32, 32, generator=g).to(dev).to(Engine.compute_dtype()).contiguous(
+        memory_format=torch.channels_last)
+    y = (torch.randint(0, 10, (B,), generator=g) + 1).float().to(dev)
+    batch = MiniBatch(x, y)
+    sgd = SGD(learningrate=0.01, weightdecay=5e-4, momentum=0.9, dampening=0.0)
+    opt = LocalOptimizer(VggForCifar10(10), [batch], ClassNLLCriterion(), sgd, batch_size=B)
+    opt.prepare()
+    el, loss = _time_steps(lambda: opt.train_step(batch), dev, args.steps, args.warmup)
+    return {"metric": "images/sec VggForCifar10 CIFAR-shape 1 GPU", "value": round(B * args.steps / el, 1),
+            "unit": "images/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+            "data": "synthetic", "config": {"model": "VggForCifar10", "global_batch": B},
+            "final_loss": float(loss)}
+
+
+def bench_ptb(args):
+    """Config 4: PTB LSTM language model (``DL/example/languagemodel/PTBModel.scala``, defaults
+    ``languagemodel/Utils.scala:44-53``: vocab 10000, hidden 200, 2 layers, 20 steps, batch 20),
+    TimeDistributedCriterion(CrossEntropy, sizeAverage=false), Adagrad(lr 0.01, decay 0.001).
+    N>1 ranks run the DistriOptimizer; ``value`` is whole-job tokens/sec."""
+    import torch
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.utils.engine import Engine
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    Engine.init(dist=world > 1)
+    dev = Engine.device()
+    rank = Engine.rank()
+    from bigdl.models.rnn import PTBModel
+    from bigdl.nn import CrossEntropyCriterion, TimeDistributedCriterion
+    from bigdl.optim import Adagrad
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    from bigdl.parallel import comm
+    B = args.batch or 20
+    T = args.seq_len
+    V, H = 10000, args.hidden
+    g = torch.Generator().manual_seed(3 + rank)
+    x = (torch.randint(0, V, (B, T), generator=g) + 1).float().to(dev)
+    y = (torch.randint(0, V, (B, T), generator=g) + 1).float().to(dev)
+    batch = MiniBatch(x, y)
+    model = PTBModel.lstm(V, H, V, 2)
+    crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=False)
+    ada = Adagrad(learningrate=0.01, learningrate_decay=0.001)
+    if world > 1:
+        from bigdl.parallel import DistriOptimizer
+        opt = DistriOptimizer(model, [batch], crit, ada, batch_size=B)
+    else:
+        opt = LocalOptimizer(model, [batch], crit, ada, batch_size=B)
+    opt.prepare()
+    for _ in range(args.warmup):
+        opt.train_step(batch)
+    if hasattr(opt, "_wait_all_gathers"):
+        opt._wait_all_gathers()
+    comm.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = opt.train_step(batch)
+    if hasattr(opt, "_wait_all_gathers"):
+        opt._wait_all_gathers()
+    _sync(dev)
+    comm.barrier()
+    el = comm.allreduce_max(time.perf_counter() - t0)
+    res = {"metric": "tokens/sec PTB 2-layer LSTM LM", "value": round(B * T * world * args.steps / el, 1),
+           "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+           "data": "synthetic", "scaling": "weak",
+           "config": {"model": "PTBModel.lstm", "vocab": V, "hidden": H, "layers": 2, "seq_len": T,
+                      "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+           "final_loss": float(loss)}
+    return res if rank == 0 else None
+
+
+def bench_inception(args):
+    """Config 5: Inception-v1 (bvlc_googlenet topology, ``DL/models/inception/Inception_v1.scala``)
+    written to / loaded from Caffe prototxt+caffemodel and .bigdl, then batch inference, bf16."""
+    import torch
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.utils.engine import Engine
+    Engine.init()
+    dev = Engine.device()
+    from bigdl.models.inception import Inception_v1_NoAuxClassifier
+    from bigdl.serialization.caffe_persister import save_caffe
+    from bigdl.serialization.caffe_loader import load_caffe_model
+    from bigdl.nn.module import Module
+    from bigdl.utils.random import RNG
+    RNG.setSeed(5)
+    src = Inception_v1_NoAuxClassifier.graph(1000, has_dropout=True)
+    with tempfile.TemporaryDirectory() as td:
+        proto, cm, bd = (os.path.join(td, n) for n in ("googlenet.prototxt", "googlenet.caffemodel", "g.bigdl"))
+        t0 = time.perf_counter()
+        save_caffe(src.evaluate(), proto, cm, use_v2=True, overwrite=True)
+        loaded = load_caffe_model(proto, cm)
+        loaded.saveModule(bd, over_write=True)
+        model = Module.loadModule(bd)
+        load_s = time.perf_counter() - t0
+    B = args.batch or 256
+    g = torch.Generator().manual_seed(5)
+    xc = torch.randn(4, 3, 224, 224, generator=g)
+    # loader correctness gate (fp32 CPU): the round-tripped model matches the source model
+    src.evaluate()
+    model.evaluate()
+    with torch.no_grad():
+        ref = src.forward(xc).float()
+        got = model.forward(xc).float()
+    # Caffe has no LogSoftMax layer: the persister writes a Softmax and the loader maps it back to
+    # SoftMax (``Converter.scala``), so compare probabilities.
+    if torch.allclose(got.sum(1), torch.ones(got.shape[0]), atol=1e-3):
+        ref = ref.exp()
+    err = float((ref - got).abs().max())
+    assert err < 1e-4, f"Caffe/.bigdl round trip changed the output: max|diff|={err}"
+    model.cuda() if dev.type == "cuda" else None
+    model.evaluate()
+    dt = Engine.compute_dtype() if dev.type == "cuda" else torch.float32
+    x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(dt).contiguous(memory_format=torch.channels_last)
+
+    def step():
+        with torch.no_grad():
+            return model.forward(x)
+    el, out = _time_steps(step, dev, args.steps, args.warmup)
+    return {"metric": "images/sec Inception-v1 (Caffe-loaded) batch inference 1 GPU",
+            "value": round(B * args.steps / el, 1), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "dtype": "bf16" if dev.type == "cuda" else "fp32", "data": "synthetic",
+            "config": {"model": "Inception-v1 (NoAux, Caffe round-trip)", "global_batch": B,
+                       "load_roundtrip_s": round(load_s, 2), "roundtrip_max_abs_diff": err}}
+
+
+CONFIGS = {"lenet": bench_lenet, "vgg": bench_vgg, "ptb": bench_ptb, "inception": bench_inception}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="all", choices=list(CONFIGS) + ["all"])
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
+    ap.add_argument("--seq-len", type=int, default=20)
+    ap.add_argument("--hidden", type=int, default=200)
+    args = ap.parse_args()
+    names = list(CONFIGS) if args.config == "all" else [args.config]
+    for n in names:
+        r = CONFIGS[n](args)
+        if r is not None:
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
