@@ -13,3 +13,4 @@ from .recurrent import *  # noqa: F401,F403
 from .attention import Attention, FeedForwardNetwork, Transformer, SequenceBeamSearch  # noqa: F401
 from .detection import (Anchor, Nms, Proposal, RegionProposal, PriorBox, DetectionOutputSSD,  # noqa: F401
                         DetectionOutputFrcnn, Pooler, FPN, BoxHead, MaskHead, nms, box_iou, roi_align)
+from .tree_lstm import TreeLSTM, BinaryTreeLSTM, TensorTree  # noqa: F401

@@ -120,10 +120,13 @@ class TreeNNAccuracy(ValidationMethod):
     def __call__(self, output, target):
         o = output.float()
         if o.dim() == 3:
-            o = o[:, 0, :]
+            o = o[:, 0, :]          # node 1 = the root in the TensorTree encoding
+        elif o.dim() == 2:
+            o = o[0:1, :]
         t = target.float()
-        t = t[:, 0] if t.dim() == 2 else t
-        pred = o.argmax(-1) + 1
+        t = t[:, 0] if t.dim() == 2 else t.reshape(-1)[:1]
+        # one output unit = binary classifier thresholded at 0.5 (``ValidationMethod.scala:121-166``)
+        pred = (o[:, 0] >= 0.5).float() if o.shape[-1] == 1 else o.argmax(-1) + 1
         return AccuracyResult(int((pred == t.long()).sum()), t.numel())
 
 
