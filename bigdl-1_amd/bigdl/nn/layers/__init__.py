@@ -14,3 +14,4 @@ from .attention import Attention, FeedForwardNetwork, Transformer, SequenceBeamS
 from .detection import (Anchor, Nms, Proposal, RegionProposal, PriorBox, DetectionOutputSSD,  # noqa: F401
                         DetectionOutputFrcnn, Pooler, FPN, BoxHead, MaskHead, nms, box_iou, roi_align)
 from .tree_lstm import TreeLSTM, BinaryTreeLSTM, TensorTree  # noqa: F401
+from .sparse import DenseToSparse, SparseJoinTable  # noqa: F401

@@ -181,3 +181,23 @@ def test_pyspark_style_numpy_io():
     out = m.forward(np.ones((4, 3), dtype=np.float32))
     assert isinstance(out, np.ndarray) and out.shape == (4, 2)
     assert len(m.get_weights()) == 2
+
+
+def test_dense_to_sparse_and_sparse_join_table():
+    import torch
+    from bigdl.nn import DenseToSparse, SparseJoinTable, SparseLinear
+    from bigdl.utils.table import Table
+    a = torch.tensor([[0.0, 2.0, 0.0], [1.0, 0.0, 0.0]])
+    b = torch.tensor([[0.0, 0.0], [0.0, 3.0]])
+    d2s = DenseToSparse()
+    sa = d2s.forward(a)
+    assert sa.is_sparse and torch.equal(sa.to_dense(), a)
+    assert torch.equal(d2s.backward(a, torch.ones(2, 3)), torch.ones(2, 3))
+    j = SparseJoinTable(2)
+    out = j.forward(Table(sa, DenseToSparse().forward(b)))
+    assert torch.equal(out.to_dense(), torch.cat([a, b], 1))
+    gi = j.backward(Table(sa, b), torch.arange(10.0).view(2, 5))
+    assert torch.equal(gi[2], torch.tensor([[3.0, 4.0], [8.0, 9.0]]))
+    lin = SparseLinear(5, 4)
+    dense = lin.forward(torch.cat([a, b], 1)).clone()
+    assert torch.allclose(lin.forward(out), dense, atol=1e-6)

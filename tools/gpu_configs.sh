@@ -11,8 +11,8 @@ if [ "${PROFILE:-1}" = "1" ]; then
   for c in ${PCONFIGS:-vgg ptb inception}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run -- python tools/bench_configs.py --config $c --steps 5 --warmup 2 > gpurun_out/prof_$c.log 2>&1 || { tail -20 gpurun_out/prof_$c.log; exit 1; }
     db=$(find gpurun_out/prof_$c -name '*.db' | head -1)
-    ms=$(python -c "import json,sys; print(json.loads(open('gpurun_out/prof_$c.log').read().strip().splitlines()[-1])['ms_per_step']*5)")
-    LAST_MS=$ms python tools/rocpd_summary.py "$db" 5 30 > gpurun_out/prof_${c}_summary.txt && rm -rf gpurun_out/prof_$c
+    ms=$(python -c "import json; print([json.loads(l) for l in open('gpurun_out/prof_$c.log') if l.startswith('{\"metric')][-1]['ms_per_step']*5)")
+    LAST_MS=$ms python tools/rocpd_summary.py "$db" 5 30 > gpurun_out/prof_${c}_summary.txt; rm -rf gpurun_out/prof_$c
     head -8 gpurun_out/prof_${c}_summary.txt
   done
 fi
