@@ -163,17 +163,88 @@ class Sequential(Container):
         return g
 
 
+def _final_conv(m):
+    """The conv whose output IS ``m``'s output (a conv, or a Sequential ending in conv [→ fused
+    ReLU]), else None."""
+    from .layers.conv import SpatialConvolution
+    from .layers.activation import Threshold
+    while isinstance(m, Sequential) and m.modules:
+        last = m.modules[-1]
+        if isinstance(last, Threshold) and last._passthrough == "mask" and len(m.modules) > 1:
+            prev = m.modules[-2]
+            return prev if isinstance(prev, SpatialConvolution) and prev._fused_relu else None
+        m = last
+    return m if isinstance(m, SpatialConvolution) and not m._fused_relu else None
+
+
+class ConcatPlan:
+    """Zero-copy channel concat for inference (K19): once the output shape of a concat is known for
+    an input shape, the next forward preallocates the NHWC output and every branch's final conv
+    writes its channel slice in its epilogue — the concat copy disappears.  Eval mode on the device
+    only (training keeps separate branch tensors for the backward slices)."""
+
+    def __init__(self, convs):
+        self.convs = convs
+        self.shapes = {}
+
+    def arm(self, key, x):
+        shp = self.shapes.get(key)
+        if shp is None or not (isinstance(x, torch.Tensor) and x.is_cuda) or any(c is None for c in self.convs):
+            return None
+        big = torch.empty(shp, dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        c0 = 0
+        for c in self.convs:
+            k = c.nOutputPlane
+            c._out_target = big[:, c0:c0 + k]
+            c0 += k
+        return big
+
+    def disarm(self):
+        for c in self.convs:
+            if c is not None:
+                c._out_target = None
+
+    def record(self, key, out):
+        if (isinstance(out, torch.Tensor) and out.is_cuda and out.dim() == 4 and out.dtype == torch.bfloat16
+                and out.shape[1] == sum(c.nOutputPlane for c in self.convs if c is not None)):
+            self.shapes[key] = tuple(out.shape)
+
+
+def _plan_key(x):
+    return tuple(x.shape) if isinstance(x, torch.Tensor) else None
+
+
 class Concat(Container):
     """Run every branch on the same input and concatenate along ``dimension`` (1-based)."""
 
     def __init__(self, dimension: int, *modules):
         super().__init__(*modules)
         self.dimension = dimension
+        self._plan = None
 
     def updateOutput(self, input):
-        outs = [m.forward(input) for m in self.modules]
+        plan = None
+        if not self.train and self.dimension == 2 and isinstance(input, torch.Tensor) and input.dim() == 4:
+            if self._plan is None:
+                self._plan = ConcatPlan([_final_conv(m) for m in self.modules])
+            plan = self._plan
+        big = plan.arm(_plan_key(input), input) if plan is not None else None
+        try:
+            outs = [m.forward(input) for m in self.modules]
+        finally:
+            if plan is not None:
+                plan.disarm()
         self._sizes = [o.shape[self.dimension - 1] for o in outs]
-        return torch.cat(outs, dim=self.dimension - 1)
+        if big is not None:
+            from .layers.table_ops import _tiles_channels
+            if _tiles_channels(big, outs):
+                return big
+        out = torch.cat(outs, dim=self.dimension - 1)
+        if plan is not None:
+            if out.is_cuda:
+                out = out.contiguous(memory_format=torch.channels_last)
+            plan.record(_plan_key(input), out)
+        return out
 
     def _split_grad(self, gradOutput):
         return torch.split(gradOutput, self._sizes, dim=self.dimension - 1)

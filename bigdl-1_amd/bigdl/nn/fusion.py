@@ -5,6 +5,9 @@
 The module tree is NOT rewritten (serialisation, ``parameters()`` order and user-visible structure
 stay identical); matched modules get execution flags instead:
 
+* conv → ReLU (``convrelu``, Sequential chains and Graph edges): the conv applies the ReLU in its
+  epilogue; the ReLU module keeps only the gradient mask (taken from its input, which is now
+  ReLU(conv) — positive exactly where the conv output was).
 * conv → BN (``convbn``): the conv skips its bias add and the BN folds the bias in (batch
   normalisation is shift-invariant, so only the running mean sees it); the conv-bias gradient
   Σ_rows gx is produced by the BN backward's finalize kernel from its closed form.
@@ -33,13 +36,46 @@ def _is_relu(m):
     return isinstance(m, Threshold) and m.threshold == 0.0 and m.value == 0.0
 
 
+from .layers.conv import SpatialShareConvolution  # noqa: E402
+
+_PLAIN_CONVS = (SpatialConvolution, SpatialShareConvolution)
+
+
 def _is_nchw_bn(m):
     return isinstance(m, BatchNormalization) and getattr(m, "dataFormat", "NCHW") == "NCHW"
 
 
-def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
+def _relu_fusable_conv(m):
+    return type(m) in _PLAIN_CONVS and m.format == "NCHW" and m._bias_folded_into is None
+
+
+def _fuse_conv_relu(a, b):
+    a._fused_relu = True
+    b._passthrough = "mask"
+
+
+def _fuse_graphs(model, convrelu):
+    """conv → ReLU edges inside Graphs (Caffe/TF-loaded models are graphs): the ReLU must be the
+    conv's only consumer."""
+    from .graph import Graph
+    for g in model.flattened_modules():
+        if not isinstance(g, Graph) or not hasattr(g, "forward_order"):
+            continue
+        g._plans = None  # concat plans depend on the fusion state
+        for n in g.forward_order:
+            if (convrelu and _relu_fusable_conv(n.element) and len(n.next_nodes) == 1
+                    and _is_relu(n.next_nodes[0].element) and len(n.next_nodes[0].prev_nodes) == 1
+                    and not n.element._fused_relu):
+                _fuse_conv_relu(n.element, n.next_nodes[0].element)
+
+
+def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=None):
     if not config.get_property("bigdl.fusion"):
         return model
+    if getattr(model, "_fused", False):
+        return model
+    model._fused = True
+    convrelu = config.get_property("bigdl.fusion.convrelu") if convrelu is None else convrelu
     convbn = config.get_property("bigdl.fusion.convbn") if convbn is None else convbn
     bnrelu = config.get_property("bigdl.fusion.bnrelu") if bnrelu is None else bnrelu
     convsum = config.get_property("bigdl.fusion.convsum") if convsum is None else convsum
@@ -56,6 +92,8 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
                     and b._bias_producer is None:
                 a._bias_folded_into = b
                 b._bias_producer = a
+            if convrelu and _relu_fusable_conv(a) and _is_relu(b) and not b._passthrough:
+                _fuse_conv_relu(a, b)
             if bnrelu and _is_nchw_bn(a) and _is_relu(b):
                 a._fused_relu = True
                 b._passthrough = True
@@ -89,13 +127,20 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None):
     if bnbwd and tails:
         for h in heads:
             h._tail_candidates = tails
+    _fuse_graphs(model, convrelu)
     return model
 
 
 def unfuse(model):
+    model._fused = False
     for m in model.flattened_modules():
+        if hasattr(m, "_plans"):
+            m._plans = None
+        if hasattr(m, "_plan"):
+            m._plan = None
         if isinstance(m, SpatialConvolution):
             m._bias_folded_into = None
+            m._fused_relu = False
             m._bn_bwd_target = None
             m._tail_candidates = None
         if isinstance(m, BatchNormalization):

@@ -136,6 +136,33 @@ class Graph(Container):
             return None
         return vals[0] if len(vals) == 1 else Table(*vals)
 
+    def _concat_plans(self):
+        """JoinTable nodes whose every input is produced by a single-consumer conv (optionally
+        through its fused ReLU) → :class:`ConcatPlan` (zero-copy concat at inference)."""
+        from .containers import ConcatPlan
+        from .layers.activation import Threshold
+        from .layers.conv import SpatialConvolution
+        from .layers.table_ops import JoinTable
+        plans = []
+        for n in self.forward_order:
+            if not isinstance(n.element, JoinTable) or len(n.prev_nodes) < 2:
+                continue
+            convs = []
+            for p in n.prev_nodes:
+                c = None
+                e = p.element
+                if (isinstance(e, Threshold) and e._passthrough == "mask" and len(p.prev_nodes) == 1
+                        and len(p.next_nodes) == 1):
+                    q = p.prev_nodes[0]
+                    if isinstance(q.element, SpatialConvolution) and q.element._fused_relu and len(q.next_nodes) == 1:
+                        c = q.element
+                elif isinstance(e, SpatialConvolution) and not e._fused_relu and len(p.next_nodes) == 1:
+                    c = e
+                convs.append(c)
+            if all(c is not None for c in convs) and len({id(c) for c in convs}) == len(convs):
+                plans.append((n.element, ConcatPlan(convs)))
+        return plans
+
     def updateOutput(self, input):
         acts = {}
         if len(self.inputs) == 1:
@@ -143,13 +170,28 @@ class Graph(Container):
         else:
             feeds = {n._id: input[i + 1] for i, n in enumerate(self.inputs)}
         self._node_inputs = {}
-        for n in self.forward_order:
-            if n._id in feeds:
-                x = feeds[n._id]
-            else:
-                x = self._node_input(n, acts)
-            self._node_inputs[n._id] = x
-            acts[n._id] = n.element.forward(x)
+        plans = ()
+        first = input if isinstance(input, torch.Tensor) else None
+        if not self.train and first is not None and first.is_cuda:
+            if getattr(self, "_plans", None) is None:
+                self._plans = self._concat_plans()
+            plans = self._plans
+        key = tuple(first.shape) if first is not None else None
+        for join, plan in plans:
+            join._planned = plan.arm(key, first)
+        try:
+            for n in self.forward_order:
+                if n._id in feeds:
+                    x = feeds[n._id]
+                else:
+                    x = self._node_input(n, acts)
+                self._node_inputs[n._id] = x
+                acts[n._id] = n.element.forward(x)
+        finally:
+            for join, plan in plans:
+                plan.disarm()
+                join._planned = None
+                plan.record(key, join.output)
         self._acts = acts
         outs = [acts[o._id] for o in self.outputs_nodes]
         return outs[0] if len(outs) == 1 else Table(*outs)

@@ -29,6 +29,10 @@ class Threshold(TensorModule):
         return ops.relu_forward(input, self.threshold, self.value, inplace=False)
 
     def updateGradInput(self, input, gradOutput):
+        if self._passthrough == "mask":
+            # the producer applied this ReLU in its epilogue: input is already ReLU(x), and
+            # ReLU(x) > 0 ⇔ x > 0, so the mask comes from it
+            return ops.relu_backward(gradOutput, input, 0.0)
         if self._passthrough:
             return gradOutput
         ref = self.output if self.value <= self.threshold else input

@@ -130,6 +130,12 @@ class SpatialConvolution(TensorModule):
     #: BN this conv's bias is folded into (set by bigdl.nn.fusion); the BN adds it implicitly and
     #: accumulates its gradient, so the conv skips both
     _bias_folded_into = None
+    #: the following ReLU is applied in this conv's epilogue (bigdl.nn.fusion ``convrelu``; the ReLU
+    #: module then only masks the gradient)
+    _fused_relu = False
+    #: channel slice of a concat output this conv writes straight into (set per forward by a
+    #: zero-copy JoinTable/Concat plan); consumed once
+    _out_target = None
 
     #: gradient added to this conv's gradInput in the dgrad epilogue (set by a fused residual
     #: ConcatTable for the first conv of a block: the branch/shortcut gradient sum)
@@ -163,7 +169,8 @@ class SpatialConvolution(TensorModule):
     def updateOutput(self, input):
         x, pad, batched, _ = self._prep(input)
         w4 = self._w4(self.cw("weight"))
-        b = self.cw("bias") if (self.withBias and self._bias_folded_into is None) else None
+        # fp32 master bias: the HIP epilogue adds fp32 (no per-call cast), the reference casts
+        b = self.bias if (self.withBias and self._bias_folded_into is None) else None
         bn = self._stats_consumer(x) if batched else None
         y = NotImplemented
         if bn is not None and ops.native_has("conv2d_forward"):
@@ -173,8 +180,11 @@ class SpatialConvolution(TensorModule):
                 y, part, G = r
                 bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G)
         if y is NotImplemented:
+            tgt, self._out_target = self._out_target, None
+            if tgt is not None and (not batched or self.format != "NCHW"):
+                tgt = None
             y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
-                                   self.nGroup)
+                                   self.nGroup, relu=self._fused_relu, out=tgt)
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)

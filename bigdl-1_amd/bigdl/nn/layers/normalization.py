@@ -352,13 +352,17 @@ class SpatialCrossMapLRN(TensorModule):
         return self._f(input)
 
     def updateGradInput(self, input, gradOutput):
-        x = input.detach().requires_grad_(True)
-        with torch.enable_grad():
-            y = F.local_response_norm(x if x.dim() == 4 else x.unsqueeze(0), self.size, self.alpha, self.beta, self.k) \
-                if self.format != "NHWC" else self._f(x)
-            if self.format != "NHWC" and input.dim() == 3:
-                y = y.squeeze(0)
-        return torch.autograd.grad(y, x, gradOutput.to(y.dtype))[0]
+        nhwc = self.format == "NHWC"
+        x, gy = input, gradOutput
+        if nhwc:
+            x, gy = x.permute(0, 3, 1, 2), gy.permute(0, 3, 1, 2)
+        batched = x.dim() == 4
+        if not batched:
+            x, gy = x.unsqueeze(0), gy.unsqueeze(0)
+        gx = ops.lrn_backward(gy, x, self.size, self.alpha, self.beta, self.k)
+        if not batched:
+            gx = gx.squeeze(0)
+        return gx.permute(0, 2, 3, 1) if nhwc else gx
 
 
 class SpatialWithinChannelLRN(AutogradModule):

@@ -108,6 +108,18 @@ class CAveTable(AutogradModule):
         return sum(ts) / len(ts)
 
 
+def _tiles_channels(big, ts) -> bool:
+    """``ts`` are, in order, the consecutive channel slices of 4-D ``big``."""
+    c0 = 0
+    es = big.element_size()
+    for t in ts:
+        if (t.dim() != 4 or t.shape[0] != big.shape[0] or t.shape[2:] != big.shape[2:]
+                or t.data_ptr() != big.data_ptr() + c0 * es or t.stride() != big.stride()):
+            return False
+        c0 += t.shape[1]
+    return c0 == big.shape[1]
+
+
 class JoinTable(TensorModule):
     """Concatenate table entries along ``dimension`` (1-based, batch-shifted by nInputDims)."""
 
@@ -121,10 +133,17 @@ class JoinTable(TensorModule):
             d += x.dim() - self.nInputDims
         return d
 
+    #: preallocated output whose channel slices the producing convs wrote directly (zero-copy
+    #: concat, planned by :func:`bigdl.nn.containers.plan_concat`); consumed once
+    _planned = None
+
     def updateOutput(self, input):
         ts = list(input)
         d = self._d(ts[0])
         self._sizes = [t.shape[d] for t in ts]
+        big, self._planned = self._planned, None
+        if big is not None and d == 1 and _tiles_channels(big, ts):
+            return big
         if ts[0].is_cuda and ts[0].dim() == 4 and d == 1:
             return torch.cat(ts, d).contiguous(memory_format=torch.channels_last)
         return torch.cat(ts, d)

@@ -48,6 +48,9 @@ struct ConvParams {
   // optional explicit mask source for that mode (ResNet block tail: the block output, whose ReLU
   // saw BN(bnx) + shortcut): g ← (g + res) · [bn_mask > 0] instead of the recomputed mask
   const bf16_t* bn_mask;
+  // output row stride in elements (== K unless the conv writes a channel slice of a wider tensor,
+  // e.g. its branch of an Inception concat: y points at the slice, rows are ldy apart)
+  int ldy;
 };
 
 constexpr int BM = 128;
@@ -301,11 +304,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
     const int m = m0 + r;
     if (m >= p.M || n >= p.K) continue;
     size_t off = (size_t)m * p.K + n;
+    size_t yoff = (size_t)m * p.ldy + n;
     if (p.scatter) {
       const int nimg = m / (p.P * p.Q);
       const int pq = m - nimg * p.P * p.Q;
       const int pp = pq / p.Q, qq = pq - pp * p.Q;
       off = ((size_t)(nimg * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow) * p.K + n;
+      yoff = off;
     }
     if (full && p.bnx) {
       float g[8], xv[8];
@@ -331,7 +336,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(g[2 * e]) | ((uint32_t)f2bf(g[2 * e + 1]) << 16);
-      *reinterpret_cast<uint4*>(p.y + off) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      *reinterpret_cast<uint4*>(p.y + yoff) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float a = __uint_as_float(w4[e] << 16), b = __uint_as_float(w4[e] & 0xFFFF0000u);
@@ -360,7 +365,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
         for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
         u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
-      *reinterpret_cast<uint4*>(p.y + off) = u;
+      *reinterpret_cast<uint4*>(p.y + yoff) = u;
       if (p.stats) {
         // statistics of the values as stored (bf16-rounded), which is what the BN reads
         const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
@@ -380,7 +385,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
         float t = v[e] + (p.res ? bf2f(p.res[off + e]) : 0.f);
         if (p.relu) t = fmaxf(t, 0.f);
         const bf16_t o = f2bf(t);
-        p.y[off + e] = o;
+        p.y[yoff + e] = o;
         const float w = bf2f(o);
         s8[e] += w;
         q8[e] = fmaf(w, w, q8[e]);
@@ -415,13 +420,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
 // ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
 BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + BM - 1) / BM); }
 
-BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* bias, const void* res, void* y,
-                                     float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
-                                     int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
-                                     int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
-                                     const float* bn_sh, const float* bn_mean, const void* bn_mask,
-                                     hipStream_t s) {
+static int conv_fwd_launch(const void* x, const void* w, const float* bias, const void* res, void* y,
+                           float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                           int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
+                           int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
+                           const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
+                           hipStream_t s) {
   if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
+  if (ldy < K || (ldy != K && (ldy % 8 || K % 8 || ((uintptr_t)y & 15)))) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
   if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * R * S * C * 2 >= 0x80000000ull)
@@ -443,6 +449,8 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
   p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
   p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
   if (p.scatter && stats) return (int)hipErrorInvalidValue;
+  p.ldy = ldy;
+  if (ldy != K && (p.scatter || bnx)) return (int)hipErrorInvalidValue;
   p.bnx = (const bf16_t*)bnx;
   p.bn_sc = bn_sc;
   p.bn_sh = bn_sh;
@@ -466,6 +474,24 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
   else
     hipLaunchKernelGGL((k_conv_fwd<128, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                     float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                     int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
+                                     int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
+                                     const float* bn_sh, const float* bn_mean, const void* bn_mask,
+                                     hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
+                         osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s);
+}
+
+// Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).
+BIGDL_EXPORT int bigdl_conv_fwd_ldy(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                    float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                    int sh, int sw, int ph, int pw, int dh, int dw, int relu, int ldy, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, 1, 1, 0,
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const float* bias, const void* res, void* y,

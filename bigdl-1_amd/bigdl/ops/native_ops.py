@@ -310,7 +310,9 @@ def _conv_geom_ok(x, w4, groups, dilation):
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
 
 
-def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False):
+def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None):
+    """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
+    writes into directly (zero-copy concat); returned as the result."""
     if not _conv_geom_ok(x, w4, groups, dilation):
         return NotImplemented
     N_, C_, H, W = x.shape
@@ -333,23 +335,31 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     if res is not None and not (res.shape == (N_, K, P, Q) and res.dtype == _bf16 and
                                 res.is_contiguous(memory_format=torch.channels_last) and _al16(res)):
         return NotImplemented
-    y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
-    bias = b.float().contiguous() if b is not None else None
+    ldy = K
+    if out is not None:
+        if not (out.dim() == 4 and tuple(out.shape) == (N_, K, P, Q) and out.dtype == _bf16 and not stats
+                and res is None and out.stride(1) == 1 and out.stride(3) % 8 == 0 and K % 8 == 0
+                and out.stride(2) == out.stride(3) * Q and out.stride(0) == out.stride(2) * P and _al16(out)):
+            return NotImplemented
+        y, ldy = out, out.stride(3)
+    else:
+        y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    bias = b if (b is None or (b.dtype == _f32 and b.is_contiguous())) else b.float().contiguous()
     part, G = None, 0
     if stats:
         G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
         part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
-    check(_lib().bigdl_conv_fwd_ex(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
-                                   P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0, _s()),
-          "conv_fwd")
+    check(_lib().bigdl_conv_fwd_ldy(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
+                                    P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy,
+                                    _s()), "conv_fwd")
     if stats:
         return y, part, G
     return y
 
 
 @register("conv2d_forward")
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups)
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None):
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, relu=relu, out=out)
 
 
 def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
@@ -784,4 +794,35 @@ def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
     check(_lib().bigdl_maxpool_bwd(ptr(gy), ptr(idx.t), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0],
                                    p[1], _s()), "maxpool_bwd")
+    return gx
+
+
+# ---------------------------------------------------------------------------------- K18 LRN
+def _lrn_ok(x, size):
+    return (x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)
+            and x.shape[1] % 8 == 0 and size % 2 == 1 and x.numel() > 0)
+
+
+@register("lrn_forward")
+def lrn_forward(x, size, alpha, beta, k):
+    if not _lrn_ok(x, size) or size > 17:
+        return NotImplemented
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    check(_lib().bigdl_lrn_fwd(ptr(x), ptr(y), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta),
+                               C.c_float(k), _s()), "lrn_fwd")
+    return y
+
+
+@register("lrn_backward")
+def lrn_backward(gy, x, size, alpha, beta, k):
+    if not _lrn_ok(x, size) or size > 9:
+        return NotImplemented
+    gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    if gy.shape != x.shape or not _al16(gy):
+        return NotImplemented
+    gx = torch.empty_like(x, memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    check(_lib().bigdl_lrn_bwd(ptr(x), ptr(gy), ptr(gx), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta),
+                               C.c_float(k), _s()), "lrn_bwd")
     return gx

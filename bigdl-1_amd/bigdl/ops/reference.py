@@ -37,12 +37,19 @@ def relu_backward(gy: torch.Tensor, y_or_x: torch.Tensor, threshold: float = 0.0
 
 
 # ------------------------------------------------------------------------- convolution
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None):
     """``SpatialConvolution.updateOutput`` (``DL/nn/SpatialConvolution.scala:253-362``).
 
-    ``w4`` is (O, I/g, kH, kW); ``pad`` is (padH, padW) after SAME resolution.
+    ``w4`` is (O, I/g, kH, kW); ``pad`` is (padH, padW) after SAME resolution.  ``relu`` applies a
+    fused ReLU; ``out`` (optional) receives the result (a slice of a concat output).
     """
-    return F.conv2d(x, w4.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dilation, groups)
+    y = F.conv2d(x, w4.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dilation, groups)
+    if relu:
+        y = torch.relu(y)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
 
 
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
@@ -381,6 +388,14 @@ def lrn_forward(x, size, alpha, beta, k):
     """``SpatialCrossMapLRN`` (``DL/nn/SpatialCrossMapLRN.scala:96-200``):
     y = x / (k + α/size · Σ_{window} x²)^β."""
     return F.local_response_norm(x, size, alpha, beta, k)
+
+
+def lrn_backward(gy, x, size, alpha, beta, k):
+    """Gradient of :func:`lrn_forward` w.r.t. ``x`` (``SpatialCrossMapLRN.updateGradInput``)."""
+    xr = x.detach().requires_grad_(True)
+    with torch.enable_grad():
+        y = F.local_response_norm(xr, size, alpha, beta, k)
+    return torch.autograd.grad(y, xr, gy.to(y.dtype))[0]
 
 
 # ------------------------------------------------------------------------- int8 (K26)

@@ -100,6 +100,9 @@ class LocalPredictor:
         dev = _model_device(m)
         was_training = m.isTraining()
         m.evaluate()
+        if dev.type == "cuda":
+            from ..nn.fusion import fuse
+            fuse(m)  # conv+ReLU epilogues, zero-copy concats (idempotent)
         outs = []
         try:
             with torch.no_grad():

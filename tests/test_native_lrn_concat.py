@@ -1,0 +1,82 @@
+"""GPU numerics: LRN forward/backward kernels (K18), conv epilogue ReLU + strided output slice,
+zero-copy Inception concat — each vs the fp32 PyTorch reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _N():
+    from bigdl.ops import native, native_status
+    assert native_status()["loaded"]
+    return native
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("C,size", [(64, 5), (192, 5), (24, 3), (16, 9), (8, 5)])
+def test_lrn_forward_backward(C, size):
+    N = _N()
+    torch.manual_seed(0)
+    x = _cl(torch.randn(3, C, 7, 5, device=dev) * 3).to(torch.bfloat16)
+    x = _cl(x)
+    gy = _cl(torch.randn(3, C, 7, 5, device=dev)).to(torch.bfloat16)
+    gy = _cl(gy)
+    alpha, beta, k = 1e-2, 0.75, 1.0
+    y = N.lrn_forward(x, size, alpha, beta, k)
+    assert y is not NotImplemented
+    xr = x.float().requires_grad_(True)
+    yr = F.local_response_norm(xr, size, alpha, beta, k)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=2e-2, atol=2e-2)
+    gx = N.lrn_backward(gy, x, size, alpha, beta, k)
+    assert gx is not NotImplemented
+    (gr,) = torch.autograd.grad(yr, xr, gy.float())
+    torch.testing.assert_close(gx.float(), gr, rtol=3e-2, atol=3e-2)
+
+
+def test_conv_relu_epilogue_and_slice_output():
+    N = _N()
+    torch.manual_seed(1)
+    x = _cl(torch.randn(2, 64, 9, 9, device=dev)).to(torch.bfloat16)
+    x = _cl(x)
+    w = torch.randn(48, 64, 3, 3, device=dev) * 0.05
+    b = torch.randn(48, device=dev)
+    ref = torch.relu(F.conv2d(x.float(), w.to(torch.bfloat16).float(), b, 1, 1))
+    y = N.conv2d_forward(x, w.to(torch.bfloat16), b, (1, 1), (1, 1), relu=True)
+    assert y is not NotImplemented
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    big = torch.full((2, 80, 9, 9), 7.0, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    out = big[:, 16:64]
+    y2 = N.conv2d_forward(x, w.to(torch.bfloat16), b, (1, 1), (1, 1), relu=True, out=out)
+    assert y2 is not NotImplemented and y2.data_ptr() == out.data_ptr()
+    torch.testing.assert_close(big[:, 16:64].float(), ref, rtol=2e-2, atol=2e-2)
+    assert bool((big[:, :16] == 7).all()) and bool((big[:, 64:] == 7).all())  # neighbours untouched
+
+
+def test_inception_zero_copy_concat_and_lrn_model():
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.models.inception import Inception_v1_NoAuxClassifier
+    from bigdl.nn.fusion import fuse
+    from bigdl.utils.random import RNG
+    RNG.setSeed(3)
+    ref_model = Inception_v1_NoAuxClassifier.graph(1000, has_dropout=False)
+    ref_model.evaluate()
+    x = torch.randn(2, 3, 224, 224)
+    with torch.no_grad():
+        ref = ref_model.forward(x).float().clone()
+    m = ref_model.cuda()
+    m.evaluate()
+    fuse(m)
+    xd = _cl(x.to(dev).to(torch.bfloat16))
+    with torch.no_grad():
+        y1 = m.forward(xd).float().cpu()   # plans record shapes
+        y2 = m.forward(xd).float().cpu()   # zero-copy concats armed
+    assert any(p.shapes for _, p in m._plans), "no concat plan recorded"
+    torch.testing.assert_close(y1, y2, rtol=0, atol=0)
+    # bf16 end-to-end vs the fp32 CPU model: log-probabilities agree to bf16 accuracy
+    assert (y2 - ref).abs().max().item() < 0.15

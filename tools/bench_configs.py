@@ -207,6 +207,8 @@ def bench_inception(args):
     assert err < 1e-4, f"Caffe/.bigdl round trip changed the output: max|diff|={err}"
     model.cuda() if dev.type == "cuda" else None
     model.evaluate()
+    from bigdl.nn.fusion import fuse
+    fuse(model)  # what LocalPredictor does: conv+ReLU epilogues, zero-copy concats
     dt = Engine.compute_dtype() if dev.type == "cuda" else torch.float32
     x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(dt).contiguous(memory_format=torch.channels_last)
 
