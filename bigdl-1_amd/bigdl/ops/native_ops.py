@@ -826,3 +826,52 @@ def lrn_backward(gy, x, size, alpha, beta, k):
     check(_lib().bigdl_lrn_bwd(ptr(x), ptr(gy), ptr(gx), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta),
                                C.c_float(k), _s()), "lrn_bwd")
     return gx
+
+
+# ---------------------------------------------------------------------------------- K17 dropout
+class _DropMask:
+    """Stands in for the dropout mask: the kernel regenerates the keep decisions from ``seed``."""
+    __slots__ = ("seed", "cl", "shape")
+
+    def __init__(self, seed, cl, shape):
+        self.seed, self.cl, self.shape = seed, cl, shape
+
+
+def _dense_layout(t):
+    if t.is_contiguous():
+        return False
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return True
+    return None
+
+
+@register("dropout_forward")
+def dropout_forward(x, p, generator=None):
+    if p <= 0 or p >= 1 or x.dtype not in (_bf16, _f32) or not _al16(x) or x.numel() == 0:
+        return NotImplemented
+    cl = _dense_layout(x)
+    if cl is None:
+        return NotImplemented
+    seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator if (generator is not None and
+                                                                         generator.device.type == "cpu") else None))
+    y = torch.empty_like(x)
+    check(_lib().bigdl_dropout(ptr(x), ptr(y), _ll(x.numel()), 0 if x.dtype == _bf16 else 1, C.c_float(p),
+                               C.c_ulonglong(seed), _s()), "dropout_fwd")
+    return y, _DropMask(seed, cl, tuple(x.shape))
+
+
+@register("dropout_backward")
+def dropout_backward(gy, mask, p):
+    if not isinstance(mask, _DropMask):
+        return NotImplemented
+    if tuple(gy.shape) != mask.shape:
+        raise ValueError(f"dropout backward: gradient shape {tuple(gy.shape)} != forward {mask.shape}")
+    if gy.dtype not in (_bf16, _f32):
+        gy = gy.float()
+    gy = gy.contiguous(memory_format=torch.channels_last) if mask.cl else gy.contiguous()
+    if not _al16(gy):
+        gy = gy.clone()
+    gx = torch.empty_like(gy)
+    check(_lib().bigdl_dropout(ptr(gy), ptr(gx), _ll(gy.numel()), 0 if gy.dtype == _bf16 else 1, C.c_float(p),
+                               C.c_ulonglong(mask.seed), _s()), "dropout_bwd")
+    return gx

@@ -80,3 +80,33 @@ def test_inception_zero_copy_concat_and_lrn_model():
     torch.testing.assert_close(y1, y2, rtol=0, atol=0)
     # bf16 end-to-end vs the fp32 CPU model: log-probabilities agree to bf16 accuracy
     assert (y2 - ref).abs().max().item() < 0.15
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n", [1 << 20, 1000003])
+def test_dropout_regenerated_mask(dtype, n):
+    N = _N()
+    p = 0.3
+    x = (torch.rand(n, device=dev) + 1.0).to(dtype)  # never exactly zero
+    r = N.dropout_forward(x, p)
+    assert r is not NotImplemented
+    y, mask = r
+    kept = y != 0
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 5e-3, frac
+    torch.testing.assert_close(y[kept].float(), (x[kept].float() / (1 - p)).to(dtype).float(), rtol=1e-2, atol=1e-2)
+    gy = torch.randn(n, device=dev).to(dtype)
+    gx = N.dropout_backward(gy, mask, p)
+    assert torch.equal(gx != 0, kept & (gy != 0))
+    # a new call draws a new seed
+    y2, _ = N.dropout_forward(x, p)
+    assert not torch.equal(y2 != 0, kept)
+
+
+def test_dropout_layer_channels_last_backward():
+    from bigdl.nn import Dropout
+    d = Dropout(0.5)
+    x = (torch.randn(4, 16, 8, 8, device=dev) + 3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = d.forward(x)
+    g = d.backward(x, torch.ones_like(y).contiguous())  # gradient arrives in the other layout
+    assert torch.equal((g != 0), (y != 0))
