@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from ... import ops
 from ...utils.engine import Engine
 from ...utils import config
-from ..abstractnn import TensorModule, AutogradModule
+from ..abstractnn import AbstractModule, TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, VariableFormats
 
 
@@ -263,6 +263,36 @@ class SpatialConvolution(TensorModule):
     def __repr__(self):
         return (f"SpatialConvolution[{self.get_name()}]({self.nInputPlane} -> {self.nOutputPlane}, "
                 f"{self.kernelW} x {self.kernelH}, {self.strideW}, {self.strideH}, {self.padW}, {self.padH})")
+
+
+class FusedConvSum(AbstractModule):
+    """Inference form of a residual block tail produced by the IR lowering: input
+    ``Table(x, shortcut)`` → ``[ReLU](conv(x) + shortcut)``, the add and ReLU done in the conv
+    epilogue (the reference's conv+sum MKL-DNN post-op, ``Fusion.fusionCAddTable``)."""
+
+    def __init__(self, conv, relu=True):
+        super().__init__()
+        self.conv, self.relu = conv, relu
+        self.set_name(conv.get_name() + "/sum")
+
+    def children(self):
+        return [self.conv]
+
+    def updateOutput(self, input):
+        c = self.conv
+        x, pad, batched, _ = c._prep(input[1])
+        r = input[2] if batched else input[2].unsqueeze(0)
+        r = to_device_layout(r)
+        b = c.bias if c.withBias else None
+        y = ops.conv2d_forward(x, c._w4(c.cw("weight")), b, (c.strideH, c.strideW), pad, (c.dilationH, c.dilationW),
+                               c.nGroup, relu=self.relu, res=r)
+        return y if batched else y.squeeze(0)
+
+    def updateGradInput(self, input, gradOutput):
+        raise RuntimeError("FusedConvSum is an inference-only node")
+
+    def __repr__(self):
+        return f"FusedConvSum({self.conv!r}, relu={self.relu})"
 
 
 class SpatialShareConvolution(SpatialConvolution):

@@ -358,8 +358,10 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
 
 
 @register("conv2d_forward")
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None):
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, relu=relu, out=out)
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None):
+    if res is not None and (res.dtype != _bf16 or not res.is_contiguous(memory_format=torch.channels_last)):
+        res = res.to(_bf16).contiguous(memory_format=torch.channels_last)
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out)
 
 
 def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1):

@@ -37,13 +37,15 @@ def relu_backward(gy: torch.Tensor, y_or_x: torch.Tensor, threshold: float = 0.0
 
 
 # ------------------------------------------------------------------------- convolution
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None):
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None):
     """``SpatialConvolution.updateOutput`` (``DL/nn/SpatialConvolution.scala:253-362``).
 
     ``w4`` is (O, I/g, kH, kW); ``pad`` is (padH, padW) after SAME resolution.  ``relu`` applies a
     fused ReLU; ``out`` (optional) receives the result (a slice of a concat output).
     """
     y = F.conv2d(x, w4.to(x.dtype), None if b is None else b.to(x.dtype), stride, pad, dilation, groups)
+    if res is not None:
+        y = y + res.to(y.dtype)
     if relu:
         y = torch.relu(y)
     if out is not None:

@@ -110,3 +110,25 @@ def test_dropout_layer_channels_last_backward():
     y = d.forward(x)
     g = d.backward(x, torch.ones_like(y).contiguous())  # gradient arrives in the other layout
     assert torch.equal((g != 0), (y != 0))
+
+
+def test_ir_resnet_inference_native():
+    """IR lowering on the device: BN-folded convs with ReLU / residual-sum epilogues (bf16) vs the
+    fp32 eval model on the CPU."""
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.utils.intermediate import ConversionUtils
+    torch.manual_seed(0)
+    m = model_init(ResNet(10, depth=20, dataset=DatasetType.CIFAR10))
+    m.training()
+    m.forward(torch.randn(8, 3, 32, 32))
+    m.evaluate()
+    x = torch.randn(16, 3, 32, 32)
+    ref = m.forward(x).float().clone()
+    ir = ConversionUtils.convert(m)
+    ir.to(dev)
+    with torch.no_grad():
+        y = ir.forward(_cl(x.to(dev).to(torch.bfloat16))).float().cpu()
+    assert (y - ref).abs().max().item() < 0.1
+    assert (y.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.9

@@ -224,7 +224,52 @@ def bench_inception(args):
                        "load_roundtrip_s": round(load_s, 2), "roundtrip_max_abs_diff": err}}
 
 
-CONFIGS = {"lenet": bench_lenet, "vgg": bench_vgg, "ptb": bench_ptb, "inception": bench_inception}
+def bench_resnet_infer(args):
+    """ResNet-50 batch inference through the IR lowering (``ConversionUtils.convert``: BN folded
+    into the convs, ReLU in the conv epilogues), bf16, random-init weights with non-trivial BN
+    running statistics; checked against the unfolded eval model before timing."""
+    import torch
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.utils.engine import Engine
+    Engine.init()
+    dev = Engine.device()
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.utils.intermediate import ConversionUtils
+    from bigdl.utils.random import RNG
+    RNG.setSeed(7)
+    model = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+    model.training()
+    with torch.no_grad():  # a few training forwards on CPU give the BNs real running statistics
+        model.forward(torch.randn(2, 3, 224, 224))
+    model.evaluate()
+    xc = torch.randn(2, 3, 224, 224)
+    with torch.no_grad():
+        ref = model.forward(xc).float().clone()
+    ir = ConversionUtils.convert(model)
+    with torch.no_grad():
+        err = float((ir.forward(xc).float() - ref).abs().max())
+    assert err < 1e-3, f"IR lowering changed the output: {err}"
+    if dev.type == "cuda":
+        ir.to(dev)
+    B = args.batch or 256
+    dt = Engine.compute_dtype() if dev.type == "cuda" else torch.float32
+    x = torch.randn(B, 3, 224, 224).to(dev).to(dt).contiguous(memory_format=torch.channels_last)
+
+    def step():
+        with torch.no_grad():
+            return ir.forward(x)
+    el, _ = _time_steps(step, dev, args.steps, args.warmup)
+    return {"metric": "images/sec ResNet-50 batch inference (IR: BN folded) 1 GPU",
+            "value": round(B * args.steps / el, 1), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "dtype": "bf16" if dev.type == "cuda" else "fp32", "data": "synthetic",
+            "config": {"model": "ResNet-50 (IRGraph inference lowering)", "global_batch": B,
+                       "fold_max_abs_diff": err}}
+
+
+CONFIGS = {"lenet": bench_lenet, "vgg": bench_vgg, "ptb": bench_ptb, "inception": bench_inception,
+           "resnet_infer": bench_resnet_infer}
 
 
 def main():
