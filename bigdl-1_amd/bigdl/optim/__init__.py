@@ -16,4 +16,7 @@ def __getattr__(name):
     if name == "DistriOptimizer":
         from ..parallel.distri_optimizer import DistriOptimizer
         return DistriOptimizer
+    if name == "ParallelOptimizer":
+        from ..parallel.distri_optimizer import ParallelOptimizer
+        return ParallelOptimizer
     raise AttributeError(name)

@@ -302,7 +302,7 @@ class DistriOptimizer(BaseOptimizer):
         for meth in self.optim_methods.values():
             meth.begin_iteration(self.shard_w)
         done = set()
-        for b in reversed(self.buckets):  # in readiness order
+        for b in self._update_order():
             self._finish_reduce(b)
             for name, meth in self.optim_methods.items():
                 for (bb, lo, hi) in self._method_shard_ranges[name]:
@@ -317,6 +317,11 @@ class DistriOptimizer(BaseOptimizer):
                 meth.grad_scale = 1.0 / self.world
         self.flat.mark_shadow_fresh()
         self._first_iter = False
+
+    def _update_order(self):
+        """Buckets in the order their shard update + all-gather is issued: readiness order (the
+        reverse of the arena layout, which is backward order)."""
+        return list(reversed(self.buckets))
 
     def _wait_all_gathers(self):
         for b in self.buckets:
@@ -360,3 +365,55 @@ class DistriOptimizer(BaseOptimizer):
         if self.sharded:
             save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite)
         comm.barrier()
+
+
+class ParallelOptimizer(DistriOptimizer):
+    """Layer-wise overlapped data parallelism (``DL/optim/ParallelOptimizer.scala:42-791``).
+
+    The reference pushes each layer group's gradient as soon as its backward finishes (parameters
+    split into ``parameterBlocks`` = 10 groups), aggregates and updates the groups in PRIORITY
+    order and lets the next forward start on a layer as soon as its weights are fetched.  Default
+    priority = execution order (the first layer of the forward is highest, ``defaultPrioritize``
+    675-683); ``setPriorities({module_name: priority})`` overrides it.
+
+    Here: the flat arena is cut into ``parameter_blocks`` RCCL buckets; reduce-scatters launch from
+    the backward hooks as each bucket completes; shard updates and all-gathers are then issued in
+    descending bucket priority (a bucket's priority = the highest of its modules), so the buckets
+    the next forward needs first are gathered first and the forward's per-layer wait (pre-forward
+    hook) releases as early as possible.  Per-sub-module OptimMethods (``setOptimMethods`` by
+    module name) are supported as in DistriOptimizer.
+    """
+
+    def __init__(self, model, training_set, criterion, optim_method=None, end_trigger=None, batch_size=32,
+                 parameter_blocks: int = 10, bigdl_type="float"):
+        super().__init__(model, training_set, criterion, optim_method, end_trigger, batch_size, bigdl_type)
+        self.parameter_blocks = max(1, int(parameter_blocks))
+        self._priorities: Optional[Dict[str, int]] = None
+
+    def setPriorities(self, priorities: Dict[str, int]):
+        self._priorities = dict(priorities)
+        return self
+
+    set_priorities = setPriorities
+
+    def _default_priorities(self) -> Dict[str, int]:
+        order = [m for m in self.model.flattened_modules() if m.parameters() and m.parameters()[0]]
+        n = len(order)
+        return {m.get_name(): n - i for i, m in enumerate(order)}
+
+    def _setup_model(self):
+        total = 0
+        for w in (self.model.parameters() or ([], []))[0]:
+            total += w.numel()
+        per = (total + self.parameter_blocks - 1) // self.parameter_blocks
+        self.bucket_bytes = max(per * 4, 1 << 20)
+        super()._setup_model()
+        prio = self._default_priorities()
+        if self._priorities:
+            prio.update(self._priorities)
+        self._bucket_prio = {}
+        for b in self.buckets:
+            self._bucket_prio[b.idx] = max((prio.get(m.get_name(), 0) for m in b.modules), default=0)
+
+    def _update_order(self):
+        return sorted(self.buckets, key=lambda b: (-self._bucket_prio.get(b.idx, 0), -b.idx))

@@ -39,7 +39,7 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from bigdl.utils import config
-    config.set_property("bigdl.comm.sharded", mode == "sharded")
+    config.set_property("bigdl.comm.sharded", mode in ("sharded", "parallel"))
     config.set_property("bigdl.comm.dtype", comm_dtype)
     config.set_property("bigdl.comm.bucketMB", 0.0005)  # several buckets even for a tiny model
     from bigdl.utils.engine import Engine
@@ -51,8 +51,14 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     model = _model()
     x, y = _data()
     per = x.shape[0] // world
-    opt = DistriOptimizer(model, [MiniBatch(x[:per], y[:per])], ClassNLLCriterion(),
-                          SGD(learningrate=0.1, momentum=0.9, dampening=0.0, weightdecay=1e-3))
+    sgd = SGD(learningrate=0.1, momentum=0.9, dampening=0.0, weightdecay=1e-3)
+    if mode == "parallel":
+        from bigdl.parallel import ParallelOptimizer
+        opt = ParallelOptimizer(model, [MiniBatch(x[:per], y[:per])], ClassNLLCriterion(), sgd, parameter_blocks=3)
+        last = [m for m in model.modules if m.parameters() and m.parameters()[0]][-1]
+        opt.setPriorities({last.get_name(): 100})
+    else:
+        opt = DistriOptimizer(model, [MiniBatch(x[:per], y[:per])], ClassNLLCriterion(), sgd)
     opt.prepare()
     for step in range(4):
         xs = x[rank * per:(rank + 1) * per]
@@ -83,7 +89,8 @@ def _reference_weights():
     return torch.cat([p.reshape(-1) for p in model.parameters()[0]])
 
 
-@pytest.mark.parametrize("mode,comm_dtype", [("sharded", "fp32"), ("replicated", "fp32"), ("sharded", "bf16")])
+@pytest.mark.parametrize("mode,comm_dtype", [("sharded", "fp32"), ("replicated", "fp32"), ("sharded", "bf16"),
+                                             ("parallel", "fp32")])
 def test_distri_matches_serial(mode, comm_dtype):
     ref = _reference_weights()
     ctx = mp.get_context("spawn")
