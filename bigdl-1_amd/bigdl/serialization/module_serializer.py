@@ -398,6 +398,14 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
     if isinstance(m, BatchNormalization):
         for k in ("runningMean", "runningVar", "saveMean", "saveStd"):
             _set_attr(ctx, mp.attr[k], getattr(m, k))
+    elif getattr(m, "_buffer_names", None):
+        # other non-trainable state (e.g. the int8 weights + scales of quantized layers, the
+        # reference's QuantizedTensor parameters) as extra attributes; readers that do not know
+        # them ignore unknown attribute names
+        for k in m._buffer_names:
+            v = getattr(m, k, None)
+            if isinstance(v, torch.Tensor):
+                _set_attr(ctx, mp.attr[_BUF + k], v)
     if isinstance(m, Graph):
         names = {}
         for n in m.forward_order:
@@ -418,6 +426,9 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
         for w in p[0]:
             mp.parameters.add().CopyFrom(_reset(_tensor_to_pb(ctx, w)))
     return mp
+
+
+_BUF = "buffer:"
 
 
 def _instantiate(cls, attrs: dict):
@@ -475,6 +486,11 @@ def _module_from_pb(ctx: _DeCtx, mp):
             t = attrs.get(k)
             if isinstance(t, torch.Tensor):
                 getattr(m, k).copy_(t.reshape(getattr(m, k).shape))
+    for k, t in attrs.items():
+        if k.startswith(_BUF) and isinstance(t, torch.Tensor):
+            dst = getattr(m, k[len(_BUF):], None)
+            if isinstance(dst, torch.Tensor) and dst.numel() == t.numel():
+                dst.copy_(t.reshape(dst.shape).to(dst.dtype))
     if mp.hasParameters and len(mp.parameters):
         p = m.parameters()
         if p is not None:

@@ -286,8 +286,27 @@ def save_torch_file(obj, path: str, over_write: bool = False):
         f.write(w.bytes())
 
 
+def _chain_to_sequential(module):
+    """Torch7 has no graph container: a Graph whose nodes form one chain is written as the
+    equivalent ``nn.Sequential`` (input placeholders dropped)."""
+    from ..nn.graph import Graph, _InputLayer
+    from ..nn.containers import Sequential
+    if not isinstance(module, Graph) or len(module.inputs) != 1 or len(module.outputs_nodes) != 1:
+        return module
+    order = module.forward_order
+    for a, b in zip(order, order[1:]):
+        if b.prev_nodes != [a] or a.next_nodes != [b] or any(b.prev_index):
+            return module
+    seq = Sequential()
+    seq.set_name(module.get_name())
+    for n in order:
+        if not isinstance(n.element, _InputLayer):
+            seq.add(n.element)
+    return seq
+
+
 def save_torch(module, path: str, over_write: bool = False):
-    save_torch_file(module, path, over_write)
+    save_torch_file(_chain_to_sequential(module), path, over_write)
 
 
 def load_torch(path: str):

@@ -106,3 +106,37 @@ def test_prediction_service_concurrent():
         t.join()
     for x, o in zip(xs, outs):
         torch.testing.assert_close(o, m.forward(x))
+
+
+def test_convert_model_cli_roundtrips(tmp_path):
+    """``ConvertModel`` CLI: bigdl → caffe → bigdl (+quantize) → torch, outputs preserved."""
+    import torch
+    from bigdl.nn import Sequential, SpatialConvolution, ReLU, SpatialMaxPooling, View, Linear
+    from bigdl.nn.module import Module
+    from bigdl.utils.convert_model import main
+    torch.manual_seed(0)
+    m = (Sequential().add(SpatialConvolution(3, 8, 3, 3)).add(ReLU()).add(SpatialMaxPooling(2, 2, 2, 2))
+         .add(View(8 * 3 * 3)).add(Linear(72, 5)))
+    m.evaluate()
+    x = torch.randn(2, 3, 8, 8)
+    ref = m.forward(x).clone()
+    src = str(tmp_path / "m.bigdl")
+    m.saveModule(src, over_write=True)
+    cm = str(tmp_path / "m.caffemodel")
+    assert main(["--from", "bigdl", "--to", "caffe", "--input", src, "--output", cm]) == 0
+    back = str(tmp_path / "back.bigdl")
+    assert main(["--from", "caffe", "--to", "bigdl", "--prototxt", str(tmp_path / "m.prototxt"), "--input", cm,
+                 "--output", back]) == 0
+    m2 = Module.loadModule(back)
+    m2.evaluate()
+    torch.testing.assert_close(m2.forward(x), ref, rtol=1e-5, atol=1e-5)
+    t7 = str(tmp_path / "m.t7")
+    assert main(["--from", "bigdl", "--to", "torch", "--input", back, "--output", t7]) == 0
+    m3 = Module.loadTorch(t7)
+    m3.evaluate()
+    torch.testing.assert_close(m3.forward(x), ref, rtol=1e-5, atol=1e-5)
+    q = str(tmp_path / "q.bigdl")
+    assert main(["--from", "bigdl", "--to", "bigdl", "--input", src, "--output", q, "--quantize", "true"]) == 0
+    mq = Module.loadModule(q)
+    mq.evaluate()
+    assert (mq.forward(x) - ref).abs().max() < 0.1
