@@ -169,3 +169,34 @@ def test_image_kernel_matches_reference():
             out = NO.image_crop_flip_norm(src, oy, ox, fl, 12, 16, (1, 2, 3), (2, 3, 4), to_rgb, dt)
             ref = R.image_crop_flip_norm(src, oy, ox, fl, 12, 16, (1, 2, 3), (2, 3, 4), to_rgb, dt)
             torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_pyspark_dataset_modules(tmp_path):
+    """``bigdl.dataset.{mnist,movielens,news20,sentence,base}`` on synthetic local files."""
+    import gzip
+    import struct
+    import numpy as np
+    from bigdl.dataset import mnist, movielens, news20, sentence, base
+    imgs = (np.arange(3 * 28 * 28) % 256).astype(np.uint8)
+    with gzip.open(tmp_path / "train-images-idx3-ubyte.gz", "wb") as f:
+        f.write(struct.pack(">IIII", 2051, 3, 28, 28) + imgs.tobytes())
+    with gzip.open(tmp_path / "train-labels-idx1-ubyte.gz", "wb") as f:
+        f.write(struct.pack(">II", 2049, 3) + bytes([7, 0, 9]))
+    x, y = mnist.read_data_sets(str(tmp_path), "train")
+    assert x.shape == (3, 28, 28, 1) and list(y) == [7, 0, 9]
+    with open(tmp_path / "train-images-idx3-ubyte.gz", "rb") as f:
+        assert mnist.extract_images(f).shape == (3, 28, 28, 1)
+    (tmp_path / "ml-1m").mkdir()
+    (tmp_path / "ml-1m" / "ratings.dat").write_text("1::10::5::978\n2::20::3::979\n")
+    assert movielens.get_id_ratings(str(tmp_path)).tolist() == [[1, 10, 5], [2, 20, 3]]
+    d = tmp_path / "news" / "20news-18828"
+    for c, docs in (("alt.atheism", ["1", "2"]), ("sci.space", ["5"])):
+        (d / c).mkdir(parents=True)
+        for n in docs:
+            (d / c / n).write_text(f"text {c} {n}")
+    texts = news20.get_news20(str(tmp_path / "news"))
+    assert [t[1] for t in texts] == [1, 1, 2]
+    assert sentence.sentences_split("Hi there. How are you? Fine!") == ["Hi there.", "How are you?", "Fine!"]
+    assert sentence.sentence_tokenizer("a, b") == ["a", ",", "b"]
+    with pytest.raises(FileNotFoundError):
+        base.maybe_download("nope.gz", str(tmp_path), "http://example/nope.gz")
