@@ -6,7 +6,7 @@ from .trigger import (Trigger, EveryEpoch, SeveralIteration, MaxEpoch, MaxIterat
                       TriggerOr)
 from .validation import (ValidationMethod, ValidationResult, AccuracyResult, LossResult, Top1Accuracy, Top5Accuracy,
                          TreeNNAccuracy, Loss, MAE, HitRatio, NDCG, MeanAveragePrecision,
-                         MeanAveragePrecisionObjectDetection)
+                         MeanAveragePrecisionObjectDetection, PrecisionRecallAUC, PRAUCResult, EvaluateMethods)
 from .regularizer import Regularizer, L1L2Regularizer, L1Regularizer, L2Regularizer
 from .metrics import Metrics
 from .optimizer import BaseOptimizer, LocalOptimizer, Optimizer

@@ -256,11 +256,96 @@ class MeanAveragePrecisionObjectDetection(ValidationMethod):
         return float(np.mean(aps)) if aps else 0.0
 
 
+class PRAUCResult(ValidationResult):
+    """(score, label) pairs; ``result()`` = area under the precision-recall curve
+    (``PrecisionRecallAUC.scala``: scores sorted descending, trapezoids in (recall, precision)
+    starting from (0, 1), stopping once every positive is recalled)."""
+
+    gather = True  # variable-size: merged by all-gather, not by a fixed-size all-reduce
+
+    def __init__(self, results=None):
+        self.results = list(results or [])
+
+    def result(self):
+        srt = sorted(self.results, key=lambda r: r[0], reverse=True)
+        total_pos = sum(1 for _, t in srt if t == 1.0)
+        tp = fp = 0.0
+        auc, prev_p, prev_r = 0.0, 1.0, 0.0
+        i = 0
+        while tp != total_pos:
+            if srt[i][1] == 1.0:
+                tp += 1
+            else:
+                fp += 1
+            prec, rec = tp / (tp + fp), tp / total_pos
+            auc += (rec - prev_r) * (prec + prev_p)
+            prev_r, prev_p = rec, prec
+            i += 1
+        return auc / 2, len(self.results)
+
+    def __add__(self, o):
+        return PRAUCResult(self.results + o.results)
+
+    def __repr__(self):
+        r, n = self.result()
+        return f"Precision Recall AUC is {r} on {n}"
+
+
+class PrecisionRecallAUC(ValidationMethod):
+    """Binary PR-AUC over (score, 0/1 label) tensors of the same size."""
+
+    def __call__(self, output, target):
+        o = output.detach().float().reshape(-1).cpu().tolist()
+        t = target.detach().float().reshape(-1).cpu().tolist()
+        if not o or not t:
+            raise ValueError("the output and target should not be empty")
+        return PRAUCResult(list(zip(o, t)))
+
+    def format(self):
+        return "PrecisionRecallAUC"
+
+
+class EvaluateMethods:
+    """``EvaluateMethods.calcAccuracy`` / ``calcTop5Accuracy``: (correct, count) for a batch of
+    scores (N, C) or one score vector (C) against 1-based targets."""
+
+    @staticmethod
+    def _rows(output, target):
+        o = output.detach().float()
+        t = target.detach().reshape(-1).long()
+        if o.dim() == 1:
+            if t.numel() != 1:
+                raise ValueError("a single score vector needs a single target")
+            o = o.unsqueeze(0)
+        elif o.dim() != 2:
+            raise ValueError("output must be 1-D or 2-D")
+        return o, t
+
+    @staticmethod
+    def calcAccuracy(output, target):
+        o, t = EvaluateMethods._rows(output, target)
+        return int(((o.argmax(1) + 1).cpu() == t.cpu()).sum()), o.shape[0]
+
+    @staticmethod
+    def calcTop5Accuracy(output, target):
+        o, t = EvaluateMethods._rows(output, target)
+        top = o.topk(min(5, o.shape[1]), 1).indices.cpu() + 1
+        return int((top == t.cpu()[:, None]).any(1).sum()), o.shape[0]
+
+
 def allreduce_results(results):
-    """Merge per-rank results (X12): one all-reduce of the concatenated small vectors."""
+    """Merge per-rank results (X12): one all-reduce of the concatenated small vectors; variable-size
+    results (``gather = True``, e.g. PR-AUC pairs) are all-gathered and summed instead."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
         return results
+    if any(getattr(r, "gather", False) for r in results):
+        gathered = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, results)
+        out = list(gathered[0])
+        for other in gathered[1:]:
+            out = [a + b for a, b in zip(out, other)]
+        return out
     vecs = [r.to_vector() for r in results]
     lens = [len(v) for v in vecs]
     flat = torch.tensor([x for v in vecs for x in v], dtype=torch.float64)

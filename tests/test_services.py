@@ -140,3 +140,21 @@ def test_convert_model_cli_roundtrips(tmp_path):
     mq = Module.loadModule(q)
     mq.evaluate()
     assert (mq.forward(x) - ref).abs().max() < 0.1
+
+
+def test_precision_recall_auc_and_evaluate_methods():
+    import torch
+    from bigdl.optim import PrecisionRecallAUC, EvaluateMethods
+    # perfect ranking → AUC 1; reference PRAUCResult semantics (trapezoids from (0, 1))
+    r = PrecisionRecallAUC()(torch.tensor([0.9, 0.8, 0.3, 0.1]), torch.tensor([1.0, 1.0, 0.0, 0.0]))
+    assert abs(r.result()[0] - 1.0) < 1e-6 and r.result()[1] == 4
+    r2 = PrecisionRecallAUC()(torch.tensor([0.9, 0.8, 0.3]), torch.tensor([0.0, 1.0, 1.0]))
+    # steps: (P=0, R=0) → (1/2, 1/2) → (2/3, 1): 0.5·(0 + 1)/2 ... computed by hand:
+    # i1 neg: p=0, r=0 → area += 0; i2 pos: p=.5, r=.5 → += .5·(.5+0); i3 pos: p=2/3, r=1 → += .5·(2/3+.5)
+    exp = (0.5 * 0.5 + 0.5 * (2 / 3 + 0.5)) / 2
+    assert abs(r2.result()[0] - exp) < 1e-6
+    merged = r + r2
+    assert merged.result()[1] == 7
+    out = torch.tensor([[0.1, 0.7, 0.2], [0.5, 0.2, 0.3]])
+    assert EvaluateMethods.calcAccuracy(out, torch.tensor([2.0, 3.0])) == (1, 2)
+    assert EvaluateMethods.calcTop5Accuracy(out, torch.tensor([2.0, 3.0])) == (2, 2)
