@@ -9,3 +9,5 @@ from .layers import *  # noqa: F401,F403
 from .criterion import *  # noqa: F401,F403
 from .initialization_method import *  # noqa: F401,F403
 Module = AbstractModule
+from .int8_convertible import MklInt8Convertible, calc_tensor_scale, install as _install_int8
+_install_int8()

@@ -406,6 +406,14 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
             v = getattr(m, k, None)
             if isinstance(v, torch.Tensor):
                 _set_attr(ctx, mp.attr[_BUF + k], v)
+    st = m.__dict__.get("_int8_state")
+    if st is not None and (st["in"] or st["out"] or st["w"] or st["inMask"] or st["outMask"] or st["wMask"]):
+        # MklInt8Convertible state (bigdl.proto fields 17-23)
+        mp.isMklInt8Enabled = True
+        mp.inputDimMasks, mp.outputDimMasks, mp.weightDimMasks = st["inMask"], st["outMask"], st["wMask"]
+        for field, key in ((mp.inputScales, "in"), (mp.outputScales, "out"), (mp.weightScales, "w")):
+            for sc in st[key]:
+                _set_attr(ctx, field.add(), [float(x) for x in sc])
     if isinstance(m, Graph):
         names = {}
         for n in m.forward_order:
@@ -474,6 +482,13 @@ def _module_from_pb(ctx: _DeCtx, mp):
     m = _instantiate(cls, attrs)
     if mp.name:
         m.set_name(mp.name)
+    if mp.isMklInt8Enabled or len(mp.inputScales) or len(mp.outputScales) or len(mp.weightScales):
+        m.setInputDimMask(mp.inputDimMasks)
+        m.setOutputDimMask(mp.outputDimMasks)
+        m.setWeightDimMask(mp.weightDimMasks)
+        m.setInputScales([list(_get_attr(ctx, a)) for a in mp.inputScales])
+        m.setOutputScales([list(_get_attr(ctx, a)) for a in mp.outputScales])
+        m.setWeightScales([list(_get_attr(ctx, a)) for a in mp.weightScales])
     if isinstance(m, Container):
         for sub in mp.subModules:
             m.add(_module_from_pb(ctx, sub))

@@ -83,3 +83,33 @@ def test_quantized_model_gpu_matches_cpu():
     qg = q.cuda()
     yg = qg.forward(x.cuda()).float().cpu()
     torch.testing.assert_close(yg, ycpu, rtol=1e-3, atol=1e-3)
+
+
+def test_mkl_int8_convertible_calc_scales_and_serialization(tmp_path):
+    """``MklInt8Convertible.calcScales`` on a Sequential (``MklInt8ConvertibleSpec``): input/output/
+    weight max-abs per mask; the scales survive a .bigdl round trip (proto fields 17-23)."""
+    import torch
+    from bigdl.nn import Sequential, Linear, ReLU, SpatialConvolution, View
+    from bigdl.nn.module import Module
+    from bigdl.nn.int8_convertible import calc_tensor_scale
+    torch.manual_seed(0)
+    m = Sequential().add(SpatialConvolution(2, 4, 3, 3)).add(ReLU()).add(View(4 * 3 * 3)).add(Linear(36, 5))
+    conv, lin = m.modules[0], m.modules[3]
+    conv.setWeightDimMask(1)
+    conv.setOutputDimMask(2)
+    x = torch.randn(3, 2, 5, 5)
+    m.evaluate()
+    m.forward(x)
+    m.calcScales(x)
+    assert m.getInputScales() == [[float(x.abs().max())]]
+    assert conv.getWeightScales()[0] == [float(v) for v in conv.weight.reshape(4, -1).abs().amax(1)]
+    assert len(conv.getOutputScales()[0]) == 4  # per output channel (mask bit of dim 1)
+    assert lin.getInputScales()[0] == [float(m.modules[2].output.abs().max())]
+    assert calc_tensor_scale(torch.tensor([[1.0, -3.0], [2.0, 0.5]]), 3) == [1.0, 3.0, 2.0, 0.5]
+    assert calc_tensor_scale(torch.tensor([[1.0, -3.0], [2.0, 0.5]]), 2) == [2.0, 3.0]
+    p = str(tmp_path / "s.bigdl")
+    m.saveModule(p, over_write=True)
+    m2 = Module.loadModule(p)
+    assert m2.modules[0].getWeightScales() == conv.getWeightScales()
+    assert m2.modules[0].getWeightDimMask() == 1 and m2.modules[0].getOutputDimMask() == 2
+    assert m2.getInputScales() == m.getInputScales()
