@@ -112,3 +112,26 @@ def test_bf16_truncate_golden():
     from bigdl.parallel.comm import bf16_truncate
     t = bf16_truncate(torch.tensor([1.111111]))
     assert float(t.float()) == 1.109375
+
+
+def test_launcher_runs_ranks(tmp_path):
+    """``python -m bigdl.launch --nproc 3 script``: env:// rendezvous, every rank joins, exit 0."""
+    import subprocess
+    child = tmp_path / "child.py"
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bigdl-1_amd")
+    child.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from bigdl.utils.engine import Engine\n"
+        "Engine.init(device='cpu', dist=True, backend='gloo')\n"
+        "import torch, torch.distributed as dist\n"
+        "t = torch.tensor([float(Engine.rank() + 1)])\n"
+        "dist.all_reduce(t)\n"
+        "assert float(t) == 6.0\n"
+        "print('rank', Engine.rank(), 'ok', flush=True)\n"
+        "Engine.shutdown()\n")
+    env = dict(os.environ, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-m", "bigdl.launch", "--nproc", "3", "--no-numa-bind", str(child)],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert sorted(l for l in r.stdout.splitlines() if l.startswith("rank")) == ["rank 0 ok", "rank 1 ok", "rank 2 ok"]
