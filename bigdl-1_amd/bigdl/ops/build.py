@@ -81,12 +81,37 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = True) -> str:
     return out
 
 
+RT_CSRC = os.path.join(os.path.dirname(HERE), "runtime", "csrc")
+RT_LIB = os.path.join(os.path.dirname(HERE), "runtime", "lib", "libbigdl_runtime.so")
+
+
+def build_runtime(verbose: bool = True, debug: bool = False) -> str:
+    """Host-only native runtime (threaded batch loader, …): ``runtime/csrc/*.cpp`` → g++ -O3."""
+    srcs = sorted(glob.glob(os.path.join(RT_CSRC, "*.cpp")))
+    os.makedirs(os.path.dirname(RT_LIB), exist_ok=True)
+    if not srcs:
+        return RT_LIB
+    if os.path.exists(RT_LIB) and all(os.path.getmtime(s) <= os.path.getmtime(RT_LIB) for s in srcs):
+        return RT_LIB
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-fvisibility=hidden", "-o", RT_LIB] + srcs
+    if debug:
+        cmd[1:1] = ["-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"runtime build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[bigdl.ops.build] {RT_LIB} ({len(srcs)} sources, host)")
+    return RT_LIB
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--debug", action="store_true")
     a = ap.parse_args()
     build(a.jobs, a.debug)
+    build_runtime(debug=a.debug)
 
 
 if __name__ == "__main__":
