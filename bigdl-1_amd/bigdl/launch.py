@@ -79,7 +79,23 @@ def rank_env(rank: int, world: int, addr: str, port: int, base: Optional[dict] =
 
 
 def launch(nproc: int, cmd: List[str], master_addr: str = "127.0.0.1", master_port: int = 0,
-           bind_numa: bool = True) -> int:
+           bind_numa: bool = True, max_restarts: int = 0) -> int:
+    """Run ``nproc`` ranks; if any rank fails, stop the others and relaunch ALL ranks (up to
+    ``max_restarts`` times, SURVEY §5.3 supervisor).  ``BIGDL_RESTART_COUNT`` tells the script it is
+    a restart (resume from the latest checkpoint, ``Optimizer`` does this when a checkpoint path is
+    set)."""
+    rc = 0
+    for attempt in range(max_restarts + 1):
+        os.environ["BIGDL_RESTART_COUNT"] = str(attempt)
+        rc = _launch_once(nproc, cmd, master_addr, master_port, bind_numa)
+        if rc in (0, 130):
+            return rc
+        print(f"[bigdl.launch] a rank failed with code {rc}; "
+              f"{'restarting all ranks' if attempt < max_restarts else 'giving up'}", file=sys.stderr, flush=True)
+    return rc
+
+
+def _launch_once(nproc: int, cmd: List[str], master_addr: str, master_port: int, bind_numa: bool) -> int:
     port = master_port or _free_port()
     numa = gpu_numa_nodes() if bind_numa else {}
     procs = []
@@ -123,6 +139,7 @@ def main(argv=None) -> int:
     ap.add_argument("--master-addr", default="127.0.0.1")
     ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--no-numa-bind", action="store_true")
+    ap.add_argument("--max-restarts", type=int, default=0, help="relaunch all ranks after a failure")
     ap.add_argument("script")
     ap.add_argument("args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
@@ -131,7 +148,7 @@ def main(argv=None) -> int:
         import torch
         n = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
     cmd = [sys.executable, a.script] + a.args if a.script.endswith(".py") else [a.script] + a.args
-    return launch(n, cmd, a.master_addr, a.master_port, not a.no_numa_bind)
+    return launch(n, cmd, a.master_addr, a.master_port, not a.no_numa_bind, a.max_restarts)
 
 
 if __name__ == "__main__":

@@ -354,3 +354,31 @@ class MaskedSelect(TensorModule):
         g = torch.zeros_like(input[1], dtype=gradOutput.dtype)
         g[input[2].bool()] = gradOutput
         return Table(g, torch.zeros_like(input[2]))
+
+
+class FaultInject(Identity):
+    """Test-only fault injection (the reference's ``ExceptionTest``, ``TS/utils/TestUtils.scala:126-155``):
+    a pass-through that raises on its ``fail_at``-th forward (1-based) — or on every forward from
+    then on when ``once`` is False — to exercise the optimizer retry loop and the launcher's
+    restart path.  The counter is class-wide per ``key`` so it survives module reloads from a
+    checkpoint within one process."""
+
+    _counts = {}
+
+    def __init__(self, fail_at: int = 1, once: bool = True, key: str = "default", bigdl_type="float"):
+        super().__init__()
+        self.fail_at, self.once, self.key = fail_at, once, key
+
+    def updateOutput(self, input):
+        n = FaultInject._counts.get(self.key, 0) + 1
+        FaultInject._counts[self.key] = n
+        if n == self.fail_at or (not self.once and n >= self.fail_at):
+            raise RuntimeError(f"FaultInject[{self.key}]: injected failure at forward {n}")
+        return input
+
+    @staticmethod
+    def reset(key: str = None):
+        if key is None:
+            FaultInject._counts.clear()
+        else:
+            FaultInject._counts.pop(key, None)

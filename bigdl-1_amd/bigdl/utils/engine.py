@@ -73,7 +73,10 @@ class Engine:
                 import torch.distributed as tdist
                 if not tdist.is_initialized():
                     be = backend or ("nccl" if _S.device.type == "cuda" else "gloo")
-                    kw = {}
+                    import datetime
+                    # collective watchdog: a hung collective becomes an error after
+                    # this many seconds, which the optimizer's retry loop / the launcher can handle
+                    kw = {"timeout": datetime.timedelta(seconds=float(config.get_property("bigdl.comm.timeout")))}
                     if be == "nccl":
                         kw["device_id"] = _S.device
                     tdist.init_process_group(backend=be, **kw)

@@ -135,3 +135,23 @@ def test_launcher_runs_ranks(tmp_path):
                        capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert sorted(l for l in r.stdout.splitlines() if l.startswith("rank")) == ["rank 0 ok", "rank 1 ok", "rank 2 ok"]
+
+
+def test_launcher_restarts_all_ranks(tmp_path):
+    """``--max-restarts``: a rank that fails on the first attempt makes the launcher stop the others
+    and relaunch every rank; the second attempt (BIGDL_RESTART_COUNT=1) succeeds."""
+    import subprocess
+    child = tmp_path / "child.py"
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bigdl-1_amd")
+    child.write_text(
+        "import os, sys, time\n"
+        "if os.environ['BIGDL_RESTART_COUNT'] == '0' and os.environ['RANK'] == '1':\n"
+        "    sys.exit(3)\n"
+        "if os.environ['BIGDL_RESTART_COUNT'] == '0':\n"
+        "    time.sleep(30)\n"
+        "print('attempt', os.environ['BIGDL_RESTART_COUNT'], 'rank', os.environ['RANK'], flush=True)\n")
+    env = dict(os.environ, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-m", "bigdl.launch", "--nproc", "2", "--no-numa-bind", "--max-restarts", "1",
+                        str(child)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert sorted(r.stdout.split("\n"))[-2:] == ["attempt 1 rank 0", "attempt 1 rank 1"]

@@ -158,3 +158,24 @@ def test_precision_recall_auc_and_evaluate_methods():
     out = torch.tensor([[0.1, 0.7, 0.2], [0.5, 0.2, 0.3]])
     assert EvaluateMethods.calcAccuracy(out, torch.tensor([2.0, 3.0])) == (1, 2)
     assert EvaluateMethods.calcTop5Accuracy(out, torch.tensor([2.0, 3.0])) == (2, 2)
+
+
+def test_retry_from_checkpoint_after_injected_fault(tmp_path):
+    """an injected failure mid-training is retried from the latest checkpoint
+    (``DistriOptimizer.scala:881-963`` retry loop; fault injection = ``ExceptionTest``)."""
+    import torch
+    from bigdl.nn import Sequential, Linear, ReLU, LogSoftMax, ClassNLLCriterion, FaultInject
+    from bigdl.optim import SGD, MaxIteration, SeveralIteration
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import Sample
+    FaultInject.reset("retry_test")
+    torch.manual_seed(0)
+    m = (Sequential().add(Linear(4, 8)).add(FaultInject(fail_at=5, key="retry_test")).add(ReLU())
+         .add(Linear(8, 3)).add(LogSoftMax()))
+    data = [Sample(torch.randn(4), torch.tensor(float(i % 3 + 1))) for i in range(32)]
+    opt = LocalOptimizer(m, data, ClassNLLCriterion(), SGD(learningrate=0.1), MaxIteration(8), batch_size=8)
+    opt.setCheckpoint(str(tmp_path), SeveralIteration(1))
+    trained = opt.optimize()
+    assert opt.state["neval"] >= 8
+    assert FaultInject._counts["retry_test"] >= 8  # the failure happened and training went on
+    assert trained is not None
