@@ -132,3 +132,23 @@ def test_ir_resnet_inference_native():
         y = ir.forward(_cl(x.to(dev).to(torch.bfloat16))).float().cpu()
     assert (y - ref).abs().max().item() < 0.1
     assert (y.argmax(1) == ref.argmax(1)).float().mean().item() >= 0.9
+
+
+def test_native_loader_to_device():
+    """C++ batch loader → pinned slots → async H2D on a side stream (bf16, NHWC memory)."""
+    import numpy as np
+    from bigdl.runtime import NativeBatchLoader
+    x = np.random.RandomState(0).randint(0, 256, size=(40, 16, 16, 3)).astype(np.uint8)
+    y = np.arange(40, dtype=np.float32) + 1
+    ld = NativeBatchLoader(x, y, 8, crop=(16, 16), pad=2, flip=True, train=True, dtype=torch.bfloat16,
+                           layout="NHWC", mean=[125.0] * 3, std=[60.0] * 3, threads=4, prefetch=3, device=dev)
+    seen = []
+    for _ in range(10):
+        b = ld.next_batch()
+        xb = b.getInput()
+        assert xb.is_cuda and xb.dtype == torch.bfloat16 and xb.shape == (8, 3, 16, 16)
+        assert xb.is_contiguous(memory_format=torch.channels_last)
+        seen.append(b.getTarget().cpu())
+    torch.cuda.synchronize()
+    assert sorted(torch.cat(seen[:5]).tolist()) == list(range(1, 41))
+    ld.close()
