@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--model", default="resnet50", choices=["resnet50"])
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--comm-dtype", default=os.environ.get("BIGDL_COMM_DTYPE", "fp32"))
+    ap.add_argument("--force-distri", action="store_true",
+                    help="use the DistriOptimizer (RCCL path) even at world size 1 (path validation)")
     args = ap.parse_args()
 
     import torch
@@ -47,7 +49,7 @@ def main():
     config.set_property("bigdl.comm.dtype", args.comm_dtype)
     from bigdl.utils.engine import Engine
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    Engine.init(dist=world > 1)
+    Engine.init(dist=world > 1 or args.force_distri)
     dev = Engine.device()
     rank = Engine.rank()
 
@@ -71,7 +73,7 @@ def main():
     y = (torch.randint(0, 1000, (B,), generator=g) + 1).float().to(dev)
     batch = MiniBatch(x, y)
 
-    if world > 1:
+    if world > 1 or args.force_distri:
         from bigdl.parallel import DistriOptimizer
         opt = DistriOptimizer(model, [batch], crit, sgd, batch_size=B)
     else:

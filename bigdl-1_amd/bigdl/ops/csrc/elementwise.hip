@@ -169,11 +169,20 @@ BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow,
     else if (!M && SH) SGD_LAUNCH(false, false, false, true, false);
     else SGD_LAUNCH(false, false, false, false, false);
   } else {
-    if (M && NS && F) SGD_LAUNCH(true, true, true, true, true);
-    else if (M && NS) SGD_LAUNCH(true, true, false, true, true);
-    else if (M && F) SGD_LAUNCH(true, false, true, true, true);
-    else if (M) SGD_LAUNCH(true, false, false, true, true);
-    else SGD_LAUNCH(false, false, false, true, true);
+    // the shadow flag must follow the pointer: a sharded fp32-wire update passes no shadow
+    if (SH) {
+      if (M && NS && F) SGD_LAUNCH(true, true, true, true, true);
+      else if (M && NS) SGD_LAUNCH(true, true, false, true, true);
+      else if (M && F) SGD_LAUNCH(true, false, true, true, true);
+      else if (M) SGD_LAUNCH(true, false, false, true, true);
+      else SGD_LAUNCH(false, false, false, true, true);
+    } else {
+      if (M && NS && F) SGD_LAUNCH(true, true, true, false, true);
+      else if (M && NS) SGD_LAUNCH(true, true, false, false, true);
+      else if (M && F) SGD_LAUNCH(true, false, true, false, true);
+      else if (M) SGD_LAUNCH(true, false, false, false, true);
+      else SGD_LAUNCH(false, false, false, false, true);
+    }
   }
   BIGDL_CHECK_LAUNCH();
 }

@@ -152,3 +152,26 @@ def test_native_loader_to_device():
     torch.cuda.synchronize()
     assert sorted(torch.cat(seen[:5]).tolist()) == list(range(1, 41))
     ld.close()
+
+
+@pytest.mark.parametrize("shadow", [False, True])
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_sgd_per_element_decay_with_and_without_shadow(shadow, nesterov):
+    """Fused SGD with per-element weight decays (folded L2 regularizers), with and without the bf16
+    shadow output — the sharded fp32-wire DistriOptimizer update passes no shadow."""
+    from bigdl.ops import reference as R
+    N = _N()
+    torch.manual_seed(0)
+    n = 4096 + 64
+    w = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    buf = torch.randn(n, device=dev)
+    wds = torch.rand(n, device=dev)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=dev) if shadow else None
+    w_ref, buf_ref = w.clone(), buf.clone()
+    R.sgd_step(w_ref, g.clone(), buf_ref, 0.1, 0.9, 0.0, 1e-3, nesterov, False, 0.5, None, None, wds.clone())
+    assert N.sgd_step(w, g, buf, 0.1, 0.9, 0.0, 1e-3, nesterov, False, 0.5, sh, None, wds) is not NotImplemented
+    torch.testing.assert_close(w, w_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(buf, buf_ref, rtol=1e-5, atol=1e-6)
+    if shadow:
+        torch.testing.assert_close(sh, w.to(torch.bfloat16), rtol=0, atol=0)
