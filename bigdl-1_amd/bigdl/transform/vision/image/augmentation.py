@@ -473,3 +473,94 @@ class RandomTransformer(FeatureTransformer):
         if RNG.uniform(0, 1) < self.p:
             return self.t.transform(f)
         return f
+
+
+# ---------------------------------------------------------------------------------------------- SSD sampling
+def _jaccard(a, b) -> float:
+    ix1, iy1, ix2, iy2 = max(a[0], b[0]), max(a[1], b[1]), min(a[2], b[2]), min(a[3], b[3])
+    if ix2 <= ix1 or iy2 <= iy1:
+        return 0.0
+    inter = (ix2 - ix1) * (iy2 - iy1)
+    ua = (a[2] - a[0]) * (a[3] - a[1]) + (b[2] - b[0]) * (b[3] - b[1]) - inter
+    return inter / ua if ua > 0 else 0.0
+
+
+class BatchSampler:
+    """One SSD crop sampler (``label/roi/BatchSampler.scala``): up to ``max_sample`` boxes in
+    ``max_trials`` draws of scale ∈ [min_scale, max_scale] and aspect ratio ∈ [min, max] (clamped to
+    [scale², 1/scale²]) inside the unit box; a box is kept when some ground-truth box overlaps it
+    with Jaccard ∈ [min_overlap, max_overlap] (or always, without constraints)."""
+
+    def __init__(self, max_sample=1, max_trials=50, min_scale=1.0, max_scale=1.0, min_aspect_ratio=1.0,
+                 max_aspect_ratio=1.0, min_overlap=None, max_overlap=None):
+        if not (0 < min_scale <= max_scale <= 1):
+            raise ValueError("scales must satisfy 0 < minScale <= maxScale <= 1")
+        if not (0 < min_aspect_ratio <= 1 <= max_aspect_ratio):
+            raise ValueError("aspect ratios must satisfy 0 < min <= 1 <= max")
+        self.max_sample, self.max_trials = max_sample, max_trials
+        self.min_scale, self.max_scale = min_scale, max_scale
+        self.min_ar, self.max_ar = min_aspect_ratio, max_aspect_ratio
+        self.min_overlap, self.max_overlap = min_overlap, max_overlap
+
+    def _sample_box(self):
+
+        scale = RNG.uniform(self.min_scale, self.max_scale)
+        ratio = RNG.uniform(self.min_ar, self.max_ar)
+        ratio = min(max(ratio, scale * scale), 1.0 / scale / scale)
+        w, h = scale * ratio ** 0.5, scale / ratio ** 0.5
+        x1, y1 = RNG.uniform(0, 1 - w), RNG.uniform(0, 1 - h)
+        return (x1, y1, x1 + w, y1 + h)
+
+    def _ok(self, box, gt) -> bool:
+        if self.min_overlap is None and self.max_overlap is None:
+            return True
+        for g in gt:
+            o = _jaccard(box, g)
+            if (self.min_overlap is None or o >= self.min_overlap) and (self.max_overlap is None or o <= self.max_overlap):
+                return True
+        return False
+
+    def sample(self, gt, out: list):
+        found = 0
+        for _ in range(self.max_trials):
+            if found >= self.max_sample:
+                return
+            b = self._sample_box()
+            if self._ok(b, gt):
+                found += 1
+                out.append(b)
+
+    @staticmethod
+    def generate_batch_samples(gt, samplers) -> list:
+        boxes = []
+        for s in samplers:
+            s.sample(gt, boxes)
+        return boxes
+
+
+class RandomSampler(Crop):
+    """SSD training crop (``label/roi/RandomSampler.scala``): the seven default batch samplers
+    (whole image; scale ≥ 0.3, aspect ∈ [1/2, 2] with min Jaccard 0.1/0.3/0.5/0.7/0.9 to a
+    ground-truth box; max Jaccard 1.0), one of the sampled boxes picked uniformly, the image cropped
+    to it; follow with ``RoiProject`` to move the labels (``RandomSampler()`` in pyspark returns the
+    pair)."""
+
+    def __init__(self):
+        super().__init__(normalized=True, is_clip=True)
+        self.samplers = [BatchSampler(max_trials=1)] + [
+            BatchSampler(min_scale=0.3, min_aspect_ratio=0.5, max_aspect_ratio=2, min_overlap=o)
+            for o in (0.1, 0.3, 0.5, 0.7, 0.9)] + [
+            BatchSampler(min_scale=0.3, min_aspect_ratio=0.5, max_aspect_ratio=2, max_overlap=1.0)]
+
+    def box(self, f):
+
+        lab = f.get(ImageFeature.label)
+        gt = lab.bboxes.tolist() if hasattr(lab, "bboxes") else []
+        boxes = BatchSampler.generate_batch_samples(gt, self.samplers)
+        if not boxes:
+            return (0.0, 0.0, 1.0, 1.0)
+        return boxes[min(len(boxes) - 1, int(RNG.uniform(0, 1) * len(boxes)))]
+
+
+class PixelNormalize(PixelNormalizer):
+    """pyspark name of :class:`PixelNormalizer` (``data(i) - mean(i)``, means in H·W·C order)."""

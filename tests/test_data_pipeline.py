@@ -200,3 +200,43 @@ def test_pyspark_dataset_modules(tmp_path):
     assert sentence.sentence_tokenizer("a, b") == ["a", ",", "b"]
     with pytest.raises(FileNotFoundError):
         base.maybe_download("nope.gz", str(tmp_path), "http://example/nope.gz")
+
+
+def test_sequence_file_roundtrip_and_seqfilefolder(tmp_path):
+    """Hadoop SequenceFile container (Text key "name\\nlabel", Text value w/h + BGR bytes) as the
+    reference's ``BGRImgToLocalSeqFile`` writes it, read back by ``SeqFileFolder``."""
+    import numpy as np
+    from bigdl.dataset.seqfile import (BGRImgToLocalSeqFile, SeqFileFolder, read_sequence_file, write_vlong,
+                                       read_vlong)
+    import io
+    for v in (0, 5, -7, 127, -112, 128, 300, -1000, 2 ** 31, -(2 ** 40)):
+        b = io.BytesIO()
+        write_vlong(b, v)
+        b.seek(0)
+        assert read_vlong(b) == v
+    rng = np.random.RandomState(0)
+    items = [(rng.randint(0, 256, (5 + i, 7, 3)).astype(np.uint8), i % 3 + 1, f"img{i}") for i in range(9)]
+    files = BGRImgToLocalSeqFile(4, str(tmp_path / "part"), has_name=True)(items)
+    assert len(files) == 3
+    recs = list(SeqFileFolder.read(str(tmp_path)))
+    assert len(recs) == 9
+    for (img, lab, name), (i0, l0, n0) in zip(recs, items):
+        assert np.array_equal(img, i0) and lab == l0 and name == n0
+    frame = SeqFileFolder.files_to_image_frame(str(tmp_path), None, 3)
+    assert len(list(frame)) == 9
+    assert sum(1 for _ in read_sequence_file(files[0])) == 4
+
+
+def test_ssd_random_sampler():
+    import torch
+    from bigdl.transform.vision.image import ImageFeature, RandomSampler, RoiProject
+    from bigdl.transform.vision.image.label import RoiLabel
+    from bigdl.utils.random import RNG
+    RNG.setSeed(3)
+    for _ in range(10):
+        f = ImageFeature(image=torch.rand(60, 80, 3) * 255)
+        f[ImageFeature.label] = RoiLabel(torch.tensor([1.0]), torch.tensor([[0.2, 0.2, 0.6, 0.7]]))
+        RandomSampler().transform(f)
+        h, w = f.get_height(), f.get_width()
+        assert 1 <= h <= 60 and 1 <= w <= 80
+        assert ImageFeature.cropBbox in f
