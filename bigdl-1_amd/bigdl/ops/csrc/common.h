@@ -37,6 +37,15 @@ __device__ __forceinline__ void load8(const bf16_t* p, float* o) {
   }
 }
 
+__device__ __forceinline__ void unpack8(uint4 u, float* o) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+
 __device__ __forceinline__ void store8(bf16_t* p, const float* o) {
   uint32_t w[4];
 #pragma unroll

@@ -262,8 +262,19 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   //  2. the block walks the tile row-major, 8 channels per thread: optional residual add (same
   //     16-B chunk of `res`), ReLU, one global_store_dwordx4, and optional per-channel Σy / Σy²
   //     partials for a following BatchNormalization (the conv then replaces the BN stats pass).
-  constexpr int LDR = BN + 16;  // 288/160-B rows: the b64 fragment writes of 16 rows hit distinct banks
+  // Staging layout: rows of BN bf16 (no pad); the 8-B unit u of row r lives at unit u ^ (r & UMASK).
+  // A fragment write covers 16 rows × one unit: the XOR spreads them over 16 distinct units, i.e.
+  // all 32 banks (conflict-free; a padded layout left 4-way conflicts).  A 16-B read of chunk c
+  // finds its two units at the aligned pair c ^ (s >> 1), swapped when s is odd.
+  constexpr int LDR = BN;
+  constexpr int UMASK = (BN / 4 - 1) & 31;
   bf16_t* et = &lds[0][0];
+  auto rd_chunk = [&](int r, int c) -> uint4 {
+    const int sw = r & UMASK;
+    uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + ((c ^ (sw >> 1)) << 3)]);
+    if (sw & 1) u = make_uint4(u.z, u.w, u.x, u.y);
+    return u;
+  };
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int nl = wave_n * (BN / 2) + i * 16 + fq * 4;
@@ -278,7 +289,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       const int ml = wave_m * 64 + j * 16 + fr;
       uint32_t lo = (uint32_t)f2bf(acc[i][j][0] + b4[0]) | ((uint32_t)f2bf(acc[i][j][1] + b4[1]) << 16);
       uint32_t hi = (uint32_t)f2bf(acc[i][j][2] + b4[2]) | ((uint32_t)f2bf(acc[i][j][3] + b4[3]) << 16);
-      *reinterpret_cast<uint2*>(&et[ml * LDR + nl]) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(&et[ml * LDR + (((nl >> 2) ^ (ml & UMASK)) << 2)]) = make_uint2(lo, hi);
     }
   }
   __syncthreads();
@@ -314,7 +325,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
     }
     if (full && p.bnx) {
       float g[8], xv[8];
-      load8(&et[r * LDR + cc * 8], g);
+      unpack8(rd_chunk(r, cc), g);
       load8(p.bnx + off, xv);
       uint32_t w4[4];
       if (p.bn_mask) {
@@ -346,10 +357,10 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
         q8[2 * e + 1] = fmaf(b, xv[2 * e + 1] - bmu[2 * e + 1], q8[2 * e + 1]);
       }
     } else if (full) {
-      uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + cc * 8]);
+      uint4 u = rd_chunk(r, cc);
       if (p.res || p.relu) {
         float v[8];
-        load8(&et[r * LDR + cc * 8], v);
+        unpack8(u, v);
         if (p.res) {
           float rv[8];
           load8(p.res + off, rv);
@@ -380,7 +391,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       }
     } else {
       float v[8];
-      load8(&et[r * LDR + cc * 8], v);
+      unpack8(rd_chunk(r, cc), v);
       for (int e = 0; e < 8 && n + e < p.K; ++e) {
         float t = v[e] + (p.res ? bf2f(p.res[off + e]) : 0.f);
         if (p.relu) t = fmaxf(t, 0.f);
