@@ -64,7 +64,11 @@ __device__ __forceinline__ void stx(float* p, float v) { *p = v; }
 // y = x · keep · scale  (the same kernel is the backward: x ← gy)
 template <typename T>
 __global__ void __launch_bounds__(256) k_dropout(const T* __restrict__ x, T* __restrict__ y, long long n,
-                                                 unsigned long long seed, uint32_t thresh, float scale) {
+                                                 unsigned long long seed, uint32_t thresh, float scale,
+                                                 const unsigned long long* __restrict__ seed_ptr) {
+  // graph-captured launches read the seed from device memory (a counter advanced inside the graph),
+  // so every replay draws a fresh mask
+  if (seed_ptr) seed = *seed_ptr;
   const long long groups = n >> 3;
   for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < groups;
        j += (long long)gridDim.x * blockDim.x) {
@@ -84,9 +88,24 @@ __global__ void __launch_bounds__(256) k_dropout(const T* __restrict__ x, T* __r
   }
 }
 
+static int dropout_launch(const void* x, void* y, long long n, int dtype, float p, unsigned long long seed,
+                          const unsigned long long* seed_ptr, hipStream_t s);
+
 // dtype: 0 = bf16, 1 = fp32.  p ∈ [0, 1): drop probability.  Pointers 16-B aligned.
 BIGDL_EXPORT int bigdl_dropout(const void* x, void* y, long long n, int dtype, float p, unsigned long long seed,
                                hipStream_t s) {
+  return dropout_launch(x, y, n, dtype, p, seed, nullptr, s);
+}
+
+// Same, seed read on the device from `seed_ptr` (HIP-graph capture).
+BIGDL_EXPORT int bigdl_dropout_devseed(const void* x, void* y, long long n, int dtype, float p,
+                                       const unsigned long long* seed_ptr, hipStream_t s) {
+  if (!seed_ptr) return (int)hipErrorInvalidValue;
+  return dropout_launch(x, y, n, dtype, p, 0ull, seed_ptr, s);
+}
+
+static int dropout_launch(const void* x, void* y, long long n, int dtype, float p, unsigned long long seed,
+                          const unsigned long long* seed_ptr, hipStream_t s) {
   if (n <= 0 || p < 0.f || p >= 1.f || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) || dtype < 0 || dtype > 1)
     return (int)hipErrorInvalidValue;
   double t = (double)p * 4294967296.0;
@@ -96,9 +115,9 @@ BIGDL_EXPORT int bigdl_dropout(const void* x, void* y, long long n, int dtype, f
   const int grid = bigdl_grid((n >> 3) + 1, 256, 16384);
   if (dtype == 0)
     hipLaunchKernelGGL(k_dropout<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n, seed, thresh,
-                       scale);
+                       scale, seed_ptr);
   else
     hipLaunchKernelGGL(k_dropout<float>, dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, n, seed, thresh,
-                       scale);
+                       scale, seed_ptr);
   BIGDL_CHECK_LAUNCH();
 }

@@ -832,11 +832,24 @@ def lrn_backward(gy, x, size, alpha, beta, k):
 
 # ---------------------------------------------------------------------------------- K17 dropout
 class _DropMask:
-    """Stands in for the dropout mask: the kernel regenerates the keep decisions from ``seed``."""
-    __slots__ = ("seed", "cl", "shape")
+    """Stands in for the dropout mask: the kernel regenerates the keep decisions from ``seed``
+    (or, under HIP-graph capture, from the device-side seed snapshot ``dev``)."""
+    __slots__ = ("seed", "cl", "shape", "dev")
 
-    def __init__(self, seed, cl, shape):
-        self.seed, self.cl, self.shape = seed, cl, shape
+    def __init__(self, seed, cl, shape, dev=None):
+        self.seed, self.cl, self.shape, self.dev = seed, cl, shape, dev
+
+
+_DEV_SEED = {}
+
+
+def _device_seed(device) -> torch.Tensor:
+    """Per-device int64 seed counter advanced on the stream (captured into graphs)."""
+    t = _DEV_SEED.get(device)
+    if t is None:
+        t = torch.tensor([int(torch.randint(0, 2 ** 62, (1,)))], dtype=torch.int64, device=device)
+        _DEV_SEED[device] = t
+    return t
 
 
 def _dense_layout(t):
@@ -854,9 +867,15 @@ def dropout_forward(x, p, generator=None):
     cl = _dense_layout(x)
     if cl is None:
         return NotImplemented
+    y = torch.empty_like(x)
+    if torch.cuda.is_current_stream_capturing():
+        snap = _device_seed(x.device).clone()
+        check(_lib().bigdl_dropout_devseed(ptr(x), ptr(y), _ll(x.numel()), 0 if x.dtype == _bf16 else 1, C.c_float(p),
+                                           ptr(snap), _s()), "dropout_fwd")
+        _device_seed(x.device).add_(1)
+        return y, _DropMask(None, cl, tuple(x.shape), snap)
     seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator if (generator is not None and
                                                                          generator.device.type == "cpu") else None))
-    y = torch.empty_like(x)
     check(_lib().bigdl_dropout(ptr(x), ptr(y), _ll(x.numel()), 0 if x.dtype == _bf16 else 1, C.c_float(p),
                                C.c_ulonglong(seed), _s()), "dropout_fwd")
     return y, _DropMask(seed, cl, tuple(x.shape))
@@ -874,6 +893,10 @@ def dropout_backward(gy, mask, p):
     if not _al16(gy):
         gy = gy.clone()
     gx = torch.empty_like(gy)
+    if mask.dev is not None:
+        check(_lib().bigdl_dropout_devseed(ptr(gy), ptr(gx), _ll(gy.numel()), 0 if gy.dtype == _bf16 else 1,
+                                           C.c_float(p), ptr(mask.dev), _s()), "dropout_bwd")
+        return gx
     check(_lib().bigdl_dropout(ptr(gy), ptr(gx), _ll(gy.numel()), 0 if gy.dtype == _bf16 else 1, C.c_float(p),
                                C.c_ulonglong(mask.seed), _s()), "dropout_bwd")
     return gx

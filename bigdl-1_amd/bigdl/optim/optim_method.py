@@ -34,6 +34,16 @@ class OptimMethod:
     def optimize(self, feval: Callable, x: torch.Tensor):
         raise NotImplementedError
 
+    # ---- HIP-graph capture (optim/graph_step.py) ----------------------------------------------
+    def prepare_graph(self) -> bool:
+        """Switch to a replay-safe form (no per-iteration host scalars baked into kernels); False
+        when this method/configuration cannot be captured."""
+        return False
+
+    def after_graph_replay(self):
+        """Advance the host-side counters one iteration (a replay runs no Python)."""
+        self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
+
     def clearHistory(self):
         keep = {k: self.state[k] for k in ("epoch", "neval", "evalCounter", "recordsProcessedThisEpoch", "Loss",
                                            "score", "trainingTime") if k in self.state}
@@ -303,6 +313,10 @@ class EpochDecayWithWarmUp(LearningRateSchedule):
 
 # ----------------------------------------------------------------------------------------- SGD
 class SGD(OptimMethod):
+    def prepare_graph(self) -> bool:
+        # the fused kernel takes lr by value: replayable only while the schedule is constant
+        return type(self.learningRateSchedule) is Default and self.learningRateDecay == 0
+
     def __init__(self, learningrate=1e-3, learningrate_decay=0.0, weightdecay=0.0, momentum=0.0,
                  dampening=float("inf"), nesterov=False, leaningrate_schedule=None, learningrates=None,
                  weightdecays=None, bigdl_type="float"):
@@ -476,13 +490,27 @@ class Adagrad(OptimMethod):
         n = self.state.get("evalCounter", 0)
         if self.weightDecay != 0:
             g = g + self.weightDecay * x
-        clr = self.learningRate / (1 + n * self.learningRateDecay)
         s = self._state_tensor("paramVariance", x)
         s.addcmul_(g, g)
-        x.addcdiv_(g, s.sqrt().add_(1e-10), value=-clr)
+        if getattr(self, "_graph_mode", False):
+            # replay-safe: the iteration counter lives on the device and the decayed rate is a tensor
+            nt = self.state.get("_dev_n")
+            if not isinstance(nt, torch.Tensor) or nt.device != x.device:
+                nt = torch.full((1,), float(n), device=x.device)
+                self.state["_dev_n"] = nt
+            clr_t = (1 + nt * self.learningRateDecay).reciprocal_().mul_(self.learningRate)
+            x.sub_(g / s.sqrt().add_(1e-10) * clr_t)
+            nt.add_(1)
+        else:
+            clr = self.learningRate / (1 + n * self.learningRateDecay)
+            x.addcdiv_(g, s.sqrt().add_(1e-10), value=-clr)
         self.state["evalCounter"] = n + 1
         _sync_shadow(self, x)
         return x, [fx]
+
+    def prepare_graph(self) -> bool:
+        self._graph_mode = True
+        return True
 
 
 class Adadelta(OptimMethod):

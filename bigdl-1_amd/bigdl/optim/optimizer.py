@@ -396,7 +396,7 @@ class BaseOptimizer:
             t0 = time.perf_counter()
             batch = next(batches)
             bs = batch.size()
-            loss_t = self.train_step(batch)
+            loss_t = self._step(batch)
             # bookkeeping (no device sync: the loss is read one iteration late)
             if not (isinstance(loss_t, torch.Tensor) and loss_t.is_cuda) or self._needs_loss():
                 # host tensor, or a consumer (summary / MinLoss trigger) needs this iteration's value
@@ -434,6 +434,18 @@ class BaseOptimizer:
         """Set the model up for stepping without running the loop (used by bench/smoke)."""
         self._setup_model()
         return self
+
+    def _step(self, batch: MiniBatch) -> torch.Tensor:
+        """One iteration of the optimize loop: HIP-graph replay when ``bigdl.graph.capture`` is on
+        and the batch has the captured shape (LocalOptimizer on a GPU), else eager."""
+        if (type(self) is LocalOptimizer and self.device.type == "cuda"
+                and config.get_property("bigdl.graph.capture")):
+            from .graph_step import graphed_train_step
+            g = getattr(self, "_graphed", None)
+            x = batch.getInput()
+            if g is None or (isinstance(x, torch.Tensor) and x.shape == g.sx.shape and x.dtype == g.sx.dtype):
+                return graphed_train_step(self, batch)
+        return self.train_step(batch)
 
     def train_step(self, batch: MiniBatch) -> torch.Tensor:
         """One synchronous-SGD iteration on ``batch``; returns the (rank-averaged) loss as a

@@ -24,6 +24,7 @@ _REGISTRY = {
     "bigdl.check.singleton": (bool, False, "compat"),
     # failure handling
     "bigdl.failure.retryTimes": (int, 5, "optimizer retry budget"),
+    "bigdl.graph.capture": (bool, False, "LocalOptimizer on a GPU: capture the training step into a HIP graph"),
     "bigdl.comm.timeout": (float, 600.0, "collective watchdog: seconds before a hung RCCL/gloo collective raises"),
     "bigdl.failure.retryTimeInterval": (int, 120, "retry window seconds"),
     # parameter sync

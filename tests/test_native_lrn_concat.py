@@ -175,3 +175,35 @@ def test_sgd_per_element_decay_with_and_without_shadow(shadow, nesterov):
     torch.testing.assert_close(buf, buf_ref, rtol=1e-5, atol=1e-6)
     if shadow:
         torch.testing.assert_close(sh, w.to(torch.bfloat16), rtol=0, atol=0)
+
+
+def test_hip_graph_train_step_vgg_like():
+    """A LocalOptimizer step with conv/BN/ReLU/dropout/linear captured into a HIP graph: replays
+    train (loss falls), draw fresh dropout masks each replay, and keep the host counters."""
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.nn import (Sequential, SpatialConvolution, SpatialBatchNormalization, ReLU, Dropout, View, Linear,
+                          LogSoftMax, ClassNLLCriterion, SpatialMaxPooling)
+    from bigdl.optim import SGD
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.optim.graph_step import GraphedTrainStep
+    from bigdl.dataset import MiniBatch
+    torch.manual_seed(0)
+    m = (Sequential().add(SpatialConvolution(3, 16, 3, 3, 1, 1, 1, 1)).add(SpatialBatchNormalization(16)).add(ReLU())
+         .add(Dropout(0.3)).add(SpatialMaxPooling(2, 2, 2, 2)).add(View(16 * 8 * 8)).add(Linear(1024, 10))
+         .add(LogSoftMax()))
+    x = _cl(torch.randn(32, 3, 16, 16, device=dev).to(torch.bfloat16))
+    y = (torch.randint(0, 10, (32,), device=dev) + 1).float()
+    b = MiniBatch(x, y)
+    opt = LocalOptimizer(m, [b], ClassNLLCriterion(), SGD(learningrate=0.05, momentum=0.9, dampening=0.0), batch_size=32)
+    opt.prepare()
+    g = GraphedTrainStep(opt, b)
+    n0 = opt.state.get("neval", 0)
+    drop = m.modules[3]
+    losses, masks = [], []
+    for _ in range(30):
+        losses.append(float(g.step(b)))
+        masks.append((drop.output != 0).clone())
+    assert opt.state["neval"] == n0 + 30
+    assert losses[-1] < losses[0]
+    assert not torch.equal(masks[0], masks[1])

@@ -43,3 +43,21 @@ def test_fold_with_user_weight_decays():
     torch.testing.assert_close(_run(True, user_wds=True), _run(False, user_wds=True), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(_run(True, wd=0.0, user_wds=True), _run(False, wd=0.0, user_wds=True),
                                rtol=1e-5, atol=1e-6)
+
+
+def test_adagrad_graph_mode_matches_eager():
+    """Adagrad's replay-safe form (device-side iteration counter, tensor learning rate) computes
+    the same updates as the eager form."""
+    import torch
+    from bigdl.optim import Adagrad
+    torch.manual_seed(0)
+    x1 = torch.randn(64)
+    x2 = x1.clone()
+    a, b = Adagrad(0.1, 0.01), Adagrad(0.1, 0.01)
+    assert b.prepare_graph()
+    for _ in range(5):
+        g = torch.randn(64)
+        a.optimize(lambda _x, g=g: (0.0, g.clone()), x1)
+        b.optimize(lambda _x, g=g: (0.0, g.clone()), x2)
+    torch.testing.assert_close(x1, x2, rtol=1e-6, atol=1e-7)
+    assert float(b.state["_dev_n"]) == 5.0

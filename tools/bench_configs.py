@@ -98,11 +98,16 @@ def bench_vgg(args):
     sgd = SGD(learningrate=0.01, weightdecay=5e-4, momentum=0.9, dampening=0.0)
     opt = LocalOptimizer(VggForCifar10(10), [batch], ClassNLLCriterion(), sgd, batch_size=B)
     opt.prepare()
-    el, loss = _time_steps(lambda: opt.train_step(batch), dev, args.steps, args.warmup)
+    step = opt.train_step
+    if args.graph:
+        from bigdl.optim.graph_step import graphed_train_step
+        step = lambda b: graphed_train_step(opt, b)  # noqa: E731
+    el, loss = _time_steps(lambda: step(batch), dev, args.steps, args.warmup)
     return {"metric": "images/sec VggForCifar10 CIFAR-shape 1 GPU", "value": round(B * args.steps / el, 1),
             "unit": "images/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
-            "data": "synthetic", "config": {"model": "VggForCifar10", "global_batch": B},
+            "data": "synthetic", "config": {"model": "VggForCifar10", "global_batch": B,
+                                            "hip_graph": bool(args.graph and getattr(opt, "_graphed", None))},
             "final_loss": float(loss)}
 
 
@@ -141,8 +146,12 @@ def bench_ptb(args):
     else:
         opt = LocalOptimizer(model, [batch], crit, ada, batch_size=B)
     opt.prepare()
+    step = opt.train_step
+    if args.graph and world == 1:
+        from bigdl.optim.graph_step import graphed_train_step
+        step = lambda b: graphed_train_step(opt, b)  # noqa: E731
     for _ in range(args.warmup):
-        opt.train_step(batch)
+        step(batch)
     if hasattr(opt, "_wait_all_gathers"):
         opt._wait_all_gathers()
     comm.barrier()
@@ -150,7 +159,7 @@ def bench_ptb(args):
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
-        loss = opt.train_step(batch)
+        loss = step(batch)
     if hasattr(opt, "_wait_all_gathers"):
         opt._wait_all_gathers()
     _sync(dev)
@@ -161,7 +170,8 @@ def bench_ptb(args):
            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
            "data": "synthetic", "scaling": "weak",
            "config": {"model": "PTBModel.lstm", "vocab": V, "hidden": H, "layers": 2, "seq_len": T,
-                      "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+                      "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
+                      "hip_graph": bool(getattr(opt, "_graphed", None))},
            "final_loss": float(loss)}
     return res if rank == 0 else None
 
@@ -280,6 +290,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
+    ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb)")
     args = ap.parse_args()
     names = list(CONFIGS) if args.config == "all" else [args.config]
     for n in names:
