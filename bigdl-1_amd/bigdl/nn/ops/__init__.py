@@ -523,7 +523,9 @@ class BucketizedCol(Operation):
 
 
 def _hash_bucket(s: str, n: int) -> int:
-    return int.from_bytes(hashlib.md5(s.encode()).digest()[:8], "little") % n
+    """Scala ``MurmurHash3.stringHash(s) % n`` made non-negative (``HashFunc.stringHashBucket32``)."""
+    from ...utils.hash_func import stringHashBucket32
+    return stringHashBucket32(s, n)
 
 
 class CategoricalColHashBucket(Operation):
@@ -591,14 +593,34 @@ class CrossCol(Operation):
 
     def updateOutput(self, cols):
         cols = [cols[i + 1] for i in range(len(cols))] if isinstance(cols, Table) else list(cols)
+        from ...utils.hash_func import string_hash
         rows = []
         for vals in zip(*cols):
-            parts = [v.split(self.strDelimiter) for v in vals]
-            combos = [[]]
-            for p in parts:
-                combos = [c + [x] for c in combos for x in p]
-            rows.append([_hash_bucket("_X_".join(c), self.hashBucketSize) for c in combos])
+            parts = [str(v).split(self.strDelimiter) for v in vals]
+            rows.append([self._bucket(c, string_hash) for c in self._recombine(parts)])
         return _sparse_or_dense(rows, True)
+
+    @staticmethod
+    def _recombine(parts):
+        """The reference's stack-based cartesian product order (``CrossCol.reCombine``): every level
+        but the last is visited in reverse, the last in order."""
+        out = []
+
+        def rec(prefix, lvl):
+            if lvl == len(parts) - 1:
+                out.extend(prefix + [x] for x in parts[lvl])
+                return
+            for x in reversed(parts[lvl]):
+                rec(prefix + [x], lvl + 1)
+        rec([], 0)
+        return out
+
+    def _bucket(self, combo, string_hash):
+        h = string_hash(combo[0])
+        for s in combo[1:]:
+            h = string_hash(s, h & 0xFFFFFFFF)
+        r = int(h - self.hashBucketSize * int(h / self.hashBucketSize))
+        return r + self.hashBucketSize if r < 0 else r
 
 
 class IndicatorCol(Operation):

@@ -242,3 +242,16 @@ def test_load_while_loop_as_dynamic_graph(tmp_path):
     assert float(g.forward(torch.tensor(1.0))) == 10.0
     assert float(g.forward(torch.tensor(-3.5))) == 10.5
     assert float(g.forward(torch.tensor(12.0))) == 12.0  # zero trips
+
+
+def test_hash_bucket_matches_reference_golden():
+    """``CategoricalColHashBucketSpec``: "1","2","3" → buckets 5, 53, 77 of 100 (Scala MurmurHash3)."""
+    from bigdl.utils.hash_func import stringHashBucket32
+    assert [stringHashBucket32(s, 100) for s in ("1", "2", "3")] == [5, 53, 77]
+    sp = O.CategoricalColHashBucket(100).forward(["1,2", "2", "1,3,2"])
+    assert sp[2].tolist() == [5, 53, 53, 5, 77, 53]
+    # CrossColSpec goldens (two and three columns)
+    c2 = O.CrossCol(100).forward(Table(["A,D", "B", "A,C"], ["1", "2", "3,4"]))
+    assert c2[2].tolist() == [80, 98, 50, 99, 27, 89, 33]
+    c3 = O.CrossCol(100).forward(Table(["A,D", "B", "A,C"], ["1", "2", "3,4"], ["1", "2", "3"]))
+    assert c3[2].tolist() == [94, 34, 68, 82, 83, 97, 12]

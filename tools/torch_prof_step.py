@@ -1,0 +1,41 @@
+"""Attribute the non-HIP-kernel work of one ResNet-50 training step (copies, fills, torch
+elementwise) to its Python call sites with torch.profiler (CPU-side op stacks)."""
+import os
+import sys
+import collections
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bigdl-1_amd"))
+import torch
+from bigdl.utils import config
+config.set_property("bigdl.compute.dtype", "bf16")
+from bigdl.utils.engine import Engine
+Engine.init()
+from bigdl.models.resnet import ResNet, DatasetType, model_init
+from bigdl.nn import CrossEntropyCriterion
+from bigdl.optim import SGD
+from bigdl.optim.optimizer import LocalOptimizer
+from bigdl.dataset import MiniBatch
+
+B = int(os.environ.get("B", "64"))
+model = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+x = torch.randn(B, 3, 224, 224, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+y = (torch.randint(0, 1000, (B,), device="cuda") + 1).float()
+opt = LocalOptimizer(model, [MiniBatch(x, y)], CrossEntropyCriterion(),
+                     SGD(learningrate=0.1, momentum=0.9, dampening=0.0, nesterov=True, weightdecay=1e-4), batch_size=B)
+opt.prepare()
+for _ in range(3):
+    opt.train_step(MiniBatch(x, y))
+torch.cuda.synchronize()
+from torch.profiler import profile, ProfilerActivity
+with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+    opt.train_step(MiniBatch(x, y))
+    torch.cuda.synchronize()
+cnt = collections.Counter()
+for ev in prof.events():
+    if ev.name in ("aten::copy_", "aten::fill_", "aten::zero_", "aten::flip", "aten::index", "aten::clone",
+                   "aten::contiguous", "aten::cat", "aten::mul", "aten::add", "aten::sum", "aten::to", "aten::_to_copy",
+                   "aten::zeros", "aten::empty_strided", "aten::index_select", "aten::gather"):
+        frames = [f for f in (ev.stack or []) if "bigdl" in f][:3]
+        cnt[(ev.name, " <- ".join(frames))] += 1
+for (name, st), c in cnt.most_common(40):
+    print(f"{c:5d} {name:22s} {st}")
