@@ -20,3 +20,4 @@ def __getattr__(name):
         from ..parallel.distri_optimizer import ParallelOptimizer
         return ParallelOptimizer
     raise AttributeError(name)
+from .line_search import LineSearch, LswolfeLineSearch  # noqa: E402,F401

@@ -636,11 +636,20 @@ class LBFGS(OptimMethod):
             gtd = float((g * d).sum())
             if gtd > -self.tolX:
                 break
-            x.add_(d, alpha=t)
-            if it != self.maxIter - 1:
-                fx, g = feval(x)
-                n_eval += 1
+            if self.lineSearch is not None:
+                # strong-Wolfe search along d (LineSearch.scala); it evaluates feval itself
+                f_new, g_new, x_new, t, ls_evals = self.lineSearch.apply(
+                    lambda xx: feval(xx), x, t, d, float(fx), g, gtd)
+                x.copy_(x_new)
+                fx, g = f_new, g_new
+                n_eval += ls_evals
                 f_hist.append(float(fx))
+            else:
+                x.add_(d, alpha=t)
+                if it != self.maxIter - 1:
+                    fx, g = feval(x)
+                    n_eval += 1
+                    f_hist.append(float(fx))
             if n_eval >= self.maxEval or float((d * t).abs().sum()) <= self.tolX:
                 break
             if len(f_hist) > 1 and abs(f_hist[-1] - f_hist[-2]) < self.tolFun:

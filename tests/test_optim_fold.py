@@ -61,3 +61,20 @@ def test_adagrad_graph_mode_matches_eager():
         b.optimize(lambda _x, g=g: (0.0, g.clone()), x2)
     torch.testing.assert_close(x1, x2, rtol=1e-6, atol=1e-7)
     assert float(b.state["_dev_n"]) == 5.0
+
+
+def test_lbfgs_with_wolfe_line_search_rosenbrock():
+    """LBFGS + LswolfeLineSearch (``LBFGSSpec`` style: Rosenbrock minimum at (1, 1))."""
+    import torch
+    from bigdl.optim import LBFGS, LswolfeLineSearch
+
+    def rosen(x):
+        a, b = x[0], x[1]
+        f = (1 - a) ** 2 + 100 * (b - a * a) ** 2
+        g = torch.stack([-2 * (1 - a) - 400 * a * (b - a * a), 200 * (b - a * a)])
+        return f, g
+    x = torch.tensor([-1.2, 1.0], dtype=torch.float64)
+    opt = LBFGS(max_iter=100, tolfun=1e-12, tolx=1e-12, linesearch=LswolfeLineSearch())
+    x, fs = opt.optimize(rosen, x)
+    assert torch.allclose(x, torch.tensor([1.0, 1.0], dtype=torch.float64), atol=1e-4), x
+    assert fs[-1] < 1e-8

@@ -179,3 +179,36 @@ def test_retry_from_checkpoint_after_injected_fault(tmp_path):
     assert opt.state["neval"] >= 8
     assert FaultInject._counts["retry_test"] >= 8  # the failure happened and training went on
     assert trained is not None
+
+
+def test_util_thread_pool_model_utils(tmp_path):
+    import time
+    import numpy as np
+    from bigdl.utils.util import kthLargest
+    from bigdl.utils.thread_pool import ThreadPool
+    arr = [5, 1, 9, 3, 7, 7, 2]
+    assert kthLargest(list(arr), 0, len(arr) - 1, 1) == 9
+    assert kthLargest(list(arr), 0, len(arr) - 1, 3) == 7
+    assert kthLargest(list(arr), 0, len(arr) - 1, 7) == 1
+    pool = ThreadPool(4)
+    assert pool.invokeAndWait([lambda i=i: i * i for i in range(5)]) == [0, 1, 4, 9, 16]
+    futs = pool.invokeAndWait2([lambda: 1, lambda: time.sleep(2) or 2], timeout=0.3)
+    assert futs[0].done() and futs[0].result() == 1
+    assert not futs[1].done() or futs[1].cancelled()  # the straggler did not finish within the timeout
+    pool.shutdown()
+    # seq file generator over a tiny image folder
+    from PIL import Image
+    from bigdl.models.utils.seqfile_generator import main as gen
+    from bigdl.dataset.seqfile import SeqFileFolder
+    for c in ("cat", "dog"):
+        (tmp_path / "img" / c).mkdir(parents=True)
+        Image.fromarray(np.full((6, 9, 3), 100, np.uint8)).save(tmp_path / "img" / c / "a.png")
+    assert gen(["-f", str(tmp_path / "img"), "-o", str(tmp_path / "seq"), "-b", "1", "-r", "4", "--hasName"]) == 0
+    recs = list(SeqFileFolder.read(str(tmp_path / "seq")))
+    assert [r[1] for r in recs] == [1.0, 2.0] and recs[0][0].shape == (4, 6, 3) and recs[0][2] == "a.png"
+
+
+def test_perf_harness_runs_cpu(capsys):
+    from bigdl.models.utils.perf import main
+    assert main(["--model", "lenet5", "--batch", "8", "--iteration", "2", "--warmup", "1", "--dtype", "fp32"]) == 0
+    assert "records/second" in capsys.readouterr().out
