@@ -9,8 +9,8 @@
 //   so each lane's accumulator holds 4 consecutive OUTPUT CHANNELS of one pixel (D layout of
 //   mfma_f32_16x16x32_bf16: row=(lane>>4)*4+j, col=lane&15) → 8-byte NHWC stores.
 //
-// Tiling: block 128 pixels × BN channels × BK=64, 256 threads = 4 waves (2 × 2), each wave
-// (BN/2) × 64 = (BN/32) × 4 MFMA 16×16×32 tiles.  Global→LDS through registers (the gather needs
+// Tiling: block 128 pixels × BN channels × BK (64, or 32 for shallow reductions), 256 threads =
+// 4 waves (2 × 2), each wave (BN/2) × 64 = (BN/32) × 4 MFMA 16×16×32 tiles.  Global→LDS through registers (the gather needs
 // per-row zero padding, so no global_load_lds), double-buffered LDS, one barrier per k-tile, the
 // next tile's loads issued before the current tile's MFMAs (T14 split).  LDS rows are 128 B with
 // a 16-B-chunk XOR swizzle (chunk ^ (row & 7)) so the ds_read_b128 fragment reads of 16 distinct
@@ -53,10 +53,15 @@ struct ConvParams {
   int ldy;
 };
 
-constexpr int BM = 128;
-constexpr int BK = 64;
-
-__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+constexpr int SBM = 128;  // row granularity of the BN-statistics partials (any BM writes BM / SBM rows)
+// k-tile depth is a kernel parameter (64 or 32).  64-wide rows (128 B) take a 16-B-chunk XOR
+// swizzle so a fragment read of 16 rows is conflict-free; 32-wide rows (64 B) are read as one
+// contiguous 1-KiB span per fragment and need none.
+template <int BK>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  if constexpr (BK == 64) return row * BK + ((chunk ^ (row & 7)) << 3);
+  else return row * BK + (chunk << 3);
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -66,21 +71,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // FAST: C % 64 == 0 and R·S ≤ 64 — every k-tile lies inside one filter tap, so the tap / channel
 // position of a k-tile is wave-uniform (scalar registers, no per-lane division) and the padding test
 // of a staged row is one bit of a per-row tap-validity mask built once in the prologue.
-template <int BN, bool FAST>
-__global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
+template <int BN, bool FAST, int BM, int BK>
+__global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_conv_fwd(ConvParams p) {
   constexpr int ROWS = BM + BN;
+  constexpr int CPK = BK / 8;    // 16-B chunks per staged row
+  constexpr int RPS = 256 / CPK; // rows staged per pass of the block
   constexpr int TN = BN / 32;  // MFMA tiles along channels per wave
-  constexpr int TM = 4;        // MFMA tiles along pixels per wave (64 pixels)
-  constexpr int A_CHUNKS = BM * BK / 8 / 256;  // activation chunks per thread (4)
+  constexpr int TM = BM / 32;  // MFMA tiles along pixels per wave (BM / 2 pixels)
+  constexpr int A_CHUNKS = BM * BK / 8 / 256;  // activation chunks per thread (4 or 8)
   constexpr int B_CHUNKS = BN * BK / 8 / 256;  // weight chunks per thread (4 or 2)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][ROWS * BK];
+  constexpr int STAGE = ROWS * BK;
+  constexpr int EPI = BM * BN + 4 * (256 / (BN / 8)) * BN;  // epilogue tile + Σ/Σ² reduction rows
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE > EPI ? 2 * STAGE : EPI];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wave_m = wid & 1, wave_n = wid >> 1;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int col8 = tid & 7;  // this thread's 16-B chunk column inside a 64-wide k tile
+  const int col8 = tid & (CPK - 1);  // this thread's 16-B chunk column inside a k tile
 
   // Operand loads are raw buffer loads: the descriptor's num_records bounds-check returns zeros
   // for an out-of-range offset, so conv padding, the M / K tails and the channel tail need no
@@ -96,7 +105,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
 #pragma unroll
   for (int i = 0; i < A_CHUNKS; ++i) {
-    int m = m0 + (tid >> 3) + 32 * i;
+    int m = m0 + tid / CPK + RPS * i;
     if (m < p.M) {
       int n = m / (p.P * p.Q);
       int pq = m - n * p.P * p.Q;
@@ -113,7 +122,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   uint32_t b_row[B_CHUNKS];
 #pragma unroll
   for (int i = 0; i < B_CHUNKS; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
+    const int n = n0 + tid / CPK + RPS * i;
     b_row[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 2u : 0x80000000u;  // + any k stays out of range
   }
 
@@ -191,13 +200,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   auto store_tile = [&](int buf, const uint4 (&ra)[A_CHUNKS], const uint4 (&rb)[B_CHUNKS]) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      int row = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(&lds[buf][swz(row, col8)]) = ra[i];
+      int row = tid / CPK + RPS * i;
+      *reinterpret_cast<uint4*>(&lds[buf * STAGE + swz<BK>(row, col8)]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_CHUNKS; ++i) {
-      int row = BM + (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(&lds[buf][swz(row, col8)]) = rb[i];
+      int row = BM + tid / CPK + RPS * i;
+      *reinterpret_cast<uint4*>(&lds[buf * STAGE + swz<BK>(row, col8)]) = rb[i];
     }
   };
 
@@ -210,18 +219,18 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   const int fr = lane & 15, fq = lane >> 4;
   auto compute = [&](int buf) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + fq;
       v8s af[TN], bfr[TM];
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         int row = BM + wave_n * (BN / 2) + i * 16 + fr;
-        af[i] = *reinterpret_cast<const v8s*>(&lds[buf][swz(row, chunk)]);
+        af[i] = *reinterpret_cast<const v8s*>(&lds[buf * STAGE + swz<BK>(row, chunk)]);
       }
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
-        int row = wave_m * 64 + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const v8s*>(&lds[buf][swz(row, chunk)]);
+        int row = wave_m * (BM / 2) + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v8s*>(&lds[buf * STAGE + swz<BK>(row, chunk)]);
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -268,7 +277,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   // finds its two units at the aligned pair c ^ (s >> 1), swapped when s is odd.
   constexpr int LDR = BN;
   constexpr int UMASK = (BN / 4 - 1) & 31;
-  bf16_t* et = &lds[0][0];
+  bf16_t* et = &lds[0];
   auto rd_chunk = [&](int r, int c) -> uint4 {
     const int sw = r & UMASK;
     uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + ((c ^ (sw >> 1)) << 3)]);
@@ -286,7 +295,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
     }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
-      const int ml = wave_m * 64 + j * 16 + fr;
+      const int ml = wave_m * (BM / 2) + j * 16 + fr;
       uint32_t lo = (uint32_t)f2bf(acc[i][j][0] + b4[0]) | ((uint32_t)f2bf(acc[i][j][1] + b4[1]) << 16);
       uint32_t hi = (uint32_t)f2bf(acc[i][j][2] + b4[2]) | ((uint32_t)f2bf(acc[i][j][3] + b4[3]) << 16);
       *reinterpret_cast<uint2*>(&et[ml * LDR + (((nl >> 2) ^ (ml & UMASK)) << 2)]) = make_uint2(lo, hi);
@@ -298,8 +307,6 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
   const int cc = tid % CPR, rr = tid / CPR;
   const int n = n0 + cc * 8;
   float s8[8], q8[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
   const bool full = n + 8 <= p.K;
   float bsc[8], bsh[8], bmu[8];
   if (p.bnx && full) {
@@ -310,8 +317,12 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
       bmu[e] = p.bn_mean[n + e];
     }
   }
+  // the statistics partials are per SBM-row group: a BM = 256 tile reduces its two halves separately
+  for (int h = 0; h < BM / SBM; ++h) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
 #pragma unroll 2
-  for (int r = rr; r < BM; r += RPP) {
+  for (int r = h * SBM + rr; r < (h + 1) * SBM; r += RPP) {
     const int m = m0 + r;
     if (m >= p.M || n >= p.K) continue;
     size_t off = (size_t)m * p.K + n;
@@ -419,17 +430,36 @@ __global__ void __launch_bounds__(256, 2) k_conv_fwd(ConvParams p) {
         a += red[g * BN + c];
         b += red[RPP * BN + g * BN + c];
       }
-      if (n0 + c < p.K) {
-        p.stats[(size_t)tm * p.K + n0 + c] = a;
-        p.stats[((size_t)p.tiles_m + tm) * p.K + n0 + c] = b;
+      const int g = tm * (BM / SBM) + h;
+      if (n0 + c < p.K && g < p.tiles_m) {
+        p.stats[(size_t)g * p.K + n0 + c] = a;
+        p.stats[((size_t)p.tiles_m + g) * p.K + n0 + c] = b;
       }
     }
+    if (h + 1 < BM / SBM) __syncthreads();  // the next half rewrites `red`
   }
+  }
+}
+
+// Environment pin of a tile parameter (A/B measurements): returns a or b if the variable names one
+// of them, else 0 (= use the heuristic).
+static int conv_env_override(const char* name, int a, int b) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return (v == a || v == b) ? v : 0;
+}
+
+template <int BN, int BM, int BK>
+static void launch_fwd(bool fast, dim3 grid, hipStream_t s, const ConvParams& p) {
+  if (fast)
+    hipLaunchKernelGGL((k_conv_fwd<BN, true, BM, BK>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((k_conv_fwd<BN, false, BM, BK>), grid, dim3(256), 0, s, p);
 }
 
 // Host launchers.  Requirements (checked): C % 8 == 0, K % 4 == 0, 16-B aligned x/w/y/res.
 // ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
-BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + BM - 1) / BM); }
+BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + SBM - 1) / SBM); }
 
 static int conv_fwd_launch(const void* x, const void* w, const float* bias, const void* res, void* y,
                            float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
@@ -472,18 +502,26 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
   const int BN = K <= 64 ? 64 : 128;
   p.tiles_n = (K + BN - 1) / BN;
-  p.tiles_m = (p.M + BM - 1) / BM;
-  long long tiles = (long long)p.tiles_m * p.tiles_n;
+  p.tiles_m = (p.M + SBM - 1) / SBM;
+  // Tile shape: 128 pixels × BN × BK.  BK = 32 halves the LDS stage (48 KiB incl. the epilogue) and
+  // the register prefetch so 3 blocks share a CU; BM = 256 (128 × 64 per wave) trades occupancy for
+  // less LDS traffic per MFMA.  BIGDL_CONV_BM / BIGDL_CONV_BK pin a shape for A/B measurements.
+  // Measured on the ResNet-50 shapes (profiles/r1_conv_bk_ab.txt): BK = 32 wins on every reduction
+  // of ≤ 512 (the 1×1 convs; more blocks in flight hide the short k-loop's prologue/epilogue),
+  // BK = 64 on the deeper ones (3×3, C ≥ 1024).
+  const int bk_env = conv_env_override("BIGDL_CONV_BK", 32, 64);
+  const int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
+  const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
+  const bool fast = (C % bk == 0) && R * S <= 64;
+  long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
-  const bool fast = (C % 64 == 0) && R * S <= 64;
-  if (BN == 64 && fast)
-    hipLaunchKernelGGL((k_conv_fwd<64, true>), dim3((unsigned)tiles), dim3(256), 0, s, p);
-  else if (BN == 64)
-    hipLaunchKernelGGL((k_conv_fwd<64, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
-  else if (fast)
-    hipLaunchKernelGGL((k_conv_fwd<128, true>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+  const dim3 g((unsigned)tiles);
+  if (bm == 256)
+    BN == 64 ? launch_fwd<64, 256, 64>(fast, g, s, p) : launch_fwd<128, 256, 64>(fast, g, s, p);
+  else if (bk == 32)
+    BN == 64 ? launch_fwd<64, 128, 32>(fast, g, s, p) : launch_fwd<128, 128, 32>(fast, g, s, p);
   else
-    hipLaunchKernelGGL((k_conv_fwd<128, false>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+    BN == 64 ? launch_fwd<64, 128, 64>(fast, g, s, p) : launch_fwd<128, 128, 64>(fast, g, s, p);
   BIGDL_CHECK_LAUNCH();
 }
 
