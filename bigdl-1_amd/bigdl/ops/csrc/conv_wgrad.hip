@@ -45,7 +45,7 @@ struct WgradParams {
   FastDiv fPQ, fQ;
 };
 
-constexpr int BP = 64;  // pixels per k-tile
+constexpr int BP = 64;  // split granularity (pixels); the k-tile depth BPT is 64 or 32
 
 // byte offset inside a [BP rows][WIDTH bf16] tile for a 16-B chunk / 8-B quad
 template <int WIDTH>
@@ -59,14 +59,14 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
   }
 }
 
-template <int TILE_N, int TILE_K>
-__global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
-  constexpr int DY_CH = BP * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
-  constexpr int X_CH = BP * TILE_K / 8 / 256;   // for the X̂ tile
+template <int TILE_N, int TILE_K, int BPT>
+__global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradParams p) {
+  constexpr int DY_CH = BPT * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
+  constexpr int X_CH = BPT * TILE_K / 8 / 256;   // for the X̂ tile
   constexpr int TMN = TILE_N / 32;              // MFMA tiles per wave along n
   constexpr int TMK = TILE_K / 32;              // along k
-  constexpr int DY_WORDS = BP * TILE_N / 2;     // dwords per tile
-  constexpr int X_WORDS = BP * TILE_K / 2;
+  constexpr int DY_WORDS = BPT * TILE_N / 2;     // dwords per tile
+  constexpr int X_WORDS = BPT * TILE_K / 2;
   __shared__ __attribute__((aligned(16))) uint32_t lds[2][DY_WORDS + X_WORDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
   const int t = lane & 15, q4 = t >> 2, p4 = t & 3;
   auto compute = [&](int buf) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BPT / 32; ++kk) {
       v8s af[TMN], bfr[TMK];
 #pragma unroll
       for (int i = 0; i < TMN; ++i) {
@@ -183,18 +183,18 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradParams p) {
   };
 
   uint4 dy0[DY_CH], x0[X_CH], dy1[DY_CH], x1[X_CH];
-  const int NT = (mend - mbeg + BP - 1) / BP;
+  const int NT = (mend - mbeg + BPT - 1) / BPT;
   load(mbeg, true, dy0, x0);
-  load(mbeg + BP, NT > 1, dy1, x1);
+  load(mbeg + BPT, NT > 1, dy1, x1);
   store(0, dy0, x0);
   __syncthreads();
   int it = 0;
   for (; it + 2 <= NT; it += 2) {
-    load(mbeg + (it + 2) * BP, it + 2 < NT, dy0, x0);
+    load(mbeg + (it + 2) * BPT, it + 2 < NT, dy0, x0);
     compute(0);
     store(1, dy1, x1);
     __syncthreads();
-    load(mbeg + (it + 3) * BP, it + 3 < NT, dy1, x1);
+    load(mbeg + (it + 3) * BPT, it + 3 < NT, dy1, x1);
     compute(1);
     if (it + 2 < NT) store(0, dy0, x0);
     __syncthreads();
@@ -259,9 +259,22 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   p.m_per_split = mps;
   splits = (p.M + mps - 1) / mps;
   dim3 grid(tiles, splits);
-  if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64>), grid, dim3(256), 0, s, p);
-  else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128>), grid, dim3(256), 0, s, p);
-  else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((k_conv_wgrad<128, 128>), grid, dim3(256), 0, s, p);
+  // Pixel depth of a k-tile: 32 (half the LDS / prefetch registers, 3 blocks per CU) wins on the
+  // small weight grids (≤ 16 tiles, K ≥ 128: few tiles, long split reductions), 64 elsewhere
+  // (profiles/r1_conv_bk_ab.txt).  BIGDL_WGRAD_BP=32|64 pins it for A/B measurements.
+  const char* ev = getenv("BIGDL_WGRAD_BP");
+  const int bp_env = ev ? atoi(ev) : 0;
+  const int bp = (bp_env == 32 || bp_env == 64) ? bp_env : (tiles <= 16 && K >= 128 ? 32 : 64);
+  if (bp == 32) {
+    if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32>), grid, dim3(256), 0, s, p);
+    else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32>), grid, dim3(256), 0, s, p);
+    else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 32>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32>), grid, dim3(256), 0, s, p);
+  } else {
+    if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 64>), grid, dim3(256), 0, s, p);
+    else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 64>), grid, dim3(256), 0, s, p);
+    else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 64>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64>), grid, dim3(256), 0, s, p);
+  }
   BIGDL_CHECK_LAUNCH();
 }
