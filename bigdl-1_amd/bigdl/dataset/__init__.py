@@ -1,3 +1,3 @@
-from .core import (Sample, MiniBatch, PaddingParam, Transformer, ChainedTransformer, FnTransformer, SampleToMiniBatch,
+from .core import (Sample, MiniBatch, ArrayTensorMiniBatch, SparseMiniBatch, DefaultPadding, PaddingParam, Transformer, ChainedTransformer, FnTransformer, SampleToMiniBatch,
                    AbstractDataSet, LocalArrayDataSet, DistributedDataSet, TransformedDataSet, SyntheticDataSet, DataSet,
                    DevicePrefetcher)

@@ -80,6 +80,8 @@ class PaddingParam:
 
 
 class MiniBatch:
+    """A batch of input / target activities (``MiniBatch.scala:34``; ``ArrayTensorMiniBatch`` 111)."""
+
     def __init__(self, input, target=None):
         self.input = input
         self.target = target
@@ -132,6 +134,61 @@ class MiniBatch:
                 return t
             return a.pin_memory() if (torch.cuda.is_available() and not a.is_cuda) else a
         return MiniBatch(pn(self.input), pn(self.target))
+
+
+ArrayTensorMiniBatch = MiniBatch
+
+
+class DefaultPadding(PaddingParam):
+    """Pad with zeros to the longest sample (``MiniBatch.scala:528-580``)."""
+
+    def __init__(self):
+        super().__init__(None, None)
+
+
+class SparseMiniBatch(MiniBatch):
+    """MiniBatch whose features may be sparse (``MiniBatch.scala:588``): ``set(samples)`` stacks
+    dense features densely and sparse (COO) features into one [batch, ...] sparse tensor (the
+    reference's ``SparseMiniBatch.batch``: indices shifted by the sample's batch row)."""
+
+    def __init__(self, input=None, target=None):
+        super().__init__(input, target)
+
+    @staticmethod
+    def _batch(ts: List[torch.Tensor]) -> torch.Tensor:
+        if not ts[0].is_sparse:
+            return torch.stack([t.to_dense() if t.is_sparse else t for t in ts], 0)
+        idx, val = [], []
+        for b, t in enumerate(ts):
+            t = t.coalesce()
+            i = t.indices()
+            idx.append(torch.cat([torch.full((1, i.shape[1]), b, dtype=i.dtype), i], 0))
+            val.append(t.values())
+        shape = (len(ts),) + tuple(ts[0].shape)
+        return torch.sparse_coo_tensor(torch.cat(idx, 1), torch.cat(val), shape).coalesce()
+
+    def set(self, samples: Sequence["Sample"]) -> "SparseMiniBatch":
+        if not samples:
+            raise ValueError("samples is empty")
+        nf, nl = len(samples[0].features), len(samples[0].labels)
+        feats = [self._batch([s.features[i] for s in samples]) for i in range(nf)]
+        labs = [self._batch([s.labels[j] for s in samples]) for j in range(nl)]
+
+        def act(xs):
+            if not xs:
+                return None
+            if len(xs) == 1:
+                return xs[0]
+            t = Table()
+            for k, x in enumerate(xs):
+                t[k + 1] = x
+            return t
+        self.input, self.target = act(feats), act(labs)
+        return self
+
+    def size(self) -> int:
+        x = self.input[1] if isinstance(self.input, Table) else self.input
+        return int(x.shape[0])
 
 
 def _stack(tensors: List[torch.Tensor], padding: Optional[PaddingParam] = None):
@@ -362,6 +419,43 @@ class DataSet:
     @staticmethod
     def from_samples(samples: Sequence[Sample], batch_size: int, distributed: bool = False):
         return DataSet.array(samples, distributed).transform(SampleToMiniBatch(batch_size))
+
+    @staticmethod
+    def imageFrame(frame, distributed: bool = False) -> AbstractDataSet:
+        """DataSet of the ImageFeatures of an ImageFrame (``DataSet.imageFrame``)."""
+        feats = frame.to_local().array if hasattr(frame, "to_local") else list(frame)
+        return DataSet.array(list(feats), distributed)
+
+    image_frame = imageFrame
+
+    class ImageFolder:
+        """Class-per-subfolder image trees (``DataSet.scala:424-481``): subfolder i (sorted) is
+        label i + 1."""
+
+        @staticmethod
+        def paths(path: str, distributed: bool = False) -> AbstractDataSet:
+            from .image import LocalImageFiles
+            return DataSet.array(LocalImageFiles.read_paths(path), distributed)
+
+        @staticmethod
+        def images(path: str, scale_to: int = -1, distributed: bool = False) -> AbstractDataSet:
+            """Decoded LabeledBGRImage records (pixels / 255, shorter side scaled to ``scale_to``),
+            cached in memory like the reference."""
+            from .image import LocalImageFiles, LocalImgReader
+            imgs = list(LocalImgReader(scale_to).apply(iter(LocalImageFiles.read_paths(path))))
+            return DataSet.array(imgs, distributed)
+
+    class SeqFileFolder:
+        """Hadoop SequenceFile image folders (``DataSet.scala:486-640``): LabeledBGRImage records
+        (pixels / 255) of every ``.seq`` file under ``path``."""
+
+        @staticmethod
+        def files(path: str, class_num: Optional[int] = None, distributed: bool = False) -> AbstractDataSet:
+            from .image import LabeledBGRImage
+            from .seqfile import SeqFileFolder as _SF
+            recs = [LabeledBGRImage(torch.from_numpy(img.astype(np.float32) / 255.0), label)
+                    for img, label, _ in _SF.read(path, class_num)]
+            return DataSet.array(recs, distributed)
 
 
 class DevicePrefetcher:

@@ -1,3 +1,3 @@
 """Model utilities (``DL/models/utils``): ``ModelBroadcast``, the optimizer perf harnesses and the
 ImageNet / COCO sequence-file generators."""
-from .model_broadcast import ModelBroadcast  # noqa: F401
+from .model_broadcast import ModelBroadcast, CachedModels  # noqa: F401

@@ -22,3 +22,34 @@ class ModelBroadcast:
         if init_gradient:
             m.zeroGradParameters()
         return m
+
+
+class CachedModels:
+    """Per-process cache of model replicas keyed by a broadcast id (``ModelBroadcast.scala:301-349``):
+    the reference keeps executor-side clones so repeated ``value()`` calls share weights and a
+    finished job can drop them.  ``add`` registers a replica under ``uuid``; ``delete_key`` /
+    ``delete_all(current)`` release replicas (their parameter storage goes back to the caching
+    allocator)."""
+
+    _cache = {}
+
+    @classmethod
+    def add(cls, uuid: str, model) -> None:
+        cls._cache.setdefault(uuid, []).append(model)
+
+    @classmethod
+    def get(cls, uuid: str):
+        return list(cls._cache.get(uuid, []))
+
+    @classmethod
+    def delete_key(cls, uuid: str) -> None:
+        cls._cache.pop(uuid, None)
+
+    @classmethod
+    def delete_all(cls, current: str = None) -> None:
+        for k in list(cls._cache):
+            if k != current:
+                del cls._cache[k]
+
+    deleteKey = delete_key
+    deleteAll = delete_all

@@ -992,3 +992,18 @@ class Activity:
     @staticmethod
     def allocate(is_table: bool):
         return Table() if is_table else torch.empty(0)
+
+
+class EmptyGradInput(Activity):
+    """``gradInput`` placeholder of a module that never propagates a gradient to its input
+    (``Activity.scala`` ``EmptyGradInput``): any use as a tensor raises, naming the module."""
+
+    def __init__(self, module_name: str = ""):
+        self.module_name = module_name
+
+    def __getattr__(self, item):
+        raise RuntimeError(f"{self.module_name or 'module'} does not compute a gradInput "
+                           f"(EmptyGradInput.{item} accessed)")
+
+    def __repr__(self):
+        return f"EmptyGradInput({self.module_name})"

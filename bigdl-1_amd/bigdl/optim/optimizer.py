@@ -323,15 +323,22 @@ class BaseOptimizer:
         if self.flat.shadow is not None:
             self.flat.mark_shadow_fresh()
 
-    def _clip(self, grad: torch.Tensor, local_shard: torch.Tensor):
+    def parameter_processors(self):
+        """The gradient processors of this optimizer, in application order
+        (``Optimizer.scala:76`` ``parameterProcessors``): constant clipping, then L2-norm clipping."""
+        from ..parameters import ConstantClippingProcessor, L2NormClippingProcessor
+        procs = []
         if self.constant_clip is not None:
-            grad.clamp_(self.constant_clip[0], self.constant_clip[1])
+            procs.append(ConstantClippingProcessor(*self.constant_clip))
         if self.l2_clip is not None:
-            sq = (local_shard.float() ** 2).sum()
-            sq = self._global_sum(sq)
-            norm = torch.sqrt(sq)
-            scale = torch.clamp(self.l2_clip / (norm + 1e-6), max=1.0)
-            grad.mul_(scale)
+            procs.append(L2NormClippingProcessor(self.l2_clip))
+        return procs
+
+    def _clip(self, grad: torch.Tensor, local_shard: torch.Tensor):
+        from ..parameters import run_processors
+        # ``grad`` is this rank's gradient shard (the whole arena on one process); the norm of a
+        # sharded gradient is completed by ``_global_sum`` (one all-reduce per processor)
+        run_processors(self.parameter_processors(), None, grad, self._global_sum)
 
     def _global_sum(self, t: torch.Tensor) -> torch.Tensor:
         return t
