@@ -377,8 +377,9 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
     K, Ci, R, S = w4.shape
     if C_ % 4 or K % 8:
         return None
-    # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]
-    wt = w4.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]: one cached-index gather from the KRSC storage (a
+    # flip + transpose copy would be two launches per layer per step)
+    wt = _subfilters(w4, [(0, 0, list(range(R)), list(range(S)))])[0]
     P, Q = gy.shape[2], gy.shape[3]
     ph = dilation[0] * (R - 1) - pad[0]
     pw = dilation[1] * (S - 1) - pad[1]
@@ -426,6 +427,31 @@ def _subfilters(w4, classes):
     K, C_, R, S = w4.shape
     krsc = w4.permute(0, 2, 3, 1)
     phys = krsc if krsc.is_contiguous() else krsc.contiguous()
+    live = [c for c in classes if c[2] and c[3]]
+    if (phys.dtype == _bf16 and phys.is_cuda and C_ % 8 == 0 and K % 8 == 0 and _al16(phys) and 0 < len(live) <= 4
+            and max(max(len(c[2]), len(c[3])) for c in live) <= 8):
+        # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor
+        n = [len(rs) * len(ss) * C_ * K if (rs and ss) else 0 for (a, b, rs, ss, *_r) in classes]
+        out = torch.empty(sum(n), dtype=_bf16, device=w4.device)
+        ros, sos, rm, sm, offs = [], [], [0] * 32, [0] * 32, []
+        off = 0
+        for (a, b, rs, ss, *_r), ni in zip(classes, n):
+            if ni:
+                q = len(ros)
+                ros.append(len(rs))
+                sos.append(len(ss))
+                rm[q * 8:q * 8 + len(rs)] = rs[::-1]
+                sm[q * 8:q * 8 + len(ss)] = ss[::-1]
+                offs.append(off)
+            off += ni
+        IA, LA = C.c_int * 32, C.c_longlong * 4
+        check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, len(ros), IA(*ros), IA(*sos), IA(*rm),
+                                         IA(*sm), LA(*offs), _s()), "w_dgrad_xform")
+        res, off = [], 0
+        for (a, b, rs, ss, *_r), ni in zip(classes, n):
+            res.append(out[off:off + ni].view(C_, len(rs), len(ss), K) if ni else None)
+            off += ni
+        return res
     key = (K, C_, R, S, tuple((a, b, tuple(rs), tuple(ss)) for (a, b, rs, ss, *_r) in classes), w4.device)
     ent = _SUBFILTER_IDX.get(key)
     if ent is None:

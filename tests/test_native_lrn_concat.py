@@ -207,3 +207,26 @@ def test_hip_graph_train_step_vgg_like():
     assert opt.state["neval"] == n0 + 30
     assert losses[-1] < losses[0]
     assert not torch.equal(masks[0], masks[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,C,R,S,stride", [(64, 32, 3, 3, 1), (72, 40, 7, 7, 2), (128, 64, 1, 1, 2), (48, 24, 3, 3, 2), (200, 136, 1, 1, 1)])
+def test_dgrad_weight_transform_kernel(K, C, R, S, stride):
+    """weight_xform.hip: every parity sub-filter W'[c][i][j][k] = W[k][c][rs[-1-i]][ss[-1-j]] in one
+    launch, against the plain index gather."""
+    from bigdl.ops import native_ops as NO
+    w = torch.randn(K, R, S, C, device="cuda").to(torch.bfloat16).permute(0, 3, 1, 2)  # KRSC storage
+    pad = R // 2
+    classes = []
+    for a in range(stride):
+        rs = list(range((a + pad) % stride, R, stride))
+        for b in range(stride):
+            ss = list(range((b + pad) % stride, S, stride))
+            classes.append((a, b, rs, ss))
+    got = NO._subfilters(w, classes)
+    for (a, b, rs, ss), g in zip(classes, got):
+        if not rs or not ss:
+            assert g is None
+            continue
+        ref = w[:, :, rs[::-1]][:, :, :, ss[::-1]].permute(1, 2, 3, 0)
+        torch.testing.assert_close(g, ref, rtol=0, atol=0)
