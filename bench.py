@@ -49,6 +49,14 @@ def main():
     config.set_property("bigdl.comm.dtype", args.comm_dtype)
     from bigdl.utils.engine import Engine
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.force_distri and "RANK" not in os.environ:
+        # a single rank outside torchrun: env:// rendezvous with itself on 127.0.0.1
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     Engine.init(dist=world > 1 or args.force_distri)
     dev = Engine.device()
     rank = Engine.rank()
