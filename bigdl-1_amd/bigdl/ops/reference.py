@@ -177,6 +177,13 @@ def avgpool2d_forward(x, k, s, p, ceil_mode, count_include_pad, divisor=None):
 
 
 def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=None):
+    if (x.dim() == 4 and tuple(k) == tuple(x.shape[-2:]) and tuple(p) == (0, 0) and tuple(gy.shape[-2:]) == (1, 1)):
+        # global average pool (ResNet / Inception heads): gx is gy / (H·W) broadcast — one copy
+        # kernel instead of the generic windowed backward
+        fmt = torch.channels_last if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous() \
+            else torch.contiguous_format
+        g = torch.div(gy, float(divisor or x.shape[-2] * x.shape[-1]))
+        return g.expand(x.shape).contiguous(memory_format=fmt)
     return aten.avg_pool2d_backward(gy, x, list(k), list(s), list(p), ceil_mode, count_include_pad, divisor)
 
 
