@@ -3,6 +3,8 @@
 //
 // Forward: one thread per (output pixel, 8-channel group) — 16-B loads per window tap, the argmax
 // kept as an int8 offset kh·kW + kw inside the window (1 B/element instead of torch's int64).
+// Index math is 32-bit whenever the element count allows (64-bit division is a long software
+// sequence on CDNA), 64-bit otherwise.
 // Backward is a GATHER: each input pixel sums gy over the ≤⌈k/s⌉² windows that chose it, so gx is
 // written exactly once (no zero-fill, no atomics).  Padding is implicit (-inf); ceil mode allowed.
 #include "common.h"
@@ -11,14 +13,14 @@ struct PoolGeom {
   int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
 };
 
+template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                      int8_t* __restrict__ idx, PoolGeom g) {
   const int CG = g.C >> 3;
-  const long long total = (long long)g.N * g.P * g.Q * CG;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
+  const IT total = (IT)g.N * g.P * g.Q * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
     const int cg = (int)(t % CG);
-    long long pix = t / CG;
+    IT pix = t / CG;
     const int q = (int)(pix % g.Q);
     pix /= g.Q;
     const int p = (int)(pix % g.P);
@@ -56,14 +58,14 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
   }
 }
 
+template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ gy, const int8_t* __restrict__ idx,
                                                      bf16_t* __restrict__ gx, PoolGeom g) {
   const int CG = g.C >> 3;
-  const long long total = (long long)g.N * g.H * g.W * CG;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
+  const IT total = (IT)g.N * g.H * g.W * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
     const int cg = (int)(t % CG);
-    long long pix = t / CG;
+    IT pix = t / CG;
     const int w = (int)(pix % g.W);
     pix /= g.W;
     const int h = (int)(pix % g.H);
@@ -113,8 +115,12 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
                                    int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   if (C % 8 || kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
-  const int grid = bigdl_grid((long long)N * P * Q * (C / 8), 256, 16384);
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
+  const long long total = (long long)N * P * Q * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(k_maxpool_fwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_fwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -122,8 +128,13 @@ BIGDL_EXPORT int bigdl_maxpool_bwd(const void* gy, const void* idx, void* gx, in
                                    int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   if (C % 8 || kh * kw > 127 || N <= 0) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
-  const int grid = bigdl_grid((long long)N * H * W * (C / 8), 256, 16384);
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx, (bf16_t*)gx,
-                     g);
+  const long long total = (long long)N * H * W * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(k_maxpool_bwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx,
+                       (bf16_t*)gx, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx,
+                       (bf16_t*)gx, g);
   BIGDL_CHECK_LAUNCH();
 }
