@@ -54,13 +54,15 @@ struct ConvParams {
 };
 
 constexpr int SBM = 128;  // row granularity of the BN-statistics partials (any BM writes BM / SBM rows)
-// k-tile depth is a kernel parameter (64 or 32).  64-wide rows (128 B) take a 16-B-chunk XOR
-// swizzle so a fragment read of 16 rows is conflict-free; 32-wide rows (64 B) are read as one
-// contiguous 1-KiB span per fragment and need none.
+// k-tile depth is a kernel parameter (64 or 32).  A fragment read (ds_read_b128) serves 16 lanes =
+// 16 consecutive rows of one 16-B chunk per cycle; the XOR swizzle places them in 16 distinct 16-B
+// slots of the 256-B bank window.  64-wide rows (128 B, 2 rows per window): chunk ^ (row & 7);
+// 32-wide rows (64 B, 4 rows per window): chunk ^ ((row >> 2) & 3) — unswizzled, rows r and r + 4
+// collide (4-way conflicts, profiles/r1_conv_pmc_v1.txt).
 template <int BK>
 __device__ __forceinline__ int swz(int row, int chunk) {
   if constexpr (BK == 64) return row * BK + ((chunk ^ (row & 7)) << 3);
-  else return row * BK + (chunk << 3);
+  else return row * BK + ((chunk ^ ((row >> 2) & 3)) << 3);
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -417,11 +419,14 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   if (p.stats) {
     // reduce the RPP row groups of each channel chunk through LDS (after the tile reads retire)
     float* red = reinterpret_cast<float*>(&et[BM * LDR]);  // [RPP][BN] Σ, then [RPP][BN] Σ²
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[rr * BN + cc * 8 + e] = s8[e];
-      red[RPP * BN + rr * BN + cc * 8 + e] = q8[e];
-    }
+    // 16-B stores: lanes (consecutive cc) land 32 B apart — conflict-free, where 8 scalar stores
+    // per array at that stride were 8-way bank conflicts (profiles/r1_conv_pmc_v1.txt)
+    float4* rs = reinterpret_cast<float4*>(&red[rr * BN + cc * 8]);
+    float4* rq = reinterpret_cast<float4*>(&red[RPP * BN + rr * BN + cc * 8]);
+    rs[0] = make_float4(s8[0], s8[1], s8[2], s8[3]);
+    rs[1] = make_float4(s8[4], s8[5], s8[6], s8[7]);
+    rq[0] = make_float4(q8[0], q8[1], q8[2], q8[3]);
+    rq[1] = make_float4(q8[4], q8[5], q8[6], q8[7]);
     __syncthreads();
     for (int c = tid; c < BN; c += 256) {
       float a = 0.f, b = 0.f;

@@ -430,23 +430,30 @@ def _subfilters(w4, classes):
     live = [c for c in classes if c[2] and c[3]]
     if (phys.dtype == _bf16 and phys.is_cuda and C_ % 8 == 0 and K % 8 == 0 and _al16(phys) and 0 < len(live) <= 4
             and max(max(len(c[2]), len(c[3])) for c in live) <= 8):
-        # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor
-        n = [len(rs) * len(ss) * C_ * K if (rs and ss) else 0 for (a, b, rs, ss, *_r) in classes]
-        out = torch.empty(sum(n), dtype=_bf16, device=w4.device)
-        ros, sos, rm, sm, offs = [], [], [0] * 32, [0] * 32, []
-        off = 0
-        for (a, b, rs, ss, *_r), ni in zip(classes, n):
-            if ni:
-                q = len(ros)
-                ros.append(len(rs))
-                sos.append(len(ss))
-                rm[q * 8:q * 8 + len(rs)] = rs[::-1]
-                sm[q * 8:q * 8 + len(ss)] = ss[::-1]
-                offs.append(off)
-            off += ni
-        IA, LA = C.c_int * 32, C.c_longlong * 4
-        check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, len(ros), IA(*ros), IA(*sos), IA(*rm),
-                                         IA(*sm), LA(*offs), _s()), "w_dgrad_xform")
+        # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor.  The
+        # ctypes argument block is built once per (shape, classes) — this runs per layer per step.
+        key = ("xf", K, C_, R, S, tuple((tuple(c[2]), tuple(c[3])) for c in classes))
+        ent = _SUBFILTER_IDX.get(key)
+        if ent is None:
+            n = [len(rs) * len(ss) * C_ * K if (rs and ss) else 0 for (a, b, rs, ss, *_r) in classes]
+            ros, sos, rm, sm, offs = [], [], [0] * 32, [0] * 32, []
+            off = 0
+            for (a, b, rs, ss, *_r), ni in zip(classes, n):
+                if ni:
+                    q = len(ros)
+                    ros.append(len(rs))
+                    sos.append(len(ss))
+                    rm[q * 8:q * 8 + len(rs)] = rs[::-1]
+                    sm[q * 8:q * 8 + len(ss)] = ss[::-1]
+                    offs.append(off)
+                off += ni
+            IA, LA = C.c_int * 32, C.c_longlong * 4
+            ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs))
+            _SUBFILTER_IDX[key] = ent
+        n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off = ent
+        out = torch.empty(total, dtype=_bf16, device=w4.device)
+        check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off, _s()),
+              "w_dgrad_xform")
         res, off = [], 0
         for (a, b, rs, ss, *_r), ni in zip(classes, n):
             res.append(out[off:off + ni].view(C_, len(rs), len(ss), K) if ni else None)
