@@ -297,12 +297,23 @@ def _krsc(w4):
     return k if k.is_contiguous() else k.contiguous()
 
 
+_PAD_CACHE = [None]  # (source tensor, its version, c_to, padded): the last padded input
+
+
 def _pad_channels(x_nhwc_4d, c_to):
-    """Zero-pad the channel dim of a channels-last NCHW-logical tensor to ``c_to``."""
+    """Zero-pad the channel dim of a channels-last NCHW-logical tensor to ``c_to``.  The last result
+    is kept (keyed by tensor identity + version counter), so the backward pass of a C % 8 conv (the
+    RGB stem) reuses the forward's padded copy instead of zero-filling and copying 8 channels again."""
+    ent = _PAD_CACHE[0]
+    if ent is not None and ent[0] is x_nhwc_4d and ent[1] == x_nhwc_4d._version and ent[2] == c_to:
+        return ent[3]
     n, c, h, w = x_nhwc_4d.shape
-    out = torch.zeros((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
+    out = torch.empty((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
+    out[..., c:].zero_()
     out[..., :c] = x_nhwc_4d.permute(0, 2, 3, 1)
-    return out.permute(0, 3, 1, 2)
+    res = out.permute(0, 3, 1, 2)
+    _PAD_CACHE[0] = (x_nhwc_4d, x_nhwc_4d._version, c_to, res)
+    return res
 
 
 def _conv_geom_ok(x, w4, groups, dilation):
