@@ -390,7 +390,10 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         return None
     # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]: one cached-index gather from the KRSC storage (a
     # flip + transpose copy would be two launches per layer per step)
-    wt = _subfilters(w4, [(0, 0, list(range(R)), list(range(S)))])[0]
+    ent = _S1_XFORM.get((K, Ci, R, S))
+    if ent is None:
+        ent = _S1_XFORM[(K, Ci, R, S)] = [(0, 0, list(range(R)), list(range(S)))]
+    wt = _subfilters(w4, ent)[0]
     P, Q = gy.shape[2], gy.shape[3]
     ph = dilation[0] * (R - 1) - pad[0]
     pw = dilation[1] * (S - 1) - pad[1]
@@ -431,6 +434,9 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
 _SUBFILTER_IDX: dict = {}
 
 
+_S1_XFORM = {}  # (K, C, R, S) → the single full-filter class list of a stride-1 dgrad
+
+
 def _subfilters(w4, classes):
     """All parity sub-filters of a strided dgrad in ONE gather: W'_ab[c][j'][i'][k] =
     W[k][c][rs[Ra-1-j']][ss[Sb-1-i']], indexed straight from the weight's physical storage (KRSC
@@ -438,13 +444,16 @@ def _subfilters(w4, classes):
     K, C_, R, S = w4.shape
     krsc = w4.permute(0, 2, 3, 1)
     phys = krsc if krsc.is_contiguous() else krsc.contiguous()
-    live = [c for c in classes if c[2] and c[3]]
-    if (phys.dtype == _bf16 and phys.is_cuda and C_ % 8 == 0 and K % 8 == 0 and _al16(phys) and 0 < len(live) <= 4
-            and max(max(len(c[2]), len(c[3])) for c in live) <= 8):
-        # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor.  The
-        # ctypes argument block is built once per (shape, classes) — this runs per layer per step.
-        key = ("xf", K, C_, R, S, tuple((tuple(c[2]), tuple(c[3])) for c in classes))
-        ent = _SUBFILTER_IDX.get(key)
+    # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor.  The
+    # ctypes argument block is built once per (shape, classes object) — this runs per layer per step,
+    # so the hot path is one dict lookup.
+    key = ("xf", K, C_, R, S, id(classes))
+    ent = _SUBFILTER_IDX.get(key)
+    if ent is not None and ent[-1] is not classes:
+        ent = None
+    live = [c for c in classes if c[2] and c[3]] if ent is None else None
+    if (phys.dtype == _bf16 and phys.is_cuda and C_ % 8 == 0 and K % 8 == 0 and _al16(phys)
+            and (ent is not None or (0 < len(live) <= 4 and max(max(len(c[2]), len(c[3])) for c in live) <= 8))):
         if ent is None:
             n = [len(rs) * len(ss) * C_ * K if (rs and ss) else 0 for (a, b, rs, ss, *_r) in classes]
             ros, sos, rm, sm, offs = [], [], [0] * 32, [0] * 32, []
@@ -459,9 +468,9 @@ def _subfilters(w4, classes):
                     offs.append(off)
                 off += ni
             IA, LA = C.c_int * 32, C.c_longlong * 4
-            ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs))
+            ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs), classes)
             _SUBFILTER_IDX[key] = ent
-        n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off = ent
+        n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off, _ = ent
         out = torch.empty(total, dtype=_bf16, device=w4.device)
         check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off, _s()),
               "w_dgrad_xform")
@@ -496,6 +505,25 @@ def _subfilters(w4, classes):
     return out
 
 
+_STRIDED_CLASSES = {}  # geometry → parity-class list (one object per geometry: _subfilters keys on it)
+
+
+def _parity_classes(H, W, R, S, sh, sw, ph, pw):
+    classes = []
+    for a in range(sh):
+        ra = (a + ph) % sh
+        rs = list(range(ra, R, sh))
+        for b in range(sw):
+            sb = (b + pw) % sw
+            ss = list(range(sb, S, sw))
+            ho = (H - a + sh - 1) // sh
+            wo = (W - b + sw - 1) // sw
+            if ho <= 0 or wo <= 0:
+                continue
+            classes.append((a, b, rs, ss, ho, wo, (a + ph - ra) // sh, (b + pw - sb) // sw))
+    return classes
+
+
 def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
     """Strided backward-data by sub-pixel decomposition: the input-gradient pixels of parity
     (a, b) = (h mod sh, w mod sw) receive only the filter taps r ≡ a + ph (mod sh), s ≡ b + pw
@@ -514,18 +542,10 @@ def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
         return None
     P, Q = gy.shape[2], gy.shape[3]
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
-    classes = []
-    for a in range(sh):
-        ra = (a + ph) % sh
-        rs = list(range(ra, R, sh))
-        for b in range(sw):
-            sb = (b + pw) % sw
-            ss = list(range(sb, S, sw))
-            ho = (H - a + sh - 1) // sh
-            wo = (W - b + sw - 1) // sw
-            if ho <= 0 or wo <= 0:
-                continue
-            classes.append((a, b, rs, ss, ho, wo, (a + ph - ra) // sh, (b + pw - sb) // sw))
+    ckey = (H, W, R, S, sh, sw, ph, pw)
+    classes = _STRIDED_CLASSES.get(ckey)
+    if classes is None:
+        classes = _STRIDED_CLASSES[ckey] = _parity_classes(H, W, R, S, sh, sw, ph, pw)
     if any(not rs or not ss for (_, _, rs, ss, *_r) in classes):
         # some parity receives no tap (e.g. 1x1 stride 2): those pixels are exactly zero / the residual
         if residual is not None:
