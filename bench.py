@@ -76,10 +76,15 @@ def main():
               nesterov=True)
     B = args.batch
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(Engine.compute_dtype()).contiguous(
-        memory_format=torch.channels_last)
-    y = (torch.randint(0, 1000, (B,), generator=g) + 1).float().to(dev)
-    batch = MiniBatch(x, y)
+    # two distinct preallocated batches, alternated every step: no step can reuse work cached from
+    # the previous step's input (a real loader hands over a fresh tensor each iteration)
+    batches = []
+    for _ in range(2):
+        x = torch.randn(B, 3, 224, 224, generator=g).to(dev).to(Engine.compute_dtype()).contiguous(
+            memory_format=torch.channels_last)
+        y = (torch.randint(0, 1000, (B,), generator=g) + 1).float().to(dev)
+        batches.append(MiniBatch(x, y))
+    batch = batches[0]
 
     if world > 1 or args.force_distri:
         from bigdl.parallel import DistriOptimizer
@@ -89,8 +94,8 @@ def main():
     opt.prepare()
 
     from bigdl.parallel import comm
-    for _ in range(args.warmup):
-        opt.train_step(batch)
+    for i in range(args.warmup):
+        opt.train_step(batches[i % 2])
     if hasattr(opt, "_wait_all_gathers"):
         opt._wait_all_gathers()
     comm.barrier()
@@ -98,8 +103,8 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = None
-    for _ in range(args.steps):
-        loss = opt.train_step(batch)
+    for i in range(args.steps):
+        loss = opt.train_step(batches[i % 2])
     if hasattr(opt, "_wait_all_gathers"):
         opt._wait_all_gathers()
     if dev.type == "cuda":

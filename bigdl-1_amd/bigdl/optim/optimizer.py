@@ -352,6 +352,7 @@ class BaseOptimizer:
         interval = float(config.get_property("bigdl.failure.retryTimeInterval"))
         failures: List[float] = []
         self._setup_model()
+        self._maybe_resume()
         while True:
             try:
                 self._train_loop()
@@ -359,6 +360,14 @@ class BaseOptimizer:
             except (ValueError, KeyboardInterrupt):
                 raise
             except Exception as e:  # noqa: BLE001 - retry loop (DistriOptimizer.scala:881-963)
+                if Engine.world_size() > 1:
+                    # after a collective failure / watchdog abort the RCCL communicator is dead: a
+                    # distributed rank must not retry in-process (a restore would broadcast over the
+                    # broken group).  Exit non-zero; ``python -m bigdl.launch --max-restarts N``
+                    # relaunches every rank and they resume from the latest checkpoint
+                    # (``_maybe_resume``), the reference's retry-from-checkpoint semantics.
+                    log.error(f"rank {Engine.rank()} failed ({e!r}); exiting so the launcher restarts all ranks")
+                    raise
                 now = time.time()
                 failures = [t for t in failures if now - t < retry * interval] + [now]
                 if self.checkpoint_path is None or len(failures) > retry:
@@ -563,9 +572,25 @@ class BaseOptimizer:
         if Engine.rank() == 0:
             save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite)
 
+    def _maybe_resume(self):
+        """Resume from the latest checkpoint when this process is a launcher restart
+        (``BIGDL_RESTART_COUNT`` > 0, set by ``bigdl.launch --max-restarts``) or when
+        ``bigdl.failure.resume`` is set, and a checkpoint exists under the checkpoint path."""
+        import os
+        from ..serialization.checkpoint import has_checkpoint
+        restart = int(os.environ.get("BIGDL_RESTART_COUNT", "0") or 0) > 0
+        if not (restart or config.get_property("bigdl.failure.resume")):
+            return False
+        if self.checkpoint_path is None or not has_checkpoint(self.checkpoint_path):
+            return False
+        log.info(f"resuming from the latest checkpoint under {self.checkpoint_path}")
+        self._restore_latest()
+        return True
+
     def _restore_latest(self):
         from ..serialization.checkpoint import load_latest_checkpoint
-        model, methods, state = load_latest_checkpoint(self.checkpoint_path)
+        model, methods, state = load_latest_checkpoint(
+            self.checkpoint_path, world_size=Engine.world_size(), sharded=bool(getattr(self, "sharded", False)))
         if model is not None:
             p_dst = self.model.parameters()
             p_src = model.parameters()
@@ -577,11 +602,16 @@ class BaseOptimizer:
                 for a, b in zip(ex_dst, ex_src):
                     a.copy_(b.to(a.device))
         if methods:
+            # copy only the restored STATE into the live method objects: the per-run installation
+            # (grad_scale = 1/W, folded L2 decay vectors, shard-space lr/decay vectors) lives on
+            # those objects and is not part of a checkpoint
             for k, v in methods.items():
-                if k in self.optim_methods:
-                    for sk, sv in v.state.items():
-                        v.state[sk] = sv.to(self.device) if isinstance(sv, torch.Tensor) else sv
-                    self.optim_methods[k] = v
+                cur = self.optim_methods.get(k)
+                if cur is None:
+                    continue
+                cur.state.clear()
+                for sk, sv in v.state.items():
+                    cur.state[sk] = sv.to(self.device) if isinstance(sv, torch.Tensor) else sv
         if state:
             self.state.update(state)
         if self.flat is not None and self.flat.shadow is not None:

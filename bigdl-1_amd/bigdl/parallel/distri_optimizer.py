@@ -361,7 +361,8 @@ class DistriOptimizer(BaseOptimizer):
         from ..serialization.checkpoint import save_checkpoint, save_shard_state
         self._flush_weights()
         if Engine.rank() == 0:
-            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite)
+            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite,
+                            world_size=self.world, sharded=self.sharded)
         if self.sharded:
             save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite)
         comm.barrier()

@@ -122,16 +122,22 @@ def _suffix(state, overwrite):
     return "" if overwrite else f".{state['neval'] - 1}"
 
 
-def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: bool = False):
+def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: bool = False, world_size: int = 1,
+                    sharded: bool = False):
     os.makedirs(path, exist_ok=True)
     sfx = _suffix(state, overwrite)
     save_module(model, os.path.join(path, "model" + sfx), over_write=True)
     for name, m in methods.items():
         m.state.update({k: state[k] for k in ("epoch", "neval", "recordsProcessedThisEpoch") if k in state})
         save_optim_method(m, os.path.join(path, f"optimMethod-{name}" + sfx), over_write=True)
+    meta = {k: (float(v) if isinstance(v, (int, float)) else v) for k, v in state.items()
+            if isinstance(v, (int, float, str))}
+    # how the optimizer state was laid out: a sharded (ZeRO-1) run's un-suffixed optimMethod file
+    # holds only rank 0's shard, so a resume must find its own ``.rank<r>`` file at the same world size
+    meta["_world_size"] = int(world_size)
+    meta["_sharded"] = bool(sharded)
     with open(os.path.join(path, "state" + sfx), "w") as f:
-        json.dump({k: (float(v) if isinstance(v, (int, float)) else v) for k, v in state.items()
-                   if isinstance(v, (int, float, str))}, f)
+        json.dump(meta, f)
 
 
 def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False):
@@ -147,7 +153,26 @@ def _latest(pattern: str) -> Optional[str]:
     return max(files, key=os.path.getmtime)
 
 
-def load_latest_checkpoint(path: str) -> Tuple[Optional[object], Dict, Dict]:
+def has_checkpoint(path: str) -> bool:
+    return _latest(os.path.join(path, "model*")) is not None
+
+
+def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
+                           sharded: Optional[bool] = None) -> Tuple[Optional[object], Dict, Dict]:
+    """Latest model / optimMethods / driver state under ``path``.  With ``world_size`` given, a
+    checkpoint whose optimizer state was sharded is only accepted by a sharded run of the SAME world
+    size that finds its own ``.rank<r>`` state file (no silent fallback to rank 0's shard)."""
+    sfile = _latest(os.path.join(path, "state*"))
+    meta = {}
+    if sfile:
+        with open(sfile) as fh:
+            meta = json.load(fh)
+    ck_sharded = bool(meta.get("_sharded", False))
+    ck_world = int(meta.get("_world_size", 1))
+    if world_size is not None and ck_sharded and (not sharded or ck_world != world_size):
+        raise ValueError(f"checkpoint under {path} holds sharded optimizer state for world size {ck_world}; "
+                         f"this run is world size {world_size} ({'sharded' if sharded else 'replicated'}) — "
+                         "resume with the same world size and bigdl.comm.sharded")
     mfile = _latest(os.path.join(path, "model*"))
     model = load_module(mfile) if mfile else None
     methods = {}
@@ -163,13 +188,11 @@ def load_latest_checkpoint(path: str) -> Tuple[Optional[object], Dict, Dict]:
     rank = int(os.environ.get("RANK", "0"))
     for name, (_, f) in methods.items():
         shard = f + f".rank{rank}"
-        loaded[name] = load_optim_method(shard if os.path.exists(shard) else f)
-    sfile = _latest(os.path.join(path, "state*"))
-    state = {}
-    if sfile:
-        with open(sfile) as fh:
-            state = json.load(fh)
-        for k in ("epoch", "neval", "recordsProcessedThisEpoch"):
-            if k in state:
-                state[k] = int(state[k])
+        if ck_sharded and not os.path.exists(shard):
+            raise FileNotFoundError(f"sharded checkpoint: missing this rank's optimizer state {shard}")
+        loaded[name] = load_optim_method(shard if ck_sharded else f)
+    state = {k: v for k, v in meta.items() if not k.startswith("_")}
+    for k in ("epoch", "neval", "recordsProcessedThisEpoch"):
+        if k in state:
+            state[k] = int(state[k])
     return model, loaded, state

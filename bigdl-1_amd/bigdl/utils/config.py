@@ -27,16 +27,26 @@ _REGISTRY = {
     "bigdl.graph.capture": (bool, False, "LocalOptimizer on a GPU: capture the training step into a HIP graph"),
     "bigdl.comm.timeout": (float, 600.0, "collective watchdog: seconds before a hung RCCL/gloo collective raises"),
     "bigdl.failure.retryTimeInterval": (int, 120, "retry window seconds"),
+    "bigdl.failure.resume": (bool, False, "resume from the latest checkpoint at optimize() start (automatic after a launcher restart)"),
+    # straggler monitor (P5, DistriOptimizer.scala:246-278,421-449)
+    "bigdl.straggler.window": (int, 20, "iterations between straggler checks (all-gather of per-rank step times)"),
+    "bigdl.straggler.factor": (float, 1.5, "a rank is slow when its step time exceeds factor x the kthLargest threshold"),
     # parameter sync
     "bigdl.Parameter.syncPoolSize": (int, 4, "compat"),
     "bigdl.Parameter.computePoolSize": (int, 0, "compat"),
     "bigdl.parallelOptimizer.parameterBlocks": (int, 10, "number of gradient buckets for overlap mode"),
     # device / precision (new)
-    "bigdl.compute.dtype": (str, "fp32", "fp32 | bf16 activations/weights for device compute"),
+    "bigdl.compute.dtype": (str, "auto", "auto (bf16 on a GPU, fp32 on the host) | fp32 | bf16 compute dtype"),
     "bigdl.comm.dtype": (str, "fp32", "fp32 | bf16 | bf16_truncate wire format for gradient reduction"),
     "bigdl.comm.bucketMB": (float, 32.0, "gradient bucket size for RCCL collectives"),
     "bigdl.comm.overlap": (bool, True, "overlap gradient reduce-scatter with backward"),
     "bigdl.comm.sharded": (bool, True, "reduce-scatter + sharded update + all-gather (ZeRO-1)"),
+    "bigdl.comm.channels": (int, 0, "RCCL channel cap (NCCL_MIN/MAX_NCHANNELS, set by the launcher before any GPU call; 0 = RCCL default): bounds the CUs collectives take from compute"),
+    "bigdl.comm.streamPriority": (int, -1, "priority of the comm-side stream that runs the shard update + all-gather (-1 = high, 0 = normal)"),
+    # observability
+    "bigdl.metrics.jsonPath": (str, "", "per-rank JSON metrics stream: one line per iteration to <path>.rank<r>.jsonl ('' = off)"),
+    "bigdl.metrics.deviceTimers": (bool, False, "time the distributed phases with HIP events (adds no host sync)"),
+    "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),

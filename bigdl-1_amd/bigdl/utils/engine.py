@@ -67,7 +67,12 @@ class Engine:
                 _S.device = torch.device("cpu")
             if _S.device.type == "cuda":
                 torch.cuda.set_device(_S.device)
-            _S.compute_dtype = _DTYPES[config.get_property("bigdl.compute.dtype")]
+            want = str(config.get_property("bigdl.compute.dtype")).lower()
+            if want == "auto":
+                # device compute is bf16 with fp32 master weights (the HIP conv/GEMM kernels are
+                # bf16 MFMA); host compute stays fp32 like the reference
+                want = "bf16" if _S.device.type == "cuda" else "fp32"
+            _S.compute_dtype = _DTYPES[want]
             want_dist = dist if dist is not None else env_world > 1
             if want_dist:
                 import torch.distributed as tdist

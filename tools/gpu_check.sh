@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 STEPS=${STEPS:-20}
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -15 gpurun_out/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 5 ]; then echo "pytest gpu failed rc=$rc"; exit $rc; fi
 fi
