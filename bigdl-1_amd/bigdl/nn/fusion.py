@@ -131,6 +131,30 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=Non
     return model
 
 
+def mark_input_no_grad(model):
+    """The optimizer discards the model's gradInput, so the first layer need not compute it: flag
+    the conv(s) that consume the model input (first module of nested Sequentials / the input nodes
+    of a Graph) to skip their backward-data pass.  For an RGB (C = 3) stem that pass is also the
+    one shape the native dgrad does not cover.  Execution flag only, like :func:`fuse`."""
+    from .graph import Graph
+    todo, seen = [model], set()
+    while todo:
+        m = todo.pop()
+        if id(m) in seen:
+            continue
+        seen.add(id(m))
+        if isinstance(m, Sequential):
+            if m.modules:
+                todo.append(m.modules[0])
+        elif isinstance(m, Graph) and hasattr(m, "forward_order"):
+            for n in m.forward_order:
+                if not n.prev_nodes:
+                    todo.append(n.element)
+        elif isinstance(m, SpatialConvolution):
+            m._input_grad_needed = False
+    return model
+
+
 def unfuse(model):
     model._fused = False
     for m in model.flattened_modules():
@@ -143,6 +167,7 @@ def unfuse(model):
             m._fused_relu = False
             m._bn_bwd_target = None
             m._tail_candidates = None
+            m._input_grad_needed = True
         if isinstance(m, BatchNormalization):
             m._bias_producer = None
             m._fused_relu = False

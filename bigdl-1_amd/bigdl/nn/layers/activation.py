@@ -85,6 +85,12 @@ class SoftMax(TensorModule):
         d = self._dim(input)
         if d == -1:
             return ops.softmax_forward(input)
+        if d == 1 and input.is_cuda and ops.native_has("softmax_forward"):
+            # NHWC device layout: the channel softmax is a row softmax over contiguous channels
+            r = ops.native_ops.softmax_channels_nhwc(input)
+            if r is not NotImplemented:
+                return r
+            ops.native.note_fallback("softmax_forward.channels", "layout", (input,))
         return torch.softmax(input.float(), dim=d).to(input.dtype)
 
     def updateGradInput(self, input, gradOutput):
@@ -92,6 +98,11 @@ class SoftMax(TensorModule):
         y = self.output
         if d == -1:
             return ops.softmax_backward(gradOutput, y)
+        if d == 1 and y.is_cuda and ops.native_has("softmax_backward"):
+            r = ops.native_ops.softmax_channels_nhwc(y, backward_gy=gradOutput)
+            if r is not NotImplemented:
+                return r
+            ops.native.note_fallback("softmax_backward.channels", "layout", (y,))
         return (y * (gradOutput - (gradOutput * y).sum(d, keepdim=True))).to(y.dtype)
 
 

@@ -147,6 +147,14 @@ class SpatialConvolution(TensorModule):
     #: dgrad epilogue then also applies that ReLU mask and produces the tail BN's reductions
     _tail_candidates = None
 
+    def _pad_slot_(self):
+        """One-entry holder for the channel-padded copy of a C % 8 input (RGB stem): made by the
+        forward, reused by this layer's backward of the same input (ops.native_ops._pad_channels)."""
+        s = self.__dict__.get("_pad_slot")
+        if s is None:
+            s = self.__dict__["_pad_slot"] = [None]
+        return s
+
     def _tail_target(self, x):
         for bn in self._tail_candidates or ():
             y = bn.output
@@ -175,7 +183,8 @@ class SpatialConvolution(TensorModule):
         y = NotImplemented
         if bn is not None and ops.native_has("conv2d_forward"):
             r = ops.native_ops.conv2d_forward_stats(x, w4, b, (self.strideH, self.strideW), pad,
-                                                (self.dilationH, self.dilationW), self.nGroup)
+                                                (self.dilationH, self.dilationW), self.nGroup,
+                                                pad_slot=self._pad_slot_())
             if r is not NotImplemented:
                 y, part, G = r
                 bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G)
@@ -184,7 +193,7 @@ class SpatialConvolution(TensorModule):
             if tgt is not None and (not batched or self.format != "NCHW"):
                 tgt = None
             y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
-                                   self.nGroup, relu=self._fused_relu, out=tgt)
+                                   self.nGroup, relu=self._fused_relu, out=tgt, pad_slot=self._pad_slot_())
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)
@@ -218,7 +227,8 @@ class SpatialConvolution(TensorModule):
                 bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output}
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                  self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0,
-                                 residual=to_device_layout(res) if fuse_res else None, bn_fuse=bn_fuse)
+                                 residual=to_device_layout(res) if fuse_res else None, bn_fuse=bn_fuse,
+                                 pad_slot=self._pad_slot_())
         if bn_fuse is not None and "partial" in bn_fuse and gi is not None:
             bn._pending_grad = (gi.data_ptr(), bn_fuse["partial"], bn_fuse["G"])
         if acc and own_bias and not same_scale and self.scale_b != 0:
@@ -235,7 +245,15 @@ class SpatialConvolution(TensorModule):
                 gi = gi + res
         return gi
 
+    #: False when this conv consumes the model input of a training run (set by
+    #: bigdl.nn.fusion.mark_input_no_grad): the optimizer never reads that gradInput
+    _input_grad_needed = True
+
     def updateGradInput(self, input, gradOutput):
+        if not self._input_grad_needed and self.propagateBack:
+            self._gi_done = False
+            if self._grad_residual is None:
+                return torch.empty(0, device=input.device, dtype=input.dtype)
         if not self.propagateBack:
             self._gi_done = False
             res, self._grad_residual = self._grad_residual, None

@@ -61,7 +61,9 @@ class Linear(TensorModule):
             if x.dtype != dt and x.is_floating_point():
                 x = x.to(dt)
             x = x.contiguous()
-        y = ops.linear_forward(x, self.cw("weight"), self.cw("bias") if self.withBias else None)
+        # device: the fp32 master bias goes straight into the GEMM epilogue (no per-call cast)
+        b = (self.bias if x.is_cuda else self.cw("bias")) if self.withBias else None
+        y = ops.linear_forward(x, self.cw("weight"), b)
         if input.dim() == 1:
             return y.squeeze(0)
         if input.dim() > 2:

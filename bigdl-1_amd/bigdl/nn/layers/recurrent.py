@@ -153,6 +153,14 @@ def _fire_grad_ready(mods):
             h(m)
 
 
+def _fused_rnn_ok(H, *ts) -> bool:
+    """Fused MFMA recurrent step applies: bf16 device rows, H % 8 == 0, native library loaded."""
+    if not all(isinstance(t, torch.Tensor) for t in ts) or not ts[0].is_cuda:
+        return False
+    from ...ops import native_ops as NO
+    return NO.rnn_fast_ok(H, *ts)
+
+
 def _cdtype(t: torch.Tensor):
     if t.is_cuda:
         from ...utils.engine import Engine
@@ -770,6 +778,14 @@ class Recurrent(Container):
         c = self.topology
         return self.fast_lstm and type(c) is LSTM and c.fused and not self.maskZero
 
+    def _use_fast_gru(self, x2):
+        c = self.topology
+        if not (self.fast_lstm and type(c) is GRU and c.p == 0 and not self.maskZero and x2.dim() == 3):
+            return False
+        if not (_is_default(c.activation, Tanh) and _is_default(c.innerActivation, Sigmoid)):
+            return False
+        return _fused_rnn_ok(c.outputSize, x2, c.h2g[0].cw("weight"), c.u_h.cw("weight"))
+
     def updateOutput(self, input):
         if input.dim() not in (3, 5, 6):
             raise ValueError(f"Recurrent: input should be a 3D/5D/6D Tensor, e.g [batch, times, nDim], "
@@ -780,6 +796,8 @@ class Recurrent(Container):
         self._x2 = x2
         if self._use_fast_lstm():
             return self._lstm_forward(x2)
+        if self._use_fast_gru(x2):
+            return self._gru_forward(x2)
         return self._generic_forward(input, x2)
 
     def _lstm_forward(self, x2):
@@ -797,16 +815,61 @@ class Recurrent(Container):
             acts = torch.empty(Tn, B, G, device=x2.device, dtype=torch.float32)
             tcs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
             cs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
-        h, c = h0, c0
-        for t in range(Tn):
-            hg = torch.mm(h, U.t())
-            if train:
-                h, c, _, _ = ops.lstm_cell_forward(x2[:, t], hg, c, h_out=out[:, t], c_out=cs[t], act_out=acts[t],
-                                                   tc_out=tcs[t])
-            else:
-                h, c, _, _ = ops.lstm_cell_forward(x2[:, t], hg, c, h_out=out[:, t])
+        if _fused_rnn_ok(H, x2, U):
+            # one launch per step: h·Uᵀ on MFMA + the cell update in the GEMM epilogue (rnn_step.hip)
+            from ...ops import native_ops as NO
+            h0 = h0.contiguous()
+            c0 = c0.contiguous()
+            if not train:
+                cbuf = [torch.empty(B, H, device=x2.device, dtype=torch.float32) for _ in range(2)]
+            c = c0
+            for t in range(Tn):
+                a = h0 if t == 0 else out[:, t - 1]
+                c_out = cs[t] if train else cbuf[t % 2]
+                NO.rnn_step("lstm_fwd", a, U, B, H, H, xg=x2[:, t], c_prev=c, h_out=out[:, t], c_out=c_out,
+                            act=acts[t] if train else None, tc=tcs[t] if train else None)
+                c = c_out
+            h = out[:, Tn - 1]
+        else:
+            h, c = h0, c0
+            for t in range(Tn):
+                hg = torch.mm(h, U.t())
+                if train:
+                    h, c, _, _ = ops.lstm_cell_forward(x2[:, t], hg, c, h_out=out[:, t], c_out=cs[t],
+                                                       act_out=acts[t], tc_out=tcs[t])
+                else:
+                    h, c, _, _ = ops.lstm_cell_forward(x2[:, t], hg, c, h_out=out[:, t])
         self._last_hidden = T(h, c)
         self._rec = ("lstm", h0, c0, out, acts, tcs, cs) if train else None
+        return out
+
+    def _gru_forward(self, x2):
+        """GRU time loop on two fused launches per step (rnn_step.hip cells 2 and 3)."""
+        from ...ops import native_ops as NO
+        cell: GRU = self.topology
+        B, Tn, _ = x2.shape
+        H = cell.outputSize
+        urz, uh = cell.h2g[0], cell.u_h
+        _fire_pre_forward([urz, uh])
+        Urz, Uh = urz.cw("weight"), uh.cw("weight")
+        (h0,) = self._h0(B, [H], x2.device, x2.dtype)
+        h0 = h0.to(x2.dtype).contiguous()
+        dev = x2.device
+        out = torch.empty(B, Tn, H, device=dev, dtype=x2.dtype)
+        train = self.train
+        nS = Tn if train else 1
+        R = torch.empty(nS, B, H, device=dev, dtype=torch.float32)
+        Z = torch.empty(nS, B, H, device=dev, dtype=torch.float32)
+        Nn = torch.empty(nS, B, H, device=dev, dtype=torch.float32) if train else None
+        RH = torch.empty(B, Tn if train else 1, H, device=dev, dtype=x2.dtype)
+        for t in range(Tn):
+            hp = h0 if t == 0 else out[:, t - 1]
+            k = t if train else 0
+            NO.rnn_step("gru_fwd1", hp, Urz, B, H, H, xg=x2[:, t], hprev=hp, rh=RH[:, k], s0=R[k], s1=Z[k])
+            NO.rnn_step("gru_fwd2", RH[:, k], Uh, B, H, H, xg=x2[:, t], hprev=hp, s1=Z[k], h_out=out[:, t],
+                        s2=Nn[k] if train else None)
+        self._last_hidden = out[:, Tn - 1]
+        self._rec = ("gru", h0, out, R, Z, Nn, RH) if train else None
         return out
 
     def _generic_forward(self, input, x2):
@@ -853,6 +916,8 @@ class Recurrent(Container):
             raise RuntimeError("Recurrent: backward called without a training-mode forward")
         if rec[0] == "lstm":
             return self._lstm_backward(gradOutput)
+        if rec[0] == "gru":
+            return self._gru_backward(gradOutput)
         _, tape, xl, flat0, out = rec
         targets = ([xl] if xl.requires_grad else []) + flat0 + tape.param_leaves()
         grads = torch.autograd.grad([out], targets, [gradOutput.to(out.dtype)], allow_unused=True)
@@ -873,11 +938,22 @@ class Recurrent(Container):
         if not gy.is_contiguous():
             gy = gy.contiguous()
         DG = torch.empty(B, Tn, 4 * H, device=out.device, dtype=out.dtype)
-        gh_rec, gc = None, None
-        for t in range(Tn - 1, -1, -1):
-            c_prev = cs[t - 1] if t > 0 else c0
-            dg, gc = ops.lstm_cell_backward(gy[:, t], gh_rec, gc, acts[t], tcs[t], c_prev, dg_out=DG[:, t])
-            gh_rec = torch.mm(dg, U)
+        if _fused_rnn_ok(H, out, U, gy):
+            # one launch per step: dh = gy_t + dg_{t+1}·U on MFMA, cell backward in the epilogue
+            from ...ops import native_ops as NO
+            Ut = NO.transpose_bf16(U)  # (H, 4H)
+            gc = torch.empty(B, H, device=out.device, dtype=torch.float32)
+            for t in range(Tn - 1, -1, -1):
+                NO.rnn_step("lstm_bwd", DG[:, t + 1] if t + 1 < Tn else None, Ut, B, 4 * H, H, gy=gy[:, t],
+                            act=acts[t], tc=tcs[t], c_prev=cs[t - 1] if t > 0 else c0,
+                            gc_next=gc if t + 1 < Tn else None, dg=DG[:, t], dc_prev=gc)
+            gh_rec = NO.gemm(DG[:, 0], Ut)
+        else:
+            gh_rec, gc = None, None
+            for t in range(Tn - 1, -1, -1):
+                c_prev = cs[t - 1] if t > 0 else c0
+                dg, gc = ops.lstm_cell_backward(gy[:, t], gh_rec, gc, acts[t], tcs[t], c_prev, dg_out=DG[:, t])
+                gh_rec = torch.mm(dg, U)
         self._grad_hidden_state = [gh_rec, gc]
         # dU = Σ_t dgᵀ h_{t-1}: one GEMM over all B·T rows
         hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)
@@ -888,6 +964,42 @@ class Recurrent(Container):
             if m.wRegularizer is not None:
                 m.wRegularizer.accRegularization(m.weight, m.gradWeight, m.scale_w)
         _fire_grad_ready([m])
+        self._rec = None
+        return DG
+
+    def _gru_backward(self, gradOutput):
+        from ...ops import native_ops as NO
+        _, h0, out, R, Z, Nn, RH = self._rec
+        cell: GRU = self.topology
+        urz, uh = cell.h2g[0], cell.u_h
+        Urz, Uh = urz.cw("weight"), uh.cw("weight")
+        B, Tn, H = out.shape
+        gy = gradOutput.to(out.dtype)
+        if not gy.is_contiguous():
+            gy = gy.contiguous()
+        dev = out.device
+        Urz_t, Uh_t = NO.transpose_bf16(Urz), NO.transpose_bf16(Uh)  # (H, 2H), (H, H)
+        DG = torch.empty(B, Tn, 3 * H, device=dev, dtype=out.dtype)  # (da_r, da_z, da_n) per step
+        carry = torch.zeros(B, H, device=dev, dtype=torch.float32)
+        for t in range(Tn - 1, -1, -1):
+            hp = h0 if t == 0 else out[:, t - 1]
+            NO.rnn_step("gru_bwd1", DG[:, t + 1, :2 * H] if t + 1 < Tn else None, Urz_t, B, 2 * H, H, gy=gy[:, t],
+                        s0=carry, s1=Z[t], s2=Nn[t], hprev=hp, dg=DG[:, t])
+            NO.rnn_step("gru_bwd2", DG[:, t, 2 * H:], Uh_t, B, H, H, s0=carry, s1=R[t], hprev=hp, dg=DG[:, t])
+        NO.gemm(DG[:, 0, :2 * H], Urz_t, out=carry, beta=1.0)  # dh0 = carry + da_rz_0 · U_rz
+        self._grad_hidden_state = [carry]
+        hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)
+        if urz.scale_w != 0:
+            ops.linear_backward(DG[:, :, :2 * H].reshape(B * Tn, 2 * H), hprev.reshape(B * Tn, H), Urz, False,
+                                urz.gradWeight, None, urz.scale_w)
+            if urz.wRegularizer is not None:
+                urz.wRegularizer.accRegularization(urz.weight, urz.gradWeight, urz.scale_w)
+        if uh.scale_w != 0:
+            ops.linear_backward(DG[:, :, 2 * H:].reshape(B * Tn, H), RH.reshape(B * Tn, H), Uh, False,
+                                uh.gradWeight, None, uh.scale_w)
+            if uh.wRegularizer is not None:
+                uh.wRegularizer.accRegularization(uh.weight, uh.gradWeight, uh.scale_w)
+        _fire_grad_ready([urz, uh])
         self._rec = None
         return DG
 

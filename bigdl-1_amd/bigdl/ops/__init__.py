@@ -11,6 +11,9 @@ from __future__ import annotations
 from . import reference
 from .dispatch import *  # noqa: F401,F403
 from .dispatch import native_status, native_has, __all__ as _dispatch_all  # noqa: F401
+from .dispatch import fallback_counts, reset_fallbacks  # noqa: F401
 from . import native_ops  # noqa: F401  (fused entry points beyond the dispatch table)
+from . import native  # noqa: F401
 
-__all__ = list(_dispatch_all) + ["reference", "native_status", "native_has", "native_ops"]
+__all__ = list(_dispatch_all) + ["reference", "native_status", "native_has", "native_ops", "native",
+                                 "fallback_counts", "reset_fallbacks"]

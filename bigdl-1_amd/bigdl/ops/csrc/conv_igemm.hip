@@ -462,7 +462,7 @@ static void launch_fwd(bool fast, dim3 grid, hipStream_t s, const ConvParams& p)
     hipLaunchKernelGGL((k_conv_fwd<BN, false, BM, BK>), grid, dim3(256), 0, s, p);
 }
 
-// Host launchers.  Requirements (checked): C % 8 == 0, K % 4 == 0, 16-B aligned x/w/y/res.
+// Host launchers.  Requirements (checked): C % 8 == 0 (any K; residual / statistics need K % 8), 16-B aligned x/w/y/res.
 // ``stats`` (optional) receives 2·G·K floats, G = bigdl_conv_num_row_tiles(Nb·P·Q).
 BIGDL_EXPORT int bigdl_conv_num_row_tiles(long long M) { return (int)((M + SBM - 1) / SBM); }
 
@@ -472,7 +472,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
                            hipStream_t s) {
-  if (C % 8 || K % 4 || Nb <= 0) return (int)hipErrorInvalidValue;
+  if (C % 8 || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;  // any K: partial 8-channel chunks store per element
   if (ldy < K || (ldy != K && (ldy % 8 || K % 8 || ((uintptr_t)y & 15)))) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB

@@ -99,8 +99,23 @@ BIGDL_EXPORT int bigdl_threshold_bwd_bf16(const void* gy, const void* ref, void*
 template <bool MOM, bool NEST, bool FIRST, bool SHADOW, bool PERELEM>
 __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ buf,
                       bf16_t* __restrict__ shadow, const float* __restrict__ lrs, const float* __restrict__ wds,
-                      long long n4, float lr, float mom, float damp, float wd, float scale) {
+                      long long n4, float lr, float mom, float damp, float wd, float scale, int tail) {
   long long stride = (long long)gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < tail) {
+    // the n % 4 trailing elements (scalar; the arena slice need not be a multiple of 4)
+    const long long e = n4 * 4 + threadIdx.x;
+    const float wv = w[e];
+    const float gg = g[e] * scale + wd * (PERELEM && wds ? wds[e] : 1.f) * wv;
+    float d = gg;
+    if (MOM) {
+      const float b = FIRST ? gg : mom * buf[e] + (1.f - damp) * gg;
+      buf[e] = b;
+      d = NEST ? gg + mom * b : b;
+    }
+    const float nw = wv - lr * (PERELEM && lrs ? lrs[e] : 1.f) * d;
+    w[e] = nw;
+    if (SHADOW) shadow[e] = f2bf(nw);
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 W = reinterpret_cast<float4*>(w)[i];
     float4 G = reinterpret_cast<const float4*>(g)[i];
@@ -145,16 +160,16 @@ __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float*
 
 #define SGD_LAUNCH(M, NS, F, SH, PE)                                                                    \
   hipLaunchKernelGGL((k_sgd<M, NS, F, SH, PE>), dim3(grid), dim3(256), 0, s, w, g, buf, shadow, lrs, wds, n4, lr, \
-                     mom, damp, wd, scale)
+                     mom, damp, wd, scale, tail)
 
-// n must be a multiple of 4 and all pointers 16-B aligned (host-checked).
+// all pointers 16-B aligned (host-checked); the n % 4 tail is handled by block 0.
 BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
                            long long n, float lr, float mom, float damp, float wd, int nesterov, int first,
                            float scale, hipStream_t s) {
   if (n <= 0) return 0;
-  if (n % 4) return (int)hipErrorInvalidValue;
-  long long n4 = n / 4;
-  int grid = bigdl_grid(n4, 256);
+  const long long n4 = n / 4;
+  const int tail = (int)(n & 3);
+  int grid = bigdl_grid(n4 > 0 ? n4 : 1, 256);
   bool M = mom != 0.f, NS = nesterov != 0, F = first != 0, SH = shadow != nullptr, PE = (lrs || wds);
   // dispatch the common combinations without per-element branches
   if (!PE) {
@@ -193,8 +208,18 @@ BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow,
 // ------------------------------------------------------------------------------------------------
 __global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, bf16_t* __restrict__ shadow, long long n4, float step_size, float b1,
-                       float b2, float eps, float wd, float scale) {
+                       float b2, float eps, float wd, float scale, int tail) {
   long long stride = (long long)gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < tail) {
+    const long long e = n4 * 4 + threadIdx.x;
+    const float gg = g[e] * scale + wd * w[e];
+    const float mm = b1 * m[e] + (1.f - b1) * gg, vv = b2 * v[e] + (1.f - b2) * gg * gg;
+    m[e] = mm;
+    v[e] = vv;
+    const float nw = w[e] - step_size * mm / (sqrtf(vv) + eps);
+    w[e] = nw;
+    if (shadow) shadow[e] = f2bf(nw);
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 W = reinterpret_cast<float4*>(w)[i];
     float4 G = reinterpret_cast<const float4*>(g)[i];
@@ -223,9 +248,8 @@ __global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float
 BIGDL_EXPORT int bigdl_adam(float* w, const float* g, float* m, float* v, bf16_t* shadow, long long n,
                             float step_size, float b1, float b2, float eps, float wd, float scale, hipStream_t s) {
   if (n <= 0) return 0;
-  if (n % 4) return (int)hipErrorInvalidValue;
-  long long n4 = n / 4;
-  hipLaunchKernelGGL(k_adam, dim3(bigdl_grid(n4, 256)), dim3(256), 0, s, w, g, m, v, shadow, n4, step_size, b1, b2,
-                     eps, wd, scale);
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adam, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, m, v, shadow, n4,
+                     step_size, b1, b2, eps, wd, scale, (int)(n & 3));
   BIGDL_CHECK_LAUNCH();
 }

@@ -104,6 +104,64 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
   }
 }
 
+// Channel counts that are not a multiple of 8 (LeNet's 6 / 12 maps): one thread per element, same
+// int8 window-offset argmax and gather backward as the vector kernels above.
+__global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                        int8_t* __restrict__ idx, PoolGeom g, long long total) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % g.C);
+    long long pix = t / g.C;
+    const int q = (int)(pix % g.Q);
+    pix /= g.Q;
+    const int p = (int)(pix % g.P);
+    const int n = (int)(pix / g.P);
+    float best = -INFINITY;
+    int arg = 0;
+    const int h0 = p * g.sh - g.ph, w0 = q * g.sw - g.pw;
+    for (int i = 0; i < g.kh; ++i) {
+      const int h = h0 + i;
+      if ((unsigned)h >= (unsigned)g.H) continue;
+      for (int j = 0; j < g.kw; ++j) {
+        const int w = w0 + j;
+        if ((unsigned)w >= (unsigned)g.W) continue;
+        const float v = bf2f(x[(((size_t)n * g.H + h) * g.W + w) * g.C + c]);
+        if (v > best || v != v) {
+          best = v;
+          arg = i * g.kw + j;
+        }
+      }
+    }
+    y[t] = f2bf(best);
+    idx[t] = (int8_t)arg;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd_c1(const bf16_t* __restrict__ gy, const int8_t* __restrict__ idx,
+                                                        bf16_t* __restrict__ gx, PoolGeom g, long long total) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % g.C);
+    long long pix = t / g.C;
+    const int w = (int)(pix % g.W);
+    pix /= g.W;
+    const int h = (int)(pix % g.H);
+    const int n = (int)(pix / g.H);
+    const int hp = h + g.ph, wp = w + g.pw;
+    int p_lo = hp - g.kh + 1;
+    p_lo = p_lo <= 0 ? 0 : (p_lo + g.sh - 1) / g.sh;
+    const int p_hi = min(hp / g.sh, g.P - 1);
+    int q_lo = wp - g.kw + 1;
+    q_lo = q_lo <= 0 ? 0 : (q_lo + g.sw - 1) / g.sw;
+    const int q_hi = min(wp / g.sw, g.Q - 1);
+    float acc = 0.f;
+    for (int p = p_lo; p <= p_hi; ++p)
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + c;
+        if (idx[o] == (int8_t)((hp - p * g.sh) * g.kw + (wp - q * g.sw))) acc += bf2f(gy[o]);
+      }
+    gx[t] = f2bf(acc);
+  }
+}
+
 static PoolGeom make_geom(int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw) {
   PoolGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q;
@@ -113,8 +171,14 @@ static PoolGeom make_geom(int N, int H, int W, int C, int P, int Q, int kh, int 
 
 BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int P, int Q, int kh,
                                    int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
-  if (C % 8 || kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0) return (int)hipErrorInvalidValue;
+  if (kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (C % 8) {
+    const long long te = (long long)N * P * Q * C;
+    hipLaunchKernelGGL(k_maxpool_fwd_c1, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+                       (int8_t*)idx, g, te);
+    BIGDL_CHECK_LAUNCH();
+  }
   const long long total = (long long)N * P * Q * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
   if (total < 0x7fffffffLL)
@@ -126,8 +190,14 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
 
 BIGDL_EXPORT int bigdl_maxpool_bwd(const void* gy, const void* idx, void* gx, int N, int H, int W, int C, int P, int Q,
                                    int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
-  if (C % 8 || kh * kw > 127 || N <= 0) return (int)hipErrorInvalidValue;
+  if (kh * kw > 127 || N <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (C % 8) {
+    const long long te = (long long)N * H * W * C;
+    hipLaunchKernelGGL(k_maxpool_bwd_c1, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)gy,
+                       (const int8_t*)idx, (bf16_t*)gx, g, te);
+    BIGDL_CHECK_LAUNCH();
+  }
   const long long total = (long long)N * H * W * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
   if (total < 0x7fffffffLL)
@@ -136,5 +206,115 @@ BIGDL_EXPORT int bigdl_maxpool_bwd(const void* gy, const void* idx, void* gx, in
   else
     hipLaunchKernelGGL(k_maxpool_bwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx,
                        (bf16_t*)gx, g);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// K11: average pooling, NHWC bf16 (SpatialAveragePooling.updateOutput / updateGradInput,
+// DL/nn/SpatialAveragePooling.scala:115-700).  Divisor semantics are torch's avg_pool2d ones (the
+// reference path): count_include_pad counts the padded window clipped to the padded extent
+// (ceil-mode overhang excluded); otherwise the in-image tap count; `divisor` > 0 overrides both.
+// Forward: one thread per (output pixel, 8 channels).  Backward: a gather — each input pixel sums
+// gy / count over the windows that cover it, so gx is written once with no zero-fill or atomics.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float avg_count(const PoolGeom& g, int p, int q, int cip, int divisor) {
+  if (divisor > 0) return (float)divisor;
+  int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+  int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
+  if (cip) return (float)((he - hs) * (we - ws));
+  hs = max(hs, 0); ws = max(ws, 0);
+  he = min(he, g.H); we = min(we, g.W);
+  return (float)((he - hs) * (we - ws));
+}
+
+template <typename IT>
+__global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g,
+                                                     int cip, int divisor) {
+  const int CG = g.C >> 3;
+  const IT total = (IT)g.N * g.P * g.Q * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    IT pix = t / CG;
+    const int q = (int)(pix % g.Q);
+    pix /= g.Q;
+    const int p = (int)(pix % g.P);
+    const int n = (int)(pix / g.P);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int h0 = p * g.sh - g.ph, w0 = q * g.sw - g.pw;
+    const int hb = max(h0, 0), he = min(h0 + g.kh, g.H), wb = max(w0, 0), we = min(w0 + g.kw, g.W);
+    for (int h = hb; h < he; ++h)
+      for (int w = wb; w < we; ++w) {
+        float v[8];
+        load8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    const float inv = 1.f / fmaxf(avg_count(g, p, q, cip, divisor), 1.f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    store8(y + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, acc);
+  }
+}
+
+template <typename IT>
+__global__ void __launch_bounds__(256) k_avgpool_bwd(const bf16_t* __restrict__ gy, bf16_t* __restrict__ gx, PoolGeom g,
+                                                     int cip, int divisor) {
+  const int CG = g.C >> 3;
+  const IT total = (IT)g.N * g.H * g.W * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    IT pix = t / CG;
+    const int w = (int)(pix % g.W);
+    pix /= g.W;
+    const int h = (int)(pix % g.H);
+    const int n = (int)(pix / g.H);
+    // output windows p with p·sh − ph ≤ h < p·sh − ph + kh
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int p_lo = hp < g.kh ? 0 : (hp - g.kh) / g.sh + 1, p_hi = min(hp / g.sh, g.P - 1);
+    const int q_lo = wp < g.kw ? 0 : (wp - g.kw) / g.sw + 1, q_hi = min(wp / g.sw, g.Q - 1);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = p_lo; p <= p_hi; ++p)
+      for (int q = q_lo; q <= q_hi; ++q) {
+        float v[8];
+        load8(gy + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, v);
+        const float inv = 1.f / fmaxf(avg_count(g, p, q, cip, divisor), 1.f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(v[e], inv, acc[e]);
+      }
+    store8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+  }
+}
+
+BIGDL_EXPORT int bigdl_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                                   int sh, int sw, int ph, int pw, int count_include_pad, int divisor, hipStream_t s) {
+  if (C % 8 || N <= 0 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0) return (int)hipErrorInvalidValue;
+  if (2 * ph > kh || 2 * pw > kw) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * P * Q * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(k_avgpool_fwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, g,
+                       count_include_pad, divisor);
+  else
+    hipLaunchKernelGGL(k_avgpool_fwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, g,
+                       count_include_pad, divisor);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_avgpool_bwd(const void* gy, void* gx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                                   int sh, int sw, int ph, int pw, int count_include_pad, int divisor, hipStream_t s) {
+  if (C % 8 || N <= 0 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0) return (int)hipErrorInvalidValue;
+  if (2 * ph > kh || 2 * pw > kw) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)gy & 15) || ((uintptr_t)gx & 15)) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * H * W * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(k_avgpool_bwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (bf16_t*)gx, g,
+                       count_include_pad, divisor);
+  else
+    hipLaunchKernelGGL(k_avgpool_bwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (bf16_t*)gx, g,
+                       count_include_pad, divisor);
   BIGDL_CHECK_LAUNCH();
 }

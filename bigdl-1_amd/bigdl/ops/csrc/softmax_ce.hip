@@ -159,3 +159,115 @@ BIGDL_EXPORT int bigdl_logsoftmax(const void* a, const void* b, void* out, long 
   }
   BIGDL_CHECK_LAUNCH();
 }
+
+// ------------------------------------------------------------------------------------------------
+// K12: row-wise softmax forward / backward over the last (memory-contiguous) dim — SoftMax.scala
+// (1-D/2-D rows; on the NHWC device layout a 4-D channel softmax is also a contiguous-row softmax)
+//   y = exp(x − max) / Σ exp(x − max);   gx = y · (gy − Σ gy·y)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) k_softmax_fwd(const T* __restrict__ x, T* __restrict__ y, int K) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  const T* xr = x + row * K;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) m = fmaxf(m, ld(xr, i));
+  m = block_reduce(m, red, true);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) s += __expf(ld(xr, i) - m);
+  s = block_reduce(s, red, false);
+  const float inv = 1.f / s;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) st(y + row * K, i, __expf(ld(xr, i) - m) * inv);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_softmax_bwd(const T* __restrict__ gy, const T* __restrict__ y,
+                                                     T* __restrict__ gx, int K) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) s += ld(gy + row * K, i) * ld(y + row * K, i);
+  s = block_reduce(s, red, false);
+  for (int i = threadIdx.x; i < K; i += blockDim.x)
+    st(gx + row * K, i, ld(y + row * K, i) * (ld(gy + row * K, i) - s));
+}
+
+BIGDL_EXPORT int bigdl_softmax(const void* a, const void* b, void* out, long long rows, int K, int backward, int dtype,
+                               hipStream_t s) {
+  if (rows <= 0 || K <= 0 || rows > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if (!backward) {
+    if (dtype == 1) hipLaunchKernelGGL(k_softmax_fwd<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)a, (bf16_t*)out, K);
+    else hipLaunchKernelGGL(k_softmax_fwd<float>, dim3(rows), dim3(256), 0, s, (const float*)a, (float*)out, K);
+  } else {
+    if (dtype == 1)
+      hipLaunchKernelGGL(k_softmax_bwd<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
+                         (bf16_t*)out, K);
+    else
+      hipLaunchKernelGGL(k_softmax_bwd<float>, dim3(rows), dim3(256), 0, s, (const float*)a, (const float*)b,
+                         (float*)out, K);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// ClassNLLCriterion on log-probabilities (ClassNLLCriterion.scala:89-230, K13 without the fused
+// log-softmax): loss = −Σ w[t]·logp[i][t] / (sizeAverage ? Σ w : 1) over rows whose 1-based target
+// is not paddingValue; gradient −w[t]/denominator at the target column, zero elsewhere.  One block
+// reduces the B rows (out[0] = loss, out[1] = denominator); the gradient kernel writes every element
+// once (no separate zero fill) and reads the denominator from device memory.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) k_nll_fwd(const T* __restrict__ lp, const int* __restrict__ tgt,
+                                                 const float* __restrict__ cw, long long B, int K, int padding,
+                                                 int size_avg, float* __restrict__ out) {
+  __shared__ float red[8];
+  float l = 0.f, wsum = 0.f;
+  for (long long i = threadIdx.x; i < B; i += blockDim.x) {
+    const int t = tgt[i];
+    if (t == padding) continue;
+    const int c = min(max(t - 1, 0), K - 1);
+    const float w = cw ? cw[c] : 1.f;
+    l -= w * ld(lp, i * K + c);
+    wsum += w;
+  }
+  l = block_reduce(l, red, false);
+  wsum = block_reduce(wsum, red, false);
+  if (threadIdx.x == 0) {
+    const float den = size_avg ? (cw ? fmaxf(wsum, 1e-12f) : fmaxf(wsum, 1.f)) : 1.f;
+    out[0] = l / den;
+    out[1] = den;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_nll_bwd(const int* __restrict__ tgt, const float* __restrict__ cw,
+                                                 const float* __restrict__ out, long long B, int K, int padding,
+                                                 T* __restrict__ gx) {
+  const float den = out[1];
+  const long long total = B * K;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long i = e / K;
+    const int k = (int)(e - i * K);
+    const int t = tgt[i];
+    float v = 0.f;
+    if (t != padding && k == min(max(t - 1, 0), K - 1)) v = -(cw ? cw[k] : 1.f) / den;
+    st(gx, e, v);
+  }
+}
+
+BIGDL_EXPORT int bigdl_class_nll(const void* lp, const int* tgt, const float* cw, void* gx, long long B, int K,
+                                 int padding, int size_avg, int dtype, float* out, hipStream_t s) {
+  if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (dtype == 1)
+    hipLaunchKernelGGL(k_nll_fwd<bf16_t>, dim3(1), dim3(256), 0, s, (const bf16_t*)lp, tgt, cw, B, K, padding, size_avg, out);
+  else
+    hipLaunchKernelGGL(k_nll_fwd<float>, dim3(1), dim3(256), 0, s, (const float*)lp, tgt, cw, B, K, padding, size_avg, out);
+  if (gx) {
+    const int grid = bigdl_grid(B * K, 256, 4096);
+    if (dtype == 1)
+      hipLaunchKernelGGL(k_nll_bwd<bf16_t>, dim3(grid), dim3(256), 0, s, tgt, cw, out, B, K, padding, (bf16_t*)gx);
+    else
+      hipLaunchKernelGGL(k_nll_bwd<float>, dim3(grid), dim3(256), 0, s, tgt, cw, out, B, K, padding, (float*)gx);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

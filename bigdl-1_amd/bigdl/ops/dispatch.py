@@ -20,6 +20,16 @@ __all__ = [
 ]
 
 
+def fallback_counts() -> dict:
+    """{(op, reason, signature): count} of device-tensor calls that ran the torch reference op
+    instead of a HIP kernel since the last :func:`reset_fallbacks`."""
+    return N.fallback_counts()
+
+
+def reset_fallbacks() -> None:
+    N.reset_fallbacks()
+
+
 def native_status() -> dict:
     return N.status()
 
@@ -46,10 +56,14 @@ def _g(opname):
             if isinstance(a, torch.Tensor):
                 t = a
                 break
-        if nat is not None and t is not None and _nat(t, opname):
-            r = nat(*args, **kwargs)
-            if r is not NotImplemented:
-                return r
+        if t is not None and t.is_cuda:
+            if nat is not None and N.has(opname):
+                r = nat(*args, **kwargs)
+                if r is not NotImplemented:
+                    return r
+                N.note_fallback(opname, "unsupported", args)
+            else:
+                N.note_fallback(opname, "no-kernel" if nat is None else "disabled", args)
         return ref(*args, **kwargs)
 
     f.__name__ = opname

@@ -11,6 +11,7 @@ cover so the dispatcher can fall back explicitly.
 from __future__ import annotations
 
 import ctypes
+import logging
 import os
 from typing import Optional
 
@@ -89,6 +90,43 @@ def register(name):
         globals()[name] = fn
         return fn
     return deco
+
+
+# ---------------------------------------------------------------------------- fallback accounting
+# Every device-tensor call of a dispatched op that does NOT reach a HIP kernel is counted here and
+# warned about once per (op, reason, signature); ``bigdl.native.strict`` turns it into an error.
+# Tests assert zero fallbacks over the flagship training steps (tests/test_no_fallback.py).
+_FALLBACKS: dict = {}
+_log = logging.getLogger("bigdl.ops")
+
+
+def _sig(args) -> str:
+    parts = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            parts.append(f"{str(a.dtype).replace('torch.', '')}{list(a.shape)}")
+            if len(parts) == 3:
+                break
+    return ",".join(parts)
+
+
+def note_fallback(opname: str, reason: str, args=()) -> None:
+    key = (opname, reason, _sig(args))
+    n = _FALLBACKS.get(key, 0)
+    _FALLBACKS[key] = n + 1
+    if n == 0:
+        msg = f"bigdl op {opname} fell back to the torch reference on a device tensor ({reason}: {key[2]})"
+        if config.get_property("bigdl.native.strict"):
+            raise RuntimeError(msg)
+        _log.warning(msg)
+
+
+def fallback_counts() -> dict:
+    return dict(_FALLBACKS)
+
+
+def reset_fallbacks() -> None:
+    _FALLBACKS.clear()
 
 
 def stream_ptr() -> int:

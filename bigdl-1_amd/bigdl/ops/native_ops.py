@@ -297,22 +297,25 @@ def _krsc(w4):
     return k if k.is_contiguous() else k.contiguous()
 
 
-_PAD_CACHE = [None]  # (source tensor, its version, c_to, padded): the last padded input
+def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
+    """Zero-pad the channel dim of a channels-last NCHW-logical tensor to ``c_to``.
 
-
-def _pad_channels(x_nhwc_4d, c_to):
-    """Zero-pad the channel dim of a channels-last NCHW-logical tensor to ``c_to``.  The last result
-    is kept (keyed by tensor identity + version counter), so the backward pass of a C % 8 conv (the
-    RGB stem) reuses the forward's padded copy instead of zero-filling and copying 8 channels again."""
-    ent = _PAD_CACHE[0]
-    if ent is not None and ent[0] is x_nhwc_4d and ent[1] == x_nhwc_4d._version and ent[2] == c_to:
-        return ent[3]
+    ``slot`` is the calling layer's one-entry holder: the forward (``reuse=False``) always pads
+    afresh and parks (source, version, padded) there; the same layer's backward (``reuse=True``)
+    takes the forward's copy when it still describes the same input.  The copy therefore lives
+    exactly as long as the layer's forward→backward pair and, under HIP-graph capture, is produced
+    by a captured kernel of the same graph (no process-global cache)."""
+    if reuse and slot is not None and slot[0] is not None:
+        src, ver, ct, padded = slot[0]
+        if src is x_nhwc_4d and ver == x_nhwc_4d._version and ct == c_to:
+            return padded
     n, c, h, w = x_nhwc_4d.shape
     out = torch.empty((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
     out[..., c:].zero_()
     out[..., :c] = x_nhwc_4d.permute(0, 2, 3, 1)
     res = out.permute(0, 3, 1, 2)
-    _PAD_CACHE[0] = (x_nhwc_4d, x_nhwc_4d._version, c_to, res)
+    if slot is not None:
+        slot[0] = (x_nhwc_4d, x_nhwc_4d._version, c_to, res)
     return res
 
 
@@ -321,21 +324,22 @@ def _conv_geom_ok(x, w4, groups, dilation):
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
 
 
-def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None):
+def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None,
+                   pad_slot=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
     writes into directly (zero-copy concat); returned as the result."""
     if not _conv_geom_ok(x, w4, groups, dilation):
         return NotImplemented
     N_, C_, H, W = x.shape
     K, Ci, R, S = w4.shape
-    if Ci != C_ or K % 4:
+    if Ci != C_:
         return NotImplemented
     if (res is not None or stats) and K % 8:
         return NotImplemented
     wk = _krsc(w4)
     if C_ % 8:
         cp = (C_ + 7) // 8 * 8
-        x = _pad_channels(x, cp)
+        x = _pad_channels(x, cp, pad_slot)
         wp = torch.zeros((K, R, S, cp), dtype=wk.dtype, device=wk.device)
         wp[..., :C_] = wk
         wk, C_ = wp, cp
@@ -369,16 +373,16 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
 
 
 @register("conv2d_forward")
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None):
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
     if res is not None and (res.dtype != _bf16 or not res.is_contiguous(memory_format=torch.channels_last)):
         res = res.to(_bf16).contiguous(memory_format=torch.channels_last)
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out)
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out, pad_slot=pad_slot)
 
 
-def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1):
+def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None):
     """Forward conv whose epilogue also emits per-row-tile Σy/Σy² partials for a following BN.
     Returns ``(y, partials, G)`` or NotImplemented."""
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True)
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot)
 
 
 def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
@@ -386,14 +390,14 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
     ``residual`` gradient (same shape as x) is summed in the epilogue."""
     N_, C_, H, W = x_shape
     K, Ci, R, S = w4.shape
-    if C_ % 4 or K % 8:
+    if K % 8:
         return None
     # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]: one cached-index gather from the KRSC storage (a
     # flip + transpose copy would be two launches per layer per step)
     ent = _S1_XFORM.get((K, Ci, R, S))
     if ent is None:
         ent = _S1_XFORM[(K, Ci, R, S)] = [(0, 0, list(range(R)), list(range(S)))]
-    wt = _subfilters(w4, ent)[0]
+    wt = _subfilters(w4, ent, ("s1", K, Ci, R, S))[0]
     P, Q = gy.shape[2], gy.shape[3]
     ph = dilation[0] * (R - 1) - pad[0]
     pw = dilation[1] * (S - 1) - pad[1]
@@ -437,7 +441,7 @@ _SUBFILTER_IDX: dict = {}
 _S1_XFORM = {}  # (K, C, R, S) → the single full-filter class list of a stride-1 dgrad
 
 
-def _subfilters(w4, classes):
+def _subfilters(w4, classes, gkey=None):
     """All parity sub-filters of a strided dgrad in ONE gather: W'_ab[c][j'][i'][k] =
     W[k][c][rs[Ra-1-j']][ss[Sb-1-i']], indexed straight from the weight's physical storage (KRSC
     in the arena) with a cached index vector — one small kernel per layer per step."""
@@ -445,12 +449,13 @@ def _subfilters(w4, classes):
     krsc = w4.permute(0, 2, 3, 1)
     phys = krsc if krsc.is_contiguous() else krsc.contiguous()
     # HIP transform kernel (weight_xform.hip): every class in one launch, no index tensor.  The
-    # ctypes argument block is built once per (shape, classes object) — this runs per layer per step,
-    # so the hot path is one dict lookup.
-    key = ("xf", K, C_, R, S, id(classes))
+    # ctypes argument block is built once per (shape, geometry) — this runs per layer per step, so
+    # the hot path is one dict lookup.  ``gkey`` is the caller's hashable geometry key (the internal
+    # callers have one); without it the key is derived from the class list's contents.
+    if gkey is None:
+        gkey = tuple((a, b, tuple(rs), tuple(ss)) for (a, b, rs, ss, *_r) in classes)
+    key = ("xf", K, C_, R, S, gkey)
     ent = _SUBFILTER_IDX.get(key)
-    if ent is not None and ent[-1] is not classes:
-        ent = None
     live = [c for c in classes if c[2] and c[3]] if ent is None else None
     if (phys.dtype == _bf16 and phys.is_cuda and C_ % 8 == 0 and K % 8 == 0 and _al16(phys)
             and (ent is not None or (0 < len(live) <= 4 and max(max(len(c[2]), len(c[3])) for c in live) <= 8))):
@@ -468,9 +473,9 @@ def _subfilters(w4, classes):
                     offs.append(off)
                 off += ni
             IA, LA = C.c_int * 32, C.c_longlong * 4
-            ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs), classes)
+            ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs))
             _SUBFILTER_IDX[key] = ent
-        n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off, _ = ent
+        n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off = ent
         out = torch.empty(total, dtype=_bf16, device=w4.device)
         check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off, _s()),
               "w_dgrad_xform")
@@ -552,7 +557,7 @@ def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
             gx.copy_(residual)
         else:
             gx.zero_()
-    subs = _subfilters(w4, classes)
+    subs = _subfilters(w4, classes, ckey)
     for ci, (a, b, rs, ss, ho, wo, ea, eb) in enumerate(classes):
         if not rs or not ss:
             continue
@@ -602,7 +607,7 @@ def _wgrad_blocks(M, C_, K):
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                    scale=1.0, residual=None, bn_fuse=None):
+                    scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
     if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
         return NotImplemented
     if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):
@@ -610,7 +615,28 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     N_, C_, H, W = x.shape
     K, Ci, R, S = w4.shape
     if K % 8:
-        return NotImplemented
+        # odd output-channel count (LeNet's 6 / 12 maps): zero-pad the gradient's channels (and
+        # the filter bank) to a multiple of 8 — padded channels contribute exactly zero
+        if residual is not None or bn_fuse is not None:
+            return NotImplemented
+        K8 = (K + 7) // 8 * 8
+        P, Q = gy.shape[2], gy.shape[3]
+        gyp = torch.zeros((N_, P, Q, K8), dtype=_bf16, device=gy.device).permute(0, 3, 1, 2)
+        gyp[:, :K] = gy
+        wk = torch.zeros((K8, R, S, Ci), dtype=w4.dtype, device=w4.device)
+        wk[:K] = w4.permute(0, 2, 3, 1)
+        tmp = None
+        if gw_acc is not None and scale != 0:
+            tmp = torch.zeros((K8, R, S, Ci), dtype=_f32, device=x.device).permute(0, 3, 1, 2)
+        gi = conv2d_backward(gyp, x, wk.permute(0, 3, 1, 2), stride, pad, dilation, groups, need_input, tmp, None,
+                             scale, pad_slot=pad_slot)
+        if gi is NotImplemented:
+            return NotImplemented
+        if tmp is not None:
+            gw_acc.add_(tmp[:K])
+        if gb_acc is not None and scale != 0:
+            gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
+        return gi
     from . import reference as R_
     gi = None
     if need_input:
@@ -624,6 +650,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             gi = _dgrad_strided(gy, w4, x.shape, tuple(stride), tuple(pad), dilation, residual)
             res_done = gi is not None
         if gi is None:  # dilated strided backward-data: library path
+            N.note_fallback("conv2d_backward.dgrad", "dilated-strided", (gy, x, w4))
             gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
         if residual is not None and not res_done:
             gi = gi + residual
@@ -631,7 +658,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         xx, cc = x, C_
         if C_ % 8:
             cc = (C_ + 7) // 8 * 8
-            xx = _pad_channels(x, cc)
+            xx = _pad_channels(x, cc, pad_slot, reuse=True)
         direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
         P, Q = gy.shape[2], gy.shape[3]
@@ -659,7 +686,7 @@ def _vec_ok(*ts, n):
 def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale=1.0, shadow=None,
              lrs=None, wds=None):
     n = w.numel()
-    if w.dtype != _f32 or g.dtype != _f32 or n % 4 or not _vec_ok(w, g, buf, lrs, wds, n=n):
+    if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, buf, lrs, wds, n=n):
         return NotImplemented
     if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.numel() == n
                                    and shadow.data_ptr() % 8 == 0):
@@ -676,7 +703,7 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
 def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0, shadow=None):
     import math
     n = w.numel()
-    if w.dtype != _f32 or n % 4 or not _vec_ok(w, g, m, v, n=n):
+    if w.dtype != _f32 or not _vec_ok(w, g, m, v, n=n):
         return NotImplemented
     if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
         return NotImplemented
@@ -837,7 +864,8 @@ def maxpool2d_forward(x, k, s, p, ceil_mode):
     if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
         return NotImplemented
     N_, C_, H, W = x.shape
-    if C_ % 8 or k[0] * k[1] > 127 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
+    if k[0] * k[1] > 127 or p[0] * 2 > k[0] or p[1] * 2 > k[1] or (C_ % 8 and not x.is_contiguous(
+            memory_format=torch.channels_last)):
         return NotImplemented
     P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
     Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
@@ -964,3 +992,356 @@ def dropout_backward(gy, mask, p):
     check(_lib().bigdl_dropout(ptr(gy), ptr(gx), _ll(gy.numel()), 0 if gy.dtype == _bf16 else 1, C.c_float(p),
                                C.c_ulonglong(mask.seed), _s()), "dropout_bwd")
     return gx
+
+
+# ---------------------------------------------------------------------------------- K4 dense GEMM
+def _mat_ok(t, cols=None):
+    """2-D bf16 device matrix with unit column stride, 16-B aligned rows (row stride % 8)."""
+    return (t is not None and t.dim() == 2 and t.dtype == _bf16 and t.is_cuda and t.stride(1) == 1
+            and t.stride(0) % 8 == 0 and t.stride(0) >= t.shape[1] and _al16(t)
+            and (cols is None or t.shape[1] == cols))
+
+
+def _bias_f32(b, n):
+    if b is None:
+        return None
+    if b.dtype != _f32 or not b.is_contiguous() or not _al16(b):
+        b = b.float().contiguous()
+    return b if b.numel() == n else None
+
+
+def gemm(a, b, bias=None, act=0, out=None, d=None, alpha=1.0, beta=0.0):
+    """C = act(alpha·A·Bᵀ + bias + D) (+ beta·C for an fp32 ``out``) on the MFMA GEMM kernel
+    (gemm.hip).  A [M][K], B [N][K] bf16 rows; ``out`` bf16 or fp32 [M][N] (row stride % 4)."""
+    if not (_mat_ok(a) and _mat_ok(b)) or a.shape[1] != b.shape[1]:
+        return NotImplemented
+    M, K = a.shape
+    N = b.shape[0]
+    if K % 8 or N % 4 or M == 0:
+        return NotImplemented
+    bb = _bias_f32(bias, N)
+    if bias is not None and bb is None:
+        return NotImplemented
+    if out is None:
+        out = torch.empty((M, N), dtype=_bf16, device=a.device)
+    if out.dim() != 2 or tuple(out.shape) != (M, N) or out.stride(1) != 1 or out.stride(0) % 4 or \
+            out.dtype not in (_bf16, _f32) or out.data_ptr() % (16 if out.dtype == _f32 else 8):
+        return NotImplemented
+    if d is not None and (d.dtype != _bf16 or d.dim() != 2 or tuple(d.shape) != (M, N) or d.stride(1) != 1
+                          or d.stride(0) % 4 or d.data_ptr() % 8):
+        return NotImplemented
+    check(_lib().bigdl_gemm(ptr(a), _ll(a.stride(0)), ptr(b), _ll(b.stride(0)), ptr(bb), ptr(d),
+                            _ll(d.stride(0) if d is not None else 0), ptr(out), _ll(out.stride(0)), C.c_int(M),
+                            C.c_int(N), C.c_int(K), C.c_int(act), C.c_int(1 if out.dtype == _f32 else 0), _f(alpha),
+                            _f(beta), _s()), "gemm")
+    return out
+
+
+def transpose_bf16(src):
+    """[R][C] bf16 (unit column stride) → contiguous [C][R]."""
+    R_, C_ = src.shape
+    dst = torch.empty((C_, R_), dtype=_bf16, device=src.device)
+    check(_lib().bigdl_transpose_bf16(ptr(src), _ll(src.stride(0)), ptr(dst), _ll(R_), C.c_int(R_), C.c_int(C_),
+                                      _s()), "transpose")
+    return dst
+
+
+def colsum_acc(x, out, scale=1.0):
+    """out[n] += scale · Σ_m x[m][n]  (bias gradient, bf16 rows → fp32)."""
+    M, N_ = x.shape
+    if not (_mat_ok(x) and N_ % 8 == 0 and out.dtype == _f32 and out.is_contiguous() and out.numel() == N_):
+        return NotImplemented
+    check(_lib().bigdl_colsum_bf16(ptr(x), _ll(x.stride(0)), ptr(out), C.c_int(M), C.c_int(N_), _f(scale), _s()),
+          "colsum")
+    return out
+
+
+def wgrad_rows(gy, x, gw_acc, scale):
+    """gw_acc[N][K] += scale · gyᵀ·x for row-major gy [M][N], x [M][K] (the 1×1 case of the conv
+    wgrad kernel: transposed LDS reads, split-K over rows with fp32 atomics)."""
+    M, N_ = gy.shape
+    K = x.shape[1]
+    if not (gy.is_contiguous() and x.is_contiguous() and gy.dtype == _bf16 and x.dtype == _bf16 and _al16(gy)
+            and _al16(x) and N_ % 8 == 0 and K % 8 == 0 and gw_acc.dtype == _f32 and gw_acc.is_contiguous()
+            and gw_acc.numel() == N_ * K):
+        return NotImplemented
+    check(_lib().bigdl_conv_wgrad(ptr(x), ptr(gy), ptr(gw_acc), _f(scale), M, 1, 1, K, N_, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1,
+                                  -_wgrad_blocks(M, K, N_), _s()), "linear_wgrad")
+    return gw_acc
+
+
+def _r8(n):
+    return (n + 7) // 8 * 8
+
+
+def _padded(t, rows, cols):
+    """``t`` as a dense bf16 [rows][cols] matrix, zero-padded (a copy only when needed)."""
+    if tuple(t.shape) == (rows, cols) and _mat_ok(t):
+        return t
+    out = torch.zeros((rows, cols), dtype=_bf16, device=t.device)
+    out[:t.shape[0], :t.shape[1]] = t
+    return out
+
+
+@register("linear_forward")
+def linear_forward(x, w, b, act=0):
+    if x.dim() != 2 or w.dim() != 2 or x.dtype != _bf16 or w.dtype != _bf16 or x.shape[1] != w.shape[1]:
+        return NotImplemented
+    M, K = x.shape
+    N_ = w.shape[0]
+    if M == 0:
+        return NotImplemented
+    # odd sizes (LeNet's 100 → 10 classifier): zero-pad K to a multiple of 8 and N to 4, slice after
+    K8, N4 = _r8(K), (N_ + 3) // 4 * 4
+    xp, wp = _padded(x, M, K8), _padded(w, N4, K8)
+    bp = b
+    if b is not None and N4 != N_:
+        bp = torch.zeros(N4, dtype=_f32, device=x.device)
+        bp[:N_] = b
+    y = gemm(xp, wp, bp, act=act)
+    if y is NotImplemented or N4 == N_:
+        return y
+    return y[:, :N_].contiguous()
+
+
+@register("linear_backward")
+def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1.0):
+    if gy.dim() != 2 or x.dim() != 2 or w.dim() != 2 or not (gy.dtype == x.dtype == w.dtype == _bf16):
+        return NotImplemented
+    M, N_ = gy.shape
+    K = x.shape[1]
+    if x.shape[0] != M or tuple(w.shape) != (N_, K) or M == 0:
+        return NotImplemented
+    do_w = gw_acc is not None and scale != 0
+    do_b = gb_acc is not None and scale != 0
+    if do_w and not (gw_acc.dtype == _f32 and gw_acc.is_contiguous() and gw_acc.numel() == N_ * K):
+        return NotImplemented
+    if do_b and not (gb_acc.dtype == _f32 and gb_acc.is_contiguous() and gb_acc.numel() == N_):
+        return NotImplemented
+    N8, K8 = _r8(N_), _r8(K)
+    gyp = _padded(gy, M, N8)
+    gi = None
+    if need_input:
+        # gx = gy·W = gy · (Wᵀ)ᵀ: transposed weight copy [K][N] (zero-padded to [K8][N8] if odd)
+        wt = transpose_bf16(w) if (N8 == N_ and _mat_ok(w)) else None
+        wt = _padded(wt if wt is not None else w.t(), K8, N8)
+        gi = gemm(gyp, wt)
+        if gi is NotImplemented:
+            return NotImplemented
+        if K8 != K:
+            gi = gi[:, :K].contiguous()
+    if do_w:
+        # the wgrad kernel reads dense rows: strided views (e.g. a gate slice) are packed first
+        if N8 == N_ and K8 == K:
+            r = wgrad_rows(gyp.contiguous(), x.contiguous(), gw_acc, scale)
+        else:
+            tmp = torch.zeros(N8 * K8, dtype=_f32, device=x.device)
+            r = wgrad_rows(gyp.contiguous(), _padded(x, M, K8).contiguous(), tmp, scale)
+            gw_acc.view(N_, K).add_(tmp.view(N8, K8)[:N_, :K])
+        if r is NotImplemented:
+            return NotImplemented
+    if do_b:
+        if N8 == N_:
+            colsum_acc(gyp, gb_acc, scale)
+        else:
+            tmp = torch.zeros(N8, dtype=_f32, device=x.device)
+            colsum_acc(gyp, tmp, scale)
+            gb_acc.add_(tmp[:N_])
+    return gi
+
+
+# ---------------------------------------------------------------------------------- K12 softmax
+def _rowwise(x):
+    return x.is_cuda and x.dtype in (_bf16, _f32) and x.dim() >= 1 and x.numel() > 0 and x.is_contiguous()
+
+
+@register("softmax_forward")
+def softmax_forward(x):
+    if not _rowwise(x):
+        return NotImplemented
+    K = x.shape[-1]
+    y = torch.empty_like(x)
+    check(_lib().bigdl_softmax(ptr(x), ptr(None), ptr(y), _ll(x.numel() // K), C.c_int(K), C.c_int(0),
+                               C.c_int(1 if x.dtype == _bf16 else 0), _s()), "softmax")
+    return y
+
+
+@register("softmax_backward")
+def softmax_backward(gy, y):
+    if not (_rowwise(y) and gy.shape == y.shape):
+        return NotImplemented
+    if gy.dtype != y.dtype or not gy.is_contiguous():
+        gy = gy.to(y.dtype).contiguous()
+    K = y.shape[-1]
+    gx = torch.empty_like(y)
+    check(_lib().bigdl_softmax(ptr(gy), ptr(y), ptr(gx), _ll(y.numel() // K), C.c_int(K), C.c_int(1),
+                               C.c_int(1 if y.dtype == _bf16 else 0), _s()), "softmax_bwd")
+    return gx
+
+
+def softmax_channels_nhwc(x, backward_gy=None):
+    """Channel-dim softmax (SoftMax on a 4-D batch) on the NHWC device layout: channels are the
+    contiguous dim, so it is the row-wise kernel over N·H·W rows."""
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.dtype not in (_bf16, _f32):
+        return NotImplemented
+    n, c, h, w = x.shape
+    rows = x.permute(0, 2, 3, 1).reshape(-1, c)
+    if backward_gy is None:
+        r = softmax_forward(rows)
+    else:
+        g = backward_gy.to(x.dtype).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
+        r = softmax_backward(g, rows)
+    if r is NotImplemented:
+        return r
+    return r.reshape(n, h, w, c).permute(0, 3, 1, 2)
+
+
+# ---------------------------------------------------------------------------------- K11 avg-pool
+@register("avgpool2d_forward")
+def avgpool2d_forward(x, k, s, p, ceil_mode, count_include_pad, divisor=None):
+    if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if C_ % 8 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
+        return NotImplemented
+    P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
+    Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
+    if P <= 0 or Q <= 0:
+        return NotImplemented
+    y = torch.empty((N_, C_, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_avgpool_fwd(ptr(x), ptr(y), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+                                   int(bool(count_include_pad)), int(divisor or 0), _s()), "avgpool_fwd")
+    return y
+
+
+@register("avgpool2d_backward")
+def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=None):
+    if x.dim() != 4 or x.dtype != _bf16 or gy.dim() != 4:
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if C_ % 8 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
+        return NotImplemented
+    P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
+    Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
+    if tuple(gy.shape) != (N_, C_, P, Q):
+        return NotImplemented
+    gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    if not _al16(gy):
+        gy = gy.clone(memory_format=torch.channels_last)
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_avgpool_bwd(ptr(gy), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+                                   int(bool(count_include_pad)), int(divisor or 0), _s()), "avgpool_bwd")
+    return gx
+
+
+# ---------------------------------------------------------------------------------- K16 embedding
+_ITYPE = {_f32: 0, torch.int64: 1, torch.int32: 2}
+
+
+@register("embedding_forward")
+def embedding_forward(weight, idx_1b, padding_value=0):
+    if weight.dim() != 2 or weight.dtype not in (_bf16, _f32) or not weight.is_contiguous() or not _al16(weight):
+        return NotImplemented
+    if not idx_1b.is_cuda or idx_1b.dtype not in _ITYPE or idx_1b.numel() == 0:
+        return NotImplemented
+    idx = idx_1b if idx_1b.is_contiguous() else idx_1b.contiguous()
+    n = idx.numel()
+    D = weight.shape[1]
+    out = torch.empty((*idx_1b.shape, D), dtype=weight.dtype, device=weight.device)
+    check(_lib().bigdl_embedding_fwd(ptr(weight), ptr(idx), C.c_int(_ITYPE[idx.dtype]), ptr(out), _ll(n),
+                                     _ll(weight.shape[0]), C.c_int(D), C.c_int(0 if weight.dtype == _bf16 else 1),
+                                     _s()), "embedding_fwd")
+    return out
+
+
+@register("embedding_backward")
+def embedding_backward(grad_weight, idx_1b, gy, scale=1.0, padding_value=0):
+    if grad_weight.dtype != _f32 or not grad_weight.is_contiguous() or grad_weight.dim() != 2:
+        return NotImplemented
+    if not idx_1b.is_cuda or idx_1b.dtype not in _ITYPE:
+        return NotImplemented
+    D = grad_weight.shape[1]
+    n = idx_1b.numel()
+    if gy.numel() != n * D or gy.dtype not in (_bf16, _f32):
+        return NotImplemented
+    if scale == 0 or n == 0:
+        return grad_weight
+    idx = idx_1b.contiguous()
+    g = gy.contiguous()
+    check(_lib().bigdl_embedding_bwd(ptr(grad_weight), ptr(idx), C.c_int(_ITYPE[idx.dtype]), ptr(g), _ll(n),
+                                     _ll(grad_weight.shape[0]), C.c_int(D), C.c_int(0 if g.dtype == _bf16 else 1),
+                                     _f(scale), C.c_int(1 if padding_value != 0 else 0), _f(padding_value), _s()),
+          "embedding_bwd")
+    return grad_weight
+
+
+# ---------------------------------------------------------------------------------- K14/K15 fused recurrent step
+_RNN_CELLS = {"lstm_fwd": 0, "lstm_bwd": 1, "gru_fwd1": 2, "gru_fwd2": 3, "gru_bwd1": 4, "gru_bwd2": 5}
+
+
+def _ld(t):
+    return 0 if t is None else t.stride(0)
+
+
+def rnn_step(cell, a, u, M, K, Hs, xg=None, hprev=None, c_prev=None, h_out=None, c_out=None, act=None, tc=None,
+             gy=None, gc_next=None, dg=None, dc_prev=None, s0=None, s1=None, s2=None, rh=None):
+    """One fused recurrent step (rnn_step.hip).  Row operands are 2-D views (unit column stride);
+    fp32 state tensors are contiguous [M][Hs] (act [M][4Hs]).  The launcher re-validates every
+    alignment / stride the kernel assumes and returns an error instead of launching."""
+    x_f32 = 1 if (xg is not None and xg.dtype == _f32) else 0
+    check(_lib().bigdl_rnn_step(C.c_int(_RNN_CELLS[cell]), ptr(a), _ll(_ld(a)), ptr(u), C.c_int(M), C.c_int(K),
+                                C.c_int(Hs), ptr(xg), _ll(_ld(xg)), C.c_int(x_f32), ptr(hprev), _ll(_ld(hprev)),
+                                ptr(c_prev), ptr(h_out), _ll(_ld(h_out)), ptr(c_out), ptr(act), ptr(tc), ptr(gy),
+                                _ll(_ld(gy)), ptr(gc_next), ptr(dg), _ll(_ld(dg)), ptr(dc_prev), ptr(s0), ptr(s1),
+                                ptr(s2), ptr(rh), _ll(_ld(rh)), _s()), f"rnn_step[{cell}]")
+
+
+def rnn_fast_ok(H, *ts):
+    """The fused step covers bf16 rows with H % 8 == 0 on a device with the library loaded."""
+    if H % 8 or not N.has("lstm_cell_forward"):
+        return False
+    return all(t is None or (t.is_cuda and t.dtype == _bf16) for t in ts)
+
+
+# ---------------------------------------------------------------------------------- K13 ClassNLL
+def _nll_args(logp, target_1b, weights):
+    lp = logp.unsqueeze(0) if logp.dim() == 1 else logp
+    if lp.dim() != 2 or lp.dtype not in (_bf16, _f32) or not lp.is_contiguous():
+        return None
+    B, K = lp.shape
+    t = _targets_i32(target_1b.to(lp.device), B)
+    if t is None:
+        return None
+    w = None
+    if weights is not None:
+        w = weights.to(lp.device, _f32).contiguous()
+        if w.numel() != K:
+            return None
+    return lp, t, w, B, K
+
+
+@register("class_nll_forward")
+def class_nll_forward(logp, target_1b, weights=None, size_average=True, padding_value=-1):
+    a = _nll_args(logp, target_1b, weights)
+    if a is None:
+        return NotImplemented
+    lp, t, w, B, K = a
+    out = torch.empty(2, dtype=_f32, device=lp.device)
+    check(_lib().bigdl_class_nll(ptr(lp), ptr(t), ptr(w), ptr(None), _ll(B), C.c_int(K), C.c_int(int(padding_value)),
+                                 C.c_int(1 if size_average else 0), C.c_int(1 if lp.dtype == _bf16 else 0), ptr(out),
+                                 _s()), "class_nll")
+    return out[0]
+
+
+@register("class_nll_backward")
+def class_nll_backward(logp, target_1b, weights=None, size_average=True, padding_value=-1):
+    a = _nll_args(logp, target_1b, weights)
+    if a is None:
+        return NotImplemented
+    lp, t, w, B, K = a
+    out = torch.empty(2, dtype=_f32, device=lp.device)
+    gx = torch.empty_like(lp)
+    check(_lib().bigdl_class_nll(ptr(lp), ptr(t), ptr(w), ptr(gx), _ll(B), C.c_int(K), C.c_int(int(padding_value)),
+                                 C.c_int(1 if size_average else 0), C.c_int(1 if lp.dtype == _bf16 else 0), ptr(out),
+                                 _s()), "class_nll_bwd")
+    return gx.squeeze(0) if logp.dim() == 1 else gx

@@ -37,7 +37,7 @@ def relu_backward(gy: torch.Tensor, y_or_x: torch.Tensor, threshold: float = 0.0
 
 
 # ------------------------------------------------------------------------- convolution
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None):
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
     """``SpatialConvolution.updateOutput`` (``DL/nn/SpatialConvolution.scala:253-362``).
 
     ``w4`` is (O, I/g, kH, kW); ``pad`` is (padH, padW) after SAME resolution.  ``relu`` applies a
@@ -55,7 +55,7 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
 
 
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
-                    gb_acc=None, scale=1.0, residual=None, bn_fuse=None):
+                    gb_acc=None, scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
     """``SpatialConvolution.updateGradInput`` + ``accGradParameters`` (``:364-505``).
 
     Returns gradInput (or None); ACCUMULATES ``scale·dW`` into ``gw_acc`` (O, I/g, kH, kW view,

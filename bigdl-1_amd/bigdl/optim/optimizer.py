@@ -241,6 +241,8 @@ class BaseOptimizer:
         m.to(self.device)
         m.training()
         fuse(m)
+        from ..nn.fusion import mark_input_no_grad
+        mark_input_no_grad(m)
         flat_w, flat_g = m.getParameters()
         self.flat = m.flat_parameters()
         if self.flat is not None and self.device.type == "cuda" and self.compute_dtype != torch.float32:

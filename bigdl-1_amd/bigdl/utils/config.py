@@ -48,6 +48,7 @@ _REGISTRY = {
     "bigdl.metrics.deviceTimers": (bool, False, "time the distributed phases with HIP events (adds no host sync)"),
     "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
+    "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),
     "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
     "bigdl.optim.foldRegularizers": (bool, True, "apply pure-L2 layer regularizers inside the fused SGD update"),

@@ -1,0 +1,103 @@
+"""No silent fallbacks: one training step (or inference batch) of each BASELINE.json config's model on
+the GPU must run every dispatched op on a HIP kernel — ``ops.fallback_counts()`` stays empty.
+
+LeNet-5 (MNIST shape), VggForCifar10, ResNet-50 (ImageNet topology, small batch), the PTB 2-layer
+LSTM LM and Inception-v1 inference; small batches so the test stays a few seconds."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _setup():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    from bigdl import ops
+    assert ops.native_status()["loaded"]
+    ops.reset_fallbacks()
+    yield
+    config.set_property("bigdl.compute.dtype", "auto")
+
+
+def _train_steps(model, x, y, crit, method, n=2):
+    from bigdl.dataset import MiniBatch
+    from bigdl.optim.optimizer import LocalOptimizer
+    opt = LocalOptimizer(model, [MiniBatch(x, y)], crit, method, batch_size=x.shape[0])
+    opt.prepare()
+    losses = [float(opt.train_step(MiniBatch(x, y))) for _ in range(n)]
+    torch.cuda.synchronize()
+    assert all(l == l for l in losses), losses
+    return losses
+
+
+def _assert_clean():
+    from bigdl import ops
+    fb = ops.fallback_counts()
+    assert fb == {}, "device ops fell back to torch: " + "; ".join(f"{k}: {v}" for k, v in fb.items())
+
+
+def _img(b, c, h, w):
+    from bigdl.utils.engine import Engine
+    return torch.randn(b, c, h, w, device=dev).to(Engine.compute_dtype()).contiguous(memory_format=torch.channels_last)
+
+
+def test_lenet_step_native():
+    from bigdl.models.lenet import LeNet5
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    x = _img(16, 1, 28, 28)
+    y = (torch.randint(0, 10, (16,)) + 1).float().to(dev)
+    _train_steps(LeNet5(10), x, y, ClassNLLCriterion(), SGD(learningrate=0.05))
+    _assert_clean()
+
+
+def test_vgg_cifar_step_native():
+    from bigdl.models.vgg import VggForCifar10
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    x = _img(16, 3, 32, 32)
+    y = (torch.randint(0, 10, (16,)) + 1).float().to(dev)
+    _train_steps(VggForCifar10(10), x, y, ClassNLLCriterion(), SGD(learningrate=0.01, momentum=0.9, dampening=0.0))
+    _assert_clean()
+
+
+def test_resnet50_step_native():
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.optim import SGD
+    x = _img(4, 3, 224, 224)
+    y = (torch.randint(0, 1000, (4,)) + 1).float().to(dev)
+    model = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+    _train_steps(model, x, y, CrossEntropyCriterion(),
+                 SGD(learningrate=0.1, momentum=0.9, dampening=0.0, nesterov=True, weightdecay=1e-4))
+    _assert_clean()
+
+
+def test_ptb_lstm_step_native():
+    from bigdl.models.rnn import PTBModel
+    from bigdl.nn import CrossEntropyCriterion, TimeDistributedCriterion
+    from bigdl.optim import Adagrad
+    V, B, T = 10000, 20, 20
+    x = (torch.randint(0, V, (B, T)) + 1).float().to(dev)
+    y = (torch.randint(0, V, (B, T)) + 1).float().to(dev)
+    crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=False)
+    _train_steps(PTBModel.lstm(V, 200, V, 2), x, y, crit, Adagrad(learningrate=0.01, learningrate_decay=0.001))
+    _assert_clean()
+
+
+def test_inception_v1_inference_native():
+    from bigdl.models.inception import Inception_v1_NoAuxClassifier
+    from bigdl.nn.fusion import fuse
+    model = Inception_v1_NoAuxClassifier.graph(1000, has_dropout=True)
+    model.cuda()
+    model.evaluate()
+    fuse(model)
+    with torch.no_grad():
+        out = model.forward(_img(4, 3, 224, 224))
+    torch.cuda.synchronize()
+    assert out.shape == (4, 1000)
+    _assert_clean()
