@@ -816,20 +816,17 @@ class Recurrent(Container):
             tcs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
             cs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
         if _fused_rnn_ok(H, x2, U):
-            # one launch per step: h·Uᵀ on MFMA + the cell update in the GEMM epilogue (rnn_step.hip)
+            # one launch per step (h·Uᵀ on MFMA + the cell update in the GEMM epilogue, rnn_step.hip),
+            # the time loop itself in C++: one host call for the whole sequence
             from ...ops import native_ops as NO
+            x2 = x2.contiguous()
             h0 = h0.contiguous()
             c0 = c0.contiguous()
-            if not train:
-                cbuf = [torch.empty(B, H, device=x2.device, dtype=torch.float32) for _ in range(2)]
-            c = c0
-            for t in range(Tn):
-                a = h0 if t == 0 else out[:, t - 1]
-                c_out = cs[t] if train else cbuf[t % 2]
-                NO.rnn_step("lstm_fwd", a, U, B, H, H, xg=x2[:, t], c_prev=c, h_out=out[:, t], c_out=c_out,
-                            act=acts[t] if train else None, tc=tcs[t] if train else None)
-                c = c_out
+            cbuf = None if train else torch.empty(2, B, H, device=x2.device, dtype=torch.float32)
+            NO.lstm_seq_forward(x2, h0, c0, U, out, cs if train else None, acts if train else None,
+                                tcs if train else None, cbuf)
             h = out[:, Tn - 1]
+            c = cs[Tn - 1] if train else cbuf[(Tn - 1) % 2]
         else:
             h, c = h0, c0
             for t in range(Tn):
@@ -862,12 +859,7 @@ class Recurrent(Container):
         Z = torch.empty(nS, B, H, device=dev, dtype=torch.float32)
         Nn = torch.empty(nS, B, H, device=dev, dtype=torch.float32) if train else None
         RH = torch.empty(B, Tn if train else 1, H, device=dev, dtype=x2.dtype)
-        for t in range(Tn):
-            hp = h0 if t == 0 else out[:, t - 1]
-            k = t if train else 0
-            NO.rnn_step("gru_fwd1", hp, Urz, B, H, H, xg=x2[:, t], hprev=hp, rh=RH[:, k], s0=R[k], s1=Z[k])
-            NO.rnn_step("gru_fwd2", RH[:, k], Uh, B, H, H, xg=x2[:, t], hprev=hp, s1=Z[k], h_out=out[:, t],
-                        s2=Nn[k] if train else None)
+        NO.gru_seq_forward(x2.contiguous(), h0, Urz, Uh, out, R, Z, Nn, RH, train)
         self._last_hidden = out[:, Tn - 1]
         self._rec = ("gru", h0, out, R, Z, Nn, RH) if train else None
         return out
@@ -943,10 +935,7 @@ class Recurrent(Container):
             from ...ops import native_ops as NO
             Ut = NO.transpose_bf16(U)  # (H, 4H)
             gc = torch.empty(B, H, device=out.device, dtype=torch.float32)
-            for t in range(Tn - 1, -1, -1):
-                NO.rnn_step("lstm_bwd", DG[:, t + 1] if t + 1 < Tn else None, Ut, B, 4 * H, H, gy=gy[:, t],
-                            act=acts[t], tc=tcs[t], c_prev=cs[t - 1] if t > 0 else c0,
-                            gc_next=gc if t + 1 < Tn else None, dg=DG[:, t], dc_prev=gc)
+            NO.lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc)
             gh_rec = NO.gemm(DG[:, 0], Ut)
         else:
             gh_rec, gc = None, None
@@ -981,11 +970,7 @@ class Recurrent(Container):
         Urz_t, Uh_t = NO.transpose_bf16(Urz), NO.transpose_bf16(Uh)  # (H, 2H), (H, H)
         DG = torch.empty(B, Tn, 3 * H, device=dev, dtype=out.dtype)  # (da_r, da_z, da_n) per step
         carry = torch.zeros(B, H, device=dev, dtype=torch.float32)
-        for t in range(Tn - 1, -1, -1):
-            hp = h0 if t == 0 else out[:, t - 1]
-            NO.rnn_step("gru_bwd1", DG[:, t + 1, :2 * H] if t + 1 < Tn else None, Urz_t, B, 2 * H, H, gy=gy[:, t],
-                        s0=carry, s1=Z[t], s2=Nn[t], hprev=hp, dg=DG[:, t])
-            NO.rnn_step("gru_bwd2", DG[:, t, 2 * H:], Uh_t, B, H, H, s0=carry, s1=R[t], hprev=hp, dg=DG[:, t])
+        NO.gru_seq_backward(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry)
         NO.gemm(DG[:, 0, :2 * H], Urz_t, out=carry, beta=1.0)  # dh0 = carry + da_rz_0 · U_rz
         self._grad_hidden_state = [carry]
         hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)

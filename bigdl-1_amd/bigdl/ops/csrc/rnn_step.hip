@@ -79,42 +79,196 @@ __device__ __forceinline__ void stb4(bf16_t* p, const float* v) {
                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
 }
 
+// number of fp32 quads of per-(row, unit) epilogue operands each cell reads
+template <int CELL> struct NPre;
+template <> struct NPre<0> { static constexpr int v = 5; };  // xg i,g,f,o, c_prev
+template <> struct NPre<1> { static constexpr int v = 8; };  // gy, act i,g,f,o, tanh(c), c_prev, dc_next
+template <> struct NPre<2> { static constexpr int v = 3; };  // x_r, x_z, h_prev
+template <> struct NPre<3> { static constexpr int v = 3; };  // x_h, h_prev, z
+template <> struct NPre<4> { static constexpr int v = 5; };  // gy, carry, z, n, h_prev
+template <> struct NPre<5> { static constexpr int v = 3; };  // carry, r, h_prev
+
+// The epilogue's operands are fetched by wave 0 BEFORE the reduction loop so their memory latency
+// overlaps the MFMA chain instead of following it (the step kernels are latency-bound).
+template <int CELL>
+__device__ __forceinline__ void pre_load(const RnnStep& p, int m, int j, float (&v)[NPre<CELL>::v][4]) {
+  const int H = p.Hs;
+  const long long mh = (long long)m * H + j;
+  if constexpr (CELL == 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ld4(p.xg, p.x_f32, (long long)m * p.ldx + g * H + j, v[g]);
+    ldf4(p.c_prev ? p.c_prev + mh : nullptr, v[4]);
+  } else if constexpr (CELL == 1) {
+    ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    const float* a = p.act + (long long)m * 4 * H + j;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ldf4(a + g * H, v[1 + g]);
+    ldf4(p.tc + mh, v[5]);
+    ldf4(p.c_prev ? p.c_prev + mh : nullptr, v[6]);
+    ldf4(p.gc_next ? p.gc_next + mh : nullptr, v[7]);
+  } else if constexpr (CELL == 2) {
+    ld4(p.xg, p.x_f32, (long long)m * p.ldx + j, v[0]);
+    ld4(p.xg, p.x_f32, (long long)m * p.ldx + H + j, v[1]);
+    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[2]);
+  } else if constexpr (CELL == 3) {
+    ld4(p.xg, p.x_f32, (long long)m * p.ldx + 2 * H + j, v[0]);
+    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[1]);
+    ldf4(p.s1 + mh, v[2]);
+  } else if constexpr (CELL == 4) {
+    ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    ldf4(p.s0 + mh, v[1]);
+    ldf4(p.s1 + mh, v[2]);
+    ldf4(p.s2 + mh, v[3]);
+    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[4]);
+  } else {
+    ldf4(p.s0 + mh, v[0]);
+    ldf4(p.s1 + mh, v[1]);
+    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[2]);
+  }
+}
+
+template <int CELL, int G>
+__device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const float (&v)[NPre<CELL>::v][4],
+                                         const v4f (&acc)[G]) {
+  const int H = p.Hs;
+  const long long mh = (long long)m * H + j;
+  if constexpr (CELL == 0) {
+    float gi[4], gg[4], gf[4], go[4], h[4], c[4], tcv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gi[e] = sgm(v[0][e] + acc[0][e]);
+      gg[e] = tanhf(v[1][e] + acc[1][e]);
+      gf[e] = sgm(v[2][e] + acc[2][e]);
+      go[e] = sgm(v[3][e] + acc[3][e]);
+      c[e] = gi[e] * gg[e] + gf[e] * v[4][e];
+      tcv[e] = tanhf(c[e]);
+      h[e] = go[e] * tcv[e];
+    }
+    stb4(p.h_out + (long long)m * p.ldho + j, h);
+    if (p.c_out) stf4(p.c_out + mh, c);
+    if (p.act) {
+      float* a = p.act + (long long)m * 4 * H + j;
+      stf4(a, gi);
+      stf4(a + H, gg);
+      stf4(a + 2 * H, gf);
+      stf4(a + 3 * H, go);
+    }
+    if (p.tc) stf4(p.tc + mh, tcv);
+  } else if constexpr (CELL == 1) {
+    float di[4], dgg[4], df[4], dout[4], dcp[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float i = v[1][e], g = v[2][e], f = v[3][e], o = v[4][e], tcv = v[5][e];
+      const float d_h = v[0][e] + acc[0][e];
+      const float dc = d_h * o * (1.f - tcv * tcv) + v[7][e];
+      di[e] = dc * g * i * (1.f - i);
+      dgg[e] = dc * i * (1.f - g * g);
+      df[e] = dc * v[6][e] * f * (1.f - f);
+      dout[e] = d_h * tcv * o * (1.f - o);
+      dcp[e] = dc * f;
+    }
+    bf16_t* o = p.dg + (long long)m * p.lddg + j;
+    stb4(o, di);
+    stb4(o + H, dgg);
+    stb4(o + 2 * H, df);
+    stb4(o + 3 * H, dout);
+    stf4(p.dc_prev + mh, dcp);
+  } else if constexpr (CELL == 2) {
+    float r[4], z[4], rh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r[e] = sgm(v[0][e] + acc[0][e]);
+      z[e] = sgm(v[1][e] + acc[1][e]);
+      rh[e] = r[e] * v[2][e];
+    }
+    stb4(p.rh + (long long)m * p.ldrh + j, rh);
+    stf4(p.s0 + mh, r);
+    stf4(p.s1 + mh, z);
+  } else if constexpr (CELL == 3) {
+    float n[4], h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      n[e] = tanhf(v[0][e] + acc[0][e]);
+      h[e] = (1.f - v[2][e]) * n[e] + v[2][e] * v[1][e];
+    }
+    stb4(p.h_out + (long long)m * p.ldho + j, h);
+    if (p.s2) stf4(p.s2 + mh, n);
+  } else if constexpr (CELL == 4) {
+    float daz[4], dan[4], nc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = v[2][e], n = v[3][e];
+      const float dh = v[0][e] + v[1][e] + acc[0][e];
+      dan[e] = dh * (1.f - z) * (1.f - n * n);
+      daz[e] = dh * (v[4][e] - n) * z * (1.f - z);
+      nc[e] = dh * z;
+    }
+    bf16_t* o = p.dg + (long long)m * p.lddg + j;
+    stb4(o + H, daz);
+    stb4(o + 2 * H, dan);
+    stf4(p.s0 + mh, nc);
+  } else {
+    float dar[4], carry[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float drh = acc[0][e], r = v[1][e];
+      dar[e] = drh * v[2][e] * r * (1.f - r);
+      carry[e] = v[0][e] + drh * r;
+    }
+    stb4(p.dg + (long long)m * p.lddg + j, dar);
+    stf4(p.s0 + mh, carry);
+  }
+}
+
 template <int CELL, int G>
 __global__ void __launch_bounds__(256) k_rnn_step(RnnStep p) {
   __shared__ v4f red[3][G * 2][64];
+  constexpr int NP = NPre<CELL>::v;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int j0 = blockIdx.x * 16, m0 = blockIdx.y * 32;
+  const int j = j0 + fq * 4;
+  const bool jin = j < p.Hs;  // Hs % 4 == 0: a unit quad is all in or all out
+  const bool min0 = m0 + fr < p.M, min1 = m0 + 16 + fr < p.M;
 
-  v4f acc[G][2];
+  float pre0[NP][4], pre1[NP][4];
+  if (wid == 0 && jin) {
+    if (min0) pre_load<CELL>(p, m0 + fr, j, pre0);
+    if (min1) pre_load<CELL>(p, m0 + 16 + fr, j, pre1);
+  }
+
+  v4f acc0[G], acc1[G];
 #pragma unroll
-  for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < G; ++g) acc0[g] = acc1[g] = v4f{0.f, 0.f, 0.f, 0.f};
 
   if (p.a) {
-    const bool ar0 = m0 + fr < p.M, ar1 = m0 + 16 + fr < p.M, bu = j0 + fr < p.Hs;
-    const bf16_t* pa0 = p.a + (long long)(ar0 ? m0 + fr : 0) * p.lda;
-    const bf16_t* pa1 = p.a + (long long)(ar1 ? m0 + 16 + fr : 0) * p.lda;
+    const bool bu = j0 + fr < p.Hs;
+    const bf16_t* pa0 = p.a + (long long)(min0 ? m0 + fr : 0) * p.lda;
+    const bf16_t* pa1 = p.a + (long long)(min1 ? m0 + 16 + fr : 0) * p.lda;
     const bf16_t* pu = p.u + (long long)(bu ? j0 + fr : 0) * p.K;
     const long long gstride = (long long)p.Hs * p.K;
     const int KS = (p.K + 31) / 32;
     const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 2
     for (int ks = wid; ks < KS; ks += 4) {
       const int k = ks * 32 + fq * 8;
       const bool kin = k < p.K;
-      const v8s x0 = (kin && ar0) ? *reinterpret_cast<const v8s*>(pa0 + k) : zero;
-      const v8s x1 = (kin && ar1) ? *reinterpret_cast<const v8s*>(pa1 + k) : zero;
+      const v8s x0 = (kin && min0) ? *reinterpret_cast<const v8s*>(pa0 + k) : zero;
+      const v8s x1 = (kin && min1) ? *reinterpret_cast<const v8s*>(pa1 + k) : zero;
+      v8s w[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) w[g] = (kin && bu) ? *reinterpret_cast<const v8s*>(pu + g * gstride + k) : zero;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const v8s w = (kin && bu) ? *reinterpret_cast<const v8s*>(pu + g * gstride + k) : zero;
-        acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x0, acc[g][0], 0, 0, 0);
-        acc[g][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x1, acc[g][1], 0, 0, 0);
+        acc0[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[g], x0, acc0[g], 0, 0, 0);
+        acc1[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[g], x1, acc1[g], 0, 0, 0);
       }
     }
     if (wid > 0) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        red[wid - 1][g * 2][lane] = acc[g][0];
-        red[wid - 1][g * 2 + 1][lane] = acc[g][1];
+        red[wid - 1][g * 2][lane] = acc0[g];
+        red[wid - 1][g * 2 + 1][lane] = acc1[g];
       }
     }
     __syncthreads();
@@ -123,136 +277,15 @@ __global__ void __launch_bounds__(256) k_rnn_step(RnnStep p) {
     for (int w = 0; w < 3; ++w)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        acc[g][0] += red[w][g * 2][lane];
-        acc[g][1] += red[w][g * 2 + 1][lane];
+        acc0[g] += red[w][g * 2][lane];
+        acc1[g] += red[w][g * 2 + 1][lane];
       }
   } else if (wid > 0) {
     return;
   }
-
-  const int H = p.Hs;
-  const int j = j0 + fq * 4;
-  if (j >= H) return;  // H % 4 == 0: a unit quad is all in or all out
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int m = m0 + t * 16 + fr;
-    if (m >= p.M) continue;
-    const long long mh = (long long)m * H + j;
-    if constexpr (CELL == 0) {
-      float gi[4], gg[4], gf[4], go[4], cp[4];
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + j, gi);
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + H + j, gg);
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + 2 * H + j, gf);
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + 3 * H + j, go);
-      ldf4(p.c_prev ? p.c_prev + mh : nullptr, cp);
-      float h[4], c[4], tcv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gi[e] = sgm(gi[e] + acc[0][t][e]);
-        gg[e] = tanhf(gg[e] + acc[1][t][e]);
-        gf[e] = sgm(gf[e] + acc[2][t][e]);
-        go[e] = sgm(go[e] + acc[3][t][e]);
-        c[e] = gi[e] * gg[e] + gf[e] * cp[e];
-        tcv[e] = tanhf(c[e]);
-        h[e] = go[e] * tcv[e];
-      }
-      stb4(p.h_out + (long long)m * p.ldho + j, h);
-      if (p.c_out) stf4(p.c_out + mh, c);
-      if (p.act) {
-        float* a = p.act + (long long)m * 4 * H + j;
-        stf4(a, gi);
-        stf4(a + H, gg);
-        stf4(a + 2 * H, gf);
-        stf4(a + 3 * H, go);
-      }
-      if (p.tc) stf4(p.tc + mh, tcv);
-    } else if constexpr (CELL == 1) {
-      float dh[4], i4[4], g4[4], f4[4], o4[4], tcv[4], cp[4], gcn[4];
-      ld4(p.gy, 0, (long long)m * p.ldgy + j, dh);
-      const float* a = p.act + (long long)m * 4 * H + j;
-      ldf4(a, i4);
-      ldf4(a + H, g4);
-      ldf4(a + 2 * H, f4);
-      ldf4(a + 3 * H, o4);
-      ldf4(p.tc + mh, tcv);
-      ldf4(p.c_prev ? p.c_prev + mh : nullptr, cp);
-      ldf4(p.gc_next ? p.gc_next + mh : nullptr, gcn);
-      float di[4], dgg[4], df[4], dout[4], dcp[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d_h = dh[e] + acc[0][t][e];
-        const float dc = d_h * o4[e] * (1.f - tcv[e] * tcv[e]) + gcn[e];
-        di[e] = dc * g4[e] * i4[e] * (1.f - i4[e]);
-        dgg[e] = dc * i4[e] * (1.f - g4[e] * g4[e]);
-        df[e] = dc * cp[e] * f4[e] * (1.f - f4[e]);
-        dout[e] = d_h * tcv[e] * o4[e] * (1.f - o4[e]);
-        dcp[e] = dc * f4[e];
-      }
-      bf16_t* o = p.dg + (long long)m * p.lddg + j;
-      stb4(o, di);
-      stb4(o + H, dgg);
-      stb4(o + 2 * H, df);
-      stb4(o + 3 * H, dout);
-      stf4(p.dc_prev + mh, dcp);
-    } else if constexpr (CELL == 2) {
-      float xr[4], xz[4], hp[4], r[4], z[4], rh[4];
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + j, xr);
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + H + j, xz);
-      ld4(p.hprev, 0, (long long)m * p.ldhp + j, hp);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        r[e] = sgm(xr[e] + acc[0][t][e]);
-        z[e] = sgm(xz[e] + acc[1][t][e]);
-        rh[e] = r[e] * hp[e];
-      }
-      stb4(p.rh + (long long)m * p.ldrh + j, rh);
-      stf4(p.s0 + mh, r);
-      stf4(p.s1 + mh, z);
-    } else if constexpr (CELL == 3) {
-      float xn[4], hp[4], z[4], n[4], h[4];
-      ld4(p.xg, p.x_f32, (long long)m * p.ldx + 2 * H + j, xn);
-      ld4(p.hprev, 0, (long long)m * p.ldhp + j, hp);
-      ldf4(p.s1 + mh, z);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        n[e] = tanhf(xn[e] + acc[0][t][e]);
-        h[e] = (1.f - z[e]) * n[e] + z[e] * hp[e];
-      }
-      stb4(p.h_out + (long long)m * p.ldho + j, h);
-      if (p.s2) stf4(p.s2 + mh, n);
-    } else if constexpr (CELL == 4) {
-      float gy[4], carry[4], z[4], n[4], hp[4], daz[4], dan[4], nc[4];
-      ld4(p.gy, 0, (long long)m * p.ldgy + j, gy);
-      ldf4(p.s0 + mh, carry);
-      ldf4(p.s1 + mh, z);
-      ldf4(p.s2 + mh, n);
-      ld4(p.hprev, 0, (long long)m * p.ldhp + j, hp);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float dh = gy[e] + carry[e] + acc[0][t][e];
-        dan[e] = dh * (1.f - z[e]) * (1.f - n[e] * n[e]);
-        daz[e] = dh * (hp[e] - n[e]) * z[e] * (1.f - z[e]);
-        nc[e] = dh * z[e];
-      }
-      bf16_t* o = p.dg + (long long)m * p.lddg + j;
-      stb4(o + H, daz);
-      stb4(o + 2 * H, dan);
-      stf4(p.s0 + mh, nc);
-    } else {  // CELL == 5
-      float carry[4], r[4], hp[4], dar[4];
-      ldf4(p.s0 + mh, carry);
-      ldf4(p.s1 + mh, r);
-      ld4(p.hprev, 0, (long long)m * p.ldhp + j, hp);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float drh = acc[0][t][e];
-        dar[e] = drh * hp[e] * r[e] * (1.f - r[e]);
-        carry[e] += drh * r[e];
-      }
-      stb4(p.dg + (long long)m * p.lddg + j, dar);
-      stf4(p.s0 + mh, carry);
-    }
-  }
+  if (!jin) return;
+  if (min0) epilogue<CELL, G>(p, m0 + fr, j, pre0, acc0);
+  if (min1) epilogue<CELL, G>(p, m0 + 16 + fr, j, pre1, acc1);
 }
 
 static bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -308,4 +341,102 @@ BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const vo
     default: hipLaunchKernelGGL((k_rnn_step<5, 1>), grid, block, 0, s, p); break;
   }
   BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Whole-sequence launchers: the time loop runs on the host in C++, one validated rnn_step launch
+// per step — the Python side makes ONE call per layer per direction (the eager PTB step was bound
+// by per-step Python/ctypes dispatch, not by the GPU).  Layouts (elements, bf16 unless noted):
+//   x2 [B][T][G·H] input projection, out [B][T][H] hidden sequence, per-step fp32 saves [T][B][·],
+//   DG [B][T][G·H] gate gradients.  Graph-capturable (launches only, no host sync).
+// ------------------------------------------------------------------------------------------------
+static const bf16_t* bo(const void* p, long long off) { return p ? (const bf16_t*)p + off : nullptr; }
+
+BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, const float* c0, const void* U, void* out,
+                                    float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H,
+                                    hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !U || !out) return (int)hipErrorInvalidValue;
+  const bool train = cs && acts && tcs;
+  if (!train && !cbuf) return (int)hipErrorInvalidValue;
+  const long long G = 4LL * H, BH = (long long)B * H;
+  const int esz = x_f32 ? 4 : 2;
+  for (int t = 0; t < T; ++t) {
+    const void* a = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
+    const long long lda = t == 0 ? H : (long long)T * H;
+    const void* xg = (const char*)x2 + (long long)t * G * esz;
+    const float* cp = t == 0 ? c0 : (train ? cs + (t - 1) * BH : cbuf + ((t - 1) & 1) * BH);
+    float* co = train ? cs + t * BH : cbuf + (t & 1) * BH;
+    int rc = bigdl_rnn_step(0, a, lda, U, B, H, H, xg, (long long)T * G, x_f32, nullptr, 0, cp,
+                            (bf16_t*)out + (long long)t * H, (long long)T * H, co, train ? acts + t * B * G : nullptr,
+                            train ? tcs + t * BH : nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                            nullptr, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float* acts, const float* tcs, const float* cs,
+                                    const float* c0, void* DG, float* gc, int B, int T, int H, hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !gy || !Ut || !DG || !gc) return (int)hipErrorInvalidValue;
+  const long long G = 4LL * H, BH = (long long)B * H;
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t + 1 == T;
+    int rc = bigdl_rnn_step(1, last ? nullptr : bo(DG, (t + 1) * G), (long long)T * G, Ut, B, (int)G, H, nullptr, 0, 0,
+                            nullptr, 0, t > 0 ? cs + (t - 1) * BH : c0, nullptr, 0, nullptr, (float*)acts + t * B * G,
+                            (float*)tcs + t * BH, bo(gy, (long long)t * H), (long long)T * H, last ? nullptr : gc,
+                            (bf16_t*)DG + t * G, (long long)T * G, gc, nullptr, nullptr, nullptr, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// GRU: R, Z, Nn fp32 [S][B][H] and RH bf16 [B][S][H] with S = T (training) or 1 (inference: slot 0
+// reused every step; Nn may be null)
+BIGDL_EXPORT int bigdl_gru_seq_fwd(const void* x2, int x_f32, const void* h0, const void* Urz, const void* Uh, void* out,
+                                   float* R, float* Z, float* Nn, void* RH, int train, int B, int T, int H,
+                                   hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !Urz || !Uh || !out || !R || !Z || !RH) return (int)hipErrorInvalidValue;
+  const long long G = 3LL * H, BH = (long long)B * H;
+  const int S = train ? T : 1;
+  const int esz = x_f32 ? 4 : 2;
+  for (int t = 0; t < T; ++t) {
+    const int k = train ? t : 0;
+    const void* hp = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
+    const long long ldhp = t == 0 ? H : (long long)T * H;
+    const void* xg = (const char*)x2 + (long long)t * G * esz;
+    bf16_t* rh = (bf16_t*)RH + (long long)k * H;
+    int rc = bigdl_rnn_step(2, hp, ldhp, Urz, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr, nullptr, 0, nullptr,
+                            nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, R + k * BH, Z + k * BH, nullptr,
+                            rh, (long long)S * H, s);
+    if (rc) return rc;
+    rc = bigdl_rnn_step(3, rh, (long long)S * H, Uh, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr,
+                        (bf16_t*)out + (long long)t * H, (long long)T * H, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                        nullptr, 0, nullptr, nullptr, Z + k * BH, (train && Nn) ? Nn + k * BH : nullptr, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+BIGDL_EXPORT int bigdl_gru_seq_bwd(const void* gy, const void* Urz_t, const void* Uh_t, const float* R, const float* Z,
+                                   const float* Nn, const void* out, const void* h0, void* DG, float* carry, int B, int T,
+                                   int H, hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !gy || !Urz_t || !Uh_t || !R || !Z || !Nn || !out || !h0 || !DG || !carry)
+    return (int)hipErrorInvalidValue;
+  const long long G = 3LL * H, BH = (long long)B * H;
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t + 1 == T;
+    const void* hp = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
+    const long long ldhp = t == 0 ? H : (long long)T * H;
+    bf16_t* dg = (bf16_t*)DG + t * G;
+    int rc = bigdl_rnn_step(4, last ? nullptr : bo(DG, (t + 1) * G), (long long)T * G, Urz_t, B, 2 * H, H, nullptr, 0,
+                            0, hp, ldhp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, bo(gy, (long long)t * H),
+                            (long long)T * H, nullptr, dg, (long long)T * G, nullptr, carry, (float*)Z + t * BH,
+                            (float*)Nn + t * BH, nullptr, 0, s);
+    if (rc) return rc;
+    rc = bigdl_rnn_step(5, dg + 2 * H, (long long)T * G, Uh_t, B, H, H, nullptr, 0, 0, hp, ldhp, nullptr, nullptr, 0,
+                        nullptr, nullptr, nullptr, nullptr, 0, nullptr, dg, (long long)T * G, nullptr, carry,
+                        (float*)R + t * BH, nullptr, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  return 0;
 }

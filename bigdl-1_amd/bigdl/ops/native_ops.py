@@ -1296,6 +1296,44 @@ def rnn_step(cell, a, u, M, K, Hs, xg=None, hprev=None, c_prev=None, h_out=None,
                                 ptr(s2), ptr(rh), _ll(_ld(rh)), _s()), f"rnn_step[{cell}]")
 
 
+def _dense_bf16(*ts):
+    return all(t is None or (t.is_cuda and t.is_contiguous() and _al16(t)) for t in ts)
+
+
+def lstm_seq_forward(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
+    """Whole-sequence fused LSTM forward (bigdl_lstm_seq_fwd): x2 [B][T][4H], out [B][T][H]; training
+    saves cs / tcs [T][B][H], acts [T][B][4H] (fp32), inference ping-pongs c through cbuf [2][B][H]."""
+    B, T, G = x2.shape
+    H = G // 4
+    assert _dense_bf16(x2, h0, c0, U, out, cs, acts, tcs, cbuf) and tuple(out.shape) == (B, T, H), "lstm_seq_forward"
+    check(_lib().bigdl_lstm_seq_fwd(ptr(x2), C.c_int(1 if x2.dtype == _f32 else 0), ptr(h0), ptr(c0), ptr(U), ptr(out),
+                                    ptr(cs), ptr(acts), ptr(tcs), ptr(cbuf), C.c_int(B), C.c_int(T), C.c_int(H), _s()),
+          "lstm_seq_fwd")
+
+
+def lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc):
+    B, T, H = gy.shape
+    assert _dense_bf16(gy, Ut, acts, tcs, cs, c0, DG, gc), "lstm_seq_backward"
+    check(_lib().bigdl_lstm_seq_bwd(ptr(gy), ptr(Ut), ptr(acts), ptr(tcs), ptr(cs), ptr(c0), ptr(DG), ptr(gc),
+                                    C.c_int(B), C.c_int(T), C.c_int(H), _s()), "lstm_seq_bwd")
+
+
+def gru_seq_forward(x2, h0, Urz, Uh, out, R, Z, Nn, RH, train):
+    B, T, G = x2.shape
+    H = G // 3
+    assert _dense_bf16(x2, h0, Urz, Uh, out, R, Z, Nn, RH), "gru_seq_forward"
+    check(_lib().bigdl_gru_seq_fwd(ptr(x2), C.c_int(1 if x2.dtype == _f32 else 0), ptr(h0), ptr(Urz), ptr(Uh), ptr(out),
+                                   ptr(R), ptr(Z), ptr(Nn), ptr(RH), C.c_int(1 if train else 0), C.c_int(B), C.c_int(T),
+                                   C.c_int(H), _s()), "gru_seq_fwd")
+
+
+def gru_seq_backward(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry):
+    B, T, H = gy.shape
+    assert _dense_bf16(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry), "gru_seq_backward"
+    check(_lib().bigdl_gru_seq_bwd(ptr(gy), ptr(Urz_t), ptr(Uh_t), ptr(R), ptr(Z), ptr(Nn), ptr(out), ptr(h0), ptr(DG),
+                                   ptr(carry), C.c_int(B), C.c_int(T), C.c_int(H), _s()), "gru_seq_bwd")
+
+
 def rnn_fast_ok(H, *ts):
     """The fused step covers bf16 rows with H % 8 == 0 on a device with the library loaded."""
     if H % 8 or not N.has("lstm_cell_forward"):
