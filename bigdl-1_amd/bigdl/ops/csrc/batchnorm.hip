@@ -81,11 +81,16 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
 // Parallel reduction of the G per-block partials: a 1024-thread block owns 32 channels; its 32 row
 // groups each sum G/32 partials with coalesced 128-B loads (8 in flight per thread), then a LDS tree.
 // Results: red[0][c] = Σ partial[0..G), red[1][c] = Σ partial[G..2G) for the block's 32 channels.
-__device__ __forceinline__ void reduce_partials(const float* __restrict__ partial, int G, int C, int c0,
-                                                float (*lds)[2][33], float& outA, float& outB) {
+// The sums over partials are fp64: the conv epilogue's partials are unshifted 128-row Σy, Σy², so
+// var = Σy²/M − mean² cancels; summing thousands of partials in double keeps that difference exact
+// to the partials' own fp32 rounding (profiles: a shifted fp32 epilogue cost 11 % of conv-forward
+// time, the fp64 combine costs nothing measurable).
+template <typename T>
+__device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, int G, int C, int c0,
+                                                double (*lds)[2][33], double& outA, double& outB) {
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = c0 + tx;
-  float a = 0.f, b = 0.f;
+  double a = 0.0, b = 0.0;
   if (c < C) {
     int i = ty;
 #pragma unroll 8
@@ -111,7 +116,8 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ partia
 // Combine partials; write save_mean/save_invstd, apply coefficients scale/shift, update running stats.
 // ``in_bias`` (optional) is a per-channel constant the producer did NOT add to x (a conv bias folded
 // into this BN): normalisation is shift-invariant, so only the running mean sees it.
-__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const float* __restrict__ partial,
+template <typename T>
+__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const T* __restrict__ partial,
                                                       int G, long long M, int C, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
                                                       const float* __restrict__ in_bias,
@@ -119,14 +125,16 @@ __global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__
                                                       float momentum, float eps, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
                                                       float* __restrict__ shift) {
-  __shared__ float lds[32][2][33];
-  float s, q;
+  __shared__ double lds[32][2][33];
+  double s, q;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
-  float K = x ? bf2f(x[c]) : 0.f;  // x == null: partials are unshifted (conv-epilogue stats)
-  float dm = s / (float)M;
-  float var = fmaxf(q / (float)M - dm * dm, 0.f);
+  // partials are shifted by the first row (standalone stats pass) or unshifted (conv epilogue)
+  const float K = x ? bf2f(x[c]) : 0.f;
+  const double dmd = s / (double)M;
+  const float var = (float)fmax(q / (double)M - dmd * dmd, 0.0);
+  const float dm = (float)dmd;
   float mean = K + dm;
   float invstd = rsqrtf(var + eps);
   save_mean[c] = mean;
@@ -233,8 +241,8 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, ws, G, M, C, gamma,
-                     beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, (const float*)ws, G,
+                     M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;
@@ -250,14 +258,14 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
 // rows, so the per-channel finalize reads a short column instead of a latency-bound 6k-long one.
 // grid (ceil(C/64), S), 256 threads = 64 channels × 4 row groups; rows [sy·R, sy·R + R) per block.
 __global__ void __launch_bounds__(256) k_bn_fold_partials(const float* __restrict__ partial, int G, int C, int R,
-                                                          int S, float* __restrict__ out) {
-  __shared__ float red[2][4][64];
+                                                          int S, double* __restrict__ out) {
+  __shared__ double red[2][4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   const int g0 = blockIdx.y * R;
   int g1 = g0 + R;
   if (g1 > G) g1 = G;
-  float a = 0.f, b = 0.f;
+  double a = 0.0, b = 0.0;
   if (c < C) {
 #pragma unroll 4
     for (int g = g0 + ty; g < g1; g += 4) {
@@ -276,20 +284,22 @@ __global__ void __launch_bounds__(256) k_bn_fold_partials(const float* __restric
 
 static constexpr int kFoldRows = 128;
 
-// floats of scratch bigdl_bn_*_partials needs for G partials of C channels (0: no pre-fold)
+// floats of scratch bigdl_bn_*_partials needs for G partials of C channels (0: no pre-fold); the
+// folded rows are fp64 (2 floats each)
 BIGDL_EXPORT long long bigdl_bn_fold_scratch(int G, int C) {
   if (G <= 512) return 0;
   const int S = (G + kFoldRows - 1) / kFoldRows;
-  return 2LL * S * C;
+  return 4LL * S * C;
 }
 
-static const float* maybe_fold(const float* partial, int& G, int C, float* scratch, hipStream_t s) {
-  if (G <= 512 || !scratch) return partial;
+// launch the finalize-type kernel on either the raw fp32 partials or their fp64 pre-fold
+static bool maybe_fold(const float* partial, int& G, int C, float* scratch, hipStream_t s) {
+  if (G <= 512 || !scratch) return false;
   const int S = (G + kFoldRows - 1) / kFoldRows;
   hipLaunchKernelGGL(k_bn_fold_partials, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, G, C, kFoldRows, S,
-                     scratch);
+                     (double*)scratch);
   G = S;
-  return scratch;
+  return true;
 }
 
 // Training forward from precomputed partials (the producing conv's epilogue wrote Σy, Σy² per row
@@ -300,9 +310,14 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
                                              float* save_mean, float* save_invstd, const float* partial, int G,
                                              float* coef, int relu, float* scratch, hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  partial = maybe_fold(partial, G, C, scratch, s);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, partial, G, M, C,
-                     gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
+  if (maybe_fold(partial, G, C, scratch, s))
+    hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr,
+                       (const double*)scratch, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
+                       save_invstd, coef, coef + C);
+  else
+    hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, partial, G,
+                       M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
+                       coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;
@@ -391,18 +406,20 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const bf16_t* __restrict_
 // coefficients for gx = A·g' + B·x + Cc
 // ``cbias`` (optional): gradient of a producer bias folded into this BN = Σ_rows gx, evaluated from
 // the closed form A·Σg' + B·Σx + M·Cc (Σx = M·mean) and accumulated with ``cbscale``.
-__global__ void __launch_bounds__(1024) k_bn_bwd_finalize(const float* __restrict__ partial, int G, long long M,
+template <typename T>
+__global__ void __launch_bounds__(1024) k_bn_bwd_finalize(const T* __restrict__ partial, int G, long long M,
                                                           int C, const float* __restrict__ gamma,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ ggamma, float* __restrict__ gbeta,
                                                           float gscale, float* __restrict__ cbias, float cbscale,
                                                           float* __restrict__ coef) {
-  __shared__ float lds[32][2][33];
-  float a, b;
-  reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
+  __shared__ double lds[32][2][33];
+  double ad, bd;
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, ad, bd);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
+  const float a = (float)ad, b = (float)bd;
   float is = invstd[c];
   float dbeta = a;
   float dgamma = b * is;
@@ -472,8 +489,8 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
                        (const bf16_t*)y, M, C, rpb, mean, ws, G);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, ws, G, M, C, gamma, mean, invstd,
-                     ggamma, gbeta, gscale, cbias, cbscale, coef);
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const float*)ws, G, M, C, gamma,
+                     mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
     const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;
@@ -494,9 +511,12 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
                                        float gscale, float* cbias, float cbscale, const float* partial, int G,
                                        float* coef, float* scratch, hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  partial = maybe_fold(partial, G, C, scratch, s);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, M, C, gamma, mean, invstd,
-                     ggamma, gbeta, gscale, cbias, cbscale, coef);
+  if (maybe_fold(partial, G, C, scratch, s))
+    hipLaunchKernelGGL(k_bn_bwd_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const double*)scratch, G, M,
+                       C, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, M, C, gamma, mean,
+                       invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
     hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,

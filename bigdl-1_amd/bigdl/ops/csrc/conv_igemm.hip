@@ -51,6 +51,9 @@ struct ConvParams {
   // output row stride in elements (== K unless the conv writes a channel slice of a wider tensor,
   // e.g. its branch of an Inception concat: y points at the slice, rows are ldy apart)
   int ldy;
+  // weight row stride in elements (== Kg, or Kg rounded up to 8 for the C = 4 stem, whose rows are
+  // zero-padded so every weight chunk stays 16-B aligned)
+  int ldw;
 };
 
 constexpr int SBM = 128;  // row granularity of the BN-statistics partials (any BM writes BM / SBM rows)
@@ -70,11 +73,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// FAST: C % 64 == 0 and R·S ≤ 64 — every k-tile lies inside one filter tap, so the tap / channel
-// position of a k-tile is wave-uniform (scalar registers, no per-lane division) and the padding test
-// of a staged row is one bit of a per-row tap-validity mask built once in the prologue.
-template <int BN, bool FAST, int BM, int BK>
+// MODE 1 (FAST): C % BK == 0 and R·S ≤ 64 — every k-tile lies inside one filter tap, so the tap /
+// channel position of a k-tile is wave-uniform (scalar registers, no per-lane division) and the
+// padding test of a staged row is one bit of a per-row tap-validity mask built once in the prologue.
+// MODE 2 (C4): 4-channel input (the RGB stem padded 3 → 4, not 8: 1.33× instead of 2.67× padded
+// MACs and half the input bytes) — a 16-B chunk holds two consecutive taps, gathered as two 8-B
+// loads with their own padding tests.  MODE 0: any C % 8 == 0.
+template <int BN, int MODE, int BM, int BK>
 __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_conv_fwd(ConvParams p) {
+  constexpr bool FAST = MODE == 1;
   constexpr int ROWS = BM + BN;
   constexpr int CPK = BK / 8;    // 16-B chunks per staged row
   constexpr int RPS = 256 / CPK; // rows staged per pass of the block
@@ -98,7 +105,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // branches (a per-element "load or zero" select makes hipcc branch and drain vmcnt per load,
   // cdna_hip_programming.md §5 item 4(c)).  OOB = an offset past the end of the tensor.
   const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C * 2);
-  const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.Kg * 2);
+  const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw * 2);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
   constexpr uint32_t OOB = 0xFFFFFFF0u;
@@ -125,7 +132,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 #pragma unroll
   for (int i = 0; i < B_CHUNKS; ++i) {
     const int n = n0 + tid / CPK + RPS * i;
-    b_row[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 2u : 0x80000000u;  // + any k stays out of range
+    b_row[i] = n < p.K ? (uint32_t)n * (uint32_t)p.ldw * 2u : 0x80000000u;  // + any k stays out of range
   }
 
   const int KT = (p.Kg + BK - 1) / BK;
@@ -173,6 +180,31 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 #pragma unroll
       for (int i = 0; i < B_CHUNKS; ++i) {
         const uint32_t off = (b_row[i] + (uint32_t)(kb + col8 * 8) * 2u) | dead;  // OOB rows stay out of range
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+      }
+    } else if constexpr (MODE == 2) {
+      const int k = kt * BK + col8 * 8;
+      const bool kin0 = live && k < p.Kg, kin1 = live && k + 4 < p.Kg;
+      const int t0 = k >> 2;
+      int r0 = t0 / p.S, s0 = t0 - (t0 / p.S) * p.S;
+      int r1 = r0, s1 = s0 + 1;
+      if (s1 == p.S) { s1 = 0; ++r1; }
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const int h0 = a_h[i] + r0 * p.dh, w0 = a_w[i] + s0 * p.dw;
+        const int h1 = a_h[i] + r1 * p.dh, w1 = a_w[i] + s1 * p.dw;
+        const bool ok0 = kin0 && (unsigned)h0 < (unsigned)p.H && (unsigned)w0 < (unsigned)p.W;
+        const bool ok1 = kin1 && (unsigned)h1 < (unsigned)p.H && (unsigned)w1 < (unsigned)p.W;
+        const uint32_t off0 = ok0 ? (uint32_t)((a_img[i] + h0 * p.W + w0) * 4) * 2u : OOB;
+        const uint32_t off1 = ok1 ? (uint32_t)((a_img[i] + h1 * p.W + w1) * 4) * 2u : OOB;
+        const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off0, 0, 0));
+        const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
+        ra[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+      const bool kw = live && k < p.ldw;
+#pragma unroll
+      for (int i = 0; i < B_CHUNKS; ++i) {
+        const uint32_t off = kw && b_row[i] != OOB ? b_row[i] + (uint32_t)k * 2u : OOB;
         rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
       }
     } else {
@@ -455,11 +487,13 @@ static int conv_env_override(const char* name, int a, int b) {
 }
 
 template <int BN, int BM, int BK>
-static void launch_fwd(bool fast, dim3 grid, hipStream_t s, const ConvParams& p) {
-  if (fast)
-    hipLaunchKernelGGL((k_conv_fwd<BN, true, BM, BK>), grid, dim3(256), 0, s, p);
+static void launch_fwd(int mode, dim3 grid, hipStream_t s, const ConvParams& p) {
+  if (mode == 1)
+    hipLaunchKernelGGL((k_conv_fwd<BN, 1, BM, BK>), grid, dim3(256), 0, s, p);
+  else if (mode == 2)
+    hipLaunchKernelGGL((k_conv_fwd<BN, 2, BM, BK>), grid, dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((k_conv_fwd<BN, false, BM, BK>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((k_conv_fwd<BN, 0, BM, BK>), grid, dim3(256), 0, s, p);
 }
 
 // Host launchers.  Requirements (checked): C % 8 == 0 (any K; residual / statistics need K % 8), 16-B aligned x/w/y/res.
@@ -471,12 +505,16 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
-                           hipStream_t s) {
-  if (C % 8 || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;  // any K: partial 8-channel chunks store per element
+                           hipStream_t s, int ldw = 0) {
+  const bool c4 = C == 4;
+  // any K: partial 8-channel chunks are stored per element in the epilogue
+  if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if (c4 && (ldw < R * S * C || ldw % 8 || dh != 1 || dw != 1)) return (int)hipErrorInvalidValue;
   if (ldy < K || (ldy != K && (ldy % 8 || K % 8 || ((uintptr_t)y & 15)))) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
-  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * R * S * C * 2 >= 0x80000000ull)
+  if (!c4) ldw = R * S * C;
+  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * ldw * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
   ConvParams p;
   p.x = (const bf16_t*)x;
@@ -491,6 +529,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   p.M = (int)Ml;
   p.Kg = R * S * C;
+  p.ldw = ldw;
   p.relu = relu;
   p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
   p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
@@ -517,16 +556,16 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const int bk_env = conv_env_override("BIGDL_CONV_BK", 32, 64);
   const int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
   const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
-  const bool fast = (C % bk == 0) && R * S <= 64;
+  const int mode = c4 ? 2 : ((C % bk == 0) && R * S <= 64 ? 1 : 0);
   long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles);
   if (bm == 256)
-    BN == 64 ? launch_fwd<64, 256, 64>(fast, g, s, p) : launch_fwd<128, 256, 64>(fast, g, s, p);
+    BN == 64 ? launch_fwd<64, 256, 64>(mode, g, s, p) : launch_fwd<128, 256, 64>(mode, g, s, p);
   else if (bk == 32)
-    BN == 64 ? launch_fwd<64, 128, 32>(fast, g, s, p) : launch_fwd<128, 128, 32>(fast, g, s, p);
+    BN == 64 ? launch_fwd<64, 128, 32>(mode, g, s, p) : launch_fwd<128, 128, 32>(mode, g, s, p);
   else
-    BN == 64 ? launch_fwd<64, 128, 64>(fast, g, s, p) : launch_fwd<128, 128, 64>(fast, g, s, p);
+    BN == 64 ? launch_fwd<64, 128, 64>(mode, g, s, p) : launch_fwd<128, 128, 64>(mode, g, s, p);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -568,4 +607,42 @@ BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias,
                                 int relu, hipStream_t s) {
   return bigdl_conv_fwd_ex(x, w, bias, nullptr, y, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu,
                            s);
+}
+
+// 4-channel (RGB-padded) input with weight rows ldw elements apart (ldw % 8 == 0, zero beyond R·S·4).
+BIGDL_EXPORT int bigdl_conv_fwd_c4(const void* x, const void* w, int ldw, const float* bias, const void* res, void* y,
+                                   float* stats, int Nb, int H, int W, int K, int R, int S, int P, int Q, int sh, int sw,
+                                   int ph, int pw, int relu, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, 4, K, R, S, P, Q, sh, sw, ph, pw, 1, 1, relu, 1, 1, 0, 0,
+                         P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw);
+}
+
+// NHWC channel zero-pad (the RGB stem: 3 → 4 channels, one 8-B store per pixel): dst[p][0:C] = src[p],
+// dst[p][C:Cp] = 0.  One thread per pixel; C ≤ Cp ≤ 8.
+__global__ void __launch_bounds__(256) k_pad_channels(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, long long npix,
+                                                     int C, int Cp) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix; i += (long long)gridDim.x * blockDim.x) {
+    bf16_t v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < C ? src[i * C + c] : (bf16_t)0;
+    if (Cp == 4) {
+      *reinterpret_cast<uint2*>(dst + i * 4) = make_uint2((uint32_t)v[0] | ((uint32_t)v[1] << 16),
+                                                          (uint32_t)v[2] | ((uint32_t)v[3] << 16));
+    } else if (Cp == 8) {
+      *reinterpret_cast<uint4*>(dst + i * 8) = make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16),
+                                                          (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                                                          (uint32_t)v[4] | ((uint32_t)v[5] << 16),
+                                                          (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+    } else {
+      for (int c = 0; c < Cp; ++c) dst[i * Cp + c] = v[c];
+    }
+  }
+}
+
+BIGDL_EXPORT int bigdl_pad_channels(const void* src, void* dst, long long npix, int C, int Cp, hipStream_t s) {
+  if (npix <= 0 || C <= 0 || C > Cp || Cp > 8) return (int)hipErrorInvalidValue;
+  if ((Cp == 4 && ((uintptr_t)dst & 7)) || (Cp == 8 && ((uintptr_t)dst & 15))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pad_channels, dim3(bigdl_grid(npix, 256, 16384)), dim3(256), 0, s, (const bf16_t*)src,
+                     (bf16_t*)dst, npix, C, Cp);
+  BIGDL_CHECK_LAUNCH();
 }

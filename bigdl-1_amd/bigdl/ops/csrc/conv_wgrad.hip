@@ -59,7 +59,9 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
   }
 }
 
-template <int TILE_N, int TILE_K, int BPT>
+// C4: 4-channel input (RGB stem padded 3 → 4): an X̂ chunk of 8 k-values is two consecutive taps,
+// gathered as two 8-B loads with separate padding tests (see conv_igemm.hip MODE 2).
+template <int TILE_N, int TILE_K, int BPT, bool C4 = false>
 __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradParams p) {
   constexpr int DY_CH = BPT * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
   constexpr int X_CH = BPT * TILE_K / 8 / 256;   // for the X̂ tile
@@ -94,6 +96,10 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   int tap = kx_ok ? kx / p.C : 0;
   const int cx = kx - tap * p.C;
   const int rx = tap / p.S, sx = tap - (tap / p.S) * p.S;
+  // C4: the chunk's second tap (tap + 1, wrapping to the next filter row)
+  const bool kx1_ok = kx + 4 < p.Kg;
+  int rx1 = rx, sx1 = sx + 1;
+  if (sx1 == p.S) { sx1 = 0; ++rx1; }
   const int ndy = n0 + dy_col * 8;
   const bool ndy_ok = ndy < p.K;
 
@@ -126,8 +132,18 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
       const int h = (int)pp * p.sh - p.ph + rx * p.dh;
       const int w = (int)q * p.sw - p.pw + sx * p.dw_;
       const bool ok = kx_ok && m < mend && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
-      const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.C + (uint32_t)cx) * 2u : DEAD) | dead;
-      rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      if constexpr (C4) {
+        const int h1 = (int)pp * p.sh - p.ph + rx1, w1 = (int)q * p.sw - p.pw + sx1;
+        const bool ok1 = kx1_ok && m < mend && (unsigned)h1 < (unsigned)p.H && (unsigned)w1 < (unsigned)p.W;
+        const uint32_t off0 = (ok ? (uint32_t)((n * p.H + h) * p.W + w) * 8u : DEAD) | dead;
+        const uint32_t off1 = (ok1 ? (uint32_t)((n * p.H + h1) * p.W + w1) * 8u : DEAD) | dead;
+        const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off0, 0, 0));
+        const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
+        rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.C + (uint32_t)cx) * 2u : DEAD) | dead;
+        rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      }
     }
   };
   auto store = [&](int buf, const uint4 (&rdy)[DY_CH], const uint4 (&rx_)[X_CH]) {
@@ -223,7 +239,9 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
 BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C,
                                   int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
                                   int splits, hipStream_t s) {
-  if (C % 8 || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
+  const bool c4 = C == 4;
+  if ((C % 8 && !c4) || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
+  if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
   if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)Nb * P * Q * K * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   WgradParams p;
@@ -238,7 +256,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   p.fPQ = make_fastdiv((uint32_t)(P * Q));
   p.fQ = make_fastdiv((uint32_t)Q);
   const int TN = K <= 64 ? 64 : 128;
-  const int TK = p.Kg <= 64 ? 64 : 128;
+  const int TK = (p.Kg <= 64 && !c4) ? 64 : 128;  // the C4 kernels are instantiated with 128-wide k tiles only
   p.tiles_n = (K + TN - 1) / TN;
   p.tiles_k = (p.Kg + TK - 1) / TK;
   const int tiles = p.tiles_n * p.tiles_k;
@@ -265,7 +283,15 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   const char* ev = getenv("BIGDL_WGRAD_BP");
   const int bp_env = ev ? atoi(ev) : 0;
   const int bp = (bp_env == 32 || bp_env == 64) ? bp_env : (tiles <= 16 && K >= 128 ? 32 : 64);
-  if (bp == 32) {
+  if (c4) {
+    if (bp == 32) {
+      if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32, true>), grid, dim3(256), 0, s, p);
+    } else {
+      if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 64, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64, true>), grid, dim3(256), 0, s, p);
+    }
+  } else if (bp == 32) {
     if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32>), grid, dim3(256), 0, s, p);
     else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32>), grid, dim3(256), 0, s, p);
     else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 32>), grid, dim3(256), 0, s, p);

@@ -311,8 +311,14 @@ def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
             return padded
     n, c, h, w = x_nhwc_4d.shape
     out = torch.empty((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
-    out[..., c:].zero_()
-    out[..., :c] = x_nhwc_4d.permute(0, 2, 3, 1)
+    if (x_nhwc_4d.is_cuda and x_nhwc_4d.dtype == _bf16 and c_to <= 8 and _al16(out)
+            and x_nhwc_4d.is_contiguous(memory_format=torch.channels_last)):
+        # one HIP pass: read C, write C_to (8-B / 16-B stores), no separate zero fill
+        check(_lib().bigdl_pad_channels(ptr(x_nhwc_4d), ptr(out), _ll(n * h * w), C.c_int(c), C.c_int(c_to), _s()),
+              "pad_channels")
+    else:
+        out[..., c:].zero_()
+        out[..., :c] = x_nhwc_4d.permute(0, 2, 3, 1)
     res = out.permute(0, 3, 1, 2)
     if slot is not None:
         slot[0] = (x_nhwc_4d, x_nhwc_4d._version, c_to, res)
@@ -337,7 +343,18 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     if (res is not None or stats) and K % 8:
         return NotImplemented
     wk = _krsc(w4)
-    if C_ % 8:
+    c4 = C_ <= 4 and out is None and tuple(dilation) == (1, 1)
+    ldw = 0
+    if c4:
+        # RGB stem: pad 3 → 4 channels (not 8) and run the two-taps-per-chunk C4 gather; weight rows
+        # are zero-padded to a multiple of 8 elements so every 16-B weight chunk stays aligned
+        x = _pad_channels(x, 4, pad_slot)
+        kg = R * S * 4
+        ldw = (kg + 7) // 8 * 8
+        wp = torch.zeros((K, ldw), dtype=wk.dtype, device=wk.device)
+        wp[:, :kg].view(K, R, S, 4)[..., :C_] = wk
+        wk, C_ = wp, 4
+    elif C_ % 8:
         cp = (C_ + 7) // 8 * 8
         x = _pad_channels(x, cp, pad_slot)
         wp = torch.zeros((K, R, S, cp), dtype=wk.dtype, device=wk.device)
@@ -364,6 +381,10 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     if stats:
         G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
         part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
+    if c4:
+        check(_lib().bigdl_conv_fwd_c4(ptr(x), ptr(wk), ldw, ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, K, R, S,
+                                       P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()), "conv_fwd_c4")
+        return (y, part, G) if stats else y
     check(_lib().bigdl_conv_fwd_ldy(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
                                     P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy,
                                     _s()), "conv_fwd")
@@ -380,8 +401,9 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
 
 
 def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None):
-    """Forward conv whose epilogue also emits per-row-tile Σy/Σy² partials for a following BN.
-    Returns ``(y, partials, G)`` or NotImplemented."""
+    """Forward conv whose epilogue also emits per-row-tile Σy/Σy² partials for a following BN
+    (128-row tiles; the BN finalize combines them in fp64).  Returns ``(y, partials, G)`` or
+    NotImplemented."""
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot)
 
 
@@ -657,7 +679,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     if gw_acc is not None and scale != 0:
         xx, cc = x, C_
         if C_ % 8:
-            cc = (C_ + 7) // 8 * 8
+            cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
             xx = _pad_channels(x, cc, pad_slot, reuse=True)
         direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)

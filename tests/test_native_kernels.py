@@ -190,7 +190,10 @@ CONV_CASES = [
     (2, 64, 15, 13, 64, 3, 3, 1, 1),      # 3x3 s1, odd spatial
     (2, 128, 16, 16, 128, 3, 3, 2, 1),    # 3x3 s2 (ResNet v1.5 downsample)
     (2, 256, 14, 14, 512, 1, 1, 2, 0),    # 1x1 s2 projection shortcut
-    (2, 3, 32, 32, 64, 7, 7, 2, 3),       # stem (C=3 padded to 8)
+    (2, 3, 32, 32, 64, 7, 7, 2, 3),       # stem (C=3 padded to 4: two-tap C4 gather)
+    (2, 3, 17, 19, 16, 3, 3, 1, 1),       # RGB 3x3 (C4, R·S odd → half-chunk tail)
+    (2, 4, 12, 12, 32, 5, 5, 2, 2),       # C = 4 exactly
+    (2, 1, 28, 28, 6, 5, 5, 1, 0),        # LeNet conv1 (C=1 → 4, K=6: per-element epilogue tail)
     (3, 24, 9, 9, 40, 5, 5, 1, 2),        # Inception-ish odd channels
 ]
 
@@ -320,6 +323,28 @@ def test_bn_forward_from_conv_partials():
     torch.testing.assert_close(rm1, rm2, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(rv1, rv2, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(out.float(), ro.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_bn_from_conv_partials_large_mean():
+    """Conv-epilogue statistics with outputs of mean ≈ 64 and std ≈ 0.5 over a 56²-sized batch
+    (thousands of 128-row partials): the fp64 combine of the unshifted Σy, Σy² partials must keep
+    the variance of the stored values (fp32 two-pass reference)."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    C, K = 64, 64
+    x = _cl(torch.randn(80, C, 32, 32, device=dev).bfloat16())
+    w4 = _cl((torch.randn(K, C, 1, 1, device=dev) * 0.06).bfloat16())
+    bias = torch.full((K,), 64.0, device=dev)
+    y, part, G = NO.conv2d_forward_stats(x, w4, bias, (1, 1), (0, 0))
+    assert G > 512  # exercises the fp64 pre-fold
+    g, b = torch.ones(K, device=dev), torch.zeros(K, device=dev)
+    rm, rv = torch.zeros(K, device=dev), torch.ones(K, device=dev)
+    out, mean, invstd = NO.batchnorm_forward_train_partials(y, part, G, g, b, rm, rv, 0.1, 1e-5)
+    yf = y.float()
+    ref_mean = yf.mean((0, 2, 3))
+    ref_var = yf.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(mean, ref_mean, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, ref_var, rtol=1e-2, atol=1e-4)
 
 
 def test_dgrad_residual_fold():
