@@ -85,6 +85,8 @@ class DistriOptimizer(BaseOptimizer):
         m.to(self.device)
         m.training()
         fuse(m)
+        from ..nn.fusion import mark_input_no_grad
+        mark_input_no_grad(m)
         W = self.world
         self.flat = m.compactParametersBucketed(self.bucket_bytes, 64 * W)
         if self.flat is None:

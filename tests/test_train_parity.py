@@ -1,0 +1,204 @@
+"""Training-step parity of the fused native bf16 GPU path against an fp32 oracle.
+
+1. One ResNet training forward/backward with every fusion on (conv-epilogue BN statistics,
+   BN-backward prologues in the dgrad epilogue, fused block tails, C = 4 stem) vs the same model in
+   fp32 on the host (plain torch reference ops) on the same bf16-rounded weights and input:
+   ResNet-18 — loss within 1e-2, gradient cosines median > 0.9 / min > 0.8; ResNet-50 — loss
+   within 1e-2 and gradient agreement no worse than torch's own bf16 ops (ResNet-50 at init is
+   gradient-chaotic under any bf16 storage, see tools/parity_diag.py); plus a memorisation run.
+   Reference method: spark/dl/src/test/scala/.../nn/mkldnn/TopologySpec.scala:946-1057 (a fused
+   DNN topology compared layer by layer against the plain BigDL one).
+2. LocalOptimizer vs DistriOptimizer at world size 1 over the RCCL path (sharded RS → update → AG,
+   bucket hooks firing during the fused backward) for 3 SGD steps: identical weights.
+   Reference: spark/dl/src/test/scala/.../optim/DistriOptimizerSpec.scala:378,428.
+"""
+import copy
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _setup_bf16():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+
+
+def _cos(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
+
+
+def _resnet(classes=100, depth=50):
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.utils.random import RNG
+    RNG.setSeed(7)
+    torch.manual_seed(7)
+    return model_init(ResNet(classes, depth=depth, dataset=DatasetType.ImageNet))
+
+
+def _grad_cosines(depth, native, batch=4):
+    """(loss_device, loss_host, [per-tensor gradient cosine]) of one bf16 device training step vs the
+    fp32 host oracle run on the SAME function (bf16-rounded weights and input).  Conv biases that feed
+    a BatchNormalization are skipped: their true gradient is 0, so their cosine is pure noise."""
+    from bigdl.utils import config
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.nn.fusion import fuse, mark_input_no_grad
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.native.enable", bool(native))
+    try:
+        cpu = _resnet(100, depth)
+        with torch.no_grad():
+            for w in cpu.parameters()[0]:
+                w.copy_(w.to(torch.bfloat16).float())
+        gpu = copy.deepcopy(cpu)
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(batch, 3, 224, 224, generator=g).to(torch.bfloat16).float()
+        y = (torch.randint(0, 100, (batch,), generator=g) + 1).float()
+        cc, cg = CrossEntropyCriterion(), CrossEntropyCriterion()
+        cpu.training()
+        cpu.zeroGradParameters()
+        oc = cpu.forward(x)
+        lc = float(cc.forward(oc, y))
+        cpu.backward(x, cc.backward(oc, y))
+        gpu.cuda()
+        gpu.training()
+        fuse(gpu)
+        mark_input_no_grad(gpu)
+        gpu.getParameters()
+        gpu.flat_parameters().enable_shadow(Engine.compute_dtype())
+        gpu.zeroGradParameters()
+        xg = x.to(dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        og = gpu.forward(xg)
+        lg = float(cg.forward(og, y.to(dev)))
+        gpu.backward(xg, cg.backward(og, y.to(dev)))
+        torch.cuda.synchronize()
+    finally:
+        config.set_property("bigdl.native.enable", True)
+    names = [f"{type(m).__name__}.{n}" for (m, n, _g) in cpu._param_entries()]
+    cos = [_cos(a.float().cpu(), b) for nm, a, b in zip(names, gpu.parameters()[1], cpu.parameters()[1])
+           if not (nm.endswith(".bias") and "Convolution" in nm) and float(b.norm()) > 1e-8]
+    return lg, lc, cos
+
+
+def test_resnet18_fused_bf16_step_matches_fp32_oracle():
+    """ResNet-18 (ImageNet topology): loss within 1e-2 relative, median gradient cosine > 0.9,
+    minimum > 0.8 (bf16 activation / gradient storage is the remaining difference)."""
+    _setup_bf16()
+    lg, lc, cos = _grad_cosines(18, native=True)
+    assert abs(lg - lc) <= 1e-2 * abs(lc), (lg, lc)
+    cs = sorted(cos)
+    assert cs[len(cs) // 2] > 0.9 and cs[0] > 0.8, cs[:5]
+
+
+def test_resnet50_fused_bf16_step_vs_fp32_no_worse_than_torch_bf16():
+    """ResNet-50 at initialisation is gradient-chaotic under ANY bf16 storage: with torch's own bf16
+    ops the per-tensor gradient cosine against fp32 is ≈ 0.17 median (measured, tools/parity_diag.py).
+    The native fused path must match the loss (1e-2) and be no worse than torch-bf16 on the same step."""
+    _setup_bf16()
+    lg, lc, cos_n = _grad_cosines(50, native=True)
+    _, _, cos_t = _grad_cosines(50, native=False)
+    assert abs(lg - lc) <= 1e-2 * abs(lc), (lg, lc)
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    assert med(cos_n) >= med(cos_t) - 0.05, (med(cos_n), med(cos_t))
+
+
+def test_resnet50_bf16_training_trajectory_tracks_fp32():
+    """Five SGD steps (lr 0.05, momentum 0.9) of ResNet-50 on one fixed batch: the fused native bf16
+    device run and the fp32 host reference run from the same weights must follow the same loss
+    trajectory (within 5 % per step; the full 20-step curves of both, which blow up to ~100 and come
+    back together, are in profiles/r2_train_parity.txt — tools/memorize_check.py)."""
+    _setup_bf16()
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.optim import SGD
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    from bigdl.utils.engine import Engine
+    dev_model = _resnet(10)
+    host_model = copy.deepcopy(dev_model)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(16, 3, 224, 224, generator=g)
+    y = (torch.randint(0, 10, (16,), generator=g) + 1).float()
+    mk = lambda: SGD(learningrate=0.05, momentum=0.9, dampening=0.0)  # noqa: E731
+    b = MiniBatch(x.to(dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last), y.to(dev))
+    opt = LocalOptimizer(dev_model, [b], CrossEntropyCriterion(), mk(), batch_size=16)
+    opt.prepare()
+    dev_curve = [float(opt.train_step(b)) for _ in range(5)]
+    try:
+        Engine.set_device("cpu")
+        Engine.set_compute_dtype("fp32")
+        hb = MiniBatch(x, y)
+        hopt = LocalOptimizer(host_model, [hb], CrossEntropyCriterion(), mk(), batch_size=16)
+        hopt.device, hopt.compute_dtype = torch.device("cpu"), torch.float32
+        hopt.prepare()
+        host_curve = [float(hopt.train_step(hb)) for _ in range(5)]
+    finally:
+        Engine.set_device("cuda:0")
+        Engine.set_compute_dtype("bf16")
+    for d, h in zip(dev_curve, host_curve):
+        assert abs(d - h) <= 0.05 * abs(h), (dev_curve, host_curve)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_local_vs_distri_world1_same_weights_after_3_steps():
+    """Same fused ResNet (depth 18: ResNet-50's gradients at init are chaotic under bf16, so two runs
+    that differ only in atomic summation order diverge; see the test above), same batches: the
+    LocalOptimizer and the DistriOptimizer (RCCL, world 1: reduce-scatter / sharded update /
+    all-gather with the grad-ready bucket hooks live during the fused backward) must agree."""
+    _setup_bf16()
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.optim import SGD
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    from bigdl.utils.engine import Engine
+    m1 = _resnet(10, 18)
+    m2 = copy.deepcopy(m1)
+    w0 = [w.detach().clone() for w in m1.parameters()[0]]
+    g = torch.Generator().manual_seed(5)
+    bs = [MiniBatch(torch.randn(4, 3, 224, 224, generator=g).to(dev).to(torch.bfloat16)
+                    .contiguous(memory_format=torch.channels_last),
+                    (torch.randint(0, 10, (4,), generator=g) + 1).float().to(dev)) for _ in range(3)]
+    mk = lambda: SGD(learningrate=0.05, momentum=0.9, dampening=0.0, nesterov=True, weightdecay=1e-4)  # noqa: E731
+    local = LocalOptimizer(m1, [bs[0]], CrossEntropyCriterion(), mk(), batch_size=4)
+    local.prepare()
+    l_local = [float(local.train_step(b)) for b in bs]
+    torch.cuda.synchronize()
+
+    saved = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    try:
+        Engine.init(device="cuda:0", dist=True)
+        from bigdl.parallel import DistriOptimizer
+        distri = DistriOptimizer(m2, [bs[0]], CrossEntropyCriterion(), mk(), batch_size=4)
+        distri.prepare()
+        l_distri = [float(distri.train_step(b)) for b in bs]
+        distri._wait_all_gathers()
+        torch.cuda.synchronize()
+    finally:
+        Engine.shutdown()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        Engine.init(device="cuda:0")
+    torch.testing.assert_close(torch.tensor(l_distri), torch.tensor(l_local), rtol=2e-2, atol=2e-2)
+    # the weight CHANGE of the two runs must agree (the weights themselves are dominated by the init)
+    # (wgrad's split-K float atomics make both runs non-bit-exact, so compare statistically)
+    cs = sorted(_cos(a.float().cpu() - b0, c.float().cpu() - b0)
+                for a, c, b0 in zip(m1.parameters()[0], m2.parameters()[0], w0)
+                if float((a.float().cpu() - b0).norm()) > 1e-6)
+    assert cs[len(cs) // 2] > 0.99 and cs[0] > 0.9, (cs[0], cs[len(cs) // 2])
