@@ -84,17 +84,27 @@ class BatchNormalization(TensorModule):
         return input
 
     def _sync_stats(self, x):
+        """Cross-rank batch statistics: every rank contributes (mean, M2 = Σ(x − mean)², count) of its
+        shard and the ranks' triples are merged with Chan's parallel formula
+        (M2 = Σ M2_r + Σ n_r (mean_r − mean)²), so the variance never comes from a difference of
+        two large sums (the E[x²] − E[x]² form cancels for activations with |mean| ≫ std)."""
         import torch.distributed as dist
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
+        shape = [1, C] + [1] * (x.dim() - 2)
         xf = x.float()
-        n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
-        s = torch.cat([xf.sum(dims), (xf * xf).sum(dims), n])
-        dist.all_reduce(s, group=self._sync_group)
-        cnt = s[-1]
-        mean = s[:C] / cnt
-        var = s[C:2 * C] / cnt - mean * mean
-        return mean, var.clamp_min(0), cnt
+        n_loc = float(x.numel() // C)
+        mean_l = xf.mean(dims)
+        m2_l = (xf - mean_l.view(shape)).square().sum(dims)
+        mine = torch.stack([mean_l, m2_l, torch.full_like(mean_l, n_loc)])
+        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(self._sync_group))]
+        dist.all_gather(parts, mine, group=self._sync_group)
+        allp = torch.stack(parts)  # [W, 3, C]
+        n_r, mean_r, m2_r = allp[:, 2], allp[:, 0], allp[:, 1]
+        cnt = n_r.sum(0)
+        mean = (n_r * mean_r).sum(0) / cnt
+        m2 = m2_r.sum(0) + (n_r * (mean_r - mean).square()).sum(0)
+        return mean, (m2 / cnt).clamp_min(0), cnt[0]
 
     # --- fusion hooks (set by bigdl.nn.fusion) ---------------------------------------------
     #: conv whose bias was folded into this BN (its output excludes the bias)

@@ -607,8 +607,12 @@ class BaseOptimizer:
             # copy only the restored STATE into the live method objects: the per-run installation
             # (grad_scale = 1/W, folded L2 decay vectors, shard-space lr/decay vectors) lives on
             # those objects and is not part of a checkpoint
-            for k, v in methods.items():
-                cur = self.optim_methods.get(k)
+            pairs = [(self.optim_methods.get(k), v) for k, v in methods.items()]
+            if any(c is None for c, _ in pairs) and len(methods) == len(self.optim_methods):
+                # keys built from default module names differ per process: match by sorted position
+                pairs = [(self.optim_methods[k], methods[kk]) for k, kk in zip(sorted(self.optim_methods),
+                                                                                sorted(methods))]
+            for cur, v in pairs:
                 if cur is None:
                     continue
                 cur.state.clear()

@@ -141,9 +141,13 @@ def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: boo
 
 
 def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False):
+    """Each rank's shard of the optimizer state.  Files are keyed by the method's POSITION in sorted
+    key order, not by its key: a key derived from a default module name is random per process (the
+    reference's ``getName`` postfix), so rank 1 — and a restarted process — could never find a file
+    named after rank 0's key."""
     sfx = _suffix(state, overwrite)
-    for name, m in methods.items():
-        save_optim_method(m, os.path.join(path, f"optimMethod-{name}{sfx}.rank{rank}"), over_write=True)
+    for i, name in enumerate(sorted(methods)):
+        save_optim_method(methods[name], os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}"), over_write=True)
 
 
 def _latest(pattern: str) -> Optional[str]:
@@ -177,7 +181,7 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
     model = load_module(mfile) if mfile else None
     methods = {}
     for f in glob.glob(os.path.join(path, "optimMethod-*")):
-        if ".rank" in f:
+        if ".rank" in f or os.path.basename(f).startswith("optimMethod-#"):
             continue
         base = os.path.basename(f)[len("optimMethod-"):]
         name = base.rsplit(".", 1)[0] if base.rsplit(".", 1)[-1].isdigit() else base
@@ -186,8 +190,10 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
             methods[name] = (os.path.getmtime(f), f)
     loaded = {}
     rank = int(os.environ.get("RANK", "0"))
-    for name, (_, f) in methods.items():
-        shard = f + f".rank{rank}"
+    for i, name in enumerate(sorted(methods)):  # sorted: the position key of save_shard_state
+        f = methods[name][1]
+        sfx = f[len(os.path.join(path, "optimMethod-" + name)):]
+        shard = os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}")
         if ck_sharded and not os.path.exists(shard):
             raise FileNotFoundError(f"sharded checkpoint: missing this rank's optimizer state {shard}")
         loaded[name] = load_optim_method(shard if ck_sharded else f)
