@@ -75,3 +75,9 @@ static inline int bigdl_grid(long long work, int block, int cap = 2048) {
 }
 
 #define BIGDL_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// Deterministic mode (bigdl.deterministic): kernels that reduce with float atomics
+// from several blocks (split-K wgrad, column sums, embedding scatter-add) switch to a single
+// writer per output element, so two runs on the same inputs are bit-identical.  Set from Python
+// through bigdl_set_deterministic(); defined in registry.cpp.
+extern int g_bigdl_deterministic;

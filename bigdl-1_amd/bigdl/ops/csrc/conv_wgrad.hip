@@ -260,6 +260,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   p.tiles_n = (K + TN - 1) / TN;
   p.tiles_k = (p.Kg + TK - 1) / TK;
   const int tiles = p.tiles_n * p.tiles_k;
+  if (g_bigdl_deterministic) splits = 1;  // one block per output tile: no racing atomics
   if (splits <= 0) {
     // splits <= 0: aim for -splits blocks in total (default 512 = two resident blocks per CU), but
     // ≥ 8 k-tiles of pixels per block.  Every split adds its full K×Kg partial with fp32 atomics

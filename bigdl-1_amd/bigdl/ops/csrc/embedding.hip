@@ -51,6 +51,21 @@ __global__ void __launch_bounds__(256) k_embed_bwd(float* __restrict__ gw, const
   for (int c = lane; c < D; c += 64) atomicAdd(dst + c, scale * tof(src[c]));
 }
 
+// Deterministic variant (bigdl.deterministic): one thread owns one column and walks the indices in
+// order, so repeated ids accumulate in a fixed sequence (no atomics; D-way parallel only).
+template <typename I, typename T>
+__global__ void __launch_bounds__(256) k_embed_bwd_det(float* __restrict__ gw, const I* __restrict__ idx,
+                                                       const T* __restrict__ gy, long long n, long long n_index, int D,
+                                                       float scale, int has_pad, float pad) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  for (long long i = 0; i < n; ++i) {
+    if (has_pad && (float)idx[i] == pad) continue;
+    const long long r = row_of(idx, i, n_index);
+    gw[r * D + c] += scale * tof(gy[i * D + c]);
+  }
+}
+
 // itype: 0 = float32 ids, 1 = int64, 2 = int32; dtype: 0 = bf16 table/gradient, 1 = fp32
 template <typename T>
 static void launch_fwd(int itype, dim3 g, hipStream_t s, const void* w, const void* idx, void* out, long long n,
@@ -77,6 +92,19 @@ BIGDL_EXPORT int bigdl_embedding_fwd(const void* w, const void* idx, int itype, 
 template <typename T>
 static void launch_bwd(int itype, dim3 g, hipStream_t s, float* gw, const void* idx, const void* gy, long long n,
                        long long ni, int D, float scale, int has_pad, float pad) {
+  if (g_bigdl_deterministic) {
+    const dim3 gd((unsigned)((D + 255) / 256));
+    if (itype == 0)
+      hipLaunchKernelGGL((k_embed_bwd_det<float, T>), gd, dim3(256), 0, s, gw, (const float*)idx, (const T*)gy, n, ni,
+                         D, scale, has_pad, pad);
+    else if (itype == 1)
+      hipLaunchKernelGGL((k_embed_bwd_det<long long, T>), gd, dim3(256), 0, s, gw, (const long long*)idx,
+                         (const T*)gy, n, ni, D, scale, has_pad, pad);
+    else
+      hipLaunchKernelGGL((k_embed_bwd_det<int, T>), gd, dim3(256), 0, s, gw, (const int*)idx, (const T*)gy, n, ni, D,
+                         scale, has_pad, pad);
+    return;
+  }
   if (itype == 0)
     hipLaunchKernelGGL((k_embed_bwd<float, T>), g, dim3(256), 0, s, gw, (const float*)idx, (const T*)gy, n, ni, D, scale,
                        has_pad, pad);

@@ -300,7 +300,7 @@ BIGDL_EXPORT int bigdl_colsum_bf16(const void* x, long long ld, float* out, int 
   int splits = (512 + gx - 1) / gx;
   const int max_splits = (M + 63) / 64;
   if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
+  if (splits < 1 || g_bigdl_deterministic) splits = 1;
   const int rps = (M + splits - 1) / splits;
   splits = (M + rps - 1) / rps;
   hipLaunchKernelGGL(k_colsum, dim3((unsigned)gx, (unsigned)splits), dim3(256), 0, s, (const bf16_t*)x, ld, out, M, N,

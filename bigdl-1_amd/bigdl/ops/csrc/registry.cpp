@@ -18,4 +18,11 @@ extern "C" __attribute__((visibility("default"))) const char* bigdl_op_name(int 
   return (i >= 0 && i < n) ? kOps[i] : "";
 }
 
+int g_bigdl_deterministic = 0;
+
+extern "C" __attribute__((visibility("default"))) int bigdl_set_deterministic(int on) {
+  g_bigdl_deterministic = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" __attribute__((visibility("default"))) int bigdl_device_sync() { return (int)hipDeviceSynchronize(); }

@@ -40,7 +40,16 @@ def _load():
         _load_error = str(e)
         return None
     _declare(_lib)
+    _push_deterministic(config.get_property("bigdl.deterministic"))
     return _lib
+
+
+def _push_deterministic(on) -> None:
+    if _lib is not None:
+        _lib.bigdl_set_deterministic(1 if on else 0)
+
+
+config.on_change("bigdl.deterministic", _push_deterministic)
 
 
 def _declare(lib):

@@ -49,6 +49,7 @@ _REGISTRY = {
     "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),
+    "bigdl.deterministic": (bool, False, "bit-reproducible kernels: single-writer reductions instead of split-K float atomics (slower wgrad / embedding backward)"),
     "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
     "bigdl.optim.foldRegularizers": (bool, True, "apply pure-L2 layer regularizers inside the fused SGD update"),
@@ -67,6 +68,13 @@ _REGISTRY = {
 }
 
 _overrides: dict = {}
+_listeners: dict = {}
+
+
+def on_change(key: str, fn):
+    """Call ``fn(value)`` whenever ``set_property``/``clear_property`` changes ``key`` (used to push
+    flags such as ``bigdl.deterministic`` into the native library once instead of per call)."""
+    _listeners.setdefault(key, []).append(fn)
 
 
 def _env_name(key: str) -> str:
@@ -99,11 +107,15 @@ def set_property(key: str, value):
     typ = _REGISTRY.get(key, (type(value), None, ""))[0]
     with _lock:
         _overrides[key] = _coerce(typ, value)
+    for fn in _listeners.get(key, ()):
+        fn(get_property(key))
 
 
 def clear_property(key: str):
     with _lock:
         _overrides.pop(key, None)
+    for fn in _listeners.get(key, ()):
+        fn(get_property(key))
 
 
 def describe() -> dict:
