@@ -78,10 +78,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // padding test of a staged row is one bit of a per-row tap-validity mask built once in the prologue.
 // MODE 2 (C4): 4-channel input (the RGB stem padded 3 → 4, not 8: 1.33× instead of 2.67× padded
 // MACs and half the input bytes) — a 16-B chunk holds two consecutive taps, gathered as two 8-B
-// loads with their own padding tests.  MODE 0: any C % 8 == 0.
+// loads with their own padding tests.  MODE 0: any C % 8 == 0.  MODE 3 (POINTWISE): a 1×1
+// filter with no padding (C % BK == 0) — every staged row is in bounds, the k-tile is a plain
+// channel offset, no tap mask at all (the bottleneck 1×1 convs and their dgrads, half the FLOPs).
 template <int BN, int MODE, int BM, int BK>
 __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_conv_fwd(ConvParams p) {
-  constexpr bool FAST = MODE == 1;
+  constexpr bool PW = MODE == 3;
+  constexpr bool FAST = MODE == 1 || PW;
   constexpr int ROWS = BM + BN;
   constexpr int CPK = BK / 8;    // 16-B chunks per staged row
   constexpr int RPS = 256 / CPK; // rows staged per pass of the block
@@ -145,7 +148,9 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
     for (int i = 0; i < A_CHUNKS; ++i) {
       rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.C) + col8 * 8;
       uint64_t msk = 0;
-      if (a_img[i] >= 0) {
+      if (PW) {
+        msk = a_img[i] >= 0 ? 1ull : 0ull;
+      } else if (a_img[i] >= 0) {
         for (int r = 0; r < p.R; ++r) {
           const int h = a_h[i] + r * p.dh;
           if ((unsigned)h >= (unsigned)p.H) continue;
@@ -162,18 +167,32 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // ``live`` = false issues the same loads with out-of-range offsets (they return zeros and touch no
   // memory): keeping every load unconditional keeps hipcc's vmcnt counting exact — a conditionally
   // issued group makes it wait as if the group were absent, draining the pipeline every k-tile.
+  // FAST-path k-tile iterator (wave-uniform, scalar registers): live tiles are requested in
+  // increasing order, so the (tap, channel) position advances by BK per live call instead of two
+  // scalar divisions per k-tile (the round-1 PMC showed ~2.5 SALU per MFMA from them).
+  int it_c0 = 0, it_s = 0, it_tap = 0, it_off = 0;  // channel in tap, s, tap index, element offset
   auto load_tile = [&](int kt, bool live, uint4 (&ra)[A_CHUNKS], uint4 (&rb)[B_CHUNKS]) {
     const uint32_t dead = live ? 0u : 0x80000000u;
     if constexpr (FAST) {
-      kt = live ? kt : 0;
-      const int kb = kt * BK;                 // wave-uniform
-      const int tap = kb / p.C;
-      const int c0 = kb - tap * p.C;
-      const int r = tap / p.S, sx = tap - (tap / p.S) * p.S;
-      const int tap_off = (r * p.dh * p.W + sx * p.dw) * p.C + c0;
+      const int kb = live ? kt * BK : 0;      // wave-uniform
+      const int tap = (PW || !live) ? 0 : it_tap;  // a dead call's offsets are forced out of range below
+      const int tap_off = PW ? kb : it_off + it_c0;
+      if (!PW && live) {
+        it_c0 += BK;
+        if (it_c0 == p.C) {
+          it_c0 = 0;
+          ++it_tap;
+          if (++it_s == p.S) {
+            it_s = 0;
+            it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+          } else {
+            it_off += p.dw * p.C;
+          }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < A_CHUNKS; ++i) {
-        const bool ok = (vmask[i] >> tap) & 1ull;
+        const bool ok = PW ? (vmask[i] != 0) : ((vmask[i] >> tap) & 1ull);
         const uint32_t off = (ok ? (uint32_t)(rbase[i] + tap_off) * 2u : OOB) | dead;
         ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
       }
@@ -312,6 +331,41 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   constexpr int LDR = BN;
   constexpr int UMASK = (BN / 4 - 1) & 31;
   bf16_t* et = &lds[0];
+  // BN statistics straight from the fp32 accumulators (the plain conv → BN case: no bias, residual,
+  // ReLU or BN-backward prologue): each lane sums its TM pixels per channel, two DPP row rotations
+  // fold the 16 pixel lanes of a row to 4, and lanes fr < 4 park [2 wave_m × 4] partials per channel
+  // in LDS behind the staging tile — ~2 VALU per output instead of unpack + 4 per output in the
+  // store loop (round-2 PMC: the expand 1×1 convs issued 8.7 VALU per MFMA, mostly here).
+  constexpr int SRED = 8;
+  const bool rstats = (BM == SBM) && p.stats && !p.res && !p.relu && !p.bnx && !p.bias && !p.scatter;
+  float* red8 = reinterpret_cast<float*>(&et[BM * LDR]);  // [2][SRED][BN]: Σ then Σ²
+  if (rstats) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = acc[i][j][e];
+          s4[e] += a;
+          q4[e] = fmaf(a, a, q4[e]);
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x128, 0xF, 0xF, false));
+        q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x128, 0xF, 0xF, false));
+        s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x124, 0xF, 0xF, false));
+        q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x124, 0xF, 0xF, false));
+      }
+      if (fr < 4) {
+        const int nl = wave_n * (BN / 2) + i * 16 + fq * 4;
+        const int g = wave_m * 4 + fr;
+        *reinterpret_cast<float4*>(&red8[g * BN + nl]) = make_float4(s4[0], s4[1], s4[2], s4[3]);
+        *reinterpret_cast<float4*>(&red8[(SRED + g) * BN + nl]) = make_float4(q4[0], q4[1], q4[2], q4[3]);
+      }
+    }
+  }
   auto rd_chunk = [&](int r, int c) -> uint4 {
     const int sw = r & UMASK;
     uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + ((c ^ (sw >> 1)) << 3)]);
@@ -422,7 +476,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
         u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
       *reinterpret_cast<uint4*>(p.y + yoff) = u;
-      if (p.stats) {
+      if (p.stats && !rstats) {
         // statistics of the values as stored (bf16-rounded), which is what the BN reads
         const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -448,7 +502,16 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       }
     }
   }
-  if (p.stats) {
+  if (rstats) {
+    // the staging barrier above also ordered the partial writes: fold the SRED partials
+    if (tid < 2 * BN) {
+      const int which = tid / BN, c = tid - which * BN;
+      float a = 0.f;
+#pragma unroll
+      for (int g = 0; g < SRED; ++g) a += red8[(which * SRED + g) * BN + c];
+      if (n0 + c < p.K && tm < p.tiles_m) p.stats[((size_t)which * p.tiles_m + tm) * p.K + n0 + c] = a;
+    }
+  } else if (p.stats) {
     // reduce the RPP row groups of each channel chunk through LDS (after the tile reads retire)
     float* red = reinterpret_cast<float*>(&et[BM * LDR]);  // [RPP][BN] Σ, then [RPP][BN] Σ²
     // 16-B stores: lanes (consecutive cc) land 32 B apart — conflict-free, where 8 scalar stores
@@ -488,7 +551,9 @@ static int conv_env_override(const char* name, int a, int b) {
 
 template <int BN, int BM, int BK>
 static void launch_fwd(int mode, dim3 grid, hipStream_t s, const ConvParams& p) {
-  if (mode == 1)
+  if (mode == 3)
+    hipLaunchKernelGGL((k_conv_fwd<BN, 3, BM, BK>), grid, dim3(256), 0, s, p);
+  else if (mode == 1)
     hipLaunchKernelGGL((k_conv_fwd<BN, 1, BM, BK>), grid, dim3(256), 0, s, p);
   else if (mode == 2)
     hipLaunchKernelGGL((k_conv_fwd<BN, 2, BM, BK>), grid, dim3(256), 0, s, p);
@@ -556,7 +621,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const int bk_env = conv_env_override("BIGDL_CONV_BK", 32, 64);
   const int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
   const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
-  const int mode = c4 ? 2 : ((C % bk == 0) && R * S <= 64 ? 1 : 0);
+  const bool fast = (C % bk == 0) && R * S <= 64;
+  const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
   long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles);

@@ -203,9 +203,18 @@ class BaseOptimizer:
         return self.prepareInput()
 
     def setDropModuleProperty(self, drop_percentage, max_drop_percentage, batchsize=100, warmup_iteration=200):
-        """Straggler dropping (P5).  One GPU per rank rarely straggles; the knob is accepted and
-        a per-rank step-time watchdog logs slow ranks instead of cancelling work."""
-        self.drop_percentage = drop_percentage
+        """Straggler handling (P5, ``DistriOptimizer.scala:246-278,421-449``).  With
+        ``drop_percentage > 0`` every rank times its iterations with HIP events and every
+        ``batchsize`` iterations (after ``warmup_iteration``) the ranks all-gather their step times:
+        the threshold is ``Util.kthLargest`` at k = drop_percentage · batchsize · world and ranks whose
+        mean step time exceeds ``bigdl.straggler.factor`` × the median are logged
+        (:class:`bigdl.utils.tracing.StepTracer`).  A synchronous RCCL reduce-scatter cannot discard a
+        late rank's gradient the way the reference cancels late replica threads, so slow ranks are
+        detected and reported, not dropped."""
+        self.drop_percentage = float(drop_percentage)
+        self.max_drop_percentage = float(max_drop_percentage)
+        self._straggler_window = int(batchsize)
+        self._straggler_warmup = int(warmup_iteration)
         return self
 
     def disableGradientClipping(self):
@@ -235,8 +244,20 @@ class BaseOptimizer:
         return self
 
     # ------------------------------------------------------------------------------ setup
+    def _make_tracer(self):
+        from ..utils.tracing import StepTracer
+        self.tracer = StepTracer(self.metrics, Engine.rank(), Engine.world_size())
+        if self.drop_percentage > 0:
+            # the straggler monitor needs device-side step times
+            self.tracer.window = getattr(self, "_straggler_window", self.tracer.window)
+            self.tracer.device = torch.cuda.is_available() and self.device.type == "cuda"
+            self.tracer.host_timers = True
+            self.tracer.enabled = True
+        return self.tracer
+
     def _setup_model(self):
         from ..nn.fusion import fuse
+        self._make_tracer()
         m = self.model
         m.to(self.device)
         m.training()
@@ -316,12 +337,13 @@ class BaseOptimizer:
     def _sync_and_update(self, loss_t: torch.Tensor, batch_size: int):
         """Gradient aggregation + clipping + optimizer update (local: no aggregation)."""
         self._clip(self.flat.grad, self.flat.grad)
-        for name, meth in self.optim_methods.items():
-            off, n = self._method_slices[name]
-            w = self.flat.weight[off:off + n]
-            g = self.flat.grad[off:off + n]
-            meth.shadow = self.flat.shadow[off:off + n] if self.flat.shadow is not None else None
-            meth.optimize(lambda _x, g=g: (loss_t, g), w)
+        with self.tracer.phase("compute weight"):
+            for name, meth in self.optim_methods.items():
+                off, n = self._method_slices[name]
+                w = self.flat.weight[off:off + n]
+                g = self.flat.grad[off:off + n]
+                meth.shadow = self.flat.shadow[off:off + n] if self.flat.shadow is not None else None
+                meth.optimize(lambda _x, g=g: (loss_t, g), w)
         if self.flat.shadow is not None:
             self.flat.mark_shadow_fresh()
 
@@ -388,6 +410,8 @@ class BaseOptimizer:
     def _finish(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize()
+        if getattr(self, "tracer", None) is not None:
+            self.tracer.flush()
         self.metrics.resolve()
 
     def _batches(self):
@@ -442,6 +466,7 @@ class BaseOptimizer:
             for meth in self.optim_methods.values():
                 meth.state["epoch"] = self.state["epoch"]
                 meth.state["neval"] = self.state["neval"]
+            self._observe_straggler(it, dt)
             self._save_summary(global_bs, dt)
             self._maybe_validate()
             self._maybe_checkpoint()
@@ -467,20 +492,40 @@ class BaseOptimizer:
 
     def train_step(self, batch: MiniBatch) -> torch.Tensor:
         """One synchronous-SGD iteration on ``batch``; returns the (rank-averaged) loss as a
-        device scalar without synchronising the host."""
+        device scalar without synchronising the host.  Phases (roctx ranges / HIP-event timers /
+        JSON metrics per ``bigdl.roctx`` / ``bigdl.metrics.*``): forward, backward, then the
+        optimizer's own (local: "compute weight"; distributed: "aggregate gradient",
+        "compute weight", "send weights")."""
         m, crit = self.model, self.criterion
+        tr = getattr(self, "tracer", None) or self._make_tracer()
         x, y = batch.getInput(), batch.getTarget()
         self._before_forward()
         m.zeroGradParameters()
-        out = m.forward(x)
-        loss = crit.forward(out, y)
-        gout = crit.backward(out, y)
-        self._before_backward()
-        m.backward(x, gout)
+        with tr.phase("forward"):
+            out = m.forward(x)
+            loss = crit.forward(out, y)
+        with tr.phase("backward"):
+            gout = crit.backward(out, y)
+            self._before_backward()
+            m.backward(x, gout)
         loss_t = loss if isinstance(loss, torch.Tensor) else torch.tensor(float(loss))
         loss_t = self._reduce_scalar(loss_t.detach().float().reshape(()))
         self._sync_and_update(loss_t, batch.size())
+        if tr.enabled:
+            tr.end_iteration(self.state["neval"], {"epoch": self.state["epoch"], "batch": batch.size(),
+                                                   "global_batch": batch.size() * Engine.world_size(),
+                                                   "loss_prev": self.state.get("Loss")})
         return loss_t
+
+    def _observe_straggler(self, it, host_dt):
+        if self.drop_percentage <= 0 or it < getattr(self, "_straggler_warmup", 0):
+            return
+        tr = self.tracer
+        ph = tr.last_phases
+        dt = sum(ph.values()) if ph else host_dt
+        from ..utils.tracing import allgather_floats
+        tr.observe_step_time(it, dt, self.drop_percentage,
+                             allgather_floats if Engine.world_size() > 1 else None)
 
     def _needs_loss(self) -> bool:
         from .trigger import MinLoss, TriggerAnd, TriggerOr

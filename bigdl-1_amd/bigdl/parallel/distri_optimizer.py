@@ -44,7 +44,7 @@ log = get_logger("bigdl.parallel")
 
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "slo", "shi", "pending", "expected", "rs_work", "ag_work", "ready",
-                 "modules", "needs_shadow")
+                 "modules", "needs_shadow", "early", "rs_keep")
 
     def __init__(self, idx, lo, hi, slo, shi):
         self.idx, self.lo, self.hi, self.slo, self.shi = idx, lo, hi, slo, shi
@@ -55,6 +55,8 @@ class _Bucket:
         self.ready = False
         self.modules = []
         self.needs_shadow = False
+        self.early = False
+        self.rs_keep = None
 
 
 class DistriOptimizer(BaseOptimizer):
@@ -77,10 +79,13 @@ class DistriOptimizer(BaseOptimizer):
         self._hook_counts: Dict[int, int] = {}
         self._overlap_active = False
         self._first_iter = True
+        self._early = False
+        self._side = None
 
     # ------------------------------------------------------------------------------ setup
     def _setup_model(self):
         from ..nn.fusion import fuse
+        self._make_tracer()
         m = self.model
         m.to(self.device)
         m.training()
@@ -170,6 +175,10 @@ class DistriOptimizer(BaseOptimizer):
         for b in self.buckets:
             b.expected = len(b.modules)
         self._install_hooks()
+        self._side = None
+        if (self.sharded and dev.type == "cuda" and config.get_property("bigdl.comm.earlyUpdate")):
+            prio = int(config.get_property("bigdl.comm.streamPriority"))
+            self._side = torch.cuda.Stream(device=dev, priority=prio)
         log.info(f"DistriOptimizer: world={W} params={self.flat.numel} buckets={len(self.buckets)} "
                  f"mode={'sharded' if self.sharded else 'replicated'} comm={self.comm_dtype} overlap={self.overlap}")
 
@@ -193,12 +202,28 @@ class DistriOptimizer(BaseOptimizer):
             b.pending -= 1
             if b.pending == 0:
                 self._launch_reduce(b)
+                if self._early:
+                    self._early_update(b)
+
+    def _early_update(self, b: _Bucket):
+        """Shard update + all-gather of bucket ``b`` on the comm-side stream, queued behind its
+        reduce-scatter while backward continues on the compute stream (the reference's lazy
+        per-block ``updateParameter``, ParallelOptimizer.scala:404-470, without the wait)."""
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream())  # the bucket's gradients / wire copy
+        b.rs_keep = b.rs_work
+        with torch.cuda.stream(side):
+            self._finish_reduce(b)
+            self._update_bucket(b)
+            self._launch_gather(b)
+        b.early = True
 
     def _on_pre_forward(self, mod):
         for bi in self._mod_buckets.get(id(mod), ()):
             b = self.buckets[bi]
             if b.ag_work is not None:
-                b.ag_work.wait()
+                with self.tracer.phase("send weights"):
+                    b.ag_work.wait()
                 b.ag_work = None
                 self._after_gather(b)
 
@@ -221,7 +246,8 @@ class DistriOptimizer(BaseOptimizer):
     def _finish_reduce(self, b: _Bucket):
         if b.rs_work is None:
             return
-        b.rs_work.wait()
+        with self.tracer.phase("aggregate gradient"):
+            b.rs_work.wait()
         b.rs_work = None
         if self.sharded and self.grad_wire is not None:
             self.shard_g[b.slo:b.shi].copy_(self.shard_g_wire[b.slo:b.shi])
@@ -257,7 +283,16 @@ class DistriOptimizer(BaseOptimizer):
     def _before_forward(self):
         for b in self.buckets:
             b.pending = b.expected
+            b.early = False
+            b.rs_keep = None
         self._overlap_active = self.overlap and not self._first_iter and self._overlap_ok
+        # early (in-backward) shard updates: sharded, on a GPU, no clipping (which needs the global
+        # gradient norm before any update)
+        self._early = (self._overlap_active and self._side is not None
+                       and self.constant_clip is None and self.l2_clip is None)
+        if self._early:
+            for meth in self.optim_methods.values():
+                meth.begin_iteration(self.shard_w)
         self._hook_counts = {}
 
     @property
@@ -282,7 +317,7 @@ class DistriOptimizer(BaseOptimizer):
                 log.info("gradient/backward overlap disabled: shared or directly-driven parameter modules")
         # launch any bucket not launched during backward
         for b in reversed(self.buckets):
-            if b.rs_work is None:
+            if b.rs_work is None and not b.early:
                 self._launch_reduce(b)
         if not self.sharded:
             for b in self.buckets:
@@ -301,24 +336,33 @@ class DistriOptimizer(BaseOptimizer):
             for meth in self.optim_methods.values():
                 meth.grad_scale = 1.0
             self._clip(self.shard_g, self.shard_g)
-        for meth in self.optim_methods.values():
-            meth.begin_iteration(self.shard_w)
-        done = set()
+        if not self._early:
+            for meth in self.optim_methods.values():
+                meth.begin_iteration(self.shard_w)
+        else:
+            # buckets updated during backward: the compute stream must not touch their gradients /
+            # weights (next zeroGrad, forward) before the comm-side stream has consumed them
+            torch.cuda.current_stream().wait_stream(self._side)
         for b in self._update_order():
+            if b.early:
+                continue
             self._finish_reduce(b)
+            self._update_bucket(b)
+            self._launch_gather(b)
+        if self.constant_clip is not None or self.l2_clip is not None:
+            for meth in self.optim_methods.values():
+                meth.grad_scale = 1.0 / self.world
+        self.flat.mark_shadow_fresh()
+        self._first_iter = False
+
+    def _update_bucket(self, b: _Bucket):
+        with self.tracer.phase("compute weight"):
             for name, meth in self.optim_methods.items():
                 for (bb, lo, hi) in self._method_shard_ranges[name]:
                     if bb is b:
                         sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
                                                           self.comm_dtype.startswith("bf16")) else None
                         meth.apply_update(self.shard_w, self.shard_g, lo, hi, shadow=sh)
-            self._launch_gather(b)
-            done.add(b.idx)
-        if self.constant_clip is not None or self.l2_clip is not None:
-            for meth in self.optim_methods.values():
-                meth.grad_scale = 1.0 / self.world
-        self.flat.mark_shadow_fresh()
-        self._first_iter = False
 
     def _update_order(self):
         """Buckets in the order their shard update + all-gather is issued: readiness order (the
@@ -417,6 +461,15 @@ class ParallelOptimizer(DistriOptimizer):
         self._bucket_prio = {}
         for b in self.buckets:
             self._bucket_prio[b.idx] = max((prio.get(m.get_name(), 0) for m in b.modules), default=0)
+
+    def _update_bucket(self, b: _Bucket):
+        with self.tracer.phase("compute weight"):
+            for name, meth in self.optim_methods.items():
+                for (bb, lo, hi) in self._method_shard_ranges[name]:
+                    if bb is b:
+                        sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
+                                                          self.comm_dtype.startswith("bf16")) else None
+                        meth.apply_update(self.shard_w, self.shard_g, lo, hi, shadow=sh)
 
     def _update_order(self):
         return sorted(self.buckets, key=lambda b: (-self._bucket_prio.get(b.idx, 0), -b.idx))

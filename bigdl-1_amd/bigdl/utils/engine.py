@@ -84,6 +84,7 @@ class Engine:
                     kw = {"timeout": datetime.timedelta(seconds=float(config.get_property("bigdl.comm.timeout")))}
                     if be == "nccl":
                         kw["device_id"] = _S.device
+                        apply_comm_env()
                     tdist.init_process_group(backend=be, **kw)
                     _S.process_group_owned = True
                 _S.rank = tdist.get_rank()
@@ -186,6 +187,19 @@ class Engine:
     def reset():
         Engine.shutdown()
         _S.__init__()
+
+
+def apply_comm_env(env=None) -> dict:
+    """RCCL knobs that must be in the environment before the first communicator is created
+    (SURVEY §5.8): ``bigdl.comm.channels`` caps the channels — and with them the CUs — a collective
+    takes from compute (``NCCL_MIN_NCHANNELS`` / ``NCCL_MAX_NCHANNELS``).  Values the user already
+    exported win.  ``env`` defaults to ``os.environ`` (the launcher passes the child env)."""
+    env = os.environ if env is None else env
+    ch = int(config.get_property("bigdl.comm.channels") or 0)
+    if ch > 0:
+        env.setdefault("NCCL_MIN_NCHANNELS", str(ch))
+        env.setdefault("NCCL_MAX_NCHANNELS", str(ch))
+    return env
 
 
 def init_engine(*args, **kwargs):

@@ -12,7 +12,7 @@ def main():
     ap.add_argument("--shape", default="256,256,3,1,14")  # C,K,R,stride,H
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--op", default="fwd", choices=["fwd", "fwdstats", "dgrad", "wgrad"])
     a = ap.parse_args()
     import torch
     from bigdl.ops import native_ops as NO
@@ -26,6 +26,8 @@ def main():
     for _ in range(a.iters):
         if a.op == "fwd":
             NO.conv2d_forward(x, w, None, (s, s), (pad, pad))
+        elif a.op == "fwdstats":
+            NO.conv2d_forward_stats(x, w, None, (s, s), (pad, pad))
         elif a.op == "dgrad":
             NO.conv2d_backward(gy, x, w, (s, s), (pad, pad), need_input=True)
         else:

@@ -23,9 +23,13 @@ for (shape, k), cnt in sorted(res.items()):
     for c in sorted(m):
         print(f"   {c:28s} {m[c]:16.1f}")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
-        # MFMA busy is summed over SIMDs (256 CUs x 4)
-        print(f"   MFMA util ≈ {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] * 1024):.3f}"
-              f"  (busy / (gui_active x 1024 SIMDs))")
+        # SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs (16 per 16x16x32 MFMA);
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md 'DVFS give-back'), so the
+        # kernel's wall cycles are GUI/8 and utilisation = busy / (GUI/8 x 1024) — this reconciles
+        # with the measured TF/s ÷ 2.5 PF (the round-1 formula omitted the /8)
+        wall = m["GRBM_GUI_ACTIVE"] / 8
+        print(f"   MFMA util = {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (wall * 1024):.3f}"
+              f"  (busy / (GUI_ACTIVE/8 x 1024 SIMDs)); wall cycles {wall:.0f}")
     if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
         print(f"   VALU per MFMA = {m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f}")
     if "TCC_HIT_sum" in m:
