@@ -522,7 +522,9 @@ class BaseOptimizer:
             return
         tr = self.tracer
         ph = tr.last_phases
-        dt = sum(ph.values()) if ph else host_dt
+        # the rank's own computing time (forward + backward), like the reference's per-model
+        # moduleTimeList: a synchronous collective makes every rank's wall time the slowest's
+        dt = (ph.get("forward", 0.0) + ph.get("backward", 0.0)) if ph else host_dt
         from ..utils.tracing import allgather_floats
         tr.observe_step_time(it, dt, self.drop_percentage,
                              allgather_floats if Engine.world_size() > 1 else None)

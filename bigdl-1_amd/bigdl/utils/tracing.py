@@ -15,7 +15,8 @@ gradient time", "compute weight average", "send weights average" — ``DL/optim/
 * the **straggler monitor** (P5, ``DistriOptimizer.scala:246-278,421-449``): every
   ``bigdl.straggler.window`` iterations the ranks all-gather their per-iteration step times, the
   threshold is ``Util.kthLargest`` of that list at k = dropPercentage · window · world (the
-  reference's formula), and ranks whose mean step time exceeds ``factor`` × the median are logged
+  reference's formula), and ranks whose mean computing time (forward + backward) exceeds ``factor`` ×
+  the lower median are logged
   as slow.  Synchronous RCCL collectives cannot drop a late rank's gradient the way the reference's
   thread pool cancels a late model replica (the reduce-scatter waits for every rank), so on MI355X
   the mechanism detects and reports stragglers rather than discarding their work.
@@ -214,7 +215,7 @@ class StepTracer:
             us = [int(t * 1e6) for t in flat]
             self.threshold = kthLargest(us, 0, len(us) - 1, min(k, len(us))) / 1e6
         means = [sum(r) / max(1, len(r)) for r in per_rank]
-        med = sorted(means)[len(means) // 2]
+        med = sorted(means)[(len(means) - 1) // 2]  # lower median: with two ranks, the faster one
         self.slow_ranks = [i for i, m in enumerate(means) if med > 0 and m > self.factor * med]
         self.metrics.set("straggler threshold", self.threshold or 0.0)
         self.metrics.set("slow ranks", len(self.slow_ranks))
