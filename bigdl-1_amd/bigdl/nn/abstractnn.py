@@ -461,7 +461,9 @@ class AbstractModule:
     def compute_dtype_for(self, t: torch.Tensor) -> torch.dtype:
         if t.device.type == "cuda":
             return Engine.compute_dtype()
-        return torch.float32
+        # host: fp32 like the reference's Float models; a module cast to float64 (the gradient
+        # checker, nn/gradient_checker.py) keeps computing in float64
+        return torch.float64 if t.dtype == torch.float64 else torch.float32
 
     # ---- device ----------------------------------------------------------------------------------
     def _tensors_attrs(self):
@@ -922,7 +924,7 @@ class AbstractCriterion:
         input = to_torch(input)
         target = to_torch(target)
         out = self.updateOutput(input, target)
-        if isinstance(out, torch.Tensor):
+        if isinstance(out, torch.Tensor) and out.dtype != torch.float64:
             out = out.float()
         self.output = out
         if numpy_out:

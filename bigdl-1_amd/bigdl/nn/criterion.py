@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..utils.table import Table
 from .abstractnn import AbstractCriterion, AutogradCriterion
+from ..utils import acc_float
 
 
 def _targets_1b(target):
@@ -35,14 +36,14 @@ class ClassNLLCriterion(AbstractCriterion):
         return self.weights
 
     def updateOutput(self, input, target):
-        lp = input if self.logProbAsInput else torch.log(input.float().clamp_min(1e-8))
+        lp = input if self.logProbAsInput else torch.log(acc_float(input).clamp_min(1e-8))
         return ops.class_nll_forward(lp, target, self._w(input), self.sizeAverage, self.paddingValue)
 
     def updateGradInput(self, input, target):
-        lp = input if self.logProbAsInput else torch.log(input.float().clamp_min(1e-8))
+        lp = input if self.logProbAsInput else torch.log(acc_float(input).clamp_min(1e-8))
         g = ops.class_nll_backward(lp, target, self._w(input), self.sizeAverage, self.paddingValue)
         if not self.logProbAsInput:
-            g = g / input.float().clamp_min(1e-8)
+            g = g / acc_float(input).clamp_min(1e-8)
         return g
 
 
@@ -76,12 +77,12 @@ class MSECriterion(AbstractCriterion):
         super().__init__(size_average)
 
     def updateOutput(self, input, target):
-        d = input.float() - target.float().reshape(input.shape)
+        d = acc_float(input) - acc_float(target).reshape(input.shape)
         s = (d * d).sum()
         return s / input.numel() if self.sizeAverage else s
 
     def updateGradInput(self, input, target):
-        d = input.float() - target.float().reshape(input.shape)
+        d = acc_float(input) - acc_float(target).reshape(input.shape)
         g = 2 * d / (input.numel() if self.sizeAverage else 1)
         return g.to(input.dtype)
 
@@ -91,11 +92,11 @@ class AbsCriterion(AbstractCriterion):
         super().__init__(size_average)
 
     def updateOutput(self, input, target):
-        s = (input.float() - target.float().reshape(input.shape)).abs().sum()
+        s = (acc_float(input) - acc_float(target).reshape(input.shape)).abs().sum()
         return s / input.numel() if self.sizeAverage else s
 
     def updateGradInput(self, input, target):
-        g = torch.sign(input.float() - target.float().reshape(input.shape))
+        g = torch.sign(acc_float(input) - acc_float(target).reshape(input.shape))
         return (g / (input.numel() if self.sizeAverage else 1)).to(input.dtype)
 
 
@@ -107,7 +108,7 @@ class BCECriterion(AutogradCriterion):
     def _loss(self, x, t):
         w = None if self.weights is None else self.weights.to(x.device)
         eps = 1e-12
-        t = t.float().reshape(x.shape)
+        t = acc_float(t).reshape(x.shape)
         l = -(t * torch.log(x + eps) + (1 - t) * torch.log(1 - x + eps))
         if w is not None:
             l = l * w
@@ -119,7 +120,7 @@ class SmoothL1Criterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        return F.smooth_l1_loss(x.float(), t.float().reshape(x.shape), reduction="mean" if self.sizeAverage else "sum")
+        return F.smooth_l1_loss(acc_float(x), acc_float(t).reshape(x.shape), reduction="mean" if self.sizeAverage else "sum")
 
 
 class SmoothL1CriterionWithWeights(AutogradCriterion):
@@ -132,13 +133,13 @@ class SmoothL1CriterionWithWeights(AutogradCriterion):
     def _loss(self, x, target):
         t, inw, outw = (target[1], target[2], target[3]) if isinstance(target, Table) else (target, None, None)
         s2 = self.sigma * self.sigma
-        d = x.float() - t.float()
+        d = acc_float(x) - acc_float(t)
         if inw is not None:
-            d = d * inw.float()
+            d = d * acc_float(inw)
         ad = d.abs()
         l = torch.where(ad < 1.0 / s2, 0.5 * d * d * s2, ad - 0.5 / s2)
         if outw is not None:
-            l = l * outw.float()
+            l = l * acc_float(outw)
         s = l.sum()
         return s / self.num if self.num > 0 else s
 
@@ -149,7 +150,7 @@ class MarginCriterion(AutogradCriterion):
         self.margin, self.squared = margin, squared
 
     def _loss(self, x, t):
-        l = torch.clamp(self.margin - x.float() * t.float().reshape(x.shape), min=0)
+        l = torch.clamp(self.margin - acc_float(x) * acc_float(t).reshape(x.shape), min=0)
         if self.squared:
             l = l * l
         return l.sum() / x.numel() if self.sizeAverage else l.sum()
@@ -162,7 +163,7 @@ class MarginRankingCriterion(AutogradCriterion):
 
     def _loss(self, x, t):
         y = t[1] if isinstance(t, Table) else t
-        l = torch.clamp(-y.float() * (x[1].float() - x[2].float()) + self.margin, min=0)
+        l = torch.clamp(-acc_float(y) * (acc_float(x[1]) - acc_float(x[2])) + self.margin, min=0)
         return l.mean() if self.sizeAverage else l.sum()
 
 
@@ -172,8 +173,8 @@ class HingeEmbeddingCriterion(AutogradCriterion):
         self.margin = margin
 
     def _loss(self, x, t):
-        t = t.float().reshape(x.shape)
-        l = torch.where(t > 0, x.float(), torch.clamp(self.margin - x.float(), min=0))
+        t = acc_float(t).reshape(x.shape)
+        l = torch.where(t > 0, acc_float(x), torch.clamp(self.margin - acc_float(x), min=0))
         return l.sum() / x.numel() if self.sizeAverage else l.sum()
 
 
@@ -183,7 +184,7 @@ class L1HingeEmbeddingCriterion(AutogradCriterion):
         self.margin = margin
 
     def _loss(self, x, t):
-        d = (x[1].float() - x[2].float()).abs().sum()
+        d = (acc_float(x[1]) - acc_float(x[2])).abs().sum()
         y = float(t.reshape(-1)[0]) if isinstance(t, torch.Tensor) else float(t)
         return d if y > 0 else torch.clamp(self.margin - d, min=0)
 
@@ -195,7 +196,7 @@ class CosineEmbeddingCriterion(AutogradCriterion):
 
     def _loss(self, x, t):
         y = t[1] if isinstance(t, Table) else t
-        return F.cosine_embedding_loss(x[1].float(), x[2].float(), y.float().reshape(-1), self.margin,
+        return F.cosine_embedding_loss(acc_float(x[1]), acc_float(x[2]), acc_float(y).reshape(-1), self.margin,
                                        reduction="mean" if self.sizeAverage else "sum")
 
 
@@ -204,7 +205,7 @@ class CosineDistanceCriterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        l = 1 - F.cosine_similarity(x.float(), t.float().reshape(x.shape), dim=-1)
+        l = 1 - F.cosine_similarity(acc_float(x), acc_float(t).reshape(x.shape), dim=-1)
         return l.mean() if self.sizeAverage else l.sum()
 
 
@@ -215,8 +216,8 @@ class DistKLDivCriterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        t = t.float().reshape(x.shape)
-        l = torch.where(t > 0, t * (torch.log(t.clamp_min(1e-30)) - x.float()), torch.zeros_like(t))
+        t = acc_float(t).reshape(x.shape)
+        l = torch.where(t > 0, t * (torch.log(t.clamp_min(1e-30)) - acc_float(x)), torch.zeros_like(t))
         return l.sum() / x.numel() if self.sizeAverage else l.sum()
 
 
@@ -227,9 +228,9 @@ class CategoricalCrossEntropy(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        p = x.float() / x.float().sum(-1, keepdim=True)
+        p = acc_float(x) / acc_float(x).sum(-1, keepdim=True)
         p = p.clamp(1e-7, 1 - 1e-7)
-        return -(t.float().reshape(p.shape) * torch.log(p)).sum(-1).mean()
+        return -(acc_float(t).reshape(p.shape) * torch.log(p)).sum(-1).mean()
 
 
 class ClassSimplexCriterion(AutogradCriterion):
@@ -253,7 +254,7 @@ class ClassSimplexCriterion(AutogradCriterion):
 
     def _loss(self, x, t):
         s = self.simplex.to(x.device)[t.long().reshape(-1) - 1][:, :x.shape[-1]]
-        d = x.float() - s
+        d = acc_float(x) - s
         return (d * d).sum() / x.numel()
 
 
@@ -262,7 +263,7 @@ class MultiLabelMarginCriterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        xx = x.float() if x.dim() == 2 else x.float().unsqueeze(0)
+        xx = acc_float(x) if x.dim() == 2 else acc_float(x).unsqueeze(0)
         tt = (t.long() if t.dim() == 2 else t.long().unsqueeze(0)) - 1  # 1-based, 0 terminates → -1
         return F.multilabel_margin_loss(xx, tt, reduction="mean" if self.sizeAverage else "sum")
 
@@ -274,7 +275,7 @@ class MultiLabelSoftMarginCriterion(AutogradCriterion):
 
     def _loss(self, x, t):
         w = None if self.weights is None else self.weights.to(x.device)
-        l = F.binary_cross_entropy_with_logits(x.float(), t.float().reshape(x.shape), weight=w, reduction="none")
+        l = F.binary_cross_entropy_with_logits(acc_float(x), acc_float(t).reshape(x.shape), weight=w, reduction="none")
         l = l.mean(-1)
         return l.mean() if self.sizeAverage else l.sum()
 
@@ -286,7 +287,7 @@ class MultiMarginCriterion(AutogradCriterion):
         self.weights = None if weights is None else torch.as_tensor(weights, dtype=torch.float32)
 
     def _loss(self, x, t):
-        xx = x.float() if x.dim() == 2 else x.float().unsqueeze(0)
+        xx = acc_float(x) if x.dim() == 2 else acc_float(x).unsqueeze(0)
         w = None if self.weights is None else self.weights.to(x.device)
         return F.multi_margin_loss(xx, t.long().reshape(-1) - 1, self.p, self.margin, w,
                                    reduction="mean" if self.sizeAverage else "sum")
@@ -297,7 +298,7 @@ class SoftMarginCriterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        return F.soft_margin_loss(x.float(), t.float().reshape(x.shape), reduction="mean" if self.sizeAverage else "sum")
+        return F.soft_margin_loss(acc_float(x), acc_float(t).reshape(x.shape), reduction="mean" if self.sizeAverage else "sum")
 
 
 class DiceCoefficientCriterion(AutogradCriterion):
@@ -306,8 +307,8 @@ class DiceCoefficientCriterion(AutogradCriterion):
         self.epsilon = epsilon
 
     def _loss(self, x, t):
-        xx = x.float().reshape(x.shape[0], -1) if x.dim() > 1 else x.float().unsqueeze(0)
-        tt = t.float().reshape(xx.shape)
+        xx = acc_float(x).reshape(x.shape[0], -1) if x.dim() > 1 else acc_float(x).unsqueeze(0)
+        tt = acc_float(t).reshape(xx.shape)
         inter = (xx * tt).sum(1)
         l = 1 - (2 * inter + self.epsilon) / (xx.sum(1) + tt.sum(1) + self.epsilon)
         return l.mean() if self.sizeAverage else l.sum()
@@ -318,7 +319,7 @@ class L1Cost(AutogradCriterion):
         super().__init__(False)
 
     def _loss(self, x, t):
-        return x.float().abs().sum()
+        return acc_float(x).abs().sum()
 
 
 class CosineProximityCriterion(AutogradCriterion):
@@ -326,8 +327,8 @@ class CosineProximityCriterion(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        xn = F.normalize(x.float(), dim=-1)
-        tn = F.normalize(t.float().reshape(x.shape), dim=-1)
+        xn = F.normalize(acc_float(x), dim=-1)
+        tn = F.normalize(acc_float(t).reshape(x.shape), dim=-1)
         return -(xn * tn).sum(-1).mean()
 
 
@@ -336,8 +337,8 @@ class MeanAbsolutePercentageCriterion(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        t = t.float().reshape(x.shape)
-        return 100 * ((t - x.float()).abs() / t.abs().clamp_min(1e-7)).mean()
+        t = acc_float(t).reshape(x.shape)
+        return 100 * ((t - acc_float(x)).abs() / t.abs().clamp_min(1e-7)).mean()
 
 
 class MeanSquaredLogarithmicCriterion(AutogradCriterion):
@@ -345,8 +346,8 @@ class MeanSquaredLogarithmicCriterion(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        t = t.float().reshape(x.shape)
-        a = torch.log(x.float().clamp_min(1e-7) + 1)
+        t = acc_float(t).reshape(x.shape)
+        a = torch.log(acc_float(x).clamp_min(1e-7) + 1)
         b = torch.log(t.clamp_min(1e-7) + 1)
         return ((a - b) ** 2).mean()
 
@@ -356,8 +357,8 @@ class KullbackLeiblerDivergenceCriterion(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        xx = x.float().clamp(1e-7, 1)
-        tt = t.float().reshape(x.shape).clamp(1e-7, 1)
+        xx = acc_float(x).clamp(1e-7, 1)
+        tt = acc_float(t).reshape(x.shape).clamp(1e-7, 1)
         return (tt * torch.log(tt / xx)).sum(-1).mean()
 
 
@@ -366,7 +367,7 @@ class PoissonCriterion(AutogradCriterion):
         super().__init__(True)
 
     def _loss(self, x, t):
-        return (x.float() - t.float().reshape(x.shape) * torch.log(x.float() + 1e-7)).mean()
+        return (acc_float(x) - acc_float(t).reshape(x.shape) * torch.log(acc_float(x) + 1e-7)).mean()
 
 
 class KLDCriterion(AutogradCriterion):
@@ -376,7 +377,7 @@ class KLDCriterion(AutogradCriterion):
         super().__init__(size_average)
 
     def _loss(self, x, t):
-        mean, logvar = x[1].float(), x[2].float()
+        mean, logvar = acc_float(x[1]), acc_float(x[2])
         l = -0.5 * (1 + logvar - mean * mean - torch.exp(logvar))
         return l.sum() / mean.shape[0] if self.sizeAverage else l.sum()
 
@@ -388,8 +389,8 @@ class GaussianCriterion(AutogradCriterion):
         super().__init__(False)
 
     def _loss(self, x, t):
-        mean, logvar = x[1].float(), x[2].float()
-        return (0.5 * math.log(2 * math.pi) + 0.5 * logvar + (t.float() - mean) ** 2 / (2 * torch.exp(logvar))).sum()
+        mean, logvar = acc_float(x[1]), acc_float(x[2])
+        return (0.5 * math.log(2 * math.pi) + 0.5 * logvar + (acc_float(t) - mean) ** 2 / (2 * torch.exp(logvar))).sum()
 
 
 class SoftmaxWithCriterion(AutogradCriterion):
@@ -401,16 +402,16 @@ class SoftmaxWithCriterion(AutogradCriterion):
         self.ignoreLabel, self.normalizeMode = ignore_label, normalize_mode
 
     def _loss(self, x, t):
-        lp = torch.log_softmax(x.float(), dim=1)
+        lp = torch.log_softmax(acc_float(x), dim=1)
         tt = t.long().reshape(lp.shape[0], *lp.shape[2:]) - 1
         valid = torch.ones_like(tt, dtype=torch.bool) if self.ignoreLabel is None else (tt != self.ignoreLabel - 1)
         picked = lp.gather(1, tt.clamp_min(0).unsqueeze(1)).squeeze(1)
-        l = -(picked * valid.float()).sum()
+        l = -(picked * acc_float(valid)).sum()
         mode = self.normalizeMode
         if mode == "FULL":
             return l / tt.numel()
         if mode == "VALID":
-            return l / valid.float().sum().clamp_min(1)
+            return l / acc_float(valid).sum().clamp_min(1)
         if mode == "BATCH_SIZE":
             return l / lp.shape[0]
         return l
@@ -580,11 +581,11 @@ class DotProductCriterion(AbstractCriterion):
         super().__init__(size_average)
 
     def updateOutput(self, input, target):
-        s = (input.float() * target.float()).sum()
+        s = (acc_float(input) * acc_float(target)).sum()
         return s / input.shape[0] if self.sizeAverage else s
 
     def updateGradInput(self, input, target):
-        g = target.float().reshape(input.shape)
+        g = acc_float(target).reshape(input.shape)
         return g / input.shape[0] if self.sizeAverage else g
 
 
@@ -595,11 +596,11 @@ class PGCriterion(AbstractCriterion):
         super().__init__(sizeAverage)
 
     def updateOutput(self, input, target):
-        l = -(torch.log(input.float().clamp_min(1e-12)) * target.float()).sum()
+        l = -(torch.log(acc_float(input).clamp_min(1e-12)) * acc_float(target)).sum()
         return l / input.shape[0] if self.sizeAverage else l
 
     def updateGradInput(self, input, target):
-        g = -target.float() / input.float().clamp_min(1e-12)
+        g = -acc_float(target) / acc_float(input).clamp_min(1e-12)
         return g / input.shape[0] if self.sizeAverage else g
 
 

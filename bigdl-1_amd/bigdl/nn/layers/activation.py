@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from ... import ops
 from ..abstractnn import TensorModule, AutogradModule
+from ...utils import acc_float
 
 
 class Threshold(TensorModule):
@@ -91,7 +92,7 @@ class SoftMax(TensorModule):
             if r is not NotImplemented:
                 return r
             ops.native.note_fallback("softmax_forward.channels", "layout", (input,))
-        return torch.softmax(input.float(), dim=d).to(input.dtype)
+        return torch.softmax(acc_float(input), dim=d).to(input.dtype)
 
     def updateGradInput(self, input, gradOutput):
         d = self._dim(input)

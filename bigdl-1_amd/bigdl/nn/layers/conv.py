@@ -23,6 +23,7 @@ from ...utils.engine import Engine
 from ...utils import config
 from ..abstractnn import AbstractModule, TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, VariableFormats
+from ...utils import acc_float
 
 
 def same_padding(in_h, in_w, stride_h, stride_w, k_h, k_w, dil_h=1, dil_w=1):
@@ -232,7 +233,7 @@ class SpatialConvolution(TensorModule):
         if bn_fuse is not None and "partial" in bn_fuse and gi is not None:
             bn._pending_grad = (gi.data_ptr(), bn_fuse["partial"], bn_fuse["G"])
         if acc and own_bias and not same_scale and self.scale_b != 0:
-            self.gradBias.add_(gy.float().sum((0, 2, 3)), alpha=self.scale_b)
+            self.gradBias.add_(acc_float(gy).sum((0, 2, 3)), alpha=self.scale_b)
         if need_input and gi is not None:
             pt, pb, pl, pr = pads
             if pt != pb or pl != pr:

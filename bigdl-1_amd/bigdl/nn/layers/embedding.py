@@ -9,6 +9,7 @@ import torch
 from ... import ops
 from ..abstractnn import TensorModule
 from ...utils.table import Table
+from ...utils import acc_float
 
 DOUBLEMAX = 1.7976931348623157e308
 
@@ -62,7 +63,7 @@ class LookupTable(TensorModule):
             idx = input.long().reshape(-1)
             uniq, counts = torch.unique(idx, return_counts=True)
             freq = torch.zeros(self.nIndex + 1, device=idx.device)
-            freq[uniq] = counts.float()
+            freq[uniq] = acc_float(counts)
             g = gradOutput.reshape(idx.numel(), -1) / freq[idx].unsqueeze(1)
             ops.embedding_backward(self.gradWeight, input, g, scale, self.paddingValue)
         else:

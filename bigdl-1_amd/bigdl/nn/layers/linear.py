@@ -15,6 +15,7 @@ from ... import ops
 from ..abstractnn import TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, VariableFormats
 from ...utils.table import Table
+from ...utils import acc_float
 
 
 class Linear(TensorModule):
@@ -84,7 +85,7 @@ class Linear(TensorModule):
                                  self.gradBias if (acc and self.withBias and same) else None,
                                  self.scale_w if acc else 0.0)
         if acc and self.withBias and not same and self.scale_b != 0:
-            self.gradBias.add_(gy.float().sum(0), alpha=self.scale_b)
+            self.gradBias.add_(acc_float(gy).sum(0), alpha=self.scale_b)
         if acc and self.wRegularizer is not None and self.scale_w != 0:
             self.wRegularizer.accRegularization(self.weight, self.gradWeight, self.scale_w)
         if acc and self.withBias and self.bRegularizer is not None and self.scale_b != 0:
@@ -118,7 +119,7 @@ class SparseLinear(Linear):
 
     def updateOutput(self, input):
         if input.is_sparse:
-            y = torch.sparse.mm(input.float(), self.weight.t())
+            y = torch.sparse.mm(acc_float(input), self.weight.t())
             if self.withBias:
                 y = y + self.bias
             return y
@@ -127,11 +128,11 @@ class SparseLinear(Linear):
     def _bwd(self, input, gradOutput, need_input, acc):
         if input.is_sparse:
             if acc:
-                self.gradWeight.add_(torch.sparse.mm(input.float().t(), gradOutput.float()).t(), alpha=self.scale_w)
+                self.gradWeight.add_(torch.sparse.mm(acc_float(input).t(), acc_float(gradOutput)).t(), alpha=self.scale_w)
                 if self.withBias:
-                    self.gradBias.add_(gradOutput.float().sum(0), alpha=self.scale_b)
+                    self.gradBias.add_(acc_float(gradOutput).sum(0), alpha=self.scale_b)
             if need_input and self.backwardStart > 0:
-                g = gradOutput.float() @ self.weight
+                g = acc_float(gradOutput) @ self.weight
                 return g[:, self.backwardStart - 1:self.backwardStart - 1 + self.backwardLength]
             return None
         return super()._bwd(input, gradOutput, need_input, acc)

@@ -21,6 +21,7 @@ from ... import ops
 from ..abstractnn import TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, Ones, VariableFormats
 from .conv import to_device_layout
+from ...utils import acc_float
 
 
 class BatchNormalization(TensorModule):
@@ -92,7 +93,7 @@ class BatchNormalization(TensorModule):
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
         shape = [1, C] + [1] * (x.dim() - 2)
-        xf = x.float()
+        xf = acc_float(x)
         n_loc = float(x.numel() // C)
         mean_l = xf.mean(dims)
         m2_l = (xf - mean_l.view(shape)).square().sum(dims)
@@ -143,8 +144,9 @@ class BatchNormalization(TensorModule):
         x = to_device_layout(x) if x.dim() == 4 else x
         if residual is not None and residual.dim() == 4:
             residual = to_device_layout(residual)
-        g = self.cw("weight", torch.float32) if self.affine else None
-        b = self.cw("bias", torch.float32) if self.affine else None
+        pdt = torch.float64 if x.dtype == torch.float64 else torch.float32  # statistics dtype
+        g = self.cw("weight", pdt) if self.affine else None
+        b = self.cw("bias", pdt) if self.affine else None
         ib = self._in_bias()
         self._last_relu = relu
         if self.train:
@@ -185,11 +187,11 @@ class BatchNormalization(TensorModule):
             self.runningMean.mul_(1 - self.momentum).add_(tm, alpha=self.momentum)
             self.runningVar.mul_(1 - self.momentum).add_(var * (cnt / (cnt - 1).clamp_min(1)), alpha=self.momentum)
         shape = [1, x.shape[1]] + [1] * (x.dim() - 2)
-        y = (x.float() - mean.view(shape)) * invstd.view(shape)
+        y = (acc_float(x) - mean.view(shape)) * invstd.view(shape)
         if g is not None:
             y = y * g.view(shape) + b.view(shape)
         if residual is not None:
-            y = y + residual.float()
+            y = y + acc_float(residual)
         if relu:
             y = torch.relu(y)
         return y.to(x.dtype), mean, invstd
@@ -204,7 +206,7 @@ class BatchNormalization(TensorModule):
         y = self.output if relu else None
         if y is not None and y.dim() == 1:
             y = y.unsqueeze(0)
-        g = self.cw("weight", torch.float32) if self.affine else None
+        g = self.cw("weight", torch.float64 if x.dtype == torch.float64 else torch.float32) if self.affine else None
         prod = self._bias_producer
         cb = prod.gradBias if (acc and prod is not None and getattr(prod, "withBias", False)) else None
         cbs = prod.scale_b if prod is not None else 0.0
@@ -212,7 +214,7 @@ class BatchNormalization(TensorModule):
         if self._sync and _dist_ready() and self.train:
             gi = self._sync_backward(x, gy, g, y, need_input, acc, relu)
             if cb is not None and gi is not None:
-                cb.add_(gi.float().sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
+                cb.add_(acc_float(gi).sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
             if want_gres:
                 gres = gy * (y > 0).to(gy.dtype) if relu else gy
         else:
@@ -237,7 +239,7 @@ class BatchNormalization(TensorModule):
                                               scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs,
                                               want_gres=want_gres)
             if acc and self.affine and not same and self.scale_b != 0:
-                gf = gy.float() * ((y > 0).float() if relu else 1.0)
+                gf = acc_float(gy) * ((y > 0).float() if relu else 1.0)
                 dims = [d for d in range(gf.dim()) if d != 1]
                 self.gradBias.add_(gf.sum(dims), alpha=self.scale_b)
         if gi is not None and input.dim() == 1:
@@ -260,10 +262,10 @@ class BatchNormalization(TensorModule):
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
         shape = [1, C] + [1] * (x.dim() - 2)
-        gf = gy.float()
+        gf = acc_float(gy)
         if relu:
             gf = gf * (y > 0).float()
-        xhat = (x.float() - self.saveMean.view(shape)) * self.saveStd.view(shape)
+        xhat = (acc_float(x) - self.saveMean.view(shape)) * self.saveStd.view(shape)
         n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
         s = torch.cat([gf.sum(dims), (gf * xhat).sum(dims), n])
         local_db, local_dg = s[:C].clone(), s[C:2 * C].clone()
@@ -438,7 +440,7 @@ class NormalizeScale(AutogradModule):
 
 def _gauss_kernel(size):
     if isinstance(size, torch.Tensor):
-        return size.float()
+        return acc_float(size)
     k = torch.ones(size, size)
     return k
 

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from ... import ops
 from ..abstractnn import TensorModule, AutogradModule
 from .conv import to_device_layout, same_padding
+from ...utils import acc_float
 
 
 def _pool_pad(x, kh, kw, dh, dw, ph, pw):
@@ -255,7 +256,7 @@ def roi_align(data: torch.Tensor, rois: torch.Tensor, spatial_scale: float, out_
     off = 0.5 if aligned else 0.0
     if sampling_ratio <= 0:
         # adaptive grid: ceil(roi_size / bins) samples per bin, per ROI — group ROIs sharing a grid
-        r = rois.float()
+        r = acc_float(rois)
         rw = ((r[:, 3] - r[:, 1]) * spatial_scale).clamp_min(0.0 if aligned else 1.0)
         rh = ((r[:, 4] - r[:, 2]) * spatial_scale).clamp_min(0.0 if aligned else 1.0)
         gh = torch.ceil(rh / out_h).clamp_min(1).long()
@@ -278,7 +279,7 @@ def _roi_align_grid(data, rois, spatial_scale, out_h, out_w, srh, srw, off, alig
     gx = (torch.arange(out_w * srw, device=data.device, dtype=torch.float32) + 0.5) / srw
     outs = []
     for s in range(0, K, chunk):
-        r = rois[s:s + chunk].float()
+        r = acc_float(rois[s:s + chunk])
         k = r.shape[0]
         bi = r[:, 0].long()
         x1 = r[:, 1] * spatial_scale - off

@@ -40,6 +40,7 @@ from .dropout import Dropout
 from .linear import Linear
 from .math_ops import CMul
 from .shape import Identity
+from ...utils import acc_float
 
 
 # ============================================================================ tape
@@ -165,7 +166,12 @@ def _cdtype(t: torch.Tensor):
     if t.is_cuda:
         from ...utils.engine import Engine
         return Engine.compute_dtype()
-    return torch.float32
+    return torch.float64 if t.dtype == torch.float64 else torch.float32
+
+
+def _state_dt(dtype):
+    """Cell-state dtype: fp32 under bf16/fp32 compute, float64 for a float64 model."""
+    return torch.float64 if dtype == torch.float64 else torch.float32
 
 
 # ============================================================================ cells
@@ -343,20 +349,20 @@ class LSTM(Cell):
         if self.fused:
             hn, cn = _LSTMCellFn.apply(i2g, h2g, c)
             return hn, [hn, cn]
-        gates = i2g.float() + h2g.float()
+        gates = acc_float(i2g) + acc_float(h2g)
         act, inner = self.activation, self.innerActivation
         i = tape.apply(inner, gates[:, :H])
         g = tape.apply(act, gates[:, H:2 * H])
         f = tape.apply(inner, gates[:, 2 * H:3 * H])
         o = tape.apply(inner, gates[:, 3 * H:])
-        cn = i * g + f * c.float()
+        cn = i * g + f * acc_float(c)
         hn = (o * tape.apply(act, cn)).to(x.dtype)
         return hn, [hn, cn]
 
     def init_hidden(self, batch, step_shape, device, dtype):
         H = self.hiddenSize
         return [torch.zeros(batch, H, device=device, dtype=dtype), torch.zeros(batch, H, device=device,
-                                                                               dtype=torch.float32)]
+                                                                               dtype=_state_dt(dtype))]
 
     def __repr__(self):
         return f"LSTM({self.inputSize}, {self.hiddenSize}, {self.p})"
@@ -409,20 +415,20 @@ class LSTMPeephole(Cell):
     def init_hidden(self, batch, step_shape, device, dtype):
         H = self.hiddenSize
         return [torch.zeros(batch, H, device=device, dtype=dtype), torch.zeros(batch, H, device=device,
-                                                                               dtype=torch.float32)]
+                                                                               dtype=_state_dt(dtype))]
 
     def step(self, x, hidden, tape):
         h, c = hidden
         H = self.hiddenSize
         if self.p != 0:
-            xs = [tape.apply(l, tape.dropout(d, x)).float() for l, d in zip(self.i2g, self.drops[:4])]
+            xs = [acc_float(tape.apply(l, tape.dropout(d, x))) for l, d in zip(self.i2g, self.drops[:4])]
             hs = [tape.dropout(d, h) for d in self.drops[4:]]
         else:
-            xf = x.float()
+            xf = acc_float(x)
             xs = [xf[:, k * H:(k + 1) * H] for k in range(4)]
             hs = [h] * 4
-        u = [tape.apply(l, hh).float() for l, hh in zip(self.h2g, hs)]
-        cf = c.float()
+        u = [acc_float(tape.apply(l, hh)) for l, hh in zip(self.h2g, hs)]
+        cf = acc_float(c)
         i = torch.sigmoid(xs[0] + u[0] + tape.apply(self.peep[0], cf))
         f = torch.sigmoid(xs[1] + u[1] + tape.apply(self.peep[1], cf))
         g = torch.tanh(xs[2] + u[2])
@@ -467,22 +473,22 @@ class GRU(Cell):
         (h,) = hidden
         H = self.outputSize
         if self.p != 0:
-            xr = tape.apply(self.i2g[0], tape.dropout(self.drops[0], x)).float()
-            xz = tape.apply(self.i2g[1], tape.dropout(self.drops[1], x)).float()
-            ur = tape.apply(self.h2g[0], tape.dropout(self.drops[2], h)).float()
-            uz = tape.apply(self.h2g[1], tape.dropout(self.drops[3], h)).float()
-            xh = tape.apply(self.i2g[2], tape.dropout(self.drops[4], x)).float()
+            xr = acc_float(tape.apply(self.i2g[0], tape.dropout(self.drops[0], x)))
+            xz = acc_float(tape.apply(self.i2g[1], tape.dropout(self.drops[1], x)))
+            ur = acc_float(tape.apply(self.h2g[0], tape.dropout(self.drops[2], h)))
+            uz = acc_float(tape.apply(self.h2g[1], tape.dropout(self.drops[3], h)))
+            xh = acc_float(tape.apply(self.i2g[2], tape.dropout(self.drops[4], x)))
             rz = torch.cat([xr + ur, xz + uz], -1)
             hd = self.drops[5]
         else:
-            xf = x.float()
-            rz = xf[:, :2 * H] + tape.apply(self.h2g[0], h).float()
+            xf = acc_float(x)
+            rz = xf[:, :2 * H] + acc_float(tape.apply(self.h2g[0], h))
             xh = xf[:, 2 * H:]
             hd = self.drops[0]
         r = tape.apply(self.innerActivation, rz[:, :H])
         z = tape.apply(self.innerActivation, rz[:, H:])
-        hh = tape.apply(self.activation, xh + tape.apply(self.u_h, tape.dropout(hd, (h.float() * r).to(h.dtype))).float())
-        hn = ((1 - z) * hh + z * h.float()).to(x.dtype)
+        hh = tape.apply(self.activation, xh + acc_float(tape.apply(self.u_h, tape.dropout(hd, (acc_float(h) * r).to(h.dtype)))))
+        hn = ((1 - z) * hh + z * acc_float(h)).to(x.dtype)
         return hn, [hn]
 
 
@@ -504,7 +510,7 @@ class RnnCell(Cell):
 
     def step(self, x, hidden, tape):
         (h,) = hidden
-        hn = tape.apply(self.activation, x.float() + tape.apply(self.h2h, h).float()).to(x.dtype)
+        hn = tape.apply(self.activation, acc_float(x) + acc_float(tape.apply(self.h2h, h))).to(x.dtype)
         return hn, [hn]
 
 
@@ -543,12 +549,12 @@ class ConvLSTMPeephole(Cell):
     def init_hidden(self, batch, step_shape, device, dtype):
         rest = list(step_shape[1:])
         return [torch.zeros([batch, self.outputSize] + rest, device=device, dtype=dtype),
-                torch.zeros([batch, self.outputSize] + rest, device=device, dtype=torch.float32)]
+                torch.zeros([batch, self.outputSize] + rest, device=device, dtype=_state_dt(dtype))]
 
     def step(self, x, hidden, tape):
         h, c = hidden
-        cf = c.float()
-        gate = [tape.apply(a, x).float() + tape.apply(b, h).float() for a, b in zip(self.gx, self.gh)]
+        cf = acc_float(c)
+        gate = [acc_float(tape.apply(a, x)) + acc_float(tape.apply(b, h)) for a, b in zip(self.gx, self.gh)]
         inner, act = self.innerActivation, self.activation
         if self.withPeephole:
             i = tape.apply(inner, gate[0] + tape.apply(self.peep[0], cf))
@@ -808,13 +814,13 @@ class Recurrent(Container):
         U = cell.h2g.cw("weight")  # (4H, H)
         h0, c0 = self._h0(B, [H], x2.device, x2.dtype)
         h0 = h0.to(x2.dtype)
-        c0 = c0.float()
+        c0 = acc_float(c0)
         out = torch.empty(B, Tn, H, device=x2.device, dtype=x2.dtype)
         train = self.train
         if train:
-            acts = torch.empty(Tn, B, G, device=x2.device, dtype=torch.float32)
-            tcs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
-            cs = torch.empty(Tn, B, H, device=x2.device, dtype=torch.float32)
+            acts = torch.empty(Tn, B, G, device=x2.device, dtype=_state_dt(x2.dtype))
+            tcs = torch.empty(Tn, B, H, device=x2.device, dtype=_state_dt(x2.dtype))
+            cs = torch.empty(Tn, B, H, device=x2.device, dtype=_state_dt(x2.dtype))
         if _fused_rnn_ok(H, x2, U):
             # one launch per step (h·Uᵀ on MFMA + the cell update in the GEMM epilogue, rnn_step.hip),
             # the time loop itself in C++: one host call for the whole sequence
@@ -822,7 +828,7 @@ class Recurrent(Container):
             x2 = x2.contiguous()
             h0 = h0.contiguous()
             c0 = c0.contiguous()
-            cbuf = None if train else torch.empty(2, B, H, device=x2.device, dtype=torch.float32)
+            cbuf = None if train else torch.empty(2, B, H, device=x2.device, dtype=_state_dt(x2.dtype))
             NO.lstm_seq_forward(x2, h0, c0, U, out, cs if train else None, acts if train else None,
                                 tcs if train else None, cbuf)
             h = out[:, Tn - 1]
@@ -934,7 +940,7 @@ class Recurrent(Container):
             # one launch per step: dh = gy_t + dg_{t+1}·U on MFMA, cell backward in the epilogue
             from ...ops import native_ops as NO
             Ut = NO.transpose_bf16(U)  # (H, 4H)
-            gc = torch.empty(B, H, device=out.device, dtype=torch.float32)
+            gc = torch.empty(B, H, device=out.device, dtype=_state_dt(out.dtype))
             NO.lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc)
             gh_rec = NO.gemm(DG[:, 0], Ut)
         else:

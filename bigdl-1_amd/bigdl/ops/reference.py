@@ -11,6 +11,7 @@ from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
+from ..utils import acc_float
 
 aten = torch.ops.aten
 
@@ -67,9 +68,9 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
                                            list(stride), list(pad), list(dilation), False, [0, 0], groups,
                                            [need_input, need_w, need_b])
     if need_w:
-        gw_acc.add_(gw.float(), alpha=scale)
+        gw_acc.add_(acc_float(gw), alpha=scale)
     if need_b:
-        gb_acc.add_(gb.float(), alpha=scale)
+        gb_acc.add_(acc_float(gb), alpha=scale)
     if residual is not None and gi is not None:
         gi = gi + residual.to(gi.dtype)
     return gi
@@ -91,7 +92,7 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     """
     C = x.shape[1]
     dims = [d for d in range(x.dim()) if d != 1]
-    xf = x.float()
+    xf = acc_float(x)
     n = x.numel() // C
     mean = xf.mean(dim=dims)
     var = xf.var(dim=dims, unbiased=False)
@@ -99,19 +100,19 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     if running_mean is not None:
         with torch.no_grad():
             unbiased = var * (n / max(n - 1, 1))
-            true_mean = mean if in_bias is None else mean + in_bias.float()
+            true_mean = mean if in_bias is None else mean + acc_float(in_bias)
             running_mean.mul_(1 - momentum).add_(true_mean, alpha=momentum)
             running_var.mul_(1 - momentum).add_(unbiased, alpha=momentum)
     shape = [1, C] + [1] * (x.dim() - 2)
-    g = gamma.float().view(shape) if gamma is not None else 1.0
-    bb = beta.float().view(shape) if beta is not None else 0.0
+    g = acc_float(gamma).view(shape) if gamma is not None else 1.0
+    bb = acc_float(beta).view(shape) if beta is not None else 0.0
     if coef_out is not None:
-        sc = invstd * (gamma.float() if gamma is not None else 1.0)
+        sc = invstd * (acc_float(gamma) if gamma is not None else 1.0)
         coef_out[:C].copy_(sc)
-        coef_out[C:2 * C].copy_((beta.float() if beta is not None else 0.0) - mean * sc)
+        coef_out[C:2 * C].copy_((acc_float(beta) if beta is not None else 0.0) - mean * sc)
     y = (xf - mean.view(shape)) * invstd.view(shape) * g + bb
     if residual is not None:
-        y = y + residual.float()
+        y = y + acc_float(residual)
     if relu:
         y = torch.relu(y)
     return y.to(x.dtype), mean, invstd
@@ -121,11 +122,11 @@ def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu
     """Inference BN; ``in_bias`` is a per-channel producer bias folded into this BN (x excludes it)."""
     C = x.shape[1]
     shape = [1, C] + [1] * (x.dim() - 2)
-    invstd = torch.rsqrt(running_var.float() + eps)
-    scale = invstd * (gamma.float() if gamma is not None else 1.0)
-    rm = running_mean.float() - (in_bias.float() if in_bias is not None else 0.0)
-    shift = (beta.float() if beta is not None else 0.0) - rm * scale
-    y = x.float() * scale.view(shape) + shift.view(shape)
+    invstd = torch.rsqrt(acc_float(running_var) + eps)
+    scale = invstd * (acc_float(gamma) if gamma is not None else 1.0)
+    rm = acc_float(running_mean) - (acc_float(in_bias) if in_bias is not None else 0.0)
+    shift = (acc_float(beta) if beta is not None else 0.0) - rm * scale
+    y = acc_float(x) * scale.view(shape) + shift.view(shape)
     if relu:
         y = torch.relu(y)
     return y.to(x.dtype)
@@ -139,16 +140,16 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
     C = x.shape[1]
     dims = [d for d in range(x.dim()) if d != 1]
     shape = [1, C] + [1] * (x.dim() - 2)
-    g = gy.float()
+    g = acc_float(gy)
     if relu:
         g = g * (y > 0).float()
-    xhat = (x.float() - save_mean.view(shape)) * save_invstd.view(shape)
+    xhat = (acc_float(x) - save_mean.view(shape)) * save_invstd.view(shape)
     dbeta = g.sum(dim=dims)
     dgamma = (g * xhat).sum(dim=dims)
     gi = None
     if need_input or cbias_acc is not None:
         n = x.numel() // C
-        gam = gamma.float().view(shape) if gamma is not None else 1.0
+        gam = acc_float(gamma).view(shape) if gamma is not None else 1.0
         gif = (gam * save_invstd.view(shape) / n) * (n * g - dbeta.view(shape) - xhat * dgamma.view(shape))
         if cbias_acc is not None and cbias_scale != 0:
             cbias_acc.add_(gif.sum(dim=dims), alpha=cbias_scale)
@@ -200,29 +201,29 @@ def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1
     """``Linear.scala:128-158``: gradInput = gy·W; gradWeight += scale·gyᵀx; gradBias += scale·Σgy."""
     gi = gy @ w.to(gy.dtype) if need_input else None
     if gw_acc is not None and scale != 0:
-        gw_acc.add_(gy.float().t() @ x.float(), alpha=scale)
+        gw_acc.add_(acc_float(gy).t() @ acc_float(x), alpha=scale)
     if gb_acc is not None and scale != 0:
-        gb_acc.add_(gy.float().sum(0), alpha=scale)
+        gb_acc.add_(acc_float(gy).sum(0), alpha=scale)
     return gi
 
 
 # ------------------------------------------------------------------------- softmax / criteria
 def log_softmax_forward(x):
     """Row-wise log-softmax over the last dim (``DL/nn/LogSoftMax.scala:49-130``)."""
-    return torch.log_softmax(x.float(), dim=-1).to(x.dtype)
+    return torch.log_softmax(acc_float(x), dim=-1).to(x.dtype)
 
 
 def log_softmax_backward(gy, y):
-    gyf = gy.float()
-    return (gyf - torch.exp(y.float()) * gyf.sum(-1, keepdim=True)).to(y.dtype)
+    gyf = acc_float(gy)
+    return (gyf - torch.exp(acc_float(y)) * gyf.sum(-1, keepdim=True)).to(y.dtype)
 
 
 def softmax_forward(x):
-    return torch.softmax(x.float(), dim=-1).to(x.dtype)
+    return torch.softmax(acc_float(x), dim=-1).to(x.dtype)
 
 
 def softmax_backward(gy, y):
-    gyf, yf = gy.float(), y.float()
+    gyf, yf = acc_float(gy), acc_float(y)
     return (yf * (gyf - (gyf * yf).sum(-1, keepdim=True))).to(y.dtype)
 
 
@@ -235,13 +236,13 @@ def class_nll_forward(logp, target_1b, weights=None, size_average=True, padding_
     t = target_1b.long().reshape(-1)
     valid = t != padding_value
     idx = torch.where(valid, t - 1, torch.zeros_like(t))
-    picked = logp.float().gather(1, idx.unsqueeze(1)).squeeze(1)
-    w = weights.float()[idx] if weights is not None else torch.ones_like(picked)
-    w = w * valid.float()
+    picked = acc_float(logp).gather(1, idx.unsqueeze(1)).squeeze(1)
+    w = acc_float(weights)[idx] if weights is not None else torch.ones_like(picked)
+    w = w * acc_float(valid)
     total = -(picked * w).sum()
     if size_average:
         denom = w.sum()
-        total = total / torch.clamp(denom, min=1e-12) if weights is not None else total / torch.clamp(valid.float().sum(), min=1)
+        total = total / torch.clamp(denom, min=1e-12) if weights is not None else total / torch.clamp(acc_float(valid).sum(), min=1)
     return total
 
 
@@ -251,10 +252,10 @@ def class_nll_backward(logp, target_1b, weights=None, size_average=True, padding
     t = target_1b.long().reshape(-1)
     valid = t != padding_value
     idx = torch.where(valid, t - 1, torch.zeros_like(t))
-    w = weights.float()[idx] if weights is not None else torch.ones(t.shape[0], device=lp.device)
-    w = w * valid.float()
+    w = acc_float(weights)[idx] if weights is not None else torch.ones(t.shape[0], device=lp.device)
+    w = w * acc_float(valid)
     if size_average:
-        denom = w.sum() if weights is not None else valid.float().sum()
+        denom = w.sum() if weights is not None else acc_float(valid).sum()
         w = w / torch.clamp(denom, min=1e-12 if weights is not None else 1)
     g = torch.zeros(lp.shape, dtype=torch.float32, device=lp.device)
     g.scatter_(1, idx.unsqueeze(1), (-w).unsqueeze(1))
@@ -264,7 +265,7 @@ def class_nll_backward(logp, target_1b, weights=None, size_average=True, padding
 
 def cross_entropy_fused(x, target_1b, weights=None, size_average=True, padding_value=-1):
     """Fused LogSoftMax + ClassNLL (K12+K13): returns (loss, grad_x)."""
-    logp = torch.log_softmax(x.float(), dim=-1)
+    logp = torch.log_softmax(acc_float(x), dim=-1)
     loss = class_nll_forward(logp, target_1b, weights, size_average, padding_value)
     gl = class_nll_backward(logp, target_1b, weights, size_average, padding_value).float()
     gx = gl - torch.exp(logp) * gl.sum(-1, keepdim=True)
@@ -323,12 +324,12 @@ def lstm_cell_forward(xg, hg, c_prev, h_out=None, c_out=None, act_out=None, tc_o
     projection h·Uᵀ (or None); the gate sum is formed here in fp32.  Returns (h, c, act, tc):
     h in xg's dtype (written into ``h_out`` when given), c/act/tc fp32 (saved for backward)."""
     H = c_prev.shape[-1]
-    gf = xg.float() if hg is None else xg.float() + hg.float()
+    gf = acc_float(xg) if hg is None else acc_float(xg) + acc_float(hg)
     i = torch.sigmoid(gf[..., 0:H])
     g = torch.tanh(gf[..., H:2 * H])
     f = torch.sigmoid(gf[..., 2 * H:3 * H])
     o = torch.sigmoid(gf[..., 3 * H:4 * H])
-    c = i * g + f * c_prev.float()
+    c = i * g + f * acc_float(c_prev)
     tc = torch.tanh(c)
     h = (o * tc).to(xg.dtype)
     act = torch.cat([i, g, f, o], dim=-1)
@@ -347,12 +348,12 @@ def lstm_cell_backward(gh, gh2, gc_next, act, tc, c_prev, dg_out=None):
     (d gates [compute dtype of gh], dc_prev fp32)."""
     H = c_prev.shape[-1]
     i, g, f, o = act[..., 0:H], act[..., H:2 * H], act[..., 2 * H:3 * H], act[..., 3 * H:]
-    ghf = gh.float() if gh2 is None else gh.float() + gh2.float()
-    dc = ghf * o * (1 - tc * tc) + (gc_next.float() if gc_next is not None else 0.0)
+    ghf = acc_float(gh) if gh2 is None else acc_float(gh) + acc_float(gh2)
+    dc = ghf * o * (1 - tc * tc) + (acc_float(gc_next) if gc_next is not None else 0.0)
     do = ghf * tc
     di = dc * g
     dg = dc * i
-    df = dc * c_prev.float()
+    df = dc * acc_float(c_prev)
     dc_prev = dc * f
     dgates = torch.cat([di * i * (1 - i), dg * (1 - g * g), df * f * (1 - f), do * o * (1 - o)], dim=-1)
     dgates = dgates.to(gh.dtype)
@@ -413,7 +414,7 @@ def quant_rows(x2d: torch.Tensor, kp: Optional[int] = None):
     Returns (q [M][Kp] int8 zero-padded, scale [M] fp32 = max|row| / 127)."""
     M, K = x2d.shape
     kp = kp or (K + 63) // 64 * 64
-    xf = x2d.float()
+    xf = acc_float(x2d)
     amax = xf.abs().amax(dim=1) if K else torch.zeros(M, device=x2d.device)
     inv = torch.where(amax > 0, 127.0 / amax, torch.zeros_like(amax))
     q = torch.floor(xf * inv[:, None] + 0.5).clamp(-127, 127).to(torch.int8)
@@ -443,7 +444,7 @@ def image_crop_flip_norm(src, oy, ox, flip, out_h, out_w, mean, std, to_rgb, out
     outs = []
     for i in range(B):
         y, x = int(oy[i]), int(ox[i])
-        t = src[i, y:y + out_h, x:x + out_w].float()
+        t = acc_float(src[i, y:y + out_h, x:x + out_w])
         if int(flip[i]):
             t = t.flip(1)
         if to_rgb and C == 3:
