@@ -157,7 +157,11 @@ class Unsqueeze(TensorModule):
 class Transpose(TensorModule):
     def __init__(self, permutations, bigdl_type="float"):
         super().__init__()
-        self.permutations = [tuple(p) for p in permutations]
+        perms = list(permutations)
+        if perms and not isinstance(perms[0], (tuple, list)):
+            # flat [a1, b1, a2, b2, ...] (a deserialized permutation table)
+            perms = [(perms[i], perms[i + 1]) for i in range(0, len(perms), 2)]
+        self.permutations = [tuple(int(v) for v in p) for p in perms]
 
     def updateOutput(self, input):
         y = input

@@ -313,6 +313,14 @@ def _set_attr(ctx: _SerCtx, av: pb.AttrValue, v):
             arr.datatype = DT["TENSOR"]
             for x in v:
                 arr.tensor.add().CopyFrom(_reset(_tensor_to_pb(ctx, x)))
+        elif v and all(isinstance(x, (list, tuple)) and all(isinstance(y, int) and not isinstance(y, bool)
+                                                           for y in x) for x in v):
+            # an int table (Transpose permutations, crop pairs): flattened row-major like the
+            # reference's Array[(Int, Int)] serializer; the constructors re-pair a flat list
+            flat = [int(y) for x in v for y in x]
+            arr.size = len(flat)
+            arr.datatype = DT["INT32"]
+            arr.i32.extend(flat)
         else:
             av.dataType = DT["STRING"]
             av.stringValue = repr(v)
@@ -387,8 +395,9 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
     _set_attr(ctx, mp.attr[MODULE_NUMERICS], ["Float"])
     for k, v in _ctor_items(m):
         from ..nn.abstractnn import AbstractModule
-        if isinstance(m, Container) and isinstance(v, AbstractModule):
-            continue
+        if isinstance(m, Container) and (isinstance(v, AbstractModule) or (
+                isinstance(v, (list, tuple)) and v and all(isinstance(x, AbstractModule) for x in v))):
+            continue  # children travel as subModules
         _set_attr(ctx, mp.attr[_camel(k)], v)
     # extra state
     if hasattr(m, "ceilMode"):
@@ -424,6 +433,20 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
         _set_attr(ctx, mp.attr["inputNames"], [n.element.get_name() for n in m.inputs])
         _set_attr(ctx, mp.attr["outputNames"], [n.element.get_name() for n in m.outputs_nodes])
         return mp
+    from ..nn.layers.recurrent import Recurrent, Cell, MultiRNNCell
+    if isinstance(m, Recurrent):
+        # the preTopology (i2g) belongs to the cell; Recurrent.add rebuilds its TimeDistributed
+        # wrapper (and the optional BN) from the cell on load
+        if m.topology is not None:
+            mp.subModules.add().CopyFrom(_module_to_pb(ctx, m.topology))
+        return mp
+    if isinstance(m, Cell) and not isinstance(m, MultiRNNCell):
+        # a cell rebuilds its gate layers in its constructor: store it as a leaf holding every
+        # weight it owns (preTopology first, as Recurrent.parameters() orders them)
+        mp.hasParameters = True
+        for w in _cell_params(m):
+            mp.parameters.add().CopyFrom(_reset(_tensor_to_pb(ctx, w)))
+        return mp
     if isinstance(m, Container):
         for c in m.modules:
             mp.subModules.add().CopyFrom(_module_to_pb(ctx, c))
@@ -437,6 +460,16 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
 
 
 _BUF = "buffer:"
+
+
+def _cell_params(m):
+    ps = []
+    if m.preTopology is not None and not m.includePreTopology:
+        p = m.preTopology.parameters()
+        ps += list(p[0]) if p else []
+    p = m.parameters()
+    ps += list(p[0]) if p else []
+    return ps
 
 
 def _instantiate(cls, attrs: dict):
@@ -479,7 +512,27 @@ def _module_from_pb(ctx: _DeCtx, mp):
         g = Graph(ins, outs)
         g.set_name(mp.name)
         return g
-    m = _instantiate(cls, attrs)
+    from ..nn.layers.recurrent import Cell, MultiRNNCell
+    subs = None
+    consumed = False
+    if issubclass(cls, Container) and not (issubclass(cls, Cell) and not issubclass(cls, MultiRNNCell)):
+        subs = [_module_from_pb(ctx, sub) for sub in mp.subModules]
+    try:
+        m = _instantiate(cls, attrs)
+    except TypeError:
+        # a container whose constructor takes its child module(s) (Bottle(module), MultiRNNCell(cells),
+        # TableOperation(layer), ...): feed the deserialized children to the missing argument
+        if not subs:
+            raise
+        sig = inspect.signature(cls.__init__)
+        req = [p for p, prm in sig.parameters.items() if p != "self" and prm.default is prm.empty and
+               prm.kind not in (prm.VAR_POSITIONAL, prm.VAR_KEYWORD) and _camel(p) not in attrs and p not in attrs]
+        if len(req) != 1:
+            raise
+        extra = dict(attrs)
+        extra[req[0]] = subs if req[0] in ("cells", "modules", "layers") else subs[0]
+        m = _instantiate(cls, extra)
+        consumed = True
     if mp.name:
         m.set_name(mp.name)
     if mp.isMklInt8Enabled or len(mp.inputScales) or len(mp.outputScales) or len(mp.weightScales):
@@ -489,12 +542,13 @@ def _module_from_pb(ctx: _DeCtx, mp):
         m.setInputScales([list(_get_attr(ctx, a)) for a in mp.inputScales])
         m.setOutputScales([list(_get_attr(ctx, a)) for a in mp.outputScales])
         m.setWeightScales([list(_get_attr(ctx, a)) for a in mp.weightScales])
-    if isinstance(m, Container):
-        for sub in mp.subModules:
-            m.add(_module_from_pb(ctx, sub))
+    if isinstance(m, Container) and subs is not None and not consumed:
+        for sub in subs:
+            m.add(sub)
     if "ceilMode" in attrs and hasattr(m, "ceilMode") and attrs["ceilMode"] is not None:
         m.ceilMode = bool(attrs["ceilMode"])
-    if "numInputDims" in attrs and hasattr(m, "numInputDims") and attrs["numInputDims"] is not None:
+    if ("numInputDims" in attrs and type(m).__name__ == "View" and hasattr(m, "numInputDims")
+            and attrs["numInputDims"] is not None):
         m.numInputDims = int(attrs["numInputDims"])
     if isinstance(m, BatchNormalization):
         for k in ("runningMean", "runningVar"):
@@ -508,6 +562,8 @@ def _module_from_pb(ctx: _DeCtx, mp):
                 dst.copy_(t.reshape(dst.shape).to(dst.dtype))
     if mp.hasParameters and len(mp.parameters):
         p = m.parameters()
+        if isinstance(m, Cell) and not isinstance(m, MultiRNNCell):
+            p = (_cell_params(m), None)
         if p is not None:
             for dst, tp in zip(p[0], mp.parameters):
                 src = _tensor_from_pb(ctx, tp)
