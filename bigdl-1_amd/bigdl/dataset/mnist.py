@@ -10,7 +10,6 @@ import gzip
 import numpy as np
 
 from . import base
-from .readers import read_idx_images, read_idx_labels
 from .transformer import normalizer
 
 SOURCE_URL = "http://yann.lecun.com/exdb/mnist/"
@@ -45,7 +44,8 @@ def read_data_sets(train_dir, data_type="train"):
     pre = "train" if data_type == "train" else "t10k"
     img = base.maybe_download(f"{pre}-images-idx3-ubyte.gz", train_dir, SOURCE_URL)
     lab = base.maybe_download(f"{pre}-labels-idx1-ubyte.gz", train_dir, SOURCE_URL)
-    return read_idx_images(img)[..., None], read_idx_labels(lab)
+    with open(img, "rb") as fi, open(lab, "rb") as fl:
+        return extract_images(fi), extract_labels(fl)
 
 
 def load_data(location="/tmp/mnist"):

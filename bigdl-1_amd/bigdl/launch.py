@@ -2,6 +2,7 @@
 ``scripts/spark-submit-with-bigdl.sh`` + Spark executors, SURVEY §2.13 CLI row).
 
     python -m bigdl.launch --nproc 8 train.py --arg ...
+    python -m bigdl.launch --nproc 8 -m bigdl.models.train.imagenet --folder /data/imagenet-seq ...
 
 Each rank gets ``RANK`` / ``LOCAL_RANK`` / ``WORLD_SIZE`` / ``MASTER_ADDR`` / ``MASTER_PORT`` (the
 ``torch.distributed`` env:// contract that :class:`bigdl.utils.engine.Engine` reads; device =
@@ -140,14 +141,31 @@ def main(argv=None) -> int:
     ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--no-numa-bind", action="store_true")
     ap.add_argument("--max-restarts", type=int, default=0, help="relaunch all ranks after a failure")
-    ap.add_argument("script")
+    ap.add_argument("-m", dest="module", default=None, help="run a module (python -m MODULE) instead of a script")
+    ap.add_argument("script", nargs="?")
     ap.add_argument("args", nargs=argparse.REMAINDER)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    module_rest = None
+    if "-m" in argv:  # everything after ``-m MODULE`` belongs to the module, like python -m
+        i = argv.index("-m")
+        if i + 1 >= len(argv):
+            ap.error("-m needs a module name")
+        module_rest = argv[i + 1:]
+        argv = argv[:i]
     a = ap.parse_args(argv)
+    if module_rest is not None:
+        a.module, a.script, a.args = module_rest[0], None, module_rest[1:]
+    if a.module is None and a.script is None:
+        ap.error("a script or -m MODULE is required")
     n = a.nproc
     if n is None:
         import torch
         n = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
-    cmd = [sys.executable, a.script] + a.args if a.script.endswith(".py") else [a.script] + a.args
+    if a.module is not None:
+        rest = ([a.script] if a.script is not None else []) + a.args
+        cmd = [sys.executable, "-m", a.module] + rest
+    else:
+        cmd = [sys.executable, a.script] + a.args if a.script.endswith(".py") else [a.script] + a.args
     return launch(n, cmd, a.master_addr, a.master_port, not a.no_numa_bind, a.max_restarts)
 
 

@@ -107,6 +107,8 @@ class BaseOptimizer:
             if items and isinstance(items[0], MiniBatch):
                 return DataSet.array(items)
             return DataSet.array(items).transform(SampleToMiniBatch(batch_size))
+        if callable(getattr(ds, "data", None)) and callable(getattr(ds, "size", None)):
+            return ds  # a batch source with the data-set protocol (runtime.NativeBatchLoader)
         raise TypeError(f"unsupported training data {type(ds)}")
 
     # ------------------------------------------------------------------------------ builder setters
@@ -421,7 +423,12 @@ class BaseOptimizer:
         return it
 
     def _epoch_size(self) -> int:
+        """Records per epoch on this rank.  A data set of ready-made MiniBatches counts their
+        records (the reference sums ``batch.size()`` over one pass, LocalOptimizer.scala:93-96)."""
         ds = self.dataset
+        buf = getattr(ds, "buffer", None)
+        if buf and isinstance(buf[0], MiniBatch) and type(ds).__name__ == "LocalArrayDataSet":
+            return max(1, sum(b.size() for b in buf))
         n = getattr(ds, "local_size", None)
         n = n() if callable(n) else ds.size()
         return max(1, n)

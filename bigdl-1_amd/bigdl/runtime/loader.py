@@ -137,7 +137,23 @@ class NativeBatchLoader:
             yield self.next_batch()
 
     def data(self, train: bool = True):
-        return iter(self)
+        """Training: the infinite shuffled stream.  ``train=False`` (validation / evaluation): one
+        pass over the partition, ``batches_per_epoch()`` batches."""
+        if train:
+            return iter(self)
+        return (self.next_batch() for _ in range(self.batches_per_epoch()))
+
+    # AbstractDataSet protocol (the optimizers take a loader directly as their data set)
+    def size(self) -> int:
+        return int(self.images.shape[0])
+
+    local_size = size
+
+    def shuffle(self):
+        return self  # the workers reshuffle every epoch themselves
+
+    def transform(self, t):
+        raise TypeError("NativeBatchLoader batches are final; apply transforms before building it")
 
     def close(self):
         if getattr(self, "_h", None):
