@@ -115,10 +115,16 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 
   // per-row gather state for the activation rows this thread stages
   int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
+  // a pointwise stride-1 conv reads input pixel m for output pixel m: skip the (n, p, q) split
+  const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
 #pragma unroll
   for (int i = 0; i < A_CHUNKS; ++i) {
     int m = m0 + tid / CPK + RPS * i;
-    if (m < p.M) {
+    if (pw_direct) {
+      a_img[i] = m < p.M ? m : -1;
+      a_h[i] = 0;
+      a_w[i] = 0;
+    } else if (m < p.M) {
       int n = m / (p.P * p.Q);
       int pq = m - n * p.P * p.Q;
       int pp = pq / p.Q, qq = pq - pp * p.Q;
@@ -324,12 +330,12 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   //  2. the block walks the tile row-major, 8 channels per thread: optional residual add (same
   //     16-B chunk of `res`), ReLU, one global_store_dwordx4, and optional per-channel Σy / Σy²
   //     partials for a following BatchNormalization (the conv then replaces the BN stats pass).
-  // Staging layout: rows of BN bf16 (no pad); the 8-B unit u of row r lives at unit u ^ (r & UMASK).
-  // A fragment write covers 16 rows × one unit: the XOR spreads them over 16 distinct units, i.e.
-  // all 32 banks (conflict-free; a padded layout left 4-way conflicts).  A 16-B read of chunk c
-  // finds its two units at the aligned pair c ^ (s >> 1), swapped when s is odd.
+  // Staging layout: rows of BN bf16 (no pad); the 16-B chunk c of row r lives at chunk c ^ (r & CMASK).
+  // A fragment write (16 rows × one 8-B half-chunk) lands in 16 distinct chunk slots (at most 2-way
+  // bank conflicts), and the store loop reads every chunk back with ONE ds_read_b128 — the 8-B-unit
+  // swizzle this replaces needed a compare and four selects per chunk to undo odd-row swaps.
   constexpr int LDR = BN;
-  constexpr int UMASK = (BN / 4 - 1) & 31;
+  constexpr int CMASK = (BN / 8 - 1) & 15;
   bf16_t* et = &lds[0];
   // BN statistics straight from the fp32 accumulators (the plain conv → BN case: no bias, residual,
   // ReLU or BN-backward prologue): each lane sums its TM pixels per channel, two DPP row rotations
@@ -367,26 +373,29 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
     }
   }
   auto rd_chunk = [&](int r, int c) -> uint4 {
-    const int sw = r & UMASK;
-    uint4 u = *reinterpret_cast<const uint4*>(&et[r * LDR + ((c ^ (sw >> 1)) << 3)]);
-    if (sw & 1) u = make_uint4(u.z, u.w, u.x, u.y);
-    return u;
+    return *reinterpret_cast<const uint4*>(&et[r * LDR + ((c ^ (r & CMASK)) << 3)]);
   };
+  if (p.bias) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float b = (n + e < p.K) ? p.bias[n + e] : 0.f;
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j][e] += b;
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int nl = wave_n * (BN / 2) + i * 16 + fq * 4;
-    const int n = n0 + nl;
-    float b4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b4[j] = (n + j < p.K) ? p.bias[n + j] : 0.f;
-    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int ml = wave_m * (BM / 2) + j * 16 + fr;
-      uint32_t lo = (uint32_t)f2bf(acc[i][j][0] + b4[0]) | ((uint32_t)f2bf(acc[i][j][1] + b4[1]) << 16);
-      uint32_t hi = (uint32_t)f2bf(acc[i][j][2] + b4[2]) | ((uint32_t)f2bf(acc[i][j][3] + b4[3]) << 16);
-      *reinterpret_cast<uint2*>(&et[ml * LDR + (((nl >> 2) ^ (ml & UMASK)) << 2)]) = make_uint2(lo, hi);
+      uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      *reinterpret_cast<uint2*>(&et[ml * LDR + (((nl >> 3) ^ (ml & CMASK)) << 3) + (nl & 4)]) = make_uint2(lo, hi);
     }
   }
   __syncthreads();
@@ -394,6 +403,24 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   constexpr int RPP = 256 / CPR;   // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
   const int n = n0 + cc * 8;
+  // plain store (no residual / ReLU / BN prologue / scatter, whole channel tile): one LDS read and
+  // one 16-B global store per chunk on an incrementally advanced row pointer
+  if (!p.res && !p.relu && !p.bnx && !p.scatter && (p.stats == nullptr || rstats) && n0 + BN <= p.K) {
+    bf16_t* yp = p.y + (size_t)(m0 + rr) * p.ldy + n;
+    const size_t step = (size_t)RPP * p.ldy;
+    const int rmax = p.M - m0;
+#pragma unroll 4
+    for (int r = rr; r < BM; r += RPP, yp += step)
+      if (r < rmax) *reinterpret_cast<uint4*>(yp) = rd_chunk(r, cc);
+    if (rstats && tid < 2 * BN) {
+      const int which = tid / BN, c = tid - which * BN;
+      float a = 0.f;
+#pragma unroll
+      for (int g = 0; g < SRED; ++g) a += red8[(which * SRED + g) * BN + c];
+      if (tm < p.tiles_m) p.stats[((size_t)which * p.tiles_m + tm) * p.K + n0 + c] = a;
+    }
+    return;
+  }
   float s8[8], q8[8];
   const bool full = n + 8 <= p.K;
   float bsc[8], bsh[8], bmu[8];

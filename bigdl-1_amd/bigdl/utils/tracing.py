@@ -46,11 +46,13 @@ _roctx_tried = False
 
 
 def _roctx():
-    """``libroctx64`` via ctypes (ROCm's marker API; torch's nvtx shim is a no-op on some builds)."""
+    """The roctx marker API via ctypes.  ``librocprofiler-sdk-roctx`` first: that is the library
+    rocprofv3 ``--marker-trace`` intercepts (the legacy ``libroctx64`` belongs to roctracer)."""
     global _roctx_lib, _roctx_tried
     if not _roctx_tried:
         _roctx_tried = True
-        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                     "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
             try:
                 lib = ctypes.CDLL(name)
                 lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
@@ -132,6 +134,7 @@ class StepTracer:
         self._cur_host: Dict[str, float] = {}
         self._pending: List = []      # closed iterations whose events are not resolved yet
         self._json = None
+        self._steps = 0  # iterations closed by this tracer (train_step driven outside optimize())
         self.last_phases: Dict[str, float] = {}
         # straggler monitor
         self.window = max(1, int(config.get_property("bigdl.straggler.window")))
@@ -151,6 +154,8 @@ class StepTracer:
     def end_iteration(self, it: int, record: Dict):
         """Close iteration ``it``; ``record`` holds host-side facts (loss may be None if not yet
         read).  Returns the phase dict of the most recent iteration resolved so far."""
+        self._steps += 1
+        record = dict(record, step=self._steps)
         if self.device:
             marker = torch.cuda.Event()
             marker.record()

@@ -5,7 +5,8 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc2
 i=0
-for spec in ${SPECS:-"256,1024,1,1,14 fwdstats" "64,256,1,1,56 fwdstats" "128,128,3,1,28 fwdstats" "256,1024,1,1,14 dgrad"}; do
+IFS=';' read -ra LIST <<< "${SPECS:-256,1024,1,1,14 fwdstats;64,256,1,1,56 fwdstats;128,128,3,1,28 fwdstats;256,1024,1,1,14 dgrad}"
+for spec in "${LIST[@]}"; do
   set -- $spec
   for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU" "SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU" "TCC_HIT_sum TCC_MISS_sum"; do
     i=$((i+1))
