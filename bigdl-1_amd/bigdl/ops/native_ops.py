@@ -6,12 +6,14 @@ reference op).  No wrapper launches a kernel whose shape assumptions were not ve
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from typing import Optional
 
 import torch
 
 from . import native as N
+from ..utils import config
 from .native import register, ptr, stream_ptr, check
 
 _bf16 = torch.bfloat16
@@ -609,6 +611,41 @@ def _dgrad_1x1_strided(gy, w4, x_shape, stride):
     return gx
 
 
+# ------------------------------------------------------------------------------------------------ async wgrad
+# Backward-weight convolutions are compute-bound and independent of the backward-data chain, which
+# alternates with memory-bound BatchNorm passes: inside an optimizer step they run on a second HIP
+# stream so the two overlap (cdna_hip_programming.md Guideline 15).  The optimizer joins the side
+# stream before anything reads the gradients (update, reduce-scatter).  Off outside optimizer steps
+# (a plain module.backward() leaves every gradient complete on the current stream) and during
+# HIP-graph capture.
+_WG = {"on": False, "streams": {}}
+
+
+def async_wgrad(on: bool) -> None:
+    _WG["on"] = bool(on) and config.get_property("bigdl.conv.asyncWgrad")
+
+
+def _wgrad_side_stream(t):
+    if not _WG["on"] or not t.is_cuda or torch.cuda.is_current_stream_capturing():
+        return None
+    dev = t.device
+    st = _WG["streams"].get(dev)
+    if st is None:
+        st = _WG["streams"][dev] = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream(dev))  # gy / x / zeroed gradients are ready
+    return st
+
+
+def join_wgrad(stream=None) -> None:
+    """Make ``stream`` (default: the current stream) wait for every wgrad queued on the side stream."""
+    if not _WG["streams"] or torch.cuda.is_current_stream_capturing():
+        return
+    cur = stream or torch.cuda.current_stream()
+    st = _WG["streams"].get(cur.device)
+    if st is not None:
+        cur.wait_stream(st)
+
+
 #: total blocks the wgrad kernel aims for (split-K over pixels); 0 = per-shape heuristic below.
 #: tools/bench_conv.py --wgrad-sweep A/Bs fixed values.
 _WGRAD_TARGET_BLOCKS = [int(__import__("os").environ.get("BIGDL_WGRAD_BLOCKS", "0"))]
@@ -677,18 +714,27 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         if residual is not None and not res_done:
             gi = gi + residual
     if gw_acc is not None and scale != 0:
-        xx, cc = x, C_
-        if C_ % 8:
-            cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
-            xx = _pad_channels(x, cc, pad_slot, reuse=True)
-        direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
-        target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
-        P, Q = gy.shape[2], gy.shape[3]
-        check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
-                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
-                                      -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
-        if not direct:
-            gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
+        side = _wgrad_side_stream(gy)
+        ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+        with ctx:
+            xx, cc = x, C_
+            if C_ % 8:
+                cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
+                xx = _pad_channels(x, cc, pad_slot, reuse=True)
+            direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
+            target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32,
+                                                                            device=x.device)
+            P, Q = gy.shape[2], gy.shape[3]
+            check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc,
+                                          K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0],
+                                          dilation[1], -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
+            if not direct:
+                gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
+        if side is not None:
+            # the caching allocator must not hand these blocks to the compute stream while the
+            # side stream still reads them
+            for t in (x, xx, gy):
+                t.record_stream(side)
     if gb_acc is not None and scale != 0:
         gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
     return gi

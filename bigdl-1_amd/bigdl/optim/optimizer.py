@@ -338,6 +338,8 @@ class BaseOptimizer:
 
     def _sync_and_update(self, loss_t: torch.Tensor, batch_size: int):
         """Gradient aggregation + clipping + optimizer update (local: no aggregation)."""
+        from ..ops import native_ops as NO
+        NO.join_wgrad()  # weight gradients computed on the side stream
         self._clip(self.flat.grad, self.flat.grad)
         with self.tracer.phase("compute weight"):
             for name, meth in self.optim_methods.items():
@@ -514,7 +516,12 @@ class BaseOptimizer:
         with tr.phase("backward"):
             gout = crit.backward(out, y)
             self._before_backward()
-            m.backward(x, gout)
+            from ..ops import native_ops as NO
+            NO.async_wgrad(self.device.type == "cuda")
+            try:
+                m.backward(x, gout)
+            finally:
+                NO.async_wgrad(False)
         loss_t = loss if isinstance(loss, torch.Tensor) else torch.tensor(float(loss))
         loss_t = self._reduce_scalar(loss_t.detach().float().reshape(()))
         self._sync_and_update(loss_t, batch.size())

@@ -229,6 +229,8 @@ class DistriOptimizer(BaseOptimizer):
 
     # ------------------------------------------------------------------------------ collectives
     def _launch_reduce(self, b: _Bucket):
+        from ..ops import native_ops as NO
+        NO.join_wgrad()  # the bucket's conv weight gradients may still be running on the side stream
         g = self.flat.grad[b.lo:b.hi]
         if self.sharded:
             if self.grad_wire is not None:
@@ -309,6 +311,8 @@ class DistriOptimizer(BaseOptimizer):
         return t
 
     def _sync_and_update(self, loss_t, batch_size):
+        from ..ops import native_ops as NO
+        NO.join_wgrad()
         if self._first_iter:
             # enable overlap only if every parameterised module ran backward exactly once
             ok = all(self._hook_counts.get(id(m), 0) == 1 for b in self.buckets for m in b.modules)
