@@ -500,6 +500,29 @@ class BaseOptimizer:
         return self.train_step(batch)
 
     def train_step(self, batch: MiniBatch) -> torch.Tensor:
+        """One synchronous-SGD iteration on ``batch`` (see :meth:`_train_step_impl`).  On a GPU with
+        ``bigdl.step.highPriority`` the iteration runs on a high-priority HIP stream, so the
+        backward-data / BatchNorm chain wins the CUs over the side-stream weight-gradient kernels
+        it overlaps with (``bigdl.conv.asyncWgrad``); the caller's stream waits for it at the end."""
+        if (self.device.type != "cuda" or not config.get_property("bigdl.step.highPriority")
+                or torch.cuda.is_current_stream_capturing()):
+            return self._train_step_impl(batch)
+        hs = getattr(self, "_hp_stream", None)
+        if hs is None:
+            hs = self._hp_stream = torch.cuda.Stream(device=self.device, priority=-1)
+        cur = torch.cuda.current_stream(self.device)
+        hs.wait_stream(cur)
+        for t in (batch.getInput(), batch.getTarget()):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(hs)
+        with torch.cuda.stream(hs):
+            loss = self._train_step_impl(batch)
+        cur.wait_stream(hs)
+        if isinstance(loss, torch.Tensor) and loss.is_cuda:
+            loss.record_stream(cur)
+        return loss
+
+    def _train_step_impl(self, batch: MiniBatch) -> torch.Tensor:
         """One synchronous-SGD iteration on ``batch``; returns the (rank-averaged) loss as a
         device scalar without synchronising the host.  Phases (roctx ranges / HIP-event timers /
         JSON metrics per ``bigdl.roctx`` / ``bigdl.metrics.*``): forward, backward, then the
