@@ -17,6 +17,7 @@ from __future__ import annotations
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from ...nn import Graph, Input, Linear, SpatialConvolution
@@ -265,14 +266,46 @@ class TensorflowLoader:
     @staticmethod
     def load(path: str, inputs: Sequence[str], outputs: Sequence[str], byte_order: str = "little",
              bin_file: Optional[str] = None, generated_backward: bool = False):
+        """``bin_file``: variable values for the graph's ``VariableV2`` / ``VarHandleOp`` nodes — a
+        TensorFlow V2 checkpoint prefix (``<prefix>.index`` + data shards, read without
+        TensorFlow, :mod:`bigdl.utils.tf.checkpoint`) or an ``.npz`` / ``.safetensors`` file of
+        name → array.  Variables consumed by MatMul / Conv2D / BiasAdd become the trainable
+        weights of the fused Linear / SpatialConvolution layers."""
         nodes = TensorflowLoader.parse(path)
-        return _Builder(nodes, byte_order).build(list(inputs), list(outputs))
+        variables = load_variables(bin_file) if bin_file else None
+        return _Builder(nodes, byte_order, variables).build(list(inputs), list(outputs))
+
+    @staticmethod
+    def checkpoints(graph_file: str, bin_file: str, byte_order: str = "little"):
+        """``TensorflowLoader.checkpoints`` (TensorflowLoader.scala:88): a :class:`Session` over the
+        graph with its variables loaded from ``bin_file``."""
+        from .session import Session
+        return Session(TensorflowLoader.parse(graph_file), load_variables(bin_file), byte_order)
+
+
+def load_variables(path: str) -> Dict[str, torch.Tensor]:
+    from .checkpoint import is_checkpoint, read_checkpoint
+    if is_checkpoint(path):
+        arrs = read_checkpoint(path)
+    elif path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        arrs = load_file(path)
+    else:
+        with np.load(path, allow_pickle=False) as z:
+            arrs = {k: z[k] for k in z.files}
+    return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in arrs.items()}
+
+
+_VAR_OPS = ("VariableV2", "Variable", "VarHandleOp")
+_VAR_READS = ("ReadVariableOp", "Identity", "StopGradient", "Snapshot")
 
 
 class _Builder:
-    def __init__(self, nodes, byte_order):
+    def __init__(self, nodes, byte_order, variables: Optional[Dict[str, torch.Tensor]] = None):
         self.nodes = {n.name: n for n in nodes}
         self.byte_order = byte_order
+        self.variables = variables or {}
+        self.var_bindings: List = []   # (variable, module, attr, module-param → TF-layout fn)
         self.consts: Dict[str, object] = {}
         self.consumers: Dict[str, List[str]] = {}
         for n in nodes:
@@ -306,7 +339,11 @@ class _Builder:
             return self.consts[key]
         node = self.nodes[n]
         val = None
-        if n in self._fed_nodes or node.op in _STATEFUL or node.op in _NOT_LOADABLE or node.op in _CONTROL:
+        if n not in self._fed_nodes and node.op in _VAR_OPS and n in self.variables:
+            val = self.variables[n]
+        elif (n not in self._fed_nodes and node.op in _VAR_READS and self._var_of(ref) is not None):
+            val = self.variables[self._var_of(ref)]
+        elif n in self._fed_nodes or node.op in _STATEFUL or node.op in _NOT_LOADABLE or node.op in _CONTROL:
             val = None
         elif node.op == "Const":
             val = tensor_to_torch(node.attr["value"].tensor, self.byte_order)
@@ -319,6 +356,28 @@ class _Builder:
                 val = out[idx + 1] if isinstance(out, Table) else out
         self.consts[key] = val
         return val
+
+    def _var_of(self, ref: str) -> Optional[str]:
+        """The variable whose value tensor ``ref`` is (through reads / identities), if any."""
+        n, _ = _split_ref(ref)
+        seen = 0
+        while n in self.nodes and seen < 64:
+            node = self.nodes[n]
+            if node.op in _VAR_OPS:
+                return n if n in self.variables else None
+            if node.op not in _VAR_READS:
+                return None
+            data_in = [i for i in node.input if not i.startswith("^")]
+            if not data_in:
+                return None
+            n, _ = _split_ref(data_in[0])
+            seen += 1
+        return None
+
+    def _bind(self, ref, module, attr, to_tf):
+        v = self._var_of(ref)
+        if v is not None:
+            self.var_bindings.append((v, module, attr, to_tf))
 
     # ------------------------------------------------------------------ graph construction
     def build(self, inputs, outputs):
@@ -421,12 +480,9 @@ class _Builder:
     def _fuse(self, node):
         ins = [i for i in node.input if not i.startswith("^")]
         if node.op == "MatMul" and not _attr(node, "transpose_a"):
-            w = self._const(ins[1])
-            if w is not None and w.dim() == 2:
-                w = w.t() if not _attr(node, "transpose_b") else w  # Linear weight is [out, in]
-                lin = Linear(w.shape[1], w.shape[0], with_bias=False)
-                lin.weight.data.copy_(w.float())
-                return lin, [(node.name, 0)]
+            fused = self._producer_fusable(node)  # Linear weight is [out, in]
+            if fused is not None:
+                return fused
         if node.op in ("BiasAdd", "Add", "AddV2"):
             src = self.nodes[_split_ref(ins[0])[0]]
             if src.name in self._feed_node:
@@ -439,9 +495,12 @@ class _Builder:
                     nl = Linear(layer.weight.shape[1], layer.weight.shape[0])
                     nl.weight.data.copy_(layer.weight.data)
                     nl.bias.data.copy_(b.float())
+                    self.var_bindings = [(v, nl if m is layer else m, a, f) for (v, m, a, f) in self.var_bindings]
                     layer = nl
                 else:
                     layer.bias.data.copy_(b.float())
+                other = [i for i in ins if _split_ref(i)[0] != src.name]
+                self._bind(other[0], layer, "bias", lambda t: t)
                 return layer, data
         if node.op == "Conv2D":
             prod = self._producer_fusable(node)
@@ -454,9 +513,11 @@ class _Builder:
         if node.op == "MatMul" and not _attr(node, "transpose_a"):
             w = self._const(ins[1])
             if w is not None and w.dim() == 2:
-                w = w.t() if not _attr(node, "transpose_b") else w
+                tb = bool(_attr(node, "transpose_b"))
+                w = w.t() if not tb else w
                 lin = Linear(w.shape[1], w.shape[0], with_bias=False)
                 lin.weight.data.copy_(w.float())
+                self._bind(ins[1], lin, "weight", (lambda t: t) if tb else (lambda t: t.t()))
                 return lin, [(node.name, 0)]
         if node.op == "Conv2D" and _attr(node, "data_format", "NHWC") == "NHWC":
             f = self._const(ins[1])
@@ -468,5 +529,7 @@ class _Builder:
                 conv = SpatialConvolution(cin, cout, kw, kh, s[2], s[1], pad, pad, data_format="NHWC")
                 conv.weight.data.copy_(f.permute(3, 2, 0, 1).reshape(conv.weight.shape).float())
                 conv.bias.data.zero_()
+                self._bind(ins[1], conv, "weight", lambda t, shp=tuple(f.shape): t.reshape(
+                    shp[3], shp[2], shp[0], shp[1]).permute(2, 3, 1, 0))
                 return conv, [(node.name, 0)]
         return None
