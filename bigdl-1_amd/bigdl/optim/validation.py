@@ -96,6 +96,9 @@ def _to_2d(output):
 class Top1Accuracy(ValidationMethod):
     def __call__(self, output, target):
         o = _to_2d(output).float()
+        if target.dim() == 2 and target.shape == o.shape and o.shape[1] > 1:
+            # one-hot / probability targets (Keras "accuracy" with categorical_crossentropy)
+            target = target.float().argmax(1) + 1
         t = target.reshape(-1).long()
         if o.shape[1] == 1:  # binary
             pred = (o.reshape(-1) > 0.5).long()
