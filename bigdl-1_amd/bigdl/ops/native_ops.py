@@ -622,7 +622,7 @@ _WG = {"on": False, "streams": {}}
 
 
 def async_wgrad(on: bool) -> None:
-    _WG["on"] = bool(on) and config.get_property("bigdl.conv.asyncWgrad")
+    _WG["on"] = bool(on) and bool(config.get_property("bigdl.conv.asyncWgrad"))
 
 
 def _wgrad_side_stream(t):
@@ -662,6 +662,25 @@ def _wgrad_blocks(M, C_, K):
     if M >= 400000 and (C_ <= 64 or K <= 64):
         return 768
     return 384
+
+
+def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
+    """Backward-weight conv on the current stream; returns the activation operand it read."""
+    N_, C_, H, W = x.shape
+    K, Ci, R, S = w4.shape
+    xx, cc = x, C_
+    if C_ % 8:
+        cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
+        xx = _pad_channels(x, cc, pad_slot, reuse=True)
+    direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
+    target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
+    P, Q = gy.shape[2], gy.shape[3]
+    check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
+                                  R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                  -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
+    if not direct:
+        gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
+    return xx
 
 
 @register("conv2d_backward")
@@ -714,23 +733,12 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         if residual is not None and not res_done:
             gi = gi + residual
     if gw_acc is not None and scale != 0:
-        side = _wgrad_side_stream(gy)
-        ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
-        with ctx:
-            xx, cc = x, C_
-            if C_ % 8:
-                cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
-                xx = _pad_channels(x, cc, pad_slot, reuse=True)
-            direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
-            target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32,
-                                                                            device=x.device)
-            P, Q = gy.shape[2], gy.shape[3]
-            check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc,
-                                          K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0],
-                                          dilation[1], -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
-            if not direct:
-                gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
-        if side is not None:
+        side = _wgrad_side_stream(gy) if _WG["on"] else None
+        if side is None:
+            _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
+        else:
+            with torch.cuda.stream(side):
+                xx = _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
             # the caching allocator must not hand these blocks to the compute stream while the
             # side stream still reads them
             for t in (x, xx, gy):

@@ -50,6 +50,7 @@ _REGISTRY = {
     "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),
+    "bigdl.step.overlapMinMs": (float, 8.0, "enable the high-priority step stream and async wgrad once the measured step period is at least this long (GPU-bound steps; launch-bound ones lose to the extra host work)"),
     "bigdl.step.highPriority": (bool, True, "run each GPU training iteration on a high-priority HIP stream (the critical path outranks side-stream wgrad work)"),
     "bigdl.conv.asyncWgrad": (bool, True, "inside optimizer steps run conv backward-weight kernels on a second HIP stream, overlapping the backward-data / BatchNorm chain"),
     "bigdl.deterministic": (bool, False, "bit-reproducible kernels: single-writer reductions instead of split-K float atomics (slower wgrad / embedding backward)"),
