@@ -117,9 +117,22 @@ class SparseLinear(Linear):
         super().__init__(input_size, output_size, with_bias, wRegularizer, bRegularizer, init_weight, init_bias)
         self.backwardStart, self.backwardLength = backwardStart, backwardLength
 
+    @staticmethod
+    def _spmm(a, b):
+        """sparse × dense: the native CSR SpMM kernel on a GPU (ops/csrc/sparse.hip), torch.sparse
+        on the host."""
+        if a.is_cuda:
+            from ...ops import native as N
+            if N.has("spmm"):
+                r = N.native_ops.spmm(a, b.contiguous())
+                if r is not NotImplemented:
+                    return r
+                N.note_fallback("spmm", "shape", (b,))
+        return torch.sparse.mm(acc_float(a), b)
+
     def updateOutput(self, input):
         if input.is_sparse:
-            y = torch.sparse.mm(acc_float(input), self.weight.t())
+            y = self._spmm(input, acc_float(self.weight).t())
             if self.withBias:
                 y = y + self.bias
             return y
@@ -128,7 +141,8 @@ class SparseLinear(Linear):
     def _bwd(self, input, gradOutput, need_input, acc):
         if input.is_sparse:
             if acc:
-                self.gradWeight.add_(torch.sparse.mm(acc_float(input).t(), acc_float(gradOutput)).t(), alpha=self.scale_w)
+                # dW = Gᵀ·X, formed as (Xᵀ·G)ᵀ so the sparse operand stays on the left
+                self.gradWeight.add_(self._spmm(input.t().coalesce(), acc_float(gradOutput)).t(), alpha=self.scale_w)
                 if self.withBias:
                     self.gradBias.add_(acc_float(gradOutput).sum(0), alpha=self.scale_b)
             if need_input and self.backwardStart > 0:

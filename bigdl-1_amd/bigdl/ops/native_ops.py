@@ -1459,3 +1459,31 @@ def class_nll_backward(logp, target_1b, weights=None, size_average=True, padding
                                  C.c_int(1 if size_average else 0), C.c_int(1 if lp.dtype == _bf16 else 0), ptr(out),
                                  _s()), "class_nll_bwd")
     return gx.squeeze(0) if logp.dim() == 1 else gx
+
+
+# ------------------------------------------------------------------------------------------------ sparse
+@register("spmm")
+def spmm(a, b, alpha=1.0):
+    """fp32 ``alpha · a @ b`` for a sparse COO ``a`` [M, K] and a dense ``b`` [K, N] (fp32 or bf16)
+    on the device: CSR SpMM kernel (sparse.hip), one wave per output row, no atomics."""
+    if not (a.is_sparse and a.is_cuda and b.is_cuda and a.dim() == 2 and b.dim() == 2):
+        return NotImplemented
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K or N % 4 or b.dtype not in (_f32, _bf16):
+        return NotImplemented
+    a = a.coalesce()  # row-major sorted (row, col) → CSR order
+    b = b.contiguous()
+    idx = a.indices()
+    nnz = idx.shape[1]
+    it = torch.int32 if nnz < 2 ** 31 - 1 else torch.int64
+    rowptr = torch.zeros(M + 1, dtype=it, device=b.device)
+    if nnz:
+        rowptr[1:] = torch.bincount(idx[0], minlength=M).cumsum(0).to(it)
+    col = idx[1].to(it).contiguous()
+    val = a.values().float().contiguous()
+    out = torch.empty((M, N), dtype=_f32, device=b.device)
+    check(_lib().bigdl_spmm_csr(ptr(rowptr), ptr(col), ptr(val), C.c_int(0 if it == torch.int32 else 1), ptr(b),
+                                C.c_int(0 if b.dtype == _f32 else 1), ptr(out), C.c_int(M), C.c_int(N),
+                                _ll(b.stride(0)), _ll(out.stride(0)), _f(alpha), _f(0.0), _s()), "spmm_csr")
+    return out
