@@ -41,6 +41,13 @@ def to_device_layout(x: torch.Tensor) -> torch.Tensor:
     """Device activations are NHWC (channels_last) in the compute dtype."""
     if x.is_cuda and x.dim() == 4:
         dt = Engine.compute_dtype()
+        if (dt == torch.bfloat16 and x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous()
+                and not x.is_contiguous(memory_format=torch.channels_last)):
+            from ...ops import native as N
+            if N.has("nchw_to_nhwc_bf16"):
+                y = N.native_ops.nchw_to_nhwc_bf16(x)  # cast + relayout in one pass
+                if y is not NotImplemented:
+                    return y
         if x.dtype != dt and x.is_floating_point():
             x = x.to(dt)
         if not x.is_contiguous(memory_format=torch.channels_last):

@@ -253,3 +253,73 @@ BIGDL_EXPORT int bigdl_adam(float* w, const float* g, float* m, float* v, bf16_t
                      step_size, b1, b2, eps, wd, scale, (int)(n & 3));
   BIGDL_CHECK_LAUNCH();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Reference wire format (K23, FP16CompressedTensor.scala:43-277): fp32 → bf16 by truncation (the
+// top 16 bits, no rounding), written straight into the reduce-scatter wire buffer — one pass in
+// place of the int32 view / shift / narrow temporaries of the torch formulation.
+__global__ void __launch_bounds__(256) k_trunc_bf16(const uint32_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                    long long n) {
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 u = reinterpret_cast<const uint4*>(src)[i];
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2((u.x >> 16) | (u.y & 0xFFFF0000u), (u.z >> 16) | (u.w & 0xFFFF0000u));
+  }
+  for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    dst[i] = (bf16_t)(src[i] >> 16);
+}
+
+BIGDL_EXPORT int bigdl_trunc_bf16(const float* src, void* dst, long long n, hipStream_t s) {
+  if (n <= 0 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 7)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_trunc_bf16, dim3(bigdl_grid((n + 3) / 4, 256, 8192)), dim3(256), 0, s, (const uint32_t*)src,
+                     (bf16_t*)dst, n);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// NCHW (fp32 or bf16) → NHWC bf16 in one pass (K24: the host-layout → device-layout boundary,
+// a cast plus a channels-last copy otherwise).  A block transposes a 32-channel × 64-pixel tile
+// through LDS: reads coalesced along pixels, writes 64-B runs along channels.
+template <typename T>
+__global__ void __launch_bounds__(256) k_nchw_to_nhwc(const T* __restrict__ x, bf16_t* __restrict__ y, int C,
+                                                      long long HW) {
+  __shared__ float tile[32][65];
+  const int n = blockIdx.z;
+  const int c0 = blockIdx.y * 32;
+  const long long p0 = (long long)blockIdx.x * 64;
+  const T* xs = x + (long long)n * C * HW;
+  for (int i = threadIdx.x; i < 32 * 64; i += 256) {
+    const int cl = i >> 6, pl = i & 63;
+    const int c = c0 + cl;
+    const long long p = p0 + pl;
+    float v = 0.f;
+    if (c < C && p < HW) {
+      if constexpr (sizeof(T) == 4) v = xs[(long long)c * HW + p];
+      else v = bf2f(xs[(long long)c * HW + p]);
+    }
+    tile[cl][pl] = v;
+  }
+  __syncthreads();
+  bf16_t* ys = y + (long long)n * HW * C;
+  for (int i = threadIdx.x; i < 32 * 64; i += 256) {
+    const int pl = i >> 5, cl = i & 31;
+    const int c = c0 + cl;
+    const long long p = p0 + pl;
+    if (c < C && p < HW) ys[p * C + c] = f2bf(tile[cl][pl]);
+  }
+}
+
+// dtype: 0 = fp32 input, 1 = bf16 input
+BIGDL_EXPORT int bigdl_nchw_to_nhwc_bf16(const void* x, int dtype, void* y, int N, int C, long long HW,
+                                         hipStream_t s) {
+  if (N <= 0 || C <= 0 || HW <= 0 || N > 65535 || (C + 31) / 32 > 65535) return (int)hipErrorInvalidValue;
+  const long long gx = (HW + 63) / 64;
+  if (gx > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)gx, (unsigned)((C + 31) / 32), (unsigned)N);
+  if (dtype == 0)
+    hipLaunchKernelGGL((k_nchw_to_nhwc<float>), g, dim3(256), 0, s, (const float*)x, (bf16_t*)y, C, HW);
+  else
+    hipLaunchKernelGGL((k_nchw_to_nhwc<bf16_t>), g, dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, C, HW);
+  BIGDL_CHECK_LAUNCH();
+}

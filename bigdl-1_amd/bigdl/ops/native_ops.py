@@ -1487,3 +1487,29 @@ def spmm(a, b, alpha=1.0):
                                 C.c_int(0 if b.dtype == _f32 else 1), ptr(out), C.c_int(M), C.c_int(N),
                                 _ll(b.stride(0)), _ll(out.stride(0)), _f(alpha), _f(0.0), _s()), "spmm_csr")
     return out
+
+
+# ------------------------------------------------------------------------------------------------ layout / wire
+@register("trunc_bf16")
+def trunc_bf16(src, dst):
+    """dst (bf16) ← the top 16 bits of src (fp32): the reference's truncating wire format."""
+    if not (src.is_cuda and src.dtype == _f32 and dst.dtype == _bf16 and src.is_contiguous() and dst.is_contiguous()
+            and src.numel() == dst.numel() and _al16(src) and dst.data_ptr() % 8 == 0):
+        return NotImplemented
+    if src.numel():
+        check(_lib().bigdl_trunc_bf16(ptr(src), ptr(dst), _ll(src.numel()), _s()), "trunc_bf16")
+    return dst
+
+
+@register("nchw_to_nhwc_bf16")
+def nchw_to_nhwc_bf16(x):
+    """Contiguous NCHW (fp32 / bf16) → channels-last bf16 in one pass (tiled LDS transpose)."""
+    if not (x.is_cuda and x.dim() == 4 and x.is_contiguous() and x.dtype in (_f32, _bf16)):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if N_ > 65535 or N_ * C_ * H * W == 0:
+        return NotImplemented
+    y = torch.empty((N_, C_, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_nchw_to_nhwc_bf16(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), ptr(y), C.c_int(N_),
+                                         C.c_int(C_), _ll(H * W), _s()), "nchw_to_nhwc_bf16")
+    return y

@@ -236,7 +236,9 @@ class DistriOptimizer(BaseOptimizer):
             if self.grad_wire is not None:
                 wire = self.grad_wire[b.lo:b.hi]
                 if self.comm_dtype == "bf16_truncate":
-                    wire.copy_(comm.bf16_truncate(g))
+                    from ..ops import native as N
+                    if not (N.has("trunc_bf16") and N.native_ops.trunc_bf16(g, wire) is not NotImplemented):
+                        wire.copy_(comm.bf16_truncate(g))
                 else:
                     wire.copy_(g)
                 b.rs_work = dist.reduce_scatter_tensor(self.shard_g_wire[b.slo:b.shi], wire, async_op=True)
