@@ -101,6 +101,13 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, thresh: float, plus_one: floa
         return torch.zeros(0, dtype=torch.long, device=boxes.device)
     order = torch.argsort(scores, descending=True)
     b = boxes[order].float()
+    if b.is_cuda:
+        from ...ops import native as N
+        if N.has("nms"):
+            k = N.native_ops.nms(b, thresh, plus_one, max_keep)  # device bitmask + one-wave scan
+            if k is not NotImplemented:
+                return order[k]
+            N.note_fallback("nms", "size", (b,))
     over = (box_iou(b, b, plus_one) > thresh).cpu().numpy()
     keep = []
     removed = np.zeros(n, dtype=bool)

@@ -253,6 +253,13 @@ def roi_align(data: torch.Tensor, rois: torch.Tensor, spatial_scale: float, out_
     N, C, H, W = data.shape
     if K == 0:
         return data.new_zeros((0, C, out_h, out_w))
+    if data.is_cuda:
+        from ...ops import native as NO
+        if NO.has("roi_align"):
+            y = NO.native_ops.roi_align(data, rois, spatial_scale, out_h, out_w, sampling_ratio, aligned)
+            if y is not NotImplemented:
+                return y
+            NO.note_fallback("roi_align", "shape/dtype", (data, rois))
     off = 0.5 if aligned else 0.0
     if sampling_ratio <= 0:
         # adaptive grid: ceil(roi_size / bins) samples per bin, per ROI — group ROIs sharing a grid

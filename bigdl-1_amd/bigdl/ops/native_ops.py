@@ -1513,3 +1513,73 @@ def nchw_to_nhwc_bf16(x):
     check(_lib().bigdl_nchw_to_nhwc_bf16(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), ptr(y), C.c_int(N_),
                                          C.c_int(C_), _ll(H * W), _s()), "nchw_to_nhwc_bf16")
     return y
+
+
+# ------------------------------------------------------------------------------------------------ detection
+_NMS_MAX = 32768
+
+
+@register("nms")
+def nms(boxes_sorted, thresh, plus_one=1.0, max_keep=-1):
+    """Greedy NMS of score-sorted ``boxes_sorted [n, 4]`` on the device (pairwise IoU bitmask +
+    one-wave scan, detection.hip); returns the kept positions (int64, score order)."""
+    if not (boxes_sorted.is_cuda and boxes_sorted.dim() == 2 and boxes_sorted.shape[1] == 4):
+        return NotImplemented
+    n = boxes_sorted.shape[0]
+    if n == 0 or n > _NMS_MAX:
+        return NotImplemented
+    b = boxes_sorted.float().contiguous()
+    words = (n + 63) // 64
+    mask = torch.empty(n * words, dtype=torch.int64, device=b.device)
+    keep = torch.empty(n, dtype=torch.int64, device=b.device)
+    count = torch.empty(1, dtype=torch.int32, device=b.device)
+    check(_lib().bigdl_nms(ptr(b), C.c_int(n), _f(thresh), _f(plus_one), C.c_int(int(max_keep)), ptr(mask), ptr(keep),
+                           ptr(count), _s()), "nms")
+    return keep[:int(count.item())]
+
+
+def _roi_strides(x, y):
+    return (C.c_longlong * 8)(*[int(s) for s in x.stride()], *[int(s) for s in y.stride()])
+
+
+class _RoiAlignFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, data, rois, scale, oh, ow, sr, aligned):
+        K = rois.shape[0]
+        N_, C_, H, W = data.shape
+        y = torch.empty((K, C_, oh, ow), dtype=_f32, device=data.device)
+        st = _roi_strides(data, y)
+        check(_lib().bigdl_roi_align_fwd(ptr(data), C.c_int(0 if data.dtype == _f32 else 1), ptr(rois), ptr(y),
+                                         C.c_int(K), C.c_int(C_), C.c_int(H), C.c_int(W), C.c_int(oh), C.c_int(ow),
+                                         _f(scale), C.c_int(sr), C.c_int(1 if aligned else 0), st, _s()),
+              "roi_align_fwd")
+        ctx.save_for_backward(rois)
+        ctx.meta = (data.shape, data.dtype, data.stride(), scale, oh, ow, sr, aligned)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (rois,) = ctx.saved_tensors
+        shape, dtype, stride, scale, oh, ow, sr, aligned = ctx.meta
+        N_, C_, H, W = shape
+        cl = stride[1] == 1 and C_ > 1
+        gx = torch.empty(shape, dtype=_f32, device=gy.device,
+                         memory_format=torch.channels_last if cl else torch.contiguous_format).zero_()
+        gy = gy.float()
+        st = _roi_strides(gx, gy)
+        check(_lib().bigdl_roi_align_bwd(ptr(gy), ptr(rois), ptr(gx), C.c_int(rois.shape[0]), C.c_int(C_), C.c_int(H),
+                                         C.c_int(W), C.c_int(oh), C.c_int(ow), _f(scale), C.c_int(sr),
+                                         C.c_int(1 if aligned else 0), st, _s()), "roi_align_bwd")
+        return gx.to(dtype), None, None, None, None, None, None
+
+
+@register("roi_align")
+def roi_align(data, rois, spatial_scale, out_h, out_w, sampling_ratio=2, aligned=True):
+    """Bilinear ROI align on the device (detection.hip); fp32 output cast to ``data.dtype``,
+    differentiable w.r.t. ``data``."""
+    if not (data.is_cuda and data.dim() == 4 and data.dtype in (_f32, _bf16) and rois.dim() == 2
+            and rois.shape[1] == 5 and rois.shape[0] > 0 and min(data.shape) > 0):
+        return NotImplemented
+    r = rois.detach().float().contiguous().to(data.device)
+    y = _RoiAlignFn.apply(data, r, float(spatial_scale), int(out_h), int(out_w), int(sampling_ratio), bool(aligned))
+    return y.to(data.dtype)
