@@ -38,7 +38,7 @@ struct GemmParams {
 template <int BK>
 __device__ __forceinline__ int gswz(int row, int chunk) {
   if constexpr (BK == 64) return row * BK + ((chunk ^ (row & 7)) << 3);
-  else return row * BK + ((chunk ^ ((row >> 2) & 3)) << 3);
+  else return row * BK + ((chunk ^ ((row >> 2) & 2)) << 3);  // conflict-free for the b128 lane groups
 }
 
 __device__ __forceinline__ int gxcd_remap(int bid, int nwg) {
