@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import ops
+from ...ops import vml
 from ..abstractnn import TensorModule, AutogradModule
 from ...utils import acc_float
 
@@ -46,21 +47,27 @@ class ReLU(Threshold):
 
 
 class Tanh(TensorModule):
+    """``Tanh.scala`` (VML vsTanh); device tensors run the vml.hip kernels forward and backward."""
+
     def updateOutput(self, input):
-        return torch.tanh(input)
+        r = vml.unary(input, "tanh")
+        return r if r is not None else torch.tanh(input)
 
     def updateGradInput(self, input, gradOutput):
         y = self.output
-        return gradOutput * (1 - y * y)
+        r = vml.binary(gradOutput, y, "tanh_bwd")
+        return r if r is not None else gradOutput * (1 - y * y)
 
 
 class Sigmoid(TensorModule):
     def updateOutput(self, input):
-        return torch.sigmoid(input)
+        r = vml.unary(input, "sigmoid")
+        return r if r is not None else torch.sigmoid(input)
 
     def updateGradInput(self, input, gradOutput):
         y = self.output
-        return gradOutput * y * (1 - y)
+        r = vml.binary(gradOutput, y, "sigmoid_bwd")
+        return r if r is not None else gradOutput * y * (1 - y)
 
 
 class LogSoftMax(TensorModule):

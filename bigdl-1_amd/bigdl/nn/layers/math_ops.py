@@ -9,6 +9,7 @@ import torch
 
 from ..abstractnn import TensorModule, AutogradModule
 from ..initialization_method import RandomUniform
+from ...ops import vml
 from .shape import _bdim
 
 
@@ -111,29 +112,76 @@ class Power(AutogradModule):
         return torch.pow(self.shift + self.scale * x, self.power)
 
 
-class Sqrt(AutogradModule):
-    def _forward(self, x):
+class _Elementwise(TensorModule):
+    """y = f(x) with an explicit gradient: device tensors run the ``ops/csrc/vml.hip`` kernels
+    (the reference's VML calls), host tensors the torch formulas.  ``_saved`` names the forward
+    value the gradient needs ("output" or "input")."""
+    _op = _bwd = None
+    _saved = "output"
+
+    def _f(self, x):
+        raise NotImplementedError
+
+    def _df(self, x, y, g):
+        raise NotImplementedError
+
+    def updateOutput(self, input):
+        r = vml.unary(input, self._op)
+        return r if r is not None else self._f(input)
+
+    def updateGradInput(self, input, gradOutput):
+        r = vml.binary(gradOutput, self.output if self._saved == "output" else input, self._bwd)
+        return r if r is not None else self._df(input, self.output, gradOutput)
+
+
+class Sqrt(_Elementwise):
+    _op, _bwd = "sqrt", "sqrt_bwd"
+
+    def _f(self, x):
         return torch.sqrt(x)
 
+    def _df(self, x, y, g):
+        return 0.5 * g / y
 
-class Square(AutogradModule):
-    def _forward(self, x):
+
+class Square(_Elementwise):
+    _op, _bwd, _saved = "square", "square_bwd", "input"
+
+    def _f(self, x):
         return x * x
 
+    def _df(self, x, y, g):
+        return 2.0 * g * x
 
-class Exp(AutogradModule):
-    def _forward(self, x):
+
+class Exp(_Elementwise):
+    _op, _bwd = "exp", "exp_bwd"
+
+    def _f(self, x):
         return torch.exp(x)
 
+    def _df(self, x, y, g):
+        return g * y
 
-class Log(AutogradModule):
-    def _forward(self, x):
+
+class Log(_Elementwise):
+    _op, _bwd, _saved = "log", "log_bwd", "input"
+
+    def _f(self, x):
         return torch.log(x)
 
+    def _df(self, x, y, g):
+        return g / x
 
-class Abs(AutogradModule):
-    def _forward(self, x):
+
+class Abs(_Elementwise):
+    _op, _bwd, _saved = "abs", "abs_bwd", "input"
+
+    def _f(self, x):
         return torch.abs(x)
+
+    def _df(self, x, y, g):
+        return g * torch.sign(x)
 
 
 class Negative(AutogradModule):

@@ -1583,3 +1583,69 @@ def roi_align(data, rois, spatial_scale, out_h, out_w, sampling_ratio=2, aligned
     r = rois.detach().float().contiguous().to(data.device)
     y = _RoiAlignFn.apply(data, r, float(spatial_scale), int(out_h), int(out_w), int(sampling_ratio), bool(aligned))
     return y.to(data.dtype)
+
+
+# ------------------------------------------------------------------------------------------------ vector math
+# op codes of ops/csrc/vml.hip
+VML_UNARY = {"abs": 0, "exp": 1, "log": 2, "log1p": 3, "sqrt": 4, "tanh": 5, "sigmoid": 6, "pow": 7,
+             "square": 8, "inv": 9, "neg": 10, "affine": 11}
+VML_BINARY = {"add": 0, "sub": 1, "mul": 2, "div": 3, "tanh_bwd": 4, "sigmoid_bwd": 5, "sqrt_bwd": 6,
+              "log_bwd": 7, "exp_bwd": 8, "square_bwd": 9, "abs_bwd": 10, "pow_bwd": 11}
+REDUCE = {"sum": 0, "mean": 1, "max": 2, "min": 3}
+
+
+def _vml_ok(*ts):
+    t0 = ts[0]
+    return all(t is not None and t.is_cuda and t.dtype == t0.dtype and t.dtype in (_f32, _bf16) and t.is_contiguous()
+               and t.numel() == t0.numel() and _al16(t) for t in ts) and t0.numel() > 0
+
+
+@register("vml_unary")
+def vml_unary(x, op, p=0.0, q=0.0, out=None):
+    """Elementwise ``op`` (a VML_UNARY name) of a contiguous fp32/bf16 device tensor; ``out`` may
+    alias ``x`` (in place).  pow: x**p; affine: x·p + q."""
+    y = torch.empty_like(x) if out is None else out
+    if not _vml_ok(x, y):
+        return NotImplemented
+    check(_lib().bigdl_vml_unary(C.c_int(VML_UNARY[op]), C.c_int(0 if x.dtype == _f32 else 1), ptr(x), ptr(y),
+                                 _ll(x.numel()), _f(p), _f(q), _s()), "vml_unary")
+    return y
+
+
+@register("vml_binary")
+def vml_binary(a, b, op, p=1.0, out=None):
+    """Elementwise ``op`` (a VML_BINARY name) of two same-shape contiguous device tensors
+    (add/sub: a ± p·b; *_bwd: a = upstream gradient, b = saved forward value; pow_bwd uses p)."""
+    z = torch.empty_like(a) if out is None else out
+    if not _vml_ok(a, b, z) or a.shape != b.shape:
+        return NotImplemented
+    check(_lib().bigdl_vml_binary(C.c_int(VML_BINARY[op]), C.c_int(0 if a.dtype == _f32 else 1), ptr(a), ptr(b),
+                                  ptr(z), _ll(a.numel()), _f(p), _s()), "vml_binary")
+    return z
+
+
+@register("reduce")
+def reduce(x, op, dim=None, keepdim=False):
+    """sum / mean / max / min of a contiguous fp32/bf16 device tensor over ``dim`` (None: all
+    elements), fp32 result (deterministic two-level order)."""
+    if not (x.is_cuda and x.dtype in (_f32, _bf16) and x.is_contiguous() and x.numel() > 0):
+        return NotImplemented
+    shape = list(x.shape)
+    if dim is None:
+        outer, n, inner = 1, x.numel(), 1
+        oshape = [1] * len(shape) if keepdim else []
+    else:
+        d = dim % max(1, x.dim())
+        outer = 1
+        for s_ in shape[:d]:
+            outer *= s_
+        inner = 1
+        for s_ in shape[d + 1:]:
+            inner *= s_
+        n = shape[d]
+        oshape = shape[:d] + ([1] if keepdim else []) + shape[d + 1:]
+    out = torch.empty(outer * inner, dtype=_f32, device=x.device)
+    scratch = torch.empty(max(outer * 64, 8192), dtype=_f32, device=x.device)
+    check(_lib().bigdl_reduce(C.c_int(REDUCE[op]), C.c_int(0 if x.dtype == _f32 else 1), ptr(x), _ll(outer), _ll(n),
+                              _ll(inner), ptr(out), ptr(scratch), _ll(scratch.numel()), _s()), "reduce")
+    return out.view(oshape)

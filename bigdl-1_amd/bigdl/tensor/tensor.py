@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from ..utils.random import RNG
+from ..ops import vml as _vml
 
 
 def _dim0(d: int, nd: int) -> int:
@@ -23,6 +24,10 @@ def _dim0(d: int, nd: int) -> int:
     if d < 1 or d > nd:
         raise IndexError(f"dimension {d} out of range [1, {nd}]")
     return d - 1
+
+
+_VML_UNARY = {torch.abs: "abs", torch.exp: "exp", torch.log: "log", torch.log1p: "log1p", torch.sqrt: "sqrt",
+              torch.tanh: "tanh", torch.sigmoid: "sigmoid", torch.neg: "neg", torch.reciprocal: "inv"}
 
 
 def _unwrap(x):
@@ -267,13 +272,21 @@ class Tensor:
         return self
 
     # ---- arithmetic (TensorMath) ---------------------------------------------------------------------
+    def _vml2(self, other, op, p=1.0) -> bool:
+        """in-place ``self ← self (op) other`` through the VML kernels (same-shape device tensors)."""
+        o = _unwrap(other)
+        return (isinstance(o, torch.Tensor) and self.data.is_cuda and o.shape == self.data.shape
+                and _vml.binary(self.data, o, op, p, out=self.data) is not None)
+
     def add(self, *args):
         """add(value) | add(y) | add(value, y) | add(x, value, y) (Torch overloads)."""
         if len(args) == 1:
             a = _unwrap(args[0])
-            self.data.add_(a)
+            if not self._vml2(a, "add"):
+                self.data.add_(a)
         elif len(args) == 2:
-            self.data.add_(_unwrap(args[1]), alpha=args[0])
+            if not self._vml2(args[1], "add", float(args[0])):
+                self.data.add_(_unwrap(args[1]), alpha=args[0])
         else:
             x, v, y = args
             self.data.copy_(_unwrap(x) + v * _unwrap(y))
@@ -281,8 +294,9 @@ class Tensor:
 
     def sub(self, *args):
         if len(args) == 1:
-            self.data.sub_(_unwrap(args[0]))
-        else:
+            if not self._vml2(args[0], "sub"):
+                self.data.sub_(_unwrap(args[0]))
+        elif not self._vml2(args[1], "sub", float(args[0])):
             self.data.sub_(_unwrap(args[1]), alpha=args[0])
         return self
 
@@ -299,14 +313,16 @@ class Tensor:
 
     def cmul(self, *args):
         if len(args) == 1:
-            self.data.mul_(_unwrap(args[0]))
+            if not self._vml2(args[0], "mul"):
+                self.data.mul_(_unwrap(args[0]))
         else:
             self.data.copy_(_unwrap(args[0]) * _unwrap(args[1]))
         return self
 
     def cdiv(self, *args):
         if len(args) == 1:
-            self.data.div_(_unwrap(args[0]))
+            if not self._vml2(args[0], "div"):
+                self.data.div_(_unwrap(args[0]))
         else:
             self.data.copy_(_unwrap(args[0]) / _unwrap(args[1]))
         return self
@@ -384,6 +400,9 @@ class Tensor:
 
     # elementwise unary (return new tensors like Torch's functional forms, or in place with no args)
     def _unary(self, fn, inplace=True):
+        op = _VML_UNARY.get(fn)
+        if op is not None and self.data.is_cuda and _vml.unary(self.data, op, out=self.data) is not None:
+            return self
         r = fn(self.data)
         self.data.copy_(r)
         return self
@@ -434,7 +453,9 @@ class Tensor:
         return self._unary(torch.digamma)
 
     def pow(self, n):
-        self.data.pow_(n)
+        if not (isinstance(n, (int, float)) and self.data.is_cuda
+                and _vml.unary(self.data, "pow", float(n), out=self.data) is not None):
+            self.data.pow_(n)
         return self
 
     def square(self):
@@ -445,12 +466,27 @@ class Tensor:
         return self
 
     # ---- reductions ---------------------------------------------------------------------------------
+    def _vml_reduce(self, op, dim):
+        d = self.data
+        if not d.is_cuda:
+            return None
+        r = _vml.reduce(d, op, None if dim is None else _dim0(dim, d.dim()), keepdim=True)
+        if r is None:
+            return None
+        return float(r) if dim is None else Tensor(r.to(d.dtype))
+
     def sum(self, dim: int | None = None):
+        r = self._vml_reduce("sum", dim)
+        if r is not None:
+            return r
         if dim is None:
             return float(self.data.sum())
         return Tensor(self.data.sum(_dim0(dim, self.data.dim()), keepdim=True))
 
     def mean(self, dim: int | None = None):
+        r = self._vml_reduce("mean", dim)
+        if r is not None:
+            return r
         if dim is None:
             return float(self.data.float().mean())
         return Tensor(self.data.mean(_dim0(dim, self.data.dim()), keepdim=True))
@@ -462,13 +498,15 @@ class Tensor:
 
     def max(self, dim: int | None = None):
         if dim is None:
-            return float(self.data.max())
+            r = self._vml_reduce("max", None)
+            return r if r is not None else float(self.data.max())
         v, i = self.data.max(_dim0(dim, self.data.dim()), keepdim=True)
         return Tensor(v), Tensor((i + 1).float())
 
     def min(self, dim: int | None = None):
         if dim is None:
-            return float(self.data.min())
+            r = self._vml_reduce("min", None)
+            return r if r is not None else float(self.data.min())
         v, i = self.data.min(_dim0(dim, self.data.dim()), keepdim=True)
         return Tensor(v), Tensor((i + 1).float())
 
