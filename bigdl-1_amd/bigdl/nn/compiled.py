@@ -1,0 +1,259 @@
+"""Two-phase execution: plan a model once for a fixed input shape, then run it repeatedly.
+
+The reference compiles its MKL-DNN graphs in a separate phase (``nn/mkldnn/DnnGraph.scala``
+``compile(phase)`` → ``initFwdPrimitives`` / ``initBwdPrimitives``: input formats fixed, memory
+descriptors chosen, reorders inserted, buffers allocated) before the first iteration.  Here the
+same split is:
+
+* **plan** (:func:`plan`): one forward at the target shape with every leaf module instrumented —
+  per-layer input/output shapes, dtypes and memory layout (NCHW vs the NHWC device layout the
+  conv path switches to: the "reorder" points), the activation buffers (by storage, so views are
+  one buffer), their live ranges in execution order, the peak live bytes and a first-fit offset
+  assignment of every buffer into one workspace (what an arena allocator for this shape needs);
+* **execute** (:class:`CompiledModule`): on a GPU and in the inference phase the forward is
+  captured once into a HIP graph with a static input buffer — every kernel and every workspace
+  allocation of the forward is then fixed (the graph's private memory pool), and each call is a
+  copy-in plus one graph replay, with no per-layer host dispatch.  Models whose forward syncs with
+  the host (data-dependent shapes, ``.item()``) cannot be captured and run eagerly with a warning.
+
+``compile(model, example, phase)`` does both.
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from ..utils.table import Table
+
+_log = logging.getLogger("bigdl.nn.compiled")
+
+
+def _leaves(m) -> List:
+    subs = getattr(m, "modules", None)
+    if isinstance(subs, list) and subs and all(hasattr(s, "updateOutput") for s in subs):
+        out = []
+        for s in subs:
+            out.extend(_leaves(s))
+        return out
+    return [m]
+
+
+def _tensors(a) -> List[torch.Tensor]:
+    if isinstance(a, torch.Tensor):
+        return [a]
+    if isinstance(a, Table):
+        return [t for v in a.values() for t in _tensors(v)]
+    if isinstance(a, (list, tuple)):
+        return [t for v in a for t in _tensors(v)]
+    return []
+
+
+def _layout(t: torch.Tensor) -> str:
+    if t.dim() == 4:
+        if t.is_contiguous():
+            return "NCHW"
+        if t.is_contiguous(memory_format=torch.channels_last):
+            return "NHWC"
+    return "dense" if t.is_contiguous() else "strided"
+
+
+@dataclass
+class LayerRecord:
+    index: int
+    name: str
+    kind: str
+    in_shapes: List[tuple]
+    out_shapes: List[tuple]
+    out_dtype: str
+    in_layout: str
+    out_layout: str
+    out_bytes: int
+
+
+@dataclass
+class Buffer:
+    key: int
+    nbytes: int
+    first: int
+    last: int
+    offset: int = -1
+
+
+@dataclass
+class Plan:
+    phase: str
+    input_shape: tuple
+    layers: List[LayerRecord] = field(default_factory=list)
+    buffers: List[Buffer] = field(default_factory=list)
+    reorders: List[int] = field(default_factory=list)   # layer indices whose output layout differs from their input's
+    peak_bytes: int = 0
+    arena_bytes: int = 0
+    total_bytes: int = 0
+
+    def summary(self) -> str:
+        mb = 1 / 2 ** 20
+        lines = [f"plan ({self.phase}) input {self.input_shape}: {len(self.layers)} layers, "
+                 f"{len(self.buffers)} activation buffers, total {self.total_bytes * mb:.1f} MiB, "
+                 f"peak live {self.peak_bytes * mb:.1f} MiB, arena {self.arena_bytes * mb:.1f} MiB, "
+                 f"{len(self.reorders)} layout changes"]
+        for r in self.layers:
+            lines.append(f"  {r.index:4d} {r.kind:28s} {str(r.in_shapes[:1]):24s} -> {str(r.out_shapes[:1]):24s} "
+                         f"{r.in_layout}->{r.out_layout} {r.out_dtype}")
+        return "\n".join(lines)
+
+
+def _assign_offsets(bufs: List[Buffer], align: int = 256) -> int:
+    """First-fit placement, largest first, of buffers whose live ranges overlap in time."""
+    placed: List[Buffer] = []
+    top = 0
+    for b in sorted(bufs, key=lambda x: (-x.nbytes, x.first)):
+        size = (b.nbytes + align - 1) // align * align
+        busy = sorted((p.offset, p.offset + (p.nbytes + align - 1) // align * align) for p in placed
+                      if not (p.last < b.first or b.last < p.first))
+        off = 0
+        for lo, hi in busy:
+            if off + size <= lo:
+                break
+            off = max(off, hi)
+        b.offset = off
+        placed.append(b)
+        top = max(top, off + size)
+    return top
+
+
+def plan(model, example, phase: str = "inference") -> Plan:
+    """Run one forward of ``model`` on ``example`` with instrumented leaf modules and build the
+    shape / layout / workspace plan (``phase``: "inference" frees a buffer after its last use,
+    "training" keeps every activation for the backward)."""
+    if phase not in ("inference", "training"):
+        raise ValueError(phase)
+    leaves = _leaves(model)
+    records: List[LayerRecord] = []
+    uses: Dict[int, List[int]] = {}
+    sizes: Dict[int, int] = {}
+    first: Dict[int, int] = {}
+    in_keys = set()
+
+    def key(t):
+        return t.untyped_storage().data_ptr()
+
+    for t in _tensors(example):
+        in_keys.add(key(t))
+
+    def wrap(m):
+        orig = m.updateOutput
+
+        def rec(inp):
+            out = orig(inp)
+            i = len(records)
+            ins, outs = _tensors(inp), _tensors(out)
+            for t in ins + outs:
+                k = key(t)
+                uses.setdefault(k, []).append(i)
+                sizes[k] = max(sizes.get(k, 0), t.untyped_storage().nbytes())
+                first.setdefault(k, i)
+            il = _layout(ins[0]) if ins else "-"
+            ol = _layout(outs[0]) if outs else "-"
+            records.append(LayerRecord(i, getattr(m, "getName", lambda: type(m).__name__)(), type(m).__name__,
+                                       [tuple(t.shape) for t in ins], [tuple(t.shape) for t in outs],
+                                       str(outs[0].dtype).replace("torch.", "") if outs else "-", il, ol,
+                                       sum(t.untyped_storage().nbytes() for t in outs)))
+            return out
+        m.updateOutput = rec
+
+    was_training = model.isTraining()
+    for m in leaves:
+        wrap(m)
+    try:
+        if phase == "inference":
+            model.evaluate()
+        with torch.no_grad():
+            out = model.forward(example)
+    finally:
+        for m in leaves:
+            m.__dict__.pop("updateOutput", None)
+        if was_training:
+            model.training()
+    n = len(records)
+    out_keys = {key(t) for t in _tensors(out)}
+    bufs = []
+    for k, idx in uses.items():
+        if k in in_keys:
+            continue  # the caller's input, not a workspace
+        last = n if (k in out_keys or phase == "training") else max(idx)
+        bufs.append(Buffer(k, sizes[k], first[k], last))
+    p = Plan(phase, tuple(_tensors(example)[0].shape) if _tensors(example) else (), records, bufs)
+    p.reorders = [r.index for r in records if r.in_layout in ("NCHW", "NHWC") and r.out_layout in ("NCHW", "NHWC")
+                  and r.in_layout != r.out_layout]
+    p.total_bytes = sum(b.nbytes for b in bufs)
+    live = [0] * (n + 1)
+    for b in bufs:
+        for i in range(b.first, min(b.last, n) + 1):
+            live[i] += b.nbytes
+    p.peak_bytes = max(live) if live else 0
+    p.arena_bytes = _assign_offsets(bufs)
+    return p
+
+
+class CompiledModule:
+    """``model`` planned for ``example``'s shape; in the inference phase on a GPU the forward is a
+    captured HIP graph (``graph=False`` forces eager execution).  The returned output tensor is the
+    graph's static output buffer: it is overwritten by the next call (clone it to keep it)."""
+
+    def __init__(self, model, example, phase: str = "inference", graph: Optional[bool] = None, warmup: int = 2):
+        self.model, self.phase = model, phase
+        self.plan = plan(model, example, phase)
+        ex = _tensors(example)
+        self.graph = None
+        want = graph if graph is not None else (phase == "inference" and bool(ex) and ex[0].is_cuda)
+        if want and isinstance(example, torch.Tensor) and example.is_cuda:
+            try:
+                self._capture(example, warmup)
+            except Exception as e:  # noqa: BLE001 - host-synchronising forward: stay eager
+                _log.warning("HIP graph capture of %s failed (%s); running eagerly", type(model).__name__, e)
+                self.graph = None
+
+    def _capture(self, example, warmup):
+        m = self.model
+        m.evaluate()
+        self.static_in = example.detach().clone()
+        side = torch.cuda.Stream(device=example.device)
+        side.wait_stream(torch.cuda.current_stream(example.device))
+        with torch.cuda.stream(side), torch.no_grad():
+            for _ in range(max(1, warmup)):
+                m.forward(self.static_in)
+        torch.cuda.current_stream(example.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(g):
+            self.static_out = m.forward(self.static_in)
+        self.graph = g
+
+    @property
+    def captured(self) -> bool:
+        return self.graph is not None
+
+    def forward(self, x):
+        if self.graph is None:
+            if self.phase == "inference":
+                self.model.evaluate()
+                with torch.no_grad():
+                    return self.model.forward(x)
+            return self.model.forward(x)
+        if tuple(x.shape) != tuple(self.static_in.shape):
+            raise ValueError(f"compiled for input {tuple(self.static_in.shape)}, got {tuple(x.shape)}")
+        self.static_in.copy_(x)
+        self.graph.replay()
+        return self.static_out
+
+    __call__ = forward
+
+
+def compile(model, example, phase: str = "inference", graph: Optional[bool] = None) -> CompiledModule:  # noqa: A001
+    """Plan ``model`` for ``example``'s shape and return the executor (see module docstring)."""
+    return CompiledModule(model, example, phase, graph)
+
+
+__all__ = ["plan", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer"]

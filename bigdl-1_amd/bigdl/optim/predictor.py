@@ -86,14 +86,32 @@ def _batches(data, batch_size: int):
 
 
 class LocalPredictor:
-    def __init__(self, model, feature_padding=None, batch_size: int = -1):
+    """``compiled=True`` (or ``bigdl.predict.compiled``): on a GPU each distinct batch shape is
+    planned once and its forward captured into a HIP graph (``nn/compiled.py``), later batches of
+    that shape are a copy-in plus one graph replay."""
+
+    def __init__(self, model, feature_padding=None, batch_size: int = -1, compiled: Optional[bool] = None):
         self.model = model
         self.batch_size = batch_size if batch_size > 0 else 4 * max(1, Engine.core_number())
         self.feature_padding = feature_padding
+        self.compiled = compiled
+        self._graphs = {}
 
     @staticmethod
     def create(model, batch_size=-1, feature_padding=None):
         return LocalPredictor(model, feature_padding, batch_size)
+
+    def _run(self, m, x):
+        from ..utils import config
+        use = self.compiled if self.compiled is not None else bool(config.get_property("bigdl.predict.compiled"))
+        if not (use and isinstance(x, torch.Tensor) and x.is_cuda):
+            return m.forward(x)
+        key = (tuple(x.shape), x.dtype)
+        c = self._graphs.get(key)
+        if c is None:
+            from ..nn.compiled import compile as compile_module
+            c = self._graphs[key] = compile_module(m, x)
+        return c(x)
 
     def _forward_all(self, data):
         m = self.model
@@ -108,7 +126,7 @@ class LocalPredictor:
             with torch.no_grad():
                 for b in _batches(data, self.batch_size):
                     b = b.to(dev, dtype=Engine.compute_dtype() if dev.type == "cuda" else None)
-                    out = m.forward(b.getInput())
+                    out = self._run(m, b.getInput())
                     outs.extend(_split_batch(_to_host(out), b.size()))
         finally:
             if was_training:

@@ -47,6 +47,7 @@ _REGISTRY = {
     # observability
     "bigdl.metrics.jsonPath": (str, "", "per-rank JSON metrics stream: one line per iteration to <path>.rank<r>.jsonl ('' = off)"),
     "bigdl.metrics.deviceTimers": (bool, False, "time the distributed phases with HIP events (adds no host sync)"),
+    "bigdl.predict.compiled": (bool, False, "LocalPredictor: plan each batch shape once and replay its forward as a HIP graph"),
     "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),

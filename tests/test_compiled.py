@@ -1,0 +1,70 @@
+"""Two-phase execution (nn/compiled.py; reference nn/mkldnn/DnnGraph.scala compile(phase)):
+the shape / layout / workspace plan on the host, and the HIP-graph executor on a GPU."""
+import pytest
+import torch
+
+
+def _cnn():
+    import bigdl.nn as nn
+    m = nn.Sequential()
+    m.add(nn.SpatialConvolution(3, 8, 3, 3, 1, 1, 1, 1)).add(nn.SpatialBatchNormalization(8)).add(nn.ReLU())
+    m.add(nn.SpatialMaxPooling(2, 2, 2, 2)).add(nn.SpatialConvolution(8, 16, 3, 3, 1, 1, 1, 1)).add(nn.ReLU())
+    m.add(nn.View(16 * 8 * 8)).add(nn.Linear(16 * 8 * 8, 10)).add(nn.LogSoftMax())
+    return m
+
+
+def test_plan_shapes_and_workspace():
+    from bigdl.nn.compiled import plan
+    m = _cnn()
+    x = torch.randn(4, 3, 16, 16)
+    p = plan(m, x, "inference")
+    kinds = [r.kind for r in p.layers]
+    assert kinds[0] == "SpatialConvolution" and kinds[-1] == "LogSoftMax"
+    assert p.layers[0].out_shapes[0] == (4, 8, 16, 16)
+    assert p.layers[-1].out_shapes[0] == (4, 10)
+    # inference frees buffers after their last use: peak and arena below the sum of all outputs
+    assert 0 < p.peak_bytes <= p.arena_bytes <= p.total_bytes
+    assert p.peak_bytes < p.total_bytes
+    # no two buffers that are live at the same time overlap in the arena
+    for a in p.buffers:
+        for b in p.buffers:
+            if a is b or a.last < b.first or b.last < a.first:
+                continue
+            assert a.offset + a.nbytes <= b.offset or b.offset + b.nbytes <= a.offset
+    tr = plan(m, x, "training")
+    assert tr.peak_bytes >= p.peak_bytes and tr.peak_bytes == tr.total_bytes
+    assert m.isTraining()  # planning restores the mode
+    assert "LogSoftMax" in p.summary()
+
+
+def test_compiled_eager_on_host_matches_model():
+    from bigdl.nn.compiled import compile
+    m = _cnn()
+    x = torch.randn(2, 3, 16, 16)
+    c = compile(m, x)
+    assert not c.captured
+    m.evaluate()
+    torch.testing.assert_close(c(x), m.forward(x))
+
+
+@pytest.mark.gpu
+def test_compiled_hip_graph_inference():
+    from bigdl.nn.compiled import compile
+    from bigdl.utils.engine import Engine
+    from bigdl.models.resnet import ResNet
+    Engine.init(device="cuda:0")
+    torch.manual_seed(0)
+    m = ResNet(10, depth=20).to(device="cuda")
+    x = torch.randn(8, 3, 32, 32, device="cuda")
+    c = compile(m, x)
+    assert c.captured
+    for seed in (1, 2):
+        xi = torch.randn(8, 3, 32, 32, device="cuda", generator=torch.Generator("cuda").manual_seed(seed))
+        m.evaluate()
+        with torch.no_grad():
+            ref = m.forward(xi).float().clone()
+        got = c(xi).float()
+        torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    p = c.plan
+    assert any(r.out_layout == "NHWC" for r in p.layers)  # the conv path's device layout
+    assert p.reorders  # NCHW input → NHWC conv output at least once
