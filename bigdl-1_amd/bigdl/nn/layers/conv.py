@@ -190,12 +190,13 @@ class SpatialConvolution(TensorModule):
         bn = self._stats_consumer(x) if batched else None
         y = NotImplemented
         if bn is not None and ops.native_has("conv2d_forward"):
+            shift = bn.runningMean if config.get_property("bigdl.bn.shiftedStats") else None
             r = ops.native_ops.conv2d_forward_stats(x, w4, b, (self.strideH, self.strideW), pad,
                                                 (self.dilationH, self.dilationW), self.nGroup,
-                                                pad_slot=self._pad_slot_())
+                                                pad_slot=self._pad_slot_(), shift=shift)
             if r is not NotImplemented:
                 y, part, G = r
-                bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G)
+                bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G, shift)
         if y is NotImplemented:
             tgt, self._out_target = self._out_target, None
             if tgt is not None and (not batched or self.format != "NCHW"):

@@ -162,7 +162,7 @@ class BatchNormalization(TensorModule):
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
-                        relu=relu, residual=residual, in_bias=ib, coef_out=coef)
+                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4])
                 if r is NotImplemented:
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
                                                     self.momentum, self.eps, relu=relu, residual=residual,

@@ -117,11 +117,12 @@ __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, i
 // ``in_bias`` (optional) is a per-channel constant the producer did NOT add to x (a conv bias folded
 // into this BN): normalisation is shift-invariant, so only the running mean sees it.
 template <typename T>
-__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const T* __restrict__ partial,
+__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const float* kshift,
+                                                      const T* __restrict__ partial,
                                                       int G, long long M, int C, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
                                                       const float* __restrict__ in_bias,
-                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                      float* run_mean, float* __restrict__ run_var,
                                                       float momentum, float eps, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
                                                       float* __restrict__ shift) {
@@ -130,8 +131,10 @@ __global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
-  // partials are shifted by the first row (standalone stats pass) or unshifted (conv epilogue)
-  const float K = x ? bf2f(x[c]) : 0.f;
+  // partials are shifted by the first row (standalone stats pass), by ``kshift`` (conv epilogue
+  // given the running mean — it may alias run_mean: read here, before run_mean is written below,
+  // hence neither pointer is __restrict__) or unshifted
+  const float K = kshift ? kshift[c] : (x ? bf2f(x[c]) : 0.f);
   const double dmd = s / (double)M;
   const float var = (float)fmax(q / (double)M - dmd * dmd, 0.0);
   const float dm = (float)dmd;
@@ -241,7 +244,8 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
-  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, (const float*)ws, G,
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, nullptr,
+                     (const float*)ws, G,
                      M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
@@ -308,16 +312,17 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
                                              const float* gamma, const float* beta, const float* in_bias,
                                              float* run_mean, float* run_var, float momentum, float eps,
                                              float* save_mean, float* save_invstd, const float* partial, int G,
-                                             float* coef, int relu, float* scratch, hipStream_t s) {
+                                             const float* kshift, float* coef, int relu, float* scratch,
+                                             hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
   if (maybe_fold(partial, G, C, scratch, s))
-    hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr,
+    hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
                        (const double*)scratch, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                        save_invstd, coef, coef + C);
   else
-    hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, partial, G,
-                       M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
-                       coef + C);
+    hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
+                       partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd,
+                       coef, coef + C);
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;

@@ -54,6 +54,10 @@ struct ConvParams {
   // weight row stride in elements (== Kg, or Kg rounded up to 8 for the C = 4 stem, whose rows are
   // zero-padded so every weight chunk stays 16-B aligned)
   int ldw;
+  // optional per-channel shift K of the BN statistics partials: Σ(y − K), Σ(y − K)² instead of the
+  // raw sums, so E[y²] − E[y]² never cancels catastrophically (the BN passes its running mean —
+  // any value is exact, one near the batch mean keeps the variance well conditioned)
+  const float* stat_shift;
 };
 
 constexpr int SBM = 128;  // row granularity of the BN-statistics partials (any BM writes BM / SBM rows)
@@ -352,14 +356,23 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+      float k4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.stat_shift) {
+        const int nk = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
 #pragma unroll
-      for (int j = 0; j < TM; ++j)
+        for (int e = 0; e < 4; ++e) k4[e] = nk + e < p.K ? p.stat_shift[nk + e] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        // rows past M (the last tile's padding) hold acc = 0 and must stay 0 after the shift
+        const float live = (m0 + wave_m * (BM / 2) + j * 16 + fr < p.M) ? 1.f : 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = acc[i][j][e];
+          const float a = fmaf(-live, k4[e], acc[i][j][e]);
           s4[e] += a;
           q4[e] = fmaf(a, a, q4[e]);
         }
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x128, 0xF, 0xF, false));
@@ -426,6 +439,9 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   }
   float s8[8], q8[8];
   const bool full = n + 8 <= p.K;
+  float sk[8];  // statistics shift of this thread's 8 channels
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sk[e] = (p.stat_shift && p.stats && !p.bnx && n + e < p.K) ? p.stat_shift[n + e] : 0.f;
   float bsc[8], bsh[8], bmu[8];
   if (p.bnx && full) {
 #pragma unroll
@@ -511,7 +527,8 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
         const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = __uint_as_float(uw[e] << 16), b = __uint_as_float(uw[e] & 0xFFFF0000u);
+          const float a = __uint_as_float(uw[e] << 16) - sk[2 * e];
+          const float b = __uint_as_float(uw[e] & 0xFFFF0000u) - sk[2 * e + 1];
           s8[2 * e] += a;
           q8[2 * e] = fmaf(a, a, q8[2 * e]);
           s8[2 * e + 1] += b;
@@ -526,7 +543,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
         if (p.relu) t = fmaxf(t, 0.f);
         const bf16_t o = f2bf(t);
         p.y[yoff + e] = o;
-        const float w = bf2f(o);
+        const float w = bf2f(o) - sk[e];
         s8[e] += w;
         q8[e] = fmaf(w, w, q8[e]);
       }
@@ -600,7 +617,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
-                           hipStream_t s, int ldw = 0) {
+                           hipStream_t s, int ldw = 0, const float* stat_shift = nullptr) {
   const bool c4 = C == 4;
   // any K: partial 8-channel chunks are stored per element in the epilogue
   if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -618,6 +635,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.y = (bf16_t*)y;
   p.res = (const bf16_t*)res;
   p.stats = stats;
+  p.stat_shift = stats ? stat_shift : nullptr;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
   long long Ml = (long long)Nb * P * Q;
@@ -704,6 +722,22 @@ BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias,
                                 int relu, hipStream_t s) {
   return bigdl_conv_fwd_ex(x, w, bias, nullptr, y, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu,
                            s);
+}
+
+// Forward conv + shifted BN statistics partials (``shift``: per-output-channel K, see ConvParams).
+BIGDL_EXPORT int bigdl_conv_fwd_stats_shift(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                            const float* shift, int Nb, int H, int W, int C, int K, int R, int S,
+                                            int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                                            hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, nullptr, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, 0, shift);
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd_c4_stats_shift(const void* x, const void* w, int ldw, const float* bias, void* y,
+                                               float* stats, const float* shift, int Nb, int H, int W, int K, int R,
+                                               int S, int P, int Q, int sh, int sw, int ph, int pw, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, nullptr, y, stats, Nb, H, W, 4, K, R, S, P, Q, sh, sw, ph, pw, 1, 1, 0, 1, 1, 0,
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw, shift);
 }
 
 // 4-channel (RGB-padded) input with weight rows ldw elements apart (ldw % 8 == 0, zero beyond R·S·4).

@@ -145,7 +145,7 @@ def _coef_ok(t, C_):
 
 
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
-                                    relu=False, residual=None, in_bias=None, coef_out=None):
+                                    relu=False, residual=None, in_bias=None, coef_out=None, shift=None):
     """Training BN whose statistics were produced by the preceding conv's epilogue
     (:func:`conv2d_forward_stats`): finalize + apply only."""
     rc = _rows_c(x)
@@ -166,7 +166,8 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     check(_lib().bigdl_bn_fwd_train_partials(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
                                              ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
                                              _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
-                                             C.c_int(G), ptr(coef), C.c_int(1 if relu else 0),
+                                             C.c_int(G), ptr(shift if _f32vec(shift, C_) else None), ptr(coef),
+                                             C.c_int(1 if relu else 0),
                                              ptr(_fold_scratch(G, C_, x.device)), _s()),
           "bn_fwd_train_partials")
     return y, mean, invstd
@@ -333,7 +334,7 @@ def _conv_geom_ok(x, w4, groups, dilation):
 
 
 def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None,
-                   pad_slot=None):
+                   pad_slot=None, shift=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
     writes into directly (zero-copy concat); returned as the result."""
     if not _conv_geom_ok(x, w4, groups, dilation):
@@ -383,10 +384,23 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     if stats:
         G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
         part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
+    if shift is not None and not (stats and res is None and not relu and out is None and tuple(dilation) == (1, 1)
+                                  and _f32vec(shift, K)):
+        shift = None
     if c4:
+        if shift is not None:
+            check(_lib().bigdl_conv_fwd_c4_stats_shift(ptr(x), ptr(wk), ldw, ptr(bias), ptr(y), ptr(part), ptr(shift),
+                                                       N_, H, W, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1],
+                                                       _s()), "conv_fwd_c4_stats_shift")
+            return y, part, G
         check(_lib().bigdl_conv_fwd_c4(ptr(x), ptr(wk), ldw, ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, K, R, S,
                                        P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()), "conv_fwd_c4")
         return (y, part, G) if stats else y
+    if shift is not None:
+        check(_lib().bigdl_conv_fwd_stats_shift(ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W,
+                                                C_, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], 1, 1, _s()),
+              "conv_fwd_stats_shift")
+        return y, part, G
     check(_lib().bigdl_conv_fwd_ldy(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
                                     P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy,
                                     _s()), "conv_fwd")
@@ -402,11 +416,12 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out, pad_slot=pad_slot)
 
 
-def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None):
-    """Forward conv whose epilogue also emits per-row-tile Σy/Σy² partials for a following BN
-    (128-row tiles; the BN finalize combines them in fp64).  Returns ``(y, partials, G)`` or
+def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None, shift=None):
+    """Forward conv whose epilogue also emits per-row-tile Σ(y−K)/Σ(y−K)² partials for a following
+    BN (128-row tiles; the BN finalize combines them in fp64).  ``shift`` (fp32 [K], e.g. the BN's
+    running mean) is K; the same array must reach the finalize.  Returns ``(y, partials, G)`` or
     NotImplemented."""
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot)
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot, shift=shift)
 
 
 def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):

@@ -449,3 +449,30 @@ def test_block_tail_bn_backward_fused_into_next_dgrad():
     torch.testing.assert_close(ga.float(), gb.float(), rtol=5e-2, atol=5e-2)
     for u, v in zip(a.parameters()[1], b.parameters()[1]):
         torch.testing.assert_close(u.float(), v.float(), rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("case", [(8, 64, 14, 14, 128, 3, 3, 1, 1), (4, 64, 28, 28, 256, 1, 1, 1, 0),
+                                  (2, 3, 32, 32, 64, 7, 7, 2, 3)])
+def test_conv_stats_shifted_partials(case):
+    """Shifted statistics partials Σ(y−K), Σ(y−K)² (K = a per-channel shift such as the BN running
+    mean) against the fp32 convolution; and the BN built on them recovers mean/variance of a
+    large-mean output where raw Σy² − (Σy)²/M would cancel."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    n, c, h, w, k, r, s, st, pd = case
+    x = _cl((torch.randn(n, c, h, w, device=dev) + 3.0).bfloat16())
+    w4 = _cl((torch.randn(k, c, r, s, device=dev) * 0.05 + 0.02).bfloat16())
+    ref = _conv_ref(x, w4, (st, st), (pd, pd)).double()
+    K = ref.mean((0, 2, 3)).float() + 0.1 * torch.randn(k, device=dev)
+    y, part, G = NO.conv2d_forward_stats(x, w4, None, (st, st), (pd, pd), shift=K)
+    s1 = part.view(2, G, k).double().sum(1)
+    d = ref - K.double().view(1, k, 1, 1)
+    torch.testing.assert_close(s1[0], d.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(s1[1], (d * d).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    g = torch.ones(k, device=dev)
+    b = torch.zeros(k, device=dev)
+    rm, rv = K.clone(), torch.ones(k, device=dev)
+    out, mean, invstd = NO.batchnorm_forward_train_partials(y, part, G, g, b, rm, rv, 0.1, 1e-5, shift=K)
+    torch.testing.assert_close(mean.double(), ref.mean((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    var = ref.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close((1.0 / invstd.double() ** 2 - 1e-5), var, rtol=2e-3, atol=1e-4)
