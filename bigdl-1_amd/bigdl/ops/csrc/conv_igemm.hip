@@ -668,6 +668,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   // of ≤ 512 (the 1×1 convs; more blocks in flight hide the short k-loop's prologue/epilogue),
   // BK = 64 on the deeper ones (3×3, C ≥ 1024).
   const int bk_env = conv_env_override("BIGDL_CONV_BK", 32, 64);
+  // (The 3×3 convs with Kg ≤ 1152 run 3–5 % faster alone at BK = 32 — profiles/r2_conv3x3_tile_ab.txt —
+  // but the whole step, with wgrad overlapping on a side stream, measured 23.5 vs 23.1 ms: kept at 64.)
   const int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
   const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
   const bool fast = (C % bk == 0) && R * S <= 64;
