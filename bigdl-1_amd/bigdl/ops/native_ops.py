@@ -1609,10 +1609,16 @@ VML_BINARY = {"add": 0, "sub": 1, "mul": 2, "div": 3, "tanh_bwd": 4, "sigmoid_bw
 REDUCE = {"sum": 0, "mean": 1, "max": 2, "min": 3}
 
 
+def _dense(t):
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
 def _vml_ok(*ts):
+    """Elementwise kernels walk the storage linearly: every operand dense (row-major or NHWC) with
+    the same strides, same dtype and element count."""
     t0 = ts[0]
-    return all(t is not None and t.is_cuda and t.dtype == t0.dtype and t.dtype in (_f32, _bf16) and t.is_contiguous()
-               and t.numel() == t0.numel() and _al16(t) for t in ts) and t0.numel() > 0
+    return all(t is not None and t.is_cuda and t.dtype == t0.dtype and t.dtype in (_f32, _bf16) and _dense(t)
+               and t.shape == t0.shape and t.stride() == t0.stride() and _al16(t) for t in ts) and t0.numel() > 0
 
 
 @register("vml_unary")
@@ -1632,7 +1638,7 @@ def vml_binary(a, b, op, p=1.0, out=None):
     """Elementwise ``op`` (a VML_BINARY name) of two same-shape contiguous device tensors
     (add/sub: a ± p·b; *_bwd: a = upstream gradient, b = saved forward value; pow_bwd uses p)."""
     z = torch.empty_like(a) if out is None else out
-    if not _vml_ok(a, b, z) or a.shape != b.shape:
+    if not _vml_ok(a, b, z):
         return NotImplemented
     check(_lib().bigdl_vml_binary(C.c_int(VML_BINARY[op]), C.c_int(0 if a.dtype == _f32 else 1), ptr(a), ptr(b),
                                   ptr(z), _ll(a.numel()), _f(p), _s()), "vml_binary")

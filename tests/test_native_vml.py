@@ -122,3 +122,15 @@ def test_layers_on_device(NO, name, dt):
     tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(yd.float().cpu(), yh.float(), **tol)
     torch.testing.assert_close(gd.float().cpu(), gh.float(), **tol)
+
+
+def test_channels_last_operands(NO):
+    x = torch.randn(4, 16, 9, 9, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = NO.vml_unary(x, "tanh")
+    assert y is not NotImplemented and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), torch.tanh(x.float()), rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(x)
+    z = NO.vml_binary(g, y, "tanh_bwd")
+    torch.testing.assert_close(z.float(), (g.float() * (1 - y.float() ** 2)), rtol=2e-2, atol=2e-2)
+    # mixed layouts are refused (caller falls back)
+    assert NO.vml_binary(g.contiguous(), y, "mul") is NotImplemented
