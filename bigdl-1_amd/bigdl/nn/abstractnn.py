@@ -39,6 +39,9 @@ from ..utils.engine import Engine
 from ..utils.table import Table
 from ..utils import config
 
+_DEV_TIMERS = [bool(config.get_property("bigdl.profile.deviceTimers"))]
+config.on_change("bigdl.profile.deviceTimers", lambda v: _DEV_TIMERS.__setitem__(0, bool(v)))
+
 
 class LayerException(RuntimeError):
     """Wraps a failure with the module path (``DL/utils/LayerException.scala``)."""
@@ -578,6 +581,47 @@ class AbstractModule:
     def accGradParameters(self, input, gradOutput):
         pass
 
+    # HIP-event per-module timers (bigdl.profile.deviceTimers): events are recorded around
+    # forward / backward on the current stream and resolved only when getDeviceTimes() asks, so
+    # timing never synchronises the step (SURVEY §2.12 "HIP-event per-module timers")
+    def _dev_start(self, x):
+        if not _DEV_TIMERS[0]:
+            return None
+        t = x if isinstance(x, torch.Tensor) else next((v for v in (x.values() if isinstance(x, Table) else ())
+                                                         if isinstance(v, torch.Tensor)), None)
+        if t is None or not t.is_cuda or torch.cuda.is_current_stream_capturing():
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _dev_stop(self, start, which):
+        if start is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        pend = self.__dict__.setdefault("_dev_pending", [])
+        pend.append((start, e, which))
+
+    def _dev_resolve(self):
+        pend = self.__dict__.get("_dev_pending")
+        acc = self.__dict__.setdefault("_dev_times", [0.0, 0.0])
+        if pend:
+            for s, e, which in pend:
+                e.synchronize()
+                acc[which] += s.elapsed_time(e) / 1e3
+            pend.clear()
+        return acc
+
+    def getDeviceTimes(self):
+        """[(module, forward_s, backward_s)] measured on the device by HIP events (requires
+        ``bigdl.profile.deviceTimers``); containers include their children's time."""
+        f, b = self._dev_resolve()
+        out = [(self, f, b)]
+        for c in self.children():
+            out.extend(c.getDeviceTimes())
+        return out
+
     def _sync_for_timing(self):
         if config.get_property("bigdl.profile.sync") and torch.cuda.is_available():
             torch.cuda.synchronize()
@@ -591,12 +635,14 @@ class AbstractModule:
             h(self)
         self._sync_for_timing()
         t0 = time.perf_counter()
+        ev = self._dev_start(input)
         try:
             self.output = self.updateOutput(input)
         except LayerException:
             raise
         except Exception as e:  # noqa: BLE001 - wrap with the layer path as the reference does
             raise LayerException(f"Layer info: {self}", e) from e
+        self._dev_stop(ev, 0)
         self._sync_for_timing()
         self.forward_time += time.perf_counter() - t0
         if conv_back is np.ndarray:
@@ -614,8 +660,10 @@ class AbstractModule:
             gradOutput = to_torch(gradOutput)
         self._sync_for_timing()
         t0 = time.perf_counter()
+        ev = self._dev_start(gradOutput)
         self.gradInput = self.updateGradInput(input, gradOutput)
         self.accGradParameters(input, gradOutput)
+        self._dev_stop(ev, 1)
         self._sync_for_timing()
         self.backward_time += time.perf_counter() - t0
         for h in self._grad_ready_hooks:
@@ -647,6 +695,8 @@ class AbstractModule:
     def resetTimes(self):
         self.forward_time = 0.0
         self.backward_time = 0.0
+        self.__dict__.pop("_dev_pending", None)
+        self.__dict__.pop("_dev_times", None)
         for c in self.children():
             c.resetTimes()
 

@@ -152,11 +152,13 @@ class Sequential(Container):
     def backward(self, input, gradOutput):
         import time
         t0 = time.perf_counter()
+        ev = self._dev_start(gradOutput)
         g = gradOutput
         for i in range(len(self.modules) - 1, 0, -1):
             g = self.modules[i].backward(self.modules[i - 1].output, g)
         g = self.modules[0].backward(input, g)
         self.gradInput = g
+        self._dev_stop(ev, 1)
         self.backward_time += time.perf_counter() - t0
         for h in self._grad_ready_hooks:
             h(self)

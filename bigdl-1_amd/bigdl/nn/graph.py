@@ -252,7 +252,9 @@ class Graph(Container):
     def backward(self, input, gradOutput):
         import time
         t0 = time.perf_counter()
+        ev = self._dev_start(gradOutput)
         self.gradInput = self._backward_impl(input, gradOutput, lambda m, x, g: m.backward(x, g))
+        self._dev_stop(ev, 1)
         self.backward_time += time.perf_counter() - t0
         return self.gradInput
 

@@ -58,6 +58,7 @@ _REGISTRY = {
     "bigdl.deterministic": (bool, False, "bit-reproducible kernels: single-writer reductions instead of split-K float atomics (slower wgrad / embedding backward)"),
     "bigdl.native.enable": (bool, True, "False routes device tensors to the torch reference ops (debug/A-B only)"),
     "bigdl.profile.sync": (bool, False, "synchronize the device around per-module timers"),
+    "bigdl.profile.deviceTimers": (bool, False, "per-module HIP-event forward/backward timers (resolved lazily by getDeviceTimes)"),
     "bigdl.optim.foldRegularizers": (bool, True, "apply pure-L2 layer regularizers inside the fused SGD update"),
     # fusion flags (bigdl.mkldnn.fusion.* equivalents, nn/mkldnn/Fusion.scala:34)
     "bigdl.fusion": (bool, True, "enable layer fusion"),

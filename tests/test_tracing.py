@@ -162,3 +162,46 @@ def test_comm_channel_cap_env():
     finally:
         config.clear_property("bigdl.comm.channels")
     assert env2["NCCL_MAX_NCHANNELS"] == "4"  # a user-exported value wins
+
+
+def test_device_timers_are_noop_on_host():
+    from bigdl.utils import config
+    config.set_property("bigdl.profile.deviceTimers", True)
+    try:
+        m = _mlp()
+        x = torch.randn(4, 8)
+        m.forward(x)
+        m.backward(x, torch.randn(4, 4))
+        assert all(f == 0.0 and b == 0.0 for _, f, b in m.getDeviceTimes())
+    finally:
+        config.clear_property("bigdl.profile.deviceTimers")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_device_timers_hip_events():
+    """HIP-event per-module timers: resolved lazily, positive for the layers that ran on the device,
+    a container's time covers its children's."""
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    import bigdl.nn as nn
+    Engine.init(device="cuda:0")
+    config.set_property("bigdl.profile.deviceTimers", True)
+    try:
+        m = nn.Sequential().add(nn.SpatialConvolution(8, 16, 3, 3, 1, 1, 1, 1)).add(nn.ReLU()) \
+            .add(nn.SpatialConvolution(16, 16, 3, 3, 1, 1, 1, 1)).to(device="cuda")
+        x = torch.randn(16, 8, 32, 32, device="cuda")
+        for _ in range(3):
+            y = m.forward(x)
+            m.backward(x, torch.ones_like(y))
+        times = m.getDeviceTimes()
+        top_f, top_b = times[0][1], times[0][2]
+        convs = [(f, b) for mod, f, b in times if type(mod).__name__ == "SpatialConvolution"]
+        assert len(convs) == 2 and all(f > 0 and b > 0 for f, b in convs)
+        assert top_f >= 0.9 * sum(f for f, _ in convs) and top_b >= 0.9 * sum(b for _, b in convs)
+        m.resetTimes()
+        assert all(f == 0.0 for _, f, _ in m.getDeviceTimes())
+    finally:
+        config.clear_property("bigdl.profile.deviceTimers")
