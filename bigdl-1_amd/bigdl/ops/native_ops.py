@@ -333,10 +333,46 @@ def _conv_geom_ok(x, w4, groups, dilation):
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
 
 
+def _grouped_ok(x, w4, groups):
+    return (groups > 1 and x.dim() == 4 and x.dtype == _bf16 and w4.dtype == _bf16 and x.shape[1] % groups == 0
+            and w4.shape[0] % groups == 0 and w4.shape[1] == x.shape[1] // groups)
+
+
+def _group_slice(t, g, n):
+    """channel slice g (width n) of an NCHW-shaped tensor as its own channels-last tensor (one copy)."""
+    return t[:, g * n:(g + 1) * n].contiguous(memory_format=torch.channels_last)
+
+
+def _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot=None, relu=False):
+    """Grouped convolution (the reference's nGroup, SpatialConvolution.scala:93-98) on the native
+    kernels: one groups=1 launch per group on channel slices; each group's output goes straight
+    into its channel slice of the result when the slice is 16-B aligned (the zero-copy concat
+    path), else through a copy."""
+    N_, C_, H, W = x.shape
+    K = w4.shape[0]
+    Cg, Kg = C_ // groups, K // groups
+    P = (H + 2 * pad[0] - dilation[0] * (w4.shape[2] - 1) - 1) // stride[0] + 1
+    Q = (W + 2 * pad[1] - dilation[1] * (w4.shape[3] - 1) - 1) // stride[1] + 1
+    y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    for g in range(groups):
+        xg = _group_slice(x, g, Cg)
+        wg = w4[g * Kg:(g + 1) * Kg]
+        bg = None if b is None else b[g * Kg:(g + 1) * Kg]
+        tgt = y[:, g * Kg:(g + 1) * Kg] if (Kg % 8 == 0 and K % 8 == 0) else None
+        r = _conv_fwd_impl(xg, wg, bg, stride, pad, dilation, 1, relu=relu, out=tgt)
+        if r is NotImplemented:
+            return NotImplemented
+        if tgt is None:
+            y[:, g * Kg:(g + 1) * Kg] = r
+    return y
+
+
 def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None,
                    pad_slot=None, shift=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
     writes into directly (zero-copy concat); returned as the result."""
+    if groups > 1 and res is None and not stats and out is None and _grouped_ok(x, w4, groups):
+        return _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot, relu)
     if not _conv_geom_ok(x, w4, groups, dilation):
         return NotImplemented
     N_, C_, H, W = x.shape
@@ -701,6 +737,23 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
                     scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
+    if groups > 1 and residual is None and bn_fuse is None and _grouped_ok(x, w4, groups) and gy.dtype == _bf16:
+        # grouped: one groups=1 backward per channel slice (gradient-weight rows of a group are a
+        # contiguous block of the arena, so they accumulate in place)
+        C_, K = x.shape[1], w4.shape[0]
+        Cg, Kg = C_ // groups, K // groups
+        gi = torch.empty(x.shape, dtype=_bf16, device=x.device,
+                         memory_format=torch.channels_last) if need_input else None
+        for g in range(groups):
+            r = conv2d_backward(_group_slice(gy, g, Kg), _group_slice(x, g, Cg), w4[g * Kg:(g + 1) * Kg], stride,
+                                pad, dilation, 1, need_input,
+                                None if gw_acc is None else gw_acc[g * Kg:(g + 1) * Kg],
+                                None if gb_acc is None else gb_acc[g * Kg:(g + 1) * Kg], scale)
+            if r is NotImplemented:
+                return NotImplemented
+            if need_input:
+                gi[:, g * Cg:(g + 1) * Cg] = r
+        return gi
     if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
         return NotImplemented
     if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):

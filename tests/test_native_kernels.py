@@ -476,3 +476,34 @@ def test_conv_stats_shifted_partials(case):
     torch.testing.assert_close(mean.double(), ref.mean((0, 2, 3)), rtol=1e-4, atol=1e-3)
     var = ref.var((0, 2, 3), unbiased=False)
     torch.testing.assert_close((1.0 / invstd.double() ** 2 - 1e-5), var, rtol=2e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("groups,C,K,st,R", [(2, 32, 64, 1, 3), (4, 32, 32, 2, 3), (2, 16, 16, 1, 1), (8, 64, 64, 1, 3)])
+def test_grouped_conv_native(groups, C, K, st, R):
+    """Grouped convolution (reference nGroup) on the native kernels, one launch per group, vs the
+    fp32 torch grouped conv; no torch fallback."""
+    N = _native()
+    from bigdl.ops import native_ops as NO
+    from bigdl.ops import native
+    native.reset_fallbacks()
+    pd = R // 2
+    x = _cl(torch.randn(4, C, 12, 12, device=dev).bfloat16())
+    w4 = (torch.randn(K, C // groups, R, R, device=dev) * 0.1).bfloat16()
+    b = torch.randn(K, device=dev)
+    y = NO.conv2d_forward(x, w4, b, (st, st), (pd, pd), groups=groups)
+    assert y is not NotImplemented
+    ref = torch.nn.functional.conv2d(x.float(), w4.float(), b, (st, st), (pd, pd), groups=groups)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
+    gy = _cl(torch.randn_like(ref).bfloat16())
+    gw = torch.zeros(K, C // groups, R, R, device=dev)
+    gb = torch.zeros(K, device=dev)
+    gi = NO.conv2d_backward(gy, x, w4, (st, st), (pd, pd), groups=groups, need_input=True, gw_acc=gw, gb_acc=gb)
+    assert gi is not NotImplemented
+    xr = x.float().requires_grad_(True)
+    wr = w4.float().requires_grad_(True)
+    out = torch.nn.functional.conv2d(xr, wr, None, (st, st), (pd, pd), groups=groups)
+    out.backward(gy.float())
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(gw, wr.grad, rtol=2e-2, atol=5e-2 * float(wr.grad.abs().max()))
+    torch.testing.assert_close(gb, gy.float().sum((0, 2, 3)), rtol=1e-2, atol=1e-1)
+    assert not any(k[0].startswith("conv") for k in native.fallback_counts()), native.fallback_counts()

@@ -101,3 +101,19 @@ def test_inception_v1_inference_native():
     torch.cuda.synchronize()
     assert out.shape == (4, 1000)
     _assert_clean()
+
+
+def test_grouped_conv_model_step_native():
+    """An AlexNet-style grouped-convolution stack (nGroup = 2) trains through the native kernels."""
+    import bigdl.nn as nn
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    m = nn.Sequential()
+    m.add(nn.SpatialConvolution(3, 32, 3, 3, 1, 1, 1, 1)).add(nn.ReLU())
+    m.add(nn.SpatialConvolution(32, 64, 3, 3, 1, 1, 1, 1, n_group=2)).add(nn.ReLU())
+    m.add(nn.SpatialConvolution(64, 64, 3, 3, 2, 2, 1, 1, n_group=4)).add(nn.ReLU())
+    m.add(nn.SpatialAveragePooling(8, 8, 8, 8)).add(nn.View(64)).add(nn.Linear(64, 10)).add(nn.LogSoftMax())
+    x = _img(8, 3, 16, 16)
+    y = (torch.randint(0, 10, (8,)) + 1).float().to(dev)
+    _train_steps(m, x, y, ClassNLLCriterion(), SGD(learningrate=0.05))
+    _assert_clean()
