@@ -18,6 +18,12 @@
 // contiguous range of tiles (T1; bijective for any grid size).
 #include "common.h"
 
+// raising the wave priority around the MFMA phase (the 256² GEMM template's idiom) measured 4 %
+// slower on the ResNet-50 conv set at this 128² 2–3-blocks/CU structure: off by default
+#ifndef BIGDL_CONV_SETPRIO
+#define BIGDL_CONV_SETPRIO 0
+#endif
+
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -284,6 +290,9 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 
   const int fr = lane & 15, fq = lane >> 4;
   auto compute = [&](int buf) {
+#if BIGDL_CONV_SETPRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -303,6 +312,9 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+#if BIGDL_CONV_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   };
 
   // Two register sets, loads issued two k-tiles ahead of their use: tile t+2 is requested while
