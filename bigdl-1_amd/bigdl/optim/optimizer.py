@@ -412,6 +412,8 @@ class BaseOptimizer:
         return local_epoch_size
 
     def _finish(self):
+        from ..serialization.checkpoint import wait_checkpoints
+        wait_checkpoints()
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         if getattr(self, "tracer", None) is not None:
@@ -669,13 +671,16 @@ class BaseOptimizer:
             return
         if not self.checkpoint_trigger(self.state):
             return
-        self.checkpoint()
+        self.checkpoint(asynchronous=bool(config.get_property("bigdl.checkpoint.async")))
 
-    def checkpoint(self):
+    def checkpoint(self, asynchronous: bool = False):
+        """Write ``model.<neval>`` / ``optimMethod-*`` / ``state``; ``asynchronous`` returns after
+        the host snapshot and leaves serialisation + file writes to the checkpoint writer thread."""
         from ..serialization.checkpoint import save_checkpoint
         self._flush_weights()
         if Engine.rank() == 0:
-            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite)
+            save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite,
+                            asynchronous=asynchronous)
 
     def _maybe_resume(self):
         """Resume from the latest checkpoint when this process is a launcher restart

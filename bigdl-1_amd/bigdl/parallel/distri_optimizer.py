@@ -407,16 +407,19 @@ class DistriOptimizer(BaseOptimizer):
         if self.flat.shadow is not None:
             self.flat.refresh_shadow()
 
-    def checkpoint(self):
+    def checkpoint(self, asynchronous: bool = False):
         """Gather the shards (X14) then rank 0 writes ``model.<neval>`` / ``optimMethod-*``.
         Optimizer state is per shard: each rank writes its own state file next to it."""
-        from ..serialization.checkpoint import save_checkpoint, save_shard_state
+        from ..serialization.checkpoint import save_checkpoint, save_shard_state, wait_checkpoints
         self._flush_weights()
         if Engine.rank() == 0:
             save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite,
-                            world_size=self.world, sharded=self.sharded)
+                            world_size=self.world, sharded=self.sharded, asynchronous=asynchronous)
         if self.sharded:
-            save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite)
+            save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite,
+                             asynchronous=asynchronous)
+        if not asynchronous:
+            wait_checkpoints()
         comm.barrier()
 
 

@@ -22,13 +22,17 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import bigdl_pb as pb
-from .module_serializer import _SerCtx, _DeCtx, _set_attr, _get_attr, _storage_from_pb, save_module, load_module
+from .module_serializer import (_SerCtx, _DeCtx, _set_attr, _get_attr, _storage_from_pb, save_module, load_module,
+                                fill_global_storage, module_snapshot, module_snapshot_bytes)
 
 _SKIP = {"state", "shadow", "grad_scale", "slices", "_first", "_clr", "_t"}
 
 
-def optim_to_pb(method) -> pb.BigDLModule:
+def optim_to_pb(method, defer: bool = False):
+    """OptimMethod → protobuf; ``defer`` returns ``(proto, ctx)`` with the state tensors
+    snapshotted but not yet merged (finish with ``fill_global_storage(proto, ctx, "global_storage")``)."""
     ctx = _SerCtx()
+    ctx.defer = defer
     mp = pb.BigDLModule()
     mp.moduleType = method.scala_class_name()
     mp.name = type(method).__name__
@@ -53,13 +57,9 @@ def optim_to_pb(method) -> pb.BigDLModule:
         if isinstance(v, (torch.Tensor, int, float, bool, str)):
             _set_attr(ctx, st.nameAttrListValue.attr[k], v)
     # storages inline (optimizer state is never shared with a model)
-    g = mp.attr["global_storage"]
-    g.dataType = pb.DataType["NAME_ATTR_LIST"]
-    g.nameAttrListValue.name = "global_storage"
-    for tid, tp in ctx.storages.items():
-        av = g.nameAttrListValue.attr[str(tid)]
-        av.dataType = pb.DataType["TENSOR"]
-        av.tensorValue.CopyFrom(tp)
+    if defer:
+        return mp, ctx
+    fill_global_storage(mp, ctx, "global_storage")
     return mp
 
 
@@ -122,36 +122,108 @@ def _suffix(state, overwrite):
     return "" if overwrite else f".{state['neval'] - 1}"
 
 
+# ------------------------------------------------------------------------------------------ async writer
+# checkpoints are written asynchronously from a host snapshot.  The calling (training)
+# thread only walks the model / optimizer state and copies the tensors to host memory; merging the
+# payloads into the protobufs, serialising and writing run on one background thread.  Files appear
+# by atomic rename, the ``state`` file last, so a crash mid-write never leaves a torn file behind.
+_WRITER = {"queue": None, "thread": None, "error": None}
+
+
+def _atomic_write(path: str, data, mode: str = "wb"):
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, mode) as f:
+        f.write(data)
+    os.replace(tmp, path)
+
+
+def _worker(q):
+    while True:
+        job = q.get()
+        try:
+            if job is None:
+                return
+            job()
+        except BaseException as e:  # noqa: BLE001 - surfaced by the next wait_checkpoints()
+            _WRITER["error"] = e
+        finally:
+            q.task_done()
+
+
+def wait_checkpoints():
+    """Block until every queued checkpoint write has finished; re-raise a writer error."""
+    q = _WRITER["queue"]
+    if q is not None:
+        q.join()
+    err, _WRITER["error"] = _WRITER["error"], None
+    if err is not None:
+        raise RuntimeError("asynchronous checkpoint write failed") from err
+
+
+def _submit(job):
+    import queue
+    import threading
+    q = _WRITER["queue"]
+    if q is None or not _WRITER["thread"].is_alive():
+        q = _WRITER["queue"] = queue.Queue()
+        _WRITER["thread"] = threading.Thread(target=_worker, args=(q,), name="bigdl-checkpoint-writer", daemon=True)
+        _WRITER["thread"].start()
+    if q.unfinished_tasks >= 4:  # bound the host snapshots held in flight
+        q.join()
+    q.put(job)
+
+
 def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: bool = False, world_size: int = 1,
-                    sharded: bool = False):
+                    sharded: bool = False, asynchronous: bool = False):
     os.makedirs(path, exist_ok=True)
     sfx = _suffix(state, overwrite)
-    save_module(model, os.path.join(path, "model" + sfx), over_write=True)
+    msnap = module_snapshot(model)
+    osnaps = []
     for name, m in methods.items():
         m.state.update({k: state[k] for k in ("epoch", "neval", "recordsProcessedThisEpoch") if k in state})
-        save_optim_method(m, os.path.join(path, f"optimMethod-{name}" + sfx), over_write=True)
+        osnaps.append((name, optim_to_pb(m, defer=True)))
     meta = {k: (float(v) if isinstance(v, (int, float)) else v) for k, v in state.items()
             if isinstance(v, (int, float, str))}
     # how the optimizer state was laid out: a sharded (ZeRO-1) run's un-suffixed optimMethod file
     # holds only rank 0's shard, so a resume must find its own ``.rank<r>`` file at the same world size
     meta["_world_size"] = int(world_size)
     meta["_sharded"] = bool(sharded)
-    with open(os.path.join(path, "state" + sfx), "w") as f:
-        json.dump(meta, f)
+
+    def job():
+        _atomic_write(os.path.join(path, "model" + sfx), module_snapshot_bytes(msnap))
+        for name, (mp, ctx) in osnaps:
+            fill_global_storage(mp, ctx, "global_storage")
+            _atomic_write(os.path.join(path, f"optimMethod-{name}" + sfx), mp.SerializeToString())
+        _atomic_write(os.path.join(path, "state" + sfx), json.dumps(meta), "w")
+    if asynchronous:
+        _submit(job)
+    else:
+        wait_checkpoints()
+        job()
 
 
-def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False):
+def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False,
+                     asynchronous: bool = False):
     """Each rank's shard of the optimizer state.  Files are keyed by the method's POSITION in sorted
     key order, not by its key: a key derived from a default module name is random per process (the
     reference's ``getName`` postfix), so rank 1 — and a restarted process — could never find a file
     named after rank 0's key."""
     sfx = _suffix(state, overwrite)
-    for i, name in enumerate(sorted(methods)):
-        save_optim_method(methods[name], os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}"), over_write=True)
+    snaps = [(i, optim_to_pb(methods[name], defer=True)) for i, name in enumerate(sorted(methods))]
+
+    def job():
+        for i, (mp, ctx) in snaps:
+            fill_global_storage(mp, ctx, "global_storage")
+            _atomic_write(os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}"), mp.SerializeToString())
+    if asynchronous:
+        _submit(job)
+    else:
+        wait_checkpoints()
+        job()
 
 
 def _latest(pattern: str) -> Optional[str]:
-    files = [f for f in glob.glob(pattern) if ".rank" not in f]
+    files = [f for f in glob.glob(pattern) if ".rank" not in f and ".tmp" not in f]
     if not files:
         return None
     return max(files, key=os.path.getmtime)
@@ -166,6 +238,7 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
     """Latest model / optimMethods / driver state under ``path``.  With ``world_size`` given, a
     checkpoint whose optimizer state was sharded is only accepted by a sharded run of the SAME world
     size that finds its own ``.rank<r>`` state file (no silent fallback to rank 0's shard)."""
+    wait_checkpoints()
     sfile = _latest(os.path.join(path, "state*"))
     meta = {}
     if sfile:
@@ -181,7 +254,7 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
     model = load_module(mfile) if mfile else None
     methods = {}
     for f in glob.glob(os.path.join(path, "optimMethod-*")):
-        if ".rank" in f or os.path.basename(f).startswith("optimMethod-#"):
+        if ".rank" in f or ".tmp" in f or os.path.basename(f).startswith("optimMethod-#"):
             continue
         base = os.path.basename(f)[len("optimMethod-"):]
         name = base.rsplit(".", 1)[0] if base.rsplit(".", 1)[-1].isdigit() else base

@@ -212,3 +212,39 @@ def test_perf_harness_runs_cpu(capsys):
     from bigdl.models.utils.perf import main
     assert main(["--model", "lenet5", "--batch", "8", "--iteration", "2", "--warmup", "1", "--dtype", "fp32"]) == 0
     assert "records/second" in capsys.readouterr().out
+
+
+def test_async_checkpoint_matches_sync_and_is_atomic(tmp_path):
+    """trigger-driven checkpoints snapshot on the training thread and serialise/write on
+    the writer thread; the files equal a synchronous save, temp files are never picked up as the
+    latest checkpoint, and writer errors surface on the next wait."""
+    import os
+    import pytest
+    import torch
+    from bigdl.nn import Sequential, Linear, ReLU
+    from bigdl.optim import SGD
+    from bigdl.serialization import checkpoint as ck
+    torch.manual_seed(0)
+    m = Sequential().add(Linear(16, 32)).add(ReLU()).add(Linear(32, 4))
+    sgd = SGD(learningrate=0.1, momentum=0.9)
+    sgd.state["buf"] = torch.randn(100)
+    state = {"epoch": 1, "neval": 3, "Loss": 0.5}
+    a, b = str(tmp_path / "sync"), str(tmp_path / "async")
+    ck.save_checkpoint(a, m, {"sgd": sgd}, state)
+    ck.save_checkpoint(b, m, {"sgd": sgd}, state, asynchronous=True)
+    # mutate right away: the async snapshot must not see it
+    with torch.no_grad():
+        for w in m.parameters()[0]:
+            w.add_(1.0)
+    ck.wait_checkpoints()
+    for f in ("model.2", "optimMethod-sgd.2", "state.2"):
+        assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
+    open(os.path.join(b, "model.9.tmp123"), "wb").write(b"partial")
+    assert ck._latest(os.path.join(b, "model*")).endswith("model.2")
+
+    def boom():
+        raise IOError("disk full")
+    ck._submit(boom)
+    with pytest.raises(RuntimeError):
+        ck.wait_checkpoints()
+    ck.wait_checkpoints()  # the error is reported once
