@@ -37,6 +37,18 @@ __device__ __forceinline__ void load8(const bf16_t* p, float* o) {
   }
 }
 
+// streaming (non-temporal) variant: for operands read once per pass whose next use is far away
+// (BN apply / backward-apply inputs), so they do not displace reusable lines from L2 / MALL
+typedef unsigned int bigdl_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load8_nt(const bf16_t* p, float* o) {
+  const bigdl_u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(p));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(u[i] << 16);
+    o[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+  }
+}
+
 __device__ __forceinline__ void unpack8(uint4 u, float* o) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
