@@ -416,8 +416,19 @@ class SpatialSeparableConvolution(AutogradModule):
             pt, pb, pl, pr, _, _ = same_padding(x.shape[2], x.shape[3], self.sH, self.sW, self.kH, self.kW)
             x = F.pad(x, (pl, pr, pt, pb))
             pad = (0, 0)
+        bias = self.P("bias") if self.withBias else None
+        if x.is_cuda and ops.native_has("conv2d_forward"):
+            # depthwise stencil kernel + pointwise MFMA conv, both differentiable native ops
+            xd = to_device_layout(x)
+            y = ops.native_ops.conv2d_autograd(xd, self.P("depthWeight"), None, (self.sH, self.sW), pad, (1, 1),
+                                               self.nIn)
+            if y is not NotImplemented:
+                y2 = ops.native_ops.conv2d_autograd(y, self.P("pointWeight"), bias, (1, 1), (0, 0))
+                if y2 is not NotImplemented:
+                    return y2.permute(0, 2, 3, 1) if nhwc else y2
+            ops.native.note_fallback("separable_conv", "geometry", (xd,))
         y = F.conv2d(x, self.P("depthWeight").to(x.dtype), None, (self.sH, self.sW), pad, 1, self.nIn)
-        y = F.conv2d(y, self.P("pointWeight").to(x.dtype), self.P("bias").to(x.dtype) if self.withBias else None)
+        y = F.conv2d(y, self.P("pointWeight").to(x.dtype), bias.to(x.dtype) if bias is not None else None)
         return y.permute(0, 2, 3, 1) if nhwc else y
 
 

@@ -333,6 +333,57 @@ def _conv_geom_ok(x, w4, groups, dilation):
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
 
 
+def _depthwise_ok(x, w4, groups):
+    """groups == C == K (one filter per channel): the depthwise stencil kernels (depthwise.hip)."""
+    return (groups > 1 and x.dim() == 4 and x.dtype == _bf16 and x.shape[1] == groups and w4.shape[0] == groups
+            and w4.shape[1] == 1 and groups % 8 == 0 and w4.shape[2] * w4.shape[3] <= 25
+            and x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
+
+
+def _dw_weight(w4):
+    C_, _, R, S = w4.shape
+    return w4.detach().float().reshape(C_, R * S).t().contiguous()  # [R·S][C] fp32
+
+
+def _dw_out_hw(H, W, R, S, stride, pad, dilation):
+    return ((H + 2 * pad[0] - dilation[0] * (R - 1) - 1) // stride[0] + 1,
+            (W + 2 * pad[1] - dilation[1] * (S - 1) - 1) // stride[1] + 1)
+
+
+def _depthwise_fwd(x, w4, b, stride, pad, dilation, relu=False):
+    N_, C_, H, W = x.shape
+    R, S = w4.shape[2], w4.shape[3]
+    P, Q = _dw_out_hw(H, W, R, S, stride, pad, dilation)
+    if P <= 0 or Q <= 0:
+        return NotImplemented
+    y = torch.empty((N_, C_, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    bias = None if b is None else b.detach().float().contiguous()
+    check(_lib().bigdl_dw_fwd(ptr(x), ptr(_dw_weight(w4)), ptr(bias), ptr(y), N_, H, W, C_, P, Q, R, S, stride[0],
+                              stride[1], pad[0], pad[1], dilation[0], dilation[1], int(bool(relu)), _s()), "dw_fwd")
+    return y
+
+
+def _depthwise_bwd(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale):
+    N_, C_, H, W = x.shape
+    R, S = w4.shape[2], w4.shape[3]
+    P, Q = gy.shape[2], gy.shape[3]
+    if not (gy.dtype == _bf16 and gy.is_contiguous(memory_format=torch.channels_last) and _al16(gy)):
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    gi = None
+    if need_input:
+        gi = torch.empty(x.shape, dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+        check(_lib().bigdl_dw_dgrad(ptr(gy), ptr(_dw_weight(w4)), ptr(gi), N_, H, W, C_, P, Q, R, S, stride[0],
+                                    stride[1], pad[0], pad[1], dilation[0], dilation[1], _s()), "dw_dgrad")
+    if gw_acc is not None and scale != 0:
+        tmp = torch.zeros((R * S, C_), dtype=_f32, device=x.device)
+        check(_lib().bigdl_dw_wgrad(ptr(x), ptr(gy), ptr(tmp), _f(1.0), N_, H, W, C_, P, Q, R, S, stride[0], stride[1],
+                                    pad[0], pad[1], dilation[0], dilation[1], _s()), "dw_wgrad")
+        gw_acc.add_(tmp.t().reshape(C_, 1, R, S), alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
+    return gi
+
+
 def _grouped_ok(x, w4, groups):
     return (groups > 1 and x.dim() == 4 and x.dtype == _bf16 and w4.dtype == _bf16 and x.shape[1] % groups == 0
             and w4.shape[0] % groups == 0 and w4.shape[1] == x.shape[1] // groups)
@@ -371,6 +422,8 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
                    pad_slot=None, shift=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
     writes into directly (zero-copy concat); returned as the result."""
+    if groups > 1 and res is None and not stats and out is None and _depthwise_ok(x, w4, groups):
+        return _depthwise_fwd(x, w4, b, stride, pad, dilation, relu)
     if groups > 1 and res is None and not stats and out is None and _grouped_ok(x, w4, groups):
         return _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot, relu)
     if not _conv_geom_ok(x, w4, groups, dilation):
@@ -737,6 +790,8 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
                     scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
+    if groups > 1 and residual is None and bn_fuse is None and _depthwise_ok(x, w4, groups):
+        return _depthwise_bwd(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale)
     if groups > 1 and residual is None and bn_fuse is None and _grouped_ok(x, w4, groups) and gy.dtype == _bf16:
         # grouped: one groups=1 backward per channel slice (gradient-weight rows of a group are a
         # contiguous block of the arena, so they accumulate in place)
@@ -1723,3 +1778,43 @@ def reduce(x, op, dim=None, keepdim=False):
     check(_lib().bigdl_reduce(C.c_int(REDUCE[op]), C.c_int(0 if x.dtype == _f32 else 1), ptr(x), _ll(outer), _ll(n),
                               _ll(inner), ptr(out), ptr(scratch), _ll(scratch.numel()), _s()), "reduce")
     return out.view(oshape)
+
+
+# ------------------------------------------------------------------------------------------------ autograd conv
+class _ConvFn(torch.autograd.Function):
+    """The native conv as an autograd op, for layers defined by their forward (AutogradModule):
+    forward = conv2d_forward, backward = conv2d_backward (data, weight and bias gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dilation, groups):
+        y = conv2d_forward(x, w.to(_bf16), b, stride, pad, dilation, groups)
+        if y is NotImplemented:
+            raise RuntimeError("native conv refused its geometry after the eligibility check")
+        ctx.save_for_backward(x, w, b)
+        ctx.geom = (stride, pad, dilation, groups)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b = ctx.saved_tensors
+        stride, pad, dilation, groups = ctx.geom
+        gw = torch.zeros(w.shape, dtype=_f32, device=w.device)
+        gb = torch.zeros(b.shape, dtype=_f32, device=w.device) if b is not None else None
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+        gi = conv2d_backward(gy, x, w.to(_bf16), stride, pad, dilation, groups, ctx.needs_input_grad[0], gw, gb, 1.0)
+        if gi is NotImplemented:
+            raise RuntimeError("native conv backward refused its geometry")
+        return gi, gw.to(w.dtype), (gb.to(b.dtype) if gb is not None else None), None, None, None, None
+
+
+def conv2d_autograd(x, w, b, stride, pad, dilation=(1, 1), groups=1):
+    """Differentiable native conv (NotImplemented when the geometry is not native-eligible)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last)
+            and _al16(x)):
+        return NotImplemented
+    wb = w.detach().to(_bf16)
+    ok = _depthwise_ok(x, wb, groups) or (groups == 1 and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0) or \
+        (groups > 1 and _grouped_ok(x, wb, groups))
+    if not ok:
+        return NotImplemented
+    return _ConvFn.apply(x, w, b, tuple(stride), tuple(pad), tuple(dilation), groups)

@@ -507,3 +507,30 @@ def test_grouped_conv_native(groups, C, K, st, R):
     torch.testing.assert_close(gw, wr.grad, rtol=2e-2, atol=5e-2 * float(wr.grad.abs().max()))
     torch.testing.assert_close(gb, gy.float().sum((0, 2, 3)), rtol=1e-2, atol=1e-1)
     assert not any(k[0].startswith("conv") for k in native.fallback_counts()), native.fallback_counts()
+
+
+@pytest.mark.parametrize("C,R,st,dil", [(32, 3, 1, 1), (64, 3, 2, 1), (16, 5, 1, 1), (48, 3, 1, 2), (24, 1, 1, 1)])
+def test_depthwise_conv_native(C, R, st, dil):
+    """Depthwise convolution (groups == C == K) on the stencil kernels vs torch fp32."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    from bigdl.ops import native
+    native.reset_fallbacks()
+    pd = dil * (R // 2)
+    x = _cl(torch.randn(4, C, 15, 17, device=dev).bfloat16())
+    w4 = (torch.randn(C, 1, R, R, device=dev) * 0.3).bfloat16()
+    b = torch.randn(C, device=dev)
+    y = NO.conv2d_forward(x, w4, b, (st, st), (pd, pd), (dil, dil), groups=C)
+    assert y is not NotImplemented
+    xr = x.float().requires_grad_(True)
+    wr = w4.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wr, b, (st, st), (pd, pd), (dil, dil), groups=C)
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=2e-2, atol=3e-2)
+    gy = _cl(torch.randn_like(ref).bfloat16())
+    ref.backward(gy.float())
+    gw = torch.zeros(C, 1, R, R, device=dev)
+    gb = torch.zeros(C, device=dev)
+    gi = NO.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (dil, dil), groups=C, need_input=True, gw_acc=gw, gb_acc=gb)
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(gw, wr.grad, rtol=1e-2, atol=1e-2 * float(wr.grad.abs().max()))
+    assert not any(k[0].startswith("conv") for k in native.fallback_counts())

@@ -117,3 +117,27 @@ def test_grouped_conv_model_step_native():
     y = (torch.randint(0, 10, (8,)) + 1).float().to(dev)
     _train_steps(m, x, y, ClassNLLCriterion(), SGD(learningrate=0.05))
     _assert_clean()
+
+
+def test_separable_conv_native_matches_torch():
+    """SpatialSeparableConvolution (depthwise + pointwise) through the native depthwise stencil and
+    MFMA conv kernels as autograd ops: forward and gradients vs the torch fp32 composition."""
+    import bigdl.nn as nn
+    from bigdl import ops
+    ops.reset_fallbacks()
+    torch.manual_seed(0)
+    m = nn.SpatialSeparableConvolution(32, 64, 1, 3, 3, 1, 1, 1, 1).to(device=dev)
+    x = torch.randn(4, 32, 12, 12, device=dev)
+    xb = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    y = m.forward(xb)
+    gy = torch.randn_like(y.float())
+    gi = m.backward(xb, gy.bfloat16().contiguous(memory_format=torch.channels_last))
+    dw, pw, b = (m.depthWeight.detach().float().clone().requires_grad_(True),
+                 m.pointWeight.detach().float().clone().requires_grad_(True),
+                 m.bias.detach().float().clone().requires_grad_(True))
+    xr = xb.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.conv2d(xr, dw, None, 1, 1, 1, 32), pw, b)
+    ref.backward(gy)
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=3e-2, atol=5e-2)
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    _assert_clean()
