@@ -69,7 +69,9 @@ class SpatialMaxPooling(TensorModule):
 
     def updateOutput(self, input):
         x, pad, batched, _ = self._prep(input)
-        y, idx = ops.maxpool2d_forward(x, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode)
+        # evaluate mode: no argmax (no backward follows; updateGradInput recomputes it if one does)
+        y, idx = ops.maxpool2d_forward(x, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode,
+                                       need_indices=bool(self.train))
         self._indices = idx
         return self._post(y, batched)
 
@@ -81,6 +83,8 @@ class SpatialMaxPooling(TensorModule):
         if not batched:
             gy = gy.unsqueeze(0)
         gy = to_device_layout(gy)
+        if self._indices is None:  # forward ran in evaluate mode: recompute the argmax
+            _, self._indices = ops.maxpool2d_forward(x, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode)
         gi = ops.maxpool2d_backward(gy, x, self._indices, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode)
         pt, pb, pl, pr = pads
         if pt != pb or pl != pr:

@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
     }
     const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8;
     store8(y + o, best);
+    if (!idx) continue;  // inference: no argmax for a backward (uniform per launch)
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lo |= (uint32_t)(arg[e] & 0xFF) << (8 * e);
@@ -132,7 +133,61 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const bf16_t* __restrict
       }
     }
     y[t] = f2bf(best);
-    idx[t] = (int8_t)arg;
+    if (idx) idx[t] = (int8_t)arg;
+  }
+}
+
+// Inference max-pool (no argmax): a thread produces MP_ROWS vertically adjacent outputs of one
+// 8-channel chunk and walks the union of their input rows once — each input row's kw-wide maximum
+// is computed once and folded into every output whose window covers it (a 3×3 stride-1 pool loads
+// 6 rows for 4 outputs instead of 12).
+constexpr int MP_ROWS = 4;
+
+__global__ void __launch_bounds__(256) k_maxpool_fwd_rows(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                          PoolGeom g) {
+  const int CG = g.C >> 3;
+  const int PB = (g.P + MP_ROWS - 1) / MP_ROWS;
+  const long long total = (long long)g.N * PB * g.Q * CG;
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int cg = (int)(t % CG);
+    long long pix = t / CG;
+    const int q = (int)(pix % g.Q);
+    pix /= g.Q;
+    const int pb = (int)(pix % PB);
+    const int n = (int)(pix / PB);
+    const int p0 = pb * MP_ROWS;
+    const int np = min(MP_ROWS, g.P - p0);
+    float best[MP_ROWS][8];
+#pragma unroll
+    for (int j = 0; j < MP_ROWS; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) best[j][e] = -INFINITY;
+    const int w0 = q * g.sw - g.pw;
+    const int hlo = p0 * g.sh - g.ph, hhi = (p0 + np - 1) * g.sh - g.ph + g.kh;  // [hlo, hhi)
+    for (int h = max(hlo, 0); h < min(hhi, g.H); ++h) {
+      float rm[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rm[e] = -INFINITY;
+      for (int j = 0; j < g.kw; ++j) {
+        const int w = w0 + j;
+        if ((unsigned)w >= (unsigned)g.W) continue;
+        float v[8];
+        load8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rm[e] = (v[e] > rm[e] || v[e] != v[e]) ? v[e] : rm[e];
+      }
+#pragma unroll
+      for (int j = 0; j < MP_ROWS; ++j) {
+        const int top = (p0 + j) * g.sh - g.ph;
+        if (j < np && h >= top && h < top + g.kh) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) best[j][e] = (rm[e] > best[j][e] || rm[e] != rm[e]) ? rm[e] : best[j][e];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MP_ROWS; ++j)
+      if (j < np) store8(y + (((size_t)n * g.P + p0 + j) * g.Q + q) * g.C + cg * 8, best[j]);
   }
 }
 
@@ -177,6 +232,12 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
     const long long te = (long long)N * P * Q * C;
     hipLaunchKernelGGL(k_maxpool_fwd_c1, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
                        (int8_t*)idx, g, te);
+    BIGDL_CHECK_LAUNCH();
+  }
+  if (!idx) {
+    const long long rows = (long long)N * ((P + MP_ROWS - 1) / MP_ROWS) * Q * (C / 8);
+    hipLaunchKernelGGL(k_maxpool_fwd_rows, dim3(bigdl_grid(rows, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x,
+                       (bf16_t*)y, g);
     BIGDL_CHECK_LAUNCH();
   }
   const long long total = (long long)N * P * Q * (C / 8);

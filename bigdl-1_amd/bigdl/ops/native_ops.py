@@ -1059,7 +1059,8 @@ class _Int8Idx:
 
 
 @register("maxpool2d_forward")
-def maxpool2d_forward(x, k, s, p, ceil_mode):
+def maxpool2d_forward(x, k, s, p, ceil_mode, need_indices=True):
+    """``need_indices=False`` (inference) skips the int8 argmax: 1/3 less traffic."""
     if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
         return NotImplemented
     N_, C_, H, W = x.shape
@@ -1069,10 +1070,10 @@ def maxpool2d_forward(x, k, s, p, ceil_mode):
     P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
     Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
     y = torch.empty((N_, C_, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
-    idx = torch.empty((N_, P, Q, C_), dtype=torch.int8, device=x.device)
+    idx = torch.empty((N_, P, Q, C_), dtype=torch.int8, device=x.device) if need_indices else None
     check(_lib().bigdl_maxpool_fwd(ptr(x), ptr(y), ptr(idx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
                                    _s()), "maxpool_fwd")
-    return y, _Int8Idx(idx)
+    return y, (_Int8Idx(idx) if need_indices else None)
 
 
 @register("maxpool2d_backward")

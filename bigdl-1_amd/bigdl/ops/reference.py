@@ -162,7 +162,9 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
 
 
 # ------------------------------------------------------------------------- pooling
-def maxpool2d_forward(x, k, s, p, ceil_mode):
+def maxpool2d_forward(x, k, s, p, ceil_mode, need_indices=True):
+    if not need_indices:
+        return F.max_pool2d(x, k, s, p, 1, ceil_mode), None
     y, idx = F.max_pool2d(x, k, s, p, 1, ceil_mode, return_indices=True)
     return y, idx
 

@@ -534,3 +534,16 @@ def test_depthwise_conv_native(C, R, st, dil):
     torch.testing.assert_close(gi.float(), xr.grad, rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(gw, wr.grad, rtol=1e-2, atol=1e-2 * float(wr.grad.abs().max()))
     assert not any(k[0].startswith("conv") for k in native.fallback_counts())
+
+
+@pytest.mark.parametrize("shape,k,s,p,ceil", [((4, 64, 28, 28), 3, 1, 1, False), ((2, 192, 56, 56), 3, 2, 0, True),
+                                              ((3, 16, 13, 11), 2, 2, 0, False), ((2, 8, 9, 9), 5, 1, 2, False)])
+def test_maxpool_inference_rows_kernel(shape, k, s, p, ceil):
+    """Inference max-pool (no argmax, row-reuse kernel) vs torch."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    x = _cl(torch.randn(shape, device=dev).bfloat16())
+    y, idx = NO.maxpool2d_forward(x, (k, k), (s, s), (p, p), ceil, need_indices=False)
+    assert idx is None
+    ref = torch.nn.functional.max_pool2d(x.float(), k, s, p, 1, ceil)
+    assert torch.equal(y.float(), ref)
