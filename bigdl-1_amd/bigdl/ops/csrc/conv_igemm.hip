@@ -682,7 +682,10 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const int bk_env = conv_env_override("BIGDL_CONV_BK", 32, 64);
   // (The 3×3 convs with Kg ≤ 1152 run 3–5 % faster alone at BK = 32 — profiles/r2_conv3x3_tile_ab.txt —
   // but the whole step, with wgrad overlapping on a side stream, measured 23.5 vs 23.1 ms: kept at 64.)
-  const int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
+  int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
+  // a channel count that is a multiple of 32 but not 64 (Inception's 96 / 480 / 528-style reductions)
+  // keeps the tap-uniform FAST path at BK = 32 instead of the per-chunk generic gather at BK = 64
+  if (!bk_env && bk == 64 && C % 64 != 0 && C % 32 == 0) bk = 32;
   const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
   const bool fast = (C % bk == 0) && R * S <= 64;
   const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
