@@ -377,6 +377,12 @@ class SpatialFullConvolution(AutogradModule):
         g = self.nGroup
         w4 = w.reshape(g * w.shape[1], w.shape[2], self.kH, self.kW)
         b = self.P("bias") if not self.noBias else None
+        if inp.is_cuda and g == 1 and ops.native_has("conv2d_forward"):
+            y = ops.native_ops.conv_transpose2d(to_device_layout(inp), w4, b, (self.dH, self.dW),
+                                                (self.padH, self.padW), adj)
+            if y is not NotImplemented:
+                return y if batched else y.squeeze(0)
+            ops.native.note_fallback("conv_transpose2d", "geometry", (inp, w4))
         y = F.conv_transpose2d(inp, w4.to(inp.dtype), None if b is None else b.to(inp.dtype), (self.dH, self.dW),
                                (self.padH, self.padW), adj, g)
         return y if batched else y.squeeze(0)

@@ -1819,3 +1819,64 @@ def conv2d_autograd(x, w, b, stride, pad, dilation=(1, 1), groups=1):
     if not ok:
         return NotImplemented
     return _ConvFn.apply(x, w, b, tuple(stride), tuple(pad), tuple(dilation), groups)
+
+
+# ------------------------------------------------------------------------------------------------ transposed conv
+class _DeconvFn(torch.autograd.Function):
+    """Transposed convolution (SpatialFullConvolution) on the conv kernels: its forward is the
+    backward-data of the conv whose weight is [K = C_in][C = C_out][R][S]; its backward-data is that
+    conv's forward; its weight gradient is that conv's weight gradient with the roles of input and
+    output gradient exchanged (conv input = dY, conv output gradient = X)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, out_hw):
+        N_, Cin, H, W = x.shape
+        Cout = w.shape[1]
+        wb = w.detach().to(_bf16)
+        shape = (N_, Cout, out_hw[0], out_hw[1])
+        if tuple(stride) == (1, 1):
+            y = _dgrad_s1(x, wb, shape, pad, (1, 1))
+        else:
+            y = _dgrad_strided(x, wb, shape, tuple(stride), tuple(pad), (1, 1))
+        if y is None:
+            raise RuntimeError("native transposed conv refused its geometry after the eligibility check")
+        if b is not None:
+            y = y + b.to(y.dtype).view(1, -1, 1, 1)
+        ctx.save_for_backward(x, w, b)
+        ctx.geom = (tuple(stride), tuple(pad))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b = ctx.saved_tensors
+        stride, pad = ctx.geom
+        gb = gy.float().sum((0, 2, 3)).to(b.dtype) if b is not None else None  # before the bf16 cast
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+        wb = w.detach().to(_bf16)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = conv2d_forward(gy, wb, None, stride, pad)
+            if gx is NotImplemented:
+                raise RuntimeError("native transposed-conv backward-data refused its geometry")
+        gw = torch.zeros(w.shape, dtype=_f32, device=w.device)
+        _wgrad_launch(gy, x, wb, gw, 1.0, stride, pad, (1, 1), None)
+        return gx, gw.to(w.dtype), gb, None, None, None
+
+
+def conv_transpose2d(x, w, b, stride, pad, adj=(0, 0)):
+    """Differentiable native transposed conv (groups 1); NotImplemented when not eligible.
+    ``w``: [C_in][C_out][R][S]."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last)
+            and _al16(x) and w.dim() == 4 and w.shape[0] == x.shape[1]):
+        return NotImplemented
+    Cin, Cout, R, S = w.shape
+    if Cin % 8 or Cout % 8:
+        return NotImplemented
+    H, W = x.shape[2], x.shape[3]
+    oh = (H - 1) * stride[0] - 2 * pad[0] + R + adj[0]
+    ow = (W - 1) * stride[1] - 2 * pad[1] + S + adj[1]
+    if oh <= 0 or ow <= 0 or adj[0] >= max(stride[0], 1) or adj[1] >= max(stride[1], 1):
+        return NotImplemented
+    if stride[0] == 1 and stride[1] == 1 and (R - 1 - pad[0] < 0 or S - 1 - pad[1] < 0):
+        return NotImplemented
+    return _DeconvFn.apply(x, w, b, tuple(stride), tuple(pad), (oh, ow))

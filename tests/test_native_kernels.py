@@ -547,3 +547,30 @@ def test_maxpool_inference_rows_kernel(shape, k, s, p, ceil):
     assert idx is None
     ref = torch.nn.functional.max_pool2d(x.float(), k, s, p, 1, ceil)
     assert torch.equal(y.float(), ref)
+
+
+@pytest.mark.parametrize("Cin,Cout,R,st,pd,adj", [(32, 16, 3, 1, 1, 0), (16, 32, 4, 2, 1, 0), (64, 32, 3, 2, 1, 1),
+                                                  (32, 32, 2, 2, 0, 0)])
+def test_transposed_conv_native(Cin, Cout, R, st, pd, adj):
+    """SpatialFullConvolution's math (transposed conv) on the conv kernels: forward = conv dgrad,
+    backward-data = conv forward, weight gradient = conv wgrad with roles exchanged — vs torch."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    x = _cl(torch.randn(3, Cin, 9, 11, device=dev).bfloat16())
+    w = (torch.randn(Cin, Cout, R, R, device=dev) * 0.1).requires_grad_(True)
+    b = torch.randn(Cout, device=dev).requires_grad_(True)
+    xg = x.detach().requires_grad_(True)
+    y = NO.conv_transpose2d(xg, w, b, (st, st), (pd, pd), (adj, adj))
+    assert y is not NotImplemented
+    xr = x.float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.conv_transpose2d(xr, wr, br, st, pd, adj)
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=2e-2, atol=3e-2)
+    gy = torch.randn_like(ref)
+    y.float().backward(gy)
+    ref.backward(gy)
+    torch.testing.assert_close(xg.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=3e-2, atol=3e-2 * float(wr.grad.abs().max()))
+    # the output is bf16, so the incoming gradient is bf16-rounded before the bias sum
+    torch.testing.assert_close(b.grad, gy.bfloat16().float().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
