@@ -517,6 +517,19 @@ class TemporalConvolution(AutogradModule):
         batched = x.dim() == 3
         if not batched:
             x = x.unsqueeze(0)
+        if x.is_cuda and ops.native_has("conv2d_forward") and Engine.compute_dtype() == torch.bfloat16:
+            # (N, T, C) frames are the NHWC image (N, C, 1, T): the 2-D native conv with a 1×kW filter
+            # runs on the same memory (weight (out, kW·in) → [out][in][1][kW])
+            xb = x.to(torch.bfloat16).contiguous()
+            x4 = xb.permute(0, 2, 1).unsqueeze(2)
+            if x4.is_contiguous(memory_format=torch.channels_last):
+                w4 = self.P("weight").view(self.outputFrameSize, self.kernelW, self.inputFrameSize) \
+                    .permute(0, 2, 1).unsqueeze(2)
+                y = ops.native_ops.conv2d_autograd(x4, w4, self.P("bias"), (1, self.strideW), (0, 0))
+                if y is not NotImplemented:
+                    y = y.squeeze(2).permute(0, 2, 1)
+                    return y if batched else y.squeeze(0)
+            ops.native.note_fallback("temporal_conv", "geometry", (x,))
         w = self.P("weight").to(x.dtype).view(self.outputFrameSize, self.kernelW, self.inputFrameSize).permute(0, 2, 1)
         y = F.conv1d(x.transpose(1, 2), w, self.P("bias").to(x.dtype), self.strideW).transpose(1, 2)
         return y if batched else y.squeeze(0)

@@ -141,3 +141,28 @@ def test_separable_conv_native_matches_torch():
     torch.testing.assert_close(y.float(), ref.detach(), rtol=3e-2, atol=5e-2)
     torch.testing.assert_close(gi.float(), xr.grad, rtol=3e-2, atol=5e-2)
     _assert_clean()
+
+
+def test_temporal_conv_native_matches_torch():
+    """TemporalConvolution (1-D conv over frames) as the 2-D native conv with a 1×kW filter on the
+    same NHWC memory: forward and input/weight gradients vs torch conv1d."""
+    import bigdl.nn as nn
+    from bigdl import ops
+    ops.reset_fallbacks()
+    torch.manual_seed(0)
+    m = nn.TemporalConvolution(64, 32, 3, 1).to(device=dev)
+    x = torch.randn(4, 20, 64, device=dev).bfloat16()
+    y = m.forward(x)
+    gy = torch.randn(y.shape, device=dev)
+    m.zeroGradParameters()
+    gi = m.backward(x, gy.bfloat16())
+    xr = x.float().requires_grad_(True)
+    w = m.weight.detach().float().view(32, 3, 64).permute(0, 2, 1).contiguous().bfloat16().float().requires_grad_(True)
+    b = m.bias.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.conv1d(xr.transpose(1, 2), w, b, 1).transpose(1, 2)
+    ref.backward(gy.bfloat16().float())
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(gi.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    gw = m.gradWeight.float().view(32, 3, 64).permute(0, 2, 1)
+    torch.testing.assert_close(gw, w.grad, rtol=3e-2, atol=3e-2 * float(w.grad.abs().max()))
+    _assert_clean()
