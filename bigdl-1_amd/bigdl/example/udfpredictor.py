@@ -15,13 +15,15 @@ from .textclassification import synthetic_corpus, train, vectorize
 
 def make_udf(model, w2v, dim, seq_len, batch=256):
     model.evaluate()
+    params = model.parameters()[0]
+    dev = params[0].device if params else torch.device("cpu")
 
     def predict(texts):
         out = []
         for i in range(0, len(texts), batch):
-            x = vectorize(list(texts[i:i + batch]), w2v, dim, seq_len)
+            x = vectorize(list(texts[i:i + batch]), w2v, dim, seq_len).to(dev)  # rows go to the model's device
             with torch.no_grad():
-                out += (model.forward(x).argmax(-1) + 1).tolist()
+                out += (model.forward(x).argmax(-1) + 1).cpu().tolist()
         return out
     return predict
 
