@@ -1880,3 +1880,57 @@ def conv_transpose2d(x, w, b, stride, pad, adj=(0, 0)):
     if stride[0] == 1 and stride[1] == 1 and (R - 1 - pad[0] < 0 or S - 1 - pad[1] < 0):
         return NotImplemented
     return _DeconvFn.apply(x, w, b, tuple(stride), tuple(pad), (oh, ow))
+
+
+# ------------------------------------------------------------------------------------------------ layer norm
+_LN_MAX_H = 4096
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        H = x.shape[-1]
+        rows = x.numel() // H
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=_f32, device=x.device)
+        rstd = torch.empty(rows, dtype=_f32, device=x.device)
+        wf = None if w is None else w.detach().float().contiguous()
+        bf = None if b is None else b.detach().float().contiguous()
+        check(_lib().bigdl_ln_fwd(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), ptr(wf), ptr(bf), ptr(y), ptr(mean),
+                                  ptr(rstd), _ll(rows), C.c_int(H), _f(eps), _s()), "ln_fwd")
+        ctx.save_for_backward(x, wf, mean, rstd)
+        ctx.meta = (w is not None and w.requires_grad, b is not None and b.requires_grad,
+                    None if w is None else w.dtype, None if b is None else b.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wf, mean, rstd = ctx.saved_tensors
+        need_w, need_b, wdt, bdt = ctx.meta
+        H = x.shape[-1]
+        rows = x.numel() // H
+        gy = gy.to(x.dtype).contiguous()
+        gx = torch.empty_like(x)
+        # one buffer: [gw | gb | block partials (≤ 512 rows of 2H)] — a single allocation and memset
+        G = min(512, max(1, (rows + 3) // 4))
+        buf = torch.empty(2 * H + G * 2 * H, dtype=_f32, device=x.device)
+        buf[:2 * H].zero_()
+        gw = buf[:H] if need_w else None
+        gb = buf[H:2 * H] if need_b else None
+        check(_lib().bigdl_ln_bwd(ptr(gy), ptr(x), C.c_int(0 if x.dtype == _f32 else 1), ptr(wf), ptr(mean), ptr(rstd),
+                                  ptr(gx), ptr(gw), ptr(gb), _ll(rows), C.c_int(H), ptr(buf[2 * H:]), _ll(G * 2 * H),
+                                  _s()), "ln_bwd")
+        return gx, None if gw is None else gw.to(wdt), None if gb is None else gb.to(bdt), None
+
+
+@register("layer_norm")
+def layer_norm(x, weight=None, bias=None, eps=1e-5):
+    """Layer normalisation over the last dimension (layernorm.hip): one wave per row, fp32
+    statistics, fp32/bf16 I/O; differentiable w.r.t. x, weight and bias (fp32 [H] each)."""
+    if not (x.is_cuda and x.dtype in (_f32, _bf16) and x.dim() >= 1 and 0 < x.shape[-1] <= _LN_MAX_H
+            and x.numel() > 0):
+        return NotImplemented
+    H = x.shape[-1]
+    if any(p is not None and (p.numel() != H or not p.is_cuda) for p in (weight, bias)):
+        return NotImplemented
+    return _LayerNormFn.apply(x.contiguous(), weight, bias, float(eps))
