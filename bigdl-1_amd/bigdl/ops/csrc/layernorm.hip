@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) k_ln_fwd_v(const T* __restrict__ x, const
 // backward: gx per row from registers; Σ gy·x̂ / Σ gy per lane-owned column across the block's rows,
 // folded over the block's 4 waves in LDS in wave order, one partial row [2H] per block (no atomics:
 // deterministic), summed over blocks by k_ln_colsum
-template <typename T, int J>
+template <typename T, int J, bool KEEP>
 __global__ void __launch_bounds__(256) k_ln_bwd_v(const T* __restrict__ gy, const T* __restrict__ x,
                                                   const float* __restrict__ w, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, T* __restrict__ gx,
@@ -207,24 +207,29 @@ __global__ void __launch_bounds__(256) k_ln_bwd_v(const T* __restrict__ gy, cons
     const T* gr = gy + r * H;
     const T* xr = x + r * H;
     const float mu = mean[r], rs = rstd[r];
-    float g[J][V], xh[J][V];
+    // KEEP: the row stays in registers between the two sweeps; otherwise (wide rows, where
+    // registers go to the parameter-gradient accumulators) the second sweep re-reads it from L2
+    float g[KEEP ? J : 1][V], xh[KEEP ? J : 1][V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int c0 = (lane + 64 * j) * V;
       if (c0 < H) {
+        constexpr int dummy = 0;
         float wv[V];
-        LnVec<T>::ld(gr + c0, g[j]);
-        LnVec<T>::ld(xr + c0, xh[j]);
+        float* gj = g[KEEP ? j : dummy];
+        float* xj = xh[KEEP ? j : dummy];
+        LnVec<T>::ld(gr + c0, gj);
+        LnVec<T>::ld(xr + c0, xj);
         if (w) ln_ldp<V>(w + c0, wv);
 #pragma unroll
         for (int i = 0; i < V; ++i) {
-          xh[j][i] = (xh[j][i] - mu) * rs;
-          aw[j][i] = fmaf(g[j][i], xh[j][i], aw[j][i]);
-          ab[j][i] += g[j][i];
-          g[j][i] *= w ? wv[i] : 1.f;  // ĝ
-          s1 += g[j][i];
-          s2 = fmaf(g[j][i], xh[j][i], s2);
+          xj[i] = (xj[i] - mu) * rs;
+          aw[j][i] = fmaf(gj[i], xj[i], aw[j][i]);
+          ab[j][i] += gj[i];
+          gj[i] *= w ? wv[i] : 1.f;  // ĝ
+          s1 += gj[i];
+          s2 = fmaf(gj[i], xj[i], s2);
         }
       }
     }
@@ -235,8 +240,18 @@ __global__ void __launch_bounds__(256) k_ln_bwd_v(const T* __restrict__ gy, cons
       const int c0 = (lane + 64 * j) * V;
       if (c0 < H) {
         float o[V];
+        if constexpr (KEEP) {
 #pragma unroll
-        for (int i = 0; i < V; ++i) o[i] = rs * (g[j][i] - m1 - xh[j][i] * m2);
+          for (int i = 0; i < V; ++i) o[i] = rs * (g[j][i] - m1 - xh[j][i] * m2);
+        } else {
+          float gv[V], xv[V], wv[V];
+          LnVec<T>::ld(gr + c0, gv);
+          LnVec<T>::ld(xr + c0, xv);
+          if (w) ln_ldp<V>(w + c0, wv);
+#pragma unroll
+          for (int i = 0; i < V; ++i)
+            o[i] = rs * (gv[i] * (w ? wv[i] : 1.f) - m1 - (xv[i] - mu) * rs * m2);
+        }
         LnVec<T>::st(gxr + c0, o);
       }
     }
@@ -314,7 +329,7 @@ static bool ln_bwd_vec(const void* gy, const void* x, const float* w, const floa
   const int per = 64 * V;
   const size_t shm = 2 * H * sizeof(float);
 #define LN_BWD(JJ)                                                                                            \
-  hipLaunchKernelGGL((k_ln_bwd_v<T, JJ>), dim3(G), dim3(256), shm, s, (const T*)gy, (const T*)x, w, mean, rstd, \
+  hipLaunchKernelGGL((k_ln_bwd_v<T, JJ, (JJ * V <= 16)>), dim3(G), dim3(256), shm, s, (const T*)gy, (const T*)x, w, mean, rstd, \
                      (T*)gx, scratch, rows, H)
   if (H <= per) LN_BWD(1);
   else if (H <= 2 * per) LN_BWD(2);
