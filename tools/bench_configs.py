@@ -5,6 +5,7 @@
     python tools/bench_configs.py --config vgg        # 2: VggForCifar10 CIFAR-shape, 1 GPU bf16
     python tools/bench_configs.py --config ptb        # 4: PTB 2-layer LSTM LM (N GPUs via torch.distributed.run)
     python tools/bench_configs.py --config inception  # 5: Inception-v1 from Caffe files, batch inference
+    python tools/bench_configs.py --config transformer  # Transformer LM 6x512 (native LayerNorm A/B)
     python tools/bench_configs.py --config all
 
 Every config builds the model exactly as the reference's example/model builder does, uses synthetic
@@ -278,8 +279,47 @@ def bench_resnet_infer(args):
                        "fold_max_abs_diff": err}}
 
 
+def bench_transformer(args):
+    """Transformer language model (``DL/nn/Transformer.scala``, type LanguageModel with the shared
+    embedding/softmax projection): pre-norm blocks (native LayerNorm kernels), fused attention,
+    TimeDistributedCriterion(CrossEntropy), Adam; bf16 compute, 1 GPU.  ``--no-native-ln`` runs the
+    composed torch LayerNorm for an A/B of the kernel."""
+    import torch
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    from bigdl.utils.engine import Engine
+    Engine.init()
+    dev = Engine.device()
+    if args.no_native_ln:
+        from bigdl.ops import native
+        native._PY_OPS.pop("layer_norm", None)
+    from bigdl.nn import Transformer, CrossEntropyCriterion, TimeDistributedCriterion
+    from bigdl.optim import Adam
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.dataset import MiniBatch
+    B = args.batch or 32
+    L, V, H = args.seq_len if args.seq_len != 20 else 128, 8000, 512
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randint(1, V, (B, L), generator=g)).float().to(dev)
+    y = (torch.randint(0, V, (B, L), generator=g) + 1).float().to(dev)
+    batch = MiniBatch(x, y)
+    model = Transformer(V, H, 8, 2048, 6, 1.0, 1.0, 1.0, with_share_weights_linear=True,
+                        transformer_type="LanguageModel")
+    crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=True)
+    opt = LocalOptimizer(model, [batch], crit, Adam(learningrate=1e-4), batch_size=B)
+    opt.prepare()
+    el, loss = _time_steps(lambda: opt.train_step(batch), dev, args.steps, args.warmup)
+    return {"metric": "tokens/sec Transformer LM 6x512 1 GPU", "value": round(B * L * args.steps / el, 1),
+            "unit": "tokens/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+            "data": "synthetic", "config": {"model": "Transformer-LM", "layers": 6, "hidden": H, "heads": 8,
+                                            "filter": 2048, "vocab": V, "seq_len": L, "global_batch": B,
+                                            "native_layernorm": not args.no_native_ln},
+            "final_loss": float(loss)}
+
+
 CONFIGS = {"lenet": bench_lenet, "vgg": bench_vgg, "ptb": bench_ptb, "inception": bench_inception,
-           "resnet_infer": bench_resnet_infer}
+           "resnet_infer": bench_resnet_infer, "transformer": bench_transformer}
 
 
 def main():
@@ -291,6 +331,7 @@ def main():
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb)")
+    ap.add_argument("--no-native-ln", action="store_true", help="transformer: composed torch LayerNorm")
     args = ap.parse_args()
     names = list(CONFIGS) if args.config == "all" else [args.config]
     for n in names:
