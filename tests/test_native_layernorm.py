@@ -69,3 +69,27 @@ def test_layer_normalization_layer_native(monkeypatch):
     assert gx.shape == x.shape and torch.isfinite(gx).all()
     gw = m.parameters()[1][0]
     assert gw.abs().sum() > 0
+
+
+def test_transformer_lm_step_bf16_on_gpu():
+    """Transformer LM on the GPU under the bf16 config: native LayerNorm in the graph, fp32 master
+    gradients; output within bf16 tolerance of the fp32 CPU model."""
+    from bigdl.utils import config
+    from bigdl.nn import Transformer
+    old = config.get_property("bigdl.compute.dtype")
+    config.set_property("bigdl.compute.dtype", "bf16")
+    try:
+        torch.manual_seed(0)
+        m = Transformer(50, 64, 4, 128, 2, 1.0, 1.0, 1.0, transformer_type="LanguageModel")
+        x = torch.randint(1, 50, (2, 12)).float()
+        ref = m.forward(x).detach().clone()
+        m.cuda()
+        y = m.forward(x.cuda())
+        assert y.is_cuda
+        torch.testing.assert_close(y.float().cpu(), ref, rtol=5e-2, atol=5e-2)
+        m.backward(x.cuda(), torch.ones_like(y))
+        w, g = m.parameters()
+        assert all(t.dtype == torch.float32 for t in g) and all(torch.isfinite(t).all() for t in g)
+        assert sum(float(t.abs().sum()) for t in g) > 0
+    finally:
+        config.set_property("bigdl.compute.dtype", old)
