@@ -208,8 +208,15 @@ BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow,
 // ------------------------------------------------------------------------------------------------
 __global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, bf16_t* __restrict__ shadow, long long n4, float step_size, float b1,
-                       float b2, float eps, float wd, float scale, int tail) {
+                       float b2, float eps, float wd, float scale, int tail, const float* __restrict__ dev_n,
+                       float lr, float lr_decay) {
   long long stride = (long long)gridDim.x * blockDim.x;
+  if (dev_n) {
+    // replay-safe form (HIP graphs): the iteration count n lives on the device, so the decayed
+    // rate and the bias corrections are formed here instead of baked in as a host scalar
+    const float n = dev_n[0], t = n + 1.f;
+    step_size = lr / (1.f + n * lr_decay) * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+  }
   if (blockIdx.x == 0 && threadIdx.x < tail) {
     const long long e = n4 * 4 + threadIdx.x;
     const float gg = g[e] * scale + wd * w[e];
@@ -250,7 +257,18 @@ BIGDL_EXPORT int bigdl_adam(float* w, const float* g, float* m, float* v, bf16_t
   if (n <= 0) return 0;
   const long long n4 = n / 4;
   hipLaunchKernelGGL(k_adam, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, m, v, shadow, n4,
-                     step_size, b1, b2, eps, wd, scale, (int)(n & 3));
+                     step_size, b1, b2, eps, wd, scale, (int)(n & 3), (const float*)nullptr, 0.f, 0.f);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// dev_n: fp32 [1] iteration count before this step (the caller advances it after the launch)
+BIGDL_EXPORT int bigdl_adam_dev(float* w, const float* g, float* m, float* v, bf16_t* shadow, long long n,
+                                const float* dev_n, float lr, float lr_decay, float b1, float b2, float eps, float wd,
+                                float scale, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adam, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, m, v, shadow, n4, 0.f,
+                     b1, b2, eps, wd, scale, (int)(n & 3), dev_n, lr, lr_decay);
   BIGDL_CHECK_LAUNCH();
 }
 

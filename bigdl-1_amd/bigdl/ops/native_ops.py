@@ -912,6 +912,20 @@ def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_sc
     return w
 
 
+@register("adam_step_dev")
+def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0, shadow=None):
+    """Adam whose iteration count ``dev_n`` (fp32 [1], before this step) is read on the device —
+    the replay-safe form for HIP-graph capture; the caller advances ``dev_n`` afterwards."""
+    n = w.numel()
+    if w.dtype != _f32 or not _vec_ok(w, g, m, v, n=n) or not (dev_n.is_cuda and dev_n.dtype == _f32):
+        return NotImplemented
+    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
+        return NotImplemented
+    check(_lib().bigdl_adam_dev(ptr(w), ptr(g), ptr(m), ptr(v), ptr(shadow), _ll(n), ptr(dev_n), _f(lr), _f(lr_decay),
+                                _f(beta1), _f(beta2), _f(eps), _f(weight_decay), _f(grad_scale), _s()), "adam_dev")
+    return w
+
+
 # ------------------------------------------------------------------------------------------------ LSTM
 def _row_view(t, rows, cols):
     """(row stride) of a 2-D view with unit column stride, else None."""

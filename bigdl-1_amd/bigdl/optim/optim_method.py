@@ -446,9 +446,28 @@ class Adam(OptimMethod):
         t = n + 1
         m = self._state_tensor("s", x)
         v = self._state_tensor("r", x)
-        ops.adam_step(x, g, m, v, clr, self.beta1, self.beta2, self.epsilon, t, 0.0, self.grad_scale, self.shadow)
+        if getattr(self, "_graph_mode", False) and x.is_cuda:
+            # replay-safe: iteration count on the device, decayed rate / bias corrections in the kernel
+            nt = self.state.get("_dev_n")
+            if not isinstance(nt, torch.Tensor) or nt.device != x.device:
+                nt = torch.full((1,), float(n), device=x.device)
+                self.state["_dev_n"] = nt
+            r = ops.native_ops.adam_step_dev(x, g, m, v, nt, self.learningRate, self.learningRateDecay, self.beta1,
+                                             self.beta2, self.epsilon, 0.0, self.grad_scale, self.shadow)
+            if r is NotImplemented:
+                raise NotImplementedError("Adam graph mode needs the native fused kernel")
+            nt.add_(1)
+        else:
+            ops.adam_step(x, g, m, v, clr, self.beta1, self.beta2, self.epsilon, t, 0.0, self.grad_scale,
+                          self.shadow)
         self.state["evalCounter"] = t
         return x, [fx]
+
+    def prepare_graph(self) -> bool:
+        if not ops.native_has("adam_step_dev"):
+            return False
+        self._graph_mode = True
+        return True
 
 
 class ParallelAdam(Adam):

@@ -308,13 +308,18 @@ def bench_transformer(args):
     crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=True)
     opt = LocalOptimizer(model, [batch], crit, Adam(learningrate=1e-4), batch_size=B)
     opt.prepare()
-    el, loss = _time_steps(lambda: opt.train_step(batch), dev, args.steps, args.warmup)
+    step = opt.train_step
+    if args.graph:
+        from bigdl.optim.graph_step import graphed_train_step
+        step = lambda b: graphed_train_step(opt, b)  # noqa: E731
+    el, loss = _time_steps(lambda: step(batch), dev, args.steps, args.warmup)
     return {"metric": "tokens/sec Transformer LM 6x512 1 GPU", "value": round(B * L * args.steps / el, 1),
             "unit": "tokens/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
             "data": "synthetic", "config": {"model": "Transformer-LM", "layers": 6, "hidden": H, "heads": 8,
                                             "filter": 2048, "vocab": V, "seq_len": L, "global_batch": B,
-                                            "native_layernorm": not args.no_native_ln},
+                                            "native_layernorm": not args.no_native_ln,
+                                            "hip_graph": bool(args.graph and getattr(opt, "_graphed", None))},
             "final_loss": float(loss)}
 
 
@@ -330,7 +335,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
-    ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb)")
+    ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
     ap.add_argument("--no-native-ln", action="store_true", help="transformer: composed torch LayerNorm")
     args = ap.parse_args()
     names = list(CONFIGS) if args.config == "all" else [args.config]
