@@ -8,7 +8,8 @@ launch.  Requirements, checked at capture time:
 * static shapes (the batch is copied into the graph's static input buffers);
 * no host synchronisation inside the step (a sync raises during capture → eager fallback);
 * per-iteration scalars must not be baked in: dropout draws its Philox seed from a device counter
-  advanced inside the graph, Adagrad keeps its iteration counter on the device, SGD is captured
+  advanced inside the graph, Adagrad and Adam keep their iteration counters on the device (Adam's
+  fused kernel forms the decayed rate and bias corrections from it), SGD is captured
   only with a constant learning rate (``OptimMethod.prepare_graph``).
 
 Only :class:`~bigdl.optim.optimizer.LocalOptimizer` steps are captured (the DistriOptimizer's RCCL
