@@ -54,6 +54,18 @@ def gpu_numa_nodes() -> Dict[int, int]:
     return out
 
 
+def gpu_count() -> int:
+    """Visible AMD GPUs without touching HIP: the DRM render nodes of vendor 0x1002, restricted by
+    ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` when set."""
+    n = len(gpu_numa_nodes())
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [t for t in v.split(",") if t.strip() != ""]
+            n = min(n, len(ids)) if n else len(ids)
+    return max(1, n)
+
+
 def numa_cpus(node: int) -> Optional[List[int]]:
     try:
         with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
@@ -159,8 +171,7 @@ def main(argv=None) -> int:
         ap.error("a script or -m MODULE is required")
     n = a.nproc
     if n is None:
-        import torch
-        n = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
+        n = gpu_count()  # sysfs only: the supervisor never loads the HIP runtime
     if a.module is not None:
         rest = ([a.script] if a.script is not None else []) + a.args
         cmd = [sys.executable, "-m", a.module] + rest

@@ -44,7 +44,9 @@ def Sbn(n, eps=1e-3, momentum=0.1, affine=True):
 
 
 def ResNet(class_num: int, depth: int = 18, shortcut_type: str = ShortcutType.B, dataset: str = DatasetType.CIFAR10,
-           optnet: bool = True):
+           optnet: bool = True, image_size: int = 224):
+    """``image_size`` (ImageNet only) sizes the final average pool (7 at the reference's 224²), so
+    the same topology runs on smaller synthetic images (CPU launch tests)."""
     state = {"iChannels": 64}
 
     def shortcut(n_in, n_out, stride):
@@ -97,7 +99,8 @@ def ResNet(class_num: int, depth: int = 18, shortcut_type: str = ShortcutType.B,
         model.add(layer(block, 128, loop[1], 2))
         model.add(layer(block, 256, loop[2], 2))
         model.add(layer(block, 512, loop[3], 2))
-        model.add(SpatialAveragePooling(7, 7, 1, 1))
+        pool = max(1, -(-int(image_size) // 32))
+        model.add(SpatialAveragePooling(pool, pool, 1, 1))
         model.add(View(n_features).setNumInputDims(3))
         model.add(Linear(n_features, class_num, True, L2Regularizer(1e-4), L2Regularizer(1e-4))
                   .setInitMethod(RandomNormal(0.0, 0.01), Zeros()))

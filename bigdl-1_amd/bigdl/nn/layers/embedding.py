@@ -49,7 +49,7 @@ class LookupTable(TensorModule):
                 self.weight[int(self.paddingValue) - 1].zero_()
         self._renorm(input)
         w = self.cw("weight")
-        y = ops.embedding_forward(w, input, self.paddingValue)
+        y = ops.embedding_forward(w, input, self.paddingValue, self.maskZero)
         if self.maskZero:
             y = y * (input != self.paddingValue).unsqueeze(-1).to(y.dtype)
         return y

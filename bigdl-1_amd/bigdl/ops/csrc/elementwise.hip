@@ -96,8 +96,22 @@ BIGDL_EXPORT int bigdl_threshold_bwd_bf16(const void* gy, const void* ref, void*
 //   d = nesterov ? g' + mom*v : v (or g' when mom == 0) ; w -= lr * (lrs ? lrs*d : d) ;
 //   shadow = bf16(w)
 // ------------------------------------------------------------------------------------------------
-template <bool MOM, bool NEST, bool FIRST, bool SHADOW, bool PERELEM>
-__global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ buf,
+// gradient loads: fp32, or the bf16 reduce-scatter output of the bf16 wire format (read
+// directly — no separate unpack pass over the shard)
+__device__ __forceinline__ float g_at(const float* g, long long e) { return g[e]; }
+__device__ __forceinline__ float g_at(const bf16_t* g, long long e) { return bf2f(g[e]); }
+__device__ __forceinline__ void g_load4(const float* g, long long i, float* o) {
+  float4 G = reinterpret_cast<const float4*>(g)[i];
+  o[0] = G.x; o[1] = G.y; o[2] = G.z; o[3] = G.w;
+}
+__device__ __forceinline__ void g_load4(const bf16_t* g, long long i, float* o) {
+  uint2 G = reinterpret_cast<const uint2*>(g)[i];
+  o[0] = __uint_as_float(G.x << 16); o[1] = __uint_as_float(G.x & 0xffff0000u);
+  o[2] = __uint_as_float(G.y << 16); o[3] = __uint_as_float(G.y & 0xffff0000u);
+}
+
+template <typename GT, bool MOM, bool NEST, bool FIRST, bool SHADOW, bool PERELEM>
+__global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __restrict__ buf,
                       bf16_t* __restrict__ shadow, const float* __restrict__ lrs, const float* __restrict__ wds,
                       long long n4, float lr, float mom, float damp, float wd, float scale, int tail) {
   long long stride = (long long)gridDim.x * blockDim.x;
@@ -105,7 +119,7 @@ __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float*
     // the n % 4 trailing elements (scalar; the arena slice need not be a multiple of 4)
     const long long e = n4 * 4 + threadIdx.x;
     const float wv = w[e];
-    const float gg = g[e] * scale + wd * (PERELEM && wds ? wds[e] : 1.f) * wv;
+    const float gg = g_at(g, e) * scale + wd * (PERELEM && wds ? wds[e] : 1.f) * wv;
     float d = gg;
     if (MOM) {
       const float b = FIRST ? gg : mom * buf[e] + (1.f - damp) * gg;
@@ -118,9 +132,9 @@ __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float*
   }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 W = reinterpret_cast<float4*>(w)[i];
-    float4 G = reinterpret_cast<const float4*>(g)[i];
     float wv[4] = {W.x, W.y, W.z, W.w};
-    float gv[4] = {G.x, G.y, G.z, G.w};
+    float gv[4];
+    g_load4(g, i, gv);
     float wdv[4] = {1.f, 1.f, 1.f, 1.f};
     float lrv[4] = {1.f, 1.f, 1.f, 1.f};
     if (PERELEM) {
@@ -159,13 +173,13 @@ __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float*
 }
 
 #define SGD_LAUNCH(M, NS, F, SH, PE)                                                                    \
-  hipLaunchKernelGGL((k_sgd<M, NS, F, SH, PE>), dim3(grid), dim3(256), 0, s, w, g, buf, shadow, lrs, wds, n4, lr, \
-                     mom, damp, wd, scale, tail)
+  hipLaunchKernelGGL((k_sgd<GT, M, NS, F, SH, PE>), dim3(grid), dim3(256), 0, s, w, g, buf, shadow, lrs, wds, n4, \
+                     lr, mom, damp, wd, scale, tail)
 
-// all pointers 16-B aligned (host-checked); the n % 4 tail is handled by block 0.
-BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
-                           long long n, float lr, float mom, float damp, float wd, int nesterov, int first,
-                           float scale, hipStream_t s) {
+template <typename GT>
+static int sgd_impl(float* w, const GT* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
+                    long long n, float lr, float mom, float damp, float wd, int nesterov, int first, float scale,
+                    hipStream_t s) {
   if (n <= 0) return 0;
   const long long n4 = n / 4;
   const int tail = (int)(n & 3);
@@ -200,6 +214,21 @@ BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow,
     }
   }
   BIGDL_CHECK_LAUNCH();
+}
+
+
+// all pointers 16-B aligned (host-checked); the n % 4 tail is handled by block 0.
+BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
+                           long long n, float lr, float mom, float damp, float wd, int nesterov, int first,
+                           float scale, hipStream_t s) {
+  return sgd_impl<float>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, s);
+}
+
+// same update with a bf16 gradient (the bf16-wire reduce-scatter output); g 8-B aligned
+BIGDL_EXPORT int bigdl_sgd_g16(float* w, const bf16_t* g, float* buf, bf16_t* shadow, const float* lrs,
+                               const float* wds, long long n, float lr, float mom, float damp, float wd, int nesterov,
+                               int first, float scale, hipStream_t s) {
+  return sgd_impl<bf16_t>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, s);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,7 +1,10 @@
 // Embedding lookup (K16): LookupTable.updateOutput gather and accGradParameters scatter-add
 // (DL/nn/LookupTable.scala:170-230).  1-based indices arrive as the layer's float tensor (the
-// reference's Tensor[T] of ids) or as int32 / int64; an index is clamped into [1, nIndex] on the
-// device so a bad id can never address outside the table (the host wrapper range-checks first).
+// reference's Tensor[T] of ids) or as int32 / int64.  The reference requires 1 <= id <= nIndex
+// (LookupTable.scala:96-98,227-229): the forward kernel sets a device error flag (a vector atomic
+// OR into a 4-byte buffer) for any id outside that range, which the host wrapper reads back
+// asynchronously and raises on; the index is still clamped on the device so a bad id can never
+// address outside the table.
 //
 // Forward: one wave per index row, 16-B vector copies (8 bf16 / 4 fp32 per lane).
 // Backward: grad[id − 1][:] += scale · gy[i][:] with no-return fp32 atomics (many ids repeat —
@@ -17,10 +20,16 @@ __device__ __forceinline__ long long row_of(const I* idx, long long i, long long
 
 template <typename I, typename T>
 __global__ void __launch_bounds__(256) k_embed_fwd(const T* __restrict__ w, const I* __restrict__ idx, T* __restrict__ out,
-                                                   long long n, long long n_index, int D) {
+                                                   long long n, long long n_index, int D, int* __restrict__ err,
+                                                   int has_allow, float allow_v) {
   const long long i = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const int lane = threadIdx.x & 63;
+  if (err != nullptr && lane == 0) {
+    const long long raw = (long long)idx[i];
+    const bool allowed = has_allow && (float)idx[i] == allow_v;  // masked padding id (maskZero)
+    if (!allowed && (raw < 1 || raw > n_index || (float)idx[i] != (float)raw)) atomicOr(err, 1);
+  }
   const long long r = row_of(idx, i, n_index);
   const T* src = w + r * D;
   T* dst = out + i * D;
@@ -69,23 +78,28 @@ __global__ void __launch_bounds__(256) k_embed_bwd_det(float* __restrict__ gw, c
 // itype: 0 = float32 ids, 1 = int64, 2 = int32; dtype: 0 = bf16 table/gradient, 1 = fp32
 template <typename T>
 static void launch_fwd(int itype, dim3 g, hipStream_t s, const void* w, const void* idx, void* out, long long n,
-                       long long ni, int D) {
+                       long long ni, int D, int* err, int ha, float av) {
   if (itype == 0)
-    hipLaunchKernelGGL((k_embed_fwd<float, T>), g, dim3(256), 0, s, (const T*)w, (const float*)idx, (T*)out, n, ni, D);
+    hipLaunchKernelGGL((k_embed_fwd<float, T>), g, dim3(256), 0, s, (const T*)w, (const float*)idx, (T*)out, n, ni, D,
+                       err, ha, av);
   else if (itype == 1)
     hipLaunchKernelGGL((k_embed_fwd<long long, T>), g, dim3(256), 0, s, (const T*)w, (const long long*)idx, (T*)out, n,
-                       ni, D);
+                       ni, D, err, ha, av);
   else
-    hipLaunchKernelGGL((k_embed_fwd<int, T>), g, dim3(256), 0, s, (const T*)w, (const int*)idx, (T*)out, n, ni, D);
+    hipLaunchKernelGGL((k_embed_fwd<int, T>), g, dim3(256), 0, s, (const T*)w, (const int*)idx, (T*)out, n, ni, D,
+                       err, ha, av);
 }
 
+// err: optional device int (4-B aligned) OR-ed with 1 when an id is outside [1, n_index]; an id
+// equal to allow_v (has_allow: the maskZero padding id) is exempt
 BIGDL_EXPORT int bigdl_embedding_fwd(const void* w, const void* idx, int itype, void* out, long long n,
-                                     long long n_index, int D, int dtype, hipStream_t s) {
+                                     long long n_index, int D, int dtype, int* err, int has_allow, float allow_v,
+                                     hipStream_t s) {
   if (n <= 0 || n_index <= 0 || D <= 0 || itype < 0 || itype > 2) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)w & 15) || ((uintptr_t)out & 15)) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)w & 15) || ((uintptr_t)out & 15) || ((uintptr_t)err & 3)) return (int)hipErrorInvalidValue;
   dim3 g((unsigned)((n + 3) / 4));
-  if (dtype == 0) launch_fwd<bf16_t>(itype, g, s, w, idx, out, n, n_index, D);
-  else launch_fwd<float>(itype, g, s, w, idx, out, n, n_index, D);
+  if (dtype == 0) launch_fwd<bf16_t>(itype, g, s, w, idx, out, n, n_index, D, err, has_allow, allow_v);
+  else launch_fwd<float>(itype, g, s, w, idx, out, n, n_index, D, err, has_allow, allow_v);
   BIGDL_CHECK_LAUNCH();
 }
 

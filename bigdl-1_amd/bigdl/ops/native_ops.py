@@ -884,17 +884,23 @@ def _vec_ok(*ts, n):
 @register("sgd_step")
 def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale=1.0, shadow=None,
              lrs=None, wds=None):
+    """Fused SGD over a flat fp32 slice; ``g`` is fp32 or bf16 (the bf16-wire reduce-scatter output,
+    read directly by the kernel instead of being unpacked into an fp32 shard first)."""
     n = w.numel()
-    if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, buf, lrs, wds, n=n):
+    if w.dtype != _f32 or g.dtype not in (_f32, _bf16) or not _vec_ok(w, buf, lrs, wds, n=n):
+        return NotImplemented
+    g16 = g.dtype == _bf16
+    if not (g.is_cuda and g.is_contiguous() and g.numel() == n and g.data_ptr() % (8 if g16 else 16) == 0):
         return NotImplemented
     if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.numel() == n
                                    and shadow.data_ptr() % 8 == 0):
         return NotImplemented
     if momentum != 0 and buf is None:
         return NotImplemented
-    check(_lib().bigdl_sgd(ptr(w), ptr(g), ptr(buf if momentum != 0 else None), ptr(shadow), ptr(lrs), ptr(wds),
-                           _ll(n), _f(lr), _f(momentum), _f(dampening), _f(weight_decay), C.c_int(int(bool(nesterov))),
-                           C.c_int(int(bool(first_step))), _f(grad_scale), _s()), "sgd")
+    fn = _lib().bigdl_sgd_g16 if g16 else _lib().bigdl_sgd
+    check(fn(ptr(w), ptr(g), ptr(buf if momentum != 0 else None), ptr(shadow), ptr(lrs), ptr(wds),
+             _ll(n), _f(lr), _f(momentum), _f(dampening), _f(weight_decay), C.c_int(int(bool(nesterov))),
+             C.c_int(int(bool(first_step))), _f(grad_scale), _s()), "sgd")
     return w
 
 
@@ -902,7 +908,7 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
 def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0, shadow=None):
     import math
     n = w.numel()
-    if w.dtype != _f32 or not _vec_ok(w, g, m, v, n=n):
+    if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n):
         return NotImplemented
     if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
         return NotImplemented
@@ -917,7 +923,8 @@ def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_dec
     """Adam whose iteration count ``dev_n`` (fp32 [1], before this step) is read on the device —
     the replay-safe form for HIP-graph capture; the caller advances ``dev_n`` afterwards."""
     n = w.numel()
-    if w.dtype != _f32 or not _vec_ok(w, g, m, v, n=n) or not (dev_n.is_cuda and dev_n.dtype == _f32):
+    if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n) or not (dev_n.is_cuda and
+                                                                                  dev_n.dtype == _f32):
         return NotImplemented
     if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
         return NotImplemented
@@ -1452,8 +1459,46 @@ def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=Non
 _ITYPE = {_f32: 0, torch.int64: 1, torch.int32: 2}
 
 
+# Out-of-range ids (the reference requires 1 <= id <= nIndex, LookupTable.scala:96-98,227-229):
+# the forward kernel ORs a per-device error flag; after each launch the flag is copied to pinned
+# host memory behind an event, and the NEXT embedding call (or embedding_check) raises once that
+# copy has landed — no host/device synchronisation on the hot path.  bigdl.embedding.syncCheck
+# checks synchronously after every launch (debugging).
+_EMB = {}
+
+
+def _emb_state(dev):
+    st = _EMB.get(dev)
+    if st is None:
+        st = _EMB[dev] = {"flag": torch.zeros(1, dtype=torch.int32, device=dev),
+                          "host": torch.zeros(1, dtype=torch.int32, pin_memory=True), "event": None, "n_index": 0}
+    return st
+
+
+def embedding_check(dev=None, sync: bool = False) -> None:
+    """Raise if an embedding lookup since the last check saw an id outside [1, nIndex]."""
+    for d, st in list(_EMB.items()):
+        if dev is not None and d != dev:
+            continue
+        ev = st["event"]
+        if ev is None:
+            continue
+        if sync:
+            ev.synchronize()
+        elif not ev.query():
+            continue
+        st["event"] = None
+        if int(st["host"][0]) != 0:
+            st["flag"].zero_()
+            st["host"].zero_()
+            raise IndexError(f"LookupTable: an input id is outside [1, {st['n_index']}] "
+                             "(elements of input should be >= 1 and <= nIndex)")
+
+
 @register("embedding_forward")
-def embedding_forward(weight, idx_1b, padding_value=0):
+def embedding_forward(weight, idx_1b, padding_value=0, mask_zero=False):
+    """Gather rows ``weight[id - 1]``; ids must lie in [1, nIndex] (``mask_zero``: the padding id is
+    also accepted — the layer zeroes its rows)."""
     if weight.dim() != 2 or weight.dtype not in (_bf16, _f32) or not weight.is_contiguous() or not _al16(weight):
         return NotImplemented
     if not idx_1b.is_cuda or idx_1b.dtype not in _ITYPE or idx_1b.numel() == 0:
@@ -1461,10 +1506,23 @@ def embedding_forward(weight, idx_1b, padding_value=0):
     idx = idx_1b if idx_1b.is_contiguous() else idx_1b.contiguous()
     n = idx.numel()
     D = weight.shape[1]
+    capturing = torch.cuda.is_current_stream_capturing()
+    st = _emb_state(weight.device)
+    if not capturing:
+        embedding_check(weight.device)
     out = torch.empty((*idx_1b.shape, D), dtype=weight.dtype, device=weight.device)
     check(_lib().bigdl_embedding_fwd(ptr(weight), ptr(idx), C.c_int(_ITYPE[idx.dtype]), ptr(out), _ll(n),
                                      _ll(weight.shape[0]), C.c_int(D), C.c_int(0 if weight.dtype == _bf16 else 1),
-                                     _s()), "embedding_fwd")
+                                     ptr(st["flag"]), C.c_int(1 if mask_zero else 0), _f(padding_value), _s()),
+          "embedding_fwd")
+    st["n_index"] = int(weight.shape[0])
+    if not capturing and st["event"] is None:
+        st["host"].copy_(st["flag"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st["event"] = ev
+        if config.get_property("bigdl.embedding.syncCheck"):
+            embedding_check(weight.device, sync=True)
     return out
 
 

@@ -281,6 +281,7 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
 
     ``grad_scale`` folds the 1/N gradient averaging in; ``lrs``/``wds`` are per-element
     learning-rate / weight-decay multipliers (``learningRates``/``weightDecays``)."""
+    g = g.float()  # a bf16-wire gradient shard is consumed directly
     gg = g * grad_scale if grad_scale != 1.0 else g.clone()
     if weight_decay != 0:
         gg.add_(w * (wds if wds is not None else 1.0), alpha=weight_decay)
@@ -366,9 +367,17 @@ def lstm_cell_backward(gh, gh2, gc_next, act, tc, c_prev, dg_out=None):
 
 
 # ------------------------------------------------------------------------- embedding / dropout / lrn
-def embedding_forward(weight, idx_1b, padding_value=0):
+def embedding_forward(weight, idx_1b, padding_value=0, mask_zero=False):
+    """``weight[id - 1]``; ids outside [1, nIndex] raise (``LookupTable.scala:96-98``) except the
+    padding id under ``mask_zero`` (its rows are zeroed by the layer)."""
     idx = idx_1b.long() - 1
-    return weight[idx.clamp(min=0)]
+    bad = (idx < 0) | (idx >= weight.shape[0]) | (idx_1b != idx_1b.long().to(idx_1b.dtype))
+    if mask_zero:
+        bad &= idx_1b != padding_value
+    if bool(bad.any()):
+        raise IndexError(f"LookupTable: an input id is outside [1, {weight.shape[0]}] "
+                         "(elements of input should be >= 1 and <= nIndex)")
+    return weight[idx.clamp(min=0, max=weight.shape[0] - 1)]
 
 
 def embedding_backward(grad_weight, idx_1b, gy, scale=1.0, padding_value=0):

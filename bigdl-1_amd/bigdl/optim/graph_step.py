@@ -26,6 +26,16 @@ log = get_logger("bigdl.optim")
 
 
 class GraphedTrainStep:
+    """Capture ``optimizer.train_step`` into one HIP graph.
+
+    Capture needs ``warmup`` eager steps first (allocator pools, lazily built state).  Those steps
+    are NOT part of training: every tensor they change — master weights, the bf16 shadow, BN
+    running statistics, optimizer state — is snapshotted before and restored IN PLACE after the
+    capture (the graph keeps pointing at the same storage), host counters (``evalCounter``) are
+    restored and device counters (``_dev_n``) re-synchronised, so the first :meth:`step` is the
+    trajectory's first iteration.  Optimizer state that the warmup created (SGD's momentum buffer)
+    is zeroed and the next step runs eagerly once with first-iteration semantics."""
+
     def __init__(self, optimizer, batch: MiniBatch, warmup: int = 3):
         if not torch.cuda.is_available():
             raise RuntimeError("HIP graph capture needs a GPU")
@@ -39,6 +49,7 @@ class GraphedTrainStep:
         self.sx = x.clone(memory_format=torch.preserve_format)
         self.sy = y.clone() if isinstance(y, torch.Tensor) else y
         b = MiniBatch(self.sx, self.sy)
+        snap = self._snapshot()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -50,6 +61,49 @@ class GraphedTrainStep:
         with torch.cuda.graph(self.graph):
             self.loss = optimizer.train_step(b)
         torch.cuda.synchronize()
+        self.eager_next = self._restore(snap)
+        torch.cuda.synchronize()
+
+    # -------------------------------------------------------------------------- warmup undo
+    def _tensors(self):
+        opt = self.opt
+        flat = getattr(opt, "flat", None)
+        ts = []
+        if flat is not None:
+            ts += [t for t in (flat.weight, flat.shadow) if t is not None]
+        ts += list(opt.model.getExtraParameter() or [])
+        return ts
+
+    def _snapshot(self):
+        ts = [(t, t.detach().clone()) for t in self._tensors()]
+        states = {}
+        for name, meth in self.opt.optim_methods.items():
+            states[name] = {k: (v.detach().clone() if isinstance(v, torch.Tensor) else v)
+                            for k, v in meth.state.items()}
+        return ts, states
+
+    def _restore(self, snap) -> bool:
+        ts, states = snap
+        for t, c in ts:
+            t.copy_(c)
+        eager_next = False
+        for name, meth in self.opt.optim_methods.items():
+            pre = states[name]
+            for k in list(meth.state.keys()):
+                v = meth.state[k]
+                if k in pre:
+                    if isinstance(v, torch.Tensor) and isinstance(pre[k], torch.Tensor) and v.shape == pre[k].shape:
+                        v.copy_(pre[k])
+                    else:
+                        meth.state[k] = pre[k]
+                elif isinstance(v, torch.Tensor):
+                    v.zero_()  # created by the warmup: back to its initial (zero) value
+                    if meth.graph_state_created(k):
+                        eager_next = True
+                else:
+                    del meth.state[k]
+            meth.sync_device_counter()
+        return eager_next
 
     def step(self, batch: MiniBatch = None) -> torch.Tensor:
         if batch is not None:
@@ -58,8 +112,12 @@ class GraphedTrainStep:
                 self.sx.copy_(x, non_blocking=True)
             if isinstance(y, torch.Tensor) and y is not self.sy:
                 self.sy.copy_(y, non_blocking=True)
-        self.graph.replay()
         self.opt.state["neval"] = self.opt.state.get("neval", 0) + 1
+        if self.eager_next:
+            # first iteration after capture with freshly created state (SGD momentum: v = g)
+            self.eager_next = False
+            return self.opt.train_step(MiniBatch(self.sx, self.sy))
+        self.graph.replay()
         for meth in self.opt.optim_methods.values():
             meth.after_graph_replay()
         return self.loss

@@ -44,6 +44,18 @@ class OptimMethod:
         """Advance the host-side counters one iteration (a replay runs no Python)."""
         self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
 
+    def sync_device_counter(self):
+        """Set the device-side iteration counter (graph mode) from the host ``evalCounter`` — after
+        a checkpoint restore or when a graph capture's warmup steps are undone."""
+        nt = self.state.get("_dev_n")
+        if isinstance(nt, torch.Tensor):
+            nt.fill_(float(self.state.get("evalCounter", 0)))
+
+    def graph_state_created(self, key: str) -> bool:
+        """True when state ``key``, newly created by capture warmup, needs an eager
+        first-iteration update (it cannot be emulated by a zero tensor)."""
+        return False
+
     def clearHistory(self):
         keep = {k: self.state[k] for k in ("epoch", "neval", "evalCounter", "recordsProcessedThisEpoch", "Loss",
                                            "score", "trainingTime") if k in self.state}
@@ -317,6 +329,13 @@ class SGD(OptimMethod):
         # the fused kernel takes lr by value: replayable only while the schedule is constant
         return type(self.learningRateSchedule) is Default and self.learningRateDecay == 0
 
+    def graph_state_created(self, key):
+        # a zero momentum buffer equals the first-iteration rule (v = g) only without dampening
+        if key == "dfdx" and self.momentum != 0:
+            self._first_pending = True
+            return True
+        return False
+
     def __init__(self, learningrate=1e-3, learningrate_decay=0.0, weightdecay=0.0, momentum=0.0,
                  dampening=float("inf"), nesterov=False, leaningrate_schedule=None, learningrates=None,
                  weightdecays=None, bigdl_type="float"):
@@ -399,7 +418,7 @@ class SGD(OptimMethod):
         fx, dfdx = feval(x)
         clr = self.learningRateSchedule.currentRate  # negative
         first = "dfdx" not in self.state or not isinstance(self.state.get("dfdx"), torch.Tensor) or \
-            self.state["dfdx"].shape != x.shape
+            self.state["dfdx"].shape != x.shape or self.__dict__.pop("_first_pending", False)
         buf = self._state_tensor("dfdx", x) if self.momentum != 0 else None
         lrs, wd, wds = self._decays(x.device)
         ops.sgd_step(x, dfdx, buf, -clr, self.momentum, self.dampening, wd, self.nesterov, first,

@@ -88,12 +88,14 @@ class BaseOptimizer:
         self.constant_clip = None
         self.l2_clip = None
         self.drop_percentage = 0.0
+        self.max_drop_percentage = 0.0
         self.reserve_optim_state = False
         self.metrics = Metrics()
         self.log_interval = 1
         self.device = Engine.device()
         self.compute_dtype = Engine.compute_dtype()
         self._pending_loss: Optional[_LazyScalar] = None
+        self._skipped = False
 
     # ------------------------------------------------------------------------------ data helpers
     @staticmethod
@@ -205,14 +207,14 @@ class BaseOptimizer:
         return self.prepareInput()
 
     def setDropModuleProperty(self, drop_percentage, max_drop_percentage, batchsize=100, warmup_iteration=200):
-        """Straggler handling (P5, ``DistriOptimizer.scala:246-278,421-449``).  With
-        ``drop_percentage > 0`` every rank times its iterations with HIP events and every
-        ``batchsize`` iterations (after ``warmup_iteration``) the ranks all-gather their step times:
-        the threshold is ``Util.kthLargest`` at k = drop_percentage · batchsize · world and ranks whose
-        mean step time exceeds ``bigdl.straggler.factor`` × the median are logged
-        (:class:`bigdl.utils.tracing.StepTracer`).  A synchronous RCCL reduce-scatter cannot discard a
-        late rank's gradient the way the reference cancels late replica threads, so slow ranks are
-        detected and reported, not dropped."""
+        """Straggler handling (P5, ``DistriOptimizer.scala:240-280,343-345,421-449,510-515``).  With
+        ``drop_percentage > 0`` the DistriOptimizer times every rank's forward + backward; every
+        ``batchsize`` iterations after ``warmup_iteration`` the ranks all-gather those times and the
+        threshold becomes ``Util.kthLargest`` at k = drop_percentage · batchsize · world minus the
+        ranks already dropped in the window.  A rank over the threshold contributes a zero gradient
+        and a finished-count of 0; the update averages over the finished ranks, and an iteration
+        where fewer than ``(1 − max_drop_percentage)·world`` ranks finished is discarded (see
+        :mod:`bigdl.parallel.distri_optimizer`)."""
         self.drop_percentage = float(drop_percentage)
         self.max_drop_percentage = float(max_drop_percentage)
         self._straggler_window = int(batchsize)
@@ -449,7 +451,13 @@ class BaseOptimizer:
             t0 = time.perf_counter()
             batch = next(batches)
             bs = batch.size()
+            it = self.state["neval"]
             loss_t = self._step(batch)
+            if self._skipped:
+                # straggler drop discarded this iteration's gradients: it does not count
+                # (DistriOptimizer.scala:510-515 — neval / records do not advance)
+                self._skipped = False
+                continue
             # bookkeeping (no device sync: the loss is read one iteration late)
             if not (isinstance(loss_t, torch.Tensor) and loss_t.is_cuda) or self._needs_loss():
                 # host tensor, or a consumer (summary / MinLoss trigger) needs this iteration's value
@@ -460,7 +468,6 @@ class BaseOptimizer:
                 self._pending_loss = _LazyScalar(loss_t)
                 if prev is not None:
                     self.state["Loss"] = prev.value() if prev.ready() else self.state["Loss"]
-            it = self.state["neval"]
             global_bs = bs * Engine.world_size()
             self.state["recordsProcessedThisEpoch"] += global_bs
             dt = time.perf_counter() - t0
@@ -680,7 +687,7 @@ class BaseOptimizer:
         self._flush_weights()
         if Engine.rank() == 0:
             save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite,
-                            asynchronous=asynchronous)
+                            asynchronous=asynchronous, slices=getattr(self, "_method_slices", None))
 
     def _maybe_resume(self):
         """Resume from the latest checkpoint when this process is a launcher restart
@@ -714,18 +721,31 @@ class BaseOptimizer:
         if methods:
             # copy only the restored STATE into the live method objects: the per-run installation
             # (grad_scale = 1/W, folded L2 decay vectors, shard-space lr/decay vectors) lives on
-            # those objects and is not part of a checkpoint
-            pairs = [(self.optim_methods.get(k), v) for k, v in methods.items()]
-            if any(c is None for c, _ in pairs) and len(methods) == len(self.optim_methods):
-                # keys built from default module names differ per process: match by sorted position
-                pairs = [(self.optim_methods[k], methods[kk]) for k, kk in zip(sorted(self.optim_methods),
-                                                                                sorted(methods))]
-            for cur, v in pairs:
-                if cur is None:
-                    continue
-                cur.state.clear()
+            # those objects and is not part of a checkpoint.  Tensors are copied IN PLACE so a
+            # captured HIP graph keeps pointing at the live state; when that is impossible (a
+            # state tensor appears, disappears or changes shape) the graph is dropped and recaptured.
+            graph_stale = False
+            for cur, v in self._match_restored_methods(methods):
                 for sk, sv in v.state.items():
-                    cur.state[sk] = sv.to(self.device) if isinstance(sv, torch.Tensor) else sv
+                    old = cur.state.get(sk)
+                    if isinstance(sv, torch.Tensor):
+                        sv = sv.to(self.device)
+                        if (isinstance(old, torch.Tensor) and old.shape == sv.shape and old.dtype == sv.dtype
+                                and old.device == sv.device):
+                            old.copy_(sv)
+                            continue
+                        graph_stale = True
+                    cur.state[sk] = sv
+                for sk in [k for k, t in cur.state.items() if isinstance(t, torch.Tensor) and k not in v.state]:
+                    if sk == "_dev_n":
+                        continue  # re-derived from evalCounter below
+                    del cur.state[sk]
+                    graph_stale = True
+                cur.sync_device_counter()
+            if graph_stale and getattr(self, "_graphed", None) is not None:
+                log.info("optimizer state layout changed by the restore: the HIP-graph step will be recaptured")
+                self._graphed = None
+                self._graph_failed = False
         if state:
             self.state.update(state)
         if self.flat is not None and self.flat.shadow is not None:
@@ -734,6 +754,25 @@ class BaseOptimizer:
 
     def _on_restore(self):
         pass
+
+    def _match_restored_methods(self, methods):
+        """Pair restored OptimMethods with the live ones: by the arena slice each owns when the
+        checkpoint recorded it, else by key, else (one method on each side) directly.  Anything
+        else is ambiguous and raises instead of guessing."""
+        by_slice = {tuple(v): k for k, v in getattr(self, "_method_slices", {}).items()}
+        pairs = []
+        for k, v in methods.items():
+            sl = getattr(v, "_arena_slice", None)
+            if sl is not None and tuple(sl) in by_slice:
+                pairs.append((self.optim_methods[by_slice[tuple(sl)]], v))
+            elif k in self.optim_methods:
+                pairs.append((self.optim_methods[k], v))
+            elif len(methods) == 1 and len(self.optim_methods) == 1:
+                pairs.append((next(iter(self.optim_methods.values())), v))
+            else:
+                raise ValueError(f"checkpointed OptimMethod '{k}' matches no live OptimMethod "
+                                 f"({sorted(self.optim_methods)}) by arena slice or name")
+        return pairs
 
 
 class LocalOptimizer(BaseOptimizer):

@@ -24,9 +24,30 @@ MI355X mapping (``bigdl.comm.*`` config keys):
     ``bf16_truncate`` reproduces the reference's truncating wire format exactly.
   * Non-sliceable methods (LBFGS, Ftrl, …) or several OptimMethods with non-SGD/Adam members fall
     back to "replicated" mode: all-reduce of the full gradient, full update on every rank.
+
+Streams.  Every collective is issued from the comm-side stream (``_side``): it first waits for the
+compute stream's work so far and for the side-stream weight-gradient kernels queued so far
+(``join_wgrad(side)``), packs the bucket to the wire dtype there (one cast kernel per bucket) and
+launches the RCCL op — the compute stream never blocks on a bucket; only the consumer of the
+result (the shard update, or the next forward's first use of a bucket) waits.  On the CPU the side
+stream is a no-op stand-in (:class:`_HostStream`), so the same early-update code path runs under
+gloo in the multi-process tests.  The SGD kernel reads the bf16 reduce-scatter output directly.
+
+Straggler drop (P5, ``DistriOptimizer.scala:240-280,343-345,421-449,510-515``): with
+``setDropModuleProperty(dropPercentage, maxDropPercentage, batchsize, warmup)`` each rank times its
+forward + backward; every ``batchsize`` iterations after warm-up the ranks all-gather those times and
+the threshold becomes ``kthLargest(times, k − dropped)`` with ``k = dropPercentage·batchsize·N``
+(or grows 1 % when enough were dropped).  A rank whose compute time exceeds the threshold
+contributes a ZERO gradient and a finished-count of 0 to the same collectives; the update divides
+by the all-reduced finished count, the loss is averaged over the finished ranks, and when fewer than
+``(1 − maxDropPercentage)·N`` ranks finished the iteration's gradients are discarded (no update, the
+iteration counter does not advance).  Unlike the reference's thread pool a rank cannot cancel its
+queued GPU kernels, so a straggler still finishes its backward before the collectives proceed: the
+mechanism reproduces the reference's update semantics, not its latency cut.
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from typing import Dict, List, Optional
 
@@ -42,9 +63,28 @@ from . import comm
 log = get_logger("bigdl.parallel")
 
 
+class _HostStream:
+    """Stand-in for the comm-side HIP stream on the CPU: work issued "on" it runs in program
+    order on the host, so waits are no-ops (lets the gloo tests drive the early-update path)."""
+
+    def wait_stream(self, other):
+        pass
+
+    def wait_event(self, ev):
+        pass
+
+
+def _on(stream):
+    return torch.cuda.stream(stream) if isinstance(stream, torch.cuda.Stream) else contextlib.nullcontext()
+
+
+def _cur_stream(dev):
+    return torch.cuda.current_stream(dev) if dev.type == "cuda" else _HostStream()
+
+
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "slo", "shi", "pending", "expected", "rs_work", "ag_work", "ready",
-                 "modules", "needs_shadow", "early", "rs_keep")
+                 "modules", "needs_shadow", "early", "rs_keep", "unpacked")
 
     def __init__(self, idx, lo, hi, slo, shi):
         self.idx, self.lo, self.hi, self.slo, self.shi = idx, lo, hi, slo, shi
@@ -57,6 +97,7 @@ class _Bucket:
         self.needs_shadow = False
         self.early = False
         self.rs_keep = None
+        self.unpacked = False
 
 
 class DistriOptimizer(BaseOptimizer):
@@ -175,10 +216,19 @@ class DistriOptimizer(BaseOptimizer):
         for b in self.buckets:
             b.expected = len(b.modules)
         self._install_hooks()
-        self._side = None
-        if (self.sharded and dev.type == "cuda" and config.get_property("bigdl.comm.earlyUpdate")):
+        if dev.type == "cuda":
             prio = int(config.get_property("bigdl.comm.streamPriority"))
             self._side = torch.cuda.Stream(device=dev, priority=prio)
+        else:
+            self._side = _HostStream()
+        self._early_ok = self.sharded and bool(config.get_property("bigdl.comm.earlyUpdate"))
+        # straggler drop state (P5)
+        self._drop_iter = 0
+        self._drop_threshold = None
+        self._drop_times = [0.0] * max(1, getattr(self, "_straggler_window", 1))
+        self._dropped_in_window = 0
+        self._finished = self.world
+        self._skipped = False
         log.info(f"DistriOptimizer: world={W} params={self.flat.numel} buckets={len(self.buckets)} "
                  f"mode={'sharded' if self.sharded else 'replicated'} comm={self.comm_dtype} overlap={self.overlap}")
 
@@ -207,12 +257,11 @@ class DistriOptimizer(BaseOptimizer):
 
     def _early_update(self, b: _Bucket):
         """Shard update + all-gather of bucket ``b`` on the comm-side stream, queued behind its
-        reduce-scatter while backward continues on the compute stream (the reference's lazy
-        per-block ``updateParameter``, ParallelOptimizer.scala:404-470, without the wait)."""
-        side = self._side
-        side.wait_stream(torch.cuda.current_stream())  # the bucket's gradients / wire copy
+        reduce-scatter (issued on the same stream) while backward continues on the compute stream
+        (the reference's lazy per-block ``updateParameter``, ParallelOptimizer.scala:404-470,
+        without the wait)."""
         b.rs_keep = b.rs_work
-        with torch.cuda.stream(side):
+        with _on(self._side):
             self._finish_reduce(b)
             self._update_bucket(b)
             self._launch_gather(b)
@@ -229,32 +278,43 @@ class DistriOptimizer(BaseOptimizer):
 
     # ------------------------------------------------------------------------------ collectives
     def _launch_reduce(self, b: _Bucket):
+        """Issue bucket ``b``'s reduce-scatter (all-reduce in replicated mode) from the comm-side
+        stream.  That stream waits for the compute stream's work so far and for the weight
+        gradients queued so far on the wgrad side stream — events on the GPU, the compute stream
+        itself never waits here."""
         from ..ops import native_ops as NO
-        NO.join_wgrad()  # the bucket's conv weight gradients may still be running on the side stream
-        g = self.flat.grad[b.lo:b.hi]
-        if self.sharded:
-            if self.grad_wire is not None:
-                wire = self.grad_wire[b.lo:b.hi]
-                if self.comm_dtype == "bf16_truncate":
-                    from ..ops import native as N
-                    if not (N.has("trunc_bf16") and N.native_ops.trunc_bf16(g, wire) is not NotImplemented):
-                        wire.copy_(comm.bf16_truncate(g))
+        side = self._side
+        side.wait_stream(_cur_stream(self.flat.grad.device))
+        if isinstance(side, torch.cuda.Stream):
+            NO.join_wgrad(side)
+        with _on(side):
+            g = self.flat.grad[b.lo:b.hi]
+            if self.sharded:
+                if self.grad_wire is not None:
+                    wire = self.grad_wire[b.lo:b.hi]
+                    if self.comm_dtype == "bf16_truncate":
+                        from ..ops import native as N
+                        if not (N.has("trunc_bf16") and N.native_ops.trunc_bf16(g, wire) is not NotImplemented):
+                            wire.copy_(comm.bf16_truncate(g))
+                    else:
+                        wire.copy_(g)
+                    b.rs_work = dist.reduce_scatter_tensor(self.shard_g_wire[b.slo:b.shi], wire, async_op=True)
                 else:
-                    wire.copy_(g)
-                b.rs_work = dist.reduce_scatter_tensor(self.shard_g_wire[b.slo:b.shi], wire, async_op=True)
+                    b.rs_work = dist.reduce_scatter_tensor(self.shard_g[b.slo:b.shi], g, async_op=True)
             else:
-                b.rs_work = dist.reduce_scatter_tensor(self.shard_g[b.slo:b.shi], g, async_op=True)
-        else:
-            b.rs_work = dist.all_reduce(g, async_op=True)
+                b.rs_work = dist.all_reduce(g, async_op=True)
 
-    def _finish_reduce(self, b: _Bucket):
-        if b.rs_work is None:
-            return
-        with self.tracer.phase("aggregate gradient"):
-            b.rs_work.wait()
-        b.rs_work = None
-        if self.sharded and self.grad_wire is not None:
+    def _finish_reduce(self, b: _Bucket, unpack: bool = False):
+        """Make the current stream wait for ``b``'s reduce-scatter.  The bf16 wire shard is read
+        directly by the SGD kernel; ``unpack`` widens it into the fp32 shard (other methods,
+        clipping)."""
+        if b.rs_work is not None:
+            with self.tracer.phase("aggregate gradient"):
+                b.rs_work.wait()
+            b.rs_work = None
+        if unpack and self.sharded and self.grad_wire is not None and not getattr(b, "unpacked", False):
             self.shard_g[b.slo:b.shi].copy_(self.shard_g_wire[b.slo:b.shi])
+            b.unpacked = True
 
     def _bf16_gather(self) -> bool:
         return self.comm_dtype.startswith("bf16") and self.flat.shadow is not None
@@ -284,16 +344,27 @@ class DistriOptimizer(BaseOptimizer):
         b.needs_shadow = False
 
     # ------------------------------------------------------------------------------ iteration
+    def _drop_mode(self) -> bool:
+        return self.drop_percentage > 0
+
     def _before_forward(self):
         for b in self.buckets:
             b.pending = b.expected
             b.early = False
             b.rs_keep = None
-        self._overlap_active = self.overlap and not self._first_iter and self._overlap_ok
-        # early (in-backward) shard updates: sharded, on a GPU, no clipping (which needs the global
-        # gradient norm before any update)
-        self._early = (self._overlap_active and self._side is not None
+            b.unpacked = False
+        # drop mode: a rank's gradient may still be zeroed after its backward, so no bucket is
+        # sent during backward
+        self._overlap_active = (self.overlap and not self._first_iter and self._overlap_ok
+                                and not self._drop_mode())
+        # early (in-backward) shard updates: sharded, no clipping (which needs the global gradient
+        # norm before any update)
+        self._early = (self._overlap_active and self._early_ok
                        and self.constant_clip is None and self.l2_clip is None)
+        if self._drop_mode():
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self._t_compute0 = time.perf_counter()
         if self._early:
             for meth in self.optim_methods.values():
                 meth.begin_iteration(self.shard_w)
@@ -304,7 +375,63 @@ class DistriOptimizer(BaseOptimizer):
         return getattr(self, "_overlap_checked", False)
 
     def _reduce_scalar(self, t):
-        return comm.allreduce_scalar(t, average=True)
+        if not self._drop_mode():
+            return comm.allreduce_scalar(t, average=True)
+        return self._drop_decide(t)
+
+    # ------------------------------------------------------------------------------ straggler drop (P5)
+    def _drop_decide(self, loss_t):
+        """After backward: this rank's compute time vs the threshold → keep or zero its gradient;
+        all-reduce (loss·kept, kept) → loss over the finished ranks and the finished count."""
+        from ..ops import native_ops as NO
+        NO.join_wgrad()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - self._t_compute0
+        window = len(self._drop_times)
+        warm = int(getattr(self, "_straggler_warmup", 0))
+        dropped = (self._drop_threshold is not None and self._drop_iter > warm + window - 1
+                   and dt > self._drop_threshold)
+        if dropped:
+            self.flat.grad.zero_()
+        # a cancelled replica records no time (the reference leaves its slot at 0)
+        self._drop_times[self._drop_iter % window] = 0.0 if dropped else dt
+        kept = 0.0 if dropped else 1.0
+        v = torch.stack([loss_t.reshape(()).float() * kept, torch.ones((), device=loss_t.device) * kept])
+        if comm.is_dist():
+            dist.all_reduce(v)
+        fin = int(round(float(v[1])))
+        self._finished = fin
+        self._dropped_in_window += self.world - fin
+        self._rank_dropped = dropped
+        if dropped:
+            log.info(f"rank {self.rank}: compute {dt * 1e3:.1f} ms > drop threshold "
+                     f"{self._drop_threshold * 1e3:.1f} ms, gradient dropped")
+        return v[0] / max(fin, 1)
+
+    def _drop_after_iteration(self):
+        """Every ``batchsize`` counted iterations after warm-up: new threshold from the
+        all-gathered compute times (``DistriOptimizer.scala:421-449``)."""
+        self._drop_iter += 1
+        window = len(self._drop_times)
+        warm = int(getattr(self, "_straggler_warmup", 0))
+        if not (self._drop_iter > warm and self._drop_iter % window == 0):
+            return
+        from ..utils.tracing import allgather_floats
+        from ..utils.util import kthLargest
+        per_rank = allgather_floats(self._drop_times) if comm.is_dist() else [self._drop_times]
+        times = [int(t * 1e9) for r in per_rank for t in r]
+        k = int(self.drop_percentage * window * self.world)
+        if k > self._dropped_in_window:
+            self._drop_threshold = kthLargest(times, 0, len(times) - 1, k - self._dropped_in_window) / 1e9
+        elif self._drop_threshold is not None:
+            self._drop_threshold *= 1.01
+        if self.rank == 0:
+            log.info(f"straggler drop threshold: {self._drop_threshold}")
+        self._drop_times = [0.0] * window
+        self._dropped_in_window = 0
+
+
 
     def _global_sum(self, t):
         if comm.is_dist():
@@ -321,6 +448,16 @@ class DistriOptimizer(BaseOptimizer):
             self._overlap_checked = ok
             if not ok and self.overlap:
                 log.info("gradient/backward overlap disabled: shared or directly-driven parameter modules")
+        fin = self.world
+        if self._drop_mode():
+            fin = self._finished
+            if fin < self.world * (1.0 - self.max_drop_percentage) or fin == 0:
+                log.warning(f"Warning! Not enough training samples were successfully processed in this iteration "
+                            f"due to some slow tasks. The gradients computed in this iteration will be discarded. "
+                            f"Only {fin}/{self.world} ranks successfully completed training.")
+                self._skipped = True
+                self._first_iter = False
+                return
         # launch any bucket not launched during backward
         for b in reversed(self.buckets):
             if b.rs_work is None and not b.early:
@@ -328,17 +465,22 @@ class DistriOptimizer(BaseOptimizer):
         if not self.sharded:
             for b in self.buckets:
                 self._finish_reduce(b)
-            self.flat.grad.mul_(1.0 / self.world)
+            self.flat.grad.mul_(1.0 / fin)
             for meth in self.optim_methods.values():
                 meth.grad_scale = 1.0
             BaseOptimizer._sync_and_update(self, loss_t, batch_size)
             self._first_iter = False
+            if self._drop_mode():
+                self._drop_after_iteration()
             return
+        for meth in self.optim_methods.values():
+            meth.grad_scale = 1.0 / fin
         # sharded: clipping needs the global gradient norm before any update
-        if self.constant_clip is not None or self.l2_clip is not None:
+        clipping = self.constant_clip is not None or self.l2_clip is not None
+        if clipping:
             for b in self.buckets:
-                self._finish_reduce(b)
-            self.shard_g.mul_(1.0 / self.world)
+                self._finish_reduce(b, unpack=True)
+            self.shard_g.mul_(1.0 / fin)
             for meth in self.optim_methods.values():
                 meth.grad_scale = 1.0
             self._clip(self.shard_g, self.shard_g)
@@ -348,18 +490,30 @@ class DistriOptimizer(BaseOptimizer):
         else:
             # buckets updated during backward: the compute stream must not touch their gradients /
             # weights (next zeroGrad, forward) before the comm-side stream has consumed them
-            torch.cuda.current_stream().wait_stream(self._side)
+            _cur_stream(self.flat.grad.device).wait_stream(self._side)
         for b in self._update_order():
             if b.early:
                 continue
             self._finish_reduce(b)
             self._update_bucket(b)
             self._launch_gather(b)
-        if self.constant_clip is not None or self.l2_clip is not None:
-            for meth in self.optim_methods.values():
-                meth.grad_scale = 1.0 / self.world
+        for meth in self.optim_methods.values():
+            meth.grad_scale = 1.0 / self.world
         self.flat.mark_shadow_fresh()
         self._first_iter = False
+        if self._drop_mode():
+            self._drop_after_iteration()
+
+    def _grad_for(self, meth, b: _Bucket):
+        """The gradient shard ``meth`` reads for bucket ``b``: the bf16 wire shard itself for SGD
+        (its fused kernel widens on load), else the fp32 shard (unpacked once per bucket)."""
+        from ..optim.optim_method import SGD
+        if self.grad_wire is None:
+            return self.shard_g
+        if type(meth) is SGD and not b.unpacked:
+            return self.shard_g_wire
+        self._finish_reduce(b, unpack=True)
+        return self.shard_g
 
     def _update_bucket(self, b: _Bucket):
         with self.tracer.phase("compute weight"):
@@ -368,7 +522,7 @@ class DistriOptimizer(BaseOptimizer):
                     if bb is b:
                         sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
                                                           self.comm_dtype.startswith("bf16")) else None
-                        meth.apply_update(self.shard_w, self.shard_g, lo, hi, shadow=sh)
+                        meth.apply_update(self.shard_w, self._grad_for(meth, b), lo, hi, shadow=sh)
 
     def _update_order(self):
         """Buckets in the order their shard update + all-gather is issued: readiness order (the
@@ -378,7 +532,8 @@ class DistriOptimizer(BaseOptimizer):
     def _wait_all_gathers(self):
         for b in self.buckets:
             if b.ag_work is not None:
-                b.ag_work.wait()
+                with self.tracer.phase("send weights"):
+                    b.ag_work.wait()
                 b.ag_work = None
                 self._after_gather(b)
         self.flat.mark_shadow_fresh()
@@ -414,10 +569,11 @@ class DistriOptimizer(BaseOptimizer):
         self._flush_weights()
         if Engine.rank() == 0:
             save_checkpoint(self.checkpoint_path, self.model, self.optim_methods, self.state, self.is_overwrite,
-                            world_size=self.world, sharded=self.sharded, asynchronous=asynchronous)
+                            world_size=self.world, sharded=self.sharded, asynchronous=asynchronous,
+                            slices=self._method_slices)
         if self.sharded:
             save_shard_state(self.checkpoint_path, self.optim_methods, self.state, self.rank, self.is_overwrite,
-                             asynchronous=asynchronous)
+                             asynchronous=asynchronous, slices=self._method_slices)
         if not asynchronous:
             wait_checkpoints()
         comm.barrier()
@@ -470,15 +626,6 @@ class ParallelOptimizer(DistriOptimizer):
         self._bucket_prio = {}
         for b in self.buckets:
             self._bucket_prio[b.idx] = max((prio.get(m.get_name(), 0) for m in b.modules), default=0)
-
-    def _update_bucket(self, b: _Bucket):
-        with self.tracer.phase("compute weight"):
-            for name, meth in self.optim_methods.items():
-                for (bb, lo, hi) in self._method_shard_ranges[name]:
-                    if bb is b:
-                        sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
-                                                          self.comm_dtype.startswith("bf16")) else None
-                        meth.apply_update(self.shard_w, self.shard_g, lo, hi, shadow=sh)
 
     def _update_order(self):
         return sorted(self.buckets, key=lambda b: (-self._bucket_prio.get(b.idx, 0), -b.idx))

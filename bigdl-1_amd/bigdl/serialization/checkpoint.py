@@ -174,7 +174,10 @@ def _submit(job):
 
 
 def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: bool = False, world_size: int = 1,
-                    sharded: bool = False, asynchronous: bool = False):
+                    sharded: bool = False, asynchronous: bool = False, slices: Optional[Dict] = None):
+    """``slices`` = {method key: (arena offset, length)}: recorded in the state file so a resume
+    matches optimizer methods by the parameters they own (keys built from default module names
+    differ in every process)."""
     os.makedirs(path, exist_ok=True)
     sfx = _suffix(state, overwrite)
     msnap = module_snapshot(model)
@@ -188,8 +191,11 @@ def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: boo
     # holds only rank 0's shard, so a resume must find its own ``.rank<r>`` file at the same world size
     meta["_world_size"] = int(world_size)
     meta["_sharded"] = bool(sharded)
+    if slices:
+        meta["_slices"] = {name: [int(o), int(n)] for name, (o, n) in slices.items()}
 
     def job():
+        # model and optimizer files first, the state file LAST: a state file names a complete set
         _atomic_write(os.path.join(path, "model" + sfx), module_snapshot_bytes(msnap))
         for name, (mp, ctx) in osnaps:
             fill_global_storage(mp, ctx, "global_storage")
@@ -202,19 +208,28 @@ def save_checkpoint(path: str, model, methods: Dict, state: Dict, overwrite: boo
         job()
 
 
+def _shard_key(i: int, name: str, slices: Optional[Dict]) -> str:
+    """File key of a method's per-rank shard: its arena offset when known (stable across processes
+    and restarts), else its position in sorted key order."""
+    if slices and name in slices:
+        return f"@{int(slices[name][0])}"
+    return f"#{i}"
+
+
 def save_shard_state(path: str, methods: Dict, state: Dict, rank: int, overwrite: bool = False,
-                     asynchronous: bool = False):
-    """Each rank's shard of the optimizer state.  Files are keyed by the method's POSITION in sorted
-    key order, not by its key: a key derived from a default module name is random per process (the
+                     asynchronous: bool = False, slices: Optional[Dict] = None):
+    """Each rank's shard of the optimizer state, keyed by the method's arena offset (see
+    :func:`_shard_key`) — a key derived from a default module name is random per process (the
     reference's ``getName`` postfix), so rank 1 — and a restarted process — could never find a file
     named after rank 0's key."""
     sfx = _suffix(state, overwrite)
-    snaps = [(i, optim_to_pb(methods[name], defer=True)) for i, name in enumerate(sorted(methods))]
+    snaps = [(_shard_key(i, name, slices), optim_to_pb(methods[name], defer=True))
+             for i, name in enumerate(sorted(methods))]
 
     def job():
-        for i, (mp, ctx) in snaps:
+        for key, (mp, ctx) in snaps:
             fill_global_storage(mp, ctx, "global_storage")
-            _atomic_write(os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}"), mp.SerializeToString())
+            _atomic_write(os.path.join(path, f"optimMethod-{key}{sfx}.rank{rank}"), mp.SerializeToString())
     if asynchronous:
         _submit(job)
     else:
@@ -235,41 +250,61 @@ def has_checkpoint(path: str) -> bool:
 
 def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
                            sharded: Optional[bool] = None) -> Tuple[Optional[object], Dict, Dict]:
-    """Latest model / optimMethods / driver state under ``path``.  With ``world_size`` given, a
-    checkpoint whose optimizer state was sharded is only accepted by a sharded run of the SAME world
-    size that finds its own ``.rank<r>`` state file (no silent fallback to rank 0's shard)."""
+    """Latest COMPLETE checkpoint under ``path``: the newest ``state<sfx>`` file (written last by
+    :func:`save_checkpoint`) fixes the suffix, and the model / optimMethod files of that same suffix
+    are loaded — never a newer model with older optimizer state from an interrupted write.  With
+    ``world_size`` given, a checkpoint whose optimizer state was sharded is only accepted by a
+    sharded run of the SAME world size that finds its own ``.rank<r>`` state file.  Loaded methods
+    carry ``_arena_slice`` (offset, length) when the checkpoint recorded it."""
     wait_checkpoints()
     sfile = _latest(os.path.join(path, "state*"))
     meta = {}
+    sfx = None
     if sfile:
         with open(sfile) as fh:
             meta = json.load(fh)
+        sfx = os.path.basename(sfile)[len("state"):]
     ck_sharded = bool(meta.get("_sharded", False))
     ck_world = int(meta.get("_world_size", 1))
     if world_size is not None and ck_sharded and (not sharded or ck_world != world_size):
         raise ValueError(f"checkpoint under {path} holds sharded optimizer state for world size {ck_world}; "
                          f"this run is world size {world_size} ({'sharded' if sharded else 'replicated'}) — "
                          "resume with the same world size and bigdl.comm.sharded")
-    mfile = _latest(os.path.join(path, "model*"))
+    mfile = os.path.join(path, "model" + sfx) if sfx is not None else None
+    if mfile is None or not os.path.exists(mfile):
+        mfile = _latest(os.path.join(path, "model*"))
     model = load_module(mfile) if mfile else None
     methods = {}
     for f in glob.glob(os.path.join(path, "optimMethod-*")):
-        if ".rank" in f or ".tmp" in f or os.path.basename(f).startswith("optimMethod-#"):
+        b = os.path.basename(f)
+        if ".rank" in f or ".tmp" in f or b.startswith("optimMethod-#") or b.startswith("optimMethod-@"):
             continue
-        base = os.path.basename(f)[len("optimMethod-"):]
+        base = b[len("optimMethod-"):]
+        if sfx is not None:
+            if sfx and not base.endswith(sfx):
+                continue
+            name = base[:len(base) - len(sfx)] if sfx else base
+            if not sfx and base.rsplit(".", 1)[-1].isdigit():
+                continue
+            methods[name] = (os.path.getmtime(f), f)
+            continue
         name = base.rsplit(".", 1)[0] if base.rsplit(".", 1)[-1].isdigit() else base
         cur = methods.get(name)
         if cur is None or os.path.getmtime(f) > cur[0]:
             methods[name] = (os.path.getmtime(f), f)
+    slices = meta.get("_slices") or {}
     loaded = {}
     rank = int(os.environ.get("RANK", "0"))
-    for i, name in enumerate(sorted(methods)):  # sorted: the position key of save_shard_state
+    for i, name in enumerate(sorted(methods)):
         f = methods[name][1]
-        sfx = f[len(os.path.join(path, "optimMethod-" + name)):]
-        shard = os.path.join(path, f"optimMethod-#{i}{sfx}.rank{rank}")
+        fsfx = f[len(os.path.join(path, "optimMethod-" + name)):]
+        shard = os.path.join(path, f"optimMethod-{_shard_key(i, name, slices)}{fsfx}.rank{rank}")
         if ck_sharded and not os.path.exists(shard):
             raise FileNotFoundError(f"sharded checkpoint: missing this rank's optimizer state {shard}")
-        loaded[name] = load_optim_method(shard if ck_sharded else f)
+        m = load_optim_method(shard if ck_sharded else f)
+        if name in slices:
+            m._arena_slice = tuple(slices[name])
+        loaded[name] = m
     state = {k: v for k, v in meta.items() if not k.startswith("_")}
     for k in ("epoch", "neval", "recordsProcessedThisEpoch"):
         if k in state:

@@ -29,6 +29,7 @@ _REGISTRY = {
     "bigdl.failure.retryTimeInterval": (int, 120, "retry window seconds"),
     "bigdl.failure.resume": (bool, False, "resume from the latest checkpoint at optimize() start (automatic after a launcher restart)"),
     # straggler monitor (P5, DistriOptimizer.scala:246-278,421-449)
+    "bigdl.embedding.syncCheck": (bool, False, "check LookupTable ids synchronously after every GPU lookup (debug; default: the out-of-range flag is read back asynchronously and raised at the next lookup)"),
     "bigdl.straggler.window": (int, 20, "iterations between straggler checks (all-gather of per-rank step times)"),
     "bigdl.straggler.factor": (float, 1.5, "a rank is slow when its step time exceeds factor x the kthLargest threshold"),
     # parameter sync

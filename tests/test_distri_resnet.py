@@ -55,7 +55,7 @@ def _sgd():
     return SGD(learningrate=0.05, momentum=0.9, dampening=0.0, weightdecay=1e-4)
 
 
-def _worker(rank, world, port, mode, comm_dtype, out_q):
+def _worker(rank, world, port, mode, comm_dtype, out_q, early=True):
     sys.path.insert(0, _ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
@@ -64,6 +64,7 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     config.set_property("bigdl.comm.sharded", mode in ("sharded", "parallel"))
     config.set_property("bigdl.comm.dtype", comm_dtype)
     config.set_property("bigdl.comm.bucketMB", 0.05)  # several buckets even for ResNet-20
+    config.set_property("bigdl.comm.earlyUpdate", early)
     from bigdl.utils.engine import Engine
     Engine.init(device="cpu", dist=True, backend="gloo")
     from bigdl.nn import CrossEntropyCriterion
@@ -80,11 +81,13 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
         from bigdl.parallel import DistriOptimizer
         opt = DistriOptimizer(model, [MiniBatch(xs, ys)], CrossEntropyCriterion(), _sgd())
     opt.prepare()
+    n_early = 0
     for _ in range(STEPS):
         opt.train_step(MiniBatch(xs, ys))
+        n_early += sum(1 for b in opt.buckets if b.early)
     opt._finish()
     if rank == 0:
-        out_q.put(torch.cat([p.reshape(-1) for p in model.parameters()[0]]).numpy())
+        out_q.put((torch.cat([p.reshape(-1) for p in model.parameters()[0]]).numpy(), n_early, len(opt.buckets)))
     Engine.shutdown()
 
 
@@ -107,9 +110,14 @@ _REF = {}
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("mode,comm_dtype", [("sharded", "fp32"), ("replicated", "fp32"), ("sharded", "bf16"),
-                                             ("sharded", "bf16_truncate"), ("parallel", "fp32")])
-def test_resnet20_syncbn_distri_matches_serial(world, mode, comm_dtype):
+@pytest.mark.parametrize("mode,comm_dtype,early", [
+    ("sharded", "fp32", True), ("sharded", "fp32", False), ("replicated", "fp32", False),
+    ("sharded", "bf16", True), ("sharded", "bf16", False), ("sharded", "bf16_truncate", True),
+    ("sharded", "bf16_truncate", False), ("parallel", "fp32", True)])
+def test_resnet20_syncbn_distri_matches_serial(world, mode, comm_dtype, early):
+    """``early`` = the in-backward shard update + all-gather path (``bigdl.comm.earlyUpdate``; on the
+    CPU its comm-side stream is the host stand-in): from the second iteration on every bucket of a
+    sharded run must be updated during backward."""
     if "ref" not in _REF:
         _REF["ref"] = _serial_weights()
         _REF["w0"] = torch.cat([p.reshape(-1) for p in _model(1).parameters()[0]])
@@ -117,10 +125,15 @@ def test_resnet20_syncbn_distri_matches_serial(world, mode, comm_dtype):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, comm_dtype, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, comm_dtype, q, early)) for r in range(world)]
     for p in procs:
         p.start()
-    got = torch.from_numpy(q.get(timeout=300))
+    got, n_early, n_buckets = q.get(timeout=300)
+    got = torch.from_numpy(got)
+    if early and mode != "replicated":
+        assert n_buckets > 1 and n_early == (STEPS - 1) * n_buckets, (n_early, n_buckets)
+    else:
+        assert n_early == 0
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

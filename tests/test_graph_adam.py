@@ -45,11 +45,80 @@ def test_hip_graph_train_step_adam_matches_eager():
     eager, graphed = mk(m), mk(m2)
     eager.prepare()
     graphed.prepare()
-    g = GraphedTrainStep(graphed, bs[0], warmup=3)
-    for _ in range(3):
-        eager.train_step(bs[0])
+    g = GraphedTrainStep(graphed, bs[0], warmup=3)  # the warmup updates are undone after capture
     le = [float(eager.train_step(bs[i % 3])) for i in range(8)]
     lg = [float(g.step(bs[i % 3])) for i in range(8)]
     torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-3, atol=1e-3)
     meth = list(graphed.optim_methods.values())[0]
-    assert float(meth.state["_dev_n"]) == 3 + 8
+    assert float(meth.state["_dev_n"]) == 8
+    assert meth.state["evalCounter"] == 8  # host and device counters agree (no capture-pass drift)
+    for a, b in zip(m.parameters()[0], m2.parameters()[0]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def _mlp_opt(meth, bs):
+    from bigdl.nn import Sequential, Linear, ReLU, LogSoftMax, ClassNLLCriterion
+    from bigdl.optim.optimizer import LocalOptimizer
+    torch.manual_seed(0)
+    m = Sequential().add(Linear(32, 64)).add(ReLU()).add(Linear(64, 10)).add(LogSoftMax()).cuda()
+    opt = LocalOptimizer(m, [bs[0]], ClassNLLCriterion(), meth, batch_size=16)
+    opt.prepare()
+    return m, opt
+
+
+def _batches(n=3):
+    from bigdl.dataset import MiniBatch
+    g = torch.Generator().manual_seed(1)
+    return [MiniBatch(torch.randn(16, 32, generator=g).to(dev),
+                      (torch.randint(0, 10, (16,), generator=g) + 1).float().to(dev)) for _ in range(n)]
+
+
+def test_hip_graph_sgd_momentum_dampening_first_step_matches_eager():
+    """SGD with momentum and the default dampening (= momentum): the first update is v = g, later
+    ones v = μv + (1-d)g.  The capture warmup created the momentum buffer, so the first step after
+    capture runs eagerly with first-iteration semantics, then replays take over."""
+    from bigdl.optim import SGD
+    from bigdl.optim.graph_step import GraphedTrainStep
+    bs = _batches()
+    m1, eager = _mlp_opt(SGD(learningrate=0.1, momentum=0.9), bs)
+    m2, graphed = _mlp_opt(SGD(learningrate=0.1, momentum=0.9), bs)
+    g = GraphedTrainStep(graphed, bs[0])
+    le = [float(eager.train_step(bs[i % 3])) for i in range(6)]
+    lg = [float(g.step(bs[i % 3])) for i in range(6)]
+    torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-4, atol=1e-4)
+    for a, b in zip(m1.parameters()[0], m2.parameters()[0]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_hip_graph_restore_checkpoint_follows_eager(tmp_path):
+    """Capture a graphed Adam step, train, checkpoint, train on, then restore the checkpoint: the
+    restored moments / counter are copied into the captured state tensors in place, so the graphed
+    run continues exactly like an eager run restored from the same checkpoint."""
+    from bigdl.optim import Adam
+    from bigdl.optim.graph_step import graphed_train_step
+    from bigdl.utils import config
+    bs = _batches()
+    config.set_property("bigdl.graph.capture", True)
+    try:
+        m1, eager = _mlp_opt(Adam(learningrate=0.01, learningrate_decay=0.05), bs)
+        m2, graphed = _mlp_opt(Adam(learningrate=0.01, learningrate_decay=0.05), bs)
+        for o in (eager, graphed):
+            o.setCheckpoint(str(tmp_path / ("g" if o is graphed else "e")), None, is_overwrite=True)
+        for i in range(4):
+            eager.train_step(bs[i % 3])
+            graphed_train_step(graphed, bs[i % 3])
+        assert getattr(graphed, "_graphed", None) is not None
+        eager.checkpoint()
+        graphed.checkpoint()
+        for i in range(3):  # diverge from the checkpoint, then come back
+            eager.train_step(bs[i % 3])
+            graphed_train_step(graphed, bs[i % 3])
+        eager._restore_latest()
+        graphed._restore_latest()
+        le = [float(eager.train_step(bs[i % 3])) for i in range(5)]
+        lg = [float(graphed_train_step(graphed, bs[i % 3])) for i in range(5)]
+    finally:
+        config.set_property("bigdl.graph.capture", False)
+    torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-3, atol=1e-3)
+    mg = list(graphed.optim_methods.values())[0]
+    assert float(mg.state["_dev_n"]) == mg.state["evalCounter"] == 9

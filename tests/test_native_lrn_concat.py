@@ -256,9 +256,7 @@ def test_hip_graph_step_fresh_batches_matches_eager():
     eager, graphed = mk(m), mk(m2)
     eager.prepare()
     graphed.prepare()
-    g = GraphedTrainStep(graphed, bs[0], warmup=3)  # 3 eager warmup updates on bs[0]; capture runs nothing
-    for _ in range(3):
-        eager.train_step(bs[0])
+    g = GraphedTrainStep(graphed, bs[0], warmup=3)  # warmup updates are undone after capture
     le = [float(eager.train_step(bs[i % 4])) for i in range(8)]
     lg = [float(g.step(bs[i % 4])) for i in range(8)]
     torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=2e-2, atol=2e-2)

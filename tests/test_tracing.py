@@ -110,7 +110,7 @@ def _straggler_worker(rank, world, port, out_q):
     bs = _batches()
     opt = DistriOptimizer(_mlp(), bs, ClassNLLCriterion(), SGD(learningrate=0.1), batch_size=16)
     opt.setEndWhen(MaxIteration(7))
-    opt.setDropModuleProperty(0.2, 0.3, batchsize=3, warmup_iteration=0)
+    opt.setDropModuleProperty(0.2, 0.5, batchsize=3, warmup_iteration=0)
     if rank == 1:  # this rank computes slowly in every iteration
         model = opt.model
         orig = model.forward
