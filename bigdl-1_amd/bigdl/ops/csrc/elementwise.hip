@@ -113,8 +113,12 @@ __device__ __forceinline__ void g_load4(const bf16_t* g, long long i, float* o) 
 template <typename GT, bool MOM, bool NEST, bool FIRST, bool SHADOW, bool PERELEM>
 __global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __restrict__ buf,
                       bf16_t* __restrict__ shadow, const float* __restrict__ lrs, const float* __restrict__ wds,
-                      long long n4, float lr, float mom, float damp, float wd, float scale, int tail) {
+                      long long n4, float lr, float mom, float damp, float wd, float scale, int tail,
+                      const float* __restrict__ first_dev) {
   long long stride = (long long)gridDim.x * blockDim.x;
+  // first-iteration rule (v = g) from the template or, in HIP-graph mode, from a device flag the
+  // captured step clears after the update (so a replayed graph can start a fresh trajectory)
+  const bool first = FIRST || (first_dev != nullptr && *first_dev != 0.f);
   if (blockIdx.x == 0 && threadIdx.x < tail) {
     // the n % 4 trailing elements (scalar; the arena slice need not be a multiple of 4)
     const long long e = n4 * 4 + threadIdx.x;
@@ -122,7 +126,7 @@ __global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __
     const float gg = g_at(g, e) * scale + wd * (PERELEM && wds ? wds[e] : 1.f) * wv;
     float d = gg;
     if (MOM) {
-      const float b = FIRST ? gg : mom * buf[e] + (1.f - damp) * gg;
+      const float b = first ? gg : mom * buf[e] + (1.f - damp) * gg;
       buf[e] = b;
       d = NEST ? gg + mom * b : b;
     }
@@ -148,7 +152,7 @@ __global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __
       }
     }
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (MOM && !FIRST) {
+    if (MOM && !first) {
       float4 B = reinterpret_cast<float4*>(buf)[i];
       bv[0] = B.x; bv[1] = B.y; bv[2] = B.z; bv[3] = B.w;
     }
@@ -157,7 +161,7 @@ __global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __
       float gg = gv[k] * scale + wd * wdv[k] * wv[k];
       float d = gg;
       if (MOM) {
-        bv[k] = FIRST ? gg : mom * bv[k] + (1.f - damp) * gg;
+        bv[k] = first ? gg : mom * bv[k] + (1.f - damp) * gg;
         d = NEST ? gg + mom * bv[k] : bv[k];
       }
       wv[k] -= lr * lrv[k] * d;
@@ -174,12 +178,12 @@ __global__ void k_sgd(float* __restrict__ w, const GT* __restrict__ g, float* __
 
 #define SGD_LAUNCH(M, NS, F, SH, PE)                                                                    \
   hipLaunchKernelGGL((k_sgd<GT, M, NS, F, SH, PE>), dim3(grid), dim3(256), 0, s, w, g, buf, shadow, lrs, wds, n4, \
-                     lr, mom, damp, wd, scale, tail)
+                     lr, mom, damp, wd, scale, tail, first_dev)
 
 template <typename GT>
 static int sgd_impl(float* w, const GT* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
                     long long n, float lr, float mom, float damp, float wd, int nesterov, int first, float scale,
-                    hipStream_t s) {
+                    const float* first_dev, hipStream_t s) {
   if (n <= 0) return 0;
   const long long n4 = n / 4;
   const int tail = (int)(n & 3);
@@ -218,17 +222,18 @@ static int sgd_impl(float* w, const GT* g, float* buf, bf16_t* shadow, const flo
 
 
 // all pointers 16-B aligned (host-checked); the n % 4 tail is handled by block 0.
+// first_dev: optional device flag (graph mode), non-zero = apply the first-iteration rule
 BIGDL_EXPORT int bigdl_sgd(float* w, const float* g, float* buf, bf16_t* shadow, const float* lrs, const float* wds,
                            long long n, float lr, float mom, float damp, float wd, int nesterov, int first,
-                           float scale, hipStream_t s) {
-  return sgd_impl<float>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, s);
+                           float scale, const float* first_dev, hipStream_t s) {
+  return sgd_impl<float>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, first_dev, s);
 }
 
 // same update with a bf16 gradient (the bf16-wire reduce-scatter output); g 8-B aligned
 BIGDL_EXPORT int bigdl_sgd_g16(float* w, const bf16_t* g, float* buf, bf16_t* shadow, const float* lrs,
                                const float* wds, long long n, float lr, float mom, float damp, float wd, int nesterov,
-                               int first, float scale, hipStream_t s) {
-  return sgd_impl<bf16_t>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, s);
+                               int first, float scale, const float* first_dev, hipStream_t s) {
+  return sgd_impl<bf16_t>(w, g, buf, shadow, lrs, wds, n, lr, mom, damp, wd, nesterov, first, scale, first_dev, s);
 }
 
 // ------------------------------------------------------------------------------------------------

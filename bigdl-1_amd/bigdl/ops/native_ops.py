@@ -883,7 +883,7 @@ def _vec_ok(*ts, n):
 
 @register("sgd_step")
 def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale=1.0, shadow=None,
-             lrs=None, wds=None):
+             lrs=None, wds=None, first_dev=None):
     """Fused SGD over a flat fp32 slice; ``g`` is fp32 or bf16 (the bf16-wire reduce-scatter output,
     read directly by the kernel instead of being unpacked into an fp32 shard first)."""
     n = w.numel()
@@ -897,10 +897,12 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
         return NotImplemented
     if momentum != 0 and buf is None:
         return NotImplemented
+    if first_dev is not None and not (first_dev.is_cuda and first_dev.dtype == _f32):
+        return NotImplemented
     fn = _lib().bigdl_sgd_g16 if g16 else _lib().bigdl_sgd
     check(fn(ptr(w), ptr(g), ptr(buf if momentum != 0 else None), ptr(shadow), ptr(lrs), ptr(wds),
              _ll(n), _f(lr), _f(momentum), _f(dampening), _f(weight_decay), C.c_int(int(bool(nesterov))),
-             C.c_int(int(bool(first_step))), _f(grad_scale), _s()), "sgd")
+             C.c_int(int(bool(first_step))), _f(grad_scale), ptr(first_dev), _s()), "sgd")
     return w
 
 

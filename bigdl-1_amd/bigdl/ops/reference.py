@@ -276,12 +276,14 @@ def cross_entropy_fused(x, target_1b, weights=None, size_average=True, padding_v
 
 # ------------------------------------------------------------------------- optimizer
 def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale=1.0,
-             shadow=None, lrs=None, wds=None):
+             shadow=None, lrs=None, wds=None, first_dev=None):
     """Fused SGD (``DL/optim/SGD.scala:61-124``): g += wd·x; v = μv + (1-d)g; nesterov; x -= lr·v.
 
     ``grad_scale`` folds the 1/N gradient averaging in; ``lrs``/``wds`` are per-element
     learning-rate / weight-decay multipliers (``learningRates``/``weightDecays``)."""
     g = g.float()  # a bf16-wire gradient shard is consumed directly
+    if first_dev is not None and float(first_dev.reshape(-1)[0]) != 0:
+        first_step = True
     gg = g * grad_scale if grad_scale != 1.0 else g.clone()
     if weight_decay != 0:
         gg.add_(w * (wds if wds is not None else 1.0), alpha=weight_decay)

@@ -33,8 +33,9 @@ class GraphedTrainStep:
     running statistics, optimizer state — is snapshotted before and restored IN PLACE after the
     capture (the graph keeps pointing at the same storage), host counters (``evalCounter``) are
     restored and device counters (``_dev_n``) re-synchronised, so the first :meth:`step` is the
-    trajectory's first iteration.  Optimizer state that the warmup created (SGD's momentum buffer)
-    is zeroed and the next step runs eagerly once with first-iteration semantics."""
+    trajectory's first iteration.  Optimizer state that the warmup created is zeroed; SGD's
+    first-iteration momentum rule (v = g) is raised through a device flag its captured kernel reads
+    and clears (``_dev_first``)."""
 
     def __init__(self, optimizer, batch: MiniBatch, warmup: int = 3):
         if not torch.cuda.is_available():
@@ -61,7 +62,7 @@ class GraphedTrainStep:
         with torch.cuda.graph(self.graph):
             self.loss = optimizer.train_step(b)
         torch.cuda.synchronize()
-        self.eager_next = self._restore(snap)
+        self._restore(snap)
         torch.cuda.synchronize()
 
     # -------------------------------------------------------------------------- warmup undo
@@ -82,13 +83,13 @@ class GraphedTrainStep:
                             for k, v in meth.state.items()}
         return ts, states
 
-    def _restore(self, snap) -> bool:
+    def _restore(self, snap):
         ts, states = snap
         for t, c in ts:
             t.copy_(c)
-        eager_next = False
         for name, meth in self.opt.optim_methods.items():
             pre = states[name]
+            fresh = []
             for k in list(meth.state.keys()):
                 v = meth.state[k]
                 if k in pre:
@@ -98,12 +99,11 @@ class GraphedTrainStep:
                         meth.state[k] = pre[k]
                 elif isinstance(v, torch.Tensor):
                     v.zero_()  # created by the warmup: back to its initial (zero) value
-                    if meth.graph_state_created(k):
-                        eager_next = True
+                    fresh.append(k)
                 else:
                     del meth.state[k]
             meth.sync_device_counter()
-        return eager_next
+            meth.graph_state_restored(fresh)
 
     def step(self, batch: MiniBatch = None) -> torch.Tensor:
         if batch is not None:
@@ -113,10 +113,6 @@ class GraphedTrainStep:
             if isinstance(y, torch.Tensor) and y is not self.sy:
                 self.sy.copy_(y, non_blocking=True)
         self.opt.state["neval"] = self.opt.state.get("neval", 0) + 1
-        if self.eager_next:
-            # first iteration after capture with freshly created state (SGD momentum: v = g)
-            self.eager_next = False
-            return self.opt.train_step(MiniBatch(self.sx, self.sy))
         self.graph.replay()
         for meth in self.opt.optim_methods.values():
             meth.after_graph_replay()

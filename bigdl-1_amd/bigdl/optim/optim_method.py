@@ -51,10 +51,9 @@ class OptimMethod:
         if isinstance(nt, torch.Tensor):
             nt.fill_(float(self.state.get("evalCounter", 0)))
 
-    def graph_state_created(self, key: str) -> bool:
-        """True when state ``key``, newly created by capture warmup, needs an eager
-        first-iteration update (it cannot be emulated by a zero tensor)."""
-        return False
+    def graph_state_restored(self, fresh):
+        """Called after a graph capture's warmup was undone; ``fresh`` = state keys the warmup
+        created (now zeroed)."""
 
     def clearHistory(self):
         keep = {k: self.state[k] for k in ("epoch", "neval", "evalCounter", "recordsProcessedThisEpoch", "Loss",
@@ -327,14 +326,16 @@ class EpochDecayWithWarmUp(LearningRateSchedule):
 class SGD(OptimMethod):
     def prepare_graph(self) -> bool:
         # the fused kernel takes lr by value: replayable only while the schedule is constant
-        return type(self.learningRateSchedule) is Default and self.learningRateDecay == 0
-
-    def graph_state_created(self, key):
-        # a zero momentum buffer equals the first-iteration rule (v = g) only without dampening
-        if key == "dfdx" and self.momentum != 0:
-            self._first_pending = True
+        if type(self.learningRateSchedule) is Default and self.learningRateDecay == 0:
+            self._graph_mode = True
             return True
         return False
+
+    def graph_state_restored(self, fresh):
+        # the warmup created the momentum buffer: the next (replayed) update must apply the
+        # first-iteration rule v = g — raised through the device flag the kernel reads
+        if "dfdx" in fresh and isinstance(self.state.get("_dev_first"), torch.Tensor):
+            self.state["_dev_first"].fill_(1.0)
 
     def __init__(self, learningrate=1e-3, learningrate_decay=0.0, weightdecay=0.0, momentum=0.0,
                  dampening=float("inf"), nesterov=False, leaningrate_schedule=None, learningrates=None,
@@ -418,11 +419,19 @@ class SGD(OptimMethod):
         fx, dfdx = feval(x)
         clr = self.learningRateSchedule.currentRate  # negative
         first = "dfdx" not in self.state or not isinstance(self.state.get("dfdx"), torch.Tensor) or \
-            self.state["dfdx"].shape != x.shape or self.__dict__.pop("_first_pending", False)
+            self.state["dfdx"].shape != x.shape
         buf = self._state_tensor("dfdx", x) if self.momentum != 0 else None
         lrs, wd, wds = self._decays(x.device)
+        fdev = None
+        if getattr(self, "_graph_mode", False) and x.is_cuda and self.momentum != 0:
+            # replay-safe first-iteration rule: a device flag read by the kernel, cleared after it
+            fdev = self.state.get("_dev_first")
+            if not isinstance(fdev, torch.Tensor) or fdev.device != x.device:
+                fdev = self.state["_dev_first"] = torch.zeros(1, device=x.device)
         ops.sgd_step(x, dfdx, buf, -clr, self.momentum, self.dampening, wd, self.nesterov, first,
-                     self.grad_scale, self.shadow, lrs, wds)
+                     self.grad_scale, self.shadow, lrs, wds, first_dev=fdev)
+        if fdev is not None:
+            fdev.zero_()
         return x, [fx]
 
     def __getstate__(self):
