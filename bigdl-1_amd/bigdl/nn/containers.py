@@ -301,8 +301,12 @@ class ConcatTable(Container):
         # shortcut first, so the branch's first conv can sum its gradient in the dgrad epilogue
         gs = shortcut.backward(input, gres)
         from .layers.conv import SpatialConvolution
+        from ..ops.reference import StridedGrad
         first = br.modules[0]
-        fold = isinstance(first, SpatialConvolution) and isinstance(gs, torch.Tensor) and len(br.modules) > 1
+        fold = (isinstance(first, SpatialConvolution) and isinstance(gs, (torch.Tensor, StridedGrad))
+                and len(br.modules) > 1)
+        if isinstance(gs, StridedGrad) and not fold:
+            gs = gs.dense()
         if fold:
             first._grad_residual = gs
         for i in range(len(br.modules) - 2, -1, -1):

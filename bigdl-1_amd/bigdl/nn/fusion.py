@@ -121,6 +121,14 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=Non
             first = br.modules[0]
             if isinstance(first, SpatialConvolution) and len(br.modules) > 1:
                 heads.append(first)
+                # 1×1 strided shortcut conv: its input gradient (nonzero only on the stride grid)
+                # reaches `first`'s dgrad epilogue as a strided residual, never zero-filled
+                sc = ct.modules[1]
+                sc0 = sc.modules[0] if isinstance(sc, Sequential) and sc.modules else None
+                if (isinstance(sc0, SpatialConvolution) and type(sc0) in _PLAIN_CONVS and sc0.format == "NCHW"
+                        and sc0.kernelW == 1 and sc0.kernelH == 1 and sc0.padW == 0 and sc0.padH == 0
+                        and sc0.nGroup == 1 and (sc0.strideW > 1 or sc0.strideH > 1)):
+                    sc0._lazy_strided_ok = True
     # block tail → next block: the first conv of a fused block (whose dgrad epilogue already sums
     # the shortcut gradient) also applies the previous tail's ReLU mask and produces that BN's
     # backward reductions; the match is made at backward time by tensor identity
@@ -168,6 +176,7 @@ def unfuse(model):
             m._bn_bwd_target = None
             m._tail_candidates = None
             m._input_grad_needed = True
+            m._lazy_strided_ok = False
         if isinstance(m, BatchNormalization):
             m._bias_producer = None
             m._fused_relu = False

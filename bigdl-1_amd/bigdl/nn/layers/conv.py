@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import ops
+from ...ops.reference import StridedGrad, as_dense
 from ...utils.engine import Engine
 from ...utils import config
 from ..abstractnn import AbstractModule, TensorModule, AutogradModule
@@ -154,6 +155,9 @@ class SpatialConvolution(TensorModule):
     #: fused block-tail BNs (ReLU(BN(x) + shortcut)) whose output may be this conv's input: the
     #: dgrad epilogue then also applies that ReLU mask and produces the tail BN's reductions
     _tail_candidates = None
+    #: this conv is a fused block's 1×1 strided shortcut: its input gradient may be returned as a
+    #: StridedGrad (set by bigdl.nn.fusion; the block's first conv consumes it)
+    _lazy_strided_ok = False
 
     def _pad_slot_(self):
         """One-entry holder for the channel-padded copy of a C % 8 input (RGB stem): made by the
@@ -222,6 +226,8 @@ class SpatialConvolution(TensorModule):
         self._grad_residual = None
         pt, pb, pl, pr = pads
         fuse_res = res is not None and pt == pb and pl == pr and self.format == "NCHW" and batched
+        if isinstance(res, StridedGrad) and not (fuse_res and gy.is_cuda):
+            res = res.dense()
         bn = self._bn_bwd_target
         bn_fuse = None
         if (bn is not None and need_input and res is None and pt == pb and pl == pr and self.format == "NCHW"
@@ -234,10 +240,18 @@ class SpatialConvolution(TensorModule):
             bn = self._tail_target(x)
             if bn is not None:
                 bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output}
+        # the shortcut conv of a fused ResNet block (1×1 stride 2) may hand its input gradient back
+        # as a StridedGrad: the block's first conv sums it in its dgrad epilogue
+        lazy = (need_input and self._lazy_strided_ok and res is None and bn_fuse is None and batched
+                and self.format == "NCHW" and pt == pb and pl == pr and gy.is_cuda)
+        if fuse_res and not isinstance(res, StridedGrad):
+            res = to_device_layout(res)
         gi = ops.conv2d_backward(gy, x, w4, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                  self.nGroup, need_input, gw, gb, self.scale_w if acc else 0.0,
-                                 residual=to_device_layout(res) if fuse_res else None, bn_fuse=bn_fuse,
-                                 pad_slot=self._pad_slot_())
+                                 residual=res if fuse_res else None, bn_fuse=bn_fuse,
+                                 pad_slot=self._pad_slot_(), lazy_strided=lazy)
+        if isinstance(gi, StridedGrad):
+            return gi
         if bn_fuse is not None and "partial" in bn_fuse and gi is not None:
             bn._pending_grad = (gi.data_ptr(), bn_fuse["partial"], bn_fuse["G"])
         if acc and own_bias and not same_scale and self.scale_b != 0:
@@ -251,7 +265,7 @@ class SpatialConvolution(TensorModule):
             if not batched:
                 gi = gi.squeeze(0)
             if res is not None and not fuse_res:
-                gi = gi + res
+                gi = gi + as_dense(res)
         return gi
 
     #: False when this conv consumes the model input of a training run (set by
@@ -267,7 +281,7 @@ class SpatialConvolution(TensorModule):
             self._gi_done = False
             res, self._grad_residual = self._grad_residual, None
             if res is not None:
-                return res.clone()
+                return as_dense(res).clone()
             return torch.zeros_like(input) if isinstance(input, torch.Tensor) else None
         # compute gradInput and (fused) parameter gradients in one pass; accGradParameters then
         # only applies regularisers

@@ -64,7 +64,27 @@ struct ConvParams {
   // raw sums, so E[y²] − E[y]² never cancels catastrophically (the BN passes its running mean —
   // any value is exact, one near the batch mean keeps the variance well conditioned)
   const float* stat_shift;
+  // optional strided residual (res_sh > 0): `res` is a [Nb][res_H][res_W][K] tensor holding only
+  // the output pixels (h, w) with h % res_sh == 0 and w % res_sw == 0 (the input gradient of a 1×1
+  // stride-s shortcut conv); every other pixel's residual is zero — the dense zero-filled copy is
+  // never materialised
+  int res_sh, res_sw, res_H, res_W;
 };
+
+// Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
+// residual is zero at this pixel (strided residual, off-grid pixel).
+__device__ __forceinline__ bool res_at(const ConvParams& p, int m, int n, size_t dense_off, size_t& roff) {
+  if (p.res_sh == 0) {
+    roff = dense_off;
+    return true;
+  }
+  const int img = m / (p.P * p.Q);
+  const int pq = m - img * p.P * p.Q;
+  const int h = pq / p.Q, w = pq - h * p.Q;
+  if (h % p.res_sh || w % p.res_sw) return false;
+  roff = ((size_t)(img * p.res_H + h / p.res_sh) * p.res_W + w / p.res_sw) * p.K + n;
+  return true;
+}
 
 constexpr int SBM = 128;  // row granularity of the BN-statistics partials (any BM writes BM / SBM rows)
 // k-tile depth is a kernel parameter (64 or 32).  A fragment read (ds_read_b128) is serviced in four
@@ -488,8 +508,9 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       if (p.bn_mask) {
         float rv[8], mv[8];
         load8(p.bn_mask + off, mv);
-        if (p.res) {
-          load8(p.res + off, rv);
+        size_t ro;
+        if (p.res && res_at(p, m, n, off, ro)) {
+          load8(p.res + ro, rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) g[e] += rv[e];
         }
@@ -518,9 +539,10 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       if (p.res || p.relu) {
         float v[8];
         unpack8(u, v);
-        if (p.res) {
+        size_t ro;
+        if (p.res && res_at(p, m, n, off, ro)) {
           float rv[8];
-          load8(p.res + off, rv);
+          load8(p.res + ro, rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rv[e];
         }
@@ -550,8 +572,10 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
     } else {
       float v[8];
       unpack8(rd_chunk(r, cc), v);
+      size_t ro = 0;
+      const bool rlive = p.res && res_at(p, m, n, off, ro);
       for (int e = 0; e < 8 && n + e < p.K; ++e) {
-        float t = v[e] + (p.res ? bf2f(p.res[off + e]) : 0.f);
+        float t = v[e] + (rlive ? bf2f(p.res[ro + e]) : 0.f);
         if (p.relu) t = fmaxf(t, 0.f);
         const bf16_t o = f2bf(t);
         p.y[yoff + e] = o;
@@ -629,7 +653,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
-                           hipStream_t s, int ldw = 0, const float* stat_shift = nullptr) {
+                           hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
+                           int res_sw = 0, int res_H = 0, int res_W = 0) {
   const bool c4 = C == 4;
   // any K: partial 8-channel chunks are stored per element in the epilogue
   if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -646,7 +671,12 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.bias = bias;
   p.y = (bf16_t*)y;
   p.res = (const bf16_t*)res;
-  p.stats = stats;
+  p.res_sh = res ? res_sh : 0;
+  p.res_sw = res ? res_sw : 0;
+  p.res_H = res_H;
+  p.res_W = res_W;
+  if (p.res_sh && (p.res_sw <= 0 || res_H * p.res_sh < P || res_W * p.res_sw < Q || res_H <= 0 || res_W <= 0))
+    return (int)hipErrorInvalidValue;
   p.stat_shift = stats ? stat_shift : nullptr;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -659,6 +689,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
   p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
   if (p.scatter && stats) return (int)hipErrorInvalidValue;
+  if (p.scatter && p.res_sh) return (int)hipErrorInvalidValue;
   p.ldy = ldy;
   if (ldy != K && (p.scatter || bnx)) return (int)hipErrorInvalidValue;
   p.bnx = (const bf16_t*)bnx;
@@ -709,6 +740,17 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
                                      hipStream_t s) {
   return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
                          osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s);
+}
+
+// bigdl_conv_fwd_full with a STRIDED residual (see ConvParams::res_sh): res is [Nb][res_H][res_W][K].
+BIGDL_EXPORT int bigdl_conv_fwd_full_rs(const void* x, const void* w, const void* res, void* y, float* stats, int Nb,
+                                        int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
+                                        int pw, int dh, int dw, const void* bnx, const float* bn_sc, const float* bn_sh,
+                                        const float* bn_mean, const void* bn_mask, int res_sh, int res_sw, int res_H,
+                                        int res_W, hipStream_t s) {
+  if (!res || res_sh <= 0 || res_sw <= 0) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
+                         0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W);
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).

@@ -13,6 +13,7 @@ from typing import Optional
 import torch
 
 from . import native as N
+from . import reference as R_
 from ..utils import config
 from .native import register, ptr, stream_ptr, check
 
@@ -531,9 +532,18 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
     pw = dilation[1] * (S - 1) - pad[1]
     if ph < 0 or pw < 0:
         return None
-    if residual is not None and not (C_ % 8 == 0 and residual.shape == (N_, C_, H, W) and residual.dtype == _bf16
-                                     and residual.is_contiguous(memory_format=torch.channels_last)
-                                     and _al16(residual)):
+    rs = None  # strided residual geometry (res_sh, res_sw, res_H, res_W)
+    if isinstance(residual, R_.StridedGrad):
+        t = residual.t
+        if not (C_ % 8 == 0 and residual.shape == (N_, C_, H, W) and t.dtype == _bf16 and t.shape[:2] == (N_, C_)
+                and t.is_contiguous(memory_format=torch.channels_last) and _al16(t)):
+            return None
+        rs = (residual.stride[0], residual.stride[1], t.shape[2], t.shape[3])
+        residual = t
+    elif residual is not None and not (C_ % 8 == 0 and residual.shape == (N_, C_, H, W)
+                                       and residual.dtype == _bf16
+                                       and residual.is_contiguous(memory_format=torch.channels_last)
+                                       and _al16(residual)):
         return None
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
     if bn_fuse is not None and C_ % 8 == 0:
@@ -552,12 +562,23 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         if ok:
             G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
             part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)
-            check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_, P,
-                                             Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, 1, 1,
-                                             0, 0, H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), _s()),
-                  "conv_dgrad_bnbwd")
+            if rs is not None:
+                check(_lib().bigdl_conv_fwd_full_rs(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q,
+                                                    K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
+                                                    ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), *rs, _s()),
+                      "conv_dgrad_bnbwd_rs")
+            else:
+                check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_,
+                                                 P, Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0,
+                                                 1, 1, 0, 0, H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
+                                                 _s()), "conv_dgrad_bnbwd")
             bn_fuse["partial"], bn_fuse["G"] = part, G
             return gx
+    if rs is not None:
+        check(_lib().bigdl_conv_fwd_full_rs(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
+                                            S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(None), ptr(None),
+                                            ptr(None), ptr(None), ptr(None), *rs, _s()), "conv_dgrad_rs")
+        return gx
     check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
                                    S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, _s()), "conv_dgrad")
     return gx
@@ -657,7 +678,7 @@ def _parity_classes(H, W, R, S, sh, sw, ph, pw):
     return classes
 
 
-def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
+def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None, lazy=False):
     """Strided backward-data by sub-pixel decomposition: the input-gradient pixels of parity
     (a, b) = (h mod sh, w mod sw) receive only the filter taps r ≡ a + ph (mod sh), s ≡ b + pw
     (mod sw), so each parity class is a STRIDE-1 convolution of gy with a flipped sub-filter whose
@@ -674,11 +695,20 @@ def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None):
                                      residual.is_contiguous(memory_format=torch.channels_last) and _al16(residual)):
         return None
     P, Q = gy.shape[2], gy.shape[3]
-    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
     ckey = (H, W, R, S, sh, sw, ph, pw)
     classes = _STRIDED_CLASSES.get(ckey)
     if classes is None:
         classes = _STRIDED_CLASSES[ckey] = _parity_classes(H, W, R, S, sh, sw, ph, pw)
+    if lazy and residual is None and R == 1 and S == 1 and ph == 0 and pw == 0:
+        # 1×1 stride-s: only parity (0, 0) has a tap — return its pixels densely packed and let the
+        # consumer read them as a strided residual (no zero-filled full-resolution tensor)
+        (a, b, rs, ss, ho, wo, ea, eb) = classes[0]
+        wt = _subfilters(w4, classes, ckey)[0]
+        tmp = torch.empty((N_, C_, ho, wo), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+        check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(None), ptr(tmp), ptr(None), N_, P, Q, K, C_,
+                                       1, 1, ho, wo, 1, 1, 0, 0, 1, 1, 0, _s()), "conv_dgrad_1x1s_lazy")
+        return R_.StridedGrad(tmp, stride, (N_, C_, H, W))
+    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
     if any(not rs or not ss for (_, _, rs, ss, *_r) in classes):
         # some parity receives no tap (e.g. 1x1 stride 2): those pixels are exactly zero / the residual
         if residual is not None:
@@ -789,7 +819,11 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                    scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
+                    scale=1.0, residual=None, bn_fuse=None, pad_slot=None, lazy_strided=False):
+    """``lazy_strided``: a 1×1 stride-s unpadded conv may return its input gradient as a
+    :class:`~bigdl.ops.reference.StridedGrad` (the caller sums it as a strided residual)."""
+    if isinstance(residual, R_.StridedGrad) and (tuple(stride) != (1, 1) or groups > 1 or gy.dtype != _bf16):
+        residual = residual.dense()
     if groups > 1 and residual is None and bn_fuse is None and _depthwise_ok(x, w4, groups):
         return _depthwise_bwd(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale)
     if groups > 1 and residual is None and bn_fuse is None and _grouped_ok(x, w4, groups) and gy.dtype == _bf16:
@@ -848,13 +882,14 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             if gi is None and residual is not None:
                 gi = _dgrad_s1(gy, w4, x.shape, pad, dilation)
         else:
-            gi = _dgrad_strided(gy, w4, x.shape, tuple(stride), tuple(pad), dilation, residual)
+            gi = _dgrad_strided(gy, w4, x.shape, tuple(stride), tuple(pad), dilation, residual,
+                                lazy=lazy_strided and bn_fuse is None)
             res_done = gi is not None
         if gi is None:  # dilated strided backward-data: library path
             N.note_fallback("conv2d_backward.dgrad", "dilated-strided", (gy, x, w4))
             gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
         if residual is not None and not res_done:
-            gi = gi + residual
+            gi = R_.as_dense(gi) + R_.as_dense(residual)
     if gw_acc is not None and scale != 0:
         side = _wgrad_side_stream(gy) if _WG["on"] else None
         if side is None:

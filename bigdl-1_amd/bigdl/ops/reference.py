@@ -56,7 +56,7 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
 
 
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None,
-                    gb_acc=None, scale=1.0, residual=None, bn_fuse=None, pad_slot=None):
+                    gb_acc=None, scale=1.0, residual=None, bn_fuse=None, pad_slot=None, lazy_strided=False):
     """``SpatialConvolution.updateGradInput`` + ``accGradParameters`` (``:364-505``).
 
     Returns gradInput (or None); ACCUMULATES ``scale·dW`` into ``gw_acc`` (O, I/g, kH, kW view,
@@ -72,8 +72,30 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     if need_b:
         gb_acc.add_(acc_float(gb), alpha=scale)
     if residual is not None and gi is not None:
-        gi = gi + residual.to(gi.dtype)
+        gi = gi + as_dense(residual).to(gi.dtype)
     return gi
+
+
+class StridedGrad:
+    """Input gradient of a 1×1, stride-s, unpadded convolution: nonzero only at pixels (s·i, s·j),
+    kept as the dense tensor ``t`` [N][C][ceil(H/s)][ceil(W/s)] of exactly those pixels.  A conv whose
+    dgrad sums it as a residual reads it in its epilogue (``res_sh``/``res_sw``) — the zero-filled
+    full-resolution copy is built only by :meth:`dense` when something else needs it."""
+    __slots__ = ("t", "stride", "shape")
+
+    def __init__(self, t, stride, shape):
+        self.t, self.stride, self.shape = t, tuple(stride), tuple(shape)
+
+    def dense(self):
+        out = torch.zeros(self.shape, dtype=self.t.dtype, device=self.t.device,
+                          memory_format=torch.channels_last if self.t.is_contiguous(
+                              memory_format=torch.channels_last) else torch.contiguous_format)
+        out[:, :, ::self.stride[0], ::self.stride[1]] = self.t
+        return out
+
+
+def as_dense(g):
+    return g.dense() if isinstance(g, StridedGrad) else g
 
 
 def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups=1):
