@@ -56,6 +56,8 @@ def _parse(argv=None):
     ap.add_argument("--comm-dtype", default=os.environ.get("BIGDL_COMM_DTYPE", "fp32"))
     ap.add_argument("--phase-steps", type=int, default=3,
                     help="extra untimed steps with per-phase timers (0 = off)")
+    ap.add_argument("--syncbn", action="store_true",
+                    help="cross-rank SyncBN in every BN (setParallism), the reference's TrainImageNet option")
     ap.add_argument("--force-distri", action="store_true",
                     help="use the DistriOptimizer (RCCL path) even at world size 1 (path validation)")
     return ap.parse_args(argv)
@@ -93,6 +95,11 @@ def _build(args, dev, rank):
     RNG.setSeed(42)
     model = ResNet(1000, depth=50, dataset=DatasetType.ImageNet, image_size=args.image_size)
     model_init(model)
+    if args.syncbn:
+        from bigdl.nn import SpatialBatchNormalization
+        for m in model.flattened_modules():
+            if isinstance(m, SpatialBatchNormalization):
+                m.setParallism(2)
     crit = CrossEntropyCriterion()
     sgd = SGD(learningrate=0.1, learningrate_decay=0.0, weightdecay=1e-4, momentum=0.9, dampening=0.0,
               nesterov=True)
@@ -204,7 +211,7 @@ def main(argv=None):
             "config": {"model": "ResNet-50", "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image_size, "classes": 1000, "parallelism": f"dp{world}",
                        "optimizer": "SGD(lr=0.1,m=0.9,nesterov,wd=1e-4)+L2Reg(1e-4)",
-                       "comm_dtype": args.comm_dtype, "device": dev.type,
+                       "comm_dtype": args.comm_dtype, "device": dev.type, "syncbn": bool(args.syncbn),
                        "driver": type(opt).__name__},
             "phase_ms_max_over_ranks": phases,
             "final_loss": final_loss, "native_kernels": ns.get("loaded", False),

@@ -180,8 +180,10 @@ class SpatialConvolution(TensorModule):
         """The training BN that will consume this conv's output (fusion), if the epilogue can
         produce its statistics."""
         bn = self._bias_folded_into
-        if bn is None or not bn.train or getattr(bn, "_sync", False) or not x.is_cuda:
+        if bn is None or not bn.train or not x.is_cuda:
             return None
+        if getattr(bn, "_sync", False) and not config.get_property("bigdl.bn.shiftedStats"):
+            return None  # SyncBN sums partials across ranks: they need the common running-mean shift
         if self.format != "NCHW" or not config.get_property("bigdl.fusion.convstats"):
             return None
         return bn
@@ -239,7 +241,8 @@ class SpatialConvolution(TensorModule):
         elif (fuse_res and self._tail_candidates and gy.is_cuda and config.get_property("bigdl.fusion.bnbwd")):
             bn = self._tail_target(x)
             if bn is not None:
-                bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output}
+                bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output,
+                           "bits": getattr(bn, "_relu_bits", None)}
         # the shortcut conv of a fused ResNet block (1×1 stride 2) may hand its input gradient back
         # as a StridedGrad: the block's first conv sums it in its dgrad epilogue
         lazy = (need_input and self._lazy_strided_ok and res is None and bn_fuse is None and batched

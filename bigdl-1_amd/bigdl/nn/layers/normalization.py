@@ -117,6 +117,8 @@ class BatchNormalization(TensorModule):
     _last_input = None
     #: (gm data_ptr, partials, G) left by the consuming conv's dgrad epilogue for this backward
     _pending_grad = None
+    #: ReLU mask of the last fused-tail forward output as bits (uint8, one byte per 8 channels)
+    _relu_bits = None
 
     def _in_bias(self):
         p = self._bias_producer
@@ -159,14 +161,25 @@ class BatchNormalization(TensorModule):
                 if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
                     coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
                 ps, self._pending_stats = self._pending_stats, None
+                # a fused block tail (ReLU(BN(x) + shortcut)) on the GPU also emits its output's ReLU
+                # mask as bits: the next block's dgrad epilogue reads 1/16 of the bytes of the output
+                bits = None
+                if (residual is not None and relu and x.is_cuda and x.dim() == 4 and C_ % 8 == 0
+                        and getattr(self, "_residual_mode", False)):
+                    n = x.numel() // 8
+                    bits = self._relu_bits
+                    if bits is None or bits.numel() != n or bits.device != x.device:
+                        bits = torch.empty(n, dtype=torch.uint8, device=x.device)
+                self._relu_bits = None
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
-                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4])
+                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits)
                 if r is NotImplemented:
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
                                                     self.momentum, self.eps, relu=relu, residual=residual,
-                                                    in_bias=ib, coef_out=coef)
+                                                    in_bias=ib, coef_out=coef, bits_out=bits)
+                self._relu_bits = bits
                 y, mean, invstd = r
                 self._last_input = x
             self.saveMean, self.saveStd = mean, invstd
@@ -179,7 +192,56 @@ class BatchNormalization(TensorModule):
                 y = torch.relu(y)
         return y.reshape(input.shape) if input.dim() == 1 else y
 
+    def _sync_count(self, x):
+        """Rows over all ranks of the sync group (one collective per new input shape, cached)."""
+        import torch.distributed as dist
+        key = (tuple(x.shape), id(self._sync_group))
+        cache = self.__dict__.setdefault("_sync_counts", {})
+        n = cache.get(key)
+        if n is None:
+            t = torch.tensor([float(x.numel() // x.shape[1])], dtype=torch.float64,
+                             device=x.device if dist.get_backend(self._sync_group) == "nccl" else "cpu")
+            dist.all_reduce(t, group=self._sync_group)
+            n = cache[key] = int(t.item())
+        return n
+
+    def _sync_native_ok(self, x):
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+                and ops.native_has("batchnorm_forward_train"))
+
+    def _sync_forward_native(self, x, g, b, relu, residual, in_bias):
+        """SyncBN on the HIP kernels: local shifted sums (the conv epilogue's partials when it
+        produced them, else one stats pass) → one RCCL all-reduce of 2·C floats → finalize over the
+        global row count → apply (+residual, ReLU).  The shift is the running mean, identical on
+        every rank.  NotImplemented → torch path."""
+        import torch.distributed as dist
+        from ...ops import native_ops as NO
+        C_ = x.shape[1]
+        ps, self._pending_stats = self._pending_stats, None
+        if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape) and ps[4] is not None:
+            shift = ps[4]
+            sums = NO.bn_local_sums(x, shift, ps[2], ps[3])
+        else:
+            shift = self.runningMean
+            sums = NO.bn_local_sums(x, shift)
+        if sums is NotImplemented:
+            return NotImplemented
+        dist.all_reduce(sums, group=self._sync_group)
+        coef = self._coef
+        if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
+            coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
+        r = NO.bn_forward_from_sums(x, sums, self._sync_count(x), shift, g, b, self.runningMean, self.runningVar,
+                                    self.momentum, self.eps, relu=relu, residual=residual, in_bias=in_bias,
+                                    coef_out=coef)
+        if r is not NotImplemented:
+            self._last_input = x
+        return r
+
     def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None):
+        if self._sync_native_ok(x):
+            r = self._sync_forward_native(x, g, b, relu, residual, in_bias)
+            if r is not NotImplemented:
+                return r
         mean, var, cnt = self._sync_stats(x)
         invstd = torch.rsqrt(var + self.eps)
         with torch.no_grad():
@@ -259,6 +321,24 @@ class BatchNormalization(TensorModule):
     def _sync_backward(self, x, gy, g, y, need_input, acc, relu=None):
         relu = self._fused_relu if relu is None else relu
         import torch.distributed as dist
+        if self._sync_native_ok(x) and gy.dtype == torch.bfloat16:
+            # native: local [Σg, Σg·(x − μ)] → RCCL all-reduce of 2·C floats → local dγ/dβ and the
+            # global input-gradient coefficients → one apply pass
+            from ...ops import native_ops as NO
+            both = NO.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=relu)
+            if both is not NotImplemented:
+                C2 = 2 * x.shape[1]
+                loc, glob = both[:C2], both[C2:]
+                dist.all_reduce(glob, group=self._sync_group)
+                gi = NO.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, self._sync_count(x),
+                                              y=y, relu=relu, need_input=need_input,
+                                              gg_acc=self.gradWeight if (acc and self.affine) else None,
+                                              gb_acc=self.gradBias if (acc and self.affine) else None,
+                                              scale=self.scale_w if acc else 0.0)
+                if gi is not NotImplemented:
+                    if acc and self.affine and self.scale_b != self.scale_w:
+                        self.gradBias.add_(loc[:x.shape[1]], alpha=self.scale_b - self.scale_w)
+                    return gi
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
         shape = [1, C] + [1] * (x.dim() - 2)

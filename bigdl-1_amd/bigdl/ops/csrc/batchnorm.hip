@@ -31,8 +31,11 @@ __device__ __forceinline__ BnGeom bn_geom(int C) {
 
 // ------------------------------------------------------------------------------------------------ stats
 // partial[b][c] = Σ_{rows of block b} (x − K_c),  partial[G + b][c] = Σ (x − K_c)²
+// kshift (optional): per-channel shift K (a cross-rank SyncBN needs the SAME K on every rank — the
+// running mean); default K = x[row 0]
 __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, long long M, int C,
-                                                  long long rows_per_block, float* __restrict__ partial, int G) {
+                                                  long long rows_per_block, float* __restrict__ partial, int G,
+                                                  const float* __restrict__ kshift = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
@@ -45,7 +48,12 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
   float* s_sq = smem + g.RPI * C;      // [RPI][C]
   for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
     float K[8], s[8], q[8];
-    load8(x + (size_t)cg * 8, K);  // row 0
+    if (kshift) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) K[k] = kshift[cg * 8 + k];
+    } else {
+      load8(x + (size_t)cg * 8, K);  // row 0
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
     if (r_off < g.RPI) {
@@ -172,10 +180,14 @@ __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const fl
 // inputs are streamed with non-temporal loads (read once per pass, next use a whole step later):
 // k_bn_apply<res, relu> 1.56 → 1.37 ms per ResNet-50 step, step 23.1 → 22.8 ms
 // (profiles/r2_bench_v7_profile.txt)
-template <bool RES, bool RELU>
+// BITS (with RELU): also emit the ReLU mask as one byte per 8-channel chunk (bit e = output channel
+// cg·8 + e is > 0) — a ResNet block tail's output mask for the backward, 1/16 of the bytes of
+// re-reading the bf16 output there.
+template <bool RES, bool RELU, bool BITS = false>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                   bf16_t* __restrict__ y, long long M, int C,
-                                                  const float* __restrict__ scale, const float* __restrict__ shift) {
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  uint8_t* __restrict__ bits = nullptr) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -203,6 +215,14 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
         v[k] = o;
       }
       store8(y + off, v);
+      if (BITS) {
+        // the bit must agree with the stored bf16 value (> 0 after rounding: a positive fp32 never
+        // rounds to +0 in bf16, so o > 0 is exact)
+        uint32_t b = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+        bits[off >> 3] = (uint8_t)b;
+      }
     }
   }
 }
@@ -215,6 +235,23 @@ static int apply_grid(long long M, int C) {
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
+}
+
+static void launch_apply(const void* x, const void* res, void* y, long long M, int C, const float* coef, int relu,
+                         void* bits, hipStream_t s) {
+  int grid = apply_grid(M, C);
+  const bf16_t* xr = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  bf16_t* yr = (bf16_t*)y;
+  uint8_t* br = (uint8_t*)bits;
+  if (relu && bits && res)
+    hipLaunchKernelGGL((k_bn_apply<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+  else if (relu && bits)
+    hipLaunchKernelGGL((k_bn_apply<false, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+  else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
 }
 
 // number of partial blocks used by the stats / backward-reduce kernels (mirrored in Python)
@@ -237,10 +274,12 @@ static size_t stats_smem(int C) {
 }
 
 // Training forward.  ws: partial buffer of 2·G·C floats; coef: 2·C floats (scale, shift).
+// bits (optional, relu only): M·C/8 bytes receiving the output's ReLU mask (see k_bn_apply)
 BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
                                     const float* beta, const float* in_bias, float* run_mean, float* run_var,
                                     float momentum, float eps, float* save_mean, float* save_invstd, float* ws,
-                                    float* coef, int relu, hipStream_t s) {
+                                    float* coef, int relu, void* bits, hipStream_t s) {
+  if (bits && !relu) return (int)hipErrorInvalidValue;
   if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
   int G = bigdl_bn_num_partials(M, C);
   long long rpb = (M + G - 1) / G;
@@ -250,14 +289,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, nullptr,
                      (const float*)ws, G,
                      M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
-  int grid = apply_grid(M, C);
-  const bf16_t* xr = (const bf16_t*)x;
-  const bf16_t* rr = (const bf16_t*)res;
-  bf16_t* yr = (bf16_t*)y;
-  if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  launch_apply(x, res, y, M, C, coef, relu, bits, s);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -315,9 +347,9 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
                                              const float* gamma, const float* beta, const float* in_bias,
                                              float* run_mean, float* run_var, float momentum, float eps,
                                              float* save_mean, float* save_invstd, const float* partial, int G,
-                                             const float* kshift, float* coef, int relu, float* scratch,
+                                             const float* kshift, float* coef, int relu, float* scratch, void* bits,
                                              hipStream_t s) {
-  if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  if (C % 8 || M <= 0 || G <= 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
   if (maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
                        (const double*)scratch, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
@@ -326,14 +358,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
     hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
                        partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd,
                        coef, coef + C);
-  int grid = apply_grid(M, C);
-  const bf16_t* xr = (const bf16_t*)x;
-  const bf16_t* rr = (const bf16_t*)res;
-  bf16_t* yr = (bf16_t*)y;
-  if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
-  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C);
+  launch_apply(x, res, y, M, C, coef, relu, bits, s);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -529,6 +554,119 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
     int grid = apply_grid(M, C);
     hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,
                        (const bf16_t*)x, (const bf16_t*)nullptr, (bf16_t*)gx, (bf16_t*)nullptr, M, C, coef);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------ SyncBN
+// Cross-rank BatchNormalization (P6 / X11, SpatialBatchNormalization.scala:1114-1151,1257-1329):
+// each rank reduces its partials to one [2][C] fp32 vector (Σ(x−K), Σ(x−K)² forward; Σg, Σg·(x−μ)
+// backward), the host all-reduces those 2·C floats over RCCL, and the finalize/apply kernels below
+// take the GLOBAL sums (G = 1 row) with the global row count — the same finalize code as the local
+// path, so SyncBN costs two tiny kernels and one 2·C collective per direction.
+template <typename T>
+__global__ void __launch_bounds__(1024) k_bn_sum_rows(const T* __restrict__ partial, int G, int C,
+                                                      float* __restrict__ out, float* __restrict__ out2) {
+  __shared__ double lds[32][2][33];
+  double a, b;
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  if ((threadIdx.x >> 5) != 0 || c >= C) return;
+  out[c] = (float)a;
+  out[C + c] = (float)b;
+  if (out2) {  // a second copy (the buffer the collective sums in place, next to the local sums)
+    out2[c] = (float)a;
+    out2[C + c] = (float)b;
+  }
+}
+
+static void sum_rows(const float* partial, int G, int C, float* scratch, float* out, hipStream_t s,
+                     float* out2 = nullptr) {
+  if (maybe_fold(partial, G, C, scratch, s))
+    hipLaunchKernelGGL(k_bn_sum_rows<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const double*)scratch, G, C, out,
+                       out2);
+  else
+    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, C, out, out2);
+}
+
+// Local shifted sums of x (kshift = the running mean, identical on every rank): out[2C].
+BIGDL_EXPORT int bigdl_bn_stats_sums(const void* x, long long M, int C, const float* kshift, float* ws,
+                                     float* scratch, float* out, hipStream_t s) {
+  if (C % 8 || M <= 0 || !kshift) return (int)hipErrorInvalidValue;
+  int G = bigdl_bn_num_partials(M, C);
+  long long rpb = (M + G - 1) / G;
+  size_t sm = stats_smem(C);
+  if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G, kshift);
+  sum_rows(ws, G, C, scratch, out, s);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Reduce G partial rows (a conv epilogue's, or any [2][G][C] fp32 block) to out[2C].
+BIGDL_EXPORT int bigdl_bn_partials_sums(const float* partial, int G, int C, float* scratch, float* out,
+                                        hipStream_t s) {
+  if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  sum_rows(partial, G, C, scratch, out, s);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Forward from GLOBAL sums (2C, shifted by kshift): finalize over `count` rows (all ranks), apply
+// to this rank's M rows.
+BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y, long long M, long long count, int C,
+                                         const float* gamma, const float* beta, const float* in_bias,
+                                         float* run_mean, float* run_var, float momentum, float eps,
+                                         float* save_mean, float* save_invstd, const float* sums,
+                                         const float* kshift, float* coef, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift, sums,
+                     1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
+                     coef + C);
+  launch_apply(x, res, y, M, C, coef, relu, nullptr, s);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Backward local sums: Σg', Σg'·(x − mean) (g' = gy masked by y > 0 when relu) → out[2C] and the
+// same values in out[2C..4C) (the copy the all-reduce turns into the global sums).
+BIGDL_EXPORT int bigdl_bn_bwd_sums(const void* gy, const void* x, const void* y, long long M, int C, const float* mean,
+                                   float* ws, float* scratch, float* out, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
+  int G = bigdl_bn_num_partials(M, C);
+  long long rpb = (M + G - 1) / G;
+  size_t sm = stats_smem(C);
+  if (relu)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
+                       (const bf16_t*)y, M, C, rpb, mean, ws, G);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
+                       (const bf16_t*)y, M, C, rpb, mean, ws, G);
+  sum_rows(ws, G, C, scratch, out, s, out + 2 * C);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Backward from sums: the LOCAL sums accumulate this rank's dγ, dβ (the data-parallel gradient
+// all-reduce sums them across ranks); the GLOBAL sums over `count` rows give the input-gradient
+// coefficients, applied to this rank's M rows.
+BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const void* y, void* gx, long long M,
+                                         long long count, int C, const float* gamma, const float* mean,
+                                         const float* invstd, float* ggamma, float* gbeta, float gscale,
+                                         const float* local_sums, const float* global_sums, float* coef,
+                                         float* coef_scratch, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
+  if (ggamma || gbeta)
+    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, local_sums, 1, count, C, gamma,
+                       mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch);
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, global_sums, 1, count, C, gamma,
+                     mean, invstd, (float*)nullptr, (float*)nullptr, 0.f, (float*)nullptr, 0.f, coef);
+  if (gx) {
+    int grid = apply_grid(M, C);
+    const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;
+    bf16_t* gx_ = (bf16_t*)gx;
+    if (relu)
+      hipLaunchKernelGGL((k_bn_bwd_apply<true, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M, C,
+                         coef);
+    else
+      hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M,
+                         C, coef);
   }
   BIGDL_CHECK_LAUNCH();
 }

@@ -54,6 +54,9 @@ struct ConvParams {
   // optional explicit mask source for that mode (ResNet block tail: the block output, whose ReLU
   // saw BN(bnx) + shortcut): g ← (g + res) · [bn_mask > 0] instead of the recomputed mask
   const bf16_t* bn_mask;
+  // the same mask as bits (one byte per 8-channel chunk, written by the tail BN's apply kernel):
+  // read instead of bn_mask when set
+  const uint8_t* bn_bits;
   // output row stride in elements (== K unless the conv writes a channel slice of a wider tensor,
   // e.g. its branch of an Inception concat: y points at the slice, rows are ldy apart)
   int ldy;
@@ -507,7 +510,13 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       uint32_t w4[4];
       if (p.bn_mask) {
         float rv[8], mv[8];
-        load8(p.bn_mask + off, mv);
+        if (p.bn_bits) {
+          const uint32_t b = p.bn_bits[off >> 3];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mv[e] = (b >> e) & 1u ? 1.f : 0.f;
+        } else {
+          load8(p.bn_mask + off, mv);
+        }
         size_t ro;
         if (p.res && res_at(p, m, n, off, ro)) {
           load8(p.res + ro, rv);
@@ -654,7 +663,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
-                           int res_sw = 0, int res_H = 0, int res_W = 0) {
+                           int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr) {
   const bool c4 = C == 4;
   // any K: partial 8-channel chunks are stored per element in the epilogue
   if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -697,6 +706,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.bn_sh = bn_sh;
   p.bn_mean = bn_mean;
   p.bn_mask = (const bf16_t*)bn_mask;
+  p.bn_bits = (const uint8_t*)bn_bits;
+  if (bn_bits && (!bn_mask || K % 8)) return (int)hipErrorInvalidValue;
   if (bnx && (!stats || !bn_mean || relu || bias || p.scatter)) return (int)hipErrorInvalidValue;
   if (bnx && !bn_mask && (!bn_sc || !bn_sh || res)) return (int)hipErrorInvalidValue;
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
@@ -742,15 +753,18 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
                          osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s);
 }
 
-// bigdl_conv_fwd_full with a STRIDED residual (see ConvParams::res_sh): res is [Nb][res_H][res_W][K].
-BIGDL_EXPORT int bigdl_conv_fwd_full_rs(const void* x, const void* w, const void* res, void* y, float* stats, int Nb,
-                                        int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
-                                        int pw, int dh, int dw, const void* bnx, const float* bn_sc, const float* bn_sh,
-                                        const float* bn_mean, const void* bn_mask, int res_sh, int res_sw, int res_H,
-                                        int res_W, hipStream_t s) {
-  if (!res || res_sh <= 0 || res_sw <= 0) return (int)hipErrorInvalidValue;
+// bigdl_conv_fwd_full (no bias / ReLU / scatter) with the dgrad extensions: a STRIDED residual
+// (res_sh > 0, see ConvParams::res_sh; res is [Nb][res_H][res_W][K]) and/or the block-tail ReLU mask
+// as bits (bn_bits, with bn_mask given as the fallback source of the same mask).
+BIGDL_EXPORT int bigdl_conv_fwd_full2(const void* x, const void* w, const void* res, void* y, float* stats, int Nb,
+                                      int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
+                                      int pw, int dh, int dw, const void* bnx, const float* bn_sc, const float* bn_sh,
+                                      const float* bn_mean, const void* bn_mask, const void* bn_bits, int res_sh,
+                                      int res_sw, int res_H, int res_W, hipStream_t s) {
+  if (res_sh < 0 || res_sw < 0 || (res_sh > 0) != (res_sw > 0) || (res_sh && !res)) return (int)hipErrorInvalidValue;
   return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
-                         0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W);
+                         0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
+                         bn_bits);
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).

@@ -111,7 +111,7 @@ def _f32vec(t, C_):
 
 @register("batchnorm_forward_train")
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
-                            in_bias=None, coef_out=None):
+                            in_bias=None, coef_out=None, bits_out=None):
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -130,8 +130,18 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     y = torch.empty_like(x)
     check(lib.bigdl_bn_fwd_train(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
                                  ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum), _f(eps), ptr(mean),
-                                 ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()), "bn_fwd_train")
+                                 ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
+                                 ptr(_bits_ok(bits_out, M, C_, relu)), _s()), "bn_fwd_train")
     return y, mean, invstd
+
+
+def _bits_ok(bits, M, C_, relu):
+    """The ReLU-mask byte buffer (M·C/8 uint8) if usable, else None."""
+    if bits is None or not relu:
+        return None
+    if bits.dtype != torch.uint8 or not bits.is_contiguous() or bits.numel() != M * C_ // 8 or not bits.is_cuda:
+        return None
+    return bits
 
 
 def _fold_scratch(G, C_, dev):
@@ -146,7 +156,7 @@ def _coef_ok(t, C_):
 
 
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
-                                    relu=False, residual=None, in_bias=None, coef_out=None, shift=None):
+                                    relu=False, residual=None, in_bias=None, coef_out=None, shift=None, bits_out=None):
     """Training BN whose statistics were produced by the preceding conv's epilogue
     (:func:`conv2d_forward_stats`): finalize + apply only."""
     rc = _rows_c(x)
@@ -169,7 +179,8 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
                                              _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
                                              C.c_int(G), ptr(shift if _f32vec(shift, C_) else None), ptr(coef),
                                              C.c_int(1 if relu else 0),
-                                             ptr(_fold_scratch(G, C_, x.device)), _s()),
+                                             ptr(_fold_scratch(G, C_, x.device)),
+                                             ptr(_bits_ok(bits_out, M, C_, relu)), _s()),
           "bn_fwd_train_partials")
     return y, mean, invstd
 
@@ -192,6 +203,97 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
                                        ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
                                        _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
                                        ptr(_fold_scratch(G, C_, x.device)), _s()), "bn_bwd_partials")
+    return gx
+
+
+# ---- SyncBN (cross-rank statistics; the caller all-reduces the 2·C sums between the halves) ----
+def bn_local_sums(x, shift, partial=None, G=0):
+    """This rank's shifted sums [Σ(x−K), Σ(x−K)²] (fp32 [2C]) with K = ``shift`` (the running mean,
+    identical on every rank): from a producing conv's epilogue partials (``partial``/``G``, which
+    must have been computed with the same shift) or a stats pass over x.  NotImplemented when the
+    native path cannot run."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not _bn_ok(x, C_) or not _f32vec(shift, C_):
+        return NotImplemented
+    out = torch.empty(2 * C_, dtype=_f32, device=x.device)
+    if partial is not None:
+        if partial.numel() != 2 * G * C_ or partial.dtype != _f32:
+            return NotImplemented
+        check(_lib().bigdl_bn_partials_sums(ptr(partial), C.c_int(G), C.c_int(C_),
+                                            ptr(_fold_scratch(G, C_, x.device)), ptr(out), _s()), "bn_partials_sums")
+        return out
+    lib = _lib()
+    Gs = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
+    ws = torch.empty(2 * Gs * C_, dtype=_f32, device=x.device)
+    check(lib.bigdl_bn_stats_sums(ptr(x), _ll(M), C.c_int(C_), ptr(shift), ptr(ws), ptr(_fold_scratch(Gs, C_, x.device)),
+                                  ptr(out), _s()), "bn_stats_sums")
+    return out
+
+
+def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
+                         residual=None, in_bias=None, coef_out=None):
+    """Training BN from GLOBAL shifted sums over ``count`` rows: (y, save_mean, save_invstd)."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias, shift)):
+        return NotImplemented
+    if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
+                                 residual.dtype != _bf16 or not _al16(residual)):
+        return NotImplemented
+    coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
+    mean = torch.empty(C_, dtype=_f32, device=x.device)
+    invstd = torch.empty(C_, dtype=_f32, device=x.device)
+    y = torch.empty_like(x)
+    check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
+                                         ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum),
+                                         _f(eps), ptr(mean), ptr(invstd), ptr(sums), ptr(shift), ptr(coef),
+                                         C.c_int(1 if relu else 0), _s()), "bn_fwd_train_sums")
+    return y, mean, invstd
+
+
+def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
+    """This rank's [Σg', Σg'·(x − mean)] twice (fp32 [4C]: the local sums, then a copy for the
+    in-place all-reduce); g' = gy·[y > 0] when ``relu``."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not _bn_ok(x, C_) or gy.dtype != _bf16 or gy.shape != x.shape or gy.stride() != x.stride() or not _al16(gy):
+        return NotImplemented
+    if relu and (y is None or y.dtype != _bf16 or y.stride() != x.stride() or not _al16(y)):
+        return NotImplemented
+    lib = _lib()
+    G = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
+    ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
+    out = torch.empty(4 * C_, dtype=_f32, device=x.device)
+    check(lib.bigdl_bn_bwd_sums(ptr(gy), ptr(x), ptr(y if relu else None), _ll(M), C.c_int(C_), ptr(save_mean), ptr(ws),
+                                ptr(_fold_scratch(G, C_, x.device)), ptr(out), C.c_int(1 if relu else 0), _s()),
+          "bn_bwd_sums")
+    return out
+
+
+def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
+                          need_input=True, gg_acc=None, gb_acc=None, scale=1.0):
+    """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows → gradInput."""
+    rc = _rows_c(x)
+    if rc is None:
+        return NotImplemented
+    M, C_ = rc
+    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc)):
+        return NotImplemented
+    coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
+    scratch = torch.empty(3 * C_, dtype=_f32, device=x.device)
+    gx = torch.empty_like(x) if need_input else None
+    check(_lib().bigdl_bn_bwd_apply_sums(ptr(gy), ptr(x), ptr(y if relu else None), ptr(gx), _ll(M), _ll(count),
+                                         C.c_int(C_), ptr(gamma), ptr(save_mean), ptr(save_invstd),
+                                         ptr(gg_acc if scale != 0 else None), ptr(gb_acc if scale != 0 else None),
+                                         _f(scale), ptr(local_sums), ptr(global_sums), ptr(coef), ptr(scratch),
+                                         C.c_int(1 if relu else 0), _s()), "bn_bwd_apply_sums")
     return gx
 
 
@@ -552,6 +654,10 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         # first (ResNet block tail: mask = block output)
         bx, mu, mask = bn_fuse["x"], bn_fuse["mean"], bn_fuse.get("mask")
         sc, sh = bn_fuse.get("scale"), bn_fuse.get("shift")
+        bits = bn_fuse.get("bits") if mask is not None else None
+        if bits is not None and not (bits.dtype == torch.uint8 and bits.is_cuda and bits.is_contiguous()
+                                     and bits.numel() == N_ * H * W * C_ // 8):
+            bits = None
 
         def _act_ok(t):
             return (t.shape == (N_, C_, H, W) and t.dtype == _bf16
@@ -562,11 +668,11 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         if ok:
             G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
             part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)
-            if rs is not None:
-                check(_lib().bigdl_conv_fwd_full_rs(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q,
-                                                    K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
-                                                    ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), *rs, _s()),
-                      "conv_dgrad_bnbwd_rs")
+            if rs is not None or bits is not None:
+                check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q,
+                                                  K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
+                                                  ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), ptr(bits),
+                                                  *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_bnbwd2")
             else:
                 check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_,
                                                  P, Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0,
@@ -575,9 +681,9 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
             bn_fuse["partial"], bn_fuse["G"] = part, G
             return gx
     if rs is not None:
-        check(_lib().bigdl_conv_fwd_full_rs(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
-                                            S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(None), ptr(None),
-                                            ptr(None), ptr(None), ptr(None), *rs, _s()), "conv_dgrad_rs")
+        check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
+                                          S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(None), ptr(None),
+                                          ptr(None), ptr(None), ptr(None), ptr(None), *rs, _s()), "conv_dgrad_rs")
         return gx
     check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
                                    S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, _s()), "conv_dgrad")

@@ -105,7 +105,7 @@ def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups
 
 # ------------------------------------------------------------------------- batch norm
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
-                            in_bias=None, coef_out=None):
+                            in_bias=None, coef_out=None, bits_out=None):
     """Training BN (``SpatialBatchNormalization.updateOutputNCHWTrainFloat``, ``:1211``).
 
     Normalises with the biased variance, updates ``runningVar`` with the UNBIASED variance and
@@ -137,7 +137,13 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
         y = y + acc_float(residual)
     if relu:
         y = torch.relu(y)
-    return y.to(x.dtype), mean, invstd
+    y = y.to(x.dtype)
+    if bits_out is not None and relu and x.dim() == 4 and C % 8 == 0:
+        # ReLU mask bits in NHWC chunk order: byte (pixel·C + c) / 8, bit c % 8
+        pos = (y.permute(0, 2, 3, 1).reshape(-1, 8) > 0).to(torch.int32)
+        w = (2 ** torch.arange(8, device=y.device, dtype=torch.int32)).view(1, 8)
+        bits_out.copy_((pos * w).sum(1).to(torch.uint8))
+    return y, mean, invstd
 
 
 def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu=False, in_bias=None):

@@ -51,3 +51,25 @@ def test_embedding_out_of_range_id_raises():
     # maskZero: the padding id is accepted
     NO.embedding_forward(w, torch.tensor([0.0, 2.0], device=dev), 0.0, True)
     NO.embedding_check(sync=True)
+
+
+def test_bn_apply_relu_bits_match_output():
+    """The fused block-tail BN writes its output's ReLU mask as bits (one byte per 8 channels,
+    NHWC chunk order) — must equal (y > 0) of the stored bf16 output."""
+    from bigdl.ops import native_ops as NO, reference as R
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 7, 9, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x)
+    C = 64
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    bits = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+    y, _, _ = NO.batchnorm_forward_train(x, g, b, rm, rv, 0.1, 1e-3, relu=True, residual=res, bits_out=bits)
+    ref_bits = torch.empty_like(bits)
+    pos = (y.permute(0, 2, 3, 1).reshape(-1, 8) > 0).to(torch.int32)
+    ref_bits.copy_((pos * (2 ** torch.arange(8, device=dev, dtype=torch.int32))).sum(1).to(torch.uint8))
+    assert torch.equal(bits, ref_bits)
+    bits2 = torch.empty_like(bits)
+    R.batchnorm_forward_train(x.float(), g, b, rm.clone(), rv.clone(), 0.1, 1e-3, relu=True, residual=res.float(),
+                              bits_out=bits2)
+    assert (bits2 != bits).float().mean() < 0.01  # fp32 vs bf16 rounding at the ReLU edge only

@@ -1,0 +1,97 @@
+"""Native SyncBN (P6, SpatialBatchNormalization.scala:1114-1151,1257-1329) on the HIP kernels over
+RCCL at world size 1: the cross-rank path (local shifted sums → all-reduce of 2·C floats → finalize
+from global sums → apply; backward likewise) must reproduce plain training BN, and its forward +
+backward must launch no torch elementwise kernels (every pass is a bigdl kernel or the
+collective).  Multi-rank correctness of the same math is the gloo world-2/4 oracle test
+(tests/test_distri_resnet.py)."""
+import copy
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _init_world1():
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+
+
+def _block():
+    from bigdl.models.resnet import Convolution, Sbn
+    from bigdl.nn import Sequential, ReLU
+    from bigdl.utils.random import RNG
+    RNG.setSeed(3)
+    m = Sequential().add(Convolution(64, 64, 3, 3, 1, 1, 1, 1)).add(Sbn(64)).add(ReLU(True))
+    m.add(Convolution(64, 128, 1, 1)).add(Sbn(128))
+    with torch.no_grad():
+        for mod in m.modules:
+            if type(mod).__name__ == "SpatialBatchNormalization":
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.2, 0.2)
+    return m
+
+
+def _prep(m, sync):
+    from bigdl.nn.fusion import fuse
+    from bigdl.utils.engine import Engine
+    m.cuda()
+    m.training()
+    for mod in m.modules:
+        if type(mod).__name__ == "SpatialBatchNormalization":
+            mod.setParallism(2 if sync else 1)
+    fuse(m)
+    m.getParameters()
+    m.flat_parameters().enable_shadow(Engine.compute_dtype())
+    return m
+
+
+def test_syncbn_world1_matches_local_bn_and_runs_native():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    _init_world1()
+    a = _block()
+    b = copy.deepcopy(a)
+    a, b = _prep(a, False), _prep(b, True)
+    assert all(getattr(mod, "_sync", False) for mod in b.modules if type(mod).__name__ == "SpatialBatchNormalization")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(16, 64, 28, 28, generator=g).to(dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(16, 128, 28, 28, generator=g).to(dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    outs = []
+    for m in (a, b):
+        m.zeroGradParameters()
+        y = m.forward(x)
+        gi = m.backward(x, gy)
+        torch.cuda.synchronize()
+        outs.append((y.float(), gi.float(), [p.clone() for p in m.parameters()[1]],
+                     [e.clone() for e in m.getExtraParameter()]))
+    (ya, ga, pa, ea), (yb, gb, pb, eb) = outs
+    torch.testing.assert_close(yb, ya, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(gb, ga, rtol=5e-2, atol=5e-2)
+    for u, v in zip(pb, pa):
+        assert float((u - v).norm() / v.norm().clamp_min(1e-12)) < 2e-2
+    for u, v in zip(eb, ea):  # running statistics
+        torch.testing.assert_close(u, v, rtol=1e-3, atol=1e-4)
+    # no torch elementwise kernels in the SyncBN forward/backward
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        b.zeroGradParameters()
+        y = b.forward(x)
+        b.backward(x, gy)
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+    torch_kernels = sorted(n for n in names if "at::native" in n and "Fill" not in n)
+    assert not torch_kernels, torch_kernels
+    assert any("k_bn_sum_rows" in n for n in names), sorted(names)
