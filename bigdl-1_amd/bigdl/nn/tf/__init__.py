@@ -461,3 +461,7 @@ class DecodeRaw(Operation):
 
 __all__ = [n for n, v in list(globals().items()) if isinstance(v, type) and issubclass(v, AbstractModule)
            and v.__module__ == __name__]
+
+from .grad_ops import *  # noqa: E402,F401,F403  (TF backward / training-graph ops)
+from . import grad_ops as _grad_ops  # noqa: E402
+__all__ += _grad_ops.__all__

@@ -26,6 +26,7 @@ from ...nn.tf import Const as _Const
 import sys
 O = sys.modules[_Operation.__module__]  # bigdl.nn.ops (bigdl.nn's namespace also has bigdl.ops as "ops")
 T = sys.modules[_Const.__module__]
+from ...nn.tf import grad_ops as G  # noqa: E402
 from ...nn.layers import activation as A
 from ...utils.table import Table
 from .proto import graph_classes, tensor_to_torch, torch_dtype
@@ -55,10 +56,16 @@ def _num_outputs(node) -> int:
         return int(_attr(node, "num", 1))
     if op in ("TopKV2", "TopK", "Switch", "RefSwitch"):
         return 2
+    if op.startswith("FusedBatchNormGrad"):
+        return 5
     if op.startswith("FusedBatchNorm"):
         return 6 if op.endswith("V3") else 5
     if op == "ParseExample":
         return len(_attr(node, "Tdense", []) or []) + 3 * int(_attr(node, "Nsparse", 0) or 0)
+    if op == "ParseSingleExample":
+        return len(_attr(node, "dense_keys", []) or []) + 3 * int(_attr(node, "num_sparse", 0) or 0)
+    if op == "BroadcastGradientArgs":
+        return 2
     return 1
 
 
@@ -201,6 +208,73 @@ _OPS = {
     "DecodeGif": lambda n: T.DecodeImage(3), "DecodeBmp": lambda n: T.DecodeImage(3),
     "DecodeRaw": lambda n: T.DecodeRaw(torch_dtype(_attr(n, "out_type", 4)), bool(_attr(n, "little_endian", True))),
 }
+
+
+def _g(cls, *attrs, **kw):
+    """Builder of a grad op class from node attributes: ``attrs`` = (attr name, default) pairs."""
+    return lambda n: cls(*[_attr(n, a, d) if not callable(d) else d(n) for a, d in attrs], **kw)
+
+
+def _fmt(n):
+    return _attr(n, "data_format", "NHWC") or "NHWC"
+
+
+def _dil(n):
+    return _attr(n, "dilations", [1, 1, 1, 1]) or [1, 1, 1, 1]
+
+
+def _parse_single(n):
+    dense_t = [torch_dtype(t) for t in (_attr(n, "Tdense", []) or [])]
+    shapes = []
+    for sh in (_attr(n, "dense_shapes", []) or []):
+        dims = [int(d.size) for d in getattr(sh, "dim", [])]
+        shapes.append(dims)
+    return G.ParseSingleExample(_attr(n, "dense_keys", []) or [], dense_t, shapes or [[] for _ in dense_t],
+                                _attr(n, "sparse_keys", []) or [],
+                                [torch_dtype(t) for t in (_attr(n, "sparse_types", []) or [])])
+
+
+_OPS.update({
+    "ReluGrad": lambda n: G.ReluGrad(), "Relu6Grad": lambda n: G.Relu6Grad(), "EluGrad": lambda n: G.EluGrad(),
+    "SoftplusGrad": lambda n: G.SoftplusGrad(), "SoftsignGrad": lambda n: G.SoftsignGrad(),
+    "TanhGrad": lambda n: G.TanhGrad(), "SigmoidGrad": lambda n: G.SigmoidGrad(),
+    "SqrtGrad": lambda n: G.SqrtGrad(), "RsqrtGrad": lambda n: G.RsqrtGrad(),
+    "InvGrad": lambda n: G.InvGrad(), "ReciprocalGrad": lambda n: G.ReciprocalGrad(),
+    "Mod": lambda n: G.Mod(), "TruncateMod": lambda n: G.TruncateMod(),
+    "BiasAddGrad": lambda n: G.BiasAddGrad(_fmt(n)),
+    "BiasAddV1": lambda n: _Lambda(lambda x, b: x + b, "BiasAddV1"),
+    "BroadcastGradientArgs": lambda n: G.BroadcastGradientArgs(),
+    "Conv2DBackpropInput": lambda n: G.Conv2DTranspose(_attr(n, "strides"), _pads_of(n), _fmt(n), _dil(n)),
+    "Conv2DBackpropFilter": lambda n: G.Conv2DBackFilter(_attr(n, "strides"), _pads_of(n), _fmt(n), _dil(n)),
+    "Conv3D": lambda n: G.Conv3D(_attr(n, "strides"), _pads_of(n), _attr(n, "data_format", "NDHWC") or "NDHWC"),
+    "Conv3DBackpropInput": lambda n: G.Conv3DBackpropInput(_attr(n, "strides"), _pads_of(n),
+                                                          _attr(n, "data_format", "NDHWC") or "NDHWC"),
+    "Conv3DBackpropInputV2": lambda n: G.Conv3DBackpropInputV2(_attr(n, "strides"), _pads_of(n),
+                                                              _attr(n, "data_format", "NDHWC") or "NDHWC"),
+    "Conv3DBackpropFilter": lambda n: G.Conv3DBackpropFilter(_attr(n, "strides"), _pads_of(n),
+                                                            _attr(n, "data_format", "NDHWC") or "NDHWC"),
+    "Conv3DBackpropFilterV2": lambda n: G.Conv3DBackpropFilterV2(_attr(n, "strides"), _pads_of(n),
+                                                                _attr(n, "data_format", "NDHWC") or "NDHWC"),
+    "DepthwiseConv2dNativeBackpropInput": lambda n: G.DepthwiseConv2dNativeBackpropInput(
+        _attr(n, "strides"), _pads_of(n), _fmt(n)),
+    "DepthwiseConv2dNativeBackpropFilter": lambda n: G.DepthwiseConv2dNativeBackpropFilter(
+        _attr(n, "strides"), _pads_of(n), _fmt(n)),
+    "Dilation2D": lambda n: O.Dilation2D(_attr(n, "strides"), _attr(n, "rates"), _pads_of(n)),
+    "Dilation2DBackpropInput": lambda n: G.Dilation2DBackpropInput(_attr(n, "strides"), _attr(n, "rates"),
+                                                                  _pads_of(n)),
+    "Dilation2DBackpropFilter": lambda n: G.Dilation2DBackpropFilter(_attr(n, "strides"), _attr(n, "rates"),
+                                                                    _pads_of(n)),
+    "FusedBatchNormGrad": lambda n: G.FusedBatchNormGrad(_attr(n, "epsilon", 1e-4), _fmt(n),
+                                                         bool(_attr(n, "is_training", True))),
+    "FusedBatchNormGradV2": lambda n: _OPS["FusedBatchNormGrad"](n),
+    "FusedBatchNormGradV3": lambda n: _OPS["FusedBatchNormGrad"](n),
+    "MaxPoolGrad": lambda n: G.MaxPoolGrad(_attr(n, "ksize"), _attr(n, "strides"), _pads_of(n), _fmt(n)),
+    "AvgPoolGrad": lambda n: G.AvgPoolGrad(_attr(n, "ksize"), _attr(n, "strides"), _pads_of(n), _fmt(n)),
+    "LRNGrad": lambda n: G.LRNGrad(_attr(n, "depth_radius", 5), _attr(n, "bias", 1.0), _attr(n, "alpha", 1.0),
+                                   _attr(n, "beta", 0.5)),
+    "ResizeBilinearGrad": lambda n: G.ResizeBilinearGrad(bool(_attr(n, "align_corners", False))),
+    "ParseSingleExample": _parse_single,
+})
 
 
 def _squeeze(x, dims):
