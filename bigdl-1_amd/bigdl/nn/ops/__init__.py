@@ -366,7 +366,9 @@ class Tile(Operation):
     """Table(x, multiples) → ``x.repeat(multiples)`` (``Tile.scala``)."""
 
     def updateOutput(self, t):
-        return t[1].repeat(*[int(v) for v in t[2].flatten().tolist()])
+        reps = [int(v) for v in t[2].flatten().tolist()]
+        x = torch.as_tensor(t[1])
+        return x.repeat(*reps) if reps else x.clone()  # a scalar tiles to itself
 
 
 class Select(Operation):

@@ -120,7 +120,8 @@ def tensor_to_torch(tp, byte_order="little"):
         arr = arr.astype(np.int32)
     elif npt in (np.uint32, np.uint64):
         arr = arr.astype(np.int64)
-    return torch.from_numpy(np.ascontiguousarray(arr.reshape(shape)))
+    # (np.ascontiguousarray would turn a 0-d scalar into shape [1])
+    return torch.from_numpy(np.array(arr.reshape(shape), copy=True, order="C"))
 
 
 _DT_OF = {torch.float32: 1, torch.float64: 2, torch.int32: 3, torch.uint8: 4, torch.int16: 5, torch.int8: 6,

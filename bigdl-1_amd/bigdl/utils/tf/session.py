@@ -11,9 +11,16 @@ TF checkpoint by :func:`bigdl.utils.tf.checkpoint.read_checkpoint`):
 * ``saveParameters(path)`` — writes the context as a TF V2 checkpoint (``path.index`` +
   ``path.data-00000-of-00001``) — the reference dumps a Java-serialised map instead.
 
-The reference's queue/reader-fed variant (``train(endPoints, …)`` pulling from TFRecord reader
-nodes on a SparkContext) maps to feeding the same graph from :mod:`bigdl.utils.tf.tfrecord` data
-through ``train``'s ``dataset`` argument; in-graph queue runners are not executed.
+Queue-fed graphs (``Session.scala:132-176,536-680``): ``get_records(endpoints)`` (the reference's
+``getRDD``) runs the graph's own input pipeline — file-name queue, TFRecord readers, shuffle / batch
+queues, parsing and decoding ops — with :class:`~bigdl.utils.tf.executor.GraphExecutor` until the
+data is exhausted and returns one Table per record (batches split along dim 0, the reference's
+``splitTensorByFirstDim``); ``train_graph(end_points, optim_method, end_when, batch_size)`` trains a
+TF TRAINING graph: the updater nodes under ``end_points`` (``ApplyRMSProp``, ``ApplyGradientDescent``,
+…) name each variable and the graph tensor holding its gradient (TF's own backward ops —
+``Conv2DBackpropFilter``, ``ReluGrad``, ``MaxPoolGrad``, …), every iteration evaluates the loss and
+those gradients on a batch from the input pipeline and the BigDL OptimMethod updates the variables
+(one flat parameter vector, like the reference's ``FakeCriterion`` + assigned gradients).
 """
 from __future__ import annotations
 
@@ -81,6 +88,119 @@ class Session:
             for i in range(0, xs.shape[0], batch_size):
                 outs.append(model.forward(xs[i:i + batch_size]))
         return torch.cat(outs) if outs and isinstance(outs[0], torch.Tensor) else outs
+
+    # ------------------------------------------------------------------ queue-fed graphs
+    def _executor(self, seed: int = 0):
+        from .executor import GraphExecutor
+        return GraphExecutor(self.nodes, self.byte_order, seed, variables=self.context)
+
+    def get_records(self, end_points: Sequence[str], has_to_batch: bool = True, seed: int = 0):
+        """Every record the graph's input pipeline produces at ``end_points[0]`` (a dequeue node), as
+        Tables (``getRDD``)."""
+        ex = self._executor(seed)
+        recs = ex.records(end_points[0])
+        if not has_to_batch:
+            return recs
+        return recs
+
+    getRDD = get_records
+
+    _UPDATERS = {"ApplyRMSProp": 7, "ApplyGradientDescent": 2, "ApplyMomentum": 3, "ApplyAdam": 9,
+                 "ApplyAdagrad": 3, "ApplyAdadelta": 6, "ApplyFtrl": 3, "ApplyProximalGradientDescent": 4,
+                 "ResourceApplyRMSProp": 7, "ResourceApplyGradientDescent": 2, "ResourceApplyMomentum": 3,
+                 "ResourceApplyAdam": 9}
+
+    def _updaters(self, end_points):
+        by = {n.name: n for n in self.nodes}
+        seen, todo, found = set(), [_split_ref(e.lstrip("^"))[0] for e in end_points], []
+        while todo:
+            n = todo.pop()
+            if n in seen or n not in by:
+                continue
+            seen.add(n)
+            node = by[n]
+            gi = self._UPDATERS.get(node.op)
+            if gi is not None:
+                found.append((_split_ref(node.input[0])[0], node.input[gi]))
+                continue
+            todo.extend(_split_ref(i.lstrip("^"))[0] for i in node.input)
+        order = [n.name for n in self.nodes]
+        return sorted(set(found), key=lambda t: order.index(t[0]))
+
+    def _data_dequeue(self, refs):
+        by = {n.name: n for n in self.nodes}
+        seen, todo = set(), [_split_ref(r.lstrip("^"))[0] for r in refs]
+        while todo:
+            n = todo.pop(0)
+            if n in seen or n not in by:
+                continue
+            seen.add(n)
+            node = by[n]
+            if node.op.startswith("QueueDequeue"):
+                return node
+            todo.extend(_split_ref(i.lstrip("^"))[0] for i in node.input if not i.startswith("^"))
+        raise ValueError("no queue dequeue feeds the training graph")
+
+    def train_graph(self, end_points: Sequence[str], optim_method, end_when, batch_size: int,
+                    loss: Optional[str] = None, seed: int = 0):
+        """Train a TF training graph from its own input pipeline and gradient ops (see module doc).
+        Returns the per-iteration losses."""
+        from ..table import Table
+        updaters = self._updaters(end_points)
+        if not updaters:
+            raise ValueError("Cannot find updater nodes")
+        ex = self._executor(seed)
+        ex.initialize_variables()
+        # one flat fp32 parameter vector; the context tensors become views of it, so the executor
+        # reads the updated values every iteration
+        names = [v for v, _ in updaters]
+        sizes = [self.context[v].numel() for v in names]
+        w = torch.cat([self.context[v].detach().float().reshape(-1) for v in names])
+        g = torch.zeros_like(w)
+        off = 0
+        for v, n in zip(names, sizes):
+            shape = self.context[v].shape
+            self.context[v] = w[off:off + n].view(shape)
+            off += n
+        loss_ref = loss or end_points[0]
+        by = {n.name: n for n in self.nodes}
+        # an endpoint like ``train_op = Identity(total_loss, ^update_ops)``: take the loss through its
+        # data input — the control inputs are the TF updaters this loop replaces
+        while by[_split_ref(loss_ref)[0]].op in ("Identity", "Snapshot"):
+            data_in = [i for i in by[_split_ref(loss_ref)[0]].input if not i.startswith("^")]
+            if not data_in:
+                break
+            loss_ref = data_in[0]
+        deq = self._data_dequeue([r for _, r in updaters])
+        records = ex.records(deq.name)
+        if not records:
+            raise ValueError(f"the input pipeline of {deq.name} produced no data")
+        state = {"epoch": 1, "neval": 1, "Loss": float("nan"), "score": 0.0, "recordsProcessedThisEpoch": 0}
+        losses = []
+        i = 0
+        n_rec = len(records)
+        while not end_when(state):
+            # the data set is cycled (an epoch ends after n_rec records), so a graph with a baked-in
+            # batch dimension larger than the data still trains
+            batch = [records[(i + j) % n_rec] for j in range(batch_size)]
+            i += batch_size
+            if i >= n_rec:
+                i %= n_rec
+                state["epoch"] += 1
+                state["recordsProcessedThisEpoch"] = 0
+            comps = tuple(torch.stack([torch.as_tensor(r[c + 1]) for r in batch]) for c in range(batch[0].length()))
+            outs = ex.run([loss_ref] + [r for _, r in updaters], feeds={deq.name: comps})
+            off = 0
+            for t, n in zip(outs[1:], sizes):
+                g[off:off + n].copy_(torch.as_tensor(t).float().reshape(-1))
+                off += n
+            lv = torch.as_tensor(outs[0]).float().reshape(-1)[0]
+            optim_method.optimize(lambda _x: (lv, g), w)
+            losses.append(float(lv))
+            state["Loss"] = float(lv)
+            state["neval"] += 1
+            state["recordsProcessedThisEpoch"] += batch_size
+        return losses
 
     def saveParameters(self, path: str):
         from .checkpoint import write_checkpoint
