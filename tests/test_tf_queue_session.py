@@ -77,7 +77,7 @@ def test_train_tf_training_graph_gradients_and_loss():
     (gw,) = run(["gradients/AddN_3"])
     w = sess.context["LeNet/conv1/weights"]
     for idx in ((0, 0, 0, 0), (2, 3, 0, 17)):
-        eps = 1e-2
+        eps = 2e-3  # small: ReLU / max-pool switches make the loss only piecewise smooth
         w[idx] += eps
         lp = float(run(["total_loss"])[0])
         w[idx] -= 2 * eps
