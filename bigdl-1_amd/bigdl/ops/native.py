@@ -71,10 +71,39 @@ def status() -> dict:
             "ops": sorted(_ops_available)}
 
 
+class _TracedLib:
+    """``BIGDL_TRACE_NATIVE=1``: print every native entry point before it runs (stderr, flushed);
+    ``=2``: also synchronize after it and print ``ok`` — a GPU fault is then attributed to the last
+    name printed without its ``ok`` (fault triage without a debugger)."""
+
+    def __init__(self, l, sync):
+        self._l, self._sync = l, sync
+
+    def __getattr__(self, name):
+        f = getattr(self._l, name)
+        if not callable(f) or not name.startswith("bigdl_"):
+            return f
+        import sys
+
+        def call(*a):
+            print(f"[native] {name}", file=sys.stderr, flush=True)
+            r = f(*a)
+            if self._sync and torch.cuda.is_available():
+                torch.cuda.synchronize()
+                print(f"[native] {name} ok rc={r}", file=sys.stderr, flush=True)
+            return r
+        return call
+
+
+_TRACE = os.environ.get("BIGDL_TRACE_NATIVE", "")
+
+
 def lib():
     l = _load()
     if l is None and torch.cuda.is_available() and config.get_property("bigdl.native.require"):
         raise RuntimeError(f"bigdl native HIP kernels are required on a GPU but not loaded: {_load_error}")
+    if _TRACE and l is not None:
+        return _TracedLib(l, _TRACE == "2")
     return l
 
 

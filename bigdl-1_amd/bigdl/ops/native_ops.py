@@ -145,7 +145,7 @@ def _bits_ok(bits, M, C_, relu):
 
 
 def _fold_scratch(G, C_, dev):
-    f = _lib().bigdl_bn_fold_scratch
+    f = N._load().bigdl_bn_fold_scratch  # the raw CDLL symbol (restype must stick)
     f.restype = C.c_longlong
     n = f(C.c_int(G), C.c_int(C_))
     return torch.empty(n, dtype=_f32, device=dev) if n > 0 else None
@@ -978,7 +978,6 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         if gb_acc is not None and scale != 0:
             gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
         return gi
-    from . import reference as R_
     gi = None
     if need_input:
         res_done = False
