@@ -674,12 +674,13 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (!c4) ldw = R * S * C;
   if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * ldw * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
-  ConvParams p;
+  ConvParams p{};  // value-initialised: a field a launcher forgets is null / 0, never stack garbage
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)w;
   p.bias = bias;
   p.y = (bf16_t*)y;
   p.res = (const bf16_t*)res;
+  p.stats = stats;
   p.res_sh = res ? res_sh : 0;
   p.res_sw = res ? res_sw : 0;
   p.res_H = res_H;

@@ -244,7 +244,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
   if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)Nb * P * Q * K * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
-  WgradParams p;
+  WgradParams p{};
   p.x = (const bf16_t*)x;
   p.dy = (const bf16_t*)dy;
   p.dw = dw;

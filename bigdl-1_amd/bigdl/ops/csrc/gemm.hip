@@ -215,7 +215,7 @@ BIGDL_EXPORT int bigdl_gemm(const void* a, long long lda, const void* b, long lo
   const unsigned long long ab = ((unsigned long long)(M - 1) * lda + K) * 2ull;
   const unsigned long long bb = ((unsigned long long)(N - 1) * ldb + K) * 2ull;
   if (ab >= 0x7fff0000ull || bb >= 0x7fff0000ull) return (int)hipErrorInvalidValue;
-  GemmParams p;
+  GemmParams p{};
   p.a = (const bf16_t*)a; p.b = (const bf16_t*)b; p.bias = bias; p.d = (const bf16_t*)d; p.c = c;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldd = ldd;
   p.M = M; p.N = N; p.K = K; p.act = act; p.out_f32 = out_f32; p.alpha = alpha; p.beta = beta;

@@ -69,7 +69,7 @@ BIGDL_EXPORT int bigdl_w_dgrad_xform(const void* w, void* out, int K, int R, int
   // 16-B vectors along both c (reads) and k (writes): C, K multiples of 8, 16-B aligned buffers
   if (ncls < 1 || ncls > XF_MAXC || K <= 0 || C <= 0 || C % 8 || K % 8 || ((uintptr_t)w & 15) || ((uintptr_t)out & 15))
     return (int)hipErrorInvalidValue;
-  XformParams p;
+  XformParams p{};
   p.in = (const bf16_t*)w;
   p.out = (bf16_t*)out;
   p.K = K; p.R = R; p.S = S; p.C = C; p.ncls = ncls;
