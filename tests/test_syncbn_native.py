@@ -81,8 +81,17 @@ def test_syncbn_world1_matches_local_bn_and_runs_native():
     (ya, ga, pa, ea), (yb, gb, pb, eb) = outs
     torch.testing.assert_close(yb, ya, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(gb, ga, rtol=5e-2, atol=5e-2)
-    for u, v in zip(pb, pa):
-        assert float((u - v).norm() / v.norm().clamp_min(1e-12)) < 2e-2
+    assert float((gb - ga).norm() / ga.norm()) < 3e-2
+    # a conv bias feeding a training BN has an exactly-zero true gradient (BN is shift-invariant):
+    # both paths return rounding noise there, so those entries are compared in absolute terms
+    names = [f"{type(m).__name__}.{n}" for (m, n, _g) in a._param_entries()]
+    errs = []
+    for nm, u, v in zip(names, pb, pa):
+        if nm.endswith(".bias") and "Convolution" in nm:
+            errs.append((nm, float((u - v).abs().max()), 1e-2))
+        else:
+            errs.append((nm, float((u - v).norm() / v.norm().clamp_min(1e-12)), 2e-2))
+    assert all(e < tol for _, e, tol in errs), errs
     for u, v in zip(eb, ea):  # running statistics
         torch.testing.assert_close(u, v, rtol=1e-3, atol=1e-4)
     # no torch elementwise kernels in the SyncBN forward/backward
