@@ -11,9 +11,15 @@ Reference quirks kept on purpose (parity): every Dropout in these layers is buil
 ``Dropout(1 - rate)``, i.e. the configured rate is the KEEP probability; the beam-search length
 penalty is ``(5 + len/6)^alpha``; token ids produced by the search are 1-based.
 
-MI355X notes: the score/softmax/value product runs as one fused scaled-dot-product attention
-(flash kernel of the ROCm PyTorch build) whenever no attention-dropout mask is needed; the
-projections are bf16 GEMMs on the compute dtype with fp32 master weights.
+MI355X path (device tensors, bf16 compute): ``Attention`` runs the Q/K/V projections as ONE
+GEMM on the MFMA kernel (gemm.hip) over the adjacent query/key/value weight rows of the
+parameter arena (self-attention; K/V fused for encoder-decoder attention), the fused attention
+kernels of ``ops/csrc/attention.hip`` read Q/K/V straight out of that [B·L][3H] buffer (no
+split/combine-heads copies; causal masking, padding bias and attention dropout in-kernel), and
+the output projection is one more GEMM; the backward writes dQ/dK/dV into one [B·L][3H] buffer
+that feeds a single weight-gradient GEMM.  ``FeedForwardNetwork`` is GEMM+bias+ReLU epilogue →
+dropout → GEMM+bias, backward on the same kernels.  Host tensors (and cached incremental
+decoding) use the torch composition below.
 """
 from __future__ import annotations
 
@@ -44,6 +50,51 @@ def _drop(x, keep_rate, train):
     if p >= 1:
         return torch.zeros_like(x)
     return F.dropout(x, p, True)
+
+
+def _native_dense_ok(x):
+    """Device activations with bf16 compute and the native attention/GEMM kernels loaded."""
+    from ... import ops
+    from ...utils.engine import Engine
+    return (isinstance(x, torch.Tensor) and x.is_cuda and x.dim() >= 2 and Engine.compute_dtype() == torch.bfloat16
+            and ops.native_has("attention_forward"))
+
+
+def _fused_rows(ts):
+    """One [Σrows][cols] view over row blocks that sit back to back in memory (consecutive
+    parameters of one flat arena / shadow), else None."""
+    t0 = ts[0]
+    cols, n = t0.shape[-1], 0
+    for t in ts:
+        if (t.dim() != 2 or t.shape[1] != cols or not t.is_contiguous() or t.dtype != t0.dtype
+                or t.device != t0.device or t.data_ptr() != t0.data_ptr() + n * cols * t0.element_size()):
+            return None
+        n += t.shape[0]
+    return torch.as_strided(t0, (n, cols), (cols, 1))
+
+
+def _proj_bwd(dbuf, src, ws, gws, scale, need_input):
+    """Backward of ``dbuf = src · [W₀; W₁; …]ᵀ`` (one GEMM over the stacked weights when they are
+    adjacent): weight gradients accumulated with ``scale``, returns d(src) (or None)."""
+    from ...ops import native_ops as NO
+    H = src.shape[1]
+    wf = _fused_rows(ws)
+    if scale != 0:
+        gf = _fused_rows(gws)
+        if gf is not None:
+            NO.wgrad_rows(dbuf, src, gf, scale)
+        else:
+            for i, g in enumerate(gws):
+                NO.wgrad_rows(dbuf[:, i * H:(i + 1) * H].contiguous(), src, g, scale)
+    if not need_input:
+        return None
+    if wf is not None:
+        return NO.gemm(dbuf, NO.transpose_bf16(wf))
+    d = None
+    for i, w in enumerate(ws):
+        r = NO.gemm(dbuf[:, i * H:(i + 1) * H], NO.transpose_bf16(w))
+        d = r if d is None else d.add_(r)
+    return d
 
 
 def split_heads(x, n_heads):
@@ -96,6 +147,115 @@ class Attention(AutogradModule):
             return self._forward_cached(x, y, b[1], b[2])
         return self._attend(self._proj(x, "query"), self._proj(y, "key"), self._proj(y, "value"), b)
 
+    # ---- native (device) path -----------------------------------------------------------------
+    def _nat_ok(self, x, y, b):
+        D = self.hiddenSize // self.numHeads
+        return (D in (64, 128) and _native_dense_ok(x) and x.dim() == 3 and isinstance(y, torch.Tensor)
+                and y.is_cuda and y.dim() == 3 and (b is None or isinstance(b, torch.Tensor)))
+
+    def updateOutput(self, input):
+        x, y, b = input[1], input[2], input[3]
+        if not isinstance(b, Table) and self._nat_ok(x, y, b):
+            return self._nat_forward(x, y, b)
+        self._nat = None
+        return super().updateOutput(input)
+
+    def _nat_forward(self, x, y, b):
+        from ... import ops
+        from ...ops import native_ops as NO
+        bf = torch.bfloat16
+        H, nh = self.hiddenSize, self.numHeads
+        D = H // nh
+        B, Lq, _ = x.shape
+        Lk = y.shape[1]
+        x2 = x.reshape(B * Lq, H).to(bf).contiguous()
+        same = y is x or (y.data_ptr() == x.data_ptr() and y.shape == x.shape and y.stride() == x.stride())
+        y2 = x2 if same else y.reshape(B * Lk, H).to(bf).contiguous()
+        ws = [self.cw(n + "Weight", bf) for n in ("query", "key", "value")]
+        wqkv = _fused_rows(ws) if same else None
+        if wqkv is not None:  # self-attention: one [B·L][3H] projection
+            qkv = NO.gemm(x2, wqkv)
+            q, k, v = qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:]
+        else:
+            q = NO.gemm(x2, ws[0])
+            wkv = _fused_rows(ws[1:])
+            if wkv is not None:
+                kv = NO.gemm(y2, wkv)
+                k, v = kv[:, :H], kv[:, H:]
+            else:
+                k, v = NO.gemm(y2, ws[1]), NO.gemm(y2, ws[2])
+        causal = bool(getattr(b, "_bigdl_causal", False)) and Lq == Lk
+        bias = None if (causal or b is None) else b
+        keep = float(self.attentionDropout) if (self.train and self.attentionDropout < 1.0) else 1.0
+        seed = NO.attention_seed(x.device) if keep < 1.0 else 0
+        o, lse = ops.attention_forward(q, k, v, B, nh, Lq, Lk, D, D ** -0.5, bias, causal, keep, seed)
+        out = NO.gemm(o, self.cw("outputWeight", bf))
+        self._nat = (x2, y2, same, q, k, v, o, lse, bias, causal, keep, seed, B, Lq, Lk, x.dtype, y.dtype,
+                     b) if self.train else None
+        self._gi_done = False
+        return out.view(B, Lq, H)
+
+    def _nat_backward(self, gradOutput, need_input):
+        from ... import ops
+        from ...ops import native_ops as NO
+        (x2, y2, same, q, k, v, o, lse, bias, causal, keep, seed, B, Lq, Lk, xdt, ydt, b) = self._nat
+        self._nat = None
+        bf = torch.bfloat16
+        H, nh = self.hiddenSize, self.numHeads
+        D = H // nh
+        s = self.scale_w
+        gy = gradOutput.reshape(B * Lq, H).to(bf).contiguous()
+        do = NO.linear_backward(gy, o, self.cw("outputWeight", bf), True, self.outputGradWeight, None, s)
+        names = ("query", "key", "value")
+        ws = [self.cw(n + "Weight", bf) for n in names]
+        gws = [getattr(self, n + "GradWeight") for n in names]
+        if same:
+            dqkv = torch.empty((B * Lq, 3 * H), dtype=bf, device=gy.device)
+            ops.attention_backward(do, q, k, v, o, lse, B, nh, Lq, Lk, D, D ** -0.5, bias, causal, keep, seed,
+                                   dq=dqkv[:, :H], dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:])
+            if s != 0:
+                gf = _fused_rows(gws)
+                if gf is not None:
+                    NO.wgrad_rows(dqkv, x2, gf, s)
+                else:
+                    for i, g in enumerate(gws):
+                        NO.wgrad_rows(dqkv[:, i * H:(i + 1) * H].contiguous(), x2, g, s)
+            dx = dy = None
+            if need_input:
+                wf = _fused_rows(ws)
+                wt = NO.transpose_bf16(wf) if wf is not None else torch.cat([NO.transpose_bf16(w) for w in ws], 1)
+                dx = NO.gemm(dqkv[:, :H], wt[:, :H])
+                dy = NO.gemm(dqkv[:, H:], wt[:, H:])
+        else:
+            dq = torch.empty((B * Lq, H), dtype=bf, device=gy.device)
+            dkv = torch.empty((B * Lk, 2 * H), dtype=bf, device=gy.device)
+            ops.attention_backward(do, q, k, v, o, lse, B, nh, Lq, Lk, D, D ** -0.5, bias, causal, keep, seed,
+                                   dq=dq, dk=dkv[:, :H], dv=dkv[:, H:])
+            dx = _proj_bwd(dq, x2, ws[:1], gws[:1], s, need_input)
+            dy = _proj_bwd(dkv, y2, ws[1:], gws[1:], s, need_input)
+        self._gi_done = True
+        if not need_input:
+            return None
+        gi = [dx.view(B, Lq, H).to(xdt), dy.view(B, Lk, H).to(ydt)]
+        if b is not None:  # the mask inputs (PaddingMask / SelfAttentionMask) take no gradient
+            gi.append(torch.zeros_like(b))
+        return T(*gi)
+
+    def updateGradInput(self, input, gradOutput):
+        if getattr(self, "_nat", None) is not None:
+            return self._nat_backward(gradOutput, True)
+        return super().updateGradInput(input, gradOutput)
+
+    def accGradParameters(self, input, gradOutput):
+        if getattr(self, "_gi_done", False):
+            self._gi_done = False
+            return
+        if getattr(self, "_nat", None) is not None:
+            self._nat_backward(gradOutput, False)
+            self._gi_done = False
+            return
+        super().accGradParameters(input, gradOutput)
+
     def _forward_cached(self, x, y, bias, cache):
         if self.train:
             raise RuntimeError("Only support input cache for model inference")
@@ -122,6 +282,65 @@ class FeedForwardNetwork(AutogradModule):
         _dense_param(self, "filter", filter_size, hidden_size, True)
         _dense_param(self, "output", hidden_size, filter_size, True)
 
+    def updateOutput(self, x):
+        if (_native_dense_ok(x) and self.hiddenSize % 8 == 0 and self.filterSize % 8 == 0
+                and x.shape[-1] == self.hiddenSize):
+            return self._nat_forward(x)
+        self._nat = None
+        return super().updateOutput(x)
+
+    def _nat_forward(self, x):
+        from ... import ops
+        from ...ops import native_ops as NO
+        bf = torch.bfloat16
+        x2 = x.reshape(-1, self.hiddenSize).to(bf).contiguous()
+        h = NO.linear_forward(x2, self.cw("filterWeight", bf), self.filterBias, act=1)  # GEMM+bias+ReLU
+        p = 1.0 - self.reluDropout
+        hd, mask = h, None
+        if self.train and p > 0:
+            if p >= 1:
+                hd = torch.zeros_like(h)
+            else:
+                hd, mask = ops.dropout_forward(h, p)
+        y = NO.linear_forward(hd, self.cw("outputWeight", bf), self.outputBias)
+        self._nat = (x2, h, hd, mask, p, x.shape, x.dtype) if self.train else None
+        self._gi_done = False
+        return y.view(*x.shape[:-1], self.hiddenSize)
+
+    def _nat_backward(self, gradOutput, need_input):
+        from ... import ops
+        from ...ops import native_ops as NO
+        x2, h, hd, mask, p, shape, xdt = self._nat
+        self._nat = None
+        bf, s = torch.bfloat16, self.scale_w
+        gy = gradOutput.reshape(-1, self.hiddenSize).to(bf).contiguous()
+        dhd = NO.linear_backward(gy, hd, self.cw("outputWeight", bf), True, self.outputGradWeight,
+                                 self.outputGradBias, s)
+        if mask is not None:
+            dhd = ops.dropout_backward(dhd, mask, p)
+        elif self.train and p >= 1:
+            dhd = torch.zeros_like(dhd)
+        dh = NO.relu_backward(dhd, h)
+        dx = NO.linear_backward(dh, x2, self.cw("filterWeight", bf), need_input, self.filterGradWeight,
+                                self.filterGradBias, s)
+        self._gi_done = True
+        return None if dx is None else dx.view(shape).to(xdt)
+
+    def updateGradInput(self, input, gradOutput):
+        if getattr(self, "_nat", None) is not None:
+            return self._nat_backward(gradOutput, True)
+        return super().updateGradInput(input, gradOutput)
+
+    def accGradParameters(self, input, gradOutput):
+        if getattr(self, "_gi_done", False):
+            self._gi_done = False
+            return
+        if getattr(self, "_nat", None) is not None:
+            self._nat_backward(gradOutput, False)
+            self._gi_done = False
+            return
+        super().accGradParameters(input, gradOutput)
+
     def _forward(self, x):
         w1, b1 = self.P("filterWeight"), self.P("filterBias")
         h = F.relu(F.linear(x.to(w1.dtype), w1, b1.to(w1.dtype)))
@@ -144,8 +363,9 @@ def position_signal(length, channels, min_timescale=1.0, max_timescale=1.0e4, de
 
 def lower_triangle_bias(length, device=None):
     """(1, 1, L, L) with −1e9 above the diagonal (``attentionBiasLowerTriangle``)."""
-    m = torch.triu(torch.full((length, length), _MASK, device=device), diagonal=1)
-    return m.reshape(1, 1, length, length)
+    m = torch.triu(torch.full((length, length), _MASK, device=device), diagonal=1).reshape(1, 1, length, length)
+    m._bigdl_causal = True  # the native attention applies this mask in-kernel (and skips masked tiles)
+    return m
 
 
 class PositionEncode(TensorModule):

@@ -2148,3 +2148,100 @@ def layer_norm(x, weight=None, bias=None, eps=1e-5):
     if any(p is not None and (p.numel() != H or not p.is_cuda) for p in (weight, bias)):
         return NotImplemented
     return _LayerNormFn.apply(x.contiguous(), weight, bias, float(eps))
+
+
+# ---------------------------------------------------------------------------------- K30 attention
+def _attn_rows_ok(t, rows, cols):
+    """[rows][≥cols] bf16 device rows, unit column stride, 16-B aligned, row stride % 8 == 0."""
+    return (isinstance(t, torch.Tensor) and t.dim() == 2 and t.dtype == _bf16 and t.is_cuda
+            and t.shape[0] == rows and t.shape[1] >= cols and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.stride(0) >= cols and _al16(t))
+
+
+def _attn_bias(bias, B, Hh, Lq, Lk, device):
+    """fp32 bias broadcast to (B, Hh, Lq, Lk) → (tensor, element strides); broadcast dims get
+    stride 0, so a (1, 1, L, L) or (B, 1, 1, L) mask is read in place."""
+    if bias is None:
+        return None, (0, 0, 0, 0)
+    b = bias.to(device=device, dtype=_f32)
+    while b.dim() < 4:
+        b = b.unsqueeze(0)
+    try:
+        b = torch.broadcast_to(b, (B, Hh, Lq, Lk))
+    except RuntimeError:
+        return NotImplemented, None
+    return b, tuple(b.stride())
+
+
+def attention_seed(device, rng=None):
+    """The dropout seed of one attention call, shared by its forward and backward: a host int, or
+    under HIP-graph capture a snapshot of the per-device seed counter (a fresh mask per replay)."""
+    if torch.cuda.is_current_stream_capturing():
+        snap = _device_seed(device).clone()
+        _device_seed(device).add_(1)
+        return snap
+    return int(torch.randint(0, 2 ** 31, (1,), generator=rng))
+
+
+def _seed_args(seed):
+    if isinstance(seed, torch.Tensor):
+        return C.c_uint(0), ptr(seed)
+    return C.c_uint(int(seed) & 0xFFFFFFFF), ptr(None)
+
+
+@register("attention_forward")
+def attention_forward(q, k, v, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0):
+    """Fused multi-head attention (attention.hip) on projection rows; see the reference op."""
+    HD = Hh * D
+    if D not in (64, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
+                                  and _attn_rows_ok(v, B * Lk, HD)):
+        return NotImplemented
+    if (causal and Lq != Lk) or not (0.0 < keep <= 1.0):
+        return NotImplemented
+    bt, bs = _attn_bias(bias, B, Hh, Lq, Lk, q.device)
+    if bt is NotImplemented:
+        return NotImplemented
+    out = torch.empty((B * Lq, HD), dtype=_bf16, device=q.device)
+    lse = torch.empty((B, Hh, Lq), dtype=_f32, device=q.device)
+    hs, ds = _seed_args(seed)
+    check(_lib().bigdl_attn_fwd(ptr(q), _ll(q.stride(0)), ptr(k), _ll(k.stride(0)), ptr(v), _ll(v.stride(0)),
+                                ptr(out), _ll(HD), ptr(lse), ptr(bt), *[_ll(x) for x in bs], C.c_int(B), C.c_int(Hh),
+                                C.c_int(Lq), C.c_int(Lk), C.c_int(D), _f(scale), C.c_int(1 if causal else 0),
+                                _f(keep), hs, ds, _s()), "attn_fwd")
+    return out, lse
+
+
+@register("attention_backward")
+def attention_backward(dout, q, k, v, o, lse, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0,
+                       dq=None, dk=None, dv=None):
+    """dQ, dK, dV of :func:`attention_forward` (two kernels, no atomics); ``dq``/``dk``/``dv`` may be
+    column slices of one fused [B·L][3·H] buffer (the QKV projection's backward reads it whole)."""
+    HD = Hh * D
+    if D not in (64, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
+                                  and _attn_rows_ok(v, B * Lk, HD) and _attn_rows_ok(o, B * Lq, HD)
+                                  and _attn_rows_ok(dout, B * Lq, HD)):
+        return NotImplemented
+    if (causal and Lq != Lk) or not (0.0 < keep <= 1.0):
+        return NotImplemented
+    if not (lse.dtype == _f32 and lse.is_contiguous() and lse.numel() == B * Hh * Lq):
+        return NotImplemented
+    bt, bs = _attn_bias(bias, B, Hh, Lq, Lk, q.device)
+    if bt is NotImplemented:
+        return NotImplemented
+    outs = []
+    for t, L in ((dq, Lq), (dk, Lk), (dv, Lk)):
+        if t is None:
+            t = torch.empty((B * L, HD), dtype=_bf16, device=q.device)
+        elif not _attn_rows_ok(t, B * L, HD):
+            return NotImplemented
+        outs.append(t)
+    dq, dk, dv = outs
+    delta = torch.empty((B, Hh, Lq), dtype=_f32, device=q.device)
+    hs, ds = _seed_args(seed)
+    check(_lib().bigdl_attn_bwd(ptr(q), _ll(q.stride(0)), ptr(k), _ll(k.stride(0)), ptr(v), _ll(v.stride(0)),
+                                ptr(o), _ll(o.stride(0)), ptr(dout), _ll(dout.stride(0)), ptr(lse), ptr(delta),
+                                ptr(bt), *[_ll(x) for x in bs], ptr(dq), _ll(dq.stride(0)), ptr(dk),
+                                _ll(dk.stride(0)), ptr(dv), _ll(dv.stride(0)), C.c_int(B), C.c_int(Hh), C.c_int(Lq),
+                                C.c_int(Lk), C.c_int(D), _f(scale), C.c_int(1 if causal else 0), _f(keep), hs, ds,
+                                _s()), "attn_bwd")
+    return dq, dk, dv

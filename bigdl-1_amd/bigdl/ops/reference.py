@@ -496,3 +496,99 @@ def image_crop_flip_norm(src, oy, ox, flip, out_h, out_w, mean, std, to_rgb, out
     s = torch.tensor(list(std)[:C], dtype=torch.float32, device=src.device)
     t = (t - m) / s
     return t.permute(0, 3, 1, 2).to(out_dtype)
+
+
+# ------------------------------------------------------------------------- attention (K30)
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x, c):
+    """(x · c) mod 2³² for an int64 tensor x ∈ [0, 2³²) (split so no int64 product overflows)."""
+    lo, hi = x & 0xFFFF, x >> 16
+    return (lo * c + (((hi * c) & 0xFFFF) << 16)) & _M32
+
+
+def _amix(x):
+    x = x ^ (x >> 16)
+    x = _mul32(x, 0x7feb352d)
+    x = x ^ (x >> 15)
+    x = _mul32(x, 0x846ca68b)
+    return x ^ (x >> 16)
+
+
+def _seed32(seed):
+    """A host seed, or the device seed snapshot a captured forward used (its low 32 bits)."""
+    if isinstance(seed, torch.Tensor):
+        return int(seed.reshape(-1)[0].item()) & _M32
+    return int(seed) & _M32
+
+
+def attention_dropout_mask(seed, B, Hh, Lq, Lk, keep, device="cpu"):
+    """The attention kernels' dropout keep mask (bool [B, Hh, Lq, Lk]) — the same counter hash as
+    ``attention.hip`` (akeep): bit = mix(mix(seed + (b·Hh + h)·c₁) ^ mix(q·c₂ + k)) < keep·2³²."""
+    import numpy as np
+    thr = min(int(float(np.float32(keep)) * 4294967296.0), _M32)
+    bh = torch.arange(B * Hh, dtype=torch.int64, device=device)
+    s = _amix((_seed32(seed) + _mul32(bh, 0x85EBCA77)) & _M32).view(B, Hh, 1, 1)
+    q = torch.arange(Lq, dtype=torch.int64, device=device).view(Lq, 1)
+    k = torch.arange(Lk, dtype=torch.int64, device=device).view(1, Lk)
+    inner = _amix((_mul32(q, 0x9E3779B1) + k) & _M32).view(1, 1, Lq, Lk)
+    return _amix(s ^ inner) < thr
+
+
+def _heads(t, B, L, Hh, D):
+    return acc_float(t[:, :Hh * D]).reshape(B, L, Hh, D).transpose(1, 2)
+
+
+def _attn_probs(q, k, B, Hh, Lq, Lk, D, scale, bias, causal):
+    s = (_heads(q, B, Lq, Hh, D) @ _heads(k, B, Lk, Hh, D).transpose(-1, -2)) * scale
+    if bias is not None:
+        s = s + acc_float(bias)
+    if causal:
+        s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    return s
+
+
+def attention_forward(q, k, v, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0):
+    """Multi-head attention on projection rows (``Attention.scala:30-111``): q [B·Lq][≥Hh·D],
+    k / v [B·Lk][≥Hh·D] with head h at columns h·D; O = (softmax(scale·QKᵀ + bias [causal]) ∘ M /
+    keep)·V with the kernels' dropout mask M when keep < 1.  Returns (o [B·Lq][Hh·D] in q's
+    dtype, lse₂ fp32 [B][Hh][Lq] = log2 Σ exp of the logits)."""
+    s = _attn_probs(q, k, B, Hh, Lq, Lk, D, scale, bias, causal)
+    lse2 = torch.logsumexp(s, -1) / math.log(2.0)
+    p = torch.softmax(s, -1)
+    if keep < 1.0:
+        p = p * attention_dropout_mask(seed, B, Hh, Lq, Lk, keep, s.device).to(p.dtype) / keep
+    o = p @ _heads(v, B, Lk, Hh, D)
+    return o.transpose(1, 2).reshape(B * Lq, Hh * D).to(q.dtype), lse2
+
+
+def attention_backward(dout, q, k, v, o, lse, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0,
+                       dq=None, dk=None, dv=None):
+    """(dq, dk, dv), each [B·L][Hh·D] in q's dtype, of :func:`attention_forward` (recomputed in fp32
+    through autograd; ``o`` / ``lse`` are accepted for signature parity with the kernel).  Given
+    ``dq``/``dk``/``dv`` (e.g. column slices of one fused buffer) receive the results."""
+    qf = _heads(q, B, Lq, Hh, D).detach().requires_grad_(True)
+    kf = _heads(k, B, Lk, Hh, D).detach().requires_grad_(True)
+    vf = _heads(v, B, Lk, Hh, D).detach().requires_grad_(True)
+    with torch.enable_grad():
+        s = (qf @ kf.transpose(-1, -2)) * scale
+        if bias is not None:
+            s = s + acc_float(bias)
+        if causal:
+            s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+        p = torch.softmax(s, -1)
+        if keep < 1.0:
+            p = p * attention_dropout_mask(seed, B, Hh, Lq, Lk, keep, s.device).to(p.dtype) / keep
+        out = p @ vf
+    g = _heads(dout, B, Lq, Hh, D)
+    dq_out, dk_out, dv_out = dq, dk, dv
+    dq, dk, dv = torch.autograd.grad(out, (qf, kf, vf), g)
+    res = []
+    for t, L, dst in ((dq, Lq, dq_out), (dk, Lk, dk_out), (dv, Lk, dv_out)):
+        r = t.transpose(1, 2).reshape(B * L, Hh * D).to(q.dtype)
+        if dst is not None:
+            dst.copy_(r)
+            r = dst
+        res.append(r)
+    return tuple(res)

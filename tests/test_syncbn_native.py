@@ -95,12 +95,29 @@ def test_syncbn_world1_matches_local_bn_and_runs_native():
     for u, v in zip(eb, ea):  # running statistics
         torch.testing.assert_close(u, v, rtol=1e-3, atol=1e-4)
     # no torch elementwise kernels in the SyncBN forward/backward
-    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
-        b.zeroGradParameters()
-        y = b.forward(x)
-        b.backward(x, gy)
-        torch.cuda.synchronize()
+    import traceback
+    sites = []  # where a torch add ran (named in the failure message)
+    orig = {n: getattr(torch.Tensor, n) for n in ("add_", "add", "__add__", "__iadd__")}
+
+    def _spy(n):
+        def f(self, *a, **k):
+            if self.is_cuda:
+                sites.append(n + " @ " + " <- ".join(
+                    f"{fs.name}:{fs.lineno}" for fs in traceback.extract_stack(limit=6)[:-1]))
+            return orig[n](self, *a, **k)
+        return f
+    for n in orig:
+        setattr(torch.Tensor, n, _spy(n))
+    try:
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+            b.zeroGradParameters()
+            y = b.forward(x)
+            b.backward(x, gy)
+            torch.cuda.synchronize()
+    finally:
+        for n, f in orig.items():
+            setattr(torch.Tensor, n, f)
     names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
     torch_kernels = sorted(n for n in names if "at::native" in n and "Fill" not in n)
-    assert not torch_kernels, torch_kernels
+    assert not torch_kernels, (torch_kernels, sites)
     assert any("k_bn_sum_rows" in n for n in names), sorted(names)
