@@ -344,6 +344,245 @@ BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const vo
 }
 
 // ------------------------------------------------------------------------------------------------
+// Persistent whole-sequence LSTM (small batch, H ≤ 256): ONE workgroup of 16 waves runs every time
+// step of a layer-direction, so a PTB-shape layer (B 20, H 200, T 20) is one launch instead of T.
+// The recurrent state never leaves the CU between steps: h_{t-1} (forward) / dg_{t+1} (backward)
+// sits in an LDS double buffer (the step writes the other buffer; one barrier per step), c / dc
+// live in the registers of the lane that owns the (row, unit quad), and only the U fragments are
+// re-read from L2 each step (U is L2-resident: 4H·H bf16).  Wave w owns unit tile w (16 units ×
+// 4 gates as MFMA rows, the batch rows as MFMA columns — the tiling of k_rnn_step, whose epilogue
+// math this reuses) and all ⌈B/16⌉ batch tiles, so a U fragment feeds NBT MFMAs.  No inter-
+// workgroup communication: nothing to spin on, nothing placement-dependent.
+// ------------------------------------------------------------------------------------------------
+struct LstmSeqP {
+  const void* x2;  // [B][T][4H] input projection (bf16, or fp32 when x_f32)
+  int x_f32;
+  const bf16_t* h0;  // [B][H]
+  const float* c0;   // [B][H] or null
+  const bf16_t* u;   // forward: U [4H][H]; backward: Uᵀ [H][4H]
+  bf16_t* out;       // [B][T][H]
+  float* cs;         // [T][B][H] (training saves; null = inference)
+  float* acts;       // [T][B][4H]
+  float* tcs;        // [T][B][H]
+  float* cbuf;       // inference: c ping-pong [2][B][H]
+  const bf16_t* gy;  // backward: [B][T][H]
+  bf16_t* dg;        // backward: [B][T][4H]
+  float* gc;         // backward: dc of step 0 → [B][H]
+  int B, T, H;
+};
+
+constexpr int kPersistMaxH = 256;
+
+template <int NBT>
+__global__ void __launch_bounds__(1024) k_lstm_seq_fwd_p(LstmSeqP p) {
+  constexpr int LDH = kPersistMaxH + 8;  // padded LDS row (elements)
+  __shared__ __attribute__((aligned(16))) bf16_t hs[2][NBT * 16 * LDH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int j = w * 16 + fq * 4;                 // this lane's unit quad
+  const bool jin = j < H;
+  const bool urow = w * 16 + fr < H;             // this lane's U row (A operand) exists
+  const int KC = (H + 31) / 32;
+  for (int i = tid; i < 2 * NBT * 16 * LDH; i += 1024) (&hs[0][0])[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < B * H; i += 1024) hs[0][(i / H) * LDH + i % H] = p.h0[i];
+  float c[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int m = bt * 16 + fr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[bt][e] = (p.c0 && m < B && jin) ? p.c0[(long long)m * H + j + e] : 0.f;
+  }
+  __syncthreads();
+  const bf16_t* ub = p.u + (long long)(urow ? w * 16 + fr : 0) * H;
+  const long long gstride = (long long)H * H;
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int t = 0; t < T; ++t) {
+    const bf16_t* hc = hs[t & 1];
+    bf16_t* hn = hs[(t + 1) & 1];
+    if (w * 16 < H) {
+      // epilogue operands first (bf16 x2: raw 8-B quads, 2 VGPRs each), so their latency hides under
+      // the MFMA chain; an fp32 x2 is read in the epilogue
+      uint2 xr[NBT][4];
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          xr[bt][g] = (!p.x_f32 && m < B && jin)
+                          ? *reinterpret_cast<const uint2*>((const bf16_t*)p.x2 + ((long long)m * T + t) * G + g * H + j)
+                          : make_uint2(0u, 0u);
+      }
+      v4f acc[NBT][4];
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[bt][g] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int kc = 0; kc < KC; ++kc) {
+        const int k = kc * 32 + fq * 8;
+        const bool kin = k < H;
+        v8s wf[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) wf[g] = (kin && urow) ? *reinterpret_cast<const v8s*>(ub + g * gstride + k) : zero;
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) {
+          const v8s hf = kin ? *reinterpret_cast<const v8s*>(&hc[(bt * 16 + fr) * LDH + k]) : zero;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[bt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[g], hf, acc[bt][g], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        if (m >= B || !jin) continue;
+        float xg[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (p.x_f32) {
+            ld4(p.x2, 1, ((long long)m * T + t) * G + g * H + j, xg[g]);
+          } else {
+            xg[g][0] = __uint_as_float(xr[bt][g].x << 16);
+            xg[g][1] = __uint_as_float(xr[bt][g].x & 0xFFFF0000u);
+            xg[g][2] = __uint_as_float(xr[bt][g].y << 16);
+            xg[g][3] = __uint_as_float(xr[bt][g].y & 0xFFFF0000u);
+          }
+        }
+        float gi[4], gg[4], gf[4], go[4], h[4], tcv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gi[e] = sgm(xg[0][e] + acc[bt][0][e]);
+          gg[e] = tanhf(xg[1][e] + acc[bt][1][e]);
+          gf[e] = sgm(xg[2][e] + acc[bt][2][e]);
+          go[e] = sgm(xg[3][e] + acc[bt][3][e]);
+          c[bt][e] = gi[e] * gg[e] + gf[e] * c[bt][e];
+          tcv[e] = tanhf(c[bt][e]);
+          h[e] = go[e] * tcv[e];
+        }
+        stb4(p.out + ((long long)m * T + t) * H + j, h);
+        stb4(&hn[m * LDH + j], h);
+        const long long mh = ((long long)t * B + m) * H + j;
+        if (p.cs) {
+          stf4(p.cs + mh, c[bt]);
+          stf4(p.tcs + mh, tcv);
+          float* a = p.acts + ((long long)t * B + m) * G + j;
+          stf4(a, gi);
+          stf4(a + H, gg);
+          stf4(a + 2 * H, gf);
+          stf4(a + 3 * H, go);
+        } else if (p.cbuf) {
+          stf4(p.cbuf + (long long)(t & 1) * B * H + (long long)m * H + j, c[bt]);
+        }
+      }
+    }
+    __syncthreads();  // h_t complete in LDS; every read of h_{t-1} retired
+  }
+}
+
+template <int NBT>
+__global__ void __launch_bounds__(1024) k_lstm_seq_bwd_p(LstmSeqP p) {
+  constexpr int LDG = 4 * kPersistMaxH + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t gs[2][NBT * 16 * LDG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int j = w * 16 + fq * 4;
+  const bool jin = j < H;
+  const bool urow = w * 16 + fr < H;
+  const int KC = (G + 31) / 32;
+  for (int i = tid; i < 2 * NBT * 16 * LDG; i += 1024) (&gs[0][0])[i] = 0;
+  __syncthreads();
+  float dc[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dc[bt][e] = 0.f;
+  const bf16_t* ub = p.u + (long long)(urow ? w * 16 + fr : 0) * G;  // Uᵀ row j: Σ_k dg[k]·U[k][j]
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int t = T - 1; t >= 0; --t) {
+    const bf16_t* gc_ = gs[t & 1];  // dg_{t+1} (zero at the last step)
+    bf16_t* gn = gs[(t + 1) & 1];
+    if (w * 16 < H) {
+      float pre[NBT][7][4];  // gy, act i, g, f, o, tanh(c), c_prev
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        if (m < B && jin) {
+          ld4(p.gy, 0, ((long long)m * T + t) * H + j, pre[bt][0]);
+          const float* a = p.acts + ((long long)t * B + m) * G + j;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) ldf4(a + g * H, pre[bt][1 + g]);
+          ldf4(p.tcs + ((long long)t * B + m) * H + j, pre[bt][5]);
+          ldf4(t > 0 ? p.cs + ((long long)(t - 1) * B + m) * H + j : (p.c0 ? p.c0 + (long long)m * H + j : nullptr),
+               pre[bt][6]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 7; ++q) pre[bt][q][0] = pre[bt][q][1] = pre[bt][q][2] = pre[bt][q][3] = 0.f;
+        }
+      }
+      v4f acc[NBT];
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) acc[bt] = v4f{0.f, 0.f, 0.f, 0.f};
+      if (t + 1 < T) {
+#pragma unroll 4
+        for (int kc = 0; kc < KC; ++kc) {
+          const int k = kc * 32 + fq * 8;
+          const bool kin = k < G;
+          const v8s wf = (kin && urow) ? *reinterpret_cast<const v8s*>(ub + k) : zero;
+#pragma unroll
+          for (int bt = 0; bt < NBT; ++bt) {
+            const v8s gf = kin ? *reinterpret_cast<const v8s*>(&gc_[(bt * 16 + fr) * LDG + k]) : zero;
+            acc[bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, gf, acc[bt], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        if (m >= B || !jin) continue;
+        float di[4], dgg[4], df[4], dout[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float i = pre[bt][1][e], g = pre[bt][2][e], f = pre[bt][3][e], o = pre[bt][4][e], tcv = pre[bt][5][e];
+          const float d_h = pre[bt][0][e] + acc[bt][e];
+          const float d_c = d_h * o * (1.f - tcv * tcv) + dc[bt][e];
+          di[e] = d_c * g * i * (1.f - i);
+          dgg[e] = d_c * i * (1.f - g * g);
+          df[e] = d_c * pre[bt][6][e] * f * (1.f - f);
+          dout[e] = d_h * tcv * o * (1.f - o);
+          dc[bt][e] = d_c * f;
+        }
+        bf16_t* o = p.dg + ((long long)m * T + t) * G + j;
+        stb4(o, di);
+        stb4(o + H, dgg);
+        stb4(o + 2 * H, df);
+        stb4(o + 3 * H, dout);
+        bf16_t* l = &gn[m * LDG + j];
+        stb4(l, di);
+        stb4(l + H, dgg);
+        stb4(l + 2 * H, df);
+        stb4(l + 3 * H, dout);
+      }
+    }
+    __syncthreads();
+  }
+  if (w * 16 < H) {
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m < B && jin) stf4(p.gc + (long long)m * H + j, dc[bt]);
+    }
+  }
+}
+
+// The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0); BIGDL_RNN_PERSIST=0 forces the
+// per-step launches (A/B).
+static bool lstm_persist_ok(int B, int H) {
+  const char* e = getenv("BIGDL_RNN_PERSIST");
+  if (e && e[0] == '0') return false;
+  return B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Whole-sequence launchers: the time loop runs on the host in C++, one validated rnn_step launch
 // per step — the Python side makes ONE call per layer per direction (the eager PTB step was bound
 // by per-step Python/ctypes dispatch, not by the GPU).  Layouts (elements, bf16 unless noted):
@@ -360,6 +599,19 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
   if (!train && !cbuf) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
   const int esz = x_f32 ? 4 : 2;
+  if (lstm_persist_ok(B, H)) {
+    if (!a16(U) || !a8(h0) || !a8(out) || (x_f32 ? !a16(x2) : !a8(x2))) return (int)hipErrorInvalidValue;
+    const void* f32s[] = {c0, cs, acts, tcs, cbuf};
+    for (const void* q : f32s)
+      if (q && !a16(q)) return (int)hipErrorInvalidValue;
+    LstmSeqP p{};
+    p.x2 = x2; p.x_f32 = x_f32; p.h0 = (const bf16_t*)h0; p.c0 = c0; p.u = (const bf16_t*)U; p.out = (bf16_t*)out;
+    p.cs = train ? cs : nullptr; p.acts = acts; p.tcs = tcs; p.cbuf = train ? nullptr : cbuf;
+    p.B = B; p.T = T; p.H = H;
+    if (B <= 16) hipLaunchKernelGGL(k_lstm_seq_fwd_p<1>, dim3(1), dim3(1024), 0, s, p);
+    else hipLaunchKernelGGL(k_lstm_seq_fwd_p<2>, dim3(1), dim3(1024), 0, s, p);
+    BIGDL_CHECK_LAUNCH();
+  }
   for (int t = 0; t < T; ++t) {
     const void* a = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
     const long long lda = t == 0 ? H : (long long)T * H;
@@ -379,6 +631,17 @@ BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float*
                                     const float* c0, void* DG, float* gc, int B, int T, int H, hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !gy || !Ut || !DG || !gc) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
+  if (lstm_persist_ok(B, H)) {
+    if (!acts || !tcs || !cs || !a16(Ut) || !a8(gy) || !a8(DG) || !a16(acts) || !a16(tcs) || !a16(cs) || !a16(gc) ||
+        (c0 && !a16(c0)))
+      return (int)hipErrorInvalidValue;
+    LstmSeqP p{};
+    p.u = (const bf16_t*)Ut; p.acts = (float*)acts; p.tcs = (float*)tcs; p.cs = (float*)cs; p.c0 = c0;
+    p.gy = (const bf16_t*)gy; p.dg = (bf16_t*)DG; p.gc = gc; p.B = B; p.T = T; p.H = H;
+    if (B <= 16) hipLaunchKernelGGL(k_lstm_seq_bwd_p<1>, dim3(1), dim3(1024), 0, s, p);
+    else hipLaunchKernelGGL(k_lstm_seq_bwd_p<2>, dim3(1), dim3(1024), 0, s, p);
+    BIGDL_CHECK_LAUNCH();
+  }
   for (int t = T - 1; t >= 0; --t) {
     const bool last = t + 1 == T;
     int rc = bigdl_rnn_step(1, last ? nullptr : bo(DG, (t + 1) * G), (long long)T * G, Ut, B, (int)G, H, nullptr, 0, 0,
