@@ -237,3 +237,56 @@ class DLImageTransformer(_Params):
         return out
 
     _transform = transform
+
+
+class Pipeline:
+    """Spark ML ``Pipeline`` over these stages: ``fit(df)`` runs the stages in order — an estimator
+    (``fit``) is fitted on the DataFrame as transformed so far and its model used as the stage — and
+    returns a :class:`PipelineModel` whose ``transform`` applies every stage (the reference's
+    ImageTransferLearning chains a ``DLModel`` featurizer and a ``DLClassifier``)."""
+
+    def __init__(self, stages=None):
+        self.stages = list(stages or [])
+
+    def setStages(self, stages):
+        self.stages = list(stages)
+        return self
+
+    def getStages(self):
+        return self.stages
+
+    def fit(self, df):
+        fitted = []
+        cur = df
+        for i, st in enumerate(self.stages):
+            if hasattr(st, "fit") and not hasattr(st, "transform"):
+                st = st.fit(cur)
+            fitted.append(st)
+            if i + 1 < len(self.stages):
+                cur = st.transform(cur)
+        return PipelineModel(fitted)
+
+
+class PipelineModel:
+    def __init__(self, stages):
+        self.stages = list(stages)
+
+    def transform(self, df):
+        for st in self.stages:
+            df = st.transform(df)
+        return df
+
+
+def weighted_precision(df, label_col="label", prediction_col="prediction") -> float:
+    """``MulticlassClassificationEvaluator(metricName = "weightedPrecision")``: per-class precision
+    weighted by the class's share of the true labels."""
+    y = np.asarray(df[label_col].tolist(), dtype=np.float64).reshape(-1)
+    p = np.asarray(df[prediction_col].tolist(), dtype=np.float64).reshape(-1)
+    if y.size == 0:
+        return 0.0
+    total = 0.0
+    for c in np.unique(y):
+        predicted = p == c
+        prec = float((predicted & (y == c)).sum() / predicted.sum()) if predicted.any() else 0.0
+        total += prec * float((y == c).sum()) / y.size
+    return total

@@ -142,7 +142,7 @@ class Attention(AutogradModule):
         return self._proj(combine_heads(o), "output")
 
     def _forward(self, input):
-        x, y, b = input[1], input[2], input[3]
+        x, y, b = input[1], input[2], input.get(3)  # the bias input is optional
         if isinstance(b, Table):
             return self._forward_cached(x, y, b[1], b[2])
         return self._attend(self._proj(x, "query"), self._proj(y, "key"), self._proj(y, "value"), b)
@@ -154,7 +154,7 @@ class Attention(AutogradModule):
                 and y.is_cuda and y.dim() == 3 and (b is None or isinstance(b, torch.Tensor)))
 
     def updateOutput(self, input):
-        x, y, b = input[1], input[2], input[3]
+        x, y, b = input[1], input[2], input.get(3)  # the bias input is optional
         if not isinstance(b, Table) and self._nat_ok(x, y, b):
             return self._nat_forward(x, y, b)
         self._nat = None

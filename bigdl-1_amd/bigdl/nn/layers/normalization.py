@@ -325,7 +325,16 @@ class BatchNormalization(TensorModule):
             # native: local [Σg, Σg·(x − μ)] → RCCL all-reduce of 2·C floats → local dγ/dβ and the
             # global input-gradient coefficients → one apply pass
             from ...ops import native_ops as NO
-            both = NO.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=relu)
+            both = NotImplemented
+            pg, self._pending_grad = self._pending_grad, None
+            if pg is not None and pg[0] == gy.data_ptr() and relu:
+                # gy is already ReLU-masked by the consumer conv's dgrad epilogue, which also left
+                # the backward partial sums: reduce those instead of re-reading gy, x, y
+                both = NO.bn_bwd_partials_sums(pg[1], pg[2], x.shape[1], x.device)
+                if both is not NotImplemented:
+                    relu = False
+            if both is NotImplemented:
+                both = NO.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=relu)
             if both is not NotImplemented:
                 C2 = 2 * x.shape[1]
                 loc, glob = both[:C2], both[C2:]

@@ -121,13 +121,19 @@ class InferReshape(TensorModule):
 
 
 class Squeeze(TensorModule):
-    def __init__(self, dim=INTMIN, num_input_dims=INTMIN, bigdl_type="float"):
+    """``batch_mode`` (Squeeze.scala's ``batchMode``): with no ``dim``, squeeze every size-1 dimension
+    except the first (a batch of one keeps its batch dimension)."""
+
+    def __init__(self, dim=INTMIN, num_input_dims=INTMIN, bigdl_type="float", batch_mode=False):
         super().__init__()
         self.dims = None if dim == INTMIN or dim is None else ([dim] if isinstance(dim, int) else list(dim))
         self.numInputDims = None if num_input_dims == INTMIN else num_input_dims
+        self.batchMode = bool(batch_mode)
 
     def updateOutput(self, input):
         if self.dims is None:
+            if self.batchMode and input.dim() > 0:
+                return input.reshape([input.shape[0]] + [s for s in input.shape[1:] if s != 1])
             return input.squeeze()
         y = input
         for d in sorted((_bdim(d, input, self.numInputDims) for d in self.dims), reverse=True):

@@ -37,9 +37,12 @@ class Module:
         return load_caffe_weights(model, def_path, model_path, match_all)
 
     @staticmethod
-    def loadTF(path, inputs, outputs, byte_order="little_endian", bin_file=None):
-        from ..serialization.tf_loader import load_tf
-        return load_tf(path, inputs, outputs, byte_order, bin_file)
+    def loadTF(path, inputs, outputs, byte_order="little_endian", bin_file=None, generated_backward=False):
+        """``Module.loadTF`` (Module.scala:72-86): a TensorFlow GraphDef (binary .pb or text
+        .pbtxt) → BigDL Graph, see :meth:`bigdl.utils.tf.loader.TensorflowLoader.load`."""
+        from ..utils.tf.loader import TensorflowLoader
+        bo = "big" if str(byte_order).lower().startswith("big") else "little"
+        return TensorflowLoader.load(path, list(inputs), list(outputs), bo, bin_file, generated_backward)
 
     @staticmethod
     def flatten(parameters):

@@ -602,11 +602,19 @@ BIGDL_EXPORT int bigdl_bn_stats_sums(const void* x, long long M, int C, const fl
   BIGDL_CHECK_LAUNCH();
 }
 
-// Reduce G partial rows (a conv epilogue's, or any [2][G][C] fp32 block) to out[2C].
+// Reduce G partial rows (a conv epilogue's, or any [2][G][C] fp32 block) to out[2C] (and the same
+// values to out2[2C] when given: the copy an in-place all-reduce turns into the global sums).
 BIGDL_EXPORT int bigdl_bn_partials_sums(const float* partial, int G, int C, float* scratch, float* out,
                                         hipStream_t s) {
   if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
   sum_rows(partial, G, C, scratch, out, s);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_bn_partials_sums2(const float* partial, int G, int C, float* scratch, float* out, float* out2,
+                                         hipStream_t s) {
+  if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
+  sum_rows(partial, G, C, scratch, out, s, out2);
   BIGDL_CHECK_LAUNCH();
 }
 

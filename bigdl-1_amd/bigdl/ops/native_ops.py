@@ -277,6 +277,17 @@ def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
     return out
 
 
+def bn_bwd_partials_sums(partial, G, C_, dev):
+    """[Σg', Σg'·(x − mean)] twice (fp32 [4C]) from the consumer conv's dgrad-epilogue partials
+    (``_pending_grad``): no pass over the activations."""
+    if partial is None or partial.dtype != _f32 or partial.numel() != 2 * G * C_:
+        return NotImplemented
+    out = torch.empty(4 * C_, dtype=_f32, device=dev)
+    check(_lib().bigdl_bn_partials_sums2(ptr(partial), C.c_int(G), C.c_int(C_), ptr(_fold_scratch(G, C_, dev)),
+                                         ptr(out), ptr(out[2 * C_:]), _s()), "bn_partials_sums2")
+    return out
+
+
 def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
                           need_input=True, gg_acc=None, gb_acc=None, scale=1.0):
     """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows → gradInput."""

@@ -87,9 +87,9 @@ class StridedGrad:
         self.t, self.stride, self.shape = t, tuple(stride), tuple(shape)
 
     def dense(self):
-        out = torch.zeros(self.shape, dtype=self.t.dtype, device=self.t.device,
-                          memory_format=torch.channels_last if self.t.is_contiguous(
-                              memory_format=torch.channels_last) else torch.contiguous_format)
+        fmt = torch.channels_last if self.t.is_contiguous(memory_format=torch.channels_last) else \
+            torch.contiguous_format
+        out = torch.empty(self.shape, dtype=self.t.dtype, device=self.t.device, memory_format=fmt).zero_()
         out[:, :, ::self.stride[0], ::self.stride[1]] = self.t
         return out
 

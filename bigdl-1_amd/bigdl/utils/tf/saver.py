@@ -105,7 +105,9 @@ def _emit(w: _GraphDefWriter, m, x):
         acts = {}
         ins = x if isinstance(x, list) else [x]
         for n, v in zip(m.inputs, ins):
-            acts[n._id] = v
+            # an input node is a placeholder (Input()) or a real layer with no predecessor
+            # (``conv1.inputs()`` in Save.scala): the latter is applied to the placeholder
+            acts[n._id] = v if isinstance(n.element, S.Identity) else _emit(w, n.element, v)
         for n in m.forward_order:
             if n._id in acts:
                 continue

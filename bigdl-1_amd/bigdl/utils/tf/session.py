@@ -94,14 +94,36 @@ class Session:
         from .executor import GraphExecutor
         return GraphExecutor(self.nodes, self.byte_order, seed, variables=self.context)
 
-    def get_records(self, end_points: Sequence[str], has_to_batch: bool = True, seed: int = 0):
-        """Every record the graph's input pipeline produces at ``end_points[0]`` (a dequeue node), as
-        Tables (``getRDD``)."""
+    def get_records(self, end_points: Sequence[str], has_to_batch: bool = True, seed: int = 0,
+                    batch_size: Optional[int] = None):
+        """``getRDD`` (BigDLSessionImpl.getRDD): one Table per record.
+
+        * ``end_points[0]`` a dequeue node: the records its input pipeline produces.
+        * otherwise (e.g. a feature layer and the label node of a transfer-learning graph): the
+          records of the data dequeue feeding them are run through the graph ``batch_size`` at a
+          time (default: the dequeue's own batch; a graph with a baked-in batch is filled by
+          cycling records) and the end points' values are split back into per-record Tables."""
+        from ..table import T
         ex = self._executor(seed)
-        recs = ex.records(end_points[0])
-        if not has_to_batch:
-            return recs
-        return recs
+        by = {n.name: n for n in self.nodes}
+        first = by.get(_split_ref(end_points[0])[0])
+        if first is not None and first.op.startswith("QueueDequeue") and len(end_points) == 1:
+            return ex.records(end_points[0])
+        ex.initialize_variables()  # variables without a checkpoint value take their initializers
+        deq = self._data_dequeue(list(end_points))
+        records = ex.records(deq.name)
+        if not records:
+            return []
+        bs = batch_size or len(records)
+        out = []
+        for s in range(0, len(records), bs):
+            real = records[s:s + bs]
+            batch = [records[(s + j) % len(records)] for j in range(bs)]
+            comps = tuple(torch.stack([torch.as_tensor(r[c + 1]) for r in batch]) for c in range(batch[0].length()))
+            vals = ex.run(list(end_points), feeds={deq.name: comps})
+            for j in range(len(real)):
+                out.append(T(*[torch.as_tensor(v)[j] for v in vals]))
+        return out
 
     getRDD = get_records
 

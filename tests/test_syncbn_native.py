@@ -34,6 +34,9 @@ def _block():
     RNG.setSeed(3)
     m = Sequential().add(Convolution(64, 64, 3, 3, 1, 1, 1, 1)).add(Sbn(64)).add(ReLU(True))
     m.add(Convolution(64, 128, 1, 1)).add(Sbn(128))
+    for mod in m.modules:  # the convs' L2 regularizers are torch adds outside the SyncBN path
+        if hasattr(mod, "wRegularizer"):
+            mod.wRegularizer = mod.bRegularizer = None
     with torch.no_grad():
         for mod in m.modules:
             if type(mod).__name__ == "SpatialBatchNormalization":
