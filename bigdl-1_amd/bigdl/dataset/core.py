@@ -191,6 +191,17 @@ class SparseMiniBatch(MiniBatch):
         return int(x.shape[0])
 
 
+def _pad_for(padding: Optional[PaddingParam], i: int) -> Optional[PaddingParam]:
+    """The padding of feature / label ``i``: a PaddingParam whose ``paddingTensor`` is a list holds
+    one padding tensor per feature (``PaddingParam(Some(Array(t1, t2)))``, MiniBatch.scala:528)."""
+    if padding is None or not isinstance(padding.paddingTensor, (list, tuple)):
+        return padding
+    pts = padding.paddingTensor
+    if pts and isinstance(pts[0], (torch.Tensor, list, tuple)) and not all(isinstance(v, (int, float)) for v in pts):
+        return PaddingParam(pts[i] if i < len(pts) else None, padding.fixedLength)
+    return padding
+
+
 def _stack(tensors: List[torch.Tensor], padding: Optional[PaddingParam] = None):
     shapes = {tuple(t.shape) for t in tensors}
     if len(shapes) == 1 and (padding is None or padding.fixedLength is None):
@@ -253,8 +264,8 @@ class SampleToMiniBatch(Transformer):
     def _make(self, buf: List[Sample]) -> MiniBatch:
         nf = buf[0].numFeature()
         nl = buf[0].numLabel()
-        feats = [_stack([s.features[i] for s in buf], self.featurePadding) for i in range(nf)]
-        labs = [_stack([s.labels[i] for s in buf], self.labelPadding) for i in range(nl)]
+        feats = [_stack([s.features[i] for s in buf], _pad_for(self.featurePadding, i)) for i in range(nf)]
+        labs = [_stack([s.labels[i] for s in buf], _pad_for(self.labelPadding, i)) for i in range(nl)]
         inp = feats[0] if nf == 1 else Table(*feats)
         tgt = None if nl == 0 else (labs[0] if nl == 1 else Table(*labs))
         return MiniBatch(inp, tgt)

@@ -7,7 +7,7 @@
 // G gate groups of those units (LSTM: 4 tiles = rows g·H + j of U).  mfma_f32_16x16x32_bf16 with
 // the weight row as the MFMA "A" side leaves, in each lane, the SAME (batch row, 4 consecutive
 // units) for every gate tile — so the cell update runs in registers right after the MFMAs, with no
-// LDS exchange between gates.  The reduction dim is split over the block's 4 waves (the per-step
+// LDS exchange between gates.  The reduction dim is split over the block's 8 waves (the per-step
 // GEMMs are tiny and latency-bound: B·4H·H ≈ 20·800·200) and folded through LDS.  Fragments are
 // read straight from global/L2 (each U row is used by one block only; h rows are L2-resident).
 //
@@ -220,9 +220,14 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
   }
 }
 
+// 8 waves per block split the reduction dim 8 ways: every wave has at most ⌈K/256⌉ fragment loads
+// in flight for the whole step (one L2 round trip instead of up to 7 dependent ones at K = 4H = 800)
+constexpr int kStepWaves = 8;
+
 template <int CELL, int G>
-__global__ void __launch_bounds__(256) k_rnn_step(RnnStep p) {
-  __shared__ v4f red[3][G * 2][64];
+__global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
+  constexpr int NW = kStepWaves;
+  __shared__ v4f red[NW - 1][G * 2][64];
   constexpr int NP = NPre<CELL>::v;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -249,8 +254,8 @@ __global__ void __launch_bounds__(256) k_rnn_step(RnnStep p) {
     const long long gstride = (long long)p.Hs * p.K;
     const int KS = (p.K + 31) / 32;
     const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 2
-    for (int ks = wid; ks < KS; ks += 4) {
+#pragma unroll 4
+    for (int ks = wid; ks < KS; ks += NW) {
       const int k = ks * 32 + fq * 8;
       const bool kin = k < p.K;
       const v8s x0 = (kin && min0) ? *reinterpret_cast<const v8s*>(pa0 + k) : zero;
@@ -274,7 +279,7 @@ __global__ void __launch_bounds__(256) k_rnn_step(RnnStep p) {
     __syncthreads();
     if (wid > 0) return;
 #pragma unroll
-    for (int w = 0; w < 3; ++w)
+    for (int w = 0; w < NW - 1; ++w)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         acc0[g] += red[w][g * 2][lane];
@@ -330,7 +335,7 @@ BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const vo
   p.h_out = (bf16_t*)h_out; p.ldho = ldho; p.c_out = c_out; p.act = act; p.tc = tc; p.gy = (const bf16_t*)gy;
   p.ldgy = ldgy; p.gc_next = gc_next; p.dg = (bf16_t*)dg; p.lddg = lddg; p.dc_prev = dc_prev; p.s0 = s0; p.s1 = s1;
   p.s2 = s2; p.rh = (bf16_t*)rh; p.ldrh = ldrh;
-  dim3 grid((unsigned)((Hs + 15) / 16), (unsigned)((M + 31) / 32)), block(256);
+  dim3 grid((unsigned)((Hs + 15) / 16), (unsigned)((M + 31) / 32)), block(64 * kStepWaves);
   (void)G;
   switch (cell) {
     case 0: hipLaunchKernelGGL((k_rnn_step<0, 4>), grid, block, 0, s, p); break;
@@ -574,11 +579,13 @@ __global__ void __launch_bounds__(1024) k_lstm_seq_bwd_p(LstmSeqP p) {
   }
 }
 
-// The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0); BIGDL_RNN_PERSIST=0 forces the
-// per-step launches (A/B).
+// The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0).  It is OPT-IN
+// (BIGDL_RNN_PERSIST=1): one CU re-streams all of U from L2 every step, and a single CU's L2 read
+// rate (tens of GB/s) makes that ~3× slower than the 13-workgroup step launches at the PTB shape
+// (B 20, H 200: 1.50 vs 1.13 ms per training step, profiles/r3_ptb_persist_ab.txt).
 static bool lstm_persist_ok(int B, int H) {
   const char* e = getenv("BIGDL_RNN_PERSIST");
-  if (e && e[0] == '0') return false;
+  if (!e || e[0] != '1') return false;
   return B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
 }
 
