@@ -145,6 +145,9 @@ class FlatParameters:
         self.slices = slices
         self.shadow: Optional[torch.Tensor] = None
         self.shadow_version = -1
+        #: bumped whenever the shadow's contents change (refresh / optimizer update): caches derived
+        #: from the bf16 weights (the dgrad weight transforms, ops/native_ops.py) key on it
+        self.shadow_gen = 0
         self.buckets = [(0, weight.numel())]
 
     @property
@@ -157,6 +160,9 @@ class FlatParameters:
             for (m, wname, gname, off, n, shape) in self.slices:
                 m._shadow_views[wname] = m._view_param(self.shadow[off:off + n], wname, shape)
                 m._arena = self
+            if self.shadow.is_cuda:
+                from ..ops import native_ops
+                native_ops.register_shadow_arena(self)
         self.refresh_shadow()
 
     def refresh_shadow(self):
@@ -164,9 +170,11 @@ class FlatParameters:
             from .. import ops
             ops.cast_copy(self.shadow, self.weight)
             self.shadow_version = self.weight._version
+            self.shadow_gen += 1
 
     def mark_shadow_fresh(self):
         self.shadow_version = self.weight._version
+        self.shadow_gen += 1
 
     def shadow_is_fresh(self) -> bool:
         return self.shadow is not None and self.shadow_version == self.weight._version

@@ -86,13 +86,18 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
   }
 }
 
-// Parallel reduction of the G per-block partials: a 1024-thread block owns 32 channels; its 32 row
-// groups each sum G/32 partials with coalesced 128-B loads (8 in flight per thread), then a LDS tree.
+// Parallel reduction of the G per-block partials: a block owns 32 channels; its kFinRG row groups
+// each sum G/kFinRG partials with coalesced 128-B loads (8 in flight per thread), then a LDS tree.
 // Results: red[0][c] = Σ partial[0..G), red[1][c] = Σ partial[G..2G) for the block's 32 channels.
 // The sums over partials are fp64: the conv epilogue's partials are unshifted 128-row Σy, Σy², so
 // var = Σy²/M − mean² cancels; summing thousands of partials in double keeps that difference exact
 // to the partials' own fp32 rounding (profiles: a shifted fp32 epilogue cost 11 % of conv-forward
 // time, the fp64 combine costs nothing measurable).
+// 256 threads = 32 channels × kFinRG row groups: small blocks, so a finalize queued behind the
+// side-stream weight-gradient kernels finds a CU with room quickly (1024-thread blocks waited for a
+// CU with 16 free wave slots: ~40 µs per finalize in a contended step, profiles/r3_bench_prof_a.txt)
+constexpr int kFinRG = 8;
+
 template <typename T>
 __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, int G, int C, int c0,
                                                 double (*lds)[2][33], double& outA, double& outB) {
@@ -102,7 +107,7 @@ __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, i
   if (c < C) {
     int i = ty;
 #pragma unroll 8
-    for (; i < G; i += 32) {
+    for (; i < G; i += kFinRG) {
       a += partial[(size_t)i * C + c];
       b += partial[(size_t)(G + i) * C + c];
     }
@@ -110,7 +115,7 @@ __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, i
   lds[ty][0][tx] = a;
   lds[ty][1][tx] = b;
   __syncthreads();
-  for (int s = 16; s > 0; s >>= 1) {
+  for (int s = kFinRG / 2; s > 0; s >>= 1) {
     if (ty < s) {
       lds[ty][0][tx] += lds[ty + s][0][tx];
       lds[ty][1][tx] += lds[ty + s][1][tx];
@@ -125,7 +130,7 @@ __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, i
 // ``in_bias`` (optional) is a per-channel constant the producer did NOT add to x (a conv bias folded
 // into this BN): normalisation is shift-invariant, so only the running mean sees it.
 template <typename T>
-__global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__ x, const float* kshift,
+__global__ void __launch_bounds__(32 * kFinRG) k_bn_finalize(const bf16_t* __restrict__ x, const float* kshift,
                                                       const T* __restrict__ partial,
                                                       int G, long long M, int C, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
@@ -134,7 +139,7 @@ __global__ void __launch_bounds__(1024) k_bn_finalize(const bf16_t* __restrict__
                                                       float momentum, float eps, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
                                                       float* __restrict__ shift) {
-  __shared__ double lds[32][2][33];
+  __shared__ double lds[kFinRG][2][33];
   double s, q;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
@@ -286,7 +291,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train(const void* x, const void* res, void* y, lon
   size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G);
-  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)x, nullptr,
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)x, nullptr,
                      (const float*)ws, G,
                      M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef, coef + C);
   launch_apply(x, res, y, M, C, coef, relu, bits, s);
@@ -351,11 +356,11 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
                                              hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
   if (maybe_fold(partial, G, C, scratch, s))
-    hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
+    hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                        (const double*)scratch, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                        save_invstd, coef, coef + C);
   else
-    hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift,
+    hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                        partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd,
                        coef, coef + C);
   launch_apply(x, res, y, M, C, coef, relu, bits, s);
@@ -440,14 +445,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const bf16_t* __restrict_
 // ``cbias`` (optional): gradient of a producer bias folded into this BN = Σ_rows gx, evaluated from
 // the closed form A·Σg' + B·Σx + M·Cc (Σx = M·mean) and accumulated with ``cbscale``.
 template <typename T>
-__global__ void __launch_bounds__(1024) k_bn_bwd_finalize(const T* __restrict__ partial, int G, long long M,
+__global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __restrict__ partial, int G, long long M,
                                                           int C, const float* __restrict__ gamma,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ ggamma, float* __restrict__ gbeta,
                                                           float gscale, float* __restrict__ cbias, float cbscale,
                                                           float* __restrict__ coef) {
-  __shared__ double lds[32][2][33];
+  __shared__ double lds[kFinRG][2][33];
   double ad, bd;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, ad, bd);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
@@ -522,7 +527,7 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
                        (const bf16_t*)y, M, C, rpb, mean, ws, G);
-  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const float*)ws, G, M, C, gamma,
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)ws, G, M, C, gamma,
                      mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
@@ -545,10 +550,10 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
                                        float* coef, float* scratch, hipStream_t s) {
   if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
   if (maybe_fold(partial, G, C, scratch, s))
-    hipLaunchKernelGGL(k_bn_bwd_finalize<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const double*)scratch, G, M,
+    hipLaunchKernelGGL(k_bn_bwd_finalize<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const double*)scratch, G, M,
                        C, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   else
-    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, M, C, gamma, mean,
+    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, M, C, gamma, mean,
                        invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
@@ -565,9 +570,9 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
 // take the GLOBAL sums (G = 1 row) with the global row count — the same finalize code as the local
 // path, so SyncBN costs two tiny kernels and one 2·C collective per direction.
 template <typename T>
-__global__ void __launch_bounds__(1024) k_bn_sum_rows(const T* __restrict__ partial, int G, int C,
+__global__ void __launch_bounds__(32 * kFinRG) k_bn_sum_rows(const T* __restrict__ partial, int G, int C,
                                                       float* __restrict__ out, float* __restrict__ out2) {
-  __shared__ double lds[32][2][33];
+  __shared__ double lds[kFinRG][2][33];
   double a, b;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
@@ -583,10 +588,10 @@ __global__ void __launch_bounds__(1024) k_bn_sum_rows(const T* __restrict__ part
 static void sum_rows(const float* partial, int G, int C, float* scratch, float* out, hipStream_t s,
                      float* out2 = nullptr) {
   if (maybe_fold(partial, G, C, scratch, s))
-    hipLaunchKernelGGL(k_bn_sum_rows<double>, dim3((C + 31) / 32), dim3(1024), 0, s, (const double*)scratch, G, C, out,
+    hipLaunchKernelGGL(k_bn_sum_rows<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const double*)scratch, G, C, out,
                        out2);
   else
-    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(1024), 0, s, partial, G, C, out, out2);
+    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, C, out, out2);
 }
 
 // Local shifted sums of x (kshift = the running mean, identical on every rank): out[2C].
@@ -626,7 +631,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
                                          float* save_mean, float* save_invstd, const float* sums,
                                          const float* kshift, float* coef, int relu, hipStream_t s) {
   if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, (const bf16_t*)nullptr, kshift, sums,
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift, sums,
                      1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
                      coef + C);
   launch_apply(x, res, y, M, C, coef, relu, nullptr, s);
@@ -661,9 +666,9 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
                                          float* coef_scratch, int relu, hipStream_t s) {
   if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
   if (ggamma || gbeta)
-    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, local_sums, 1, count, C, gamma,
+    hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, local_sums, 1, count, C, gamma,
                        mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch);
-  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(1024), 0, s, global_sums, 1, count, C, gamma,
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, global_sums, 1, count, C, gamma,
                      mean, invstd, (float*)nullptr, (float*)nullptr, 0.f, (float*)nullptr, 0.f, coef);
   if (gx) {
     int grid = apply_grid(M, C);

@@ -703,6 +703,63 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
 
 _SUBFILTER_IDX: dict = {}
 
+# ---- dgrad weight transforms of a whole step in one launch (weight_xform.hip k_w_xform_multi) ----
+# Transforms of weights that live in a parameter arena's bf16 shadow are cached per (weight, class
+# list) with the arena's shadow generation; after an optimizer update the first dgrad refreshes
+# every cached transform of that arena in ONE batched launch instead of one launch per layer.
+_XFC: dict = {}
+_XF_ARENAS: dict = {}   # shadow storage data_ptr → weakref(arena)
+_XF_TABLE: dict = {}    # id(arena) → (device job table, njobs, total blocks, entry list)
+
+
+def register_shadow_arena(arena) -> None:
+    import weakref
+    _XF_ARENAS[arena.shadow.untyped_storage().data_ptr()] = weakref.ref(arena)
+
+
+def _shadow_arena(t):
+    try:
+        sp = t.untyped_storage().data_ptr()
+    except RuntimeError:
+        return None
+    ref = _XF_ARENAS.get(sp)
+    a = ref() if ref is not None else None
+    if a is None or a.shadow is None or a.shadow.untyped_storage().data_ptr() != sp:
+        return None
+    return a
+
+
+def _xf_refresh(arena) -> None:
+    """Re-run every cached dgrad weight transform of ``arena`` in one launch (job table built once,
+    outside HIP-graph capture; without a table, the stale entries are left for per-layer launches)."""
+    entries = [c for c in _XFC.values() if c["arena"] == id(arena)]
+    if not entries:
+        return
+    tab = _XF_TABLE.get(id(arena))
+    if tab is None:
+        if torch.cuda.is_current_stream_capturing():
+            return
+        lib = _lib()
+        rec = int(lib.bigdl_w_xform_job_size())
+        buf = (C.c_ubyte * (rec * len(entries)))()
+        first = 0
+        nb = C.c_longlong(0)
+        for i, c in enumerate(entries):
+            K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off = c["args"]
+            check(lib.bigdl_w_xform_job(C.byref(buf, i * rec), ptr(c["phys"]), ptr(c["out"]), K, R, S, C_, ncls, a_ro,
+                                        a_so, a_rm, a_sm, a_off, C.c_longlong(first), C.byref(nb)), "w_xform_job")
+            first += nb.value
+        host = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+        dev = torch.empty(host.numel() + 16, dtype=torch.uint8, device=entries[0]["out"].device)
+        off = (-dev.data_ptr()) % 16
+        table = dev[off:off + host.numel()]
+        table.copy_(host)
+        tab = _XF_TABLE[id(arena)] = (table, len(entries), first, entries, dev)
+    table, nj, total, ents, _keep = tab
+    check(_lib().bigdl_w_xform_multi(ptr(table), C.c_int(nj), C.c_longlong(total), _s()), "w_xform_multi")
+    for c in ents:
+        c["gen"] = arena.shadow_gen
+
 
 _S1_XFORM = {}  # (K, C, R, S) → the single full-filter class list of a stride-1 dgrad
 
@@ -742,6 +799,15 @@ def _subfilters(w4, classes, gkey=None):
             ent = (n, sum(n), len(ros), IA(*ros), IA(*sos), IA(*rm), IA(*sm), LA(*offs))
             _SUBFILTER_IDX[key] = ent
         n, total, ncls, a_ro, a_so, a_rm, a_sm, a_off = ent
+        arena = _shadow_arena(phys)
+        ck = (phys.data_ptr(), key)
+        if arena is not None:
+            c = _XFC.get(ck)
+            if c is not None:
+                if c["gen"] != arena.shadow_gen:
+                    _xf_refresh(arena)
+                if c["gen"] == arena.shadow_gen:
+                    return c["views"]
         out = torch.empty(total, dtype=_bf16, device=w4.device)
         check(_lib().bigdl_w_dgrad_xform(ptr(phys), ptr(out), K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off, _s()),
               "w_dgrad_xform")
@@ -749,6 +815,10 @@ def _subfilters(w4, classes, gkey=None):
         for (a, b, rs, ss, *_r), ni in zip(classes, n):
             res.append(out[off:off + ni].view(C_, len(rs), len(ss), K) if ni else None)
             off += ni
+        if arena is not None:
+            _XFC[ck] = {"gen": arena.shadow_gen, "out": out, "views": res, "arena": id(arena), "phys": phys,
+                        "args": (K, R, S, C_, ncls, a_ro, a_so, a_rm, a_sm, a_off)}
+            _XF_TABLE.pop(id(arena), None)  # the job table gains an entry
         return res
     key = (K, C_, R, S, tuple((a, b, tuple(rs), tuple(ss)) for (a, b, rs, ss, *_r) in classes), w4.device)
     ent = _SUBFILTER_IDX.get(key)

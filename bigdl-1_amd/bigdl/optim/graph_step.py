@@ -87,6 +87,9 @@ class GraphedTrainStep:
         ts, states = snap
         for t, c in ts:
             t.copy_(c)
+        flat = getattr(self.opt, "flat", None)
+        if flat is not None and hasattr(flat, "shadow_gen"):
+            flat.shadow_gen += 1  # the shadow changed under the weight-derived caches
         for name, meth in self.opt.optim_methods.items():
             pre = states[name]
             fresh = []
