@@ -577,12 +577,23 @@ class VolumetricConvolution(AutogradModule):
         if not batched:
             x = x.unsqueeze(0)
         pad = self.p
+        pads = None
         if self.p[1] == -1:
             pads = []
             for dim, k, s in zip(x.shape[2:], self.k, self.d):
                 o = math.ceil(dim / s)
                 tot = max((o - 1) * s + k - dim, 0)
                 pads.append((tot // 2, tot - tot // 2))
+        if x.is_cuda and ops.native_has("conv2d_forward") and Engine.compute_dtype() == torch.bfloat16:
+            # implicit-GEMM 3-D conv (conv_igemm.hip D3): SAME padding is the leading pad + output size
+            lead = tuple(p_[0] for p_ in pads) if pads else pad
+            outd = tuple(math.ceil(dim / s) for dim, s in zip(x.shape[2:], self.d)) if pads else None
+            y = ops.native_ops.conv3d_autograd(x, self.P("weight"), self.P("bias") if self.withBias else None,
+                                               self.d, lead, (1, 1, 1), outd)
+            if y is not NotImplemented:
+                return y if batched else y.squeeze(0)
+            ops.native.note_fallback("volumetric_conv", "geometry", (x,))
+        if pads:
             x = F.pad(x, (pads[2][0], pads[2][1], pads[1][0], pads[1][1], pads[0][0], pads[0][1]))
             pad = (0, 0, 0)
         y = F.conv3d(x, self.P("weight").to(x.dtype), self.P("bias").to(x.dtype) if self.withBias else None, self.d,

@@ -52,6 +52,7 @@ class BatchNormalization(TensorModule):
         self._fused_relu = False
         self._sync_group = None
         self._sync = False
+        self._sync_force = False
         self.reset()
 
     def reset(self):
@@ -72,10 +73,16 @@ class BatchNormalization(TensorModule):
         self._sync = parallism is not None and parallism > 1
         return self
 
-    def set_sync_group(self, group=None, enabled: bool = True):
+    def set_sync_group(self, group=None, enabled: bool = True, force: bool = False):
+        """Cross-rank statistics over ``group``; ``force`` keeps the collective path even when the
+        group has a single rank (a world-size-1 rehearsal of the multi-rank kernels)."""
         self._sync = enabled
         self._sync_group = group
+        self._sync_force = force
         return self
+
+    def _sync_active(self):
+        return self._sync and _dist_ready(self._sync_force)
 
     def _to_nchw_like(self, x):
         return x
@@ -152,7 +159,7 @@ class BatchNormalization(TensorModule):
         ib = self._in_bias()
         self._last_relu = relu
         if self.train:
-            if self._sync and _dist_ready():
+            if self._sync_active():
                 y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib)
             else:
                 r = NotImplemented
@@ -273,7 +280,7 @@ class BatchNormalization(TensorModule):
         cb = prod.gradBias if (acc and prod is not None and getattr(prod, "withBias", False)) else None
         cbs = prod.scale_b if prod is not None else 0.0
         gres = None
-        if self._sync and _dist_ready() and self.train:
+        if self._sync_active() and self.train:
             gi = self._sync_backward(x, gy, g, y, need_input, acc, relu)
             if cb is not None and gi is not None:
                 cb.add_(acc_float(gi).sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
@@ -424,9 +431,9 @@ class SpatialBatchNormalization(BatchNormalization):
         super().accGradParameters(input, gradOutput)
 
 
-def _dist_ready():
+def _dist_ready(single_rank_ok=False):
     import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (single_rank_ok or dist.get_world_size() > 1)
 
 
 class SpatialCrossMapLRN(TensorModule):

@@ -72,6 +72,10 @@ struct ConvParams {
   // stride-s shortcut conv); every other pixel's residual is zero — the dense zero-filled copy is
   // never materialised
   int res_sh, res_sw, res_H, res_W;
+  // 3-D convolution (VolumetricConvolution, D3 instantiations only): input depth T, filter depth
+  // KT, depth stride / pad / dilation, output depth To; x is [Nb][T][H][W][C], w [K][KT][R][S][C],
+  // y [Nb][To][P][Q][K] (M = Nb·To·P·Q).  2-D launches leave T = KT = To = 1.
+  int T, KT, st, pt, dtd, To;
 };
 
 // Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
@@ -117,8 +121,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // loads with their own padding tests.  MODE 0: any C % 8 == 0.  MODE 3 (POINTWISE): a 1×1
 // filter with no padding (C % BK == 0) — every staged row is in bounds, the k-tile is a plain
 // channel offset, no tap mask at all (the bottleneck 1×1 convs and their dgrads, half the FLOPs).
-template <int BN, int MODE, int BM, int BK>
+template <int BN, int MODE, int BM, int BK, bool D3 = false>
 __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_conv_fwd(ConvParams p) {
+  static_assert(!D3 || MODE == 0 || MODE == 1, "3-D: generic or tap-uniform gather only");
   constexpr bool PW = MODE == 3;
   constexpr bool FAST = MODE == 1 || PW;
   constexpr int ROWS = BM + BN;
@@ -143,7 +148,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // for an out-of-range offset, so conv padding, the M / K tails and the channel tail need no
   // branches (a per-element "load or zero" select makes hipcc branch and drain vmcnt per load,
   // cdna_hip_programming.md §5 item 4(c)).  OOB = an offset past the end of the tensor.
-  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C * 2);
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.C * 2);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw * 2);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
@@ -151,11 +156,13 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 
   // per-row gather state for the activation rows this thread stages
   int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
+  int a_t[D3 ? A_CHUNKS : 1];  // 3-D: first input frame of the row's window (may be < 0: padding)
   // a pointwise stride-1 conv reads input pixel m for output pixel m: skip the (n, p, q) split
   const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
 #pragma unroll
   for (int i = 0; i < A_CHUNKS; ++i) {
     int m = m0 + tid / CPK + RPS * i;
+    if constexpr (D3) a_t[i] = -(1 << 28);
     if (pw_direct) {
       a_img[i] = m < p.M ? m : -1;
       a_h[i] = 0;
@@ -164,7 +171,14 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       int n = m / (p.P * p.Q);
       int pq = m - n * p.P * p.Q;
       int pp = pq / p.Q, qq = pq - pp * p.Q;
-      a_img[i] = n * p.H * p.W;
+      if constexpr (D3) {
+        const int img = n;  // (sample, output frame)
+        n = img / p.To;
+        a_t[i] = (img - n * p.To) * p.st - p.pt;
+        a_img[i] = n * p.T * p.H * p.W;
+      } else {
+        a_img[i] = n * p.H * p.W;
+      }
       a_h[i] = pp * p.sh - p.ph;
       a_w[i] = qq * p.sw - p.pw;
     } else {
@@ -188,17 +202,23 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   if constexpr (FAST) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.C) + col8 * 8;
+      if constexpr (D3) rbase[i] = ((a_img[i] + (a_t[i] * p.H + a_h[i]) * p.W + a_w[i]) * p.C) + col8 * 8;
+      else rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.C) + col8 * 8;
       uint64_t msk = 0;
       if (PW) {
         msk = a_img[i] >= 0 ? 1ull : 0ull;
       } else if (a_img[i] >= 0) {
-        for (int r = 0; r < p.R; ++r) {
-          const int h = a_h[i] + r * p.dh;
-          if ((unsigned)h >= (unsigned)p.H) continue;
-          for (int sx = 0; sx < p.S; ++sx) {
-            const int w = a_w[i] + sx * p.dw;
-            if ((unsigned)w < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
+        for (int d = 0; d < (D3 ? p.KT : 1); ++d) {
+          if constexpr (D3) {
+            if ((unsigned)(a_t[i] + d * p.dtd) >= (unsigned)p.T) continue;
+          }
+          for (int r = 0; r < p.R; ++r) {
+            const int h = a_h[i] + r * p.dh;
+            if ((unsigned)h >= (unsigned)p.H) continue;
+            for (int sx = 0; sx < p.S; ++sx) {
+              const int w = a_w[i] + sx * p.dw;
+              if ((unsigned)w < (unsigned)p.W) msk |= 1ull << ((d * p.R + r) * p.S + sx);
+            }
           }
         }
       }
@@ -213,6 +233,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // increasing order, so the (tap, channel) position advances by BK per live call instead of two
   // scalar divisions per k-tile (the round-1 PMC showed ~2.5 SALU per MFMA from them).
   int it_c0 = 0, it_s = 0, it_tap = 0, it_off = 0;  // channel in tap, s, tap index, element offset
+  int it_r = 0;                                       // 3-D: filter row inside the depth tap
   auto load_tile = [&](int kt, bool live, uint4 (&ra)[A_CHUNKS], uint4 (&rb)[B_CHUNKS]) {
     const uint32_t dead = live ? 0u : 0x80000000u;
     if constexpr (FAST) {
@@ -226,7 +247,12 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
           ++it_tap;
           if (++it_s == p.S) {
             it_s = 0;
-            it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+            if (D3 && ++it_r == p.R) {  // next depth tap: back to row 0, column 0, one frame on
+              it_r = 0;
+              it_off += (p.dtd * p.H * p.W - (p.R - 1) * p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+            } else {
+              it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+            }
           } else {
             it_off += p.dw * p.C;
           }
@@ -270,19 +296,29 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       }
     } else {
       const int k = kt * BK + col8 * 8;
-      int tap = 0, c = k, r = 0, sx = 0;
+      int tap = 0, c = k, r = 0, sx = 0, d = 0;
       const bool kin = live && k < p.Kg;
       if (kin) {
         tap = k / p.C;
         c = k - tap * p.C;
+        if constexpr (D3) {
+          d = tap / (p.R * p.S);
+          tap -= d * p.R * p.S;
+        }
         r = tap / p.S;
         sx = tap - r * p.S;
       }
 #pragma unroll
       for (int i = 0; i < A_CHUNKS; ++i) {
         const int h = a_h[i] + r * p.dh, w = a_w[i] + sx * p.dw;
-        const bool ok = kin && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
-        const uint32_t off = ok ? (uint32_t)((a_img[i] + h * p.W + w) * p.C + c) * 2u : OOB;
+        bool ok = kin && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+        int pix = a_img[i] + h * p.W + w;
+        if constexpr (D3) {
+          const int tt = a_t[i] + d * p.dtd;
+          ok = ok && (unsigned)tt < (unsigned)p.T;
+          pix += tt * p.H * p.W;
+        }
+        const uint32_t off = ok ? (uint32_t)(pix * p.C + c) * 2u : OOB;
         ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
       }
 #pragma unroll
@@ -675,6 +711,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * ldw * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
   ConvParams p{};  // value-initialised: a field a launcher forgets is null / 0, never stack garbage
+  p.T = p.KT = p.st = p.dtd = p.To = 1;
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)w;
   p.bias = bias;
@@ -766,6 +803,52 @@ BIGDL_EXPORT int bigdl_conv_fwd_full2(const void* x, const void* w, const void* 
   return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
                          0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
                          bn_bits);
+}
+
+// 3-D convolution (VolumetricConvolution.scala) on the same implicit-GEMM kernel: x [Nb][T][H][W][C],
+// w [K][KT][R][S][C], y [Nb][To][P][Q][K] (+ fp32 bias, ReLU).  C % 8 == 0.
+BIGDL_EXPORT int bigdl_conv3d_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int T, int H, int W,
+                                  int C, int K, int KT, int R, int S, int To, int P, int Q, int st, int sh, int sw,
+                                  int pt, int ph, int pw, int dtd, int dh, int dw, int relu, hipStream_t s) {
+  if (C % 8 || Nb <= 0 || K <= 0 || T <= 0 || KT <= 0 || To <= 0 || st <= 0 || dtd <= 0 || R <= 0 || S <= 0)
+    return (int)hipErrorInvalidValue;
+  if (P <= 0 || Q <= 0) return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * T * H * W * C * 2 >= 0x80000000ull || (size_t)K * KT * R * S * C * 2 >= 0x80000000ull ||
+      (size_t)Nb * To * P * Q * K * 2 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15)) return (int)hipErrorInvalidValue;
+  ConvParams p{};
+  p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.bias = bias; p.y = (bf16_t*)y;
+  p.Nb = Nb;  // samples; the kernel's row split yields (sample, output frame) pairs from M / (P·Q)
+  p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.T = T; p.KT = KT; p.st = st; p.pt = pt; p.dtd = dtd; p.To = To;
+  const long long Ml = (long long)Nb * To * P * Q;
+  if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  p.M = (int)Ml;
+  p.Kg = KT * R * S * C;
+  p.ldw = p.Kg;
+  p.ldy = K;
+  p.relu = relu;
+  p.osh = p.osw = 1; p.oH = P; p.oW = Q;
+  const int BN = K <= 64 ? 64 : 128;
+  p.tiles_n = (K + BN - 1) / BN;
+  p.tiles_m = (p.M + SBM - 1) / SBM;
+  const int bk = p.Kg <= 512 ? 32 : 64;
+  const bool fast = C % bk == 0 && KT * R * S <= 64;  // the tap-uniform gather keeps a 64-bit tap mask
+  const long long tiles = (long long)((p.M + 127) / 128) * p.tiles_n;
+  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)tiles);
+#define BIGDL_C3(BN_, MODE_, BK_) hipLaunchKernelGGL((k_conv_fwd<BN_, MODE_, 128, BK_, true>), g, dim3(256), 0, s, p)
+  if (bk == 32) {
+    if (fast) { if (BN == 64) BIGDL_C3(64, 1, 32); else BIGDL_C3(128, 1, 32); }
+    else { if (BN == 64) BIGDL_C3(64, 0, 32); else BIGDL_C3(128, 0, 32); }
+  } else {
+    if (fast) { if (BN == 64) BIGDL_C3(64, 1, 64); else BIGDL_C3(128, 1, 64); }
+    else { if (BN == 64) BIGDL_C3(64, 0, 64); else BIGDL_C3(128, 0, 64); }
+  }
+#undef BIGDL_C3
+  BIGDL_CHECK_LAUNCH();
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).

@@ -43,6 +43,9 @@ struct WgradParams {
   int Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw_;
   int M, Kg, tiles_k, tiles_n, m_per_split;
   FastDiv fPQ, fQ;
+  // 3-D (D3 instantiations): x [Nb][T][H][W][C], dy [Nb][To][P][Q][K], dw [K][KT][R][S][C]
+  int T, KT, st, pt, dtd, To;
+  FastDiv fRS, fTo;
 };
 
 constexpr int BP = 64;  // split granularity (pixels); the k-tile depth BPT is 64 or 32
@@ -61,8 +64,9 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 
 // C4: 4-channel input (RGB stem padded 3 → 4): an X̂ chunk of 8 k-values is two consecutive taps,
 // gathered as two 8-B loads with separate padding tests (see conv_igemm.hip MODE 2).
-template <int TILE_N, int TILE_K, int BPT, bool C4 = false>
+template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false>
 __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradParams p) {
+  static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
   constexpr int DY_CH = BPT * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
   constexpr int X_CH = BPT * TILE_K / 8 / 256;   // for the X̂ tile
   constexpr int TMN = TILE_N / 32;              // MFMA tiles per wave along n
@@ -95,6 +99,11 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   const bool kx_ok = kx < p.Kg;
   int tap = kx_ok ? kx / p.C : 0;
   const int cx = kx - tap * p.C;
+  int dx = 0;  // 3-D: depth tap of this column
+  if constexpr (D3) {
+    dx = (int)fdiv((uint32_t)tap, p.fRS);
+    tap -= dx * p.R * p.S;
+  }
   const int rx = tap / p.S, sx = tap - (tap / p.S) * p.S;
   // C4: the chunk's second tap (tap + 1, wrapping to the next filter row)
   const bool kx1_ok = kx + 4 < p.Kg;
@@ -106,7 +115,7 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   // Raw buffer loads (OOB offsets → zeros, no branches) into two register sets; tile t+2 is
   // requested while tile t is multiplied (loads always issued — beyond the range with a dead
   // offset — so hipcc's vmcnt counts stay exact; see conv_igemm.hip).
-  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C * 2);
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.C * 2);
   const uint32_t dy_bytes = (uint32_t)((size_t)p.M * p.K * 2);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)dy_bytes, 0x00020000);
@@ -125,13 +134,20 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
     for (int i = 0; i < X_CH; ++i) {
       const int m = mt + x_row0 + i * X_RSTEP;
       const uint32_t mm = (uint32_t)(m < mend ? m : mbeg);
-      const uint32_t n = fdiv(mm, p.fPQ);
+      uint32_t n = fdiv(mm, p.fPQ);
       const uint32_t pq = mm - n * (uint32_t)(p.P * p.Q);
       const uint32_t pp = fdiv(pq, p.fQ);
       const uint32_t q = pq - pp * (uint32_t)p.Q;
       const int h = (int)pp * p.sh - p.ph + rx * p.dh;
       const int w = (int)q * p.sw - p.pw + sx * p.dw_;
-      const bool ok = kx_ok && m < mend && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+      bool ok = kx_ok && m < mend && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+      const uint32_t pq_n = n;
+      if constexpr (D3) {  // n = (sample, output frame) → input frame plane index sample·T + t
+        const uint32_t ns = fdiv(pq_n, p.fTo);
+        const int tt = (int)(pq_n - ns * (uint32_t)p.To) * p.st - p.pt + dx * p.dtd;
+        ok = ok && (unsigned)tt < (unsigned)p.T;
+        n = ns * (uint32_t)p.T + (uint32_t)(tt < 0 ? 0 : tt);
+      }
       if constexpr (C4) {
         const int h1 = (int)pp * p.sh - p.ph + rx1, w1 = (int)q * p.sw - p.pw + sx1;
         const bool ok1 = kx1_ok && m < mend && (unsigned)h1 < (unsigned)p.H && (unsigned)w1 < (unsigned)p.W;
@@ -233,6 +249,44 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
       }
     }
   }
+}
+
+// 3-D weight gradient (VolumetricConvolution.scala accGradParameters): dw [K][KT][R][S][C] +=
+// scale · Σ x̂ᵀ·dy over (sample, output frame, p, q).  C % 8 == 0, K % 8 == 0.
+BIGDL_EXPORT int bigdl_conv3d_wgrad(const void* x, const void* dy, float* dw, float scale, int Nb, int T, int H, int W,
+                                    int C, int K, int KT, int R, int S, int To, int P, int Q, int st, int sh, int sw,
+                                    int pt, int ph, int pw, int dtd, int dh, int dwd, hipStream_t s) {
+  if (C % 8 || K % 8 || Nb <= 0 || T <= 0 || To <= 0 || KT <= 0 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * T * H * W * C * 2 >= 0x80000000ull || (size_t)Nb * To * P * Q * K * 2 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15)) return (int)hipErrorInvalidValue;
+  WgradParams p{};
+  p.x = (const bf16_t*)x; p.dy = (const bf16_t*)dy; p.dw = dw; p.scale = scale;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw_ = dwd;
+  p.T = T; p.KT = KT; p.st = st; p.pt = pt; p.dtd = dtd; p.To = To;
+  p.M = Nb * To * P * Q;
+  p.Kg = KT * R * S * C;
+  p.fPQ = make_fastdiv((uint32_t)(P * Q));
+  p.fQ = make_fastdiv((uint32_t)Q);
+  p.fRS = make_fastdiv((uint32_t)(R * S));
+  p.fTo = make_fastdiv((uint32_t)To);
+  const int TN = K <= 64 ? 64 : 128;
+  p.tiles_n = (K + TN - 1) / TN;
+  p.tiles_k = (p.Kg + 127) / 128;
+  const int tiles = p.tiles_n * p.tiles_k;
+  long long splits = g_bigdl_deterministic ? 1 : (512 + tiles - 1) / tiles;
+  const long long max_by_work = (p.M + 8 * BP - 1) / (8 * BP);
+  if (splits > max_by_work) splits = max_by_work;
+  if (splits < 1) splits = 1;
+  if (splits > 65535) splits = 65535;
+  int mps = (int)((p.M + splits - 1) / splits);
+  mps = (mps + BP - 1) / BP * BP;
+  p.m_per_split = mps;
+  const dim3 grid(tiles, (p.M + mps - 1) / mps);
+  if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 64, false, true>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64, false, true>), grid, dim3(256), 0, s, p);
+  BIGDL_CHECK_LAUNCH();
 }
 
 // dw += scale · wgrad.  Requirements (checked): C % 8 == 0, K % 8 == 0, 16-B aligned x/dy.

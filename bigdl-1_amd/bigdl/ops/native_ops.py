@@ -2116,6 +2116,99 @@ def conv2d_autograd(x, w, b, stride, pad, dilation=(1, 1), groups=1):
     return _ConvFn.apply(x, w, b, tuple(stride), tuple(pad), tuple(dilation), groups)
 
 
+# ------------------------------------------------------------------------------------------------ 3-D conv
+_cl3 = torch.channels_last_3d
+
+
+def _conv3d_launch(x, w, b, out_dims, stride, pad, dilation):
+    """y [N][To][P][Q][K] = conv3d(x [N][T][H][W][C], w [K][KT][R][S][C]) (+ fp32 bias) on the
+    implicit-GEMM kernel (conv_igemm.hip D3 instantiations); x, w bf16 channels_last_3d, C % 8 == 0."""
+    N_, C_, T, H, W = x.shape
+    K, _, KT, R, S = w.shape
+    To, P, Q = out_dims
+    y = torch.empty((N_, K, To, P, Q), dtype=_bf16, device=x.device, memory_format=_cl3)
+    check(_lib().bigdl_conv3d_fwd(ptr(x), ptr(w), ptr(b), ptr(y), N_, T, H, W, C_, K, KT, R, S, To, P, Q,
+                                  stride[0], stride[1], stride[2], pad[0], pad[1], pad[2],
+                                  dilation[0], dilation[1], dilation[2], 0, _s()), "conv3d_fwd")
+    return y
+
+
+def _pad_c8(t):
+    """Zero-pad dim 1 (channels) to a multiple of 8, channels_last_3d bf16."""
+    c = t.shape[1]
+    cp = -(-c // 8) * 8
+    if cp != c:
+        t = torch.nn.functional.pad(t, (0, 0, 0, 0, 0, 0, 0, cp - c))
+    return t.to(_bf16).contiguous(memory_format=_cl3)
+
+
+class _Conv3dFn(torch.autograd.Function):
+    """VolumetricConvolution on the implicit-GEMM kernels: forward and the stride-1 data gradient
+    (a forward conv of dY with the flipped, transposed filter; strided convs first scatter dY onto
+    the stride lattice) on k_conv_fwd<…, D3>, the weight gradient on k_conv_wgrad<…, D3>
+    (VolumetricConvolution.scala updateOutput / updateGradInput / accGradParameters)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dilation, out_dims):
+        C_ = x.shape[1]
+        xp, wp = _pad_c8(x), _pad_c8(w.detach())
+        bias = b.detach().float().contiguous() if b is not None else None
+        y = _conv3d_launch(xp, wp, bias, out_dims, stride, pad, dilation)
+        ctx.save_for_backward(xp, wp)
+        ctx.geom = (stride, pad, dilation, tuple(x.shape[2:]), C_, b is not None, w.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xp, wp = ctx.saved_tensors
+        stride, pad, dilation, in_dims, C_, has_b, wdt = ctx.geom
+        gb = gy.float().sum((0, 2, 3, 4)).to(wdt) if has_b else None
+        gy = gy.to(_bf16).contiguous(memory_format=_cl3)
+        N_, K, To, P, Q = gy.shape
+        KT, R, S = wp.shape[2:]
+        Cp = xp.shape[1]
+        gx = None
+        if ctx.needs_input_grad[0]:
+            src = gy
+            if any(s_ != 1 for s_ in stride):  # dY on the stride lattice, zeros between
+                src = torch.empty((N_, K, (To - 1) * stride[0] + 1, (P - 1) * stride[1] + 1, (Q - 1) * stride[2] + 1),
+                                  dtype=_bf16, device=gy.device, memory_format=_cl3).zero_()
+                src[:, :, ::stride[0], ::stride[1], ::stride[2]] = gy
+            wt = wp.flip(2, 3, 4).transpose(0, 1).contiguous(memory_format=_cl3)  # [Cp][KT][R][S][K]
+            pd = tuple(d * (k - 1) - p_ for d, k, p_ in zip(dilation, (KT, R, S), pad))
+            gx = _conv3d_launch(src, wt, None, in_dims, (1, 1, 1), pd, dilation)[:, :C_]
+        gw = torch.zeros(wp.shape, dtype=_f32, device=gy.device).contiguous(memory_format=_cl3)
+        T, H, W = in_dims
+        check(_lib().bigdl_conv3d_wgrad(ptr(xp), ptr(gy), ptr(gw), _f(1.0), N_, T, H, W, Cp, K, KT, R, S, To, P, Q,
+                                        stride[0], stride[1], stride[2], pad[0], pad[1], pad[2],
+                                        dilation[0], dilation[1], dilation[2], _s()), "conv3d_wgrad")
+        return gx, gw[:, :C_].to(wdt), gb, None, None, None, None
+
+
+def conv3d_autograd(x, w, b, stride, pad, dilation=(1, 1, 1), out_dims=None):
+    """Differentiable native 3-D conv (NotImplemented when not eligible).  ``pad`` is the leading
+    pad per dim; ``out_dims`` (To, P, Q) defaults to the symmetric-padding output size."""
+    if not (x.is_cuda and x.dim() == 5 and w.dim() == 5 and w.shape[1] == x.shape[1]):
+        return NotImplemented
+    K, C_, KT, R, S = w.shape
+    if K % 8:
+        return NotImplemented
+    if out_dims is None:
+        out_dims = tuple((i + 2 * p_ - d * (k - 1) - 1) // s_ + 1
+                         for i, p_, d, k, s_ in zip(x.shape[2:], pad, dilation, (KT, R, S), stride))
+    if min(out_dims) <= 0:
+        return NotImplemented
+    N_ = x.shape[0]
+    Cp = -(-C_ // 8) * 8
+    T, H, W = x.shape[2:]
+    To, P, Q = out_dims
+    lim = 0x7fffffff
+    if N_ * T * H * W * max(Cp, K) * 2 >= lim or N_ * To * P * Q * K * 2 >= lim or \
+            N_ * (To * stride[0]) * (P * stride[1]) * (Q * stride[2]) * K * 2 >= lim:
+        return NotImplemented
+    return _Conv3dFn.apply(x, w, b, tuple(stride), tuple(pad), tuple(dilation), tuple(out_dims))
+
+
 # ------------------------------------------------------------------------------------------------ transposed conv
 class _DeconvFn(torch.autograd.Function):
     """Transposed convolution (SpatialFullConvolution) on the conv kernels: its forward is the
