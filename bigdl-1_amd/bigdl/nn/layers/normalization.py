@@ -281,8 +281,8 @@ class BatchNormalization(TensorModule):
         cbs = prod.scale_b if prod is not None else 0.0
         gres = None
         if self._sync_active() and self.train:
-            gi = self._sync_backward(x, gy, g, y, need_input, acc, relu)
-            if cb is not None and gi is not None:
+            gi, cb_done = self._sync_backward(x, gy, g, y, need_input, acc, relu, cb, cbs)
+            if cb is not None and gi is not None and not cb_done:
                 cb.add_(acc_float(gi).sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
             if want_gres:
                 gres = gy * (y > 0).to(gy.dtype) if relu else gy
@@ -325,7 +325,8 @@ class BatchNormalization(TensorModule):
             h(self)
         return gi, gres
 
-    def _sync_backward(self, x, gy, g, y, need_input, acc, relu=None):
+    def _sync_backward(self, x, gy, g, y, need_input, acc, relu=None, cb=None, cbs=0.0):
+        """→ (gradInput, whether the folded producer bias ``cb`` was accumulated here)."""
         relu = self._fused_relu if relu is None else relu
         import torch.distributed as dist
         if self._sync_native_ok(x) and gy.dtype == torch.bfloat16:
@@ -350,11 +351,11 @@ class BatchNormalization(TensorModule):
                                               y=y, relu=relu, need_input=need_input,
                                               gg_acc=self.gradWeight if (acc and self.affine) else None,
                                               gb_acc=self.gradBias if (acc and self.affine) else None,
-                                              scale=self.scale_w if acc else 0.0)
+                                              scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
                 if gi is not NotImplemented:
                     if acc and self.affine and self.scale_b != self.scale_w:
                         self.gradBias.add_(loc[:x.shape[1]], alpha=self.scale_b - self.scale_w)
-                    return gi
+                    return gi, cb is not None
         C = x.shape[1]
         dims = [d for d in range(x.dim()) if d != 1]
         shape = [1, C] + [1] * (x.dim() - 2)
@@ -370,11 +371,13 @@ class BatchNormalization(TensorModule):
         if acc and self.affine:
             self.gradWeight.add_(local_dg, alpha=self.scale_w)
             self.gradBias.add_(local_db, alpha=self.scale_b)
-        if not need_input:
-            return None
+        if not need_input and cb is None:
+            return None, False
         gam = g.view(shape) if g is not None else 1.0
         gi = (gam * self.saveStd.view(shape) / cnt) * (cnt * gf - db.view(shape) - xhat * dg.view(shape))
-        return gi.to(x.dtype)
+        if cb is not None:  # from the fp32 gradient, before rounding
+            cb.add_(gi.sum(dims), alpha=cbs)
+        return (gi.to(x.dtype) if need_input else None), cb is not None
 
     def updateGradInput(self, input, gradOutput):
         gi = self._bwd(input, gradOutput, True, True)

@@ -656,20 +656,35 @@ BIGDL_EXPORT int bigdl_bn_bwd_sums(const void* gy, const void* x, const void* y,
   BIGDL_CHECK_LAUNCH();
 }
 
+// Gradient of a producer bias folded into a SyncBN: this rank's Σ_rows gx = A·Σ_l g' + B·Σ_l x +
+// M_l·Cc with the GLOBAL coefficients; Σ_l x is taken as M_l·μ (exact at one rank; across ranks the
+// per-rank deviations B·(Σ_l x − M_l·μ) cancel in the gradient all-reduce, since Σ_ranks = N·μ).
+__global__ void __launch_bounds__(256) k_bn_cbias_sync(const float* __restrict__ local_sums,
+                                                       const float* __restrict__ coef, const float* __restrict__ mean,
+                                                       long long M, int C, float* __restrict__ cbias, float cbscale) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float A = coef[c], B = coef[C + c], Cc = coef[2 * C + c];
+  cbias[c] += cbscale * (A * local_sums[c] + (float)M * (B * mean[c] + Cc));
+}
+
 // Backward from sums: the LOCAL sums accumulate this rank's dγ, dβ (the data-parallel gradient
 // all-reduce sums them across ranks); the GLOBAL sums over `count` rows give the input-gradient
-// coefficients, applied to this rank's M rows.
+// coefficients, applied to this rank's M rows.  ``cbias``: see k_bn_cbias_sync.
 BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const void* y, void* gx, long long M,
                                          long long count, int C, const float* gamma, const float* mean,
                                          const float* invstd, float* ggamma, float* gbeta, float gscale,
                                          const float* local_sums, const float* global_sums, float* coef,
-                                         float* coef_scratch, int relu, hipStream_t s) {
+                                         float* coef_scratch, int relu, float* cbias, float cbscale, hipStream_t s) {
   if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
   if (ggamma || gbeta)
     hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, local_sums, 1, count, C, gamma,
                        mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch);
   hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, global_sums, 1, count, C, gamma,
                      mean, invstd, (float*)nullptr, (float*)nullptr, 0.f, (float*)nullptr, 0.f, coef);
+  if (cbias)
+    hipLaunchKernelGGL(k_bn_cbias_sync, dim3((C + 255) / 256), dim3(256), 0, s, local_sums, coef, mean, M, C, cbias,
+                       cbscale);
   if (gx) {
     int grid = apply_grid(M, C);
     const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;

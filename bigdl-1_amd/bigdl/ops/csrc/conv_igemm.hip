@@ -76,6 +76,11 @@ struct ConvParams {
   // KT, depth stride / pad / dilation, output depth To; x is [Nb][T][H][W][C], w [K][KT][R][S][C],
   // y [Nb][To][P][Q][K] (M = Nb·To·P·Q).  2-D launches leave T = KT = To = 1.
   int T, KT, st, pt, dtd, To;
+  // Pixel stride of x in elements (C unless x is a channel slice of a wider NHWC tensor) and, for
+  // grouped convolution (SpatialConvolution.scala nGroup; one launch, group = blockIdx.y), the
+  // per-group element offsets of x (channels), w (filters·ldw) and y / bias (channels).
+  int ldx;
+  long long gx, gw, gy;
 };
 
 // Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
@@ -139,6 +144,13 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wave_m = wid & 1, wave_n = wid >> 1;
+  const long long grp = blockIdx.y;  // grouped conv: this block's group (0 otherwise)
+  if (grp) {
+    p.x += grp * p.gx;
+    p.w += grp * p.gw;
+    p.y += grp * p.gy;
+    if (p.bias) p.bias += grp * p.gy;
+  }
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -148,7 +160,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // for an out-of-range offset, so conv padding, the M / K tails and the channel tail need no
   // branches (a per-element "load or zero" select makes hipcc branch and drain vmcnt per load,
   // cdna_hip_programming.md §5 item 4(c)).  OOB = an offset past the end of the tensor.
-  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.C * 2);
+  const uint32_t x_bytes = (uint32_t)(((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.ldx - grp * p.gx) * 2);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw * 2);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
@@ -202,8 +214,8 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   if constexpr (FAST) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      if constexpr (D3) rbase[i] = ((a_img[i] + (a_t[i] * p.H + a_h[i]) * p.W + a_w[i]) * p.C) + col8 * 8;
-      else rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.C) + col8 * 8;
+      if constexpr (D3) rbase[i] = ((a_img[i] + (a_t[i] * p.H + a_h[i]) * p.W + a_w[i]) * p.ldx) + col8 * 8;
+      else rbase[i] = ((a_img[i] + a_h[i] * p.W + a_w[i]) * p.ldx) + col8 * 8;
       uint64_t msk = 0;
       if (PW) {
         msk = a_img[i] >= 0 ? 1ull : 0ull;
@@ -249,12 +261,12 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
             it_s = 0;
             if (D3 && ++it_r == p.R) {  // next depth tap: back to row 0, column 0, one frame on
               it_r = 0;
-              it_off += (p.dtd * p.H * p.W - (p.R - 1) * p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+              it_off += (p.dtd * p.H * p.W - (p.R - 1) * p.dh * p.W - (p.S - 1) * p.dw) * p.ldx;
             } else {
-              it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+              it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.ldx;
             }
           } else {
-            it_off += p.dw * p.C;
+            it_off += p.dw * p.ldx;
           }
         }
       }
@@ -318,7 +330,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
           ok = ok && (unsigned)tt < (unsigned)p.T;
           pix += tt * p.H * p.W;
         }
-        const uint32_t off = ok ? (uint32_t)(pix * p.C + c) * 2u : OOB;
+        const uint32_t off = ok ? (uint32_t)(pix * p.ldx + c) * 2u : OOB;
         ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
       }
 #pragma unroll
@@ -699,8 +711,16 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
-                           int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr) {
+                           int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
+                           int ldx = 0, int groups = 1) {
   const bool c4 = C == 4;
+  if (ldx == 0) ldx = C;
+  if (groups < 1 || ldx < C || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
+  // grouped: C / K are per group; x pixels are ldx apart with group g at channel g·C; y rows ldy
+  // apart with group g at channel g·K; w holds the groups' [K][R][S][C] blocks back to back
+  if (groups > 1 && (c4 || res || stats || bnx || ldx < groups * C || ldy < groups * K || K % 8 ||
+                     osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
+    return (int)hipErrorInvalidValue;
   // any K: partial 8-channel chunks are stored per element in the epilogue
   if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   if (c4 && (ldw < R * S * C || ldw % 8 || dh != 1 || dw != 1)) return (int)hipErrorInvalidValue;
@@ -708,10 +728,14 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
   if (!c4) ldw = R * S * C;
-  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)K * ldw * 2 >= 0x80000000ull)
+  if ((size_t)Nb * H * W * ldx * 2 >= 0x80000000ull || (size_t)groups * K * ldw * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
   ConvParams p{};  // value-initialised: a field a launcher forgets is null / 0, never stack garbage
   p.T = p.KT = p.st = p.dtd = p.To = 1;
+  p.ldx = ldx;
+  p.gx = C;
+  p.gw = (long long)K * (c4 ? ldw : R * S * C);
+  p.gy = K;
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)w;
   p.bias = bias;
@@ -770,8 +794,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const bool fast = (C % bk == 0) && R * S <= 64;
   const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
   long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
-  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
-  const dim3 g((unsigned)tiles);
+  if (tiles > 0x7fffffff || groups > 65535) return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)tiles, (unsigned)groups);
   if (bm == 256)
     BN == 64 ? launch_fwd<64, 256, 64>(mode, g, s, p) : launch_fwd<128, 256, 64>(mode, g, s, p);
   else if (bk == 32)
@@ -805,6 +829,17 @@ BIGDL_EXPORT int bigdl_conv_fwd_full2(const void* x, const void* w, const void* 
                          bn_bits);
 }
 
+// Grouped convolution in ONE launch (SpatialConvolution.scala:93-98 nGroup): x [Nb][H][W][ldx] with
+// group g's Cg input channels at channel g·Cg, w = groups × [Kg][R][S][Cg], y [Nb][P][Q][ldy] with
+// group g's Kg outputs at channel g·Kg; the group is blockIdx.y.  Cg % 8 == 0, Kg % 8 == 0.
+BIGDL_EXPORT int bigdl_conv_fwd_grouped(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W,
+                                        int ldx, int Cg, int Kg, int groups, int R, int S, int P, int Q, int sh,
+                                        int sw, int ph, int pw, int dh, int dw, int relu, int ldy, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, nullptr, y, nullptr, Nb, H, W, Cg, Kg, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, 1,
+                         1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0, 0, 0,
+                         nullptr, ldx, groups);
+}
+
 // 3-D convolution (VolumetricConvolution.scala) on the same implicit-GEMM kernel: x [Nb][T][H][W][C],
 // w [K][KT][R][S][C], y [Nb][To][P][Q][K] (+ fp32 bias, ReLU).  C % 8 == 0.
 BIGDL_EXPORT int bigdl_conv3d_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int T, int H, int W,
@@ -823,6 +858,7 @@ BIGDL_EXPORT int bigdl_conv3d_fwd(const void* x, const void* w, const float* bia
   p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
   p.T = T; p.KT = KT; p.st = st; p.pt = pt; p.dtd = dtd; p.To = To;
+  p.ldx = C;
   const long long Ml = (long long)Nb * To * P * Q;
   if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   p.M = (int)Ml;

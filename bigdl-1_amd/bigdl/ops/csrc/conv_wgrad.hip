@@ -46,6 +46,10 @@ struct WgradParams {
   // 3-D (D3 instantiations): x [Nb][T][H][W][C], dy [Nb][To][P][Q][K], dw [K][KT][R][S][C]
   int T, KT, st, pt, dtd, To;
   FastDiv fRS, fTo;
+  // pixel strides of x / dy in elements (C / K unless channel slices of wider tensors) and the
+  // grouped-conv per-group offsets (group = blockIdx.z) of x, dy (channels) and dw (elements)
+  int ldx, ldk;
+  long long gx, gdy, gdw;
 };
 
 constexpr int BP = 64;  // split granularity (pixels); the k-tile depth BPT is 64 or 32
@@ -77,6 +81,12 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wave_n = wid & 1, wave_k = wid >> 1;
+  const long long grp = blockIdx.z;
+  if (grp) {
+    p.x += grp * p.gx;
+    p.dy += grp * p.gdy;
+    p.dw += grp * p.gdw;
+  }
   // tile mapping (XCD-contiguous ranges of the tile grid)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -115,8 +125,8 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   // Raw buffer loads (OOB offsets → zeros, no branches) into two register sets; tile t+2 is
   // requested while tile t is multiplied (loads always issued — beyond the range with a dead
   // offset — so hipcc's vmcnt counts stay exact; see conv_igemm.hip).
-  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.C * 2);
-  const uint32_t dy_bytes = (uint32_t)((size_t)p.M * p.K * 2);
+  const uint32_t x_bytes = (uint32_t)(((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.ldx - grp * p.gx) * 2);
+  const uint32_t dy_bytes = (uint32_t)(((size_t)p.M * p.ldk - grp * p.gdy) * 2);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)dy_bytes, 0x00020000);
   constexpr uint32_t DEAD = 0x80000000u;
@@ -127,7 +137,7 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
     for (int i = 0; i < DY_CH; ++i) {
       const int m = mt + dy_row0 + i * DY_RSTEP;
       const bool ok = ndy_ok && m < mend;
-      const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.K + (uint32_t)ndy) * 2u : DEAD) | dead;
+      const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldk + (uint32_t)ndy) * 2u : DEAD) | dead;
       rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
     }
 #pragma unroll
@@ -157,7 +167,7 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
         const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
         rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       } else {
-        const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.C + (uint32_t)cx) * 2u : DEAD) | dead;
+        const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.ldx + (uint32_t)cx) * 2u : DEAD) | dead;
         rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
       }
     }
@@ -265,6 +275,7 @@ BIGDL_EXPORT int bigdl_conv3d_wgrad(const void* x, const void* dy, float* dw, fl
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw_ = dwd;
   p.T = T; p.KT = KT; p.st = st; p.pt = pt; p.dtd = dtd; p.To = To;
+  p.ldx = C; p.ldk = K;
   p.M = Nb * To * P * Q;
   p.Kg = KT * R * S * C;
   p.fPQ = make_fastdiv((uint32_t)(P * Q));
@@ -290,15 +301,21 @@ BIGDL_EXPORT int bigdl_conv3d_wgrad(const void* x, const void* dy, float* dw, fl
 }
 
 // dw += scale · wgrad.  Requirements (checked): C % 8 == 0, K % 8 == 0, 16-B aligned x/dy.
-BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C,
-                                  int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
-                                  int splits, hipStream_t s) {
+// Grouped (groups > 1): C / K are per group, x / dy pixels ldx / ldk apart with group g at channel
+// g·C / g·K, dw = groups × [K][R][S][C] blocks; the group is blockIdx.z.
+static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C, int K,
+                        int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd, int splits,
+                        hipStream_t s, int ldx, int ldk, int groups) {
   const bool c4 = C == 4;
   if ((C % 8 && !c4) || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
   if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
-  if ((size_t)Nb * H * W * C * 2 >= 0x80000000ull || (size_t)Nb * P * Q * K * 2 >= 0x80000000ull)
+  if (groups < 1 || groups > 65535 || ldx < groups * C || ldk < groups * K) return (int)hipErrorInvalidValue;
+  if ((ldx != C || ldk != K) && (c4 || ldx % 8 || ldk % 8)) return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * H * W * ldx * 2 >= 0x80000000ull || (size_t)Nb * P * Q * ldk * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   WgradParams p{};
+  p.ldx = ldx; p.ldk = ldk;
+  p.gx = C; p.gdy = K; p.gdw = (long long)K * R * S * C;
   p.x = (const bf16_t*)x;
   p.dy = (const bf16_t*)dy;
   p.dw = dw;
@@ -321,7 +338,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
     // (≈1.3 TB/s chip-wide, MI355X_MICROARCH.md 'Global float atomics'), so fewer, longer splits win
     // once the grid fills the chip.
     const long long target = splits < 0 ? -(long long)splits : 512;
-    long long want = (target + tiles - 1) / tiles;
+    long long want = (target + (long long)tiles * groups - 1) / ((long long)tiles * groups);
     long long max_by_work = (p.M + 8 * BP - 1) / (8 * BP);
     splits = (int)(want < max_by_work ? want : max_by_work);
     if (splits < 1) splits = 1;
@@ -331,7 +348,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
   mps = (mps + BP - 1) / BP * BP;
   p.m_per_split = mps;
   splits = (p.M + mps - 1) / mps;
-  dim3 grid(tiles, splits);
+  dim3 grid(tiles, splits, groups);
   // Pixel depth of a k-tile: 32 (half the LDS / prefetch registers, 3 blocks per CU) wins on the
   // small weight grids (≤ 16 tiles, K ≥ 128: few tiles, long split reductions), 64 elsewhere
   // (profiles/r1_conv_bk_ab.txt).  BIGDL_WGRAD_BP=32|64 pins it for A/B measurements.
@@ -358,4 +375,18 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
     else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64>), grid, dim3(256), 0, s, p);
   }
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C,
+                                  int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
+                                  int splits, hipStream_t s) {
+  return wgrad_launch(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, C, K, 1);
+}
+
+// Grouped weight gradient in one launch (SpatialConvolution.scala:93-98 nGroup accGradParameters).
+BIGDL_EXPORT int bigdl_conv_wgrad_grouped(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W,
+                                          int ldx, int Cg, int ldk, int Kg, int groups, int R, int S, int P, int Q,
+                                          int sh, int sw, int ph, int pw, int dh, int dwd, hipStream_t s) {
+  if (Cg == 4) return (int)hipErrorInvalidValue;
+  return wgrad_launch(x, dy, dw, scale, Nb, H, W, Cg, Kg, R, S, P, Q, sh, sw, ph, pw, dh, dwd, 0, s, ldx, ldk, groups);
 }

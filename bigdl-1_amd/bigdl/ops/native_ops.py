@@ -289,13 +289,14 @@ def bn_bwd_partials_sums(partial, G, C_, dev):
 
 
 def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
-                          need_input=True, gg_acc=None, gb_acc=None, scale=1.0):
-    """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows → gradInput."""
+                          need_input=True, gg_acc=None, gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0):
+    """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows → gradInput;
+    ``cbias_acc`` receives this rank's share of a folded producer bias's gradient (fp32 closed form)."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
-    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc)):
+    if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc)):
         return NotImplemented
     coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
     scratch = torch.empty(3 * C_, dtype=_f32, device=x.device)
@@ -304,7 +305,8 @@ def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, glob
                                          C.c_int(C_), ptr(gamma), ptr(save_mean), ptr(save_invstd),
                                          ptr(gg_acc if scale != 0 else None), ptr(gb_acc if scale != 0 else None),
                                          _f(scale), ptr(local_sums), ptr(global_sums), ptr(coef), ptr(scratch),
-                                         C.c_int(1 if relu else 0), _s()), "bn_bwd_apply_sums")
+                                         C.c_int(1 if relu else 0), ptr(cbias_acc if cbias_scale != 0 else None),
+                                         _f(cbias_scale), _s()), "bn_bwd_apply_sums")
     return gx
 
 
@@ -508,11 +510,109 @@ def _group_slice(t, g, n):
     return t[:, g * n:(g + 1) * n].contiguous(memory_format=torch.channels_last)
 
 
+def _group_pack(G, Cg, Kg):
+    """Groups per launch group ("pack"): a divisor of G whose packed widths gps·Cg and gps·Kg are
+    multiples of 8 (16-B chunks), as large as fits one 64-channel output tile.  A pack runs as one
+    dense conv on a block-diagonal filter: the MFMA tile pays 64 output channels per pixel however
+    the groups are split, so packing small groups adds no work and fills the k loop.  None when no
+    divisor gives 8-aligned widths."""
+    best = None
+    for gps in range(1, G + 1):
+        if G % gps or (gps * Cg) % 8 or (gps * Kg) % 8:
+            continue
+        if best is None or gps * Kg <= 64:
+            best = gps
+    return best
+
+
+def _packed_filter(w4, G, gps):
+    """[K][Cg][R][S] grouped filter → [G/gps · gps·Kg][R][S][gps·Cg] bf16: each pack's groups on the
+    block diagonal (zeros elsewhere)."""
+    K, Cg, R, S = w4.shape
+    Kg = K // G
+    if gps == 1:
+        return _krsc(w4.to(_bf16))
+    wv = w4.detach().to(_bf16).reshape(G // gps, gps, Kg, Cg, R, S)
+    eye = torch.eye(gps, dtype=_bf16, device=w4.device)
+    bd = torch.einsum("aikcrs,ij->aikrsjc", wv, eye)  # exact: products with 0 / 1
+    return bd.reshape(K, R, S, gps * Cg).contiguous()
+
+
+def _conv_fwd_grouped_1(x, w4, b, stride, pad, dilation, groups, relu=False, out_hw=None):
+    """Grouped convolution (SpatialConvolution.scala:93-98 nGroup) in ONE launch: packs of groups
+    (``_group_pack``) are the grid's y index, x is read in place (pixel stride C), y written in
+    place (pixel stride K).  NotImplemented when no 8-aligned packing exists."""
+    N_, C_, H, W = x.shape
+    K, Cg, R, S = w4.shape
+    Kg = K // groups
+    gps = _group_pack(groups, Cg, Kg)
+    if gps is None or not (x.is_contiguous(memory_format=torch.channels_last) and _al16(x)):
+        return NotImplemented
+    if out_hw is None:
+        out_hw = _dw_out_hw(H, W, R, S, stride, pad, dilation)
+    P, Q = out_hw
+    if P <= 0 or Q <= 0:
+        return NotImplemented
+    wp = _packed_filter(w4, groups, gps)
+    y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    bias = None if b is None else b.detach().float().contiguous()
+    check(_lib().bigdl_conv_fwd_grouped(ptr(x), ptr(wp), ptr(bias), ptr(y), N_, H, W, C_, gps * Cg, gps * Kg,
+                                        groups // gps, R, S, P, Q, stride[0], stride[1], pad[0], pad[1],
+                                        dilation[0], dilation[1], int(bool(relu)), K, _s()), "conv_fwd_grouped")
+    return y
+
+
+def _conv_bwd_grouped_1(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale):
+    """Backward of ``_conv_fwd_grouped_1``: data gradient = the grouped forward of dY with each
+    group's flipped, transposed filter (strided convs scatter dY onto the stride lattice first);
+    weight gradient = one grouped wgrad launch over the packs, block diagonals extracted."""
+    N_, C_, H, W = x.shape
+    K, Cg, R, S = w4.shape
+    Kg = K // groups
+    P, Q = gy.shape[2], gy.shape[3]
+    gps = _group_pack(groups, Cg, Kg)
+    if gps is None or _group_pack(groups, Kg, Cg) is None:
+        return NotImplemented
+    if not (x.is_contiguous(memory_format=torch.channels_last) and _al16(x)):
+        return NotImplemented
+    if not (gy.is_contiguous(memory_format=torch.channels_last) and _al16(gy)):
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    gi = None
+    if need_input:
+        src = gy
+        if tuple(stride) != (1, 1):
+            src = torch.empty((N_, K, (P - 1) * stride[0] + 1, (Q - 1) * stride[1] + 1), dtype=_bf16,
+                              device=gy.device, memory_format=torch.channels_last).zero_()
+            src[:, :, ::stride[0], ::stride[1]] = gy
+        wt = w4.detach().reshape(groups, Kg, Cg, R, S).flip(3, 4).transpose(1, 2).reshape(C_, Kg, R, S)
+        pd = (dilation[0] * (R - 1) - pad[0], dilation[1] * (S - 1) - pad[1])
+        gi = _conv_fwd_grouped_1(src, wt, None, (1, 1), pd, dilation, groups, out_hw=(H, W))
+        if gi is NotImplemented:
+            return NotImplemented
+    if gw_acc is not None and scale != 0:
+        NS, KS, CS = groups // gps, gps * Kg, gps * Cg
+        tmp = torch.zeros((NS, KS, R, S, CS), dtype=_f32, device=x.device)
+        check(_lib().bigdl_conv_wgrad_grouped(ptr(x), ptr(gy), ptr(tmp), _f(1.0), N_, H, W, C_, CS, K, KS, NS, R, S,
+                                              P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                              _s()), "conv_wgrad_grouped")
+        if gps > 1:  # the packs' block diagonals: [NS][gps][Kg][R][S][gps][Cg] → [K][Cg][R][S]
+            d = torch.diagonal(tmp.view(NS, gps, Kg, R, S, gps, Cg), dim1=1, dim2=5)  # [NS][Kg][R][S][Cg][gps]
+            gw = d.permute(0, 5, 1, 4, 2, 3).reshape(K, Cg, R, S)
+        else:
+            gw = tmp.view(K, R, S, Cg).permute(0, 3, 1, 2)
+        gw_acc.add_(gw, alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
+    return gi
+
+
 def _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot=None, relu=False):
-    """Grouped convolution (the reference's nGroup, SpatialConvolution.scala:93-98) on the native
-    kernels: one groups=1 launch per group on channel slices; each group's output goes straight
-    into its channel slice of the result when the slice is 16-B aligned (the zero-copy concat
-    path), else through a copy."""
+    """Grouped convolution (the reference's nGroup, SpatialConvolution.scala:93-98): one launch over
+    all groups (``_conv_fwd_grouped_1``); only a grouping with no 8-aligned packing falls back to
+    one groups=1 launch per group on channel slices."""
+    y = _conv_fwd_grouped_1(x, w4, b, stride, pad, dilation, groups, relu)
+    if y is not NotImplemented:
+        return y
     N_, C_, H, W = x.shape
     K = w4.shape[0]
     Cg, Kg = C_ // groups, K // groups
@@ -1014,8 +1114,11 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     if groups > 1 and residual is None and bn_fuse is None and _depthwise_ok(x, w4, groups):
         return _depthwise_bwd(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale)
     if groups > 1 and residual is None and bn_fuse is None and _grouped_ok(x, w4, groups) and gy.dtype == _bf16:
-        # grouped: one groups=1 backward per channel slice (gradient-weight rows of a group are a
-        # contiguous block of the arena, so they accumulate in place)
+        r = _conv_bwd_grouped_1(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale)
+        if r is not NotImplemented:
+            return r
+        # no 8-aligned packing: one groups=1 backward per channel slice (gradient-weight rows of a
+        # group are a contiguous block of the arena, so they accumulate in place)
         C_, K = x.shape[1], w4.shape[0]
         Cg, Kg = C_ // groups, K // groups
         gi = torch.empty(x.shape, dtype=_bf16, device=x.device,
