@@ -188,6 +188,8 @@ __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const fl
 // BITS (with RELU): also emit the ReLU mask as one byte per 8-channel chunk (bit e = output channel
 // cg·8 + e is > 0) — a ResNet block tail's output mask for the backward, 1/16 of the bytes of
 // re-reading the bf16 output there.
+constexpr int kApplyUnroll = 4;
+
 template <bool RES, bool RELU, bool BITS = false>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                   bf16_t* __restrict__ y, long long M, int C,
@@ -206,27 +208,42 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       sc[k] = scale[cg * 8 + k];
       sh[k] = shift[cg * 8 + k];
     }
-    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
-      size_t off = (size_t)r * C + (size_t)cg * 8;
-      float v[8];
-      load8_nt(x + off, v);
-      float rv[8];
-      if (RES) load8_nt(res + off, rv);
+    // kApplyUnroll rows per trip: all their loads are issued before the first use, so each thread
+    // keeps several 16-B requests in flight (one per trip left the streaming passes latency-bound)
+    long long r = (long long)blockIdx.x * g.RPI + r_off;
+    for (; r < M; r += kApplyUnroll * rstride) {
+      bigdl_u32x4 xv[kApplyUnroll], rvv[kApplyUnroll];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float o = fmaf(v[k], sc[k], sh[k]);
-        if (RES) o += rv[k];
-        if (RELU) o = fmaxf(o, 0.f);
-        v[k] = o;
+      for (int u = 0; u < kApplyUnroll; ++u) {
+        const long long ru = r + u * rstride;
+        const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
+        xv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
+        if (RES) rvv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(res + off));
       }
-      store8(y + off, v);
-      if (BITS) {
-        // the bit must agree with the stored bf16 value (> 0 after rounding: a positive fp32 never
-        // rounds to +0 in bf16, so o > 0 is exact)
-        uint32_t b = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
-        bits[off >> 3] = (uint8_t)b;
+      for (int u = 0; u < kApplyUnroll; ++u) {
+        const long long ru = r + u * rstride;
+        if (ru >= M) break;
+        const size_t off = (size_t)ru * C + (size_t)cg * 8;
+        float v[8], rv[8];
+        unpack8(make_uint4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]), v);
+        if (RES) unpack8(make_uint4(rvv[u][0], rvv[u][1], rvv[u][2], rvv[u][3]), rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float o = fmaf(v[k], sc[k], sh[k]);
+          if (RES) o += rv[k];
+          if (RELU) o = fmaxf(o, 0.f);
+          v[k] = o;
+        }
+        store8(y + off, v);
+        if (BITS) {
+          // the bit must agree with the stored bf16 value (> 0 after rounding: a positive fp32 never
+          // rounds to +0 in bf16, so o > 0 is exact)
+          uint32_t b = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+          bits[off >> 3] = (uint8_t)b;
+        }
       }
     }
   }
@@ -492,21 +509,36 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
       B[k] = coef[C + cg * 8 + k];
       Cc[k] = coef[2 * C + cg * 8 + k];
     }
-    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
-      size_t off = (size_t)r * C + (size_t)cg * 8;
-      float gv[8], xv[8];
-      load8_nt(gy + off, gv);
-      load8_nt(x + off, xv);
-      if (RELU) {
-        float yv[8];
-        load8_nt(y + off, yv);
+    long long r = (long long)blockIdx.x * g.RPI + r_off;
+    for (; r < M; r += kApplyUnroll * rstride) {  // see k_bn_apply: loads of all rows of a trip first
+      bigdl_u32x4 gq[kApplyUnroll], xq[kApplyUnroll], yq[kApplyUnroll];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+      for (int u = 0; u < kApplyUnroll; ++u) {
+        const long long ru = r + u * rstride;
+        const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
+        gq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(gy + off));
+        xq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
+        if (RELU) yq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(y + off));
       }
-      if (GRES) store8(gres + off, gv);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) xv[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
-      store8(gx + off, xv);
+      for (int u = 0; u < kApplyUnroll; ++u) {
+        const long long ru = r + u * rstride;
+        if (ru >= M) break;
+        const size_t off = (size_t)ru * C + (size_t)cg * 8;
+        float gv[8], xv[8];
+        unpack8(make_uint4(gq[u][0], gq[u][1], gq[u][2], gq[u][3]), gv);
+        unpack8(make_uint4(xq[u][0], xq[u][1], xq[u][2], xq[u][3]), xv);
+        if (RELU) {
+          float yv[8];
+          unpack8(make_uint4(yq[u][0], yq[u][1], yq[u][2], yq[u][3]), yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+        }
+        if (GRES) store8(gres + off, gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
+        store8(gx + off, xv);
+      }
     }
   }
 }

@@ -579,6 +579,295 @@ __global__ void __launch_bounds__(1024) k_lstm_seq_bwd_p(LstmSeqP p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-workgroup persistent LSTM (K14 resident-weight variant): ⌈H/16⌉ single-wave workgroups, one
+// per 16-unit tile, run every time step of a layer-direction.  A workgroup's slice of the recurrent
+// weight (forward: the 4 gate rows of its 16 units, 4·16×H; backward: the 16 Uᵀ rows, 16×4H) is
+// loaded into REGISTERS once and stays there for the whole sequence — the step only reads the
+// B×H (forward) / B×4H (backward) recurrent state written by all tiles in the previous step.
+// Steps are separated by a grid barrier: a monotone arrival counter in global memory (agent-scope
+// release add by each tile after its stores, agent-scope acquire spin before the next step's
+// reads).  The tiles are few (≤ 16 workgroups of one wave) so they are always co-resident; the spin
+// is bounded (a tile that waits ~1 s gives up and raises the error word instead of hanging).
+// ------------------------------------------------------------------------------------------------
+constexpr int kMpMaxKC = 8;    // forward: H ≤ 256 → ≤ 8 k-chunks of 32
+constexpr int kMpMaxKCb = 32;  // backward: 4H ≤ 1024 → ≤ 32 k-chunks
+
+// Two exchange protocols (template SC), selected by BIGDL_RNN_MP_SYNC (default 1):
+//   SC = 0: plain stores / loads of the exchanged state; an agent-scope release fence (L2 write-back)
+//           before the arrival and an agent-scope acquire fence (L2 invalidate) after the wait.
+//   SC = 1: the exchanged state itself is written and read with agent-scope (device-coherent) 8-byte
+//           accesses, so the barrier needs only the store acknowledgements (workgroup-scope release)
+//           before the arrival — no whole-L2 write-back / invalidate per step.
+// Either way the spin polls with relaxed agent-scope loads.
+template <bool SC>
+__device__ __forceinline__ void mp_arrive(int* cnt) {
+  if constexpr (SC) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores → visible device-wide
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool SC>
+__device__ __forceinline__ bool mp_wait(int* cnt, int target, int* err) {
+  int spins = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 22)) {  // seconds: a tile never arrived (not co-resident?) — fail, do not hang
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  if constexpr (SC) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// exchanged-state accessors: 4 bf16 (8 B) store, 8 bf16 (16 B) fragment load
+template <bool SC>
+__device__ __forceinline__ void xst4(bf16_t* p, const float* v) {
+  if constexpr (SC) {
+    const unsigned long long w = (unsigned long long)((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16)) |
+                                 ((unsigned long long)((uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)) << 32);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    stb4(p, v);
+  }
+}
+template <bool SC>
+__device__ __forceinline__ v8s xld8(const bf16_t* p) {
+  if constexpr (SC) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(v8s, u2{a, b});
+  } else {
+    return *reinterpret_cast<const v8s*>(p);
+  }
+}
+
+template <int NBT, bool SC>
+__global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int u0 = blockIdx.x * 16;
+  const int j = u0 + fq * 4;  // this lane's unit quad
+  const bool jin = j < H;
+  const bool urow = u0 + fr < H;
+  const int KC = (H + 31) / 32;
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  // resident weight fragments: gate g, k-chunk kc (lane = U row u0 + fr, k = 32 kc + 8 fq .. +7)
+  v8s wf[4][kMpMaxKC];
+  const bf16_t* ub = p.u + (long long)(urow ? u0 + fr : 0) * H;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int kc = 0; kc < kMpMaxKC; ++kc) {
+      const int k = kc * 32 + fq * 8;
+      wf[g][kc] = (kc < KC && k < H && urow) ? *reinterpret_cast<const v8s*>(ub + (long long)g * H * H + k) : zero;
+    }
+  float c[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int m = bt * 16 + fr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[bt][e] = (p.c0 && m < B && jin) ? p.c0[(long long)m * H + j + e] : 0.f;
+  }
+  int* cnt = sync;
+  int* err = sync + 1;
+  for (int t = 0; t < T; ++t) {
+    // epilogue operands first: they do not depend on the other tiles
+    uint2 xr[NBT][4];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[bt][g] = (!p.x_f32 && m < B && jin)
+                        ? *reinterpret_cast<const uint2*>((const bf16_t*)p.x2 + ((long long)m * T + t) * G + g * H + j)
+                        : make_uint2(0u, 0u);
+    }
+    if (t > 0 && !mp_wait<SC>(cnt, t * (int)gridDim.x, err)) return;
+    // h_{t-1}: the initial state or the previous step's output column of every tile
+    const bf16_t* hb = t == 0 ? p.h0 : p.out + (long long)(t - 1) * H;
+    const long long ldh = t == 0 ? H : (long long)T * H;
+    v4f acc[NBT][4];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[bt][g] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < kMpMaxKC; ++kc) {
+      const int k = kc * 32 + fq * 8;
+      const bool kin = kc < KC && k < H;
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        const v8s hf = (kin && m < B) ? (t == 0 ? *reinterpret_cast<const v8s*>(hb + m * ldh + k) : xld8<SC>(hb + m * ldh + k))
+                                      : zero;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[bt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[g][kc], hf, acc[bt][g], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m >= B || !jin) continue;
+      float xg[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (p.x_f32) {
+          ld4(p.x2, 1, ((long long)m * T + t) * G + g * H + j, xg[g]);
+        } else {
+          xg[g][0] = __uint_as_float(xr[bt][g].x << 16);
+          xg[g][1] = __uint_as_float(xr[bt][g].x & 0xFFFF0000u);
+          xg[g][2] = __uint_as_float(xr[bt][g].y << 16);
+          xg[g][3] = __uint_as_float(xr[bt][g].y & 0xFFFF0000u);
+        }
+      }
+      float gi[4], gg[4], gf[4], go[4], h[4], tcv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gi[e] = sgm(xg[0][e] + acc[bt][0][e]);
+        gg[e] = tanhf(xg[1][e] + acc[bt][1][e]);
+        gf[e] = sgm(xg[2][e] + acc[bt][2][e]);
+        go[e] = sgm(xg[3][e] + acc[bt][3][e]);
+        c[bt][e] = gi[e] * gg[e] + gf[e] * c[bt][e];
+        tcv[e] = tanhf(c[bt][e]);
+        h[e] = go[e] * tcv[e];
+      }
+      xst4<SC>(p.out + ((long long)m * T + t) * H + j, h);
+      const long long mh = ((long long)t * B + m) * H + j;
+      if (p.cs) {
+        stf4(p.cs + mh, c[bt]);
+        stf4(p.tcs + mh, tcv);
+        float* a = p.acts + ((long long)t * B + m) * G + j;
+        stf4(a, gi);
+        stf4(a + H, gg);
+        stf4(a + 2 * H, gf);
+        stf4(a + 3 * H, go);
+      }
+    }
+    if (t + 1 < T) mp_arrive<SC>(cnt);
+  }
+  if (p.cbuf) {  // inference: the final c, where the step path leaves it (slot (T-1)&1)
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m < B && jin) stf4(p.cbuf + (long long)((T - 1) & 1) * B * H + (long long)m * H + j, c[bt]);
+    }
+  }
+}
+
+template <int NBT, bool SC>
+__global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int u0 = blockIdx.x * 16;
+  const int j = u0 + fq * 4;
+  const bool jin = j < H;
+  const bool urow = u0 + fr < H;
+  const int KC = (G + 31) / 32;
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  v8s wf[kMpMaxKCb];  // Uᵀ row u0 + fr: Σ_k dg[k]·U[k][j]
+  const bf16_t* ub = p.u + (long long)(urow ? u0 + fr : 0) * G;
+#pragma unroll
+  for (int kc = 0; kc < kMpMaxKCb; ++kc) {
+    const int k = kc * 32 + fq * 8;
+    wf[kc] = (kc < KC && k < G && urow) ? *reinterpret_cast<const v8s*>(ub + k) : zero;
+  }
+  float dc[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dc[bt][e] = 0.f;
+  int* cnt = sync;
+  int* err = sync + 1;
+  for (int t = T - 1; t >= 0; --t) {
+    float pre[NBT][7][4];  // gy, act i, g, f, o, tanh(c), c_prev
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m < B && jin) {
+        ld4(p.gy, 0, ((long long)m * T + t) * H + j, pre[bt][0]);
+        const float* a = p.acts + ((long long)t * B + m) * G + j;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) ldf4(a + g * H, pre[bt][1 + g]);
+        ldf4(p.tcs + ((long long)t * B + m) * H + j, pre[bt][5]);
+        ldf4(t > 0 ? p.cs + ((long long)(t - 1) * B + m) * H + j : (p.c0 ? p.c0 + (long long)m * H + j : nullptr),
+             pre[bt][6]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 7; ++q) pre[bt][q][0] = pre[bt][q][1] = pre[bt][q][2] = pre[bt][q][3] = 0.f;
+      }
+    }
+    v4f acc[NBT];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) acc[bt] = v4f{0.f, 0.f, 0.f, 0.f};
+    if (t + 1 < T) {
+      if (!mp_wait<SC>(cnt, (T - 1 - t) * (int)gridDim.x, err)) return;
+      const bf16_t* gb = p.dg + (long long)(t + 1) * G;  // dg_{t+1} rows, stride T·G
+#pragma unroll
+      for (int kc = 0; kc < kMpMaxKCb; ++kc) {  // chunks past 4H hold zero fragments (no branch: keeps wf in VGPRs)
+        const int k = kc * 32 + fq * 8;
+        const bool kin = kc < KC && k < G;
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) {
+          const int m = bt * 16 + fr;
+          const v8s gf = (kin && m < B) ? xld8<SC>(gb + (long long)m * T * G + k) : zero;
+          acc[bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], gf, acc[bt], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m >= B || !jin) continue;
+      float di[4], dgg[4], df[4], dout[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float i = pre[bt][1][e], g = pre[bt][2][e], f = pre[bt][3][e], o = pre[bt][4][e], tcv = pre[bt][5][e];
+        const float d_h = pre[bt][0][e] + acc[bt][e];
+        const float d_c = d_h * o * (1.f - tcv * tcv) + dc[bt][e];
+        di[e] = d_c * g * i * (1.f - i);
+        dgg[e] = d_c * i * (1.f - g * g);
+        df[e] = d_c * pre[bt][6][e] * f * (1.f - f);
+        dout[e] = d_h * tcv * o * (1.f - o);
+        dc[bt][e] = d_c * f;
+      }
+      bf16_t* o = p.dg + ((long long)m * T + t) * G + j;
+      xst4<SC>(o, di);
+      xst4<SC>(o + H, dgg);
+      xst4<SC>(o + 2 * H, df);
+      xst4<SC>(o + 3 * H, dout);
+    }
+    if (t > 0) mp_arrive<SC>(cnt);
+  }
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int m = bt * 16 + fr;
+    if (m < B && jin) stf4(p.gc + (long long)m * H + j, dc[bt]);
+  }
+}
+
+// Resident-weight multi-workgroup path: B ≤ 32, 8 ≤ H ≤ 256, H % 8 == 0, a sync word pair given.
+// OPT-IN (BIGDL_RNN_PERSIST=2).  Measured at the PTB shape (B 20, H 200, T 20, 2 layers) it is
+// SLOWER than one k_rnn_step launch per step — 1.34 (fence protocol) / 1.40 (scoped accesses) vs
+// 1.05–1.12 ms per training step, profiles/r3_ptb_persist_ab.txt: the step-to-step hand-off crosses
+// XCDs (each has its own L2), so every step pays device-coherent store → counter → poll → load round
+// trips at memory-side latency, which costs more than the back-to-back launch of the next step
+// whose h reads hit L2.
+static bool lstm_mp_sc() {
+  const char* e = getenv("BIGDL_RNN_MP_SYNC");
+  return !(e && e[0] == '0');
+}
+
+static bool lstm_mp_ok(int B, int H, const int* sync) {
+  const char* e = getenv("BIGDL_RNN_PERSIST");
+  if (!e || e[0] != '2') return false;
+  return sync && B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
+}
+
 // The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0).  It is OPT-IN
 // (BIGDL_RNN_PERSIST=1): one CU re-streams all of U from L2 every step, and a single CU's L2 read
 // rate (tens of GB/s) makes that ~3× slower than the 13-workgroup step launches at the PTB shape
@@ -599,13 +888,36 @@ static bool lstm_persist_ok(int B, int H) {
 static const bf16_t* bo(const void* p, long long off) { return p ? (const bf16_t*)p + off : nullptr; }
 
 BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, const float* c0, const void* U, void* out,
-                                    float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H,
+                                    float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H, int* sync,
                                     hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !U || !out) return (int)hipErrorInvalidValue;
   const bool train = cs && acts && tcs;
   if (!train && !cbuf) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
   const int esz = x_f32 ? 4 : 2;
+  if (lstm_mp_ok(B, H, sync)) {
+    if (!a16(U) || !a16(h0) || !a16(out) || (x_f32 ? !a16(x2) : !a8(x2)) || ((uintptr_t)sync & 7))
+      return (int)hipErrorInvalidValue;
+    const void* f32s[] = {c0, cs, acts, tcs, cbuf};
+    for (const void* q : f32s)
+      if (q && !a16(q)) return (int)hipErrorInvalidValue;
+    LstmSeqP p{};
+    p.x2 = x2; p.x_f32 = x_f32; p.h0 = (const bf16_t*)h0; p.c0 = c0; p.u = (const bf16_t*)U; p.out = (bf16_t*)out;
+    p.cs = train ? cs : nullptr; p.acts = acts; p.tcs = tcs; p.cbuf = train ? nullptr : cbuf;
+    p.B = B; p.T = T; p.H = H;
+    hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
+    if (e != hipSuccess) return (int)e;
+    const dim3 grid((unsigned)((H + 15) / 16));
+    const bool sc = lstm_mp_sc();
+    if (B <= 16) {
+      if (sc) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);
+      else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<1, false>), grid, dim3(64), 0, s, p, sync);
+    } else {
+      if (sc) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<2, true>), grid, dim3(64), 0, s, p, sync);
+      else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<2, false>), grid, dim3(64), 0, s, p, sync);
+    }
+    BIGDL_CHECK_LAUNCH();
+  }
   if (lstm_persist_ok(B, H)) {
     if (!a16(U) || !a8(h0) || !a8(out) || (x_f32 ? !a16(x2) : !a8(x2))) return (int)hipErrorInvalidValue;
     const void* f32s[] = {c0, cs, acts, tcs, cbuf};
@@ -635,9 +947,30 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
 }
 
 BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float* acts, const float* tcs, const float* cs,
-                                    const float* c0, void* DG, float* gc, int B, int T, int H, hipStream_t s) {
+                                    const float* c0, void* DG, float* gc, int B, int T, int H, int* sync,
+                                    hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !gy || !Ut || !DG || !gc) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
+  if (lstm_mp_ok(B, H, sync)) {
+    if (!acts || !tcs || !cs || !a16(Ut) || !a8(gy) || !a16(DG) || !a16(acts) || !a16(tcs) || !a16(cs) || !a16(gc) ||
+        (c0 && !a16(c0)) || ((uintptr_t)sync & 7))
+      return (int)hipErrorInvalidValue;
+    LstmSeqP p{};
+    p.u = (const bf16_t*)Ut; p.acts = (float*)acts; p.tcs = (float*)tcs; p.cs = (float*)cs; p.c0 = c0;
+    p.gy = (const bf16_t*)gy; p.dg = (bf16_t*)DG; p.gc = gc; p.B = B; p.T = T; p.H = H;
+    hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
+    if (e != hipSuccess) return (int)e;
+    const dim3 grid((unsigned)((H + 15) / 16));
+    const bool sc = lstm_mp_sc();
+    if (B <= 16) {
+      if (sc) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);
+      else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<1, false>), grid, dim3(64), 0, s, p, sync);
+    } else {
+      if (sc) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<2, true>), grid, dim3(64), 0, s, p, sync);
+      else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<2, false>), grid, dim3(64), 0, s, p, sync);
+    }
+    BIGDL_CHECK_LAUNCH();
+  }
   if (lstm_persist_ok(B, H)) {
     if (!acts || !tcs || !cs || !a16(Ut) || !a8(gy) || !a8(DG) || !a16(acts) || !a16(tcs) || !a16(cs) || !a16(gc) ||
         (c0 && !a16(c0)))

@@ -1898,6 +1898,20 @@ def _dense_bf16(*ts):
     return all(t is None or (t.is_cuda and t.is_contiguous() and _al16(t)) for t in ts)
 
 
+_RNN_SYNC = {}
+
+
+def _rnn_sync(device):
+    """Two int32 words (arrival counter, error flag) for the resident-weight LSTM kernels' grid
+    barrier, from a per-device ring of 32 slots (each launch zeroes its slot on the stream first)."""
+    ent = _RNN_SYNC.get(device)
+    if ent is None:
+        ent = _RNN_SYNC[device] = [torch.zeros(64, dtype=torch.int32, device=device), 0]
+    buf, i = ent
+    ent[1] = (i + 1) % 32
+    return buf[2 * i:2 * i + 2]
+
+
 def lstm_seq_forward(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
     """Whole-sequence fused LSTM forward (bigdl_lstm_seq_fwd): x2 [B][T][4H], out [B][T][H]; training
     saves cs / tcs [T][B][H], acts [T][B][4H] (fp32), inference ping-pongs c through cbuf [2][B][H]."""
@@ -1905,15 +1919,16 @@ def lstm_seq_forward(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
     H = G // 4
     assert _dense_bf16(x2, h0, c0, U, out, cs, acts, tcs, cbuf) and tuple(out.shape) == (B, T, H), "lstm_seq_forward"
     check(_lib().bigdl_lstm_seq_fwd(ptr(x2), C.c_int(1 if x2.dtype == _f32 else 0), ptr(h0), ptr(c0), ptr(U), ptr(out),
-                                    ptr(cs), ptr(acts), ptr(tcs), ptr(cbuf), C.c_int(B), C.c_int(T), C.c_int(H), _s()),
-          "lstm_seq_fwd")
+                                    ptr(cs), ptr(acts), ptr(tcs), ptr(cbuf), C.c_int(B), C.c_int(T), C.c_int(H),
+                                    ptr(_rnn_sync(x2.device)), _s()), "lstm_seq_fwd")
 
 
 def lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc):
     B, T, H = gy.shape
     assert _dense_bf16(gy, Ut, acts, tcs, cs, c0, DG, gc), "lstm_seq_backward"
     check(_lib().bigdl_lstm_seq_bwd(ptr(gy), ptr(Ut), ptr(acts), ptr(tcs), ptr(cs), ptr(c0), ptr(DG), ptr(gc),
-                                    C.c_int(B), C.c_int(T), C.c_int(H), _s()), "lstm_seq_bwd")
+                                    C.c_int(B), C.c_int(T), C.c_int(H), ptr(_rnn_sync(gy.device)), _s()),
+          "lstm_seq_bwd")
 
 
 def gru_seq_forward(x2, h0, Urz, Uh, out, R, Z, Nn, RH, train):
