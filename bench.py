@@ -100,6 +100,10 @@ def _build(args, dev, rank):
         for m in model.flattened_modules():
             if isinstance(m, SpatialBatchNormalization):
                 m.setParallism(2)
+                if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+                    # one rank: still run the cross-rank kernels (local sums -> finalize from sums),
+                    # the 1-rank collective being the identity
+                    m.set_sync_group(None, True, force=True)
     crit = CrossEntropyCriterion()
     sgd = SGD(learningrate=0.1, learningrate_decay=0.0, weightdecay=1e-4, momentum=0.9, dampening=0.0,
               nesterov=True)

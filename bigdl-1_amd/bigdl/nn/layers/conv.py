@@ -171,7 +171,7 @@ class SpatialConvolution(TensorModule):
         for bn in self._tail_candidates or ():
             y = bn.output
             if (isinstance(y, torch.Tensor) and y.data_ptr() == x.data_ptr() and y.shape == x.shape and bn.train
-                    and getattr(bn, "_last_relu", False) and not getattr(bn, "_sync", False)
+                    and getattr(bn, "_last_relu", False)
                     and bn._last_input is not None and bn._last_input.shape == x.shape):
                 return bn
         return None
@@ -233,7 +233,7 @@ class SpatialConvolution(TensorModule):
         bn = self._bn_bwd_target
         bn_fuse = None
         if (bn is not None and need_input and res is None and pt == pb and pl == pr and self.format == "NCHW"
-                and batched and gy.is_cuda and bn.train and bn._fused_relu and not getattr(bn, "_sync", False)
+                and batched and gy.is_cuda and bn.train and bn._fused_relu
                 and bn._coef is not None and bn._last_input is not None
                 and config.get_property("bigdl.fusion.bnbwd")):
             C_ = bn._coef.numel() // 2

@@ -199,6 +199,16 @@ class BatchNormalization(TensorModule):
                 y = torch.relu(y)
         return y.reshape(input.shape) if input.dim() == 1 else y
 
+    def _sync_allreduce(self, t):
+        """Sum ``t`` over the sync group in place; a one-rank group (the forced world-size-1
+        rehearsal) is the identity, so no collective is issued."""
+        import torch.distributed as dist
+        ws = self.__dict__.get("_sync_ws")
+        if ws is None or ws[0] is not self._sync_group:
+            ws = self.__dict__["_sync_ws"] = (self._sync_group, dist.get_world_size(self._sync_group))
+        if ws[1] > 1:
+            dist.all_reduce(t, group=self._sync_group)
+
     def _sync_count(self, x):
         """Rows over all ranks of the sync group (one collective per new input shape, cached)."""
         import torch.distributed as dist
@@ -208,7 +218,7 @@ class BatchNormalization(TensorModule):
         if n is None:
             t = torch.tensor([float(x.numel() // x.shape[1])], dtype=torch.float64,
                              device=x.device if dist.get_backend(self._sync_group) == "nccl" else "cpu")
-            dist.all_reduce(t, group=self._sync_group)
+            self._sync_allreduce(t)
             n = cache[key] = int(t.item())
         return n
 
@@ -233,7 +243,7 @@ class BatchNormalization(TensorModule):
             sums = NO.bn_local_sums(x, shift)
         if sums is NotImplemented:
             return NotImplemented
-        dist.all_reduce(sums, group=self._sync_group)
+        self._sync_allreduce(sums)
         coef = self._coef
         if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
             coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
@@ -281,11 +291,15 @@ class BatchNormalization(TensorModule):
         cbs = prod.scale_b if prod is not None else 0.0
         gres = None
         if self._sync_active() and self.train:
+            # gy already ReLU-masked by the consumer conv's dgrad epilogue (which also left the
+            # backward partials): it is then also exactly the residual branch's gradient
+            pg = self._pending_grad
+            pre_masked = pg is not None and pg[0] == gy.data_ptr()
             gi, cb_done = self._sync_backward(x, gy, g, y, need_input, acc, relu, cb, cbs)
             if cb is not None and gi is not None and not cb_done:
                 cb.add_(acc_float(gi).sum([d for d in range(gi.dim()) if d != 1]), alpha=cbs)
             if want_gres:
-                gres = gy * (y > 0).to(gy.dtype) if relu else gy
+                gres = gy * (y > 0).to(gy.dtype) if (relu and not pre_masked) else gy
         else:
             same = self.scale_w == self.scale_b
             pg, self._pending_grad = self._pending_grad, None
@@ -346,7 +360,7 @@ class BatchNormalization(TensorModule):
             if both is not NotImplemented:
                 C2 = 2 * x.shape[1]
                 loc, glob = both[:C2], both[C2:]
-                dist.all_reduce(glob, group=self._sync_group)
+                self._sync_allreduce(glob)
                 gi = NO.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, self._sync_count(x),
                                               y=y, relu=relu, need_input=need_input,
                                               gg_acc=self.gradWeight if (acc and self.affine) else None,
@@ -366,7 +380,7 @@ class BatchNormalization(TensorModule):
         n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
         s = torch.cat([gf.sum(dims), (gf * xhat).sum(dims), n])
         local_db, local_dg = s[:C].clone(), s[C:2 * C].clone()
-        dist.all_reduce(s, group=self._sync_group)
+        self._sync_allreduce(s)
         db, dg, cnt = s[:C], s[C:2 * C], s[-1]
         if acc and self.affine:
             self.gradWeight.add_(local_dg, alpha=self.scale_w)

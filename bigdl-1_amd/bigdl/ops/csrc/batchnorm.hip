@@ -188,9 +188,7 @@ __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const fl
 // BITS (with RELU): also emit the ReLU mask as one byte per 8-channel chunk (bit e = output channel
 // cg·8 + e is > 0) — a ResNet block tail's output mask for the backward, 1/16 of the bytes of
 // re-reading the bf16 output there.
-constexpr int kApplyUnroll = 4;
-
-template <bool RES, bool RELU, bool BITS = false>
+template <bool RES, bool RELU, bool BITS = false, int kApplyUnroll = 4>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                   bf16_t* __restrict__ y, long long M, int C,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
@@ -249,12 +247,31 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   }
 }
 
+// A/B knobs (profiles/r3_bn_apply_ab.txt): BIGDL_BN_APPLY_BLOCKS caps the grid (default 1024: 0.87-1.06
+// of the best streaming copy in isolation vs 0.64-0.98 at 2048; neutral inside the ResNet step),
+// BIGDL_BN_UNROLL=1 issues one row per trip instead of 4.
+static int apply_cap() {
+  static int cap = [] {
+    const char* e = getenv("BIGDL_BN_APPLY_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 ? v : 1024;
+  }();
+  return cap;
+}
+static bool apply_unroll1() {
+  static bool u1 = [] {
+    const char* e = getenv("BIGDL_BN_UNROLL");
+    return e && e[0] == '1';
+  }();
+  return u1;
+}
+
 static int apply_grid(long long M, int C) {
   int CG = C / 8;
   int tpr = CG < 256 ? CG : 256;
   int rpi = 256 / tpr;
   long long blocks = (M + rpi - 1) / rpi;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > apply_cap()) blocks = apply_cap();
   if (blocks < 1) blocks = 1;
   return (int)blocks;
 }
@@ -266,6 +283,17 @@ static void launch_apply(const void* x, const void* res, void* y, long long M, i
   const bf16_t* rr = (const bf16_t*)res;
   bf16_t* yr = (bf16_t*)y;
   uint8_t* br = (uint8_t*)bits;
+  if (apply_unroll1()) {
+    if (relu && bits && res)
+      hipLaunchKernelGGL((k_bn_apply<true, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    else if (relu && bits)
+      hipLaunchKernelGGL((k_bn_apply<false, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    else if (res) hipLaunchKernelGGL((k_bn_apply<true, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    else hipLaunchKernelGGL((k_bn_apply<false, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    return;
+  }
   if (relu && bits && res)
     hipLaunchKernelGGL((k_bn_apply<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
   else if (relu && bits)
@@ -490,7 +518,7 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __rest
   if (cbias) cbias[c] += cbscale * (A * dbeta + B * (float)M * mean[c] + (float)M * Cc);
 }
 
-template <bool RELU, bool GRES>
+template <bool RELU, bool GRES, int kApplyUnroll = 4>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ y, bf16_t* __restrict__ gx,
                                                       bf16_t* __restrict__ gres, long long M, int C,
@@ -566,9 +594,9 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
     const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;
     bf16_t *gx_ = (bf16_t*)gx, *gr_ = (bf16_t*)gres;
     if (relu && gres) hipLaunchKernelGGL((k_bn_bwd_apply<true, true>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
-    else if (relu) hipLaunchKernelGGL((k_bn_bwd_apply<true, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+    else if (relu) hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<true, false, 1> : k_bn_bwd_apply<true, false, 4>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
     else if (gres) hipLaunchKernelGGL((k_bn_bwd_apply<false, true>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
-    else hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
+    else hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<false, false, 1> : k_bn_bwd_apply<false, false, 4>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, gr_, M, C, coef);
   }
   BIGDL_CHECK_LAUNCH();
 }
@@ -589,7 +617,7 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
                        invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx) {
     int grid = apply_grid(M, C);
-    hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,
+    hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<false, false, 1> : k_bn_bwd_apply<false, false, 4>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,
                        (const bf16_t*)x, (const bf16_t*)nullptr, (bf16_t*)gx, (bf16_t*)nullptr, M, C, coef);
   }
   BIGDL_CHECK_LAUNCH();
@@ -722,10 +750,10 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
     const bf16_t *g_ = (const bf16_t*)gy, *x_ = (const bf16_t*)x, *y_ = (const bf16_t*)y;
     bf16_t* gx_ = (bf16_t*)gx;
     if (relu)
-      hipLaunchKernelGGL((k_bn_bwd_apply<true, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M, C,
+      hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<true, false, 1> : k_bn_bwd_apply<true, false, 4>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M, C,
                          coef);
     else
-      hipLaunchKernelGGL((k_bn_bwd_apply<false, false>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M,
+      hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<false, false, 1> : k_bn_bwd_apply<false, false, 4>), dim3(grid), dim3(256), 0, s, g_, x_, y_, gx_, (bf16_t*)nullptr, M,
                          C, coef);
   }
   BIGDL_CHECK_LAUNCH();
