@@ -394,9 +394,9 @@ class SpatialFullConvolution(AutogradModule):
         g = self.nGroup
         w4 = w.reshape(g * w.shape[1], w.shape[2], self.kH, self.kW)
         b = self.P("bias") if not self.noBias else None
-        if inp.is_cuda and g == 1 and ops.native_has("conv2d_forward"):
+        if inp.is_cuda and ops.native_has("conv2d_forward"):
             y = ops.native_ops.conv_transpose2d(to_device_layout(inp), w4, b, (self.dH, self.dW),
-                                                (self.padH, self.padW), adj)
+                                                (self.padH, self.padW), adj, g)
             if y is not NotImplemented:
                 return y if batched else y.squeeze(0)
             ops.native.note_fallback("conv_transpose2d", "geometry", (inp, w4))

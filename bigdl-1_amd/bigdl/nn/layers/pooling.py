@@ -373,8 +373,16 @@ class ResizeBilinear(AutogradModule):
         self.oh, self.ow, self.alignCorners, self.format = output_height, output_width, align_corner, data_format
 
     def _forward(self, x):
+        """TensorFlow-style sampling as the reference (``nn/ResizeBilinear.scala:266-284,406-412``:
+        src = dst·in/out, no half-pixel offset) — not ``F.interpolate``'s half-pixel centres."""
         nhwc = self.format == "NHWC"
         if nhwc:
             x = x.permute(0, 3, 1, 2)
-        y = F.interpolate(x, size=(self.oh, self.ow), mode="bilinear", align_corners=self.alignCorners)
+        y = NotImplemented
+        if x.is_cuda and ops.native_has("resize_bilinear"):
+            xd = x if x.dtype != torch.bfloat16 else x.contiguous(memory_format=torch.channels_last)
+            y = ops.native_ops.resize_bilinear(xd, self.oh, self.ow, self.alignCorners)
+        if y is NotImplemented:
+            from ...ops.reference import resize_bilinear
+            y = resize_bilinear(x, self.oh, self.ow, self.alignCorners)
         return y.permute(0, 2, 3, 1) if nhwc else y

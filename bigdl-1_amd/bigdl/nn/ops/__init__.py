@@ -471,9 +471,9 @@ class ResizeBilinearOps(Operation):
         self.alignCorner = align_corner
 
     def updateOutput(self, t):
+        from ...ops.reference import resize_bilinear
         x, size = t[1], [int(v) for v in t[2].flatten().tolist()]
-        y = F.interpolate(x.permute(0, 3, 1, 2).float(), size=size, mode="bilinear",
-                          align_corners=self.alignCorner)
+        y = resize_bilinear(x.permute(0, 3, 1, 2).float(), size[0], size[1], self.alignCorner)
         return y.permute(0, 2, 3, 1).contiguous().to(x.dtype if x.is_floating_point() else torch.float32)
 
 

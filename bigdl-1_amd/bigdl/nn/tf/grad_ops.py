@@ -432,9 +432,10 @@ class ResizeBilinearGrad(Operation):
         g, img = _vals(t)[:2]
         size = [g.shape[1], g.shape[2]]
 
+        from ...ops.reference import resize_bilinear
+
         def fwd(x):
-            y = F.interpolate(x.permute(0, 3, 1, 2), size=size, mode="bilinear", align_corners=self.alignCorners)
-            return y.permute(0, 2, 3, 1)
+            return resize_bilinear(x.permute(0, 3, 1, 2), size[0], size[1], self.alignCorners).permute(0, 2, 3, 1)
         return _vjp(fwd, img, g).to(g.dtype if g.is_floating_point() else torch.float32)
 
 

@@ -2369,12 +2369,67 @@ class _DeconvFn(torch.autograd.Function):
         return gx, gw.to(w.dtype), gb, None, None, None
 
 
-def conv_transpose2d(x, w, b, stride, pad, adj=(0, 0)):
-    """Differentiable native transposed conv (groups 1); NotImplemented when not eligible.
-    ``w``: [C_in][C_out][R][S]."""
+class _GroupedDeconvFn(torch.autograd.Function):
+    """Grouped transposed convolution (SpatialFullConvolution nGroup > 1) on the single-launch
+    grouped conv kernels: with W [C_in][C_out/G][R][S] the weight of the grouped conv whose
+    backward-data this is, the forward is that conv's data gradient (x on the stride lattice, each
+    group's flipped, transposed filter), the input gradient is that conv's forward of dY, and the
+    weight gradient is its grouped weight gradient with input = dY and output gradient = x."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, out_hw, groups):
+        N_, Cin, H, W = x.shape
+        _, Cog, R, S = w.shape
+        src = x
+        if tuple(stride) != (1, 1):
+            src = torch.empty((N_, Cin, (H - 1) * stride[0] + 1, (W - 1) * stride[1] + 1), dtype=_bf16,
+                              device=x.device, memory_format=torch.channels_last).zero_()
+            src[:, :, ::stride[0], ::stride[1]] = x
+        Cig = Cin // groups
+        wt = w.detach().reshape(groups, Cig, Cog, R, S).flip(3, 4).transpose(1, 2).reshape(groups * Cog, Cig, R, S)
+        y = _conv_fwd_grouped_1(src, wt, b, (1, 1), (R - 1 - pad[0], S - 1 - pad[1]), (1, 1), groups, out_hw=out_hw)
+        if y is NotImplemented:
+            raise RuntimeError("native grouped transposed conv refused its geometry after the eligibility check")
+        ctx.save_for_backward(x, w)
+        ctx.geom = (tuple(stride), tuple(pad), groups, b is not None, None if b is None else b.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, pad, groups, has_b, bdt = ctx.geom
+        gb = gy.float().sum((0, 2, 3)).to(bdt) if has_b else None
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = _conv_fwd_grouped_1(gy, w.detach().to(_bf16), None, stride, pad, (1, 1), groups,
+                                     out_hw=(x.shape[2], x.shape[3]))
+            if gx is NotImplemented:
+                raise RuntimeError("native grouped transposed-conv backward-data refused its geometry")
+        gw = torch.zeros(w.shape, dtype=_f32, device=w.device)
+        r = _conv_bwd_grouped_1(x, gy, w.detach().to(_bf16), stride, pad, (1, 1), groups, False, gw, None, 1.0)
+        if r is NotImplemented:
+            raise RuntimeError("native grouped transposed-conv weight gradient refused its geometry")
+        return gx, gw.to(w.dtype), gb, None, None, None, None
+
+
+def conv_transpose2d(x, w, b, stride, pad, adj=(0, 0), groups=1):
+    """Differentiable native transposed conv; NotImplemented when not eligible.
+    ``w``: [C_in][C_out / groups][R][S]."""
     if not (x.is_cuda and x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last)
             and _al16(x) and w.dim() == 4 and w.shape[0] == x.shape[1]):
         return NotImplemented
+    if groups > 1:
+        Cin, Cog, R, S = w.shape
+        H, W = x.shape[2], x.shape[3]
+        oh = (H - 1) * stride[0] - 2 * pad[0] + R + adj[0]
+        ow = (W - 1) * stride[1] - 2 * pad[1] + S + adj[1]
+        if Cin % groups or oh <= 0 or ow <= 0 or adj[0] >= max(stride[0], 1) or adj[1] >= max(stride[1], 1):
+            return NotImplemented
+        Cig = Cin // groups
+        if _group_pack(groups, Cig, Cog) is None or _group_pack(groups, Cog, Cig) is None:
+            return NotImplemented
+        return _GroupedDeconvFn.apply(x, w, b, tuple(stride), tuple(pad), (oh, ow), groups)
     Cin, Cout, R, S = w.shape
     if Cin % 8 or Cout % 8:
         return NotImplemented
@@ -2386,6 +2441,40 @@ def conv_transpose2d(x, w, b, stride, pad, adj=(0, 0)):
     if stride[0] == 1 and stride[1] == 1 and (R - 1 - pad[0] < 0 or S - 1 - pad[1] < 0):
         return NotImplemented
     return _DeconvFn.apply(x, w, b, tuple(stride), tuple(pad), (oh, ow))
+
+
+# ------------------------------------------------------------------------------------------------ bilinear resize
+class _ResizeFn(torch.autograd.Function):
+    """Bilinear resize (reference sampling) on resize.hip: NHWC bf16 forward, fp32-atomic backward."""
+
+    @staticmethod
+    def forward(ctx, x, oh, ow, align):
+        N_, C_, H, W = x.shape
+        y = torch.empty((N_, C_, oh, ow), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+        check(_lib().bigdl_resize_bilinear_fwd(ptr(x), ptr(y), N_, H, W, C_, oh, ow, int(bool(align)), _s()),
+              "resize_bilinear_fwd")
+        ctx.geom = (N_, C_, H, W, oh, ow, int(bool(align)))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        N_, C_, H, W, oh, ow, align = ctx.geom
+        gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+        gx = torch.zeros((N_, H, W, C_), dtype=_f32, device=gy.device)
+        check(_lib().bigdl_resize_bilinear_bwd(ptr(gy), ptr(gx), N_, H, W, C_, oh, ow, align, _s()),
+              "resize_bilinear_bwd")
+        return gx.permute(0, 3, 1, 2).to(_bf16), None, None, None
+
+
+def resize_bilinear(x, oh, ow, align=False):
+    """Differentiable native bilinear resize of an NCHW-logical bf16 channels-last tensor
+    (NotImplemented when not eligible; deterministic mode keeps the atomic-free reference)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == _bf16 and x.shape[1] % 8 == 0 and _al16(x)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return NotImplemented
+    if config.get_property("bigdl.deterministic"):
+        return NotImplemented
+    return _ResizeFn.apply(x, int(oh), int(ow), bool(align))
 
 
 # ------------------------------------------------------------------------------------------------ layer norm

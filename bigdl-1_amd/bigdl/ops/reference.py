@@ -103,6 +103,29 @@ def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups
                               dilation)
 
 
+# ------------------------------------------------------------------------- bilinear resize
+def _resize_axis(n_in, n_out, align, device):
+    """(lower, upper, lerp) per output index, the reference's sampling (ResizeBilinear.scala:266-284,
+    406-412): src = dst·scale, scale = in/out or (in−1)/(out−1) with alignCorners — no half-pixel."""
+    scale = (n_in - 1) / (n_out - 1) if (align and n_out > 1) else n_in / n_out
+    src = torch.arange(n_out, dtype=torch.float32, device=device) * torch.tensor(scale, dtype=torch.float32)
+    lo = src.to(torch.int64).clamp_max(n_in - 1)
+    hi = (lo + 1).clamp_max(n_in - 1)
+    return lo, hi, src - lo.to(torch.float32)
+
+
+def resize_bilinear(x, oh, ow, align=False):
+    """Differentiable bilinear resize of an NCHW tensor with the reference's sampling (fp32 math)."""
+    y0, y1, ly = _resize_axis(x.shape[2], oh, align, x.device)
+    x0, x1, lx = _resize_axis(x.shape[3], ow, align, x.device)
+    xf = x if x.dtype == torch.float64 else x.float()
+    top, bot = xf.index_select(2, y0), xf.index_select(2, y1)
+    lx_, ly_ = lx.to(xf.dtype).view(1, 1, 1, -1), ly.to(xf.dtype).view(1, 1, -1, 1)
+    t = top.index_select(3, x0) + (top.index_select(3, x1) - top.index_select(3, x0)) * lx_
+    b = bot.index_select(3, x0) + (bot.index_select(3, x1) - bot.index_select(3, x0)) * lx_
+    return (t + (b - t) * ly_).to(x.dtype)
+
+
 # ------------------------------------------------------------------------- batch norm
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
                             in_bias=None, coef_out=None, bits_out=None):

@@ -77,3 +77,36 @@ def test_resnext_block_grouped_conv_module():
     assert sum("k_conv_fwd" in n for n in ev) <= 6, ev
     assert _rel(y.float().cpu(), yr) < 3e-2
     assert _rel(gi.float().cpu(), gr) < 1e-1  # bf16 through two training BNs at 784 rows per channel
+
+
+@pytest.mark.parametrize("N,Cin,Cout,G,H,R,st,pd,adj", [
+    (2, 64, 32, 4, 9, 3, 2, 1, 1),
+    (2, 128, 128, 32, 7, 4, 2, 1, 0),
+    (2, 32, 64, 2, 8, 3, 1, 1, 0),
+])
+def test_grouped_transposed_conv_matches_fp32(N, Cin, Cout, G, H, R, st, pd, adj):
+    """SpatialFullConvolution nGroup > 1 on the single-launch grouped kernels vs F.conv_transpose2d."""
+    from bigdl.ops import native_ops as NO
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, Cin, H, H, generator=g).bfloat16()
+    w = (torch.randn(Cin, Cout // G, R, R, generator=g) * 0.1).bfloat16()
+    b = torch.randn(Cout, generator=g)
+    xr, wr, br = x.float().requires_grad_(), w.float().requires_grad_(), b.clone().requires_grad_()
+    yr = F.conv_transpose2d(xr, wr, br, st, pd, adj, G)
+    gy = torch.randn(yr.shape, generator=g).bfloat16()
+    yr.backward(gy.float())
+    xc = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_()
+    wc = w.float().to(dev).requires_grad_()
+    bc = b.to(dev).requires_grad_()
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        y = NO.conv_transpose2d(xc, wc, bc, (st, st), (pd, pd), (adj, adj), G)
+        assert y is not NotImplemented
+        y.backward(gy.to(dev))
+        torch.cuda.synchronize()
+    ev = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    assert sum("k_conv_fwd" in n for n in ev) == 2 and sum("k_conv_wgrad" in n for n in ev) == 1, ev
+    assert y.shape == yr.shape
+    assert _rel(y.cpu(), yr) < 1e-2
+    assert _rel(xc.grad.cpu(), xr.grad) < 1e-2
+    assert _rel(wc.grad.cpu(), wr.grad) < 1e-2
+    assert _rel(bc.grad.cpu(), br.grad) < 1e-3

@@ -150,8 +150,8 @@ def test_dilation2d_grads_and_resize_grad():
     torch.testing.assert_close(gf, _grad(lambda w: dil(x, w), f, g))
     img = torch.randn(1, 4, 4, 2)
     gr = torch.randn(1, 8, 8, 2)
-    up = lambda v: F.interpolate(v.permute(0, 3, 1, 2), size=(8, 8), mode="bilinear",  # noqa
-                                 align_corners=False).permute(0, 2, 3, 1)
+    from bigdl.ops.reference import resize_bilinear  # the reference's TF-style sampling
+    up = lambda v: resize_bilinear(v.permute(0, 3, 1, 2), 8, 8, False).permute(0, 2, 3, 1)  # noqa
     torch.testing.assert_close(T.ResizeBilinearGrad(False).forward(_T(gr, img)), _grad(up, img, gr))
 
 
