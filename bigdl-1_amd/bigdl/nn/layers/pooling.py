@@ -195,7 +195,12 @@ class VolumetricMaxPooling(AutogradModule):
         batched = x.dim() == 5
         if not batched:
             x = x.unsqueeze(0)
-        y = F.max_pool3d(x, self.k, self.d, self.p, ceil_mode=self.ceilMode)
+        y = NotImplemented
+        if x.is_cuda and x.dtype == torch.bfloat16 and ops.native_has("pool3d"):
+            y = ops.native_ops.pool3d(x.contiguous(memory_format=torch.channels_last_3d), 0, self.k, self.d, self.p,
+                                      self.ceilMode)
+        if y is NotImplemented:
+            y = F.max_pool3d(x, self.k, self.d, self.p, ceil_mode=self.ceilMode)
         return y if batched else y.squeeze(0)
 
 
@@ -210,7 +215,12 @@ class VolumetricAveragePooling(AutogradModule):
         batched = x.dim() == 5
         if not batched:
             x = x.unsqueeze(0)
-        y = F.avg_pool3d(x, self.k, self.d, self.p, self.ceilMode, self.countIncludePad)
+        y = NotImplemented
+        if x.is_cuda and x.dtype == torch.bfloat16 and ops.native_has("pool3d"):
+            y = ops.native_ops.pool3d(x.contiguous(memory_format=torch.channels_last_3d), 1, self.k, self.d, self.p,
+                                      self.ceilMode, self.countIncludePad)
+        if y is NotImplemented:
+            y = F.avg_pool3d(x, self.k, self.d, self.p, self.ceilMode, self.countIncludePad)
         return y if batched else y.squeeze(0)
 
 

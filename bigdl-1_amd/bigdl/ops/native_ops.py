@@ -2466,6 +2466,7 @@ class _ResizeFn(torch.autograd.Function):
         return gx.permute(0, 3, 1, 2).to(_bf16), None, None, None
 
 
+@register("resize_bilinear")
 def resize_bilinear(x, oh, ow, align=False):
     """Differentiable native bilinear resize of an NCHW-logical bf16 channels-last tensor
     (NotImplemented when not eligible; deterministic mode keeps the atomic-free reference)."""
@@ -2475,6 +2476,58 @@ def resize_bilinear(x, oh, ow, align=False):
     if config.get_property("bigdl.deterministic"):
         return NotImplemented
     return _ResizeFn.apply(x, int(oh), int(ow), bool(align))
+
+
+# ------------------------------------------------------------------------------------------------ 3-D pooling
+def _pool_out(n, k, s_, p_, ceil):
+    o = (n + 2 * p_ - k + ((s_ - 1) if ceil else 0)) // s_ + 1
+    if ceil and (o - 1) * s_ >= n + p_:
+        o -= 1
+    return o
+
+
+class _Pool3dFn(torch.autograd.Function):
+    """VolumetricMax/AveragePooling on pool3d.hip (NDHWC bf16; max keeps a uint8 window argmax)."""
+
+    @staticmethod
+    def forward(ctx, x, mode, k, st, pd, out, cip):
+        N_, C_, T, H, W = x.shape
+        OT, OH, OW = out
+        y = torch.empty((N_, C_, OT, OH, OW), dtype=_bf16, device=x.device, memory_format=_cl3)
+        idx = torch.empty((N_, OT, OH, OW, C_), dtype=torch.uint8, device=x.device) if mode == 0 else None
+        check(_lib().bigdl_pool3d_fwd(mode, ptr(x), ptr(y), ptr(idx), N_, T, H, W, C_, OT, OH, OW, k[0], k[1], k[2],
+                                      st[0], st[1], st[2], pd[0], pd[1], pd[2], int(bool(cip)), _s()), "pool3d_fwd")
+        if idx is not None:
+            ctx.save_for_backward(idx)
+        ctx.geom = (mode, k, st, pd, (N_, C_, T, H, W), out, int(bool(cip)))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        mode, k, st, pd, (N_, C_, T, H, W), (OT, OH, OW), cip = ctx.geom
+        idx = ctx.saved_tensors[0] if mode == 0 else None
+        gy = gy.to(_bf16).contiguous(memory_format=_cl3)
+        gx = torch.zeros((N_, T, H, W, C_), dtype=_f32, device=gy.device)
+        check(_lib().bigdl_pool3d_bwd(mode, ptr(gy), ptr(idx), ptr(gx), N_, T, H, W, C_, OT, OH, OW, k[0], k[1], k[2],
+                                      st[0], st[1], st[2], pd[0], pd[1], pd[2], cip, _s()), "pool3d_bwd")
+        return gx.permute(0, 4, 1, 2, 3).to(_bf16), None, None, None, None, None, None
+
+
+@register("pool3d")
+def pool3d(x, mode, k, st, pd, ceil=False, count_include_pad=True):
+    """Differentiable native 3-D pooling (mode 0 max, 1 average) of an NCDHW-logical bf16 tensor;
+    NotImplemented when not eligible (deterministic mode keeps the atomic-free reference)."""
+    if not (x.is_cuda and x.dim() == 5 and x.dtype == _bf16 and x.shape[1] % 8 == 0 and _al16(x)
+            and x.is_contiguous(memory_format=_cl3)):
+        return NotImplemented
+    if config.get_property("bigdl.deterministic") or k[0] * k[1] * k[2] > 255:
+        return NotImplemented
+    if any(p_ * 2 > kk for p_, kk in zip(pd, k)):
+        return NotImplemented  # torch's rule: pad ≤ kernel / 2 (windows always touch the input)
+    out = tuple(_pool_out(n, kk, s_, p_, ceil) for n, kk, s_, p_ in zip(x.shape[2:], k, st, pd))
+    if min(out) <= 0:
+        return NotImplemented
+    return _Pool3dFn.apply(x, mode, tuple(k), tuple(st), tuple(pd), out, count_include_pad)
 
 
 # ------------------------------------------------------------------------------------------------ layer norm

@@ -65,3 +65,18 @@ def test_native_resize_matches_reference(N, C, H, W, oh, ow, align):
     assert any("k_resize_bilinear_fwd" in n for n in names) and any("k_resize_bilinear_bwd" in n for n in names)
     torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(xc.grad.float().cpu(), xr.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_resize_module_runs_native():
+    from bigdl.nn import ResizeBilinear
+    m = ResizeBilinear(12, 14)
+    x = torch.randn(2, 16, 5, 7).bfloat16().cuda()
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        y = m.forward(x)
+        m.backward(x, torch.ones_like(y))
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    assert any("k_resize_bilinear_fwd" in n for n in names) and any("k_resize_bilinear_bwd" in n for n in names)
+    from bigdl.ops.reference import resize_bilinear
+    torch.testing.assert_close(y.float().cpu(), resize_bilinear(x.float().cpu(), 12, 14), rtol=1e-2, atol=1e-2)
