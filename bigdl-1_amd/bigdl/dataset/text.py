@@ -194,8 +194,13 @@ class TextToSentenceWithSteps(Transformer):
 
 
 class LabeledSentenceToSample(Transformer):
-    """LabeledSentence → Sample.  ``one_hot``: feature ``[len, vocab]`` one-hot, padded with the
-    end token; labels +1 (1-based); otherwise index features (+1) of fixed length."""
+    """LabeledSentence → Sample (``dataset/text/LabeledSentenceToSample.scala``).
+
+    ``one_hot`` (default): feature ``[len, vocab]`` one-hot of the 0-based word indices, rows past
+    the sentence set at the END token (the last label); labels +1 (1-based class ids), padded with
+    the START token (the first data index) + 1.  ``one_hot=False``: feature and label are the raw
+    index arrays copied as they are (the PTB reader already made them 1-based), truncated or
+    zero-padded to the fixed lengths."""
 
     def __init__(self, vocab_length: int, fix_data_length: Optional[int] = None,
                  fix_label_length: Optional[int] = None, one_hot: bool = True):
@@ -205,18 +210,22 @@ class LabeledSentenceToSample(Transformer):
         for s in it:
             dl = self.fd or s.dataLength()
             ll = self.fl or s.labelLength()
-            end_tok = 0 if ll == 1 else int(s.getLabel(s.labelLength() - 1))
             if self.one_hot:
+                start_tok = int(s.getData(0))
+                end_tok = 0 if ll == 1 else int(s.getLabel(s.labelLength() - 1))
                 feat = torch.zeros(dl, self.V)
                 n = min(s.dataLength(), dl)
                 feat[torch.arange(n), torch.as_tensor(s.data()[:n], dtype=torch.long)] = 1.0
                 if n < dl:
                     feat[n:, end_tok] = 1.0
+                lab = torch.full((ll,), float(start_tok + 1))
+                m = min(s.labelLength(), ll)
+                lab[:m] = torch.as_tensor(s.label()[:m]) + 1
             else:
-                feat = torch.full((dl,), float(end_tok + 1))
+                feat = torch.zeros(dl)
                 n = min(s.dataLength(), dl)
-                feat[:n] = torch.as_tensor(s.data()[:n]) + 1
-            lab = torch.full((ll,), float(end_tok + 1))
-            m = min(s.labelLength(), ll)
-            lab[:m] = torch.as_tensor(s.label()[:m]) + 1
+                feat[:n] = torch.as_tensor(s.data()[:n])
+                lab = torch.zeros(ll)
+                m = min(s.labelLength(), ll)
+                lab[:m] = torch.as_tensor(s.label()[:m])
             yield Sample(feat, lab)

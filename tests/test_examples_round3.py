@@ -179,3 +179,68 @@ def test_tree_lstm_sentiment_example(tmp_path):
     _sst(d)
     model = E.main(["-b", d, "--glove", "glove/g.txt", "-i", "8", "-h", "16", "-e", "2", "-p", "0.0", "-l", "0.1"])
     assert model is not None
+
+
+def _ptb(d):
+    rng = random.Random(0)
+    words = [f"w{i}" for i in range(40)]
+    for split, n in (("train", 120), ("valid", 30), ("test", 30)):
+        with open(os.path.join(d, f"ptb.{split}.txt"), "w") as f:
+            for _ in range(n):
+                f.write(" " + " ".join(rng.choice(words[:25] if split == "train" else words) for _ in range(8)) + " \n")
+
+
+def test_languagemodel_ptbwordlm_example(tmp_path):
+    from bigdl.example import languagemodel as E
+    d = str(tmp_path)
+    _ptb(d)
+    train, valid, test, dic = E.sequence_preprocess(d, 20)
+    assert dic.get_vocab_size() == 19 and min(train) >= 1.0 and max(train) <= 20.0
+    assert E.reader([1.0, 2.0, 3.0, 4.0, 5.0, 6.0], 2) == [[1.0, 2.0, 3.0], [3.0, 4.0, 5.0]]
+    mb = next(iter(E.to_dataset(train, 5, 4).data(train=False)))
+    x, y = mb.getInput(), mb.getTarget()
+    assert x.shape == (4, 5) and torch.equal(x[0, 1:], y[0, :-1])  # next-word targets, ids unchanged
+    model, loss = E.main(["-f", d, "-b", "4", "--vocab", "20", "-h", "16", "--numLayers", "1", "--numSteps", "5",
+                          "-e", "1", "--test"])
+    assert model is not None and 0 < loss < 1e4
+
+
+def _val_seq(d, n=12, size=40):
+    from bigdl.dataset.seqfile import BGRImgToLocalSeqFile
+    rng = np.random.default_rng(3)
+    items = []
+    for i in range(n):
+        img = (rng.random((size, size, 3)) * 200).astype(np.uint8)
+        items.append((img, i % 5 + 1))
+    os.makedirs(os.path.join(d, "val"), exist_ok=True)
+    BGRImgToLocalSeqFile(6, os.path.join(d, "val", "part"))(items)
+
+
+def test_loadmodel_example_models_and_validator(tmp_path):
+    from bigdl.example import loadmodel as L
+    from bigdl.nn import Linear, LogSoftMax, Reshape, Sequential, SpatialAveragePooling, SpatialConvolution
+    from bigdl.serialization.caffe_persister import save_caffe
+    for f, s in ((L.AlexNet_OWT, 224), (L.AlexNet_OWT_graph, 224), (L.AlexNet, 227)):
+        m = f(7)
+        m.evaluate()
+        assert m.forward(torch.randn(2, 3, s, s)).shape == (2, 7)
+    d = str(tmp_path)
+    _val_seq(d)
+    # bigdl vgg16 / resnet paths with a small 224-input network
+    net = (Sequential().add(SpatialConvolution(3, 8, 3, 3, 2, 2)).add(SpatialAveragePooling(111, 111, 111, 111))
+           .add(Reshape([8])).add(Linear(8, 1000)).add(LogSoftMax()))
+    mp = str(tmp_path / "m.bigdl")
+    net.saveModule(mp, over_write=True)
+    for name in ("vgg16", "resnet"):
+        res = L.main(["-t", "bigdl", "-m", name, "-f", d, "--modelPath", mp, "-b", "4"])
+        assert res[0][0].result()[1] == 12
+    # caffe alexnet path: mean file of 256·256·3 pixel means, 227 crop
+    cnet = (Sequential().add(SpatialConvolution(3, 4, 3, 3, 2, 2)).add(SpatialAveragePooling(113, 113, 113, 113))
+            .add(Reshape([4])).add(Linear(4, 1000)).add(LogSoftMax()))
+    proto, weights = str(tmp_path / "a.prototxt"), str(tmp_path / "a.caffemodel")
+    save_caffe(cnet, proto, weights, overwrite=True)
+    mean = tmp_path / "mean.txt"
+    mean.write_text("\n".join(["100.0"] * (256 * 256 * 3)) + "\n")
+    res = L.main(["-t", "caffe", "-m", "alexnet", "-f", d, "--caffeDefPath", proto, "--modelPath", weights,
+                  "--meanFile", str(mean), "-b", "5"])
+    assert res[0][0].result()[1] == 12
