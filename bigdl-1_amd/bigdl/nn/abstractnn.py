@@ -659,11 +659,12 @@ class AbstractModule:
 
     def backward(self, input, gradOutput):
         conv_back = None
+        from ..ops.reference import BNGrad  # a deferred BN input gradient passes through as is
         if not isinstance(input, (torch.Tensor, Table)):
             conv_back = type(gradOutput)
             input = to_torch(input)
             gradOutput = to_torch(gradOutput)
-        elif not isinstance(gradOutput, (torch.Tensor, Table)):
+        elif not isinstance(gradOutput, (torch.Tensor, Table, BNGrad)):
             conv_back = type(gradOutput)
             gradOutput = to_torch(gradOutput)
         self._sync_for_timing()

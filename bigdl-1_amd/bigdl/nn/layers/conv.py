@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import ops
-from ...ops.reference import StridedGrad, as_dense
+from ...ops.reference import BNGrad, StridedGrad, as_dense
 from ...utils.engine import Engine
 from ...utils import config
 from ..abstractnn import AbstractModule, TensorModule, AutogradModule
@@ -215,10 +215,21 @@ class SpatialConvolution(TensorModule):
 
     def _backward(self, input, gradOutput, need_input, acc):
         x, pad, batched, pads = self._prep(input)
-        gy = gradOutput if batched else gradOutput.unsqueeze(0)
-        if self.format == "NHWC":
-            gy = gy.permute(0, 3, 1, 2)
-        gy = to_device_layout(gy)
+        if isinstance(gradOutput, BNGrad):
+            # a deferred BN input gradient: consumed in the backward prologues when this conv can
+            # (ops.native_ops.bngrad_consumable), built as a tensor otherwise
+            own = self.withBias and self._bias_folded_into is None and acc
+            if not (batched and self.format == "NCHW" and not own and ops.native_has("conv2d_backward")
+                    and ops.native_ops.bngrad_consumable(gradOutput, x, self._w4(self.cw("weight")),
+                                                          (self.strideH, self.strideW), pad, self.nGroup)):
+                gradOutput = gradOutput.dense()
+        if isinstance(gradOutput, BNGrad):
+            gy = gradOutput
+        else:
+            gy = gradOutput if batched else gradOutput.unsqueeze(0)
+            if self.format == "NHWC":
+                gy = gy.permute(0, 3, 1, 2)
+            gy = to_device_layout(gy)
         w4 = self._w4(self.cw("weight"))
         gw = self._w4(self.gradWeight) if acc else None
         same_scale = self.scale_b == self.scale_w

@@ -21,7 +21,7 @@ from ... import ops
 from ..abstractnn import TensorModule, AutogradModule
 from ..initialization_method import RandomUniform, Zeros, Ones, VariableFormats
 from .conv import to_device_layout
-from ...utils import acc_float
+from ...utils import acc_float, config
 
 
 class BatchNormalization(TensorModule):
@@ -199,6 +199,21 @@ class BatchNormalization(TensorModule):
                 y = torch.relu(y)
         return y.reshape(input.shape) if input.dim() == 1 else y
 
+    def _lazy_grad_ok(self, input, x):
+        """Return the input gradient deferred (a BNGrad) when the producing conv — the only consumer
+        of that gradient — is a 1×1 stride-1 native conv that applies it in its backward prologues."""
+        prod = self._bias_producer
+        if prod is None or input is not x or x.dim() != 4 or not x.is_cuda or x.dtype != torch.bfloat16:
+            return False
+        mode = int(config.get_property("bigdl.fusion.bnprologue"))
+        if mode <= 0 or (mode == 1 and x.shape[1] >= getattr(prod, "nInputPlane", 0)):
+            return False
+        k = (getattr(prod, "kernelH", 0), getattr(prod, "kernelW", 0), getattr(prod, "strideH", 0),
+             getattr(prod, "strideW", 0), getattr(prod, "padH", -1), getattr(prod, "padW", -1),
+             getattr(prod, "nGroup", 0))
+        return (k == (1, 1, 1, 1, 0, 0, 1) and prod.format == "NCHW" and x.shape[1] % 32 == 0
+                and x.is_contiguous(memory_format=torch.channels_last))
+
     def _sync_allreduce(self, t):
         """Sum ``t`` over the sync group in place; a one-rank group (the forced world-size-1
         rehearsal) is the identity, so no collective is issued."""
@@ -310,7 +325,8 @@ class BatchNormalization(TensorModule):
                     gy, x, g, self.saveMean, self.saveStd, pg[1], pg[2], need_input=need_input,
                     gg_acc=self.gradWeight if (acc and self.affine) else None,
                     gb_acc=self.gradBias if (acc and self.affine) else None,
-                    scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
+                    scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs,
+                    lazy=self._lazy_grad_ok(input, x))
                 if gi is not NotImplemented:
                     if gi is not None and input.dim() == 1:
                         gi = gi.reshape(input.shape)

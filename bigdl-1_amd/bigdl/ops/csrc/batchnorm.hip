@@ -623,6 +623,17 @@ BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, 
   BIGDL_CHECK_LAUNCH();
 }
 
+// Apply-only backward: gx = A·gm + B·x + Cc with precomputed coefficients (coef [3][C]) — the
+// materialisation of a deferred BN input gradient whose consumer could not take it as a prologue.
+BIGDL_EXPORT int bigdl_bn_bwd_apply_coef(const void* gm, const void* x, void* gx, long long M, int C,
+                                         const float* coef, hipStream_t s) {
+  if (C % 8 || M <= 0 || !gm || !x || !gx || !coef) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<false, false, 1> : k_bn_bwd_apply<false, false, 4>),
+                     dim3(apply_grid(M, C)), dim3(256), 0, s, (const bf16_t*)gm, (const bf16_t*)x,
+                     (const bf16_t*)nullptr, (bf16_t*)gx, (bf16_t*)nullptr, M, C, coef);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // ------------------------------------------------------------------------------------------------ SyncBN
 // Cross-rank BatchNormalization (P6 / X11, SpatialBatchNormalization.scala:1114-1151,1257-1329):
 // each rank reduces its partials to one [2][C] fp32 vector (Σ(x−K), Σ(x−K)² forward; Σg, Σg·(x−μ)

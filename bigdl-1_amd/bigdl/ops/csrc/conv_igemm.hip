@@ -81,6 +81,12 @@ struct ConvParams {
   // per-group element offsets of x (channels), w (filters·ldw) and y / bias (channels).
   int ldx;
   long long gx, gw, gy;
+  // BatchNorm-backward prologue (AT instantiations, pointwise mode): the A operand x is the
+  // gradient g' at a BN's output and ``ax`` that BN's input (same layout); the kernel reads
+  // A·g' + B·ax + Cc per channel (acoef = [3][C] fp32) — the BN's input gradient — instead of a
+  // materialised tensor (one fewer write + read of it per consumer).
+  const bf16_t* ax;
+  const float* acoef;
 };
 
 // Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
@@ -126,9 +132,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // loads with their own padding tests.  MODE 0: any C % 8 == 0.  MODE 3 (POINTWISE): a 1×1
 // filter with no padding (C % BK == 0) — every staged row is in bounds, the k-tile is a plain
 // channel offset, no tap mask at all (the bottleneck 1×1 convs and their dgrads, half the FLOPs).
-template <int BN, int MODE, int BM, int BK, bool D3 = false>
-__global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_conv_fwd(ConvParams p) {
+template <int BN, int MODE, int BM, int BK, bool D3 = false, bool AT = false>
+__global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)) k_conv_fwd(ConvParams p) {
   static_assert(!D3 || MODE == 0 || MODE == 1, "3-D: generic or tap-uniform gather only");
+  static_assert(!AT || MODE == 3, "BN-backward prologue: pointwise mode only");
   constexpr bool PW = MODE == 3;
   constexpr bool FAST = MODE == 1 || PW;
   constexpr int ROWS = BM + BN;
@@ -165,6 +172,11 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
   constexpr uint32_t OOB = 0xFFFFFFF0u;
+  // AT: the BN input rides along with the A operand (same offsets); coefficient tiles [3][BK] for
+  // two k-tiles in flight (slot = LDS stage of the tile)
+  const __amdgpu_buffer_rsrc_t axr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(AT ? p.ax : p.x), 0, (int)x_bytes, 0x00020000);
+  __shared__ __attribute__((aligned(16))) float acf[AT ? 2 : 1][3][AT ? BK : 4];
 
   // per-row gather state for the activation rows this thread stages
   int a_img[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
@@ -340,6 +352,54 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
       }
     }
   };
+  // AT: BN-input chunks at the A offsets (issued unconditionally like the A loads) and one float4 of
+  // the k-tile's coefficients for the first 3·BK/4 threads
+  auto load_aux = [&](int kt, bool live, uint4 (&xa)[A_CHUNKS], float4& cf) {
+    if constexpr (AT) {
+      const uint32_t dead = live ? 0u : 0x80000000u;
+      const int kb = live ? kt * BK : 0;
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const uint32_t off = (vmask[i] != 0 ? (uint32_t)(rbase[i] + kb) * 2u : OOB) | dead;
+        xa[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(axr, off, 0, 0));
+      }
+      if (tid < 3 * BK / 4) {
+        const int arr = tid / (BK / 4), q = tid - arr * (BK / 4);
+        cf = live ? *reinterpret_cast<const float4*>(p.acoef + (size_t)arr * p.C + kb + 4 * q)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  // AT: rewrite the A chunks as the BN input gradient (zero for rows past M), then stage as usual;
+  // also park the NEXT k-tile's coefficients in the other slot (read after the next barrier)
+  auto transform_a = [&](int buf, uint4 (&ra)[A_CHUNKS], const uint4 (&xa)[A_CHUNKS], const float4& cfn) {
+    if constexpr (AT) {
+      float Av[8], Bv[8], Cv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        Av[e] = acf[buf][0][col8 * 8 + e];
+        Bv[e] = acf[buf][1][col8 * 8 + e];
+        Cv[e] = acf[buf][2][col8 * 8 + e];
+      }
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        float g[8], xv[8], o[8];
+        unpack8(ra[i], g);
+        unpack8(xa[i], xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = vmask[i] != 0 ? fmaf(Av[e], g[e], fmaf(Bv[e], xv[e], Cv[e])) : 0.f;
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
+        ra[i] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      if (tid < 3 * BK / 4) {
+        const int arr = tid / (BK / 4), q = tid - arr * (BK / 4);
+        *reinterpret_cast<float4*>(&acf[buf ^ 1][arr][4 * q]) = cfn;
+      }
+    }
+  };
+
   auto store_tile = [&](int buf, const uint4 (&ra)[A_CHUNKS], const uint4 (&rb)[B_CHUNKS]) {
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
@@ -393,20 +453,38 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 ? 3 : 2)) k_con
   // hides under two compute phases (one barrier per k-tile; the loop is unrolled by two so both
   // register sets stay statically indexed — runtime-indexed vectors would go to scratch).
   uint4 ra0[A_CHUNKS], rb0[B_CHUNKS], ra1[A_CHUNKS], rb1[B_CHUNKS];
+  uint4 xa0[AT ? A_CHUNKS : 1], xa1[AT ? A_CHUNKS : 1];
+  float4 cf0 = make_float4(0.f, 0.f, 0.f, 0.f), cf1 = cf0;
   load_tile(0, true, ra0, rb0);
+  if constexpr (AT) load_aux(0, true, xa0, cf0);
   load_tile(1, KT > 1, ra1, rb1);
+  if constexpr (AT) {
+    load_aux(1, KT > 1, xa1, cf1);
+    if (tid < 3 * BK / 4) {  // tile 0's coefficients → slot 0 before the first transform
+      const int arr = tid / (BK / 4), q = tid - arr * (BK / 4);
+      *reinterpret_cast<float4*>(&acf[0][arr][4 * q]) = cf0;
+    }
+    __syncthreads();
+    transform_a(0, ra0, xa0, cf1);
+  }
   store_tile(0, ra0, rb0);
   __syncthreads();
   int kt = 0;
   for (; kt + 2 <= KT; kt += 2) {
     // lds[0] = tile kt; set 1 = tile kt+1 (in flight)
     load_tile(kt + 2, kt + 2 < KT, ra0, rb0);
+    if constexpr (AT) load_aux(kt + 2, kt + 2 < KT, xa0, cf0);
     compute(0);
+    if constexpr (AT) transform_a(1, ra1, xa1, cf0);
     store_tile(1, ra1, rb1);
     __syncthreads();
     load_tile(kt + 3, kt + 3 < KT, ra1, rb1);
+    if constexpr (AT) load_aux(kt + 3, kt + 3 < KT, xa1, cf1);
     compute(1);
-    if (kt + 2 < KT) store_tile(0, ra0, rb0);
+    if (kt + 2 < KT) {
+      if constexpr (AT) transform_a(0, ra0, xa0, cf1);
+      store_tile(0, ra0, rb0);
+    }
     __syncthreads();
   }
   if (kt < KT) {  // odd KT: the last tile sits in lds[0]
@@ -712,7 +790,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
-                           int ldx = 0, int groups = 1) {
+                           int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr) {
   const bool c4 = C == 4;
   if (ldx == 0) ldx = C;
   if (groups < 1 || ldx < C || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
@@ -733,6 +811,9 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   ConvParams p{};  // value-initialised: a field a launcher forgets is null / 0, never stack garbage
   p.T = p.KT = p.st = p.dtd = p.To = 1;
   p.ldx = ldx;
+  p.ax = (const bf16_t*)ax;
+  p.acoef = acoef;
+  if ((ax != nullptr) != (acoef != nullptr) || (ax && ((uintptr_t)ax & 15))) return (int)hipErrorInvalidValue;
   p.gx = C;
   p.gw = (long long)K * (c4 ? ldw : R * S * C);
   p.gy = K;
@@ -793,9 +874,20 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const int bm = conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128;
   const bool fast = (C % bk == 0) && R * S <= 64;
   const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
+  if (ax && (mode != 3 || groups != 1 || bm != 128)) return (int)hipErrorInvalidValue;  // prologue: pointwise only
   long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
   if (tiles > 0x7fffffff || groups > 65535) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles, (unsigned)groups);
+  if (ax) {
+    if (bk == 32) {
+      if (BN == 64) hipLaunchKernelGGL((k_conv_fwd<64, 3, 128, 32, false, true>), g, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_fwd<128, 3, 128, 32, false, true>), g, dim3(256), 0, s, p);
+    } else {
+      if (BN == 64) hipLaunchKernelGGL((k_conv_fwd<64, 3, 128, 64, false, true>), g, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_fwd<128, 3, 128, 64, false, true>), g, dim3(256), 0, s, p);
+    }
+    BIGDL_CHECK_LAUNCH();
+  }
   if (bm == 256)
     BN == 64 ? launch_fwd<64, 256, 64>(mode, g, s, p) : launch_fwd<128, 256, 64>(mode, g, s, p);
   else if (bk == 32)
@@ -827,6 +919,22 @@ BIGDL_EXPORT int bigdl_conv_fwd_full2(const void* x, const void* w, const void* 
   return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
                          0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
                          bn_bits);
+}
+
+// bigdl_conv_fwd_full2 with a BatchNorm-backward prologue on the A operand (pointwise convs: the
+// stride-1 backward-data of a 1×1 conv): x is g' (the gradient at a BN output), ax the BN input, acoef
+// [3][C] the BN's input-gradient coefficients (gx = A·g' + B·ax + Cc).
+BIGDL_EXPORT int bigdl_conv_fwd_full3(const void* x, const void* ax, const float* acoef, const void* w, const void* res,
+                                      void* y, float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P,
+                                      int Q, int sh, int sw, int ph, int pw, int dh, int dw, const void* bnx,
+                                      const float* bn_sc, const float* bn_sh, const float* bn_mean,
+                                      const void* bn_mask, const void* bn_bits, int res_sh, int res_sw, int res_H,
+                                      int res_W, hipStream_t s) {
+  if (!ax || !acoef) return (int)hipErrorInvalidValue;
+  if (res_sh < 0 || res_sw < 0 || (res_sh > 0) != (res_sw > 0) || (res_sh && !res)) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
+                         0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
+                         bn_bits, 0, 1, ax, acoef);
 }
 
 // Grouped convolution in ONE launch (SpatialConvolution.scala:93-98 nGroup): x [Nb][H][W][ldx] with

@@ -50,6 +50,10 @@ struct WgradParams {
   // grouped-conv per-group offsets (group = blockIdx.z) of x, dy (channels) and dw (elements)
   int ldx, ldk;
   long long gx, gdy, gdw;
+  // BatchNorm-backward prologue on dY (AT instantiations): dy is g' at a BN output, dy2 the BN input
+  // (same layout), dcoef [3][K]: the kernel uses A·g' + B·dy2 + Cc (the BN input gradient)
+  const bf16_t* dy2;
+  const float* dcoef;
 };
 
 constexpr int BP = 64;  // split granularity (pixels); the k-tile depth BPT is 64 or 32
@@ -68,9 +72,10 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 
 // C4: 4-channel input (RGB stem padded 3 → 4): an X̂ chunk of 8 k-values is two consecutive taps,
 // gathered as two 8-B loads with separate padding tests (see conv_igemm.hip MODE 2).
-template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false>
-__global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradParams p) {
+template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false>
+__global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(WgradParams p) {
   static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
+  static_assert(!(AT && (C4 || D3)), "BN-backward prologue: 2-D, 8-channel chunks");
   constexpr int DY_CH = BPT * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
   constexpr int X_CH = BPT * TILE_K / 8 / 256;   // for the X̂ tile
   constexpr int TMN = TILE_N / 32;              // MFMA tiles per wave along n
@@ -130,8 +135,20 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)dy_bytes, 0x00020000);
   constexpr uint32_t DEAD = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t y2r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(AT ? p.dy2 : p.dy), 0, (int)dy_bytes, 0x00020000);
+  float cA[AT ? 8 : 1], cB[AT ? 8 : 1], cC[AT ? 8 : 1];  // this thread's dY column coefficients
+  if constexpr (AT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool in = ndy_ok;
+      cA[e] = in ? p.dcoef[ndy + e] : 0.f;
+      cB[e] = in ? p.dcoef[p.K + ndy + e] : 0.f;
+      cC[e] = in ? p.dcoef[2 * p.K + ndy + e] : 0.f;
+    }
+  }
 
-  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH], uint4 (&rx_)[X_CH]) {
+  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH], uint4 (&rx_)[X_CH], uint4 (&r2)[AT ? DY_CH : 1]) {
     const uint32_t dead = live ? 0u : DEAD;
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
@@ -139,6 +156,7 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
       const bool ok = ndy_ok && m < mend;
       const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldk + (uint32_t)ndy) * 2u : DEAD) | dead;
       rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
+      if constexpr (AT) r2[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(y2r, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
@@ -172,11 +190,27 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
       }
     }
   };
-  auto store = [&](int buf, const uint4 (&rdy)[DY_CH], const uint4 (&rx_)[X_CH]) {
+  auto store = [&](int buf, int mt, const uint4 (&rdy)[DY_CH], const uint4 (&rx_)[X_CH],
+                   const uint4 (&r2)[AT ? DY_CH : 1]) {
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
       int row = dy_row0 + i * DY_RSTEP;
-      *reinterpret_cast<uint4*>(&lds[buf][tr_swz_dword<TILE_N>(row, dy_col * 4)]) = rdy[i];
+      uint4 v = rdy[i];
+      if constexpr (AT) {  // dY := the BN input gradient; rows past the split end stay zero
+        const bool ok = ndy_ok && mt + row < mend;
+        float g[8], xv[8];
+        unpack8(rdy[i], g);
+        unpack8(r2[i], xv);
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float o0 = ok ? fmaf(cA[2 * e], g[2 * e], fmaf(cB[2 * e], xv[2 * e], cC[2 * e])) : 0.f;
+          const float o1 = ok ? fmaf(cA[2 * e + 1], g[2 * e + 1], fmaf(cB[2 * e + 1], xv[2 * e + 1], cC[2 * e + 1])) : 0.f;
+          w4[e] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+        }
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      *reinterpret_cast<uint4*>(&lds[buf][tr_swz_dword<TILE_N>(row, dy_col * 4)]) = v;
     }
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
@@ -225,20 +259,21 @@ __global__ void __launch_bounds__(256, BPT == 32 ? 3 : 2) k_conv_wgrad(WgradPara
   };
 
   uint4 dy0[DY_CH], x0[X_CH], dy1[DY_CH], x1[X_CH];
+  uint4 z0[AT ? DY_CH : 1], z1[AT ? DY_CH : 1];
   const int NT = (mend - mbeg + BPT - 1) / BPT;
-  load(mbeg, true, dy0, x0);
-  load(mbeg + BPT, NT > 1, dy1, x1);
-  store(0, dy0, x0);
+  load(mbeg, true, dy0, x0, z0);
+  load(mbeg + BPT, NT > 1, dy1, x1, z1);
+  store(0, mbeg, dy0, x0, z0);
   __syncthreads();
   int it = 0;
   for (; it + 2 <= NT; it += 2) {
-    load(mbeg + (it + 2) * BPT, it + 2 < NT, dy0, x0);
+    load(mbeg + (it + 2) * BPT, it + 2 < NT, dy0, x0, z0);
     compute(0);
-    store(1, dy1, x1);
+    store(1, mbeg + (it + 1) * BPT, dy1, x1, z1);
     __syncthreads();
-    load(mbeg + (it + 3) * BPT, it + 3 < NT, dy1, x1);
+    load(mbeg + (it + 3) * BPT, it + 3 < NT, dy1, x1, z1);
     compute(1);
-    if (it + 2 < NT) store(0, dy0, x0);
+    if (it + 2 < NT) store(0, mbeg + (it + 2) * BPT, dy0, x0, z0);
     __syncthreads();
   }
   if (it < NT) {
@@ -305,7 +340,8 @@ BIGDL_EXPORT int bigdl_conv3d_wgrad(const void* x, const void* dy, float* dw, fl
 // g·C / g·K, dw = groups × [K][R][S][C] blocks; the group is blockIdx.z.
 static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C, int K,
                         int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd, int splits,
-                        hipStream_t s, int ldx, int ldk, int groups) {
+                        hipStream_t s, int ldx, int ldk, int groups, const void* dy2 = nullptr,
+                        const float* dcoef = nullptr) {
   const bool c4 = C == 4;
   if ((C % 8 && !c4) || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
   if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
@@ -315,6 +351,10 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   WgradParams p{};
   p.ldx = ldx; p.ldk = ldk;
+  if ((dy2 != nullptr) != (dcoef != nullptr) || (dy2 && (c4 || groups != 1 || ((uintptr_t)dy2 & 15))))
+    return (int)hipErrorInvalidValue;
+  p.dy2 = (const bf16_t*)dy2;
+  p.dcoef = dcoef;
   p.gx = C; p.gdy = K; p.gdw = (long long)K * R * S * C;
   p.x = (const bf16_t*)x;
   p.dy = (const bf16_t*)dy;
@@ -355,6 +395,16 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
   const char* ev = getenv("BIGDL_WGRAD_BP");
   const int bp_env = ev ? atoi(ev) : 0;
   const int bp = (bp_env == 32 || bp_env == 64) ? bp_env : (tiles <= 16 && K >= 128 ? 32 : 64);
+  if (dy2) {  // BN-backward prologue: the 32-deep k-tile variants (register budget for the second dY)
+    if (TN == 64) {
+      if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32, false, false, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, false, false, true>), grid, dim3(256), 0, s, p);
+    } else {
+      if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 32, false, false, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32, false, false, true>), grid, dim3(256), 0, s, p);
+    }
+    BIGDL_CHECK_LAUNCH();
+  }
   if (c4) {
     if (bp == 32) {
       if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, true>), grid, dim3(256), 0, s, p);
@@ -381,6 +431,16 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
                                   int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
                                   int splits, hipStream_t s) {
   return wgrad_launch(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, C, K, 1);
+}
+
+// bigdl_conv_wgrad with a BatchNorm-backward prologue on dY: dy = g' at the BN output, dy2 = the BN input,
+// dcoef [3][K] (dY := A·g' + B·dy2 + Cc).
+BIGDL_EXPORT int bigdl_conv_wgrad_bnbwd(const void* x, const void* dy, const void* dy2, const float* dcoef, float* dw,
+                                        float scale, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                        int sh, int sw, int ph, int pw, int dh, int dwd, int splits, hipStream_t s) {
+  if (!dy2 || !dcoef) return (int)hipErrorInvalidValue;
+  return wgrad_launch(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, C, K, 1, dy2,
+                      dcoef);
 }
 
 // Grouped weight gradient in one launch (SpatialConvolution.scala:93-98 nGroup accGradParameters).

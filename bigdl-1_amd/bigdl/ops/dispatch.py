@@ -64,6 +64,8 @@ def _g(opname):
                 N.note_fallback(opname, "unsupported", args)
             else:
                 N.note_fallback(opname, "no-kernel" if nat is None else "disabled", args)
+        # the reference ops take plain tensors: build any deferred BN input gradient first
+        args = tuple(a.dense() if isinstance(a, R.BNGrad) else a for a in args)
         return ref(*args, **kwargs)
 
     f.__name__ = opname

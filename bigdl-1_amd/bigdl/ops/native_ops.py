@@ -186,9 +186,10 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
 
 
 def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G, need_input=True, gg_acc=None,
-                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0):
+                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, lazy=False):
     """BN backward whose reductions came from the consumer conv's dgrad epilogue; ``gm`` is the
-    already ReLU-masked gradient.  Returns gradInput (or None) / NotImplemented."""
+    already ReLU-masked gradient.  Returns gradInput (or None) / NotImplemented; ``lazy`` returns
+    it as a :class:`~bigdl.ops.reference.BNGrad` (coefficients only, no apply pass)."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -198,11 +199,13 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
     if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc)):
         return NotImplemented
     coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
-    gx = torch.empty_like(x) if need_input else None
+    gx = torch.empty_like(x) if (need_input and not lazy) else None
     check(_lib().bigdl_bn_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
                                        ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
                                        _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
                                        ptr(_fold_scratch(G, C_, x.device)), _s()), "bn_bwd_partials")
+    if need_input and lazy:
+        return R_.BNGrad(gm, x, coef)
     return gx
 
 
@@ -734,6 +737,9 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
     K, Ci, R, S = w4.shape
     if K % 8:
         return None
+    ax = acoef = None
+    if isinstance(gy, R_.BNGrad):  # the BN input gradient, applied in the A-operand prologue
+        gy, ax, acoef = gy.g, gy.x, gy.coef
     # W'[c][r][s][k] = W[k][R-1-r][S-1-s][c]: one cached-index gather from the KRSC storage (a
     # flip + transpose copy would be two launches per layer per step)
     ent = _S1_XFORM.get((K, Ci, R, S))
@@ -779,7 +785,12 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         if ok:
             G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
             part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)
-            if rs is not None or bits is not None:
+            if ax is not None:
+                check(_lib().bigdl_conv_fwd_full3(ptr(gy), ptr(ax), ptr(acoef), ptr(wt), ptr(residual), ptr(gx),
+                                                  ptr(part), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0],
+                                                  dilation[1], ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
+                                                  ptr(bits), *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_bnbwd3")
+            elif rs is not None or bits is not None:
                 check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q,
                                                   K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
                                                   ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), ptr(bits),
@@ -791,6 +802,12 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
                                                  _s()), "conv_dgrad_bnbwd")
             bn_fuse["partial"], bn_fuse["G"] = part, G
             return gx
+    if ax is not None:
+        check(_lib().bigdl_conv_fwd_full3(ptr(gy), ptr(ax), ptr(acoef), ptr(wt), ptr(residual), ptr(gx), ptr(None),
+                                          N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
+                                          ptr(None), ptr(None), ptr(None), ptr(None), ptr(None), ptr(None),
+                                          *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_at")
+        return gx
     if rs is not None:
         check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
                                           S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(None), ptr(None),
@@ -1096,19 +1113,61 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
     direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
     target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
     P, Q = gy.shape[2], gy.shape[3]
-    check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
-                                  R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
-                                  -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
+    if isinstance(gy, R_.BNGrad):  # dY = the BN input gradient, applied while loading dY
+        check(_lib().bigdl_conv_wgrad_bnbwd(ptr(xx), ptr(gy.g), ptr(gy.x), ptr(gy.coef), ptr(target),
+                                            _f(scale if direct else 1.0), N_, H, W, cc, K, R, S, P, Q, stride[0],
+                                            stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                            -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad_bnbwd")
+    else:
+        check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
+                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                      -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
     if not direct:
         gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
     return xx
+
+
+def bngrad_consumable(g, x, w4, stride, pad, groups=1):
+    """A deferred BN gradient can feed this conv's backward prologues: 1×1, stride 1, unpadded,
+    one group, channel counts the pointwise kernel tiles exactly (K % 32, C % 8), dense bf16."""
+    if not isinstance(g, R_.BNGrad) or groups != 1 or tuple(stride) != (1, 1) or tuple(pad) != (0, 0):
+        return False
+    K, Ci, R, S = w4.shape
+    if R != 1 or S != 1 or K % 32 or x.dim() != 4 or x.shape[1] % 8 or g.shape[1] != K:
+        return False
+    cl = torch.channels_last
+    return all(t.is_cuda and t.dtype == _bf16 and t.is_contiguous(memory_format=cl) and _al16(t) for t in (g.g, g.x)) \
+        and g.g.shape == g.x.shape and _f32vec(g.coef, 3 * K) and x.dtype == _bf16 \
+        and x.is_contiguous(memory_format=cl) and _al16(x)
 
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
                     scale=1.0, residual=None, bn_fuse=None, pad_slot=None, lazy_strided=False):
     """``lazy_strided``: a 1×1 stride-s unpadded conv may return its input gradient as a
-    :class:`~bigdl.ops.reference.StridedGrad` (the caller sums it as a strided residual)."""
+    :class:`~bigdl.ops.reference.StridedGrad` (the caller sums it as a strided residual).  ``gy`` may
+    be a deferred :class:`~bigdl.ops.reference.BNGrad` (consumed in the operand prologues of a 1×1
+    stride-1 conv, materialised otherwise)."""
+    if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):
+        gy = gy.dense()
+    if isinstance(gy, R_.BNGrad):
+        if need_input:
+            gi = _dgrad_s1(gy, w4, x.shape, pad, dilation, residual, bn_fuse)
+            if gi is None:
+                return conv2d_backward(gy.dense(), x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc,
+                                       scale, residual, bn_fuse, pad_slot, lazy_strided)
+        else:
+            gi = None
+        if gw_acc is not None and scale != 0:
+            side = _wgrad_side_stream(gy.g) if _WG["on"] else None
+            if side is None:
+                _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
+            else:
+                with torch.cuda.stream(side):
+                    xx = _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
+                for t in (x, xx, gy.g, gy.x, gy.coef):
+                    t.record_stream(side)
+        return gi
     if isinstance(residual, R_.StridedGrad) and (tuple(stride) != (1, 1) or groups > 1 or gy.dtype != _bf16):
         residual = residual.dense()
     if groups > 1 and residual is None and bn_fuse is None and _depthwise_ok(x, w4, groups):

@@ -6,6 +6,7 @@ Semantics follow the reference layers cited per function.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional, Tuple
 
@@ -94,8 +95,42 @@ class StridedGrad:
         return out
 
 
+class BNGrad:
+    """Deferred input gradient of a training BatchNorm: gx = A·g + B·x + Cc per channel, with ``g``
+    the (ReLU-masked) gradient at the BN output, ``x`` the BN input and ``coef`` = fp32 [A; B; Cc]
+    ([3][C]).  A 1×1 stride-1 conv consuming it applies the affine map while loading its backward-
+    data and weight-gradient operands (conv_igemm.hip / conv_wgrad.hip AT prologues), so the
+    gradient tensor is never written; :meth:`dense` builds it for any other consumer."""
+    __slots__ = ("g", "x", "coef", "shape")
+
+    def __init__(self, g, x, coef):
+        self.g, self.x, self.coef, self.shape = g, x, coef, tuple(x.shape)
+
+    @property
+    def dtype(self):
+        return self.g.dtype
+
+    @property
+    def is_cuda(self):
+        return self.g.is_cuda
+
+    def dense(self):
+        from . import native as N
+        if self.g.is_cuda and N.has("batchnorm_backward"):
+            M, C = self.g.numel() // self.shape[1], self.shape[1]
+            gx = torch.empty_like(self.g)
+            N.check(N.lib().bigdl_bn_bwd_apply_coef(N.ptr(self.g), N.ptr(self.x), N.ptr(gx), ctypes.c_longlong(M),
+                                                    ctypes.c_int(C), N.ptr(self.coef),
+                                                    ctypes.c_void_p(N.stream_ptr())), "bn_bwd_apply_coef")
+            return gx
+        C = self.shape[1]
+        sh = [1, C] + [1] * (len(self.shape) - 2)
+        a, b, c = (self.coef[i * C:(i + 1) * C].view(sh) for i in range(3))
+        return (a * self.g.float() + b * self.x.float() + c).to(self.g.dtype)
+
+
 def as_dense(g):
-    return g.dense() if isinstance(g, StridedGrad) else g
+    return g.dense() if isinstance(g, (StridedGrad, BNGrad)) else g
 
 
 def conv_transpose2d_forward(x, w4, b, stride, pad, adj, dilation=(1, 1), groups=1):

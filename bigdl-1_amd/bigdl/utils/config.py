@@ -70,6 +70,10 @@ _REGISTRY = {
     "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
     "bigdl.fusion.convstats": (bool, True, "conv epilogue emits the following training BN's statistics"),
     "bigdl.fusion.bnbwd": (bool, True, "dgrad epilogue applies the producing BN's ReLU mask and its backward reductions"),
+    "bigdl.fusion.bnprologue": (int, 0, "a BN whose producer is a 1x1 stride-1 conv hands it the input gradient "
+                                         "deferred (A*g + B*x + C applied in the conv's dgrad / wgrad operand loads): "
+                                         "0 off, 1 when the BN is narrower than the conv input, 2 always "
+                                         "(profiles/r3_bn_prologue_ab.txt)"),
     # logging
     "bigdl.utils.LoggerFilter.disable": (bool, False, "disable log redirect"),
     "bigdl.utils.LoggerFilter.logFile": (str, "bigdl.log", "log file"),
