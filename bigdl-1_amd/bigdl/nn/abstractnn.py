@@ -41,6 +41,9 @@ from ..utils import config
 
 _DEV_TIMERS = [bool(config.get_property("bigdl.profile.deviceTimers"))]
 config.on_change("bigdl.profile.deviceTimers", lambda v: _DEV_TIMERS.__setitem__(0, bool(v)))
+# read on every module forward / backward: cached, refreshed by config.set_property listeners
+_PROFILE_SYNC = [bool(config.get_property("bigdl.profile.sync"))]
+config.on_change("bigdl.profile.sync", lambda v: _PROFILE_SYNC.__setitem__(0, bool(v)))
 
 
 class LayerException(RuntimeError):
@@ -631,7 +634,7 @@ class AbstractModule:
         return out
 
     def _sync_for_timing(self):
-        if config.get_property("bigdl.profile.sync") and torch.cuda.is_available():
+        if _PROFILE_SYNC[0] and torch.cuda.is_available():
             torch.cuda.synchronize()
 
     def forward(self, input):

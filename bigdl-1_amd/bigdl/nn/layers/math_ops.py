@@ -202,7 +202,8 @@ class Sum(AutogradModule):
         y = x.sum(d, keepdim=not self.squeeze)
         if self.sizeAverage:
             y = y / x.shape[d]
-        return y
+        # Sum.scala:82-90: a 1-D input sums to a 1-element tensor, not a 0-d scalar
+        return y.reshape(1) if y.dim() == 0 else y
 
 
 class Mean(Sum):

@@ -107,8 +107,13 @@ def lib():
     return l
 
 
+# asked on every op dispatch: cached, refreshed by config.set_property listeners
+_ENABLED = [bool(config.get_property("bigdl.native.enable"))]
+config.on_change("bigdl.native.enable", lambda v: _ENABLED.__setitem__(0, bool(v)))
+
+
 def has(opname: str) -> bool:
-    if not config.get_property("bigdl.native.enable"):
+    if not _ENABLED[0]:
         return False
     l = _load()
     if l is None:
@@ -167,7 +172,14 @@ def reset_fallbacks() -> None:
     _FALLBACKS.clear()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr() -> int:
+    """The current HIP stream of the current device (raw handle; called once per kernel launch, so it
+    skips the torch.cuda.Stream object that ``current_stream()`` builds)."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(torch._C._cuda_getDevice())
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -36,6 +36,9 @@ def _sync(dev):
         torch.cuda.synchronize()
 
 
+_CPROFILE = {"n": 0}
+
+
 def _time_steps(fn, dev, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -45,7 +48,21 @@ def _time_steps(fn, dev, steps, warmup):
     for _ in range(steps):
         r = fn()
     _sync(dev)
-    return time.perf_counter() - t0, r
+    el = time.perf_counter() - t0
+    if _CPROFILE["n"]:  # host-side hot spots of the step (stderr), after the timed run
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(_CPROFILE["n"]):
+            fn()
+        _sync(dev)
+        pr.disable()
+        out = io.StringIO()
+        pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(35)
+        print(out.getvalue()[:9000], file=sys.stderr, flush=True)
+    return el, r
 
 
 def bench_lenet(args):
@@ -336,8 +353,10 @@ def main():
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
+    ap.add_argument("--cprofile", type=int, default=0, help="cProfile this many extra steps (host hot spots, stderr)")
     ap.add_argument("--no-native-ln", action="store_true", help="transformer: composed torch LayerNorm")
     args = ap.parse_args()
+    _CPROFILE["n"] = args.cprofile
     names = list(CONFIGS) if args.config == "all" else [args.config]
     for n in names:
         r = CONFIGS[n](args)
