@@ -1063,13 +1063,30 @@ def async_wgrad(on: bool) -> None:
     _WG["on"] = bool(on) and bool(config.get_property("bigdl.conv.asyncWgrad"))
 
 
+def _new_side_stream(dev):
+    """The wgrad side stream.  ``BIGDL_WGRAD_CUMASK=keep/period`` (e.g. ``3/4``) restricts it to the
+    CUs with ``i % period < keep`` (hipExtStreamCreateWithCUMask), so the weight gradients can never
+    hold every CU while the backward-data chain on the step stream waits for workgroup slots."""
+    spec = __import__("os").environ.get("BIGDL_WGRAD_CUMASK", "")
+    if spec:
+        keep, period = (int(v) for v in spec.split("/"))
+        f = N._load().bigdl_stream_create_cumask  # the raw CDLL symbol: a 64-bit handle
+        f.restype = C.c_longlong
+        with torch.cuda.device(dev):
+            h = f(C.c_int(keep), C.c_int(period))
+        if h:
+            return torch.cuda.ExternalStream(h, device=dev)
+        __import__("logging").getLogger("bigdl.ops").warning("CU-masked wgrad stream %s unavailable; using a plain stream", spec)
+    return torch.cuda.Stream(device=dev)
+
+
 def _wgrad_side_stream(t):
     if not _WG["on"] or not t.is_cuda or torch.cuda.is_current_stream_capturing():
         return None
     dev = t.device
     st = _WG["streams"].get(dev)
     if st is None:
-        st = _WG["streams"][dev] = torch.cuda.Stream(device=dev)
+        st = _WG["streams"][dev] = _new_side_stream(dev)
     st.wait_stream(torch.cuda.current_stream(dev))  # gy / x / zeroed gradients are ready
     return st
 
