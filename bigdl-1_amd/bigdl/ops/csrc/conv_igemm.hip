@@ -87,6 +87,10 @@ struct ConvParams {
   // materialised tensor (one fewer write + read of it per consumer).
   const bf16_t* ax;
   const float* acoef;
+  // optional fp32 output [M][ldy] (the bf16x3 fp32 path, precision.hip): the accumulators (+ bias,
+  // ReLU) are stored straight from registers as float4 per lane — no bf16 rounding, no LDS staging;
+  // `y` is unused.  Plain epilogue only (no residual / statistics / BN prologue / scatter / groups).
+  float* y32;
 };
 
 // Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
@@ -492,6 +496,28 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
     __syncthreads();
   }
 
+  if (p.y32) {  // fp32 output (uniform branch): 4 consecutive channels of one pixel per accumulator
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
+      if (n >= p.K) continue;  // K % 4 == 0 (host-checked): a 4-channel group is all in or all out
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = p.bias[n + e];
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wave_m * (BM / 2) + j * 16 + fr;
+        if (m >= p.M) continue;
+        float4 v = make_float4(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1], acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
+        if (p.relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+        *reinterpret_cast<float4*>(p.y32 + (size_t)m * p.ldy + n) = v;
+      }
+    }
+    return;
+  }
+
   // Epilogue, staged through LDS so every global access is a full 16-B chunk of a pixel row:
   //  1. each lane parks its 4-channel fragments (+bias) as bf16 in a [BM][BN+8] tile (the +8 pad
   //     spreads the 16 pixel rows a ds_write_b64 covers over distinct banks);
@@ -790,8 +816,12 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            const float* bn_sh, const float* bn_mean, const void* bn_mask, int ldy,
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
-                           int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr) {
+                           int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
+                           float* y32 = nullptr) {
   const bool c4 = C == 4;
+  if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
+              osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
+    return (int)hipErrorInvalidValue;
   if (ldx == 0) ldx = C;
   if (groups < 1 || ldx < C || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
   // grouped: C / K are per group; x pixels are ldx apart with group g at channel g·C; y rows ldy
@@ -802,7 +832,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   // any K: partial 8-channel chunks are stored per element in the epilogue
   if ((C % 8 && !c4) || Nb <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   if (c4 && (ldw < R * S * C || ldw % 8 || dh != 1 || dw != 1)) return (int)hipErrorInvalidValue;
-  if (ldy < K || (ldy != K && (ldy % 8 || K % 8 || ((uintptr_t)y & 15)))) return (int)hipErrorInvalidValue;
+  if (!y32 && (ldy < K || (ldy != K && (ldy % 8 || K % 8 || ((uintptr_t)y & 15))))) return (int)hipErrorInvalidValue;
+  if (y32 && ldy < K) return (int)hipErrorInvalidValue;
   if ((res || stats) && K % 8) return (int)hipErrorInvalidValue;
   // 32-bit buffer offsets: both operands must stay below 2 GiB
   if (!c4) ldw = R * S * C;
@@ -821,6 +852,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.w = (const bf16_t*)w;
   p.bias = bias;
   p.y = (bf16_t*)y;
+  p.y32 = y32;
   p.res = (const bf16_t*)res;
   p.stats = stats;
   p.res_sh = res ? res_sh : 0;
@@ -993,6 +1025,17 @@ BIGDL_EXPORT int bigdl_conv3d_fwd(const void* x, const void* w, const float* bia
   }
 #undef BIGDL_C3
   BIGDL_CHECK_LAUNCH();
+}
+
+// Forward conv with an fp32 NHWC output [Nb][P][Q][ldy] (+ fp32 bias, ReLU): the bf16x3 fp32 path
+// (precision.hip splits the fp32 operands into bf16 hi / lo parts concatenated along C).  K % 4 == 0.
+BIGDL_EXPORT int bigdl_conv_fwd_f32out(const void* x, const void* w, const float* bias, float* y32, int Nb, int H,
+                                       int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                       int dh, int dw, int relu, int ldy, hipStream_t s) {
+  if (!y32) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+                         relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
+                         0, 0, nullptr, 0, 1, nullptr, nullptr, y32);
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).

@@ -1,0 +1,221 @@
+"""fp32 compute mode on the bf16 MFMA kernels ("bf16x3", ``csrc/precision.hip``).
+
+The reference trains in fp32 (MKL sgemm / MKL-DNN fp32 primitives: ``DL/nn/SpatialConvolution.scala:253-362``,
+``DL/nn/Linear.scala:108-158``).  On CDNA4 an fp32 MFMA runs at 1/16 of the bf16 rate, so with
+``bigdl.compute.dtype=fp32`` the convolutions and Linear layers on a GPU split every fp32 operand
+into ``hi = bf16(v)`` and ``lo = bf16(v - hi)`` and evaluate ``a_hi·b_hi + a_hi·b_lo + a_lo·b_hi``
+with fp32 accumulation (the dropped ``a_lo·b_lo`` term is ≤ 2^-16 relative per product, ~100× below
+bf16 rounding and below TF32) — on the SAME tuned kernels as the bf16 path, the three products
+being one GEMM over a 3× longer reduction:
+
+* conv forward / data gradient: parts concatenated along the input channels — activations
+  ``[hi | hi | lo]``, filters ``[hi | lo | hi]`` — into the implicit-GEMM conv with an fp32 epilogue
+  (``ConvParams::y32``); strided data gradients run on a zero lattice of dY (stride-1 conv of the
+  flipped filter);
+* conv weight gradient: parts stacked along the batch — ``x = [hi; hi; lo]``, ``dY = [hi; lo; hi]`` —
+  into the split-K wgrad kernel, which accumulates in fp32 already;
+* Linear: the same concatenation along K into the MFMA GEMM with an fp32 C.
+
+Every entry returns ``NotImplemented`` for a case it does not cover (grouped conv, fused BN
+prologues) and the caller falls back to the torch op.  ``bigdl.fp32.native=false`` turns the path
+off (torch / MIOpen fp32 everywhere).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .native import ptr, check, stream_ptr
+from . import native as N
+from ..utils import config
+
+_bf16 = torch.bfloat16
+_f32 = torch.float32
+_cl = torch.channels_last
+
+#: part codes: bit q set → part q holds the lo half
+HHL = 0b100  # [hi | hi | lo]  (the "A" side)
+HLH = 0b010  # [hi | lo | hi]  (the "B" side)
+
+
+def enabled(t) -> bool:
+    return (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == _f32 and N.has("conv2d_forward")
+            and bool(config.get_property("bigdl.fp32.native")))
+
+
+def _r(n, m):
+    return (n + m - 1) // m * m
+
+
+def _s():
+    return C.c_void_p(stream_ptr())
+
+
+def split(rows2d: torch.Tensor, cp: int, code: int, stacked: bool, out: torch.Tensor = None) -> torch.Tensor:
+    """fp32 [rows][C] (unit column stride) → bf16 parts, each ``cp`` wide (zero-padded): side by
+    side ``[rows][3·cp]`` or stacked ``[3·rows][cp]``.  ``out`` (optional) receives them (it may
+    have more rows than written, e.g. zero rows padding a GEMM operand)."""
+    rows, c = rows2d.shape
+    if rows2d.stride(1) != 1 or rows2d.dtype != _f32:
+        rows2d = rows2d.float().contiguous()
+    shape = (3 * rows, cp) if stacked else (rows, 3 * cp)
+    if out is None:
+        out = torch.empty(shape, dtype=_bf16, device=rows2d.device)
+    check(N.lib().bigdl_split_bf16x3(ptr(rows2d), C.c_longlong(rows), C.c_int(c), C.c_longlong(rows2d.stride(0)),
+                                     C.c_int(cp), ptr(out), C.c_int(code), C.c_int(1 if stacked else 0), _s()),
+          "split_bf16x3")
+    return out
+
+
+def _nhwc_rows(x: torch.Tensor) -> torch.Tensor:
+    """[N][C][H][W] fp32 → its channels-last storage as a [N·H·W][C] matrix."""
+    xc = x.contiguous(memory_format=_cl)
+    return xc.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
+
+def _conv_f32out(x3, w3, bias, y, nb, h, w, c3, k, r, s, p, q, stride, pad, dil, relu, ldy):
+    check(N.lib().bigdl_conv_fwd_f32out(ptr(x3), ptr(w3), ptr(bias), ptr(y), nb, h, w, c3, k, r, s, p, q, stride[0],
+                                        stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), ldy, _s()),
+          "conv_fwd_f32out")
+
+
+def _out_hw(h, w, r, s, stride, pad, dil):
+    return ((h + 2 * pad[0] - dil[0] * (r - 1) - 1) // stride[0] + 1,
+            (w + 2 * pad[1] - dil[1] * (s - 1) - 1) // stride[1] + 1)
+
+
+def _fits(*nbytes) -> bool:
+    return all(b < 0x80000000 for b in nbytes)  # 32-bit buffer offsets in the conv kernels
+
+
+def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False):
+    """fp32 NCHW-logical conv (any memory format in, channels-last fp32 out)."""
+    if groups != 1 or x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1]:
+        return NotImplemented
+    nb, c, h, w = x.shape
+    k, _, r, s = w4.shape
+    p, q = _out_hw(h, w, r, s, stride, pad, dilation)
+    cp, kq = _r(c, 8), _r(k, 4)
+    if p <= 0 or q <= 0 or not _fits(nb * h * w * 3 * cp * 2, kq * r * s * 3 * cp * 2):
+        return NotImplemented
+    x3 = split(_nhwc_rows(x), cp, HHL, False)
+    wk = w4.detach().float().permute(0, 2, 3, 1).reshape(k * r * s, c)
+    w3 = torch.zeros((kq * r * s, 3 * cp), dtype=_bf16, device=x.device) if kq != k else None
+    w3 = split(wk, cp, HLH, False, out=w3)
+    bias = None
+    if b is not None:
+        bias = torch.zeros(kq, dtype=_f32, device=x.device)
+        bias[:k] = b.detach().float().reshape(-1)
+    y = torch.empty((nb, kq, p, q), dtype=_f32, device=x.device, memory_format=_cl)
+    _conv_f32out(x3, w3, bias, y, nb, h, w, 3 * cp, kq, r, s, p, q, stride, pad, dilation, relu, kq)
+    if kq != k:
+        y = y[:, :k].contiguous(memory_format=_cl)
+    return y
+
+
+def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
+                  scale=1.0, residual=None):
+    """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation."""
+    if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
+        return NotImplemented
+    nb, c, h, w = x.shape
+    k, _, r, s = w4.shape
+    p, q = gy.shape[2], gy.shape[3]
+    kp, cq, cp = _r(k, 8), _r(c, 4), _r(c, 8)
+    gi = None
+    if need_input:
+        hl, wl = h + 2 * pad[0] - dilation[0] * (r - 1), w + 2 * pad[1] - dilation[1] * (s - 1)
+        pd = (dilation[0] * (r - 1) - pad[0], dilation[1] * (s - 1) - pad[1])
+        if pd[0] < 0 or pd[1] < 0 or not _fits(nb * hl * wl * 3 * kp * 2, cq * r * s * 3 * kp * 2):
+            return NotImplemented
+        src = gy
+        if tuple(stride) != (1, 1):  # dY on the stride lattice (zeros between), then a stride-1 conv
+            src = torch.empty((nb, k, hl, wl), dtype=_f32, device=gy.device, memory_format=_cl).zero_()
+            src[:, :, ::stride[0], ::stride[1]] = gy
+        elif (hl, wl) != (p, q):
+            return NotImplemented
+        g3 = split(_nhwc_rows(src), kp, HHL, False)
+        wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c * r * s, k)  # [C][R][S][K]
+        wt3 = torch.zeros((cq * r * s, 3 * kp), dtype=_bf16, device=x.device) if cq != c else None
+        wt3 = split(wt, kp, HLH, False, out=wt3)
+        gi = torch.empty((nb, cq, h, w), dtype=_f32, device=x.device, memory_format=_cl)
+        _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq)
+        if cq != c:
+            gi = gi[:, :c].contiguous(memory_format=_cl)
+        if residual is not None:
+            gi.add_(residual)
+    if gw_acc is not None and scale != 0:
+        if not _fits(3 * nb * h * w * cp * 2, 3 * nb * p * q * kp * 2):
+            return NotImplemented
+        x3 = split(_nhwc_rows(x), cp, HHL, True)       # [3·N·H·W][Cp]  = [hi; hi; lo] images
+        g3 = split(_nhwc_rows(gy), kp, HLH, True)      # [3·N·P·Q][Kp]  = [hi; lo; hi] images
+        direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
+        target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)
+        from .native_ops import _wgrad_blocks
+        check(N.lib().bigdl_conv_wgrad(ptr(x3), ptr(g3), ptr(target), C.c_float(float(scale) if direct else 1.0),
+                                       3 * nb, h, w, cp, kp, r, s, p, q, stride[0], stride[1], pad[0], pad[1],
+                                       dilation[0], dilation[1], -_wgrad_blocks(3 * nb * p * q, cp, kp), _s()),
+              "conv_wgrad(bf16x3)")
+        if not direct:
+            gw_acc.add_(target[:k, :, :, :c].permute(0, 3, 1, 2), alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+    return gi
+
+
+def _gemm_f32(a3, b3, m, n4, bias=None, act=0):
+    from .native_ops import gemm
+    out = torch.empty((m, n4), dtype=_f32, device=a3.device)
+    return gemm(a3, b3, bias, act=act, out=out)
+
+
+def linear_forward(x, w, b, act=0):
+    """y = act(x·Wᵀ + b), fp32 in / out."""
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1] or x.shape[0] == 0:
+        return NotImplemented
+    m, k = x.shape
+    n = w.shape[0]
+    k8, n4 = _r(k, 8), _r(n, 4)
+    a3 = split(x, k8, HHL, False)
+    b3 = split(w.detach().float(), k8, HLH, False,
+               out=torch.zeros((n4, 3 * k8), dtype=_bf16, device=x.device) if n4 != n else None)
+    bias = None
+    if b is not None:
+        bias = torch.zeros(n4, dtype=_f32, device=x.device)
+        bias[:n] = b.detach().float().reshape(-1)
+    y = _gemm_f32(a3, b3, m, n4, bias, act)
+    if y is NotImplemented:
+        return NotImplemented
+    return y if n4 == n else y[:, :n].contiguous()
+
+
+def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1.0):
+    if gy.dim() != 2 or x.dim() != 2 or w.dim() != 2 or gy.dtype != _f32:
+        return NotImplemented
+    m, n = gy.shape
+    k = x.shape[1]
+    n8, k4, k8 = _r(n, 8), _r(k, 4), _r(k, 8)
+    gi = None
+    if need_input:
+        g3 = split(gy, n8, HHL, False)
+        wt3 = split(w.detach().float().t(), n8, HLH, False,
+                    out=torch.zeros((k4, 3 * n8), dtype=_bf16, device=gy.device) if k4 != k else None)
+        gi = _gemm_f32(g3, wt3, m, k4)
+        if gi is NotImplemented:
+            return NotImplemented
+        if k4 != k:
+            gi = gi[:, :k].contiguous()
+    if gw_acc is not None and scale != 0:
+        from .native_ops import wgrad_rows
+        g3 = split(gy, n8, HLH, True)   # [3M][N8] = [hi; lo; hi]
+        x3 = split(x, k8, HHL, True)    # [3M][K8] = [hi; hi; lo]
+        direct = n8 == n and k8 == k and gw_acc.dtype == _f32 and gw_acc.is_contiguous()
+        tgt = gw_acc if direct else torch.zeros((n8, k8), dtype=_f32, device=gy.device)
+        if wgrad_rows(g3, x3, tgt, scale if direct else 1.0) is NotImplemented:
+            return NotImplemented
+        if not direct:
+            gw_acc.add_(tgt[:n, :k].reshape(gw_acc.shape), alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(gy.sum(0).reshape(gb_acc.shape), alpha=scale)
+    return gi

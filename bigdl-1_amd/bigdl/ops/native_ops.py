@@ -14,6 +14,7 @@ import torch
 
 from . import native as N
 from . import reference as R_
+from . import fp32x3 as F3
 from ..utils import config
 from .native import register, ptr, stream_ptr, check
 
@@ -717,6 +718,10 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
 
 @register("conv2d_forward")
 def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
+    if x.dtype == _f32 and res is None and out is None and F3.enabled(x):
+        r = F3.conv_forward(x, w4, b, stride, pad, dilation, groups, relu)
+        if r is not NotImplemented:
+            return r
     if res is not None and (res.dtype != _bf16 or not res.is_contiguous(memory_format=torch.channels_last)):
         res = res.to(_bf16).contiguous(memory_format=torch.channels_last)
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out, pad_slot=pad_slot)
@@ -1165,6 +1170,13 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     :class:`~bigdl.ops.reference.StridedGrad` (the caller sums it as a strided residual).  ``gy`` may
     be a deferred :class:`~bigdl.ops.reference.BNGrad` (consumed in the operand prologues of a 1×1
     stride-1 conv, materialised otherwise)."""
+    if isinstance(gy, torch.Tensor) and gy.dtype == _f32 and x.dtype == _f32 and F3.enabled(gy):
+        # fp32 (bf16x3): the bf16 epilogue fusions are optional — bn_fuse is left unconsumed (the BN
+        # runs its own backward), a lazy strided gradient is returned dense
+        res = residual.dense() if isinstance(residual, R_.StridedGrad) else residual
+        r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, res)
+        if r is not NotImplemented:
+            return r
     if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):
         gy = gy.dense()
     if isinstance(gy, R_.BNGrad):
@@ -1708,6 +1720,10 @@ def _padded(t, rows, cols):
 
 @register("linear_forward")
 def linear_forward(x, w, b, act=0):
+    if x.dtype == _f32 and F3.enabled(x):
+        r = F3.linear_forward(x, w, b, act)
+        if r is not NotImplemented:
+            return r
     if x.dim() != 2 or w.dim() != 2 or x.dtype != _bf16 or w.dtype != _bf16 or x.shape[1] != w.shape[1]:
         return NotImplemented
     M, K = x.shape
@@ -1729,6 +1745,10 @@ def linear_forward(x, w, b, act=0):
 
 @register("linear_backward")
 def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1.0):
+    if gy.dtype == _f32 and x.dtype == _f32 and F3.enabled(gy):
+        r = F3.linear_backward(gy, x, w, need_input, gw_acc, gb_acc, scale)
+        if r is not NotImplemented:
+            return r
     if gy.dim() != 2 or x.dim() != 2 or w.dim() != 2 or not (gy.dtype == x.dtype == w.dtype == _bf16):
         return NotImplemented
     M, N_ = gy.shape

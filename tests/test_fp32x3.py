@@ -1,0 +1,125 @@
+"""fp32 compute mode on the bf16 MFMA kernels (ops/fp32x3.py, csrc/precision.hip): the hi/lo split
+is exact against torch's own bf16 rounding, and conv forward / data gradient / weight gradient and
+Linear forward / backward match an fp64 reference to fp32-class accuracy (far below bf16 rounding),
+through the ops and through the nn modules with ``bigdl.compute.dtype=fp32`` (no torch fallback)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def test_split_matches_torch_rounding():
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(0)
+    x = (torch.randn(37, 21, generator=g) * torch.logspace(-3, 3, 21)).to(dev)
+    hi = x.bfloat16()
+    lo = (x - hi.float()).bfloat16()
+    side = F3.split(x, 24, F3.HHL, False).cpu()
+    assert torch.equal(side[:, 0:21], hi.cpu()) and torch.equal(side[:, 24:45], hi.cpu())
+    assert torch.equal(side[:, 48:69], lo.cpu())
+    assert side[:, 21:24].abs().sum() == 0 and side[:, 69:72].abs().sum() == 0
+    st = F3.split(x, 24, F3.HLH, True).cpu()
+    assert torch.equal(st[0:37, :21], hi.cpu()) and torch.equal(st[37:74, :21], lo.cpu())
+    assert torch.equal(st[74:111, :21], hi.cpu())
+    rec = hi.double() + lo.double()
+    assert float(((rec - x.double()).abs() / x.double().abs().clamp_min(1e-30)).max()) < 2 ** -16
+
+
+@pytest.mark.parametrize("N,C,K,H,W,k,s,p,d", [
+    (4, 64, 128, 14, 14, 3, 1, 1, 1),
+    (2, 3, 64, 32, 32, 7, 2, 3, 1),      # RGB stem: C padded to 8, strided dgrad on the lattice
+    (3, 32, 48, 9, 11, 1, 2, 0, 1),      # 1x1 stride 2
+    (2, 16, 20, 10, 10, 3, 1, 2, 2),     # dilated, K % 8 != 0
+    (2, 24, 8, 15, 15, 3, 2, 1, 1),
+])
+def test_conv_fp32x3_matches_fp64(N, C, K, H, W, k, s, p, d):
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, k, k, generator=g) * (1.0 / (C * k * k) ** 0.5)
+    b = torch.randn(K, generator=g)
+    xr, wr, br = (t.double().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr, wr, br, s, p, d)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy.double())
+
+    y = F3.conv_forward(x.to(dev), w.to(dev), b.to(dev), (s, s), (p, p), (d, d))
+    assert y is not NotImplemented and y.dtype == torch.float32 and y.shape == yr.shape
+    gw = torch.zeros(K, k, k, C, device=dev).permute(0, 3, 1, 2)  # KRSC arena layout
+    gb = torch.zeros(K, device=dev)
+    gi = F3.conv_backward(gy.to(dev), x.to(dev), w.to(dev), (s, s), (p, p), (d, d), 1, True, gw, gb, 1.0)
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 2e-5, _rel(y, yr)
+    assert _rel(gi, xr.grad) < 2e-5, _rel(gi, xr.grad)
+    assert _rel(gw, wr.grad) < 2e-5, _rel(gw, wr.grad)
+    assert _rel(gb, br.grad) < 1e-6
+    # and it is not the bf16 path: plain bf16 operands are ~100x further off
+    yb = F.conv2d(x.bfloat16().double(), w.bfloat16().double(), b.double(), s, p, d)
+    assert _rel(yb, yr) > 20 * _rel(y, yr)
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 256, 128), (33, 100, 10), (7, 24, 36)])
+def test_linear_fp32x3_matches_fp64(M, K, N):
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(2)
+    x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * K ** -0.5, torch.randn(N, generator=g)
+    xr, wr, br = (t.double().requires_grad_() for t in (x, w, b))
+    yr = F.linear(xr, wr, br)
+    gy = torch.randn(M, N, generator=g)
+    yr.backward(gy.double())
+    y = F3.linear_forward(x.to(dev), w.to(dev), b.to(dev))
+    gw, gb = torch.zeros(N, K, device=dev), torch.zeros(N, device=dev)
+    gi = F3.linear_backward(gy.to(dev), x.to(dev), w.to(dev), True, gw, gb, 0.5)
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 2e-5
+    assert _rel(gi, xr.grad) < 2e-5
+    assert _rel(gw, 0.5 * wr.grad) < 2e-5
+    assert _rel(gb, 0.5 * br.grad) < 1e-6
+
+
+def test_fp32_modules_run_native_without_fallback():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    from bigdl import ops
+    from bigdl.nn import Sequential, SpatialConvolution, ReLU, Reshape, Linear
+    config.set_property("bigdl.compute.dtype", "fp32")
+    try:
+        Engine.init(device="cuda:0")
+        torch.manual_seed(0)
+        m = Sequential().add(SpatialConvolution(8, 16, 3, 3, 1, 1, 1, 1)).add(ReLU()) \
+            .add(SpatialConvolution(16, 16, 3, 3, 2, 2, 1, 1)).add(Reshape([16 * 4 * 4])).add(Linear(256, 10))
+        ref = [p.detach().double().clone() for p in m.parameters()[0]]
+        x = torch.randn(4, 8, 8, 8)
+        gy = torch.randn(4, 10)
+        m.cuda()
+        ops.reset_fallbacks()
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+            y = m.forward(x.to(dev))
+            m.zeroGradParameters()
+            m.backward(x.to(dev), gy.to(dev))
+            torch.cuda.synchronize()
+        names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+        assert any("k_split_bf16x3" in n for n in names) and any("k_conv_fwd" in n for n in names), sorted(names)
+        assert any("k_gemm" in n for n in names) and any("k_conv_wgrad" in n for n in names), sorted(names)
+        assert not any("miopen" in n.lower() or "Cijk" in n for n in names), sorted(names)
+        fb = {k[0] for k in ops.fallback_counts()}
+        assert not ({"conv2d_forward", "conv2d_backward", "linear_forward", "linear_backward"} & fb), fb
+        w1, b1, w2, b2, wl, bl = ref
+        xr = x.double().requires_grad_()
+        h = F.relu(F.conv2d(xr, w1.reshape(16, 8, 3, 3), b1, 1, 1))
+        h = F.conv2d(h, w2.reshape(16, 16, 3, 3), b2, 2, 1)
+        yr = F.linear(h.permute(0, 1, 2, 3).reshape(4, -1), wl.reshape(10, 256), bl)
+        yr.backward(gy.double())
+        assert _rel(y, yr) < 5e-5
+        gin = m.gradInput
+        assert _rel(gin, xr.grad) < 5e-5
+    finally:
+        config.set_property("bigdl.compute.dtype", "bf16")
+        Engine.init(device="cuda:0")
