@@ -769,3 +769,200 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
   }
   BIGDL_CHECK_LAUNCH();
 }
+
+// ------------------------------------------------------------------------------------------------ fp32
+// fp32 NHWC BatchNormalization (bigdl.compute.dtype=fp32 on a GPU, next to the bf16x3 convolutions of
+// precision.hip): the same pass structure and finalize kernels as the bf16 path, 8 fp32 channels
+// (two 16-B loads) per thread and row.  Statistics are shifted by row 0 (kshift = x itself).
+__device__ __forceinline__ void ld8f(const float* __restrict__ p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* __restrict__ p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// mode 0: partial = Σ(x − x[row 0]), Σ(x − x[row 0])²;  mode 1 (backward): Σg', Σg'·(x − mean)
+template <int MODE, bool RELU>
+__global__ void __launch_bounds__(256) k_bn32_reduce(const float* __restrict__ x, const float* __restrict__ gy,
+                                                     const float* __restrict__ y, long long M, int C,
+                                                     long long rows_per_block, const float* __restrict__ ref,
+                                                     float* __restrict__ partial, int G) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  long long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float* s_a = smem;
+  float* s_b = smem + g.RPI * C;
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    float K[8], a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { K[k] = ref[cg * 8 + k]; a[k] = 0.f; b[k] = 0.f; }
+    if (r_off < g.RPI) {
+      for (long long r = r0 + r_off; r < r1; r += g.RPI) {
+        const size_t off = (size_t)r * C + (size_t)cg * 8;
+        float xv[8];
+        ld8f(x + off, xv);
+        if (MODE == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float d = xv[k] - K[k];
+            a[k] += d;
+            b[k] = fmaf(d, d, b[k]);
+          }
+        } else {
+          float gv[8];
+          ld8f(gy + off, gv);
+          if (RELU) {
+            float yv[8];
+            ld8f(y + off, yv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            a[k] += gv[k];
+            b[k] = fmaf(gv[k], xv[k] - K[k], b[k]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s_a[r_off * C + cg * 8 + k] = a[k];
+        s_b[r_off * C + cg * 8 + k] = b[k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < g.RPI; ++i) {
+      a += s_a[i * C + c];
+      b += s_b[i * C + c];
+    }
+    partial[(size_t)blockIdx.x * C + c] = a;
+    partial[(size_t)(G + blockIdx.x) * C + c] = b;
+  }
+}
+
+// forward: y = relu?(x·scale + shift (+ res));  backward (BWD): gx = A·g' + B·x + Cc, g' = gy masked
+// by y > 0 (RELU), g' also stored to gres when given
+template <bool BWD, bool RELU>
+__global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x, const float* __restrict__ aux,
+                                                    const float* __restrict__ y_mask, float* __restrict__ out,
+                                                    float* __restrict__ gres, long long M, int C,
+                                                    const float* __restrict__ coef) {
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  if (r_off >= g.RPI) return;
+  const long long rstride = (long long)gridDim.x * g.RPI;
+  for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+    float A[8], B[8], Cc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      A[k] = coef[cg * 8 + k];
+      B[k] = coef[C + cg * 8 + k];
+      Cc[k] = BWD ? coef[2 * C + cg * 8 + k] : 0.f;
+    }
+    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
+      const size_t off = (size_t)r * C + (size_t)cg * 8;
+      float xv[8], o[8];
+      ld8f(x + off, xv);
+      if (BWD) {
+        float gv[8];
+        ld8f(aux + off, gv);
+        if (RELU) {
+          float yv[8];
+          ld8f(y_mask + off, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+        }
+        if (gres) st8f(gres + off, gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
+      } else {
+        float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (aux) ld8f(aux + off, rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float v = fmaf(xv[k], A[k], B[k]) + rv[k];
+          o[k] = RELU ? fmaxf(v, 0.f) : v;
+        }
+      }
+      if (out) st8f(out + off, o);
+    }
+  }
+}
+
+static bool bn32_ok(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y, long long M, int C,
+                                      const float* gamma, const float* beta, const float* in_bias, float* run_mean,
+                                      float* run_var, float momentum, float eps, float* save_mean, float* save_invstd,
+                                      float* ws, float* coef, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res))) return (int)hipErrorInvalidValue;
+  const int G = bigdl_bn_num_partials(M, C);
+  const long long rpb = (M + G - 1) / G;
+  const size_t sm = stats_smem(C);
+  if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_bn32_reduce<0, false>), dim3(G), dim3(256), sm, s, x, nullptr, nullptr, M, C, rpb, x, ws, G);
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, x,
+                     (const float*)ws, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
+                     save_invstd, coef, coef + C);
+  const int grid = apply_grid(M, C);
+  if (relu)
+    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef);
+  else
+    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int C, const float* gamma,
+                                      const float* beta, const float* run_mean, const float* run_var,
+                                      const float* in_bias, float eps, float* coef, int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_infer_coef, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, run_mean, run_var,
+                     in_bias, eps, coef, coef + C);
+  const int grid = apply_grid(M, C);
+  if (relu)
+    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, nullptr, nullptr, y, nullptr, M, C, coef);
+  else
+    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, nullptr, nullptr, y, nullptr, M, C,
+                       coef);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Backward.  ws: 2·G·C floats; coef: 3·C floats.  gx / gres optional; y is the BN+ReLU output (relu).
+BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y, float* gx, float* gres, long long M,
+                                int C, const float* gamma, const float* mean, const float* invstd, float* ggamma,
+                                float* gbeta, float gscale, float* cbias, float cbscale, float* ws, float* coef,
+                                int relu, hipStream_t s) {
+  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(gy) || (relu && (!y || !bn32_ok(y))) || (gx && !bn32_ok(gx)) ||
+      (gres && !bn32_ok(gres)))
+    return (int)hipErrorInvalidValue;
+  const int G = bigdl_bn_num_partials(M, C);
+  const long long rpb = (M + G - 1) / G;
+  const size_t sm = stats_smem(C);
+  if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
+  if (relu)
+    hipLaunchKernelGGL((k_bn32_reduce<1, true>), dim3(G), dim3(256), sm, s, x, gy, y, M, C, rpb, mean, ws, G);
+  else
+    hipLaunchKernelGGL((k_bn32_reduce<1, false>), dim3(G), dim3(256), sm, s, x, gy, y, M, C, rpb, mean, ws, G);
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)ws, G, M, C,
+                     gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
+  if (gx || gres) {
+    const int grid = apply_grid(M, C);
+    if (relu)
+      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef);
+    else
+      hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

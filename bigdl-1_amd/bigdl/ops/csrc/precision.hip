@@ -11,41 +11,50 @@
 // (conv_igemm.hip, ConvParams::y32 fp32 output; conv_wgrad.hip, fp32 accumulation) do the rest.
 #include "common.h"
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
 // src: `rows` rows of C fp32 values, row stride ld (elements).  dst: the three parts, each Cp ≥ C
 // wide (zero beyond C), either side by side in one row (stacked = 0: dst row r = [p0 | p1 | p2],
 // 3·Cp elements) or stacked along rows (stacked = 1: part q is rows [q·rows, (q+1)·rows)).  Bit q
-// of `code` selects lo (1) or hi (0) for part q.  One thread per 8-channel chunk of a row.
+// of `code` selects lo (1) or hi (0) for part q.  A block covers 256 / tpr rows per trip, tpr
+// threads per row one 8-channel chunk each (no per-element index division; streaming-bound).
 __global__ void __launch_bounds__(256) k_split_bf16x3(const float* __restrict__ src, long long rows, int C, long long ld,
                                                       int Cp, bf16_t* __restrict__ dst, int code, int stacked,
                                                       int vec4) {
   const int chunks = Cp / 8;
-  const long long total = rows * chunks;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / chunks;
-    const int c0 = (int)(i - r * chunks) * 8;
-    const float* sp = src + r * ld + c0;
-    float v[8];
-    if (vec4 && c0 + 8 <= C) {
-      const float4 a = *reinterpret_cast<const float4*>(sp), b = *reinterpret_cast<const float4*>(sp + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else {
+  const int tpr = chunks < 256 ? chunks : 256;
+  const int rpi = 256 / tpr;
+  const int tl = threadIdx.x % tpr, rl = threadIdx.x / tpr;
+  if (rl >= rpi) return;
+  const long long rstep = (long long)gridDim.x * rpi;
+  for (long long r = (long long)blockIdx.x * rpi + rl; r < rows; r += rstep) {
+    for (int ch = tl; ch < chunks; ch += tpr) {
+      const int c0 = ch * 8;
+      const float* sp = src + r * ld + c0;
+      float v[8];
+      if (vec4 && c0 + 8 <= C) {
+        const f4v a = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(sp));
+        const f4v b = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(sp + 4));
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = c0 + e < C ? sp[e] : 0.f;
-    }
-    uint32_t hw[4], lw[4];
+        for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+      } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bf16_t h0 = f2bf(v[2 * e]), h1 = f2bf(v[2 * e + 1]);
-      const bf16_t l0 = f2bf(v[2 * e] - bf2f(h0)), l1 = f2bf(v[2 * e + 1] - bf2f(h1));
-      hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      lw[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
-    }
-    const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]), L = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        for (int e = 0; e < 8; ++e) v[e] = c0 + e < C ? sp[e] : 0.f;
+      }
+      uint32_t hw[4], lw[4];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const size_t off = stacked ? ((size_t)(q * rows + r) * Cp + c0) : ((size_t)r * 3 * Cp + (size_t)q * Cp + c0);
-      *reinterpret_cast<uint4*>(dst + off) = ((code >> q) & 1) ? L : H;
+      for (int e = 0; e < 4; ++e) {
+        const bf16_t h0 = f2bf(v[2 * e]), h1 = f2bf(v[2 * e + 1]);
+        const bf16_t l0 = f2bf(v[2 * e] - bf2f(h0)), l1 = f2bf(v[2 * e + 1] - bf2f(h1));
+        hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        lw[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+      }
+      const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]), L = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const size_t off = stacked ? ((size_t)(q * rows + r) * Cp + c0) : ((size_t)r * 3 * Cp + (size_t)q * Cp + c0);
+        *reinterpret_cast<uint4*>(dst + off) = ((code >> q) & 1) ? L : H;
+      }
     }
   }
 }
@@ -55,9 +64,9 @@ BIGDL_EXPORT int bigdl_split_bf16x3(const float* src, long long rows, int C, lon
   if (rows <= 0 || C <= 0 || Cp < C || Cp % 8 || ld < C || code < 0 || code > 7 || ((uintptr_t)dst & 15))
     return (int)hipErrorInvalidValue;
   const int vec4 = (ld % 4 == 0 && ((uintptr_t)src & 15) == 0) ? 1 : 0;
-  const long long total = rows * (Cp / 8);
-  long long grid = (total + 255) / 256;
-  if (grid > 8192) grid = 8192;
+  const int chunks = Cp / 8, tpr = chunks < 256 ? chunks : 256, rpi = 256 / tpr;
+  long long grid = (rows + rpi - 1) / rpi;
+  if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_split_bf16x3, dim3((unsigned)grid), dim3(256), 0, s, src, rows, C, ld, Cp, (bf16_t*)dst, code,
                      stacked, vec4);
   BIGDL_CHECK_LAUNCH();

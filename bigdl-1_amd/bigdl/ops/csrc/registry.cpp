@@ -6,7 +6,7 @@ static const char* kOps[] = {
     "cross_entropy", "logsoftmax", "conv_fwd_igemm", "conv_dgrad_igemm", "conv_wgrad_igemm",
     "lstm_fwd", "lstm_bwd", "conv_fwd_stats", "bn_fwd_train_partials", "quant_rows", "gemm_i8", "image_crop_flip_norm", "maxpool_fwd", "maxpool_bwd", "bn_fold_partials", "lrn_fwd", "lrn_bwd", "conv_fwd_ldy", "dropout", "w_dgrad_xform",
     "conv_fwd_c4", "pad_channels", "gemm", "transpose_bf16", "colsum_bf16", "rnn_step", "embedding_fwd", "embedding_bwd", "avgpool_fwd",
-    "avgpool_bwd", "softmax", "class_nll", "spmm_csr", "trunc_bf16", "nchw_to_nhwc_bf16", "nms", "roi_align", "vml_unary", "vml_binary", "reduce", "depthwise", "layernorm", "adam_dev", "attention", "stream_probe", "resize_bilinear", "pool3d", "split_bf16x3", "conv_fwd_f32out",
+    "avgpool_bwd", "softmax", "class_nll", "spmm_csr", "trunc_bf16", "nchw_to_nhwc_bf16", "nms", "roi_align", "vml_unary", "vml_binary", "reduce", "depthwise", "layernorm", "adam_dev", "attention", "stream_probe", "resize_bilinear", "pool3d", "split_bf16x3", "conv_fwd_f32out", "bn32",
 };
 
 extern "C" __attribute__((visibility("default"))) int bigdl_num_ops() {

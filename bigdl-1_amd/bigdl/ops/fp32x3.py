@@ -12,8 +12,9 @@ being one GEMM over a 3× longer reduction:
   ``[hi | hi | lo]``, filters ``[hi | lo | hi]`` — into the implicit-GEMM conv with an fp32 epilogue
   (``ConvParams::y32``); strided data gradients run on a zero lattice of dY (stride-1 conv of the
   flipped filter);
-* conv weight gradient: parts stacked along the batch — ``x = [hi; hi; lo]``, ``dY = [hi; lo; hi]`` —
-  into the split-K wgrad kernel, which accumulates in fp32 already;
+* conv weight gradient: three launches of the split-K wgrad kernel (fp32 accumulation) over channel
+  slices of the side-by-side splits — (x_hi, dY_hi), (x_hi, dY_lo), (x_lo, dY_hi) — reusing the
+  data gradient's split of dY for stride-1 convs;
 * Linear: the same concatenation along K into the MFMA GEMM with an fp32 C.
 
 Every entry returns ``NotImplemented`` for a case it does not cover (grouped conv, fused BN
@@ -146,17 +147,22 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         if residual is not None:
             gi.add_(residual)
     if gw_acc is not None and scale != 0:
-        if not _fits(3 * nb * h * w * cp * 2, 3 * nb * p * q * kp * 2):
+        # three launches over the side-by-side parts — (x_hi, dY_hi), (x_hi, dY_lo), (x_lo, dY_hi) —
+        # each a channel slice (pixel stride 3·Cp / 3·Kp) of the [hi | hi | lo] splits; a stride-1
+        # conv reuses the data gradient's split of dY
+        if not _fits(nb * h * w * 3 * cp * 2, nb * p * q * 3 * kp * 2):
             return NotImplemented
-        x3 = split(_nhwc_rows(x), cp, HHL, True)       # [3·N·H·W][Cp]  = [hi; hi; lo] images
-        g3 = split(_nhwc_rows(gy), kp, HLH, True)      # [3·N·P·Q][Kp]  = [hi; lo; hi] images
+        x3 = split(_nhwc_rows(x), cp, HHL, False)
+        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else split(_nhwc_rows(gy), kp, HHL, False)
         direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)
-        from .native_ops import _wgrad_blocks
-        check(N.lib().bigdl_conv_wgrad(ptr(x3), ptr(g3), ptr(target), C.c_float(float(scale) if direct else 1.0),
-                                       3 * nb, h, w, cp, kp, r, s, p, q, stride[0], stride[1], pad[0], pad[1],
-                                       dilation[0], dilation[1], -_wgrad_blocks(3 * nb * p * q, cp, kp), _s()),
-              "conv_wgrad(bf16x3)")
+        sc = C.c_float(float(scale) if direct else 1.0)
+        for xq, gq in ((0, 0), (0, 2), (2, 0)):
+            check(N.lib().bigdl_conv_wgrad_grouped(C.c_void_p(x3.data_ptr() + 2 * xq * cp),
+                                                   C.c_void_p(gy3.data_ptr() + 2 * gq * kp), ptr(target), sc, nb, h,
+                                                   w, 3 * cp, cp, 3 * kp, kp, 1, r, s, p, q, stride[0], stride[1],
+                                                   pad[0], pad[1], dilation[0], dilation[1], _s()),
+                  "conv_wgrad(bf16x3)")
         if not direct:
             gw_acc.add_(target[:k, :, :, :c].permute(0, 3, 1, 2), alpha=scale)
     if gb_acc is not None and scale != 0:

@@ -110,6 +110,13 @@ def _f32vec(t, C_):
     return t is None or (t.dtype == _f32 and t.is_contiguous() and t.numel() == C_ and t.is_cuda)
 
 
+def _bn32_ok(x, C_, *more):
+    """fp32 NHWC tensors of the fp32 compute mode (csrc/batchnorm.hip k_bn32_*)."""
+    return (x.dtype == _f32 and C_ % 8 == 0 and C_ <= 8192 and _al16(x) and F3.enabled(x)
+            and all(t is None or (t.dtype == _f32 and t.shape == x.shape and t.stride() == x.stride() and _al16(t))
+                    for t in more))
+
+
 @register("batchnorm_forward_train")
 def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum, eps, relu=False, residual=None,
                             in_bias=None, coef_out=None, bits_out=None):
@@ -117,6 +124,18 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    if _bn32_ok(x, C_, residual) and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
+        G = _lib().bigdl_bn_num_partials(_ll(M), C.c_int(C_))
+        ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
+        coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
+        mean = torch.empty(C_, dtype=_f32, device=x.device)
+        invstd = torch.empty(C_, dtype=_f32, device=x.device)
+        y = torch.empty_like(x)
+        check(_lib().bigdl_bn32_fwd_train(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
+                                          ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum), _f(eps),
+                                          ptr(mean), ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()),
+              "bn32_fwd_train")
+        return y, mean, invstd
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
@@ -320,6 +339,13 @@ def batchnorm_forward_infer(x, gamma, beta, running_mean, running_var, eps, relu
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    if _bn32_ok(x, C_) and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
+        coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
+        y = torch.empty_like(x)
+        check(_lib().bigdl_bn32_fwd_infer(ptr(x), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
+                                          ptr(running_mean), ptr(running_var), ptr(in_bias), _f(eps), ptr(coef),
+                                          C.c_int(1 if relu else 0), _s()), "bn32_fwd_infer")
+        return y
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     coef = torch.empty(2 * C_, dtype=_f32, device=x.device)
@@ -339,6 +365,18 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    if (_bn32_ok(x, C_, gy, y if relu else None) and (y is not None or not relu)
+            and all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc))):
+        G = _lib().bigdl_bn_num_partials(_ll(M), C.c_int(C_))
+        ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
+        coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
+        gx = torch.empty_like(x) if need_input else None
+        gres = torch.empty_like(x) if want_gres else None
+        check(_lib().bigdl_bn32_bwd(ptr(gy), ptr(x), ptr(y if relu else None), ptr(gx), ptr(gres), _ll(M), C.c_int(C_),
+                                    ptr(gamma), ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
+                                    ptr(cbias_acc), _f(cbias_scale), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
+                                    _s()), "bn32_bwd")
+        return gx, gres
     if not _bn_ok(x, C_) or gy.dtype != _bf16 or gy.shape != x.shape or gy.stride() != x.stride() or not _al16(gy):
         return NotImplemented
     if relu and (y is None or y.dtype != _bf16 or y.stride() != x.stride() or not _al16(y)):

@@ -123,3 +123,31 @@ def test_fp32_modules_run_native_without_fallback():
     finally:
         config.set_property("bigdl.compute.dtype", "bf16")
         Engine.init(device="cuda:0")
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_bn32_native_matches_reference(relu, res):
+    """fp32 BatchNorm kernels (batchnorm.hip k_bn32_*) vs the torch reference ops in fp64."""
+    from bigdl.ops import native_ops as NO, reference as R
+    g = torch.Generator().manual_seed(3)
+    N_, C_, H, W = 4, 48, 9, 7
+    x = (torch.randn(N_, C_, H, W, generator=g) * 3 + 5).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(N_, C_, H, W, generator=g).contiguous(memory_format=torch.channels_last) if res else None
+    gam, bet = torch.rand(C_, generator=g) + 0.5, torch.randn(C_, generator=g)
+    rm, rv = torch.zeros(C_), torch.ones(C_)
+    y, m, inv = NO.batchnorm_forward_train(x.to(dev), gam.to(dev), bet.to(dev), rm.to(dev), rv.to(dev), 0.1, 1e-3,
+                                           relu, None if r is None else r.to(dev))
+    rm_d, rv_d = rm.double(), rv.double()
+    yr, mr, ir = R.batchnorm_forward_train(x.double(), gam.double(), bet.double(), rm_d, rv_d, 0.1, 1e-3, relu,
+                                           None if r is None else r.double())
+    assert _rel(y, yr) < 1e-5 and _rel(m, mr) < 1e-6 and _rel(inv, ir) < 1e-5
+    gy = torch.randn(N_, C_, H, W, generator=g).contiguous(memory_format=torch.channels_last)
+    gg, gb = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
+    gx, gres = NO.batchnorm_backward(gy.to(dev), x.to(dev), gam.to(dev), m, inv, y, relu, True, gg, gb, 1.0,
+                                     want_gres=res)
+    ggr, gbr = torch.zeros(C_, dtype=torch.float64), torch.zeros(C_, dtype=torch.float64)
+    out = R.batchnorm_backward(gy.double(), x.double(), gam.double(), mr, ir, yr, relu, True, ggr, gbr, 1.0)
+    torch.cuda.synchronize()
+    assert _rel(gx, out[0]) < 1e-4 and _rel(gg, ggr) < 1e-5 and _rel(gb, gbr) < 1e-5
+    if res:
+        assert _rel(gres, gy.double() * (yr > 0)) < 1e-6
