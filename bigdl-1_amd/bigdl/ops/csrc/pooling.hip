@@ -143,18 +143,24 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const bf16_t* __restrict
 // 6 rows for 4 outputs instead of 12).
 constexpr int MP_ROWS = 4;
 
+// IDX: the flat thread index type — 32-bit whenever the index space fits (the three index
+// divisions per output chunk were 64-bit before: ~4× the integer instructions of the 32-bit form,
+// and this kernel was 21 % of Inception-v1 inference, profiles/r2_cfg_inception_v4_profile.txt)
+template <typename IDX>
 __global__ void __launch_bounds__(256) k_maxpool_fwd_rows(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                           PoolGeom g) {
-  const int CG = g.C >> 3;
-  const int PB = (g.P + MP_ROWS - 1) / MP_ROWS;
-  const long long total = (long long)g.N * PB * g.Q * CG;
-  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
-    const int cg = (int)(t % CG);
-    long long pix = t / CG;
-    const int q = (int)(pix % g.Q);
-    pix /= g.Q;
-    const int pb = (int)(pix % PB);
-    const int n = (int)(pix / PB);
+  const IDX CG = (IDX)(g.C >> 3);
+  const IDX PB = (IDX)((g.P + MP_ROWS - 1) / MP_ROWS);
+  const IDX Q = (IDX)g.Q;
+  const IDX total = (IDX)g.N * PB * Q * CG;
+  for (IDX t = (IDX)blockIdx.x * 256 + threadIdx.x; t < total; t += (IDX)gridDim.x * 256) {
+    IDX pix = t / CG;
+    const int cg = (int)(t - pix * CG);
+    IDX pq = pix / Q;
+    const int q = (int)(pix - pq * Q);
+    const IDX nn = pq / PB;
+    const int pb = (int)(pq - nn * PB);
+    const int n = (int)nn;
     const int p0 = pb * MP_ROWS;
     const int np = min(MP_ROWS, g.P - p0);
     float best[MP_ROWS][8];
@@ -236,8 +242,12 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
   }
   if (!idx) {
     const long long rows = (long long)N * ((P + MP_ROWS - 1) / MP_ROWS) * Q * (C / 8);
-    hipLaunchKernelGGL(k_maxpool_fwd_rows, dim3(bigdl_grid(rows, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x,
-                       (bf16_t*)y, g);
+    if (rows < 0x7fffffffLL - 65536LL * 256)
+      hipLaunchKernelGGL(k_maxpool_fwd_rows<uint32_t>, dim3(bigdl_grid(rows, 256, 16384)), dim3(256), 0, s,
+                         (const bf16_t*)x, (bf16_t*)y, g);
+    else
+      hipLaunchKernelGGL(k_maxpool_fwd_rows<long long>, dim3(bigdl_grid(rows, 256, 16384)), dim3(256), 0, s,
+                         (const bf16_t*)x, (bf16_t*)y, g);
     BIGDL_CHECK_LAUNCH();
   }
   const long long total = (long long)N * P * Q * (C / 8);
