@@ -208,7 +208,8 @@ class SpatialConvolution(TensorModule):
             if tgt is not None and (not batched or self.format != "NCHW"):
                 tgt = None
             y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
-                                   self.nGroup, relu=self._fused_relu, out=tgt, pad_slot=self._pad_slot_())
+                                   self.nGroup, relu=self._fused_relu, out=tgt,
+                                   pad_slot=self._pad_slot_() if self.train else None)
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)

@@ -90,8 +90,14 @@ def _fits(*nbytes) -> bool:
     return all(b < 0x80000000 for b in nbytes)  # 32-bit buffer offsets in the conv kernels
 
 
-def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False):
-    """fp32 NCHW-logical conv (any memory format in, channels-last fp32 out)."""
+def _slot_key(x, cp):
+    return ("bf16x3", x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), cp)
+
+
+def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, slot=None):
+    """fp32 NCHW-logical conv (any memory format in, channels-last fp32 out).  ``slot`` (the layer's
+    one-entry holder, passed while training): keeps the input split for the weight gradient of the
+    same input, which then skips its own split of x."""
     if groups != 1 or x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1]:
         return NotImplemented
     nb, c, h, w = x.shape
@@ -101,6 +107,8 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False):
     if p <= 0 or q <= 0 or not _fits(nb * h * w * 3 * cp * 2, kq * r * s * 3 * cp * 2):
         return NotImplemented
     x3 = split(_nhwc_rows(x), cp, HHL, False)
+    if slot is not None:
+        slot[0] = (_slot_key(x, cp), x3)
     wk = w4.detach().float().permute(0, 2, 3, 1).reshape(k * r * s, c)
     w3 = torch.zeros((kq * r * s, 3 * cp), dtype=_bf16, device=x.device) if kq != k else None
     w3 = split(wk, cp, HLH, False, out=w3)
@@ -116,7 +124,7 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False):
 
 
 def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                  scale=1.0, residual=None):
+                  scale=1.0, residual=None, slot=None):
     """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
@@ -152,7 +160,12 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         # conv reuses the data gradient's split of dY
         if not _fits(nb * h * w * 3 * cp * 2, nb * p * q * 3 * kp * 2):
             return NotImplemented
-        x3 = split(_nhwc_rows(x), cp, HHL, False)
+        held = slot[0] if slot is not None else None
+        if isinstance(held, tuple) and len(held) == 2 and held[0] == _slot_key(x, cp):
+            x3 = held[1]  # the forward's split of this same input
+            slot[0] = None
+        else:
+            x3 = split(_nhwc_rows(x), cp, HHL, False)
         gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else split(_nhwc_rows(gy), kp, HHL, False)
         direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)

@@ -466,7 +466,7 @@ def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
     takes the forward's copy when it still describes the same input.  The copy therefore lives
     exactly as long as the layer's forward→backward pair and, under HIP-graph capture, is produced
     by a captured kernel of the same graph (no process-global cache)."""
-    if reuse and slot is not None and slot[0] is not None:
+    if reuse and slot is not None and isinstance(slot[0], tuple) and len(slot[0]) == 4:
         src, ver, ct, padded = slot[0]
         if src is x_nhwc_4d and ver == x_nhwc_4d._version and ct == c_to:
             return padded
@@ -757,7 +757,7 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
 @register("conv2d_forward")
 def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
     if x.dtype == _f32 and res is None and out is None and F3.enabled(x):
-        r = F3.conv_forward(x, w4, b, stride, pad, dilation, groups, relu)
+        r = F3.conv_forward(x, w4, b, stride, pad, dilation, groups, relu, slot=pad_slot)
         if r is not NotImplemented:
             return r
     if res is not None and (res.dtype != _bf16 or not res.is_contiguous(memory_format=torch.channels_last)):
@@ -1212,7 +1212,8 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         # fp32 (bf16x3): the bf16 epilogue fusions are optional — bn_fuse is left unconsumed (the BN
         # runs its own backward), a lazy strided gradient is returned dense
         res = residual.dense() if isinstance(residual, R_.StridedGrad) else residual
-        r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, res)
+        r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, res,
+                             slot=pad_slot)
         if r is not NotImplemented:
             return r
     if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):
