@@ -10,6 +10,8 @@ same split is:
   conv path switches to: the "reorder" points), the activation buffers (by storage, so views are
   one buffer), their live ranges in execution order, the peak live bytes and a first-fit offset
   assignment of every buffer into one workspace (what an arena allocator for this shape needs);
+* **select kernels** (:func:`autotune`, ``bigdl.compile.autotune``): every distinct conv geometry of
+  the planned forward is timed under each implicit-GEMM tile candidate and the winner pinned;
 * **execute** (:class:`CompiledModule`): on a GPU and in the inference phase the forward is
   captured once into a HIP graph with a static input buffer — every kernel and every workspace
   allocation of the forward is then fixed (the graph's private memory pool), and each call is a
@@ -198,16 +200,87 @@ def plan(model, example, phase: str = "inference") -> Plan:
     return p
 
 
+#: tile candidates (BN output channels, BK k-tile depth, BM output pixels) of the implicit-GEMM
+#: forward; (0, 0, 0) is the launcher's shape heuristic
+TILE_CANDIDATES = ((0, 0, 0), (64, 32, 128), (64, 64, 128), (128, 32, 128), (128, 64, 128), (64, 64, 256),
+                   (128, 64, 256))
+
+
+def autotune(model, example, iters: int = 5, min_gain: float = 0.03) -> Dict[tuple, tuple]:
+    """Kernel selection for the planned shape (the reference's compile step creates its MKL-DNN
+    primitives per layer, ``DL/nn/mkldnn/DnnBase.scala:321-366``): run one forward recording every
+    implicit-GEMM conv launch, time each distinct conv geometry under every tile candidate
+    (HIP events, ``iters`` launches after a warm-up) and pin the fastest one for that geometry when
+    it beats the shape heuristic by more than ``min_gain``.  The choice is process-wide, keyed by
+    geometry (``ops.native_ops.conv_tile_table()``), like a cuDNN benchmark-mode cache.  Returns
+    {geometry: (BN, BK, BM)} of the pinned entries (empty off the GPU)."""
+    from ..ops import native_ops as NO
+    ex = _tensors(example)
+    if not ex or not ex[0].is_cuda:
+        return {}
+    was_training = model.isTraining() if hasattr(model, "isTraining") else False
+    model.evaluate()
+    rec = NO._TILE["record"] = []
+    try:
+        with torch.no_grad():
+            model.forward(example)
+    finally:
+        NO._TILE["record"] = None
+        if was_training:
+            model.training()
+    lib = NO._lib()
+    table = NO._TILE["table"]
+    chosen = {}
+    seen = {}
+    for key, fn in rec:
+        seen.setdefault(key, fn)
+    for key, fn in seen.items():
+        table.pop(key, None)
+        times = {}
+        for cand in TILE_CANDIDATES:
+            if lib.bigdl_conv_set_tile(*cand) != 0:
+                continue
+            try:
+                fn()  # warm-up (and validity: an unsupported combination raises)
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(iters):
+                    fn()
+                t1.record()
+                t1.synchronize()
+                times[cand] = t0.elapsed_time(t1) / iters
+            except RuntimeError:
+                continue
+            finally:
+                lib.bigdl_conv_set_tile(0, 0, 0)
+        base = times.get((0, 0, 0))
+        if base is None or not times:
+            continue
+        best = min(times, key=times.get)
+        if best != (0, 0, 0) and times[best] < base * (1.0 - min_gain):
+            table[key] = best
+            chosen[key] = best
+            _log.info("conv %s: tile %s %.1f us (heuristic %.1f us)", key, best, times[best] * 1e3, base * 1e3)
+    return chosen
+
+
 class CompiledModule:
     """``model`` planned for ``example``'s shape; in the inference phase on a GPU the forward is a
     captured HIP graph (``graph=False`` forces eager execution).  The returned output tensor is the
     graph's static output buffer: it is overwritten by the next call (clone it to keep it)."""
 
-    def __init__(self, model, example, phase: str = "inference", graph: Optional[bool] = None, warmup: int = 2):
+    def __init__(self, model, example, phase: str = "inference", graph: Optional[bool] = None, warmup: int = 2,
+                 tune: Optional[bool] = None):
         self.model, self.phase = model, phase
         self.plan = plan(model, example, phase)
         ex = _tensors(example)
         self.graph = None
+        self.tiles = {}
+        if tune is None:
+            from ..utils import config
+            tune = bool(config.get_property("bigdl.compile.autotune"))
+        if tune and phase == "inference" and bool(ex) and ex[0].is_cuda:
+            self.tiles = autotune(model, example)
         want = graph if graph is not None else (phase == "inference" and bool(ex) and ex[0].is_cuda)
         if want and isinstance(example, torch.Tensor) and example.is_cuda:
             try:
@@ -251,9 +324,11 @@ class CompiledModule:
     __call__ = forward
 
 
-def compile(model, example, phase: str = "inference", graph: Optional[bool] = None) -> CompiledModule:  # noqa: A001
-    """Plan ``model`` for ``example``'s shape and return the executor (see module docstring)."""
-    return CompiledModule(model, example, phase, graph)
+def compile(model, example, phase: str = "inference", graph: Optional[bool] = None,  # noqa: A001
+            tune: Optional[bool] = None) -> CompiledModule:
+    """Plan ``model`` for ``example``'s shape, select conv kernels (``autotune``) and return the
+    executor (see module docstring)."""
+    return CompiledModule(model, example, phase, graph, tune=tune)
 
 
-__all__ = ["plan", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer"]
+__all__ = ["plan", "autotune", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer", "TILE_CANDIDATES"]

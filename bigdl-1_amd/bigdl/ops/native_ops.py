@@ -674,6 +674,32 @@ def _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot=None, re
     return y
 
 
+# ------------------------------------------------------------------------------------------------ kernel selection
+#: per-geometry tile choice (BN, BK, BM) of the implicit-GEMM forward, filled by the compile phase's
+#: autotuner (nn/compiled.py ``autotune``); ``record`` collects (geometry, relaunch) pairs while a
+#: planned forward runs.  Empty table = the launcher's shape heuristic everywhere.
+_TILE = {"table": {}, "record": None}
+
+
+def _tiled_launch(key, fn):
+    rec = _TILE["record"]
+    if rec is not None:
+        rec.append((key, fn))
+    t = _TILE["table"].get(key)
+    if t is None:
+        fn()
+        return
+    check(_lib().bigdl_conv_set_tile(*t), "conv_set_tile")
+    try:
+        fn()
+    finally:
+        _lib().bigdl_conv_set_tile(0, 0, 0)
+
+
+def conv_tile_table() -> dict:
+    return _TILE["table"]
+
+
 def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None,
                    pad_slot=None, shift=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
@@ -741,14 +767,15 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         check(_lib().bigdl_conv_fwd_c4(ptr(x), ptr(wk), ldw, ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, K, R, S,
                                        P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()), "conv_fwd_c4")
         return (y, part, G) if stats else y
+    key = (N_, H, W, C_, K, R, S, tuple(stride), tuple(pad), tuple(dilation), bool(stats), res is not None)
     if shift is not None:
-        check(_lib().bigdl_conv_fwd_stats_shift(ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W,
-                                                C_, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], 1, 1, _s()),
-              "conv_fwd_stats_shift")
+        _tiled_launch(key, lambda: check(_lib().bigdl_conv_fwd_stats_shift(
+            ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W, C_, K, R, S, P, Q, stride[0],
+            stride[1], pad[0], pad[1], 1, 1, _s()), "conv_fwd_stats_shift"))
         return y, part, G
-    check(_lib().bigdl_conv_fwd_ldy(ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S,
-                                    P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy,
-                                    _s()), "conv_fwd")
+    _tiled_launch(key, lambda: check(_lib().bigdl_conv_fwd_ldy(
+        ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1],
+        pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy, _s()), "conv_fwd"))
     if stats:
         return y, part, G
     return y

@@ -68,3 +68,35 @@ def test_compiled_hip_graph_inference():
     p = c.plan
     assert any(r.out_layout == "NHWC" for r in p.layers)  # the conv path's device layout
     assert p.reorders  # NCHW input → NHWC conv output at least once
+
+
+@pytest.mark.gpu
+def test_compile_autotune_pins_tiles_and_keeps_outputs():
+    """Kernel selection: every recorded conv geometry is timed under the tile candidates; pinned
+    choices are valid launcher tiles and the tuned, captured forward still matches eager."""
+    from bigdl.nn.compiled import compile, autotune
+    from bigdl.ops import native_ops as NO
+    from bigdl.utils.engine import Engine
+    from bigdl.models.resnet import ResNet
+    Engine.init(device="cuda:0")
+    torch.manual_seed(0)
+    lib = NO._lib()
+    assert lib.bigdl_conv_set_tile(96, 0, 0) != 0 and lib.bigdl_conv_set_tile(0, 32, 256) != 0
+    assert lib.bigdl_conv_set_tile(0, 0, 0) == 0
+    m = ResNet(10, depth=20).to(device="cuda")
+    x = torch.randn(64, 3, 32, 32, device="cuda")
+    NO.conv_tile_table().clear()
+    chosen = autotune(m, x, iters=2, min_gain=-1.0)  # pin the fastest candidate for every geometry
+    assert chosen and all(t in __import__("bigdl.nn.compiled", fromlist=["x"]).TILE_CANDIDATES for t in chosen.values())
+    assert set(chosen) <= set(NO.conv_tile_table())
+    m.evaluate()
+    with torch.no_grad():
+        ref = m.forward(x).float().clone()
+    NO.conv_tile_table().clear()
+    with torch.no_grad():
+        ref0 = m.forward(x).float().clone()
+    torch.testing.assert_close(ref, ref0, rtol=2e-2, atol=2e-2)
+    c = compile(m, x)
+    assert c.captured
+    torch.testing.assert_close(c(x).float(), ref0, rtol=2e-2, atol=2e-2)
+    NO.conv_tile_table().clear()

@@ -19,7 +19,7 @@ def main():
     m = ResNet(1000, depth=50, dataset=DatasetType.ImageNet).to(device="cuda")
     m.evaluate()
     fuse(m)
-    for bs in [int(v) for v in os.environ.get("BATCHES", "1,8,32,128").split(",")]:
+    for bs in [int(v) for v in os.environ.get("BATCHES", "1,8,32,256").split(",")]:
         x = torch.randn(bs, 3, 224, 224, device="cuda")
 
         def eager():
@@ -43,10 +43,19 @@ def main():
             c(x)
         torch.cuda.synchronize()
         tc = (time.perf_counter() - t0) / it * 1e3
+        for _ in range(3):
+            eager()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(it):
+            eager()  # the same eager forward, now with the compile phase's pinned conv tiles
+        torch.cuda.synchronize()
+        tt = (time.perf_counter() - t0) / it * 1e3
         ref = eager().float()
         err = float((c(x).float() - ref).abs().max())
         print(json.dumps({"batch": bs, "eager_ms": round(te, 3), "compiled_ms": round(tc, 3), "captured": c.captured,
-                          "speedup": round(te / tc, 2), "img_per_s_compiled": round(bs / tc * 1e3, 1),
+                          "speedup": round(te / tc, 2),
+                          "eager_tuned_ms": round(tt, 3), "tiles_pinned": len(c.tiles), "img_per_s_compiled": round(bs / tc * 1e3, 1),
                           "max_abs_diff": err, "arena_MiB": round(c.plan.arena_bytes / 2 ** 20, 1),
                           "total_MiB": round(c.plan.total_bytes / 2 ** 20, 1)}), flush=True)
 
