@@ -243,12 +243,22 @@ def bench_inception(args):
     def step():
         with torch.no_grad():
             return model.forward(x)
+    tiles = None
+    if getattr(args, "compiled", False) and dev.type == "cuda":
+        # the LocalPredictor path: plan + conv kernel selection + HIP-graph forward (nn/compiled.py)
+        from bigdl.nn.compiled import compile as compile_module
+        cm = compile_module(model, x)
+        tiles = len(cm.tiles)
+
+        def step():  # noqa: F811
+            return cm(x)
     el, out = _time_steps(step, dev, args.steps, args.warmup)
     return {"metric": "images/sec Inception-v1 (Caffe-loaded) batch inference 1 GPU",
             "value": round(B * args.steps / el, 1), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "dtype": "bf16" if dev.type == "cuda" else "fp32", "data": "synthetic",
             "config": {"model": "Inception-v1 (NoAux, Caffe round-trip)", "global_batch": B,
+                       "executor": "compiled (autotuned tiles %s, HIP graph)" % tiles if tiles is not None else "eager",
                        "load_roundtrip_s": round(load_s, 2), "roundtrip_max_abs_diff": err}}
 
 
@@ -352,6 +362,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
+    ap.add_argument("--compiled", action="store_true", help="inception: run through nn.compiled (kernel selection + HIP graph)")
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
     ap.add_argument("--cprofile", type=int, default=0, help="cProfile this many extra steps (host hot spots, stderr)")
     ap.add_argument("--no-native-ln", action="store_true", help="transformer: composed torch LayerNorm")
