@@ -767,7 +767,9 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         check(_lib().bigdl_conv_fwd_c4(ptr(x), ptr(wk), ldw, ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, K, R, S,
                                        P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()), "conv_fwd_c4")
         return (y, part, G) if stats else y
-    key = (N_, H, W, C_, K, R, S, tuple(stride), tuple(pad), tuple(dilation), bool(stats), res is not None)
+    # geometry only: a tile tuned on the plain forward also serves the BN-statistics / residual
+    # epilogues of the same conv (training), which every tile shape instantiates
+    key = (N_, H, W, C_, K, R, S, tuple(stride), tuple(pad), tuple(dilation))
     if shift is not None:
         _tiled_launch(key, lambda: check(_lib().bigdl_conv_fwd_stats_shift(
             ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W, C_, K, R, S, P, Q, stride[0],

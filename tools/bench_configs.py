@@ -116,6 +116,11 @@ def bench_vgg(args):
     sgd = SGD(learningrate=0.01, weightdecay=5e-4, momentum=0.9, dampening=0.0)
     opt = LocalOptimizer(VggForCifar10(10), [batch], ClassNLLCriterion(), sgd, batch_size=B)
     opt.prepare()
+    tiles = None
+    if getattr(args, "tune", False) and dev.type == "cuda":
+        # compile-phase kernel selection on this model's conv geometries (nn/compiled.py autotune)
+        from bigdl.nn.compiled import autotune
+        tiles = len(autotune(opt.model, batch.getInput()))
     step = opt.train_step
     if args.graph:
         from bigdl.optim.graph_step import graphed_train_step
@@ -125,7 +130,8 @@ def bench_vgg(args):
             "unit": "images/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
             "data": "synthetic", "config": {"model": "VggForCifar10", "global_batch": B,
-                                            "hip_graph": bool(args.graph and getattr(opt, "_graphed", None))},
+                                            "hip_graph": bool(args.graph and getattr(opt, "_graphed", None)),
+                                            "tuned_tiles": tiles},
             "final_loss": float(loss)}
 
 
@@ -362,6 +368,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
+    ap.add_argument("--tune", action="store_true", help="vgg: pin autotuned conv tiles before timing")
     ap.add_argument("--compiled", action="store_true", help="inception: run through nn.compiled (kernel selection + HIP graph)")
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
     ap.add_argument("--cprofile", type=int, default=0, help="cProfile this many extra steps (host hot spots, stderr)")
