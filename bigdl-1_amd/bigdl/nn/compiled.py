@@ -238,21 +238,19 @@ def autotune(model, example, iters: int = 5, min_gain: float = 0.03) -> Dict[tup
         table.pop(key, None)
         times = {}
         for cand in TILE_CANDIDATES:
-            if lib.bigdl_conv_set_tile(*cand) != 0:
+            if lib.bigdl_conv_tile_ok(*cand) != 0:
                 continue
             try:
-                fn()  # warm-up (and validity: an unsupported combination raises)
+                fn(cand)  # warm-up (and validity: an unsupported combination raises)
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record()
                 for _ in range(iters):
-                    fn()
+                    fn(cand)
                 t1.record()
                 t1.synchronize()
                 times[cand] = t0.elapsed_time(t1) / iters
             except RuntimeError:
                 continue
-            finally:
-                lib.bigdl_conv_set_tile(0, 0, 0)
         base = times.get((0, 0, 0))
         if base is None or not times:
             continue

@@ -793,20 +793,15 @@ static int conv_env_override(const char* name, int a, int b) {
   return (v == a || v == b) ? v : 0;
 }
 
-// Tile choice pinned by the caller for the next launches (0 = the shape heuristic below): the
-// compile phase's kernel selection (nn/compiled.py autotune times every candidate on each conv
-// geometry of a planned model and pins the winner around that conv's launch).
-static int g_tile_bn = 0, g_tile_bk = 0, g_tile_bm = 0;
-
-BIGDL_EXPORT int bigdl_conv_set_tile(int bn, int bk, int bm) {
-  if ((bn && bn != 64 && bn != 128) || (bk && bk != 32 && bk != 64) || (bm && bm != 128 && bm != 256) ||
-      (bm == 256 && bk == 32))
-    return (int)hipErrorInvalidValue;
-  g_tile_bn = bn;
-  g_tile_bk = bk;
-  g_tile_bm = bm;
-  return 0;
+// Tile choice passed with a launch (0 = the shape heuristic in conv_fwd_launch): the compile phase's
+// kernel selection (nn/compiled.py autotune times every candidate per conv geometry and launches
+// that conv with the winner).  Valid: BN ∈ {64, 128}, BK ∈ {32, 64}, BM ∈ {128, 256}, BM 256 ⇒ BK 64.
+static bool tile_ok(int bn, int bk, int bm) {
+  return !((bn && bn != 64 && bn != 128) || (bk && bk != 32 && bk != 64) || (bm && bm != 128 && bm != 256) ||
+           (bm == 256 && bk == 32));
 }
+
+BIGDL_EXPORT int bigdl_conv_tile_ok(int bn, int bk, int bm) { return tile_ok(bn, bk, bm) ? 0 : (int)hipErrorInvalidValue; }
 
 template <int BN, int BM, int BK>
 static void launch_fwd(int mode, dim3 grid, hipStream_t s, const ConvParams& p) {
@@ -832,8 +827,9 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
-                           float* y32 = nullptr) {
+                           float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0) {
   const bool c4 = C == 4;
+  if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
   if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
               osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
     return (int)hipErrorInvalidValue;
@@ -901,7 +897,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (bnx && (!stats || !bn_mean || relu || bias || p.scatter)) return (int)hipErrorInvalidValue;
   if (bnx && !bn_mask && (!bn_sc || !bn_sh || res)) return (int)hipErrorInvalidValue;
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
-  const int bn_env = g_tile_bn ? g_tile_bn : conv_env_override("BIGDL_CONV_BN", 64, 128);
+  const int bn_env = tile_bn ? tile_bn : conv_env_override("BIGDL_CONV_BN", 64, 128);
   const int BN = bn_env ? bn_env : (K <= 64 ? 64 : 128);
   p.tiles_n = (K + BN - 1) / BN;
   p.tiles_m = (p.M + SBM - 1) / SBM;
@@ -911,15 +907,15 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   // Measured on the ResNet-50 shapes (profiles/r1_conv_bk_ab.txt): BK = 32 wins on every reduction
   // of ≤ 512 (the 1×1 convs; more blocks in flight hide the short k-loop's prologue/epilogue),
   // BK = 64 on the deeper ones (3×3, C ≥ 1024).
-  const int bk_env = g_tile_bk ? g_tile_bk : conv_env_override("BIGDL_CONV_BK", 32, 64);
+  const int bk_env = tile_bk ? tile_bk : conv_env_override("BIGDL_CONV_BK", 32, 64);
   // (The 3×3 convs with Kg ≤ 1152 run 3–5 % faster alone at BK = 32 — profiles/r2_conv3x3_tile_ab.txt —
   // but the whole step, with wgrad overlapping on a side stream, measured 23.5 vs 23.1 ms: kept at 64.)
   int bk = bk_env ? bk_env : (p.Kg <= 512 ? 32 : 64);
   // a channel count that is a multiple of 32 but not 64 (Inception's 96 / 480 / 528-style reductions)
   // keeps the tap-uniform FAST path at BK = 32 instead of the per-chunk generic gather at BK = 64
   if (!bk_env && bk == 64 && C % 64 != 0 && C % 32 == 0) bk = 32;
-  const int bm = g_tile_bm ? g_tile_bm
-                            : (conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128);
+  const int bm = tile_bm ? tile_bm
+                          : (conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128);
   const bool fast = (C % bk == 0) && R * S <= 64;
   const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
   if (ax && (mode != 3 || groups != 1 || bm != 128)) return (int)hipErrorInvalidValue;  // prologue: pointwise only
@@ -1052,6 +1048,25 @@ BIGDL_EXPORT int bigdl_conv_fwd_f32out(const void* x, const void* w, const float
   return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
                          relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
                          0, 0, nullptr, 0, 1, nullptr, nullptr, y32);
+}
+
+// bigdl_conv_fwd_ldy / bigdl_conv_fwd_stats_shift with an explicit tile (bn, bk, bm; 0 = heuristic).
+BIGDL_EXPORT int bigdl_conv_fwd_ldy_t(const void* x, const void* w, const float* bias, const void* res, void* y,
+                                      float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                      int sh, int sw, int ph, int pw, int dh, int dw, int relu, int ldy, int bn, int bk,
+                                      int bm, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, 1, 1, 0,
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0, 0, 0, nullptr,
+                         0, 1, nullptr, nullptr, nullptr, bn, bk, bm);
+}
+
+BIGDL_EXPORT int bigdl_conv_fwd_stats_shift_t(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                              const float* shift, int Nb, int H, int W, int C, int K, int R, int S,
+                                              int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int bn,
+                                              int bk, int bm, hipStream_t s) {
+  return conv_fwd_launch(x, w, bias, nullptr, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, 0, shift, 0, 0, 0, 0, nullptr, 0,
+                         1, nullptr, nullptr, nullptr, bn, bk, bm);
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).

@@ -676,24 +676,19 @@ def _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot=None, re
 
 # ------------------------------------------------------------------------------------------------ kernel selection
 #: per-geometry tile choice (BN, BK, BM) of the implicit-GEMM forward, filled by the compile phase's
-#: autotuner (nn/compiled.py ``autotune``); ``record`` collects (geometry, relaunch) pairs while a
-#: planned forward runs.  Empty table = the launcher's shape heuristic everywhere.
+#: autotuner (nn/compiled.py ``autotune``) and passed with each launch (no launcher-global state);
+#: ``record`` collects (geometry, relaunch-with-tile) pairs while a planned forward runs.  Empty
+#: table = the launcher's shape heuristic everywhere.
 _TILE = {"table": {}, "record": None}
 
 
 def _tiled_launch(key, fn):
+    """``fn(tile)`` launches the conv with ``tile`` = (BN, BK, BM) (zeros: the launcher's
+    heuristic); the tile is this geometry's entry of the kernel-selection table, if any."""
     rec = _TILE["record"]
     if rec is not None:
         rec.append((key, fn))
-    t = _TILE["table"].get(key)
-    if t is None:
-        fn()
-        return
-    check(_lib().bigdl_conv_set_tile(*t), "conv_set_tile")
-    try:
-        fn()
-    finally:
-        _lib().bigdl_conv_set_tile(0, 0, 0)
+    fn(_TILE["table"].get(key, (0, 0, 0)))
 
 
 def conv_tile_table() -> dict:
@@ -771,13 +766,13 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     # epilogues of the same conv (training), which every tile shape instantiates
     key = (N_, H, W, C_, K, R, S, tuple(stride), tuple(pad), tuple(dilation))
     if shift is not None:
-        _tiled_launch(key, lambda: check(_lib().bigdl_conv_fwd_stats_shift(
+        _tiled_launch(key, lambda t: check(_lib().bigdl_conv_fwd_stats_shift_t(
             ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W, C_, K, R, S, P, Q, stride[0],
-            stride[1], pad[0], pad[1], 1, 1, _s()), "conv_fwd_stats_shift"))
+            stride[1], pad[0], pad[1], 1, 1, t[0], t[1], t[2], _s()), "conv_fwd_stats_shift"))
         return y, part, G
-    _tiled_launch(key, lambda: check(_lib().bigdl_conv_fwd_ldy(
+    _tiled_launch(key, lambda t: check(_lib().bigdl_conv_fwd_ldy_t(
         ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1],
-        pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy, _s()), "conv_fwd"))
+        pad[0], pad[1], dilation[0], dilation[1], int(relu), ldy, t[0], t[1], t[2], _s()), "conv_fwd"))
     if stats:
         return y, part, G
     return y

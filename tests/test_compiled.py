@@ -81,8 +81,8 @@ def test_compile_autotune_pins_tiles_and_keeps_outputs():
     Engine.init(device="cuda:0")
     torch.manual_seed(0)
     lib = NO._lib()
-    assert lib.bigdl_conv_set_tile(96, 0, 0) != 0 and lib.bigdl_conv_set_tile(0, 32, 256) != 0
-    assert lib.bigdl_conv_set_tile(0, 0, 0) == 0
+    assert lib.bigdl_conv_tile_ok(96, 0, 0) != 0 and lib.bigdl_conv_tile_ok(0, 32, 256) != 0
+    assert lib.bigdl_conv_tile_ok(0, 0, 0) == 0
     m = ResNet(10, depth=20).to(device="cuda")
     x = torch.randn(64, 3, 32, 32, device="cuda")
     NO.conv_tile_table().clear()

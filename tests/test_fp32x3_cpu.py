@@ -32,27 +32,19 @@ def test_bf16x3_concatenated_gemm_is_fp32_class():
     assert rel < 2e-5 and bf > 100 * rel, (rel, bf)
 
 
-def test_tiled_launch_pins_and_resets(monkeypatch):
+def test_tiled_launch_passes_the_pinned_tile():
     from bigdl.ops import native_ops as NO
-    calls = []
-
-    class _Lib:
-        def bigdl_conv_set_tile(self, bn, bk, bm):
-            calls.append((bn, bk, bm))
-            return 0
-
-    monkeypatch.setattr(NO, "_lib", lambda: _Lib())
     key = ("geom",)
-    ran = []
+    got = []
     NO._TILE["table"].pop(key, None)
-    NO._tiled_launch(key, lambda: ran.append(1))
-    assert ran == [1] and calls == []  # heuristic: no pin
+    NO._tiled_launch(key, got.append)
+    assert got == [(0, 0, 0)]  # heuristic
     NO._TILE["table"][key] = (64, 64, 128)
     rec = NO._TILE["record"] = []
     try:
-        NO._tiled_launch(key, lambda: ran.append(2))
+        NO._tiled_launch(key, got.append)
     finally:
         NO._TILE["record"] = None
         NO._TILE["table"].pop(key, None)
-    assert ran == [1, 2] and calls == [(64, 64, 128), (0, 0, 0)]
+    assert got == [(0, 0, 0), (64, 64, 128)]
     assert len(rec) == 1 and rec[0][0] == key
