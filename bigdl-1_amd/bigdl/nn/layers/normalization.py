@@ -91,29 +91,6 @@ class BatchNormalization(TensorModule):
         """BN over dim 1 of (N, C) or (N, C, ...)."""
         return input
 
-    def _sync_stats(self, x):
-        """Cross-rank batch statistics: every rank contributes (mean, M2 = Σ(x − mean)², count) of its
-        shard and the ranks' triples are merged with Chan's parallel formula
-        (M2 = Σ M2_r + Σ n_r (mean_r − mean)²), so the variance never comes from a difference of
-        two large sums (the E[x²] − E[x]² form cancels for activations with |mean| ≫ std)."""
-        import torch.distributed as dist
-        C = x.shape[1]
-        dims = [d for d in range(x.dim()) if d != 1]
-        shape = [1, C] + [1] * (x.dim() - 2)
-        xf = acc_float(x)
-        n_loc = float(x.numel() // C)
-        mean_l = xf.mean(dims)
-        m2_l = (xf - mean_l.view(shape)).square().sum(dims)
-        mine = torch.stack([mean_l, m2_l, torch.full_like(mean_l, n_loc)])
-        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(self._sync_group))]
-        dist.all_gather(parts, mine, group=self._sync_group)
-        allp = torch.stack(parts)  # [W, 3, C]
-        n_r, mean_r, m2_r = allp[:, 2], allp[:, 0], allp[:, 1]
-        cnt = n_r.sum(0)
-        mean = (n_r * mean_r).sum(0) / cnt
-        m2 = m2_r.sum(0) + (n_r * (mean_r - mean).square()).sum(0)
-        return mean, (m2 / cnt).clamp_min(0), cnt[0]
-
     # --- fusion hooks (set by bigdl.nn.fusion) ---------------------------------------------
     #: conv whose bias was folded into this BN (its output excludes the bias)
     _bias_producer = None
@@ -224,71 +201,49 @@ class BatchNormalization(TensorModule):
         if ws[1] > 1:
             dist.all_reduce(t, group=self._sync_group)
 
-    def _sync_count(self, x):
-        """Rows over all ranks of the sync group (one collective per new input shape, cached)."""
-        import torch.distributed as dist
-        key = (tuple(x.shape), id(self._sync_group))
-        cache = self.__dict__.setdefault("_sync_counts", {})
-        n = cache.get(key)
-        if n is None:
-            t = torch.tensor([float(x.numel() // x.shape[1])], dtype=torch.float64,
-                             device=x.device if dist.get_backend(self._sync_group) == "nccl" else "cpu")
-            self._sync_allreduce(t)
-            n = cache[key] = int(t.item())
-        return n
+    def _sync_ops(self, x):
+        """The SyncBN sums contract (``bn_local_sums`` → all-reduce → ``bn_forward_from_sums``; the
+        backward twins): the HIP kernels for a native bf16 NHWC activation, otherwise the reference
+        implementation of the same contract (CPU, fp32), so every device issues the same host
+        sequence and collectives — the gloo multi-rank tests run exactly the GPU path's logic."""
+        from ...ops import native_ops as NO, reference as R
+        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+                and ops.native_has("batchnorm_forward_train")):
+            return NO
+        return R
 
-    def _sync_native_ok(self, x):
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
-                and ops.native_has("batchnorm_forward_train"))
-
-    def _sync_forward_native(self, x, g, b, relu, residual, in_bias):
-        """SyncBN on the HIP kernels: local shifted sums (the conv epilogue's partials when it
-        produced them, else one stats pass) → one RCCL all-reduce of 2·C floats → finalize over the
-        global row count → apply (+residual, ReLU).  The shift is the running mean, identical on
-        every rank.  NotImplemented → torch path."""
-        import torch.distributed as dist
-        from ...ops import native_ops as NO
+    def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None):
+        """SyncBN forward (``SpatialBatchNormalization.scala:1114-1151``): this rank's shifted sums
+        [Σ(x−K), Σ(x−K)², rows] (from the producing conv's epilogue partials when it left them) →
+        ONE all-reduce of 2·C + 1 floats → finalize over the global row count (read on the device:
+        no host sync, and ranks with uneven batches still issue identical collectives) → apply
+        (+residual, ReLU).  K is the running mean, identical on every rank."""
+        from ...ops import reference as R
+        impl = self._sync_ops(x)
         C_ = x.shape[1]
-        ps, self._pending_stats = self._pending_stats, None
-        if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape) and ps[4] is not None:
-            shift = ps[4]
-            sums = NO.bn_local_sums(x, shift, ps[2], ps[3])
-        else:
-            shift = self.runningMean
-            sums = NO.bn_local_sums(x, shift)
-        if sums is NotImplemented:
-            return NotImplemented
-        self._sync_allreduce(sums)
         coef = self._coef
         if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
             coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
-        r = NO.bn_forward_from_sums(x, sums, self._sync_count(x), shift, g, b, self.runningMean, self.runningVar,
-                                    self.momentum, self.eps, relu=relu, residual=residual, in_bias=in_bias,
-                                    coef_out=coef)
-        if r is not NotImplemented:
-            self._last_input = x
-        return r
-
-    def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None):
-        if self._sync_native_ok(x):
-            r = self._sync_forward_native(x, g, b, relu, residual, in_bias)
+        ps, self._pending_stats = self._pending_stats, None
+        r = NotImplemented
+        for m in ((impl, R) if impl is not R else (R,)):
+            if m is not R and ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape) \
+                    and ps[4] is not None:
+                shift = ps[4]
+                sums = m.bn_local_sums(x, shift, ps[2], ps[3])
+            else:
+                shift = self.runningMean
+                sums = m.bn_local_sums(x, shift)
+            if sums is NotImplemented:
+                continue
+            self._sync_allreduce(sums)
+            r = m.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar, self.momentum,
+                                       self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef)
             if r is not NotImplemented:
-                return r
-        mean, var, cnt = self._sync_stats(x)
-        invstd = torch.rsqrt(var + self.eps)
-        with torch.no_grad():
-            tm = mean if in_bias is None else mean + in_bias
-            self.runningMean.mul_(1 - self.momentum).add_(tm, alpha=self.momentum)
-            self.runningVar.mul_(1 - self.momentum).add_(var * (cnt / (cnt - 1).clamp_min(1)), alpha=self.momentum)
-        shape = [1, x.shape[1]] + [1] * (x.dim() - 2)
-        y = (acc_float(x) - mean.view(shape)) * invstd.view(shape)
-        if g is not None:
-            y = y * g.view(shape) + b.view(shape)
-        if residual is not None:
-            y = y + acc_float(residual)
-        if relu:
-            y = torch.relu(y)
-        return y.to(x.dtype), mean, invstd
+                self._sync_path = "native" if m is not R else "reference"
+                self._last_input = x
+                break
+        return r
 
     def _bwd(self, input, gradOutput, need_input, acc, want_gres=False):
         x = input if input.dim() > 1 else input.unsqueeze(0)
@@ -356,58 +311,43 @@ class BatchNormalization(TensorModule):
         return gi, gres
 
     def _sync_backward(self, x, gy, g, y, need_input, acc, relu=None, cb=None, cbs=0.0):
-        """→ (gradInput, whether the folded producer bias ``cb`` was accumulated here)."""
+        """SyncBN backward (``SpatialBatchNormalization.scala:1257-1329``): local [Σg', Σg'·(x − μ)]
+        → this rank's dγ/dβ (the data-parallel gradient all-reduce sums them across ranks); the
+        same sums + the row count all-reduced (2·C + 1 floats) → the input-gradient coefficients
+        → one apply pass.  → (gradInput, whether the folded producer bias ``cb`` was accumulated)."""
+        from ...ops import reference as R
         relu = self._fused_relu if relu is None else relu
-        import torch.distributed as dist
-        if self._sync_native_ok(x) and gy.dtype == torch.bfloat16:
-            # native: local [Σg, Σg·(x − μ)] → RCCL all-reduce of 2·C floats → local dγ/dβ and the
-            # global input-gradient coefficients → one apply pass
-            from ...ops import native_ops as NO
+        impl = self._sync_ops(x)
+        pg, self._pending_grad = self._pending_grad, None
+        C = x.shape[1]
+        rows = x.numel() // C
+        for m in ((impl, R) if impl is not R else (R,)):
+            rl = relu
             both = NotImplemented
-            pg, self._pending_grad = self._pending_grad, None
-            if pg is not None and pg[0] == gy.data_ptr() and relu:
+            if m is not R and pg is not None and pg[0] == gy.data_ptr() and relu:
                 # gy is already ReLU-masked by the consumer conv's dgrad epilogue, which also left
                 # the backward partial sums: reduce those instead of re-reading gy, x, y
-                both = NO.bn_bwd_partials_sums(pg[1], pg[2], x.shape[1], x.device)
+                both = m.bn_bwd_partials_sums(pg[1], pg[2], C, x.device, rows=rows)
                 if both is not NotImplemented:
-                    relu = False
+                    rl = False
             if both is NotImplemented:
-                both = NO.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=relu)
-            if both is not NotImplemented:
-                C2 = 2 * x.shape[1]
-                loc, glob = both[:C2], both[C2:]
-                self._sync_allreduce(glob)
-                gi = NO.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, self._sync_count(x),
-                                              y=y, relu=relu, need_input=need_input,
-                                              gg_acc=self.gradWeight if (acc and self.affine) else None,
-                                              gb_acc=self.gradBias if (acc and self.affine) else None,
-                                              scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
-                if gi is not NotImplemented:
-                    if acc and self.affine and self.scale_b != self.scale_w:
-                        self.gradBias.add_(loc[:x.shape[1]], alpha=self.scale_b - self.scale_w)
-                    return gi, cb is not None
-        C = x.shape[1]
-        dims = [d for d in range(x.dim()) if d != 1]
-        shape = [1, C] + [1] * (x.dim() - 2)
-        gf = acc_float(gy)
-        if relu:
-            gf = gf * (y > 0).float()
-        xhat = (acc_float(x) - self.saveMean.view(shape)) * self.saveStd.view(shape)
-        n = torch.tensor([x.numel() // C], dtype=torch.float32, device=x.device)
-        s = torch.cat([gf.sum(dims), (gf * xhat).sum(dims), n])
-        local_db, local_dg = s[:C].clone(), s[C:2 * C].clone()
-        self._sync_allreduce(s)
-        db, dg, cnt = s[:C], s[C:2 * C], s[-1]
-        if acc and self.affine:
-            self.gradWeight.add_(local_dg, alpha=self.scale_w)
-            self.gradBias.add_(local_db, alpha=self.scale_b)
-        if not need_input and cb is None:
-            return None, False
-        gam = g.view(shape) if g is not None else 1.0
-        gi = (gam * self.saveStd.view(shape) / cnt) * (cnt * gf - db.view(shape) - xhat * dg.view(shape))
-        if cb is not None:  # from the fp32 gradient, before rounding
-            cb.add_(gi.sum(dims), alpha=cbs)
-        return (gi.to(x.dtype) if need_input else None), cb is not None
+                both = m.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=rl)
+            if both is NotImplemented:
+                continue
+            loc, glob = both[:2 * C], both[2 * C:]
+            self._sync_allreduce(glob)
+            gi = m.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, 0, y=y, relu=rl,
+                                         need_input=need_input,
+                                         gg_acc=self.gradWeight if (acc and self.affine) else None,
+                                         gb_acc=self.gradBias if (acc and self.affine) else None,
+                                         scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
+            if gi is NotImplemented:
+                continue
+            if acc and self.affine and self.scale_b != self.scale_w:
+                self.gradBias.add_(loc[:C], alpha=self.scale_b - self.scale_w)
+            self._sync_bwd_path = "native" if m is not R else "reference"
+            return gi, cb is not None
+        raise RuntimeError("SyncBN backward: no implementation accepted the input")
 
     def updateGradInput(self, input, gradOutput):
         gi = self._bwd(input, gradOutput, True, True)

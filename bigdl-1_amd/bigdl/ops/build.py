@@ -76,6 +76,15 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = True) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    # a kernel template whose host-side instantiation fails substitution gets no launch stub, and hipcc
+    # reports no error: the library then fails to load on the GPU box.  Refuse such a link here.
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-D", "--undefined-only", out], capture_output=True, text=True)
+    missing = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l]
+    if missing:
+        os.remove(out)
+        raise RuntimeError("kernel launch stubs undefined (host-side template substitution failed): " +
+                           ", ".join(missing[:6]))
     if verbose:
         print(f"[bigdl.ops.build] {out} ({len(objs)} objects, arch {ARCH})")
     return out

@@ -138,7 +138,9 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_finalize(const bf16_t* __res
                                                       float* run_mean, float* __restrict__ run_var,
                                                       float momentum, float eps, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
-                                                      float* __restrict__ shift) {
+                                                      float* __restrict__ shift, const float* __restrict__ dM = nullptr) {
+  // dM: the row count read from device memory (SyncBN: the all-reduced count travels in the sums
+  // buffer, so the host never waits for it); else M
   __shared__ double lds[kFinRG][2][33];
   double s, q;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
@@ -148,8 +150,9 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_finalize(const bf16_t* __res
   // given the running mean — it may alias run_mean: read here, before run_mean is written below,
   // hence neither pointer is __restrict__) or unshifted
   const float K = kshift ? kshift[c] : (x ? bf2f(x[c]) : 0.f);
-  const double dmd = s / (double)M;
-  const float var = (float)fmax(q / (double)M - dmd * dmd, 0.0);
+  const double Md = dM ? (double)*dM : (double)M;
+  const double dmd = s / Md;
+  const float var = (float)fmax(q / Md - dmd * dmd, 0.0);
   const float dm = (float)dmd;
   float mean = K + dm;
   float invstd = rsqrtf(var + eps);
@@ -161,7 +164,7 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_finalize(const bf16_t* __res
   scale[c] = sc;
   shift[c] = bt - mean * sc;
   if (run_mean) {
-    float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    float unb = Md > 1.0 ? (float)(var * Md / (Md - 1.0)) : var;
     float true_mean = mean + (in_bias ? in_bias[c] : 0.f);
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * true_mean;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
@@ -496,7 +499,7 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __rest
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ ggamma, float* __restrict__ gbeta,
                                                           float gscale, float* __restrict__ cbias, float cbscale,
-                                                          float* __restrict__ coef) {
+                                                          float* __restrict__ coef, const float* __restrict__ dM = nullptr) {
   __shared__ double lds[kFinRG][2][33];
   double ad, bd;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, ad, bd);
@@ -510,12 +513,13 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __rest
   if (gbeta) gbeta[c] += gscale * dbeta;
   float gm = gamma ? gamma[c] : 1.f;
   float A = gm * is;
-  float B = -gm * is * is * dgamma / (float)M;
-  float Cc = -gm * is * dbeta / (float)M - B * mean[c];
+  const float Mf = dM ? *dM : (float)M;
+  float B = -gm * is * is * dgamma / Mf;
+  float Cc = -gm * is * dbeta / Mf - B * mean[c];
   coef[c] = A;
   coef[C + c] = B;
   coef[2 * C + c] = Cc;
-  if (cbias) cbias[c] += cbscale * (A * dbeta + B * (float)M * mean[c] + (float)M * Cc);
+  if (cbias) cbias[c] += cbscale * (A * dbeta + B * Mf * mean[c] + Mf * Cc);
 }
 
 template <bool RELU, bool GRES, int kApplyUnroll = 4>
@@ -642,12 +646,14 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_coef(const void* gm, const void* x, void* gx
 // path, so SyncBN costs two tiny kernels and one 2·C collective per direction.
 template <typename T>
 __global__ void __launch_bounds__(32 * kFinRG) k_bn_sum_rows(const T* __restrict__ partial, int G, int C,
-                                                      float* __restrict__ out, float* __restrict__ out2) {
+                                                      float* __restrict__ out, float* __restrict__ out2, float cnt) {
   __shared__ double lds[kFinRG][2][33];
   double a, b;
   reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
+  // this rank's row count behind the sums of the buffer the collective reduces ([2C + 1])
+  if (cnt >= 0.f && c == 0) (out2 ? out2 : out)[2 * C] = cnt;
   out[c] = (float)a;
   out[C + c] = (float)b;
   if (out2) {  // a second copy (the buffer the collective sums in place, next to the local sums)
@@ -657,54 +663,55 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_sum_rows(const T* __restrict
 }
 
 static void sum_rows(const float* partial, int G, int C, float* scratch, float* out, hipStream_t s,
-                     float* out2 = nullptr) {
+                     float* out2 = nullptr, float cnt = -1.f) {
   if (maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_sum_rows<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const double*)scratch, G, C, out,
-                       out2);
+                       out2, cnt);
   else
-    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, C, out, out2);
+    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, C, out, out2, cnt);
 }
 
-// Local shifted sums of x (kshift = the running mean, identical on every rank): out[2C].
+// Local shifted sums of x (kshift = the running mean, identical on every rank): out[2C], and the row
+// count (cnt ≥ 0) at out[2C].
 BIGDL_EXPORT int bigdl_bn_stats_sums(const void* x, long long M, int C, const float* kshift, float* ws,
-                                     float* scratch, float* out, hipStream_t s) {
+                                     float* scratch, float* out, float cnt, hipStream_t s) {
   if (C % 8 || M <= 0 || !kshift) return (int)hipErrorInvalidValue;
   int G = bigdl_bn_num_partials(M, C);
   long long rpb = (M + G - 1) / G;
   size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(G), dim3(256), sm, s, (const bf16_t*)x, M, C, rpb, ws, G, kshift);
-  sum_rows(ws, G, C, scratch, out, s);
+  sum_rows(ws, G, C, scratch, out, s, nullptr, cnt);
   BIGDL_CHECK_LAUNCH();
 }
 
 // Reduce G partial rows (a conv epilogue's, or any [2][G][C] fp32 block) to out[2C] (and the same
 // values to out2[2C] when given: the copy an in-place all-reduce turns into the global sums).
-BIGDL_EXPORT int bigdl_bn_partials_sums(const float* partial, int G, int C, float* scratch, float* out,
+BIGDL_EXPORT int bigdl_bn_partials_sums(const float* partial, int G, int C, float* scratch, float* out, float cnt,
                                         hipStream_t s) {
   if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  sum_rows(partial, G, C, scratch, out, s);
+  sum_rows(partial, G, C, scratch, out, s, nullptr, cnt);
   BIGDL_CHECK_LAUNCH();
 }
 
 BIGDL_EXPORT int bigdl_bn_partials_sums2(const float* partial, int G, int C, float* scratch, float* out, float* out2,
-                                         hipStream_t s) {
+                                         float cnt, hipStream_t s) {
   if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  sum_rows(partial, G, C, scratch, out, s, out2);
+  sum_rows(partial, G, C, scratch, out, s, out2, cnt);
   BIGDL_CHECK_LAUNCH();
 }
 
-// Forward from GLOBAL sums (2C, shifted by kshift): finalize over `count` rows (all ranks), apply
-// to this rank's M rows.
+// Forward from GLOBAL sums (2C, shifted by kshift): finalize over `count` rows (all ranks; 0 = the
+// all-reduced count stored at sums[2C]), apply to this rank's M rows.
 BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y, long long M, long long count, int C,
                                          const float* gamma, const float* beta, const float* in_bias,
                                          float* run_mean, float* run_var, float momentum, float eps,
                                          float* save_mean, float* save_invstd, const float* sums,
                                          const float* kshift, float* coef, int relu, hipStream_t s) {
-  if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
+  if (C % 8 || M <= 0 || count < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift, sums,
                      1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
-                     coef + C);
+                     coef + C, count == 0 ? sums + 2 * C : nullptr);
   launch_apply(x, res, y, M, C, coef, relu, nullptr, s);
   BIGDL_CHECK_LAUNCH();
 }
@@ -712,7 +719,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
 // Backward local sums: Σg', Σg'·(x − mean) (g' = gy masked by y > 0 when relu) → out[2C] and the
 // same values in out[2C..4C) (the copy the all-reduce turns into the global sums).
 BIGDL_EXPORT int bigdl_bn_bwd_sums(const void* gy, const void* x, const void* y, long long M, int C, const float* mean,
-                                   float* ws, float* scratch, float* out, int relu, hipStream_t s) {
+                                   float* ws, float* scratch, float* out, int relu, float cnt, hipStream_t s) {
   if (C % 8 || M <= 0) return (int)hipErrorInvalidValue;
   int G = bigdl_bn_num_partials(M, C);
   long long rpb = (M + G - 1) / G;
@@ -723,7 +730,7 @@ BIGDL_EXPORT int bigdl_bn_bwd_sums(const void* gy, const void* x, const void* y,
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(G), dim3(256), sm, s, (const bf16_t*)gy, (const bf16_t*)x,
                        (const bf16_t*)y, M, C, rpb, mean, ws, G);
-  sum_rows(ws, G, C, scratch, out, s, out + 2 * C);
+  sum_rows(ws, G, C, scratch, out, s, out + 2 * C, cnt);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -747,12 +754,13 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
                                          const float* invstd, float* ggamma, float* gbeta, float gscale,
                                          const float* local_sums, const float* global_sums, float* coef,
                                          float* coef_scratch, int relu, float* cbias, float cbscale, hipStream_t s) {
-  if (C % 8 || M <= 0 || count <= 0) return (int)hipErrorInvalidValue;
+  if (C % 8 || M <= 0 || count < 0) return (int)hipErrorInvalidValue;
+  const float* dM = count == 0 ? global_sums + 2 * C : nullptr;  // the all-reduced count
   if (ggamma || gbeta)
     hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, local_sums, 1, count, C, gamma,
-                       mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch);
+                       mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch, dM);
   hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, global_sums, 1, count, C, gamma,
-                     mean, invstd, (float*)nullptr, (float*)nullptr, 0.f, (float*)nullptr, 0.f, coef);
+                     mean, invstd, (float*)nullptr, (float*)nullptr, 0.f, (float*)nullptr, 0.f, coef, dM);
   if (cbias)
     hipLaunchKernelGGL(k_bn_cbias_sync, dim3((C + 255) / 256), dim3(256), 0, s, local_sums, coef, mean, M, C, cbias,
                        cbscale);

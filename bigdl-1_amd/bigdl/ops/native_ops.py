@@ -231,34 +231,38 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
 
 # ---- SyncBN (cross-rank statistics; the caller all-reduces the 2·C sums between the halves) ----
 def bn_local_sums(x, shift, partial=None, G=0):
-    """This rank's shifted sums [Σ(x−K), Σ(x−K)²] (fp32 [2C]) with K = ``shift`` (the running mean,
-    identical on every rank): from a producing conv's epilogue partials (``partial``/``G``, which
-    must have been computed with the same shift) or a stats pass over x.  NotImplemented when the
-    native path cannot run."""
+    """This rank's shifted sums [Σ(x−K), Σ(x−K)², rows] (fp32 [2C + 1]) with K = ``shift`` (the
+    running mean, identical on every rank): from a producing conv's epilogue partials
+    (``partial``/``G``, which must have been computed with the same shift) or a stats pass over x.
+    The row count rides in the buffer the all-reduce sums, so every rank issues the same collective
+    every step whatever its batch, and the global count never needs a host read.  NotImplemented
+    when the native path cannot run."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
     if not _bn_ok(x, C_) or not _f32vec(shift, C_):
         return NotImplemented
-    out = torch.empty(2 * C_, dtype=_f32, device=x.device)
+    out = torch.empty(2 * C_ + 1, dtype=_f32, device=x.device)
     if partial is not None:
         if partial.numel() != 2 * G * C_ or partial.dtype != _f32:
             return NotImplemented
         check(_lib().bigdl_bn_partials_sums(ptr(partial), C.c_int(G), C.c_int(C_),
-                                            ptr(_fold_scratch(G, C_, x.device)), ptr(out), _s()), "bn_partials_sums")
+                                            ptr(_fold_scratch(G, C_, x.device)), ptr(out), _f(M), _s()),
+              "bn_partials_sums")
         return out
     lib = _lib()
     Gs = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
     ws = torch.empty(2 * Gs * C_, dtype=_f32, device=x.device)
     check(lib.bigdl_bn_stats_sums(ptr(x), _ll(M), C.c_int(C_), ptr(shift), ptr(ws), ptr(_fold_scratch(Gs, C_, x.device)),
-                                  ptr(out), _s()), "bn_stats_sums")
+                                  ptr(out), _f(M), _s()), "bn_stats_sums")
     return out
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
                          residual=None, in_bias=None, coef_out=None):
-    """Training BN from GLOBAL shifted sums over ``count`` rows: (y, save_mean, save_invstd)."""
+    """Training BN from GLOBAL shifted sums over ``count`` rows (0: the all-reduced count at
+    ``sums[2C]``): (y, save_mean, save_invstd)."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -280,8 +284,8 @@ def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, runni
 
 
 def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
-    """This rank's [Σg', Σg'·(x − mean)] twice (fp32 [4C]: the local sums, then a copy for the
-    in-place all-reduce); g' = gy·[y > 0] when ``relu``."""
+    """This rank's [Σg', Σg'·(x − mean)] twice (fp32 [4C + 1]: the local sums, then a copy for the
+    in-place all-reduce followed by this rank's row count); g' = gy·[y > 0] when ``relu``."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -293,28 +297,29 @@ def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
     lib = _lib()
     G = lib.bigdl_bn_num_partials(_ll(M), C.c_int(C_))
     ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
-    out = torch.empty(4 * C_, dtype=_f32, device=x.device)
+    out = torch.empty(4 * C_ + 1, dtype=_f32, device=x.device)
     check(lib.bigdl_bn_bwd_sums(ptr(gy), ptr(x), ptr(y if relu else None), _ll(M), C.c_int(C_), ptr(save_mean), ptr(ws),
-                                ptr(_fold_scratch(G, C_, x.device)), ptr(out), C.c_int(1 if relu else 0), _s()),
+                                ptr(_fold_scratch(G, C_, x.device)), ptr(out), C.c_int(1 if relu else 0), _f(M), _s()),
           "bn_bwd_sums")
     return out
 
 
-def bn_bwd_partials_sums(partial, G, C_, dev):
-    """[Σg', Σg'·(x − mean)] twice (fp32 [4C]) from the consumer conv's dgrad-epilogue partials
-    (``_pending_grad``): no pass over the activations."""
-    if partial is None or partial.dtype != _f32 or partial.numel() != 2 * G * C_:
+def bn_bwd_partials_sums(partial, G, C_, dev, rows=None):
+    """[Σg', Σg'·(x − mean)] twice (fp32 [4C + 1], ``rows`` last) from the consumer conv's
+    dgrad-epilogue partials (``_pending_grad``): no pass over the activations."""
+    if partial is None or partial.dtype != _f32 or partial.numel() != 2 * G * C_ or rows is None:
         return NotImplemented
-    out = torch.empty(4 * C_, dtype=_f32, device=dev)
+    out = torch.empty(4 * C_ + 1, dtype=_f32, device=dev)
     check(_lib().bigdl_bn_partials_sums2(ptr(partial), C.c_int(G), C.c_int(C_), ptr(_fold_scratch(G, C_, dev)),
-                                         ptr(out), ptr(out[2 * C_:]), _s()), "bn_partials_sums2")
+                                         ptr(out), ptr(out[2 * C_:]), _f(rows), _s()), "bn_partials_sums2")
     return out
 
 
 def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
                           need_input=True, gg_acc=None, gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0):
-    """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows → gradInput;
-    ``cbias_acc`` receives this rank's share of a folded producer bias's gradient (fp32 closed form)."""
+    """SyncBN backward: local sums → this rank's dγ/dβ; global sums over ``count`` rows (0: the
+    all-reduced count at ``global_sums[2C]``) → gradInput; ``cbias_acc`` receives this rank's share
+    of a folded producer bias's gradient (fp32 closed form)."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented

@@ -247,6 +247,99 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
     return gi, (g.to(gy.dtype) if want_gres else None)
 
 
+# ---- SyncBN sums contract (native_ops.bn_local_sums & co.; the host path of P6 runs on these on
+# CPU tensors, so the gloo multi-rank tests exercise exactly the collective sequence of the GPU path)
+def _bn_dims(x):
+    return [d for d in range(x.dim()) if d != 1], [1, x.shape[1]] + [1] * (x.dim() - 2)
+
+
+def bn_local_sums(x, shift, partial=None, G=0):
+    """[Σ(x−K), Σ(x−K)², rows] fp32 [2C + 1] with K = ``shift``."""
+    C = x.shape[1]
+    dims, shape = _bn_dims(x)
+    if partial is not None:
+        p = partial.view(2, G, C).sum(1)
+        return torch.cat([p.reshape(-1), p.new_tensor([float(x.numel() // C)])])
+    xf = acc_float(x) - acc_float(shift).to(acc_float(x).dtype).view(shape)
+    return torch.cat([xf.sum(dims), (xf * xf).sum(dims), xf.new_tensor([float(x.numel() // C)])])
+
+
+def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
+                         residual=None, in_bias=None, coef_out=None):
+    """Training BN from GLOBAL shifted sums over ``count`` rows (0: ``sums[2C]``)."""
+    C = x.shape[1]
+    dims, shape = _bn_dims(x)
+    n = sums[2 * C].double() if count == 0 else torch.tensor(float(count), dtype=torch.float64, device=x.device)
+    dm = sums[:C].double() / n
+    var = (sums[C:2 * C].double() / n - dm * dm).clamp_min(0)
+    fd = acc_float(x).dtype
+    mean = (acc_float(shift).double() + dm).to(fd)
+    var = var.to(fd)
+    invstd = torch.rsqrt(var + eps)
+    if running_mean is not None:
+        with torch.no_grad():
+            unb = (var.double() * n / (n - 1).clamp_min(1)).to(fd)
+            tm = mean if in_bias is None else mean + acc_float(in_bias)
+            running_mean.mul_(1 - momentum).add_(tm, alpha=momentum)
+            running_var.mul_(1 - momentum).add_(unb, alpha=momentum)
+    sc = invstd * (acc_float(gamma) if gamma is not None else 1.0)
+    sh = (acc_float(beta) if beta is not None else 0.0) - mean * sc
+    if coef_out is not None:
+        coef_out[:C].copy_(sc)
+        coef_out[C:2 * C].copy_(sh)
+    y = acc_float(x) * sc.view(shape) + sh.view(shape)
+    if residual is not None:
+        y = y + acc_float(residual)
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype), mean, invstd
+
+
+def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
+    """[Σg', Σg'·(x − μ)] twice, then this rank's rows: fp32 [4C + 1]."""
+    C = x.shape[1]
+    dims, shape = _bn_dims(x)
+    g = acc_float(gy)
+    if relu:
+        g = g * (y > 0).float()
+    xc = acc_float(x) - save_mean.view(shape)
+    loc = torch.cat([g.sum(dims), (g * xc).sum(dims)])
+    return torch.cat([loc, loc, loc.new_tensor([float(x.numel() // C)])])
+
+
+def bn_bwd_partials_sums(partial, G, C_, dev, rows=None):
+    p = partial.view(2, G, C_).sum(1).reshape(-1)
+    return torch.cat([p, p, p.new_tensor([float(rows)])])
+
+
+def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
+                          need_input=True, gg_acc=None, gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0):
+    """SyncBN backward from LOCAL (dγ/dβ of this rank) and GLOBAL (gradInput) sums."""
+    C = x.shape[1]
+    dims, shape = _bn_dims(x)
+    n = global_sums[2 * C] if count == 0 else torch.tensor(float(count), device=x.device)
+    is_ = save_invstd
+    if gg_acc is not None and scale != 0:
+        gg_acc.add_(local_sums[C:2 * C] * is_, alpha=scale)
+    if gb_acc is not None and scale != 0:
+        gb_acc.add_(local_sums[:C], alpha=scale)
+    gm = acc_float(gamma) if gamma is not None else torch.ones_like(is_)
+    db, dgc = global_sums[:C], global_sums[C:2 * C]
+    A = gm * is_
+    B = -gm * is_ * is_ * (dgc * is_) / n
+    Cc = -gm * is_ * db / n - B * save_mean
+    if cbias_acc is not None and cbias_scale != 0:
+        m_loc = float(x.numel() // C)
+        cbias_acc.add_(A * local_sums[:C] + m_loc * (B * save_mean + Cc), alpha=cbias_scale)
+    if not need_input:
+        return None
+    g = acc_float(gy)
+    if relu:
+        g = g * (y > 0).float()
+    gx = A.view(shape) * g + B.view(shape) * acc_float(x) + Cc.view(shape)
+    return gx.to(x.dtype)
+
+
 # ------------------------------------------------------------------------- pooling
 def maxpool2d_forward(x, k, s, p, ceil_mode, need_indices=True):
     if not need_indices:
@@ -368,14 +461,17 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
     ``grad_scale`` folds the 1/N gradient averaging in; ``lrs``/``wds`` are per-element
     learning-rate / weight-decay multipliers (``learningRates``/``weightDecays``)."""
     g = g.float()  # a bf16-wire gradient shard is consumed directly
-    if first_dev is not None and float(first_dev.reshape(-1)[0]) != 0:
-        first_step = True
     gg = g * grad_scale if grad_scale != 1.0 else g.clone()
     if weight_decay != 0:
         gg.add_(w * (wds if wds is not None else 1.0), alpha=weight_decay)
     if momentum != 0:
         if first_step:
             buf.copy_(gg)
+        elif first_dev is not None:
+            # the device-side first-step flag (graph mode) is applied on the device: no host read,
+            # so this fallback stays legal inside a HIP-graph capture
+            first = first_dev.reshape(-1)[:1] != 0
+            buf.copy_(torch.where(first, gg, buf * momentum + (1 - dampening) * gg))
         else:
             buf.mul_(momentum).add_(gg, alpha=1 - dampening)
         if nesterov:

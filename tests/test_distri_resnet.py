@@ -86,6 +86,11 @@ def _worker(rank, world, port, mode, comm_dtype, out_q, early=True):
         opt.train_step(MiniBatch(xs, ys))
         n_early += sum(1 for b in opt.buckets if b.early)
     opt._finish()
+    # every BN ran the SyncBN sums contract (the GPU path's host sequence) on its reference kernels
+    from bigdl.nn.layers.normalization import BatchNormalization
+    paths = {(getattr(m, "_sync_path", None), getattr(m, "_sync_bwd_path", None))
+             for m in model.flattened_modules() if isinstance(m, BatchNormalization)}
+    assert paths == {("reference", "reference")}, paths
     if rank == 0:
         out_q.put((torch.cat([p.reshape(-1) for p in model.parameters()[0]]).numpy(), n_early, len(opt.buckets)))
     Engine.shutdown()
