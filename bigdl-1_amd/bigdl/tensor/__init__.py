@@ -1,3 +1,4 @@
 from .tensor import Tensor
 from .sparse import SparseTensor
 from .quantized import QuantizedTensor
+from .storage import Storage

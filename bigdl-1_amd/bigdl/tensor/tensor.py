@@ -572,6 +572,233 @@ class Tensor:
         o = _unwrap(other)
         return self.data.shape == o.shape and bool((self.data.float() - o.float()).abs().max() <= delta) if self.data.numel() else True
 
+    # ---- comparison / element-wise extras (TensorMath.scala:222-824, DenseTensor.scala:2028-2271) ----
+    def ge(self, a, b):
+        """self = (a >= b) as 0/1 (``TensorMath.ge``, :740)."""
+        self.data = (_unwrap(a) >= _unwrap(b)).to(self.data.dtype)
+        return self
+
+    def notEqualValue(self, value) -> bool:
+        """True when any element differs from ``value``."""
+        return bool((self.data != value).any())
+
+    def _cpair(self, fn, a, b):
+        if b is None:  # x.cmax(y) / x.cmax(value): in place
+            o = _unwrap(a)
+            self.data.copy_(fn(self.data, o if isinstance(o, torch.Tensor) else torch.tensor(o, dtype=self.data.dtype)))
+            return self
+        x, y = _unwrap(a), _unwrap(b)  # z.cmax(x, y): z = max(x, y)
+        r = fn(x, y if isinstance(y, torch.Tensor) else torch.tensor(y, dtype=x.dtype))
+        if self.data.shape != r.shape:
+            self.data = torch.empty_like(r)
+        self.data.copy_(r)
+        return self
+
+    def cmax(self, a, b=None):
+        """Element-wise maximum with a tensor or a value (``TensorMath.cmax``, :305/:771/:789)."""
+        return self._cpair(torch.maximum, a, b)
+
+    def cmin(self, a, b=None):
+        return self._cpair(torch.minimum, a, b)
+
+    def sign(self):
+        """In place: +1 / −1 / 0 (``DenseTensor.sign``, :2028)."""
+        self.data.copy_(torch.sign(self.data))
+        return self
+
+    def _conv2(self, kernel, vf, flip):
+        import torch.nn.functional as F
+        vf = vf.upper() if isinstance(vf, str) else vf
+        if vf not in ("V", "F"):
+            raise ValueError(f"type must be 'V' (valid) or 'F' (full), got {vf!r}")
+        x, k = self.data, _unwrap(kernel).to(self.data.dtype)
+        if x.dim() != 2 or k.dim() != 2:
+            raise ValueError("conv2 / xcorr2 take 2-D tensors")
+        if flip:
+            k = torch.flip(k, (0, 1))
+        pad = (k.shape[0] - 1, k.shape[1] - 1) if vf == "F" else (0, 0)
+        r = F.conv2d(x[None, None], k[None, None], padding=pad)[0, 0]
+        return Tensor(r)
+
+    def conv2(self, kernel, vf="V"):
+        """2-D convolution (kernel flipped): valid ('V') or full ('F') (``TensorMath.conv2``, :222)."""
+        return self._conv2(kernel, vf, True)
+
+    def xcorr2(self, kernel, vf="V"):
+        """2-D cross-correlation, valid or full (``TensorMath.xcorr2``, :232)."""
+        return self._conv2(kernel, vf, False)
+
+    def diff(self, other, count: int = 1, reverse: bool = False) -> bool:
+        """Print up to ``count`` differing elements; True if the tensors differ (``DenseTensor.diff``,
+        :1647); ``reverse`` scans from the last element."""
+        o = _unwrap(other)
+        if self.data.dim() != o.dim():
+            print("Dimension number is different")
+            return True
+        for d in range(self.data.dim()):
+            if self.data.shape[d] != o.shape[d]:
+                print(f"Dimension {d + 1} is different, left is {self.data.shape[d]}, right is {o.shape[d]}")
+                return True
+        a, b = self.data.reshape(-1), o.reshape(-1)
+        idx = torch.nonzero(a != b).reshape(-1)
+        if reverse:
+            idx = idx.flip(0)
+        for i in idx[:count].tolist():
+            print(f"Find difference at {i + 1}: left {a[i].item()}, right {b[i].item()}")
+        return idx.numel() > 0
+
+    def reduce(self, dim: int, result, reducer):
+        """Fold dimension ``dim`` (1-based) with the binary ``reducer`` into ``result`` (size 1 along
+        ``dim``; ``TensorMath.reduce``, :824 / ``DenseTensor.scala:2260``)."""
+        import functools
+        d = _dim0(dim, self.data.dim())
+        a = self.data.detach().cpu().numpy()
+        out = np.apply_along_axis(lambda v: functools.reduce(reducer, v.tolist()), d, a)
+        r = torch.from_numpy(np.expand_dims(np.asarray(out, dtype=a.dtype), d))
+        res = _unwrap(result)
+        if tuple(res.shape) != tuple(r.shape):
+            res.resize_(r.shape)
+        res.copy_(r)
+        return result
+
+    def applyFun(self, t, func):
+        """self[i] = func(t[i]), any source dtype (``Tensor.applyFun``, :520)."""
+        src = _unwrap(t).detach().cpu().numpy()
+        out = np.vectorize(func, otypes=[np.float64])(src) if src.size else src.astype(np.float64)
+        if tuple(self.data.shape) != tuple(src.shape):
+            self.data = torch.empty(src.shape, dtype=self.data.dtype, device=self.data.device)
+        self.data.copy_(torch.from_numpy(out).to(self.data.dtype))
+        return self
+
+    def zipWith(self, t1, t2, func):
+        """self[i] = func(t1[i], t2[i]) (``Tensor.zipWith``, :547)."""
+        a = _unwrap(t1).detach().cpu().numpy()
+        b = _unwrap(t2).detach().cpu().numpy()
+        out = np.vectorize(func, otypes=[np.float64])(a, b) if a.size else a.astype(np.float64)
+        if tuple(self.data.shape) != tuple(a.shape):
+            self.data = torch.empty(a.shape, dtype=self.data.dtype, device=self.data.device)
+        self.data.copy_(torch.from_numpy(out).to(self.data.dtype))
+        return self
+
+    def cast(self, cast_tensor):
+        """Copy this tensor's values, converted, into ``cast_tensor`` (whatever its dtype) and return
+        it (``Tensor.cast``, :387)."""
+        dst = cast_tensor if isinstance(cast_tensor, Tensor) else Tensor(cast_tensor)
+        if tuple(dst.data.shape) != tuple(self.data.shape):
+            dst.data = torch.empty(self.data.shape, dtype=dst.data.dtype, device=dst.data.device)
+        dst.data.copy_(self.data.to(dst.data.dtype))
+        return dst
+
+    def forceFill(self, v):
+        """Fill with ``v`` converted to this tensor's dtype (``Tensor.forceFill``, :113)."""
+        self.data.fill_(torch.tensor(v).to(self.data.dtype).item())
+        return self
+
+    def uniform(self, *args) -> float:
+        """One uniform draw from the framework RNG: [0, 1); one arg a → between 1 and a; two args
+        → [a, b] (``TensorMath.uniform``, :500)."""
+        if not args:
+            return RNG.uniform(0.0, 1.0)
+        if len(args) == 1:
+            lo, hi = sorted((1.0, float(args[0])))
+        else:
+            lo, hi = float(args[0]), float(args[1])
+        return lo if lo == hi else RNG.uniform(lo, hi)
+
+    # ---- storage / shape helpers (Tensor.scala:200-725) -------------------------------------------
+    def storage(self):
+        """The flat storage under this tensor, shared (``Tensor.storage``, :441)."""
+        from .storage import Storage
+        return Storage.of(self.data)
+
+    def value(self):
+        """The value of a one-element tensor (``Tensor.value``, :200)."""
+        if self.data.numel() != 1:
+            raise ValueError(f"value() needs a scalar tensor, got shape {tuple(self.data.shape)}")
+        return self.data.reshape(()).item()
+
+    def toArray(self):
+        """Elements in row-major order as a flat Python list."""
+        return self.data.detach().reshape(-1).cpu().tolist()
+
+    def dim(self) -> int:
+        return self.data.dim()
+
+    def getTensorType(self) -> str:
+        return "DenseType"
+
+    def getTensorNumeric(self) -> str:
+        return {torch.float32: "float", torch.float64: "double", torch.int32: "int", torch.int64: "long",
+                torch.int16: "short", torch.bool: "boolean", torch.bfloat16: "bfloat16",
+                torch.float16: "half"}.get(self.data.dtype, str(self.data.dtype))
+
+    def shallowClone(self):
+        """A new tensor over the same storage and geometry (``Tensor.shallowClone``, :358)."""
+        return Tensor(self.data.view(self.data.shape) if self.data.numel() else self.data)
+
+    def emptyInstance(self):
+        return Tensor(torch.empty(0, dtype=self.data.dtype, device=self.data.device))
+
+    def squeezeNewTensor(self):
+        return Tensor(self.data.squeeze())
+
+    def addSingletonDimension(self, t=None, dim: int = 1):
+        """self ← a view of ``t`` (default self) with a size-1 dimension inserted at ``dim`` (1-based)."""
+        src = self.data if t is None else _unwrap(t)
+        if dim < 1 or dim > src.dim() + 1:
+            raise IndexError(f"dimension {dim} out of range [1, {src.dim() + 1}]")
+        self.data = src.unsqueeze(dim - 1)
+        return self
+
+    def addMultiDimension(self, t=None, dims=(1,)):
+        """Insert size-1 dimensions at each of ``dims`` (positions in the source's numbering, shifted
+        as earlier inserts land; ``DenseTensor.addMultiDimension``, :2095)."""
+        src = self.data if t is None else _unwrap(t)
+        ds = list(dims)
+        for i in range(len(ds)):
+            for j in range(i + 1, len(ds)):
+                if ds[j] > ds[i]:
+                    ds[j] += 1
+        out = src
+        for d in ds:
+            out = out.unsqueeze(d - 1)
+        self.data = out
+        return self
+
+    def numNonZeroByRow(self):
+        """Non-zero count of every slice along the first dimension."""
+        return (self.data.reshape(self.data.shape[0], -1) != 0).sum(1).tolist()
+
+    def update(self, index, value):
+        """``Tensor.update`` (:243-319): index = 1-based int (a value or a sub-tensor copy), a list
+        of 1-based indices (one element), or a predicate (every element it accepts ← value)."""
+        if callable(index):
+            arr = self.data.detach().cpu().numpy()
+            mask = torch.from_numpy(np.vectorize(index, otypes=[bool])(arr)).to(self.data.device)
+            self.data.masked_fill_(mask, value)
+        elif isinstance(index, (list, tuple)):
+            self.data[tuple(i - 1 for i in index)] = value
+        else:
+            v = _unwrap(value)
+            if isinstance(v, torch.Tensor):
+                self.data[index - 1].copy_(v)
+            else:
+                self.data[index - 1] = v
+
+    def save(self, path: str, over_write: bool = False):
+        """Write the tensor to ``path`` (numpy .npy; loaded back by :meth:`load` without unpickling)."""
+        import os
+        if os.path.exists(path) and not over_write:
+            raise FileExistsError(path)
+        with open(path, "wb") as fh:
+            np.save(fh, self.toNumpy(), allow_pickle=False)
+        return self
+
+    @staticmethod
+    def load(path: str):
+        with open(path, "rb") as fh:
+            return Tensor(torch.from_numpy(np.load(fh, allow_pickle=False)))
+
     # ---- conversion ------------------------------------------------------------------------------------
     def toNumpy(self):
         return self.data.detach().cpu().numpy()

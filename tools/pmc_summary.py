@@ -44,8 +44,9 @@ for (shape, k), cnt in sorted(res.items()):
         # reconciliation: every v_mfma_f32_16x16x32_bf16 is 16·16·32·2 FLOP; FLOP / trace duration
         # is the achieved rate, and ÷ 2.5 PF dense bf16 must match the busy-counter utilisation
         d = sorted(dur[(shape, k)])[len(dur[(shape, k)]) // 2]
-        tf = m["SQ_INSTS_MFMA"] * 16384 / d / 1e3
-        print(f"   median duration {d / 1e3:.1f} us; MFMA FLOP {m['SQ_INSTS_MFMA'] * 16384 / 1e9:.2f} GFLOP; "
+        fpm = 32768 if "k_conv_x8" in k else 16384  # 32x32x16 vs 16x16x32 bf16 MFMA
+        tf = m["SQ_INSTS_MFMA"] * fpm / d / 1e3
+        print(f"   median duration {d / 1e3:.1f} us; MFMA FLOP {m['SQ_INSTS_MFMA'] * fpm / 1e9:.2f} GFLOP; "
               f"{tf:.0f} TF/s = {tf / 2500:.3f} of 2.5 PF")
         print(f"   VALU per MFMA = {m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f}")
     if "TCC_HIT_sum" in m:
