@@ -397,7 +397,11 @@ class DistriOptimizer(BaseOptimizer):
         # a cancelled replica records no time (the reference leaves its slot at 0)
         self._drop_times[self._drop_iter % window] = 0.0 if dropped else dt
         kept = 0.0 if dropped else 1.0
-        v = torch.stack([loss_t.reshape(()).float() * kept, torch.ones((), device=loss_t.device) * kept])
+        # a dropped rank's loss is SELECTED away, not multiplied by 0 (NaN · 0 = NaN would poison the
+        # all-reduced loss and every loss-driven trigger)
+        lv = loss_t.reshape(()).float()
+        v = torch.stack([torch.where(torch.tensor(kept > 0, device=lv.device), lv, torch.zeros_like(lv)),
+                         torch.ones((), device=loss_t.device) * kept])
         if comm.is_dist():
             dist.all_reduce(v)
         fin = int(round(float(v[1])))

@@ -257,7 +257,21 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
     sharded run of the SAME world size that finds its own ``.rank<r>`` state file.  Loaded methods
     carry ``_arena_slice`` (offset, length) when the checkpoint recorded it."""
     wait_checkpoints()
-    sfile = _latest(os.path.join(path, "state*"))
+    # newest first; a checkpoint whose sharded optimizer files are incomplete (a crash between the
+    # state file and another rank's shard write) is skipped for the next-newest complete one
+    states = sorted((f for f in glob.glob(os.path.join(path, "state*")) if ".rank" not in f and ".tmp" not in f),
+                    key=os.path.getmtime, reverse=True)
+    last_err = None
+    for sfile in states or [None]:
+        try:
+            return _load_checkpoint_at(path, sfile, world_size, sharded)
+        except FileNotFoundError as e:
+            last_err = e
+            continue
+    raise last_err
+
+
+def _load_checkpoint_at(path, sfile, world_size, sharded):
     meta = {}
     sfx = None
     if sfile:
@@ -299,8 +313,13 @@ def load_latest_checkpoint(path: str, world_size: Optional[int] = None,
         f = methods[name][1]
         fsfx = f[len(os.path.join(path, "optimMethod-" + name)):]
         shard = os.path.join(path, f"optimMethod-{_shard_key(i, name, slices)}{fsfx}.rank{rank}")
-        if ck_sharded and not os.path.exists(shard):
-            raise FileNotFoundError(f"sharded checkpoint: missing this rank's optimizer state {shard}")
+        if ck_sharded:
+            # every rank's shard must be there (not only this rank's), so all ranks agree on which
+            # checkpoint is complete and resume from the same one
+            for r in range(ck_world):
+                sr = os.path.join(path, f"optimMethod-{_shard_key(i, name, slices)}{fsfx}.rank{r}")
+                if not os.path.exists(sr):
+                    raise FileNotFoundError(f"sharded checkpoint: missing rank {r}'s optimizer state {sr}")
         m = load_optim_method(shard if ck_sharded else f)
         if name in slices:
             m._arena_slice = tuple(slices[name])

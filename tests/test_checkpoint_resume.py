@@ -81,3 +81,28 @@ def test_torn_checkpoint_loads_complete_set(tmp_path):
     assert state["neval"] == 3
     assert float(model.weight.flatten()[0]) == 2.0
     assert float(methods["sgd"].state["dfdx"][0]) == 2.0
+
+
+def test_sharded_checkpoint_missing_shard_falls_back(tmp_path, monkeypatch):
+    """A crash after rank 0's state file but before another rank's ``.rank<r>`` shard landed: every
+    rank must resume from the previous COMPLETE checkpoint (not raise, and not disagree on which)."""
+    from bigdl.serialization.checkpoint import save_checkpoint, save_shard_state, load_latest_checkpoint
+    from bigdl.nn import Linear
+    from bigdl.optim import SGD
+    m = Linear(3, 2)
+    sgd = SGD(learningrate=0.1, momentum=0.9)
+    slices = {"sgd": (0, 8)}
+    for n in (2, 3):
+        m.weight.fill_(float(n))
+        for r in range(2):
+            sgd.state["dfdx"] = torch.full((4,), float(10 * n + r))
+            save_shard_state(str(tmp_path), {"sgd": sgd}, {"neval": n + 1}, rank=r, slices=slices)
+        save_checkpoint(str(tmp_path), m, {"sgd": sgd}, {"neval": n + 1, "epoch": 1}, world_size=2, sharded=True,
+                        slices=slices)
+    os.remove(tmp_path / "optimMethod-@0.3.rank1")
+    for rank in (0, 1):
+        monkeypatch.setenv("RANK", str(rank))
+        model, methods, state = load_latest_checkpoint(str(tmp_path), world_size=2, sharded=True)
+        assert state["neval"] == 3
+        assert float(model.weight.flatten()[0]) == 2.0
+        assert float(methods["sgd"].state["dfdx"][0]) == 20.0 + rank
