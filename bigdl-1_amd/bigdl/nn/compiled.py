@@ -201,9 +201,87 @@ def plan(model, example, phase: str = "inference") -> Plan:
 
 
 #: tile candidates (BN output channels, BK k-tile depth, BM output pixels) of the implicit-GEMM
-#: forward; (0, 0, 0) is the launcher's shape heuristic
+#: forward; (0, 0, 0) is the launcher's shape heuristic.  BK = 1 is the 8-wave 32x32x16 / LDS-DMA
+#: family (ops/csrc/conv_mfma32.hip), which wins on the deep reductions (C ≥ 256 3×3, C ≥ 1024 1×1).
 TILE_CANDIDATES = ((0, 0, 0), (64, 32, 128), (64, 64, 128), (128, 32, 128), (128, 64, 128), (64, 64, 256),
-                   (128, 64, 256))
+                   (128, 64, 256), (128, 1, 128), (64, 1, 256), (128, 1, 256))
+
+#: weight-gradient candidates (target blocks of the pixel split, k-tile pixel depth); 0 = heuristic
+WGRAD_CANDIDATES = ((0, 0), (0, 32), (0, 64), (256, 0), (768, 0), (1024, 0), (256, 32), (768, 64))
+
+
+def _candidates(key):
+    return WGRAD_CANDIDATES if (isinstance(key, tuple) and key and key[0] == "wg") else TILE_CANDIDATES
+
+
+def _time_candidates(key, fn, iters, lib):
+    import torch
+    times = {}
+    for cand in _candidates(key):
+        if len(cand) == 3 and lib.bigdl_conv_tile_ok(*cand) != 0:
+            continue
+        try:
+            fn(cand)  # warm-up (and validity: an unsupported combination raises)
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(iters):
+                fn(cand)
+            t1.record()
+            t1.synchronize()
+            times[cand] = t0.elapsed_time(t1) / iters
+        except RuntimeError:
+            continue
+    return times
+
+
+def select_kernels(records, iters: int = 5, min_gain: float = 0.03) -> Dict[tuple, tuple]:
+    """Time every candidate of every distinct recorded launch geometry (``records`` = the
+    (key, relaunch-with-tile) pairs a recorded pass left in ``native_ops._TILE["record"]``) and pin
+    the fastest one when it beats the launcher's heuristic by more than ``min_gain``.  Forward /
+    backward-data launches (conv geometry keys) take :data:`TILE_CANDIDATES`, weight-gradient
+    launches (``("wg", ...)`` keys) :data:`WGRAD_CANDIDATES`."""
+    from ..ops import native_ops as NO
+    lib = NO._lib()
+    table = NO._TILE["table"]
+    chosen = {}
+    seen = {}
+    for key, fn in records:
+        seen.setdefault(key, fn)
+    for key, fn in seen.items():
+        table.pop(key, None)
+        times = _time_candidates(key, fn, iters, lib)
+        base = times.get(_candidates(key)[0])
+        if base is None or not times:
+            continue
+        best = min(times, key=times.get)
+        if best != _candidates(key)[0] and times[best] < base * (1.0 - min_gain):
+            table[key] = best
+            chosen[key] = best
+            _log.info("kernel %s: %s %.1f us (heuristic %.1f us)", key, best, times[best] * 1e3, base * 1e3)
+    return chosen
+
+
+def autotune_training_step(step_fn, iters: int = 5, min_gain: float = 0.03) -> Dict[tuple, tuple]:
+    """The training compile phase (the reference compiles ``TrainingPhase`` per replica,
+    ``DL/optim/DistriOptimizer.scala:600-609``, ``DL/nn/mkldnn/DnnBase.scala:321-366``): run one real
+    training iteration ``step_fn()`` with launch recording on — forward (with its BN-statistics
+    epilogues), backward-data and weight-gradient convolutions exactly as training issues them —
+    then, once that iteration has finished (its collectives included), re-time each recorded launch
+    under every candidate and pin the winners per geometry.  Re-running a launch only rewrites that
+    iteration's outputs (activations, partials) or adds into gradient buffers the next iteration
+    zeroes, so the optimizer state is untouched.  Returns ``(step result, {key: choice})``."""
+    import torch
+    from ..ops import native_ops as NO
+    rec = NO._TILE["record"] = []
+    try:
+        out = step_fn()
+    finally:
+        NO._TILE["record"] = None
+    torch.cuda.synchronize()
+    chosen = select_kernels(rec, iters, min_gain)
+    rec.clear()
+    torch.cuda.synchronize()
+    return out, chosen
 
 
 def autotune(model, example, iters: int = 5, min_gain: float = 0.03) -> Dict[tuple, tuple]:
@@ -228,38 +306,7 @@ def autotune(model, example, iters: int = 5, min_gain: float = 0.03) -> Dict[tup
         NO._TILE["record"] = None
         if was_training:
             model.training()
-    lib = NO._lib()
-    table = NO._TILE["table"]
-    chosen = {}
-    seen = {}
-    for key, fn in rec:
-        seen.setdefault(key, fn)
-    for key, fn in seen.items():
-        table.pop(key, None)
-        times = {}
-        for cand in TILE_CANDIDATES:
-            if lib.bigdl_conv_tile_ok(*cand) != 0:
-                continue
-            try:
-                fn(cand)  # warm-up (and validity: an unsupported combination raises)
-                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                t0.record()
-                for _ in range(iters):
-                    fn(cand)
-                t1.record()
-                t1.synchronize()
-                times[cand] = t0.elapsed_time(t1) / iters
-            except RuntimeError:
-                continue
-        base = times.get((0, 0, 0))
-        if base is None or not times:
-            continue
-        best = min(times, key=times.get)
-        if best != (0, 0, 0) and times[best] < base * (1.0 - min_gain):
-            table[key] = best
-            chosen[key] = best
-            _log.info("conv %s: tile %s %.1f us (heuristic %.1f us)", key, best, times[best] * 1e3, base * 1e3)
-    return chosen
+    return select_kernels(rec, iters, min_gain)
 
 
 class CompiledModule:
@@ -329,4 +376,5 @@ def compile(model, example, phase: str = "inference", graph: Optional[bool] = No
     return CompiledModule(model, example, phase, graph, tune=tune)
 
 
-__all__ = ["plan", "autotune", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer", "TILE_CANDIDATES"]
+__all__ = ["plan", "autotune", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer", "TILE_CANDIDATES",
+           "WGRAD_CANDIDATES", "select_kernels", "autotune_training_step"]

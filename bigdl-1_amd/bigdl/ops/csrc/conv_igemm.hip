@@ -700,10 +700,11 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
                                      float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
                                      int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh, int osw,
                                      int ooh, int oow, int oH, int oW, const void* bnx, const float* bn_sc,
-                                     const float* bn_sh, const float* bn_mean, const void* bn_mask,
-                                     hipStream_t s) {
+                                     const float* bn_sh, const float* bn_mean, const void* bn_mask, int tbn,
+                                     int tbk, int tbm, hipStream_t s) {
   return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
-                         osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s);
+                         osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, 0, 0, 0, 0,
+                         nullptr, 0, 1, nullptr, nullptr, nullptr, tbn, tbk, tbm);
 }
 
 // bigdl_conv_fwd_full (no bias / ReLU / scatter) with the dgrad extensions: a STRIDED residual
@@ -713,11 +714,11 @@ BIGDL_EXPORT int bigdl_conv_fwd_full2(const void* x, const void* w, const void* 
                                       int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
                                       int pw, int dh, int dw, const void* bnx, const float* bn_sc, const float* bn_sh,
                                       const float* bn_mean, const void* bn_mask, const void* bn_bits, int res_sh,
-                                      int res_sw, int res_H, int res_W, hipStream_t s) {
+                                      int res_sw, int res_H, int res_W, int tbn, int tbk, int tbm, hipStream_t s) {
   if (res_sh < 0 || res_sw < 0 || (res_sh > 0) != (res_sw > 0) || (res_sh && !res)) return (int)hipErrorInvalidValue;
   return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
                          0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
-                         bn_bits);
+                         bn_bits, 0, 1, nullptr, nullptr, nullptr, tbn, tbk, tbm);
 }
 
 // bigdl_conv_fwd_full2 with a BatchNorm-backward prologue on the A operand (pointwise convs: the
@@ -835,23 +836,25 @@ BIGDL_EXPORT int bigdl_conv_fwd_ldy(const void* x, const void* w, const float* b
 BIGDL_EXPORT int bigdl_conv_fwd_scatter(const void* x, const void* w, const float* bias, const void* res, void* y,
                                         float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P,
                                         int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int osh,
-                                        int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
+                                        int osw, int ooh, int oow, int oH, int oW, int tbn, int tbk, int tbm,
+                                        hipStream_t s) {
   return bigdl_conv_fwd_full(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
-                             osw, ooh, oow, oH, oW, nullptr, nullptr, nullptr, nullptr, nullptr, s);
+                             osw, ooh, oow, oH, oW, nullptr, nullptr, nullptr, nullptr, nullptr, tbn, tbk, tbm, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd_ex(const void* x, const void* w, const float* bias, const void* res, void* y,
                                    float* stats, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
-                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, hipStream_t s) {
+                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, int tbn, int tbk, int tbm,
+                                   hipStream_t s) {
   return bigdl_conv_fwd_scatter(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, 1,
-                                1, 0, 0, P, Q, s);
+                                1, 0, 0, P, Q, tbn, tbk, tbm, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_fwd(const void* x, const void* w, const float* bias, void* y, int Nb, int H, int W, int C,
                                 int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
                                 int relu, hipStream_t s) {
   return bigdl_conv_fwd_ex(x, w, bias, nullptr, y, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu,
-                           s);
+                           0, 0, 0, s);
 }
 
 // Forward conv + shifted BN statistics partials (``shift``: per-output-channel K, see ConvParams).

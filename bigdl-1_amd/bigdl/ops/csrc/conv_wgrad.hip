@@ -341,7 +341,7 @@ BIGDL_EXPORT int bigdl_conv3d_wgrad(const void* x, const void* dy, float* dw, fl
 static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C, int K,
                         int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd, int splits,
                         hipStream_t s, int ldx, int ldk, int groups, const void* dy2 = nullptr,
-                        const float* dcoef = nullptr) {
+                        const float* dcoef = nullptr, int bp_pin = 0) {
   const bool c4 = C == 4;
   if ((C % 8 && !c4) || K % 8 || Nb <= 0) return (int)hipErrorInvalidValue;
   if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
@@ -392,9 +392,10 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
   // Pixel depth of a k-tile: 32 (half the LDS / prefetch registers, 3 blocks per CU) wins on the
   // small weight grids (≤ 16 tiles, K ≥ 128: few tiles, long split reductions), 64 elsewhere
   // (profiles/r1_conv_bk_ab.txt).  BIGDL_WGRAD_BP=32|64 pins it for A/B measurements.
-  const char* ev = getenv("BIGDL_WGRAD_BP");
-  const int bp_env = ev ? atoi(ev) : 0;
-  const int bp = (bp_env == 32 || bp_env == 64) ? bp_env : (tiles <= 16 && K >= 128 ? 32 : 64);
+  // A launch may pin it (the compile phase's kernel selection, bigdl_conv_wgrad_t).
+  static const int bp_env = [] { const char* ev = getenv("BIGDL_WGRAD_BP"); return ev ? atoi(ev) : 0; }();
+  const int bp = (bp_pin == 32 || bp_pin == 64) ? bp_pin
+                 : (bp_env == 32 || bp_env == 64) ? bp_env : (tiles <= 16 && K >= 128 ? 32 : 64);
   if (dy2) {  // BN-backward prologue: the 32-deep k-tile variants (register budget for the second dY)
     if (TN == 64) {
       if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32, false, false, true>), grid, dim3(256), 0, s, p);
@@ -431,6 +432,15 @@ BIGDL_EXPORT int bigdl_conv_wgrad(const void* x, const void* dy, float* dw, floa
                                   int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
                                   int splits, hipStream_t s) {
   return wgrad_launch(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, C, K, 1);
+}
+
+// bigdl_conv_wgrad with the k-tile pixel depth pinned (bp ∈ {32, 64}; 0 = heuristic).
+BIGDL_EXPORT int bigdl_conv_wgrad_t(const void* x, const void* dy, float* dw, float scale, int Nb, int H, int W, int C,
+                                    int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd,
+                                    int splits, int bp, hipStream_t s) {
+  if (bp != 0 && bp != 32 && bp != 64) return (int)hipErrorInvalidValue;
+  return wgrad_launch(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, C, K, 1, nullptr,
+                      nullptr, bp);
 }
 
 // bigdl_conv_wgrad with a BatchNorm-backward prologue on dY: dy = g' at the BN output, dy2 = the BN input,

@@ -837,6 +837,9 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
                                        and _al16(residual)):
         return None
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
+    # the dgrad IS a forward conv of gy (N, P, Q, K → C): it shares the forward geometry key space of
+    # the kernel-selection table
+    dkey = (N_, P, Q, K, C_, R, S, (1, 1), (ph, pw), tuple(dilation))
     if bn_fuse is not None and C_ % 8 == 0:
         # BN-backward prologue in the epilogue: either the ReLU mask recomputed from the BN input
         # (conv → BN+ReLU → this conv), or an explicit mask tensor with the residual gradient summed
@@ -863,15 +866,15 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
                                                   dilation[1], ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
                                                   ptr(bits), *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_bnbwd3")
             elif rs is not None or bits is not None:
-                check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q,
-                                                  K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1],
-                                                  ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), ptr(bits),
-                                                  *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_bnbwd2")
+                _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_full2(
+                    ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(part), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw,
+                    dilation[0], dilation[1], ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask), ptr(bits),
+                    *(rs or (0, 0, 0, 0)), t[0], t[1], t[2], _s()), "conv_dgrad_bnbwd2"))
             else:
-                check(_lib().bigdl_conv_fwd_full(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_,
-                                                 P, Q, K, C_, R, S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0,
-                                                 1, 1, 0, 0, H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
-                                                 _s()), "conv_dgrad_bnbwd")
+                _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_full(
+                    ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(part), N_, P, Q, K, C_, R, S, H, W, 1,
+                    1, ph, pw, dilation[0], dilation[1], 0, 1, 1, 0, 0, H, W, ptr(bx), ptr(sc), ptr(sh), ptr(mu),
+                    ptr(mask), t[0], t[1], t[2], _s()), "conv_dgrad_bnbwd"))
             bn_fuse["partial"], bn_fuse["G"] = part, G
             return gx
     if ax is not None:
@@ -881,12 +884,14 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
                                           *(rs or (0, 0, 0, 0)), _s()), "conv_dgrad_at")
         return gx
     if rs is not None:
-        check(_lib().bigdl_conv_fwd_full2(ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
-                                          S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(None), ptr(None),
-                                          ptr(None), ptr(None), ptr(None), ptr(None), *rs, _s()), "conv_dgrad_rs")
+        _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_full2(
+            ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw,
+            dilation[0], dilation[1], ptr(None), ptr(None), ptr(None), ptr(None), ptr(None), ptr(None), *rs,
+            t[0], t[1], t[2], _s()), "conv_dgrad_rs"))
         return gx
-    check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R,
-                                   S, H, W, 1, 1, ph, pw, dilation[0], dilation[1], 0, _s()), "conv_dgrad")
+    _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_ex(
+        ptr(gy), ptr(wt), ptr(None), ptr(residual), ptr(gx), ptr(None), N_, P, Q, K, C_, R, S, H, W, 1, 1, ph, pw,
+        dilation[0], dilation[1], 0, t[0], t[1], t[2], _s()), "conv_dgrad"))
     return gx
 
 
@@ -1081,8 +1086,9 @@ def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None, lazy=F
         (a, b, rs, ss, ho, wo, ea, eb) = classes[0]
         wt = _subfilters(w4, classes, ckey)[0]
         tmp = torch.empty((N_, C_, ho, wo), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
-        check(_lib().bigdl_conv_fwd_ex(ptr(gy), ptr(wt), ptr(None), ptr(None), ptr(tmp), ptr(None), N_, P, Q, K, C_,
-                                       1, 1, ho, wo, 1, 1, 0, 0, 1, 1, 0, _s()), "conv_dgrad_1x1s_lazy")
+        _tiled_launch((N_, P, Q, K, C_, 1, 1, (1, 1), (0, 0), (1, 1)), lambda t: check(_lib().bigdl_conv_fwd_ex(
+            ptr(gy), ptr(wt), ptr(None), ptr(None), ptr(tmp), ptr(None), N_, P, Q, K, C_, 1, 1, ho, wo, 1, 1, 0, 0, 1,
+            1, 0, t[0], t[1], t[2], _s()), "conv_dgrad_1x1s_lazy"))
         return R_.StridedGrad(tmp, stride, (N_, C_, H, W))
     gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=gy.device, memory_format=torch.channels_last)
     if any(not rs or not ss for (_, _, rs, ss, *_r) in classes):
@@ -1100,7 +1106,8 @@ def _dgrad_strided(gy, w4, x_shape, stride, pad, dilation, residual=None, lazy=F
         res_ok = residual is not None  # tap-less parities already hold the residual (copied above)
         check(_lib().bigdl_conv_fwd_scatter(ptr(gy), ptr(wt), ptr(None), ptr(residual if res_ok else None), ptr(gx),
                                             ptr(None), N_, P, Q, K, C_, Ra, Sb, ho, wo, 1, 1, Ra - 1 - ea,
-                                            Sb - 1 - eb, 1, 1, 0, sh, sw, a, b, H, W, _s()), "conv_dgrad_strided")
+                                            Sb - 1 - eb, 1, 1, 0, sh, sw, a, b, H, W, 0, 0, 0, _s()),
+              "conv_dgrad_strided")
     return gx
 
 
@@ -1208,9 +1215,12 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
                                             stride[1], pad[0], pad[1], dilation[0], dilation[1],
                                             -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad_bnbwd")
     else:
-        check(_lib().bigdl_conv_wgrad(ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K,
-                                      R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
-                                      -_wgrad_blocks(N_ * P * Q, cc, K), _s()), "conv_wgrad")
+        # kernel selection key: ("wg", geometry) → (target blocks, k-tile pixel depth); 0 = heuristic
+        wkey = ("wg", N_, H, W, cc, K, R, S, tuple(stride), tuple(pad), tuple(dilation))
+        _tiled_launch(wkey, lambda t: check(_lib().bigdl_conv_wgrad_t(
+            ptr(xx), ptr(gy), ptr(target), _f(scale if direct else 1.0), N_, H, W, cc, K, R, S, P, Q, stride[0],
+            stride[1], pad[0], pad[1], dilation[0], dilation[1], -(t[0] or _wgrad_blocks(N_ * P * Q, cc, K)), t[1],
+            _s()), "conv_wgrad"))
     if not direct:
         gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
     return xx

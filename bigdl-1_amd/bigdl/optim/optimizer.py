@@ -509,6 +509,24 @@ class BaseOptimizer:
         return self.train_step(batch)
 
     def train_step(self, batch: MiniBatch) -> torch.Tensor:
+        """One synchronous-SGD iteration.  The FIRST iteration on a GPU is also the training compile
+        phase (``bigdl.compile.trainAutotune``; the reference compiles ``TrainingPhase`` per replica,
+        ``DL/optim/DistriOptimizer.scala:600-609``): its forward / backward-data / weight-gradient
+        launches are recorded, and once it has finished each distinct geometry is re-timed under
+        every kernel candidate and the fastest pinned (``nn.compiled.autotune_training_step``)."""
+        if (not getattr(self, "_kernels_selected", False) and self.device.type == "cuda"
+                and not torch.cuda.is_current_stream_capturing()):
+            self._kernels_selected = True
+            if config.get_property("bigdl.compile.trainAutotune"):
+                from ..nn.compiled import autotune_training_step
+                loss, chosen = autotune_training_step(lambda: self._train_step_run(batch))
+                self.selected_kernels = chosen
+                if Engine.rank() == 0:
+                    log.info(f"training compile phase: {len(chosen)} launch geometries re-tiled")
+                return loss
+        return self._train_step_run(batch)
+
+    def _train_step_run(self, batch: MiniBatch) -> torch.Tensor:
         """One synchronous-SGD iteration on ``batch`` (see :meth:`_train_step_impl`).  On a GPU with
         ``bigdl.step.highPriority`` the iteration runs on a high-priority HIP stream, so the
         backward-data / BatchNorm chain wins the CUs over the side-stream weight-gradient kernels
