@@ -23,6 +23,10 @@ The model, criterion and optimizer are built exactly as the reference's ImageNet
 training (``DL/models/resnet/{ResNet,TrainImageNet,Utils}.scala``): convs with bias and
 L2Regularizer(1e-4), BN eps 1e-3, SGD(lr 0.1, momentum 0.9, dampening 0, nesterov, wd 1e-4).
 
+The same invocation then times the identical config at the reference's precision — fp32 compute
+(bf16x3 operand splits on the matrix cores, fp32 accumulation; ``--fp32-steps``, default 5 on GPU)
+— and reports it as ``"fp32": {"value", "ms_per_step", ...}`` next to the bf16 headline ``value``.
+
 ``--device cpu`` (gloo, fp32) with ``--batch`` / ``--image-size`` exists to exercise the
 multi-rank launch path on a host without GPUs (tests/test_bench_launch.py).
 """
@@ -60,6 +64,11 @@ def _parse(argv=None):
                     help="cross-rank SyncBN in every BN (setParallism), the reference's TrainImageNet option")
     ap.add_argument("--force-distri", action="store_true",
                     help="use the DistriOptimizer (RCCL path) even at world size 1 (path validation)")
+    ap.add_argument("--fp32-steps", type=int, default=None,
+                    help="also time this many steps of the same config in fp32 compute (the reference's "
+                         "precision; bf16x3 on the matrix cores) after the bf16 headline, reported as "
+                         "\"fp32\" in the JSON line (default 5 on GPU, 0 on CPU; 0 = off)")
+    ap.add_argument("--fp32-warmup", type=int, default=2)
     return ap.parse_args(argv)
 
 
@@ -121,6 +130,44 @@ def _build(args, dev, rank):
     return model, crit, sgd, batches
 
 
+def _timed(args, dev, rank, distri, warmup, steps):
+    """Build the model / optimizer at the current compute dtype, run ``warmup`` untimed steps (the
+    first is the training compile phase), then time exactly ``steps`` steps bracketed by barrier +
+    device synchronize; returns (optimizer, batches, max elapsed over ranks, final loss, sync)."""
+    import torch
+    from bigdl.optim.optimizer import LocalOptimizer
+    from bigdl.parallel import comm
+    model, crit, sgd, batches = _build(args, dev, rank)
+    B = args.batch
+    if distri:
+        from bigdl.parallel import DistriOptimizer
+        opt = DistriOptimizer(model, [batches[0]], crit, sgd, batch_size=B)
+    else:
+        opt = LocalOptimizer(model, [batches[0]], crit, sgd, batch_size=B)
+    opt.prepare()
+
+    def sync():
+        if hasattr(opt, "_wait_all_gathers"):
+            opt._wait_all_gathers()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    for i in range(warmup):
+        opt.train_step(batches[i % 2])
+    sync()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(steps):
+        loss = opt.train_step(batches[i % 2])
+    sync()
+    comm.barrier()
+    elapsed = comm.allreduce_max(time.perf_counter() - t0)
+    return opt, batches, elapsed, (float(loss) if loss is not None else float("nan")), sync
+
+
 def main(argv=None):
     args = _parse(argv)
     env_world = os.environ.get("WORLD_SIZE")
@@ -148,39 +195,9 @@ def main(argv=None):
     dev = Engine.device()
     rank = Engine.rank()
 
-    from bigdl.optim.optimizer import LocalOptimizer
-    model, crit, sgd, batches = _build(args, dev, rank)
-    B = args.batch
-    if distri:
-        from bigdl.parallel import DistriOptimizer
-        opt = DistriOptimizer(model, [batches[0]], crit, sgd, batch_size=B)
-    else:
-        opt = LocalOptimizer(model, [batches[0]], crit, sgd, batch_size=B)
-    opt.prepare()
-
     from bigdl.parallel import comm
-
-    def sync():
-        if hasattr(opt, "_wait_all_gathers"):
-            opt._wait_all_gathers()
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-
-    for i in range(args.warmup):
-        opt.train_step(batches[i % 2])
-    sync()
-    comm.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    loss = None
-    for i in range(args.steps):
-        loss = opt.train_step(batches[i % 2])
-    sync()
-    comm.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = comm.allreduce_max(elapsed)
-    final_loss = float(loss) if loss is not None else float("nan")
+    B = args.batch
+    opt, batches, elapsed, final_loss, sync = _timed(args, dev, rank, distri, args.warmup, args.steps)
 
     # per-phase means over a few extra (untimed) steps: HIP-event timers on the step stream
     phases = {}
@@ -205,6 +222,21 @@ def main(argv=None):
 
     ms = elapsed / args.steps * 1e3
     imgs = B * world * args.steps / elapsed
+
+    # the same config at the reference's precision (fp32 compute: bf16x3 splits on the matrix cores,
+    # tests/test_fp32x3.py), timed the same way after the bf16 headline
+    fp32 = None
+    n32 = args.fp32_steps if args.fp32_steps is not None else (5 if dev.type == "cuda" else 0)
+    driver = type(opt).__name__
+    if n32 > 0 and dtype != "fp32":
+        del opt, batches
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        config.set_property("bigdl.compute.dtype", "fp32")
+        o32, b32, el32, loss32, _ = _timed(args, dev, rank, distri, args.fp32_warmup, n32)
+        fp32 = {"value": round(B * world * n32 / el32, 2), "ms_per_step": round(el32 / n32 * 1e3, 3), "steps": n32,
+                "warmup": args.fp32_warmup, "dtype": "fp32", "final_loss": loss32}
+        del o32, b32
     if rank == 0:
         from bigdl.ops import native_status
         ns = native_status()
@@ -216,9 +248,10 @@ def main(argv=None):
                        "image_size": args.image_size, "classes": 1000, "parallelism": f"dp{world}",
                        "optimizer": "SGD(lr=0.1,m=0.9,nesterov,wd=1e-4)+L2Reg(1e-4)",
                        "comm_dtype": args.comm_dtype, "device": dev.type, "syncbn": bool(args.syncbn),
-                       "driver": type(opt).__name__},
+                       "driver": driver},
             "phase_ms_max_over_ranks": phases,
             "final_loss": final_loss, "native_kernels": ns.get("loaded", False),
+            "fp32": fp32,
         }), flush=True)
     Engine.shutdown()
 
