@@ -57,7 +57,10 @@ def _parse(argv=None):
     ap.add_argument("--model", default="resnet50", choices=["resnet50"])
     ap.add_argument("--dtype", default=None, help="compute dtype (default bf16 on GPU, fp32 on CPU)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
-    ap.add_argument("--comm-dtype", default=os.environ.get("BIGDL_COMM_DTYPE", "fp32"))
+    ap.add_argument("--comm-dtype", default=os.environ.get("BIGDL_COMM_DTYPE"),
+                    help="gradient wire format (fp32 | bf16 | bf16_truncate); default bf16_truncate for "
+                         "N > 1 — the reference's FP16CompressedTensor bit format "
+                         "(DL/parameters/FP16CompressedTensor.scala:271-277) — and fp32 at N = 1")
     ap.add_argument("--phase-steps", type=int, default=3,
                     help="extra untimed steps with per-phase timers (0 = off)")
     ap.add_argument("--syncbn", action="store_true",
@@ -179,6 +182,8 @@ def main(argv=None):
 
     import torch
     from bigdl.utils import config
+    if args.comm_dtype is None:
+        args.comm_dtype = "bf16_truncate" if (world > 1 or args.force_distri) else "fp32"
     dtype = args.dtype or ("bf16" if args.device == "cuda" else "fp32")
     config.set_property("bigdl.compute.dtype", dtype)
     config.set_property("bigdl.comm.dtype", args.comm_dtype)

@@ -297,7 +297,11 @@ class DistriOptimizer(BaseOptimizer):
                         if not (N.has("trunc_bf16") and N.native_ops.trunc_bf16(g, wire) is not NotImplemented):
                             wire.copy_(comm.bf16_truncate(g))
                     else:
-                        wire.copy_(g)
+                        # RNE pack by the bigdl cast kernel (one vectorised pass; torch copy_ if the
+                        # bucket slice is not 16-B aligned or off the GPU)
+                        from ..ops import native_ops as NOps
+                        if NOps.cast_copy(wire, g) is NotImplemented:
+                            wire.copy_(g)
                     b.rs_work = dist.reduce_scatter_tensor(self.shard_g_wire[b.slo:b.shi], wire, async_op=True)
                 else:
                     b.rs_work = dist.reduce_scatter_tensor(self.shard_g[b.slo:b.shi], g, async_op=True)
