@@ -107,6 +107,51 @@ def combine_heads(x):
     return x.transpose(1, 2).reshape(B, L, n * d)
 
 
+class DecodeCache:
+    """Preallocated KV cache of cached incremental decoding: ``k`` / ``v`` [rows, Lmax, H] with the
+    first ``length`` positions valid, appended to IN PLACE each step (the reference concatenates
+    ``[new; cache]`` into a fresh tensor every step, ``DL/nn/Attention.scala:136-141``) and read by
+    the decode-attention kernel (``ops/csrc/attn_decode.hip``).  One object serves both the
+    ``<name>_k`` and ``<name>_v`` entries of the cache Table.  :meth:`reorder` applies a beam
+    search's surviving-beam selection to the valid rows."""
+
+    def __init__(self, rows: int, max_len: int, hidden: int, device=None):
+        self.rows, self.max_len, self.hidden, self.device = rows, max(1, int(max_len)), hidden, device
+        self.k = self.v = None
+        self.length = 0
+
+    def append(self, k, v):
+        n = k.shape[1]
+        if self.k is None or self.k.dtype != k.dtype:
+            self.k = torch.empty((self.rows, self.max_len, self.hidden), dtype=k.dtype, device=k.device)
+            self.v = torch.empty_like(self.k)
+            self.length = 0
+        if self.length + n > self.k.shape[1]:  # grow (amortised doubling) keeping the history
+            cap = max(self.length + n, 2 * self.k.shape[1])
+            nk = torch.empty((self.rows, cap, self.hidden), dtype=self.k.dtype, device=self.k.device)
+            nv = torch.empty_like(nk)
+            nk[:, :self.length].copy_(self.k[:, :self.length])
+            nv[:, :self.length].copy_(self.v[:, :self.length])
+            self.k, self.v = nk, nv
+        self.k[:, self.length:self.length + n].copy_(k)
+        self.v[:, self.length:self.length + n].copy_(v)
+        self.length += n
+
+    def reorder(self, rows_idx):
+        """Row i ← row rows_idx[i] over the valid positions (beam survivors)."""
+        L = self.length
+        if L and self.k is not None:
+            self.k[:, :L] = self.k[rows_idx, :L]
+            self.v[:, :L] = self.v[rows_idx, :L]
+
+    def keys(self):
+        """The cached keys in the reference's order (newest first), [rows, L, H]."""
+        return self.k[:, :self.length].flip(1)
+
+    def values(self):
+        return self.v[:, :self.length].flip(1)
+
+
 class Attention(AutogradModule):
     """Multi-head attention.  Input ``T(x, y, bias)``: queries from ``x`` (B, Lq, H), keys and
     values from ``y`` (B, Lk, H), additive ``bias`` broadcastable to (B, heads, Lq, Lk).  For
@@ -127,6 +172,9 @@ class Attention(AutogradModule):
 
     def _attend(self, q, k, v, bias):
         depth = self.hiddenSize // self.numHeads
+        if q.is_cuda:  # a device tensor reached the torch path: count it like any other fallback
+            from ...ops import native as N
+            N.note_fallback("attention_forward", "torch-attention", (q, k))
         q = split_heads(q, self.numHeads) * depth ** -0.5
         k = split_heads(k, self.numHeads)
         v = split_heads(v, self.numHeads)
@@ -150,7 +198,7 @@ class Attention(AutogradModule):
     # ---- native (device) path -----------------------------------------------------------------
     def _nat_ok(self, x, y, b):
         D = self.hiddenSize // self.numHeads
-        return (D in (64, 128) and _native_dense_ok(x) and x.dim() == 3 and isinstance(y, torch.Tensor)
+        return (D in (32, 64, 96, 128) and _native_dense_ok(x) and x.dim() == 3 and isinstance(y, torch.Tensor)
                 and y.is_cuda and y.dim() == 3 and (b is None or isinstance(b, torch.Tensor)))
 
     def updateOutput(self, input):
@@ -259,6 +307,10 @@ class Attention(AutogradModule):
     def _forward_cached(self, x, y, bias, cache):
         if self.train:
             raise RuntimeError("Only support input cache for model inference")
+        kn, vn = f"{self.get_name()}_k", f"{self.get_name()}_v"
+        dc = cache.get(kn) if isinstance(cache, Table) else None
+        if isinstance(dc, DecodeCache):
+            return self._forward_decode(x, y, bias, cache, dc, kn, vn)
         q = self._proj(x, "query")
         k = self._proj(y, "key")
         v = self._proj(y, "value")
@@ -271,6 +323,38 @@ class Attention(AutogradModule):
             cache[kn] = k
             cache[vn] = v
         return self._attend(q, k, v, bias)
+
+
+    def _forward_decode(self, x, y, bias, cache, dc, kn, vn):
+        """One decoding step on a :class:`DecodeCache`: project the new token(s), append K/V in
+        place, attend over the whole cache with the decode kernel (``ops.attention_decode``)."""
+        from ... import ops
+        H, nh = self.hiddenSize, self.numHeads
+        D = H // nh
+        rows, Lq, Ly = x.shape[0], x.shape[1], y.shape[1]
+        if x.is_cuda:
+            from ...ops import native_ops as NO
+            bf = torch.bfloat16
+            x2 = x.reshape(rows * Lq, H).to(bf).contiguous()
+            y2 = x2 if (y is x) else y.reshape(rows * Ly, H).to(bf).contiguous()
+            q = NO.gemm(x2, self.cw("queryWeight", bf)).view(rows, Lq, H)
+            wkv = _fused_rows([self.cw("keyWeight", bf), self.cw("valueWeight", bf)])
+            if wkv is not None:
+                kv = NO.gemm(y2, wkv).view(rows, Ly, 2 * H)
+                k, v = kv[..., :H], kv[..., H:]
+            else:
+                k = NO.gemm(y2, self.cw("keyWeight", bf)).view(rows, Ly, H)
+                v = NO.gemm(y2, self.cw("valueWeight", bf)).view(rows, Ly, H)
+        else:
+            q, k, v = self._proj(x, "query"), self._proj(y, "key"), self._proj(y, "value")
+        dc.append(k, v)
+        cache[kn] = dc
+        cache[vn] = dc
+        o = ops.attention_decode(q.contiguous(), dc.k, dc.v, dc.length, nh, D, D ** -0.5, bias, True)
+        if x.is_cuda:
+            from ...ops import native_ops as NO
+            return NO.gemm(o.reshape(rows * Lq, H), self.cw("outputWeight", torch.bfloat16)).view(rows, Lq, H)
+        return self._proj(o, "output")
 
 
 class FeedForwardNetwork(AutogradModule):
@@ -644,6 +728,8 @@ class SequenceBeamSearch(AbstractModule):
         self.maxDecodeLength, self.eosID, self.paddingValue = max_decode_length, eos_id, padding_value
         self.numHiddenLayers, self.hiddenSize = num_hidden_layers, hidden_size
         self._fn = None
+        #: decode with preallocated in-place KV caches (:class:`DecodeCache`); False = tensor caches
+        self.inPlaceCache = True
 
     INF = -1e7
 
@@ -680,8 +766,14 @@ class SequenceBeamSearch(AbstractModule):
         bias_b = bias.unsqueeze(1).expand(B, K, *bias.shape[1:]).contiguous()
         cache = Table()
         for j in range(1, self.numHiddenLayers + 1):
-            cache[f"layer_{j}_k"] = torch.empty(0, device=dev)
-            cache[f"layer_{j}_v"] = torch.empty(0, device=dev)
+            if self.inPlaceCache:
+                # one preallocated in-place KV cache per decoder layer (both Table entries)
+                dc = DecodeCache(B * K, self.maxDecodeLength + 1, self.hiddenSize, dev)
+                cache[f"layer_{j}_k"] = dc
+                cache[f"layer_{j}_v"] = dc
+            else:  # the reference's tensor cache ([new; cache] concatenation every step)
+                cache[f"layer_{j}_k"] = torch.empty(0, device=dev)
+                cache[f"layer_{j}_v"] = torch.empty(0, device=dev)
         fin_seq = torch.zeros_like(alive_seq)
         fin_scores = torch.full((B, K), self.INF, device=dev)
         fin_flags = torch.zeros(B, K, dtype=torch.bool, device=dev)
@@ -705,6 +797,13 @@ class SequenceBeamSearch(AbstractModule):
             # new alive state
             nlp = top_lp + finished_now.float() * self.INF
             _, keep = nlp.topk(K, -1)
+            # surviving beams of the in-place caches: row (b, k) ← alive row (b, beam_idx[b, keep[b, k]])
+            dcs = {id(v): v for v in ncache.values() if isinstance(v, DecodeCache)}
+            if dcs:
+                sel = beam_idx.gather(1, keep)
+                rows = (torch.arange(B, device=dev).unsqueeze(1) * K + sel).reshape(-1)
+                for dc in dcs.values():
+                    dc.reorder(rows)
             alive_seq = self._gather(top_seq, keep)
             alive_lp = self._gather(nlp, keep)
             enc_b = self._gather(enc2, keep)

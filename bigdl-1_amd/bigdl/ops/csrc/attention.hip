@@ -458,7 +458,7 @@ static int attn_setup(AttnParams& p, const void* q, long long ldq, const void* k
                       long long ldv, const float* bias, long long sbb, long long sbh, long long sbq, long long sbk,
                       int B, int Hh, int Lq, int Lk, int D, float scale, int causal, float keep, unsigned seed,
                       const void* seed_dev) {
-  if (B <= 0 || Hh <= 0 || Lq <= 0 || Lk <= 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  if (B <= 0 || Hh <= 0 || Lq <= 0 || Lk <= 0 || D <= 0 || D > 128 || D % 32) return (int)hipErrorInvalidValue;
   if (!a16(q) || !a16(k) || !a16(v) || ldq % 8 || ldk % 8 || ldv % 8) return (int)hipErrorInvalidValue;
   if (ldq < (long long)Hh * D || ldk < (long long)Hh * D || ldv < (long long)Hh * D) return (int)hipErrorInvalidValue;
   if (causal && Lq != Lk) return (int)hipErrorInvalidValue;
@@ -482,7 +482,7 @@ static int attn_setup(AttnParams& p, const void* q, long long ldq, const void* k
 }
 
 // O (and LSE₂, fp32 [B][Hh][Lq]) of softmax(scale·Q·Kᵀ + bias [+ causal]) ∘ dropout · V.
-// q/k/v/out: [B·L][ld] bf16 rows, head h at columns h·D (16-B aligned, ld % 8 == 0), D ∈ {64, 128}.
+// q/k/v/out: [B·L][ld] bf16 rows, head h at columns h·D (16-B aligned, ld % 8 == 0), D ∈ {32, 64, 96, 128}.
 BIGDL_EXPORT int bigdl_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v,
                                 long long ldv, void* out, long long ldo, float* lse, const float* bias, long long sbb,
                                 long long sbh, long long sbq, long long sbk, int B, int Hh, int Lq, int Lk, int D,
@@ -495,8 +495,14 @@ BIGDL_EXPORT int bigdl_attn_fwd(const void* q, long long ldq, const void* k, lon
   if (!a16(out) || ldo % 8 || ldo < (long long)Hh * D || !lse) return (int)hipErrorInvalidValue;
   p.out = (bf16_t*)out; p.ldo = ldo; p.lse = lse;
   const dim3 grid((unsigned)((Lq + 63) / 64), (unsigned)Hh, (unsigned)B);
-  if (D == 64) hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(k_attn_fwd<128>, grid, dim3(256), 0, s, p);
+  // head dims 32 / 64 / 96 / 128: every loop of the kernels runs over D / 32 k-slices and D / 16
+  // output slices, and the [64][D + 8] LDS rows keep the 8-B alignment the transposed reads need
+  switch (D) {
+    case 32: hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, s, p); break;
+    case 64: hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, s, p); break;
+    case 96: hipLaunchKernelGGL(k_attn_fwd<96>, grid, dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL(k_attn_fwd<128>, grid, dim3(256), 0, s, p); break;
+  }
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -520,12 +526,23 @@ BIGDL_EXPORT int bigdl_attn_bwd(const void* q, long long ldq, const void* k, lon
   p.out = (bf16_t*)dq; p.ldg = ldg; p.dk = (bf16_t*)dk; p.ldgk = ldgk; p.dv = (bf16_t*)dv; p.ldgv = ldgv;
   const dim3 gq((unsigned)((Lq + 63) / 64), (unsigned)Hh, (unsigned)B);
   const dim3 gk((unsigned)((Lk + 63) / 64), (unsigned)Hh, (unsigned)B);
-  if (D == 64) {
-    hipLaunchKernelGGL(k_attn_bwd_dq<64>, gq, dim3(256), 0, s, p);  // also writes delta
-    hipLaunchKernelGGL(k_attn_bwd_dkdv<64>, gk, dim3(256), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(k_attn_bwd_dq<128>, gq, dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_attn_bwd_dkdv<128>, gk, dim3(256), 0, s, p);
+  switch (D) {  // k_attn_bwd_dq also writes delta
+    case 32:
+      hipLaunchKernelGGL(k_attn_bwd_dq<32>, gq, dim3(256), 0, s, p);
+      hipLaunchKernelGGL(k_attn_bwd_dkdv<32>, gk, dim3(256), 0, s, p);
+      break;
+    case 64:
+      hipLaunchKernelGGL(k_attn_bwd_dq<64>, gq, dim3(256), 0, s, p);
+      hipLaunchKernelGGL(k_attn_bwd_dkdv<64>, gk, dim3(256), 0, s, p);
+      break;
+    case 96:
+      hipLaunchKernelGGL(k_attn_bwd_dq<96>, gq, dim3(256), 0, s, p);
+      hipLaunchKernelGGL(k_attn_bwd_dkdv<96>, gk, dim3(256), 0, s, p);
+      break;
+    default:
+      hipLaunchKernelGGL(k_attn_bwd_dq<128>, gq, dim3(256), 0, s, p);
+      hipLaunchKernelGGL(k_attn_bwd_dkdv<128>, gk, dim3(256), 0, s, p);
+      break;
   }
   BIGDL_CHECK_LAUNCH();
 }

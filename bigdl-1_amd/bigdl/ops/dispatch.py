@@ -17,6 +17,7 @@ __all__ = [
     "sgd_step", "adam_step", "lstm_cell_forward", "lstm_cell_backward",
     "embedding_forward", "embedding_backward", "dropout_forward", "dropout_backward", "lrn_forward", "lrn_backward",
     "quant_rows", "gemm_i8", "image_crop_flip_norm", "attention_forward", "attention_backward",
+    "attention_decode",
 ]
 
 

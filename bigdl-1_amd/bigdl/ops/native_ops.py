@@ -2801,7 +2801,7 @@ def _seed_args(seed):
 def attention_forward(q, k, v, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0):
     """Fused multi-head attention (attention.hip) on projection rows; see the reference op."""
     HD = Hh * D
-    if D not in (64, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
+    if D not in (32, 64, 96, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
                                   and _attn_rows_ok(v, B * Lk, HD)):
         return NotImplemented
     if (causal and Lq != Lk) or not (0.0 < keep <= 1.0):
@@ -2819,13 +2819,41 @@ def attention_forward(q, k, v, B, Hh, Lq, Lk, D, scale, bias=None, causal=False,
     return out, lse
 
 
+@register("attention_decode")
+def attention_decode(q, kc, vc, L, Hh, D, scale, bias=None, bias_rev=True):
+    """Cached incremental-decoding attention (attn_decode.hip): ``q`` [rows, Lq, H] attends over the
+    first ``L`` positions of the preallocated caches ``kc`` / ``vc`` [rows, Lmax, H]; ``bias``
+    broadcastable to (rows, Hh, Lq, L), indexed newest-key-first when ``bias_rev`` (the reference's
+    [new; cache] concatenation order).  Returns o [rows, Lq, H] bf16."""
+    if not (q.dim() == 3 and kc.dim() == 3 and vc.dim() == 3 and q.dtype == _bf16 and kc.dtype == _bf16
+            and vc.dtype == _bf16 and q.is_cuda):
+        return NotImplemented
+    rows, Lq, H = q.shape
+    if H != Hh * D or D % 8 or D > 256 or kc.shape[0] != rows or vc.shape[0] != rows or kc.shape[1] < L \
+            or vc.shape[1] < L or L <= 0:
+        return NotImplemented
+    if q.stride(2) != 1 or kc.stride(2) != 1 or vc.stride(2) != 1 or q.stride(0) != Lq * q.stride(1):
+        return NotImplemented
+    if not (_al16(q) and _al16(kc) and q.stride(1) % 8 == 0 and kc.stride(1) % 8 == 0 and kc.stride(0) % 8 == 0):
+        return NotImplemented
+    bt, bs = _attn_bias(bias, rows, Hh, Lq, L, q.device)
+    if bt is NotImplemented:
+        return NotImplemented
+    out = torch.empty((rows, Lq, H), dtype=_bf16, device=q.device)
+    check(_lib().bigdl_attn_decode(ptr(q), _ll(q.stride(1)), ptr(kc), _ll(kc.stride(1)), _ll(kc.stride(0)), ptr(vc),
+                                   _ll(vc.stride(1)), _ll(vc.stride(0)), ptr(out), _ll(H), ptr(bt),
+                                   *[_ll(x) for x in bs], C.c_int(1 if bias_rev else 0), C.c_int(rows), C.c_int(Hh),
+                                   C.c_int(Lq), C.c_int(L), C.c_int(D), _f(scale), _s()), "attn_decode")
+    return out
+
+
 @register("attention_backward")
 def attention_backward(dout, q, k, v, o, lse, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0,
                        dq=None, dk=None, dv=None):
     """dQ, dK, dV of :func:`attention_forward` (two kernels, no atomics); ``dq``/``dk``/``dv`` may be
     column slices of one fused [B·L][3·H] buffer (the QKV projection's backward reads it whole)."""
     HD = Hh * D
-    if D not in (64, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
+    if D not in (32, 64, 96, 128) or not (_attn_rows_ok(q, B * Lq, HD) and _attn_rows_ok(k, B * Lk, HD)
                                   and _attn_rows_ok(v, B * Lk, HD) and _attn_rows_ok(o, B * Lq, HD)
                                   and _attn_rows_ok(dout, B * Lq, HD)):
         return NotImplemented

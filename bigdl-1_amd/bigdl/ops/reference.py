@@ -703,6 +703,21 @@ def _attn_probs(q, k, B, Hh, Lq, Lk, D, scale, bias, causal):
     return s
 
 
+def attention_decode(q, kc, vc, L, Hh, D, scale, bias=None, bias_rev=True):
+    """Cached decoding attention over the first ``L`` cache positions (Attention.scala:118-140):
+    softmax(scale·q·kᵀ + bias)·v per head; ``bias_rev``: bias indexed newest key first."""
+    rows, Lq, H = q.shape
+    qh = q.float().reshape(rows, Lq, Hh, D).transpose(1, 2)
+    kh = kc[:, :L].float().reshape(rows, L, Hh, D).transpose(1, 2)
+    vh = vc[:, :L].float().reshape(rows, L, Hh, D).transpose(1, 2)
+    s = (qh @ kh.transpose(-1, -2)) * scale
+    if bias is not None:
+        b = bias.float()
+        s = s + (b.flip(-1) if bias_rev else b)
+    o = torch.softmax(s, -1) @ vh
+    return o.transpose(1, 2).reshape(rows, Lq, H).to(q.dtype)
+
+
 def attention_forward(q, k, v, B, Hh, Lq, Lk, D, scale, bias=None, causal=False, keep=1.0, seed=0):
     """Multi-head attention on projection rows (``Attention.scala:30-111``): q [B·Lq][≥Hh·D],
     k / v [B·Lk][≥Hh·D] with head h at columns h·D; O = (softmax(scale·QKᵀ + bias [causal]) ∘ M /

@@ -115,3 +115,68 @@ def test_beam_search_prefers_high_prob_path():
     assert seq.shape[0] == 1 and seq.shape[1] == 2
     assert seq[0, 0, 1].item() == 2 and seq[0, 0, 2].item() == 3  # 1-based ids: 2 then eos 3
     assert math.isfinite(scores[0, 0].item())
+
+
+def test_incremental_decoding_in_place_cache_matches_full_decoder():
+    """The same step-by-step decoding on preallocated in-place KV caches (DecodeCache +
+    ops.attention_decode) == the full teacher-forced decoder."""
+    from bigdl.nn.layers.attention import DecodeCache, PaddingMask
+    torch.manual_seed(3)
+    V, H = 30, 16
+    bs = SequenceBeamSearch(V, 2, 0.6, 6, 3, 0, 2, H)
+    tr = Transformer(V, H, 4, 32, 2, 1.0, 1.0, 1.0, with_share_weights_linear=True, transformer_type="Translation",
+                     beam_search=bs)
+    tr.evaluate()
+    src = torch.randint(1, V, (2, 6)).float()
+    tgt = torch.randint(1, V, (2, 6)).float()
+    full = tr.forward(T(src, tgt))
+    mask = PaddingMask().forward(src)
+    emb = tr._emb_seq.forward(src)
+    enc = tr.encoderStack.forward(T(emb + position_signal(6, H), mask))
+    ids = torch.cat([torch.zeros(2, 1), tgt], 1).long()
+    cache = T()
+    for j in range(1, 3):
+        dc = DecodeCache(2, 3, H)  # deliberately short: exercises the in-place growth
+        cache[f"layer_{j}_k"] = dc
+        cache[f"layer_{j}_v"] = dc
+    for i in range(6):
+        logits, cache = tr.symbols(ids, i, 6, enc, mask, cache)
+        torch.testing.assert_close(logits, full[:, i], rtol=1e-4, atol=1e-4)
+    assert cache["layer_1_k"].length == 6
+
+
+def test_beam_search_in_place_cache_matches_tensor_cache():
+    from bigdl.nn.layers.attention import PaddingMask
+    torch.manual_seed(5)
+    V, H = 24, 16
+    bs = SequenceBeamSearch(V, 3, 0.6, 7, 3, 0, 2, H)
+    tr = Transformer(V, H, 4, 32, 2, 1.0, 1.0, 1.0, with_share_weights_linear=True, transformer_type="Translation",
+                     beam_search=bs)
+    tr.evaluate()
+    src = torch.randint(1, V, (3, 5)).float()
+    a = tr.forward(src)
+    bs.inPlaceCache = False
+    b = tr.forward(src)
+    torch.testing.assert_close(a[1], b[1])
+    torch.testing.assert_close(a[2], b[2], rtol=1e-4, atol=1e-4)
+
+
+def test_attention_decode_reference_bias_order():
+    """Reference semantics: keys are [new; cache] (newest first); a bias over keys is indexed in
+    that order — the in-place cache (oldest first) reads it reversed."""
+    from bigdl.ops import reference as R
+    torch.manual_seed(0)
+    rows, Lq, Hh, D, L = 2, 1, 2, 8, 5
+    q = torch.randn(rows, Lq, Hh * D)
+    kc = torch.randn(rows, 7, Hh * D)
+    vc = torch.randn(rows, 7, Hh * D)
+    bias = torch.randn(rows, 1, Lq, L)
+    o = R.attention_decode(q, kc, vc, L, Hh, D, 0.3, bias, True)
+    # explicit: newest-first keys with the bias as given
+    k = kc[:, :L].flip(1)
+    v = vc[:, :L].flip(1)
+    qh = q.reshape(rows, Lq, Hh, D).transpose(1, 2)
+    kh = k.reshape(rows, L, Hh, D).transpose(1, 2)
+    vh = v.reshape(rows, L, Hh, D).transpose(1, 2)
+    ref = torch.softmax(qh @ kh.transpose(-1, -2) * 0.3 + bias, -1) @ vh
+    torch.testing.assert_close(o, ref.transpose(1, 2).reshape(rows, Lq, Hh * D))

@@ -57,12 +57,12 @@ def _case(B, Hh, D, Lq, Lk, bias_kind, causal, keep, seed=123):
         assert _rel(a.cpu(), b) < 3e-2, (name, _rel(a.cpu(), b))
 
 
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
 def test_self_attention_no_bias(D):
     _case(2, 4, D, 100, 100, None, False, 1.0)
 
 
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
 def test_causal_mask(D):
     _case(2, 3, D, 130, 130, None, True, 1.0)
 
