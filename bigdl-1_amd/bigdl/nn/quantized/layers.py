@@ -107,11 +107,39 @@ class SpatialConvolution(_QuantizedBase):
                                 self.dilationH, self.dilationW)
         return self.padH, self.padH, self.padW, self.padW
 
+    def _native_i8(self, x, pads):
+        """The int8 implicit-GEMM kernel (ops/csrc/conv_i8.hip): per-image activation scales, the
+        gather and the GEMM in one launch, dequantisation + bias in the epilogue."""
+        from ...ops import native_ops as NO
+        pt, pb, pl, pr = pads
+        N, C, H, W = x.shape
+        kh, kw = self.kernelH, self.kernelW
+        if not (x.is_cuda and self.nGroup == 1 and NO.conv_i8_supported(C, kh, kw) and self.nOutputPlane % 8 == 0
+                and ops.native_has("gemm_i8")):
+            return NotImplemented
+        P = (H + pt + pb - self.dilationH * (kh - 1) - 1) // self.strideH + 1
+        Q = (W + pl + pr - self.dilationW * (kw - 1) - 1) // self.strideW + 1
+        prep = getattr(self, "_i8w", None)
+        if prep is None or prep[0].device != x.device:
+            wq, ldw = NO.conv_i8_weight(self.qweight.to(x.device), self.nOutputPlane, C, kh, kw)
+            prep = self._i8w = (wq, ldw, self.weight_scale.to(x.device).float().contiguous(),
+                                self.bias_f.to(x.device).float().contiguous() if self.bias_f is not None else None)
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return NO.conv2d_i8_forward(xb, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane, kh, kw,
+                                    (self.strideH, self.strideW), (pt, pl), (self.dilationH, self.dilationW), (P, Q))
+
     def updateOutput(self, input):
         x = input if input.dim() == 4 else input.unsqueeze(0)
         if getattr(self, "format", "NCHW") == "NHWC":
             x = x.permute(0, 3, 1, 2)
         pt, pb, pl, pr = self._pads(x)
+        y = self._native_i8(x, (pt, pb, pl, pr))
+        if y is not NotImplemented:
+            if x.dtype == torch.float32:
+                y = y.float()
+            if getattr(self, "format", "NCHW") == "NHWC":
+                y = y.permute(0, 2, 3, 1)
+            return y if input.dim() == 4 else y.squeeze(0)
         x = F.pad(x, (pl, pr, pt, pb)) if (pt or pb or pl or pr) else x
         N, C, H, W = x.shape
         kh, kw = self.kernelH, self.kernelW

@@ -1,0 +1,381 @@
+// Int8 implicit-GEMM convolution for quantized inference: the MI355X form of BigQuant's
+// ConvDataInit (im2col + quantise) + MixPrecisionGEMM (DL/nn/quantized/SpatialConvolution.scala:
+// 163-208).  No im2col is materialised: the k-tiles of the implicit GEMM
+//   acc[n][m] = Σ_k Wq[n][k] · Xq[m][k],   k = (r, s, c),  m = output pixel, n = output channel
+// are gathered from the int8 NHWC activation straight into LDS by LDS-DMA (buffer_load_dwordx4 …
+// lds; out-of-range offsets — conv padding, the M tail, taps past R·S — read as zeros), and
+// multiplied with v_mfma_i32_32x32x32_i8 (2× the bf16 rate per clock).  The tile machinery is the
+// 32x32x16 bf16 family's (conv_mfma32.hip): 128-byte LDS rows — 128 int8 k-elements here —, the
+// chunk ^ ((row >> 1) & 7) swizzle applied on the per-lane source address and on the fragment read,
+// a 3-deep LDS ring with counted vmcnt and raw s_barrier.  An i8 32x32x32 fragment is 16 bytes per
+// lane at the same (row, chunk) positions as a bf16 32x32x16 fragment, so the read addressing is
+// shared.
+//
+// Scales: activations per image (sx[n] = amax_n / 127, dynamic — k_absmax_img + k_quant_img below),
+// weights per output channel (sw[k], symmetric); the epilogue dequantises acc·sx[img]·sw[k] + bias,
+// applies ReLU and stores bf16 through the shared row-major store pass.
+//
+// Channel counts: C % 128 == 0 (a k-tile lies inside one tap: the tap is wave-uniform) or C == 64
+// (a k-tile holds two taps: chunks 0–3 tap 2t, chunks 4–7 tap 2t + 1, per-lane source offsets; an
+// odd R·S leaves a zero half tile).  Weight rows are [K][ldw] int8, (r, s, c) order, zero-padded to
+// ldw = KT·128.
+#include "conv_params.h"
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void i8_lds_void_t;
+
+#define I8_WAIT(n) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory")
+#define I8_BARRIER()                   \
+  do {                                 \
+    asm volatile("" ::: "memory");     \
+    __builtin_amdgcn_s_barrier();      \
+    asm volatile("" ::: "memory");     \
+  } while (0)
+
+__device__ __forceinline__ void i8_glds16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (i8_lds_void_t*)lds, 16, voff, 0, 0, 0);
+}
+
+struct ConvI8Params {
+  const int8_t* x;    // [Nb][H][W][C]
+  const int8_t* w;    // [K][ldw]
+  const float* sx;    // [Nb]
+  const float* swt;   // [K]
+  const float* bias;  // [K] or null
+  bf16_t* y;          // [M][ldy]
+  int Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw;
+  int M, KT, ldw, ldy, relu, tiles_n;
+};
+
+template <int BM, int BN, int WM, int WN, int TPT>
+__global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int NS = 3;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;
+  static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
+  constexpr int L = GA + GB;
+  constexpr int TMI = BM / WM / 32, TNI = BN / WN / 32;
+  constexpr int EPI = BM * BN * 2;
+  constexpr int LDS_BYTES = NS * STAGE > EPI ? NS * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_m = wid % WM, wave_n = wid / WM;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C);
+  const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0x80000000u;
+  const int RS = p.R * p.S;
+
+  const int lrow = lane >> 3, slot = lane & 7;
+  uint32_t woff[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    woff[i] = n < p.K ? (uint32_t)n * (uint32_t)p.ldw + (uint32_t)chunk * 16u : OOB;
+  }
+  // per-lane activation source: pixel base + this lane's chunk inside the tap (TPT == 2: the low
+  // four chunks belong to the tile's first tap, the high four to its second)
+  int rbase[GB];
+  uint64_t vmask[GB];
+  int hi_half = 0;
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = 8 * (wid + NW * j) + lrow;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    hi_half = chunk >> 2;  // the same for every j (rows 8 apart share (row >> 1) & 7 … per group)
+    const int m = m0 + row;
+    int img = -1, h = 0, w = 0;
+    if (m < p.M) {
+      const int n = m / (p.P * p.Q);
+      const int pq = m - n * p.P * p.Q;
+      const int pp = pq / p.Q, qq = pq - pp * p.Q;
+      img = n;
+      h = pp * p.sh - p.ph;
+      w = qq * p.sw - p.pw;
+    }
+    const int cin = TPT == 2 ? (chunk & 3) * 16 : chunk * 16;
+    rbase[j] = ((img * p.H + h) * p.W + w) * p.C + cin;
+    uint64_t msk = 0;
+    if (img >= 0) {
+      for (int r = 0; r < p.R; ++r) {
+        const int hh = h + r * p.dh;
+        if ((unsigned)hh >= (unsigned)p.H) continue;
+        for (int sx = 0; sx < p.S; ++sx) {
+          const int ww = w + sx * p.dw;
+          if ((unsigned)ww < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
+        }
+      }
+    }
+    vmask[j] = msk;
+  }
+  (void)hi_half;
+
+  // wave-uniform tap iterator: (tap, offset of tap in the activation, channel base inside the tap)
+  int it_tap = 0, it_s = 0, it_off = 0, it_c0 = 0;
+  auto next_tap = [&]() {
+    ++it_tap;
+    if (++it_s == p.S) {
+      it_s = 0;
+      it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.C;
+    } else {
+      it_off += p.dw * p.C;
+    }
+  };
+  auto stage = [&](int kt, int slotbuf) {
+    unsigned char* base = lds + slotbuf * STAGE;
+    const uint32_t kb = (uint32_t)kt * 128u;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) i8_glds16(wr, base + 8 * (wid + NW * i) * 128, woff[i] + kb);
+    int tap_a, off_a, tap_b = 0, off_b = 0, c0 = 0;
+    if (TPT == 2) {
+      tap_a = it_tap;
+      off_a = it_off;
+      next_tap();
+      tap_b = it_tap;
+      off_b = it_off;
+      next_tap();
+    } else {
+      tap_a = it_tap;
+      off_a = it_off;
+      c0 = it_c0;
+      it_c0 += 128;
+      if (it_c0 == p.C) {
+        it_c0 = 0;
+        next_tap();
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = 8 * (wid + NW * j) + lrow;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      unsigned char* dst = base + (BN + 8 * (wid + NW * j)) * 128;
+      uint32_t off;
+      if (TPT == 2) {
+        const bool hi = chunk >= 4;
+        const int tap = hi ? tap_b : tap_a;
+        const bool ok = tap < RS && ((vmask[j] >> tap) & 1ull);
+        off = ok ? (uint32_t)(rbase[j] + (hi ? off_b : off_a)) : OOB;
+      } else {
+        const bool ok = (vmask[j] >> tap_a) & 1ull;
+        off = ok ? (uint32_t)(rbase[j] + off_a + c0) : OOB;
+      }
+      i8_glds16(xr, dst, off);
+    }
+  };
+
+  v16i acc[TNI][TMI];
+#pragma unroll
+  for (int i = 0; i < TNI; ++i)
+#pragma unroll
+    for (int j = 0; j < TMI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  const int frow = lane & 31, fh = lane >> 5;
+  int foff[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) foff[kk] = frow * 128 + (((kk * 2 + fh) ^ ((frow >> 1) & 7)) << 4);
+  const int a_row0 = wave_n * (BN / WN), b_row0 = BN + wave_m * (BM / WM);
+
+  auto compute = [&](int slotbuf) {
+    const unsigned char* base = lds + slotbuf * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      v4i af[TNI], bfr[TMI];
+#pragma unroll
+      for (int i = 0; i < TNI; ++i) af[i] = *reinterpret_cast<const v4i*>(base + (a_row0 + 32 * i) * 128 + foff[kk]);
+#pragma unroll
+      for (int j = 0; j < TMI; ++j) bfr[j] = *reinterpret_cast<const v4i*>(base + (b_row0 + 32 * j) * 128 + foff[kk]);
+#pragma unroll
+      for (int i = 0; i < TNI; ++i)
+#pragma unroll
+        for (int j = 0; j < TMI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int KT = p.KT;
+  stage(0, 0);
+  if (KT > 1) {
+    stage(1, 1);
+    I8_WAIT(L);
+  } else {
+    I8_WAIT(0);
+  }
+  I8_BARRIER();
+  int cur = 0, nxt = 2;
+  for (int t = 0; t + 2 < KT; ++t) {
+    stage(t + 2, nxt);
+    compute(cur);
+    I8_WAIT(L);
+    I8_BARRIER();
+    cur = cur == NS - 1 ? 0 : cur + 1;
+    nxt = nxt == NS - 1 ? 0 : nxt + 1;
+  }
+  if (KT >= 2) {
+    compute(cur);
+    I8_WAIT(0);
+    I8_BARRIER();
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  compute(cur);
+  I8_BARRIER();  // the epilogue reuses the ring's LDS
+
+  // dequantise (acc · sx[img] · sw[n] + bias, ReLU) and park as bf16 [BM][BN]
+  constexpr int CMASK = (BN / 8 - 1) & 15;
+  bf16_t* et = reinterpret_cast<bf16_t*>(lds);
+  const int pm = lane & 31;
+  float sxm[TMI];
+#pragma unroll
+  for (int j = 0; j < TMI; ++j) {
+    const int m = m0 + (b_row0 - BN) + 32 * j + pm;
+    sxm[j] = m < p.M ? p.sx[m / (p.P * p.Q)] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TNI; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
+      float s4[4], b4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + nl + e;
+        s4[e] = n < p.K ? p.swt[n] : 0.f;
+        b4[e] = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < TMI; ++j) {
+        const int ml = (b_row0 - BN) + 32 * j + pm;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+          if (p.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(&et[ml * BN + (((nl >> 3) ^ (ml & CMASK)) << 3) + (nl & 4)]) = make_uint2(lo, hi);
+      }
+    }
+  __syncthreads();
+  ConvParams q{};
+  q.y = p.y;
+  q.ldy = p.ldy;
+  q.M = p.M;
+  q.K = p.K;
+  conv_store_pass<BM, BN, NT>(q, et, tid, m0, n0, tm, false);
+}
+
+// ---- activation quantisation: per-image absmax, then int8 with scale amax / 127 ----------------
+__global__ void __launch_bounds__(256) k_absmax_img(const bf16_t* __restrict__ x, long long per_img,
+                                                    float* __restrict__ amax) {
+  const int n = blockIdx.y;
+  const bf16_t* xp = x + (long long)n * per_img;
+  float m = 0.f;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8; i < per_img; i += (long long)gridDim.x * 256 * 8) {
+    float v[8];
+    load8(xp + i, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    // non-negative floats order like their bit patterns: an integer max is a float max
+    atomicMax(reinterpret_cast<unsigned int*>(amax + n), __float_as_uint(b));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_quant_img(const bf16_t* __restrict__ x, long long per_img,
+                                                   const float* __restrict__ amax, int8_t* __restrict__ xq,
+                                                   float* __restrict__ sx) {
+  const int n = blockIdx.y;
+  const float a = amax[n];
+  const float scale = a > 0.f ? a / 127.f : 1.f;
+  const float inv = 1.f / scale;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sx[n] = scale;
+  const bf16_t* xp = x + (long long)n * per_img;
+  int8_t* qp = xq + (long long)n * per_img;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 16; i < per_img;
+       i += (long long)gridDim.x * 256 * 16) {
+    float v[16];
+    load8(xp + i, v);
+    load8(xp + i + 8, v + 8);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float r = fminf(fmaxf(rintf(v[4 * k + e] * inv), -127.f), 127.f);
+        acc |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+      }
+      w[k] = acc;
+    }
+    *reinterpret_cast<uint4*>(qp + i) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// x: [Nb][per_img] bf16 (per_img % 16 == 0, 16-B aligned) → xq int8 (same layout) and sx[Nb] (the
+// dequantisation scale of each image); amax: [Nb] fp32 workspace.
+BIGDL_EXPORT int bigdl_quant_img(const void* x, int Nb, long long per_img, float* amax, void* xq, float* sx,
+                                 hipStream_t s) {
+  if (!x || !amax || !xq || !sx || Nb <= 0 || Nb > 65535 || per_img <= 0 || per_img % 16 ||
+      ((uintptr_t)x & 15) || ((uintptr_t)xq & 15))
+    return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(amax, 0, sizeof(float) * Nb, s);
+  if (e != hipSuccess) return (int)e;
+  long long chunks = (per_img + 256 * 8 * 8 - 1) / (256 * 8 * 8);  // ≥ 8 vectors per thread
+  if (chunks > 1024) chunks = 1024;
+  hipLaunchKernelGGL(k_absmax_img, dim3((unsigned)chunks, (unsigned)Nb), dim3(256), 0, s, (const bf16_t*)x, per_img,
+                     amax);
+  hipLaunchKernelGGL(k_quant_img, dim3((unsigned)chunks, (unsigned)Nb), dim3(256), 0, s, (const bf16_t*)x, per_img,
+                     (const float*)amax, (int8_t*)xq, sx);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// y[m][n] (bf16, row stride ldy) = [ReLU](Σ_k w[n][k]·x̂[m][k] · sx[img(m)] · sw[n] + bias[n]).
+// x: int8 NHWC [Nb][H][W][C] (C % 128 == 0 or C == 64); w: int8 [K][ldw], (r, s, c) order zero-padded
+// to ldw = KT·128 (KT = R·S·C / 128, or ⌈R·S / 2⌉ for C == 64); R·S ≤ 64; K % 8 == 0.
+BIGDL_EXPORT int bigdl_conv_i8_fwd(const void* x, const void* w, int ldw, const float* sx, const float* swt,
+                                   const float* bias, void* y, int ldy, int Nb, int H, int W, int C, int K, int R,
+                                   int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu,
+                                   hipStream_t s) {
+  if (!x || !w || !sx || !swt || !y || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0) return (int)hipErrorInvalidValue;
+  const int tpt = C == 64 ? 2 : (C % 128 == 0 ? 1 : 0);
+  if (!tpt || R * S > 64 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
+  const int KT = tpt == 2 ? (R * S + 1) / 2 : R * S * C / 128;
+  if (ldw != KT * 128 || ldy < K || ldy % 8 || ((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15))
+    return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * H * W * C >= 0x80000000ull || (size_t)K * ldw >= 0x80000000ull) return (int)hipErrorInvalidValue;
+  const long long Ml = (long long)Nb * P * Q;
+  if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  ConvI8Params p{};
+  p.x = (const int8_t*)x; p.w = (const int8_t*)w; p.sx = sx; p.swt = swt; p.bias = bias; p.y = (bf16_t*)y;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.M = (int)Ml; p.KT = KT; p.ldw = ldw; p.ldy = ldy; p.relu = relu;
+  constexpr int BM = 256, BN = 128;
+  p.tiles_n = (K + BN - 1) / BN;
+  const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
+  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
+  if (tpt == 2)
+    hipLaunchKernelGGL((k_conv_i8<BM, BN, 4, 2, 2>), dim3((unsigned)tiles), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((k_conv_i8<BM, BN, 4, 2, 1>), dim3((unsigned)tiles), dim3(512), 0, s, p);
+  BIGDL_CHECK_LAUNCH();
+}

@@ -1504,6 +1504,54 @@ def quant_rows(x2d, kp=None):
     return q, sc
 
 
+# ---- int8 implicit-GEMM convolution (conv_i8.hip) ----------------------------------------------
+def conv_i8_supported(C_, R, S, groups=1) -> bool:
+    return groups == 1 and (C_ == 64 or C_ % 128 == 0) and R * S <= 64
+
+
+def conv_i8_weight(qweight, K, C_, R, S):
+    """Per-output-channel int8 weights of the (c, kh, kw)-ordered GEMM view → the kernel's
+    [K][ldw] rows in (r, s, c) order, zero-padded to whole 128-byte k-tiles.  Returns (w, ldw)."""
+    kg = C_ * R * S
+    w = qweight[:, :kg].reshape(K, C_, R, S).permute(0, 2, 3, 1).reshape(K, R * S, C_)
+    KT = (R * S + 1) // 2 if C_ == 64 else kg // 128
+    ldw = KT * 128
+    out = torch.zeros((K, ldw), dtype=torch.int8, device=qweight.device)
+    out[:, :kg] = w.reshape(K, kg)
+    return out, ldw
+
+
+def quant_images(x):
+    """Per-image dynamic int8 quantisation of an NHWC bf16 activation: (xq int8 same layout, sx
+    fp32 [N] dequantisation scales = amax / 127)."""
+    N_ = x.shape[0]
+    per = x.numel() // N_
+    xq = torch.empty_like(x, dtype=torch.int8)
+    sx = torch.empty(N_, dtype=_f32, device=x.device)
+    amax = torch.empty(N_, dtype=_f32, device=x.device)
+    check(_lib().bigdl_quant_img(ptr(x), C.c_int(N_), _ll(per), ptr(amax), ptr(xq), ptr(sx), _s()), "quant_img")
+    return xq, sx
+
+
+def conv2d_i8_forward(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation, out_hw, relu=False):
+    """int8 conv of a channels-last bf16 activation (quantised per image here) with prepared
+    weights (:func:`conv_i8_weight`); ``pad`` = (top, left), ``out_hw`` = (P, Q) from the full
+    padding.  Returns the bf16 output (N, K, P, Q), channels-last memory, or NotImplemented."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last)):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if not conv_i8_supported(C_, R, S) or K % 8 or not _al16(x):
+        return NotImplemented
+    P, Q = out_hw
+    xq, sx = quant_images(x)
+    y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    b = bias.float().contiguous() if bias is not None else None
+    check(_lib().bigdl_conv_i8_fwd(ptr(xq), ptr(wq), C.c_int(ldw), ptr(sx), ptr(w_scale), ptr(b), ptr(y), C.c_int(K),
+                                   N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0],
+                                   dilation[1], C.c_int(1 if relu else 0), _s()), "conv_i8_fwd")
+    return y
+
+
 @register("gemm_i8")
 def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
     if qa.dtype != torch.int8 or qb.dtype != torch.int8 or qa.shape[1] != qb.shape[1] or qa.shape[1] % 16:
