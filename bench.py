@@ -238,6 +238,7 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         config.set_property("bigdl.compute.dtype", "fp32")
+        Engine.set_compute_dtype("fp32")
         o32, b32, el32, loss32, _ = _timed(args, dev, rank, distri, args.fp32_warmup, n32)
         fp32 = {"value": round(B * world * n32 / el32, 2), "ms_per_step": round(el32 / n32 * 1e3, 3), "steps": n32,
                 "warmup": args.fp32_warmup, "dtype": "fp32", "final_loss": loss32}

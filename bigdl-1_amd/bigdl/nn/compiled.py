@@ -247,18 +247,26 @@ def select_kernels(records, iters: int = 5, min_gain: float = 0.03) -> Dict[tupl
     seen = {}
     for key, fn in records:
         seen.setdefault(key, fn)
-    for key, fn in seen.items():
-        table.pop(key, None)
-        times = _time_candidates(key, fn, iters, lib)
-        base = times.get(_candidates(key)[0])
-        if base is None or not times:
-            continue
-        best = min(times, key=times.get)
-        if best != _candidates(key)[0] and times[best] < base * (1.0 - min_gain):
-            table[key] = best
-            chosen[key] = best
-            _log.info("kernel %s: %s %.1f us (heuristic %.1f us)", key, best, times[best] * 1e3, base * 1e3)
+    NO._TILE["retiming"] = True
+    try:
+        for key, fn in seen.items():
+            _select_one(key, fn, iters, min_gain, lib, table, chosen)
+    finally:
+        NO._TILE["retiming"] = False
     return chosen
+
+
+def _select_one(key, fn, iters, min_gain, lib, table, chosen):
+    table.pop(key, None)
+    times = _time_candidates(key, fn, iters, lib)
+    base = times.get(_candidates(key)[0])
+    if base is None or not times:
+        return
+    best = min(times, key=times.get)
+    if best != _candidates(key)[0] and times[best] < base * (1.0 - min_gain):
+        table[key] = best
+        chosen[key] = best
+        _log.info("kernel %s: %s %.1f us (heuristic %.1f us)", key, best, times[best] * 1e3, base * 1e3)
 
 
 def autotune_training_step(step_fn, iters: int = 5, min_gain: float = 0.03) -> Dict[tuple, tuple]:

@@ -65,11 +65,17 @@ def _fused_rows(ts):
     parameters of one flat arena / shadow), else None."""
     t0 = ts[0]
     cols, n = t0.shape[-1], 0
+    st0 = t0.untyped_storage()
     for t in ts:
+        # adjacency must be WITHIN one storage: separately cast copies can sit back to back by
+        # allocator coincidence, and a view over them would run past the first storage
         if (t.dim() != 2 or t.shape[1] != cols or not t.is_contiguous() or t.dtype != t0.dtype
-                or t.device != t0.device or t.data_ptr() != t0.data_ptr() + n * cols * t0.element_size()):
+                or t.device != t0.device or t.untyped_storage().data_ptr() != st0.data_ptr()
+                or t.data_ptr() != t0.data_ptr() + n * cols * t0.element_size()):
             return None
         n += t.shape[0]
+    if (t0.storage_offset() + n * cols) * t0.element_size() > st0.nbytes():
+        return None
     return torch.as_strided(t0, (n, cols), (cols, 1))
 
 

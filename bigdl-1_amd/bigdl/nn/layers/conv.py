@@ -197,9 +197,10 @@ class SpatialConvolution(TensorModule):
         y = NotImplemented
         if bn is not None and ops.native_has("conv2d_forward"):
             shift = bn.runningMean if config.get_property("bigdl.bn.shiftedStats") else None
+            sums = bn._atomic_sums("fwd", self.nOutputPlane, x.device) if shift is not None else None
             r = ops.native_ops.conv2d_forward_stats(x, w4, b, (self.strideH, self.strideW), pad,
                                                 (self.dilationH, self.dilationW), self.nGroup,
-                                                pad_slot=self._pad_slot_(), shift=shift)
+                                                pad_slot=self._pad_slot_(), shift=shift, sums=sums)
             if r is not NotImplemented:
                 y, part, G = r
                 bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G, shift)
@@ -249,12 +250,14 @@ class SpatialConvolution(TensorModule):
                 and bn._coef is not None and bn._last_input is not None
                 and config.get_property("bigdl.fusion.bnbwd")):
             C_ = bn._coef.numel() // 2
-            bn_fuse = {"x": bn._last_input, "scale": bn._coef[:C_], "shift": bn._coef[C_:], "mean": bn.saveMean}
+            bn_fuse = {"x": bn._last_input, "scale": bn._coef[:C_], "shift": bn._coef[C_:], "mean": bn.saveMean,
+                       "sums": bn._atomic_sums("bwd", C_, gy.device)}
         elif (fuse_res and self._tail_candidates and gy.is_cuda and config.get_property("bigdl.fusion.bnbwd")):
             bn = self._tail_target(x)
             if bn is not None:
                 bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output,
-                           "bits": getattr(bn, "_relu_bits", None)}
+                           "bits": getattr(bn, "_relu_bits", None),
+                           "sums": bn._atomic_sums("bwd", bn.saveMean.numel(), gy.device)}
         # the shortcut conv of a fused ResNet block (1×1 stride 2) may hand its input gradient back
         # as a StridedGrad: the block's first conv sums it in its dgrad epilogue
         lazy = (need_input and self._lazy_strided_ok and res is None and bn_fuse is None and batched

@@ -104,6 +104,27 @@ class BatchNormalization(TensorModule):
     #: ReLU mask of the last fused-tail forward output as bits (uint8, one byte per 8 channels)
     _relu_bits = None
 
+    def _atomic_sums(self, kind, C, device):
+        """Persistent zeroed fp32 [2C + 1] buffer (Σ, Σ², arrival counter) a conv epilogue ADDS this BN's
+        statistics into — ``kind`` "fwd": the producing conv's Σ(y−K), Σ(y−K)²; "bwd": the consuming
+        conv's dgrad Σg', Σg'·(x − μ) — consumed (and re-zeroed) by the one-launch finalize+apply.
+        None when the per-tile partials path is required (SyncBN, bigdl.deterministic, off)."""
+        if (device.type != "cuda" or self._sync_active() or not config.get_property("bigdl.bn.atomicStats")
+                or config.get_property("bigdl.deterministic")):
+            return None
+        attr = "_sums_" + kind
+        buf = self.__dict__.get(attr)
+        if buf is None or buf.numel() != 2 * C + 1 or buf.device != device:
+            buf = self.__dict__[attr] = torch.zeros(2 * C + 1, dtype=torch.float32, device=device)
+        return buf
+
+    @staticmethod
+    def _drop_sums(pending, g_index):
+        """A conv left atomically accumulated sums this BN is not consuming: clear them, or the next
+        producer would add onto stale values."""
+        if pending is not None and pending[g_index] == 0:
+            pending[g_index - 1].zero_()
+
     def _in_bias(self):
         p = self._bias_producer
         if p is None or not getattr(p, "withBias", False):
@@ -160,6 +181,7 @@ class BatchNormalization(TensorModule):
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
                         relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits)
                 if r is NotImplemented:
+                    self._drop_sums(ps, 3)
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
                                                     self.momentum, self.eps, relu=relu, residual=residual,
                                                     in_bias=ib, coef_out=coef, bits_out=bits)
@@ -286,6 +308,7 @@ class BatchNormalization(TensorModule):
                     if gi is not None and input.dim() == 1:
                         gi = gi.reshape(input.shape)
                     return (gi, gy) if want_gres else gi
+            self._drop_sums(pg, 2)  # (reached only when the sums were not consumed)
             gi, gres = ops.batchnorm_backward(gy, x, g, self.saveMean, self.saveStd, y=y, relu=relu,
                                               need_input=need_input,
                                               gg_acc=self.gradWeight if (acc and self.affine) else None,

@@ -638,6 +638,256 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_coef(const void* gm, const void* x, void* gx
   BIGDL_CHECK_LAUNCH();
 }
 
+// ------------------------------------------------------------------------------------------------ fused finalize
+// Statistics accumulated with fp32 atomics (the producing conv's epilogue, ConvParams::stats_atomic,
+// ADDS each tile's partial sums into sums[2][C]; sums[2C] is an arrival counter, zero between uses):
+// the apply kernel derives the per-channel coefficients from those 2·C sums in its prologue, so a
+// training BN is ONE launch after its conv (no fold / finalize kernels).  Every block reads the sums;
+// after its last read each block takes an arrival ticket, and the block that arrives last (all the
+// others have finished reading) writes the saved statistics, the coefficient vectors and the
+// running-statistics update, then re-zeroes the sums and the counter for the next producer.  The
+// running mean may be the statistics shift K itself (it is read by every block), which is why only
+// the last arriver may update it.  Nothing is read that another block wrote, so the ticket needs no
+// acquire; the writes reach later kernels through the kernel boundary.
+struct BnFwdFin {
+  float* sums;           // [2C] Σ(y−K), Σ(y−K)², then the counter word
+  const float* kshift;   // K (nullable: 0)
+  const float* gamma;
+  const float* beta;
+  const float* in_bias;
+  float* run_mean;
+  float* run_var;
+  float* save_mean;
+  float* save_invstd;
+  float* coef;           // [2C] scale, shift
+  double M;
+  float momentum, eps;
+};
+
+__device__ __forceinline__ void fin_fwd_coef(const BnFwdFin& f, int C, int c, float& mean, float& var, float& invstd,
+                                             float& sc, float& sh) {
+  const double dm = (double)f.sums[c] / f.M;
+  var = (float)fmax((double)f.sums[C + c] / f.M - dm * dm, 0.0);
+  mean = (f.kshift ? f.kshift[c] : 0.f) + (float)dm;
+  invstd = rsqrtf(var + f.eps);
+  sc = (f.gamma ? f.gamma[c] : 1.f) * invstd;
+  sh = (f.beta ? f.beta[c] : 0.f) - mean * sc;
+}
+
+// the arrival ticket of a block that has finished reading `sums`; true in the last block
+__device__ __forceinline__ bool last_arriver(float* sums, int C) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* cnt = reinterpret_cast<unsigned*>(sums + 2 * C);
+    last = atomicAdd(cnt, 1u) == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+__device__ __forceinline__ void rezero_sums(float* sums, int C) {
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sums[i] = 0.f;
+  if (threadIdx.x == 0) *reinterpret_cast<unsigned*>(sums + 2 * C) = 0u;
+}
+
+template <bool RES, bool RELU, bool BITS>
+__global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                      bf16_t* __restrict__ y, long long M, int C, BnFwdFin f,
+                                                      uint8_t* __restrict__ bits) {
+  constexpr int U = 4;
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  if (r_off < g.RPI) {
+    const long long rstride = (long long)gridDim.x * g.RPI;
+    for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+      float sc[8], sh[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float mean, var, invstd;
+        fin_fwd_coef(f, C, cg * 8 + k, mean, var, invstd, sc[k], sh[k]);
+      }
+      long long r = (long long)blockIdx.x * g.RPI + r_off;
+      for (; r < M; r += U * rstride) {
+        bigdl_u32x4 xv[U], rvv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ru = r + u * rstride;
+          const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
+          xv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
+          if (RES) rvv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(res + off));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ru = r + u * rstride;
+          if (ru >= M) break;
+          const size_t off = (size_t)ru * C + (size_t)cg * 8;
+          float v[8], rv[8];
+          unpack8(make_uint4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]), v);
+          if (RES) unpack8(make_uint4(rvv[u][0], rvv[u][1], rvv[u][2], rvv[u][3]), rv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            float o = fmaf(v[k], sc[k], sh[k]);
+            if (RES) o += rv[k];
+            if (RELU) o = fmaxf(o, 0.f);
+            v[k] = o;
+          }
+          store8(y + off, v);
+          if (BITS) {
+            uint32_t b = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+            bits[off >> 3] = (uint8_t)b;
+          }
+        }
+      }
+    }
+  }
+  if (!last_arriver(f.sums, C)) return;
+  for (int c = t; c < C; c += blockDim.x) {
+    float mean, var, invstd, sc, sh;
+    fin_fwd_coef(f, C, c, mean, var, invstd, sc, sh);
+    f.save_mean[c] = mean;
+    f.save_invstd[c] = invstd;
+    f.coef[c] = sc;
+    f.coef[C + c] = sh;
+    if (f.run_mean) {
+      const float unb = f.M > 1.0 ? (float)(var * f.M / (f.M - 1.0)) : var;
+      const float true_mean = mean + (f.in_bias ? f.in_bias[c] : 0.f);
+      f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * true_mean;
+      f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * unb;
+    }
+  }
+  __syncthreads();  // every coefficient is computed before the sums are cleared
+  rezero_sums(f.sums, C);
+}
+
+// Training BN forward from atomically accumulated conv-epilogue statistics: ONE launch (see above).
+// sums: [2C + 1] fp32 (counter word last, zero on entry); shift: the K the conv subtracted.
+BIGDL_EXPORT int bigdl_bn_fwd_train_sums_apply(const void* x, const void* res, void* y, long long M, int C,
+                                               const float* gamma, const float* beta, const float* in_bias,
+                                               float* run_mean, float* run_var, float momentum, float eps,
+                                               float* save_mean, float* save_invstd, float* sums, const float* shift,
+                                               float* coef, int relu, void* bits, hipStream_t s) {
+  if (C % 8 || M <= 0 || !sums || !save_mean || !save_invstd || !coef || (bits && !relu)) return (int)hipErrorInvalidValue;
+  BnFwdFin f{sums, shift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef, (double)M, momentum,
+             eps};
+  const int grid = apply_grid(M, C);
+  const bf16_t* xr = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  bf16_t* yr = (bf16_t*)y;
+  uint8_t* br = (uint8_t*)bits;
+  if (relu && bits && res) hipLaunchKernelGGL((k_bn_apply_fin<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  else if (relu && bits) hipLaunchKernelGGL((k_bn_apply_fin<false, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  else if (res && relu) hipLaunchKernelGGL((k_bn_apply_fin<true, true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  else if (res) hipLaunchKernelGGL((k_bn_apply_fin<true, false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply_fin<false, true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  else hipLaunchKernelGGL((k_bn_apply_fin<false, false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// Backward twin: the consumer conv's dgrad epilogue (bnx mode, stats_atomic) ADDED Σg', Σg'·(x − μ)
+// into sums; gx = A·g' + B·x + Cc with the coefficients derived per block in the prologue; the last
+// arriver accumulates dγ / dβ (and a folded producer bias's gradient), writes the coefficients (when
+// `coef` is given: a deferred-gradient consumer), re-zeroes the sums.  gx == null: coefficients and
+// parameter gradients only (one block).
+struct BnBwdFin {
+  float* sums;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* ggamma;
+  float* gbeta;
+  float gscale;
+  float* cbias;
+  float cbscale;
+  float* coef;
+  float M;
+};
+
+__device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, float& a, float& dg, float& A, float& B,
+                                             float& Cc) {
+  a = f.sums[c];
+  const float is = f.invstd[c];
+  dg = f.sums[C + c] * is;
+  const float gm = f.gamma ? f.gamma[c] : 1.f;
+  A = gm * is;
+  B = -gm * is * is * dg / f.M;
+  Cc = -gm * is * a / f.M - B * f.mean[c];
+}
+
+__global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ gx, long long M, int C, BnBwdFin f) {
+  constexpr int U = 4;
+  BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg_local = t % g.tpr;
+  const int r_off = t / g.tpr;
+  if (gx && r_off < g.RPI) {
+    const long long rstride = (long long)gridDim.x * g.RPI;
+    for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
+      float A[8], B[8], Cc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float a, dg;
+        fin_bwd_coef(f, C, cg * 8 + k, a, dg, A[k], B[k], Cc[k]);
+      }
+      long long r = (long long)blockIdx.x * g.RPI + r_off;
+      for (; r < M; r += U * rstride) {
+        bigdl_u32x4 gq[U], xq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ru = r + u * rstride;
+          const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
+          gq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(gy + off));
+          xq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ru = r + u * rstride;
+          if (ru >= M) break;
+          const size_t off = (size_t)ru * C + (size_t)cg * 8;
+          float gv[8], xv[8];
+          unpack8(make_uint4(gq[u][0], gq[u][1], gq[u][2], gq[u][3]), gv);
+          unpack8(make_uint4(xq[u][0], xq[u][1], xq[u][2], xq[u][3]), xv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) xv[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
+          store8(gx + off, xv);
+        }
+      }
+    }
+  }
+  if (!last_arriver(f.sums, C)) return;
+  for (int c = t; c < C; c += blockDim.x) {
+    float a, dg, A, B, Cc;
+    fin_bwd_coef(f, C, c, a, dg, A, B, Cc);
+    if (f.ggamma) f.ggamma[c] += f.gscale * dg;
+    if (f.gbeta) f.gbeta[c] += f.gscale * a;
+    if (f.cbias) f.cbias[c] += f.cbscale * (A * a + B * f.M * f.mean[c] + f.M * Cc);
+    if (f.coef) {
+      f.coef[c] = A;
+      f.coef[C + c] = B;
+      f.coef[2 * C + c] = Cc;
+    }
+  }
+  __syncthreads();
+  rezero_sums(f.sums, C);
+}
+
+BIGDL_EXPORT int bigdl_bn_bwd_sums_apply(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
+                                         const float* mean, const float* invstd, float* ggamma, float* gbeta,
+                                         float gscale, float* cbias, float cbscale, float* sums, float* coef,
+                                         hipStream_t s) {
+  if (C % 8 || M <= 0 || !sums || !mean || !invstd || (gx && (!gm || !x))) return (int)hipErrorInvalidValue;
+  BnBwdFin f{sums, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, (float)M};
+  const int grid = gx ? apply_grid(M, C) : 1;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), 0, s, (const bf16_t*)gm, (const bf16_t*)x, (bf16_t*)gx,
+                     M, C, f);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // ------------------------------------------------------------------------------------------------ SyncBN
 // Cross-rank BatchNormalization (P6 / X11, SpatialBatchNormalization.scala:1114-1151,1257-1329):
 // each rank reduces its partials to one [2][C] fp32 vector (Σ(x−K), Σ(x−K)² forward; Σg, Σg·(x−μ)

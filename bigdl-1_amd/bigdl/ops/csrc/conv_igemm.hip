@@ -559,7 +559,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            hipStream_t s, int ldw = 0, const float* stat_shift = nullptr, int res_sh = 0,
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
-                           float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0) {
+                           float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0,
+                           int stats_atomic = 0) {
   const bool c4 = C == 4;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
   if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
@@ -598,6 +599,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.y32 = y32;
   p.res = (const bf16_t*)res;
   p.stats = stats;
+  p.stats_atomic = stats ? stats_atomic : 0;
   p.res_sh = res ? res_sh : 0;
   p.res_sw = res ? res_sw : 0;
   p.res_H = res_H;
@@ -705,6 +707,21 @@ BIGDL_EXPORT int bigdl_conv_fwd_full(const void* x, const void* w, const float* 
   return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, relu, osh,
                          osw, ooh, oow, oH, oW, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, 0, 0, 0, 0,
                          nullptr, 0, 1, nullptr, nullptr, nullptr, tbn, tbk, tbm);
+}
+
+// bigdl_conv_fwd_full2 with the statistics mode (stats_atomic: 1 = the partial sums are ADDED into
+// stats[2][K], see ConvParams::stats_atomic) — the dgrad + BN-backward-prologue launch of the fused
+// ResNet path.
+BIGDL_EXPORT int bigdl_conv_fwd_bnbwd(const void* x, const void* w, const void* res, void* y, float* stats,
+                                      int stats_atomic, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                      int sh, int sw, int ph, int pw, int dh, int dw, const void* bnx,
+                                      const float* bn_sc, const float* bn_sh, const float* bn_mean,
+                                      const void* bn_mask, const void* bn_bits, int res_sh, int res_sw, int res_H,
+                                      int res_W, int tbn, int tbk, int tbm, hipStream_t s) {
+  if (res_sh < 0 || res_sw < 0 || (res_sh > 0) != (res_sw > 0) || (res_sh && !res)) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, nullptr, res, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
+                         0, P, Q, bnx, bn_sc, bn_sh, bn_mean, bn_mask, K, s, 0, nullptr, res_sh, res_sw, res_H, res_W,
+                         bn_bits, 0, 1, nullptr, nullptr, nullptr, tbn, tbk, tbm, stats_atomic);
 }
 
 // bigdl_conv_fwd_full (no bias / ReLU / scatter) with the dgrad extensions: a STRIDED residual
@@ -819,10 +836,10 @@ BIGDL_EXPORT int bigdl_conv_fwd_ldy_t(const void* x, const void* w, const float*
 BIGDL_EXPORT int bigdl_conv_fwd_stats_shift_t(const void* x, const void* w, const float* bias, void* y, float* stats,
                                               const float* shift, int Nb, int H, int W, int C, int K, int R, int S,
                                               int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int bn,
-                                              int bk, int bm, hipStream_t s) {
+                                              int bk, int bm, int stats_atomic, hipStream_t s) {
   return conv_fwd_launch(x, w, bias, nullptr, y, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 1, 1, 0,
                          0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, 0, shift, 0, 0, 0, 0, nullptr, 0,
-                         1, nullptr, nullptr, nullptr, bn, bk, bm);
+                         1, nullptr, nullptr, nullptr, bn, bk, bm, stats_atomic);
 }
 
 // Forward conv writing rows `ldy` elements apart (a channel slice of a wider NHWC tensor).
@@ -868,9 +885,11 @@ BIGDL_EXPORT int bigdl_conv_fwd_stats_shift(const void* x, const void* w, const 
 
 BIGDL_EXPORT int bigdl_conv_fwd_c4_stats_shift(const void* x, const void* w, int ldw, const float* bias, void* y,
                                                float* stats, const float* shift, int Nb, int H, int W, int K, int R,
-                                               int S, int P, int Q, int sh, int sw, int ph, int pw, hipStream_t s) {
+                                               int S, int P, int Q, int sh, int sw, int ph, int pw, int stats_atomic,
+                                               hipStream_t s) {
   return conv_fwd_launch(x, w, bias, nullptr, y, stats, Nb, H, W, 4, K, R, S, P, Q, sh, sw, ph, pw, 1, 1, 0, 1, 1, 0,
-                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw, shift);
+                         0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw, shift, 0, 0, 0, 0, nullptr, 0, 1,
+                         nullptr, nullptr, nullptr, 0, 0, 0, stats_atomic);
 }
 
 // 4-channel (RGB-padded) input with weight rows ldw elements apart (ldw % 8 == 0, zero beyond R·S·4).

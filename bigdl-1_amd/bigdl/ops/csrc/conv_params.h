@@ -70,7 +70,20 @@ struct ConvParams {
   // ReLU) are stored straight from registers as float4 per lane — no bf16 rounding, no LDS staging;
   // `y` is unused.  Plain epilogue only (no residual / statistics / BN prologue / scatter / groups).
   float* y32;
+  // statistics mode: 0 = per-row-tile partial rows stats[2][tiles_m][K] (reduced later by a
+  // fold / finalize pass), 1 = every tile ADDS its partial sums into stats[2][K] with fp32 atomics
+  // (the consumer's apply kernel finalises in its prologue and re-zeroes the buffer: no separate
+  // reduction launches; not bit-reproducible — bigdl.deterministic keeps mode 0)
+  int stats_atomic;
 };
+
+// one tile's per-channel partial sum `v` of statistic `which` (0: Σ, 1: Σ²) for channel n, row group g
+__device__ __forceinline__ void put_stat(const ConvParams& p, int which, int g, int n, float v) {
+  if (p.stats_atomic)
+    atomicAdd(&p.stats[(size_t)which * p.K + n], v);
+  else
+    p.stats[((size_t)which * p.tiles_m + g) * p.K + n] = v;
+}
 
 // Residual offset of output pixel m, channel n (dense: the output offset itself); false = the
 // residual is zero at this pixel (strided residual, off-grid pixel).
@@ -128,7 +141,7 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
       float a = 0.f;
 #pragma unroll
       for (int g = 0; g < SRED; ++g) a += red8[(which * SRED + g) * BN + c];
-      if (tm < p.tiles_m) p.stats[((size_t)which * p.tiles_m + tm) * p.K + n0 + c] = a;
+      if (tm < p.tiles_m) put_stat(p, which, tm, n0 + c, a);
     }
     return;
   }
@@ -261,7 +274,7 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
       float a = 0.f;
 #pragma unroll
       for (int g = 0; g < SRED; ++g) a += red8[(which * SRED + g) * BN + c];
-      if (n0 + c < p.K && tm < p.tiles_m) p.stats[((size_t)which * p.tiles_m + tm) * p.K + n0 + c] = a;
+      if (n0 + c < p.K && tm < p.tiles_m) put_stat(p, which, tm, n0 + c, a);
     }
   } else if (p.stats) {
     // reduce the RPP row groups of each channel chunk through LDS (after the tile reads retire)
@@ -284,8 +297,8 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
       }
       const int g = tm * (BM / SBM) + h;
       if (n0 + c < p.K && g < p.tiles_m) {
-        p.stats[(size_t)g * p.K + n0 + c] = a;
-        p.stats[((size_t)p.tiles_m + g) * p.K + n0 + c] = b;
+        put_stat(p, 0, g, n0 + c, a);
+        put_stat(p, 1, g, n0 + c, b);
       }
     }
     if (h + 1 < BM / SBM) __syncthreads();  // the next half rewrites `red`

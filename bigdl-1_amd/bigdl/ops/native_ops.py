@@ -185,7 +185,10 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     M, C_ = rc
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
-    if partial is None or partial.numel() != 2 * G * C_ or partial.dtype != _f32:
+    if G == 0:  # atomically accumulated sums [2C + 1] (conv epilogue, stats_atomic)
+        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32:
+            return NotImplemented
+    elif partial is None or partial.numel() != 2 * G * C_ or partial.dtype != _f32:
         return NotImplemented
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
                                  residual.dtype != _bf16 or not _al16(residual)):
@@ -194,6 +197,14 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     mean = torch.empty(C_, dtype=_f32, device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
+    if G == 0:
+        check(_lib().bigdl_bn_fwd_train_sums_apply(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
+                                                   ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
+                                                   _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
+                                                   ptr(shift if _f32vec(shift, C_) else None), ptr(coef),
+                                                   C.c_int(1 if relu else 0), ptr(_bits_ok(bits_out, M, C_, relu)),
+                                                   _s()), "bn_fwd_train_sums_apply")
+        return y, mean, invstd
     check(_lib().bigdl_bn_fwd_train_partials(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
                                              ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
                                              _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
@@ -220,6 +231,16 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
         return NotImplemented
     coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
     gx = torch.empty_like(x) if (need_input and not lazy) else None
+    if G == 0:  # atomically accumulated [Σg', Σg'·(x − μ), counter] from the dgrad epilogue
+        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32:
+            return NotImplemented
+        check(_lib().bigdl_bn_bwd_sums_apply(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma),
+                                             ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
+                                             ptr(cbias_acc), _f(cbias_scale), ptr(partial), ptr(coef), _s()),
+              "bn_bwd_sums_apply")
+        if need_input and lazy:
+            return R_.BNGrad(gm, x, coef)
+        return gx
     check(_lib().bigdl_bn_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
                                        ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
                                        _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
@@ -687,6 +708,15 @@ def _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot=None, re
 _TILE = {"table": {}, "record": None}
 
 
+def _stat_target(part, atomic):
+    """Where a statistics epilogue writes: the real buffer, except while kernel selection re-times a
+    recorded launch whose tiles ADD into the consumer's sums (a repeat would corrupt the next step's
+    statistics): then a throwaway zeroed copy."""
+    if atomic and _TILE.get("retiming"):
+        return torch.zeros_like(part)
+    return part
+
+
 def _tiled_launch(key, fn):
     """``fn(tile)`` launches the conv with ``tile`` = (BN, BK, BM) (zeros: the launcher's
     heuristic); the tile is this geometry's entry of the kernel-selection table, if any."""
@@ -701,7 +731,7 @@ def conv_tile_table() -> dict:
 
 
 def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, stats=False, relu=False, out=None,
-                   pad_slot=None, shift=None):
+                   pad_slot=None, shift=None, sums=None):
     """``out`` (optional): a channel slice ``big[:, c0:c0+K]`` of a channels-last tensor the conv
     writes into directly (zero-copy concat); returned as the result."""
     if groups > 1 and res is None and not stats and out is None and _depthwise_ok(x, w4, groups):
@@ -752,17 +782,24 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
     bias = b if (b is None or (b.dtype == _f32 and b.is_contiguous())) else b.float().contiguous()
     part, G = None, 0
-    if stats:
-        G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
-        part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
     if shift is not None and not (stats and res is None and not relu and out is None and tuple(dilation) == (1, 1)
                                   and _f32vec(shift, K)):
         shift = None
+    atomic = 0
+    if stats:
+        if sums is not None and shift is not None and sums.dtype == _f32 and sums.numel() == 2 * K + 1 \
+                and sums.is_cuda:
+            # the tiles ADD their partial sums into the consumer BN's zeroed [2K + 1] buffer (G = 0
+            # marks it for the one-launch finalize+apply, ops/csrc/batchnorm.hip k_bn_apply_fin)
+            part, atomic = sums, 1
+        else:
+            G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * P * Q))
+            part = torch.empty(2 * G * K, dtype=_f32, device=x.device)
     if c4:
         if shift is not None:
             check(_lib().bigdl_conv_fwd_c4_stats_shift(ptr(x), ptr(wk), ldw, ptr(bias), ptr(y), ptr(part), ptr(shift),
                                                        N_, H, W, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1],
-                                                       _s()), "conv_fwd_c4_stats_shift")
+                                                       atomic, _s()), "conv_fwd_c4_stats_shift")
             return y, part, G
         check(_lib().bigdl_conv_fwd_c4(ptr(x), ptr(wk), ldw, ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, K, R, S,
                                        P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()), "conv_fwd_c4")
@@ -772,8 +809,9 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     key = (N_, H, W, C_, K, R, S, tuple(stride), tuple(pad), tuple(dilation))
     if shift is not None:
         _tiled_launch(key, lambda t: check(_lib().bigdl_conv_fwd_stats_shift_t(
-            ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(part), ptr(shift), N_, H, W, C_, K, R, S, P, Q, stride[0],
-            stride[1], pad[0], pad[1], 1, 1, t[0], t[1], t[2], _s()), "conv_fwd_stats_shift"))
+            ptr(x), ptr(wk), ptr(bias), ptr(y), ptr(_stat_target(part, atomic)), ptr(shift), N_, H, W, C_, K, R, S,
+            P, Q, stride[0], stride[1], pad[0], pad[1], 1, 1, t[0], t[1], t[2], atomic, _s()),
+            "conv_fwd_stats_shift"))
         return y, part, G
     _tiled_launch(key, lambda t: check(_lib().bigdl_conv_fwd_ldy_t(
         ptr(x), ptr(wk), ptr(bias), ptr(res), ptr(y), ptr(part), N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1],
@@ -794,12 +832,14 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out, pad_slot=pad_slot)
 
 
-def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None, shift=None):
+def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None, shift=None, sums=None):
     """Forward conv whose epilogue also emits per-row-tile Σ(y−K)/Σ(y−K)² partials for a following
     BN (128-row tiles; the BN finalize combines them in fp64).  ``shift`` (fp32 [K], e.g. the BN's
-    running mean) is K; the same array must reach the finalize.  Returns ``(y, partials, G)`` or
-    NotImplemented."""
-    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot, shift=shift)
+    running mean) is K; the same array must reach the finalize.  ``sums`` (fp32 [2K + 1], zero): the
+    tiles atomically ADD into it instead (returned G = 0) for the one-launch BN finalize+apply.
+    Returns ``(y, partials, G)`` or NotImplemented."""
+    return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot, shift=shift,
+                          sums=sums)
 
 
 def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
@@ -857,6 +897,17 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         ok = _act_ok(bx) and mu is not None and _f32vec(mu, C_)
         ok = ok and (_act_ok(mask) if mask is not None else (residual is None and sc is not None and sh is not None
                                                              and _f32vec(sc, C_) and _f32vec(sh, C_)))
+        sums = bn_fuse.get("sums")
+        if ok and ax is None and sums is not None and sums.dtype == _f32 and sums.numel() == 2 * C_ + 1 \
+                and sums.is_cuda:
+            # the tiles ADD Σg', Σg'·(x − μ) into the BN's zeroed [2C + 1] buffer (G = 0): the BN
+            # backward is then one finalize+apply launch (batchnorm.hip k_bn_bwd_apply_fin)
+            _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_bnbwd(
+                ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(_stat_target(sums, 1)), 1, N_, P, Q, K, C_, R, S, H,
+                W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
+                ptr(bits), *(rs or (0, 0, 0, 0)), t[0], t[1], t[2], _s()), "conv_dgrad_bnbwd_at"))
+            bn_fuse["partial"], bn_fuse["G"] = sums, 0
+            return gx
         if ok:
             G = _lib().bigdl_conv_num_row_tiles(_ll(N_ * H * W))
             part = torch.empty(2 * G * C_, dtype=_f32, device=gy.device)

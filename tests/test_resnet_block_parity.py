@@ -104,3 +104,54 @@ def test_block_pair_fused_bf16_matches_fp32(name):
            if not (nm.endswith(".bias") and "Convolution" in nm) and float(b.norm()) > 1e-8]
     cs = sorted(c for _, c in cos)
     assert cs[len(cs) // 2] > 0.95 and cs[0] > 0.9, sorted(cos, key=lambda t: t[1])[:5]
+
+
+@pytest.mark.parametrize("name", ["stage1_identity", "stage2_to_3", "stage4_identity"])
+def test_atomic_bn_statistics_match_partials_path(name):
+    """bigdl.bn.atomicStats: the conv epilogues ADD the BN statistics (forward Σ, Σ²; backward Σg',
+    Σg'·(x−μ)) into [2C] buffers and every BN is one finalize+apply launch.  Two training passes must
+    match the per-tile-partials path (fold + finalize kernels) to summation-order rounding, and every
+    buffer must be back to zero afterwards (the last arriving block re-zeroes it)."""
+    from bigdl.nn import Sequential, SpatialBatchNormalization
+    from bigdl.nn.fusion import fuse
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    blocks = _net()
+    i, j = PAIRS[name]
+    (ba, xa), (bb, _) = blocks[i], blocks[j]
+    base = Sequential().add(copy.deepcopy(ba)).add(copy.deepcopy(bb))
+    g = torch.Generator().manual_seed(23)
+    out = {}
+    for atomic in (False, True):
+        config.set_property("bigdl.bn.atomicStats", atomic)
+        try:
+            m = copy.deepcopy(base).cuda()
+            m.training()
+            fuse(m)
+            m.getParameters()
+            m.flat_parameters().enable_shadow(Engine.compute_dtype())
+            xg = xa.to(dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            ys = []
+            for step in range(2):
+                m.zeroGradParameters()
+                y = m.forward(xg)
+                gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(100 + step)).to(dev)
+                gx = m.backward(xg, gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+                ys.append((y.float().cpu(), gx.float().cpu()))
+            torch.cuda.synchronize()
+            bns = [mod for mod in m.flattened_modules() if isinstance(mod, SpatialBatchNormalization)]
+            if atomic:
+                bufs = [mod.__dict__.get(k) for mod in bns for k in ("_sums_fwd", "_sums_bwd")]
+                assert sum(b is not None for b in bufs) >= len(bns), "the atomic path was not taken"
+                assert all(b is None or float(b.abs().max()) == 0.0 for b in bufs), "sums not re-zeroed"
+            out[atomic] = (ys, [p.float().cpu().clone() for p in m.parameters()[1]],
+                           [torch.cat([b.runningMean, b.runningVar]).cpu() for b in bns])
+        finally:
+            config.set_property("bigdl.bn.atomicStats", True)
+    (ya, ga, ra), (yb, gb, rb) = out[False], out[True]
+    for (y0, gx0), (y1, gx1) in zip(ya, yb):
+        assert _cos(y1, y0) > 0.999 and _cos(gx1, gx0) > 0.995
+    for a, b in zip(ra, rb):
+        torch.testing.assert_close(b, a, rtol=2e-3, atol=2e-3)
+    cs = sorted(_cos(b, a) for a, b in zip(ga, gb) if float(a.norm()) > 1e-8)
+    assert cs[0] > 0.99, cs[:3]
