@@ -251,13 +251,13 @@ class SpatialConvolution(TensorModule):
                 and config.get_property("bigdl.fusion.bnbwd")):
             C_ = bn._coef.numel() // 2
             bn_fuse = {"x": bn._last_input, "scale": bn._coef[:C_], "shift": bn._coef[C_:], "mean": bn.saveMean,
-                       "sums": bn._atomic_sums("bwd", C_, gy.device)}
+                       "sums": bn._atomic_sums("bwd", C_, bn.saveMean.device)}
         elif (fuse_res and self._tail_candidates and gy.is_cuda and config.get_property("bigdl.fusion.bnbwd")):
             bn = self._tail_target(x)
             if bn is not None:
                 bn_fuse = {"x": bn._last_input, "mean": bn.saveMean, "mask": bn.output,
                            "bits": getattr(bn, "_relu_bits", None),
-                           "sums": bn._atomic_sums("bwd", bn.saveMean.numel(), gy.device)}
+                           "sums": bn._atomic_sums("bwd", bn.saveMean.numel(), bn.saveMean.device)}
         # the shortcut conv of a fused ResNet block (1×1 stride 2) may hand its input gradient back
         # as a StridedGrad: the block's first conv sums it in its dgrad epilogue
         lazy = (need_input and self._lazy_strided_ok and res is None and bn_fuse is None and batched

@@ -23,6 +23,7 @@
 //
 // Modes (as conv_igemm.hip): 1 = tap-uniform FAST gather (C % 64 == 0, R·S ≤ 64), 3 = pointwise.
 #include "conv_params.h"
+#include <type_traits>
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 
@@ -43,8 +44,12 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, void* lds, uint
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE>
-__global__ void __launch_bounds__(512, 1) k_conv_x8(ConvParams p) {
+// ILV = 1: the interleaved main loop — the next k-tile's LDS-DMA pieces are issued between the
+// MFMA groups of the current one (and the fragments of k-slice kk + 1 are read while slice kk's
+// MFMAs run), with sched_barrier fences pinning the order; ILV = 0 issues every piece of the stage
+// up front, then the 16 MFMAs.
+template <int BM, int BN, int WM, int WN, int MODE, int ILV = 0>
+__global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
   static_assert(MODE == 1 || MODE == 3, "FAST / pointwise gathers only");
   constexpr bool PW = MODE == 3;
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
@@ -163,6 +168,42 @@ __global__ void __launch_bounds__(512, 1) k_conv_x8(ConvParams p) {
     }
   };
 
+  // ILV: the stage split in two — prep() advances the tap iterator and computes every piece's source
+  // offset, issue(i) sends piece i (weights first, then activation row groups)
+  uint32_t poff[L];
+  auto prep = [&](int kt) {
+    const uint32_t kb2 = (uint32_t)(kt * BK) * 2u;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) poff[i] = woff[i] + kb2;
+    const int tap = PW ? 0 : it_tap;
+    const int tap_off = PW ? kt * BK : it_off + it_c0;
+    if (!PW) {
+      it_c0 += BK;
+      if (it_c0 == p.C) {
+        it_c0 = 0;
+        ++it_tap;
+        if (++it_s == p.S) {
+          it_s = 0;
+          it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.ldx;
+        } else {
+          it_off += p.dw * p.ldx;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const bool ok = PW ? (vmask[j] != 0) : ((vmask[j] >> tap) & 1ull);
+      poff[GA + j] = ok ? (uint32_t)(rbase[j] + tap_off) * 2u : OOB;
+    }
+  };
+  auto issue = [&](int i, int slotbuf) {
+    unsigned char* base = lds + slotbuf * STAGE;
+    if (i < GA)
+      glds16(wr, base + 8 * (wid + NW * i) * 128, poff[i]);
+    else
+      glds16(xr, base + (BN + 8 * (wid + NW * (i - GA))) * 128, poff[i]);
+  };
+
   v16f acc[TNI][TMI];
 #pragma unroll
   for (int i = 0; i < TNI; ++i)
@@ -198,9 +239,77 @@ __global__ void __launch_bounds__(512, 1) k_conv_x8(ConvParams p) {
     }
   };
 
+  // interleaved body: fragments of slice kk+1 in flight during slice kk's MFMAs; the L pieces of
+  // the next stage spread over the four slices (PPK per slice)
+  constexpr int PPK = (L + 3) / 4;
+  auto compute_ilv = [&](int slotbuf, int nslot, auto issue_on) {
+    const unsigned char* base = lds + slotbuf * STAGE;
+    v8s af[2][TNI], bfr[2][TMI];
+#pragma unroll
+    for (int i = 0; i < TNI; ++i) af[0][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + foff[0]);
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) bfr[0][j] = *reinterpret_cast<const v8s*>(base + (b_row0 + 32 * j) * 128 + foff[0]);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int c = kk & 1, n = c ^ 1;
+      if (kk + 1 < BK / 16) {
+#pragma unroll
+        for (int i = 0; i < TNI; ++i)
+          af[n][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + foff[kk + 1]);
+#pragma unroll
+        for (int j = 0; j < TMI; ++j)
+          bfr[n][j] = *reinterpret_cast<const v8s*>(base + (b_row0 + 32 * j) * 128 + foff[kk + 1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TNI; ++i) {
+#pragma unroll
+        for (int j = 0; j < TMI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c][i], bfr[c][j], acc[i][j], 0, 0, 0);
+        if (decltype(issue_on)::value && i < PPK && kk * PPK + i < L) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue(kk * PPK + i, nslot);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   // 3-deep ring: tile t+2 is issued before tile t is multiplied; the wait after the MFMAs retires
   // only tile t+1 (counted vmcnt = L), and the barrier then publishes it to every wave and frees the
   // slot just read for the next issue.
+  if constexpr (ILV == 1) {
+    prep(0);
+#pragma unroll
+    for (int i = 0; i < L; ++i) issue(i, 0);
+    if (KT > 1) {
+      prep(1);
+#pragma unroll
+      for (int i = 0; i < L; ++i) issue(i, 1);
+      X8_WAIT(L);
+    } else {
+      X8_WAIT(0);
+    }
+    X8_BARRIER();
+    int cur = 0, nxt = 2;
+    for (int t = 0; t + 2 < KT; ++t) {
+      prep(t + 2);
+      compute_ilv(cur, nxt, std::true_type{});
+      X8_WAIT(L);
+      X8_BARRIER();
+      cur = cur == NS - 1 ? 0 : cur + 1;
+      nxt = nxt == NS - 1 ? 0 : nxt + 1;
+    }
+    if (KT >= 2) {
+      compute_ilv(cur, -1, std::false_type{});
+      X8_WAIT(0);
+      X8_BARRIER();
+      cur = cur == NS - 1 ? 0 : cur + 1;
+    }
+    compute_ilv(cur, -1, std::false_type{});
+    X8_BARRIER();
+  } else {
   stage(0, 0);
   if (KT > 1) {
     stage(1, 1);
@@ -228,6 +337,7 @@ __global__ void __launch_bounds__(512, 1) k_conv_x8(ConvParams p) {
   }
   compute(cur);
   X8_BARRIER();  // the epilogue reuses the ring's LDS
+  }
 
   // fp32 output (bf16x3 path): four consecutive channels per register run → float4 stores
   const int pm = lane & 31;
@@ -289,21 +399,30 @@ bool conv_x8_ok(int mode, int bm, int bn, const ConvParams& p) {
   return true;
 }
 
-template <int MODE>
+template <int MODE, int ILV>
 static void launch_x8(int bm, int bn, dim3 g, hipStream_t s, const ConvParams& p) {
   if (bm == 128)
-    hipLaunchKernelGGL((k_conv_x8<128, 128, 2, 2, MODE>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((k_conv_x8<128, 128, 2, 2, MODE, ILV>), g, dim3(256), 0, s, p);
   else if (bn == 64)
-    hipLaunchKernelGGL((k_conv_x8<256, 64, 4, 2, MODE>), g, dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_conv_x8<256, 64, 4, 2, MODE, ILV>), g, dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((k_conv_x8<256, 128, 4, 2, MODE>), g, dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_conv_x8<256, 128, 4, 2, MODE, ILV>), g, dim3(512), 0, s, p);
+}
+
+// BIGDL_CONV_X8_ILV=1 selects the interleaved main loop (A/B)
+static int x8_ilv() {
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_X8_ILV"); return e ? atoi(e) : 0; }();
+  return v;
 }
 
 int conv_x8_launch(const ConvParams& p, int mode, int bm, int bn, dim3 grid, hipStream_t s) {
   if (!conv_x8_ok(mode, bm, bn, p)) return (int)hipErrorNotSupported;
-  if (mode == 3)
-    launch_x8<3>(bm, bn, grid, s, p);
-  else
-    launch_x8<1>(bm, bn, grid, s, p);
+  if (x8_ilv()) {
+    if (mode == 3) launch_x8<3, 1>(bm, bn, grid, s, p);
+    else launch_x8<1, 1>(bm, bn, grid, s, p);
+  } else {
+    if (mode == 3) launch_x8<3, 0>(bm, bn, grid, s, p);
+    else launch_x8<1, 0>(bm, bn, grid, s, p);
+  }
   return (int)hipGetLastError();
 }

@@ -374,6 +374,11 @@ struct LstmSeqP {
   bf16_t* dg;        // backward: [B][T][4H]
   float* gc;         // backward: dc of step 0 → [B][H]
   int B, T, H;
+  // multi-workgroup kernels: the grid holds `spread` × tiles workgroups and only every spread-th one
+  // works (tile = blockIdx.x / spread).  Workgroups are dealt to the 8 XCDs round-robin, so with
+  // spread 8 all working tiles share one XCD's L2 and the step-to-step hand-off stays inside it
+  // (placement is a speed matter only: the exchange protocol is agent-scope either way).
+  int spread;
 };
 
 constexpr int kPersistMaxH = 256;
@@ -648,9 +653,12 @@ __device__ __forceinline__ v8s xld8(const bf16_t* p) {
 
 template <int NBT, bool SC>
 __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
+  const int spread = p.spread > 0 ? p.spread : 1;
+  if (blockIdx.x % spread) return;  // an idle slot of the XCD-confined grid
+  const int tile = blockIdx.x / spread, ntiles = gridDim.x / spread;
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   const int H = p.H, B = p.B, T = p.T, G = 4 * H;
-  const int u0 = blockIdx.x * 16;
+  const int u0 = tile * 16;
   const int j = u0 + fq * 4;  // this lane's unit quad
   const bool jin = j < H;
   const bool urow = u0 + fr < H;
@@ -687,7 +695,7 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
                         ? *reinterpret_cast<const uint2*>((const bf16_t*)p.x2 + ((long long)m * T + t) * G + g * H + j)
                         : make_uint2(0u, 0u);
     }
-    if (t > 0 && !mp_wait<SC>(cnt, t * (int)gridDim.x, err)) return;
+    if (t > 0 && !mp_wait<SC>(cnt, t * ntiles, err)) return;
     // h_{t-1}: the initial state or the previous step's output column of every tile
     const bf16_t* hb = t == 0 ? p.h0 : p.out + (long long)(t - 1) * H;
     const long long ldh = t == 0 ? H : (long long)T * H;
@@ -761,9 +769,12 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
 
 template <int NBT, bool SC>
 __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
+  const int spread = p.spread > 0 ? p.spread : 1;
+  if (blockIdx.x % spread) return;
+  const int tile = blockIdx.x / spread, ntiles = gridDim.x / spread;
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   const int H = p.H, B = p.B, T = p.T, G = 4 * H;
-  const int u0 = blockIdx.x * 16;
+  const int u0 = tile * 16;
   const int j = u0 + fq * 4;
   const bool jin = j < H;
   const bool urow = u0 + fr < H;
@@ -805,7 +816,7 @@ __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
 #pragma unroll
     for (int bt = 0; bt < NBT; ++bt) acc[bt] = v4f{0.f, 0.f, 0.f, 0.f};
     if (t + 1 < T) {
-      if (!mp_wait<SC>(cnt, (T - 1 - t) * (int)gridDim.x, err)) return;
+      if (!mp_wait<SC>(cnt, (T - 1 - t) * ntiles, err)) return;
       const bf16_t* gb = p.dg + (long long)(t + 1) * G;  // dg_{t+1} rows, stride T·G
 #pragma unroll
       for (int kc = 0; kc < kMpMaxKCb; ++kc) {  // chunks past 4H hold zero fragments (no branch: keeps wf in VGPRs)
@@ -862,19 +873,27 @@ static bool lstm_mp_sc() {
   return !(e && e[0] == '0');
 }
 
-static bool lstm_mp_ok(int B, int H, const int* sync) {
+static int lstm_persist_mode() {  // read per whole-sequence call (tests switch it in-process)
   const char* e = getenv("BIGDL_RNN_PERSIST");
-  if (!e || e[0] != '2') return false;
+  return e ? atoi(e) : 0;
+}
+
+// BIGDL_RNN_PERSIST=2: the multi-workgroup kernels on ⌈H/16⌉ workgroups wherever they land;
+// =3: the same tiles confined to one XCD (8 × tiles workgroups, every 8th one works)
+static bool lstm_mp_ok(int B, int H, const int* sync) {
+  const int m = lstm_persist_mode();
+  if (m != 2 && m != 3) return false;
   return sync && B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
 }
+
+static int lstm_mp_spread() { return lstm_persist_mode() == 3 ? 8 : 1; }
 
 // The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0).  It is OPT-IN
 // (BIGDL_RNN_PERSIST=1): one CU re-streams all of U from L2 every step, and a single CU's L2 read
 // rate (tens of GB/s) makes that ~3× slower than the 13-workgroup step launches at the PTB shape
 // (B 20, H 200: 1.50 vs 1.13 ms per training step, profiles/r3_ptb_persist_ab.txt).
 static bool lstm_persist_ok(int B, int H) {
-  const char* e = getenv("BIGDL_RNN_PERSIST");
-  if (!e || e[0] != '1') return false;
+  if (lstm_persist_mode() != 1) return false;
   return B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
 }
 
@@ -904,10 +923,10 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
     LstmSeqP p{};
     p.x2 = x2; p.x_f32 = x_f32; p.h0 = (const bf16_t*)h0; p.c0 = c0; p.u = (const bf16_t*)U; p.out = (bf16_t*)out;
     p.cs = train ? cs : nullptr; p.acts = acts; p.tcs = tcs; p.cbuf = train ? nullptr : cbuf;
-    p.B = B; p.T = T; p.H = H;
+    p.B = B; p.T = T; p.H = H; p.spread = lstm_mp_spread();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
     if (e != hipSuccess) return (int)e;
-    const dim3 grid((unsigned)((H + 15) / 16));
+    const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
     const bool sc = lstm_mp_sc();
     if (B <= 16) {
       if (sc) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);
@@ -957,10 +976,10 @@ BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float*
       return (int)hipErrorInvalidValue;
     LstmSeqP p{};
     p.u = (const bf16_t*)Ut; p.acts = (float*)acts; p.tcs = (float*)tcs; p.cs = (float*)cs; p.c0 = c0;
-    p.gy = (const bf16_t*)gy; p.dg = (bf16_t*)DG; p.gc = gc; p.B = B; p.T = T; p.H = H;
+    p.gy = (const bf16_t*)gy; p.dg = (bf16_t*)DG; p.gc = gc; p.B = B; p.T = T; p.H = H; p.spread = lstm_mp_spread();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
     if (e != hipSuccess) return (int)e;
-    const dim3 grid((unsigned)((H + 15) / 16));
+    const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
     const bool sc = lstm_mp_sc();
     if (B <= 16) {
       if (sc) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);

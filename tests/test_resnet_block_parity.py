@@ -144,14 +144,18 @@ def test_atomic_bn_statistics_match_partials_path(name):
                 bufs = [mod.__dict__.get(k) for mod in bns for k in ("_sums_fwd", "_sums_bwd")]
                 assert sum(b is not None for b in bufs) >= len(bns), "the atomic path was not taken"
                 assert all(b is None or float(b.abs().max()) == 0.0 for b in bufs), "sums not re-zeroed"
-            out[atomic] = (ys, [p.float().cpu().clone() for p in m.parameters()[1]],
+            # conv biases feeding a training BN have an exactly-zero gradient (the BN removes the
+            # mean): what both paths produce there is rounding noise, so they are not compared
+            names = [f"{type(mm).__name__}.{n}" for (mm, n, _g) in m._param_entries()]
+            out[atomic] = ([(nm, p.float().cpu().clone()) for nm, p in zip(names, m.parameters()[1])
+                            if not (nm.endswith(".bias") and "Convolution" in nm)], ys,
                            [torch.cat([b.runningMean, b.runningVar]).cpu() for b in bns])
         finally:
             config.set_property("bigdl.bn.atomicStats", True)
-    (ya, ga, ra), (yb, gb, rb) = out[False], out[True]
+    (ga, ya, ra), (gb, yb, rb) = out[False], out[True]
     for (y0, gx0), (y1, gx1) in zip(ya, yb):
         assert _cos(y1, y0) > 0.999 and _cos(gx1, gx0) > 0.995
     for a, b in zip(ra, rb):
         torch.testing.assert_close(b, a, rtol=2e-3, atol=2e-3)
-    cs = sorted(_cos(b, a) for a, b in zip(ga, gb) if float(a.norm()) > 1e-8)
-    assert cs[0] > 0.99, cs[:3]
+    cs = sorted((_cos(b[1], a[1]), a[0]) for a, b in zip(ga, gb) if float(a[1].norm()) > 1e-8)
+    assert cs[0][0] > 0.99, cs[:3]

@@ -60,8 +60,9 @@ def _worker(rank, port, q):
     gw, gb = m.gradWeight.clone(), m.gradBias.clone()
     dist.all_reduce(gw)
     dist.all_reduce(gb)
-    q.put((rank, y.clone(), gi.clone(), gw, gb, m.runningMean.clone(), m.runningVar.clone(),
-           m._sync_path, m._sync_bwd_path))
+    # numpy arrays pickle by value: no shared-memory handles that must outlive this process
+    q.put((rank, y.numpy().copy(), gi.numpy().copy(), gw.numpy(), gb.numpy(), m.runningMean.numpy().copy(),
+           m.runningVar.numpy().copy(), m._sync_path, m._sync_bwd_path))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -82,6 +83,7 @@ def test_syncbn_uneven_batches_match_global_bn():
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    res = [(r[0],) + tuple(torch.from_numpy(a) for a in r[1:7]) + tuple(r[7:]) for r in res]
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
