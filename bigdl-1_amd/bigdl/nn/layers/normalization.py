@@ -24,6 +24,26 @@ from .conv import to_device_layout
 from ...utils import acc_float, config
 
 
+_SYNCBN_COMM = {}
+
+
+def _syncbn_comm():
+    """The process group SyncBN statistics are all-reduced over when a layer has no explicit
+    group: with ``bigdl.syncbn.ownComm`` one extra communicator over all ranks, created once (every
+    rank reaches its first SyncBN forward in the same order, so the collective ``new_group`` call
+    matches up) — RCCL gives each communicator its own stream, so the 2·C+1-float statistics
+    collectives are not serialised behind the gradient buckets (``parallel/distri_optimizer.py``);
+    otherwise the default group."""
+    import torch.distributed as dist
+    if not config.get_property("bigdl.syncbn.ownComm") or dist.get_world_size() == 1:
+        return None
+    key = id(dist.distributed_c10d._get_default_group())
+    g = _SYNCBN_COMM.get(key)
+    if g is None:
+        g = _SYNCBN_COMM[key] = dist.new_group(list(range(dist.get_world_size())))
+    return g
+
+
 class BatchNormalization(TensorModule):
     def __init__(self, n_output, eps=1e-5, momentum=0.1, affine=True, init_weight=None, init_bias=None,
                  init_grad_weight=None, init_grad_bias=None, bigdl_type="float"):
@@ -215,13 +235,17 @@ class BatchNormalization(TensorModule):
 
     def _sync_allreduce(self, t):
         """Sum ``t`` over the sync group in place; a one-rank group (the forced world-size-1
-        rehearsal) is the identity, so no collective is issued."""
+        rehearsal) is the identity, so no collective is issued.  Without an explicit group the
+        statistics go over a communicator of their own (:func:`_syncbn_comm`): its stream is not
+        the one the data-parallel gradient reduce-scatter / all-gather buckets queue on, so a
+        forward BN never waits behind the previous step's late all-gathers."""
         import torch.distributed as dist
         ws = self.__dict__.get("_sync_ws")
         if ws is None or ws[0] is not self._sync_group:
-            ws = self.__dict__["_sync_ws"] = (self._sync_group, dist.get_world_size(self._sync_group))
+            grp = self._sync_group if self._sync_group is not None else _syncbn_comm()
+            ws = self.__dict__["_sync_ws"] = (self._sync_group, dist.get_world_size(grp), grp)
         if ws[1] > 1:
-            dist.all_reduce(t, group=self._sync_group)
+            dist.all_reduce(t, group=ws[2])
 
     def _sync_ops(self, x):
         """The SyncBN sums contract (``bn_local_sums`` → all-reduce → ``bn_forward_from_sums``; the

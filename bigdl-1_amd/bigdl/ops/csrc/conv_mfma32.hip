@@ -411,7 +411,7 @@ static void launch_x8(int bm, int bn, dim3 g, hipStream_t s, const ConvParams& p
 
 // BIGDL_CONV_X8_ILV=1 selects the interleaved main loop (A/B)
 static int x8_ilv() {
-  static const int v = [] { const char* e = getenv("BIGDL_CONV_X8_ILV"); return e ? atoi(e) : 0; }();
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_X8_ILV"); return e ? atoi(e) : 1; }();
   return v;
 }
 

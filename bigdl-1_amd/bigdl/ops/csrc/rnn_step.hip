@@ -374,6 +374,7 @@ struct LstmSeqP {
   bf16_t* dg;        // backward: [B][T][4H]
   float* gc;         // backward: dc of step 0 → [B][H]
   int B, T, H;
+  unsigned long long* xg;  // multi-workgroup granule protocol: [2][B][K/2] {tag, 2 bf16} exchange slots
   // multi-workgroup kernels: the grid holds `spread` × tiles workgroups and only every spread-th one
   // works (tile = blockIdx.x / spread).  Workgroups are dealt to the 8 XCDs round-robin, so with
   // spread 8 all working tiles share one XCD's L2 and the step-to-step hand-off stays inside it
@@ -605,14 +606,14 @@ constexpr int kMpMaxKCb = 32;  // backward: 4H ≤ 1024 → ≤ 32 k-chunks
 //           accesses, so the barrier needs only the store acknowledgements (workgroup-scope release)
 //           before the arrival — no whole-L2 write-back / invalidate per step.
 // Either way the spin polls with relaxed agent-scope loads.
-template <bool SC>
+template <int SC>
 __device__ __forceinline__ void mp_arrive(int* cnt) {
-  if constexpr (SC) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if constexpr (SC == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's stores → visible device-wide
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SC>
+template <int SC>
 __device__ __forceinline__ bool mp_wait(int* cnt, int target, int* err) {
   int spins = 0;
   while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -622,15 +623,15 @@ __device__ __forceinline__ bool mp_wait(int* cnt, int target, int* err) {
       return false;
     }
   }
-  if constexpr (SC) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if constexpr (SC == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
 // exchanged-state accessors: 4 bf16 (8 B) store, 8 bf16 (16 B) fragment load
-template <bool SC>
+template <int SC>
 __device__ __forceinline__ void xst4(bf16_t* p, const float* v) {
-  if constexpr (SC) {
+  if constexpr (SC == 1) {
     const unsigned long long w = (unsigned long long)((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16)) |
                                  ((unsigned long long)((uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)) << 32);
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -638,9 +639,9 @@ __device__ __forceinline__ void xst4(bf16_t* p, const float* v) {
     stb4(p, v);
   }
 }
-template <bool SC>
+template <int SC>
 __device__ __forceinline__ v8s xld8(const bf16_t* p) {
-  if constexpr (SC) {
+  if constexpr (SC == 1) {
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
     const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -651,7 +652,41 @@ __device__ __forceinline__ v8s xld8(const bf16_t* p) {
   }
 }
 
-template <int NBT, bool SC>
+// SC = 2: no barrier at all — the exchanged state IS the flag (cdna_hip_programming.md §6 Guideline
+// 16, R2).  Every 2 bf16 of h_t (forward) / dg_t (backward) travel as one naturally aligned 8-byte
+// granule {tag = epoch, value} written by ONE agent-scope (sc1, write-through) store into a
+// double-buffered slot; a consumer re-reads the granules of a 32-wide k-chunk with agent-scope (sc1,
+// L1-bypassing) loads until every tag carries the step's epoch, then feeds them to the MFMA.  No
+// counter, fence or acquire: a step's hand-off costs one store→load round trip through L2/fabric
+// instead of store-ack → counter add → poll → fence → load.  Slot reuse (step t+2 overwrites step t)
+// is safe: a tile writes step t+2 only after reading all of step t+1, which every tile wrote only
+// after reading all of step t.  Epochs count from 1 within the launch; the launcher zeroes the
+// slots first (a memset node under graph replay).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void gput(unsigned long long* g, unsigned epoch, const float* v) {
+  const unsigned lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  const unsigned hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  __hip_atomic_store((gu64_t*)g, ((unsigned long long)epoch << 32) | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64_t*)(g + 1), ((unsigned long long)epoch << 32) | hi, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// 8 bf16 (4 granules) at g; returns whether every tag is `epoch`
+__device__ __forceinline__ bool gget8(const unsigned long long* g, unsigned epoch, v8s& out) {
+  unsigned v[4];
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned long long x = __hip_atomic_load((const gu64_t*)(g + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v[q] = (unsigned)x;
+    ok &= (unsigned)(x >> 32) == epoch;
+  }
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  out = __builtin_bit_cast(v8s, u4{v[0], v[1], v[2], v[3]});
+  return ok;
+}
+constexpr unsigned kGranSpin = 1u << 22;  // bounded spin: a tile that never publishes fails, no hang
+
+template <int NBT, int SC>
 __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
   const int spread = p.spread > 0 ? p.spread : 1;
   if (blockIdx.x % spread) return;  // an idle slot of the XCD-confined grid
@@ -695,10 +730,14 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
                         ? *reinterpret_cast<const uint2*>((const bf16_t*)p.x2 + ((long long)m * T + t) * G + g * H + j)
                         : make_uint2(0u, 0u);
     }
-    if (t > 0 && !mp_wait<SC>(cnt, t * ntiles, err)) return;
+    if constexpr (SC < 2) {
+      if (t > 0 && !mp_wait<SC>(cnt, t * ntiles, err)) return;
+    }
     // h_{t-1}: the initial state or the previous step's output column of every tile
     const bf16_t* hb = t == 0 ? p.h0 : p.out + (long long)(t - 1) * H;
     const long long ldh = t == 0 ? H : (long long)T * H;
+    // granule protocol: h_{t-1} sits in slot (t-1)&1 with epoch t
+    const unsigned long long* gsl = p.xg + (size_t)((t - 1) & 1) * B * (H / 2);
     v4f acc[NBT][4];
 #pragma unroll
     for (int bt = 0; bt < NBT; ++bt)
@@ -708,14 +747,35 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
     for (int kc = 0; kc < kMpMaxKC; ++kc) {
       const int k = kc * 32 + fq * 8;
       const bool kin = kc < KC && k < H;
+      v8s hf[NBT];
+      if (SC == 2 && t > 0) {
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
 #pragma unroll
-      for (int bt = 0; bt < NBT; ++bt) {
-        const int m = bt * 16 + fr;
-        const v8s hf = (kin && m < B) ? (t == 0 ? *reinterpret_cast<const v8s*>(hb + m * ldh + k) : xld8<SC>(hb + m * ldh + k))
-                                      : zero;
+          for (int bt = 0; bt < NBT; ++bt) {
+            const int m = bt * 16 + fr;
+            hf[bt] = zero;
+            if (kin && m < B) ok &= gget8(gsl + (size_t)m * (H / 2) + k / 2, (unsigned)t, hf[bt]);
+          }
+          if (__all(ok)) break;
+          if (spins > kGranSpin) {
+            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      } else {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[bt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[g][kc], hf, acc[bt][g], 0, 0, 0);
+        for (int bt = 0; bt < NBT; ++bt) {
+          const int m = bt * 16 + fr;
+          hf[bt] = (kin && m < B) ? (t == 0 ? *reinterpret_cast<const v8s*>(hb + m * ldh + k) : xld8<SC>(hb + m * ldh + k))
+                                  : zero;
+        }
       }
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[bt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[g][kc], hf[bt], acc[bt][g], 0, 0, 0);
     }
 #pragma unroll
     for (int bt = 0; bt < NBT; ++bt) {
@@ -745,6 +805,7 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
         h[e] = go[e] * tcv[e];
       }
       xst4<SC>(p.out + ((long long)m * T + t) * H + j, h);
+      if (SC == 2 && t + 1 < T) gput(p.xg + (size_t)(t & 1) * B * (H / 2) + (size_t)m * (H / 2) + j / 2, (unsigned)(t + 1), h);
       const long long mh = ((long long)t * B + m) * H + j;
       if (p.cs) {
         stf4(p.cs + mh, c[bt]);
@@ -756,7 +817,9 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
         stf4(a + 3 * H, go);
       }
     }
-    if (t + 1 < T) mp_arrive<SC>(cnt);
+    if constexpr (SC < 2) {
+      if (t + 1 < T) mp_arrive<SC>(cnt);
+    }
   }
   if (p.cbuf) {  // inference: the final c, where the step path leaves it (slot (T-1)&1)
 #pragma unroll
@@ -767,7 +830,7 @@ __global__ void __launch_bounds__(64) k_lstm_seq_fwd_mp(LstmSeqP p, int* sync) {
   }
 }
 
-template <int NBT, bool SC>
+template <int NBT, int SC>
 __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
   const int spread = p.spread > 0 ? p.spread : 1;
   if (blockIdx.x % spread) return;
@@ -816,18 +879,43 @@ __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
 #pragma unroll
     for (int bt = 0; bt < NBT; ++bt) acc[bt] = v4f{0.f, 0.f, 0.f, 0.f};
     if (t + 1 < T) {
-      if (!mp_wait<SC>(cnt, (T - 1 - t) * ntiles, err)) return;
+      if constexpr (SC < 2) {
+        if (!mp_wait<SC>(cnt, (T - 1 - t) * ntiles, err)) return;
+      }
       const bf16_t* gb = p.dg + (long long)(t + 1) * G;  // dg_{t+1} rows, stride T·G
+      // granule protocol: dg_{t+1} sits in slot (t+1)&1 with epoch T-1-t
+      const unsigned long long* gsl = p.xg + (size_t)((t + 1) & 1) * B * (G / 2);
+      const unsigned ep = (unsigned)(T - 1 - t);
 #pragma unroll
       for (int kc = 0; kc < kMpMaxKCb; ++kc) {  // chunks past 4H hold zero fragments (no branch: keeps wf in VGPRs)
         const int k = kc * 32 + fq * 8;
         const bool kin = kc < KC && k < G;
+        v8s gf[NBT];
+        if constexpr (SC == 2) {
+          for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
 #pragma unroll
-        for (int bt = 0; bt < NBT; ++bt) {
-          const int m = bt * 16 + fr;
-          const v8s gf = (kin && m < B) ? xld8<SC>(gb + (long long)m * T * G + k) : zero;
-          acc[bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], gf, acc[bt], 0, 0, 0);
+            for (int bt = 0; bt < NBT; ++bt) {
+              const int m = bt * 16 + fr;
+              gf[bt] = zero;
+              if (kin && m < B) ok &= gget8(gsl + (size_t)m * (G / 2) + k / 2, ep, gf[bt]);
+            }
+            if (__all(ok)) break;
+            if (spins > kGranSpin) {
+              if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        } else {
+#pragma unroll
+          for (int bt = 0; bt < NBT; ++bt) {
+            const int m = bt * 16 + fr;
+            gf[bt] = (kin && m < B) ? xld8<SC>(gb + (long long)m * T * G + k) : zero;
+          }
         }
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) acc[bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], gf[bt], acc[bt], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -851,8 +939,18 @@ __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
       xst4<SC>(o + H, dgg);
       xst4<SC>(o + 2 * H, df);
       xst4<SC>(o + 3 * H, dout);
+      if (SC == 2 && t > 0) {
+        unsigned long long* gq = p.xg + (size_t)(t & 1) * B * (G / 2) + (size_t)m * (G / 2) + j / 2;
+        const unsigned ep = (unsigned)(T - t);
+        gput(gq, ep, di);
+        gput(gq + H / 2, ep, dgg);
+        gput(gq + H, ep, df);
+        gput(gq + 3 * H / 2, ep, dout);
+      }
     }
-    if (t > 0) mp_arrive<SC>(cnt);
+    if constexpr (SC < 2) {
+      if (t > 0) mp_arrive<SC>(cnt);
+    }
   }
 #pragma unroll
   for (int bt = 0; bt < NBT; ++bt) {
@@ -878,15 +976,38 @@ static int lstm_persist_mode() {  // read per whole-sequence call (tests switch 
   return e ? atoi(e) : 0;
 }
 
-// BIGDL_RNN_PERSIST=2: the multi-workgroup kernels on ⌈H/16⌉ workgroups wherever they land;
-// =3: the same tiles confined to one XCD (8 × tiles workgroups, every 8th one works)
-static bool lstm_mp_ok(int B, int H, const int* sync) {
+// BIGDL_RNN_PERSIST=2: the multi-workgroup kernels on ⌈H/16⌉ workgroups wherever they land, counter
+// barrier (protocol BIGDL_RNN_MP_SYNC 0/1); =3: the same tiles confined to one XCD (8 × tiles
+// workgroups, every 8th one works); =4 / =5: the granule protocol (SC = 2, no barrier), spread 1 / 8
+static bool lstm_mp_ok(int B, int H, const int* sync, const void* xg) {
   const int m = lstm_persist_mode();
-  if (m != 2 && m != 3) return false;
+  if (m < 2 || m > 5 || ((m == 4 || m == 5) && !xg)) return false;
   return sync && B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
 }
 
-static int lstm_mp_spread() { return lstm_persist_mode() == 3 ? 8 : 1; }
+static int lstm_mp_spread() {
+  const int m = lstm_persist_mode();
+  return (m == 3 || m == 5) ? 8 : 1;
+}
+
+static int lstm_mp_proto() {
+  const int m = lstm_persist_mode();
+  return (m == 4 || m == 5) ? 2 : (lstm_mp_sc() ? 1 : 0);
+}
+
+template <int NBT>
+static void launch_fwd_mp(int proto, dim3 grid, hipStream_t s, const LstmSeqP& p, int* sync) {
+  if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
+  else if (proto == 1) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 1>), grid, dim3(64), 0, s, p, sync);
+  else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 0>), grid, dim3(64), 0, s, p, sync);
+}
+
+template <int NBT>
+static void launch_bwd_mp(int proto, dim3 grid, hipStream_t s, const LstmSeqP& p, int* sync) {
+  if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
+  else if (proto == 1) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 1>), grid, dim3(64), 0, s, p, sync);
+  else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 0>), grid, dim3(64), 0, s, p, sync);
+}
 
 // The persistent path covers B ≤ 32 and 8 ≤ H ≤ 256 (H % 8 == 0).  It is OPT-IN
 // (BIGDL_RNN_PERSIST=1): one CU re-streams all of U from L2 every step, and a single CU's L2 read
@@ -908,14 +1029,14 @@ static const bf16_t* bo(const void* p, long long off) { return p ? (const bf16_t
 
 BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, const float* c0, const void* U, void* out,
                                     float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H, int* sync,
-                                    hipStream_t s) {
+                                    void* xg, hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !U || !out) return (int)hipErrorInvalidValue;
   const bool train = cs && acts && tcs;
   if (!train && !cbuf) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
   const int esz = x_f32 ? 4 : 2;
-  if (lstm_mp_ok(B, H, sync)) {
-    if (!a16(U) || !a16(h0) || !a16(out) || (x_f32 ? !a16(x2) : !a8(x2)) || ((uintptr_t)sync & 7))
+  if (lstm_mp_ok(B, H, sync, xg)) {
+    if (!a16(U) || !a16(h0) || !a16(out) || (x_f32 ? !a16(x2) : !a8(x2)) || ((uintptr_t)sync & 7) || !a16(xg))
       return (int)hipErrorInvalidValue;
     const void* f32s[] = {c0, cs, acts, tcs, cbuf};
     for (const void* q : f32s)
@@ -924,17 +1045,14 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
     p.x2 = x2; p.x_f32 = x_f32; p.h0 = (const bf16_t*)h0; p.c0 = c0; p.u = (const bf16_t*)U; p.out = (bf16_t*)out;
     p.cs = train ? cs : nullptr; p.acts = acts; p.tcs = tcs; p.cbuf = train ? nullptr : cbuf;
     p.B = B; p.T = T; p.H = H; p.spread = lstm_mp_spread();
+    p.xg = (unsigned long long*)xg;
+    const int proto = lstm_mp_proto();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
+    if (e == hipSuccess && proto == 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (H / 2) * 8, s);
     if (e != hipSuccess) return (int)e;
     const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
-    const bool sc = lstm_mp_sc();
-    if (B <= 16) {
-      if (sc) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);
-      else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<1, false>), grid, dim3(64), 0, s, p, sync);
-    } else {
-      if (sc) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<2, true>), grid, dim3(64), 0, s, p, sync);
-      else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<2, false>), grid, dim3(64), 0, s, p, sync);
-    }
+    if (B <= 16) launch_fwd_mp<1>(proto, grid, s, p, sync);
+    else launch_fwd_mp<2>(proto, grid, s, p, sync);
     BIGDL_CHECK_LAUNCH();
   }
   if (lstm_persist_ok(B, H)) {
@@ -967,27 +1085,24 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
 
 BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float* acts, const float* tcs, const float* cs,
                                     const float* c0, void* DG, float* gc, int B, int T, int H, int* sync,
-                                    hipStream_t s) {
+                                    void* xg, hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !gy || !Ut || !DG || !gc) return (int)hipErrorInvalidValue;
   const long long G = 4LL * H, BH = (long long)B * H;
-  if (lstm_mp_ok(B, H, sync)) {
+  if (lstm_mp_ok(B, H, sync, xg)) {
     if (!acts || !tcs || !cs || !a16(Ut) || !a8(gy) || !a16(DG) || !a16(acts) || !a16(tcs) || !a16(cs) || !a16(gc) ||
-        (c0 && !a16(c0)) || ((uintptr_t)sync & 7))
+        (c0 && !a16(c0)) || ((uintptr_t)sync & 7) || !a16(xg))
       return (int)hipErrorInvalidValue;
     LstmSeqP p{};
     p.u = (const bf16_t*)Ut; p.acts = (float*)acts; p.tcs = (float*)tcs; p.cs = (float*)cs; p.c0 = c0;
     p.gy = (const bf16_t*)gy; p.dg = (bf16_t*)DG; p.gc = gc; p.B = B; p.T = T; p.H = H; p.spread = lstm_mp_spread();
+    p.xg = (unsigned long long*)xg;
+    const int proto = lstm_mp_proto();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
+    if (e == hipSuccess && proto == 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (2 * H) * 8, s);
     if (e != hipSuccess) return (int)e;
     const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
-    const bool sc = lstm_mp_sc();
-    if (B <= 16) {
-      if (sc) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<1, true>), grid, dim3(64), 0, s, p, sync);
-      else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<1, false>), grid, dim3(64), 0, s, p, sync);
-    } else {
-      if (sc) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<2, true>), grid, dim3(64), 0, s, p, sync);
-      else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<2, false>), grid, dim3(64), 0, s, p, sync);
-    }
+    if (B <= 16) launch_bwd_mp<1>(proto, grid, s, p, sync);
+    else launch_bwd_mp<2>(proto, grid, s, p, sync);
     BIGDL_CHECK_LAUNCH();
   }
   if (lstm_persist_ok(B, H)) {

@@ -2185,6 +2185,26 @@ def _rnn_sync(device):
     return buf[2 * i:2 * i + 2]
 
 
+_RNN_XG = {}
+
+
+def _rnn_xg(device):
+    """Granule exchange slots of the resident-weight LSTM kernels' barrier-free hand-off
+    (BIGDL_RNN_PERSIST=4/5): [2][B ≤ 32][2H ≤ 512] 8-byte granules, one per device (launches on a
+    stream are ordered; each zeroes the part it uses first)."""
+    buf = _RNN_XG.get(device)
+    if buf is None:
+        buf = _RNN_XG[device] = torch.zeros(2 * 32 * 512, dtype=torch.int64, device=device)
+    return buf
+
+
+def rnn_sync_errors(device) -> int:
+    """Error words raised by the resident-weight LSTM kernels (a tile that gave up waiting) since
+    the ring was created: 0 when every hand-off completed (host sync)."""
+    ent = _RNN_SYNC.get(torch.device(device))
+    return 0 if ent is None else int(ent[0][1::2].ne(0).sum())
+
+
 def lstm_seq_forward(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
     """Whole-sequence fused LSTM forward (bigdl_lstm_seq_fwd): x2 [B][T][4H], out [B][T][H]; training
     saves cs / tcs [T][B][H], acts [T][B][4H] (fp32), inference ping-pongs c through cbuf [2][B][H]."""
@@ -2193,14 +2213,15 @@ def lstm_seq_forward(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
     assert _dense_bf16(x2, h0, c0, U, out, cs, acts, tcs, cbuf) and tuple(out.shape) == (B, T, H), "lstm_seq_forward"
     check(_lib().bigdl_lstm_seq_fwd(ptr(x2), C.c_int(1 if x2.dtype == _f32 else 0), ptr(h0), ptr(c0), ptr(U), ptr(out),
                                     ptr(cs), ptr(acts), ptr(tcs), ptr(cbuf), C.c_int(B), C.c_int(T), C.c_int(H),
-                                    ptr(_rnn_sync(x2.device)), _s()), "lstm_seq_fwd")
+                                    ptr(_rnn_sync(x2.device)), ptr(_rnn_xg(x2.device)), _s()), "lstm_seq_fwd")
 
 
 def lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc):
     B, T, H = gy.shape
     assert _dense_bf16(gy, Ut, acts, tcs, cs, c0, DG, gc), "lstm_seq_backward"
     check(_lib().bigdl_lstm_seq_bwd(ptr(gy), ptr(Ut), ptr(acts), ptr(tcs), ptr(cs), ptr(c0), ptr(DG), ptr(gc),
-                                    C.c_int(B), C.c_int(T), C.c_int(H), ptr(_rnn_sync(gy.device)), _s()),
+                                    C.c_int(B), C.c_int(T), C.c_int(H), ptr(_rnn_sync(gy.device)),
+                                    ptr(_rnn_xg(gy.device)), _s()),
           "lstm_seq_bwd")
 
 

@@ -12,6 +12,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _partials_stats():
+    """Bit-exact comparisons: per-tile statistics partials (atomic accumulation order varies)."""
+    from bigdl.utils import config
+    prev = config.get_property("bigdl.bn.atomicStats")
+    config.set_property("bigdl.bn.atomicStats", False)
+    yield
+    config.set_property("bigdl.bn.atomicStats", prev)
+
+
 def _run(model, x, gy, prologue):
     from bigdl.utils import config
     config.set_property("bigdl.fusion.bnprologue", prologue)

@@ -451,8 +451,12 @@ def test_block_tail_bn_backward_fused_into_next_dgrad():
     d, ref = (ga.float() - gb.float()).abs(), gb.float().abs()
     assert float(d.max()) <= 2e-2 * float(ref.max()) + 5e-2, (float(d.max()), float(ref.max()))
     assert float((d > 5e-2 + 5e-2 * ref).float().mean()) < 1e-3
+    # parameter gradients to the scale of each tensor (a conv bias feeding a training BN has an
+    # exactly-zero true gradient: both paths hold rounding noise there, skipped by the scale floor)
     for u, v in zip(a.parameters()[1], b.parameters()[1]):
-        torch.testing.assert_close(u.float(), v.float(), rtol=5e-2, atol=5e-2)
+        scale = float(v.float().abs().max())
+        if scale > 1e-3:
+            assert float((u.float() - v.float()).abs().max()) <= 1e-2 * scale + 1e-2, scale
 
 
 @pytest.mark.parametrize("case", [(8, 64, 14, 14, 128, 3, 3, 1, 1), (4, 64, 28, 28, 256, 1, 1, 1, 0),

@@ -122,6 +122,7 @@ def test_atomic_bn_statistics_match_partials_path(name):
     base = Sequential().add(copy.deepcopy(ba)).add(copy.deepcopy(bb))
     g = torch.Generator().manual_seed(23)
     out = {}
+    prev = config.get_property("bigdl.bn.atomicStats")
     for atomic in (False, True):
         config.set_property("bigdl.bn.atomicStats", atomic)
         try:
@@ -151,7 +152,7 @@ def test_atomic_bn_statistics_match_partials_path(name):
                             if not (nm.endswith(".bias") and "Convolution" in nm)], ys,
                            [torch.cat([b.runningMean, b.runningVar]).cpu() for b in bns])
         finally:
-            config.set_property("bigdl.bn.atomicStats", True)
+            config.set_property("bigdl.bn.atomicStats", prev)
     (ga, ya, ra), (gb, yb, rb) = out[False], out[True]
     for (y0, gx0), (y1, gx1) in zip(ya, yb):
         assert _cos(y1, y0) > 0.999 and _cos(gx1, gx0) > 0.995

@@ -1,7 +1,8 @@
 """Persistent whole-sequence LSTM kernels (both opt-in; the per-step launches are faster at the PTB
 shape, profiles/r3_ptb_persist_ab.txt) — the resident-weight multi-workgroup kernels
 (k_lstm_seq_fwd_mp / k_lstm_seq_bwd_mp, BIGDL_RNN_PERSIST=2: U slices in registers, grid barrier per
-step, both exchange protocols) and the single-workgroup ones (k_lstm_seq_fwd_p / k_lstm_seq_bwd_p, BIGDL_RNN_PERSIST=1: h / dg_{t+1} in an
+step, both exchange protocols; =3 the same confined to one XCD; =4 / =5 the barrier-free granule
+hand-off, spread over the XCDs / confined to one) and the single-workgroup ones (k_lstm_seq_fwd_p / k_lstm_seq_bwd_p, BIGDL_RNN_PERSIST=1: h / dg_{t+1} in an
 LDS double buffer) — one launch per layer-direction, c / dc in registers, against the per-step
 launches of the same cell (BIGDL_RNN_PERSIST=0) and the fp32 host LSTM (``Recurrent.scala:283-400``,
 ``LSTM.scala:124-187``): outputs, input gradients and parameter gradients at the PTB shape
@@ -28,7 +29,7 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("mode", ["2", "2sc0", "3", "1"])
+@pytest.mark.parametrize("mode", ["2", "2sc0", "3", "4", "5", "1"])
 @pytest.mark.parametrize("B,T,IN,H", [(20, 20, 200, 200), (12, 7, 64, 48), (32, 5, 96, 256), (3, 33, 16, 8)])
 def test_persistent_lstm_matches_step_path_and_host(B, T, IN, H, mode):
     from bigdl.nn import LSTM, Recurrent
@@ -44,6 +45,8 @@ def test_persistent_lstm_matches_step_path_and_host(B, T, IN, H, mode):
         os.environ["BIGDL_RNN_PERSIST"] = mode[0]
         os.environ["BIGDL_RNN_MP_SYNC"] = "0" if mode.endswith("sc0") else "1"
         yp, gip, pp = _run(gpu, x.to(dev), gy.to(dev))
+        from bigdl.ops.native_ops import rnn_sync_errors
+        assert rnn_sync_errors(dev) == 0, "a resident-weight tile gave up waiting"
         os.environ["BIGDL_RNN_PERSIST"] = "0"
         ys, gis, ps = _run(gpu, x.to(dev), gy.to(dev))
     finally:
