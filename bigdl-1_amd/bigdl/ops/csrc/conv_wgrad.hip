@@ -54,6 +54,13 @@ struct WgradParams {
   // (same layout), dcoef [3][K]: the kernel uses A·g' + B·dy2 + Cc (the BN input gradient)
   const bf16_t* dy2;
   const float* dcoef;
+  // measurement knob only (BIGDL_DEBUG_WGRAD_NO_ATOMICS=1): skip the split-K atomic epilogue, which
+  // leaves dW WRONG — an upper bound of what a cheaper cross-split reduction could save
+  int skip_epi;
+  // 1: the split-K partial tile is staged in LDS (fp32) and added with wave-instructions covering
+  // 256 contiguous bytes of a dW row (the fast atomic shape, MI355X_MICROARCH.md 'Global float
+  // atomics'); 0: straight from the accumulators (four 64-B row segments per instruction)
+  int epi_lds;
 };
 
 constexpr int BP = 64;  // split granularity (pixels); the k-tile depth BPT is 64 or 32
@@ -281,6 +288,40 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
   }
 
   // epilogue: D[row = n][col = k]; lane holds rows (lane>>4)*4 + e of column lane&15
+  if (p.skip_epi) return;
+  if (p.epi_lds) {
+    // rows per pass: a multiple of 16 dividing TILE_N whose padded fp32 image fits the ring's LDS
+    constexpr int LDK = TILE_K + 16;  // +16 floats: the 4 rows of one write land on distinct banks
+    constexpr int LDS_F = (int)(sizeof(lds) / 4);
+    constexpr int ROWS = (TILE_N * LDK <= LDS_F) ? TILE_N : (TILE_N / 2 * LDK <= LDS_F) ? TILE_N / 2
+                         : (TILE_N / 4 * LDK <= LDS_F) ? TILE_N / 4 : 16;
+    static_assert(ROWS * LDK <= LDS_F && TILE_N % ROWS == 0 && ROWS % 16 == 0, "wgrad epilogue staging");
+    float* st = reinterpret_cast<float*>(&lds[0][0]);
+    __syncthreads();  // the last k-tile's fragment reads are done with the ring
+#pragma unroll
+    for (int pass = 0; pass < TILE_N / ROWS; ++pass) {
+#pragma unroll
+      for (int i = 0; i < TMN; ++i) {
+        const int rb = wave_n * (TILE_N / 2) + i * 16;  // this (wave, i)'s 16 rows
+        if (rb < pass * ROWS || rb >= (pass + 1) * ROWS) continue;
+#pragma unroll
+        for (int j = 0; j < TMK; ++j) {
+          const int c = wave_k * (TILE_K / 2) + j * 16 + (lane & 15);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) st[(rb - pass * ROWS + (lane >> 4) * 4 + e) * LDK + c] = acc[i][j][e];
+        }
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int idx = tid; idx < ROWS * TILE_K; idx += 256) {
+        const int r = idx / TILE_K, c = idx - r * TILE_K;
+        const int n = n0 + pass * ROWS + r, k = k0 + c;
+        if (n < p.K && k < p.Kg) atomicAdd(p.dw + (size_t)n * p.Kg + k, p.scale * st[r * LDK + c]);
+      }
+      if (pass + 1 < TILE_N / ROWS) __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TMN; ++i) {
 #pragma unroll
@@ -350,6 +391,10 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
   if ((size_t)Nb * H * W * ldx * 2 >= 0x80000000ull || (size_t)Nb * P * Q * ldk * 2 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   WgradParams p{};
+  static const int skip_env = [] { const char* ev = getenv("BIGDL_DEBUG_WGRAD_NO_ATOMICS"); return ev ? atoi(ev) : 0; }();
+  p.skip_epi = skip_env;
+  const char* epi_env = getenv("BIGDL_WGRAD_EPI");  // per launch: tests switch it in-process
+  p.epi_lds = epi_env ? atoi(epi_env) : 0;
   p.ldx = ldx; p.ldk = ldk;
   if ((dy2 != nullptr) != (dcoef != nullptr) || (dy2 && (c4 || groups != 1 || ((uintptr_t)dy2 & 15))))
     return (int)hipErrorInvalidValue;

@@ -236,6 +236,32 @@ def test_conv_backward(case):
     torch.testing.assert_close(gw, 0.5 + 2.0 * wr.grad, rtol=2e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("case", [(4, 64, 28, 28, 64, 3, 3, 1, 1), (2, 256, 14, 14, 1024, 1, 1, 1, 0),
+                                  (2, 128, 16, 16, 128, 3, 3, 2, 1), (2, 3, 32, 32, 64, 7, 7, 2, 3),
+                                  (3, 24, 9, 9, 40, 5, 5, 1, 2)])
+def test_conv_wgrad_lds_staged_epilogue(case, monkeypatch):
+    """BIGDL_WGRAD_EPI=1: split-K partial tiles staged in LDS and added with 256-B atomic
+    wave-instructions — same weight gradient as the register epilogue and the fp32 reference."""
+    N = _native()
+    n, c, h, w, k, r, s, st, pd = case
+    if k % 8:
+        pytest.skip("K % 8")
+    x = _cl(torch.randn(n, c, h, w, device=dev).bfloat16())
+    w4 = _cl(torch.randn(k, c, r, s, device=dev).bfloat16() * 0.1)
+    wr = w4.float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float(), wr, None, (st, st), (pd, pd))
+    gy = _cl(torch.randn_like(yr).bfloat16())
+    yr.backward(gy.float())
+    out = {}
+    for epi in ("0", "1"):
+        monkeypatch.setenv("BIGDL_WGRAD_EPI", epi)
+        gw = torch.zeros(k, r, s, c, device=dev).permute(0, 3, 1, 2)
+        N.conv2d_backward(gy, x, w4, (st, st), (pd, pd), (1, 1), 1, False, gw, None, 1.0)
+        out[epi] = gw.clone()
+    torch.testing.assert_close(out["1"], wr.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(out["1"], out["0"], rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_lstm_cell_kernels(dtype):
     from bigdl.ops import reference as R

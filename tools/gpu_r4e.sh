@@ -21,3 +21,7 @@ for v in 0 4 5; do
   BIGDL_RNN_PERSIST=$v timeout -k 10 300 python tools/bench_configs.py --config ptb --steps 20 --warmup 5 > gpurun_out/r4e/ptb_p$v.log 2>&1 || { tail -30 gpurun_out/r4e/ptb_p$v.log; exit 1; }
   tail -1 gpurun_out/r4e/ptb_p$v.log | cut -c1-160
 done
+for cfg in BIGDL_DEBUG_WGRAD_NO_ATOMICS=1 BIGDL_WGRAD_EPI=1 BIGDL_FUSION_BNPROLOGUE=2 BIGDL_CONV_X8_ILV=0; do
+  env $cfg timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 > gpurun_out/r4e/bench_$cfg.log 2>&1 || { tail -30 gpurun_out/r4e/bench_$cfg.log; exit 1; }
+  echo "$cfg"; tail -1 gpurun_out/r4e/bench_$cfg.log | cut -c1-200
+done
