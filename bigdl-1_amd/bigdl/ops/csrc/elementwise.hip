@@ -307,6 +307,55 @@ BIGDL_EXPORT int bigdl_adam_dev(float* w, const float* g, float* m, float* v, bf
 }
 
 // ------------------------------------------------------------------------------------------------
+// fused Adagrad (DL/optim/Adagrad.scala): g' = scale·g + wd·w ; s += g'² ;
+// w -= clr · g' / (sqrt(s) + 1e-10),  clr = lr / (1 + n·lr_decay) — one pass over (w, g, s) plus the
+// optional bf16 shadow, in place of five torch elementwise kernels.  dev_n (nullable): the
+// iteration count n read on the device (replay-safe under HIP-graph capture); else clr is given.
+__global__ void k_adagrad(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ sv,
+                          bf16_t* __restrict__ shadow, long long n4, float clr, float wd, float scale, int tail,
+                          const float* __restrict__ dev_n, float lr, float lr_decay) {
+  if (dev_n) clr = lr / (1.f + dev_n[0] * lr_decay);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < tail) {
+    const long long e = n4 * 4 + threadIdx.x;
+    const float gg = g[e] * scale + wd * w[e];
+    const float ss = sv[e] + gg * gg;
+    sv[e] = ss;
+    const float nw = w[e] - clr * gg / (sqrtf(ss) + 1e-10f);
+    w[e] = nw;
+    if (shadow) shadow[e] = f2bf(nw);
+  }
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 W = reinterpret_cast<float4*>(w)[i];
+    const float4 G = reinterpret_cast<const float4*>(g)[i];
+    const float4 S = reinterpret_cast<float4*>(sv)[i];
+    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w}, sq[4] = {S.x, S.y, S.z, S.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gg = gv[k] * scale + wd * wv[k];
+      sq[k] += gg * gg;
+      wv[k] -= clr * gg / (sqrtf(sq[k]) + 1e-10f);
+    }
+    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    reinterpret_cast<float4*>(sv)[i] = make_float4(sq[0], sq[1], sq[2], sq[3]);
+    if (shadow) {
+      const uint32_t lo = (uint32_t)f2bf(wv[0]) | ((uint32_t)f2bf(wv[1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(wv[2]) | ((uint32_t)f2bf(wv[3]) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
+    }
+  }
+}
+
+BIGDL_EXPORT int bigdl_adagrad(float* w, const float* g, float* sv, bf16_t* shadow, long long n, float clr,
+                               const float* dev_n, float lr, float lr_decay, float wd, float scale, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adagrad, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, sv, shadow, n4, clr,
+                     wd, scale, (int)(n & 3), dev_n, lr, lr_decay);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Reference wire format (K23, FP16CompressedTensor.scala:43-277): fp32 → bf16 by truncation (the
 // top 16 bits, no rounding), written straight into the reduce-scatter wire buffer — one pass in
 // place of the int32 view / shift / narrow temporaries of the torch formulation.

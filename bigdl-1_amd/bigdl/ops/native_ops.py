@@ -1476,6 +1476,23 @@ def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_dec
     return w
 
 
+@register("adagrad_step")
+def adagrad_step(w, g, s, lr, lr_decay, n, weight_decay=0.0, grad_scale=1.0, shadow=None, dev_n=None):
+    """Fused Adagrad update (bigdl_adagrad); ``dev_n`` (fp32 [1] on the device, the iteration count
+    before this step) makes it replay-safe under HIP-graph capture, else ``n`` (host) is used."""
+    numel = w.numel()
+    if w.dtype != _f32 or g.dtype != _f32 or s.dtype != _f32 or not _vec_ok(w, g, s, n=numel):
+        return NotImplemented
+    if dev_n is not None and not (dev_n.is_cuda and dev_n.dtype == _f32):
+        return NotImplemented
+    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
+        return NotImplemented
+    clr = lr / (1 + n * lr_decay)
+    check(_lib().bigdl_adagrad(ptr(w), ptr(g), ptr(s), ptr(shadow), _ll(numel), _f(clr), ptr(dev_n), _f(lr),
+                               _f(lr_decay), _f(weight_decay), _f(grad_scale), _s()), "adagrad")
+    return w
+
+
 # ------------------------------------------------------------------------------------------------ LSTM
 def _row_view(t, rows, cols):
     """(row stride) of a 2-D view with unit column stride, else None."""

@@ -533,11 +533,26 @@ class Adagrad(OptimMethod):
 
     def optimize(self, feval, x):
         fx, g = feval(x)
-        g = g * self.grad_scale
         n = self.state.get("evalCounter", 0)
+        s = self._state_tensor("paramVariance", x)
+        if x.is_cuda and ops.native_has("adagrad_step"):
+            # one fused pass (k_adagrad) over w, g, the accumulator and the bf16 shadow
+            nt = None
+            if getattr(self, "_graph_mode", False):
+                nt = self.state.get("_dev_n")
+                if not isinstance(nt, torch.Tensor) or nt.device != x.device:
+                    nt = torch.full((1,), float(n), device=x.device)
+                    self.state["_dev_n"] = nt
+            r = ops.native_ops.adagrad_step(x, g, s, self.learningRate, self.learningRateDecay, n, self.weightDecay,
+                                            self.grad_scale, self.shadow, dev_n=nt)
+            if r is not NotImplemented:
+                if nt is not None:
+                    nt.add_(1)
+                self.state["evalCounter"] = n + 1
+                return x, [fx]
+        g = g * self.grad_scale
         if self.weightDecay != 0:
             g = g + self.weightDecay * x
-        s = self._state_tensor("paramVariance", x)
         s.addcmul_(g, g)
         if getattr(self, "_graph_mode", False):
             # replay-safe: the iteration counter lives on the device and the decayed rate is a tensor

@@ -166,6 +166,31 @@ def test_adam():
     torch.testing.assert_close(w, w2, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("graph_counter", [False, True])
+def test_adagrad_fused_matches_optim_method(graph_counter):
+    """k_adagrad (one pass over w, g, the accumulator and the bf16 shadow) against the torch form
+    of Adagrad.optimize (DL/optim/Adagrad.scala), with weight decay and a gradient scale, host or
+    device iteration counter."""
+    N = _native()
+    n = 1003  # a tail past the float4 body
+    w = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    s = torch.zeros(n, device=dev)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    w2, s2 = w.clone(), s.clone()
+    lr, dec, wd, sc = 0.01, 0.001, 1e-3, 0.5
+    nt = torch.zeros(1, device=dev)
+    for it in range(3):
+        N.adagrad_step(w, g, s, lr, dec, it, wd, sc, shadow, dev_n=nt if graph_counter else None)
+        nt.add_(1)
+        gg = g * sc + wd * w2
+        s2.addcmul_(gg, gg)
+        w2.addcdiv_(gg, s2.sqrt().add_(1e-10), value=-lr / (1 + it * dec))
+    torch.testing.assert_close(w, w2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s, s2, rtol=1e-5, atol=1e-6)
+    assert torch.equal(shadow, w.bfloat16())
+
+
 def test_layers_use_native_path():
     """Spatial BN + ReLU layers on bf16 NHWC activations go through the native kernels."""
     _native()
