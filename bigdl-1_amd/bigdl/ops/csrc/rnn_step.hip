@@ -959,6 +959,307 @@ __global__ void __launch_bounds__(64) k_lstm_seq_bwd_mp(LstmSeqP p, int* sync) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Granule hand-off with FOUR waves per 16-unit tile (BIGDL_RNN_PERSIST=6 / 7): the k-chunks of the
+// recurrent product are dealt round-robin to the waves (wave w: kc ≡ w mod 4), so each wave holds a
+// quarter of the tile's weight slice and sweeps a quarter of the exchanged granules — the per-step
+// poll + load + MFMA chain, which is the step's latency, is ~4× shorter.  The partial accumulators
+// meet in LDS; wave 0 runs the cell and publishes the tile's granules.  A wave whose bounded spin
+// expires raises the block's abort word (LDS) and the error word, and the whole block leaves at the
+// next barrier (no wave is left waiting at a barrier).
+constexpr int kGw = 4;  // waves per tile
+
+template <int NBT>
+__global__ void __launch_bounds__(64 * kGw) k_lstm_seq_fwd_gw(LstmSeqP p, int* sync) {
+  const int spread = p.spread > 0 ? p.spread : 1;
+  if (blockIdx.x % spread) return;
+  const int tile = blockIdx.x / spread;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int u0 = tile * 16;
+  const int j = u0 + fq * 4;
+  const bool jin = j < H;
+  const bool urow = u0 + fr < H;
+  const int KC = (H + 31) / 32;
+  constexpr int QC = kMpMaxKC / kGw;  // chunks per wave
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  __shared__ v4f red[kGw][NBT][4][64];
+  __shared__ int abort_flag;
+  if (threadIdx.x == 0) abort_flag = 0;
+  v8s wf[4][QC];
+  const bf16_t* ub = p.u + (long long)(urow ? u0 + fr : 0) * H;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < QC; ++q) {
+      const int kc = q * kGw + w, k = kc * 32 + fq * 8;
+      wf[g][q] = (kc < KC && k < H && urow) ? *reinterpret_cast<const v8s*>(ub + (long long)g * H * H + k) : zero;
+    }
+  float c[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int m = bt * 16 + fr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[bt][e] = (w == 0 && p.c0 && m < B && jin) ? p.c0[(long long)m * H + j + e] : 0.f;
+  }
+  int* err = sync + 1;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    uint2 xr[NBT][4];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[bt][g] = (w == 0 && !p.x_f32 && m < B && jin)
+                        ? *reinterpret_cast<const uint2*>((const bf16_t*)p.x2 + ((long long)m * T + t) * G + g * H + j)
+                        : make_uint2(0u, 0u);
+    }
+    const unsigned long long* gsl = p.xg + (size_t)((t - 1) & 1) * B * (H / 2);
+    v4f acc[NBT][4];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[bt][g] = v4f{0.f, 0.f, 0.f, 0.f};
+    bool failed = false;
+#pragma unroll
+    for (int q = 0; q < QC; ++q) {
+      const int kc = q * kGw + w, k = kc * 32 + fq * 8;
+      const bool kin = kc < KC && k < H;
+      if (!kin) continue;  // wave-uniform
+      v8s hf[NBT];
+      if (t > 0) {
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int bt = 0; bt < NBT; ++bt) {
+            const int m = bt * 16 + fr;
+            hf[bt] = zero;
+            if (m < B) ok &= gget8(gsl + (size_t)m * (H / 2) + k / 2, (unsigned)t, hf[bt]);
+          }
+          if (__all(ok)) break;
+          if (spins > kGranSpin) { failed = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      } else {
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) {
+          const int m = bt * 16 + fr;
+          hf[bt] = m < B ? *reinterpret_cast<const v8s*>(p.h0 + (long long)m * H + k) : zero;
+        }
+      }
+      if (failed) break;
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[bt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[g][q], hf[bt], acc[bt][g], 0, 0, 0);
+    }
+    if (failed && lane == 0) {
+      abort_flag = 1;
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (w > 0) {
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) red[w][bt][g][lane] = acc[bt][g];
+    }
+    __syncthreads();
+    if (abort_flag) return;  // block-uniform after the barrier
+    if (w == 0) {
+#pragma unroll
+      for (int v = 1; v < kGw; ++v)
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[bt][g] += red[v][bt][g][lane];
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        if (m >= B || !jin) continue;
+        float xg[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (p.x_f32) {
+            ld4(p.x2, 1, ((long long)m * T + t) * G + g * H + j, xg[g]);
+          } else {
+            xg[g][0] = __uint_as_float(xr[bt][g].x << 16);
+            xg[g][1] = __uint_as_float(xr[bt][g].x & 0xFFFF0000u);
+            xg[g][2] = __uint_as_float(xr[bt][g].y << 16);
+            xg[g][3] = __uint_as_float(xr[bt][g].y & 0xFFFF0000u);
+          }
+        }
+        float gi[4], gg[4], gf[4], go[4], h[4], tcv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gi[e] = sgm(xg[0][e] + acc[bt][0][e]);
+          gg[e] = tanhf(xg[1][e] + acc[bt][1][e]);
+          gf[e] = sgm(xg[2][e] + acc[bt][2][e]);
+          go[e] = sgm(xg[3][e] + acc[bt][3][e]);
+          c[bt][e] = gi[e] * gg[e] + gf[e] * c[bt][e];
+          tcv[e] = tanhf(c[bt][e]);
+          h[e] = go[e] * tcv[e];
+        }
+        if (t + 1 < T) gput(p.xg + (size_t)(t & 1) * B * (H / 2) + (size_t)m * (H / 2) + j / 2, (unsigned)(t + 1), h);
+        stb4(p.out + ((long long)m * T + t) * H + j, h);
+        const long long mh = ((long long)t * B + m) * H + j;
+        if (p.cs) {
+          stf4(p.cs + mh, c[bt]);
+          stf4(p.tcs + mh, tcv);
+          float* a = p.acts + ((long long)t * B + m) * G + j;
+          stf4(a, gi);
+          stf4(a + H, gg);
+          stf4(a + 2 * H, gf);
+          stf4(a + 3 * H, go);
+        }
+      }
+    }
+    __syncthreads();  // wave 0 is done with `red` before the next step's partials land
+  }
+  if (p.cbuf && w == 0) {
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m < B && jin) stf4(p.cbuf + (long long)((T - 1) & 1) * B * H + (long long)m * H + j, c[bt]);
+    }
+  }
+}
+
+template <int NBT>
+__global__ void __launch_bounds__(64 * kGw) k_lstm_seq_bwd_gw(LstmSeqP p, int* sync) {
+  const int spread = p.spread > 0 ? p.spread : 1;
+  if (blockIdx.x % spread) return;
+  const int tile = blockIdx.x / spread;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const int H = p.H, B = p.B, T = p.T, G = 4 * H;
+  const int u0 = tile * 16;
+  const int j = u0 + fq * 4;
+  const bool jin = j < H;
+  const bool urow = u0 + fr < H;
+  const int KC = (G + 31) / 32;
+  constexpr int QC = kMpMaxKCb / kGw;
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  __shared__ v4f red[kGw][NBT][64];
+  __shared__ int abort_flag;
+  if (threadIdx.x == 0) abort_flag = 0;
+  v8s wf[QC];
+  const bf16_t* ub = p.u + (long long)(urow ? u0 + fr : 0) * G;
+#pragma unroll
+  for (int q = 0; q < QC; ++q) {
+    const int kc = q * kGw + w, k = kc * 32 + fq * 8;
+    wf[q] = (kc < KC && k < G && urow) ? *reinterpret_cast<const v8s*>(ub + k) : zero;
+  }
+  float dc[NBT][4];
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dc[bt][e] = 0.f;
+  int* err = sync + 1;
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    float pre[NBT][7][4];  // gy, act i, g, f, o, tanh(c), c_prev (wave 0)
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (w == 0 && m < B && jin) {
+        ld4(p.gy, 0, ((long long)m * T + t) * H + j, pre[bt][0]);
+        const float* a = p.acts + ((long long)t * B + m) * G + j;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) ldf4(a + g * H, pre[bt][1 + g]);
+        ldf4(p.tcs + ((long long)t * B + m) * H + j, pre[bt][5]);
+        ldf4(t > 0 ? p.cs + ((long long)(t - 1) * B + m) * H + j : (p.c0 ? p.c0 + (long long)m * H + j : nullptr),
+             pre[bt][6]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 7; ++q) pre[bt][q][0] = pre[bt][q][1] = pre[bt][q][2] = pre[bt][q][3] = 0.f;
+      }
+    }
+    v4f acc[NBT];
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) acc[bt] = v4f{0.f, 0.f, 0.f, 0.f};
+    bool failed = false;
+    if (t + 1 < T) {
+      const unsigned long long* gsl = p.xg + (size_t)((t + 1) & 1) * B * (G / 2);
+      const unsigned ep = (unsigned)(T - 1 - t);
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int kc = q * kGw + w, k = kc * 32 + fq * 8;
+        if (!(kc < KC && k < G)) continue;  // wave-uniform
+        v8s gf[NBT];
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int bt = 0; bt < NBT; ++bt) {
+            const int m = bt * 16 + fr;
+            gf[bt] = zero;
+            if (m < B) ok &= gget8(gsl + (size_t)m * (G / 2) + k / 2, ep, gf[bt]);
+          }
+          if (__all(ok)) break;
+          if (spins > kGranSpin) { failed = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (failed) break;
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) acc[bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[q], gf[bt], acc[bt], 0, 0, 0);
+      }
+    }
+    if (failed && lane == 0) {
+      abort_flag = 1;
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (w > 0) {
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) red[w][bt][lane] = acc[bt];
+    }
+    __syncthreads();
+    if (abort_flag) return;
+    if (w == 0) {
+#pragma unroll
+      for (int v = 1; v < kGw; ++v)
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) acc[bt] += red[v][bt][lane];
+#pragma unroll
+      for (int bt = 0; bt < NBT; ++bt) {
+        const int m = bt * 16 + fr;
+        if (m >= B || !jin) continue;
+        float di[4], dgg[4], df[4], dout[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float i = pre[bt][1][e], g = pre[bt][2][e], f = pre[bt][3][e], o = pre[bt][4][e], tcv = pre[bt][5][e];
+          const float d_h = pre[bt][0][e] + acc[bt][e];
+          const float d_c = d_h * o * (1.f - tcv * tcv) + dc[bt][e];
+          di[e] = d_c * g * i * (1.f - i);
+          dgg[e] = d_c * i * (1.f - g * g);
+          df[e] = d_c * pre[bt][6][e] * f * (1.f - f);
+          dout[e] = d_h * tcv * o * (1.f - o);
+          dc[bt][e] = d_c * f;
+        }
+        if (t > 0) {
+          unsigned long long* gq = p.xg + (size_t)(t & 1) * B * (G / 2) + (size_t)m * (G / 2) + j / 2;
+          const unsigned ep = (unsigned)(T - t);
+          gput(gq, ep, di);
+          gput(gq + H / 2, ep, dgg);
+          gput(gq + H, ep, df);
+          gput(gq + 3 * H / 2, ep, dout);
+        }
+        bf16_t* o = p.dg + ((long long)m * T + t) * G + j;
+        stb4(o, di);
+        stb4(o + H, dgg);
+        stb4(o + 2 * H, df);
+        stb4(o + 3 * H, dout);
+      }
+    }
+    __syncthreads();
+  }
+  if (w == 0) {
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      const int m = bt * 16 + fr;
+      if (m < B && jin) stf4(p.gc + (long long)m * H + j, dc[bt]);
+    }
+  }
+}
+
 // Resident-weight multi-workgroup path: B ≤ 32, 8 ≤ H ≤ 256, H % 8 == 0, a sync word pair given.
 // OPT-IN (BIGDL_RNN_PERSIST=2).  Measured at the PTB shape (B 20, H 200, T 20, 2 layers) it is
 // SLOWER than one k_rnn_step launch per step — 1.34 (fence protocol) / 1.40 (scoped accesses) vs
@@ -978,33 +1279,36 @@ static int lstm_persist_mode() {  // read per whole-sequence call (tests switch 
 
 // BIGDL_RNN_PERSIST=2: the multi-workgroup kernels on ⌈H/16⌉ workgroups wherever they land, counter
 // barrier (protocol BIGDL_RNN_MP_SYNC 0/1); =3: the same tiles confined to one XCD (8 × tiles
-// workgroups, every 8th one works); =4 / =5: the granule protocol (SC = 2, no barrier), spread 1 / 8
+// workgroups, every 8th one works); =4 / =5: the granule protocol (SC = 2, no barrier), spread 1 / 8;
+// =6 / =7: the granule protocol with four waves per tile (k_lstm_seq_{fwd,bwd}_gw), spread 1 / 8
 static bool lstm_mp_ok(int B, int H, const int* sync, const void* xg) {
   const int m = lstm_persist_mode();
-  if (m < 2 || m > 5 || ((m == 4 || m == 5) && !xg)) return false;
+  if (m < 2 || m > 7 || (m >= 4 && !xg)) return false;
   return sync && B >= 1 && B <= 32 && H >= 8 && H <= kPersistMaxH && H % 8 == 0;
 }
 
 static int lstm_mp_spread() {
   const int m = lstm_persist_mode();
-  return (m == 3 || m == 5) ? 8 : 1;
+  return (m == 3 || m == 5 || m == 7) ? 8 : 1;
 }
 
 static int lstm_mp_proto() {
   const int m = lstm_persist_mode();
-  return (m == 4 || m == 5) ? 2 : (lstm_mp_sc() ? 1 : 0);
+  return m >= 6 ? 3 : (m == 4 || m == 5) ? 2 : (lstm_mp_sc() ? 1 : 0);
 }
 
 template <int NBT>
 static void launch_fwd_mp(int proto, dim3 grid, hipStream_t s, const LstmSeqP& p, int* sync) {
-  if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
+  if (proto == 3) hipLaunchKernelGGL((k_lstm_seq_fwd_gw<NBT>), grid, dim3(64 * kGw), 0, s, p, sync);
+  else if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
   else if (proto == 1) hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 1>), grid, dim3(64), 0, s, p, sync);
   else hipLaunchKernelGGL((k_lstm_seq_fwd_mp<NBT, 0>), grid, dim3(64), 0, s, p, sync);
 }
 
 template <int NBT>
 static void launch_bwd_mp(int proto, dim3 grid, hipStream_t s, const LstmSeqP& p, int* sync) {
-  if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
+  if (proto == 3) hipLaunchKernelGGL((k_lstm_seq_bwd_gw<NBT>), grid, dim3(64 * kGw), 0, s, p, sync);
+  else if (proto == 2) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 2>), grid, dim3(64), 0, s, p, sync);
   else if (proto == 1) hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 1>), grid, dim3(64), 0, s, p, sync);
   else hipLaunchKernelGGL((k_lstm_seq_bwd_mp<NBT, 0>), grid, dim3(64), 0, s, p, sync);
 }
@@ -1048,7 +1352,7 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
     p.xg = (unsigned long long*)xg;
     const int proto = lstm_mp_proto();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
-    if (e == hipSuccess && proto == 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (H / 2) * 8, s);
+    if (e == hipSuccess && proto >= 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (H / 2) * 8, s);
     if (e != hipSuccess) return (int)e;
     const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
     if (B <= 16) launch_fwd_mp<1>(proto, grid, s, p, sync);
@@ -1098,7 +1402,7 @@ BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float*
     p.xg = (unsigned long long*)xg;
     const int proto = lstm_mp_proto();
     hipError_t e = hipMemsetAsync(sync, 0, 2 * sizeof(int), s);
-    if (e == hipSuccess && proto == 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (2 * H) * 8, s);
+    if (e == hipSuccess && proto >= 2) e = hipMemsetAsync(xg, 0, (size_t)2 * B * (2 * H) * 8, s);
     if (e != hipSuccess) return (int)e;
     const dim3 grid((unsigned)((H + 15) / 16 * p.spread));
     if (B <= 16) launch_bwd_mp<1>(proto, grid, s, p, sync);

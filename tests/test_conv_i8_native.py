@@ -6,6 +6,9 @@
   SpatialConvolution layer, and a whole quantized VGG16 forward.
 Reference: DL/nn/quantized/SpatialConvolution.scala:163-208 (ConvDataInit + MixPrecisionGEMM)."""
 import pytest
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
 
@@ -98,10 +101,18 @@ def test_quantized_vgg16_forward_vs_fp32():
     torch.manual_seed(0)
     m = Vgg_16(1000, has_dropout=False)
     m.evaluate()
-    x = torch.randn(2, 3, 224, 224)
+    x = torch.randn(4, 3, 224, 224)
+    # data-dependent init (tools/bench_configs.py:_lsuv): without it a random-init VGG16's log-probs
+    # are one image-independent vector and any comparison of them passes trivially
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from bench_configs import _lsuv
+    _lsuv(m, x)
     with torch.no_grad():
         ref = m.forward(x).float().clone()
     q = m.quantize().cuda()
     with torch.no_grad():
         yq = q.forward(x.cuda()).float().cpu()
-    assert _cos(yq, ref) > 0.99
+    # row-centred log-probabilities (= centred logits), image-dependent part
+    c = lambda t: (t - t.mean(1, keepdim=True)) - (t - t.mean(1, keepdim=True)).mean(0, keepdim=True)  # noqa: E731
+    assert float(c(ref).std()) > 0.1  # the logits do carry image-dependent signal
+    assert _cos(c(yq), c(ref)) > 0.99

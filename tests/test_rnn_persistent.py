@@ -29,7 +29,7 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("mode", ["2", "2sc0", "3", "4", "5", "1"])
+@pytest.mark.parametrize("mode", ["2", "2sc0", "3", "4", "5", "6", "7", "1"])
 @pytest.mark.parametrize("B,T,IN,H", [(20, 20, 200, 200), (12, 7, 64, 48), (32, 5, 96, 256), (3, 33, 16, 8)])
 def test_persistent_lstm_matches_step_path_and_host(B, T, IN, H, mode):
     from bigdl.nn import LSTM, Recurrent

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/r4e
 T="python -u -m pytest -q --timeout 120 --timeout-method thread"
 t() { local log=$1 lim=$2; shift 2; timeout -k 10 $lim $T "$@" > gpurun_out/r4e/$log 2>&1; local rc=$?
       tail -2 gpurun_out/r4e/$log; [ $rc -le 1 ] || exit $rc; }
-t tests_fix.log 300 tests/test_native_kernels.py tests/test_bn_prologue.py tests/test_resnet_block_parity.py tests/test_graph_adam.py
+t tests_fix.log 300 tests/test_native_kernels.py tests/test_bn_prologue.py tests/test_resnet_block_parity.py tests/test_graph_adam.py tests/test_conv_i8_native.py
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4e/st -o run -- python tools/stats_ab.py > gpurun_out/r4e/stats_ab.log 2>&1 || { tail -30 gpurun_out/r4e/stats_ab.log; exit 1; }
 grep '^{' gpurun_out/r4e/stats_ab.log
 db=$(find gpurun_out/r4e/st -name '*.db' | head -1)
@@ -17,7 +17,7 @@ tail -1 gpurun_out/r4e/bench.log | cut -c1-250
 timeout -k 10 400 python tools/bench_configs.py --config int8 --steps 10 --warmup 3 > gpurun_out/r4e/int8.log 2>&1 || { tail -30 gpurun_out/r4e/int8.log; exit 1; }
 tail -1 gpurun_out/r4e/int8.log
 t tests_rnn.log 400 tests/test_rnn_persistent.py
-for v in 0 4 5; do
+for v in 0 4 5 6 7; do
   BIGDL_RNN_PERSIST=$v timeout -k 10 300 python tools/bench_configs.py --config ptb --steps 20 --warmup 5 > gpurun_out/r4e/ptb_p$v.log 2>&1 || { tail -30 gpurun_out/r4e/ptb_p$v.log; exit 1; }
   tail -1 gpurun_out/r4e/ptb_p$v.log | cut -c1-160
 done
