@@ -1025,8 +1025,8 @@ __global__ void __launch_bounds__(64 * kGw) k_lstm_seq_fwd_gw(LstmSeqP p, int* s
 #pragma unroll
     for (int q = 0; q < QC; ++q) {
       const int kc = q * kGw + w, k = kc * 32 + fq * 8;
-      const bool kin = kc < KC && k < H;
-      if (!kin) continue;  // wave-uniform
+      if (kc >= KC) continue;  // wave-uniform; lanes past H (k ≥ H) feed zero fragments
+      const bool kin = k < H;
       v8s hf[NBT];
       if (t > 0) {
         for (unsigned spins = 0;; ++spins) {
@@ -1035,7 +1035,7 @@ __global__ void __launch_bounds__(64 * kGw) k_lstm_seq_fwd_gw(LstmSeqP p, int* s
           for (int bt = 0; bt < NBT; ++bt) {
             const int m = bt * 16 + fr;
             hf[bt] = zero;
-            if (m < B) ok &= gget8(gsl + (size_t)m * (H / 2) + k / 2, (unsigned)t, hf[bt]);
+            if (kin && m < B) ok &= gget8(gsl + (size_t)m * (H / 2) + k / 2, (unsigned)t, hf[bt]);
           }
           if (__all(ok)) break;
           if (spins > kGranSpin) { failed = true; break; }
@@ -1045,7 +1045,7 @@ __global__ void __launch_bounds__(64 * kGw) k_lstm_seq_fwd_gw(LstmSeqP p, int* s
 #pragma unroll
         for (int bt = 0; bt < NBT; ++bt) {
           const int m = bt * 16 + fr;
-          hf[bt] = m < B ? *reinterpret_cast<const v8s*>(p.h0 + (long long)m * H + k) : zero;
+          hf[bt] = (kin && m < B) ? *reinterpret_cast<const v8s*>(p.h0 + (long long)m * H + k) : zero;
         }
       }
       if (failed) break;
@@ -1184,7 +1184,8 @@ __global__ void __launch_bounds__(64 * kGw) k_lstm_seq_bwd_gw(LstmSeqP p, int* s
 #pragma unroll
       for (int q = 0; q < QC; ++q) {
         const int kc = q * kGw + w, k = kc * 32 + fq * 8;
-        if (!(kc < KC && k < G)) continue;  // wave-uniform
+        if (kc >= KC) continue;  // wave-uniform; lanes past 4H feed zero fragments
+        const bool kin = k < G;
         v8s gf[NBT];
         for (unsigned spins = 0;; ++spins) {
           bool ok = true;
@@ -1192,7 +1193,7 @@ __global__ void __launch_bounds__(64 * kGw) k_lstm_seq_bwd_gw(LstmSeqP p, int* s
           for (int bt = 0; bt < NBT; ++bt) {
             const int m = bt * 16 + fr;
             gf[bt] = zero;
-            if (m < B) ok &= gget8(gsl + (size_t)m * (G / 2) + k / 2, ep, gf[bt]);
+            if (kin && m < B) ok &= gget8(gsl + (size_t)m * (G / 2) + k / 2, ep, gf[bt]);
           }
           if (__all(ok)) break;
           if (spins > kGranSpin) { failed = true; break; }

@@ -359,8 +359,9 @@ def bench_transformer(args):
 
 def _lsuv(model, x):
     """Data-dependent init of a random-init plain Sequential (CPU, fp32, a small batch): layer by
-    layer, every conv / Linear output channel is shifted and scaled to zero mean and unit standard
-    deviation over the batch (bias ← (bias − μ)/σ, weight row ← row/σ).  A random-init VGG16 on
+    layer, every conv output channel is shifted and scaled to zero mean and unit standard deviation
+    over the batch and pixels (bias ← (bias − μ)/σ, weight row ← row/σ); a Linear is scaled to unit
+    output standard deviation as a whole.  A random-init VGG16 on
     random images otherwise ends in logits that are one image-independent vector (every image the
     same top-1), so an int8-vs-fp32 comparison of them measures nothing; centred, the logits carry
     image-dependent signal as a trained network's do."""
@@ -373,6 +374,10 @@ def _lsuv(model, x):
             if isinstance(m, (Linear, SpatialConvolution)) and getattr(m, "bias", None) is not None:
                 yc = y.float().transpose(0, 1).reshape(y.shape[1], -1)  # [channels][batch·pixels]
                 mu, sd = yc.mean(1), yc.std(1).clamp_min(1e-6)
+                if isinstance(m, Linear):
+                    # a few images give each FC output only a few samples: per-feature centring would
+                    # blow the weights up (cancelling W·x against a huge bias); scale globally
+                    mu, sd = torch.zeros_like(mu), torch.full_like(sd, float(yc.std()))
                 wt = m.weight  # [K][...] or the grouped [g][K/g][...] (g = 1 here)
                 lead = 2 if wt.dim() == 5 else 1
                 wt.div_(sd.view(*wt.shape[:lead], *([1] * (wt.dim() - lead))))
