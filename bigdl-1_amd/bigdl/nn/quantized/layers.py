@@ -11,6 +11,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ...utils import acc_float
+
 from ... import ops
 from ..abstractnn import TensorModule
 
@@ -148,13 +150,21 @@ class SpatialConvolution(_QuantizedBase):
         out_dt = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32
         g = self.nGroup
         cg, kg = C // g, self.nOutputPlane // g
+        # one activation scale per image (max|x| of the whole image / 127), as the reference's
+        # ConvDataInit quantises each batch element's input (quantized/SpatialConvolution.scala:
+        # 163-208) and as the int8 kernel does (ops/csrc/conv_i8.hip)
+        amax = acc_float(x).abs().amax(dim=(1, 2, 3))
+        inv = torch.where(amax > 0, 127.0 / amax, torch.zeros_like(amax)).repeat_interleave(P * Q)
         outs = []
         for gi in range(g):
             xs = x[:, gi * cg:(gi + 1) * cg]
             cols = F.unfold(xs, (kh, kw), dilation=(self.dilationH, self.dilationW),
                             stride=(self.strideH, self.strideW))  # [N, cg·kh·kw, L]
-            rows = cols.transpose(1, 2).reshape(N * P * Q, cg * kh * kw)
-            qa, sa = ops.quant_rows(rows.contiguous(), self.qweight.shape[1])
+            rows = acc_float(cols.transpose(1, 2).reshape(N * P * Q, cg * kh * kw))
+            kp = self.qweight.shape[1]
+            qa = torch.zeros((N * P * Q, kp), dtype=torch.int8, device=x.device)
+            qa[:, :cg * kh * kw] = torch.floor(rows * inv[:, None] + 0.5).clamp(-127, 127).to(torch.int8)
+            sa = (amax / 127.0).repeat_interleave(P * Q)
             bias = self.bias_f[gi * kg:(gi + 1) * kg] if self.bias_f is not None else None
             y = ops.gemm_i8(qa, sa, self.qweight[gi * kg:(gi + 1) * kg].contiguous(),
                             self.weight_scale[gi * kg:(gi + 1) * kg].contiguous(), bias, out_dtype=out_dt)
