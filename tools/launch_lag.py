@@ -13,13 +13,12 @@ def main():
     nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     c = sqlite3.connect(db)
     tabs = [r[0] for r in c.execute("select name from sqlite_master where type in ('table','view')")]
-    print("tables:", ", ".join(t for t in tabs if not t.startswith("sqlite")))
     kc = [r[1] for r in c.execute("pragma table_info(kernels)")]
     rc = [r[1] for r in c.execute("pragma table_info(regions)")] if "regions" in tabs else []
     print("kernels cols:", kc)
     print("regions cols:", rc)
-    kid = "correlation_id" if "correlation_id" in kc else None
-    rid = "correlation_id" if "correlation_id" in rc else None
+    kid = next((n for n in ("correlation_id", "corr_id") if n in kc), None)
+    rid = next((n for n in ("correlation_id", "corr_id") if n in rc), None)
     if not (kid and rid):
         print("no correlation ids; cannot pair launches")
         return
