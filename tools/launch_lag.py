@@ -23,7 +23,19 @@ def main():
         print("no correlation ids; cannot pair launches")
         return
     K = c.execute(f"select start, end, {kid}, name, {'queue_id' if 'queue_id' in kc else 'stream_id'} from kernels").fetchall()
-    R = {r[2]: r for r in c.execute(f"select start, end, {rid}, name from regions").fetchall()}
+    R = {}
+    for r in c.execute(f"select start, end, {rid}, name from regions").fetchall():
+        if "Launch" in r[3] or "launch" in r[3]:
+            R[r[2]] = r
+    # diagnostics: how a few kernels pair with their launch calls
+    for k in sorted(K, key=lambda k: k[0])[-5:]:
+        r = R.get(k[2])
+        print("sample kernel", k[2], k[3][:40], "start", k[0], "| launch", r[3][:30] if r else None,
+              r[0] if r else None, r[1] if r else None)
+    names = {}
+    for r in c.execute("select name from regions").fetchall():
+        names[r[0]] = names.get(r[0], 0) + 1
+    print("region names:", sorted(names.items(), key=lambda x: -x[1])[:12])
     tmax = max(k[1] for k in K)
     t0 = tmax - nsteps * step_ms * 1e6
     K = sorted((k for k in K if k[0] >= t0), key=lambda k: k[0])
