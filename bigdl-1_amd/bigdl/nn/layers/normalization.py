@@ -186,15 +186,7 @@ class BatchNormalization(TensorModule):
                 if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
                     coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
                 ps, self._pending_stats = self._pending_stats, None
-                # a fused block tail (ReLU(BN(x) + shortcut)) on the GPU also emits its output's ReLU
-                # mask as bits: the next block's dgrad epilogue reads 1/16 of the bytes of the output
-                bits = None
-                if (residual is not None and relu and x.is_cuda and x.dim() == 4 and C_ % 8 == 0
-                        and getattr(self, "_residual_mode", False)):
-                    n = x.numel() // 8
-                    bits = self._relu_bits
-                    if bits is None or bits.numel() != n or bits.device != x.device:
-                        bits = torch.empty(n, dtype=torch.uint8, device=x.device)
+                bits = self._tail_bits(x, relu, residual)
                 self._relu_bits = None
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     r = ops.native_ops.batchnorm_forward_train_partials(
@@ -217,6 +209,18 @@ class BatchNormalization(TensorModule):
             if relu:
                 y = torch.relu(y)
         return y.reshape(input.shape) if input.dim() == 1 else y
+
+    def _tail_bits(self, x, relu, residual):
+        """A fused block tail (ReLU(BN(x) + shortcut)) on the GPU also emits its output's ReLU mask
+        as bits: the next block's dgrad epilogue reads 1/16 of the bytes of the output."""
+        if not (residual is not None and relu and x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0
+                and getattr(self, "_residual_mode", False)):
+            return None
+        n = x.numel() // 8
+        bits = self._relu_bits
+        if bits is None or bits.numel() != n or bits.device != x.device:
+            bits = torch.empty(n, dtype=torch.uint8, device=x.device)
+        return bits
 
     def _lazy_grad_ok(self, input, x):
         """Return the input gradient deferred (a BNGrad) when the producing conv — the only consumer
@@ -271,6 +275,8 @@ class BatchNormalization(TensorModule):
         if coef is None or coef.numel() != 2 * C_ or coef.device != x.device:
             coef = self._coef = torch.empty(2 * C_, dtype=torch.float32, device=x.device)
         ps, self._pending_stats = self._pending_stats, None
+        bits = self._tail_bits(x, relu, residual) if impl is not R else None
+        self._relu_bits = None
         r = NotImplemented
         for m in ((impl, R) if impl is not R else (R,)):
             if m is not R and ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape) \
@@ -284,8 +290,10 @@ class BatchNormalization(TensorModule):
                 continue
             self._sync_allreduce(sums)
             r = m.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar, self.momentum,
-                                       self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef)
+                                       self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef,
+                                       bits_out=bits if m is not R else None)
             if r is not NotImplemented:
+                self._relu_bits = bits if m is not R else None
                 self._sync_path = "native" if m is not R else "reference"
                 self._last_input = x
                 break

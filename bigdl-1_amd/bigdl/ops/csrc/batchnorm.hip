@@ -957,12 +957,12 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
                                          const float* gamma, const float* beta, const float* in_bias,
                                          float* run_mean, float* run_var, float momentum, float eps,
                                          float* save_mean, float* save_invstd, const float* sums,
-                                         const float* kshift, float* coef, int relu, hipStream_t s) {
-  if (C % 8 || M <= 0 || count < 0) return (int)hipErrorInvalidValue;
+                                         const float* kshift, float* coef, int relu, void* bits, hipStream_t s) {
+  if (C % 8 || M <= 0 || count < 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift, sums,
                      1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
                      coef + C, count == 0 ? sums + 2 * C : nullptr);
-  launch_apply(x, res, y, M, C, coef, relu, nullptr, s);
+  launch_apply(x, res, y, M, C, coef, relu, bits, s);
   BIGDL_CHECK_LAUNCH();
 }
 

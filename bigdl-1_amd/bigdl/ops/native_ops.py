@@ -281,9 +281,10 @@ def bn_local_sums(x, shift, partial=None, G=0):
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
-                         residual=None, in_bias=None, coef_out=None):
+                         residual=None, in_bias=None, coef_out=None, bits_out=None):
     """Training BN from GLOBAL shifted sums over ``count`` rows (0: the all-reduced count at
-    ``sums[2C]``): (y, save_mean, save_invstd)."""
+    ``sums[2C]``): (y, save_mean, save_invstd).  ``bits_out`` (uint8 [M·C/8], with ``relu``): the
+    output's ReLU mask as bits for a block-tail consumer's dgrad epilogue."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -300,7 +301,8 @@ def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, runni
     check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
                                          ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum),
                                          _f(eps), ptr(mean), ptr(invstd), ptr(sums), ptr(shift), ptr(coef),
-                                         C.c_int(1 if relu else 0), _s()), "bn_fwd_train_sums")
+                                         C.c_int(1 if relu else 0), ptr(bits_out if relu else None), _s()),
+          "bn_fwd_train_sums")
     return y, mean, invstd
 
 

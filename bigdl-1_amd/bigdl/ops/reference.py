@@ -265,7 +265,7 @@ def bn_local_sums(x, shift, partial=None, G=0):
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
-                         residual=None, in_bias=None, coef_out=None):
+                         residual=None, in_bias=None, coef_out=None, bits_out=None):
     """Training BN from GLOBAL shifted sums over ``count`` rows (0: ``sums[2C]``)."""
     C = x.shape[1]
     dims, shape = _bn_dims(x)

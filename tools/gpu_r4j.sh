@@ -10,3 +10,9 @@ db=$(find /tmp/lagdb -name '*.db' | head -1)
 ms=$(python -c "import json; print([json.loads(l) for l in open('gpurun_out/r4j/lag.log') if l.startswith('{\"metric')][-1]['ms_per_step'])")
 python tools/launch_lag.py "$db" $ms 2 > gpurun_out/r4j/lag_summary.txt 2>&1
 head -50 gpurun_out/r4j/lag_summary.txt
+bash tools/gpu_r4k.sh || exit 1
+mkdir -p gpurun_out/r4j
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 --force-distri --syncbn > gpurun_out/r4j/bench_syncbn.log 2>&1 || { tail -30 gpurun_out/r4j/bench_syncbn.log; exit 1; }
+tail -1 gpurun_out/r4j/bench_syncbn.log | cut -c1-220
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 > gpurun_out/r4j/bench_local.log 2>&1 || { tail -30 gpurun_out/r4j/bench_local.log; exit 1; }
+tail -1 gpurun_out/r4j/bench_local.log | cut -c1-220
