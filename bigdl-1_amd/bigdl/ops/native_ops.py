@@ -1382,6 +1382,11 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
         return gi
     gi = None
+    wg_done = False
+    if gw_acc is not None and scale != 0 and _WG["on"] and _WG_FIRST[0]:
+        # fork the weight gradient BEFORE the data gradient: the side stream's wait then covers only
+        # what produced gy / x, so the wgrad runs beside this layer's dgrad instead of after it
+        wg_done = _wgrad_async_or_inline(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
     if need_input:
         res_done = False
         if stride == (1, 1) or tuple(stride) == (1, 1):
@@ -1398,20 +1403,30 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             gi = R_.conv2d_backward(gy, x, w4, stride, pad, dilation, groups, True, None, None, 0.0)
         if residual is not None and not res_done:
             gi = R_.as_dense(gi) + R_.as_dense(residual)
-    if gw_acc is not None and scale != 0:
-        side = _wgrad_side_stream(gy) if _WG["on"] else None
-        if side is None:
-            _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
-        else:
-            with torch.cuda.stream(side):
-                xx = _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
-            # the caching allocator must not hand these blocks to the compute stream while the
-            # side stream still reads them
-            for t in (x, xx, gy):
-                t.record_stream(side)
+    if gw_acc is not None and scale != 0 and not wg_done:
+        _wgrad_async_or_inline(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
     if gb_acc is not None and scale != 0:
         gb_acc.add_(gy.float().sum((0, 2, 3)), alpha=scale)
     return gi
+
+
+#: BIGDL_WGRAD_FIRST=1: conv2d_backward forks its weight gradient onto the side stream before the
+#: data gradient is enqueued (A/B knob; 0 = after, the round-3 order)
+_WG_FIRST = [__import__("os").environ.get("BIGDL_WGRAD_FIRST", "0") == "1"]
+
+
+def _wgrad_async_or_inline(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot) -> bool:
+    side = _wgrad_side_stream(gy) if _WG["on"] else None
+    if side is None:
+        _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
+    else:
+        with torch.cuda.stream(side):
+            xx = _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot)
+        # the caching allocator must not hand these blocks to the compute stream while the side
+        # stream still reads them
+        for t in (x, xx, gy):
+            t.record_stream(side)
+    return True
 
 
 # ------------------------------------------------------------------------------------------------ optimizers

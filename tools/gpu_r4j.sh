@@ -16,3 +16,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 --force-d
 tail -1 gpurun_out/r4j/bench_syncbn.log | cut -c1-220
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 > gpurun_out/r4j/bench_local.log 2>&1 || { tail -30 gpurun_out/r4j/bench_local.log; exit 1; }
 tail -1 gpurun_out/r4j/bench_local.log | cut -c1-220
+BIGDL_WGRAD_FIRST=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --fp32-steps 0 > gpurun_out/r4j/bench_wgfirst.log 2>&1 || { tail -30 gpurun_out/r4j/bench_wgfirst.log; exit 1; }
+echo wgrad-first; tail -1 gpurun_out/r4j/bench_wgfirst.log | cut -c1-220
