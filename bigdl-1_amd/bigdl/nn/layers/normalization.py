@@ -129,8 +129,19 @@ class BatchNormalization(TensorModule):
         statistics into — ``kind`` "fwd": the producing conv's Σ(y−K), Σ(y−K)²; "bwd": the consuming
         conv's dgrad Σg', Σg'·(x − μ) — consumed (and re-zeroed) by the one-launch finalize+apply.
         None when the per-tile partials path is required (SyncBN, bigdl.deterministic, off)."""
-        if (device.type != "cuda" or self._sync_active() or not config.get_property("bigdl.bn.atomicStats")
-                or config.get_property("bigdl.deterministic")):
+        if device.type != "cuda" or self._sync_active() or config.get_property("bigdl.deterministic"):
+            return None
+        rep = int(config.get_property("bigdl.bn.statReplicas"))
+        if rep > 0 and not config.get_property("bigdl.bn.atomicStats"):
+            # replicated form: [2][R][C] zeroed, tile tm adds into replica tm % R; the BN's finalize
+            # reads the R rows and clears them (batchnorm.hip reduce_partials rezero)
+            rep = min(rep, 512)
+            attr = "_rep_" + kind
+            buf = self.__dict__.get(attr)
+            if buf is None or buf.numel() != 2 * rep * C or buf.device != device:
+                buf = self.__dict__[attr] = torch.zeros(2 * rep * C, dtype=torch.float32, device=device)
+            return buf, rep
+        if not config.get_property("bigdl.bn.atomicStats"):
             return None
         attr = "_sums_" + kind
         buf = self.__dict__.get(attr)
@@ -138,12 +149,16 @@ class BatchNormalization(TensorModule):
             buf = self.__dict__[attr] = torch.zeros(2 * C + 1, dtype=torch.float32, device=device)
         return buf
 
-    @staticmethod
-    def _drop_sums(pending, g_index):
+    def _drop_sums(self, pending, g_index):
         """A conv left atomically accumulated sums this BN is not consuming: clear them, or the next
         producer would add onto stale values."""
-        if pending is not None and pending[g_index] == 0:
+        if pending is not None and (pending[g_index] == 0 or self._is_rep(pending[g_index - 1])):
             pending[g_index - 1].zero_()
+
+    def _is_rep(self, part):
+        """``part`` is one of this BN's replicated atomic-statistics buffers (cleared by the finalize
+        that reads it)."""
+        return part is not None and any(part is self.__dict__.get(a) for a in ("_rep_fwd", "_rep_bwd"))
 
     def _in_bias(self):
         p = self._bias_producer
@@ -191,7 +206,8 @@ class BatchNormalization(TensorModule):
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
-                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits)
+                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits,
+                        rezero=self._is_rep(ps[2]))
                 if r is NotImplemented:
                     self._drop_sums(ps, 3)
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
@@ -335,7 +351,7 @@ class BatchNormalization(TensorModule):
                     gg_acc=self.gradWeight if (acc and self.affine) else None,
                     gb_acc=self.gradBias if (acc and self.affine) else None,
                     scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs,
-                    lazy=self._lazy_grad_ok(input, x))
+                    lazy=self._lazy_grad_ok(input, x), rezero=self._is_rep(pg[1]))
                 if gi is not NotImplemented:
                     if gi is not None and input.dim() == 1:
                         gi = gi.reshape(input.shape)

@@ -100,7 +100,8 @@ constexpr int kFinRG = 8;
 
 template <typename T>
 __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, int G, int C, int c0,
-                                                double (*lds)[2][33], double& outA, double& outB) {
+                                                double (*lds)[2][33], double& outA, double& outB,
+                                                float* rezero = nullptr) {
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = c0 + tx;
   double a = 0.0, b = 0.0;
@@ -111,6 +112,14 @@ __device__ __forceinline__ void reduce_partials(const T* __restrict__ partial, i
       a += partial[(size_t)i * C + c];
       b += partial[(size_t)(G + i) * C + c];
     }
+    // replicated atomic statistics: this block owns columns c0..c0+31 — clear what it just read
+    // for the next accumulation (each thread clears exactly the elements it loaded)
+    asm volatile("" ::: "memory");  // the clears below alias `partial` (declared __restrict__)
+    if (rezero)
+      for (i = ty; i < G; i += kFinRG) {
+        rezero[(size_t)i * C + c] = 0.f;
+        rezero[(size_t)(G + i) * C + c] = 0.f;
+      }
   }
   lds[ty][0][tx] = a;
   lds[ty][1][tx] = b;
@@ -138,12 +147,14 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_finalize(const bf16_t* __res
                                                       float* run_mean, float* __restrict__ run_var,
                                                       float momentum, float eps, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
-                                                      float* __restrict__ shift, const float* __restrict__ dM = nullptr) {
+                                                      float* __restrict__ shift, const float* __restrict__ dM = nullptr,
+                                                      float* rezero = nullptr) {
   // dM: the row count read from device memory (SyncBN: the all-reduced count travels in the sums
-  // buffer, so the host never waits for it); else M
+  // buffer, so the host never waits for it); else M.  rezero: clear the partials after reading them
+  // (replicated atomic statistics, ConvParams::stats_atomic = R)
   __shared__ double lds[kFinRG][2][33];
   double s, q;
-  reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q);
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, s, q, rezero);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
   // partials are shifted by the first row (standalone stats pass), by ``kshift`` (conv epilogue
@@ -401,16 +412,16 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
                                              float* run_mean, float* run_var, float momentum, float eps,
                                              float* save_mean, float* save_invstd, const float* partial, int G,
                                              const float* kshift, float* coef, int relu, float* scratch, void* bits,
-                                             hipStream_t s) {
-  if (C % 8 || M <= 0 || G <= 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
-  if (maybe_fold(partial, G, C, scratch, s))
+                                             int rezero, hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0 || (bits && !relu) || (rezero && G > 512)) return (int)hipErrorInvalidValue;
+  if (!rezero && maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                        (const double*)scratch, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                        save_invstd, coef, coef + C);
   else
     hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                        partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd,
-                       coef, coef + C);
+                       coef, coef + C, nullptr, rezero ? const_cast<float*>(partial) : nullptr);
   launch_apply(x, res, y, M, C, coef, relu, bits, s);
   BIGDL_CHECK_LAUNCH();
 }
@@ -499,10 +510,11 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __rest
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ ggamma, float* __restrict__ gbeta,
                                                           float gscale, float* __restrict__ cbias, float cbscale,
-                                                          float* __restrict__ coef, const float* __restrict__ dM = nullptr) {
+                                                          float* __restrict__ coef, const float* __restrict__ dM = nullptr,
+                                                          float* rezero = nullptr) {
   __shared__ double lds[kFinRG][2][33];
   double ad, bd;
-  reduce_partials(partial, G, C, blockIdx.x * 32, lds, ad, bd);
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, ad, bd, rezero);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
   const float a = (float)ad, b = (float)bd;
@@ -611,14 +623,15 @@ BIGDL_EXPORT int bigdl_bn_bwd(const void* gy, const void* x, const void* y, void
 BIGDL_EXPORT int bigdl_bn_bwd_partials(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
                                        const float* mean, const float* invstd, float* ggamma, float* gbeta,
                                        float gscale, float* cbias, float cbscale, const float* partial, int G,
-                                       float* coef, float* scratch, hipStream_t s) {
-  if (C % 8 || M <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  if (maybe_fold(partial, G, C, scratch, s))
+                                       float* coef, float* scratch, int rezero, hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0 || (rezero && G > 512)) return (int)hipErrorInvalidValue;
+  if (!rezero && maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_bwd_finalize<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const double*)scratch, G, M,
                        C, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   else
     hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, M, C, gamma, mean,
-                       invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
+                       invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, nullptr,
+                       rezero ? const_cast<float*>(partial) : nullptr);
   if (gx) {
     int grid = apply_grid(M, C);
     hipLaunchKernelGGL((apply_unroll1() ? k_bn_bwd_apply<false, false, 1> : k_bn_bwd_apply<false, false, 4>), dim3(grid), dim3(256), 0, s, (const bf16_t*)gm,

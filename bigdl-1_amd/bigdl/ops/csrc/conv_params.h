@@ -78,9 +78,12 @@ struct ConvParams {
 };
 
 // one tile's per-channel partial sum `v` of statistic `which` (0: Σ, 1: Σ²) for channel n, row group g
+// stats_atomic = R ≥ 1: the partial is ADDED into replica g % R of a zeroed [2][R][K] buffer (R = 1:
+// the [2][K] sums): R replicas cut the same-address atomic contention R-fold while keeping the BN's
+// finalize input at R ≤ 512 rows (no fold pass)
 __device__ __forceinline__ void put_stat(const ConvParams& p, int which, int g, int n, float v) {
   if (p.stats_atomic)
-    atomicAdd(&p.stats[(size_t)which * p.K + n], v);
+    atomicAdd(&p.stats[((size_t)which * p.stats_atomic + (g % p.stats_atomic)) * p.K + n], v);
   else
     p.stats[((size_t)which * p.tiles_m + g) * p.K + n] = v;
 }

@@ -176,9 +176,11 @@ def _coef_ok(t, C_):
 
 
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
-                                    relu=False, residual=None, in_bias=None, coef_out=None, shift=None, bits_out=None):
+                                    relu=False, residual=None, in_bias=None, coef_out=None, shift=None, bits_out=None,
+                                    rezero=False):
     """Training BN whose statistics were produced by the preceding conv's epilogue
-    (:func:`conv2d_forward_stats`): finalize + apply only."""
+    (:func:`conv2d_forward_stats`): finalize + apply only.  ``rezero``: ``partial`` is a replicated
+    atomic-statistics buffer ([2][G][C], G replicas) that the finalize clears after reading."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
@@ -211,13 +213,13 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
                                              C.c_int(G), ptr(shift if _f32vec(shift, C_) else None), ptr(coef),
                                              C.c_int(1 if relu else 0),
                                              ptr(_fold_scratch(G, C_, x.device)),
-                                             ptr(_bits_ok(bits_out, M, C_, relu)), _s()),
+                                             ptr(_bits_ok(bits_out, M, C_, relu)), C.c_int(1 if rezero else 0), _s()),
           "bn_fwd_train_partials")
     return y, mean, invstd
 
 
 def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G, need_input=True, gg_acc=None,
-                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, lazy=False):
+                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, lazy=False, rezero=False):
     """BN backward whose reductions came from the consumer conv's dgrad epilogue; ``gm`` is the
     already ReLU-masked gradient.  Returns gradInput (or None) / NotImplemented; ``lazy`` returns
     it as a :class:`~bigdl.ops.reference.BNGrad` (coefficients only, no apply pass)."""
@@ -244,7 +246,8 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
     check(_lib().bigdl_bn_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
                                        ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale), ptr(cbias_acc),
                                        _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
-                                       ptr(_fold_scratch(G, C_, x.device)), _s()), "bn_bwd_partials")
+                                       ptr(_fold_scratch(G, C_, x.device)), C.c_int(1 if rezero else 0), _s()),
+          "bn_bwd_partials")
     if need_input and lazy:
         return R_.BNGrad(gm, x, coef)
     return gx
@@ -789,8 +792,13 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         shift = None
     atomic = 0
     if stats:
-        if sums is not None and shift is not None and sums.dtype == _f32 and sums.numel() == 2 * K + 1 \
-                and sums.is_cuda:
+        if isinstance(sums, tuple) and shift is not None and sums[0].dtype == _f32 and sums[0].is_cuda \
+                and 1 <= sums[1] <= 512 and sums[0].numel() == 2 * sums[1] * K:
+            # replicated atomic statistics: tile tm ADDS into replica tm % R of the BN's zeroed
+            # [2][R][K] buffer; the BN finalizes from the R rows (no fold pass) and clears them
+            part, atomic, G = sums[0], sums[1], sums[1]
+        elif sums is not None and not isinstance(sums, tuple) and shift is not None and sums.dtype == _f32 \
+                and sums.numel() == 2 * K + 1 and sums.is_cuda:
             # the tiles ADD their partial sums into the consumer BN's zeroed [2K + 1] buffer (G = 0
             # marks it for the one-launch finalize+apply, ops/csrc/batchnorm.hip k_bn_apply_fin)
             part, atomic = sums, 1
@@ -900,8 +908,19 @@ def _dgrad_s1(gy, w4, x_shape, pad, dilation, residual=None, bn_fuse=None):
         ok = ok and (_act_ok(mask) if mask is not None else (residual is None and sc is not None and sh is not None
                                                              and _f32vec(sc, C_) and _f32vec(sh, C_)))
         sums = bn_fuse.get("sums")
-        if ok and ax is None and sums is not None and sums.dtype == _f32 and sums.numel() == 2 * C_ + 1 \
-                and sums.is_cuda:
+        if ok and ax is None and isinstance(sums, tuple) and sums[0].dtype == _f32 and sums[0].is_cuda \
+                and 1 <= sums[1] <= 512 and sums[0].numel() == 2 * sums[1] * C_:
+            # replicated atomic statistics ([2][R][C], tile tm → replica tm % R); the BN backward
+            # finalizes from the R rows and clears them
+            buf, rep = sums
+            _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_bnbwd(
+                ptr(gy), ptr(wt), ptr(residual), ptr(gx), ptr(_stat_target(buf, 1)), rep, N_, P, Q, K, C_, R, S, H,
+                W, 1, 1, ph, pw, dilation[0], dilation[1], ptr(bx), ptr(sc), ptr(sh), ptr(mu), ptr(mask),
+                ptr(bits), *(rs or (0, 0, 0, 0)), t[0], t[1], t[2], _s()), "conv_dgrad_bnbwd_rep"))
+            bn_fuse["partial"], bn_fuse["G"] = buf, rep
+            return gx
+        if ok and ax is None and sums is not None and not isinstance(sums, tuple) and sums.dtype == _f32 \
+                and sums.numel() == 2 * C_ + 1 and sums.is_cuda:
             # the tiles ADD Σg', Σg'·(x − μ) into the BN's zeroed [2C + 1] buffer (G = 0): the BN
             # backward is then one finalize+apply launch (batchnorm.hip k_bn_bwd_apply_fin)
             _tiled_launch(dkey, lambda t: check(_lib().bigdl_conv_fwd_bnbwd(

@@ -106,12 +106,14 @@ def test_block_pair_fused_bf16_matches_fp32(name):
     assert cs[len(cs) // 2] > 0.95 and cs[0] > 0.9, sorted(cos, key=lambda t: t[1])[:5]
 
 
+@pytest.mark.parametrize("mode", ["atomic", "replicas"])
 @pytest.mark.parametrize("name", ["stage1_identity", "stage2_to_3", "stage4_identity"])
-def test_atomic_bn_statistics_match_partials_path(name):
+def test_atomic_bn_statistics_match_partials_path(name, mode):
     """bigdl.bn.atomicStats: the conv epilogues ADD the BN statistics (forward Σ, Σ²; backward Σg',
     Σg'·(x−μ)) into [2C] buffers and every BN is one finalize+apply launch.  Two training passes must
     match the per-tile-partials path (fold + finalize kernels) to summation-order rounding, and every
-    buffer must be back to zero afterwards (the last arriving block re-zeroes it)."""
+    buffer must be back to zero afterwards (the last arriving block re-zeroes it).  ``replicas``:
+    bigdl.bn.statReplicas — the tiles add into 64 replicas and the finalize clears them.""" 
     from bigdl.nn import Sequential, SpatialBatchNormalization
     from bigdl.nn.fusion import fuse
     from bigdl.utils import config
@@ -123,8 +125,10 @@ def test_atomic_bn_statistics_match_partials_path(name):
     g = torch.Generator().manual_seed(23)
     out = {}
     prev = config.get_property("bigdl.bn.atomicStats")
+    prev_rep = config.get_property("bigdl.bn.statReplicas")
     for atomic in (False, True):
-        config.set_property("bigdl.bn.atomicStats", atomic)
+        config.set_property("bigdl.bn.atomicStats", atomic and mode == "atomic")
+        config.set_property("bigdl.bn.statReplicas", 64 if (atomic and mode == "replicas") else 0)
         try:
             m = copy.deepcopy(base).cuda()
             m.training()
@@ -142,7 +146,8 @@ def test_atomic_bn_statistics_match_partials_path(name):
             torch.cuda.synchronize()
             bns = [mod for mod in m.flattened_modules() if isinstance(mod, SpatialBatchNormalization)]
             if atomic:
-                bufs = [mod.__dict__.get(k) for mod in bns for k in ("_sums_fwd", "_sums_bwd")]
+                keys = ("_sums_fwd", "_sums_bwd") if mode == "atomic" else ("_rep_fwd", "_rep_bwd")
+                bufs = [mod.__dict__.get(k) for mod in bns for k in keys]
                 assert sum(b is not None for b in bufs) >= len(bns), "the atomic path was not taken"
                 assert all(b is None or float(b.abs().max()) == 0.0 for b in bufs), "sums not re-zeroed"
             # conv biases feeding a training BN have an exactly-zero gradient (the BN removes the
@@ -153,6 +158,7 @@ def test_atomic_bn_statistics_match_partials_path(name):
                            [torch.cat([b.runningMean, b.runningVar]).cpu() for b in bns])
         finally:
             config.set_property("bigdl.bn.atomicStats", prev)
+            config.set_property("bigdl.bn.statReplicas", prev_rep)
     (ga, ya, ra), (gb, yb, rb) = out[False], out[True]
     for (y0, gx0), (y1, gx1) in zip(ya, yb):
         assert _cos(y1, y0) > 0.999 and _cos(gx1, gx0) > 0.995
