@@ -1429,9 +1429,10 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     return gi
 
 
-#: BIGDL_WGRAD_FIRST=1: conv2d_backward forks its weight gradient onto the side stream before the
-#: data gradient is enqueued (A/B knob; 0 = after, the round-3 order)
-_WG_FIRST = [__import__("os").environ.get("BIGDL_WGRAD_FIRST", "0") == "1"]
+#: conv2d_backward forks its weight gradient onto the side stream BEFORE the data gradient is
+#: enqueued, so the two run side by side (BIGDL_WGRAD_FIRST=0: after, the round-3 order; 22.08 vs
+#: 22.94 ms/step, profiles/r4_bn_replicas_ab.txt)
+_WG_FIRST = [__import__("os").environ.get("BIGDL_WGRAD_FIRST", "1") == "1"]
 
 
 def _wgrad_async_or_inline(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot) -> bool:
