@@ -242,6 +242,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
   // interleaved body: fragments of slice kk+1 in flight during slice kk's MFMAs; the L pieces of
   // the next stage spread over the four slices (PPK per slice)
   constexpr int PPK = (L + 3) / 4;
+  static_assert(4 * PPK >= L && BK / 16 == 4, "every piece of the next stage is issued in the four slices");
   auto compute_ilv = [&](int slotbuf, int nslot, auto issue_on) {
     const unsigned char* base = lds + slotbuf * STAGE;
     v8s af[2][TNI], bfr[2][TMI];
@@ -272,6 +273,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      // a slice has fewer MFMA groups (TNI) than pieces to place (PPK, e.g. the 256x64 tile: TNI 1,
+      // PPK 2): the rest of this slice's pieces go after its MFMAs — every piece is issued exactly once
+#pragma unroll
+      for (int q = TNI; q < PPK; ++q)
+        if (decltype(issue_on)::value && kk * PPK + q < L) issue(kk * PPK + q, nslot);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
