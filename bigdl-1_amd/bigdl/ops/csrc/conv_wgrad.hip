@@ -57,6 +57,8 @@ struct WgradParams {
   // measurement knob only (BIGDL_DEBUG_WGRAD_NO_ATOMICS=1): skip the split-K atomic epilogue, which
   // leaves dW WRONG — an upper bound of what a cheaper cross-split reduction could save
   int skip_epi;
+  // 1×1, stride 1, no padding (2-D): X̂ row m is input pixel m — the gather needs no index math
+  int pw1;
   // 1: the split-K partial tile is staged in LDS (fp32) and added with wave-instructions covering
   // 256 contiguous bytes of a dW row (the fast atomic shape, MI355X_MICROARCH.md 'Global float
   // atomics'); 0: straight from the accumulators (four 64-B row segments per instruction)
@@ -164,6 +166,16 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
       const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldk + (uint32_t)ndy) * 2u : DEAD) | dead;
       rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
       if constexpr (AT) r2[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(y2r, off, 0, 0));
+    }
+    if (!C4 && !D3 && p.pw1) {  // pointwise: pixel m of the output is pixel m of the input
+#pragma unroll
+      for (int i = 0; i < X_CH; ++i) {
+        const int m = mt + x_row0 + i * X_RSTEP;
+        const bool ok = kx_ok && m < mend;
+        const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldx + (uint32_t)cx) * 2u : DEAD) | dead;
+        rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
@@ -411,6 +423,7 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
   p.Kg = R * S * C;
   p.fPQ = make_fastdiv((uint32_t)(P * Q));
   p.fQ = make_fastdiv((uint32_t)Q);
+  p.pw1 = (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && P == H && Q == W && !c4) ? 1 : 0;
   const int TN = K <= 64 ? 64 : 128;
   const int TK = (p.Kg <= 64 && !c4) ? 64 : 128;  // the C4 kernels are instantiated with 128-wide k tiles only
   p.tiles_n = (K + TN - 1) / TN;
