@@ -81,8 +81,9 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 
 // C4: 4-channel input (RGB stem padded 3 → 4): an X̂ chunk of 8 k-values is two consecutive taps,
 // gathered as two 8-B loads with separate padding tests (see conv_igemm.hip MODE 2).
-template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false>
+template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false, bool PW1 = false>
 __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(WgradParams p) {
+  static_assert(!(PW1 && (C4 || D3)), "pointwise gather: 2-D, 8-channel chunks");
   static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
   static_assert(!(AT && (C4 || D3)), "BN-backward prologue: 2-D, 8-channel chunks");
   constexpr int DY_CH = BPT * TILE_N / 8 / 256;  // 16-B chunks per thread for the dY tile
@@ -167,7 +168,7 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
       rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
       if constexpr (AT) r2[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(y2r, off, 0, 0));
     }
-    if (!C4 && !D3 && p.pw1) {  // pointwise: pixel m of the output is pixel m of the input
+    if constexpr (PW1) {  // pointwise: pixel m of the output is pixel m of the input
 #pragma unroll
       for (int i = 0; i < X_CH; ++i) {
         const int m = mt + x_row0 + i * X_RSTEP;
@@ -472,6 +473,16 @@ static int wgrad_launch(const void* x, const void* dy, float* dw, float scale, i
       if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 64, true>), grid, dim3(256), 0, s, p);
       else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64, true>), grid, dim3(256), 0, s, p);
     }
+  } else if (p.pw1 && bp == 32) {
+    if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 32, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32, false, false, false, true>), grid, dim3(256), 0, s, p);
+  } else if (p.pw1) {
+    if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 64, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 64, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else if (TK == 64) hipLaunchKernelGGL((k_conv_wgrad<128, 64, 64, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 64, false, false, false, true>), grid, dim3(256), 0, s, p);
   } else if (bp == 32) {
     if (TN == 64 && TK == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 64, 32>), grid, dim3(256), 0, s, p);
     else if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32>), grid, dim3(256), 0, s, p);
