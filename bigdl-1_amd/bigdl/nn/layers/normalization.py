@@ -129,10 +129,12 @@ class BatchNormalization(TensorModule):
         statistics into — ``kind`` "fwd": the producing conv's Σ(y−K), Σ(y−K)²; "bwd": the consuming
         conv's dgrad Σg', Σg'·(x − μ) — consumed (and re-zeroed) by the one-launch finalize+apply.
         None when the per-tile partials path is required (SyncBN, bigdl.deterministic, off)."""
-        if device.type != "cuda" or self._sync_active() or config.get_property("bigdl.deterministic"):
+        if device.type != "cuda" or config.get_property("bigdl.deterministic"):
             return None
         rep = int(config.get_property("bigdl.bn.statReplicas"))
-        if rep > 0 and not config.get_property("bigdl.bn.atomicStats"):
+        if self._sync_active() and not (rep > 0 and config.get_property("bigdl.bn.shiftedStats")):
+            return None
+        if rep > 0 and (self._sync_active() or not config.get_property("bigdl.bn.atomicStats")):
             # replicated form: [2][R][C] zeroed, tile tm adds into replica tm % R; the BN's finalize
             # reads the R rows and clears them (batchnorm.hip reduce_partials rezero)
             rep = min(rep, 512)
@@ -298,7 +300,8 @@ class BatchNormalization(TensorModule):
             if m is not R and ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape) \
                     and ps[4] is not None:
                 shift = ps[4]
-                sums = m.bn_local_sums(x, shift, ps[2], ps[3])
+                sums = m.bn_local_sums(x, shift, ps[2], ps[3], rezero=self._is_rep(ps[2]))
+                ps = None  # consumed
             else:
                 shift = self.runningMean
                 sums = m.bn_local_sums(x, shift)
@@ -313,6 +316,7 @@ class BatchNormalization(TensorModule):
                 self._sync_path = "native" if m is not R else "reference"
                 self._last_input = x
                 break
+        self._drop_sums(ps, 3)  # replicated statistics left by the conv and not read: clear them
         return r
 
     def _bwd(self, input, gradOutput, need_input, acc, want_gres=False):
@@ -398,9 +402,10 @@ class BatchNormalization(TensorModule):
             if m is not R and pg is not None and pg[0] == gy.data_ptr() and relu:
                 # gy is already ReLU-masked by the consumer conv's dgrad epilogue, which also left
                 # the backward partial sums: reduce those instead of re-reading gy, x, y
-                both = m.bn_bwd_partials_sums(pg[1], pg[2], C, x.device, rows=rows)
+                both = m.bn_bwd_partials_sums(pg[1], pg[2], C, x.device, rows=rows, rezero=self._is_rep(pg[1]))
                 if both is not NotImplemented:
                     rl = False
+                    pg = None  # consumed
             if both is NotImplemented:
                 both = m.bn_bwd_local_sums(gy, x, self.saveMean, y=y, relu=rl)
             if both is NotImplemented:
@@ -417,6 +422,7 @@ class BatchNormalization(TensorModule):
             if acc and self.affine and self.scale_b != self.scale_w:
                 self.gradBias.add_(loc[:C], alpha=self.scale_b - self.scale_w)
             self._sync_bwd_path = "native" if m is not R else "reference"
+            self._drop_sums(pg, 2)  # replicated statistics left by the dgrad and not read
             return gi, cb is not None
         raise RuntimeError("SyncBN backward: no implementation accepted the input")
 

@@ -909,10 +909,11 @@ BIGDL_EXPORT int bigdl_bn_bwd_sums_apply(const void* gm, const void* x, void* gx
 // path, so SyncBN costs two tiny kernels and one 2·C collective per direction.
 template <typename T>
 __global__ void __launch_bounds__(32 * kFinRG) k_bn_sum_rows(const T* __restrict__ partial, int G, int C,
-                                                      float* __restrict__ out, float* __restrict__ out2, float cnt) {
+                                                      float* __restrict__ out, float* __restrict__ out2, float cnt,
+                                                      float* rezero = nullptr) {
   __shared__ double lds[kFinRG][2][33];
   double a, b;
-  reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b);
+  reduce_partials(partial, G, C, blockIdx.x * 32, lds, a, b, rezero);
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   if ((threadIdx.x >> 5) != 0 || c >= C) return;
   // this rank's row count behind the sums of the buffer the collective reduces ([2C + 1])
@@ -926,12 +927,13 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_sum_rows(const T* __restrict
 }
 
 static void sum_rows(const float* partial, int G, int C, float* scratch, float* out, hipStream_t s,
-                     float* out2 = nullptr, float cnt = -1.f) {
-  if (maybe_fold(partial, G, C, scratch, s))
+                     float* out2 = nullptr, float cnt = -1.f, bool rezero = false) {
+  if (!rezero && maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_sum_rows<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const double*)scratch, G, C, out,
                        out2, cnt);
   else
-    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, C, out, out2, cnt);
+    hipLaunchKernelGGL(k_bn_sum_rows<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, partial, G, C, out, out2, cnt,
+                       rezero ? const_cast<float*>(partial) : nullptr);
 }
 
 // Local shifted sums of x (kshift = the running mean, identical on every rank): out[2C], and the row
@@ -950,17 +952,18 @@ BIGDL_EXPORT int bigdl_bn_stats_sums(const void* x, long long M, int C, const fl
 
 // Reduce G partial rows (a conv epilogue's, or any [2][G][C] fp32 block) to out[2C] (and the same
 // values to out2[2C] when given: the copy an in-place all-reduce turns into the global sums).
+// rezero: `partial` is a replicated atomic-statistics buffer (G ≤ 512 replicas) cleared after reading
 BIGDL_EXPORT int bigdl_bn_partials_sums(const float* partial, int G, int C, float* scratch, float* out, float cnt,
-                                        hipStream_t s) {
-  if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  sum_rows(partial, G, C, scratch, out, s, nullptr, cnt);
+                                        int rezero, hipStream_t s) {
+  if (C <= 0 || G <= 0 || (rezero && G > 512)) return (int)hipErrorInvalidValue;
+  sum_rows(partial, G, C, scratch, out, s, nullptr, cnt, rezero != 0);
   BIGDL_CHECK_LAUNCH();
 }
 
 BIGDL_EXPORT int bigdl_bn_partials_sums2(const float* partial, int G, int C, float* scratch, float* out, float* out2,
-                                         float cnt, hipStream_t s) {
-  if (C <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  sum_rows(partial, G, C, scratch, out, s, out2, cnt);
+                                         float cnt, int rezero, hipStream_t s) {
+  if (C <= 0 || G <= 0 || (rezero && G > 512)) return (int)hipErrorInvalidValue;
+  sum_rows(partial, G, C, scratch, out, s, out2, cnt, rezero != 0);
   BIGDL_CHECK_LAUNCH();
 }
 

@@ -254,7 +254,7 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
 
 
 # ---- SyncBN (cross-rank statistics; the caller all-reduces the 2·C sums between the halves) ----
-def bn_local_sums(x, shift, partial=None, G=0):
+def bn_local_sums(x, shift, partial=None, G=0, rezero=False):
     """This rank's shifted sums [Σ(x−K), Σ(x−K)², rows] (fp32 [2C + 1]) with K = ``shift`` (the
     running mean, identical on every rank): from a producing conv's epilogue partials
     (``partial``/``G``, which must have been computed with the same shift) or a stats pass over x.
@@ -272,7 +272,8 @@ def bn_local_sums(x, shift, partial=None, G=0):
         if partial.numel() != 2 * G * C_ or partial.dtype != _f32:
             return NotImplemented
         check(_lib().bigdl_bn_partials_sums(ptr(partial), C.c_int(G), C.c_int(C_),
-                                            ptr(_fold_scratch(G, C_, x.device)), ptr(out), _f(M), _s()),
+                                            ptr(_fold_scratch(G, C_, x.device)), ptr(out), _f(M),
+                                            C.c_int(1 if rezero else 0), _s()),
               "bn_partials_sums")
         return out
     lib = _lib()
@@ -330,14 +331,14 @@ def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
     return out
 
 
-def bn_bwd_partials_sums(partial, G, C_, dev, rows=None):
+def bn_bwd_partials_sums(partial, G, C_, dev, rows=None, rezero=False):
     """[Σg', Σg'·(x − mean)] twice (fp32 [4C + 1], ``rows`` last) from the consumer conv's
     dgrad-epilogue partials (``_pending_grad``): no pass over the activations."""
     if partial is None or partial.dtype != _f32 or partial.numel() != 2 * G * C_ or rows is None:
         return NotImplemented
     out = torch.empty(4 * C_ + 1, dtype=_f32, device=dev)
     check(_lib().bigdl_bn_partials_sums2(ptr(partial), C.c_int(G), C.c_int(C_), ptr(_fold_scratch(G, C_, dev)),
-                                         ptr(out), ptr(out[2 * C_:]), _f(rows), _s()), "bn_partials_sums2")
+                                         ptr(out), ptr(out[2 * C_:]), _f(rows), C.c_int(1 if rezero else 0), _s()), "bn_partials_sums2")
     return out
 
 

@@ -253,13 +253,16 @@ def _bn_dims(x):
     return [d for d in range(x.dim()) if d != 1], [1, x.shape[1]] + [1] * (x.dim() - 2)
 
 
-def bn_local_sums(x, shift, partial=None, G=0):
+def bn_local_sums(x, shift, partial=None, G=0, rezero=False):
     """[Σ(x−K), Σ(x−K)², rows] fp32 [2C + 1] with K = ``shift``."""
     C = x.shape[1]
     dims, shape = _bn_dims(x)
     if partial is not None:
         p = partial.view(2, G, C).sum(1)
-        return torch.cat([p.reshape(-1), p.new_tensor([float(x.numel() // C)])])
+        out = torch.cat([p.reshape(-1), p.new_tensor([float(x.numel() // C)])])
+        if rezero:
+            partial.zero_()
+        return out
     xf = acc_float(x) - acc_float(shift).to(acc_float(x).dtype).view(shape)
     return torch.cat([xf.sum(dims), (xf * xf).sum(dims), xf.new_tensor([float(x.numel() // C)])])
 
@@ -307,9 +310,12 @@ def bn_bwd_local_sums(gy, x, save_mean, y=None, relu=False):
     return torch.cat([loc, loc, loc.new_tensor([float(x.numel() // C)])])
 
 
-def bn_bwd_partials_sums(partial, G, C_, dev, rows=None):
+def bn_bwd_partials_sums(partial, G, C_, dev, rows=None, rezero=False):
     p = partial.view(2, G, C_).sum(1).reshape(-1)
-    return torch.cat([p, p, p.new_tensor([float(rows)])])
+    out = torch.cat([p, p, p.new_tensor([float(rows)])])
+    if rezero:
+        partial.zero_()
+    return out
 
 
 def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, global_sums, count, y=None, relu=False,
