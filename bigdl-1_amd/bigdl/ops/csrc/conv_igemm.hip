@@ -76,6 +76,21 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  // the BN-statistics shift of this lane's channels, fetched before the main loop so the epilogue
+  // does not wait on a dependent global load per tile (shifted statistics, rstats epilogue)
+  float kpre[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kpre[i][e] = 0.f;
+  if (BM == SBM && p.stats && p.stat_shift) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int nk = n0 + wave_n * (BN / 2) + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kpre[i][e] = nk + e < p.K ? p.stat_shift[nk + e] : 0.f;
+    }
+  }
   const int col8 = tid & (CPK - 1);  // this thread's 16-B chunk column inside a k tile
 
   // Operand loads are raw buffer loads: the descriptor's num_records bounds-check returns zeros
@@ -454,12 +469,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
-      float k4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.stat_shift) {
-        const int nk = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) k4[e] = nk + e < p.K ? p.stat_shift[nk + e] : 0.f;
-      }
+      float k4[4] = {kpre[i][0], kpre[i][1], kpre[i][2], kpre[i][3]};
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         // rows past M (the last tile's padding) hold acc = 0 and must stay 0 after the shift

@@ -78,6 +78,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  // the store pass's statistics shift for this thread's 8 channels, fetched before the main loop
+  float skp[8];
+  {
+    const int ns = n0 + (tid % (BN / 8)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      skp[e] = (p.stat_shift && p.stats && !p.bnx && ns + e < p.K) ? p.stat_shift[ns + e] : 0.f;
+  }
 
   const uint32_t x_bytes = (uint32_t)(((size_t)p.Nb * p.H * p.W * p.ldx - grp * p.gx) * 2);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw * 2);
@@ -392,7 +400,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
       }
     }
   __syncthreads();
-  conv_store_pass<BM, BN, NT>(p, et, tid, m0, n0, tm, false);
+  conv_store_pass<BM, BN, NT>(p, et, tid, m0, n0, tm, false, skp);
 }
 
 // ---- host side ----

@@ -116,9 +116,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // row-major, 8 channels per thread: optional residual add, ReLU, BN-backward mask, scatter, one
 // 16-B global store per chunk, and per-channel Σ / Σ² partials for a following BatchNormalization.
 // ``rstats``: the statistics were already reduced from the fp32 accumulators into `red8`.
+// ``skp`` (optional): this thread's 8 statistics-shift values, fetched by the caller ahead of time
+// (channels n0 + (tid % (BN / 8))·8 …+7) instead of a dependent load here.
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et, int tid, int m0, int n0, int tm,
-                                                bool rstats) {
+                                                bool rstats, const float* skp = nullptr) {
   constexpr int LDR = BN;
   constexpr int CMASK = (BN / 8 - 1) & 15;
   constexpr int SRED = 8;
@@ -152,7 +154,8 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
   const bool full = n + 8 <= p.K;
   float sk[8];  // statistics shift of this thread's 8 channels
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sk[e] = (p.stat_shift && p.stats && !p.bnx && n + e < p.K) ? p.stat_shift[n + e] : 0.f;
+  for (int e = 0; e < 8; ++e)
+    sk[e] = skp ? skp[e] : (p.stat_shift && p.stats && !p.bnx && n + e < p.K) ? p.stat_shift[n + e] : 0.f;
   float bsc[8], bsh[8], bmu[8];
   if (p.bnx && full) {
 #pragma unroll
