@@ -14,8 +14,9 @@ same split is:
   the planned forward is timed under each implicit-GEMM tile candidate and the winner pinned;
 * **execute** (:class:`CompiledModule`): on a GPU and in the inference phase the forward is
   captured once into a HIP graph with a static input buffer — every kernel and every workspace
-  allocation of the forward is then fixed (the graph's private memory pool), and each call is a
-  copy-in plus one graph replay, with no per-layer host dispatch.  Models whose forward syncs with
+  allocation of the forward is then fixed (the graph's private memory pool, reserved up front as one
+  slab of the plan's first-fit arena size), and each call is a copy-in plus one graph replay, with
+  no per-layer host dispatch.  Models whose forward syncs with
   the host (data-dependent shapes, ``.item()``) cannot be captured and run eagerly with a warning.
 
 ``compile(model, example, phase)`` does both.
@@ -352,8 +353,23 @@ class CompiledModule:
             for _ in range(max(1, warmup)):
                 m.forward(self.static_in)
         torch.cuda.current_stream(example.device).wait_stream(side)
+        # the planned workspace: the graph's private pool is reserved up front as ONE segment of
+        # the first-fit arena size (plan.arena_bytes, plus kernel-side temporaries the leaf-level
+        # plan does not see), so the captured forward's activations are carved from one slab —
+        # the arena the plan laid out — rather than grown segment by segment during capture
+        pool = torch.cuda.graph_pool_handle()
+        self.arena_reserved = 0
+        if self.plan.arena_bytes > 0:
+            g0 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g0, pool=pool):
+                slab = torch.empty(int(self.plan.arena_bytes * 1.25) + (1 << 20), dtype=torch.uint8,
+                                   device=example.device)
+                slab[:1].zero_()  # (a capture with no kernel at all is reported as an empty graph)
+                self.arena_reserved = slab.numel()
+                del slab
+            del g0
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g):
+        with torch.no_grad(), torch.cuda.graph(g, pool=pool):
             self.static_out = m.forward(self.static_in)
         self.graph = g
 

@@ -68,6 +68,8 @@ def test_compiled_hip_graph_inference():
     p = c.plan
     assert any(r.out_layout == "NHWC" for r in p.layers)  # the conv path's device layout
     assert p.reorders  # NCHW input → NHWC conv output at least once
+    # the graph's pool was reserved as one slab sized from the plan's first-fit arena
+    assert c.arena_reserved >= p.arena_bytes > 0
 
 
 @pytest.mark.gpu
