@@ -437,6 +437,10 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
         const int m = m0 + wave_m * (BM / 2) + j * 16 + fr;
         if (m >= p.M) continue;
         float4 v = make_float4(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1], acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
+        if (p.res32) {
+          const float4 r = *reinterpret_cast<const float4*>(p.res32 + (size_t)m * p.ldy + n);
+          v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+        }
         if (p.relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
         *reinterpret_cast<float4*>(p.y32 + (size_t)m * p.ldy + n) = v;
       }
@@ -570,7 +574,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
                            float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0,
-                           int stats_atomic = 0) {
+                           int stats_atomic = 0, const float* res32 = nullptr) {
   const bool c4 = C == 4;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
   if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
@@ -607,6 +611,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.bias = bias;
   p.y = (bf16_t*)y;
   p.y32 = y32;
+  if (res32 && (!y32 || ((uintptr_t)res32 & 15))) return (int)hipErrorInvalidValue;
+  p.res32 = res32;
   p.res = (const bf16_t*)res;
   p.stats = stats;
   p.stats_atomic = stats ? stats_atomic : 0;
@@ -831,6 +837,17 @@ BIGDL_EXPORT int bigdl_conv_fwd_f32out(const void* x, const void* w, const float
   return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
                          relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
                          0, 0, nullptr, 0, 1, nullptr, nullptr, y32);
+}
+
+// bigdl_conv_fwd_f32out + an fp32 residual [M][ldy] summed in the epilogue (res32 16-B aligned)
+BIGDL_EXPORT int bigdl_conv_fwd_f32out_res(const void* x, const void* w, const float* bias, const float* res32,
+                                           float* y32, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                           int sh, int sw, int ph, int pw, int dh, int dw, int relu, int ldy,
+                                           hipStream_t s) {
+  if (!y32 || !res32) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+                         relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
+                         0, 0, nullptr, 0, 1, nullptr, nullptr, y32, 0, 0, 0, 0, res32);
 }
 
 // bigdl_conv_fwd_ldy / bigdl_conv_fwd_stats_shift with an explicit tile (bn, bk, bm; 0 = heuristic).

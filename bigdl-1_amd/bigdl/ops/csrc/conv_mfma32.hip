@@ -372,6 +372,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
           if (m >= p.M) continue;
           float4 v = make_float4(acc[i][j][4 * g] + b4[0], acc[i][j][4 * g + 1] + b4[1], acc[i][j][4 * g + 2] + b4[2],
                                  acc[i][j][4 * g + 3] + b4[3]);
+          if (p.res32) {
+            const float4 r = *reinterpret_cast<const float4*>(p.res32 + (size_t)m * p.ldy + n);
+            v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+          }
           if (p.relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
           *reinterpret_cast<float4*>(p.y32 + (size_t)m * p.ldy + n) = v;
         }

@@ -70,6 +70,9 @@ struct ConvParams {
   // ReLU) are stored straight from registers as float4 per lane — no bf16 rounding, no LDS staging;
   // `y` is unused.  Plain epilogue only (no residual / statistics / BN prologue / scatter / groups).
   float* y32;
+  // optional fp32 residual [M][ldy] added to the fp32 output before the ReLU (y32 mode only: the
+  // data gradient of a block's first conv summed with the shortcut's, bf16x3 path)
+  const float* res32;
   // statistics mode: 0 = per-row-tile partial rows stats[2][tiles_m][K] (reduced later by a
   // fold / finalize pass), 1 = every tile ADDS its partial sums into stats[2][K] with fp32 atomics
   // (the consumer's apply kernel finalises in its prologue and re-zeroes the buffer: no separate

@@ -75,7 +75,12 @@ def _nhwc_rows(x: torch.Tensor) -> torch.Tensor:
     return xc.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
 
 
-def _conv_f32out(x3, w3, bias, y, nb, h, w, c3, k, r, s, p, q, stride, pad, dil, relu, ldy):
+def _conv_f32out(x3, w3, bias, y, nb, h, w, c3, k, r, s, p, q, stride, pad, dil, relu, ldy, res=None):
+    if res is not None:  # fp32 residual summed in the epilogue (same [M][ldy] layout as y)
+        check(N.lib().bigdl_conv_fwd_f32out_res(ptr(x3), ptr(w3), ptr(bias), ptr(res), ptr(y), nb, h, w, c3, k, r, s,
+                                                p, q, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1],
+                                                int(bool(relu)), ldy, _s()), "conv_fwd_f32out_res")
+        return
     check(N.lib().bigdl_conv_fwd_f32out(ptr(x3), ptr(w3), ptr(bias), ptr(y), nb, h, w, c3, k, r, s, p, q, stride[0],
                                         stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), ldy, _s()),
           "conv_fwd_f32out")
@@ -149,10 +154,14 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         wt3 = torch.zeros((cq * r * s, 3 * kp), dtype=_bf16, device=x.device) if cq != c else None
         wt3 = split(wt, kp, HLH, False, out=wt3)
         gi = torch.empty((nb, cq, h, w), dtype=_f32, device=x.device, memory_format=_cl)
-        _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq)
+        # the shortcut's gradient summed in the epilogue (one pass fewer than a separate add)
+        fuse_res = (residual is not None and cq == c and residual.dtype == _f32 and tuple(residual.shape) == (nb, c, h, w)
+                    and residual.is_contiguous(memory_format=_cl) and residual.data_ptr() % 16 == 0)
+        _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
+                     res=residual if fuse_res else None)
         if cq != c:
             gi = gi[:, :c].contiguous(memory_format=_cl)
-        if residual is not None:
+        if residual is not None and not fuse_res:
             gi.add_(residual)
     if gw_acc is not None and scale != 0:
         # three launches over the side-by-side parts — (x_hi, dY_hi), (x_hi, dY_lo), (x_lo, dY_hi) —

@@ -63,9 +63,15 @@ def test_conv_fp32x3_matches_fp64(N, C, K, H, W, k, s, p, d):
     # and it is not the bf16 path: plain bf16 operands are ~100x further off
     yb = F.conv2d(x.bfloat16().double(), w.bfloat16().double(), b.double(), s, p, d)
     assert _rel(yb, yr) > 20 * _rel(y, yr)
+    # shortcut gradient summed in the data-gradient epilogue (C % 4 == 0) or by the fallback add (C == 3)
+    res = torch.randn(N, C, H, W, generator=g)
+    gi2 = F3.conv_backward(gy.to(dev), x.to(dev), w.to(dev), (s, s), (p, p), (d, d), 1, True, gw.clone(), gb.clone(),
+                           1.0, residual=res.to(dev).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    assert _rel(gi2, xr.grad + res.double()) < 2e-5, _rel(gi2, xr.grad + res.double())
 
 
-@pytest.mark.parametrize("M,K,N", [(64, 256, 128), (33, 100, 10), (7, 24, 36)])
+@pytest.mark.parametrize("M,K,N",[(64, 256, 128), (33, 100, 10), (7, 24, 36)])
 def test_linear_fp32x3_matches_fp64(M, K, N):
     from bigdl.ops import fp32x3 as F3
     g = torch.Generator().manual_seed(2)
