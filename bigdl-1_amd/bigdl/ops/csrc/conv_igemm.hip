@@ -193,7 +193,8 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
     if constexpr (FAST) {
       const int kb = live ? kt * BK : 0;      // wave-uniform
       const int tap = (PW || !live) ? 0 : it_tap;  // a dead call's offsets are forced out of range below
-      const int tap_off = PW ? kb : it_off + it_c0;
+      const int cl = PW ? kb : it_c0;  // logical channel of the tile (cdup: the duplicated part re-reads hi)
+      const int tap_off = (PW ? 0 : it_off) + ((p.cdup && cl >= p.cdup) ? cl - p.cdup : cl);
       if (!PW && live) {
         it_c0 += BK;
         if (it_c0 == p.C) {
@@ -255,6 +256,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
       if (kin) {
         tap = k / p.C;
         c = k - tap * p.C;
+        if (p.cdup && c >= p.cdup) c -= p.cdup;
         if constexpr (D3) {
           d = tap / (p.R * p.S);
           tap -= d * p.R * p.S;
@@ -574,14 +576,15 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
                            float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0,
-                           int stats_atomic = 0, const float* res32 = nullptr) {
+                           int stats_atomic = 0, const float* res32 = nullptr, int cdup = 0) {
   const bool c4 = C == 4;
+  if (cdup && (cdup < 0 || cdup % 8 || 2 * cdup > C || c4 || ax || groups != 1 || !y32)) return (int)hipErrorInvalidValue;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
   if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
               osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
     return (int)hipErrorInvalidValue;
-  if (ldx == 0) ldx = C;
-  if (groups < 1 || ldx < C || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
+  if (ldx == 0) ldx = C - cdup;
+  if (groups < 1 || ldx < C - cdup || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
   // grouped: C / K are per group; x pixels are ldx apart with group g at channel g·C; y rows ldy
   // apart with group g at channel g·K; w holds the groups' [K][R][S][C] blocks back to back
   if (groups > 1 && (c4 || res || stats || bnx || ldx < groups * C || ldy < groups * K || K % 8 ||
@@ -600,6 +603,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   ConvParams p{};  // value-initialised: a field a launcher forgets is null / 0, never stack garbage
   p.T = p.KT = p.st = p.dtd = p.To = 1;
   p.ldx = ldx;
+  p.cdup = cdup;
   p.ax = (const bf16_t*)ax;
   p.acoef = acoef;
   if ((ax != nullptr) != (acoef != nullptr) || (ax && ((uintptr_t)ax & 15))) return (int)hipErrorInvalidValue;
@@ -661,7 +665,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
       xbm = 256;
       xbn = K <= 64 ? 64 : 128;
     }
-    if (xbm && !ax && !c4) {
+    if (xbm && !ax && !c4 && !cdup) {
       const int xmode = (R == 1 && S == 1 && ph == 0 && pw == 0) ? 3 : 1;
       p.tiles_n = (K + xbn - 1) / xbn;
       p.tiles_m = (p.M + SBM - 1) / SBM;
@@ -689,7 +693,9 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (!bk_env && bk == 64 && C % 64 != 0 && C % 32 == 0) bk = 32;
   const int bm = tile_bm ? tile_bm
                           : (conv_env_override("BIGDL_CONV_BM", 128, 256) ? conv_env_override("BIGDL_CONV_BM", 128, 256) : 128);
-  const bool fast = (C % bk == 0) && R * S <= 64;
+  if (!bk_env && bk == 64 && cdup % 64 != 0 && cdup % 32 == 0) bk = 32;
+  // the tap-uniform gather maps a whole k-tile through cdup: a tile must not straddle a part boundary
+  const bool fast = (C % bk == 0) && R * S <= 64 && cdup % bk == 0;
   const int mode = c4 ? 2 : (fast && R == 1 && S == 1 && ph == 0 && pw == 0 ? 3 : (fast ? 1 : 0));
   if (ax && (mode != 3 || groups != 1 || bm != 128)) return (int)hipErrorInvalidValue;  // prologue: pointwise only
   long long tiles = (long long)((p.M + bm - 1) / bm) * p.tiles_n;
@@ -848,6 +854,18 @@ BIGDL_EXPORT int bigdl_conv_fwd_f32out_res(const void* x, const void* w, const f
   return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
                          relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
                          0, 0, nullptr, 0, 1, nullptr, nullptr, y32, 0, 0, 0, 0, res32);
+}
+
+// bigdl_conv_fwd_f32out_res on the two-part bf16x3 activation: x = [Nb][H][W][2·cp] holding [hi | lo],
+// read as the 3·cp logical channels [hi | hi | lo] (ConvParams::cdup = cp); C = 3·cp; res32 optional
+BIGDL_EXPORT int bigdl_conv_fwd_f32out2(const void* x, const void* w, const float* bias, const float* res32,
+                                        float* y32, int Nb, int H, int W, int C, int cdup, int K, int R, int S, int P,
+                                        int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int ldy,
+                                        hipStream_t s) {
+  if (!y32 || cdup <= 0 || C != 3 * cdup) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+                         relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
+                         0, 0, nullptr, 2 * cdup, 1, nullptr, nullptr, y32, 0, 0, 0, 0, res32, cdup);
 }
 
 // bigdl_conv_fwd_ldy / bigdl_conv_fwd_stats_shift with an explicit tile (bn, bk, bm; 0 = heuristic).

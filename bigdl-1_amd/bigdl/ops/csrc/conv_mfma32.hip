@@ -411,7 +411,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
 bool conv_x8_ok(int mode, int bm, int bn, const ConvParams& p) {
   if (mode != 1 && mode != 3) return false;
   if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 128))) return false;
-  if (p.C % 64 || p.Kg % 64 || p.ldx % 8 || p.ldw % 8) return false;
+  if (p.cdup || p.C % 64 || p.Kg % 64 || p.ldx % 8 || p.ldw % 8) return false;
   if (p.T != 1 || p.KT != 1 || p.ax) return false;
   if (mode == 1 && p.R * p.S > 64) return false;
   return true;

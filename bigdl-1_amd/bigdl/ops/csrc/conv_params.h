@@ -59,6 +59,9 @@ struct ConvParams {
   // grouped convolution (SpatialConvolution.scala nGroup; one launch, group = blockIdx.y), the
   // per-group element offsets of x (channels), w (filters·ldw) and y / bias (channels).
   int ldx;
+  // bf16x3 two-part input (0 = off): logical channels [cdup, 2·cdup) re-read physical [0, cdup) — the
+  // activation split is stored [hi | lo] (ldx = C − cdup) and read as [hi | hi | lo]
+  int cdup;
   long long gx, gw, gy;
   // BatchNorm-backward prologue (AT instantiations, pointwise mode): the A operand x is the
   // gradient g' at a BN's output and ``ax`` that BN's input (same layout); the kernel reads

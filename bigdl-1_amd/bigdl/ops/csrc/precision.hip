@@ -20,7 +20,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // threads per row one 8-channel chunk each (no per-element index division; streaming-bound).
 __global__ void __launch_bounds__(256) k_split_bf16x3(const float* __restrict__ src, long long rows, int C, long long ld,
                                                       int Cp, bf16_t* __restrict__ dst, int code, int stacked,
-                                                      int vec4) {
+                                                      int vec4, int nparts) {
   const int chunks = Cp / 8;
   const int tpr = chunks < 256 ? chunks : 256;
   const int rpi = 256 / tpr;
@@ -52,7 +52,8 @@ __global__ void __launch_bounds__(256) k_split_bf16x3(const float* __restrict__ 
       const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]), L = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        const size_t off = stacked ? ((size_t)(q * rows + r) * Cp + c0) : ((size_t)r * 3 * Cp + (size_t)q * Cp + c0);
+        if (q >= nparts) break;
+        const size_t off = stacked ? ((size_t)(q * rows + r) * Cp + c0) : ((size_t)r * nparts * Cp + (size_t)q * Cp + c0);
         *reinterpret_cast<uint4*>(dst + off) = ((code >> q) & 1) ? L : H;
       }
     }
@@ -68,6 +69,21 @@ BIGDL_EXPORT int bigdl_split_bf16x3(const float* src, long long rows, int C, lon
   long long grid = (rows + rpi - 1) / rpi;
   if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_split_bf16x3, dim3((unsigned)grid), dim3(256), 0, s, src, rows, C, ld, Cp, (bf16_t*)dst, code,
-                     stacked, vec4);
+                     stacked, vec4, 3);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// The two-part activation split [hi | lo] side by side ([rows][2·Cp]): the conv kernels read it as
+// [hi | hi | lo] (ConvParams::cdup) and the weight-gradient kernels take hi / lo channel slices, so the
+// duplicated hi part is never written (4 instead of 6 bytes out per element).
+BIGDL_EXPORT int bigdl_split_bf16x2(const float* src, long long rows, int C, long long ld, int Cp, void* dst,
+                                    hipStream_t s) {
+  if (rows <= 0 || C <= 0 || Cp < C || Cp % 8 || ld < C || ((uintptr_t)dst & 15)) return (int)hipErrorInvalidValue;
+  const int vec4 = (ld % 4 == 0 && ((uintptr_t)src & 15) == 0) ? 1 : 0;
+  const int chunks = Cp / 8, tpr = chunks < 256 ? chunks : 256, rpi = 256 / tpr;
+  long long grid = (rows + rpi - 1) / rpi;
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_split_bf16x3, dim3((unsigned)grid), dim3(256), 0, s, src, rows, C, ld, Cp, (bf16_t*)dst, 0b10, 0,
+                     vec4, 2);
   BIGDL_CHECK_LAUNCH();
 }

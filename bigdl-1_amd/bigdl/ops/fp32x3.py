@@ -69,6 +69,34 @@ def split(rows2d: torch.Tensor, cp: int, code: int, stacked: bool, out: torch.Te
     return out
 
 
+def split2(rows2d: torch.Tensor, cp: int) -> torch.Tensor:
+    """fp32 [rows][C] → bf16 ``[rows][2·cp]`` = [hi | lo] (zero-padded to cp each): the conv
+    kernels read it as the three logical parts [hi | hi | lo] (``ConvParams::cdup``), so the duplicated
+    hi part is never stored; the weight-gradient launches take its hi / lo halves as channel slices."""
+    rows, c = rows2d.shape
+    if rows2d.stride(1) != 1 or rows2d.dtype != _f32:
+        rows2d = rows2d.float().contiguous()
+    out = torch.empty((rows, 2 * cp), dtype=_bf16, device=rows2d.device)
+    check(N.lib().bigdl_split_bf16x2(ptr(rows2d), C.c_longlong(rows), C.c_int(c), C.c_longlong(rows2d.stride(0)),
+                                     C.c_int(cp), ptr(out), _s()), "split_bf16x2")
+    return out
+
+
+def _two_part() -> bool:
+    return bool(config.get_property("bigdl.fp32.twoPart"))
+
+
+def _act_split(rows2d, cp, two):
+    return split2(rows2d, cp) if two else split(rows2d, cp, HHL, False)
+
+
+def _conv_f32out2(x2, w3, bias, y, nb, h, w, cp, k, r, s, p, q, stride, pad, dil, relu, ldy, res=None):
+    """fp32-output conv of the two-part activation split (logical C = 3·cp)."""
+    check(N.lib().bigdl_conv_fwd_f32out2(ptr(x2), ptr(w3), ptr(bias), ptr(res), ptr(y), nb, h, w, 3 * cp, cp, k, r, s,
+                                         p, q, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)),
+                                         ldy, _s()), "conv_fwd_f32out2")
+
+
 def _nhwc_rows(x: torch.Tensor) -> torch.Tensor:
     """[N][C][H][W] fp32 → its channels-last storage as a [N·H·W][C] matrix."""
     xc = x.contiguous(memory_format=_cl)
@@ -95,8 +123,8 @@ def _fits(*nbytes) -> bool:
     return all(b < 0x80000000 for b in nbytes)  # 32-bit buffer offsets in the conv kernels
 
 
-def _slot_key(x, cp):
-    return ("bf16x3", x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), cp)
+def _slot_key(x, cp, two):
+    return ("bf16x3", x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), cp, two)
 
 
 def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, slot=None):
@@ -111,9 +139,10 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     cp, kq = _r(c, 8), _r(k, 4)
     if p <= 0 or q <= 0 or not _fits(nb * h * w * 3 * cp * 2, kq * r * s * 3 * cp * 2):
         return NotImplemented
-    x3 = split(_nhwc_rows(x), cp, HHL, False)
+    two = _two_part()
+    x3 = _act_split(_nhwc_rows(x), cp, two)
     if slot is not None:
-        slot[0] = (_slot_key(x, cp), x3)
+        slot[0] = (_slot_key(x, cp, two), x3)
     wk = w4.detach().float().permute(0, 2, 3, 1).reshape(k * r * s, c)
     w3 = torch.zeros((kq * r * s, 3 * cp), dtype=_bf16, device=x.device) if kq != k else None
     w3 = split(wk, cp, HLH, False, out=w3)
@@ -122,7 +151,10 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
         bias = torch.zeros(kq, dtype=_f32, device=x.device)
         bias[:k] = b.detach().float().reshape(-1)
     y = torch.empty((nb, kq, p, q), dtype=_f32, device=x.device, memory_format=_cl)
-    _conv_f32out(x3, w3, bias, y, nb, h, w, 3 * cp, kq, r, s, p, q, stride, pad, dilation, relu, kq)
+    if two:
+        _conv_f32out2(x3, w3, bias, y, nb, h, w, cp, kq, r, s, p, q, stride, pad, dilation, relu, kq)
+    else:
+        _conv_f32out(x3, w3, bias, y, nb, h, w, 3 * cp, kq, r, s, p, q, stride, pad, dilation, relu, kq)
     if kq != k:
         y = y[:, :k].contiguous(memory_format=_cl)
     return y
@@ -138,6 +170,7 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     p, q = gy.shape[2], gy.shape[3]
     kp, cq, cp = _r(k, 8), _r(c, 4), _r(c, 8)
     gi = None
+    two = _two_part()
     if need_input:
         hl, wl = h + 2 * pad[0] - dilation[0] * (r - 1), w + 2 * pad[1] - dilation[1] * (s - 1)
         pd = (dilation[0] * (r - 1) - pad[0], dilation[1] * (s - 1) - pad[1])
@@ -149,7 +182,7 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
             src[:, :, ::stride[0], ::stride[1]] = gy
         elif (hl, wl) != (p, q):
             return NotImplemented
-        g3 = split(_nhwc_rows(src), kp, HHL, False)
+        g3 = _act_split(_nhwc_rows(src), kp, two)
         wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c * r * s, k)  # [C][R][S][K]
         wt3 = torch.zeros((cq * r * s, 3 * kp), dtype=_bf16, device=x.device) if cq != c else None
         wt3 = split(wt, kp, HLH, False, out=wt3)
@@ -157,32 +190,38 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         # the shortcut's gradient summed in the epilogue (one pass fewer than a separate add)
         fuse_res = (residual is not None and cq == c and residual.dtype == _f32 and tuple(residual.shape) == (nb, c, h, w)
                     and residual.is_contiguous(memory_format=_cl) and residual.data_ptr() % 16 == 0)
-        _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
-                     res=residual if fuse_res else None)
+        if two:
+            _conv_f32out2(g3, wt3, None, gi, nb, hl, wl, kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
+                          res=residual if fuse_res else None)
+        else:
+            _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
+                         res=residual if fuse_res else None)
         if cq != c:
             gi = gi[:, :c].contiguous(memory_format=_cl)
         if residual is not None and not fuse_res:
             gi.add_(residual)
     if gw_acc is not None and scale != 0:
         # three launches over the side-by-side parts — (x_hi, dY_hi), (x_hi, dY_lo), (x_lo, dY_hi) —
-        # each a channel slice (pixel stride 3·Cp / 3·Kp) of the [hi | hi | lo] splits; a stride-1
-        # conv reuses the data gradient's split of dY
-        if not _fits(nb * h * w * 3 * cp * 2, nb * p * q * 3 * kp * 2):
+        # each a channel slice (pixel stride 2·Cp / 2·Kp of the [hi | lo] splits, 3·Cp / 3·Kp of the
+        # three-part ones); a stride-1 conv reuses the data gradient's split of dY
+        npart = 2 if two else 3
+        if not _fits(nb * h * w * npart * cp * 2, nb * p * q * npart * kp * 2):
             return NotImplemented
         held = slot[0] if slot is not None else None
-        if isinstance(held, tuple) and len(held) == 2 and held[0] == _slot_key(x, cp):
+        if isinstance(held, tuple) and len(held) == 2 and held[0] == _slot_key(x, cp, two):
             x3 = held[1]  # the forward's split of this same input
             slot[0] = None
         else:
-            x3 = split(_nhwc_rows(x), cp, HHL, False)
-        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else split(_nhwc_rows(gy), kp, HHL, False)
+            x3 = _act_split(_nhwc_rows(x), cp, two)
+        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else _act_split(_nhwc_rows(gy), kp, two)
         direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)
         sc = C.c_float(float(scale) if direct else 1.0)
-        for xq, gq in ((0, 0), (0, 2), (2, 0)):
+        lo = npart - 1  # the lo part's index in the stored split
+        for xq, gq in ((0, 0), (0, lo), (lo, 0)):
             check(N.lib().bigdl_conv_wgrad_grouped(C.c_void_p(x3.data_ptr() + 2 * xq * cp),
                                                    C.c_void_p(gy3.data_ptr() + 2 * gq * kp), ptr(target), sc, nb, h,
-                                                   w, 3 * cp, cp, 3 * kp, kp, 1, r, s, p, q, stride[0], stride[1],
+                                                   w, npart * cp, cp, npart * kp, kp, 1, r, s, p, q, stride[0], stride[1],
                                                    pad[0], pad[1], dilation[0], dilation[1], _s()),
                   "conv_wgrad(bf16x3)")
         if not direct:
@@ -225,6 +264,7 @@ def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1
     k = x.shape[1]
     n8, k4, k8 = _r(n, 8), _r(k, 4), _r(k, 8)
     gi = None
+    two = _two_part()
     if need_input:
         g3 = split(gy, n8, HHL, False)
         wt3 = split(w.detach().float().t(), n8, HLH, False,

@@ -60,6 +60,7 @@ _REGISTRY = {
     "bigdl.step.overlapMinMs": (float, 8.0, "enable the high-priority step stream and async wgrad once the measured step period is at least this long (GPU-bound steps; launch-bound ones lose to the extra host work)"),
     "bigdl.step.highPriority": (bool, True, "run each GPU training iteration on a high-priority HIP stream (the critical path outranks side-stream wgrad work)"),
     "bigdl.fp32.native": (bool, True, "fp32 compute on a GPU: convolutions and Linear run the bf16x3 split on the MFMA kernels (ops/fp32x3.py; ≤2^-16 relative per product) instead of torch/MIOpen fp32"),
+    "bigdl.fp32.twoPart": (bool, True, "fp32 compute: activation splits stored as [hi | lo] and read by the conv kernels as [hi | hi | lo] (ConvParams::cdup); false = the three-part [hi | hi | lo] buffers"),
     "bigdl.compile.trainAutotune": (bool, True, "training compile phase: the first GPU training iteration records its conv launches (forward, backward-data, weight-gradient) and pins the fastest kernel candidate per geometry"),
     "bigdl.compile.autotune": (bool, True, "nn.compiled.compile on a GPU (inference): time every implicit-GEMM conv tile candidate per conv geometry and pin the fastest (kernel selection)"),
     "bigdl.conv.asyncWgrad": (bool, True, "inside optimizer steps run conv backward-weight kernels on a second HIP stream, overlapping the backward-data / BatchNorm chain"),

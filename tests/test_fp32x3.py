@@ -28,6 +28,9 @@ def test_split_matches_torch_rounding():
     st = F3.split(x, 24, F3.HLH, True).cpu()
     assert torch.equal(st[0:37, :21], hi.cpu()) and torch.equal(st[37:74, :21], lo.cpu())
     assert torch.equal(st[74:111, :21], hi.cpu())
+    two = F3.split2(x, 24).cpu()  # [hi | lo], each zero-padded to 24
+    assert torch.equal(two[:, 0:21], hi.cpu()) and torch.equal(two[:, 24:45], lo.cpu())
+    assert two.shape == (37, 48) and two[:, 21:24].abs().sum() == 0 and two[:, 45:48].abs().sum() == 0
     rec = hi.double() + lo.double()
     assert float(((rec - x.double()).abs() / x.double().abs().clamp_min(1e-30)).max()) < 2 ** -16
 
@@ -39,8 +42,19 @@ def test_split_matches_torch_rounding():
     (2, 16, 20, 10, 10, 3, 1, 2, 2),     # dilated, K % 8 != 0
     (2, 24, 8, 15, 15, 3, 2, 1, 1),
 ])
-def test_conv_fp32x3_matches_fp64(N, C, K, H, W, k, s, p, d):
+@pytest.mark.parametrize("two", [True, False], ids=["hi_lo", "hi_hi_lo"])
+def test_conv_fp32x3_matches_fp64(N, C, K, H, W, k, s, p, d, two):
     from bigdl.ops import fp32x3 as F3
+    from bigdl.utils import config
+    prev = config.get_property("bigdl.fp32.twoPart")
+    config.set_property("bigdl.fp32.twoPart", two)
+    try:
+        _conv_case(F3, N, C, K, H, W, k, s, p, d)
+    finally:
+        config.set_property("bigdl.fp32.twoPart", prev)
+
+
+def _conv_case(F3, N, C, K, H, W, k, s, p, d):
     g = torch.Generator().manual_seed(1)
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(K, C, k, k, generator=g) * (1.0 / (C * k * k) ** 0.5)
