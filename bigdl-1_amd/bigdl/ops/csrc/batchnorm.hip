@@ -1130,7 +1130,7 @@ template <bool BWD, bool RELU>
 __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x, const float* __restrict__ aux,
                                                     const float* __restrict__ y_mask, float* __restrict__ out,
                                                     float* __restrict__ gres, long long M, int C,
-                                                    const float* __restrict__ coef) {
+                                                    const float* __restrict__ coef, bf16_t* __restrict__ sp = nullptr) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -1171,6 +1171,19 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
         }
       }
       if (out) st8f(out + off, o);
+      if (sp) {  // the bf16x3 [hi | lo] split of the output for the consuming conv (fp32x3.py split2)
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16_t h0 = f2bf(o[2 * e]), h1 = f2bf(o[2 * e + 1]);
+          const bf16_t l0 = f2bf(o[2 * e] - bf2f(h0)), l1 = f2bf(o[2 * e + 1] - bf2f(h1));
+          hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          lw[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+        }
+        bf16_t* d = sp + (size_t)r * 2 * C + (size_t)cg * 8;
+        *reinterpret_cast<uint4*>(d) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        *reinterpret_cast<uint4*>(d + C) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      }
     }
   }
 }
@@ -1180,8 +1193,10 @@ static bool bn32_ok(const void* p) { return ((uintptr_t)p & 15) == 0; }
 BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y, long long M, int C,
                                       const float* gamma, const float* beta, const float* in_bias, float* run_mean,
                                       float* run_var, float momentum, float eps, float* save_mean, float* save_invstd,
-                                      float* ws, float* coef, int relu, hipStream_t s) {
-  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res))) return (int)hipErrorInvalidValue;
+                                      float* ws, float* coef, int relu, void* split, hipStream_t s) {
+  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res)) || (split && !bn32_ok(split)))
+    return (int)hipErrorInvalidValue;
+  bf16_t* sp = (bf16_t*)split;
   const int G = bigdl_bn_num_partials(M, C);
   const long long rpb = (M + G - 1) / G;
   const size_t sm = stats_smem(C);
@@ -1192,9 +1207,11 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y
                      save_invstd, coef, coef + C);
   const int grid = apply_grid(M, C);
   if (relu)
-    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef);
+    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
+                       sp);
   else
-    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef);
+    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
+                       sp);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -1217,10 +1234,11 @@ BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int
 BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y, float* gx, float* gres, long long M,
                                 int C, const float* gamma, const float* mean, const float* invstd, float* ggamma,
                                 float* gbeta, float gscale, float* cbias, float cbscale, float* ws, float* coef,
-                                int relu, hipStream_t s) {
+                                int relu, void* split, hipStream_t s) {
   if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(gy) || (relu && (!y || !bn32_ok(y))) || (gx && !bn32_ok(gx)) ||
-      (gres && !bn32_ok(gres)))
+      (gres && !bn32_ok(gres)) || (split && (!gx || !bn32_ok(split))))
     return (int)hipErrorInvalidValue;
+  bf16_t* sp = (bf16_t*)split;
   const int G = bigdl_bn_num_partials(M, C);
   const long long rpb = (M + G - 1) / G;
   const size_t sm = stats_smem(C);
@@ -1234,9 +1252,9 @@ BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y,
   if (gx || gres) {
     const int grid = apply_grid(M, C);
     if (relu)
-      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef);
+      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp);
     else
-      hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef);
+      hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp);
   }
   BIGDL_CHECK_LAUNCH();
 }

@@ -24,6 +24,7 @@ off (torch / MIOpen fp32 everywhere).
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import torch
 
@@ -86,8 +87,46 @@ def _two_part() -> bool:
     return bool(config.get_property("bigdl.fp32.twoPart"))
 
 
-def _act_split(rows2d, cp, two):
-    return split2(rows2d, cp) if two else split(rows2d, cp, HHL, False)
+# Splits written by the PRODUCER of an activation (the fp32 BN apply pass emits the [hi | lo] operand of
+# the conv that consumes its output, forward and backward), keyed by the tensor's memory and checked
+# against a weak reference to it (alive ⇒ the memory is not reused) and its version counter (shared by
+# views: an in-place write invalidates the entry).
+_SPLITS: dict = {}
+
+
+def split_buffer(rows, c, device):
+    """A [rows][2·c] bf16 buffer for a producer-side split, or None when the path is off."""
+    if c % 8 or not _two_part() or not config.get_property("bigdl.fp32.producerSplit"):
+        return None
+    return torch.empty((rows, 2 * c), dtype=_bf16, device=device)
+
+
+def note_split(t, sp):
+    if sp is None or t is None:
+        return
+    key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
+    _SPLITS[key] = (weakref.ref(t, lambda _r, k=key: _SPLITS.pop(k, None)), t._version, sp)
+
+
+def _producer_split(t, cp):
+    if t is None or t.dim() != 4 or t.shape[1] != cp:
+        return None
+    key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
+    e = _SPLITS.get(key)
+    if e is None:
+        return None
+    ref, ver, sp = e
+    if ref() is None or t._version != ver:
+        _SPLITS.pop(key, None)
+        return None
+    return sp
+
+
+def _act_split(rows2d, cp, two, src=None):
+    if two:
+        sp = _producer_split(src, cp)
+        return sp if sp is not None else split2(rows2d, cp)
+    return split(rows2d, cp, HHL, False)
 
 
 def _conv_f32out2(x2, w3, bias, y, nb, h, w, cp, k, r, s, p, q, stride, pad, dil, relu, ldy, res=None):
@@ -140,7 +179,7 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     if p <= 0 or q <= 0 or not _fits(nb * h * w * 3 * cp * 2, kq * r * s * 3 * cp * 2):
         return NotImplemented
     two = _two_part()
-    x3 = _act_split(_nhwc_rows(x), cp, two)
+    x3 = _act_split(_nhwc_rows(x), cp, two, x)
     if slot is not None:
         slot[0] = (_slot_key(x, cp, two), x3)
     wk = w4.detach().float().permute(0, 2, 3, 1).reshape(k * r * s, c)
@@ -182,7 +221,7 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
             src[:, :, ::stride[0], ::stride[1]] = gy
         elif (hl, wl) != (p, q):
             return NotImplemented
-        g3 = _act_split(_nhwc_rows(src), kp, two)
+        g3 = _act_split(_nhwc_rows(src), kp, two, src)
         wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c * r * s, k)  # [C][R][S][K]
         wt3 = torch.zeros((cq * r * s, 3 * kp), dtype=_bf16, device=x.device) if cq != c else None
         wt3 = split(wt, kp, HLH, False, out=wt3)
@@ -212,8 +251,8 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
             x3 = held[1]  # the forward's split of this same input
             slot[0] = None
         else:
-            x3 = _act_split(_nhwc_rows(x), cp, two)
-        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else _act_split(_nhwc_rows(gy), kp, two)
+            x3 = _act_split(_nhwc_rows(x), cp, two, x)
+        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else _act_split(_nhwc_rows(gy), kp, two, gy)
         direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)
         sc = C.c_float(float(scale) if direct else 1.0)

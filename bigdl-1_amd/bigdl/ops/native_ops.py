@@ -131,10 +131,12 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
         mean = torch.empty(C_, dtype=_f32, device=x.device)
         invstd = torch.empty(C_, dtype=_f32, device=x.device)
         y = torch.empty_like(x)
+        sp = F3.split_buffer(M, C_, x.device)  # the next conv's [hi | lo] operand, written by the apply pass
         check(_lib().bigdl_bn32_fwd_train(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
                                           ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum), _f(eps),
-                                          ptr(mean), ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0), _s()),
-              "bn32_fwd_train")
+                                          ptr(mean), ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
+                                          ptr(sp), _s()), "bn32_fwd_train")
+        F3.note_split(y, sp)
         return y, mean, invstd
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
@@ -404,10 +406,12 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
         coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
         gx = torch.empty_like(x) if need_input else None
         gres = torch.empty_like(x) if want_gres else None
+        sp = F3.split_buffer(M, C_, x.device) if need_input else None  # the producing conv's dY split
         check(_lib().bigdl_bn32_bwd(ptr(gy), ptr(x), ptr(y if relu else None), ptr(gx), ptr(gres), _ll(M), C.c_int(C_),
                                     ptr(gamma), ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
                                     ptr(cbias_acc), _f(cbias_scale), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
-                                    _s()), "bn32_bwd")
+                                    ptr(sp), _s()), "bn32_bwd")
+        F3.note_split(gx, sp)
         return gx, gres
     if not _bn_ok(x, C_) or gy.dtype != _bf16 or gy.shape != x.shape or gy.stride() != x.stride() or not _al16(gy):
         return NotImplemented

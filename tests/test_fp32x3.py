@@ -171,3 +171,38 @@ def test_bn32_native_matches_reference(relu, res):
     assert _rel(gx, out[0]) < 1e-4 and _rel(gg, ggr) < 1e-5 and _rel(gb, gbr) < 1e-5
     if res:
         assert _rel(gres, gy.double() * (yr > 0)) < 1e-6
+    # the apply passes also wrote the consuming conv's [hi | lo] operand (producer-side split): it is
+    # exactly the split pass's output, and the conv finds it
+    from bigdl.ops import fp32x3 as F3
+    for t in (y, gx):
+        sp = F3._producer_split(t, C_)
+        assert sp is not None
+        assert torch.equal(sp, F3.split2(F3._nhwc_rows(t), C_))
+
+
+def test_fp32_conv_uses_producer_split():
+    """A BN → conv chain in fp32 gives bit-identical results with the producer-side split on and off,
+    and the conv launches one split pass fewer."""
+    from bigdl.ops import native_ops as NO, fp32x3 as F3
+    from bigdl.utils import config
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 12, 12, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(32, 64, 3, 3, generator=g) * 0.05).to(dev)
+    gam, bet = torch.rand(64, generator=g).to(dev) + 0.5, torch.randn(64, generator=g).to(dev)
+    outs = []
+    for on in (True, False):
+        config.set_property("bigdl.fp32.producerSplit", on)
+        try:
+            h, _, _ = NO.batchnorm_forward_train(x, gam, bet, torch.zeros(64, device=dev), torch.ones(64, device=dev),
+                                                 0.1, 1e-5, True)
+            hit = F3._producer_split(h, 64) is not None
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+                y = F3.conv_forward(h, w, None, (1, 1), (1, 1))
+                torch.cuda.synchronize()
+            n_split = sum(1 for e in prof.events() if "k_split_bf16x3" in e.name)
+            outs.append((y.clone(), hit, n_split))
+        finally:
+            config.set_property("bigdl.fp32.producerSplit", True)
+    (y1, hit1, n1), (y0, hit0, n0) = outs
+    assert hit1 and not hit0 and n1 == n0 - 1, (hit1, hit0, n1, n0)
+    assert torch.equal(y1, y0)
