@@ -1062,7 +1062,8 @@ template <int MODE, bool RELU>
 __global__ void __launch_bounds__(256) k_bn32_reduce(const float* __restrict__ x, const float* __restrict__ gy,
                                                      const float* __restrict__ y, long long M, int C,
                                                      long long rows_per_block, const float* __restrict__ ref,
-                                                     float* __restrict__ partial, int G) {
+                                                     float* __restrict__ partial, int G,
+                                                     const uint8_t* __restrict__ mbits = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
@@ -1093,10 +1094,16 @@ __global__ void __launch_bounds__(256) k_bn32_reduce(const float* __restrict__ x
           float gv[8];
           ld8f(gy + off, gv);
           if (RELU) {
-            float yv[8];
-            ld8f(y + off, yv);
+            if (mbits) {  // the forward's ReLU mask, one bit per element (8 channels per byte)
+              const unsigned mb = mbits[(size_t)r * (C >> 3) + cg];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+              for (int k = 0; k < 8; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
+            } else {
+              float yv[8];
+              ld8f(y + off, yv);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+            }
           }
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -1130,7 +1137,8 @@ template <bool BWD, bool RELU>
 __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x, const float* __restrict__ aux,
                                                     const float* __restrict__ y_mask, float* __restrict__ out,
                                                     float* __restrict__ gres, long long M, int C,
-                                                    const float* __restrict__ coef, bf16_t* __restrict__ sp = nullptr) {
+                                                    const float* __restrict__ coef, bf16_t* __restrict__ sp = nullptr,
+                                                    uint8_t* __restrict__ mbits = nullptr) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -1153,10 +1161,16 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
         float gv[8];
         ld8f(aux + off, gv);
         if (RELU) {
-          float yv[8];
-          ld8f(y_mask + off, yv);
+          if (mbits) {
+            const unsigned mb = mbits[(size_t)r * (C >> 3) + cg];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+            for (int k = 0; k < 8; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
+          } else {
+            float yv[8];
+            ld8f(y_mask + off, yv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+          }
         }
         if (gres) st8f(gres + off, gv);
 #pragma unroll
@@ -1168,6 +1182,12 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
         for (int k = 0; k < 8; ++k) {
           const float v = fmaf(xv[k], A[k], B[k]) + rv[k];
           o[k] = RELU ? fmaxf(v, 0.f) : v;
+        }
+        if (RELU && mbits) {  // the ReLU mask as bits for the backward (instead of re-reading y)
+          unsigned mb = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) mb |= (o[k] > 0.f ? 1u : 0u) << k;
+          mbits[(size_t)r * (C >> 3) + cg] = (uint8_t)mb;
         }
       }
       if (out) st8f(out + off, o);
@@ -1193,7 +1213,7 @@ static bool bn32_ok(const void* p) { return ((uintptr_t)p & 15) == 0; }
 BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y, long long M, int C,
                                       const float* gamma, const float* beta, const float* in_bias, float* run_mean,
                                       float* run_var, float momentum, float eps, float* save_mean, float* save_invstd,
-                                      float* ws, float* coef, int relu, void* split, hipStream_t s) {
+                                      float* ws, float* coef, int relu, void* split, void* bits, hipStream_t s) {
   if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res)) || (split && !bn32_ok(split)))
     return (int)hipErrorInvalidValue;
   bf16_t* sp = (bf16_t*)split;
@@ -1208,7 +1228,7 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y
   const int grid = apply_grid(M, C);
   if (relu)
     hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
-                       sp);
+                       sp, (uint8_t*)bits);
   else
     hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
                        sp);
@@ -1234,8 +1254,8 @@ BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int
 BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y, float* gx, float* gres, long long M,
                                 int C, const float* gamma, const float* mean, const float* invstd, float* ggamma,
                                 float* gbeta, float gscale, float* cbias, float cbscale, float* ws, float* coef,
-                                int relu, void* split, hipStream_t s) {
-  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(gy) || (relu && (!y || !bn32_ok(y))) || (gx && !bn32_ok(gx)) ||
+                                int relu, void* split, const void* bits, hipStream_t s) {
+  if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(gy) || (relu && !bits && (!y || !bn32_ok(y))) || (gx && !bn32_ok(gx)) ||
       (gres && !bn32_ok(gres)) || (split && (!gx || !bn32_ok(split))))
     return (int)hipErrorInvalidValue;
   bf16_t* sp = (bf16_t*)split;
@@ -1243,8 +1263,9 @@ BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y,
   const long long rpb = (M + G - 1) / G;
   const size_t sm = stats_smem(C);
   if (sm > 64 * 1024) return (int)hipErrorInvalidValue;
+  uint8_t* mb = (uint8_t*)bits;
   if (relu)
-    hipLaunchKernelGGL((k_bn32_reduce<1, true>), dim3(G), dim3(256), sm, s, x, gy, y, M, C, rpb, mean, ws, G);
+    hipLaunchKernelGGL((k_bn32_reduce<1, true>), dim3(G), dim3(256), sm, s, x, gy, y, M, C, rpb, mean, ws, G, mb);
   else
     hipLaunchKernelGGL((k_bn32_reduce<1, false>), dim3(G), dim3(256), sm, s, x, gy, y, M, C, rpb, mean, ws, G);
   hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)ws, G, M, C,
@@ -1252,7 +1273,8 @@ BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y,
   if (gx || gres) {
     const int grid = apply_grid(M, C);
     if (relu)
-      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp);
+      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp,
+                         mb);
     else
       hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp);
   }

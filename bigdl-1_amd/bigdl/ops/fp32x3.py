@@ -101,25 +101,38 @@ def split_buffer(rows, c, device):
     return torch.empty((rows, 2 * c), dtype=_bf16, device=device)
 
 
-def note_split(t, sp):
-    if sp is None or t is None:
+def note_split(t, sp, bits=None):
+    """Register producer-side by-products of ``t``: its [hi | lo] split and/or its ReLU mask bits."""
+    if t is None or (sp is None and bits is None):
         return
     key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
-    _SPLITS[key] = (weakref.ref(t, lambda _r, k=key: _SPLITS.pop(k, None)), t._version, sp)
+    _SPLITS[key] = (weakref.ref(t, lambda _r, k=key: _SPLITS.pop(k, None)), t._version, sp, bits)
 
 
-def _producer_split(t, cp):
-    if t is None or t.dim() != 4 or t.shape[1] != cp:
+def _entry(t):
+    if t is None or not isinstance(t, torch.Tensor):
         return None
     key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
     e = _SPLITS.get(key)
     if e is None:
         return None
-    ref, ver, sp = e
-    if ref() is None or t._version != ver:
+    if e[0]() is None or t._version != e[1]:
         _SPLITS.pop(key, None)
         return None
-    return sp
+    return e
+
+
+def _producer_split(t, cp):
+    if t is None or t.dim() != 4 or t.shape[1] != cp:
+        return None
+    e = _entry(t)
+    return None if e is None else e[2]
+
+
+def producer_bits(t):
+    """The ReLU mask bits the fp32 BN forward wrote for its output ``t`` (None if absent)."""
+    e = _entry(t)
+    return None if e is None else e[3]
 
 
 def _act_split(rows2d, cp, two, src=None):

@@ -132,11 +132,12 @@ def batchnorm_forward_train(x, gamma, beta, running_mean, running_var, momentum,
         invstd = torch.empty(C_, dtype=_f32, device=x.device)
         y = torch.empty_like(x)
         sp = F3.split_buffer(M, C_, x.device)  # the next conv's [hi | lo] operand, written by the apply pass
+        mb = torch.empty(M * (C_ // 8), dtype=torch.uint8, device=x.device) if relu else None  # ReLU mask bits
         check(_lib().bigdl_bn32_fwd_train(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
                                           ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum), _f(eps),
                                           ptr(mean), ptr(invstd), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
-                                          ptr(sp), _s()), "bn32_fwd_train")
-        F3.note_split(y, sp)
+                                          ptr(sp), ptr(mb), _s()), "bn32_fwd_train")
+        F3.note_split(y, sp, mb)
         return y, mean, invstd
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
@@ -399,7 +400,8 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
     if rc is None:
         return NotImplemented
     M, C_ = rc
-    if (_bn32_ok(x, C_, gy, y if relu else None) and (y is not None or not relu)
+    mb = F3.producer_bits(y) if relu else None  # the forward's ReLU mask bits (1 bit instead of 4 B)
+    if (_bn32_ok(x, C_, gy, y if relu and mb is None else None) and (y is not None or not relu)
             and all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc))):
         G = _lib().bigdl_bn_num_partials(_ll(M), C.c_int(C_))
         ws = torch.empty(2 * G * C_, dtype=_f32, device=x.device)
@@ -410,7 +412,7 @@ def batchnorm_backward(gy, x, gamma, save_mean, save_invstd, y=None, relu=False,
         check(_lib().bigdl_bn32_bwd(ptr(gy), ptr(x), ptr(y if relu else None), ptr(gx), ptr(gres), _ll(M), C.c_int(C_),
                                     ptr(gamma), ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
                                     ptr(cbias_acc), _f(cbias_scale), ptr(ws), ptr(coef), C.c_int(1 if relu else 0),
-                                    ptr(sp), _s()), "bn32_bwd")
+                                    ptr(sp), ptr(mb), _s()), "bn32_bwd")
         F3.note_split(gx, sp)
         return gx, gres
     if not _bn_ok(x, C_) or gy.dtype != _bf16 or gy.shape != x.shape or gy.stride() != x.stride() or not _al16(gy):

@@ -171,6 +171,12 @@ def test_bn32_native_matches_reference(relu, res):
     assert _rel(gx, out[0]) < 1e-4 and _rel(gg, ggr) < 1e-5 and _rel(gb, gbr) < 1e-5
     if res:
         assert _rel(gres, gy.double() * (yr > 0)) < 1e-6
+    if relu:  # the backward read the forward's mask bits; the y-reading path (no bits for a copy of y) agrees exactly
+        from bigdl.ops import fp32x3 as F3
+        assert F3.producer_bits(y) is not None and F3.producer_bits(y.clone()) is None
+        gx2, _ = NO.batchnorm_backward(gy.to(dev), x.to(dev), gam.to(dev), m, inv, y.clone(), relu, True,
+                                       torch.zeros(C_, device=dev), torch.zeros(C_, device=dev), 1.0)
+        assert torch.equal(gx2, gx)
     # the apply passes also wrote the consuming conv's [hi | lo] operand (producer-side split): it is
     # exactly the split pass's output, and the conv finds it
     from bigdl.ops import fp32x3 as F3
