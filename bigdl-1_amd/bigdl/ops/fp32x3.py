@@ -171,6 +171,10 @@ def _out_hw(h, w, r, s, stride, pad, dil):
             (w + 2 * pad[1] - dil[1] * (s - 1) - 1) // stride[1] + 1)
 
 
+#: bytes one conv operand may span (32-bit buffer offsets in the conv kernels)
+_OPERAND_LIMIT = 0x7fffffff
+
+
 def _fits(*nbytes) -> bool:
     return all(b < 0x80000000 for b in nbytes)  # 32-bit buffer offsets in the conv kernels
 
@@ -223,18 +227,24 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     kp, cq, cp = _r(k, 8), _r(c, 4), _r(c, 8)
     gi = None
     two = _two_part()
+    g3 = None
     if need_input:
         hl, wl = h + 2 * pad[0] - dilation[0] * (r - 1), w + 2 * pad[1] - dilation[1] * (s - 1)
         pd = (dilation[0] * (r - 1) - pad[0], dilation[1] * (s - 1) - pad[1])
-        if pd[0] < 0 or pd[1] < 0 or not _fits(nb * hl * wl * 3 * kp * 2, cq * r * s * 3 * kp * 2):
+        npart = 2 if two else 3
+        if pd[0] < 0 or pd[1] < 0 or not _fits(hl * wl * npart * kp * 2, cq * r * s * 3 * kp * 2):
             return NotImplemented
-        src = gy
-        if tuple(stride) != (1, 1):  # dY on the stride lattice (zeros between), then a stride-1 conv
-            src = torch.empty((nb, k, hl, wl), dtype=_f32, device=gy.device, memory_format=_cl).zero_()
-            src[:, :, ::stride[0], ::stride[1]] = gy
-        elif (hl, wl) != (p, q):
+        strided = tuple(stride) != (1, 1)
+        if not strided and (hl, wl) != (p, q):
             return NotImplemented
-        g3 = _act_split(_nhwc_rows(src), kp, two, src)
+        # images per launch: the dY operand must stay below the kernels' 2 GiB buffer offsets (the
+        # 224² stem's lattice at batch 256 does not), so large batches run in image chunks
+        nbc = min(nb, _OPERAND_LIMIT // (hl * wl * npart * kp * 2))
+        if nbc < nb and cq <= 4:
+            # the RGB stem at ImageNet batch sizes: a 4-channel data gradient leaves the MFMA tiles almost
+            # idle and the lattice + splits cost more than torch's fp32 kernel (measured 1.8 vs 0.9 ms/step
+            # for data + weight gradient, profiles/r4_fp32_profile.txt), so that one conv stays on torch
+            return NotImplemented
         wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c * r * s, k)  # [C][R][S][K]
         wt3 = torch.zeros((cq * r * s, 3 * kp), dtype=_bf16, device=x.device) if cq != c else None
         wt3 = split(wt, kp, HLH, False, out=wt3)
@@ -242,12 +252,29 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         # the shortcut's gradient summed in the epilogue (one pass fewer than a separate add)
         fuse_res = (residual is not None and cq == c and residual.dtype == _f32 and tuple(residual.shape) == (nb, c, h, w)
                     and residual.is_contiguous(memory_format=_cl) and residual.data_ptr() % 16 == 0)
-        if two:
-            _conv_f32out2(g3, wt3, None, gi, nb, hl, wl, kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
-                          res=residual if fuse_res else None)
-        else:
-            _conv_f32out(g3, wt3, None, gi, nb, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation, False, cq,
-                         res=residual if fuse_res else None)
+        whole = _producer_split(gy, kp) if (two and not strided) else None
+        for i0 in range(0, nb, nbc):
+            i1 = min(nb, i0 + nbc)
+            gyc = gy if (i0, i1) == (0, nb) else gy[i0:i1]
+            if strided:  # dY on the stride lattice (zeros between), then a stride-1 conv
+                src = torch.empty((i1 - i0, k, hl, wl), dtype=_f32, device=gy.device, memory_format=_cl).zero_()
+                src[:, :, ::stride[0], ::stride[1]] = gyc
+            else:
+                src = gyc
+            if whole is not None:
+                g3c = whole[i0 * p * q:i1 * p * q]
+            else:
+                g3c = _act_split(_nhwc_rows(src), kp, two, src)
+            gic = gi if (i0, i1) == (0, nb) else gi[i0:i1]
+            resc = (residual if (i0, i1) == (0, nb) else residual[i0:i1]) if fuse_res else None
+            if two:
+                _conv_f32out2(g3c, wt3, None, gic, i1 - i0, hl, wl, kp, cq, r, s, h, w, (1, 1), pd, dilation, False,
+                              cq, res=resc)
+            else:
+                _conv_f32out(g3c, wt3, None, gic, i1 - i0, hl, wl, 3 * kp, cq, r, s, h, w, (1, 1), pd, dilation,
+                             False, cq, res=resc)
+            if (i0, i1) == (0, nb) and not strided:
+                g3 = g3c  # the wgrad reuses the whole dY split
         if cq != c:
             gi = gi[:, :c].contiguous(memory_format=_cl)
         if residual is not None and not fuse_res:
@@ -265,7 +292,7 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
             slot[0] = None
         else:
             x3 = _act_split(_nhwc_rows(x), cp, two, x)
-        gy3 = g3 if (need_input and tuple(stride) == (1, 1)) else _act_split(_nhwc_rows(gy), kp, two, gy)
+        gy3 = g3 if g3 is not None else _act_split(_nhwc_rows(gy), kp, two, gy)
         direct = cp == c and kp == k and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
         target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((kp, r, s, cp), dtype=_f32, device=x.device)
         sc = C.c_float(float(scale) if direct else 1.0)

@@ -212,3 +212,26 @@ def test_fp32_conv_uses_producer_split():
     (y1, hit1, n1), (y0, hit0, n0) = outs
     assert hit1 and not hit0 and n1 == n0 - 1, (hit1, hit0, n1, n0)
     assert torch.equal(y1, y0)
+
+
+@pytest.mark.parametrize("s", [1, 2])
+def test_conv_fp32x3_dgrad_in_image_chunks(s, monkeypatch):
+    """A data gradient whose dY operand exceeds the kernels' 32-bit offsets (the 224² stem at batch 256)
+    runs in image chunks: forced here with a small limit, checked against fp64."""
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(7)
+    N, C, K, H, W = 5, 16, 32, 12, 12
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) * (1.0 / (C * 9) ** 0.5)
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    yr = F.conv2d(xr, wr, None, s, 1)
+    gy = torch.randn(yr.shape, generator=g)
+    res = torch.randn(N, C, H, W, generator=g)
+    yr.backward(gy.double())
+    monkeypatch.setattr(F3, "_OPERAND_LIMIT", 2 * H * W * 2 * K * 2 + 7)  # 2 images per launch
+    gw = torch.zeros(K, 3, 3, C, device=dev).permute(0, 3, 1, 2)
+    gi = F3.conv_backward(gy.to(dev), x.to(dev), w.to(dev), (s, s), (1, 1), (1, 1), 1, True, gw, None, 1.0,
+                          residual=res.to(dev).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    assert _rel(gi, xr.grad + res.double()) < 2e-5
+    assert _rel(gw, wr.grad) < 2e-5
