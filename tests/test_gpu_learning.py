@@ -9,6 +9,18 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _deterministic():
+    """Bit-reproducible kernels (no split-K float atomics): with them these short, high-learning-rate
+    runs are chaotic — the same seed gave VGG-CIFAR eval accuracies from 0.12 to 0.64 across runs
+    (tools/vgg_flaky.py) — and a learning check must not depend on the reduction order."""
+    from bigdl.utils import config
+    prev = config.get_property("bigdl.deterministic")
+    config.set_property("bigdl.deterministic", True)
+    yield
+    config.set_property("bigdl.deterministic", prev)
+
+
 def _setup():
     from bigdl.utils.engine import Engine
     from bigdl.ops import native
