@@ -1235,6 +1235,32 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y
   BIGDL_CHECK_LAUNCH();
 }
 
+// fp32 training forward from the replicated statistics the producing fp32-output conv added
+// (bigdl_conv_fwd_f32out2_stats: [2][G][C], shifted by kshift, cleared here after reading): finalize +
+// apply (+ the consuming conv's split and the ReLU mask bits, as bigdl_bn32_fwd_train).
+BIGDL_EXPORT int bigdl_bn32_fwd_train_partials(const float* x, const float* res, float* y, long long M, int C,
+                                               const float* gamma, const float* beta, const float* in_bias,
+                                               float* run_mean, float* run_var, float momentum, float eps,
+                                               float* save_mean, float* save_invstd, float* partial, int G,
+                                               const float* kshift, float* coef, int relu, void* split, void* bits,
+                                               hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0 || G > 512 || !partial || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res)) ||
+      (split && !bn32_ok(split)))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
+                     (const float*)partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
+                     save_invstd, coef, coef + C, nullptr, partial);
+  const int grid = apply_grid(M, C);
+  bf16_t* sp = (bf16_t*)split;
+  if (relu)
+    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
+                       sp, (uint8_t*)bits);
+  else
+    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
+                       sp);
+  BIGDL_CHECK_LAUNCH();
+}
+
 BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int C, const float* gamma,
                                       const float* beta, const float* run_mean, const float* run_var,
                                       const float* in_bias, float eps, float* coef, int relu, hipStream_t s) {

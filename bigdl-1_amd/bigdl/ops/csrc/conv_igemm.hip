@@ -425,6 +425,46 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
   }
 
   if (p.y32) {  // fp32 output (uniform branch): 4 consecutive channels of one pixel per accumulator
+    if (p.stats) {
+      // BN statistics of the fp32 output (the fp32-compute conv → BN case; host-checked: no bias, ReLU or
+      // residual, replicated atomic sums): shifted by the prefetched running mean, summed over the lane's
+      // TM pixels, folded over the 16 pixel lanes of a DPP row, then one atomic per wave and channel into
+      // replica tm % R (ConvParams::stats_atomic)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const float live = (m0 + wave_m * (BM / 2) + j * 16 + fr < p.M) ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = live * (acc[i][j][e] - kpre[i][e]);
+            s4[e] += a;
+            q4[e] = fmaf(a, a, q4[e]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x128, 0xF, 0xF, false));
+          q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x128, 0xF, 0xF, false));
+          s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x124, 0xF, 0xF, false));
+          q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x124, 0xF, 0xF, false));
+          s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x122, 0xF, 0xF, false));
+          q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x122, 0xF, 0xF, false));
+          s4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s4[e]), 0x121, 0xF, 0xF, false));
+          q4[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q4[e]), 0x121, 0xF, 0xF, false));
+        }
+        const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
+        if (fr == 0 && n < p.K) {
+          const int rep = tm % p.stats_atomic;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            atomicAdd(&p.stats[(size_t)rep * p.K + n + e], s4[e]);
+            atomicAdd(&p.stats[((size_t)p.stats_atomic + rep) * p.K + n + e], q4[e]);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
@@ -580,8 +620,11 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   const bool c4 = C == 4;
   if (cdup && (cdup < 0 || cdup % 8 || 2 * cdup > C || c4 || ax || groups != 1 || !y32)) return (int)hipErrorInvalidValue;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
-  if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || stats || bnx || ax || groups != 1 || osh != 1 ||
+  if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || bnx || ax || groups != 1 || osh != 1 ||
               osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
+    return (int)hipErrorInvalidValue;
+  // fp32-output statistics: replicated atomic sums only, of the plain conv output
+  if (y32 && stats && (stats_atomic <= 0 || bias || relu || res32 || ldy != K || tile_bm == 256))
     return (int)hipErrorInvalidValue;
   if (ldx == 0) ldx = C - cdup;
   if (groups < 1 || ldx < C - cdup || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
@@ -866,6 +909,21 @@ BIGDL_EXPORT int bigdl_conv_fwd_f32out2(const void* x, const void* w, const floa
   return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
                          relu, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, ldy, s, 0, nullptr, 0, 0,
                          0, 0, nullptr, 2 * cdup, 1, nullptr, nullptr, y32, 0, 0, 0, 0, res32, cdup);
+}
+
+// bigdl_conv_fwd_f32out2 whose epilogue also ADDS the BN statistics Σ(y − shift), Σ(y − shift)² of its
+// fp32 output into R replicas (stats [2][R][K], zero on entry; ConvParams::stats_atomic = R) for the
+// following fp32 BN (bigdl_bn32_fwd_train_partials).  No bias / ReLU / residual.
+BIGDL_EXPORT int bigdl_conv_fwd_f32out2_stats(const void* x, const void* w, float* y32, float* stats, int R_rep,
+                                              const float* shift, int Nb, int H, int W, int C, int cdup, int K, int R,
+                                              int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                                              hipStream_t s) {
+  if (!y32 || !stats || R_rep <= 0 || cdup <= 0 || C != 3 * cdup || K % 8) return (int)hipErrorInvalidValue;
+  static const int bm_env = conv_env_override("BIGDL_CONV_BM", 128, 256);
+  if (bm_env == 256) return (int)hipErrorInvalidValue;  // the statistics need 128-row tiles (kpre prefetch)
+  return conv_fwd_launch(x, w, nullptr, nullptr, nullptr, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+                         0, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, 0, shift, 0, 0,
+                         0, 0, nullptr, 2 * cdup, 1, nullptr, nullptr, y32, 0, 0, 0, R_rep, nullptr, cdup);
 }
 
 // bigdl_conv_fwd_ldy / bigdl_conv_fwd_stats_shift with an explicit tile (bn, bk, bm; 0 = heuristic).

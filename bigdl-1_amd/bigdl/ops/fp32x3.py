@@ -216,6 +216,35 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     return y
 
 
+def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
+    """fp32 conv (no bias / ReLU) whose epilogue also ADDS the following BN's statistics
+    Σ(y − shift), Σ(y − shift)² into the BN's replicated buffer ``sums = (buf [2][R][K], R)``: returns
+    ``(y, buf, R)`` for ``batchnorm_forward_train_partials`` (which finalizes from the R rows and clears
+    them), or NotImplemented."""
+    if (x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1] or not _two_part() or not isinstance(sums, tuple)
+            or not config.get_property("bigdl.fp32.convStats")):
+        return NotImplemented
+    nb, c, h, w = x.shape
+    k, _, r, s = w4.shape
+    buf, rep = sums
+    if (k % 8 or shift is None or shift.dtype != _f32 or shift.numel() != k or not shift.is_contiguous()
+            or buf.dtype != _f32 or buf.numel() != 2 * rep * k or not 1 <= rep <= 512):
+        return NotImplemented
+    p, q = _out_hw(h, w, r, s, stride, pad, dilation)
+    cp = _r(c, 8)
+    if p <= 0 or q <= 0 or not _fits(nb * h * w * 2 * cp * 2, k * r * s * 3 * cp * 2):
+        return NotImplemented
+    x3 = _act_split(_nhwc_rows(x), cp, True, x)
+    if slot is not None:
+        slot[0] = (_slot_key(x, cp, True), x3)
+    w3 = split(w4.detach().float().permute(0, 2, 3, 1).reshape(k * r * s, c), cp, HLH, False)
+    y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
+    check(N.lib().bigdl_conv_fwd_f32out2_stats(ptr(x3), ptr(w3), ptr(y), ptr(buf), rep, ptr(shift), nb, h, w, 3 * cp,
+                                               cp, k, r, s, p, q, stride[0], stride[1], pad[0], pad[1], dilation[0],
+                                               dilation[1], _s()), "conv_fwd_f32out2_stats")
+    return y, buf, rep
+
+
 def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
                   scale=1.0, residual=None, slot=None):
     """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation."""

@@ -188,6 +188,23 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    if (rezero and 1 <= G <= 512 and _bn32_ok(x, C_, residual) and partial is not None and partial.dtype == _f32
+            and partial.numel() == 2 * G * C_ and _f32vec(shift, C_)
+            and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias))):
+        # fp32 compute: the replicated sums of the fp32-output conv (fp32x3.conv_forward_stats)
+        coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
+        mean = torch.empty(C_, dtype=_f32, device=x.device)
+        invstd = torch.empty(C_, dtype=_f32, device=x.device)
+        y = torch.empty_like(x)
+        sp = F3.split_buffer(M, C_, x.device)
+        mb = torch.empty(M * (C_ // 8), dtype=torch.uint8, device=x.device) if relu else None
+        check(_lib().bigdl_bn32_fwd_train_partials(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
+                                                   ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
+                                                   _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
+                                                   C.c_int(G), ptr(shift), ptr(coef), C.c_int(1 if relu else 0),
+                                                   ptr(sp), ptr(mb), _s()), "bn32_fwd_train_partials")
+        F3.note_split(y, sp, mb)
+        return y, mean, invstd
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     if G == 0:  # atomically accumulated sums [2C + 1] (conv epilogue, stats_atomic)
@@ -855,6 +872,10 @@ def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_s
     running mean) is K; the same array must reach the finalize.  ``sums`` (fp32 [2K + 1], zero): the
     tiles atomically ADD into it instead (returned G = 0) for the one-launch BN finalize+apply.
     Returns ``(y, partials, G)`` or NotImplemented."""
+    if x.dtype == _f32 and F3.enabled(x):  # fp32 compute: the bf16x3 conv's fp32 epilogue (replicas only)
+        if groups != 1 or b is not None:
+            return NotImplemented
+        return F3.conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=pad_slot)
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot, shift=shift,
                           sums=sums)
 

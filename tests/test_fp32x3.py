@@ -235,3 +235,32 @@ def test_conv_fp32x3_dgrad_in_image_chunks(s, monkeypatch):
     torch.cuda.synchronize()
     assert _rel(gi, xr.grad + res.double()) < 2e-5
     assert _rel(gw, wr.grad) < 2e-5
+
+
+def test_fp32_conv_epilogue_bn_statistics():
+    """fp32 conv → BN with the statistics added by the conv's fp32 epilogue into the BN's replicated
+    buffer (finalize from 32 rows, cleared after reading) matches the standalone statistics pass."""
+    from bigdl.ops import native_ops as NO, fp32x3 as F3
+    g = torch.Generator().manual_seed(9)
+    N_, C_, K, H = 3, 64, 48, 13  # M = 507 rows: a partial last row tile
+    x = (torch.randn(N_, C_, H, H, generator=g) + 0.5).to(dev).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C_, 3, 3, generator=g) * 0.05).to(dev)
+    gam, bet = torch.rand(K, generator=g).to(dev) + 0.5, torch.randn(K, generator=g).to(dev)
+    rep = 32
+    buf = torch.zeros(2 * rep * K, device=dev)
+    rm1, rv1 = torch.full((K,), 0.3, device=dev), torch.ones(K, device=dev)
+    rm0, rv0 = rm1.clone(), rv1.clone()
+    r = NO.conv2d_forward_stats(x, w, None, (1, 1), (1, 1), shift=rm1, sums=(buf, rep))
+    assert r is not NotImplemented
+    y1, part, G = r
+    assert part is buf and G == rep
+    out1 = NO.batchnorm_forward_train_partials(y1, part, G, gam, bet, rm1, rv1, 0.1, 1e-5, relu=True, shift=rm1,
+                                               rezero=True)
+    assert out1 is not NotImplemented
+    y0 = F3.conv_forward(x, w, None, (1, 1), (1, 1))
+    out0 = NO.batchnorm_forward_train(y0, gam, bet, rm0, rv0, 0.1, 1e-5, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y0)
+    assert _rel(out1[0], out0[0]) < 1e-5 and _rel(out1[1], out0[1]) < 1e-5 and _rel(out1[2], out0[2]) < 1e-5
+    assert _rel(rm1, rm0) < 1e-5 and _rel(rv1, rv0) < 1e-5
+    assert float(buf.abs().sum()) == 0.0  # cleared by the finalize for the next step
