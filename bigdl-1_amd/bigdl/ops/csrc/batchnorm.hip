@@ -1261,6 +1261,26 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train_partials(const float* x, const float* res,
   BIGDL_CHECK_LAUNCH();
 }
 
+// fp32 training backward from the replicated Σg', Σg'·(x − μ) the consumer conv's fp32 dgrad epilogue
+// added (bigdl_conv_fwd_f32out2_bnbwd; gm = the ReLU-masked gradient it stored): finalize (clears the
+// replicas) + gx = A·gm + B·x + Cc, with the producing conv's [hi | lo] dY split (split, optional).
+BIGDL_EXPORT int bigdl_bn32_bwd_partials(const float* gm, const float* x, float* gx, long long M, int C,
+                                         const float* gamma, const float* mean, const float* invstd, float* ggamma,
+                                         float* gbeta, float gscale, float* cbias, float cbscale, float* partial, int G,
+                                         float* coef, void* split, hipStream_t s) {
+  if (C % 8 || M <= 0 || G <= 0 || G > 512 || !partial || !bn32_ok(x) || !bn32_ok(gm) || (gx && !bn32_ok(gx)) ||
+      (split && (!gx || !bn32_ok(split))))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)partial, G, M,
+                     C, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, nullptr, partial);
+  if (gx) {
+    const int grid = apply_grid(M, C);
+    hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gm, nullptr, gx, nullptr, M, C, coef,
+                       (bf16_t*)split);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
 BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int C, const float* gamma,
                                       const float* beta, const float* run_mean, const float* run_var,
                                       const float* in_bias, float eps, float* coef, int relu, hipStream_t s) {

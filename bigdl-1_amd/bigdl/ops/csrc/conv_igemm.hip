@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
   }
 
   if (p.y32) {  // fp32 output (uniform branch): 4 consecutive channels of one pixel per accumulator
-    if (p.stats) {
+    if (p.stats && !p.bnx32) {
       // BN statistics of the fp32 output (the fp32-compute conv → BN case; host-checked: no bias, ReLU or
       // residual, replicated atomic sums): shifted by the prefetched running mean, summed over the lane's
       // TM pixels, folded over the 16 pixel lanes of a DPP row, then one atomic per wave and channel into
@@ -469,6 +469,16 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
     for (int i = 0; i < TN; ++i) {
       const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
       if (n >= p.K) continue;  // K % 4 == 0 (host-checked): a 4-channel group is all in or all out
+      // fp32 BN backward (p.bnx32): Σg', Σg'·(x − μ) of the stored gradient masked by the BN's ReLU
+      float gs[4] = {0.f, 0.f, 0.f, 0.f}, gq[4] = {0.f, 0.f, 0.f, 0.f}, mu[4] = {0.f, 0.f, 0.f, 0.f};
+      float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sh4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bnx32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          mu[e] = p.bn_mean[n + e];
+          if (!p.bn_bits && p.bn_sc) { sc4[e] = p.bn_sc[n + e]; sh4[e] = p.bn_sh[n + e]; }
+        }
+      }
       float b4[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias) {
 #pragma unroll
@@ -484,7 +494,48 @@ __global__ void __launch_bounds__(256, BM == 256 ? 1 : (BK == 32 && !AT ? 3 : 2)
           v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
         }
         if (p.relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+        if (p.bnx32) {  // the stored gradient is the ReLU-masked g' (the BN backward's and the shortcut's input)
+          const float4 xv = *reinterpret_cast<const float4*>(p.bnx32 + (size_t)m * p.K + n);
+          const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, va[4] = {v.x, v.y, v.z, v.w};
+          unsigned mb = 0xFu;
+          if (p.bn_bits) {
+            mb = (p.bn_bits[(size_t)m * (p.K >> 3) + (n >> 3)] >> (n & 7)) & 0xFu;
+          } else if (p.bn_sc) {
+            mb = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mb |= (fmaf(xa[e], sc4[e], sh4[e]) > 0.f ? 1u : 0u) << e;
+          }
+          float ga[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ga[e] = (mb >> e) & 1u ? va[e] : 0.f;
+            gs[e] += ga[e];
+            gq[e] = fmaf(ga[e], xa[e] - mu[e], gq[e]);
+          }
+          v = make_float4(ga[0], ga[1], ga[2], ga[3]);
+        }
         *reinterpret_cast<float4*>(p.y32 + (size_t)m * p.ldy + n) = v;
+      }
+      if (p.bnx32) {  // fold the 16 pixel lanes of the DPP row, one atomic per wave and channel
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#define BIGDL_ROW_FOLD(CTL)                                                                              \
+  gs[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(gs[e]), CTL, 0xF, 0xF, false));     \
+  gq[e] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(gq[e]), CTL, 0xF, 0xF, false));
+          BIGDL_ROW_FOLD(0x128)
+          BIGDL_ROW_FOLD(0x124)
+          BIGDL_ROW_FOLD(0x122)
+          BIGDL_ROW_FOLD(0x121)
+#undef BIGDL_ROW_FOLD
+        }
+        if (fr == 0) {
+          const int rep = tm % p.stats_atomic;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            atomicAdd(&p.stats[(size_t)rep * p.K + n + e], gs[e]);
+            atomicAdd(&p.stats[((size_t)p.stats_atomic + rep) * p.K + n + e], gq[e]);
+          }
+        }
       }
     }
     return;
@@ -616,7 +667,8 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int res_sw = 0, int res_H = 0, int res_W = 0, const void* bn_bits = nullptr,
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
                            float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0,
-                           int stats_atomic = 0, const float* res32 = nullptr, int cdup = 0) {
+                           int stats_atomic = 0, const float* res32 = nullptr, int cdup = 0,
+                           const float* bnx32 = nullptr) {
   const bool c4 = C == 4;
   if (cdup && (cdup < 0 || cdup % 8 || 2 * cdup > C || c4 || ax || groups != 1 || !y32)) return (int)hipErrorInvalidValue;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
@@ -624,7 +676,9 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
               osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q))
     return (int)hipErrorInvalidValue;
   // fp32-output statistics: replicated atomic sums only, of the plain conv output
-  if (y32 && stats && (stats_atomic <= 0 || bias || relu || res32 || ldy != K || tile_bm == 256))
+  if (y32 && stats && (stats_atomic <= 0 || bias || relu || (res32 && !bnx32) || ldy != K || tile_bm == 256))
+    return (int)hipErrorInvalidValue;
+  if (bnx32 && (!y32 || !stats || !bn_mean || ((uintptr_t)bnx32 & 15) || (bn_sc != nullptr) != (bn_sh != nullptr)))
     return (int)hipErrorInvalidValue;
   if (ldx == 0) ldx = C - cdup;
   if (groups < 1 || ldx < C - cdup || (ldx != C && (c4 || ldx % 8 || ((uintptr_t)x & 15)))) return (int)hipErrorInvalidValue;
@@ -660,6 +714,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.y32 = y32;
   if (res32 && (!y32 || ((uintptr_t)res32 & 15))) return (int)hipErrorInvalidValue;
   p.res32 = res32;
+  p.bnx32 = bnx32;
   p.res = (const bf16_t*)res;
   p.stats = stats;
   p.stats_atomic = stats ? stats_atomic : 0;
@@ -690,7 +745,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.bn_mean = bn_mean;
   p.bn_mask = (const bf16_t*)bn_mask;
   p.bn_bits = (const uint8_t*)bn_bits;
-  if (bn_bits && (!bn_mask || K % 8)) return (int)hipErrorInvalidValue;
+  if (bn_bits && ((!bn_mask && !bnx32) || K % 8)) return (int)hipErrorInvalidValue;
   if (bnx && (!stats || !bn_mean || relu || bias || p.scatter)) return (int)hipErrorInvalidValue;
   if (bnx && !bn_mask && (!bn_sc || !bn_sh || res)) return (int)hipErrorInvalidValue;
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
@@ -924,6 +979,22 @@ BIGDL_EXPORT int bigdl_conv_fwd_f32out2_stats(const void* x, const void* w, floa
   return conv_fwd_launch(x, w, nullptr, nullptr, nullptr, stats, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
                          0, 1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, 0, shift, 0, 0,
                          0, 0, nullptr, 2 * cdup, 1, nullptr, nullptr, y32, 0, 0, 0, R_rep, nullptr, cdup);
+}
+
+// fp32 data gradient (two-part split, as bigdl_conv_fwd_f32out2) whose epilogue also ADDS the BN-backward
+// statistics Σg', Σg'·(x − mean) of its output g (after the optional residual) into R replicas of stats
+// ([2][R][K], zero on entry): x = bnx32 [M][K] is the BN input, the ReLU mask comes from bits ([M][K/8],
+// the forward's mask) or from scale·x + shift > 0 (sc / sh, a BN + ReLU with no residual).
+BIGDL_EXPORT int bigdl_conv_fwd_f32out2_bnbwd(const void* x, const void* w, const float* res32, float* y32,
+                                              float* stats, int R_rep, const float* bnx32, const float* mean,
+                                              const void* bits, const float* sc, const float* sh, int Nb, int H,
+                                              int W, int C, int cdup, int K, int R, int S, int P, int Q, int sh_,
+                                              int sw_, int ph, int pw, int dh, int dw, hipStream_t s) {
+  if (!y32 || !stats || !bnx32 || !mean || R_rep <= 0 || cdup <= 0 || C != 3 * cdup || K % 8 || (!bits && !sc))
+    return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, nullptr, nullptr, nullptr, stats, Nb, H, W, C, K, R, S, P, Q, sh_, sw_, ph, pw, dh, dw,
+                         0, 1, 1, 0, 0, P, Q, nullptr, sc, sh, mean, nullptr, K, s, 0, nullptr, 0, 0, 0, 0, bits,
+                         2 * cdup, 1, nullptr, nullptr, y32, 0, 0, 0, R_rep, res32, cdup, bnx32);
 }
 
 // bigdl_conv_fwd_ldy / bigdl_conv_fwd_stats_shift with an explicit tile (bn, bk, bm; 0 = heuristic).

@@ -76,6 +76,9 @@ struct ConvParams {
   // optional fp32 residual [M][ldy] added to the fp32 output before the ReLU (y32 mode only: the
   // data gradient of a block's first conv summed with the shortcut's, bf16x3 path)
   const float* res32;
+  // fp32 BN-backward statistics in the y32 epilogue: the BN input [M][K] (with bn_mean, and the ReLU mask
+  // from bn_bits or recomputed as bn_sc·x + bn_sh > 0); sums added into replicas (stats_atomic)
+  const float* bnx32;
   // statistics mode: 0 = per-row-tile partial rows stats[2][tiles_m][K] (reduced later by a
   // fold / finalize pass), 1 = every tile ADDS its partial sums into stats[2][K] with fp32 atomics
   // (the consumer's apply kernel finalises in its prologue and re-zeroes the buffer: no separate

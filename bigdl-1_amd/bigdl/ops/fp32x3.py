@@ -245,9 +245,36 @@ def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
     return y, buf, rep
 
 
+def _bnbwd_args(bn_fuse, nb, c, h, w, res):
+    """The fp32 BN-backward statistics a data gradient can add in its epilogue (conv.py bn_fuse):
+    (buf, R, bn input, mean, bits, scale, shift) or None."""
+    if bn_fuse is None or not config.get_property("bigdl.fp32.convStats") or c % 8:
+        return None
+    sums, bx, mean = bn_fuse.get("sums"), bn_fuse.get("x"), bn_fuse.get("mean")
+    if not isinstance(sums, tuple) or not isinstance(bx, torch.Tensor) or not isinstance(mean, torch.Tensor):
+        return None
+    buf, rep = sums
+    if (buf.dtype != _f32 or buf.numel() != 2 * rep * c or not 1 <= rep <= 512 or bx.dtype != _f32
+            or tuple(bx.shape) != (nb, c, h, w) or not bx.is_contiguous(memory_format=_cl) or bx.data_ptr() % 16
+            or mean.dtype != _f32 or mean.numel() != c):
+        return None
+    sc, sh, bits = bn_fuse.get("scale"), bn_fuse.get("shift"), None
+    if "mask" in bn_fuse:  # a block tail: the forward's ReLU mask bits of its output
+        bits = producer_bits(bn_fuse["mask"])
+        if bits is None or res is None:
+            return None
+        sc = sh = None
+    elif not (isinstance(sc, torch.Tensor) and isinstance(sh, torch.Tensor) and res is None):
+        return None
+    return buf, rep, bx, mean, bits, sc, sh
+
+
 def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                  scale=1.0, residual=None, slot=None):
-    """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation."""
+                  scale=1.0, residual=None, slot=None, bn_fuse=None):
+    """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation.  ``bn_fuse``
+    (conv.py: the BN + ReLU whose output this conv consumed): the data gradient's epilogue stores the
+    ReLU-masked gradient and adds that BN's backward statistics into its replicated buffer, reported
+    back as ``bn_fuse["partial"], bn_fuse["G"]``."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
     nb, c, h, w = x.shape
@@ -282,6 +309,8 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
         fuse_res = (residual is not None and cq == c and residual.dtype == _f32 and tuple(residual.shape) == (nb, c, h, w)
                     and residual.is_contiguous(memory_format=_cl) and residual.data_ptr() % 16 == 0)
         whole = _producer_split(gy, kp) if (two and not strided) else None
+        bnb = _bnbwd_args(bn_fuse, nb, c, h, w, residual if fuse_res else None) if (two and nbc == nb
+                                                                                    and cq == c) else None
         for i0 in range(0, nb, nbc):
             i1 = min(nb, i0 + nbc)
             gyc = gy if (i0, i1) == (0, nb) else gy[i0:i1]
@@ -296,7 +325,14 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
                 g3c = _act_split(_nhwc_rows(src), kp, two, src)
             gic = gi if (i0, i1) == (0, nb) else gi[i0:i1]
             resc = (residual if (i0, i1) == (0, nb) else residual[i0:i1]) if fuse_res else None
-            if two:
+            if bnb is not None:
+                buf, rep, bx, mean, bits, bsc, bsh = bnb
+                check(N.lib().bigdl_conv_fwd_f32out2_bnbwd(
+                    ptr(g3c), ptr(wt3), ptr(resc), ptr(gic), ptr(buf), rep, ptr(bx), ptr(mean), ptr(bits), ptr(bsc),
+                    ptr(bsh), i1 - i0, hl, wl, 3 * kp, kp, cq, r, s, h, w, 1, 1, pd[0], pd[1], dilation[0],
+                    dilation[1], _s()), "conv_fwd_f32out2_bnbwd")
+                bn_fuse["partial"], bn_fuse["G"] = buf, rep
+            elif two:
                 _conv_f32out2(g3c, wt3, None, gic, i1 - i0, hl, wl, kp, cq, r, s, h, w, (1, 1), pd, dilation, False,
                               cq, res=resc)
             else:

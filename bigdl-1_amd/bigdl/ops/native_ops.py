@@ -247,6 +247,19 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    if (rezero and 1 <= G <= 512 and _bn32_ok(x, C_, gm) and partial is not None and partial.dtype == _f32
+            and partial.numel() == 2 * G * C_
+            and all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc))):
+        # fp32 compute: the replicated sums of the consumer's fp32 dgrad epilogue (fp32x3.conv_backward)
+        coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
+        gx = torch.empty_like(x) if need_input else None
+        sp = F3.split_buffer(M, C_, x.device) if need_input else None
+        check(_lib().bigdl_bn32_bwd_partials(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma),
+                                             ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
+                                             ptr(cbias_acc), _f(cbias_scale), ptr(partial), C.c_int(G), ptr(coef),
+                                             ptr(sp), _s()), "bn32_bwd_partials")
+        F3.note_split(gx, sp)
+        return gx
     if not _bn_ok(x, C_) or gm.dtype != _bf16 or gm.shape != x.shape or gm.stride() != x.stride() or not _al16(gm):
         return NotImplemented
     if not all(_f32vec(t, C_) for t in (gamma, save_mean, save_invstd, gg_acc, gb_acc, cbias_acc)):
@@ -1352,7 +1365,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         # runs its own backward), a lazy strided gradient is returned dense
         res = residual.dense() if isinstance(residual, R_.StridedGrad) else residual
         r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, res,
-                             slot=pad_slot)
+                             slot=pad_slot, bn_fuse=bn_fuse)
         if r is not NotImplemented:
             return r
     if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):

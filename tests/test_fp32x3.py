@@ -264,3 +264,43 @@ def test_fp32_conv_epilogue_bn_statistics():
     assert _rel(out1[0], out0[0]) < 1e-5 and _rel(out1[1], out0[1]) < 1e-5 and _rel(out1[2], out0[2]) < 1e-5
     assert _rel(rm1, rm0) < 1e-5 and _rel(rv1, rv0) < 1e-5
     assert float(buf.abs().sum()) == 0.0  # cleared by the finalize for the next step
+
+
+@pytest.mark.parametrize("tail", [False, True], ids=["mid_block", "block_tail"])
+def test_fp32_dgrad_epilogue_bn_backward_statistics(tail):
+    """The fp32 data gradient of a conv that consumes a BN + ReLU output stores the ReLU-masked gradient
+    and adds the BN-backward sums into the BN's replicas (mask recomputed from scale·x + shift, or the
+    block tail's forward mask bits with the shortcut gradient summed first); the BN backward from them
+    matches the standalone path."""
+    from bigdl.ops import native_ops as NO, fp32x3 as F3
+    g = torch.Generator().manual_seed(11)
+    N_, C_, K, H = 2, 32, 24, 11
+    cl = torch.channels_last
+    xb = torch.randn(N_, C_, H, H, generator=g).to(dev).contiguous(memory_format=cl)
+    gam, bet = (torch.rand(C_, generator=g) + 0.5).to(dev), torch.randn(C_, generator=g).to(dev)
+    res = torch.randn(N_, C_, H, H, generator=g).to(dev).contiguous(memory_format=cl) if tail else None
+    coef = torch.empty(2 * C_, device=dev)
+    y, mean, invstd = NO.batchnorm_forward_train(xb, gam, bet, torch.zeros(C_, device=dev), torch.ones(C_, device=dev),
+                                                 0.1, 1e-5, relu=True, residual=res, coef_out=coef)
+    w = (torch.randn(K, C_, 3, 3, generator=g) * 0.1).to(dev)
+    gy = torch.randn(N_, K, H, H, generator=g).to(dev).contiguous(memory_format=cl)
+    sres = torch.randn(N_, C_, H, H, generator=g).to(dev).contiguous(memory_format=cl) if tail else None
+    rep = 32
+    buf = torch.zeros(2 * rep * C_, device=dev)
+    fuse = {"x": xb, "mean": mean, "sums": (buf, rep)}
+    if tail:
+        fuse["mask"] = y
+    else:
+        fuse["scale"], fuse["shift"] = coef[:C_], coef[C_:]
+    gi1 = F3.conv_backward(gy, y, w, (1, 1), (1, 1), (1, 1), 1, True, None, None, 1.0, residual=sres, bn_fuse=fuse)
+    assert fuse.get("partial") is buf and fuse.get("G") == rep
+    gg1, gb1 = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
+    gx1 = NO.batchnorm_backward_partials(gi1, xb, gam, mean, invstd, buf, rep, True, gg1, gb1, 1.0, rezero=True)
+    assert gx1 is not NotImplemented
+    gi0 = F3.conv_backward(gy, y, w, (1, 1), (1, 1), (1, 1), 1, True, None, None, 1.0, residual=sres)
+    gg0, gb0 = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
+    gx0, _ = NO.batchnorm_backward(gi0, xb, gam, mean, invstd, y.clone(), True, True, gg0, gb0, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(gi1, gi0 * (y > 0))
+    assert _rel(gx1, gx0) < 1e-5 and _rel(gg1, gg0) < 1e-5 and _rel(gb1, gb0) < 1e-5
+    assert float(buf.abs().sum()) == 0.0
