@@ -81,8 +81,14 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 
 // C4: 4-channel input (RGB stem padded 3 → 4): an X̂ chunk of 8 k-values is two consecutive taps,
 // gathered as two 8-B loads with separate padding tests (see conv_igemm.hip MODE 2).
-template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false, bool PW1 = false>
-__global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(WgradParams p) {
+// F32: fp32 operands (the bf16x3 fp32 compute mode, csrc/precision.hip): each 8-channel chunk is loaded as
+// two 16-B fp32 pieces, split in registers into bf16 hi = rne(v) and lo = rne(v − hi) tiles (LDS holds
+// both), and every fragment pair feeds three MFMAs (dY_hi·X_hi + dY_lo·X_hi + dY_hi·X_lo) — one launch
+// reading 4 B per element instead of three over a materialised [hi | lo] split.
+template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false, bool PW1 = false,
+          bool F32 = false>
+__global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_conv_wgrad(WgradParams p) {
+  static_assert(!(F32 && (C4 || D3 || AT)), "fp32 operands: 2-D, 8-channel chunks, no BN prologue");
   static_assert(!(PW1 && (C4 || D3)), "pointwise gather: 2-D, 8-channel chunks");
   static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
   static_assert(!(AT && (C4 || D3)), "BN-backward prologue: 2-D, 8-channel chunks");
@@ -92,7 +98,10 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
   constexpr int TMK = TILE_K / 32;              // along k
   constexpr int DY_WORDS = BPT * TILE_N / 2;     // dwords per tile
   constexpr int X_WORDS = BPT * TILE_K / 2;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[2][DY_WORDS + X_WORDS];
+  constexpr int LO = DY_WORDS + X_WORDS;          // F32: the lo tiles follow the hi tiles
+  constexpr int ES = F32 ? 4 : 2;                 // operand element bytes
+  constexpr int PC = F32 ? 2 : 1;                 // 16-B pieces per 8-channel chunk
+  __shared__ __attribute__((aligned(16))) uint32_t lds[2][LO * (F32 ? 2 : 1)];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wave_n = wid & 1, wave_k = wid >> 1;
@@ -140,8 +149,8 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
   // Raw buffer loads (OOB offsets → zeros, no branches) into two register sets; tile t+2 is
   // requested while tile t is multiplied (loads always issued — beyond the range with a dead
   // offset — so hipcc's vmcnt counts stay exact; see conv_igemm.hip).
-  const uint32_t x_bytes = (uint32_t)(((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.ldx - grp * p.gx) * 2);
-  const uint32_t dy_bytes = (uint32_t)(((size_t)p.M * p.ldk - grp * p.gdy) * 2);
+  const uint32_t x_bytes = (uint32_t)(((size_t)p.Nb * (D3 ? p.T : 1) * p.H * p.W * p.ldx - grp * p.gx) * ES);
+  const uint32_t dy_bytes = (uint32_t)(((size_t)p.M * p.ldk - grp * p.gdy) * ES);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, 0, (int)dy_bytes, 0x00020000);
   constexpr uint32_t DEAD = 0x80000000u;
@@ -158,14 +167,15 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
     }
   }
 
-  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH], uint4 (&rx_)[X_CH], uint4 (&r2)[AT ? DY_CH : 1]) {
+  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH * PC], uint4 (&rx_)[X_CH * PC], uint4 (&r2)[AT ? DY_CH : 1]) {
     const uint32_t dead = live ? 0u : DEAD;
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
       const int m = mt + dy_row0 + i * DY_RSTEP;
       const bool ok = ndy_ok && m < mend;
-      const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldk + (uint32_t)ndy) * 2u : DEAD) | dead;
-      rdy[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
+      const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldk + (uint32_t)ndy) * (uint32_t)ES : DEAD) | dead;
+      rdy[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
+      if constexpr (F32) rdy[PC * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off + 16u, 0, 0));
       if constexpr (AT) r2[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(y2r, off, 0, 0));
     }
     if constexpr (PW1) {  // pointwise: pixel m of the output is pixel m of the input
@@ -173,8 +183,9 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
       for (int i = 0; i < X_CH; ++i) {
         const int m = mt + x_row0 + i * X_RSTEP;
         const bool ok = kx_ok && m < mend;
-        const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldx + (uint32_t)cx) * 2u : DEAD) | dead;
-        rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldx + (uint32_t)cx) * (uint32_t)ES : DEAD) | dead;
+        rx_[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        if constexpr (F32) rx_[PC * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, 0, 0));
       }
       return;
     }
@@ -205,13 +216,47 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
         const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
         rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       } else {
-        const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.ldx + (uint32_t)cx) * 2u : DEAD) | dead;
-        rx_[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.ldx + (uint32_t)cx) * (uint32_t)ES : DEAD) | dead;
+        rx_[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        if constexpr (F32) rx_[PC * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, 0, 0));
       }
     }
   };
-  auto store = [&](int buf, int mt, const uint4 (&rdy)[DY_CH], const uint4 (&rx_)[X_CH],
+  // F32: 8 fp32 (two 16-B pieces) → the hi and lo bf16 chunks
+  auto split8 = [&](const uint4 a, const uint4 b, uint4& h, uint4& l) {
+    const uint32_t u[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v0 = __uint_as_float(u[2 * e]), v1 = __uint_as_float(u[2 * e + 1]);
+      const bf16_t h0 = f2bf(v0), h1 = f2bf(v1);
+      hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lw[e] = (uint32_t)f2bf(v0 - bf2f(h0)) | ((uint32_t)f2bf(v1 - bf2f(h1)) << 16);
+    }
+    h = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    l = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  };
+  auto store = [&](int buf, int mt, const uint4 (&rdy)[DY_CH * PC], const uint4 (&rx_)[X_CH * PC],
                    const uint4 (&r2)[AT ? DY_CH : 1]) {
+    if constexpr (F32) {
+#pragma unroll
+      for (int i = 0; i < DY_CH; ++i) {
+        const int row = dy_row0 + i * DY_RSTEP;
+        uint4 h, l;
+        split8(rdy[2 * i], rdy[2 * i + 1], h, l);
+        *reinterpret_cast<uint4*>(&lds[buf][tr_swz_dword<TILE_N>(row, dy_col * 4)]) = h;
+        *reinterpret_cast<uint4*>(&lds[buf][LO + tr_swz_dword<TILE_N>(row, dy_col * 4)]) = l;
+      }
+#pragma unroll
+      for (int i = 0; i < X_CH; ++i) {
+        const int row = x_row0 + i * X_RSTEP;
+        uint4 h, l;
+        split8(rx_[2 * i], rx_[2 * i + 1], h, l);
+        *reinterpret_cast<uint4*>(&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = h;
+        *reinterpret_cast<uint4*>(&lds[buf][LO + DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = l;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
       int row = dy_row0 + i * DY_RSTEP;
@@ -235,7 +280,7 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
       int row = x_row0 + i * X_RSTEP;
-      *reinterpret_cast<uint4*>(&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = rx_[i];
+      *reinterpret_cast<uint4*>(&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = rx_[PC * i];
     }
   };
 
@@ -247,38 +292,57 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? 3 : 2) k_conv_wgrad(Wg
 
   const int g = (lane >> 4) & 3;  // 16-lane group → pixels 8g..8g+7 of a 32-pixel k-step
   const int t = lane & 15, q4 = t >> 2, p4 = t & 3;
+  // fragment of 8 consecutive pixels (transposed read) at tile word offset `base` (0: hi, LO: lo tiles)
+  auto frag_n = [&](int buf, int base, int i, int kk) -> v8s {
+    const int col = wave_n * (TILE_N / 2) + i * 16 + 4 * p4;  // channel of this lane's quad
+    const int r0 = kk * 32 + 8 * g + q4;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)&lds[buf][base + tr_swz_dword<TILE_N>(r0, col >> 1)]);
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)&lds[buf][base + tr_swz_dword<TILE_N>(r0 + 4, col >> 1)]);
+    return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto frag_k = [&](int buf, int base, int j, int kk) -> v8s {
+    const int col = wave_k * (TILE_K / 2) + j * 16 + 4 * p4;
+    const int r0 = kk * 32 + 8 * g + q4;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)&lds[buf][base + DY_WORDS + tr_swz_dword<TILE_K>(r0, col >> 1)]);
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)&lds[buf][base + DY_WORDS + tr_swz_dword<TILE_K>(r0 + 4, col >> 1)]);
+    return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
   auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BPT / 32; ++kk) {
       v8s af[TMN], bfr[TMK];
 #pragma unroll
-      for (int i = 0; i < TMN; ++i) {
-        const int col = wave_n * (TILE_N / 2) + i * 16 + 4 * p4;  // channel of this lane's quad
-        const int r0 = kk * 32 + 8 * g + q4;
-        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)&lds[buf][tr_swz_dword<TILE_N>(r0, col >> 1)]);
-        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)&lds[buf][tr_swz_dword<TILE_N>(r0 + 4, col >> 1)]);
-        af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      for (int i = 0; i < TMN; ++i) af[i] = frag_n(buf, 0, i, kk);
+#pragma unroll
+      for (int j = 0; j < TMK; ++j) bfr[j] = frag_k(buf, 0, j, kk);
+      if constexpr (F32) {
+        v8s afl[TMN], bfl[TMK];
+#pragma unroll
+        for (int i = 0; i < TMN; ++i) afl[i] = frag_n(buf, LO, i, kk);
+#pragma unroll
+        for (int j = 0; j < TMK; ++j) bfl[j] = frag_k(buf, LO, j, kk);
+#pragma unroll
+        for (int i = 0; i < TMN; ++i)
+#pragma unroll
+          for (int j = 0; j < TMK; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TMN; ++i)
+#pragma unroll
+          for (int j = 0; j < TMK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < TMK; ++j) {
-        const int col = wave_k * (TILE_K / 2) + j * 16 + 4 * p4;
-        const int r0 = kk * 32 + 8 * g + q4;
-        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(r0, col >> 1)]);
-        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(r0 + 4, col >> 1)]);
-        bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int i = 0; i < TMN; ++i)
-#pragma unroll
-        for (int j = 0; j < TMK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
 
-  uint4 dy0[DY_CH], x0[X_CH], dy1[DY_CH], x1[X_CH];
+  uint4 dy0[DY_CH * PC], x0[X_CH * PC], dy1[DY_CH * PC], x1[X_CH * PC];
   uint4 z0[AT ? DY_CH : 1], z1[AT ? DY_CH : 1];
   const int NT = (mend - mbeg + BPT - 1) / BPT;
   load(mbeg, true, dy0, x0, z0);
@@ -528,4 +592,68 @@ BIGDL_EXPORT int bigdl_conv_wgrad_grouped(const void* x, const void* dy, float* 
                                           int sh, int sw, int ph, int pw, int dh, int dwd, hipStream_t s) {
   if (Cg == 4) return (int)hipErrorInvalidValue;
   return wgrad_launch(x, dy, dw, scale, Nb, H, W, Cg, Kg, R, S, P, Q, sh, sw, ph, pw, dh, dwd, 0, s, ldx, ldk, groups);
+}
+
+// fp32 operands (bf16x3 fp32 compute mode): x [Nb][H][W][C], dy [Nb][P][Q][K] fp32 NHWC (16-B aligned,
+// C % 8 == 0, K % 8 == 0); dw [K][R][S][C] fp32 += scale · Σ dyᵀ·x̂ at bf16x3 accuracy in ONE launch.
+// Pixel depth 32 per k-tile (the hi + lo tiles double the LDS image).  splits <= 0: heuristic.
+BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw, float scale, int Nb, int H, int W,
+                                      int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh,
+                                      int dwd, int splits, hipStream_t s) {
+  if (C % 8 || K % 8 || Nb <= 0 || !x || !dy || !dw) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15)) return (int)hipErrorInvalidValue;
+  if ((size_t)Nb * H * W * C * 4 >= 0x80000000ull || (size_t)Nb * P * Q * K * 4 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;
+  WgradParams p{};
+  p.ldx = C; p.ldk = K;
+  p.gx = C; p.gdy = K; p.gdw = (long long)K * R * S * C;
+  p.x = (const bf16_t*)x;
+  p.dy = (const bf16_t*)dy;
+  p.dw = dw;
+  p.scale = scale;
+  const char* epi_env = getenv("BIGDL_WGRAD_EPI");
+  p.epi_lds = epi_env ? atoi(epi_env) : 0;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw_ = dwd;
+  const long long Ml = (long long)Nb * P * Q;
+  if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  p.M = (int)Ml;
+  p.Kg = R * S * C;
+  p.fPQ = make_fastdiv((uint32_t)(P * Q));
+  p.fQ = make_fastdiv((uint32_t)Q);
+  p.pw1 = (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && P == H && Q == W) ? 1 : 0;
+  const int TN = K <= 64 ? 64 : 128;
+  const int TK = p.Kg <= 64 ? 64 : 128;
+  p.tiles_n = (K + TN - 1) / TN;
+  p.tiles_k = (p.Kg + TK - 1) / TK;
+  const int tiles = p.tiles_n * p.tiles_k;
+  if (g_bigdl_deterministic) splits = 1;
+  if (splits <= 0) {
+    const long long target = splits < 0 ? -(long long)splits : 512;
+    long long want = (target + tiles - 1) / tiles;
+    const long long max_by_work = (p.M + 8 * BP - 1) / (8 * BP);
+    splits = (int)(want < max_by_work ? want : max_by_work);
+    if (splits < 1) splits = 1;
+    if (splits > 65535) splits = 65535;
+  }
+  int mps = (p.M + splits - 1) / splits;
+  mps = (mps + BP - 1) / BP * BP;
+  p.m_per_split = mps;
+  splits = (p.M + mps - 1) / mps;
+  const dim3 grid(tiles, splits, 1);
+#define BIGDL_WF32(TN_, TK_, PW_) \
+  hipLaunchKernelGGL((k_conv_wgrad<TN_, TK_, 32, false, false, false, PW_, true>), grid, dim3(256), 0, s, p)
+  if (p.pw1) {
+    if (TN == 64 && TK == 64) BIGDL_WF32(64, 64, true);
+    else if (TN == 64) BIGDL_WF32(64, 128, true);
+    else if (TK == 64) BIGDL_WF32(128, 64, true);
+    else BIGDL_WF32(128, 128, true);
+  } else {
+    if (TN == 64 && TK == 64) BIGDL_WF32(64, 64, false);
+    else if (TN == 64) BIGDL_WF32(64, 128, false);
+    else if (TK == 64) BIGDL_WF32(128, 64, false);
+    else BIGDL_WF32(128, 128, false);
+  }
+#undef BIGDL_WF32
+  BIGDL_CHECK_LAUNCH();
 }

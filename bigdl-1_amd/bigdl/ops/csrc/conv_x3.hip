@@ -1,0 +1,641 @@
+// fp32 implicit-GEMM convolution on the bf16 matrix cores with the operand split done IN the kernel
+// ("bf16x3", csrc/precision.hip): D[n = out channel][m = output pixel] = Σ_k W[n][k] · X̂[m][k] at fp32
+// accuracy as  W_hi·X_hi + W_lo·X_hi + W_hi·X_lo  (v_mfma_f32_32x32x16_bf16, fp32 accumulation).
+// Reference: SpatialConvolution.updateOutput / updateGradInput in fp32 (MKL-DNN fp32 primitives,
+// DL/nn/SpatialConvolution.scala:253-430); no im2col is materialised.
+//
+// Why a separate family: the conv_igemm / conv_mfma32 kernels take the fp32 activations as a
+// materialised [hi | lo] bf16 split read as three logical parts [hi | hi | lo] (ConvParams::cdup), so
+// every fp32 activation costs a split pass (or a second write by its producer) and the kernel stages
+// 3 × 2 B per element through LDS for 3 MFMAs.  Here the raw fp32 activation rows go global → LDS by the
+// LDS-DMA path (4 B per element, the same bytes as the split) and each wave splits its B fragments
+// while reading them (v_cvt_pk_bf16_f32, round-to-nearest hi and lo: |v − hi − lo| ≤ 2^-17 |v|), so
+// 2 fragment reads feed 3 MFMAs and nothing upstream has to write a split.  The weights (small, per
+// step) are pre-split by the host into 32-channel [hi | lo] chunks: W2[n][kt][0:32] = hi, [32:64] = lo
+// of reduction indices kt·32 … kt·32 + 31 — one 128-B LDS row per k-tile, like the activation row.
+//
+// Tile: BM pixels × BN channels, 8 waves (WM × WN), k-tile = 32 reduction indices (one tap, 32
+// channels), a 3-deep LDS ring with counted vmcnt and raw s_barrier (as conv_mfma32.hip; the next
+// stage's LDS-DMA pieces are issued between the MFMA groups of the current one).  LDS rows are 128 B with
+// the XOR swizzle chunk ^ ((row >> 1) & 7) on the DMA source address and on every fragment read, which
+// keeps both the bf16 (A) and the fp32 (B) fragment reads conflict-free.
+//
+// Epilogues (uniform branches on the launch's arguments), straight from the accumulators
+// (lane l of a 32×32 block holds pixel l & 31 and channels 8·(r >> 2) + 4·(l >> 5) + (r & 3)):
+//   plain  : y = relu?(acc + bias + res), fp32 [M][ldy] float4 stores;
+//   stats  : y = acc, plus Σ(y − shift), Σ(y − shift)² of the following BN added into its replicated
+//            buffer [2][R][K] (fp32 atomics, one per block and channel after an LDS fold);
+//   bnbwd  : the data gradient g = acc (+ res) masked by the ReLU of the BN that produced this
+//            conv's input (mask bits, or recomputed as sc·x + sh > 0 from that BN's input x), stored,
+//            and Σg, Σg·(x − mean) of that BN's backward added into its replicated buffer.
+// Modes: 1 = tap-uniform gather (C % 32 == 0, R·S ≤ 64), 3 = pointwise (1×1, no padding).
+#include "common.h"
+#include <type_traits>
+
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+
+#define X3_WAIT(n) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(n) : "memory")
+#define X3_BARRIER()                   \
+  do {                                 \
+    asm volatile("" ::: "memory");     \
+    __builtin_amdgcn_s_barrier();      \
+    asm volatile("" ::: "memory");     \
+  } while (0)
+
+typedef __attribute__((address_space(3))) void x3_lds_t;
+
+struct X3Params {
+  const float* x;      // [Nb][H][W][ldx] fp32
+  const bf16_t* w;     // [K][Kg / 32][64] bf16: per 32-index k-chunk, hi then lo
+  const float* bias;   // [K] or null
+  const float* res;    // [M][ldy] fp32 or null (added before the ReLU / the mask)
+  float* y;            // [M][ldy] fp32
+  int Nb, H, W, C, K, R, S, P, Q;
+  int sh, sw, ph, pw, dh, dw;
+  int M, Kg, ldx, ldy;
+  int relu;
+  int tiles_n;
+  // statistics (stats != null): [2][R_rep][K], tile tm adds into replica tm % R_rep
+  float* stats;
+  int R_rep;
+  const float* shift;  // forward statistics shift (the BN's running mean), [K]
+  // BN-backward epilogue (bnx != null): the BN input [M][K], its mean, and the ReLU mask as bits
+  // ([M][K / 8], bit e of byte (m, c / 8) = channel c) or recomputed from sc · x + sh > 0
+  const float* bnx;
+  const float* mean;
+  const uint8_t* bits;
+  const float* bsc;
+  const float* bsh;
+  // output scatter (sub-pixel strided data gradient): output pixel (n, p, q) of this launch is pixel
+  // (n, p·osh + ooh, q·osw + oow) of an [Nb][oH][oW] grid (y, res and bnx are all on that grid)
+  int scatter, osh, osw, ooh, oow, oH, oW;
+  // strided residual (res_sh > 0): `res` holds only the grid pixels (h, w) with h % res_sh == 0 and
+  // w % res_sw == 0 as a dense [Nb][res_H][res_W][ldy] tensor (a 1×1 stride-s shortcut's input gradient)
+  int res_sh, res_sw, res_H, res_W;
+};
+
+// One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds): lane l's 16 bytes land at lds + 16·l.
+// (A non-template function: inside the kernel template the builtin fails host-side substitution.)
+__device__ __forceinline__ void x3_glds16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (x3_lds_t*)lds, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ int x3_xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// 8 fp32 → bf16 hi and lo fragments: hi = rne(v), lo = rne(v − hi) (both v_cvt_pk_bf16_f32)
+__device__ __forceinline__ void x3_split8(const v4f a, const v4f b, v8s& hi, v8s& lo) {
+  const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const v2bf h = __builtin_convertvector((v2f){v[2 * e], v[2 * e + 1]}, v2bf);
+    const uint32_t hu = __builtin_bit_cast(uint32_t, h);
+    const float r0 = v[2 * e] - __uint_as_float(hu << 16);
+    const float r1 = v[2 * e + 1] - __uint_as_float(hu & 0xFFFF0000u);
+    const v2bf l = __builtin_convertvector((v2f){r0, r1}, v2bf);
+    hw[e] = hu;
+    lw[e] = __builtin_bit_cast(uint32_t, l);
+  }
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  hi = __builtin_bit_cast(v8s, (u4){hw[0], hw[1], hw[2], hw[3]});
+  lo = __builtin_bit_cast(v8s, (u4){lw[0], lw[1], lw[2], lw[3]});
+}
+
+// fold a per-lane value over the 16 lanes of its DPP row (every lane of the row ends with the sum)
+__device__ __forceinline__ float x3_row_fold(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  return v;
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, bool PERSIST>
+__global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
+  static_assert(MODE == 1 || MODE == 3, "tap-uniform / pointwise gathers only");
+  constexpr bool PW = MODE == 3;
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int BK = 32;                       // reduction indices per k-tile (one 128-B row each side)
+  constexpr int NS = 3;                        // LDS ring depth
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;  // 8-row DMA groups per wave: weights, activations
+  static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
+  constexpr int L = GA + GB;
+  constexpr int TMI = BM / WM / 32, TNI = BN / WN / 32;
+  static_assert(TMI >= 1 && TNI >= 1, "wave tile below 32x32");
+  constexpr int RED = WM * 2 * BN * 2 * 4;     // epilogue statistics fold: [WM][2 row halves][2][BN] fp32
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * STAGE + RED];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_m = wid % WM, wave_n = wid / WM;
+  // Tiles of this block: one (grid = tiles), or (PERSIST) a contiguous run of the tm-major tile order —
+  // consecutive tiles share their pixel rows (L2-resident for the second n-tile) — streamed through ONE
+  // pipeline so a tile's epilogue overlaps the next tile's loads.  Runs are XCD-contiguous.
+  int t_first, t_count;
+  {
+    const int ntiles = (int)(((long long)p.M + BM - 1) / BM) * p.tiles_n;
+    const int r = x3_xcd_remap(blockIdx.x, gridDim.x);
+    if (PERSIST) {
+      const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
+      t_first = r * per;
+      t_count = min(per, ntiles - t_first);
+    } else {
+      t_first = r;
+      t_count = 1;
+    }
+  }
+  if (t_count <= 0) return;
+
+  const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.ldx * 4);
+  const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.Kg * 4);  // 2 bf16 parts per index
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0x80000000u;
+
+  const int lrow = lane >> 3, slot = lane & 7;
+  const int KT = p.Kg / BK;  // host-checked: C % 32 == 0
+  const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
+  // per-lane DMA source state of the tile being PREPARED (prep runs two k-tiles ahead of compute)
+  uint32_t woff[GA];
+  int rbase[GB];  // fp32 elements
+  uint64_t vmask[GB];
+  auto setup_tile = [&](int tile) {
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int row = 8 * (wid + NW * i) + lrow;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      const int n = n0 + row;
+      woff[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 4u + (uint32_t)chunk * 16u : OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = 8 * (wid + NW * j) + lrow;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      int img = -1, h = 0, w = 0;
+      if (m < p.M) {
+        if (pw_direct) {
+          img = m;
+        } else {
+          const int n = m / (p.P * p.Q);
+          const int pq = m - n * p.P * p.Q;
+          const int pp = pq / p.Q, qq = pq - pp * p.Q;
+          img = n * p.H * p.W;
+          h = pp * p.sh - p.ph;
+          w = qq * p.sw - p.pw;
+        }
+      }
+      rbase[j] = (img + h * p.W + w) * p.ldx + chunk * 4;
+      uint64_t msk = 0;
+      if (PW) {
+        msk = img >= 0 ? 1ull : 0ull;
+      } else if (img >= 0) {
+        for (int r = 0; r < p.R; ++r) {
+          const int hh = h + r * p.dh;
+          if ((unsigned)hh >= (unsigned)p.H) continue;
+          for (int sx = 0; sx < p.S; ++sx) {
+            const int ww = w + sx * p.dw;
+            if ((unsigned)ww < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
+          }
+        }
+      }
+      vmask[j] = msk;
+    }
+  };
+
+  // prep: the source offsets of the next k-tile of the stream (called strictly in stream order)
+  int it_c0 = 0, it_s = 0, it_tap = 0, it_off = 0;
+  int p_kt = 0, p_tl = 0;
+  uint32_t poff[L];
+  auto prep = [&]() {
+    if (p_kt == 0) {
+      setup_tile(t_first + p_tl);
+      it_c0 = it_s = it_tap = it_off = 0;
+    }
+    const int kt = p_kt;
+    const uint32_t kb = (uint32_t)kt * 128u;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) poff[i] = woff[i] + kb;
+    const int tap = PW ? 0 : it_tap;
+    const int tap_off = PW ? kt * BK : it_off + it_c0;
+    if (!PW) {
+      it_c0 += BK;
+      if (it_c0 == p.C) {
+        it_c0 = 0;
+        ++it_tap;
+        if (++it_s == p.S) {
+          it_s = 0;
+          it_off += (p.dh * p.W - (p.S - 1) * p.dw) * p.ldx;
+        } else {
+          it_off += p.dw * p.ldx;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const bool ok = PW ? (vmask[j] != 0) : ((vmask[j] >> tap) & 1ull);
+      poff[GA + j] = ok ? (uint32_t)(rbase[j] + tap_off) * 4u : OOB;
+    }
+    if (++p_kt == KT) {
+      p_kt = 0;
+      ++p_tl;
+    }
+  };
+  auto issue = [&](int i, int slotbuf) {
+    unsigned char* base = lds + slotbuf * STAGE;
+    if (i < GA)
+      x3_glds16(wr, base + 8 * (wid + NW * i) * 128, poff[i]);
+    else
+      x3_glds16(xr, base + (BN + 8 * (wid + NW * (i - GA))) * 128, poff[i]);
+  };
+
+  v16f acc[TNI][TMI];
+#pragma unroll
+  for (int i = 0; i < TNI; ++i)
+#pragma unroll
+    for (int j = 0; j < TMI; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int frow = lane & 31, fh = lane >> 5;
+  const int swz = (frow >> 1) & 7;
+  // per slice kk (16 reduction indices): A hi chunk 2kk + fh, lo chunk 4 + 2kk + fh; B fp32 chunks
+  // 4kk + 2fh and 4kk + 2fh + 1
+  int fa_hi[2], fa_lo[2], fb0[2], fb1[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    fa_hi[kk] = frow * 128 + (((2 * kk + fh) ^ swz) << 4);
+    fa_lo[kk] = frow * 128 + (((4 + 2 * kk + fh) ^ swz) << 4);
+    fb0[kk] = frow * 128 + (((4 * kk + 2 * fh) ^ swz) << 4);
+    fb1[kk] = frow * 128 + (((4 * kk + 2 * fh + 1) ^ swz) << 4);
+  }
+  const int a_row0 = wave_n * (BN / WN), b_row0 = BN + wave_m * (BM / WM);
+
+  constexpr int PPK = (L + 1) / 2;  // DMA pieces of the next stage per slice
+  auto compute = [&](int slotbuf, int nslot, auto issue_on) {
+    const unsigned char* base = lds + slotbuf * STAGE;
+    v8s ah[2][TNI], al[2][TNI];
+    v4f b0[2][TMI], b1[2][TMI];
+#pragma unroll
+    for (int i = 0; i < TNI; ++i) {
+      ah[0][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[0]);
+      al[0][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[0]);
+    }
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) {
+      b0[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[0]);
+      b1[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[0]);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 0) {  // fragments of slice 1 in flight during slice 0's MFMAs
+#pragma unroll
+        for (int i = 0; i < TNI; ++i) {
+          ah[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[1]);
+          al[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[1]);
+        }
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) {
+          b0[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[1]);
+          b1[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[1]);
+        }
+      }
+      v8s bh[TMI], bl[TMI];
+#pragma unroll
+      for (int j = 0; j < TMI; ++j) x3_split8(b0[kk][j], b1[kk][j], bh[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < TNI; ++i) {
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk][i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bl[j], acc[i][j], 0, 0, 0);
+        }
+        if (decltype(issue_on)::value && i < PPK && kk * PPK + i < L) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue(kk * PPK + i, nslot);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int q = TNI; q < PPK; ++q)
+        if (decltype(issue_on)::value && kk * PPK + q < L) issue(kk * PPK + q, nslot);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---------------------------------------------------------------------------------- epilogue
+  const int pm = lane & 31;
+  float* red = reinterpret_cast<float*>(lds + NS * STAGE);  // [WM][2][2][BN]: (wave_m, row half, stat, ch)
+  auto epilogue = [&](int tile) {
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const bool want_stats = p.stats != nullptr;
+#pragma unroll
+    for (int i = 0; i < TNI; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
+        const int n = n0 + nl;
+        const bool nok = n < p.K;  // K % 4 == 0 (host-checked): a 4-channel run is all in or all out
+        float b4[4] = {0.f, 0.f, 0.f, 0.f}, k4[4] = {0.f, 0.f, 0.f, 0.f}, mu[4] = {0.f, 0.f, 0.f, 0.f};
+        float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sh4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (nok) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (p.bias) b4[e] = p.bias[n + e];
+            if (p.shift && !p.bnx) k4[e] = p.shift[n + e];
+            if (p.bnx) {
+              mu[e] = p.mean[n + e];
+              if (!p.bits) { sc4[e] = p.bsc[n + e]; sh4[e] = p.bsh[n + e]; }
+            }
+          }
+        }
+        float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) {
+          const int m = m0 + (b_row0 - BN) + 32 * j + pm;
+          if (!nok || m >= p.M) continue;
+          int mo = m;  // pixel of the output grid
+          if (p.scatter) {
+            const int img = m / (p.P * p.Q);
+            const int pq = m - img * p.P * p.Q;
+            const int pp = pq / p.Q, qq = pq - pp * p.Q;
+            mo = (img * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow;
+          }
+          const size_t off = (size_t)mo * p.ldy + n;
+          float v[4] = {acc[i][j][4 * g] + b4[0], acc[i][j][4 * g + 1] + b4[1], acc[i][j][4 * g + 2] + b4[2],
+                        acc[i][j][4 * g + 3] + b4[3]};
+          if (p.res) {
+            bool live = true;
+            size_t roff = off;
+            if (p.res_sh) {
+              const int gridpix = p.scatter ? p.oH * p.oW : p.P * p.Q;
+              const int gw = p.scatter ? p.oW : p.Q;
+              const int img = mo / gridpix;
+              const int hw = mo - img * gridpix;
+              const int hh = hw / gw, ww = hw - hh * gw;
+              live = hh % p.res_sh == 0 && ww % p.res_sw == 0;
+              roff = ((size_t)(img * p.res_H + hh / p.res_sh) * p.res_W + ww / p.res_sw) * p.ldy + n;
+            }
+            if (live) {
+              const v4f r = *reinterpret_cast<const v4f*>(p.res + roff);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += r[e];
+            }
+          }
+          if (p.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if (p.bnx) {
+            const v4f xv = *reinterpret_cast<const v4f*>(p.bnx + (size_t)mo * p.K + n);
+            unsigned mb;
+            if (p.bits) {
+              mb = (p.bits[(size_t)mo * (p.K >> 3) + (n >> 3)] >> (n & 7)) & 0xFu;
+            } else {
+              mb = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) mb |= (fmaf(xv[e], sc4[e], sh4[e]) > 0.f ? 1u : 0u) << e;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = (mb >> e) & 1u ? v[e] : 0.f;
+              s4[e] += v[e];
+              q4[e] = fmaf(v[e], xv[e] - mu[e], q4[e]);
+            }
+          } else if (want_stats) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float a = v[e] - k4[e];
+              s4[e] += a;
+              q4[e] = fmaf(a, a, q4[e]);
+            }
+          }
+          *reinterpret_cast<v4f*>(p.y + off) = (v4f){v[0], v[1], v[2], v[3]};
+        }
+        if (want_stats) {  // fold the 16 pixel lanes of each DPP row; lanes 0 / 16 / 32 / 48 park the row sums
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s4[e] = x3_row_fold(s4[e]);
+            q4[e] = x3_row_fold(q4[e]);
+          }
+          if ((lane & 15) == 0) {
+            const int half = (lane >> 4) & 1;
+            float* rs = red + ((size_t)(wave_m * 2 + half) * 2) * BN + nl;
+            *reinterpret_cast<v4f*>(rs) = (v4f){s4[0], s4[1], s4[2], s4[3]};
+            *reinterpret_cast<v4f*>(rs + BN) = (v4f){q4[0], q4[1], q4[2], q4[3]};
+          }
+        }
+      }
+    if (want_stats) {
+      __syncthreads();
+      const int rep = tm % p.R_rep;
+      for (int t = tid; t < 2 * BN; t += NT) {
+        const int which = t / BN, c = t - which * BN;
+        if (n0 + c >= p.K) continue;
+        float a = 0.f;
+#pragma unroll
+        for (int g = 0; g < WM * 2; ++g) a += red[(g * 2 + which) * BN + c];
+        atomicAdd(&p.stats[((size_t)which * p.R_rep + rep) * p.K + n0 + c], a);
+      }
+    }
+  };
+
+  // ---------------------------------------------------------------------------------- the stream
+  // 3-deep ring over the block's V = t_count · KT k-tiles: k-tile v + 2 is issued while v is multiplied;
+  // after the last k-tile of a tile its epilogue runs first and THEN v + 2's pieces are issued, so the
+  // counted wait (vmcnt = L: stores count too) still leaves exactly those pieces in flight.
+  if constexpr (!PERSIST) {  // one tile: the plain ring, epilogue after the last k-tile
+    prep();
+#pragma unroll
+    for (int i = 0; i < L; ++i) issue(i, 0);
+    if (KT > 1) {
+      prep();
+#pragma unroll
+      for (int i = 0; i < L; ++i) issue(i, 1);
+      X3_WAIT(L);
+    } else {
+      X3_WAIT(0);
+    }
+    X3_BARRIER();
+    int cur = 0, nxt = 2;
+    for (int t = 0; t + 2 < KT; ++t) {
+      prep();
+      compute(cur, nxt, std::true_type{});
+      X3_WAIT(L);
+      X3_BARRIER();
+      cur = cur == NS - 1 ? 0 : cur + 1;
+      nxt = nxt == NS - 1 ? 0 : nxt + 1;
+    }
+    if (KT >= 2) {
+      compute(cur, 0, std::false_type{});
+      X3_WAIT(0);
+      X3_BARRIER();
+      cur = cur == NS - 1 ? 0 : cur + 1;
+    }
+    compute(cur, 0, std::false_type{});
+    epilogue(t_first);
+    return;
+  }
+  const int V = t_count * KT;
+  prep();
+#pragma unroll
+  for (int i = 0; i < L; ++i) issue(i, 0);
+  if (V > 1) {
+    prep();
+#pragma unroll
+    for (int i = 0; i < L; ++i) issue(i, 1);
+    X3_WAIT(L);
+  } else {
+    X3_WAIT(0);
+  }
+  X3_BARRIER();
+  int cur = 0, nxt = 2, c_kt = 0, c_tl = 0;
+  for (int v = 0; v < V; ++v) {
+    const bool more = v + 2 < V;
+    const bool last = c_kt == KT - 1;
+    if (more) prep();
+    if (more && !last) {
+      compute(cur, nxt, std::true_type{});
+    } else {
+      compute(cur, 0, std::false_type{});
+    }
+    if (last) {
+      epilogue(t_first + c_tl);
+#pragma unroll
+      for (int i = 0; i < TNI; ++i)
+#pragma unroll
+        for (int j = 0; j < TMI; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < L; ++i) issue(i, nxt);
+      }
+    }
+    if (v + 1 < V) {
+      if (more) {
+        X3_WAIT(L);
+      } else {
+        X3_WAIT(0);
+      }
+      X3_BARRIER();
+    }
+    cur = cur == NS - 1 ? 0 : cur + 1;
+    nxt = nxt == NS - 1 ? 0 : nxt + 1;
+    if (++c_kt == KT) {
+      c_kt = 0;
+      ++c_tl;
+    }
+  }
+}
+
+// ---- host side ----
+template <int MODE, bool PERSIST>
+static void launch_x3(int bm, int bn, dim3 g, hipStream_t s, const X3Params& p) {
+  if (bm == 128)
+    hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, PERSIST>), g, dim3(256), 0, s, p);
+  else if (bn == 64)
+    hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+}
+
+static int x3_num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// BIGDL_CONV_X3_PERSIST: 0 = one tile per block everywhere, 1 (default) = the pointwise convs stream
+// their tiles through persistent blocks (one per CU)
+static int x3_persist_env() {
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_X3_PERSIST"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
+static bool x3_al(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+// Tile pin for A/B measurements: BIGDL_CONV_X3_TILE = 1 (256×128), 2 (256×64), 3 (128×128).
+static int x3_env_tile() {
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_X3_TILE"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
+// y[M][ldy] (fp32) = conv(x, W) with the epilogues above.  x [Nb][H][W][C] fp32 (C % 32 == 0, 16-B
+// aligned), w2 the chunked [hi | lo] split of the KRSC fp32 filter (bigdl_split_bf16x2 of its
+// [K·R·S·C / 32][32] view), K % 8 == 0 for statistics / bnbwd (else K % 4).  bm / bn: the tile
+// (256 × 128, 256 × 64 or 128 × 128; 0 = heuristic).  osh … oW: the output scatter (1, 1, 0, 0, P, Q =
+// none); res_sh … res_W: the strided residual (0 = dense); persist: pointwise tile streaming (-1 = off,
+// 0 = BIGDL_CONV_X3_PERSIST / default on, 1 = on).  Returns hipError_t.
+BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias, const float* res, float* y,
+                               float* stats, int R_rep, const float* shift, const float* bnx, const float* mean,
+                               const void* bits, const float* bsc, const float* bsh, int Nb, int H, int W, int C,
+                               int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                               int relu, int ldy, int bm, int bn, int osh, int osw, int ooh, int oow, int oH,
+                               int oW, int res_sh, int res_sw, int res_H, int res_W, int persist, hipStream_t s) {
+  if (!x || !w2 || !y || Nb <= 0 || C <= 0 || K <= 0 || P <= 0 || Q <= 0 || C % 32 || K % 4 || ldy < K || ldy % 4)
+    return (int)hipErrorInvalidValue;
+  if (!x3_al(x) || !x3_al(w2) || !x3_al(y) || (res && !x3_al(res)) || (bnx && !x3_al(bnx)))
+    return (int)hipErrorInvalidValue;
+  if (stats && (R_rep <= 0 || K % 8 || ldy != K || (!bnx && (bias || relu || res)))) return (int)hipErrorInvalidValue;
+  if (bnx && (!stats || !mean || relu || bias || (!bits && (!bsc || !bsh)))) return (int)hipErrorInvalidValue;
+  const bool pw1 = R == 1 && S == 1 && ph == 0 && pw == 0;
+  if (!pw1 && R * S > 64) return (int)hipErrorNotSupported;
+  if ((size_t)Nb * H * W * C * 4 >= 0x80000000ull || (size_t)K * R * S * C * 4 >= 0x80000000ull)
+    return (int)hipErrorInvalidValue;
+  const long long Ml = (long long)Nb * P * Q;
+  if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  X3Params p{};
+  p.x = x; p.w = (const bf16_t*)w2; p.bias = bias; p.res = res; p.y = y;
+  p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
+  p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.M = (int)Ml; p.Kg = R * S * C; p.ldx = C; p.ldy = ldy; p.relu = relu;
+  p.stats = stats; p.R_rep = stats ? R_rep : 1; p.shift = bnx ? nullptr : shift;
+  p.bnx = bnx; p.mean = mean; p.bits = (const uint8_t*)bits; p.bsc = bsc; p.bsh = bsh;
+  if (osh <= 0 || osw <= 0 || ooh < 0 || oow < 0) return (int)hipErrorInvalidValue;
+  p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
+  p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
+  if (p.scatter && ((P - 1) * osh + ooh >= oH || (Q - 1) * osw + oow >= oW)) return (int)hipErrorInvalidValue;
+  if (res_sh < 0 || res_sw < 0 || (res_sh > 0) != (res_sw > 0) || (res_sh && !res)) return (int)hipErrorInvalidValue;
+  p.res_sh = res_sh; p.res_sw = res_sw; p.res_H = res_H; p.res_W = res_W;
+  if (res_sh) {
+    const int gh = p.scatter ? oH : P, gw = p.scatter ? oW : Q;
+    if (res_H * res_sh < gh || res_W * res_sw < gw || (res_H - 1) * res_sh >= gh || (res_W - 1) * res_sw >= gw)
+      return (int)hipErrorInvalidValue;
+  }
+  const int et = x3_env_tile();
+  if (et == 1) { bm = 256; bn = 128; } else if (et == 2) { bm = 256; bn = 64; } else if (et == 3) { bm = 128; bn = 128; }
+  if (bm == 0 || bn == 0) {
+    bm = 256;
+    bn = K <= 64 ? 64 : 128;
+  }
+  if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 128))) return (int)hipErrorInvalidValue;
+  p.tiles_n = (K + bn - 1) / bn;
+  const long long tiles = (Ml + bm - 1) / bm * p.tiles_n;
+  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
+  if (pw1 && persist != 0 && (persist > 0 || x3_persist_env())) {
+    const long long nblk = x3_num_cus();  // LDS: one block per CU
+    launch_x3<3, true>(bm, bn, dim3((unsigned)(tiles < nblk ? tiles : nblk)), s, p);
+  } else if (pw1) {
+    launch_x3<3, false>(bm, bn, dim3((unsigned)tiles), s, p);
+  } else {
+    launch_x3<1, false>(bm, bn, dim3((unsigned)tiles), s, p);
+  }
+  BIGDL_CHECK_LAUNCH();
+}

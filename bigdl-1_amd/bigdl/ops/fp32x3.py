@@ -17,6 +17,12 @@ being one GEMM over a 3× longer reduction:
   data gradient's split of dY for stride-1 convs;
 * Linear: the same concatenation along K into the MFMA GEMM with an fp32 C.
 
+With ``bigdl.fp32.direct`` (default) convolutions whose reduction channels are a multiple of 32 skip
+the materialised splits altogether: ``csrc/conv_x3.hip`` stages the raw fp32 activations / gradients
+by LDS-DMA and splits each MFMA fragment while reading it (pre-split 32-channel [hi | lo] weight
+chunks on the other side), and the weight gradient runs ONE launch of the fp32-operand wgrad kernel
+(split between its global load and LDS store) — so the BatchNorm passes around them write fp32 only.
+
 Every entry returns ``NotImplemented`` for a case it does not cover (grouped conv, fused BN
 prologues) and the caller falls back to the torch op.  ``bigdl.fp32.native=false`` turns the path
 off (torch / MIOpen fp32 everywhere).
@@ -95,8 +101,11 @@ _SPLITS: dict = {}
 
 
 def split_buffer(rows, c, device):
-    """A [rows][2·c] bf16 buffer for a producer-side split, or None when the path is off."""
+    """A [rows][2·c] bf16 buffer for a producer-side split, or None when the path is off (or not
+    needed: with the direct kernels a consumer of C % 32 channels reads the fp32 tensor itself)."""
     if c % 8 or not _two_part() or not config.get_property("bigdl.fp32.producerSplit"):
+        return None
+    if c % 32 == 0 and _direct():
         return None
     return torch.empty((rows, 2 * c), dtype=_bf16, device=device)
 
@@ -133,6 +142,76 @@ def producer_bits(t):
     """The ReLU mask bits the fp32 BN forward wrote for its output ``t`` (None if absent)."""
     e = _entry(t)
     return None if e is None else e[3]
+
+
+def _direct() -> bool:
+    return bool(config.get_property("bigdl.fp32.direct"))
+
+
+def _x3_has() -> bool:
+    return hasattr(N.lib(), "bigdl_conv_x3") and hasattr(N.lib(), "bigdl_conv_wgrad_f32")
+
+
+def _al(t) -> bool:
+    return t is None or t.data_ptr() % 16 == 0
+
+
+def _cl_f32(t) -> bool:
+    return t.dtype == _f32 and t.dim() == 4 and t.is_contiguous(memory_format=_cl) and t.data_ptr() % 16 == 0
+
+
+def chunk_split(w_rows: torch.Tensor) -> torch.Tensor:
+    """fp32 [rows][n] (n % 32 == 0) → the conv_x3 weight operand: bf16 [rows][n / 32][64], each
+    32-index chunk as [hi | lo] (one 128-B LDS row per k-tile)."""
+    v = w_rows.reshape(-1, 32)
+    if not v.is_contiguous():
+        v = v.contiguous()
+    return split2(v, 32)
+
+
+def _x3(x, w2, y, nb, h, w, c, k, r, s, p, q, stride, pad, dil, bias=None, res=None, relu=False, stats=None, rep=0,
+        shift=None, bnx=None, mean=None, bits=None, bsc=None, bsh=None, scatter=None, res_strided=None, tile=None,
+        persist=0):
+    """One conv_x3 launch (csrc/conv_x3.hip); ``scatter`` = (osh, osw, ooh, oow, oH, oW) of a
+    sub-pixel dgrad, ``res_strided`` = (res_sh, res_sw, res_H, res_W) of a compact residual."""
+    osh, osw, ooh, oow, oh_, ow_ = scatter if scatter is not None else (1, 1, 0, 0, p, q)
+    rsh, rsw, rh, rw = res_strided if res_strided is not None else (0, 0, 0, 0)
+    check(N.lib().bigdl_conv_x3(ptr(x), ptr(w2), ptr(bias), ptr(res), ptr(y), ptr(stats), rep, ptr(shift), ptr(bnx),
+                                ptr(mean), ptr(bits), ptr(bsc), ptr(bsh), nb, h, w, c, k, r, s, p, q, stride[0],
+                                stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), k,
+                                *(tile if tile is not None else _X3_TILES.get((nb, h, w, c, k, r, s, p, q), (0, 0))),
+                                osh, osw, ooh,
+                                oow, oh_, ow_, rsh, rsw, rh, rw, persist, _s()), "conv_x3")
+
+
+#: per-geometry tile choice (bm, bn) for conv_x3 launches, filled by the training compile phase /
+#: tools/bench_x3.py; absent = the kernel's heuristic
+_X3_TILES: dict = {}
+
+
+def _x3_geom_ok(c, k, r, s, pad):
+    return c % 32 == 0 and k % 8 == 0 and (r * s <= 64 or (r == 1 and s == 1 and tuple(pad) == (0, 0)))
+
+
+def _w_fwd(w4):
+    """The forward filter as conv_x3 chunks: KRSC rows of R·S·C."""
+    k = w4.shape[0]
+    return chunk_split(w4.detach().float().permute(0, 2, 3, 1).reshape(k, -1))
+
+
+def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None):
+    nb, c, h, w = x.shape
+    k, _, r, s = w4.shape
+    if not (_direct() and _x3_has() and _x3_geom_ok(c, k, r, s, pad) and _cl_f32(x)):
+        return NotImplemented
+    p, q = _out_hw(h, w, r, s, stride, pad, dilation)
+    if p <= 0 or q <= 0 or not _fits(nb * h * w * c * 4, k * r * s * c * 4):
+        return NotImplemented
+    y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
+    bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
+    _x3(x, _w_fwd(w4), y, nb, h, w, c, k, r, s, p, q, stride, pad, dilation, bias=bias, relu=relu, stats=stats,
+        rep=rep, shift=shift)
+    return y
 
 
 def _act_split(rows2d, cp, two, src=None):
@@ -189,6 +268,9 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     same input, which then skips its own split of x."""
     if groups != 1 or x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1]:
         return NotImplemented
+    y = _direct_forward(x, w4, b, stride, pad, dilation, relu)
+    if y is not NotImplemented:
+        return y
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
@@ -230,6 +312,9 @@ def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
     if (k % 8 or shift is None or shift.dtype != _f32 or shift.numel() != k or not shift.is_contiguous()
             or buf.dtype != _f32 or buf.numel() != 2 * rep * k or not 1 <= rep <= 512):
         return NotImplemented
+    y = _direct_forward(x, w4, None, stride, pad, dilation, False, stats=buf, rep=rep, shift=shift)
+    if y is not NotImplemented:
+        return y, buf, rep
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
     cp = _r(c, 8)
     if p <= 0 or q <= 0 or not _fits(nb * h * w * 2 * cp * 2, k * r * s * 3 * cp * 2):
@@ -269,14 +354,145 @@ def _bnbwd_args(bn_fuse, nb, c, h, w, res):
     return buf, rep, bx, mean, bits, sc, sh
 
 
+_PARITY: dict = {}
+
+
+def _parity(h, w, r, s, stride, pad):
+    key = (h, w, r, s, tuple(stride), tuple(pad))
+    cl = _PARITY.get(key)
+    if cl is None:
+        from .native_ops import _parity_classes
+        cl = _PARITY[key] = _parity_classes(h, w, r, s, stride[0], stride[1], pad[0], pad[1])
+    return cl
+
+
+def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, lazy):
+    """fp32 data gradient on conv_x3: a stride-1 conv of dY with the flipped, transposed filter
+    (C·R·S rows of K); strided convs by sub-pixel decomposition (one scatter launch per parity class
+    that receives taps).  Returns gi, a StridedGrad (``lazy`` 1×1 stride-s), or NotImplemented."""
+    from .reference import StridedGrad
+    nb, c, h, w = x_shape
+    k, _, r, s = w4.shape
+    p, q = gy.shape[2], gy.shape[3]
+    if tuple(dilation) != (1, 1) or k % 32 or c % 8 or not _cl_f32(gy):
+        return NotImplemented
+    if not _fits(nb * p * q * k * 4, c * r * s * k * 4, nb * h * w * c * 4):
+        return NotImplemented
+    res_strided = None
+    if isinstance(residual, StridedGrad):
+        rt = residual.t
+        if not (rt.dtype == _f32 and _cl_f32(rt) and rt.shape[0] == nb and rt.shape[1] == c
+                and tuple(residual.shape) == (nb, c, h, w)):
+            residual = residual.dense()
+        else:
+            res_strided = (residual.stride[0], residual.stride[1], rt.shape[2], rt.shape[3])
+            residual = rt
+    if residual is not None and res_strided is None and not (residual.dtype == _f32 and _cl_f32(residual)
+                                                             and tuple(residual.shape) == (nb, c, h, w)):
+        return NotImplemented
+    bnb = _bnbwd_args(bn_fuse, nb, c, h, w, residual) if bn_fuse is not None else None
+    if bn_fuse is not None and bnb is None:
+        bn_fuse = None
+    if tuple(stride) == (1, 1):
+        pd = (r - 1 - pad[0], s - 1 - pad[1])
+        if pd[0] < 0 or pd[1] < 0 or not _x3_geom_ok(k, c, r, s, pd) or (h, w) != (p + 2 * pd[0] - r + 1,
+                                                                                 q + 2 * pd[1] - s + 1):
+            return NotImplemented
+        wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1)  # [C][R][S][K]
+        gi = torch.empty((nb, c, h, w), dtype=_f32, device=gy.device, memory_format=_cl)
+        if bnb is not None:
+            buf, rep, bx, mean, bits, bsc, bsh = bnb
+            _x3(gy, chunk_split(wt), gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual, stats=buf,
+                rep=rep, bnx=bx, mean=mean, bits=bits, bsc=bsc, bsh=bsh, res_strided=res_strided)
+            bn_fuse["partial"], bn_fuse["G"] = buf, rep
+        else:
+            _x3(gy, chunk_split(wt), gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual,
+                res_strided=res_strided)
+        return gi
+    if bnb is not None or res_strided is not None:
+        return NotImplemented
+    classes = _parity(h, w, r, s, stride, pad)
+    live = [cl for cl in classes if cl[2] and cl[3]]
+    if not live or any(not _x3_geom_ok(k, c, len(cl[2]), len(cl[3]), (len(cl[2]) - 1 - cl[6], len(cl[3]) - 1 - cl[7]))
+                       for cl in live):
+        return NotImplemented
+    wf = w4.detach().float()
+    if lazy and residual is None and r == 1 and s == 1 and tuple(pad) == (0, 0) and len(live) == 1:
+        (a, b, rs, ss, ho, wo, ea, eb) = live[0]
+        tmp = torch.empty((nb, c, ho, wo), dtype=_f32, device=gy.device, memory_format=_cl)
+        _x3(gy, chunk_split(wf.reshape(k, c).t()), tmp, nb, p, q, k, c, 1, 1, ho, wo, (1, 1), (0, 0), (1, 1))
+        return StridedGrad(tmp, tuple(stride), (nb, c, h, w))
+    gi = torch.empty((nb, c, h, w), dtype=_f32, device=gy.device, memory_format=_cl)
+    if len(live) != len(classes) or sum(cl[4] * cl[5] for cl in live) != h * w:
+        if residual is not None:
+            gi.copy_(residual)
+        else:
+            gi.zero_()
+    for (a, b, rs, ss, ho, wo, ea, eb) in live:
+        ra, sb = len(rs), len(ss)
+        sub = wf[:, :, rs[::-1]][:, :, :, ss[::-1]].permute(1, 2, 3, 0).reshape(c, -1)  # [C][Ra][Sb][K]
+        _x3(gy, chunk_split(sub), gi, nb, p, q, k, c, ra, sb, ho, wo, (1, 1), (ra - 1 - ea, sb - 1 - eb), (1, 1),
+            res=residual, scatter=(stride[0], stride[1], a, b, h, w))
+    return gi
+
+
+def _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation):
+    nb, c, h, w = x.shape
+    k, _, r, s = gw_acc.shape
+    p, q = gy.shape[2], gy.shape[3]
+    if not (_direct() and _x3_has() and c % 8 == 0 and k % 8 == 0 and _cl_f32(x) and _cl_f32(gy)
+            and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
+            and _fits(nb * h * w * c * 4, nb * p * q * k * 4)):
+        return NotImplemented
+    check(N.lib().bigdl_conv_wgrad_f32(ptr(x), ptr(gy), ptr(gw_acc), C.c_float(float(scale)), nb, h, w, c, k, r, s, p,
+                                       q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0, _s()),
+          "conv_wgrad_f32")
+    return None
+
+
 def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                  scale=1.0, residual=None, slot=None, bn_fuse=None):
+                  scale=1.0, residual=None, slot=None, bn_fuse=None, lazy_strided=False):
     """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation.  ``bn_fuse``
     (conv.py: the BN + ReLU whose output this conv consumed): the data gradient's epilogue stores the
     ReLU-masked gradient and adds that BN's backward statistics into its replicated buffer, reported
-    back as ``bn_fuse["partial"], bn_fuse["G"]``."""
+    back as ``bn_fuse["partial"], bn_fuse["G"]``.  ``residual`` may be a StridedGrad (summed as a
+    compact strided residual by the direct kernels); ``lazy_strided``: a 1×1 stride-s conv may return
+    its input gradient as a StridedGrad."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
+    if _direct() and _x3_has() and _cl_f32(gy) and x.dtype == _f32:
+        # each half independently on the direct kernels when its shape allows, else on the split path
+        gi = None
+        if need_input:
+            gi = _direct_dgrad(gy, w4, tuple(x.shape), stride, pad, dilation, residual, bn_fuse, lazy_strided)
+            if gi is NotImplemented:
+                gi = _split_backward(gy, x, w4, stride, pad, dilation, True, None, scale, slot, residual, bn_fuse)
+                if gi is NotImplemented:
+                    return NotImplemented
+        if gw_acc is not None and scale != 0:
+            if _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation) is NotImplemented:
+                r = _split_backward(gy, x, w4, stride, pad, dilation, False, gw_acc, scale, slot)
+                if r is NotImplemented:
+                    return NotImplemented
+        if gb_acc is not None and scale != 0:
+            gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+        return gi
+    return _split_backward_full(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale, residual, slot,
+                                bn_fuse)
+
+
+
+def _split_backward(gy, x, w4, stride, pad, dilation, need_input, gw_acc, scale, slot, residual=None, bn_fuse=None):
+    return _split_backward_full(gy, x, w4, stride, pad, dilation, need_input, gw_acc, None, scale, residual, slot,
+                                bn_fuse)
+
+
+def _split_backward_full(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale, residual, slot,
+                         bn_fuse):
+    """The split-operand backward (materialised [hi | lo] splits of dY and x)."""
+    from .reference import StridedGrad
+    if isinstance(residual, StridedGrad):
+        residual = residual.dense()
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
     p, q = gy.shape[2], gy.shape[3]

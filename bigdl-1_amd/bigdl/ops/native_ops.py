@@ -1363,9 +1363,8 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
     if isinstance(gy, torch.Tensor) and gy.dtype == _f32 and x.dtype == _f32 and F3.enabled(gy):
         # fp32 (bf16x3): the bf16 epilogue fusions are optional — bn_fuse is left unconsumed (the BN
         # runs its own backward), a lazy strided gradient is returned dense
-        res = residual.dense() if isinstance(residual, R_.StridedGrad) else residual
-        r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, res,
-                             slot=pad_slot, bn_fuse=bn_fuse)
+        r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, residual,
+                             slot=pad_slot, bn_fuse=bn_fuse, lazy_strided=lazy_strided)
         if r is not NotImplemented:
             return r
     if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):

@@ -196,6 +196,7 @@ def test_fp32_conv_uses_producer_split():
     w = (torch.randn(32, 64, 3, 3, generator=g) * 0.05).to(dev)
     gam, bet = torch.rand(64, generator=g).to(dev) + 0.5, torch.randn(64, generator=g).to(dev)
     outs = []
+    config.set_property("bigdl.fp32.direct", False)  # the split-operand kernels (direct ones need no split)
     for on in (True, False):
         config.set_property("bigdl.fp32.producerSplit", on)
         try:
@@ -209,6 +210,7 @@ def test_fp32_conv_uses_producer_split():
             outs.append((y.clone(), hit, n_split))
         finally:
             config.set_property("bigdl.fp32.producerSplit", True)
+    config.set_property("bigdl.fp32.direct", True)
     (y1, hit1, n1), (y0, hit0, n0) = outs
     assert hit1 and not hit0 and n1 == n0 - 1, (hit1, hit0, n1, n0)
     assert torch.equal(y1, y0)
