@@ -300,7 +300,9 @@ class SpatialConvolution(TensorModule):
             res, self._grad_residual = self._grad_residual, None
             if res is not None:
                 return as_dense(res).clone()
-            return torch.zeros_like(input) if isinstance(input, torch.Tensor) else None
+            # the reference returns its (empty) gradInput untouched (SpatialConvolution.scala:364-366):
+            # no zero-filled input-sized tensor
+            return torch.empty(0, device=input.device, dtype=input.dtype) if isinstance(input, torch.Tensor) else None
         # compute gradInput and (fused) parameter gradients in one pass; accGradParameters then
         # only applies regularisers
         gi = self._backward(input, gradOutput, True, True)

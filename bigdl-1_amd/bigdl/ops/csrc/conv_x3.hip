@@ -117,13 +117,14 @@ __device__ __forceinline__ float x3_row_fold(float v) {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, bool PERSIST>
-__global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
+template <int BM, int BN, int WM, int WN, int MODE, bool PERSIST, int NSX = 3>
+__global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Params p) {
   static_assert(MODE == 1 || MODE == 3, "tap-uniform / pointwise gathers only");
   constexpr bool PW = MODE == 3;
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BK = 32;                       // reduction indices per k-tile (one 128-B row each side)
-  constexpr int NS = 3;                        // LDS ring depth
+  constexpr int NS = NSX;                      // LDS ring depth (2: two blocks share a CU)
+  static_assert(NS == 3 || (NS == 2 && !PERSIST), "2-deep ring: one tile per block");
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;  // 8-row DMA groups per wave: weights, activations
   static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
@@ -296,30 +297,31 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
       b0[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[0]);
       b1[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[0]);
     }
+    // fragments of slice 1 in flight during slice 0's MFMAs
+#pragma unroll
+    for (int i = 0; i < TNI; ++i) {
+      ah[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[1]);
+      al[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[1]);
+    }
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) {
+      b0[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[1]);
+      b1[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[1]);
+    }
+    // slice 0's B split is exposed; slice 1's is issued right after slice 0's MFMAs so it overlaps
+    // them in the matrix pipe (the MFMA only holds vector issue for 8 of its 32 cycles)
+    v8s bh[2][TMI], bl[2][TMI];
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) x3_split8(b0[0][j], b1[0][j], bh[0][j], bl[0][j]);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      if (kk == 0) {  // fragments of slice 1 in flight during slice 0's MFMAs
-#pragma unroll
-        for (int i = 0; i < TNI; ++i) {
-          ah[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[1]);
-          al[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[1]);
-        }
-#pragma unroll
-        for (int j = 0; j < TMI; ++j) {
-          b0[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[1]);
-          b1[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[1]);
-        }
-      }
-      v8s bh[TMI], bl[TMI];
-#pragma unroll
-      for (int j = 0; j < TMI; ++j) x3_split8(b0[kk][j], b1[kk][j], bh[j], bl[j]);
 #pragma unroll
       for (int i = 0; i < TNI; ++i) {
 #pragma unroll
         for (int j = 0; j < TMI; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk][i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bh[kk][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk][i], bh[kk][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bl[kk][j], acc[i][j], 0, 0, 0);
         }
         if (decltype(issue_on)::value && i < PPK && kk * PPK + i < L) {
           __builtin_amdgcn_sched_barrier(0);
@@ -331,6 +333,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
       for (int q = TNI; q < PPK; ++q)
         if (decltype(issue_on)::value && kk * PPK + q < L) issue(kk * PPK + q, nslot);
       __builtin_amdgcn_sched_barrier(0);
+      if (kk == 0) {
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) x3_split8(b0[1][j], b1[1][j], bh[1][j], bl[1][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
 
@@ -341,6 +348,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const bool want_stats = p.stats != nullptr;
+    // this lane's output-grid pixel per row block (−1: past M), computed once per tile
+    int mo_[TMI];
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) {
+      const int m = m0 + (b_row0 - BN) + 32 * j + pm;
+      int mo = m < p.M ? m : -1;
+      if (p.scatter && mo >= 0) {
+        const int img = m / (p.P * p.Q);
+        const int pq = m - img * p.P * p.Q;
+        const int pp = pq / p.Q, qq = pq - pp * p.Q;
+        mo = (img * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow;
+      }
+      mo_[j] = mo;
+    }
 #pragma unroll
     for (int i = 0; i < TNI; ++i)
 #pragma unroll
@@ -364,15 +385,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
         float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < TMI; ++j) {
-          const int m = m0 + (b_row0 - BN) + 32 * j + pm;
-          if (!nok || m >= p.M) continue;
-          int mo = m;  // pixel of the output grid
-          if (p.scatter) {
-            const int img = m / (p.P * p.Q);
-            const int pq = m - img * p.P * p.Q;
-            const int pp = pq / p.Q, qq = pq - pp * p.Q;
-            mo = (img * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow;
-          }
+          if (!nok || mo_[j] < 0) continue;
+          const int mo = mo_[j];
           const size_t off = (size_t)mo * p.ldy + n;
           float v[4] = {acc[i][j][4 * g] + b4[0], acc[i][j][4 * g + 1] + b4[1], acc[i][j][4 * g + 2] + b4[2],
                         acc[i][j][4 * g + 3] + b4[3]};
@@ -456,6 +470,24 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
   // 3-deep ring over the block's V = t_count · KT k-tiles: k-tile v + 2 is issued while v is multiplied;
   // after the last k-tile of a tile its epilogue runs first and THEN v + 2's pieces are issued, so the
   // counted wait (vmcnt = L: stores count too) still leaves exactly those pieces in flight.
+  if constexpr (NS == 2) {  // 2-deep ring: k-tile t + 1 in flight while t is multiplied
+    prep();
+#pragma unroll
+    for (int i = 0; i < L; ++i) issue(i, 0);
+    X3_WAIT(0);
+    X3_BARRIER();
+    int cur = 0;
+    for (int t = 0; t + 1 < KT; ++t) {
+      prep();
+      compute(cur, cur ^ 1, std::true_type{});
+      X3_WAIT(0);
+      X3_BARRIER();
+      cur ^= 1;
+    }
+    compute(cur, 0, std::false_type{});
+    epilogue(t_first);
+    return;
+  }
   if constexpr (!PERSIST) {  // one tile: the plain ring, epilogue after the last k-tile
     prep();
 #pragma unroll
@@ -542,14 +574,23 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x3(X3Params p) {
 }
 
 // ---- host side ----
+// wave layout `wl`: 0 = the 2-D split (WM × WN = 4 × 2 / 2 × 2), 1 = waves over pixels only (8 × 1 /
+// 4 × 1): each wave's split B fragment then feeds all BN / 32 channel blocks (half the split VALU per MFMA)
 template <int MODE, bool PERSIST>
-static void launch_x3(int bm, int bn, dim3 g, hipStream_t s, const X3Params& p) {
-  if (bm == 128)
-    hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, PERSIST>), g, dim3(256), 0, s, p);
-  else if (bn == 64)
-    hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
-  else
-    hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+static void launch_x3(int bm, int bn, int wl, int ns2, dim3 g, hipStream_t s, const X3Params& p) {
+  if (bm == 128 && ns2 && !PERSIST) {
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, false, 2>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, false, 2>), g, dim3(256), 0, s, p);
+  } else if (bm == 128) {
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, PERSIST>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, PERSIST>), g, dim3(256), 0, s, p);
+  } else if (bn == 64) {
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 64, 8, 1, MODE, PERSIST>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+  } else {
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 128, 8, 1, MODE, PERSIST>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+  }
 }
 
 static int x3_num_cus() {
@@ -562,10 +603,10 @@ static int x3_num_cus() {
   return n;
 }
 
-// BIGDL_CONV_X3_PERSIST: 0 = one tile per block everywhere, 1 (default) = the pointwise convs stream
-// their tiles through persistent blocks (one per CU)
+// BIGDL_CONV_X3_PERSIST: 0 (default) = one tile per block everywhere, 1 = the pointwise convs stream
+// their tiles through persistent blocks (one per CU); off by default: no gain measured (profiles/r5_x3_shapes.txt)
 static int x3_persist_env() {
-  static const int v = [] { const char* e = getenv("BIGDL_CONV_X3_PERSIST"); return e ? atoi(e) : 1; }();
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_X3_PERSIST"); return e ? atoi(e) : 0; }();
   return v;
 }
 
@@ -621,21 +662,42 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   }
   const int et = x3_env_tile();
   if (et == 1) { bm = 256; bn = 128; } else if (et == 2) { bm = 256; bn = 64; } else if (et == 3) { bm = 128; bn = 128; }
-  if (bm == 0 || bn == 0) {
-    bm = 256;
-    bn = K <= 64 ? 64 : 128;
+  if (bm == 0) {
+    // measured per ResNet-50 shape (tools/bench_x3.py, profiles/r5_x3_shapes.txt): 3×3 convs run best as
+    // two 128 × 128 blocks per CU (2-deep ring, waves over pixels) except the 64-channel ones (256 × 64,
+    // 8 × 1); pointwise convs on 256 × 128 / 256 × 64 (4 × 2), the 7² ones as two 128 × 128 blocks per CU
+    const bool pw1_ = R == 1 && S == 1 && ph == 0 && pw == 0;
+    if (!pw1_) {
+      bm = K <= 64 ? 256 : 128;
+      bn = K <= 64 ? (64 | 0x100) : (128 | 0x300);
+    } else if (K <= 64) {
+      bm = 256;
+      bn = 64;
+    } else if (Ml <= 2 * 12544) {
+      bm = 128;
+      bn = 128 | 0x300;
+    } else {
+      bm = 256;
+      bn = 128;
+    }
   }
+  int wl = (bn >> 8) & 1;  // bit 8 of bn: the pixels-only wave layout
+  const int ns2 = (bn >> 9) & 1;  // bit 9: the 2-deep ring (128 × 128 tile: two blocks per CU)
+  bn &= 0xFF;
+  if (bn == 0) bn = K <= 64 ? 64 : 128;
   if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 128))) return (int)hipErrorInvalidValue;
+  static const int wl_env = [] { const char* e = getenv("BIGDL_CONV_X3_WL"); return e ? atoi(e) : -1; }();
+  if (wl_env >= 0) wl = wl_env;
   p.tiles_n = (K + bn - 1) / bn;
   const long long tiles = (Ml + bm - 1) / bm * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   if (pw1 && persist != 0 && (persist > 0 || x3_persist_env())) {
     const long long nblk = x3_num_cus();  // LDS: one block per CU
-    launch_x3<3, true>(bm, bn, dim3((unsigned)(tiles < nblk ? tiles : nblk)), s, p);
+    launch_x3<3, true>(bm, bn, wl, ns2, dim3((unsigned)(tiles < nblk ? tiles : nblk)), s, p);
   } else if (pw1) {
-    launch_x3<3, false>(bm, bn, dim3((unsigned)tiles), s, p);
+    launch_x3<3, false>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   } else {
-    launch_x3<1, false>(bm, bn, dim3((unsigned)tiles), s, p);
+    launch_x3<1, false>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   }
   BIGDL_CHECK_LAUNCH();
 }

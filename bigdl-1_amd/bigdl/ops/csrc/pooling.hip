@@ -13,8 +13,21 @@ struct PoolGeom {
   int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
 };
 
-template <typename IT>
-__global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+// 8 consecutive channels of either element type (bf16: one 16-B access; fp32: two) — the fp32
+// instantiations serve bigdl.compute.dtype=fp32 (the reference's precision), the bf16 ones the default.
+__device__ __forceinline__ void pld8(const bf16_t* p, float* o) { load8(p, o); }
+__device__ __forceinline__ void pld8(const float* p, float* o) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void pst8(bf16_t* p, const float* o) { store8(p, o); }
+__device__ __forceinline__ void pst8(float* p, const float* o) {
+  *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_fwd(const T* __restrict__ x, T* __restrict__ y,
                                                      int8_t* __restrict__ idx, PoolGeom g) {
   const int CG = g.C >> 3;
   const IT total = (IT)g.N * g.P * g.Q * CG;
@@ -37,7 +50,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
         const int w = w0 + j;
         if ((unsigned)w >= (unsigned)g.W) continue;
         float v[8];
-        load8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+        pld8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (v[e] > best[e] || v[e] != v[e]) {  // NaN propagates like torch
@@ -48,7 +61,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
       }
     }
     const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8;
-    store8(y + o, best);
+    pst8(y + o, best);
     if (!idx) continue;  // inference: no argmax for a backward (uniform per launch)
     uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -59,9 +72,9 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
   }
 }
 
-template <typename IT>
-__global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ gy, const int8_t* __restrict__ idx,
-                                                     bf16_t* __restrict__ gx, PoolGeom g) {
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_bwd(const T* __restrict__ gy, const int8_t* __restrict__ idx,
+                                                     T* __restrict__ gx, PoolGeom g) {
   const int CG = g.C >> 3;
   const IT total = (IT)g.N * g.H * g.W * CG;
   for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
@@ -92,7 +105,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
         const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8;
         const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
         float gv[8];
-        load8(gy + o, gv);
+        pld8(gy + o, gv);
         const uint32_t aw[2] = {a.x, a.y};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -101,7 +114,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
         }
       }
     }
-    store8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+    pst8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
   }
 }
 
@@ -298,8 +311,8 @@ __device__ __forceinline__ float avg_count(const PoolGeom& g, int p, int q, int 
   return (float)((he - hs) * (we - ws));
 }
 
-template <typename IT>
-__global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g,
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_avgpool_fwd(const T* __restrict__ x, T* __restrict__ y, PoolGeom g,
                                                      int cip, int divisor) {
   const int CG = g.C >> 3;
   const IT total = (IT)g.N * g.P * g.Q * CG;
@@ -316,19 +329,19 @@ __global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ 
     for (int h = hb; h < he; ++h)
       for (int w = wb; w < we; ++w) {
         float v[8];
-        load8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+        pld8(x + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += v[e];
       }
     const float inv = 1.f / fmaxf(avg_count(g, p, q, cip, divisor), 1.f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] *= inv;
-    store8(y + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, acc);
+    pst8(y + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, acc);
   }
 }
 
-template <typename IT>
-__global__ void __launch_bounds__(256) k_avgpool_bwd(const bf16_t* __restrict__ gy, bf16_t* __restrict__ gx, PoolGeom g,
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_avgpool_bwd(const T* __restrict__ gy, T* __restrict__ gx, PoolGeom g,
                                                      int cip, int divisor) {
   const int CG = g.C >> 3;
   const IT total = (IT)g.N * g.H * g.W * CG;
@@ -347,12 +360,12 @@ __global__ void __launch_bounds__(256) k_avgpool_bwd(const bf16_t* __restrict__ 
     for (int p = p_lo; p <= p_hi; ++p)
       for (int q = q_lo; q <= q_hi; ++q) {
         float v[8];
-        load8(gy + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, v);
+        pld8(gy + (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8, v);
         const float inv = 1.f / fmaxf(avg_count(g, p, q, cip, divisor), 1.f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] = fmaf(v[e], inv, acc[e]);
       }
-    store8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+    pst8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
   }
 }
 
@@ -387,5 +400,66 @@ BIGDL_EXPORT int bigdl_avgpool_bwd(const void* gy, void* gx, int N, int H, int W
   else
     hipLaunchKernelGGL(k_avgpool_bwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (bf16_t*)gx, g,
                        count_include_pad, divisor);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// ---- fp32 NHWC (bigdl.compute.dtype=fp32): same kernels, fp32 elements; C % 8 == 0, 16-B aligned ----
+static bool pool32_ok(const void* a, const void* b, int C) {
+  return C % 8 == 0 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
+}
+
+BIGDL_EXPORT int bigdl_maxpool32_fwd(const float* x, float* y, void* idx, int N, int H, int W, int C, int P, int Q,
+                                     int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  if (kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0 || !pool32_ok(x, y, C)) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * P * Q * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL((k_maxpool_fwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, x, y, (int8_t*)idx, g);
+  else
+    hipLaunchKernelGGL((k_maxpool_fwd<long long, float>), dim3(grid), dim3(256), 0, s, x, y, (int8_t*)idx, g);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_maxpool32_bwd(const float* gy, const void* idx, float* gx, int N, int H, int W, int C, int P,
+                                     int Q, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  if (kh * kw > 127 || N <= 0 || !idx || !pool32_ok(gy, gx, C)) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * H * W * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL((k_maxpool_bwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, gy, (const int8_t*)idx, gx, g);
+  else
+    hipLaunchKernelGGL((k_maxpool_bwd<long long, float>), dim3(grid), dim3(256), 0, s, gy, (const int8_t*)idx, gx, g);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_avgpool32_fwd(const float* x, float* y, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                                     int sh, int sw, int ph, int pw, int count_include_pad, int divisor, hipStream_t s) {
+  if (N <= 0 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || !pool32_ok(x, y, C))
+    return (int)hipErrorInvalidValue;
+  if (2 * ph > kh || 2 * pw > kw) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * P * Q * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL((k_avgpool_fwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, x, y, g, count_include_pad, divisor);
+  else
+    hipLaunchKernelGGL((k_avgpool_fwd<long long, float>), dim3(grid), dim3(256), 0, s, x, y, g, count_include_pad, divisor);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_avgpool32_bwd(const float* gy, float* gx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                                     int sh, int sw, int ph, int pw, int count_include_pad, int divisor, hipStream_t s) {
+  if (N <= 0 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || !pool32_ok(gy, gx, C))
+    return (int)hipErrorInvalidValue;
+  if (2 * ph > kh || 2 * pw > kw) return (int)hipErrorInvalidValue;
+  PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long long total = (long long)N * H * W * (C / 8);
+  const int grid = bigdl_grid(total, 256, 16384);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL((k_avgpool_bwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, gy, gx, g, count_include_pad, divisor);
+  else
+    hipLaunchKernelGGL((k_avgpool_bwd<long long, float>), dim3(grid), dim3(256), 0, s, gy, gx, g, count_include_pad, divisor);
   BIGDL_CHECK_LAUNCH();
 }

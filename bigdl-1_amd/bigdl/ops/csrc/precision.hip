@@ -87,3 +87,43 @@ BIGDL_EXPORT int bigdl_split_bf16x2(const float* src, long long rows, int C, lon
                      vec4, 2);
   BIGDL_CHECK_LAUNCH();
 }
+
+// Space-to-depth of a stride-2 convolution's input (the fp32 RGB stem on the direct kernels,
+// csrc/conv_x3.hip, which need C % 32 == 0): x (any strides, element (n, c, h, w) at
+// x + n·sn + c·sc + h·sh + w·sw) padded by (ph, pw) at the top / left and by zeros beyond, split into 2×2
+// blocks: out[n][h2][w2][c·4 + bh·2 + bw] = xpad[n][c][2·h2 + bh][2·w2 + bw] for c < C, zero for the
+// channels up to Cp (% 4 == 0).  A stride-2 R×S conv of x is then a stride-1 ⌈R/2⌉×⌈S/2⌉ conv of `out`
+// with the filter rearranged the same way (ops/fp32x3.py _stem_weights).  One thread per output pixel.
+__global__ void __launch_bounds__(256) k_s2d_f32(const float* __restrict__ x, long long sn, long long sc, long long sh,
+                                                 long long sw, int N, int C, int H, int W, int ph, int pw, int H2,
+                                                 int W2, int Cp, float* __restrict__ out) {
+  const long long total = (long long)N * H2 * W2;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int w2 = (int)(t % W2);
+    const long long r = t / W2;
+    const int h2 = (int)(r % H2);
+    const int n = (int)(r / H2);
+    float* o = out + t * Cp;
+    for (int c0 = 0; c0 < Cp; c0 += 4) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = c0 + e, c = cc >> 2, bh = (cc >> 1) & 1, bw = cc & 1;
+        const int h = 2 * h2 + bh - ph, w = 2 * w2 + bw - pw;
+        v[e] = (c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+                   ? x[n * sn + c * sc + h * sh + w * sw] : 0.f;
+      }
+      *reinterpret_cast<float4*>(o + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+BIGDL_EXPORT int bigdl_s2d_f32(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C,
+                               int H, int W, int ph, int pw, int H2, int W2, int Cp, float* out, hipStream_t s) {
+  if (!x || !out || N <= 0 || C <= 0 || H2 <= 0 || W2 <= 0 || Cp % 4 || 4 * C > Cp || ((uintptr_t)out & 15))
+    return (int)hipErrorInvalidValue;
+  const long long total = (long long)N * H2 * W2;
+  hipLaunchKernelGGL(k_s2d_f32, dim3(bigdl_grid(total, 256, 16384)), dim3(256), 0, s, x, sn, sc, sh, sw, N, C, H, W, ph,
+                     pw, H2, W2, Cp, out);
+  BIGDL_CHECK_LAUNCH();
+}

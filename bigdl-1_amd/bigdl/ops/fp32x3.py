@@ -199,9 +199,80 @@ def _w_fwd(w4):
     return chunk_split(w4.detach().float().permute(0, 2, 3, 1).reshape(k, -1))
 
 
-def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None):
+def _stem_ok(c, k, stride, dilation):
+    return (tuple(stride) == (2, 2) and tuple(dilation) == (1, 1) and 4 * c <= 32 and c % 32 != 0 and k % 8 == 0
+            and _direct() and _x3_has() and hasattr(N.lib(), "bigdl_s2d_f32"))
+
+
+def _s2d(x, pad, r, s, p, q):
+    """The space-to-depth image of a stride-2 conv input (csrc/precision.hip k_s2d_f32): fp32
+    channels-last [N][32][H2][W2] with channel c·4 + bh·2 + bw = xpad[c][2·h2 + bh][2·w2 + bw]."""
+    nb, c, h, w = x.shape
+    h2, w2 = p + (r + 1) // 2 - 1, q + (s + 1) // 2 - 1
+    out = torch.empty((nb, 32, h2, w2), dtype=_f32, device=x.device, memory_format=_cl)
+    xs = x.float()
+    check(N.lib().bigdl_s2d_f32(ptr(xs), C.c_longlong(xs.stride(0)), C.c_longlong(xs.stride(1)),
+                                C.c_longlong(xs.stride(2)), C.c_longlong(xs.stride(3)), nb, c, h, w, pad[0], pad[1],
+                                h2, w2, 32, ptr(out), _s()), "s2d_f32")
+    return out
+
+
+def _stem_weights(w4):
+    """[K][C][R][S] → the s2d filter [K][⌈R/2⌉][⌈S/2⌉][32] (KRSC, channel c·4 + bh·2 + bw = tap (2a + bh,
+    2a' + bw)), zero-padded taps / channels."""
+    k, c, r, s = w4.shape
+    r2, s2 = (r + 1) // 2, (s + 1) // 2
+    wp = torch.zeros((k, c, 2 * r2, 2 * s2), dtype=_f32, device=w4.device)
+    wp[:, :, :r, :s] = w4.detach().float()
+    w6 = wp.reshape(k, c, r2, 2, s2, 2).permute(0, 2, 4, 1, 3, 5).reshape(k, r2, s2, 4 * c)
+    out = torch.zeros((k, r2, s2, 32), dtype=_f32, device=w4.device)
+    out[..., :4 * c] = w6
+    return out
+
+
+def _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot):
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
+    p, q = _out_hw(h, w, r, s, (2, 2), pad, (1, 1))
+    if p <= 0 or q <= 0:
+        return NotImplemented
+    r2, s2 = (r + 1) // 2, (s + 1) // 2
+    xs = _s2d(x, pad, r, s, p, q)
+    if slot is not None:
+        slot[0] = (("s2d",) + _slot_key(x, 32, True)[1:], xs)
+    y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
+    bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
+    _x3(xs, chunk_split(_stem_weights(w4).reshape(k, -1)), y, nb, xs.shape[2], xs.shape[3], 32, k, r2, s2, p, q,
+        (1, 1), (0, 0), (1, 1), bias=bias, relu=relu, stats=stats, rep=rep, shift=shift)
+    return y
+
+
+def _stem_wgrad(x, gy, gw_acc, scale, pad, slot):
+    """Weight gradient of the s2d stem: the fp32 wgrad of the 4×4 stride-1 conv over the s2d image,
+    folded back onto the R×S×C taps."""
+    nb, c, h, w = x.shape
+    k, _, r, s = gw_acc.shape
+    p, q = gy.shape[2], gy.shape[3]
+    r2, s2 = (r + 1) // 2, (s + 1) // 2
+    held = slot[0] if slot is not None else None
+    key = ("s2d",) + _slot_key(x, 32, True)[1:]
+    if isinstance(held, tuple) and len(held) == 2 and held[0] == key:
+        xs = held[1]
+        slot[0] = None
+    else:
+        xs = _s2d(x, pad, r, s, p, q)
+    gw2 = torch.zeros((k, r2, s2, 32), dtype=_f32, device=x.device)
+    check(N.lib().bigdl_conv_wgrad_f32(ptr(xs), ptr(gy), ptr(gw2), C.c_float(1.0), nb, xs.shape[2], xs.shape[3], 32, k,
+                                       r2, s2, p, q, 1, 1, 0, 0, 1, 1, 0, _s()), "conv_wgrad_f32(s2d)")
+    g6 = gw2[..., :4 * c].reshape(k, r2, s2, c, 2, 2).permute(0, 3, 1, 4, 2, 5).reshape(k, c, 2 * r2, 2 * s2)
+    gw_acc.add_(g6[:, :, :r, :s], alpha=scale)
+
+
+def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None, slot=None):
+    nb, c, h, w = x.shape
+    k, _, r, s = w4.shape
+    if _stem_ok(c, k, stride, dilation) and x.dtype == _f32:
+        return _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot)
     if not (_direct() and _x3_has() and _x3_geom_ok(c, k, r, s, pad) and _cl_f32(x)):
         return NotImplemented
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
@@ -268,7 +339,7 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     same input, which then skips its own split of x."""
     if groups != 1 or x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1]:
         return NotImplemented
-    y = _direct_forward(x, w4, b, stride, pad, dilation, relu)
+    y = _direct_forward(x, w4, b, stride, pad, dilation, relu, slot=slot)
     if y is not NotImplemented:
         return y
     nb, c, h, w = x.shape
@@ -312,7 +383,7 @@ def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
     if (k % 8 or shift is None or shift.dtype != _f32 or shift.numel() != k or not shift.is_contiguous()
             or buf.dtype != _f32 or buf.numel() != 2 * rep * k or not 1 <= rep <= 512):
         return NotImplemented
-    y = _direct_forward(x, w4, None, stride, pad, dilation, False, stats=buf, rep=rep, shift=shift)
+    y = _direct_forward(x, w4, None, stride, pad, dilation, False, stats=buf, rep=rep, shift=shift, slot=slot)
     if y is not NotImplemented:
         return y, buf, rep
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
@@ -409,12 +480,15 @@ def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, laz
             _x3(gy, chunk_split(wt), gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual,
                 res_strided=res_strided)
         return gi
-    if bnb is not None or res_strided is not None:
+    if res_strided is not None:
         return NotImplemented
     classes = _parity(h, w, r, s, stride, pad)
     live = [cl for cl in classes if cl[2] and cl[3]]
     if not live or any(not _x3_geom_ok(k, c, len(cl[2]), len(cl[3]), (len(cl[2]) - 1 - cl[6], len(cl[3]) - 1 - cl[7]))
                        for cl in live):
+        return NotImplemented
+    covered = len(live) == len(classes) and sum(cl[4] * cl[5] for cl in live) == h * w
+    if bnb is not None and not covered:  # tap-less pixels would miss the BN-backward sums
         return NotImplemented
     wf = w4.detach().float()
     if lazy and residual is None and r == 1 and s == 1 and tuple(pad) == (0, 0) and len(live) == 1:
@@ -423,16 +497,23 @@ def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, laz
         _x3(gy, chunk_split(wf.reshape(k, c).t()), tmp, nb, p, q, k, c, 1, 1, ho, wo, (1, 1), (0, 0), (1, 1))
         return StridedGrad(tmp, tuple(stride), (nb, c, h, w))
     gi = torch.empty((nb, c, h, w), dtype=_f32, device=gy.device, memory_format=_cl)
-    if len(live) != len(classes) or sum(cl[4] * cl[5] for cl in live) != h * w:
+    if not covered:
         if residual is not None:
             gi.copy_(residual)
         else:
             gi.zero_()
+    # every parity class adds its pixels' share of the BN-backward sums (disjoint pixel sets)
+    bn_kw = {}
+    if bnb is not None:
+        buf, rep, bx, mean, bits, bsc, bsh = bnb
+        bn_kw = dict(stats=buf, rep=rep, bnx=bx, mean=mean, bits=bits, bsc=bsc, bsh=bsh)
     for (a, b, rs, ss, ho, wo, ea, eb) in live:
         ra, sb = len(rs), len(ss)
         sub = wf[:, :, rs[::-1]][:, :, :, ss[::-1]].permute(1, 2, 3, 0).reshape(c, -1)  # [C][Ra][Sb][K]
         _x3(gy, chunk_split(sub), gi, nb, p, q, k, c, ra, sb, ho, wo, (1, 1), (ra - 1 - ea, sb - 1 - eb), (1, 1),
-            res=residual, scatter=(stride[0], stride[1], a, b, h, w))
+            res=residual, scatter=(stride[0], stride[1], a, b, h, w), **bn_kw)
+    if bnb is not None:
+        bn_fuse["partial"], bn_fuse["G"] = bnb[0], bnb[1]
     return gi
 
 
@@ -460,6 +541,13 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     its input gradient as a StridedGrad."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
+    if (not need_input and gw_acc is not None and _stem_ok(x.shape[1], w4.shape[0], stride, dilation)
+            and _cl_f32(gy) and x.dtype == _f32 and gw_acc.dtype == _f32):
+        if scale != 0:
+            _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
+        if gb_acc is not None and scale != 0:
+            gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+        return None
     if _direct() and _x3_has() and _cl_f32(gy) and x.dtype == _f32:
         # each half independently on the direct kernels when its shape allows, else on the split path
         gi = None

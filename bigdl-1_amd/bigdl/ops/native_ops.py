@@ -1766,7 +1766,19 @@ class _Int8Idx:
 
 @register("maxpool2d_forward")
 def maxpool2d_forward(x, k, s, p, ceil_mode, need_indices=True):
-    """``need_indices=False`` (inference) skips the int8 argmax: 1/3 less traffic."""
+    """``need_indices=False`` (inference) skips the int8 argmax: 1/3 less traffic.  fp32 NHWC
+    (bigdl.compute.dtype=fp32) runs the fp32 instantiation of the same kernel (C % 8 == 0)."""
+    if (x.dim() == 4 and x.dtype == _f32 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)
+            and x.shape[1] % 8 == 0 and k[0] * k[1] <= 127 and p[0] * 2 <= k[0] and p[1] * 2 <= k[1]):
+        N_, C_, H, W = x.shape
+        P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
+        Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
+        if P > 0 and Q > 0:
+            y = torch.empty((N_, C_, P, Q), dtype=_f32, device=x.device, memory_format=torch.channels_last)
+            idx = torch.empty((N_, P, Q, C_), dtype=torch.int8, device=x.device) if need_indices else None
+            check(_lib().bigdl_maxpool32_fwd(ptr(x), ptr(y), ptr(idx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1],
+                                             p[0], p[1], _s()), "maxpool32_fwd")
+            return y, (_Int8Idx(idx) if need_indices else None)
     if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
         return NotImplemented
     N_, C_, H, W = x.shape
@@ -1788,6 +1800,14 @@ def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
         return NotImplemented
     N_, C_, H, W = x.shape
     P, Q = gy.shape[2], gy.shape[3]
+    if x.dtype == _f32:
+        gy = gy.float().contiguous(memory_format=torch.channels_last)
+        if C_ % 8 or not _al16(gy):
+            return NotImplemented
+        gx = torch.empty((N_, C_, H, W), dtype=_f32, device=x.device, memory_format=torch.channels_last)
+        check(_lib().bigdl_maxpool32_bwd(ptr(gy), ptr(idx.t), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1],
+                                         p[0], p[1], _s()), "maxpool32_bwd")
+        return gx
     if gy.dtype != _bf16:
         gy = gy.to(_bf16)
     gy = gy.contiguous(memory_format=torch.channels_last)
@@ -2113,7 +2133,8 @@ def softmax_channels_nhwc(x, backward_gy=None):
 # ---------------------------------------------------------------------------------- K11 avg-pool
 @register("avgpool2d_forward")
 def avgpool2d_forward(x, k, s, p, ceil_mode, count_include_pad, divisor=None):
-    if x.dim() != 4 or x.dtype != _bf16 or not x.is_contiguous(memory_format=torch.channels_last) or not _al16(x):
+    if (x.dim() != 4 or x.dtype not in (_bf16, _f32) or not x.is_contiguous(memory_format=torch.channels_last)
+            or not _al16(x)):
         return NotImplemented
     N_, C_, H, W = x.shape
     if C_ % 8 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
@@ -2122,15 +2143,16 @@ def avgpool2d_forward(x, k, s, p, ceil_mode, count_include_pad, divisor=None):
     Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
     if P <= 0 or Q <= 0:
         return NotImplemented
-    y = torch.empty((N_, C_, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
-    check(_lib().bigdl_avgpool_fwd(ptr(x), ptr(y), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+    y = torch.empty((N_, C_, P, Q), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    fn = _lib().bigdl_avgpool32_fwd if x.dtype == _f32 else _lib().bigdl_avgpool_fwd  # fp32: the reference precision
+    check(fn(ptr(x), ptr(y), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
                                    int(bool(count_include_pad)), int(divisor or 0), _s()), "avgpool_fwd")
     return y
 
 
 @register("avgpool2d_backward")
 def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=None):
-    if x.dim() != 4 or x.dtype != _bf16 or gy.dim() != 4:
+    if x.dim() != 4 or x.dtype not in (_bf16, _f32) or gy.dim() != 4:
         return NotImplemented
     N_, C_, H, W = x.shape
     if C_ % 8 or p[0] * 2 > k[0] or p[1] * 2 > k[1]:
@@ -2139,11 +2161,12 @@ def avgpool2d_backward(gy, x, k, s, p, ceil_mode, count_include_pad, divisor=Non
     Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
     if tuple(gy.shape) != (N_, C_, P, Q):
         return NotImplemented
-    gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
     if not _al16(gy):
         gy = gy.clone(memory_format=torch.channels_last)
-    gx = torch.empty((N_, C_, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
-    check(_lib().bigdl_avgpool_bwd(ptr(gy), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+    gx = torch.empty((N_, C_, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    fn = _lib().bigdl_avgpool32_bwd if x.dtype == _f32 else _lib().bigdl_avgpool_bwd
+    check(fn(ptr(gy), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
                                    int(bool(count_include_pad)), int(divisor or 0), _s()), "avgpool_bwd")
     return gx
 

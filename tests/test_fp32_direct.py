@@ -111,8 +111,8 @@ def test_direct_stats_epilogue_matches_standalone():
     assert F3._producer_split(out1[0], K) is None
 
 
-@pytest.mark.parametrize("tail", [False, True], ids=["mid_block", "block_tail"])
-def test_direct_bnbwd_epilogue(tail):
+@pytest.mark.parametrize("tail,st", [(False, 1), (True, 1), (False, 2)], ids=["mid_block", "block_tail", "strided"])
+def test_direct_bnbwd_epilogue(tail, st):
     from bigdl.ops import native_ops as NO, fp32x3 as F3
     g = torch.Generator().manual_seed(11)
     N_, C_, K, H = 2, 64, 64, 11
@@ -123,7 +123,8 @@ def test_direct_bnbwd_epilogue(tail):
     y, mean, invstd = NO.batchnorm_forward_train(xb, gam, bet, torch.zeros(C_, device=dev), torch.ones(C_, device=dev),
                                                  0.1, 1e-5, relu=True, residual=res, coef_out=coef)
     w = (torch.randn(K, C_, 3, 3, generator=g) * 0.1).to(dev)
-    gy = torch.randn(N_, K, H, H, generator=g).to(dev).contiguous(memory_format=cl)
+    P = (H - 1) // st + 1
+    gy = torch.randn(N_, K, P, P, generator=g).to(dev).contiguous(memory_format=cl)
     sres = torch.randn(N_, C_, H, H, generator=g).to(dev).contiguous(memory_format=cl) if tail else None
     rep = 32
     buf = torch.zeros(2 * rep * C_, device=dev)
@@ -132,13 +133,13 @@ def test_direct_bnbwd_epilogue(tail):
         fuse["mask"] = y
     else:
         fuse["scale"], fuse["shift"] = coef[:C_], coef[C_:]
-    gi1, names = _kernels(lambda: F3.conv_backward(gy, y, w, (1, 1), (1, 1), (1, 1), 1, True, None, None, 1.0,
+    gi1, names = _kernels(lambda: F3.conv_backward(gy, y, w, (st, st), (1, 1), (1, 1), 1, True, None, None, 1.0,
                                                    residual=sres, bn_fuse=fuse))
     assert any("k_conv_x3" in n for n in names), names
     assert fuse.get("partial") is buf and fuse.get("G") == rep
     gg1, gb1 = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
     gx1 = NO.batchnorm_backward_partials(gi1, xb, gam, mean, invstd, buf, rep, True, gg1, gb1, 1.0, rezero=True)
-    gi0 = F3.conv_backward(gy, y, w, (1, 1), (1, 1), (1, 1), 1, True, None, None, 1.0, residual=sres)
+    gi0 = F3.conv_backward(gy, y, w, (st, st), (1, 1), (1, 1), 1, True, None, None, 1.0, residual=sres)
     gg0, gb0 = torch.zeros(C_, device=dev), torch.zeros(C_, device=dev)
     gx0, _ = NO.batchnorm_backward(gi0, xb, gam, mean, invstd, y.clone(), True, True, gg0, gb0, 1.0)
     torch.cuda.synchronize()
@@ -183,3 +184,37 @@ def test_direct_off_falls_back_to_split_path():
         config.set_property("bigdl.fp32.direct", True)
     assert not any("k_conv_x3" in n for n in names)
     assert _rel(y1, y0) < 2e-5
+
+
+def test_direct_stem_space_to_depth():
+    """The fp32 RGB stem (7×7 stride 2 over 3 channels) runs as a 4×4 stride-1 conv over the
+    space-to-depth image on the direct kernels: forward (+ BN statistics epilogue) and weight gradient
+    against fp64."""
+    from bigdl.ops import fp32x3 as F3, native_ops as NO
+    g = torch.Generator().manual_seed(17)
+    N_, H = 2, 30
+    x = torch.randn(N_, 3, H, H, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    xr, wr = x.double(), w.double().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 2, 3)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy.double())
+    xd = x.to(dev).contiguous(memory_format=cl)
+    slot = [None]
+    y, names = _kernels(lambda: F3.conv_forward(xd, w.to(dev), None, (2, 2), (3, 3), slot=slot))
+    assert any("k_s2d_f32" in n for n in names) and any("k_conv_x3" in n for n in names), names
+    assert _rel(y, yr) < 2e-5, _rel(y, yr)
+    gw = torch.zeros(64, 7, 7, 3, device=dev).permute(0, 3, 1, 2)
+    r, names = _kernels(lambda: F3.conv_backward(gy.to(dev).contiguous(memory_format=cl), xd, w.to(dev), (2, 2),
+                                                 (3, 3), (1, 1), 1, False, gw, None, 1.0, slot=slot))
+    assert r is None and not any("k_s2d_f32" in n for n in names), names  # the forward's s2d image reused
+    assert _rel(gw, wr.grad) < 2e-5, _rel(gw, wr.grad)
+    # the statistics epilogue through the s2d path
+    rep = 8
+    buf = torch.zeros(2 * rep * 64, device=dev)
+    shift = torch.zeros(64, device=dev)
+    out = NO.conv2d_forward_stats(xd, w.to(dev), None, (2, 2), (3, 3), shift=shift, sums=(buf, rep))
+    assert out is not NotImplemented
+    torch.cuda.synchronize()
+    ys = out[0].double().cpu()
+    assert _rel(buf.reshape(2, rep, 64).sum(1)[0], ys.sum((0, 2, 3))) < 1e-5

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(_HERE, "..", "bigdl-1_amd"))
 sys.path.insert(0, _HERE)
 from bench_conv import RESNET50  # noqa: E402
 
-TILES = [(256, 128), (256, 64), (128, 128)]
+TILES = [(256, 128), (256, 64), (128, 128), (256, 128 | 256), (256, 64 | 256), (128, 128 | 256), (128, 128 | 512), (128, 128 | 768)]  # bn | 256: 8x1 / 4x1 waves; | 512: 2-deep ring (2 blocks/CU)
 
 
 def main():
@@ -60,11 +60,8 @@ def main():
         rows = {"C": C, "K": K, "R": R, "s": st, "H": H, "mult": mult}
         for (bm, bn) in TILES:
             us = timeit(lambda: F3._x3(x, w2, y, N, H, H, C, K, R, R, P, P, (st, st), (pad, pad), (1, 1),
-                                       tile=(bm, bn), persist=1))
+                                       tile=(bm, bn)))
             rows[f"fwd_{bm}x{bn}"] = us
-            if R == 1:
-                rows[f"fwdnp_{bm}x{bn}"] = timeit(lambda: F3._x3(x, w2, y, N, H, H, C, K, R, R, P, P, (st, st),
-                                                                 (pad, pad), (1, 1), tile=(bm, bn), persist=-1))
         byts = 4.0 * N * (H * H * C + P * P * K)
         if st == 1:
             wt = F3.chunk_split(w.flip(2, 3).permute(1, 2, 3, 0).reshape(C, -1))
@@ -72,11 +69,8 @@ def main():
             pd = R - 1 - pad
             for (bm, bn) in TILES:
                 us = timeit(lambda: F3._x3(gy, wt, gi, N, P, P, K, C, R, R, H, H, (1, 1), (pd, pd), (1, 1),
-                                           tile=(bm, bn), persist=1))
+                                           tile=(bm, bn)))
                 rows[f"dgrad_{bm}x{bn}"] = us
-                if R == 1:
-                    rows[f"dgradnp_{bm}x{bn}"] = timeit(lambda: F3._x3(gy, wt, gi, N, P, P, K, C, R, R, H, H, (1, 1),
-                                                                       (pd, pd), (1, 1), tile=(bm, bn), persist=-1))
         gw = torch.zeros(K, R, R, C, device=dev).permute(0, 3, 1, 2)
         rows["wgrad"] = timeit(lambda: F3._direct_wgrad(x, gy, gw, 1.0, (st, st), (pad, pad), (1, 1)))
         best_f = min(v for k_, v in rows.items() if k_.startswith("fwd_"))
@@ -87,14 +81,11 @@ def main():
         for k_, v in (("fwd", best_f), ("dgrad", best_d), ("wgrad", rows["wgrad"])):
             tot[k_] = tot.get(k_, 0.0) + v * mult
         print(f"C{C:5d} K{K:5d} R{R} s{st} H{H:4d} x{mult}  fwd " +
-              " ".join(f"{rows[f'fwd_{a}x{b}']:8.1f}" for a, b in TILES) +
-              (("  dgrad " + " ".join(f"{rows[f'dgrad_{a}x{b}']:8.1f}" for a, b in TILES)) if st == 1 else " " * 34) +
+              " ".join(f"{rows[f'fwd_{a}x{b}']:7.1f}" for a, b in TILES) +
+              (("  dgrad " + " ".join(f"{rows[f'dgrad_{a}x{b}']:7.1f}" for a, b in TILES)) if st == 1 else " " * 55) +
               f"  wgrad {rows['wgrad']:8.1f}  | fwd {rows['fwd_tf']:6.0f} TF/s {rows['fwd_gbs']:6.0f} GB/s"
               f"  wgrad {rows['wgrad_tf']:6.0f} TF/s", flush=True)
-        if R == 1:
-            print("      no-persist fwd " + " ".join(f"{rows[f'fwdnp_{a}x{b}']:8.1f}" for a, b in TILES) +
-                  (("  dgrad " + " ".join(f"{rows[f'dgradnp_{a}x{b}']:8.1f}" for a, b in TILES)) if st == 1 else ""),
-                  flush=True)
+
         out.write(json.dumps(rows) + "\n")
     print("per forward pass (best tile, x multiplicity), us:", {k: round(v, 1) for k, v in tot.items()})
 
