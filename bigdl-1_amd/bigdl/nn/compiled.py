@@ -246,7 +246,7 @@ def select_kernels(records, iters: int = 5, min_gain: float = 0.03) -> Dict[tupl
     table = NO._TILE["table"]
     chosen = {}
     seen = {}
-    for key, fn in records:
+    for key, fn in (records.items() if isinstance(records, dict) else records):
         seen.setdefault(key, fn)
     NO._TILE["retiming"] = True
     try:
@@ -281,7 +281,7 @@ def autotune_training_step(step_fn, iters: int = 5, min_gain: float = 0.03) -> D
     zeroes, so the optimizer state is untouched.  Returns ``(step result, {key: choice})``."""
     import torch
     from ..ops import native_ops as NO
-    rec = NO._TILE["record"] = []
+    rec = NO._TILE["record"] = {}  # geometry → first launch (dedup while recording)
     try:
         out = step_fn()
     finally:
@@ -307,7 +307,7 @@ def autotune(model, example, iters: int = 5, min_gain: float = 0.03) -> Dict[tup
         return {}
     was_training = model.isTraining() if hasattr(model, "isTraining") else False
     model.evaluate()
-    rec = NO._TILE["record"] = []
+    rec = NO._TILE["record"] = {}
     try:
         with torch.no_grad():
             model.forward(example)

@@ -125,6 +125,7 @@ class DecodeCache:
         self.rows, self.max_len, self.hidden, self.device = rows, max(1, int(max_len)), hidden, device
         self.k = self.v = None
         self.length = 0
+        self.chunks: list = []  # positions per append, oldest first (the reference order is per chunk)
 
     def append(self, k, v):
         n = k.shape[1]
@@ -132,6 +133,7 @@ class DecodeCache:
             self.k = torch.empty((self.rows, self.max_len, self.hidden), dtype=k.dtype, device=k.device)
             self.v = torch.empty_like(self.k)
             self.length = 0
+            self.chunks = []
         if self.length + n > self.k.shape[1]:  # grow (amortised doubling) keeping the history
             cap = max(self.length + n, 2 * self.k.shape[1])
             nk = torch.empty((self.rows, cap, self.hidden), dtype=self.k.dtype, device=self.k.device)
@@ -142,6 +144,32 @@ class DecodeCache:
         self.k[:, self.length:self.length + n].copy_(k)
         self.v[:, self.length:self.length + n].copy_(v)
         self.length += n
+        self.chunks.append(n)
+
+    def ref_order(self):
+        """Storage positions in the reference's key order: the reference concatenates ``[new; cache]``
+        per call, so appends are newest first but each multi-position append keeps its own order."""
+        order, start = [], 0
+        spans = []
+        for n in self.chunks:
+            spans.append((start, n))
+            start += n
+        for s0, n in reversed(spans):
+            order.extend(range(s0, s0 + n))
+        return order
+
+    def kernel_bias(self, bias):
+        """``bias`` (last dim = the reference key order) rearranged for the decode kernel, which reads
+        key position p's bias at index L − 1 − p (a fully reversed cache): identical unless an append
+        held more than one position."""
+        L = self.length
+        if bias is None or not isinstance(bias, torch.Tensor) or bias.shape[-1] != L or all(n == 1 for n in self.chunks):
+            return bias
+        r = self.ref_order()  # r[i] = storage position of reference key i
+        idx = [0] * L
+        for i, pos in enumerate(r):
+            idx[L - 1 - pos] = i
+        return bias.index_select(-1, torch.tensor(idx, device=bias.device))
 
     def reorder(self, rows_idx):
         """Row i ← row rows_idx[i] over the valid positions (beam survivors)."""
@@ -151,11 +179,11 @@ class DecodeCache:
             self.v[:, :L] = self.v[rows_idx, :L]
 
     def keys(self):
-        """The cached keys in the reference's order (newest first), [rows, L, H]."""
-        return self.k[:, :self.length].flip(1)
+        """The cached keys in the reference's order (newest append first), [rows, L, H]."""
+        return self.k[:, self.ref_order()]
 
     def values(self):
-        return self.v[:, :self.length].flip(1)
+        return self.v[:, self.ref_order()]
 
 
 class Attention(AutogradModule):
@@ -338,28 +366,42 @@ class Attention(AutogradModule):
         H, nh = self.hiddenSize, self.numHeads
         D = H // nh
         rows, Lq, Ly = x.shape[0], x.shape[1], y.shape[1]
-        if x.is_cuda:
+        native = _native_dense_ok(x) and isinstance(y, torch.Tensor) and y.is_cuda and H % 8 == 0
+        q = k = v = None
+        if native:
+            # bf16 compute on the native GEMMs; any shape a GEMM refuses (NotImplemented) takes the
+            # reference projections below in x's dtype
             from ...ops import native_ops as NO
             bf = torch.bfloat16
             x2 = x.reshape(rows * Lq, H).to(bf).contiguous()
             y2 = x2 if (y is x) else y.reshape(rows * Ly, H).to(bf).contiguous()
-            q = NO.gemm(x2, self.cw("queryWeight", bf)).view(rows, Lq, H)
+            q = NO.gemm(x2, self.cw("queryWeight", bf))
             wkv = _fused_rows([self.cw("keyWeight", bf), self.cw("valueWeight", bf)])
             if wkv is not None:
-                kv = NO.gemm(y2, wkv).view(rows, Ly, 2 * H)
-                k, v = kv[..., :H], kv[..., H:]
+                kv = NO.gemm(y2, wkv)
+                if kv is not NotImplemented:
+                    kv = kv.view(rows, Ly, 2 * H)
+                    k, v = kv[..., :H], kv[..., H:]
             else:
-                k = NO.gemm(y2, self.cw("keyWeight", bf)).view(rows, Ly, H)
-                v = NO.gemm(y2, self.cw("valueWeight", bf)).view(rows, Ly, H)
-        else:
+                k = NO.gemm(y2, self.cw("keyWeight", bf))
+                v = NO.gemm(y2, self.cw("valueWeight", bf))
+                k = k.view(rows, Ly, H) if k is not NotImplemented else None
+                v = v.view(rows, Ly, H) if v is not NotImplemented else None
+            q = q.view(rows, Lq, H) if q is not NotImplemented else None
+            native = q is not None and k is not None and v is not None
+        if not native:
             q, k, v = self._proj(x, "query"), self._proj(y, "key"), self._proj(y, "value")
         dc.append(k, v)
         cache[kn] = dc
         cache[vn] = dc
-        o = ops.attention_decode(q.contiguous(), dc.k, dc.v, dc.length, nh, D, D ** -0.5, bias, True)
-        if x.is_cuda:
+        o = ops.attention_decode(q.contiguous(), dc.k, dc.v, dc.length, nh, D, D ** -0.5, dc.kernel_bias(bias), True)
+        if native:
             from ...ops import native_ops as NO
-            return NO.gemm(o.reshape(rows * Lq, H), self.cw("outputWeight", torch.bfloat16)).view(rows, Lq, H)
+            out = NO.gemm(o.reshape(rows * Lq, H).to(torch.bfloat16).contiguous(),
+                          self.cw("outputWeight", torch.bfloat16))
+            if out is not NotImplemented:
+                return out.view(rows, Lq, H)
+            o = o.to(x.dtype)
         return self._proj(o, "output")
 
 

@@ -307,10 +307,15 @@ class BatchNormalization(TensorModule):
                 sums = m.bn_local_sums(x, shift)
             if sums is NotImplemented:
                 continue
-            self._sync_allreduce(sums)
+            self._sync_allreduce(sums)  # the ONE collective of this call: a failed apply reuses its sums
             r = m.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar, self.momentum,
                                        self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef,
                                        bits_out=bits if m is not R else None)
+            if r is NotImplemented and m is not R:
+                m = R
+                r = R.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar,
+                                           self.momentum, self.eps, relu=relu, residual=residual, in_bias=in_bias,
+                                           coef_out=coef)
             if r is not NotImplemented:
                 self._relu_bits = bits if m is not R else None
                 self._sync_path = "native" if m is not R else "reference"
@@ -411,14 +416,16 @@ class BatchNormalization(TensorModule):
             if both is NotImplemented:
                 continue
             loc, glob = both[:2 * C], both[2 * C:]
-            self._sync_allreduce(glob)
-            gi = m.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, 0, y=y, relu=rl,
-                                         need_input=need_input,
-                                         gg_acc=self.gradWeight if (acc and self.affine) else None,
-                                         gb_acc=self.gradBias if (acc and self.affine) else None,
-                                         scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs)
+            self._sync_allreduce(glob)  # the ONE collective of this call: a failed apply reuses its sums
+            kw = dict(need_input=need_input, gg_acc=self.gradWeight if (acc and self.affine) else None,
+                      gb_acc=self.gradBias if (acc and self.affine) else None, scale=self.scale_w if acc else 0.0,
+                      cbias_acc=cb, cbias_scale=cbs)
+            gi = m.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, 0, y=y, relu=rl, **kw)
+            if gi is NotImplemented and m is not R:
+                m = R
+                gi = R.bn_backward_from_sums(gy, x, g, self.saveMean, self.saveStd, loc, glob, 0, y=y, relu=rl, **kw)
             if gi is NotImplemented:
-                continue
+                raise RuntimeError("SyncBN backward: no implementation accepted the all-reduced sums")
             if acc and self.affine and self.scale_b != self.scale_w:
                 self.gradBias.add_(loc[:C], alpha=self.scale_b - self.scale_w)
             self._sync_bwd_path = "native" if m is not R else "reference"

@@ -465,3 +465,20 @@ __all__ = [n for n, v in list(globals().items()) if isinstance(v, type) and issu
 from .grad_ops import *  # noqa: E402,F401,F403  (TF backward / training-graph ops)
 from . import grad_ops as _grad_ops  # noqa: E402
 __all__ += _grad_ops.__all__
+
+
+# data-flow resources (TensorArray / Stack) and AssignGrad: DataFlowOps.scala, StateOps.scala
+from .data_flow import (TensorArray, TensorArrayCreator, TensorArrayGrad, TensorArrayWrite, TensorArrayRead,  # noqa: E402,F401
+                        TensorArrayGather, TensorArrayScatter, TensorArrayConcat, TensorArraySplit, TensorArraySize,
+                        TensorArrayClose, StackCreator, StackPush, StackPop, AssignGrad)
+
+
+def _set_scala_package():
+    """The TF op layers live in ``com.intel.analytics.bigdl.nn.tf`` (their .bigdl module type)."""
+    for _v in list(globals().values()):
+        if (isinstance(_v, type) and issubclass(_v, AbstractModule) and _v.__module__.startswith(__name__)
+                and "SCALA_PACKAGE" not in _v.__dict__):
+            _v.SCALA_PACKAGE = "com.intel.analytics.bigdl.nn.tf"
+
+
+_set_scala_package()

@@ -20,9 +20,12 @@
 // the XOR swizzle chunk ^ ((row >> 1) & 7) on the DMA source address and on every fragment read, which
 // keeps both the bf16 (A) and the fp32 (B) fragment reads conflict-free.
 //
-// Epilogues (uniform branches on the launch's arguments), straight from the accumulators
-// (lane l of a 32×32 block holds pixel l & 31 and channels 8·(r >> 2) + 4·(l >> 5) + (r & 3)):
-//   plain  : y = relu?(acc + bias + res), fp32 [M][ldy] float4 stores;
+// Epilogues (uniform branches on the launch's arguments).  The accumulators (lane l of a 32×32 block holds
+// pixel l & 31 and channels 8·(r >> 2) + 4·(l >> 5) + (r & 3)) are parked as an fp32 tile in the ring's
+// LDS and walked row-major, so every store / residual / BN-input access of a wave-instruction covers whole
+// 4·BN-byte row segments (the register-direct form wrote 32 rows × 32 B per instruction and ran the
+// expand 1×1 convs store-bound: 372 vs 208 µs with the stores skipped, 64→256 at 56², batch 256):
+//   plain  : y = relu?(acc + bias + res), fp32 [M][ldy];
 //   stats  : y = acc, plus Σ(y − shift), Σ(y − shift)² of the following BN added into its replicated
 //            buffer [2][R][K] (fp32 atomics, one per block and channel after an LDS fold);
 //   bnbwd  : the data gradient g = acc (+ res) masked by the ReLU of the BN that produced this
@@ -76,6 +79,8 @@ struct X3Params {
   // strided residual (res_sh > 0): `res` holds only the grid pixels (h, w) with h % res_sh == 0 and
   // w % res_sw == 0 as a dense [Nb][res_H][res_W][ldy] tensor (a 1×1 stride-s shortcut's input gradient)
   int res_sh, res_sw, res_H, res_W;
+  // measurement knob (BIGDL_X3_DEBUG, read per launch): bit 0 = skip the output stores (leaves y WRONG)
+  int dbg;
 };
 
 // One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds): lane l's 16 bytes land at lds + 16·l.
@@ -117,43 +122,31 @@ __device__ __forceinline__ float x3_row_fold(float v) {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, bool PERSIST, int NSX = 3>
-__global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Params p) {
+template <int BM, int BN, int WM, int WN, int MODE, int NS>
+__global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) k_conv_x3(X3Params p) {
   static_assert(MODE == 1 || MODE == 3, "tap-uniform / pointwise gathers only");
+  static_assert(NS == 2 || NS == 3, "LDS ring depth");
   constexpr bool PW = MODE == 3;
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BK = 32;                       // reduction indices per k-tile (one 128-B row each side)
-  constexpr int NS = NSX;                      // LDS ring depth (2: two blocks share a CU)
-  static_assert(NS == 3 || (NS == 2 && !PERSIST), "2-deep ring: one tile per block");
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;  // 8-row DMA groups per wave: weights, activations
   static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
   constexpr int L = GA + GB;
   constexpr int TMI = BM / WM / 32, TNI = BN / WN / 32;
   static_assert(TMI >= 1 && TNI >= 1, "wave tile below 32x32");
-  constexpr int RED = WM * 2 * BN * 2 * 4;     // epilogue statistics fold: [WM][2 row halves][2][BN] fp32
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * STAGE + RED];
+  // epilogue staging: the fp32 tile [BM][BN] (16-B chunks XOR-swizzled by row) + [2][RPP][BN] partial sums
+  constexpr int CPR = BN / 4, RPP = NT / CPR;
+  constexpr int EPI = BM * BN * 4 + 2 * RPP * BN * 4;
+  constexpr int LDS_BYTES = NS * STAGE > EPI ? NS * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wave_m = wid % WM, wave_n = wid / WM;
-  // Tiles of this block: one (grid = tiles), or (PERSIST) a contiguous run of the tm-major tile order —
-  // consecutive tiles share their pixel rows (L2-resident for the second n-tile) — streamed through ONE
-  // pipeline so a tile's epilogue overlaps the next tile's loads.  Runs are XCD-contiguous.
-  int t_first, t_count;
-  {
-    const int ntiles = (int)(((long long)p.M + BM - 1) / BM) * p.tiles_n;
-    const int r = x3_xcd_remap(blockIdx.x, gridDim.x);
-    if (PERSIST) {
-      const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
-      t_first = r * per;
-      t_count = min(per, ntiles - t_first);
-    } else {
-      t_first = r;
-      t_count = 1;
-    }
-  }
-  if (t_count <= 0) return;
+  const int tile = x3_xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.ldx * 4);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.Kg * 4);  // 2 bf16 parts per index
@@ -163,67 +156,57 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
 
   const int lrow = lane >> 3, slot = lane & 7;
   const int KT = p.Kg / BK;  // host-checked: C % 32 == 0
-  const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
-  // per-lane DMA source state of the tile being PREPARED (prep runs two k-tiles ahead of compute)
   uint32_t woff[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    woff[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 4u + (uint32_t)chunk * 16u : OOB;
+  }
   int rbase[GB];  // fp32 elements
   uint64_t vmask[GB];
-  auto setup_tile = [&](int tile) {
-    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+  const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int row = 8 * (wid + NW * i) + lrow;
-      const int chunk = slot ^ ((row >> 1) & 7);
-      const int n = n0 + row;
-      woff[i] = n < p.K ? (uint32_t)n * (uint32_t)p.Kg * 4u + (uint32_t)chunk * 16u : OOB;
+  for (int j = 0; j < GB; ++j) {
+    const int row = 8 * (wid + NW * j) + lrow;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    int img = -1, h = 0, w = 0;
+    if (m < p.M) {
+      if (pw_direct) {
+        img = m;
+      } else {
+        const int n = m / (p.P * p.Q);
+        const int pq = m - n * p.P * p.Q;
+        const int pp = pq / p.Q, qq = pq - pp * p.Q;
+        img = n * p.H * p.W;
+        h = pp * p.sh - p.ph;
+        w = qq * p.sw - p.pw;
+      }
     }
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-      const int row = 8 * (wid + NW * j) + lrow;
-      const int chunk = slot ^ ((row >> 1) & 7);
-      const int m = m0 + row;
-      int img = -1, h = 0, w = 0;
-      if (m < p.M) {
-        if (pw_direct) {
-          img = m;
-        } else {
-          const int n = m / (p.P * p.Q);
-          const int pq = m - n * p.P * p.Q;
-          const int pp = pq / p.Q, qq = pq - pp * p.Q;
-          img = n * p.H * p.W;
-          h = pp * p.sh - p.ph;
-          w = qq * p.sw - p.pw;
+    rbase[j] = (img + h * p.W + w) * p.ldx + chunk * 4;
+    uint64_t msk = 0;
+    if (PW) {
+      msk = img >= 0 ? 1ull : 0ull;
+    } else if (img >= 0) {
+      for (int r = 0; r < p.R; ++r) {
+        const int hh = h + r * p.dh;
+        if ((unsigned)hh >= (unsigned)p.H) continue;
+        for (int sx = 0; sx < p.S; ++sx) {
+          const int ww = w + sx * p.dw;
+          if ((unsigned)ww < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
         }
       }
-      rbase[j] = (img + h * p.W + w) * p.ldx + chunk * 4;
-      uint64_t msk = 0;
-      if (PW) {
-        msk = img >= 0 ? 1ull : 0ull;
-      } else if (img >= 0) {
-        for (int r = 0; r < p.R; ++r) {
-          const int hh = h + r * p.dh;
-          if ((unsigned)hh >= (unsigned)p.H) continue;
-          for (int sx = 0; sx < p.S; ++sx) {
-            const int ww = w + sx * p.dw;
-            if ((unsigned)ww < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
-          }
-        }
-      }
-      vmask[j] = msk;
     }
-  };
+    vmask[j] = msk;
+  }
 
-  // prep: the source offsets of the next k-tile of the stream (called strictly in stream order)
-  int it_c0 = 0, it_s = 0, it_tap = 0, it_off = 0;
-  int p_kt = 0, p_tl = 0;
+  // prep: the source offsets of the next k-tile (called strictly in k order)
+  int it_c0 = 0, it_s = 0, it_tap = 0, it_off = 0, p_kt = 0;
   uint32_t poff[L];
   auto prep = [&]() {
-    if (p_kt == 0) {
-      setup_tile(t_first + p_tl);
-      it_c0 = it_s = it_tap = it_off = 0;
-    }
-    const int kt = p_kt;
+    const int kt = p_kt++;
     const uint32_t kb = (uint32_t)kt * 128u;
 #pragma unroll
     for (int i = 0; i < GA; ++i) poff[i] = woff[i] + kb;
@@ -246,10 +229,6 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
     for (int j = 0; j < GB; ++j) {
       const bool ok = PW ? (vmask[j] != 0) : ((vmask[j] >> tap) & 1ull);
       poff[GA + j] = ok ? (uint32_t)(rbase[j] + tap_off) * 4u : OOB;
-    }
-    if (++p_kt == KT) {
-      p_kt = 0;
-      ++p_tl;
     }
   };
   auto issue = [&](int i, int slotbuf) {
@@ -288,25 +267,17 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
     v8s ah[2][TNI], al[2][TNI];
     v4f b0[2][TMI], b1[2][TMI];
 #pragma unroll
-    for (int i = 0; i < TNI; ++i) {
-      ah[0][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[0]);
-      al[0][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[0]);
-    }
+    for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-    for (int j = 0; j < TMI; ++j) {
-      b0[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[0]);
-      b1[0][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[0]);
-    }
-    // fragments of slice 1 in flight during slice 0's MFMAs
+      for (int i = 0; i < TNI; ++i) {
+        ah[kk][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[kk]);
+        al[kk][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[kk]);
+      }
 #pragma unroll
-    for (int i = 0; i < TNI; ++i) {
-      ah[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_hi[1]);
-      al[1][i] = *reinterpret_cast<const v8s*>(base + (a_row0 + 32 * i) * 128 + fa_lo[1]);
-    }
-#pragma unroll
-    for (int j = 0; j < TMI; ++j) {
-      b0[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[1]);
-      b1[1][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[1]);
+      for (int j = 0; j < TMI; ++j) {
+        b0[kk][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[kk]);
+        b1[kk][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[kk]);
+      }
     }
     // slice 0's B split is exposed; slice 1's is issued right after slice 0's MFMAs so it overlaps
     // them in the matrix pipe (the MFMA only holds vector issue for 8 of its 32 cycles)
@@ -341,135 +312,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
     }
   };
 
-  // ---------------------------------------------------------------------------------- epilogue
-  const int pm = lane & 31;
-  float* red = reinterpret_cast<float*>(lds + NS * STAGE);  // [WM][2][2][BN]: (wave_m, row half, stat, ch)
-  auto epilogue = [&](int tile) {
-    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const bool want_stats = p.stats != nullptr;
-    // this lane's output-grid pixel per row block (−1: past M), computed once per tile
-    int mo_[TMI];
-#pragma unroll
-    for (int j = 0; j < TMI; ++j) {
-      const int m = m0 + (b_row0 - BN) + 32 * j + pm;
-      int mo = m < p.M ? m : -1;
-      if (p.scatter && mo >= 0) {
-        const int img = m / (p.P * p.Q);
-        const int pq = m - img * p.P * p.Q;
-        const int pp = pq / p.Q, qq = pq - pp * p.Q;
-        mo = (img * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow;
-      }
-      mo_[j] = mo;
-    }
-#pragma unroll
-    for (int i = 0; i < TNI; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
-        const int n = n0 + nl;
-        const bool nok = n < p.K;  // K % 4 == 0 (host-checked): a 4-channel run is all in or all out
-        float b4[4] = {0.f, 0.f, 0.f, 0.f}, k4[4] = {0.f, 0.f, 0.f, 0.f}, mu[4] = {0.f, 0.f, 0.f, 0.f};
-        float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sh4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (nok) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (p.bias) b4[e] = p.bias[n + e];
-            if (p.shift && !p.bnx) k4[e] = p.shift[n + e];
-            if (p.bnx) {
-              mu[e] = p.mean[n + e];
-              if (!p.bits) { sc4[e] = p.bsc[n + e]; sh4[e] = p.bsh[n + e]; }
-            }
-          }
-        }
-        float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < TMI; ++j) {
-          if (!nok || mo_[j] < 0) continue;
-          const int mo = mo_[j];
-          const size_t off = (size_t)mo * p.ldy + n;
-          float v[4] = {acc[i][j][4 * g] + b4[0], acc[i][j][4 * g + 1] + b4[1], acc[i][j][4 * g + 2] + b4[2],
-                        acc[i][j][4 * g + 3] + b4[3]};
-          if (p.res) {
-            bool live = true;
-            size_t roff = off;
-            if (p.res_sh) {
-              const int gridpix = p.scatter ? p.oH * p.oW : p.P * p.Q;
-              const int gw = p.scatter ? p.oW : p.Q;
-              const int img = mo / gridpix;
-              const int hw = mo - img * gridpix;
-              const int hh = hw / gw, ww = hw - hh * gw;
-              live = hh % p.res_sh == 0 && ww % p.res_sw == 0;
-              roff = ((size_t)(img * p.res_H + hh / p.res_sh) * p.res_W + ww / p.res_sw) * p.ldy + n;
-            }
-            if (live) {
-              const v4f r = *reinterpret_cast<const v4f*>(p.res + roff);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += r[e];
-            }
-          }
-          if (p.relu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          if (p.bnx) {
-            const v4f xv = *reinterpret_cast<const v4f*>(p.bnx + (size_t)mo * p.K + n);
-            unsigned mb;
-            if (p.bits) {
-              mb = (p.bits[(size_t)mo * (p.K >> 3) + (n >> 3)] >> (n & 7)) & 0xFu;
-            } else {
-              mb = 0;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) mb |= (fmaf(xv[e], sc4[e], sh4[e]) > 0.f ? 1u : 0u) << e;
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[e] = (mb >> e) & 1u ? v[e] : 0.f;
-              s4[e] += v[e];
-              q4[e] = fmaf(v[e], xv[e] - mu[e], q4[e]);
-            }
-          } else if (want_stats) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float a = v[e] - k4[e];
-              s4[e] += a;
-              q4[e] = fmaf(a, a, q4[e]);
-            }
-          }
-          *reinterpret_cast<v4f*>(p.y + off) = (v4f){v[0], v[1], v[2], v[3]};
-        }
-        if (want_stats) {  // fold the 16 pixel lanes of each DPP row; lanes 0 / 16 / 32 / 48 park the row sums
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            s4[e] = x3_row_fold(s4[e]);
-            q4[e] = x3_row_fold(q4[e]);
-          }
-          if ((lane & 15) == 0) {
-            const int half = (lane >> 4) & 1;
-            float* rs = red + ((size_t)(wave_m * 2 + half) * 2) * BN + nl;
-            *reinterpret_cast<v4f*>(rs) = (v4f){s4[0], s4[1], s4[2], s4[3]};
-            *reinterpret_cast<v4f*>(rs + BN) = (v4f){q4[0], q4[1], q4[2], q4[3]};
-          }
-        }
-      }
-    if (want_stats) {
-      __syncthreads();
-      const int rep = tm % p.R_rep;
-      for (int t = tid; t < 2 * BN; t += NT) {
-        const int which = t / BN, c = t - which * BN;
-        if (n0 + c >= p.K) continue;
-        float a = 0.f;
-#pragma unroll
-        for (int g = 0; g < WM * 2; ++g) a += red[(g * 2 + which) * BN + c];
-        atomicAdd(&p.stats[((size_t)which * p.R_rep + rep) * p.K + n0 + c], a);
-      }
-    }
-  };
-
-  // ---------------------------------------------------------------------------------- the stream
-  // 3-deep ring over the block's V = t_count · KT k-tiles: k-tile v + 2 is issued while v is multiplied;
-  // after the last k-tile of a tile its epilogue runs first and THEN v + 2's pieces are issued, so the
-  // counted wait (vmcnt = L: stores count too) still leaves exactly those pieces in flight.
+  // ---------------------------------------------------------------------------------- main loop
   if constexpr (NS == 2) {  // 2-deep ring: k-tile t + 1 in flight while t is multiplied
     prep();
 #pragma unroll
@@ -485,10 +328,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
       cur ^= 1;
     }
     compute(cur, 0, std::false_type{});
-    epilogue(t_first);
-    return;
-  }
-  if constexpr (!PERSIST) {  // one tile: the plain ring, epilogue after the last k-tile
+  } else {  // 3-deep ring: t + 2 issued while t is multiplied, counted vmcnt keeps one tile in flight
     prep();
 #pragma unroll
     for (int i = 0; i < L; ++i) issue(i, 0);
@@ -517,97 +357,150 @@ __global__ void __launch_bounds__(64 * WM * WN, NSX == 2 ? 2 : 1) k_conv_x3(X3Pa
       cur = cur == NS - 1 ? 0 : cur + 1;
     }
     compute(cur, 0, std::false_type{});
-    epilogue(t_first);
-    return;
   }
-  const int V = t_count * KT;
-  prep();
+  X3_BARRIER();  // every wave is done reading the ring: the epilogue reuses its LDS
+
+  // ---------------------------------------------------------------------------------- epilogue
+  // 1. park the fp32 accumulators (+ bias) as a [BM][BN] tile: 16-B chunk c of row r at c ^ (r & CMASK)
+  //    (a lane group of 16 consecutive rows writes one logical chunk into 16 distinct bank slots)
+  constexpr int CMASK = CPR - 1 < 31 ? CPR - 1 : 31;
+  float* et = reinterpret_cast<float*>(lds);
+  const int pm = lane & 31;
 #pragma unroll
-  for (int i = 0; i < L; ++i) issue(i, 0);
-  if (V > 1) {
-    prep();
+  for (int i = 0; i < TNI; ++i)
 #pragma unroll
-    for (int i = 0; i < L; ++i) issue(i, 1);
-    X3_WAIT(L);
-  } else {
-    X3_WAIT(0);
-  }
+    for (int g = 0; g < 4; ++g) {
+      const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias && n0 + nl < p.K) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = p.bias[n0 + nl + e];
+      }
+#pragma unroll
+      for (int j = 0; j < TMI; ++j) {
+        const int ml = (b_row0 - BN) + 32 * j + pm;
+        *reinterpret_cast<v4f*>(&et[ml * BN + (((nl >> 2) ^ (ml & CMASK)) << 2)]) =
+            (v4f){acc[i][j][4 * g] + b4[0], acc[i][j][4 * g + 1] + b4[1], acc[i][j][4 * g + 2] + b4[2],
+                  acc[i][j][4 * g + 3] + b4[3]};
+      }
+    }
   X3_BARRIER();
-  int cur = 0, nxt = 2, c_kt = 0, c_tl = 0;
-  for (int v = 0; v < V; ++v) {
-    const bool more = v + 2 < V;
-    const bool last = c_kt == KT - 1;
-    if (more) prep();
-    if (more && !last) {
-      compute(cur, nxt, std::true_type{});
-    } else {
-      compute(cur, 0, std::false_type{});
-    }
-    if (last) {
-      epilogue(t_first + c_tl);
+  // 2. row-major pass: thread (rr, cc) handles channels n0 + 4·cc … +3 of rows rr, rr + RPP, …, so every
+  //    global access of a wave-instruction is RPP-row-contiguous 16-B chunks (full 4·BN-byte row segments)
+  const int cc = tid % CPR, rr = tid / CPR;
+  const int n = n0 + cc * 4;
+  const bool nok = n < p.K;  // K % 4 == 0 (host-checked): a 4-channel chunk is all in or all out
+  const bool want_stats = p.stats != nullptr;
+  float k4[4] = {0.f, 0.f, 0.f, 0.f}, mu[4] = {0.f, 0.f, 0.f, 0.f}, sc4[4] = {0.f, 0.f, 0.f, 0.f},
+        sh4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (nok) {
 #pragma unroll
-      for (int i = 0; i < TNI; ++i)
-#pragma unroll
-        for (int j = 0; j < TMI; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-      if (more) {
-#pragma unroll
-        for (int i = 0; i < L; ++i) issue(i, nxt);
+    for (int e = 0; e < 4; ++e) {
+      if (p.shift && !p.bnx) k4[e] = p.shift[n + e];
+      if (p.bnx) {
+        mu[e] = p.mean[n + e];
+        if (!p.bits) { sc4[e] = p.bsc[n + e]; sh4[e] = p.bsh[n + e]; }
       }
     }
-    if (v + 1 < V) {
-      if (more) {
-        X3_WAIT(L);
-      } else {
-        X3_WAIT(0);
+  }
+  float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+  const int rmax = p.M - m0 < BM ? p.M - m0 : BM;
+  if (nok) {
+#pragma unroll 2
+    for (int r = rr; r < rmax; r += RPP) {
+      const int m = m0 + r;
+      int mo = m;  // pixel of the output grid
+      if (p.scatter) {
+        const int img = m / (p.P * p.Q);
+        const int pq = m - img * p.P * p.Q;
+        const int pp = pq / p.Q, qq = pq - pp * p.Q;
+        mo = (img * p.oH + pp * p.osh + p.ooh) * p.oW + qq * p.osw + p.oow;
       }
-      X3_BARRIER();
+      const size_t off = (size_t)mo * p.ldy + n;
+      v4f v = *reinterpret_cast<const v4f*>(&et[r * BN + ((cc ^ (r & CMASK)) << 2)]);
+      if (p.res) {
+        bool live = true;
+        size_t roff = off;
+        if (p.res_sh) {
+          const int gridpix = p.scatter ? p.oH * p.oW : p.P * p.Q;
+          const int gw = p.scatter ? p.oW : p.Q;
+          const int img = mo / gridpix;
+          const int hw = mo - img * gridpix;
+          const int hh = hw / gw, ww = hw - hh * gw;
+          live = hh % p.res_sh == 0 && ww % p.res_sw == 0;
+          roff = ((size_t)(img * p.res_H + hh / p.res_sh) * p.res_W + ww / p.res_sw) * p.ldy + n;
+        }
+        if (live) v += *reinterpret_cast<const v4f*>(p.res + roff);
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (p.bnx) {
+        const v4f xv = *reinterpret_cast<const v4f*>(p.bnx + (size_t)mo * p.K + n);
+        unsigned mb;
+        if (p.bits) {
+          mb = (p.bits[(size_t)mo * (p.K >> 3) + (n >> 3)] >> (n & 7)) & 0xFu;
+        } else {
+          mb = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mb |= (fmaf(xv[e], sc4[e], sh4[e]) > 0.f ? 1u : 0u) << e;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = (mb >> e) & 1u ? v[e] : 0.f;
+          s4[e] += v[e];
+          q4[e] = fmaf(v[e], xv[e] - mu[e], q4[e]);
+        }
+      } else if (want_stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = v[e] - k4[e];
+          s4[e] += a;
+          q4[e] = fmaf(a, a, q4[e]);
+        }
+      }
+      if (!(p.dbg & 1)) *reinterpret_cast<v4f*>(p.y + off) = v;
     }
-    cur = cur == NS - 1 ? 0 : cur + 1;
-    nxt = nxt == NS - 1 ? 0 : nxt + 1;
-    if (++c_kt == KT) {
-      c_kt = 0;
-      ++c_tl;
+  }
+  if (want_stats) {  // 3. fold the RPP row groups of each channel through LDS, one atomic per channel
+    float* red = reinterpret_cast<float*>(lds + BM * BN * 4);  // [2][RPP][BN] behind the staged tile
+    *reinterpret_cast<v4f*>(&red[rr * BN + cc * 4]) = (v4f){s4[0], s4[1], s4[2], s4[3]};
+    *reinterpret_cast<v4f*>(&red[(RPP + rr) * BN + cc * 4]) = (v4f){q4[0], q4[1], q4[2], q4[3]};
+    X3_BARRIER();
+    const int rep = tm % p.R_rep;
+    for (int t = tid; t < 2 * BN; t += NT) {
+      const int which = t / BN, c = t - which * BN;
+      if (n0 + c >= p.K) continue;
+      float a = 0.f;
+#pragma unroll 4
+      for (int g = 0; g < RPP; ++g) a += red[(which * RPP + g) * BN + c];
+      atomicAdd(&p.stats[((size_t)which * p.R_rep + rep) * p.K + n0 + c], a);
     }
   }
 }
 
 // ---- host side ----
 // wave layout `wl`: 0 = the 2-D split (WM × WN = 4 × 2 / 2 × 2), 1 = waves over pixels only (8 × 1 /
-// 4 × 1): each wave's split B fragment then feeds all BN / 32 channel blocks (half the split VALU per MFMA)
-template <int MODE, bool PERSIST>
+// 4 × 1): each wave's split B fragment then feeds all BN / 32 channel blocks (half the split VALU per MFMA).
+// ns2: the 2-deep ring (two 128 × 128 or three 128 × 64 blocks share a CU).
+template <int MODE>
 static void launch_x3(int bm, int bn, int wl, int ns2, dim3 g, hipStream_t s, const X3Params& p) {
-  if (bm == 128 && ns2 && !PERSIST) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, false, 2>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, false, 2>), g, dim3(256), 0, s, p);
+  if (bm == 128 && bn == 64) {
+    hipLaunchKernelGGL((k_conv_x3<128, 64, 4, 1, MODE, 2>), g, dim3(256), 0, s, p);
+  } else if (bm == 128 && ns2) {
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 2>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 2>), g, dim3(256), 0, s, p);
   } else if (bm == 128) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, PERSIST>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, PERSIST>), g, dim3(256), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 3>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 3>), g, dim3(256), 0, s, p);
   } else if (bn == 64) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 64, 8, 1, MODE, PERSIST>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 64, 8, 1, MODE, 3>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, 3>), g, dim3(512), 0, s, p);
   } else {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 128, 8, 1, MODE, PERSIST>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, PERSIST>), g, dim3(512), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 128, 8, 1, MODE, 3>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, 3>), g, dim3(512), 0, s, p);
   }
-}
-
-static int x3_num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      v = 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
-
-// BIGDL_CONV_X3_PERSIST: 0 (default) = one tile per block everywhere, 1 = the pointwise convs stream
-// their tiles through persistent blocks (one per CU); off by default: no gain measured (profiles/r5_x3_shapes.txt)
-static int x3_persist_env() {
-  static const int v = [] { const char* e = getenv("BIGDL_CONV_X3_PERSIST"); return e ? atoi(e) : 0; }();
-  return v;
 }
 
 static bool x3_al(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -622,8 +515,7 @@ static int x3_env_tile() {
 // aligned), w2 the chunked [hi | lo] split of the KRSC fp32 filter (bigdl_split_bf16x2 of its
 // [K·R·S·C / 32][32] view), K % 8 == 0 for statistics / bnbwd (else K % 4).  bm / bn: the tile
 // (256 × 128, 256 × 64 or 128 × 128; 0 = heuristic).  osh … oW: the output scatter (1, 1, 0, 0, P, Q =
-// none); res_sh … res_W: the strided residual (0 = dense); persist: pointwise tile streaming (-1 = off,
-// 0 = BIGDL_CONV_X3_PERSIST / default on, 1 = on).  Returns hipError_t.
+// none); res_sh … res_W: the strided residual (0 = dense); persist: unused (ABI).  Returns hipError_t.
 BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias, const float* res, float* y,
                                float* stats, int R_rep, const float* shift, const float* bnx, const float* mean,
                                const void* bits, const float* bsc, const float* bsh, int Nb, int H, int W, int C,
@@ -643,6 +535,10 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   const long long Ml = (long long)Nb * P * Q;
   if (Ml > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   X3Params p{};
+  {
+    const char* e = getenv("BIGDL_X3_DEBUG");
+    p.dbg = e ? atoi(e) : 0;
+  }
   p.x = x; p.w = (const bf16_t*)w2; p.bias = bias; p.res = res; p.y = y;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -685,19 +581,14 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   const int ns2 = (bn >> 9) & 1;  // bit 9: the 2-deep ring (128 × 128 tile: two blocks per CU)
   bn &= 0xFF;
   if (bn == 0) bn = K <= 64 ? 64 : 128;
-  if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 128))) return (int)hipErrorInvalidValue;
+  if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 64)))) return (int)hipErrorInvalidValue;
   static const int wl_env = [] { const char* e = getenv("BIGDL_CONV_X3_WL"); return e ? atoi(e) : -1; }();
   if (wl_env >= 0) wl = wl_env;
   p.tiles_n = (K + bn - 1) / bn;
   const long long tiles = (Ml + bm - 1) / bm * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
-  if (pw1 && persist != 0 && (persist > 0 || x3_persist_env())) {
-    const long long nblk = x3_num_cus();  // LDS: one block per CU
-    launch_x3<3, true>(bm, bn, wl, ns2, dim3((unsigned)(tiles < nblk ? tiles : nblk)), s, p);
-  } else if (pw1) {
-    launch_x3<3, false>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
-  } else {
-    launch_x3<1, false>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
-  }
+  (void)persist;  // (a persistent tile-stream variant measured no gain: removed)
+  if (pw1) launch_x3<3>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
+  else launch_x3<1>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   BIGDL_CHECK_LAUNCH();
 }

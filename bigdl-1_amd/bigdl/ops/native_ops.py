@@ -764,7 +764,12 @@ def _tiled_launch(key, fn):
     heuristic); the tile is this geometry's entry of the kernel-selection table, if any."""
     rec = _TILE["record"]
     if rec is not None:
-        rec.append((key, fn))
+        # first launch per geometry only: a closure pins its launch's operands (dY, partials, …) until
+        # retiming ends, so recording every repeat would hold a whole step's worth of tensors
+        if isinstance(rec, dict):
+            rec.setdefault(key, fn)
+        else:
+            rec.append((key, fn))
     fn(_TILE["table"].get(key, (0, 0, 0)))
 
 
@@ -1530,7 +1535,8 @@ def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_sc
     n = w.numel()
     if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n):
         return NotImplemented
-    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
+    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.numel() == n
+                                   and shadow.data_ptr() % 8 == 0):
         return NotImplemented
     step_size = lr * math.sqrt(1 - beta2 ** step) / (1 - beta1 ** step)
     check(_lib().bigdl_adam(ptr(w), ptr(g), ptr(m), ptr(v), ptr(shadow), _ll(n), _f(step_size), _f(beta1), _f(beta2),
@@ -1546,7 +1552,8 @@ def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_dec
     if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n) or not (dev_n.is_cuda and
                                                                                   dev_n.dtype == _f32):
         return NotImplemented
-    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
+    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.numel() == n
+                                   and shadow.data_ptr() % 8 == 0):
         return NotImplemented
     check(_lib().bigdl_adam_dev(ptr(w), ptr(g), ptr(m), ptr(v), ptr(shadow), _ll(n), ptr(dev_n), _f(lr), _f(lr_decay),
                                 _f(beta1), _f(beta2), _f(eps), _f(weight_decay), _f(grad_scale), _s()), "adam_dev")
@@ -1562,7 +1569,8 @@ def adagrad_step(w, g, s, lr, lr_decay, n, weight_decay=0.0, grad_scale=1.0, sha
         return NotImplemented
     if dev_n is not None and not (dev_n.is_cuda and dev_n.dtype == _f32):
         return NotImplemented
-    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.data_ptr() % 8 == 0):
+    if shadow is not None and not (shadow.dtype == _bf16 and shadow.is_contiguous() and shadow.numel() == numel
+                                   and shadow.data_ptr() % 8 == 0):
         return NotImplemented
     clr = lr / (1 + n * lr_decay)
     check(_lib().bigdl_adagrad(ptr(w), ptr(g), ptr(s), ptr(shadow), _ll(numel), _f(clr), ptr(dev_n), _f(lr),

@@ -263,8 +263,11 @@ def bn_local_sums(x, shift, partial=None, G=0, rezero=False):
         if rezero:
             partial.zero_()
         return out
-    xf = acc_float(x) - acc_float(shift).to(acc_float(x).dtype).view(shape)
-    return torch.cat([xf.sum(dims), (xf * xf).sum(dims), xf.new_tensor([float(x.numel() // C)])])
+    # fp64 accumulation (the fp32 buffer the collective sums is the rounding of exact-ish sums: the
+    # finalize's E[(x−K)²] − E[x−K]² then does not inherit fp32 summation error on large batches)
+    xf = acc_float(x).double() - acc_float(shift).double().view(shape)
+    out = torch.cat([xf.sum(dims), (xf * xf).sum(dims), xf.new_tensor([float(x.numel() // C)])])
+    return out.to(acc_float(x).dtype if acc_float(x).dtype != torch.float64 else torch.float64)
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,

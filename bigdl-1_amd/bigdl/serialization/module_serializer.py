@@ -74,6 +74,15 @@ def _register_all():
                 _REGISTRY[obj.scala_class_name()] = obj
     except ImportError:
         pass
+    try:  # TF op layers (nn/tf: control flow, data-flow resources, ...)
+        from ..nn import tf as tfm
+        for name in dir(tfm):
+            obj = getattr(tfm, name)
+            if isinstance(obj, type) and issubclass(obj, AbstractModule):
+                _REGISTRY[obj.scala_class_name()] = obj
+                _REGISTRY.setdefault(obj.__name__, obj)
+    except ImportError:
+        pass
     try:
         from ..nn.quantized import layers as q
         for name in dir(q):
@@ -451,14 +460,30 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
             for sc in st[key]:
                 _set_attr(ctx, field.add(), [float(x) for x in sc])
     if isinstance(m, Graph):
-        names = {}
-        for n in m.forward_order:
+        from ..nn.dynamic_graph import DynamicGraph
+        dyn = isinstance(m, DynamicGraph)
+        # a dynamic graph saves every reachable node (its execution order exists only after a run)
+        order = list(reversed(m._all_nodes)) if dyn else m.forward_order
+        for n in order:
             sub = _module_to_pb(ctx, n.element)
             sub.preModules.extend([p.element.get_name() for p in n.prev_nodes])
             sub.nextModules.extend([q.element.get_name() for q in n.next_nodes])
             mp.subModules.add().CopyFrom(sub)
+            # the edges' output selections (Graph.scala doSerializeModule "<name>_edges": previous node
+            # name → 1-based output index of its Table, -1 = the whole activity)
+            name = n.element.get_name()
+            ev = mp.attr[f"{name}_edges"]
+            ev.dataType = DT["NAME_ATTR_LIST"]
+            ev.nameAttrListValue.name = name
+            inner = ev.nameAttrListValue.attr[name]
+            inner.dataType = DT["NAME_ATTR_LIST"]
+            inner.nameAttrListValue.name = name
+            for p, idx in zip(n.prev_nodes, n.prev_index):
+                _set_attr(ctx, inner.nameAttrListValue.attr[p.element.get_name()], int(idx) if idx else -1)
         _set_attr(ctx, mp.attr["inputNames"], [n.element.get_name() for n in m.inputs])
         _set_attr(ctx, mp.attr["outputNames"], [n.element.get_name() for n in m.outputs_nodes])
+        if dyn:
+            _set_attr(ctx, mp.attr["generateBackward"], bool(m.generate_backward))
         return mp
     from ..nn.layers.recurrent import Recurrent, Cell, MultiRNNCell
     if isinstance(m, Recurrent):
@@ -532,11 +557,18 @@ def _module_from_pb(ctx: _DeCtx, mp):
         for sub in mp.subModules:
             nodes[sub.name] = (ModuleNode(_module_from_pb(ctx, sub)), list(sub.preModules))
         for name, (node, pres) in nodes.items():
+            edges = attrs.get(f"{name}_edges")
+            edges = edges.get(name, {}) if isinstance(edges, dict) else {}
             for p in pres:
-                node(nodes[p][0])
+                idx = edges.get(p, -1) if isinstance(edges, dict) else -1
+                node((nodes[p][0], int(idx)) if idx is not None and int(idx) > 0 else nodes[p][0])
         ins = [nodes[n][0] for n in attrs.get("inputNames", [])]
         outs = [nodes[n][0] for n in attrs.get("outputNames", [])]
-        g = Graph(ins, outs)
+        if "generateBackward" in attrs:  # Graph.scala doLoadModule: a DynamicGraph
+            from ..nn.dynamic_graph import DynamicGraph
+            g = DynamicGraph(ins, outs, None, bool(attrs["generateBackward"]))
+        else:
+            g = Graph(ins, outs)
         g.set_name(mp.name)
         return g
     from ..nn.layers.recurrent import Cell, MultiRNNCell

@@ -54,7 +54,7 @@ def _num_outputs(node) -> int:
         return int(_attr(node, "num_split", 1))
     if op == "Unpack":
         return int(_attr(node, "num", 1))
-    if op in ("TopKV2", "TopK", "Switch", "RefSwitch"):
+    if op in ("TopKV2", "TopK", "Switch", "RefSwitch", "TensorArrayV3", "TensorArrayGradV3", "TensorArrayConcatV3"):
         return 2
     if op.startswith("FusedBatchNormGrad"):
         return 5
@@ -313,12 +313,38 @@ def _depthwise(n):
     return O.DepthwiseConv2D(sw, sh, 0, 0, fmt)
 
 
+def _ta_shape(n):
+    """A TensorArrayV3 ``element_shape`` when fully defined, else None (no shape check)."""
+    sh = _attr(n, "element_shape", None)
+    if sh is None or getattr(sh, "unknown_rank", False):
+        return None
+    dims = [int(d.size) for d in getattr(sh, "dim", [])]
+    return dims if dims and all(d >= 0 for d in dims) else None
+
+
+# TensorArray / Stack resources (nn/tf/data_flow.py; the reference's loaders in DL/utils/tf/loaders)
+_DATA_FLOW = {
+    "TensorArrayV3": lambda n: T.TensorArrayCreator(_ta_shape(n), bool(_attr(n, "dynamic_size", False)),
+                                                    bool(_attr(n, "clear_after_read", True)),
+                                                    bool(_attr(n, "identical_element_shapes", False)),
+                                                    (_attr(n, "tensor_array_name", "") or "")),
+    "TensorArrayGradV3": lambda n: T.TensorArrayGrad(_attr(n, "source", "") or ""),
+    "TensorArrayWriteV3": lambda n: T.TensorArrayWrite(), "TensorArrayReadV3": lambda n: T.TensorArrayRead(),
+    "TensorArrayGatherV3": lambda n: T.TensorArrayGather(), "TensorArrayScatterV3": lambda n: T.TensorArrayScatter(),
+    "TensorArrayConcatV3": lambda n: T.TensorArrayConcat(), "TensorArraySplitV3": lambda n: T.TensorArraySplit(),
+    "TensorArraySizeV3": lambda n: T.TensorArraySize(), "TensorArrayCloseV3": lambda n: T.TensorArrayClose(),
+    "StackV2": lambda n: T.StackCreator(_attr(n, "stack_name", "") or ""),
+    "StackPushV2": lambda n: T.StackPush(), "StackPopV2": lambda n: T.StackPop(),
+}
+_OPS.update(_DATA_FLOW)
+
 # data-dependent control flow: executed by a DynamicGraph scheduler, never constant-folded
 _CONTROL = {"Switch", "RefSwitch", "Merge", "RefMerge", "Enter", "RefEnter", "Exit", "RefExit", "NextIteration",
             "RefNextIteration", "LoopCond"}
 _NOT_LOADABLE = {"FIFOQueueV2", "QueueDequeueV2", "QueueDequeueManyV2",
                  "QueueEnqueueV2", "QueueEnqueueManyV2", "TFRecordReaderV2", "ReaderReadV2", "RandomShuffleQueueV2"}
-_STATEFUL = {"RandomUniform", "TruncatedNormal", "RandomShuffle", "Placeholder", "PlaceholderWithDefault", "VariableV2"}
+_STATEFUL = {"RandomUniform", "TruncatedNormal", "RandomShuffle", "Placeholder", "PlaceholderWithDefault", "VariableV2",
+             *_DATA_FLOW}
 
 
 class TensorflowLoader:

@@ -180,3 +180,30 @@ def test_attention_decode_reference_bias_order():
     vh = v.reshape(rows, L, Hh, D).transpose(1, 2)
     ref = torch.softmax(qh @ kh.transpose(-1, -2) * 0.3 + bias, -1) @ vh
     torch.testing.assert_close(o, ref.transpose(1, 2).reshape(rows, Lq, Hh * D))
+
+
+def test_decode_cache_multi_position_append_bias_order():
+    """Appends of more than one position keep the reference's per-call ``[new; cache]`` order
+    (``DL/nn/Attention.scala:136-141``): with a key-dependent bias the in-place DecodeCache path equals
+    the tensor-cache path when a call appends 2 positions."""
+    from bigdl.nn.layers.attention import DecodeCache, Attention
+    torch.manual_seed(11)
+    H, nh = 16, 4
+    att = Attention(H, nh, 0.0)
+    att.evaluate()
+    steps = [torch.randn(2, 2, H), torch.randn(2, 1, H), torch.randn(2, 3, H)]
+    dc = DecodeCache(2, 2, H)
+    c_inplace = T()
+    c_inplace[f"{att.get_name()}_k"] = dc
+    c_inplace[f"{att.get_name()}_v"] = dc
+    c_tensor = T()
+    c_tensor[f"{att.get_name()}_k"] = torch.empty(2, 0, H)
+    c_tensor[f"{att.get_name()}_v"] = torch.empty(2, 0, H)
+    L = 0
+    for x in steps:
+        L += x.shape[1]
+        bias = torch.randn(2, 1, x.shape[1], L)  # key-dependent: order matters
+        a = att.forward(T(x, x, T(bias, c_inplace)))
+        b = att.forward(T(x, x, T(bias, c_tensor)))
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dc.keys(), c_tensor[f"{att.get_name()}_k"])

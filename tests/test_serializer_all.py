@@ -33,7 +33,13 @@ def _ids(*shape, hi=7):
 
 
 # class name → (constructor thunk, input thunk or None = try the generic inputs)
+import bigdl.nn.tf as TFL  # noqa: E402
+
 ARGS = {
+    "AvgPool": (lambda: TFL.AvgPool([1, 2, 2, 1], [1, 2, 2, 1]), lambda: _x(1, 4, 4, 2)),
+    "MaxPool": (lambda: TFL.MaxPool([1, 2, 2, 1], [1, 2, 2, 1]), lambda: _x(1, 4, 4, 2)),
+    "BiasAdd": (lambda: TFL.BiasAdd(torch.randn(3)), lambda: _x(2, 4, 4, 3)),
+    "Const": (lambda: TFL.Const(torch.randn(2, 3)), lambda: _x(1)),
     "ActivityRegularization": (lambda: nn.ActivityRegularization(0.1, 0.1), None),
     "Add": (lambda: nn.Add(4), None),
     "AddConstant": (lambda: nn.AddConstant(0.5), None),
@@ -139,6 +145,17 @@ EXEMPT = {
     "Proposal": "tests/test_detection.py",
     "RegionProposal": "tests/test_detection.py",
     "Input": "graph placeholder",
+    # TF op layers (bigdl.nn.tf): covered with graph inputs by their own tests
+    "AssignGrad": "tests/test_tf_data_flow.py (writes into a fixed gradient tensor)",
+    "TensorArrayGrad": "tests/test_tf_data_flow.py (needs a live source TensorArray)",
+    "AvgPoolGrad": "tests/test_tf.py / test_tf_queue_session.py (TF grad ops)",
+    "MaxPoolGrad": "tests/test_tf.py / test_tf_queue_session.py (TF grad ops)",
+    "ParseExample": "tests/test_tf.py (serialized tf.Example inputs)",
+    "ParseSingleExample": "tests/test_tf.py (serialized tf.Example inputs)",
+    "Split": "tests/test_tf.py (TF Split: Table(axis, value) input)",
+    "SplitAndSelect": "tests/test_tf.py",
+    "Variable": "tests/test_tf.py / test_tf_queue_session.py (TF variables)",
+    "_Pool": "abstract base of the TF pooling ops (MaxPool / AvgPool rows)",
 }
 
 GENERIC_INPUTS = [lambda: _x(3, 4), lambda: _x(2, 3, 4, 4), lambda: T(_x(3, 4), _x(3, 4, seed=4)), lambda: _x(2, 3, 4)]

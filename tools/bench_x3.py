@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(_HERE, "..", "bigdl-1_amd"))
 sys.path.insert(0, _HERE)
 from bench_conv import RESNET50  # noqa: E402
 
-TILES = [(256, 128), (256, 64), (128, 128), (256, 128 | 256), (256, 64 | 256), (128, 128 | 256), (128, 128 | 512), (128, 128 | 768)]  # bn | 256: 8x1 / 4x1 waves; | 512: 2-deep ring (2 blocks/CU)
+TILES = [(256, 128), (256, 64), (128, 128), (256, 128 | 256), (256, 64 | 256), (128, 128 | 256), (128, 128 | 512), (128, 128 | 768), (128, 64 | 768)]  # bn | 256: 8x1 / 4x1 waves; | 512: 2-deep ring (2-3 blocks/CU)
 
 
 def main():
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/bench_x3.jsonl")
+    ap.add_argument("--only", default="", help="C,K,R,stride,H filter (e.g. 64,256,1,1,56)")
     args = ap.parse_args()
     import torch
     from bigdl.ops import fp32x3 as F3
@@ -46,7 +47,7 @@ def main():
     out = open(args.out, "w")
     tot = {}
     for (C, K, R, st, H, mult) in RESNET50:
-        if C % 32:
+        if C % 32 or (args.only and args.only != f"{C},{K},{R},{st},{H}"):
             continue
         N = args.batch
         pad = R // 2
