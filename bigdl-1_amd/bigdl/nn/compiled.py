@@ -35,6 +35,9 @@ _log = logging.getLogger("bigdl.nn.compiled")
 
 
 def _leaves(m) -> List:
+    from ..utils.intermediate import IRGraph
+    if isinstance(m, IRGraph):  # a lowered model: plan the device graph it executes
+        return _leaves(m._need())
     subs = getattr(m, "modules", None)
     if isinstance(subs, list) and subs and all(hasattr(s, "updateOutput") for s in subs):
         out = []
@@ -133,6 +136,9 @@ def plan(model, example, phase: str = "inference") -> Plan:
     "training" keeps every activation for the backward)."""
     if phase not in ("inference", "training"):
         raise ValueError(phase)
+    was_training = model.isTraining()
+    if phase == "inference" and was_training:
+        model.evaluate()  # first: an IRGraph re-folds its device graph on the switch
     leaves = _leaves(model)
     records: List[LayerRecord] = []
     uses: Dict[int, List[int]] = {}
@@ -167,12 +173,9 @@ def plan(model, example, phase: str = "inference") -> Plan:
             return out
         m.updateOutput = rec
 
-    was_training = model.isTraining()
     for m in leaves:
         wrap(m)
     try:
-        if phase == "inference":
-            model.evaluate()
         with torch.no_grad():
             out = model.forward(example)
     finally:
@@ -324,8 +327,16 @@ class CompiledModule:
     graph's static output buffer: it is overwritten by the next call (clone it to keep it)."""
 
     def __init__(self, model, example, phase: str = "inference", graph: Optional[bool] = None, warmup: int = 2,
-                 tune: Optional[bool] = None):
-        self.model, self.phase = model, phase
+                 tune: Optional[bool] = None, lower: Optional[bool] = None):
+        self.source, self.phase = model, phase
+        # inference: lower through the IR first (BN folded into the convs / Linears, ReLU and the
+        # residual sum in the conv epilogues) — the reference's predictors always convert
+        # (LocalPredictor.scala:66, Predictor.scala:131,165 → ConversionUtils.convert)
+        self.lowered = False
+        if phase == "inference":
+            model = _lower(model, lower)
+            self.lowered = model is not self.source
+        self.model = model
         self.plan = plan(model, example, phase)
         ex = _tensors(example)
         self.graph = None
@@ -393,11 +404,52 @@ class CompiledModule:
     __call__ = forward
 
 
+def _model_device(model):
+    for p in (model.parameters() or ([], []))[0]:
+        return p.device
+    return torch.device("cpu")
+
+
+def _lower(model, lower: Optional[bool]):
+    """The IR-lowered inference form of ``model`` (``utils/intermediate.ConversionUtils.convert``), on
+    the model's device, or ``model`` itself when lowering is off (``bigdl.compile.lower``) or the model
+    cannot be expressed in the IR."""
+    from ..utils import config
+    if lower is None:
+        lower = bool(config.get_property("bigdl.compile.lower"))
+    if not lower:
+        return model
+    from ..utils.intermediate import ConversionUtils, IRGraph
+    if isinstance(model, IRGraph):
+        return model
+    was_training = model.isTraining() if hasattr(model, "isTraining") else False
+    try:
+        model.evaluate()
+        ir = ConversionUtils.convert(model)
+        dev = _model_device(model)
+        if dev.type == "cuda":
+            ir.to(dev)
+        ir.evaluate()
+    except Exception as e:  # noqa: BLE001 - a layer the IR does not cover: compile the model as is
+        _log.warning("IR lowering of %s failed (%s); compiling it unlowered", type(model).__name__, e)
+        return model
+    finally:
+        if was_training:
+            model.training()
+        if _model_device(model).type == "cuda":
+            from .fusion import fuse
+            fuse(model)  # the conversion cleared the source's execution-fusion flags: restore them
+    return ir
+
+
 def compile(model, example, phase: str = "inference", graph: Optional[bool] = None,  # noqa: A001
-            tune: Optional[bool] = None) -> CompiledModule:
+            tune: Optional[bool] = None, lower: Optional[bool] = None) -> CompiledModule:
     """Plan ``model`` for ``example``'s shape, select conv kernels (``autotune``) and return the
-    executor (see module docstring)."""
-    return CompiledModule(model, example, phase, graph, tune=tune)
+    executor (see module docstring).  In the inference phase the model is first lowered through the
+    IR (``lower``; default ``bigdl.compile.lower``): BN folding and conv+sum+ReLU epilogues, then
+    kernel selection and a HIP graph of the lowered forward.  The lowered graph holds folded copies
+    of the weights taken now: compile again after the weights change."""
+    return CompiledModule(model, example, phase, graph, tune=tune, lower=lower)
 
 
 __all__ = ["plan", "autotune", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer", "TILE_CANDIDATES",

@@ -86,9 +86,12 @@ def _batches(data, batch_size: int):
 
 
 class LocalPredictor:
-    """``compiled=True`` (or ``bigdl.predict.compiled``): on a GPU each distinct batch shape is
-    planned once and its forward captured into a HIP graph (``nn/compiled.py``), later batches of
-    that shape are a copy-in plus one graph replay."""
+    """``compiled`` (default ``bigdl.predict.compiled`` = on): on a GPU the model is lowered through
+    the IR once (``ConversionUtils.convert``: BN folded, conv+sum+ReLU epilogues — the reference's
+    LocalPredictor converts every model, ``LocalPredictor.scala:66``), each distinct batch shape is
+    planned once and its forward captured into a HIP graph (``nn/compiled.py``); later batches of
+    that shape are a copy-in plus one graph replay.  The lowered graph holds folded weights taken at
+    the first prediction: :meth:`refresh` drops it after the model's weights change."""
 
     def __init__(self, model, feature_padding=None, batch_size: int = -1, compiled: Optional[bool] = None):
         self.model = model
@@ -101,19 +104,27 @@ class LocalPredictor:
     def create(model, batch_size=-1, feature_padding=None):
         return LocalPredictor(model, feature_padding, batch_size)
 
-    def _run(self, m, x):
+    def refresh(self):
+        """Forget the lowered / captured forms (after the model's weights changed)."""
+        self._graphs = {}
+        self.__dict__.pop("_lowered", None)
+
+    def _run(self, m, x, eager: bool = False):
         from ..utils import config
         use = self.compiled if self.compiled is not None else bool(config.get_property("bigdl.predict.compiled"))
-        if not (use and isinstance(x, torch.Tensor) and x.is_cuda):
+        if eager or not (use and isinstance(x, torch.Tensor) and x.is_cuda):
             return m.forward(x)
         key = (tuple(x.shape), x.dtype)
         c = self._graphs.get(key)
         if c is None:
-            from ..nn.compiled import compile as compile_module
-            c = self._graphs[key] = compile_module(m, x)
+            from ..nn.compiled import compile as compile_module, _lower
+            low = self.__dict__.get("_lowered")
+            if low is None:  # one IR lowering per predictor, shared by every batch shape
+                low = self.__dict__["_lowered"] = _lower(m, None)
+            c = self._graphs[key] = compile_module(low, x, lower=False)
         return c(x)
 
-    def _forward_all(self, data):
+    def _forward_all(self, data, eager: bool = False):
         m = self.model
         dev = _model_device(m)
         was_training = m.isTraining()
@@ -126,7 +137,7 @@ class LocalPredictor:
             with torch.no_grad():
                 for b in _batches(data, self.batch_size):
                     b = b.to(dev, dtype=Engine.compute_dtype() if dev.type == "cuda" else None)
-                    out = self._run(m, b.getInput())
+                    out = self._run(m, b.getInput(), eager)
                     outs.extend(_split_batch(_to_host(out), b.size()))
         finally:
             if was_training:
@@ -150,7 +161,8 @@ class LocalPredictor:
         ``predict_key`` (``LocalPredictor.predictImage``)."""
         feats = image_frame.to_local().array if hasattr(image_frame, "to_local") else list(image_frame)
         samples = [f.get_sample() for f in feats]
-        outs = self._forward_all(samples)
+        # an intermediate layer's output exists only on the unlowered model: run it eagerly then
+        outs = self._forward_all(samples, eager=output_layer is not None)
         if output_layer is not None:
             layer = self.model.flattened_modules()
             target = [l for l in layer if l.get_name() == output_layer]
@@ -297,15 +309,23 @@ class PredictionService:
     Each instance is a shallow clone (parameters shared, activations private) in eval mode and —
     on a GPU — owns a dedicated HIP stream, so concurrent requests overlap on the device."""
 
-    def __init__(self, model, num_threads: int = 4):
+    def __init__(self, model, num_threads: int = 4, compiled: Optional[bool] = None):
+        from ..utils import config
         self.model = model.evaluate() if hasattr(model, "evaluate") else model
         self.num_threads = num_threads
         self._dev = _model_device(model)
         self._q: "queue.Queue" = queue.Queue()
+        use = compiled if compiled is not None else bool(config.get_property("bigdl.predict.compiled"))
+        self._compiled = use and self._dev.type == "cuda"
         for _ in range(num_threads):
             inst = _shallow_clone(model)
+            if self._compiled:
+                # each replica is IR-lowered (BN folded, fused epilogues) and captures its own HIP
+                # graph per request shape, replayed on its own stream
+                from ..nn.compiled import _lower
+                inst = _lower(inst, None)
             stream = torch.cuda.Stream(device=self._dev) if self._dev.type == "cuda" else None
-            self._q.put((inst, stream))
+            self._q.put((_ServeInstance(inst, self._compiled), stream))
 
     @staticmethod
     def create(model, num_threads: int = 4):
@@ -345,6 +365,23 @@ class PredictionService:
                 return _error_activity("Clone Result", e)
         finally:
             self._q.put((inst, stream))
+
+
+class _ServeInstance:
+    """One serving replica: its module plus, when compiled, a HIP graph per request shape."""
+
+    def __init__(self, module, compiled: bool):
+        self.module, self.compiled, self.graphs = module, compiled, {}
+
+    def forward(self, x):
+        if not (self.compiled and isinstance(x, torch.Tensor) and x.is_cuda):
+            return self.module.forward(x)
+        key = (tuple(x.shape), x.dtype)
+        c = self.graphs.get(key)
+        if c is None:
+            from ..nn.compiled import compile as compile_module
+            c = self.graphs[key] = compile_module(self.module, x, lower=False)
+        return c(x)
 
 
 def _move(a, dev):

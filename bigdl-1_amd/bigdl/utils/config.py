@@ -53,7 +53,8 @@ _REGISTRY = {
     "bigdl.bn.statReplicas": (int, 32, "R > 0 (with atomicStats off): conv epilogues ADD the BN statistics into R replicas (tile tm → replica tm % R) of a zeroed buffer — R-fold less same-address atomic contention than atomicStats, and the BN finalizes from R rows with no fold pass; 0 = per-tile partial rows. Default 32: 22.50 vs 22.94 ms/step (profiles/r4_bn_replicas_ab.txt)"),
     "bigdl.bn.shiftedStats": (bool, True, "conv-epilogue BN statistics as Σ(y−K), Σ(y−K)² with K = the BN running mean"),
     "bigdl.checkpoint.async": (bool, True, "trigger-driven checkpoints: host snapshot on the training thread, serialise + write on a writer thread"),
-    "bigdl.predict.compiled": (bool, False, "LocalPredictor: plan each batch shape once and replay its forward as a HIP graph"),
+    "bigdl.predict.compiled": (bool, True, "LocalPredictor / Predictor / PredictionService on a GPU: lower the model through the IR (BN fold, conv+sum+ReLU), plan each batch shape once and replay its forward as a HIP graph (the reference's predictors always convert, LocalPredictor.scala:66)"),
+    "bigdl.compile.lower": (bool, True, "nn.compiled.compile (inference phase): lower the model through the IR first (utils/intermediate.ConversionUtils: BN folded into convs / Linears, conv+sum+ReLU epilogues)"),
     "bigdl.roctx": (bool, False, "emit roctx ranges around forward / backward / reduce-scatter / update / all-gather"),
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),

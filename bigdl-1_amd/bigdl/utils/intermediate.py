@@ -439,6 +439,8 @@ class IRGraph(AbstractModule):
         return self.gradInput
 
     def training(self, is_training: bool = True):
+        if not is_training and not self.train and self.graph is not None and self.graph is not self._train_graph:
+            return self  # already an inference graph: re-fold only on a training → inference switch
         self.train = is_training
         if self._train_graph is not None:
             self._train_graph.training(is_training)

@@ -153,3 +153,42 @@ def test_training_compile_phase_pins_fwd_dgrad_wgrad_and_keeps_training():
     rel = float((w1 - w0).norm() / w0.norm())
     assert rel < 2e-2 and abs(l1 - l0) < 0.05 * max(1.0, abs(l0)), (rel, l0, l1)
     NO.conv_tile_table().clear()
+
+
+@pytest.mark.gpu
+def test_compiled_inference_lowers_through_ir_and_predictors_use_it():
+    """compile(model, x) in the inference phase lowers through the IR first (BN folded into the convs,
+    conv+sum+ReLU epilogues), captures the lowered forward, and matches the eager UNFUSED model within
+    bf16 tolerance; LocalPredictor uses the same lowered + captured form by default on a GPU
+    (reference: LocalPredictor.scala:66, Predictor.scala:131,165 → ConversionUtils.convert)."""
+    import bigdl.nn as nn
+    from bigdl.nn.compiled import compile
+    from bigdl.nn.fusion import unfuse
+    from bigdl.optim.predictor import LocalPredictor
+    from bigdl.utils.engine import Engine
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.utils.intermediate import IRGraph
+    Engine.init(device="cuda:0")
+    torch.manual_seed(0)
+    m = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+    m.training()
+    with torch.no_grad():  # real running statistics, so the folded BN is not the identity
+        m.forward(torch.randn(2, 3, 224, 224))
+    m.to(device="cuda")
+    m.evaluate()
+    x = torch.randn(4, 3, 224, 224, device="cuda")
+    unfuse(m)
+    with torch.no_grad():
+        ref = m.forward(x).float().clone()
+    c = compile(m, x)
+    assert c.lowered and isinstance(c.model, IRGraph) and c.captured
+    kinds = {type(mm).__name__ for mm in c.model._need().flattened_modules()}
+    assert "FusedConvSum" in kinds and "SpatialBatchNormalization" not in kinds
+    got = c(x).float()
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 2e-2, rel
+    pred = LocalPredictor(m, batch_size=4)
+    out = pred.predict(x.cpu())
+    assert pred._graphs and all(g.captured for g in pred._graphs.values())
+    rel2 = float((torch.stack([o.float() for o in out]).cuda() - ref).norm() / ref.norm())
+    assert rel2 < 2e-2, rel2

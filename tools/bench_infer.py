@@ -56,7 +56,7 @@ def main():
         print(json.dumps({"batch": bs, "eager_ms": round(te, 3), "compiled_ms": round(tc, 3), "captured": c.captured,
                           "speedup": round(te / tc, 2),
                           "eager_tuned_ms": round(tt, 3), "tiles_pinned": len(c.tiles), "img_per_s_compiled": round(bs / tc * 1e3, 1),
-                          "max_abs_diff": err, "arena_MiB": round(c.plan.arena_bytes / 2 ** 20, 1),
+                          "lowered": c.lowered, "max_abs_diff": err, "arena_MiB": round(c.plan.arena_bytes / 2 ** 20, 1),
                           "total_MiB": round(c.plan.total_bytes / 2 ** 20, 1)}), flush=True)
 
 
