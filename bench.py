@@ -24,7 +24,7 @@ training (``DL/models/resnet/{ResNet,TrainImageNet,Utils}.scala``): convs with b
 L2Regularizer(1e-4), BN eps 1e-3, SGD(lr 0.1, momentum 0.9, dampening 0, nesterov, wd 1e-4).
 
 The same invocation then times the identical config at the reference's precision — fp32 compute
-(bf16x3 operand splits on the matrix cores, fp32 accumulation; ``--fp32-steps``, default 5 on GPU)
+(bf16x3 operand splits on the matrix cores, fp32 accumulation; ``--fp32-steps``, default 10 on GPU)
 — and reports it as ``"fp32": {"value", "ms_per_step", ...}`` next to the bf16 headline ``value``.
 
 ``--device cpu`` (gloo, fp32) with ``--batch`` / ``--image-size`` exists to exercise the
@@ -231,7 +231,7 @@ def main(argv=None):
     # the same config at the reference's precision (fp32 compute: bf16x3 splits on the matrix cores,
     # tests/test_fp32x3.py), timed the same way after the bf16 headline
     fp32 = None
-    n32 = args.fp32_steps if args.fp32_steps is not None else (5 if dev.type == "cuda" else 0)
+    n32 = args.fp32_steps if args.fp32_steps is not None else (10 if dev.type == "cuda" else 0)
     driver = type(opt).__name__
     if n32 > 0 and dtype != "fp32":
         del opt, batches

@@ -214,8 +214,24 @@ TILE_CANDIDATES = ((0, 0, 0), (64, 32, 128), (64, 64, 128), (128, 32, 128), (128
 WGRAD_CANDIDATES = ((0, 0), (0, 32), (0, 64), (256, 0), (768, 0), (1024, 0), (256, 32), (768, 64))
 
 
+#: fp32 direct-operand conv (ops/csrc/conv_x3.hip) tiles (BM, BN | wave-layout bits): (0, 0) = the
+#: launcher's heuristic; bn | 256 = waves over pixels only, | 512 = 2-deep ring (2-3 blocks per CU)
+X3_CANDIDATES = ((0, 0), (256, 128), (256, 64), (128, 128), (256, 128 | 256), (256, 64 | 256), (128, 128 | 256),
+                 (128, 128 | 512), (128, 128 | 768), (128, 64 | 768))
+
+
+#: fp32 weight-gradient (conv_wgrad.hip F32): split-M block targets (0 = heuristic ≈512 blocks)
+WGRAD32_CANDIDATES = ((0,), (-256,), (-1024,), (-2048,), (-4096,))
+
+
 def _candidates(key):
-    return WGRAD_CANDIDATES if (isinstance(key, tuple) and key and key[0] == "wg") else TILE_CANDIDATES
+    if isinstance(key, tuple) and key and key[0] == "wg":
+        return WGRAD_CANDIDATES
+    if isinstance(key, tuple) and key and key[0] == "wg32":
+        return WGRAD32_CANDIDATES
+    if isinstance(key, tuple) and key and key[0] == "x3":
+        return X3_CANDIDATES
+    return TILE_CANDIDATES
 
 
 def _time_candidates(key, fn, iters, lib):

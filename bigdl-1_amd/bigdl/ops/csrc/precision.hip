@@ -97,24 +97,25 @@ BIGDL_EXPORT int bigdl_split_bf16x2(const float* src, long long rows, int C, lon
 __global__ void __launch_bounds__(256) k_s2d_f32(const float* __restrict__ x, long long sn, long long sc, long long sh,
                                                  long long sw, int N, int C, int H, int W, int ph, int pw, int H2,
                                                  int W2, int Cp, float* __restrict__ out) {
-  const long long total = (long long)N * H2 * W2;
+  // one thread per (output pixel, 4-channel group): consecutive lanes store consecutive 16 B
+  const int G = Cp >> 2;
+  const long long total = (long long)N * H2 * W2 * G;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int w2 = (int)(t % W2);
-    const long long r = t / W2;
+    const int g = (int)(t % G);
+    const long long pix = t / G;
+    const int w2 = (int)(pix % W2);
+    const long long r = pix / W2;
     const int h2 = (int)(r % H2);
     const int n = (int)(r / H2);
-    float* o = out + t * Cp;
-    for (int c0 = 0; c0 < Cp; c0 += 4) {
-      float v[4];
+    float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int cc = c0 + e, c = cc >> 2, bh = (cc >> 1) & 1, bw = cc & 1;
-        const int h = 2 * h2 + bh - ph, w = 2 * w2 + bw - pw;
-        v[e] = (c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
-                   ? x[n * sn + c * sc + h * sh + w * sw] : 0.f;
-      }
-      *reinterpret_cast<float4*>(o + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    for (int e = 0; e < 4; ++e) {
+      const int cc = 4 * g + e, c = cc >> 2, bh = (cc >> 1) & 1, bw = cc & 1;
+      const int h = 2 * h2 + bh - ph, w = 2 * w2 + bw - pw;
+      v[e] = (c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+                 ? x[n * sn + c * sc + h * sh + w * sw] : 0.f;
     }
+    *reinterpret_cast<float4*>(out + t * 4) = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -122,8 +123,8 @@ BIGDL_EXPORT int bigdl_s2d_f32(const float* x, long long sn, long long sc, long 
                                int H, int W, int ph, int pw, int H2, int W2, int Cp, float* out, hipStream_t s) {
   if (!x || !out || N <= 0 || C <= 0 || H2 <= 0 || W2 <= 0 || Cp % 4 || 4 * C > Cp || ((uintptr_t)out & 15))
     return (int)hipErrorInvalidValue;
-  const long long total = (long long)N * H2 * W2;
-  hipLaunchKernelGGL(k_s2d_f32, dim3(bigdl_grid(total, 256, 16384)), dim3(256), 0, s, x, sn, sc, sh, sw, N, C, H, W, ph,
+  const long long total = (long long)N * H2 * W2 * (Cp / 4);
+  hipLaunchKernelGGL(k_s2d_f32, dim3(bigdl_grid(total, 256, 32768)), dim3(256), 0, s, x, sn, sc, sh, sw, N, C, H, W, ph,
                      pw, H2, W2, Cp, out);
   BIGDL_CHECK_LAUNCH();
 }

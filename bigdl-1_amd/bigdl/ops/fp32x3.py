@@ -176,17 +176,25 @@ def _x3(x, w2, y, nb, h, w, c, k, r, s, p, q, stride, pad, dil, bias=None, res=N
     sub-pixel dgrad, ``res_strided`` = (res_sh, res_sw, res_H, res_W) of a compact residual."""
     osh, osw, ooh, oow, oh_, ow_ = scatter if scatter is not None else (1, 1, 0, 0, p, q)
     rsh, rsw, rh, rw = res_strided if res_strided is not None else (0, 0, 0, 0)
-    check(N.lib().bigdl_conv_x3(ptr(x), ptr(w2), ptr(bias), ptr(res), ptr(y), ptr(stats), rep, ptr(shift), ptr(bnx),
-                                ptr(mean), ptr(bits), ptr(bsc), ptr(bsh), nb, h, w, c, k, r, s, p, q, stride[0],
-                                stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), k,
-                                *(tile if tile is not None else _X3_TILES.get((nb, h, w, c, k, r, s, p, q), (0, 0))),
-                                osh, osw, ooh,
-                                oow, oh_, ow_, rsh, rsw, rh, rw, persist, _s()), "conv_x3")
 
+    def launch(t, st):
+        check(N.lib().bigdl_conv_x3(ptr(x), ptr(w2), ptr(bias), ptr(res), ptr(y), ptr(st), rep, ptr(shift), ptr(bnx),
+                                    ptr(mean), ptr(bits), ptr(bsc), ptr(bsh), nb, h, w, c, k, r, s, p, q, stride[0],
+                                    stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), k, t[0], t[1], osh,
+                                    osw, ooh, oow, oh_, ow_, rsh, rsw, rh, rw, persist, _s()), "conv_x3")
+    if tile is not None:
+        launch(tile, stats)
+        return
+    # the kernel-selection table (training / inference compile phase): candidates per launch geometry
+    from .native_ops import _tiled_launch, _stat_target
+    key = ("x3", nb, h, w, c, k, r, s, p, q, tuple(stride), tuple(pad), scatter is not None, stats is not None,
+           bnx is not None)
 
-#: per-geometry tile choice (bm, bn) for conv_x3 launches, filled by the training compile phase /
-#: tools/bench_x3.py; absent = the kernel's heuristic
-_X3_TILES: dict = {}
+    def fn(t):
+        t = (0, 0) if len(t) != 2 else t  # (0, 0, 0): no entry → the launcher's heuristic
+        # re-timed after the step: the BN already consumed (and cleared) its replicated sums
+        launch(t, None if stats is None else _stat_target(stats, True))
+    _tiled_launch(key, fn)
 
 
 def _x3_geom_ok(c, k, r, s, pad):
@@ -525,9 +533,13 @@ def _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation):
             and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
             and _fits(nb * h * w * c * 4, nb * p * q * k * 4)):
         return NotImplemented
-    check(N.lib().bigdl_conv_wgrad_f32(ptr(x), ptr(gy), ptr(gw_acc), C.c_float(float(scale)), nb, h, w, c, k, r, s, p,
-                                       q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1], 0, _s()),
-          "conv_wgrad_f32")
+    def fn(t):
+        # t = (splits,): 0 = the launcher's heuristic (≈512 blocks), < 0 = -target block count
+        check(N.lib().bigdl_conv_wgrad_f32(ptr(x), ptr(gy), ptr(gw_acc), C.c_float(float(scale)), nb, h, w, c, k, r,
+                                           s, p, q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                           t[0] if len(t) == 1 else 0, _s()), "conv_wgrad_f32")
+    from .native_ops import _tiled_launch
+    _tiled_launch(("wg32", nb, h, w, c, k, r, s, p, q, tuple(stride), tuple(pad)), fn)
     return None
 
 

@@ -166,3 +166,67 @@ def test_temporal_conv_native_matches_torch():
     gw = m.gradWeight.float().view(32, 3, 64).permute(0, 2, 1)
     torch.testing.assert_close(gw, w.grad, rtol=3e-2, atol=3e-2 * float(w.grad.abs().max()))
     _assert_clean()
+
+
+# ------------------------------------------------------------------------------------------- fp32 (bf16x3)
+class _NoTorchConv:
+    """Makes the torch conv entry points raise while active: an fp32 training step must run every
+    convolution (forward, data and weight gradients) on the bf16x3 HIP kernels, never MIOpen."""
+
+    def __enter__(self):
+        import torch.nn.functional as F
+        self.saved = [(F, "conv2d", F.conv2d), (torch, "conv2d", torch.conv2d),
+                      (torch.nn.grad, "conv2d_input", torch.nn.grad.conv2d_input),
+                      (torch.nn.grad, "conv2d_weight", torch.nn.grad.conv2d_weight)]
+
+        def boom(*a, **k):
+            raise AssertionError("torch / MIOpen convolution called on the fp32 path")
+        for mod, name, _ in self.saved:
+            setattr(mod, name, boom)
+        return self
+
+    def __exit__(self, *exc):
+        for mod, name, fn in self.saved:
+            setattr(mod, name, fn)
+
+
+def _fp32():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.compute.dtype", "fp32")
+    Engine.set_compute_dtype("fp32")
+
+
+def test_resnet50_fp32_step_native():
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.optim import SGD
+    _fp32()
+    try:
+        x = torch.randn(4, 3, 224, 224, device=dev)
+        y = (torch.randint(0, 1000, (4,)) + 1).float().to(dev)
+        model = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+        with _NoTorchConv():
+            _train_steps(model, x, y, CrossEntropyCriterion(),
+                         SGD(learningrate=0.1, momentum=0.9, dampening=0.0, nesterov=True, weightdecay=1e-4))
+        _assert_clean()
+    finally:
+        from bigdl.utils.engine import Engine
+        Engine.set_compute_dtype("bf16")
+
+
+def test_vgg_cifar_fp32_step_native():
+    from bigdl.models.vgg import VggForCifar10
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    _fp32()
+    try:
+        x = torch.randn(16, 3, 32, 32, device=dev)
+        y = (torch.randint(0, 10, (16,)) + 1).float().to(dev)
+        with _NoTorchConv():
+            _train_steps(VggForCifar10(10), x, y, ClassNLLCriterion(),
+                         SGD(learningrate=0.01, momentum=0.9, dampening=0.0))
+        _assert_clean()
+    finally:
+        from bigdl.utils.engine import Engine
+        Engine.set_compute_dtype("bf16")
