@@ -127,7 +127,15 @@ class SpatialConvolution(TensorModule):
             x = x.unsqueeze(0)
         if self.format == "NHWC":
             x = x.permute(0, 3, 1, 2)
-        x = to_device_layout(x)
+        if (self.nInputPlane <= 3 and self.nGroup == 1 and x.is_cuda and x.dim() == 4 and x.is_contiguous()
+                and not x.is_contiguous(memory_format=torch.channels_last) and (self.dilationH, self.dilationW) == (1, 1)
+                and Engine.compute_dtype() == torch.bfloat16 and x.dtype in (torch.float32, torch.bfloat16)):
+            # the RGB input: cast + relayout + channel padding for the C4 stem kernel in one pass
+            from ...ops import native as N
+            y = N.native_ops.nchw_to_nhwc_padded(x, self._pad_slot_()) if N.has("conv2d_forward") else NotImplemented
+            x = to_device_layout(x) if y is NotImplemented else y
+        else:
+            x = to_device_layout(x)
         pt, pb, pl, pr = self._pads(x)
         if pt != pb or pl != pr:
             x = F.pad(x, (pl, pr, pt, pb))
@@ -210,7 +218,7 @@ class SpatialConvolution(TensorModule):
                 tgt = None
             y = ops.conv2d_forward(x, w4, b, (self.strideH, self.strideW), pad, (self.dilationH, self.dilationW),
                                    self.nGroup, relu=self._fused_relu, out=tgt,
-                                   pad_slot=self._pad_slot_() if self.train else None)
+                                   pad_slot=self._pad_slot_() if (self.train or self.nInputPlane <= 3) else None)
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)

@@ -202,11 +202,12 @@ __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const fl
 // BITS (with RELU): also emit the ReLU mask as one byte per 8-channel chunk (bit e = output channel
 // cg·8 + e is > 0) — a ResNet block tail's output mask for the backward, 1/16 of the bytes of
 // re-reading the bf16 output there.
-template <bool RES, bool RELU, bool BITS = false, int kApplyUnroll = 4>
-__global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                                  bf16_t* __restrict__ y, long long M, int C,
-                                                  const float* __restrict__ scale, const float* __restrict__ shift,
-                                                  uint8_t* __restrict__ bits = nullptr) {
+// The streaming body (scale / shift: global memory, or the block's LDS copy in the one-launch
+// finalize+apply kernels below).
+template <bool RES, bool RELU, bool BITS, int kApplyUnroll>
+__device__ __forceinline__ void bn_apply_rows(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                              bf16_t* __restrict__ y, long long M, int C, const float* scale,
+                                              const float* shift, uint8_t* __restrict__ bits) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -259,6 +260,14 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       }
     }
   }
+}
+
+template <bool RES, bool RELU, bool BITS = false, int kApplyUnroll = 4>
+__global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                  bf16_t* __restrict__ y, long long M, int C,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  uint8_t* __restrict__ bits = nullptr) {
+  bn_apply_rows<RES, RELU, BITS, kApplyUnroll>(x, res, y, M, C, scale, shift, bits);
 }
 
 // A/B knobs (profiles/r3_bn_apply_ab.txt): BIGDL_BN_APPLY_BLOCKS caps the grid (default 1024: 0.87-1.06
@@ -534,11 +543,10 @@ __global__ void __launch_bounds__(32 * kFinRG) k_bn_bwd_finalize(const T* __rest
   if (cbias) cbias[c] += cbscale * (A * dbeta + B * Mf * mean[c] + Mf * Cc);
 }
 
-template <bool RELU, bool GRES, int kApplyUnroll = 4>
-__global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
-                                                      const bf16_t* __restrict__ y, bf16_t* __restrict__ gx,
-                                                      bf16_t* __restrict__ gres, long long M, int C,
-                                                      const float* __restrict__ coef) {
+template <bool RELU, bool GRES, int kApplyUnroll>
+__device__ __forceinline__ void bn_bwd_apply_rows(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
+                                                  const bf16_t* __restrict__ y, bf16_t* __restrict__ gx,
+                                                  bf16_t* __restrict__ gres, long long M, int C, const float* coef) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -585,6 +593,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
       }
     }
   }
+}
+
+template <bool RELU, bool GRES, int kApplyUnroll = 4>
+__global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ y, bf16_t* __restrict__ gx,
+                                                      bf16_t* __restrict__ gres, long long M, int C,
+                                                      const float* __restrict__ coef) {
+  bn_bwd_apply_rows<RELU, GRES, kApplyUnroll>(gy, x, y, gx, gres, M, C, coef);
 }
 
 // Backward.  ws: 2·G·C floats; coef: 3·C floats.  gx may be null (no input gradient needed).
@@ -675,12 +691,18 @@ struct BnFwdFin {
   float* coef;           // [2C] scale, shift
   double M;
   float momentum, eps;
+  // SyncBN (bigdl_bn_fwd_train_sums_fin): the row count read on the device (the all-reduced count at
+  // sums[2C]), the arrival ticket in a word of its own, and `keep` = leave the sums as they are
+  const float* dM;
+  unsigned* ticket;
+  int keep;
 };
 
 __device__ __forceinline__ void fin_fwd_coef(const BnFwdFin& f, int C, int c, float& mean, float& var, float& invstd,
                                              float& sc, float& sh) {
-  const double dm = (double)f.sums[c] / f.M;
-  var = (float)fmax((double)f.sums[C + c] / f.M - dm * dm, 0.0);
+  const double Mg = f.dM ? (double)*f.dM : f.M;
+  const double dm = (double)f.sums[c] / Mg;
+  var = (float)fmax((double)f.sums[C + c] / Mg - dm * dm, 0.0);
   mean = (f.kshift ? f.kshift[c] : 0.f) + (float)dm;
   invstd = rsqrtf(var + f.eps);
   sc = (f.gamma ? f.gamma[c] : 1.f) * invstd;
@@ -688,12 +710,35 @@ __device__ __forceinline__ void fin_fwd_coef(const BnFwdFin& f, int C, int c, fl
 }
 
 // the arrival ticket of a block that has finished reading `sums`; true in the last block
-__device__ __forceinline__ bool last_arriver(float* sums, int C) {
+__device__ __forceinline__ bool last_arriver(unsigned* cnt) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(cnt, 1u) == gridDim.x - 1 ? 1 : 0;
+  __syncthreads();
+  return last != 0;
+}
+
+// Two-level election over a ticket block of kTicketLeaves + 1 words (root first): block b counts
+// into leaf b % kTicketLeaves, each leaf's last arriver into the root.  ~1000 blocks arriving at
+// once on ONE word serialise at its L2 channel for microseconds; 16 leaves cut that 16x.  Every
+// word is back at zero when the elected block returns (the next launch reuses the block).
+constexpr int kTicketLeaves = 16;
+__device__ __forceinline__ bool last_arriver_tree(unsigned* cnt) {
   __shared__ int last;
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned* cnt = reinterpret_cast<unsigned*>(sums + 2 * C);
-    last = atomicAdd(cnt, 1u) == gridDim.x - 1 ? 1 : 0;
+    const unsigned nb = gridDim.x, leaf = blockIdx.x % kTicketLeaves;
+    const unsigned in_leaf = (nb - leaf + kTicketLeaves - 1) / kTicketLeaves;
+    const unsigned leaves = nb < (unsigned)kTicketLeaves ? nb : (unsigned)kTicketLeaves;
+    int l = 0;
+    if (atomicAdd(&cnt[1 + leaf], 1u) == in_leaf - 1) {
+      atomicExch(&cnt[1 + leaf], 0u);
+      if (atomicAdd(&cnt[0], 1u) == leaves - 1) {
+        atomicExch(&cnt[0], 0u);
+        l = 1;
+      }
+    }
+    last = l;
   }
   __syncthreads();
   return last != 0;
@@ -708,57 +753,18 @@ template <bool RES, bool RELU, bool BITS>
 __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       bf16_t* __restrict__ y, long long M, int C, BnFwdFin f,
                                                       uint8_t* __restrict__ bits) {
-  constexpr int U = 4;
-  BnGeom g = bn_geom(C);
+  // the block derives every channel's scale / shift once into LDS ([2][C], dynamic), then streams
+  // exactly like k_bn_apply (per-thread derivation of its 8 channels cost 2x on the relu-only tails)
+  extern __shared__ __attribute__((aligned(16))) float cf[];
   const int t = threadIdx.x;
-  const int cg_local = t % g.tpr;
-  const int r_off = t / g.tpr;
-  if (r_off < g.RPI) {
-    const long long rstride = (long long)gridDim.x * g.RPI;
-    for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
-      float sc[8], sh[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float mean, var, invstd;
-        fin_fwd_coef(f, C, cg * 8 + k, mean, var, invstd, sc[k], sh[k]);
-      }
-      long long r = (long long)blockIdx.x * g.RPI + r_off;
-      for (; r < M; r += U * rstride) {
-        bigdl_u32x4 xv[U], rvv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long ru = r + u * rstride;
-          const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
-          xv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
-          if (RES) rvv[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(res + off));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long ru = r + u * rstride;
-          if (ru >= M) break;
-          const size_t off = (size_t)ru * C + (size_t)cg * 8;
-          float v[8], rv[8];
-          unpack8(make_uint4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]), v);
-          if (RES) unpack8(make_uint4(rvv[u][0], rvv[u][1], rvv[u][2], rvv[u][3]), rv);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            float o = fmaf(v[k], sc[k], sh[k]);
-            if (RES) o += rv[k];
-            if (RELU) o = fmaxf(o, 0.f);
-            v[k] = o;
-          }
-          store8(y + off, v);
-          if (BITS) {
-            uint32_t b = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
-            bits[off >> 3] = (uint8_t)b;
-          }
-        }
-      }
-    }
+  for (int c = t; c < C; c += blockDim.x) {
+    float mean, var, invstd;
+    fin_fwd_coef(f, C, c, mean, var, invstd, cf[c], cf[C + c]);
   }
-  if (!last_arriver(f.sums, C)) return;
+  __syncthreads();
+  bn_apply_rows<RES, RELU, BITS, 4>(x, res, y, M, C, cf, cf + C, bits);
+  if (!(f.ticket ? last_arriver_tree(f.ticket) : last_arriver(reinterpret_cast<unsigned*>(f.sums + 2 * C)))) return;
+  const double Mg = f.dM ? (double)*f.dM : f.M;
   for (int c = t; c < C; c += blockDim.x) {
     float mean, var, invstd, sc, sh;
     fin_fwd_coef(f, C, c, mean, var, invstd, sc, sh);
@@ -767,14 +773,14 @@ __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__
     f.coef[c] = sc;
     f.coef[C + c] = sh;
     if (f.run_mean) {
-      const float unb = f.M > 1.0 ? (float)(var * f.M / (f.M - 1.0)) : var;
+      const float unb = Mg > 1.0 ? (float)(var * Mg / (Mg - 1.0)) : var;
       const float true_mean = mean + (f.in_bias ? f.in_bias[c] : 0.f);
       f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * true_mean;
       f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * unb;
     }
   }
   __syncthreads();  // every coefficient is computed before the sums are cleared
-  rezero_sums(f.sums, C);
+  if (!f.keep) rezero_sums(f.sums, C);
 }
 
 // Training BN forward from atomically accumulated conv-epilogue statistics: ONE launch (see above).
@@ -784,7 +790,8 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums_apply(const void* x, const void* res, v
                                                float* run_mean, float* run_var, float momentum, float eps,
                                                float* save_mean, float* save_invstd, float* sums, const float* shift,
                                                float* coef, int relu, void* bits, hipStream_t s) {
-  if (C % 8 || M <= 0 || !sums || !save_mean || !save_invstd || !coef || (bits && !relu)) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 8192 || M <= 0 || !sums || !save_mean || !save_invstd || !coef || (bits && !relu))
+    return (int)hipErrorInvalidValue;
   BnFwdFin f{sums, shift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef, (double)M, momentum,
              eps};
   const int grid = apply_grid(M, C);
@@ -792,12 +799,12 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums_apply(const void* x, const void* res, v
   const bf16_t* rr = (const bf16_t*)res;
   bf16_t* yr = (bf16_t*)y;
   uint8_t* br = (uint8_t*)bits;
-  if (relu && bits && res) hipLaunchKernelGGL((k_bn_apply_fin<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
-  else if (relu && bits) hipLaunchKernelGGL((k_bn_apply_fin<false, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
-  else if (res && relu) hipLaunchKernelGGL((k_bn_apply_fin<true, true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
-  else if (res) hipLaunchKernelGGL((k_bn_apply_fin<true, false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
-  else if (relu) hipLaunchKernelGGL((k_bn_apply_fin<false, true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
-  else hipLaunchKernelGGL((k_bn_apply_fin<false, false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, f, br);
+  if (relu && bits && res) hipLaunchKernelGGL((k_bn_apply_fin<true, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (relu && bits) hipLaunchKernelGGL((k_bn_apply_fin<false, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (res && relu) hipLaunchKernelGGL((k_bn_apply_fin<true, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (res) hipLaunchKernelGGL((k_bn_apply_fin<true, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply_fin<false, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else hipLaunchKernelGGL((k_bn_apply_fin<false, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -818,6 +825,13 @@ struct BnBwdFin {
   float cbscale;
   float* coef;
   float M;
+  // SyncBN (bigdl_bn_bwd_apply_sums): `sums` are the GLOBAL sums (the coefficients), `lsums` this
+  // rank's (dγ, dβ and the folded bias over its Ml rows); dM / ticket / keep as in BnFwdFin
+  const float* lsums;
+  float Ml;
+  const float* dM;
+  unsigned* ticket;
+  int keep;
 };
 
 __device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, float& a, float& dg, float& A, float& B,
@@ -827,58 +841,36 @@ __device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, fl
   dg = f.sums[C + c] * is;
   const float gm = f.gamma ? f.gamma[c] : 1.f;
   A = gm * is;
-  B = -gm * is * is * dg / f.M;
-  Cc = -gm * is * a / f.M - B * f.mean[c];
+  const float Mg = f.dM ? *f.dM : f.M;
+  B = -gm * is * is * dg / Mg;
+  Cc = -gm * is * a / Mg - B * f.mean[c];
 }
 
 __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ gx, long long M, int C, BnBwdFin f) {
-  constexpr int U = 4;
-  BnGeom g = bn_geom(C);
+  // coefficients once per block into LDS ([3][C], dynamic), then the k_bn_bwd_apply stream
+  extern __shared__ __attribute__((aligned(16))) float cf[];
   const int t = threadIdx.x;
-  const int cg_local = t % g.tpr;
-  const int r_off = t / g.tpr;
-  if (gx && r_off < g.RPI) {
-    const long long rstride = (long long)gridDim.x * g.RPI;
-    for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
-      float A[8], B[8], Cc[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float a, dg;
-        fin_bwd_coef(f, C, cg * 8 + k, a, dg, A[k], B[k], Cc[k]);
-      }
-      long long r = (long long)blockIdx.x * g.RPI + r_off;
-      for (; r < M; r += U * rstride) {
-        bigdl_u32x4 gq[U], xq[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long ru = r + u * rstride;
-          const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
-          gq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(gy + off));
-          xq[u] = __builtin_nontemporal_load(reinterpret_cast<const bigdl_u32x4*>(x + off));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long ru = r + u * rstride;
-          if (ru >= M) break;
-          const size_t off = (size_t)ru * C + (size_t)cg * 8;
-          float gv[8], xv[8];
-          unpack8(make_uint4(gq[u][0], gq[u][1], gq[u][2], gq[u][3]), gv);
-          unpack8(make_uint4(xq[u][0], xq[u][1], xq[u][2], xq[u][3]), xv);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) xv[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
-          store8(gx + off, xv);
-        }
-      }
+  if (gx) {
+    for (int c = t; c < C; c += blockDim.x) {
+      float a, dg;
+      fin_bwd_coef(f, C, c, a, dg, cf[c], cf[C + c], cf[2 * C + c]);
     }
+    __syncthreads();
+    bn_bwd_apply_rows<false, false, 4>(gy, x, nullptr, gx, nullptr, M, C, cf);
   }
-  if (!last_arriver(f.sums, C)) return;
+  if (!(f.ticket ? last_arriver_tree(f.ticket) : last_arriver(reinterpret_cast<unsigned*>(f.sums + 2 * C)))) return;
+  const float Ml = f.lsums ? f.Ml : (f.dM ? *f.dM : f.M);
   for (int c = t; c < C; c += blockDim.x) {
     float a, dg, A, B, Cc;
     fin_bwd_coef(f, C, c, a, dg, A, B, Cc);
+    if (f.lsums) {  // this rank's share: dγ, dβ (and the bias) over its own rows
+      a = f.lsums[c];
+      dg = f.lsums[C + c] * f.invstd[c];
+    }
     if (f.ggamma) f.ggamma[c] += f.gscale * dg;
     if (f.gbeta) f.gbeta[c] += f.gscale * a;
-    if (f.cbias) f.cbias[c] += f.cbscale * (A * a + B * f.M * f.mean[c] + f.M * Cc);
+    if (f.cbias) f.cbias[c] += f.cbscale * (A * a + B * Ml * f.mean[c] + Ml * Cc);
     if (f.coef) {
       f.coef[c] = A;
       f.coef[C + c] = B;
@@ -886,18 +878,18 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restri
     }
   }
   __syncthreads();
-  rezero_sums(f.sums, C);
+  if (!f.keep) rezero_sums(f.sums, C);
 }
 
 BIGDL_EXPORT int bigdl_bn_bwd_sums_apply(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
                                          const float* mean, const float* invstd, float* ggamma, float* gbeta,
                                          float gscale, float* cbias, float cbscale, float* sums, float* coef,
                                          hipStream_t s) {
-  if (C % 8 || M <= 0 || !sums || !mean || !invstd || (gx && (!gm || !x))) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 4096 || M <= 0 || !sums || !mean || !invstd || (gx && (!gm || !x))) return (int)hipErrorInvalidValue;
   BnBwdFin f{sums, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, (float)M};
   const int grid = gx ? apply_grid(M, C) : 1;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), 0, s, (const bf16_t*)gm, (const bf16_t*)x, (bf16_t*)gx,
-                     M, C, f);
+  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), gx ? 12 * C : 0, s, (const bf16_t*)gm, (const bf16_t*)x,
+                     (bf16_t*)gx, M, C, f);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -973,8 +965,27 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
                                          const float* gamma, const float* beta, const float* in_bias,
                                          float* run_mean, float* run_var, float momentum, float eps,
                                          float* save_mean, float* save_invstd, const float* sums,
-                                         const float* kshift, float* coef, int relu, void* bits, hipStream_t s) {
+                                         const float* kshift, float* coef, int relu, void* bits, unsigned* ticket,
+                                         hipStream_t s) {
   if (C % 8 || M <= 0 || count < 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
+  if (ticket && C <= 8192) {
+    // ONE launch: every block derives its channels' coefficients from the global sums, the last
+    // arriver writes the saved statistics / coefficients / running statistics (k_bn_apply_fin)
+    BnFwdFin f{const_cast<float*>(sums), kshift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef,
+               (double)count, momentum, eps, count == 0 ? sums + 2 * C : nullptr, ticket, 1};
+    const int grid = apply_grid(M, C);
+    const bf16_t* xr = (const bf16_t*)x;
+    const bf16_t* rr = (const bf16_t*)res;
+    bf16_t* yr = (bf16_t*)y;
+    uint8_t* br = (uint8_t*)bits;
+    if (relu && bits && res) hipLaunchKernelGGL((k_bn_apply_fin<true, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    else if (relu && bits) hipLaunchKernelGGL((k_bn_apply_fin<false, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    else if (res && relu) hipLaunchKernelGGL((k_bn_apply_fin<true, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    else if (res) hipLaunchKernelGGL((k_bn_apply_fin<true, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    else if (relu) hipLaunchKernelGGL((k_bn_apply_fin<false, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    else hipLaunchKernelGGL((k_bn_apply_fin<false, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+    BIGDL_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift, sums,
                      1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
                      coef + C, count == 0 ? sums + 2 * C : nullptr);
@@ -1019,9 +1030,20 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
                                          long long count, int C, const float* gamma, const float* mean,
                                          const float* invstd, float* ggamma, float* gbeta, float gscale,
                                          const float* local_sums, const float* global_sums, float* coef,
-                                         float* coef_scratch, int relu, float* cbias, float cbscale, hipStream_t s) {
+                                         float* coef_scratch, int relu, float* cbias, float cbscale, unsigned* ticket,
+                                         hipStream_t s) {
   if (C % 8 || M <= 0 || count < 0) return (int)hipErrorInvalidValue;
   const float* dM = count == 0 ? global_sums + 2 * C : nullptr;  // the all-reduced count
+  if (ticket && !relu && C <= 4096) {
+    // ONE launch (k_bn_bwd_apply_fin): coefficients from the global sums in every block, this rank's
+    // dγ / dβ / folded-bias share from its local sums in the last arriver
+    BnBwdFin f{const_cast<float*>(global_sums), gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, nullptr,
+               (float)count, local_sums, (float)M, dM, ticket, 1};
+    const int grid = gx ? apply_grid(M, C) : 1;
+    hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), gx ? 12 * C : 0, s, (const bf16_t*)gy,
+                       (const bf16_t*)x, (bf16_t*)gx, M, C, f);
+    BIGDL_CHECK_LAUNCH();
+  }
   if (ggamma || gbeta)
     hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, local_sums, 1, count, C, gamma,
                        mean, invstd, ggamma, gbeta, gscale, (float*)nullptr, 0.f, coef_scratch, dM);

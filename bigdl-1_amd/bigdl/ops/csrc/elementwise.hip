@@ -411,6 +411,50 @@ __global__ void __launch_bounds__(256) k_nchw_to_nhwc(const T* __restrict__ x, b
   }
 }
 
+// Few-channel images (the RGB model input): one thread per pixel reads its C planes (coalesced along
+// pixels) and writes the Cp-channel zero-padded NHWC row as ONE 8-B (Cp 4) or 16-B (Cp 8) store —
+// the stem conv's channel-padded operand directly, no tile transpose and no separate pad pass.
+template <typename T>
+__device__ __forceinline__ float ld_as_f32(const T* p) {
+  if constexpr (sizeof(T) == 4) return *p;
+  else return bf2f(*p);
+}
+
+template <typename T, int CP>
+__global__ void __launch_bounds__(256) k_nchw_to_nhwc_pad(const T* __restrict__ x, bf16_t* __restrict__ y, int C,
+                                                          long long HW, long long total) {
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long n = t / HW, p = t - n * HW;
+    const T* xs = x + n * C * HW + p;
+    uint32_t w[CP / 2];
+#pragma unroll
+    for (int e = 0; e < CP / 2; ++e) {
+      float v0 = 0.f, v1 = 0.f;
+      if (2 * e < C) v0 = ld_as_f32(xs + (2 * e) * HW);
+      if (2 * e + 1 < C) v1 = ld_as_f32(xs + (2 * e + 1) * HW);
+      w[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+    }
+    if constexpr (CP == 4) *reinterpret_cast<uint2*>(y + t * 4) = make_uint2(w[0], w[1]);
+    else *reinterpret_cast<uint4*>(y + t * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+BIGDL_EXPORT int bigdl_nchw_to_nhwc_pad_bf16(const void* x, int dtype, void* y, int N, int C, long long HW, int Cp,
+                                             hipStream_t s) {
+  if (!x || !y || N <= 0 || HW <= 0 || C <= 0 || C > Cp || (Cp != 4 && Cp != 8) || ((uintptr_t)y & (2 * Cp - 1)))
+    return (int)hipErrorInvalidValue;
+  const long long total = (long long)N * HW;
+  const dim3 g((unsigned)bigdl_grid(total, 256, 65536));
+  if (dtype == 0) {
+    if (Cp == 4) hipLaunchKernelGGL((k_nchw_to_nhwc_pad<float, 4>), g, dim3(256), 0, s, (const float*)x, (bf16_t*)y, C, HW, total);
+    else hipLaunchKernelGGL((k_nchw_to_nhwc_pad<float, 8>), g, dim3(256), 0, s, (const float*)x, (bf16_t*)y, C, HW, total);
+  } else {
+    if (Cp == 4) hipLaunchKernelGGL((k_nchw_to_nhwc_pad<bf16_t, 4>), g, dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, C, HW, total);
+    else hipLaunchKernelGGL((k_nchw_to_nhwc_pad<bf16_t, 8>), g, dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, C, HW, total);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
 // dtype: 0 = fp32 input, 1 = bf16 input
 BIGDL_EXPORT int bigdl_nchw_to_nhwc_bf16(const void* x, int dtype, void* y, int N, int C, long long HW,
                                          hipStream_t s) {

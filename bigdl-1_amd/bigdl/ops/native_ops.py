@@ -208,7 +208,7 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias)):
         return NotImplemented
     if G == 0:  # atomically accumulated sums [2C + 1] (conv epilogue, stats_atomic)
-        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32:
+        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32 or C_ > 8192:
             return NotImplemented
     elif partial is None or partial.numel() != 2 * G * C_ or partial.dtype != _f32:
         return NotImplemented
@@ -267,7 +267,7 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
     coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
     gx = torch.empty_like(x) if (need_input and not lazy) else None
     if G == 0:  # atomically accumulated [Σg', Σg'·(x − μ), counter] from the dgrad epilogue
-        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32:
+        if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32 or C_ > 4096:
             return NotImplemented
         check(_lib().bigdl_bn_bwd_sums_apply(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma),
                                              ptr(save_mean), ptr(save_invstd), ptr(gg_acc), ptr(gb_acc), _f(scale),
@@ -317,6 +317,18 @@ def bn_local_sums(x, shift, partial=None, G=0, rezero=False):
     return out
 
 
+_TICKETS: dict = {}
+
+
+def _ticket(dev):
+    """A zeroed arrival-ticket word of the device (the one-launch finalize+apply kernels' last-block
+    election; the last arriver re-zeroes it, so stream-ordered launches share it)."""
+    t = _TICKETS.get(dev)
+    if t is None:
+        t = _TICKETS[dev] = torch.zeros(32, dtype=torch.int32, device=dev)  # root + 16 leaves (batchnorm.hip)
+    return t
+
+
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
                          residual=None, in_bias=None, coef_out=None, bits_out=None):
     """Training BN from GLOBAL shifted sums over ``count`` rows (0: the all-reduced count at
@@ -338,7 +350,8 @@ def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, runni
     check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
                                          ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum),
                                          _f(eps), ptr(mean), ptr(invstd), ptr(sums), ptr(shift), ptr(coef),
-                                         C.c_int(1 if relu else 0), ptr(bits_out if relu else None), _s()),
+                                         C.c_int(1 if relu else 0), ptr(bits_out if relu else None),
+                                         ptr(_ticket(x.device)), _s()),
           "bn_fwd_train_sums")
     return y, mean, invstd
 
@@ -394,7 +407,7 @@ def bn_backward_from_sums(gy, x, gamma, save_mean, save_invstd, local_sums, glob
                                          ptr(gg_acc if scale != 0 else None), ptr(gb_acc if scale != 0 else None),
                                          _f(scale), ptr(local_sums), ptr(global_sums), ptr(coef), ptr(scratch),
                                          C.c_int(1 if relu else 0), ptr(cbias_acc if cbias_scale != 0 else None),
-                                         _f(cbias_scale), _s()), "bn_bwd_apply_sums")
+                                         _f(cbias_scale), ptr(_ticket(x.device)), _s()), "bn_bwd_apply_sums")
     return gx
 
 
@@ -534,9 +547,12 @@ def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
     takes the forward's copy when it still describes the same input.  The copy therefore lives
     exactly as long as the layer's forward→backward pair and, under HIP-graph capture, is produced
     by a captured kernel of the same graph (no process-global cache)."""
-    if reuse and slot is not None and isinstance(slot[0], tuple) and len(slot[0]) == 4:
+    if slot is not None and isinstance(slot[0], tuple) and len(slot[0]) == 4:
+        # the backward of the same input, or an input the layout conversion produced padded
         src, ver, ct, padded = slot[0]
-        if src is x_nhwc_4d and ver == x_nhwc_4d._version and ct == c_to:
+        if src is x_nhwc_4d and ver == x_nhwc_4d._version and ct == c_to and (reuse or padded.dim() == 4 and
+                                                                             padded.shape[1] == c_to and
+                                                                             padded.data_ptr() == src.data_ptr()):
             return padded
     n, c, h, w = x_nhwc_4d.shape
     out = torch.empty((n, h, w, c_to), dtype=x_nhwc_4d.dtype, device=x_nhwc_4d.device)
@@ -557,6 +573,15 @@ def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
 def _conv_geom_ok(x, w4, groups, dilation):
     return (groups == 1 and x.dim() == 4 and x.dtype == _bf16 and w4.dtype == _bf16 and
             x.is_contiguous(memory_format=torch.channels_last) and _al16(x))
+
+
+def _conv_geom_ok_slot(x, w4, groups, dilation, slot):
+    """:func:`_conv_geom_ok`, also accepting a few-channel input view whose channel-padded
+    channels-last copy the layout conversion parked in the layer's pad ``slot``."""
+    if _conv_geom_ok(x, w4, groups, dilation):
+        return True
+    pre = _prepadded(x, slot)
+    return pre is not None and x.dtype == _bf16 and _conv_geom_ok(pre, w4, groups, dilation)
 
 
 def _depthwise_ok(x, w4, groups):
@@ -785,7 +810,7 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         return _depthwise_fwd(x, w4, b, stride, pad, dilation, relu)
     if groups > 1 and res is None and not stats and out is None and _grouped_ok(x, w4, groups):
         return _conv_fwd_grouped(x, w4, b, stride, pad, dilation, groups, pad_slot, relu)
-    if not _conv_geom_ok(x, w4, groups, dilation):
+    if not _conv_geom_ok_slot(x, w4, groups, dilation, pad_slot):
         return NotImplemented
     N_, C_, H, W = x.shape
     K, Ci, R, S = w4.shape
@@ -1416,7 +1441,7 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
             if need_input:
                 gi[:, g * Cg:(g + 1) * Cg] = r
         return gi
-    if not _conv_geom_ok(x, w4, groups, dilation) or gy.dtype != _bf16:
+    if not _conv_geom_ok_slot(x, w4, groups, dilation, pad_slot) or gy.dtype != _bf16:
         return NotImplemented
     if not gy.is_contiguous(memory_format=torch.channels_last) or not _al16(gy):
         return NotImplemented
@@ -2455,6 +2480,34 @@ def trunc_bf16(src, dst):
     if src.numel():
         check(_lib().bigdl_trunc_bf16(ptr(src), ptr(dst), _ll(src.numel()), _s()), "trunc_bf16")
     return dst
+
+
+def nchw_to_nhwc_padded(x, slot, cp=4):
+    """A contiguous NCHW image batch with C < ``cp`` (the RGB model input) → the stem conv's
+    channel-padded bf16 NHWC operand in ONE pass (csrc/elementwise.hip k_nchw_to_nhwc_pad).  Returns
+    the C-channel view of it (logical NCHW, the layer's input for every other purpose) and parks
+    (view, version, cp, padded) in the conv's pad ``slot`` — :func:`_pad_channels` and the conv
+    launch take the padded tensor from there instead of padding again."""
+    if not (x.is_cuda and x.dim() == 4 and x.is_contiguous() and x.dtype in (_f32, _bf16) and slot is not None):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if C_ >= cp or N_ * H * W == 0:
+        return NotImplemented
+    padded = torch.empty((N_, cp, H, W), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_nchw_to_nhwc_pad_bf16(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), ptr(padded), C.c_int(N_),
+                                             C.c_int(C_), _ll(H * W), C.c_int(cp), _s()), "nchw_to_nhwc_pad_bf16")
+    view = padded[:, :C_]
+    slot[0] = (view, view._version, cp, padded)
+    return view
+
+
+def _prepadded(x, slot):
+    """The channel-padded copy of ``x`` a layout conversion already parked in ``slot`` (or None)."""
+    if slot is not None and isinstance(slot[0], tuple) and len(slot[0]) == 4:
+        src, ver, ct, padded = slot[0]
+        if src is x and ver == x._version:
+            return padded
+    return None
 
 
 @register("nchw_to_nhwc_bf16")
