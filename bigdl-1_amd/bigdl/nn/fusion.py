@@ -69,6 +69,40 @@ def _fuse_graphs(model, convrelu):
                 _fuse_conv_relu(n.element, n.next_nodes[0].element)
 
 
+def _stackable(a, b):
+    from .layers.recurrent import Recurrent, LSTM
+    return (type(a) is Recurrent and type(b) is Recurrent and type(a.topology) is LSTM and type(b.topology) is LSTM
+            and a.topology.p == 0 and b.topology.p == 0 and not a.maskZero and not b.maskZero
+            and b.batchNormParams is None and a._stack_next is None and a._stack_prev is None
+            and b._stack_next is None and b._stack_prev is None)
+
+
+def _link_stack(a, b):
+    a._stack_next = b
+    b._stack_prev = a
+
+
+def _fuse_lstm_stacks(model):
+    """Two stacked Recurrent(LSTM) layers, the upper one's only input being the lower one's output
+    (Sequential neighbours or a Graph edge): flag the pair for the layer-wavefront execution
+    (nn/layers/recurrent.py ``_lstm2_forward``; the runtime re-checks shapes / dtypes and falls
+    back to layer-by-layer execution otherwise)."""
+    from .graph import Graph
+    for s in model.flattened_modules():
+        if isinstance(s, Sequential):
+            mods = s.modules
+            for i in range(len(mods) - 1):
+                if _stackable(mods[i], mods[i + 1]):
+                    _link_stack(mods[i], mods[i + 1])
+        elif isinstance(s, Graph) and hasattr(s, "forward_order"):
+            for n in s.forward_order:
+                if len(n.next_nodes) != 1:
+                    continue
+                m = n.next_nodes[0]
+                if len(m.prev_nodes) == 1 and _stackable(n.element, m.element):
+                    _link_stack(n.element, m.element)
+
+
 def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=None):
     if not config.get_property("bigdl.fusion"):
         return model
@@ -136,6 +170,8 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=Non
         for h in heads:
             h._tail_candidates = tails
     _fuse_graphs(model, convrelu)
+    if config.get_property("bigdl.fusion.lstmstack"):
+        _fuse_lstm_stacks(model)
     return model
 
 

@@ -154,6 +154,18 @@ def _fire_grad_ready(mods):
             h(m)
 
 
+def _acc_recurrent_grad(m, DG, h0, out, U):
+    """dU += Σ_t dg_tᵀ h_{t-1} as ONE GEMM over all B·T rows, then the module's grad-ready hooks."""
+    B, Tn, H = out.shape
+    if m.scale_w != 0:
+        hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)
+        ops.linear_backward(DG.reshape(B * Tn, 4 * H), hprev.reshape(B * Tn, H), U, False, m.gradWeight, None,
+                            m.scale_w)
+        if m.wRegularizer is not None:
+            m.wRegularizer.accRegularization(m.weight, m.gradWeight, m.scale_w)
+    _fire_grad_ready([m])
+
+
 def _fused_rnn_ok(H, *ts) -> bool:
     """Fused MFMA recurrent step applies: bf16 device rows, H % 8 == 0, native library loaded."""
     if not all(isinstance(t, torch.Tensor) for t in ts) or not ts[0].is_cuda:
@@ -792,7 +804,37 @@ class Recurrent(Container):
             return False
         return _fused_rnn_ok(c.outputSize, x2, c.h2g[0].cw("weight"), c.u_h.cw("weight"))
 
+    # -- stacked-LSTM fusion (bigdl.nn.fusion ``lstmstack``) ----------------------------------
+    #: lower layer: the next Recurrent(LSTM) whose only input is this layer's output; upper layer:
+    #: the layer feeding it.  The pair then runs on the layer wavefront (rnn_step.hip
+    #: bigdl_lstm2_seq_*): the upper layer's input projection h·W + b becomes a second reduction
+    #: segment of its recurrent step and both layers advance in the same launches.
+    _stack_next = None
+    _stack_prev = None
+    #: upper layer: (lower output, upper output) of the fused forward, consumed by its own forward
+    _stack_fwd = None
+    #: lower layer: its gate gradients, produced by the upper layer's fused backward
+    _stack_gx2 = None
+
+    def _stack_ready(self, x2):
+        nxt = self._stack_next
+        if nxt is None or not (self._use_fast_lstm() and nxt._use_fast_lstm()) or bool(self.train) != bool(nxt.train):
+            return False
+        pre = nxt.preTopology
+        if not (isinstance(pre, TimeDistributed) and type(pre.layer) is Linear and not pre.maskZero):
+            return False
+        H0, H1 = self.topology.hiddenSize, nxt.topology.hiddenSize
+        W1 = pre.layer.cw("weight")
+        return (x2.dim() == 3 and tuple(W1.shape) == (4 * H1, H0) and H1 % 8 == 0 and nxt._init_hidden_state is None
+                and self._init_hidden_state is None
+                and _fused_rnn_ok(H0, x2, self.topology.h2g.cw("weight"), W1, nxt.topology.h2g.cw("weight")))
+
     def updateOutput(self, input):
+        sf = self._stack_fwd
+        if sf is not None:
+            self._stack_fwd = None
+            if sf[0] is input:  # computed by the lower layer's fused forward for exactly this input
+                return sf[1]
         if input.dim() not in (3, 5, 6):
             raise ValueError(f"Recurrent: input should be a 3D/5D/6D Tensor, e.g [batch, times, nDim], "
                              f"current input.dim = {input.dim()}")
@@ -801,6 +843,8 @@ class Recurrent(Container):
             x2 = x2.to(_cdtype(x2))
         self._x2 = x2
         if self._use_fast_lstm():
+            if self._stack_next is not None and self._stack_ready(x2):
+                return self._lstm2_forward(x2)
             return self._lstm_forward(x2)
         if self._use_fast_gru(x2):
             return self._gru_forward(x2)
@@ -845,6 +889,52 @@ class Recurrent(Container):
         self._last_hidden = T(h, c)
         self._rec = ("lstm", h0, c0, out, acts, tcs, cs) if train else None
         return out
+
+    def _lstm2_forward(self, x2):
+        """This layer and ``_stack_next`` in one wavefront sequence (T + 1 launches); returns this
+        layer's output and parks the upper layer's for its own forward call."""
+        from ...ops import native_ops as NO
+        nxt = self._stack_next
+        c0m, c1m = self.topology, nxt.topology
+        lin = nxt.preTopology.layer
+        B, Tn, _ = x2.shape
+        H0, H1 = c0m.hiddenSize, c1m.hiddenSize
+        _fire_pre_forward([c0m.h2g, lin, c1m.h2g])
+        U0, U1, W1 = c0m.h2g.cw("weight"), c1m.h2g.cw("weight"), lin.cw("weight")
+        dev, dt = x2.device, x2.dtype
+        if lin.withBias:
+            b1 = lin.bias.detach().to(torch.float32).contiguous()
+        else:
+            b1 = torch.zeros(4 * H1, dtype=torch.float32, device=dev)
+        h00, c00 = self._h0(B, [H0], dev, dt)
+        h01, c01 = nxt._h0(B, [H1], dev, dt)
+        h00, h01 = h00.to(dt).contiguous(), h01.to(dt).contiguous()
+        c00, c01 = acc_float(c00).contiguous(), acc_float(c01).contiguous()
+        out0 = torch.empty(B, Tn, H0, device=dev, dtype=dt)
+        out1 = torch.empty(B, Tn, H1, device=dev, dtype=dt)
+        sdt = _state_dt(dt)
+        train = self.train
+        if train:
+            sv0 = [torch.empty(Tn, B, 4 * H0, device=dev, dtype=sdt), torch.empty(Tn, B, H0, device=dev, dtype=sdt),
+                   torch.empty(Tn, B, H0, device=dev, dtype=sdt)]  # acts, tcs, cs
+            sv1 = [torch.empty(Tn, B, 4 * H1, device=dev, dtype=sdt), torch.empty(Tn, B, H1, device=dev, dtype=sdt),
+                   torch.empty(Tn, B, H1, device=dev, dtype=sdt)]
+            cb0 = cb1 = None
+        else:
+            sv0 = sv1 = [None, None, None]
+            cb0 = torch.empty(2, B, H0, device=dev, dtype=sdt)
+            cb1 = torch.empty(2, B, H1, device=dev, dtype=sdt)
+        x2 = x2.contiguous()
+        NO.lstm2_seq_forward(x2, h00, c00, U0, out0, sv0[2], sv0[0], sv0[1], cb0, b1, W1, h01, c01, U1, out1, sv1[2],
+                             sv1[0], sv1[1], cb1)
+        last = Tn - 1
+        self._last_hidden = T(out0[:, last], sv0[2][last] if train else cb0[last % 2])
+        nxt._last_hidden = T(out1[:, last], sv1[2][last] if train else cb1[last % 2])
+        self._rec = ("lstm", h00, c00, out0, sv0[0], sv0[1], sv0[2]) if train else None
+        nxt._x2 = None
+        nxt._rec = ("lstm2", h01, c01, out1, sv1[0], sv1[1], sv1[2], self, out0) if train else None
+        nxt._stack_fwd = (out0, out1)
+        return out0
 
     def _gru_forward(self, x2):
         """GRU time loop on two fused launches per step (rnn_step.hip cells 2 and 3)."""
@@ -909,11 +999,17 @@ class Recurrent(Container):
     # -- backward ------------------------------------------------------------------------
     def _bptt(self, gradOutput):
         """Run BPTT once; returns the gradient w.r.t. the preTopology output (x2)."""
+        g = self._stack_gx2
+        if g is not None:  # produced by the upper layer's fused backward
+            self._stack_gx2 = None
+            return g
         rec = self._rec
         if rec is None:
             raise RuntimeError("Recurrent: backward called without a training-mode forward")
         if rec[0] == "lstm":
             return self._lstm_backward(gradOutput)
+        if rec[0] == "lstm2":
+            return self._lstm2_backward(gradOutput)
         if rec[0] == "gru":
             return self._gru_backward(gradOutput)
         _, tape, xl, flat0, out = rec
@@ -950,17 +1046,39 @@ class Recurrent(Container):
                 dg, gc = ops.lstm_cell_backward(gy[:, t], gh_rec, gc, acts[t], tcs[t], c_prev, dg_out=DG[:, t])
                 gh_rec = torch.mm(dg, U)
         self._grad_hidden_state = [gh_rec, gc]
-        # dU = Σ_t dgᵀ h_{t-1}: one GEMM over all B·T rows
-        hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)
-        m = cell.h2g
-        if m.scale_w != 0:
-            ops.linear_backward(DG.reshape(B * Tn, 4 * H), hprev.reshape(B * Tn, H), U, False, m.gradWeight, None,
-                                m.scale_w)
-            if m.wRegularizer is not None:
-                m.wRegularizer.accRegularization(m.weight, m.gradWeight, m.scale_w)
-        _fire_grad_ready([m])
+        _acc_recurrent_grad(cell.h2g, DG, h0, out, U)
         self._rec = None
         return DG
+
+    def _lstm2_backward(self, gradOutput):
+        """Upper layer of a fused stack: BPTT of BOTH layers on the wavefront (T + 1 launches);
+        accumulates both recurrent weights, returns this layer's gate gradients (for its input
+        projection's weight gradient) and parks the lower layer's for its backward."""
+        from ...ops import native_ops as NO
+        _, h01, c01, out1, acts1, tcs1, cs1, low, out0 = self._rec
+        _, h00, c00, _, acts0, tcs0, cs0 = low._rec
+        c1m, c0m = self.topology, low.topology
+        U1, U0, W1 = c1m.h2g.cw("weight"), c0m.h2g.cw("weight"), self.preTopology.layer.cw("weight")
+        B, Tn, H1 = out1.shape
+        H0 = out0.shape[2]
+        dev, dt = out1.device, out1.dtype
+        gy = gradOutput.to(dt)
+        if not gy.is_contiguous():
+            gy = gy.contiguous()
+        DG1 = torch.empty(B, Tn, 4 * H1, device=dev, dtype=dt)
+        DG0 = torch.empty(B, Tn, 4 * H0, device=dev, dtype=dt)
+        U1t, U0t, W1t = NO.transpose_bf16(U1), NO.transpose_bf16(U0), NO.transpose_bf16(W1)
+        gc1 = torch.empty(B, H1, device=dev, dtype=_state_dt(dt))
+        gc0 = torch.empty(B, H0, device=dev, dtype=_state_dt(dt))
+        NO.lstm2_seq_backward(gy, U1t, acts1, tcs1, cs1, c01, DG1, gc1, U0t, W1t, acts0, tcs0, cs0, c00, DG0, gc0)
+        self._grad_hidden_state = [NO.gemm(DG1[:, 0], U1t), gc1]
+        low._grad_hidden_state = [NO.gemm(DG0[:, 0], U0t), gc0]
+        _acc_recurrent_grad(c1m.h2g, DG1, h01, out1, U1)
+        _acc_recurrent_grad(c0m.h2g, DG0, h00, out0, U0)
+        low._stack_gx2 = DG0
+        low._rec = None
+        self._rec = None
+        return DG1
 
     def _gru_backward(self, gradOutput):
         from ...ops import native_ops as NO
@@ -994,8 +1112,20 @@ class Recurrent(Container):
         self._rec = None
         return DG
 
+    def _stacked_upper(self):
+        return self._rec is not None and self._rec[0] == "lstm2"
+
+    @staticmethod
+    def _stack_placeholder(input):
+        """gradInput of a fused upper layer: its input gradient went straight into the lower layer's
+        steps, so the lower layer ignores what it receives — a zero-stride view of the right shape."""
+        return torch.zeros((), dtype=input.dtype, device=input.device).expand(input.shape)
+
     def updateGradInput(self, input, gradOutput):
+        stacked = self._stacked_upper()
         self._gx2 = self._bptt(gradOutput)
+        if stacked:
+            return self._stack_placeholder(input)
         if self.preTopology is not None:
             return self.preTopology.updateGradInput(input, self._gx2)
         return self._gx2
@@ -1008,8 +1138,14 @@ class Recurrent(Container):
     def backward(self, input, gradOutput):
         import time
         t0 = time.perf_counter()
+        stacked = self._stacked_upper()
         gx2 = self._bptt(gradOutput)
-        gi = self.preTopology.backward(input, gx2) if self.preTopology is not None else gx2
+        if stacked:
+            self.preTopology.accGradParameters(input, gx2)
+            _fire_grad_ready([self.preTopology.layer])
+            gi = self._stack_placeholder(input)
+        else:
+            gi = self.preTopology.backward(input, gx2) if self.preTopology is not None else gx2
         self.gradInput = gi
         self.backward_time += time.perf_counter() - t0
         for h in self._grad_ready_hooks:

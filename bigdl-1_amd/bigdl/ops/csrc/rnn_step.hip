@@ -50,6 +50,13 @@ struct RnnStep {
   float* s2;            // GRU: fwd n save / bwd n (cell 4)
   bf16_t* rh;           // GRU r∘h_{t-1} rows, row stride ldrh
   long long ldrh;
+  // optional second reduction segment (stacked layers, k_rnn_step_pair): acc += a2 · u2ᵀ over K2 more
+  // indices — layer l+1's input product h_l·W folded into its recurrent step (forward), layer l's
+  // dh contribution dg_{l+1}·W folded into its step (backward).  a2 null = zero rows; K2 = 0 = none.
+  const bf16_t* a2;
+  long long lda2;
+  const bf16_t* u2;     // [G·Hs][K2]
+  int K2;
 };
 
 __device__ __forceinline__ float sgm(float x) { return 1.f / (1.f + __expf(-x)); }
@@ -99,7 +106,8 @@ __device__ __forceinline__ void pre_load(const RnnStep& p, int m, int j, float (
     for (int g = 0; g < 4; ++g) ld4(p.xg, p.x_f32, (long long)m * p.ldx + g * H + j, v[g]);
     ldf4(p.c_prev ? p.c_prev + mh : nullptr, v[4]);
   } else if constexpr (CELL == 1) {
-    ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    if (p.gy) ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    else v[0][0] = v[0][1] = v[0][2] = v[0][3] = 0.f;
     const float* a = p.act + (long long)m * 4 * H + j;
 #pragma unroll
     for (int g = 0; g < 4; ++g) ldf4(a + g * H, v[1 + g]);
@@ -225,7 +233,7 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
 constexpr int kStepWaves = 8;
 
 template <int CELL, int G>
-__global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
+__device__ __forceinline__ void rnn_step_body(const RnnStep& p) {
   constexpr int NW = kStepWaves;
   __shared__ v4f red[NW - 1][G * 2][64];
   constexpr int NP = NPre<CELL>::v;
@@ -246,23 +254,33 @@ __global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
 #pragma unroll
   for (int g = 0; g < G; ++g) acc0[g] = acc1[g] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if (p.a) {
+  if (p.a || p.a2) {
     const bool bu = j0 + fr < p.Hs;
-    const bf16_t* pa0 = p.a + (long long)(min0 ? m0 + fr : 0) * p.lda;
-    const bf16_t* pa1 = p.a + (long long)(min1 ? m0 + 16 + fr : 0) * p.lda;
+    const long long r0 = min0 ? m0 + fr : 0, r1 = min1 ? m0 + 16 + fr : 0;
+    const bf16_t* pa0 = p.a ? p.a + r0 * p.lda : nullptr;
+    const bf16_t* pa1 = p.a ? p.a + r1 * p.lda : nullptr;
+    const bf16_t* pb0 = p.a2 ? p.a2 + r0 * p.lda2 : nullptr;
+    const bf16_t* pb1 = p.a2 ? p.a2 + r1 * p.lda2 : nullptr;
     const bf16_t* pu = p.u + (long long)(bu ? j0 + fr : 0) * p.K;
-    const long long gstride = (long long)p.Hs * p.K;
-    const int KS = (p.K + 31) / 32;
+    const bf16_t* pu2 = p.K2 ? p.u2 + (long long)(bu ? j0 + fr : 0) * p.K2 : nullptr;
+    const long long gstride = (long long)p.Hs * p.K, gstride2 = (long long)p.Hs * p.K2;
+    const int KT = p.K + p.K2;  // K % 8 == 0: a lane's 8-index chunk never straddles the segments
+    const int KS = (KT + 31) / 32;
     const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 4
     for (int ks = wid; ks < KS; ks += NW) {
       const int k = ks * 32 + fq * 8;
-      const bool kin = k < p.K;
-      const v8s x0 = (kin && min0) ? *reinterpret_cast<const v8s*>(pa0 + k) : zero;
-      const v8s x1 = (kin && min1) ? *reinterpret_cast<const v8s*>(pa1 + k) : zero;
+      const bool kin = k < KT, seg2 = k >= p.K;
+      const int kk = seg2 ? k - p.K : k;
+      const bf16_t* s0 = seg2 ? pb0 : pa0;
+      const bf16_t* s1 = seg2 ? pb1 : pa1;
+      const v8s x0 = (kin && min0 && s0) ? *reinterpret_cast<const v8s*>(s0 + kk) : zero;
+      const v8s x1 = (kin && min1 && s1) ? *reinterpret_cast<const v8s*>(s1 + kk) : zero;
+      const bf16_t* wu = seg2 ? pu2 : pu;
+      const long long gs = seg2 ? gstride2 : gstride;
       v8s w[G];
 #pragma unroll
-      for (int g = 0; g < G; ++g) w[g] = (kin && bu) ? *reinterpret_cast<const v8s*>(pu + g * gstride + k) : zero;
+      for (int g = 0; g < G; ++g) w[g] = (kin && bu) ? *reinterpret_cast<const v8s*>(wu + g * gs + kk) : zero;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         acc0[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[g], x0, acc0[g], 0, 0, 0);
@@ -293,50 +311,78 @@ __global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
   if (min1) epilogue<CELL, G>(p, m0 + 16 + fr, j, pre1, acc1);
 }
 
+template <int CELL, int G>
+__global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
+  rnn_step_body<CELL, G>(p);
+}
+
+// Two stacked layers in ONE launch (blockIdx.z = layer; bit z of `live` = that layer has a step in
+// this wave): the layer wavefront — layer 1 runs step t−1 while layer 0 runs step t (forward), layer 0
+// runs step t+1 while layer 1 runs step t (backward, reversed), so a 2-layer sequence takes T + 1
+// dependent launches instead of 2T.
+template <int CELL, int G>
+__global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step_pair(RnnStep p0, RnnStep p1, int live) {
+  const int z = blockIdx.z;
+  if (!((live >> z) & 1)) return;
+  const RnnStep& p = z ? p1 : p0;
+  if ((int)blockIdx.x * 16 >= p.Hs || (int)blockIdx.y * 32 >= p.M) return;
+  rnn_step_body<CELL, G>(p);
+}
+
 static bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 static bool a8(const void* q) { return ((uintptr_t)q & 7) == 0; }
 
-// Host launcher: validates everything the kernel's vector accesses assume (H % 8, K % 8, 16-B
-// aligned operand rows, 8-B aligned bf16 / 16-B aligned fp32 quads) before any launch.
+// Host-side validation of everything the kernel's vector accesses assume (H % 8, K % 8, 16-B aligned
+// operand rows, 8-B aligned bf16 / 16-B aligned fp32 quads), before any launch.
+static int rnn_step_check(int cell, const RnnStep& p) {
+  const int M = p.M, K = p.K, Hs = p.Hs;
+  if (M <= 0 || K <= 0 || Hs <= 0 || Hs % 8 || K % 8 || cell < 0 || cell > 5) return (int)hipErrorInvalidValue;
+  if (p.a && (p.lda < K || p.lda % 8 || !a16(p.a))) return (int)hipErrorInvalidValue;
+  if (!p.u || !a16(p.u)) return (int)hipErrorInvalidValue;
+  static const int KWANT[6] = {1, 4, 1, 1, 2, 1};  // K in units of Hs
+  if (K != KWANT[cell] * Hs) return (int)hipErrorInvalidValue;
+  if (p.K2 < 0 || p.K2 % 8 || (p.K2 && (!p.u2 || !a16(p.u2))) || (!p.K2 && p.a2)) return (int)hipErrorInvalidValue;
+  if (p.a2 && (p.lda2 < p.K2 || p.lda2 % 8 || !a16(p.a2))) return (int)hipErrorInvalidValue;
+  const void* f32s[] = {p.c_prev, p.c_out, p.act, p.tc, p.gc_next, p.dc_prev, p.s0, p.s1, p.s2};
+  for (const void* q : f32s)
+    if (q && !a16(q)) return (int)hipErrorInvalidValue;
+  if (p.xg && (p.ldx % 4 || (p.x_f32 ? !a16(p.xg) : !a8(p.xg)))) return (int)hipErrorInvalidValue;
+  const void* b8s[] = {p.hprev, p.h_out, p.gy, p.dg, p.rh};
+  const long long lds_[] = {p.ldhp, p.ldho, p.ldgy, p.lddg, p.ldrh};
+  for (int i = 0; i < 5; ++i)
+    if (b8s[i] && (!a8(b8s[i]) || lds_[i] % 4)) return (int)hipErrorInvalidValue;
+  // per-cell required tensors (cell 1: gy may be null when the second segment carries it)
+  bool ok = true;
+  switch (cell) {
+    case 0: ok = p.xg && p.h_out; break;
+    case 1: ok = (p.gy || p.K2) && p.act && p.tc && p.dg && p.dc_prev; break;
+    case 2: ok = p.xg && p.hprev && p.rh && p.s0 && p.s1; break;
+    case 3: ok = p.xg && p.hprev && p.s1 && p.h_out; break;
+    case 4: ok = p.gy && p.s0 && p.s1 && p.s2 && p.hprev && p.dg; break;
+    case 5: ok = p.a && p.s0 && p.s1 && p.hprev && p.dg; break;
+  }
+  return ok ? 0 : (int)hipErrorInvalidValue;
+}
+
+static dim3 rnn_step_grid(int Hs, int M, int z = 1) {
+  return dim3((unsigned)((Hs + 15) / 16), (unsigned)((M + 31) / 32), (unsigned)z);
+}
+
 BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const void* u, int M, int K, int Hs,
                                 const void* xg, long long ldx, int x_f32, const void* hprev, long long ldhp,
                                 const float* c_prev, void* h_out, long long ldho, float* c_out, float* act, float* tc,
                                 const void* gy, long long ldgy, const float* gc_next, void* dg, long long lddg,
                                 float* dc_prev, float* s0, float* s1, float* s2, void* rh, long long ldrh,
                                 hipStream_t s) {
-  if (M <= 0 || K <= 0 || Hs <= 0 || Hs % 8 || K % 8 || cell < 0 || cell > 5) return (int)hipErrorInvalidValue;
-  if (a && (lda < K || lda % 8 || !a16(a))) return (int)hipErrorInvalidValue;
-  if (!u || !a16(u)) return (int)hipErrorInvalidValue;
-  static const int G[6] = {4, 1, 2, 1, 1, 1};
-  static const int KWANT[6] = {1, 4, 1, 1, 2, 1};  // K in units of Hs
-  if (K != KWANT[cell] * Hs) return (int)hipErrorInvalidValue;
-  const void* f32s[] = {c_prev, c_out, act, tc, gc_next, dc_prev, s0, s1, s2};
-  for (const void* q : f32s)
-    if (q && !a16(q)) return (int)hipErrorInvalidValue;
-  if (xg && (ldx % 4 || (x_f32 ? !a16(xg) : !a8(xg)))) return (int)hipErrorInvalidValue;
-  const void* b8s[] = {hprev, h_out, gy, dg, rh};
-  const long long lds_[] = {ldhp, ldho, ldgy, lddg, ldrh};
-  for (int i = 0; i < 5; ++i)
-    if (b8s[i] && (!a8(b8s[i]) || lds_[i] % 4)) return (int)hipErrorInvalidValue;
-  // per-cell required tensors
-  bool ok = true;
-  switch (cell) {
-    case 0: ok = xg && h_out; break;
-    case 1: ok = gy && act && tc && dg && dc_prev; break;
-    case 2: ok = xg && hprev && rh && s0 && s1; break;
-    case 3: ok = xg && hprev && s1 && h_out; break;
-    case 4: ok = gy && s0 && s1 && s2 && hprev && dg; break;
-    case 5: ok = a && s0 && s1 && hprev && dg; break;
-  }
-  if (!ok) return (int)hipErrorInvalidValue;
-  RnnStep p;
+  RnnStep p{};  // value-initialised: the second segment stays off
   p.a = (const bf16_t*)a; p.lda = lda; p.u = (const bf16_t*)u; p.M = M; p.K = K; p.Hs = Hs;
   p.xg = xg; p.ldx = ldx; p.x_f32 = x_f32; p.hprev = (const bf16_t*)hprev; p.ldhp = ldhp; p.c_prev = c_prev;
   p.h_out = (bf16_t*)h_out; p.ldho = ldho; p.c_out = c_out; p.act = act; p.tc = tc; p.gy = (const bf16_t*)gy;
   p.ldgy = ldgy; p.gc_next = gc_next; p.dg = (bf16_t*)dg; p.lddg = lddg; p.dc_prev = dc_prev; p.s0 = s0; p.s1 = s1;
   p.s2 = s2; p.rh = (bf16_t*)rh; p.ldrh = ldrh;
-  dim3 grid((unsigned)((Hs + 15) / 16), (unsigned)((M + 31) / 32)), block(64 * kStepWaves);
-  (void)G;
+  const int rc = rnn_step_check(cell, p);
+  if (rc) return rc;
+  const dim3 grid = rnn_step_grid(Hs, M), block(64 * kStepWaves);
   switch (cell) {
     case 0: hipLaunchKernelGGL((k_rnn_step<0, 4>), grid, block, 0, s, p); break;
     case 1: hipLaunchKernelGGL((k_rnn_step<1, 1>), grid, block, 0, s, p); break;
@@ -1447,6 +1493,117 @@ BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float*
     if (rc) return rc;
   }
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Two stacked LSTM layers on the layer wavefront (k_rnn_step_pair): layer 1's gates are
+// b1 + h0_t·W1ᵀ + h1_{t-1}·U1ᵀ, the input product folded into the recurrent step as a second
+// reduction segment, so layer 1 runs step t−1 in the same launch as layer 0's step t and the whole
+// two-layer sequence is T + 1 dependent launches (2T + an input-projection GEMM layer by layer).
+// Backward mirrors it: layer 0's dh_t = dg0_{t+1}·U0 + dg1_t·W1 in one step.  Layouts as the
+// single-layer launchers; b1 fp32 [4H1]; W1 [4H1][H0] (forward) / W1ᵀ [H0][4H1] (backward).
+// ------------------------------------------------------------------------------------------------
+static dim3 pair_grid(int H0, int H1, int B) {
+  const int hs = H0 > H1 ? H0 : H1;
+  return rnn_step_grid(hs, B, 2);
+}
+
+BIGDL_EXPORT int bigdl_lstm2_seq_fwd(const void* x2, int x_f32, const void* h00, const float* c00, const void* U0,
+                                     void* out0, float* cs0, float* acts0, float* tcs0, float* cbuf0, const float* b1,
+                                     const void* W1, const void* h01, const float* c01, const void* U1, void* out1,
+                                     float* cs1, float* acts1, float* tcs1, float* cbuf1, int B, int T, int H0,
+                                     int H1, hipStream_t s) {
+  if (B <= 0 || T <= 0 || H0 <= 0 || H1 <= 0 || !x2 || !h00 || !U0 || !out0 || !b1 || !W1 || !h01 || !U1 || !out1)
+    return (int)hipErrorInvalidValue;
+  const bool train = cs0 && acts0 && tcs0 && cs1 && acts1 && tcs1;
+  if (!train && (!cbuf0 || !cbuf1)) return (int)hipErrorInvalidValue;
+  const long long G0 = 4LL * H0, G1 = 4LL * H1, BH0 = (long long)B * H0, BH1 = (long long)B * H1;
+  const int esz = x_f32 ? 4 : 2;
+  const dim3 grid = pair_grid(H0, H1, B), block(64 * kStepWaves);
+  for (int w = 0; w <= T; ++w) {
+    RnnStep q0{}, q1{};
+    int live = 0;
+    if (w < T) {  // layer 0, step t = w (the single-layer step)
+      const int t = w;
+      q0.a = t == 0 ? (const bf16_t*)h00 : (const bf16_t*)out0 + (long long)(t - 1) * H0;
+      q0.lda = t == 0 ? H0 : (long long)T * H0;
+      q0.u = (const bf16_t*)U0; q0.M = B; q0.K = H0; q0.Hs = H0;
+      q0.xg = (const char*)x2 + (long long)t * G0 * esz; q0.ldx = (long long)T * G0; q0.x_f32 = x_f32;
+      q0.c_prev = t == 0 ? c00 : (train ? cs0 + (t - 1) * BH0 : cbuf0 + ((t - 1) & 1) * BH0);
+      q0.h_out = (bf16_t*)out0 + (long long)t * H0; q0.ldho = (long long)T * H0;
+      q0.c_out = train ? cs0 + t * BH0 : cbuf0 + (t & 1) * BH0;
+      q0.act = train ? acts0 + t * B * G0 : nullptr;
+      q0.tc = train ? tcs0 + t * BH0 : nullptr;
+      const int rc = rnn_step_check(0, q0);
+      if (rc) return rc;
+      live |= 1;
+    }
+    if (w >= 1) {  // layer 1, step t = w − 1: recurrent segment h1_{t-1}·U1ᵀ + input segment h0_t·W1ᵀ + b1
+      const int t = w - 1;
+      q1.a = t == 0 ? (const bf16_t*)h01 : (const bf16_t*)out1 + (long long)(t - 1) * H1;
+      q1.lda = t == 0 ? H1 : (long long)T * H1;
+      q1.u = (const bf16_t*)U1; q1.M = B; q1.K = H1; q1.Hs = H1;
+      q1.a2 = (const bf16_t*)out0 + (long long)t * H0; q1.lda2 = (long long)T * H0;
+      q1.u2 = (const bf16_t*)W1; q1.K2 = H0;
+      q1.xg = b1; q1.ldx = 0; q1.x_f32 = 1;  // the bias row, broadcast over the batch
+      q1.c_prev = t == 0 ? c01 : (train ? cs1 + (t - 1) * BH1 : cbuf1 + ((t - 1) & 1) * BH1);
+      q1.h_out = (bf16_t*)out1 + (long long)t * H1; q1.ldho = (long long)T * H1;
+      q1.c_out = train ? cs1 + t * BH1 : cbuf1 + (t & 1) * BH1;
+      q1.act = train ? acts1 + t * B * G1 : nullptr;
+      q1.tc = train ? tcs1 + t * BH1 : nullptr;
+      const int rc = rnn_step_check(0, q1);
+      if (rc) return rc;
+      live |= 2;
+    }
+    hipLaunchKernelGGL((k_rnn_step_pair<0, 4>), grid, block, 0, s, q0, q1, live);
+  }
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_lstm2_seq_bwd(const void* gy1, const void* U1t, const float* acts1, const float* tcs1,
+                                     const float* cs1, const float* c01, void* DG1, float* gc1, const void* U0t,
+                                     const void* W1t, const float* acts0, const float* tcs0, const float* cs0,
+                                     const float* c00, void* DG0, float* gc0, int B, int T, int H0, int H1,
+                                     hipStream_t s) {
+  if (B <= 0 || T <= 0 || H0 <= 0 || H1 <= 0 || !gy1 || !U1t || !DG1 || !gc1 || !U0t || !W1t || !DG0 || !gc0 ||
+      !acts1 || !tcs1 || !cs1 || !acts0 || !tcs0 || !cs0)
+    return (int)hipErrorInvalidValue;
+  const long long G0 = 4LL * H0, G1 = 4LL * H1, BH0 = (long long)B * H0, BH1 = (long long)B * H1;
+  const dim3 grid = pair_grid(H0, H1, B), block(64 * kStepWaves);
+  for (int w = 0; w <= T; ++w) {
+    RnnStep q0{}, q1{};
+    int live = 0;
+    const int t1 = T - 1 - w, t0 = T - w;
+    if (t1 >= 0) {  // layer 1, step t1 (the single-layer backward step)
+      const bool last = t1 + 1 == T;
+      q1.a = last ? nullptr : (const bf16_t*)DG1 + (t1 + 1) * G1; q1.lda = (long long)T * G1;
+      q1.u = (const bf16_t*)U1t; q1.M = B; q1.K = (int)G1; q1.Hs = H1;
+      q1.c_prev = t1 > 0 ? cs1 + (t1 - 1) * BH1 : c01;
+      q1.act = (float*)acts1 + t1 * B * G1; q1.tc = (float*)tcs1 + t1 * BH1;
+      q1.gy = (const bf16_t*)gy1 + (long long)t1 * H1; q1.ldgy = (long long)T * H1;
+      q1.gc_next = last ? nullptr : gc1;
+      q1.dg = (bf16_t*)DG1 + t1 * G1; q1.lddg = (long long)T * G1; q1.dc_prev = gc1;
+      const int rc = rnn_step_check(1, q1);
+      if (rc) return rc;
+      live |= 2;
+    }
+    if (t0 >= 0 && t0 < T) {  // layer 0, step t0: dh = dg0_{t0+1}·U0 + dg1_{t0}·W1 (no separate gy)
+      const bool last = t0 + 1 == T;
+      q0.a = last ? nullptr : (const bf16_t*)DG0 + (t0 + 1) * G0; q0.lda = (long long)T * G0;
+      q0.u = (const bf16_t*)U0t; q0.M = B; q0.K = (int)G0; q0.Hs = H0;
+      q0.a2 = (const bf16_t*)DG1 + t0 * G1; q0.lda2 = (long long)T * G1;
+      q0.u2 = (const bf16_t*)W1t; q0.K2 = (int)G1;
+      q0.c_prev = t0 > 0 ? cs0 + (t0 - 1) * BH0 : c00;
+      q0.act = (float*)acts0 + t0 * B * G0; q0.tc = (float*)tcs0 + t0 * BH0;
+      q0.gc_next = last ? nullptr : gc0;
+      q0.dg = (bf16_t*)DG0 + t0 * G0; q0.lddg = (long long)T * G0; q0.dc_prev = gc0;
+      const int rc = rnn_step_check(1, q0);
+      if (rc) return rc;
+      live |= 1;
+    }
+    hipLaunchKernelGGL((k_rnn_step_pair<1, 1>), grid, block, 0, s, q0, q1, live);
+  }
+  BIGDL_CHECK_LAUNCH();
 }
 
 // GRU: R, Z, Nn fp32 [S][B][H] and RH bf16 [B][S][H] with S = T (training) or 1 (inference: slot 0

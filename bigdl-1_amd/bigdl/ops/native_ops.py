@@ -2375,6 +2375,33 @@ def lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc):
           "lstm_seq_bwd")
 
 
+def lstm2_seq_forward(x2, h00, c00, U0, out0, cs0, acts0, tcs0, cbuf0, b1, W1, h01, c01, U1, out1, cs1, acts1,
+                      tcs1, cbuf1):
+    """Two stacked LSTM layers on the layer wavefront (bigdl_lstm2_seq_fwd): layer 1's input
+    projection h0·W1ᵀ + b1 is a second reduction segment of its recurrent step, so the pair runs in
+    T + 1 launches.  Layouts as :func:`lstm_seq_forward`; W1 [4H1][H0] bf16, b1 fp32 [4H1]."""
+    B, T, G0 = x2.shape
+    H0, H1 = G0 // 4, U1.shape[1]
+    assert _dense_bf16(x2, h00, c00, U0, out0, cs0, acts0, tcs0, cbuf0, b1, W1, h01, c01, U1, out1, cs1, acts1, tcs1,
+                       cbuf1) and tuple(out1.shape) == (B, T, H1) and tuple(W1.shape) == (4 * H1, H0), "lstm2_seq_forward"
+    check(_lib().bigdl_lstm2_seq_fwd(ptr(x2), C.c_int(1 if x2.dtype == _f32 else 0), ptr(h00), ptr(c00), ptr(U0),
+                                     ptr(out0), ptr(cs0), ptr(acts0), ptr(tcs0), ptr(cbuf0), ptr(b1), ptr(W1), ptr(h01),
+                                     ptr(c01), ptr(U1), ptr(out1), ptr(cs1), ptr(acts1), ptr(tcs1), ptr(cbuf1),
+                                     C.c_int(B), C.c_int(T), C.c_int(H0), C.c_int(H1), _s()), "lstm2_seq_fwd")
+
+
+def lstm2_seq_backward(gy1, U1t, acts1, tcs1, cs1, c01, DG1, gc1, U0t, W1t, acts0, tcs0, cs0, c00, DG0, gc0):
+    """Backward twin of :func:`lstm2_seq_forward` (bigdl_lstm2_seq_bwd): DG1 / DG0 [B][T][4H] gate
+    gradients of both layers; layer 0's dh = dg0·U0 + dg1·W1 inside its step (W1ᵀ [H0][4H1])."""
+    B, T, H1 = gy1.shape
+    H0 = U0t.shape[0]
+    assert _dense_bf16(gy1, U1t, acts1, tcs1, cs1, c01, DG1, gc1, U0t, W1t, acts0, tcs0, cs0, c00, DG0, gc0) \
+        and tuple(W1t.shape) == (H0, 4 * H1), "lstm2_seq_backward"
+    check(_lib().bigdl_lstm2_seq_bwd(ptr(gy1), ptr(U1t), ptr(acts1), ptr(tcs1), ptr(cs1), ptr(c01), ptr(DG1), ptr(gc1),
+                                     ptr(U0t), ptr(W1t), ptr(acts0), ptr(tcs0), ptr(cs0), ptr(c00), ptr(DG0), ptr(gc0),
+                                     C.c_int(B), C.c_int(T), C.c_int(H0), C.c_int(H1), _s()), "lstm2_seq_bwd")
+
+
 def gru_seq_forward(x2, h0, Urz, Uh, out, R, Z, Nn, RH, train):
     B, T, G = x2.shape
     H = G // 3

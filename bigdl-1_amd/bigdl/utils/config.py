@@ -78,6 +78,7 @@ _REGISTRY = {
     "bigdl.fusion.convbn": (bool, True, "fold BN into conv for inference"),
     "bigdl.fusion.bnrelu": (bool, True, "fuse BN + ReLU"),
     "bigdl.fusion.convrelu": (bool, True, "fuse conv + ReLU"),
+    "bigdl.fusion.lstmstack": (bool, True, "run two stacked Recurrent(LSTM) layers on the layer wavefront"),
     "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
     "bigdl.fusion.convstats": (bool, True, "conv epilogue emits the following training BN's statistics"),
     "bigdl.fusion.bnbwd": (bool, True, "dgrad epilogue applies the producing BN's ReLU mask and its backward reductions"),
