@@ -26,6 +26,14 @@ class Threshold(TensorModule):
     def updateOutput(self, input):
         if self._passthrough:
             return input
+        if input.dtype == torch.int8 and getattr(input, "_qscale", None) is not None:
+            # an int8 activation of a quantised chain (its producer usually applied this ReLU already)
+            if self.threshold == 0.0 and self.value == 0.0:
+                y = input if getattr(self, "_i8_fused", False) else input.clamp_min(0)
+                y._qscale = input._qscale
+                return y
+            from ..quantized.layers import dequant
+            input = dequant(input)
         # ``ip`` is a memory hint in the reference; out-of-place costs the same HBM traffic and
         # never aliases an activation a predecessor's backward still needs
         return ops.relu_forward(input, self.threshold, self.value, inplace=False)

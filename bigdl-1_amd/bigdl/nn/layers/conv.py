@@ -204,7 +204,7 @@ class SpatialConvolution(TensorModule):
         bn = self._stats_consumer(x) if batched else None
         y = NotImplemented
         if bn is not None and ops.native_has("conv2d_forward"):
-            shift = bn.runningMean if config.get_property("bigdl.bn.shiftedStats") else None
+            shift = bn._stat_shift() if config.get_property("bigdl.bn.shiftedStats") else None
             sums = bn._atomic_sums("fwd", self.nOutputPlane, x.device) if shift is not None else None
             r = ops.native_ops.conv2d_forward_stats(x, w4, b, (self.strideH, self.strideW), pad,
                                                 (self.dilationH, self.dilationW), self.nGroup,

@@ -162,6 +162,21 @@ class BatchNormalization(TensorModule):
         that reads it)."""
         return part is not None and any(part is self.__dict__.get(a) for a in ("_rep_fwd", "_rep_bwd"))
 
+    def _stat_shift(self, device=None):
+        """The K the shifted statistics Σ(x − K), Σ(x − K)² subtract (every producer of this BN's
+        sums — the conv epilogue, the stats pass — must use the same one).  Local BN: the running
+        mean.  SyncBN: the previous step's GLOBAL batch mean (identical on every rank), held in a
+        two-buffer ring — the one-launch finalize+apply then never writes what its blocks read, so
+        block 0 updates the running statistics up front (batchnorm.hip BnFwdFin::early)."""
+        if not self._sync_active():
+            return self.runningMean
+        kb = self.__dict__.get("_kbuf")
+        rm = self.runningMean
+        if kb is None or kb[0].shape != rm.shape or kb[0].device != rm.device:
+            kb = self.__dict__["_kbuf"] = [rm.detach().to(torch.float32).clone(), torch.empty_like(rm, dtype=torch.float32)]
+            self.__dict__["_kidx"] = 0
+        return kb[self.__dict__["_kidx"]]
+
     def _in_bias(self):
         p = self._bias_producer
         if p is None or not getattr(p, "withBias", False):
@@ -303,14 +318,17 @@ class BatchNormalization(TensorModule):
                 sums = m.bn_local_sums(x, shift, ps[2], ps[3], rezero=self._is_rep(ps[2]))
                 ps = None  # consumed
             else:
-                shift = self.runningMean
+                shift = self._stat_shift()
                 sums = m.bn_local_sums(x, shift)
             if sums is NotImplemented:
                 continue
             self._sync_allreduce(sums)  # the ONE collective of this call: a failed apply reuses its sums
+            kb = self.__dict__.get("_kbuf")
+            nxt = kb[1 - self.__dict__["_kidx"]] if (kb is not None and shift is kb[self.__dict__["_kidx"]]) else None
+            kw = dict(mean_out=nxt) if (m is not R and nxt is not None) else {}
             r = m.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar, self.momentum,
                                        self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef,
-                                       bits_out=bits if m is not R else None)
+                                       bits_out=bits if m is not R else None, **kw)
             if r is NotImplemented and m is not R:
                 m = R
                 r = R.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar,
@@ -320,6 +338,10 @@ class BatchNormalization(TensorModule):
                 self._relu_bits = bits if m is not R else None
                 self._sync_path = "native" if m is not R else "reference"
                 self._last_input = x
+                if nxt is not None:  # this step's global mean is the next step's shift
+                    if r[1] is not nxt:
+                        nxt.copy_(r[1])
+                    self.__dict__["_kidx"] ^= 1
                 break
         self._drop_sums(ps, 3)  # replicated statistics left by the conv and not read: clear them
         return r

@@ -67,7 +67,28 @@ class SpatialMaxPooling(TensorModule):
             y = y.permute(0, 2, 3, 1) if y.dim() == 4 else y.permute(1, 2, 0)
         return y
 
+    def _int8_forward(self, input):
+        """Max pooling of an int8 activation of a quantised chain (NHWC int8 kernel; the scale carries
+        over) — None when it does not apply."""
+        from ...ops import native_ops as NO
+        if not (input.is_cuda and input.dim() == 4 and self.format == "NCHW" and not self.train):
+            return None
+        pt, pb, pl, pr = _pool_pad(input, self.kH, self.kW, self.dH, self.dW, self.padH, self.padW)
+        if pt != pb or pl != pr:
+            return None
+        H, W = input.shape[2], input.shape[3]
+        P = NO._pool_out(H, self.kH, self.dH, pt, self.ceilMode)
+        Q = NO._pool_out(W, self.kW, self.dW, pl, self.ceilMode)
+        y = NO.maxpool_i8(input, self.kH, self.kW, self.dH, self.dW, pt, pl, P, Q)
+        return None if y is NotImplemented else y
+
     def updateOutput(self, input):
+        if input.dtype == torch.int8 and getattr(input, "_qscale", None) is not None:
+            y = self._int8_forward(input)
+            if y is not None:
+                return y
+            from ..quantized.layers import dequant
+            input = dequant(input)
         x, pad, batched, _ = self._prep(input)
         # evaluate mode: no argmax (no backward follows; updateGradInput recomputes it if one does)
         y, idx = ops.maxpool2d_forward(x, (self.kH, self.kW), (self.dH, self.dW), pad, self.ceilMode,

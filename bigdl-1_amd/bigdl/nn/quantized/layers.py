@@ -21,8 +21,32 @@ def _kp(k: int) -> int:
     return (k + 63) // 64 * 64
 
 
+def calibrated_scale(m):
+    """The static activation scale amax / 127 of a float module's calibrated input
+    (``calcScales`` records max|x| per calibration batch, mask 0 — one value per call; the largest is
+    kept, as ``MklInt8Convertible`` does), or None when the module was never calibrated."""
+    st = m.__dict__.get("_int8_state")
+    if not st or not st.get("in") or st.get("inMask", 0) != 0:
+        return None
+    amax = max(float(v[0]) for v in st["in"] if v)
+    return amax / 127.0 if amax > 0 else None
+
+
+def dequant(x):
+    """An int8 activation tagged ``_qscale`` back to bf16 (the layer after a chain end that cannot
+    consume int8)."""
+    return (x.float() * x._qscale).to(torch.bfloat16)
+
+
 class _QuantizedBase(TensorModule):
     SCALA_PACKAGE = "com.intel.analytics.bigdl.nn.quantized"
+    #: calibrated input scale (static quantisation; None = per-image dynamic scales)
+    static_scale = None
+    #: set by the quantizer when the next layer of the chain is a quantised conv with a static
+    #: scale: this layer writes int8 requantised with it ...
+    _out_qscale = None
+    #: ... and applies the ReLU that follows it in the epilogue
+    _relu_fused = False
 
     def _quantize_weight(self, w2d: torch.Tensor):
         q, s = ops.reference.quant_rows(w2d.detach().float().cpu())
@@ -66,6 +90,8 @@ class Linear(_QuantizedBase):
         return q.to(m.weight.device)
 
     def updateOutput(self, input):
+        if input.dtype == torch.int8:
+            input = dequant(input)
         x = input if input.dim() == 2 else input.reshape(1, -1)
         out_dt = x.dtype if x.is_floating_point() and x.dtype in (torch.float32, torch.bfloat16) else torch.float32
         y = self._gemm(x, out_dt)
@@ -99,8 +125,62 @@ class SpatialConvolution(_QuantizedBase):
         if m.withBias:
             q.qbias = m.bias.detach().float().clone().cpu()
         q.format = getattr(m, "format", "NCHW")
+        q.static_scale = calibrated_scale(m)
         q.set_name(m.get_name())
         return q.to(w.device)
+
+    def _i8_prep(self, x, C):
+        from ...ops import native_ops as NO
+        prep = getattr(self, "_i8w", None)
+        if prep is None or prep[0].device != x.device:
+            wq, ldw = NO.conv_i8_weight(self.qweight.to(x.device), self.nOutputPlane, C, self.kernelH, self.kernelW)
+            prep = self._i8w = (wq, ldw, self.weight_scale.to(x.device).float().contiguous(),
+                                self.bias_f.to(x.device).float().contiguous() if self.bias_f is not None else None)
+        return prep
+
+    def _out_hw(self, x, pads):
+        pt, pb, pl, pr = pads
+        H, W = x.shape[2], x.shape[3]
+        P = (H + pt + pb - self.dilationH * (self.kernelH - 1) - 1) // self.strideH + 1
+        Q = (W + pl + pr - self.dilationW * (self.kernelW - 1) - 1) // self.strideW + 1
+        return P, Q
+
+    def _native_static(self, x, pads):
+        """Calibrated int8 path: int8 (or statically quantised) input, int8 output for the next
+        quantised layer of the chain (bias + ReLU + requantisation in the epilogue) or bf16."""
+        from ...ops import native_ops as NO
+        pt, pb, pl, pr = pads
+        if not (x.is_cuda and self.nGroup == 1 and self.nOutputPlane % 8 == 0 and pt == pb and pl == pr
+                and ops.native_has("gemm_i8")):
+            return NotImplemented
+        if x.dtype != torch.int8 and self.static_scale is None:
+            return NotImplemented
+        C = x.shape[1]
+        if NO.conv_i8_supported(C, self.kernelH, self.kernelW):
+            prep = self._i8_prep(x, C)
+            xin = x if x.dtype == torch.int8 else x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            return NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane,
+                                               self.kernelH, self.kernelW, (self.strideH, self.strideW), (pt, pl),
+                                               (self.dilationH, self.dilationW), self._out_hw(x, pads),
+                                               relu=self._relu_fused, in_scale=self.static_scale,
+                                               out_scale=self._out_qscale)
+        if x.dtype == torch.int8:
+            return NotImplemented
+        # a shape the int8 kernel does not tile (the C = 3 RGB stem): bf16 conv with the dequantised
+        # int8 weights, then the static quantisation of its output for the chain
+        wf = getattr(self, "_wdeq", None)
+        if wf is None or wf.device != x.device:
+            kg = C * self.kernelH * self.kernelW
+            wf = (self.qweight[:, :kg].float() * self.weight_scale.float()[:, None]).reshape(
+                self.nOutputPlane, C, self.kernelH, self.kernelW).to(device=x.device, dtype=torch.bfloat16)
+            self._wdeq = wf
+        b = self.bias_f.to(x.device).float() if self.bias_f is not None else None
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = NO.conv2d_forward(xb, wf, b, (self.strideH, self.strideW), (pt, pl), (self.dilationH, self.dilationW), 1,
+                              relu=self._relu_fused)
+        if y is NotImplemented or self._out_qscale is None:
+            return y
+        return NO.quant_static(y, self._out_qscale)
 
     def _pads(self, x):
         from ..layers.conv import same_padding
@@ -135,10 +215,22 @@ class SpatialConvolution(_QuantizedBase):
         if getattr(self, "format", "NCHW") == "NHWC":
             x = x.permute(0, 3, 1, 2)
         pt, pb, pl, pr = self._pads(x)
+        y = self._native_static(x, (pt, pb, pl, pr))
+        if y is not NotImplemented:
+            if getattr(self, "format", "NCHW") == "NHWC":
+                q = getattr(y, "_qscale", None)
+                y = y.permute(0, 2, 3, 1)
+                if q is not None:
+                    y._qscale = q
+            return y if input.dim() == 4 else y.squeeze(0)
+        if x.dtype == torch.int8:
+            x = dequant(x)
         y = self._native_i8(x, (pt, pb, pl, pr))
         if y is not NotImplemented:
             if x.dtype == torch.float32:
                 y = y.float()
+            if self._relu_fused:
+                y = torch.relu(y)
             if getattr(self, "format", "NCHW") == "NHWC":
                 y = y.permute(0, 2, 3, 1)
             return y if input.dim() == 4 else y.squeeze(0)
@@ -171,6 +263,8 @@ class SpatialConvolution(_QuantizedBase):
             outs.append(y.reshape(N, P, Q, kg))
         y = torch.cat(outs, dim=3) if g > 1 else outs[0]
         y = y.permute(0, 3, 1, 2)  # NCHW logical, channels-last memory
+        if self._relu_fused:
+            y = torch.relu(y)
         if getattr(self, "format", "NCHW") == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y if input.dim() == 4 else y.squeeze(0)

@@ -44,11 +44,55 @@ def _convert(m):
     return m
 
 
+def _link_int8_chains(model):
+    """Quantised convs with calibrated scales that feed each other through ReLU / max pooling /
+    (evaluation) dropout only, inside a Sequential: the producer writes the consumer's int8 input
+    directly (requantised with the consumer's static scale, the ReLU fused into its epilogue), the
+    pooling runs on int8, and no bf16 activation or per-image scale pass sits between them — the
+    MKL-DNN int8 pipeline of ``MklInt8Convertible`` (scales from ``calcScales``)."""
+    from ..containers import Sequential
+    from ..layers.activation import Threshold
+    from ..layers.pooling import SpatialMaxPooling
+    from ..layers.dropout import Dropout
+    from ...ops import native_ops as NO
+    for s in model.flattened_modules():
+        if not isinstance(s, Sequential):
+            continue
+        mods = s.modules
+        for i, a in enumerate(mods):
+            if not (isinstance(a, Q.SpatialConvolution) and a.nGroup == 1 and a.nOutputPlane % 16 == 0):
+                continue
+            j, relu = i + 1, None
+            while j < len(mods) and isinstance(mods[j], (Threshold, SpatialMaxPooling, Dropout)):
+                m = mods[j]
+                if isinstance(m, Threshold):
+                    if not (m.threshold == 0.0 and m.value == 0.0):
+                        break
+                    if j == i + 1:
+                        relu = m
+                j += 1
+            if j >= len(mods) or not isinstance(mods[j], Q.SpatialConvolution):
+                continue
+            b = mods[j]
+            if b.static_scale is None or b.nGroup != 1 or not NO.conv_i8_supported(a.nOutputPlane, b.kernelH,
+                                                                                   b.kernelW):
+                continue
+            if any(isinstance(m, Threshold) and not (m.threshold == 0.0 and m.value == 0.0) for m in mods[i + 1:j]):
+                continue
+            a._out_qscale = b.static_scale
+            if relu is not None:
+                a._relu_fused = True
+                relu._i8_fused = True
+
+
 def quantize(model):
-    """Deep-copy ``model`` and return its int8 version (evaluation mode)."""
+    """Deep-copy ``model`` and return its int8 version (evaluation mode).  Layers calibrated with
+    ``calcScales`` quantise their input statically and chain int8 activations between quantised
+    convs (:func:`_link_int8_chains`); uncalibrated ones use per-image dynamic scales."""
     from ..fusion import unfuse
     clone = model.cloneModule()
     unfuse(clone)
     q = _convert(clone)
+    _link_int8_chains(q)
     q.evaluate()
     return q

@@ -696,6 +696,10 @@ struct BnFwdFin {
   const float* dM;
   unsigned* ticket;
   int keep;
+  // early = nothing the kernel's blocks read is written by it (kshift is not the running mean and
+  // the sums are kept): block 0 writes the saved statistics / coefficients / running statistics
+  // right after its prologue, and there is no last-block election at all
+  int early;
 };
 
 __device__ __forceinline__ void fin_fwd_coef(const BnFwdFin& f, int C, int c, float& mean, float& var, float& invstd,
@@ -749,6 +753,8 @@ __device__ __forceinline__ void rezero_sums(float* sums, int C) {
   if (threadIdx.x == 0) *reinterpret_cast<unsigned*>(sums + 2 * C) = 0u;
 }
 
+__device__ __forceinline__ void fin_fwd_side(const BnFwdFin& f, int C);
+
 template <bool RES, bool RELU, bool BITS>
 __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       bf16_t* __restrict__ y, long long M, int C, BnFwdFin f,
@@ -762,10 +768,22 @@ __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__
     fin_fwd_coef(f, C, c, mean, var, invstd, cf[c], cf[C + c]);
   }
   __syncthreads();
+  if (f.early) {
+    if (blockIdx.x == 0) fin_fwd_side(f, C);
+    bn_apply_rows<RES, RELU, BITS, 4>(x, res, y, M, C, cf, cf + C, bits);
+    return;
+  }
   bn_apply_rows<RES, RELU, BITS, 4>(x, res, y, M, C, cf, cf + C, bits);
   if (!(f.ticket ? last_arriver_tree(f.ticket) : last_arriver(reinterpret_cast<unsigned*>(f.sums + 2 * C)))) return;
+  fin_fwd_side(f, C);
+  __syncthreads();  // every coefficient is computed before the sums are cleared
+  if (!f.keep) rezero_sums(f.sums, C);
+}
+
+// The saved statistics, the coefficient vectors and the running-statistics update (one block).
+__device__ __forceinline__ void fin_fwd_side(const BnFwdFin& f, int C) {
   const double Mg = f.dM ? (double)*f.dM : f.M;
-  for (int c = t; c < C; c += blockDim.x) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean, var, invstd, sc, sh;
     fin_fwd_coef(f, C, c, mean, var, invstd, sc, sh);
     f.save_mean[c] = mean;
@@ -779,8 +797,6 @@ __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__
       f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * unb;
     }
   }
-  __syncthreads();  // every coefficient is computed before the sums are cleared
-  if (!f.keep) rezero_sums(f.sums, C);
 }
 
 // Training BN forward from atomically accumulated conv-epilogue statistics: ONE launch (see above).
@@ -832,6 +848,7 @@ struct BnBwdFin {
   const float* dM;
   unsigned* ticket;
   int keep;
+  int early;  // as BnFwdFin: block 0 writes the side results after its prologue, no election
 };
 
 __device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, float& a, float& dg, float& A, float& B,
@@ -846,6 +863,8 @@ __device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, fl
   Cc = -gm * is * a / Mg - B * f.mean[c];
 }
 
+__device__ __forceinline__ void fin_bwd_side(const BnBwdFin& f, int C);
+
 __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restrict__ gy, const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ gx, long long M, int C, BnBwdFin f) {
   // coefficients once per block into LDS ([3][C], dynamic), then the k_bn_bwd_apply stream
@@ -857,11 +876,23 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restri
       fin_bwd_coef(f, C, c, a, dg, cf[c], cf[C + c], cf[2 * C + c]);
     }
     __syncthreads();
-    bn_bwd_apply_rows<false, false, 4>(gy, x, nullptr, gx, nullptr, M, C, cf);
   }
+  if (f.early) {
+    if (blockIdx.x == 0) fin_bwd_side(f, C);
+    if (gx) bn_bwd_apply_rows<false, false, 4>(gy, x, nullptr, gx, nullptr, M, C, cf);
+    return;
+  }
+  if (gx) bn_bwd_apply_rows<false, false, 4>(gy, x, nullptr, gx, nullptr, M, C, cf);
   if (!(f.ticket ? last_arriver_tree(f.ticket) : last_arriver(reinterpret_cast<unsigned*>(f.sums + 2 * C)))) return;
+  fin_bwd_side(f, C);
+  __syncthreads();
+  if (!f.keep) rezero_sums(f.sums, C);
+}
+
+// dγ / dβ, the folded producer bias's gradient and the coefficient vectors (one block).
+__device__ __forceinline__ void fin_bwd_side(const BnBwdFin& f, int C) {
   const float Ml = f.lsums ? f.Ml : (f.dM ? *f.dM : f.M);
-  for (int c = t; c < C; c += blockDim.x) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float a, dg, A, B, Cc;
     fin_bwd_coef(f, C, c, a, dg, A, B, Cc);
     if (f.lsums) {  // this rank's share: dγ, dβ (and the bias) over its own rows
@@ -877,8 +908,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restri
       f.coef[2 * C + c] = Cc;
     }
   }
-  __syncthreads();
-  if (!f.keep) rezero_sums(f.sums, C);
 }
 
 BIGDL_EXPORT int bigdl_bn_bwd_sums_apply(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
@@ -972,7 +1001,8 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
     // ONE launch: every block derives its channels' coefficients from the global sums, the last
     // arriver writes the saved statistics / coefficients / running statistics (k_bn_apply_fin)
     BnFwdFin f{const_cast<float*>(sums), kshift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef,
-               (double)count, momentum, eps, count == 0 ? sums + 2 * C : nullptr, ticket, 1};
+               (double)count, momentum, eps, count == 0 ? sums + 2 * C : nullptr, ticket, 1,
+               (kshift != run_mean && kshift != save_mean) ? 1 : 0};
     const int grid = apply_grid(M, C);
     const bf16_t* xr = (const bf16_t*)x;
     const bf16_t* rr = (const bf16_t*)res;
@@ -1038,7 +1068,7 @@ BIGDL_EXPORT int bigdl_bn_bwd_apply_sums(const void* gy, const void* x, const vo
     // ONE launch (k_bn_bwd_apply_fin): coefficients from the global sums in every block, this rank's
     // dγ / dβ / folded-bias share from its local sums in the last arriver
     BnBwdFin f{const_cast<float*>(global_sums), gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, nullptr,
-               (float)count, local_sums, (float)M, dM, ticket, 1};
+               (float)count, local_sums, (float)M, dM, ticket, 1, 1};
     const int grid = gx ? apply_grid(M, C) : 1;
     hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), gx ? 12 * C : 0, s, (const bf16_t*)gy,
                        (const bf16_t*)x, (bf16_t*)gx, M, C, f);

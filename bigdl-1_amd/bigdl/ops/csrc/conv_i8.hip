@@ -40,12 +40,15 @@ __device__ __forceinline__ void i8_glds16(__amdgpu_buffer_rsrc_t r, void* lds, u
 struct ConvI8Params {
   const int8_t* x;    // [Nb][H][W][C]
   const int8_t* w;    // [K][ldw]
-  const float* sx;    // [Nb]
+  const float* sx;    // [Nb] per-image activation scales, or null: the static scale sxs
   const float* swt;   // [K]
   const float* bias;  // [K] or null
-  bf16_t* y;          // [M][ldy]
+  bf16_t* y;          // [M][ldy] (bf16 output), or null when yq is set
   int Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw;
   int M, KT, ldw, ldy, relu, tiles_n;
+  float sxs;          // static (calibrated) activation scale
+  int8_t* yq;         // int8 output [M][ldy] requantised with 1 / out_scale (the next layer's input)
+  float out_inv;
 };
 
 template <int BM, int BN, int WM, int WN, int TPT>
@@ -240,7 +243,52 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
 #pragma unroll
   for (int j = 0; j < TMI; ++j) {
     const int m = m0 + (b_row0 - BN) + 32 * j + pm;
-    sxm[j] = m < p.M ? p.sx[m / (p.P * p.Q)] : 0.f;
+    sxm[j] = m < p.M ? (p.sx ? p.sx[m / (p.P * p.Q)] : p.sxs) : 0.f;
+  }
+  if (p.yq) {
+    // int8 output: requantise with the consumer's static scale and park the tile as bytes
+    // ([BM][BN], 16-B chunk c of row r at chunk c ^ (r & 7)), then one 16-B store per chunk
+    int8_t* eq = reinterpret_cast<int8_t*>(lds);
+#pragma unroll
+    for (int i = 0; i < TNI; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
+        float s4[4], b4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + nl + e;
+          s4[e] = n < p.K ? p.swt[n] : 0.f;
+          b4[e] = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) {
+          const int ml = (b_row0 - BN) + 32 * j + pm;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+            if (p.relu) v = fmaxf(v, 0.f);
+            const float r = fminf(fmaxf(rintf(v * p.out_inv), -127.f), 127.f);
+            packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+          }
+          const int off = ml * BN + ((((nl >> 4) ^ (ml & 7)) & (BN / 16 - 1)) << 4) + (nl & 15);
+          *reinterpret_cast<uint32_t*>(eq + off) = packed;
+        }
+      }
+    __syncthreads();
+    constexpr int CPR = BN / 16;  // 16-B chunks per tile row
+#pragma unroll
+    for (int it = 0; it < BM * CPR / NT; ++it) {
+      const int idx = tid + NT * it;
+      const int row = idx / CPR, ch = idx - row * CPR;
+      const int m = m0 + row, n = n0 + ch * 16;
+      if (m < p.M && n < p.K) {
+        const uint4 v = *reinterpret_cast<const uint4*>(eq + row * BN + (((ch ^ (row & 7)) & (CPR - 1)) << 4));
+        *reinterpret_cast<uint4*>(p.yq + (size_t)m * p.ldy + n) = v;
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < TNI; ++i)
@@ -330,6 +378,99 @@ __global__ void __launch_bounds__(256) k_quant_img(const bf16_t* __restrict__ x,
   }
 }
 
+// Static (calibrated) quantisation: xq = clamp(rint(x / scale), ±127), 16 elements per thread.
+template <typename T>
+__global__ void __launch_bounds__(256) k_quant_static(const T* __restrict__ x, long long n, float inv,
+                                                      int8_t* __restrict__ xq) {
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 16; i < n; i += (long long)gridDim.x * 256 * 16) {
+    float v[16];
+    if constexpr (sizeof(T) == 2) {
+      load8(x + i, v);
+      load8(x + i + 8, v + 8);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 f = *reinterpret_cast<const float4*>(x + i + 4 * q);
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+      }
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float r = fminf(fmaxf(rintf(v[4 * k + e] * inv), -127.f), 127.f);
+        acc |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+      }
+      w[k] = acc;
+    }
+    *reinterpret_cast<uint4*>(xq + i) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// dtype 0 = fp32, 1 = bf16; n % 16 == 0, 16-B aligned
+BIGDL_EXPORT int bigdl_quant_static(const void* x, int dtype, long long n, float scale, void* xq, hipStream_t s) {
+  if (!x || !xq || n <= 0 || n % 16 || !(scale > 0.f) || ((uintptr_t)x & 15) || ((uintptr_t)xq & 15))
+    return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)bigdl_grid((n + 15) / 16, 256, 16384));
+  if (dtype == 0) hipLaunchKernelGGL(k_quant_static<float>, g, dim3(256), 0, s, (const float*)x, n, 1.f / scale, (int8_t*)xq);
+  else hipLaunchKernelGGL(k_quant_static<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, n, 1.f / scale, (int8_t*)xq);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// int8 NHWC max pooling (the int8 activation between quantised convs: max commutes with the
+// monotone quantisation, so the scale carries over).  16 channels per thread (C % 16); window
+// positions outside the input are skipped; P, Q given (ceil / floor mode decided by the caller).
+__global__ void __launch_bounds__(256) k_maxpool_i8(const int8_t* __restrict__ x, int8_t* __restrict__ y, int Nb,
+                                                    int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
+                                                    int ph, int pw) {
+  const int CG = C >> 4;
+  const long long total = (long long)Nb * P * Q * CG;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int cg = (int)(t % CG);
+    const long long pix = t / CG;
+    const int q = (int)(pix % Q);
+    const long long r = pix / Q;
+    const int pp = (int)(r % P);
+    const int n = (int)(r / P);
+    int m[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) m[e] = -128;
+    const int h0 = pp * sh - ph, w0 = q * sw - pw;
+    for (int i = 0; i < kh; ++i) {
+      const int h = h0 + i;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int j = 0; j < kw; ++j) {
+        const int w = w0 + j;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (((long long)n * H + h) * W + w) * C + cg * 16);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int b = (int)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+          m[e] = m[e] > b ? m[e] : b;
+        }
+      }
+    }
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[e >> 2] |= ((uint32_t)m[e] & 0xFFu) << (8 * (e & 3));
+    *reinterpret_cast<uint4*>(y + pix * C + cg * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+BIGDL_EXPORT int bigdl_maxpool_i8(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
+                                  int sh, int sw, int ph, int pw, hipStream_t s) {
+  if (!x || !y || Nb <= 0 || C % 16 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 ||
+      ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return (int)hipErrorInvalidValue;
+  const long long total = (long long)Nb * P * Q * (C / 16);
+  hipLaunchKernelGGL(k_maxpool_i8, dim3((unsigned)bigdl_grid(total, 256, 65536)), dim3(256), 0, s, (const int8_t*)x,
+                     (int8_t*)y, Nb, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // x: [Nb][per_img] bf16 (per_img % 16 == 0, 16-B aligned) → xq int8 (same layout) and sx[Nb] (the
 // dequantisation scale of each image); amax: [Nb] fp32 workspace.
 BIGDL_EXPORT int bigdl_quant_img(const void* x, int Nb, long long per_img, float* amax, void* xq, float* sx,
@@ -351,11 +492,29 @@ BIGDL_EXPORT int bigdl_quant_img(const void* x, int Nb, long long per_img, float
 // y[m][n] (bf16, row stride ldy) = [ReLU](Σ_k w[n][k]·x̂[m][k] · sx[img(m)] · sw[n] + bias[n]).
 // x: int8 NHWC [Nb][H][W][C] (C % 128 == 0 or C == 64); w: int8 [K][ldw], (r, s, c) order zero-padded
 // to ldw = KT·128 (KT = R·S·C / 128, or ⌈R·S / 2⌉ for C == 64); R·S ≤ 64; K % 8 == 0.
+// sx null: one static activation scale sxs for every image (calibrated, nn/quantized); yq non-null:
+// int8 output requantised by 1 / out_scale (K % 16, ldy % 16, 16-B aligned) instead of bf16 y.
+BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, hipStream_t s);
+
 BIGDL_EXPORT int bigdl_conv_i8_fwd(const void* x, const void* w, int ldw, const float* sx, const float* swt,
                                    const float* bias, void* y, int ldy, int Nb, int H, int W, int C, int K, int R,
                                    int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int relu,
                                    hipStream_t s) {
-  if (!x || !w || !sx || !swt || !y || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0) return (int)hipErrorInvalidValue;
+  if (!sx) return (int)hipErrorInvalidValue;
+  return bigdl_conv_i8_fwd2(x, w, ldw, sx, 0.f, swt, bias, y, nullptr, 1.f, ldy, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph,
+                            pw, dh, dw, relu, s);
+}
+
+BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, hipStream_t s) {
+  if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)
+    return (int)hipErrorInvalidValue;
+  if (yq && (K % 16 || ldy % 16 || ((uintptr_t)yq & 15) || !(out_scale > 0.f))) return (int)hipErrorInvalidValue;
   const int tpt = C == 64 ? 2 : (C % 128 == 0 ? 1 : 0);
   if (!tpt || R * S > 64 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
   const int KT = tpt == 2 ? (R * S + 1) / 2 : R * S * C / 128;
@@ -369,6 +528,7 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd(const void* x, const void* w, int ldw, const 
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
   p.M = (int)Ml; p.KT = KT; p.ldw = ldw; p.ldy = ldy; p.relu = relu;
+  p.sxs = sxs; p.yq = (int8_t*)yq; p.out_inv = yq ? 1.f / out_scale : 1.f;
   constexpr int BM = 256, BN = 128;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;

@@ -330,7 +330,7 @@ def _ticket(dev):
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
-                         residual=None, in_bias=None, coef_out=None, bits_out=None):
+                         residual=None, in_bias=None, coef_out=None, bits_out=None, mean_out=None):
     """Training BN from GLOBAL shifted sums over ``count`` rows (0: the all-reduced count at
     ``sums[2C]``): (y, save_mean, save_invstd).  ``bits_out`` (uint8 [M·C/8], with ``relu``): the
     output's ReLU mask as bits for a block-tail consumer's dgrad epilogue."""
@@ -344,7 +344,7 @@ def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, runni
                                  residual.dtype != _bf16 or not _al16(residual)):
         return NotImplemented
     coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
-    mean = torch.empty(C_, dtype=_f32, device=x.device)
+    mean = mean_out if _f32vec(mean_out, C_) and mean_out is not None else torch.empty(C_, dtype=_f32, device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
     check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
@@ -1727,6 +1727,71 @@ def conv2d_i8_forward(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation,
     check(_lib().bigdl_conv_i8_fwd(ptr(xq), ptr(wq), C.c_int(ldw), ptr(sx), ptr(w_scale), ptr(b), ptr(y), C.c_int(K),
                                    N_, H, W, C_, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0],
                                    dilation[1], C.c_int(1 if relu else 0), _s()), "conv_i8_fwd")
+    return y
+
+
+def quant_static(x, scale):
+    """Calibrated (static) int8 quantisation of a channels-last fp32 / bf16 activation with one
+    scale: int8 tensor of the same logical shape and memory layout, tagged ``_qscale``."""
+    if not (x.is_cuda and x.dtype in (_f32, _bf16) and x.numel() % 16 == 0 and _al16(x)):
+        return NotImplemented
+    cl = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+    if not (cl or x.is_contiguous()):
+        return NotImplemented
+    xq = torch.empty_like(x, dtype=torch.int8)
+    check(_lib().bigdl_quant_static(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), _ll(x.numel()), C.c_float(scale),
+                                    ptr(xq), _s()), "quant_static")
+    xq._qscale = float(scale)
+    return xq
+
+
+def maxpool_i8(x, kh, kw, sh, sw, ph, pw, P, Q):
+    """Max pooling of an int8 NHWC activation (the scale carries over: max commutes with the
+    monotone quantisation).  Returns the pooled int8 tensor tagged with the input's ``_qscale``."""
+    if not (x.is_cuda and x.dtype == torch.int8 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1] % 16 == 0 and _al16(x)):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    y = torch.empty((N_, C_, P, Q), dtype=torch.int8, device=x.device, memory_format=torch.channels_last)
+    check(_lib().bigdl_maxpool_i8(ptr(x), ptr(y), N_, H, W, C_, P, Q, kh, kw, sh, sw, ph, pw, _s()), "maxpool_i8")
+    y._qscale = getattr(x, "_qscale", None)
+    return y
+
+
+def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation, out_hw, relu=False,
+                             in_scale=None, out_scale=None):
+    """int8 conv with calibrated scales: ``x`` int8 NHWC (tagged ``_qscale``, the producer's
+    requantised output) or fp32/bf16 quantised here with ``in_scale`` in one static pass; with
+    ``out_scale`` the epilogue writes the int8 NHWC input of the next quantised layer (bias, ReLU
+    and requantisation fused), else bf16.  NotImplemented when the kernel does not apply."""
+    if not (x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    if not conv_i8_supported(C_, R, S) or K % 8 or (out_scale is not None and K % 16):
+        return NotImplemented
+    if x.dtype == torch.int8:
+        sx = getattr(x, "_qscale", None)
+        if sx is None:
+            return NotImplemented
+        xq = x
+    else:
+        if in_scale is None:
+            return NotImplemented
+        xq = quant_static(x, in_scale)
+        if xq is NotImplemented:
+            return NotImplemented
+        sx = in_scale
+    P, Q = out_hw
+    odt = torch.int8 if out_scale is not None else _bf16
+    y = torch.empty((N_, K, P, Q), dtype=odt, device=x.device, memory_format=torch.channels_last)
+    b = bias.float().contiguous() if bias is not None else None
+    check(_lib().bigdl_conv_i8_fwd2(ptr(xq), ptr(wq), C.c_int(ldw), None, C.c_float(sx), ptr(w_scale), ptr(b),
+                                    None if out_scale is not None else ptr(y), ptr(y) if out_scale is not None else None,
+                                    C.c_float(out_scale if out_scale is not None else 1.0), C.c_int(K), N_, H, W, C_, K,
+                                    R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
+                                    C.c_int(1 if relu else 0), _s()), "conv_i8_fwd2")
+    if out_scale is not None:
+        y._qscale = float(out_scale)
     return y
 
 

@@ -413,7 +413,23 @@ def bench_int8(args):
         config.set_property("bigdl.compute.dtype", "fp32" if mode == "fp32" else "bf16")
         Engine.init()
         dev = Engine.device()
-        m = base.quantize() if mode == "int8" else base.cloneModule()
+        if mode == "int8" and args.calib > 0:
+            # calibration (MklInt8Convertible.calcScales): a forward of CALIB images that are not the
+            # timed batch records every layer's max|input|; quantize() then runs static int8 chains
+            cal = base.cloneModule().to(dev)
+            cal.evaluate()
+            gc = torch.Generator().manual_seed(5)
+            xc = torch.randn(args.calib, 3, 224, 224, generator=gc).to(dev).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+            with torch.no_grad():
+                cal.forward(xc)
+            cal.calcScales(xc)
+            m = cal.quantize()
+            del cal
+        elif mode == "int8":
+            m = base.quantize()
+        else:
+            m = base.cloneModule()
         m.evaluate()
         m = m.to(dev)
         dt = torch.float32 if mode == "fp32" else torch.bfloat16
@@ -446,7 +462,7 @@ def bench_int8(args):
             "fp32": res["fp32"], "bf16": res["bf16"],
             "int8_over_fp32": round(res["int8"]["value"] / res["fp32"]["value"], 3),
             "int8_over_bf16": round(res["int8"]["value"] / res["bf16"]["value"], 3),
-            "reference_int8_over_fp32": 2.04, "cosine_int8_vs_fp32": round(cos, 5),
+            "reference_int8_over_fp32": 2.04, "cosine_int8_vs_fp32": round(cos, 5), "calibration_images": args.calib,
             "cosine_image_dependent": round(cos_img, 5), "top1_agreement": top1,
             "logit_spread_fp32": round(float(cf.std()), 5)}
 
@@ -463,6 +479,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="0 = the config's reference default")
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
+    ap.add_argument("--calib", type=int, default=32, help="int8: calibration images (0 = per-image dynamic scales)")
     ap.add_argument("--tune", action="store_true", help="vgg: pin autotuned conv tiles before timing")
     ap.add_argument("--compiled", action="store_true", help="inception: run through nn.compiled (kernel selection + HIP graph)")
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
