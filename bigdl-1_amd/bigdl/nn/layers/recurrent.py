@@ -166,6 +166,14 @@ def _acc_recurrent_grad(m, DG, h0, out, U):
     _fire_grad_ready([m])
 
 
+def _fused_rnn32_ok(H, *ts) -> bool:
+    """fp32 device recurrence on the bf16x3 fused step (rnn_step.hip k_rnn_step<…, F32>)."""
+    if not all(isinstance(t, torch.Tensor) for t in ts) or not ts[0].is_cuda:
+        return False
+    from ...ops import native_ops as NO
+    return NO.rnn_fast32_ok(H, *ts)
+
+
 def _fused_rnn_ok(H, *ts) -> bool:
     """Fused MFMA recurrent step applies: bf16 device rows, H % 8 == 0, native library loaded."""
     if not all(isinstance(t, torch.Tensor) for t in ts) or not ts[0].is_cuda:
@@ -802,7 +810,8 @@ class Recurrent(Container):
             return False
         if not (_is_default(c.activation, Tanh) and _is_default(c.innerActivation, Sigmoid)):
             return False
-        return _fused_rnn_ok(c.outputSize, x2, c.h2g[0].cw("weight"), c.u_h.cw("weight"))
+        w1, w2 = c.h2g[0].cw("weight"), c.u_h.cw("weight")
+        return _fused_rnn_ok(c.outputSize, x2, w1, w2) or _fused_rnn32_ok(c.outputSize, x2, w1, w2)
 
     # -- stacked-LSTM fusion (bigdl.nn.fusion ``lstmstack``) ----------------------------------
     #: lower layer: the next Recurrent(LSTM) whose only input is this layer's output; upper layer:
@@ -875,6 +884,17 @@ class Recurrent(Container):
             cbuf = None if train else torch.empty(2, B, H, device=x2.device, dtype=_state_dt(x2.dtype))
             NO.lstm_seq_forward(x2, h0, c0, U, out, cs if train else None, acts if train else None,
                                 tcs if train else None, cbuf)
+            h = out[:, Tn - 1]
+            c = cs[Tn - 1] if train else cbuf[(Tn - 1) % 2]
+        elif _fused_rnn32_ok(H, x2, U):
+            # fp32: the same one-launch-per-step loop with bf16x3 recurrent products
+            from ...ops import native_ops as NO
+            x2 = x2.contiguous()
+            h0 = h0.contiguous()
+            c0 = c0.contiguous()
+            cbuf = None if train else torch.empty(2, B, H, device=x2.device, dtype=torch.float32)
+            NO.lstm_seq_forward32(x2, h0, c0, U.contiguous(), out, cs if train else None, acts if train else None,
+                                  tcs if train else None, cbuf)
             h = out[:, Tn - 1]
             c = cs[Tn - 1] if train else cbuf[(Tn - 1) % 2]
         else:
@@ -955,7 +975,10 @@ class Recurrent(Container):
         Z = torch.empty(nS, B, H, device=dev, dtype=torch.float32)
         Nn = torch.empty(nS, B, H, device=dev, dtype=torch.float32) if train else None
         RH = torch.empty(B, Tn if train else 1, H, device=dev, dtype=x2.dtype)
-        NO.gru_seq_forward(x2.contiguous(), h0, Urz, Uh, out, R, Z, Nn, RH, train)
+        if x2.dtype == torch.float32:
+            NO.gru_seq_forward32(x2.contiguous(), h0, Urz.contiguous(), Uh.contiguous(), out, R, Z, Nn, RH, train)
+        else:
+            NO.gru_seq_forward(x2.contiguous(), h0, Urz, Uh, out, R, Z, Nn, RH, train)
         self._last_hidden = out[:, Tn - 1]
         self._rec = ("gru", h0, out, R, Z, Nn, RH) if train else None
         return out
@@ -1039,6 +1062,12 @@ class Recurrent(Container):
             gc = torch.empty(B, H, device=out.device, dtype=_state_dt(out.dtype))
             NO.lstm_seq_backward(gy, Ut, acts, tcs, cs, c0, DG, gc)
             gh_rec = NO.gemm(DG[:, 0], Ut)
+        elif _fused_rnn32_ok(H, out, U, gy):
+            from ...ops import native_ops as NO
+            Ut = U.t().contiguous()  # (H, 4H) fp32
+            gc = torch.empty(B, H, device=out.device, dtype=torch.float32)
+            NO.lstm_seq_backward32(gy, Ut, acts, tcs, cs, c0.contiguous(), DG, gc)
+            gh_rec = DG[:, 0] @ U  # the initial hidden state's gradient (one product per sequence)
         else:
             gh_rec, gc = None, None
             for t in range(Tn - 1, -1, -1):
@@ -1091,11 +1120,16 @@ class Recurrent(Container):
         if not gy.is_contiguous():
             gy = gy.contiguous()
         dev = out.device
-        Urz_t, Uh_t = NO.transpose_bf16(Urz), NO.transpose_bf16(Uh)  # (H, 2H), (H, H)
         DG = torch.empty(B, Tn, 3 * H, device=dev, dtype=out.dtype)  # (da_r, da_z, da_n) per step
         carry = torch.zeros(B, H, device=dev, dtype=torch.float32)
-        NO.gru_seq_backward(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry)
-        NO.gemm(DG[:, 0, :2 * H], Urz_t, out=carry, beta=1.0)  # dh0 = carry + da_rz_0 · U_rz
+        if out.dtype == torch.float32:
+            Urz_t, Uh_t = Urz.t().contiguous(), Uh.t().contiguous()
+            NO.gru_seq_backward32(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry)
+            carry.add_(DG[:, 0, :2 * H] @ Urz)  # dh0 = carry + da_rz_0 · U_rz
+        else:
+            Urz_t, Uh_t = NO.transpose_bf16(Urz), NO.transpose_bf16(Uh)  # (H, 2H), (H, H)
+            NO.gru_seq_backward(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry)
+            NO.gemm(DG[:, 0, :2 * H], Urz_t, out=carry, beta=1.0)  # dh0 = carry + da_rz_0 · U_rz
         self._grad_hidden_state = [carry]
         hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1) if Tn > 1 else h0.unsqueeze(1)
         if urz.scale_w != 0:

@@ -57,6 +57,10 @@ struct RnnStep {
   long long lda2;
   const bf16_t* u2;     // [G·Hs][K2]
   int K2;
+  // fp32 recurrence (k_rnn_step<…, F32 = true>): every pointer typed bf16_t above (a, a2, u, u2,
+  // hprev, h_out, gy, dg, rh) holds fp32 instead, and the products run as bf16x3 on the matrix
+  // cores (hi·hi + lo·hi + hi·lo, hi = rne(v), lo = rne(v − hi)) — fp32-accurate recurrent GEMMs
+  int f32;
 };
 
 __device__ __forceinline__ float sgm(float x) { return 1.f / (1.f + __expf(-x)); }
@@ -85,6 +89,12 @@ __device__ __forceinline__ void stb4(bf16_t* p, const float* v) {
   *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
 }
+// a quad of the activation element type (bf16, or fp32 when F32) at element offset `off`
+template <bool F32>
+__device__ __forceinline__ void st4(bf16_t* base, long long off, const float* v) {
+  if constexpr (F32) stf4(reinterpret_cast<float*>(base) + off, v);
+  else stb4(base + off, v);
+}
 
 // number of fp32 quads of per-(row, unit) epilogue operands each cell reads
 template <int CELL> struct NPre;
@@ -97,7 +107,7 @@ template <> struct NPre<5> { static constexpr int v = 3; };  // carry, r, h_prev
 
 // The epilogue's operands are fetched by wave 0 BEFORE the reduction loop so their memory latency
 // overlaps the MFMA chain instead of following it (the step kernels are latency-bound).
-template <int CELL>
+template <int CELL, bool F32>
 __device__ __forceinline__ void pre_load(const RnnStep& p, int m, int j, float (&v)[NPre<CELL>::v][4]) {
   const int H = p.Hs;
   const long long mh = (long long)m * H + j;
@@ -106,7 +116,7 @@ __device__ __forceinline__ void pre_load(const RnnStep& p, int m, int j, float (
     for (int g = 0; g < 4; ++g) ld4(p.xg, p.x_f32, (long long)m * p.ldx + g * H + j, v[g]);
     ldf4(p.c_prev ? p.c_prev + mh : nullptr, v[4]);
   } else if constexpr (CELL == 1) {
-    if (p.gy) ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    if (p.gy) ld4(p.gy, F32, (long long)m * p.ldgy + j, v[0]);
     else v[0][0] = v[0][1] = v[0][2] = v[0][3] = 0.f;
     const float* a = p.act + (long long)m * 4 * H + j;
 #pragma unroll
@@ -117,25 +127,25 @@ __device__ __forceinline__ void pre_load(const RnnStep& p, int m, int j, float (
   } else if constexpr (CELL == 2) {
     ld4(p.xg, p.x_f32, (long long)m * p.ldx + j, v[0]);
     ld4(p.xg, p.x_f32, (long long)m * p.ldx + H + j, v[1]);
-    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[2]);
+    ld4(p.hprev, F32, (long long)m * p.ldhp + j, v[2]);
   } else if constexpr (CELL == 3) {
     ld4(p.xg, p.x_f32, (long long)m * p.ldx + 2 * H + j, v[0]);
-    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[1]);
+    ld4(p.hprev, F32, (long long)m * p.ldhp + j, v[1]);
     ldf4(p.s1 + mh, v[2]);
   } else if constexpr (CELL == 4) {
-    ld4(p.gy, 0, (long long)m * p.ldgy + j, v[0]);
+    ld4(p.gy, F32, (long long)m * p.ldgy + j, v[0]);
     ldf4(p.s0 + mh, v[1]);
     ldf4(p.s1 + mh, v[2]);
     ldf4(p.s2 + mh, v[3]);
-    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[4]);
+    ld4(p.hprev, F32, (long long)m * p.ldhp + j, v[4]);
   } else {
     ldf4(p.s0 + mh, v[0]);
     ldf4(p.s1 + mh, v[1]);
-    ld4(p.hprev, 0, (long long)m * p.ldhp + j, v[2]);
+    ld4(p.hprev, F32, (long long)m * p.ldhp + j, v[2]);
   }
 }
 
-template <int CELL, int G>
+template <int CELL, int G, bool F32>
 __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const float (&v)[NPre<CELL>::v][4],
                                          const v4f (&acc)[G]) {
   const int H = p.Hs;
@@ -152,7 +162,7 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       tcv[e] = tanhf(c[e]);
       h[e] = go[e] * tcv[e];
     }
-    stb4(p.h_out + (long long)m * p.ldho + j, h);
+    st4<F32>(p.h_out, (long long)m * p.ldho + j, h);
     if (p.c_out) stf4(p.c_out + mh, c);
     if (p.act) {
       float* a = p.act + (long long)m * 4 * H + j;
@@ -175,11 +185,11 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       dout[e] = d_h * tcv * o * (1.f - o);
       dcp[e] = dc * f;
     }
-    bf16_t* o = p.dg + (long long)m * p.lddg + j;
-    stb4(o, di);
-    stb4(o + H, dgg);
-    stb4(o + 2 * H, df);
-    stb4(o + 3 * H, dout);
+    const long long o = (long long)m * p.lddg + j;
+    st4<F32>(p.dg, o, di);
+    st4<F32>(p.dg, o + H, dgg);
+    st4<F32>(p.dg, o + 2 * H, df);
+    st4<F32>(p.dg, o + 3 * H, dout);
     stf4(p.dc_prev + mh, dcp);
   } else if constexpr (CELL == 2) {
     float r[4], z[4], rh[4];
@@ -189,7 +199,7 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       z[e] = sgm(v[1][e] + acc[1][e]);
       rh[e] = r[e] * v[2][e];
     }
-    stb4(p.rh + (long long)m * p.ldrh + j, rh);
+    st4<F32>(p.rh, (long long)m * p.ldrh + j, rh);
     stf4(p.s0 + mh, r);
     stf4(p.s1 + mh, z);
   } else if constexpr (CELL == 3) {
@@ -199,7 +209,7 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       n[e] = tanhf(v[0][e] + acc[0][e]);
       h[e] = (1.f - v[2][e]) * n[e] + v[2][e] * v[1][e];
     }
-    stb4(p.h_out + (long long)m * p.ldho + j, h);
+    st4<F32>(p.h_out, (long long)m * p.ldho + j, h);
     if (p.s2) stf4(p.s2 + mh, n);
   } else if constexpr (CELL == 4) {
     float daz[4], dan[4], nc[4];
@@ -211,9 +221,9 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       daz[e] = dh * (v[4][e] - n) * z * (1.f - z);
       nc[e] = dh * z;
     }
-    bf16_t* o = p.dg + (long long)m * p.lddg + j;
-    stb4(o + H, daz);
-    stb4(o + 2 * H, dan);
+    const long long o = (long long)m * p.lddg + j;
+    st4<F32>(p.dg, o + H, daz);
+    st4<F32>(p.dg, o + 2 * H, dan);
     stf4(p.s0 + mh, nc);
   } else {
     float dar[4], carry[4];
@@ -223,7 +233,7 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
       dar[e] = drh * v[2][e] * r * (1.f - r);
       carry[e] = v[0][e] + drh * r;
     }
-    stb4(p.dg + (long long)m * p.lddg + j, dar);
+    st4<F32>(p.dg, (long long)m * p.lddg + j, dar);
     stf4(p.s0 + mh, carry);
   }
 }
@@ -232,7 +242,25 @@ __device__ __forceinline__ void epilogue(const RnnStep& p, int m, int j, const f
 // in flight for the whole step (one L2 round trip instead of up to 7 dependent ones at K = 4H = 800)
 constexpr int kStepWaves = 8;
 
-template <int CELL, int G>
+// 8 consecutive fp32 values → (rne bf16 hi, rne bf16 of the residual) as two MFMA fragments
+__device__ __forceinline__ void split_x3(const float* q, bool live, v8s& hi, v8s& lo) {
+  float v[8];
+  if (live) {
+    const float4 a = *reinterpret_cast<const float4*>(q), b = *reinterpret_cast<const float4*>(q + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bf16_t h = f2bf(v[e]);
+    hi[e] = (short)h;
+    lo[e] = (short)f2bf(v[e] - bf2f(h));
+  }
+}
+
+template <int CELL, int G, bool F32 = false>
 __device__ __forceinline__ void rnn_step_body(const RnnStep& p) {
   constexpr int NW = kStepWaves;
   __shared__ v4f red[NW - 1][G * 2][64];
@@ -246,15 +274,72 @@ __device__ __forceinline__ void rnn_step_body(const RnnStep& p) {
 
   float pre0[NP][4], pre1[NP][4];
   if (wid == 0 && jin) {
-    if (min0) pre_load<CELL>(p, m0 + fr, j, pre0);
-    if (min1) pre_load<CELL>(p, m0 + 16 + fr, j, pre1);
+    if (min0) pre_load<CELL, F32>(p, m0 + fr, j, pre0);
+    if (min1) pre_load<CELL, F32>(p, m0 + 16 + fr, j, pre1);
   }
 
   v4f acc0[G], acc1[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc0[g] = acc1[g] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if (p.a || p.a2) {
+  if constexpr (F32) {
+    if (p.a || p.a2) {
+      const bool bu = j0 + fr < p.Hs;
+      const long long r0 = min0 ? m0 + fr : 0, r1 = min1 ? m0 + 16 + fr : 0;
+      const float* A = reinterpret_cast<const float*>(p.a);
+      const float* A2 = reinterpret_cast<const float*>(p.a2);
+      const float* pa0 = A ? A + r0 * p.lda : nullptr;
+      const float* pa1 = A ? A + r1 * p.lda : nullptr;
+      const float* pb0 = A2 ? A2 + r0 * p.lda2 : nullptr;
+      const float* pb1 = A2 ? A2 + r1 * p.lda2 : nullptr;
+      const float* pu = reinterpret_cast<const float*>(p.u) + (long long)(bu ? j0 + fr : 0) * p.K;
+      const float* pu2 = p.K2 ? reinterpret_cast<const float*>(p.u2) + (long long)(bu ? j0 + fr : 0) * p.K2 : nullptr;
+      const long long gstride = (long long)p.Hs * p.K, gstride2 = (long long)p.Hs * p.K2;
+      const int KT = p.K + p.K2;
+      const int KS = (KT + 31) / 32;
+      for (int ks = wid; ks < KS; ks += NW) {
+        const int k = ks * 32 + fq * 8;
+        const bool kin = k < KT, seg2 = k >= p.K;
+        const int kk = seg2 ? k - p.K : k;
+        const float* s0 = seg2 ? pb0 : pa0;
+        const float* s1 = seg2 ? pb1 : pa1;
+        v8s xh0, xl0, xh1, xl1;
+        split_x3(s0 ? s0 + kk : nullptr, kin && min0 && s0, xh0, xl0);
+        split_x3(s1 ? s1 + kk : nullptr, kin && min1 && s1, xh1, xl1);
+        const float* wu = seg2 ? pu2 : pu;
+        const long long gs = seg2 ? gstride2 : gstride;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          v8s wh, wl;
+          split_x3(wu ? wu + g * gs + kk : nullptr, kin && bu && wu, wh, wl);
+          acc0[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh0, acc0[g], 0, 0, 0);
+          acc1[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh1, acc1[g], 0, 0, 0);
+          acc0[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh0, acc0[g], 0, 0, 0);
+          acc1[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh1, acc1[g], 0, 0, 0);
+          acc0[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl0, acc0[g], 0, 0, 0);
+          acc1[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl1, acc1[g], 0, 0, 0);
+        }
+      }
+      if (wid > 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          red[wid - 1][g * 2][lane] = acc0[g];
+          red[wid - 1][g * 2 + 1][lane] = acc1[g];
+        }
+      }
+      __syncthreads();
+      if (wid > 0) return;
+#pragma unroll
+      for (int w = 0; w < NW - 1; ++w)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          acc0[g] += red[w][g * 2][lane];
+          acc1[g] += red[w][g * 2 + 1][lane];
+        }
+    } else if (wid > 0) {
+      return;
+    }
+  } else if (p.a || p.a2) {
     const bool bu = j0 + fr < p.Hs;
     const long long r0 = min0 ? m0 + fr : 0, r1 = min1 ? m0 + 16 + fr : 0;
     const bf16_t* pa0 = p.a ? p.a + r0 * p.lda : nullptr;
@@ -307,13 +392,13 @@ __device__ __forceinline__ void rnn_step_body(const RnnStep& p) {
     return;
   }
   if (!jin) return;
-  if (min0) epilogue<CELL, G>(p, m0 + fr, j, pre0, acc0);
-  if (min1) epilogue<CELL, G>(p, m0 + 16 + fr, j, pre1, acc1);
+  if (min0) epilogue<CELL, G, F32>(p, m0 + fr, j, pre0, acc0);
+  if (min1) epilogue<CELL, G, F32>(p, m0 + 16 + fr, j, pre1, acc1);
 }
 
-template <int CELL, int G>
+template <int CELL, int G, bool F32 = false>
 __global__ void __launch_bounds__(64 * kStepWaves) k_rnn_step(RnnStep p) {
-  rnn_step_body<CELL, G>(p);
+  rnn_step_body<CELL, G, F32>(p);
 }
 
 // Two stacked layers in ONE launch (blockIdx.z = layer; bit z of `live` = that layer has a step in
@@ -350,7 +435,7 @@ static int rnn_step_check(int cell, const RnnStep& p) {
   const void* b8s[] = {p.hprev, p.h_out, p.gy, p.dg, p.rh};
   const long long lds_[] = {p.ldhp, p.ldho, p.ldgy, p.lddg, p.ldrh};
   for (int i = 0; i < 5; ++i)
-    if (b8s[i] && (!a8(b8s[i]) || lds_[i] % 4)) return (int)hipErrorInvalidValue;
+    if (b8s[i] && (!(p.f32 ? a16(b8s[i]) : a8(b8s[i])) || lds_[i] % 4)) return (int)hipErrorInvalidValue;
   // per-cell required tensors (cell 1: gy may be null when the second segment carries it)
   bool ok = true;
   switch (cell) {
@@ -368,13 +453,13 @@ static dim3 rnn_step_grid(int Hs, int M, int z = 1) {
   return dim3((unsigned)((Hs + 15) / 16), (unsigned)((M + 31) / 32), (unsigned)z);
 }
 
-BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const void* u, int M, int K, int Hs,
-                                const void* xg, long long ldx, int x_f32, const void* hprev, long long ldhp,
-                                const float* c_prev, void* h_out, long long ldho, float* c_out, float* act, float* tc,
-                                const void* gy, long long ldgy, const float* gc_next, void* dg, long long lddg,
-                                float* dc_prev, float* s0, float* s1, float* s2, void* rh, long long ldrh,
-                                hipStream_t s) {
+static int rnn_step_run(int cell, const void* a, long long lda, const void* u, int M, int K, int Hs, const void* xg,
+                        long long ldx, int x_f32, const void* hprev, long long ldhp, const float* c_prev, void* h_out,
+                        long long ldho, float* c_out, float* act, float* tc, const void* gy, long long ldgy,
+                        const float* gc_next, void* dg, long long lddg, float* dc_prev, float* s0, float* s1, float* s2,
+                        void* rh, long long ldrh, int f32, hipStream_t s) {
   RnnStep p{};  // value-initialised: the second segment stays off
+  p.f32 = f32;
   p.a = (const bf16_t*)a; p.lda = lda; p.u = (const bf16_t*)u; p.M = M; p.K = K; p.Hs = Hs;
   p.xg = xg; p.ldx = ldx; p.x_f32 = x_f32; p.hprev = (const bf16_t*)hprev; p.ldhp = ldhp; p.c_prev = c_prev;
   p.h_out = (bf16_t*)h_out; p.ldho = ldho; p.c_out = c_out; p.act = act; p.tc = tc; p.gy = (const bf16_t*)gy;
@@ -383,15 +468,36 @@ BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const vo
   const int rc = rnn_step_check(cell, p);
   if (rc) return rc;
   const dim3 grid = rnn_step_grid(Hs, M), block(64 * kStepWaves);
-  switch (cell) {
-    case 0: hipLaunchKernelGGL((k_rnn_step<0, 4>), grid, block, 0, s, p); break;
-    case 1: hipLaunchKernelGGL((k_rnn_step<1, 1>), grid, block, 0, s, p); break;
-    case 2: hipLaunchKernelGGL((k_rnn_step<2, 2>), grid, block, 0, s, p); break;
-    case 3: hipLaunchKernelGGL((k_rnn_step<3, 1>), grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL((k_rnn_step<4, 1>), grid, block, 0, s, p); break;
-    default: hipLaunchKernelGGL((k_rnn_step<5, 1>), grid, block, 0, s, p); break;
+  if (f32) {
+    switch (cell) {
+      case 0: hipLaunchKernelGGL((k_rnn_step<0, 4, true>), grid, block, 0, s, p); break;
+      case 1: hipLaunchKernelGGL((k_rnn_step<1, 1, true>), grid, block, 0, s, p); break;
+      case 2: hipLaunchKernelGGL((k_rnn_step<2, 2, true>), grid, block, 0, s, p); break;
+      case 3: hipLaunchKernelGGL((k_rnn_step<3, 1, true>), grid, block, 0, s, p); break;
+      case 4: hipLaunchKernelGGL((k_rnn_step<4, 1, true>), grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL((k_rnn_step<5, 1, true>), grid, block, 0, s, p); break;
+    }
+  } else {
+    switch (cell) {
+      case 0: hipLaunchKernelGGL((k_rnn_step<0, 4>), grid, block, 0, s, p); break;
+      case 1: hipLaunchKernelGGL((k_rnn_step<1, 1>), grid, block, 0, s, p); break;
+      case 2: hipLaunchKernelGGL((k_rnn_step<2, 2>), grid, block, 0, s, p); break;
+      case 3: hipLaunchKernelGGL((k_rnn_step<3, 1>), grid, block, 0, s, p); break;
+      case 4: hipLaunchKernelGGL((k_rnn_step<4, 1>), grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL((k_rnn_step<5, 1>), grid, block, 0, s, p); break;
+    }
   }
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_rnn_step(int cell, const void* a, long long lda, const void* u, int M, int K, int Hs,
+                                const void* xg, long long ldx, int x_f32, const void* hprev, long long ldhp,
+                                const float* c_prev, void* h_out, long long ldho, float* c_out, float* act, float* tc,
+                                const void* gy, long long ldgy, const float* gc_next, void* dg, long long lddg,
+                                float* dc_prev, float* s0, float* s1, float* s2, void* rh, long long ldrh,
+                                hipStream_t s) {
+  return rnn_step_run(cell, a, lda, u, M, K, Hs, xg, ldx, x_f32, hprev, ldhp, c_prev, h_out, ldho, c_out, act, tc, gy,
+                      ldgy, gc_next, dg, lddg, dc_prev, s0, s1, s2, rh, ldrh, 0, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1395,6 +1501,47 @@ static bool lstm_persist_ok(int B, int H) {
 // ------------------------------------------------------------------------------------------------
 static const bf16_t* bo(const void* p, long long off) { return p ? (const bf16_t*)p + off : nullptr; }
 
+// element pointer `off` elements past p in the activation type (bf16 or fp32)
+static const void* eo(const void* p, long long off, int f32) { return p ? (const char*)p + off * (f32 ? 4 : 2) : nullptr; }
+static void* eo(void* p, long long off, int f32) { return p ? (char*)p + off * (f32 ? 4 : 2) : nullptr; }
+
+// The per-step loop of a single-layer LSTM forward (one rnn_step launch per step).
+static int lstm_fwd_steps(const void* x2, int x_f32, const void* h0, const float* c0, const void* U, void* out,
+                          float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H, int f32, hipStream_t s) {
+  const bool train = cs && acts && tcs;
+  const long long G = 4LL * H, BH = (long long)B * H;
+  const int esz = x_f32 ? 4 : 2;
+  for (int t = 0; t < T; ++t) {
+    const void* a = t == 0 ? h0 : eo((const void*)out, (long long)(t - 1) * H, f32);
+    const long long lda = t == 0 ? H : (long long)T * H;
+    const void* xg = (const char*)x2 + (long long)t * G * esz;
+    const float* cp = t == 0 ? c0 : (train ? cs + (t - 1) * BH : cbuf + ((t - 1) & 1) * BH);
+    float* co = train ? cs + t * BH : cbuf + (t & 1) * BH;
+    int rc = rnn_step_run(0, a, lda, U, B, H, H, xg, (long long)T * G, x_f32, nullptr, 0, cp,
+                          eo(out, (long long)t * H, f32), (long long)T * H, co, train ? acts + t * B * G : nullptr,
+                          train ? tcs + t * BH : nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                          nullptr, nullptr, 0, f32, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// The per-step loop of a single-layer LSTM backward.
+static int lstm_bwd_steps(const void* gy, const void* Ut, const float* acts, const float* tcs, const float* cs,
+                          const float* c0, void* DG, float* gc, int B, int T, int H, int f32, hipStream_t s) {
+  const long long G = 4LL * H, BH = (long long)B * H;
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t + 1 == T;
+    int rc = rnn_step_run(1, last ? nullptr : eo((const void*)DG, (t + 1) * G, f32), (long long)T * G, Ut, B, (int)G,
+                          H, nullptr, 0, 0, nullptr, 0, t > 0 ? cs + (t - 1) * BH : c0, nullptr, 0, nullptr,
+                          (float*)acts + t * B * G, (float*)tcs + t * BH, eo(gy, (long long)t * H, f32), (long long)T * H,
+                          last ? nullptr : gc, eo(DG, t * G, f32), (long long)T * G, gc, nullptr, nullptr, nullptr,
+                          nullptr, 0, f32, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, const float* c0, const void* U, void* out,
                                     float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H, int* sync,
                                     void* xg, hipStream_t s) {
@@ -1436,19 +1583,16 @@ BIGDL_EXPORT int bigdl_lstm_seq_fwd(const void* x2, int x_f32, const void* h0, c
     else hipLaunchKernelGGL(k_lstm_seq_fwd_p<2>, dim3(1), dim3(1024), 0, s, p);
     BIGDL_CHECK_LAUNCH();
   }
-  for (int t = 0; t < T; ++t) {
-    const void* a = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
-    const long long lda = t == 0 ? H : (long long)T * H;
-    const void* xg = (const char*)x2 + (long long)t * G * esz;
-    const float* cp = t == 0 ? c0 : (train ? cs + (t - 1) * BH : cbuf + ((t - 1) & 1) * BH);
-    float* co = train ? cs + t * BH : cbuf + (t & 1) * BH;
-    int rc = bigdl_rnn_step(0, a, lda, U, B, H, H, xg, (long long)T * G, x_f32, nullptr, 0, cp,
-                            (bf16_t*)out + (long long)t * H, (long long)T * H, co, train ? acts + t * B * G : nullptr,
-                            train ? tcs + t * BH : nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-                            nullptr, nullptr, 0, s);
-    if (rc) return rc;
-  }
-  return 0;
+  return lstm_fwd_steps(x2, x_f32, h0, c0, U, out, cs, acts, tcs, cbuf, B, T, H, 0, s);
+}
+
+// All-fp32 LSTM (bf16x3 recurrent products, k_rnn_step<…, true>): x2, h0, U, out fp32.
+BIGDL_EXPORT int bigdl_lstm_seq_fwd32(const float* x2, const float* h0, const float* c0, const float* U, float* out,
+                                      float* cs, float* acts, float* tcs, float* cbuf, int B, int T, int H,
+                                      hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !U || !out) return (int)hipErrorInvalidValue;
+  if (!(cs && acts && tcs) && !cbuf) return (int)hipErrorInvalidValue;
+  return lstm_fwd_steps(x2, 1, h0, c0, U, out, cs, acts, tcs, cbuf, B, T, H, 1, s);
 }
 
 BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float* acts, const float* tcs, const float* cs,
@@ -1484,15 +1628,14 @@ BIGDL_EXPORT int bigdl_lstm_seq_bwd(const void* gy, const void* Ut, const float*
     else hipLaunchKernelGGL(k_lstm_seq_bwd_p<2>, dim3(1), dim3(1024), 0, s, p);
     BIGDL_CHECK_LAUNCH();
   }
-  for (int t = T - 1; t >= 0; --t) {
-    const bool last = t + 1 == T;
-    int rc = bigdl_rnn_step(1, last ? nullptr : bo(DG, (t + 1) * G), (long long)T * G, Ut, B, (int)G, H, nullptr, 0, 0,
-                            nullptr, 0, t > 0 ? cs + (t - 1) * BH : c0, nullptr, 0, nullptr, (float*)acts + t * B * G,
-                            (float*)tcs + t * BH, bo(gy, (long long)t * H), (long long)T * H, last ? nullptr : gc,
-                            (bf16_t*)DG + t * G, (long long)T * G, gc, nullptr, nullptr, nullptr, nullptr, 0, s);
-    if (rc) return rc;
-  }
-  return 0;
+  return lstm_bwd_steps(gy, Ut, acts, tcs, cs, c0, DG, gc, B, T, H, 0, s);
+}
+
+BIGDL_EXPORT int bigdl_lstm_seq_bwd32(const float* gy, const float* Ut, const float* acts, const float* tcs,
+                                      const float* cs, const float* c0, float* DG, float* gc, int B, int T, int H,
+                                      hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !gy || !Ut || !DG || !gc || !acts || !tcs || !cs) return (int)hipErrorInvalidValue;
+  return lstm_bwd_steps(gy, Ut, acts, tcs, cs, c0, DG, gc, B, T, H, 1, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1608,26 +1751,61 @@ BIGDL_EXPORT int bigdl_lstm2_seq_bwd(const void* gy1, const void* U1t, const flo
 
 // GRU: R, Z, Nn fp32 [S][B][H] and RH bf16 [B][S][H] with S = T (training) or 1 (inference: slot 0
 // reused every step; Nn may be null)
-BIGDL_EXPORT int bigdl_gru_seq_fwd(const void* x2, int x_f32, const void* h0, const void* Urz, const void* Uh, void* out,
-                                   float* R, float* Z, float* Nn, void* RH, int train, int B, int T, int H,
-                                   hipStream_t s) {
-  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !Urz || !Uh || !out || !R || !Z || !RH) return (int)hipErrorInvalidValue;
+static int gru_fwd_steps(const void* x2, int x_f32, const void* h0, const void* Urz, const void* Uh, void* out, float* R,
+                         float* Z, float* Nn, void* RH, int train, int B, int T, int H, int f32, hipStream_t s) {
   const long long G = 3LL * H, BH = (long long)B * H;
   const int S = train ? T : 1;
   const int esz = x_f32 ? 4 : 2;
   for (int t = 0; t < T; ++t) {
     const int k = train ? t : 0;
-    const void* hp = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
+    const void* hp = t == 0 ? h0 : eo((const void*)out, (long long)(t - 1) * H, f32);
     const long long ldhp = t == 0 ? H : (long long)T * H;
     const void* xg = (const char*)x2 + (long long)t * G * esz;
-    bf16_t* rh = (bf16_t*)RH + (long long)k * H;
-    int rc = bigdl_rnn_step(2, hp, ldhp, Urz, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr, nullptr, 0, nullptr,
-                            nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, R + k * BH, Z + k * BH, nullptr,
-                            rh, (long long)S * H, s);
+    void* rh = eo(RH, (long long)k * H, f32);
+    int rc = rnn_step_run(2, hp, ldhp, Urz, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr, nullptr, 0, nullptr,
+                          nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, R + k * BH, Z + k * BH, nullptr,
+                          rh, (long long)S * H, f32, s);
     if (rc) return rc;
-    rc = bigdl_rnn_step(3, rh, (long long)S * H, Uh, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr,
-                        (bf16_t*)out + (long long)t * H, (long long)T * H, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
-                        nullptr, 0, nullptr, nullptr, Z + k * BH, (train && Nn) ? Nn + k * BH : nullptr, nullptr, 0, s);
+    rc = rnn_step_run(3, rh, (long long)S * H, Uh, B, H, H, xg, (long long)T * G, x_f32, hp, ldhp, nullptr,
+                      eo(out, (long long)t * H, f32), (long long)T * H, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                      nullptr, 0, nullptr, nullptr, Z + k * BH, (train && Nn) ? Nn + k * BH : nullptr, nullptr, 0, f32, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+BIGDL_EXPORT int bigdl_gru_seq_fwd(const void* x2, int x_f32, const void* h0, const void* Urz, const void* Uh, void* out,
+                                   float* R, float* Z, float* Nn, void* RH, int train, int B, int T, int H,
+                                   hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !Urz || !Uh || !out || !R || !Z || !RH) return (int)hipErrorInvalidValue;
+  return gru_fwd_steps(x2, x_f32, h0, Urz, Uh, out, R, Z, Nn, RH, train, B, T, H, 0, s);
+}
+
+// All-fp32 GRU (bf16x3 recurrent products): x2, h0, Urz, Uh, out, RH fp32.
+BIGDL_EXPORT int bigdl_gru_seq_fwd32(const float* x2, const float* h0, const float* Urz, const float* Uh, float* out,
+                                     float* R, float* Z, float* Nn, float* RH, int train, int B, int T, int H,
+                                     hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !x2 || !h0 || !Urz || !Uh || !out || !R || !Z || !RH) return (int)hipErrorInvalidValue;
+  return gru_fwd_steps(x2, 1, h0, Urz, Uh, out, R, Z, Nn, RH, train, B, T, H, 1, s);
+}
+
+static int gru_bwd_steps(const void* gy, const void* Urz_t, const void* Uh_t, const float* R, const float* Z,
+                         const float* Nn, const void* out, const void* h0, void* DG, float* carry, int B, int T, int H,
+                         int f32, hipStream_t s) {
+  const long long G = 3LL * H, BH = (long long)B * H;
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t + 1 == T;
+    const void* hp = t == 0 ? h0 : eo(out, (long long)(t - 1) * H, f32);
+    const long long ldhp = t == 0 ? H : (long long)T * H;
+    void* dg = eo(DG, t * G, f32);
+    int rc = rnn_step_run(4, last ? nullptr : eo((const void*)DG, (t + 1) * G, f32), (long long)T * G, Urz_t, B, 2 * H, H,
+                          nullptr, 0, 0, hp, ldhp, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                          eo(gy, (long long)t * H, f32), (long long)T * H, nullptr, dg, (long long)T * G, nullptr, carry,
+                          (float*)Z + t * BH, (float*)Nn + t * BH, nullptr, 0, f32, s);
+    if (rc) return rc;
+    rc = rnn_step_run(5, eo((const void*)dg, 2 * H, f32), (long long)T * G, Uh_t, B, H, H, nullptr, 0, 0, hp, ldhp,
+                      nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, dg, (long long)T * G, nullptr,
+                      carry, (float*)R + t * BH, nullptr, nullptr, 0, f32, s);
     if (rc) return rc;
   }
   return 0;
@@ -1638,21 +1816,13 @@ BIGDL_EXPORT int bigdl_gru_seq_bwd(const void* gy, const void* Urz_t, const void
                                    int H, hipStream_t s) {
   if (B <= 0 || T <= 0 || H <= 0 || !gy || !Urz_t || !Uh_t || !R || !Z || !Nn || !out || !h0 || !DG || !carry)
     return (int)hipErrorInvalidValue;
-  const long long G = 3LL * H, BH = (long long)B * H;
-  for (int t = T - 1; t >= 0; --t) {
-    const bool last = t + 1 == T;
-    const void* hp = t == 0 ? h0 : (const void*)((const bf16_t*)out + (long long)(t - 1) * H);
-    const long long ldhp = t == 0 ? H : (long long)T * H;
-    bf16_t* dg = (bf16_t*)DG + t * G;
-    int rc = bigdl_rnn_step(4, last ? nullptr : bo(DG, (t + 1) * G), (long long)T * G, Urz_t, B, 2 * H, H, nullptr, 0,
-                            0, hp, ldhp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, bo(gy, (long long)t * H),
-                            (long long)T * H, nullptr, dg, (long long)T * G, nullptr, carry, (float*)Z + t * BH,
-                            (float*)Nn + t * BH, nullptr, 0, s);
-    if (rc) return rc;
-    rc = bigdl_rnn_step(5, dg + 2 * H, (long long)T * G, Uh_t, B, H, H, nullptr, 0, 0, hp, ldhp, nullptr, nullptr, 0,
-                        nullptr, nullptr, nullptr, nullptr, 0, nullptr, dg, (long long)T * G, nullptr, carry,
-                        (float*)R + t * BH, nullptr, nullptr, 0, s);
-    if (rc) return rc;
-  }
-  return 0;
+  return gru_bwd_steps(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry, B, T, H, 0, s);
+}
+
+BIGDL_EXPORT int bigdl_gru_seq_bwd32(const float* gy, const float* Urz_t, const float* Uh_t, const float* R,
+                                     const float* Z, const float* Nn, const float* out, const float* h0, float* DG,
+                                     float* carry, int B, int T, int H, hipStream_t s) {
+  if (B <= 0 || T <= 0 || H <= 0 || !gy || !Urz_t || !Uh_t || !R || !Z || !Nn || !out || !h0 || !DG || !carry)
+    return (int)hipErrorInvalidValue;
+  return gru_bwd_steps(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry, B, T, H, 1, s);
 }

@@ -2483,6 +2483,45 @@ def gru_seq_backward(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry):
                                    ptr(carry), C.c_int(B), C.c_int(T), C.c_int(H), _s()), "gru_seq_bwd")
 
 
+def rnn_fast32_ok(H, *ts):
+    """The fp32 recurrence (bf16x3 rnn_step variant) covers dense fp32 device rows with H % 8 == 0."""
+    if H % 8 or not N.has("lstm_cell_forward") or not hasattr(_lib(), "bigdl_lstm_seq_fwd32"):
+        return False
+    return all(t is None or (t.is_cuda and t.dtype == _f32) for t in ts)
+
+
+def lstm_seq_forward32(x2, h0, c0, U, out, cs, acts, tcs, cbuf):
+    """All-fp32 fused LSTM forward (bigdl_lstm_seq_fwd32: bf16x3 recurrent products on MFMA)."""
+    B, T, G = x2.shape
+    H = G // 4
+    assert _dense_bf16(x2, h0, c0, U, out, cs, acts, tcs, cbuf) and x2.dtype == _f32, "lstm_seq_forward32"
+    check(_lib().bigdl_lstm_seq_fwd32(ptr(x2), ptr(h0), ptr(c0), ptr(U), ptr(out), ptr(cs), ptr(acts), ptr(tcs),
+                                      ptr(cbuf), C.c_int(B), C.c_int(T), C.c_int(H), _s()), "lstm_seq_fwd32")
+
+
+def lstm_seq_backward32(gy, Ut, acts, tcs, cs, c0, DG, gc):
+    B, T, H = gy.shape
+    assert _dense_bf16(gy, Ut, acts, tcs, cs, c0, DG, gc) and gy.dtype == _f32, "lstm_seq_backward32"
+    check(_lib().bigdl_lstm_seq_bwd32(ptr(gy), ptr(Ut), ptr(acts), ptr(tcs), ptr(cs), ptr(c0), ptr(DG), ptr(gc),
+                                      C.c_int(B), C.c_int(T), C.c_int(H), _s()), "lstm_seq_bwd32")
+
+
+def gru_seq_forward32(x2, h0, Urz, Uh, out, R, Z, Nn, RH, train):
+    B, T, G = x2.shape
+    H = G // 3
+    assert _dense_bf16(x2, h0, Urz, Uh, out, R, Z, Nn, RH) and x2.dtype == _f32, "gru_seq_forward32"
+    check(_lib().bigdl_gru_seq_fwd32(ptr(x2), ptr(h0), ptr(Urz), ptr(Uh), ptr(out), ptr(R), ptr(Z), ptr(Nn), ptr(RH),
+                                     C.c_int(1 if train else 0), C.c_int(B), C.c_int(T), C.c_int(H), _s()),
+          "gru_seq_fwd32")
+
+
+def gru_seq_backward32(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry):
+    B, T, H = gy.shape
+    assert _dense_bf16(gy, Urz_t, Uh_t, R, Z, Nn, out, h0, DG, carry) and gy.dtype == _f32, "gru_seq_backward32"
+    check(_lib().bigdl_gru_seq_bwd32(ptr(gy), ptr(Urz_t), ptr(Uh_t), ptr(R), ptr(Z), ptr(Nn), ptr(out), ptr(h0), ptr(DG),
+                                     ptr(carry), C.c_int(B), C.c_int(T), C.c_int(H), _s()), "gru_seq_bwd32")
+
+
 def rnn_fast_ok(H, *ts):
     """The fused step covers bf16 rows with H % 8 == 0 on a device with the library loaded."""
     if H % 8 or not N.has("lstm_cell_forward"):

@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5q
 T="python -u -m pytest -q --timeout 120 --timeout-method thread"
-timeout -k 10 300 $T tests/test_int8_static.py tests/test_quantized.py tests/test_syncbn_native.py > gpurun_out/r5q/tests.log 2>&1; rc=$?
+timeout -k 10 300 $T tests/test_int8_static.py tests/test_quantized.py tests/test_syncbn_native.py tests/test_rnn_fp32.py tests/test_lstm_stack.py > gpurun_out/r5q/tests.log 2>&1; rc=$?
 grep -E "FAILED|passed|failed|Error" gpurun_out/r5q/tests.log | tail -8; [ $rc -eq 0 ] || exit 1
 timeout -k 10 400 python tools/bench_configs.py --config int8 --steps 10 --warmup 3 > gpurun_out/r5q/int8.log 2>&1 || { tail -30 gpurun_out/r5q/int8.log; exit 1; }
 grep metric gpurun_out/r5q/int8.log | cut -c1-900
