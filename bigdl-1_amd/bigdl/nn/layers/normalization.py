@@ -102,7 +102,18 @@ class BatchNormalization(TensorModule):
         return self
 
     def _sync_active(self):
-        return self._sync and _dist_ready(self._sync_force)
+        if not (self._sync and _dist_ready(self._sync_force)):
+            return False
+        if config.get_property("bigdl.bn.syncOneRankLocal") and self._sync_world() == 1:
+            # a one-rank group: the all-reduce is the identity and the global statistics ARE the
+            # local ones, so the local finalize+apply kernels run (the launch count of local BN)
+            return False
+        return True
+
+    def _sync_world(self):
+        import torch.distributed as dist
+        grp = self._sync_group
+        return dist.get_world_size(grp) if grp is not None else dist.get_world_size()
 
     def _to_nchw_like(self, x):
         return x

@@ -159,6 +159,37 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
     }
     return;
   }
+  // residual (+ ReLU) epilogue of a whole channel tile (the inference conv+sum+ReLU, FusedConvSum):
+  // all of this thread's residual chunks are requested before the first is used — one chunk in
+  // flight per row (the general loop below) left the 56² block tails at ~3.9 TB/s
+  if (p.res && p.res_sh == 0 && !p.bnx && !p.scatter && !p.stats && n0 + BN <= p.K) {
+    constexpr int NR = BM / RPP;
+    const int rmax = p.M - m0;
+    uint4 rv[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = rr + i * RPP;
+      rv[i] = r < rmax ? *reinterpret_cast<const uint4*>(p.res + (size_t)(m0 + r) * p.K + n) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = rr + i * RPP;
+      if (r >= rmax) break;
+      float v[8], a[8];
+      unpack8(rd_chunk(r, cc), v);
+      unpack8(rv[i], a);
+      uint32_t w4[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] += a[e];
+        if (p.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+      *reinterpret_cast<uint4*>(p.y + (size_t)(m0 + r) * p.ldy + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    return;
+  }
   float s8[8], q8[8];
   const bool full = n + 8 <= p.K;
   float sk[8];  // statistics shift of this thread's 8 channels

@@ -61,7 +61,28 @@ def _prep(m, sync):
     return m
 
 
-def test_syncbn_world1_matches_local_bn_and_runs_native():
+@pytest.fixture
+def rehearse_multirank():
+    """Run the multi-rank SyncBN kernels at world size 1 (by default a one-rank group runs the
+    local BN kernels, bigdl.bn.syncOneRankLocal)."""
+    from bigdl.utils import config
+    config.set_property("bigdl.bn.syncOneRankLocal", False)
+    yield
+    config.set_property("bigdl.bn.syncOneRankLocal", True)
+
+
+def test_syncbn_one_rank_group_runs_local_kernels():
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    _init_world1()
+    b = _prep(_block(), True)
+    bns = [mod for mod in b.modules if type(mod).__name__ == "SpatialBatchNormalization"]
+    assert bns and not any(mod._sync_active() for mod in bns)
+
+
+def test_syncbn_world1_matches_local_bn_and_runs_native(rehearse_multirank):
     from bigdl.utils import config
     from bigdl.utils.engine import Engine
     config.set_property("bigdl.compute.dtype", "bf16")
