@@ -133,6 +133,10 @@ def finish(opt, model, args) -> dict:
     if args.saveModel and Engine.rank() == 0:
         model.saveModel(args.saveModel, over_write=True)
     st = dict(opt.state)
+    if Engine.is_distributed():
+        import torch.distributed as tdist
+        tdist.barrier()  # every rank is done with the group before it is torn down
+        Engine.shutdown()
     return {k: st[k] for k in ("epoch", "neval", "Loss") if k in st}
 
 

@@ -87,6 +87,10 @@ class Engine:
                         apply_comm_env()
                     tdist.init_process_group(backend=be, **kw)
                     _S.process_group_owned = True
+                    # tear the group down before interpreter exit: a live gloo / RCCL group's
+                    # threads destroyed by the C++ runtime at exit abort the process (SIGABRT)
+                    import atexit
+                    atexit.register(_shutdown_at_exit)
                 _S.rank = tdist.get_rank()
                 _S.world_size = tdist.get_world_size()
             if _S.default_pool is None:
@@ -187,6 +191,13 @@ class Engine:
     def reset():
         Engine.shutdown()
         _S.__init__()
+
+
+def _shutdown_at_exit():
+    try:
+        Engine.shutdown()
+    except Exception:  # noqa: BLE001 — best effort at interpreter exit
+        pass
 
 
 def apply_comm_env(env=None) -> dict:
