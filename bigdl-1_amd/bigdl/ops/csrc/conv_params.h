@@ -205,10 +205,57 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
       bmu[e] = p.bn_mean[n + e];
     }
   }
+  // BN-backward dgrad epilogue (bnx, dense output): every global operand of this thread's rows —
+  // the BN input chunk, the ReLU mask (bits or bf16) and the residual chunk — is requested before
+  // the first is used (the row-at-a-time loop below kept one or two rows in flight: the 56² stage-1
+  // dgrads, ~1.3 GB each, ran at ~3 TB/s)
+  constexpr int NRH = SBM / RPP;
+  const bool bnfast = p.bnx && full && !p.scatter && (!p.bn_mask || p.bn_bits);
   // the statistics partials are per SBM-row group: a BM = 256 tile reduces its two halves separately
   for (int h = 0; h < BM / SBM; ++h) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s8[e] = 0.f; q8[e] = 0.f; }
+  if (bnfast) {
+    uint4 xq[NRH], rq[NRH];
+    uint32_t bq[NRH];
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+      const int r = h * SBM + rr + i * RPP, m = m0 + r;
+      const bool live = m < p.M;
+      const size_t off = (size_t)(live ? m : m0) * p.K + n;
+      xq[i] = live ? *reinterpret_cast<const uint4*>(p.bnx + off) : make_uint4(0, 0, 0, 0);
+      bq[i] = (live && p.bn_mask) ? (uint32_t)p.bn_bits[off >> 3] : 0xFFu;
+      size_t ro;
+      rq[i] = (live && p.bn_mask && p.res && res_at(p, m, n, off, ro)) ? *reinterpret_cast<const uint4*>(p.res + ro)
+                                                         : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+      const int r = h * SBM + rr + i * RPP, m = m0 + r;
+      if (m >= p.M) break;
+      float g[8], xv[8], rv[8];
+      unpack8(rd_chunk(r, cc), g);
+      unpack8(xq[i], xv);
+      unpack8(rq[i], rv);
+      uint32_t w4[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool live = p.bn_mask ? ((bq[i] >> e) & 1u) != 0 : fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
+        g[e] = live ? g[e] + (p.bn_mask ? rv[e] : 0.f) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)f2bf(g[2 * e]) | ((uint32_t)f2bf(g[2 * e + 1]) << 16);
+      *reinterpret_cast<uint4*>(p.y + (size_t)m * p.ldy + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(w4[e] << 16), b = __uint_as_float(w4[e] & 0xFFFF0000u);
+        s8[2 * e] += a;
+        q8[2 * e] = fmaf(a, xv[2 * e] - bmu[2 * e], q8[2 * e]);
+        s8[2 * e + 1] += b;
+        q8[2 * e + 1] = fmaf(b, xv[2 * e + 1] - bmu[2 * e + 1], q8[2 * e + 1]);
+      }
+    }
+  } else
 #pragma unroll 2
   for (int r = h * SBM + rr; r < (h + 1) * SBM; r += RPP) {
     const int m = m0 + r;

@@ -71,7 +71,10 @@ def test_resnet_stage_prologue_matches_materialised():
     torch.testing.assert_close(gb, ga, rtol=1e-3, atol=1e-3)
     worst = max(float((u - v).norm() / v.norm().clamp_min(1e-12)) for u, v in zip(pb, pa))
     assert worst < 1e-3, worst
-    at = [n for n in nb if "Lb0ELb1E" in n or "true>" in n and ("k_conv_fwd" in n or "k_conv_wgrad" in n)]
+    import re
+    # the BN-backward prologue instantiations: k_conv_fwd<…, AT = true> and k_conv_wgrad<…, AT = true, …>
+    at = [n for n in nb if re.search(r"k_conv_fwd<\d+, \d+, \d+, \d+, \w+, true>", n)
+          or re.search(r"k_conv_wgrad<\d+, \d+, \d+, \w+, \w+, true", n) or "Lb0ELb1E" in n]
     assert any("k_conv_fwd" in n for n in at) and any("k_conv_wgrad" in n for n in at), sorted(set(nb))
     apply_a = sum("k_bn_bwd_apply" in n for n in na)
     apply_b = sum("k_bn_bwd_apply" in n for n in nb)
