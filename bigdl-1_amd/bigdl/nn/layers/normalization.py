@@ -146,14 +146,20 @@ class BatchNormalization(TensorModule):
         if self._sync_active() and not (rep > 0 and config.get_property("bigdl.bn.shiftedStats")):
             return None
         if rep > 0 and (self._sync_active() or not config.get_property("bigdl.bn.atomicStats")):
-            # replicated form: [2][R][C] zeroed, tile tm adds into replica tm % R; the BN's finalize
-            # reads the R rows and clears them (batchnorm.hip reduce_partials rezero)
+            # replicated form: [2][R][C] zeroed, tile tm adds into replica tm % R.  Two sets used in
+            # alternate steps: a one-launch BN (bigdl.bn.foldFinalize) reduces its set in every apply
+            # block and clears the OTHER set for the next producer; a separate finalize clears the set
+            # it read.  R ≤ 16384 / C keeps the per-block reduction at ≤ 32k floats.
             rep = min(rep, 512)
+            if config.get_property("bigdl.bn.foldFinalize"):
+                rep = min(rep, max(4, 16384 // max(C, 1)))
             attr = "_rep_" + kind
-            buf = self.__dict__.get(attr)
-            if buf is None or buf.numel() != 2 * rep * C or buf.device != device:
-                buf = self.__dict__[attr] = torch.zeros(2 * rep * C, dtype=torch.float32, device=device)
-            return buf, rep
+            sets = self.__dict__.get(attr)
+            if sets is None or sets[0].numel() != 2 * rep * C or sets[0].device != device:
+                sets = self.__dict__[attr] = [torch.zeros(2 * rep * C, dtype=torch.float32, device=device)
+                                              for _ in range(2)]
+                self.__dict__["_repi_" + kind] = 0
+            return sets[self.__dict__["_repi_" + kind]], rep
         if not config.get_property("bigdl.bn.atomicStats"):
             return None
         attr = "_sums_" + kind
@@ -171,7 +177,42 @@ class BatchNormalization(TensorModule):
     def _is_rep(self, part):
         """``part`` is one of this BN's replicated atomic-statistics buffers (cleared by the finalize
         that reads it)."""
-        return part is not None and any(part is self.__dict__.get(a) for a in ("_rep_fwd", "_rep_bwd"))
+        return part is not None and any(part is b for a in ("_rep_fwd", "_rep_bwd") for b in (self.__dict__.get(a) or ()))
+
+    def _rep_next(self, kind, part):
+        """The other replica set of ``kind`` when ``part`` is the current one (what a one-launch BN
+        clears for the next producer), else None."""
+        sets = self.__dict__.get("_rep_" + kind)
+        if not sets or not config.get_property("bigdl.bn.foldFinalize"):
+            return None
+        i = self.__dict__["_repi_" + kind]
+        return sets[1 - i] if part is sets[i] else None
+
+    def _rep_flip(self, kind, part):
+        """``part`` (the current set of ``kind``) was consumed: the next producer adds into the other."""
+        sets = self.__dict__.get("_rep_" + kind)
+        if sets and part is sets[self.__dict__["_repi_" + kind]]:
+            self.__dict__["_repi_" + kind] ^= 1
+
+    def _advance_shift(self, mean):
+        """This step's batch mean becomes the next step's statistics shift (the ring of
+        :meth:`_stat_shift`)."""
+        kb = self.__dict__.get("_kbuf")
+        if kb is None or mean is None:
+            return
+        i = self.__dict__["_kidx"]
+        nxt = kb[1 - i]
+        if mean is not nxt:
+            nxt.copy_(mean.detach().reshape(nxt.shape))
+        self.__dict__["_kidx"] = 1 - i
+
+    def _shift_next(self, shift):
+        """The ring buffer the kernel may write this step's mean into (when ``shift`` is the ring's
+        current K), else None."""
+        kb = self.__dict__.get("_kbuf")
+        if kb is None or shift is not kb[self.__dict__["_kidx"]]:
+            return None
+        return kb[1 - self.__dict__["_kidx"]]
 
     def _stat_shift(self, device=None):
         """The K the shifted statistics Σ(x − K), Σ(x − K)² subtract (every producer of this BN's
@@ -179,7 +220,7 @@ class BatchNormalization(TensorModule):
         mean.  SyncBN: the previous step's GLOBAL batch mean (identical on every rank), held in a
         two-buffer ring — the one-launch finalize+apply then never writes what its blocks read, so
         block 0 updates the running statistics up front (batchnorm.hip BnFwdFin::early)."""
-        if not self._sync_active():
+        if not (self._sync_active() or (config.get_property("bigdl.bn.foldFinalize") and self.train)):
             return self.runningMean
         kb = self.__dict__.get("_kbuf")
         rm = self.runningMean
@@ -235,7 +276,10 @@ class BatchNormalization(TensorModule):
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
                         relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits,
-                        rezero=self._is_rep(ps[2]))
+                        rezero=self._is_rep(ps[2]), zero_next=self._rep_next("fwd", ps[2]),
+                        mean_out=self._shift_next(ps[4]))
+                    if r is not NotImplemented:
+                        self._rep_flip("fwd", ps[2])
                 if r is NotImplemented:
                     self._drop_sums(ps, 3)
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
@@ -243,6 +287,7 @@ class BatchNormalization(TensorModule):
                                                     in_bias=ib, coef_out=coef, bits_out=bits)
                 self._relu_bits = bits
                 y, mean, invstd = r
+                self._advance_shift(mean)
                 self._last_input = x
             self.saveMean, self.saveStd = mean, invstd
         else:
@@ -393,8 +438,10 @@ class BatchNormalization(TensorModule):
                     gg_acc=self.gradWeight if (acc and self.affine) else None,
                     gb_acc=self.gradBias if (acc and self.affine) else None,
                     scale=self.scale_w if acc else 0.0, cbias_acc=cb, cbias_scale=cbs,
-                    lazy=self._lazy_grad_ok(input, x), rezero=self._is_rep(pg[1]))
+                    lazy=self._lazy_grad_ok(input, x), rezero=self._is_rep(pg[1]),
+                    zero_next=self._rep_next("bwd", pg[1]))
                 if gi is not NotImplemented:
+                    self._rep_flip("bwd", pg[1])
                     if gi is not None and input.dim() == 1:
                         gi = gi.reshape(input.shape)
                     return (gi, gy) if want_gres else gi

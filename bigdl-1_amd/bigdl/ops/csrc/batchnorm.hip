@@ -700,13 +700,42 @@ struct BnFwdFin {
   // the sums are kept): block 0 writes the saved statistics / coefficients / running statistics
   // right after its prologue, and there is no last-block election at all
   int early;
+  // local BN, one launch (bigdl_bn_fwd_train_rep_fin): the statistics are the producing conv's R
+  // replicated rows rep [2][R][C] (reduced per channel in every block's prologue, instead of a
+  // separate finalize launch); block 0 clears zero_next (the OTHER replica set, which the next
+  // producer adds into) — this kernel's own set is cleared by the next step's consumer
+  const float* rep;
+  int R;
+  float* zero_next;
 };
+
+__device__ __forceinline__ void fin_fwd_sums(const BnFwdFin& f, int C, int c, double& s, double& q) {
+  if (f.rep) {
+    s = 0.0;
+    q = 0.0;
+    for (int r = 0; r < f.R; ++r) {
+      s += (double)f.rep[(size_t)r * C + c];
+      q += (double)f.rep[((size_t)f.R + r) * C + c];
+    }
+  } else {
+    s = (double)f.sums[c];
+    q = (double)f.sums[C + c];
+  }
+}
+
+// zero n floats (n % 4 == 0, 16-B aligned) with this block's threads
+__device__ __forceinline__ void block_zero(float* p, long long n) {
+  for (long long i = (long long)threadIdx.x * 4; i < n; i += (long long)blockDim.x * 4)
+    *reinterpret_cast<float4*>(p + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
 
 __device__ __forceinline__ void fin_fwd_coef(const BnFwdFin& f, int C, int c, float& mean, float& var, float& invstd,
                                              float& sc, float& sh) {
   const double Mg = f.dM ? (double)*f.dM : f.M;
-  const double dm = (double)f.sums[c] / Mg;
-  var = (float)fmax((double)f.sums[C + c] / Mg - dm * dm, 0.0);
+  double s1, s2;
+  fin_fwd_sums(f, C, c, s1, s2);
+  const double dm = s1 / Mg;
+  var = (float)fmax(s2 / Mg - dm * dm, 0.0);
   mean = (f.kshift ? f.kshift[c] : 0.f) + (float)dm;
   invstd = rsqrtf(var + f.eps);
   sc = (f.gamma ? f.gamma[c] : 1.f) * invstd;
@@ -769,7 +798,10 @@ __global__ void __launch_bounds__(256) k_bn_apply_fin(const bf16_t* __restrict__
   }
   __syncthreads();
   if (f.early) {
-    if (blockIdx.x == 0) fin_fwd_side(f, C);
+    if (blockIdx.x == 0) {
+      fin_fwd_side(f, C);
+      if (f.zero_next) block_zero(f.zero_next, 2LL * f.R * C);
+    }
     bn_apply_rows<RES, RELU, BITS, 4>(x, res, y, M, C, cf, cf + C, bits);
     return;
   }
@@ -824,6 +856,36 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums_apply(const void* x, const void* res, v
   BIGDL_CHECK_LAUNCH();
 }
 
+// Local training BN forward in ONE launch from the producing conv's replicated statistics
+// rep [2][R][C] (the conv epilogue's atomics, shifted by kshift): every block reduces the R rows
+// of all C channels in its prologue, block 0 writes the saved statistics / coefficients / running
+// statistics and clears zero_next [2][R][C] (the other replica set).  kshift must not be the
+// running mean or save_mean (no block may read what block 0 writes: the caller's shift ring).
+BIGDL_EXPORT int bigdl_bn_fwd_train_rep_fin(const void* x, const void* res, void* y, long long M, int C,
+                                            const float* gamma, const float* beta, const float* in_bias,
+                                            float* run_mean, float* run_var, float momentum, float eps,
+                                            float* save_mean, float* save_invstd, const float* rep, int R,
+                                            float* zero_next, const float* kshift, float* coef, int relu, void* bits,
+                                            hipStream_t s) {
+  if (C % 8 || C > 8192 || M <= 0 || !rep || R <= 0 || !save_mean || !save_invstd || !coef || (bits && !relu) ||
+      (kshift && (kshift == run_mean || kshift == save_mean)) || ((uintptr_t)zero_next & 15))
+    return (int)hipErrorInvalidValue;
+  BnFwdFin f{nullptr, kshift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef, (double)M,
+             momentum, eps, nullptr, nullptr, 1, 1, rep, R, zero_next};
+  const int grid = apply_grid(M, C);
+  const bf16_t* xr = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  bf16_t* yr = (bf16_t*)y;
+  uint8_t* br = (uint8_t*)bits;
+  if (relu && bits && res) hipLaunchKernelGGL((k_bn_apply_fin<true, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (relu && bits) hipLaunchKernelGGL((k_bn_apply_fin<false, true, true>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (res && relu) hipLaunchKernelGGL((k_bn_apply_fin<true, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (res) hipLaunchKernelGGL((k_bn_apply_fin<true, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply_fin<false, true, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  else hipLaunchKernelGGL((k_bn_apply_fin<false, false, false>), dim3(grid), dim3(256), 8 * C, s, xr, rr, yr, M, C, f, br);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // Backward twin: the consumer conv's dgrad epilogue (bnx mode, stats_atomic) ADDED Σg', Σg'·(x − μ)
 // into sums; gx = A·g' + B·x + Cc with the coefficients derived per block in the prologue; the last
 // arriver accumulates dγ / dβ (and a folded producer bias's gradient), writes the coefficients (when
@@ -849,13 +911,27 @@ struct BnBwdFin {
   unsigned* ticket;
   int keep;
   int early;  // as BnFwdFin: block 0 writes the side results after its prologue, no election
+  const float* rep;  // as BnFwdFin: the consumer dgrad's replicated [2][R][C] sums
+  int R;
+  float* zero_next;
 };
 
 __device__ __forceinline__ void fin_bwd_coef(const BnBwdFin& f, int C, int c, float& a, float& dg, float& A, float& B,
                                              float& Cc) {
-  a = f.sums[c];
+  if (f.rep) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < f.R; ++r) {
+      s += (double)f.rep[(size_t)r * C + c];
+      q += (double)f.rep[((size_t)f.R + r) * C + c];
+    }
+    a = (float)s;
+    dg = (float)q;
+  } else {
+    a = f.sums[c];
+    dg = f.sums[C + c];
+  }
   const float is = f.invstd[c];
-  dg = f.sums[C + c] * is;
+  dg *= is;
   const float gm = f.gamma ? f.gamma[c] : 1.f;
   A = gm * is;
   const float Mg = f.dM ? *f.dM : f.M;
@@ -878,7 +954,10 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_fin(const bf16_t* __restri
     __syncthreads();
   }
   if (f.early) {
-    if (blockIdx.x == 0) fin_bwd_side(f, C);
+    if (blockIdx.x == 0) {
+      fin_bwd_side(f, C);
+      if (f.zero_next) block_zero(f.zero_next, 2LL * f.R * C);
+    }
     if (gx) bn_bwd_apply_rows<false, false, 4>(gy, x, nullptr, gx, nullptr, M, C, cf);
     return;
   }
@@ -921,6 +1000,25 @@ BIGDL_EXPORT int bigdl_bn_bwd_sums_apply(const void* gm, const void* x, void* gx
                      (bf16_t*)gx, M, C, f);
   BIGDL_CHECK_LAUNCH();
 }
+
+// Backward twin of bigdl_bn_fwd_train_rep_fin: the consumer dgrad epilogue's replicated
+// [Σg', Σg'·(x − μ)] rows; gx = A·g' + B·x + Cc (gm already ReLU-masked), block 0 accumulates dγ / dβ
+// (and a folded producer bias) and clears zero_next.  gx null: one block, parameter gradients only.
+BIGDL_EXPORT int bigdl_bn_bwd_rep_fin(const void* gm, const void* x, void* gx, long long M, int C, const float* gamma,
+                                      const float* mean, const float* invstd, float* ggamma, float* gbeta, float gscale,
+                                      float* cbias, float cbscale, const float* rep, int R, float* zero_next,
+                                      float* coef, hipStream_t s) {
+  if (C % 8 || C > 4096 || M <= 0 || !rep || R <= 0 || !mean || !invstd || (gx && (!gm || !x)) ||
+      ((uintptr_t)zero_next & 15))
+    return (int)hipErrorInvalidValue;
+  BnBwdFin f{nullptr, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, (float)M, nullptr, 0.f,
+             nullptr, nullptr, 1, 1, rep, R, zero_next};
+  const int grid = gx ? apply_grid(M, C) : 1;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3(grid), dim3(256), gx ? 12 * C : 0, s, (const bf16_t*)gm, (const bf16_t*)x,
+                     (bf16_t*)gx, M, C, f);
+  BIGDL_CHECK_LAUNCH();
+}
+
 
 // ------------------------------------------------------------------------------------------------ SyncBN
 // Cross-rank BatchNormalization (P6 / X11, SpatialBatchNormalization.scala:1114-1151,1257-1329):

@@ -180,7 +180,7 @@ def _coef_ok(t, C_):
 
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
                                     relu=False, residual=None, in_bias=None, coef_out=None, shift=None, bits_out=None,
-                                    rezero=False):
+                                    rezero=False, zero_next=None, mean_out=None):
     """Training BN whose statistics were produced by the preceding conv's epilogue
     (:func:`conv2d_forward_stats`): finalize + apply only.  ``rezero``: ``partial`` is a replicated
     atomic-statistics buffer ([2][G][C], G replicas) that the finalize clears after reading."""
@@ -216,9 +216,22 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
                                  residual.dtype != _bf16 or not _al16(residual)):
         return NotImplemented
     coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
-    mean = torch.empty(C_, dtype=_f32, device=x.device)
+    mean = mean_out if (mean_out is not None and _f32vec(mean_out, C_)) else torch.empty(C_, dtype=_f32,
+                                                                                           device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
     y = torch.empty_like(x)
+    if (rezero and G >= 1 and zero_next is not None and zero_next.numel() == partial.numel() and shift is not None
+            and _f32vec(shift, C_) and shift.data_ptr() not in (running_mean.data_ptr(), mean.data_ptr())
+            and C_ <= 8192 and 2 * G * C_ <= 32768 and _al16(zero_next)):
+        # ONE launch: each block reduces the conv's replicated statistics itself (no finalize kernel),
+        # block 0 updates the running statistics and clears the next step's replica set
+        check(_lib().bigdl_bn_fwd_train_rep_fin(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
+                                                ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
+                                                _f(momentum), _f(eps), ptr(mean), ptr(invstd), ptr(partial),
+                                                C.c_int(G), ptr(zero_next), ptr(shift), ptr(coef),
+                                                C.c_int(1 if relu else 0), ptr(_bits_ok(bits_out, M, C_, relu)), _s()),
+              "bn_fwd_train_rep_fin")
+        return y, mean, invstd
     if G == 0:
         check(_lib().bigdl_bn_fwd_train_sums_apply(ptr(x), ptr(residual), ptr(y), _ll(M), C.c_int(C_), ptr(gamma),
                                                    ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var),
@@ -239,7 +252,8 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
 
 
 def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G, need_input=True, gg_acc=None,
-                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, lazy=False, rezero=False):
+                                gb_acc=None, scale=1.0, cbias_acc=None, cbias_scale=1.0, lazy=False, rezero=False,
+                                zero_next=None):
     """BN backward whose reductions came from the consumer conv's dgrad epilogue; ``gm`` is the
     already ReLU-masked gradient.  Returns gradInput (or None) / NotImplemented; ``lazy`` returns
     it as a :class:`~bigdl.ops.reference.BNGrad` (coefficients only, no apply pass)."""
@@ -266,6 +280,18 @@ def batchnorm_backward_partials(gm, x, gamma, save_mean, save_invstd, partial, G
         return NotImplemented
     coef = torch.empty(3 * C_, dtype=_f32, device=x.device)
     gx = torch.empty_like(x) if (need_input and not lazy) else None
+    if (rezero and G >= 1 and zero_next is not None and partial is not None and zero_next.numel() == partial.numel()
+            and C_ <= 4096 and 2 * G * C_ <= 32768 and _al16(zero_next)):
+        # ONE launch (no finalize kernel): coefficients from the dgrad's replicated sums in every block,
+        # dγ / dβ / the folded bias by block 0, which also clears the next step's replica set
+        check(_lib().bigdl_bn_bwd_rep_fin(ptr(gm), ptr(x), ptr(gx), _ll(M), C.c_int(C_), ptr(gamma), ptr(save_mean),
+                                          ptr(save_invstd), ptr(gg_acc if scale != 0 else None),
+                                          ptr(gb_acc if scale != 0 else None), _f(scale),
+                                          ptr(cbias_acc if cbias_scale != 0 else None), _f(cbias_scale), ptr(partial),
+                                          C.c_int(G), ptr(zero_next), ptr(coef), _s()), "bn_bwd_rep_fin")
+        if need_input and lazy:
+            return R_.BNGrad(gm, x, coef)
+        return gx
     if G == 0:  # atomically accumulated [Σg', Σg'·(x − μ), counter] from the dgrad epilogue
         if partial is None or partial.numel() != 2 * C_ + 1 or partial.dtype != _f32 or C_ > 4096:
             return NotImplemented

@@ -51,6 +51,7 @@ _REGISTRY = {
     "bigdl.bn.atomicStats": (bool, False, "conv epilogues ADD the BN statistics into a [2C] buffer with fp32 atomics and the BN runs as ONE finalize+apply launch (forward and backward); off (or bigdl.deterministic) = per-tile partial rows + fold/finalize kernels, bit-reproducible. Off by default: the same-address atomics from thousands of tiles cost more conv time than the fold launches they remove (25.04 vs 23.09 ms/step, profiles/r4_bn_atomic_ab.txt)"),
     "bigdl.syncbn.ownComm": (bool, True, "SyncBN statistics all-reduces run over a communicator of their own (own RCCL stream), not the one the gradient buckets use"),
     "bigdl.bn.statReplicas": (int, 32, "R > 0 (with atomicStats off): conv epilogues ADD the BN statistics into R replicas (tile tm → replica tm % R) of a zeroed buffer — R-fold less same-address atomic contention than atomicStats, and the BN finalizes from R rows with no fold pass; 0 = per-tile partial rows. Default 32: 22.50 vs 22.94 ms/step (profiles/r4_bn_replicas_ab.txt)"),
+    "bigdl.bn.foldFinalize": (bool, False, "training BN from a conv's replicated statistics in ONE launch per pass: every apply block reduces the replicas itself (no finalize kernel), block 0 updates the running statistics and clears the other of two alternating replica sets; the statistics shift is the previous step's batch mean (a two-buffer ring), so no block reads what block 0 writes. Off: 22.45 vs 21.05 ms/step — re-reducing the R·C replica rows in each of ~1000 apply blocks costs more than the finalize launches it removes (profiles/r5_bn_fold_ab.txt)"),
     "bigdl.bn.syncOneRankLocal": (bool, True, "a SyncBN whose sync group has ONE rank (also the forced world-size-1 rehearsal) runs the local BN kernels: the all-reduce is the identity there, so the compaction of the statistics replicas and the one-launch global finalize+apply are skipped; False rehearses the multi-rank kernels at one rank"),
     "bigdl.bn.shiftedStats": (bool, True, "conv-epilogue BN statistics as Σ(y−K), Σ(y−K)² with K = the BN running mean"),
     "bigdl.checkpoint.async": (bool, True, "trigger-driven checkpoints: host snapshot on the training thread, serialise + write on a writer thread"),

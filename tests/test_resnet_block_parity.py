@@ -147,7 +147,15 @@ def test_atomic_bn_statistics_match_partials_path(name, mode):
             bns = [mod for mod in m.flattened_modules() if isinstance(mod, SpatialBatchNormalization)]
             if atomic:
                 keys = ("_sums_fwd", "_sums_bwd") if mode == "atomic" else ("_rep_fwd", "_rep_bwd")
-                bufs = [mod.__dict__.get(k) for mod in bns for k in keys]
+                # replica sets alternate per step (bigdl.bn.foldFinalize): the set the NEXT producer adds
+                # into (the current one after the consumer's flip) must be zero
+                bufs = []
+                for mod in bns:
+                    for k in keys:
+                        v = mod.__dict__.get(k)
+                        if isinstance(v, list):
+                            v = v[mod.__dict__["_repi_" + k[len("_rep_"):]]]
+                        bufs.append(v)
                 assert sum(b is not None for b in bufs) >= len(bns), "the atomic path was not taken"
                 assert all(b is None or float(b.abs().max()) == 0.0 for b in bufs), "sums not re-zeroed"
             # conv biases feeding a training BN have an exactly-zero gradient (the BN removes the
