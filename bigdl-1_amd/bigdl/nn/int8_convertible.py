@@ -36,6 +36,23 @@ def calc_tensor_scale(t: torch.Tensor, mask: int) -> List[float]:
     return [float(v) for v in a.reshape(-1).tolist()]
 
 
+PERCENTILES = (99.9, 99.99, 99.999)
+
+
+def abs_percentiles(t: torch.Tensor, cap: int = 1 << 22) -> List[float]:
+    """|x| at :data:`PERCENTILES` (a strided sample of at most ``cap`` elements for big tensors)."""
+    a = t.detach().float().abs().reshape(-1)
+    if a.numel() > cap:
+        a = a[:: (a.numel() + cap - 1) // cap]
+    if a.numel() == 0:
+        return [0.0 for _ in PERCENTILES]
+    out = []
+    for p in PERCENTILES:
+        k = min(a.numel(), max(1, int(round(p / 100.0 * a.numel()))))
+        out.append(float(a.kthvalue(k).values))
+    return out
+
+
 def _tensors(act):
     if isinstance(act, torch.Tensor):
         return [act]
@@ -129,6 +146,10 @@ class MklInt8Convertible:
         st = self._i8()
         for t in _tensors(inp):
             st["in"].append(calc_tensor_scale(t, st["inMask"]))
+            if st["inMask"] == 0:
+                # clipping candidates for static int8 activation scales (nn/quantized: the
+                # bigdl.int8.calibration rule), beside the reference's max|x|
+                st.setdefault("in_pct", []).append(abs_percentiles(t))
         for t in _tensors(out):
             st["out"].append(calc_tensor_scale(t, st["outMask"]))
         if weight is not None:

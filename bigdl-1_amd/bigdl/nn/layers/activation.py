@@ -29,8 +29,11 @@ class Threshold(TensorModule):
         if input.dtype == torch.int8 and getattr(input, "_qscale", None) is not None:
             # an int8 activation of a quantised chain (its producer usually applied this ReLU already)
             if self.threshold == 0.0 and self.value == 0.0:
-                y = input if getattr(self, "_i8_fused", False) else input.clamp_min(0)
+                # the unsigned (offset) code is non-negative by construction; the signed one clamps
+                fused = getattr(self, "_i8_fused", False) or getattr(input, "_qzero", 0)
+                y = input if fused else input.clamp_min(0)
                 y._qscale = input._qscale
+                y._qzero = getattr(input, "_qzero", 0)
                 return y
             from ..quantized.layers import dequant
             input = dequant(input)

@@ -22,20 +22,43 @@ def _kp(k: int) -> int:
 
 
 def calibrated_scale(m):
-    """The static activation scale amax / 127 of a float module's calibrated input
-    (``calcScales`` records max|x| per calibration batch, mask 0 — one value per call; the largest is
-    kept, as ``MklInt8Convertible`` does), or None when the module was never calibrated."""
+    """The static activation scale clip / 127 of a float module's calibrated input, or None when the
+    module was never calibrated.  ``bigdl.int8.calibration``: "max" clips at the largest max|x| over
+    the calibration batches (``MklInt8Convertible``'s rule); "p99.9" / "p99.99" / "p99.999" at that
+    percentile of |x| (the largest over the batches) — saturating the few outliers buys the bulk of a
+    heavy-tailed ReLU activation finer steps."""
+    from ...utils import config
+    from ..int8_convertible import PERCENTILES
     st = m.__dict__.get("_int8_state")
     if not st or not st.get("in") or st.get("inMask", 0) != 0:
         return None
     amax = max(float(v[0]) for v in st["in"] if v)
+    rule = str(config.get_property("bigdl.int8.calibration"))
+    if rule.startswith("p") and st.get("in_pct"):
+        try:
+            i = PERCENTILES.index(float(rule[1:]))
+        except ValueError:
+            i = None
+        if i is not None:
+            clip = max(float(v[i]) for v in st["in_pct"])
+            if clip > 0:
+                amax = min(amax, clip)
     return amax / 127.0 if amax > 0 else None
 
 
 def dequant(x):
-    """An int8 activation tagged ``_qscale`` back to bf16 (the layer after a chain end that cannot
-    consume int8)."""
-    return (x.float() * x._qscale).to(torch.bfloat16)
+    """An int8 activation tagged ``_qscale`` (and ``_qzero`` for the offset unsigned code) back to
+    bf16 (the layer after a chain end that cannot consume int8)."""
+    return ((x.float() + getattr(x, "_qzero", 0)) * x._qscale).to(torch.bfloat16)
+
+
+def _retag(y, x):
+    """Carry the quantisation tags of ``x`` over to a view ``y`` of it."""
+    for k in ("_qscale", "_qzero"):
+        v = getattr(x, k, None)
+        if v is not None:
+            setattr(y, k, v)
+    return y
 
 
 class _QuantizedBase(TensorModule):
@@ -47,6 +70,8 @@ class _QuantizedBase(TensorModule):
     _out_qscale = None
     #: ... and applies the ReLU that follows it in the epilogue
     _relu_fused = False
+    #: the ReLU'd int8 output uses the unsigned code (offset −128, ``_out_qscale`` = clip / 255)
+    _out_u8 = False
 
     def _quantize_weight(self, w2d: torch.Tensor):
         q, s = ops.reference.quant_rows(w2d.detach().float().cpu())
@@ -138,6 +163,22 @@ class SpatialConvolution(_QuantizedBase):
                                 self.bias_f.to(x.device).float().contiguous() if self.bias_f is not None else None)
         return prep
 
+    def _u8_tables(self, x, prep, C, pads):
+        """Offset-correction tables for an unsigned (offset) int8 input (bias with the offset term,
+        border deficits), cached per (device, input size, input scale)."""
+        from ...ops import native_ops as NO
+        if not getattr(x, "_qzero", 0):
+            return None
+        key = (x.device, x.shape[2], x.shape[3], x._qscale)
+        t = getattr(self, "_i8u8", None)
+        if t is None or t[0] != key:
+            tabs = NO.conv_i8_u8_tables(prep[0], prep[1], self.nOutputPlane, self.kernelH, self.kernelW, C, x.shape[2],
+                                        x.shape[3], self._out_hw(x, pads), (self.strideH, self.strideW),
+                                        (pads[0], pads[2]), (self.dilationH, self.dilationW), x._qscale, prep[2],
+                                        prep[3])
+            t = self._i8u8 = (key, tabs)
+        return t[1]
+
     def _out_hw(self, x, pads):
         pt, pb, pl, pr = pads
         H, W = x.shape[2], x.shape[3]
@@ -163,7 +204,8 @@ class SpatialConvolution(_QuantizedBase):
                                                self.kernelH, self.kernelW, (self.strideH, self.strideW), (pt, pl),
                                                (self.dilationH, self.dilationW), self._out_hw(x, pads),
                                                relu=self._relu_fused, in_scale=self.static_scale,
-                                               out_scale=self._out_qscale)
+                                               out_scale=self._out_qscale, out_u8=self._out_u8,
+                                               u8_tables=self._u8_tables(x, prep, C, pads))
         if x.dtype == torch.int8:
             return NotImplemented
         # a shape the int8 kernel does not tile (the C = 3 RGB stem): bf16 conv with the dequantised
@@ -180,7 +222,7 @@ class SpatialConvolution(_QuantizedBase):
                               relu=self._relu_fused)
         if y is NotImplemented or self._out_qscale is None:
             return y
-        return NO.quant_static(y, self._out_qscale)
+        return NO.quant_static(y, self._out_qscale, u8=self._out_u8)
 
     def _pads(self, x):
         from ..layers.conv import same_padding
@@ -218,11 +260,8 @@ class SpatialConvolution(_QuantizedBase):
         y = self._native_static(x, (pt, pb, pl, pr))
         if y is not NotImplemented:
             if getattr(self, "format", "NCHW") == "NHWC":
-                q = getattr(y, "_qscale", None)
-                y = y.permute(0, 2, 3, 1)
-                if q is not None:
-                    y._qscale = q
-            return y if input.dim() == 4 else y.squeeze(0)
+                y = _retag(y.permute(0, 2, 3, 1), y)
+            return y if input.dim() == 4 else _retag(y.squeeze(0), y)
         if x.dtype == torch.int8:
             x = dequant(x)
         y = self._native_i8(x, (pt, pb, pl, pr))

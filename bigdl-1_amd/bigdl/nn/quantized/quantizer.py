@@ -27,6 +27,9 @@ register(L.Linear, Q.Linear.from_float)
 def _convert(m):
     conv = _REGISTRY.get(type(m))
     if conv is not None:
+        from ...utils import config
+        if type(m) is L.Linear and not config.get_property("bigdl.int8.quantizeLinear"):
+            return m
         return conv(m)
     from ..graph import Graph
     if isinstance(m, Graph):
@@ -55,6 +58,7 @@ def _link_int8_chains(model):
     from ..layers.pooling import SpatialMaxPooling
     from ..layers.dropout import Dropout
     from ...ops import native_ops as NO
+    from ...utils import config
     for s in model.flattened_modules():
         if not isinstance(s, Sequential):
             continue
@@ -83,6 +87,11 @@ def _link_int8_chains(model):
             if relu is not None:
                 a._relu_fused = True
                 relu._i8_fused = True
+                if config.get_property("bigdl.int8.unsignedActivations"):
+                    # a ReLU'd tensor is non-negative: the unsigned code (offset −128) spends all
+                    # 256 levels on [0, clip], halving the step of the signed clip / 127 scale
+                    a._out_u8 = True
+                    a._out_qscale = b.static_scale * 127.0 / 255.0
 
 
 def quantize(model):

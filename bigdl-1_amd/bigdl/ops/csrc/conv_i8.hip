@@ -49,6 +49,16 @@ struct ConvI8Params {
   float sxs;          // static (calibrated) activation scale
   int8_t* yq;         // int8 output [M][ldy] requantised with 1 / out_scale (the next layer's input)
   float out_inv;
+  // unsigned 8-bit activations of a non-negative (post-ReLU) tensor, stored offset by −128 in int8:
+  // x = (q + 128)·s with q ∈ [−128, 127] — twice the resolution of the symmetric int8 scale.  The
+  // offset's share of the dot product, 128·Σ_(taps in the image, c) w, is added back: the host folds
+  // the all-taps part 128·Σ w into the bias; padded taps read 0 and so must not count, and a border
+  // pixel adds its class's deficit ucorr[class][n] = −128·Σ_(taps outside the image, c) w (class =
+  // the numbers of taps cut off at the top / bottom / left / right, < ucls = {RA, RB, SA, SB}).
+  // y_u8: write the (ReLU'd) output that way.
+  const float* ucorr;
+  int ucls[4];
+  int x_u8, y_u8;
 };
 
 template <int BM, int BN, int WM, int WN, int TPT>
@@ -240,11 +250,29 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
   bf16_t* et = reinterpret_cast<bf16_t*>(lds);
   const int pm = lane & 31;
   float sxm[TMI];
+  int ucl[TMI];  // x_u8: the row's border class (0 = interior: its offset term is in the bias)
 #pragma unroll
   for (int j = 0; j < TMI; ++j) {
     const int m = m0 + (b_row0 - BN) + 32 * j + pm;
     sxm[j] = m < p.M ? (p.sx ? p.sx[m / (p.P * p.Q)] : p.sxs) : 0.f;
+    ucl[j] = 0;
+    if (p.x_u8 && m < p.M) {
+      const int pq = m % (p.P * p.Q), pp = pq / p.Q, qq = pq - pp * p.Q;
+      const int h0 = pp * p.sh - p.ph, w0 = qq * p.sw - p.pw;
+      int ra = 0, rb = 0, sa = 0, sb = 0;
+      while (ra < p.R && h0 + ra * p.dh < 0) ++ra;
+      while (rb < p.R - ra && h0 + (p.R - 1 - rb) * p.dh >= p.H) ++rb;
+      while (sa < p.S && w0 + sa * p.dw < 0) ++sa;
+      while (sb < p.S - sa && w0 + (p.S - 1 - sb) * p.dw >= p.W) ++sb;
+      ucl[j] = ((ra * p.ucls[1] + rb) * p.ucls[2] + sa) * p.ucls[3] + sb;
+    }
   }
+  // the border deficit of the −128 offset for output channels n .. n+3 of row j
+  auto offset4 = [&](int j, int n) -> float4 {
+    if (ucl[j] == 0 || n >= p.K) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(p.ucorr + (size_t)ucl[j] * p.K + n);
+  };
+  const float qlo = p.y_u8 ? 0.f : -127.f, qhi = p.y_u8 ? 255.f : 127.f, qoff = p.y_u8 ? 128.f : 0.f;
   if (p.yq) {
     // int8 output: requantise with the consumer's static scale and park the tile as bytes
     // ([BM][BN], 16-B chunk c of row r at chunk c ^ (r & 7)), then one 16-B store per chunk
@@ -265,11 +293,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
         for (int j = 0; j < TMI; ++j) {
           const int ml = (b_row0 - BN) + 32 * j + pm;
           uint32_t packed = 0;
+          const float4 o4 = offset4(j, n0 + nl);
+          const float oa[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+            const float a = (float)acc[i][j][4 * g + e] + oa[e];
+            float v = fmaf(a * sxm[j], s4[e], b4[e]);
             if (p.relu) v = fmaxf(v, 0.f);
-            const float r = fminf(fmaxf(rintf(v * p.out_inv), -127.f), 127.f);
+            const float r = fminf(fmaxf(rintf(v * p.out_inv), qlo), qhi) - qoff;
             packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
           }
           const int off = ml * BN + ((((nl >> 4) ^ (ml & 7)) & (BN / 16 - 1)) << 4) + (nl & 15);
@@ -306,9 +337,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
       for (int j = 0; j < TMI; ++j) {
         const int ml = (b_row0 - BN) + 32 * j + pm;
         float v[4];
+        const float4 o4 = offset4(j, n0 + nl);
+        const float oa[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+          const float a = (float)acc[i][j][4 * g + e] + oa[e];
+          v[e] = fmaf(a * sxm[j], s4[e], b4[e]);
           if (p.relu) v[e] = fmaxf(v[e], 0.f);
         }
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -381,7 +415,8 @@ __global__ void __launch_bounds__(256) k_quant_img(const bf16_t* __restrict__ x,
 // Static (calibrated) quantisation: xq = clamp(rint(x / scale), ±127), 16 elements per thread.
 template <typename T>
 __global__ void __launch_bounds__(256) k_quant_static(const T* __restrict__ x, long long n, float inv,
-                                                      int8_t* __restrict__ xq) {
+                                                      int8_t* __restrict__ xq, int u8) {
+  const float lo = u8 ? 0.f : -127.f, hi = u8 ? 255.f : 127.f, off = u8 ? 128.f : 0.f;
   for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 16; i < n; i += (long long)gridDim.x * 256 * 16) {
     float v[16];
     if constexpr (sizeof(T) == 2) {
@@ -400,7 +435,7 @@ __global__ void __launch_bounds__(256) k_quant_static(const T* __restrict__ x, l
       uint32_t acc = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float r = fminf(fmaxf(rintf(v[4 * k + e] * inv), -127.f), 127.f);
+        const float r = fminf(fmaxf(rintf(v[4 * k + e] * inv), lo), hi) - off;
         acc |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
       }
       w[k] = acc;
@@ -409,13 +444,22 @@ __global__ void __launch_bounds__(256) k_quant_static(const T* __restrict__ x, l
   }
 }
 
-// dtype 0 = fp32, 1 = bf16; n % 16 == 0, 16-B aligned
+// dtype 0 = fp32, 1 = bf16; n % 16 == 0, 16-B aligned; u8: non-negative input stored offset by −128
+BIGDL_EXPORT int bigdl_quant_static2(const void* x, int dtype, long long n, float scale, void* xq, int u8,
+                                     hipStream_t s);
 BIGDL_EXPORT int bigdl_quant_static(const void* x, int dtype, long long n, float scale, void* xq, hipStream_t s) {
+  return bigdl_quant_static2(x, dtype, n, scale, xq, 0, s);
+}
+
+BIGDL_EXPORT int bigdl_quant_static2(const void* x, int dtype, long long n, float scale, void* xq, int u8,
+                                     hipStream_t s) {
   if (!x || !xq || n <= 0 || n % 16 || !(scale > 0.f) || ((uintptr_t)x & 15) || ((uintptr_t)xq & 15))
     return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)bigdl_grid((n + 15) / 16, 256, 16384));
-  if (dtype == 0) hipLaunchKernelGGL(k_quant_static<float>, g, dim3(256), 0, s, (const float*)x, n, 1.f / scale, (int8_t*)xq);
-  else hipLaunchKernelGGL(k_quant_static<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, n, 1.f / scale, (int8_t*)xq);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_quant_static<float>, g, dim3(256), 0, s, (const float*)x, n, 1.f / scale, (int8_t*)xq, u8);
+  else
+    hipLaunchKernelGGL(k_quant_static<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, n, 1.f / scale, (int8_t*)xq, u8);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -508,10 +552,30 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd(const void* x, const void* w, int ldw, const 
                             pw, dh, dw, relu, s);
 }
 
+BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, const float* ucorr, const int* ucls, int x_u8, int y_u8,
+                                    hipStream_t s);
+
 BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
                                     int dh, int dw, int relu, hipStream_t s) {
+  return bigdl_conv_i8_fwd3(x, w, ldw, sx, sxs, swt, bias, y, yq, out_scale, ldy, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph,
+                            pw, dh, dw, relu, nullptr, nullptr, 0, 0, s);
+}
+
+BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, const float* ucorr, const int* ucls, int x_u8, int y_u8,
+                                    hipStream_t s) {
+  // x_u8: ucls (host array) = the border-class grid {RA, RB, SA, SB}; ucorr device [RA·RB·SA·SB][K]
+  if ((x_u8 && (!ucorr || !ucls)) || (y_u8 && !yq)) return (int)hipErrorInvalidValue;
+  if (x_u8 && (ucls[0] < 1 || ucls[1] < 1 || ucls[2] < 1 || ucls[3] < 1 || ucls[0] > R + 1 || ucls[1] > R + 1 ||
+               ucls[2] > S + 1 || ucls[3] > S + 1))
+    return (int)hipErrorInvalidValue;
   if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)
     return (int)hipErrorInvalidValue;
   if (yq && (K % 16 || ldy % 16 || ((uintptr_t)yq & 15) || !(out_scale > 0.f))) return (int)hipErrorInvalidValue;
@@ -529,6 +593,8 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
   p.M = (int)Ml; p.KT = KT; p.ldw = ldw; p.ldy = ldy; p.relu = relu;
   p.sxs = sxs; p.yq = (int8_t*)yq; p.out_inv = yq ? 1.f / out_scale : 1.f;
+  p.ucorr = ucorr; p.x_u8 = x_u8; p.y_u8 = y_u8;
+  for (int i = 0; i < 4; ++i) p.ucls[i] = x_u8 ? ucls[i] : 1;
   constexpr int BM = 256, BN = 128;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;

@@ -33,7 +33,68 @@ def test_int8_chain_links_after_calibration():
     # conv1 → conv2 → (pool) → conv3 → conv4: three producers write int8 for their consumer
     assert [c._out_qscale is not None for c in convs] == [True, True, True, False]
     assert all(c._relu_fused for c in convs[:3])
+    # ReLU'd producers write the unsigned (offset −128) code: clip / 255 instead of clip / 127
+    assert all(c._out_u8 for c in convs[:3])
+    assert convs[0]._out_qscale == pytest.approx(convs[1].static_scale * 127 / 255)
+
+
+def test_int8_chain_signed_when_unsigned_disabled():
+    from bigdl.nn.quantized import layers as Q
+    from bigdl.utils import config
+    torch.manual_seed(0)
+    m = _net()
+    m.evaluate()
+    x = torch.randn(4, 3, 16, 16)
+    m.forward(x)
+    m.calcScales(x)
+    old = config.get_property("bigdl.int8.unsignedActivations")
+    config.set_property("bigdl.int8.unsignedActivations", False)
+    try:
+        q = m.quantize()
+    finally:
+        config.set_property("bigdl.int8.unsignedActivations", old)
+    convs = [c for c in q.modules if isinstance(c, Q.SpatialConvolution)]
+    assert not any(c._out_u8 for c in convs)
     assert convs[0]._out_qscale == convs[1].static_scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,pad,k", [(1, 1, 3), (2, 1, 3), (1, 0, 1), (2, 0, 1)])
+def test_conv_i8_unsigned_input_matches_fp32(stride, pad, k):
+    """Unsigned (offset −128) int8 input: the kernel's per-tap weight-sum correction (border pixels
+    sum their in-image taps only) reproduces the fp32 conv of the dequantised operands."""
+    from bigdl.ops import native_ops as NO
+    from bigdl.ops import reference as R
+    torch.manual_seed(0)
+    N, C, H, W, K = 2, 64, 9, 11, 32
+    x = torch.rand(N, C, H, W, device="cuda") * 3.0
+    w = torch.randn(K, C, k, k, device="cuda")
+    bias = torch.randn(K, device="cuda")
+    q, ws = R.quant_rows(w.reshape(K, -1).cpu())
+    q, ws = q.cuda(), ws.cuda().float()
+    wq, ldw = NO.conv_i8_weight(q, K, C, k, k)
+    P = (H + 2 * pad - k) // stride + 1
+    Q_ = (W + 2 * pad - k) // stride + 1
+    sx = 3.0 / 255
+    xc = x.contiguous(memory_format=torch.channels_last)
+    xq = NO.quant_static(xc, sx, u8=True)
+    assert xq._qzero == 128
+    xd = (xq.float() + 128) * sx
+    assert float((xd - x).abs().max()) <= sx / 2 + 1e-6
+    wd = (q[:, :C * k * k].float() * ws[:, None]).reshape(K, C, k, k)
+    ref = torch.nn.functional.conv2d(xd, wd, bias, stride, pad)
+    for relu, out_u8 in ((False, False), (True, True)):
+        y = NO.conv2d_i8_forward_static(xq, wq, ldw, ws, bias, K, k, k, (stride, stride), (pad, pad), (1, 1),
+                                        (P, Q_), relu=relu, out_scale=0.05 if out_u8 else None, out_u8=out_u8)
+        assert y is not NotImplemented
+        if out_u8:
+            r = torch.relu(ref)
+            got = (y.float() + 128) * 0.05
+            exp = (r / 0.05).round().clamp(0, 255) * 0.05
+            assert float((got - exp).abs().max()) <= 0.05 + 1e-4
+        else:
+            err = float((y.float() - ref).abs().max() / ref.abs().max())
+            assert err < 1e-2, err
 
 
 @pytest.mark.gpu
@@ -64,3 +125,39 @@ def test_int8_static_chain_matches_float_on_gpu():
     cos = float(a @ b / (a.norm() * b.norm()))
     assert cos >= 0.99, cos
     assert ops.fallback_counts() == {}
+
+
+@pytest.mark.parametrize("stride,pad,k,dil", [(1, 1, 3, 1), (2, 1, 3, 1), (1, 0, 1, 1), (2, 3, 7, 1), (1, 2, 3, 2)])
+def test_u8_offset_tables_reproduce_float_conv(stride, pad, k, dil):
+    """The host tables of the unsigned-input int8 conv (bias with the all-taps offset term, border
+    deficits per class): the kernel's arithmetic — integer conv of the stored codes with zero
+    padding, plus the row's class deficit, scaled, plus the bias — equals the float conv of the
+    dequantised input, on every pixel (borders included)."""
+    from bigdl.ops import native_ops as NO
+    torch.manual_seed(0)
+    N, C, H, W, K = 2, 16, 9, 10, 8
+    q = torch.randint(-128, 128, (N, C, H, W)).double()
+    wi = torch.randint(-127, 128, (K, C, k, k))
+    ldw = k * k * C + 32
+    wq = torch.zeros(K, ldw, dtype=torch.int8)
+    wq[:, :k * k * C] = wi.permute(0, 2, 3, 1).reshape(K, -1).to(torch.int8)
+    sx, sw, bias = 0.01, torch.rand(K) * 0.02, torch.randn(K)
+    P = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    Q = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    b2, ucorr, (RA, RB, SA, SB) = NO.conv_i8_u8_tables(wq, ldw, K, k, k, C, H, W, (P, Q), (stride, stride),
+                                                       (pad, pad), (dil, dil), sx, sw, bias)
+    acc = torch.nn.functional.conv2d(q, wi.double(), None, stride, pad, dil)
+    cls = torch.zeros(P, Q, dtype=torch.long)
+    for pp in range(P):
+        for qq in range(Q):
+            h0, w0 = pp * stride - pad, qq * stride - pad
+            ra = next((a for a in range(k) if h0 + a * dil >= 0), k)
+            rb = next((b for b in range(k - ra) if h0 + (k - 1 - b) * dil < H), k - ra)
+            sa = next((a for a in range(k) if w0 + a * dil >= 0), k)
+            sb = next((b for b in range(k - sa) if w0 + (k - 1 - b) * dil < W), k - sa)
+            cls[pp, qq] = ((ra * RB + rb) * SA + sa) * SB + sb
+    corr = ucorr.double()[cls].permute(2, 0, 1)  # [K, P, Q]
+    got = (acc + corr) * sx * sw.double()[:, None, None] + b2.double()[:, None, None]
+    ref = torch.nn.functional.conv2d((q + 128) * sx, wi.double() * sw.double()[:, None, None, None], bias.double(),
+                                     stride, pad, dil)
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-4), float((got - ref).abs().max())

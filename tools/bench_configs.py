@@ -424,7 +424,15 @@ def bench_int8(args):
             with torch.no_grad():
                 cal.forward(xc)
             cal.calcScales(xc)
-            m = cal.quantize()
+            # the FC head (3 GEMMs on a 128-row batch: weight-bandwidth bound, 1 % of the FLOPs)
+            # stays in bf16 unless --int8-fc: measured faster and no less accurate
+            # (profiles/r5_int8_calibration_sweep.txt)
+            old_fc = config.get_property("bigdl.int8.quantizeLinear")
+            config.set_property("bigdl.int8.quantizeLinear", bool(args.int8_fc))
+            try:
+                m = cal.quantize()
+            finally:
+                config.set_property("bigdl.int8.quantizeLinear", old_fc)
             del cal
         elif mode == "int8":
             m = base.quantize()
@@ -464,6 +472,9 @@ def bench_int8(args):
             "int8_over_bf16": round(res["int8"]["value"] / res["bf16"]["value"], 3),
             "reference_int8_over_fp32": 2.04, "cosine_int8_vs_fp32": round(cos, 5), "calibration_images": args.calib,
             "cosine_image_dependent": round(cos_img, 5), "top1_agreement": top1,
+            "calibration": str(config.get_property("bigdl.int8.calibration")),
+            "unsigned_activations": bool(config.get_property("bigdl.int8.unsignedActivations")),
+            "fc_dtype": "int8" if (args.int8_fc or args.calib <= 0) else "bf16",
             "logit_spread_fp32": round(float(cf.std()), 5)}
 
 
@@ -480,6 +491,7 @@ def main():
     ap.add_argument("--seq-len", type=int, default=20)
     ap.add_argument("--hidden", type=int, default=200)
     ap.add_argument("--calib", type=int, default=32, help="int8: calibration images (0 = per-image dynamic scales)")
+    ap.add_argument("--int8-fc", type=int, default=0, help="int8 (calibrated): quantize the Linear layers too")
     ap.add_argument("--tune", action="store_true", help="vgg: pin autotuned conv tiles before timing")
     ap.add_argument("--compiled", action="store_true", help="inception: run through nn.compiled (kernel selection + HIP graph)")
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
