@@ -54,7 +54,7 @@ def dequant(x):
 
 def _retag(y, x):
     """Carry the quantisation tags of ``x`` over to a view ``y`` of it."""
-    for k in ("_qscale", "_qzero"):
+    for k in ("_qscale", "_qzero", "_qtail"):
         v = getattr(x, k, None)
         if v is not None:
             setattr(y, k, v)
@@ -163,20 +163,17 @@ class SpatialConvolution(_QuantizedBase):
                                 self.bias_f.to(x.device).float().contiguous() if self.bias_f is not None else None)
         return prep
 
-    def _u8_tables(self, x, prep, C, pads):
-        """Offset-correction tables for an unsigned (offset) int8 input (bias with the offset term,
-        border deficits), cached per (device, input size, input scale)."""
+    def _u8_bias(self, x, prep, C):
+        """The bias with the offset term of an unsigned (offset) int8 input, cached per (device,
+        input scale)."""
         from ...ops import native_ops as NO
         if not getattr(x, "_qzero", 0):
             return None
-        key = (x.device, x.shape[2], x.shape[3], x._qscale)
+        key = (x.device, x._qscale)
         t = getattr(self, "_i8u8", None)
         if t is None or t[0] != key:
-            tabs = NO.conv_i8_u8_tables(prep[0], prep[1], self.nOutputPlane, self.kernelH, self.kernelW, C, x.shape[2],
-                                        x.shape[3], self._out_hw(x, pads), (self.strideH, self.strideW),
-                                        (pads[0], pads[2]), (self.dilationH, self.dilationW), x._qscale, prep[2],
-                                        prep[3])
-            t = self._i8u8 = (key, tabs)
+            t = self._i8u8 = (key, NO.conv_i8_u8_bias(prep[0], prep[1], self.nOutputPlane, self.kernelH, self.kernelW,
+                                                      C, x._qscale, prep[2], prep[3]))
         return t[1]
 
     def _out_hw(self, x, pads):
@@ -205,7 +202,7 @@ class SpatialConvolution(_QuantizedBase):
                                                (self.dilationH, self.dilationW), self._out_hw(x, pads),
                                                relu=self._relu_fused, in_scale=self.static_scale,
                                                out_scale=self._out_qscale, out_u8=self._out_u8,
-                                               u8_tables=self._u8_tables(x, prep, C, pads))
+                                               u8_bias=self._u8_bias(x, prep, C))
         if x.dtype == torch.int8:
             return NotImplemented
         # a shape the int8 kernel does not tile (the C = 3 RGB stem): bf16 conv with the dequantised

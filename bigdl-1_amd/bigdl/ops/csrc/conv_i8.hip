@@ -51,13 +51,10 @@ struct ConvI8Params {
   float out_inv;
   // unsigned 8-bit activations of a non-negative (post-ReLU) tensor, stored offset by −128 in int8:
   // x = (q + 128)·s with q ∈ [−128, 127] — twice the resolution of the symmetric int8 scale.  The
-  // offset's share of the dot product, 128·Σ_(taps in the image, c) w, is added back: the host folds
-  // the all-taps part 128·Σ w into the bias; padded taps read 0 and so must not count, and a border
-  // pixel adds its class's deficit ucorr[class][n] = −128·Σ_(taps outside the image, c) w (class =
-  // the numbers of taps cut off at the top / bottom / left / right, < ucls = {RA, RB, SA, SB}).
-  // y_u8: write the (ReLU'd) output that way.
-  const float* ucorr;
-  int ucls[4];
+  // offset's share of the dot product, 128·Σ_(taps, c) w, is a per-channel constant the host folds
+  // into the bias, provided a padded tap reads the code of x = 0, −128: such an input carries a
+  // 16-byte tail of 0x80 right after its last byte and the loader points padded taps at it.
+  // y_u8: write the (ReLU'd) output that way, tail included.
   int x_u8, y_u8;
 };
 
@@ -83,9 +80,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
 
   const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.C);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.ldw);
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)(x_bytes + (p.x_u8 ? 16u : 0u)), 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)w_bytes, 0x00020000);
   constexpr uint32_t OOB = 0x80000000u;
+  const uint32_t XPAD = p.x_u8 ? x_bytes : OOB;  // a padded tap: the 0x80 tail, or zero-fill
   const int RS = p.R * p.S;
 
   const int lrow = lane >> 3, slot = lane & 7;
@@ -178,10 +177,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
         const bool hi = chunk >= 4;
         const int tap = hi ? tap_b : tap_a;
         const bool ok = tap < RS && ((vmask[j] >> tap) & 1ull);
-        off = ok ? (uint32_t)(rbase[j] + (hi ? off_b : off_a)) : OOB;
+        off = ok ? (uint32_t)(rbase[j] + (hi ? off_b : off_a)) : XPAD;
       } else {
         const bool ok = (vmask[j] >> tap_a) & 1ull;
-        off = ok ? (uint32_t)(rbase[j] + off_a + c0) : OOB;
+        off = ok ? (uint32_t)(rbase[j] + off_a + c0) : XPAD;
       }
       i8_glds16(xr, dst, off);
     }
@@ -250,28 +249,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
   bf16_t* et = reinterpret_cast<bf16_t*>(lds);
   const int pm = lane & 31;
   float sxm[TMI];
-  int ucl[TMI];  // x_u8: the row's border class (0 = interior: its offset term is in the bias)
 #pragma unroll
   for (int j = 0; j < TMI; ++j) {
     const int m = m0 + (b_row0 - BN) + 32 * j + pm;
     sxm[j] = m < p.M ? (p.sx ? p.sx[m / (p.P * p.Q)] : p.sxs) : 0.f;
-    ucl[j] = 0;
-    if (p.x_u8 && m < p.M) {
-      const int pq = m % (p.P * p.Q), pp = pq / p.Q, qq = pq - pp * p.Q;
-      const int h0 = pp * p.sh - p.ph, w0 = qq * p.sw - p.pw;
-      int ra = 0, rb = 0, sa = 0, sb = 0;
-      while (ra < p.R && h0 + ra * p.dh < 0) ++ra;
-      while (rb < p.R - ra && h0 + (p.R - 1 - rb) * p.dh >= p.H) ++rb;
-      while (sa < p.S && w0 + sa * p.dw < 0) ++sa;
-      while (sb < p.S - sa && w0 + (p.S - 1 - sb) * p.dw >= p.W) ++sb;
-      ucl[j] = ((ra * p.ucls[1] + rb) * p.ucls[2] + sa) * p.ucls[3] + sb;
-    }
   }
-  // the border deficit of the −128 offset for output channels n .. n+3 of row j
-  auto offset4 = [&](int j, int n) -> float4 {
-    if (ucl[j] == 0 || n >= p.K) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(p.ucorr + (size_t)ucl[j] * p.K + n);
-  };
   const float qlo = p.y_u8 ? 0.f : -127.f, qhi = p.y_u8 ? 255.f : 127.f, qoff = p.y_u8 ? 128.f : 0.f;
   if (p.yq) {
     // int8 output: requantise with the consumer's static scale and park the tile as bytes
@@ -293,12 +275,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
         for (int j = 0; j < TMI; ++j) {
           const int ml = (b_row0 - BN) + 32 * j + pm;
           uint32_t packed = 0;
-          const float4 o4 = offset4(j, n0 + nl);
-          const float oa[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float a = (float)acc[i][j][4 * g + e] + oa[e];
-            float v = fmaf(a * sxm[j], s4[e], b4[e]);
+            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
             if (p.relu) v = fmaxf(v, 0.f);
             const float r = fminf(fmaxf(rintf(v * p.out_inv), qlo), qhi) - qoff;
             packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
@@ -319,6 +298,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
         *reinterpret_cast<uint4*>(p.yq + (size_t)m * p.ldy + n) = v;
       }
     }
+    // the unsigned code's padding tail (the code of 0) for the consumer's padded taps
+    if (p.y_u8 && blockIdx.x == 0 && tid == 0)
+      *reinterpret_cast<uint4*>(p.yq + (size_t)p.M * p.ldy) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u,
+                                                                         0x80808080u);
     return;
   }
 #pragma unroll
@@ -337,12 +320,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
       for (int j = 0; j < TMI; ++j) {
         const int ml = (b_row0 - BN) + 32 * j + pm;
         float v[4];
-        const float4 o4 = offset4(j, n0 + nl);
-        const float oa[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = (float)acc[i][j][4 * g + e] + oa[e];
-          v[e] = fmaf(a * sxm[j], s4[e], b4[e]);
+          v[e] = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
           if (p.relu) v[e] = fmaxf(v[e], 0.f);
         }
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -417,6 +397,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_quant_static(const T* __restrict__ x, long long n, float inv,
                                                       int8_t* __restrict__ xq, int u8) {
   const float lo = u8 ? 0.f : -127.f, hi = u8 ? 255.f : 127.f, off = u8 ? 128.f : 0.f;
+  if (u8 && blockIdx.x == 0 && threadIdx.x == 0)
+    *reinterpret_cast<uint4*>(xq + n) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
   for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 16; i < n; i += (long long)gridDim.x * 256 * 16) {
     float v[16];
     if constexpr (sizeof(T) == 2) {
@@ -453,6 +435,7 @@ BIGDL_EXPORT int bigdl_quant_static(const void* x, int dtype, long long n, float
 
 BIGDL_EXPORT int bigdl_quant_static2(const void* x, int dtype, long long n, float scale, void* xq, int u8,
                                      hipStream_t s) {
+  // u8: xq has 16 more bytes, the padding tail (0x80) of the unsigned code
   if (!x || !xq || n <= 0 || n % 16 || !(scale > 0.f) || ((uintptr_t)x & 15) || ((uintptr_t)xq & 15))
     return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)bigdl_grid((n + 15) / 16, 256, 16384));
@@ -468,9 +451,11 @@ BIGDL_EXPORT int bigdl_quant_static2(const void* x, int dtype, long long n, floa
 // positions outside the input are skipped; P, Q given (ceil / floor mode decided by the caller).
 __global__ void __launch_bounds__(256) k_maxpool_i8(const int8_t* __restrict__ x, int8_t* __restrict__ y, int Nb,
                                                     int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
-                                                    int ph, int pw) {
+                                                    int ph, int pw, int tail) {
   const int CG = C >> 4;
   const long long total = (long long)Nb * P * Q * CG;
+  if (tail && blockIdx.x == 0 && threadIdx.x == 0)  // the unsigned code's padding tail
+    *reinterpret_cast<uint4*>(y + total * 16) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
   for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int cg = (int)(t % CG);
     const long long pix = t / CG;
@@ -504,14 +489,22 @@ __global__ void __launch_bounds__(256) k_maxpool_i8(const int8_t* __restrict__ x
   }
 }
 
+BIGDL_EXPORT int bigdl_maxpool_i8_t(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
+                                    int sh, int sw, int ph, int pw, int tail, hipStream_t s);
 BIGDL_EXPORT int bigdl_maxpool_i8(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
                                   int sh, int sw, int ph, int pw, hipStream_t s) {
+  return bigdl_maxpool_i8_t(x, y, Nb, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, 0, s);
+}
+
+// tail: y has 16 more bytes after its last one, set to 0x80 (an unsigned-code input's padding)
+BIGDL_EXPORT int bigdl_maxpool_i8_t(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
+                                    int sh, int sw, int ph, int pw, int tail, hipStream_t s) {
   if (!x || !y || Nb <= 0 || C % 16 || P <= 0 || Q <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 ||
       ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
     return (int)hipErrorInvalidValue;
   const long long total = (long long)Nb * P * Q * (C / 16);
   hipLaunchKernelGGL(k_maxpool_i8, dim3((unsigned)bigdl_grid(total, 256, 65536)), dim3(256), 0, s, (const int8_t*)x,
-                     (int8_t*)y, Nb, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+                     (int8_t*)y, Nb, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, tail);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -555,27 +548,23 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd(const void* x, const void* w, int ldw, const 
 BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
-                                    int dh, int dw, int relu, const float* ucorr, const int* ucls, int x_u8, int y_u8,
-                                    hipStream_t s);
+                                    int dh, int dw, int relu, int x_u8, int y_u8, hipStream_t s);
 
 BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
                                     int dh, int dw, int relu, hipStream_t s) {
   return bigdl_conv_i8_fwd3(x, w, ldw, sx, sxs, swt, bias, y, yq, out_scale, ldy, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph,
-                            pw, dh, dw, relu, nullptr, nullptr, 0, 0, s);
+                            pw, dh, dw, relu, 0, 0, s);
 }
 
 BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
-                                    int dh, int dw, int relu, const float* ucorr, const int* ucls, int x_u8, int y_u8,
-                                    hipStream_t s) {
-  // x_u8: ucls (host array) = the border-class grid {RA, RB, SA, SB}; ucorr device [RA·RB·SA·SB][K]
-  if ((x_u8 && (!ucorr || !ucls)) || (y_u8 && !yq)) return (int)hipErrorInvalidValue;
-  if (x_u8 && (ucls[0] < 1 || ucls[1] < 1 || ucls[2] < 1 || ucls[3] < 1 || ucls[0] > R + 1 || ucls[1] > R + 1 ||
-               ucls[2] > S + 1 || ucls[3] > S + 1))
-    return (int)hipErrorInvalidValue;
+                                    int dh, int dw, int relu, int x_u8, int y_u8, hipStream_t s) {
+  // x_u8: x holds 16 bytes of 0x80 after its last byte (and the bias carries the offset term);
+  // y_u8: yq is dense (ldy == K) with room for that tail
+  if (y_u8 && (!yq || ldy != K)) return (int)hipErrorInvalidValue;
   if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)
     return (int)hipErrorInvalidValue;
   if (yq && (K % 16 || ldy % 16 || ((uintptr_t)yq & 15) || !(out_scale > 0.f))) return (int)hipErrorInvalidValue;
@@ -593,8 +582,7 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
   p.M = (int)Ml; p.KT = KT; p.ldw = ldw; p.ldy = ldy; p.relu = relu;
   p.sxs = sxs; p.yq = (int8_t*)yq; p.out_inv = yq ? 1.f / out_scale : 1.f;
-  p.ucorr = ucorr; p.x_u8 = x_u8; p.y_u8 = y_u8;
-  for (int i = 0; i < 4; ++i) p.ucls[i] = x_u8 ? ucls[i] : 1;
+  p.x_u8 = x_u8; p.y_u8 = y_u8;
   constexpr int BM = 256, BN = 128;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;

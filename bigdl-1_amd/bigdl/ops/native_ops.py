@@ -1756,22 +1756,41 @@ def conv2d_i8_forward(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation,
     return y
 
 
+def _i8_act(N_, C_, H, W, dev, tail):
+    """An int8 NHWC activation (logical NCHW, channels-last); ``tail``: 16 more bytes after it in
+    the same allocation, which the kernels that write the unsigned code fill with 0x80 (the code of
+    0, read by a consumer conv for its padded taps)."""
+    n = N_ * C_ * H * W
+    if not tail:
+        return torch.empty((N_, C_, H, W), dtype=torch.int8, device=dev, memory_format=torch.channels_last)
+    buf = torch.empty(n + 16, dtype=torch.int8, device=dev)
+    return buf[:n].view(N_, H, W, C_).permute(0, 3, 1, 2)
+
+
+def _tag(t, scale, u8):
+    t._qscale = float(scale) if scale is not None else None
+    t._qzero = 128 if u8 else 0
+    t._qtail = bool(u8)
+    return t
+
+
 def quant_static(x, scale, u8=False):
     """Calibrated (static) int8 quantisation of a channels-last fp32 / bf16 activation with one
     scale: int8 tensor of the same logical shape and memory layout, tagged ``_qscale``.  ``u8``: the
     input is non-negative (post-ReLU) and is stored as unsigned 8-bit offset by −128 (tagged
-    ``_qzero = 128``: x = (q + 128)·scale), doubling the resolution of the signed code."""
+    ``_qzero = 128``: x = (q + 128)·scale, with the 0x80 padding tail), doubling the resolution of
+    the signed code."""
     if not (x.is_cuda and x.dtype in (_f32, _bf16) and x.numel() % 16 == 0 and _al16(x)):
         return NotImplemented
     cl = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
     if not (cl or x.is_contiguous()):
         return NotImplemented
-    xq = torch.empty_like(x, dtype=torch.int8)
+    if u8 and not cl:
+        return NotImplemented
+    xq = _i8_act(*x.shape, x.device, True) if u8 else torch.empty_like(x, dtype=torch.int8)
     check(_lib().bigdl_quant_static2(ptr(x), C.c_int(0 if x.dtype == _f32 else 1), _ll(x.numel()), C.c_float(scale),
                                      ptr(xq), C.c_int(1 if u8 else 0), _s()), "quant_static")
-    xq._qscale = float(scale)
-    xq._qzero = 128 if u8 else 0
-    return xq
+    return _tag(xq, scale, u8)
 
 
 def maxpool_i8(x, kh, kw, sh, sw, ph, pw, P, Q):
@@ -1781,58 +1800,29 @@ def maxpool_i8(x, kh, kw, sh, sw, ph, pw, P, Q):
             and x.shape[1] % 16 == 0 and _al16(x)):
         return NotImplemented
     N_, C_, H, W = x.shape
-    y = torch.empty((N_, C_, P, Q), dtype=torch.int8, device=x.device, memory_format=torch.channels_last)
-    check(_lib().bigdl_maxpool_i8(ptr(x), ptr(y), N_, H, W, C_, P, Q, kh, kw, sh, sw, ph, pw, _s()), "maxpool_i8")
-    y._qscale = getattr(x, "_qscale", None)
-    y._qzero = getattr(x, "_qzero", 0)  # the offset code is monotone too
-    return y
+    u8 = bool(getattr(x, "_qzero", 0))  # the offset code is monotone too
+    y = _i8_act(N_, C_, P, Q, x.device, u8)
+    check(_lib().bigdl_maxpool_i8_t(ptr(x), ptr(y), N_, H, W, C_, P, Q, kh, kw, sh, sw, ph, pw, C.c_int(int(u8)), _s()),
+          "maxpool_i8")
+    return _tag(y, getattr(x, "_qscale", None), u8)
 
 
-def _cut_counts(n_out, size, k, stride, pad, dil):
-    """The distinct (taps cut off before, taps cut off after) pairs of one spatial axis."""
-    pairs = set()
-    for o in range(n_out):
-        h0 = o * stride - pad
-        a = 0
-        while a < k and h0 + a * dil < 0:
-            a += 1
-        b = 0
-        while b < k - a and h0 + (k - 1 - b) * dil >= size:
-            b += 1
-        pairs.add((a, b))
-    return pairs
-
-
-def conv_i8_u8_tables(wq, ldw, K, R, S, C_, H, W, out_hw, stride, pad, dilation, sx, w_scale, bias):
-    """Host tables for an unsigned (offset −128) int8 input of the int8 conv: the bias with the
-    all-taps offset term 128·Σw·sx·sw folded in, and the border deficits ucorr[class][K] =
-    −128·Σ_(taps outside the image) w with the class grid {RA, RB, SA, SB} (taps cut off at the top /
-    bottom / left / right) that ``bigdl_conv_i8_fwd3`` indexes.  Returns (bias, ucorr, ucls)."""
-    P, Q = out_hw
-    w = wq.view(torch.int8).reshape(K, ldw)[:, :R * S * C_].reshape(K, R, S, C_).to(torch.int32).sum(-1)
-    wt = w.double()
-    tot = wt.sum((1, 2))
-    rp = _cut_counts(P, H, R, stride[0], pad[0], dilation[0])
-    sp = _cut_counts(Q, W, S, stride[1], pad[1], dilation[1])
-    RA, RB = max(a for a, _ in rp) + 1, max(b for _, b in rp) + 1
-    SA, SB = max(a for a, _ in sp) + 1, max(b for _, b in sp) + 1
-    ucorr = torch.zeros(RA, RB, SA, SB, K, dtype=torch.float64, device=wq.device)
-    for ra, rb in rp:
-        for sa, sb in sp:
-            if ra or rb or sa or sb:
-                ucorr[ra, rb, sa, sb] = 128.0 * (wt[:, ra:R - rb, sa:S - sb].sum((1, 2)) - tot)
-    b = (bias.double() if bias is not None else torch.zeros(K, dtype=torch.float64, device=wq.device))
-    b = b + 128.0 * tot * float(sx) * w_scale.double()
-    return (b.float().contiguous(), ucorr.reshape(-1, K).float().contiguous(), (RA, RB, SA, SB))
+def conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias):
+    """The bias of the int8 conv for an unsigned (offset −128) input of scale ``sx``: the offset's
+    share of the dot product, 128·Σ_(taps, c) w · sx · sw, is a per-channel constant (padded taps
+    read the code of 0 from the input's tail) folded in here."""
+    w = wq.view(torch.int8).reshape(K, ldw)[:, :R * S * C_].to(torch.int32).sum(-1).double()
+    b = bias.double() if bias is not None else torch.zeros(K, dtype=torch.float64, device=wq.device)
+    return (b + 128.0 * w * float(sx) * w_scale.double()).float().contiguous()
 
 
 def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation, out_hw, relu=False,
-                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_tables=None):
+                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_bias=None):
     """int8 conv with calibrated scales: ``x`` int8 NHWC (tagged ``_qscale``, the producer's
     requantised output) or fp32/bf16 quantised here with ``in_scale`` in one static pass; with
     ``out_scale`` the epilogue writes the int8 NHWC input of the next quantised layer (bias, ReLU
     and requantisation fused), else bf16.  ``in_u8`` (fp32/bf16 input known non-negative) / an int8
-    input tagged ``_qzero``: offset −128 u8 input, corrected with ``u8_tables`` (:func:`conv_i8_u8_tables`);
+    input tagged ``_qzero``: offset −128 u8 input (its bias ``u8_bias``, :func:`conv_i8_u8_bias`);
     ``out_u8``: write the (ReLU'd) output that way.  NotImplemented when the kernel does not apply."""
     if not (x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)):
         return NotImplemented
@@ -1852,27 +1842,26 @@ def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, di
             return NotImplemented
         sx = in_scale
     x_u8 = bool(getattr(xq, "_qzero", 0))
+    if x_u8 and not getattr(xq, "_qtail", False):
+        return NotImplemented  # no padding tail to point the padded taps at
     if out_u8 and not (relu and out_scale is not None):
         raise ValueError("conv2d_i8_forward_static: out_u8 needs a fused ReLU and an int8 output")
     P, Q = out_hw
-    odt = torch.int8 if out_scale is not None else _bf16
-    y = torch.empty((N_, K, P, Q), dtype=odt, device=x.device, memory_format=torch.channels_last)
+    if out_scale is not None:
+        y = _i8_act(N_, K, P, Q, x.device, out_u8)
+    else:
+        y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
     b = bias.float().contiguous() if bias is not None else None
-    ucorr = ucls = None
     if x_u8:
-        if u8_tables is None:
-            u8_tables = conv_i8_u8_tables(wq, ldw, K, R, S, C_, H, W, (P, Q), stride, pad, dilation, sx, w_scale, bias)
-        b, ucorr, cls = u8_tables
-        ucls = (C.c_int * 4)(*cls)
+        b = u8_bias if u8_bias is not None else conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias)
     check(_lib().bigdl_conv_i8_fwd3(ptr(xq), ptr(wq), C.c_int(ldw), None, C.c_float(sx), ptr(w_scale), ptr(b),
                                     None if out_scale is not None else ptr(y), ptr(y) if out_scale is not None else None,
                                     C.c_float(out_scale if out_scale is not None else 1.0), C.c_int(K), N_, H, W, C_, K,
                                     R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
-                                    C.c_int(1 if relu else 0), ptr(ucorr) if x_u8 else None, ucls, C.c_int(int(x_u8)),
+                                    C.c_int(1 if relu else 0), C.c_int(int(x_u8)),
                                     C.c_int(int(out_u8)), _s()), "conv_i8_fwd3")
     if out_scale is not None:
-        y._qscale = float(out_scale)
-        y._qzero = 128 if out_u8 else 0
+        _tag(y, out_scale, out_u8)
     return y
 
 

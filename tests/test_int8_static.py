@@ -78,7 +78,9 @@ def test_conv_i8_unsigned_input_matches_fp32(stride, pad, k):
     sx = 3.0 / 255
     xc = x.contiguous(memory_format=torch.channels_last)
     xq = NO.quant_static(xc, sx, u8=True)
-    assert xq._qzero == 128
+    assert xq._qzero == 128 and xq._qtail
+    tail = torch.empty(0, dtype=torch.int8, device="cuda").set_(xq.untyped_storage(), xq.numel(), (16,), (1,))
+    assert bool((tail == -128).all())
     xd = (xq.float() + 128) * sx
     assert float((xd - x).abs().max()) <= sx / 2 + 1e-6
     wd = (q[:, :C * k * k].float() * ws[:, None]).reshape(K, C, k, k)
@@ -89,6 +91,7 @@ def test_conv_i8_unsigned_input_matches_fp32(stride, pad, k):
         assert y is not NotImplemented
         if out_u8:
             r = torch.relu(ref)
+            assert y._qtail
             got = (y.float() + 128) * 0.05
             exp = (r / 0.05).round().clamp(0, 255) * 0.05
             assert float((got - exp).abs().max()) <= 0.05 + 1e-4
@@ -128,11 +131,10 @@ def test_int8_static_chain_matches_float_on_gpu():
 
 
 @pytest.mark.parametrize("stride,pad,k,dil", [(1, 1, 3, 1), (2, 1, 3, 1), (1, 0, 1, 1), (2, 3, 7, 1), (1, 2, 3, 2)])
-def test_u8_offset_tables_reproduce_float_conv(stride, pad, k, dil):
-    """The host tables of the unsigned-input int8 conv (bias with the all-taps offset term, border
-    deficits per class): the kernel's arithmetic — integer conv of the stored codes with zero
-    padding, plus the row's class deficit, scaled, plus the bias — equals the float conv of the
-    dequantised input, on every pixel (borders included)."""
+def test_u8_offset_bias_reproduces_float_conv(stride, pad, k, dil):
+    """The unsigned-input int8 conv's arithmetic — integer conv of the stored codes whose padded taps
+    read the code of 0 (−128, the input's tail), scaled, plus the bias with the offset term folded in
+    (``conv_i8_u8_bias``) — equals the float conv of the dequantised input on every pixel."""
     from bigdl.ops import native_ops as NO
     torch.manual_seed(0)
     N, C, H, W, K = 2, 16, 9, 10, 8
@@ -142,22 +144,10 @@ def test_u8_offset_tables_reproduce_float_conv(stride, pad, k, dil):
     wq = torch.zeros(K, ldw, dtype=torch.int8)
     wq[:, :k * k * C] = wi.permute(0, 2, 3, 1).reshape(K, -1).to(torch.int8)
     sx, sw, bias = 0.01, torch.rand(K) * 0.02, torch.randn(K)
-    P = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
-    Q = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
-    b2, ucorr, (RA, RB, SA, SB) = NO.conv_i8_u8_tables(wq, ldw, K, k, k, C, H, W, (P, Q), (stride, stride),
-                                                       (pad, pad), (dil, dil), sx, sw, bias)
-    acc = torch.nn.functional.conv2d(q, wi.double(), None, stride, pad, dil)
-    cls = torch.zeros(P, Q, dtype=torch.long)
-    for pp in range(P):
-        for qq in range(Q):
-            h0, w0 = pp * stride - pad, qq * stride - pad
-            ra = next((a for a in range(k) if h0 + a * dil >= 0), k)
-            rb = next((b for b in range(k - ra) if h0 + (k - 1 - b) * dil < H), k - ra)
-            sa = next((a for a in range(k) if w0 + a * dil >= 0), k)
-            sb = next((b for b in range(k - sa) if w0 + (k - 1 - b) * dil < W), k - sa)
-            cls[pp, qq] = ((ra * RB + rb) * SA + sa) * SB + sb
-    corr = ucorr.double()[cls].permute(2, 0, 1)  # [K, P, Q]
-    got = (acc + corr) * sx * sw.double()[:, None, None] + b2.double()[:, None, None]
+    b2 = NO.conv_i8_u8_bias(wq, ldw, K, k, k, C, sx, sw, bias)
+    qp = torch.nn.functional.pad(q, (pad, pad, pad, pad), value=-128.0)
+    acc = torch.nn.functional.conv2d(qp, wi.double(), None, stride, 0, dil)
+    got = acc * sx * sw.double()[:, None, None] + b2.double()[:, None, None]
     ref = torch.nn.functional.conv2d((q + 128) * sx, wi.double() * sw.double()[:, None, None, None], bias.double(),
                                      stride, pad, dil)
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-4), float((got - ref).abs().max())
