@@ -208,7 +208,7 @@ def plan(model, example, phase: str = "inference") -> Plan:
 #: forward; (0, 0, 0) is the launcher's shape heuristic.  BK = 1 is the 8-wave 32x32x16 / LDS-DMA
 #: family (ops/csrc/conv_mfma32.hip), which wins on the deep reductions (C ≥ 256 3×3, C ≥ 1024 1×1).
 TILE_CANDIDATES = ((0, 0, 0), (64, 32, 128), (64, 64, 128), (128, 32, 128), (128, 64, 128), (64, 64, 256),
-                   (128, 64, 256), (128, 1, 128), (64, 1, 256), (128, 1, 256))
+                   (128, 64, 256), (128, 1, 128), (64, 1, 256), (128, 1, 256), (256, 1, 256))
 
 #: weight-gradient candidates (target blocks of the pixel split, k-tile pixel depth); 0 = heuristic
 WGRAD_CANDIDATES = ((0, 0), (0, 32), (0, 64), (256, 0), (768, 0), (1024, 0), (256, 32), (768, 64))

@@ -632,10 +632,10 @@ static int conv_env_override(const char* name, int a, int b) {
 // kernel selection (nn/compiled.py autotune times every candidate per conv geometry and launches
 // that conv with the winner).  Valid: BN ∈ {64, 128}, BK ∈ {32, 64}, BM ∈ {128, 256}, BM 256 ⇒ BK 64.
 // BK = 1 selects the 32x32x16 / LDS-DMA family (conv_mfma32.hip, k-tile 64): BM × BN ∈ {128 × 128,
-// 256 × 64, 256 × 128}; it needs C % 64 == 0 and falls back to the 16x16x32 family otherwise.
+// 256 × 64, 256 × 128, 256 × 256}; it needs C % 64 == 0 and falls back to the 16x16x32 family otherwise.
 constexpr int kX8 = 1;
 static bool tile_ok(int bn, int bk, int bm) {
-  if (bk == kX8) return (bm == 128 && bn == 128) || (bm == 256 && (bn == 64 || bn == 128));
+  if (bk == kX8) return (bm == 128 && bn == 128) || (bm == 256 && (bn == 64 || bn == 128 || bn == 256));
   return !((bn && bn != 64 && bn != 128) || (bk && bk != 32 && bk != 64) || (bm && bm != 128 && bm != 256) ||
            (bm == 256 && bk == 32));
 }
@@ -761,7 +761,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
       tile_bn = tile_bk = tile_bm = 0;
     } else if (!tile_bk && !tile_bn && !tile_bm && x8_env) {
       xbm = 256;
-      xbn = K <= 64 ? 64 : 128;
+      xbn = K <= 64 ? 64 : (x8_env == 2 && K >= 256 ? 256 : 128);  // 2: the 256 × 256 tile where K allows
     }
     if (xbm && !ax && !c4 && !cdup) {
       const int xmode = (R == 1 && S == 1 && ph == 0 && pw == 0) ? 3 : 1;

@@ -54,7 +54,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
   constexpr bool PW = MODE == 3;
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BK = 64;
-  constexpr int NS = 3;                        // LDS ring depth
+  // LDS ring depth: 3; the 256 × 256 tile (1.5× the FLOP per staged byte of 256 × 128 — the L2 → LDS
+  // feed, not the MFMA, bounds these convs) has room for 2 (2 × 64 KiB, its epilogue takes all 160)
+  constexpr int NS = BN == 256 ? 2 : 3;
   constexpr int STAGE = (BM + BN) * 128;       // bytes per ring slot (128-B rows)
   constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;  // 8-row DMA groups per wave: weights, activations
   static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
@@ -293,7 +295,23 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
   // 3-deep ring: tile t+2 is issued before tile t is multiplied; the wait after the MFMAs retires
   // only tile t+1 (counted vmcnt = L), and the barrier then publishes it to every wave and frees the
   // slot just read for the next issue.
-  if constexpr (ILV == 1) {
+  if constexpr (NS == 2) {
+    // 2-deep ring: the whole next k-tile is requested before this one's MFMAs (all of its compute
+    // time to land), then a full wait and the barrier that also frees the slot just read
+    stage(0, 0);
+    X8_WAIT(0);
+    X8_BARRIER();
+    int cur = 0;
+    for (int t = 0; t + 1 < KT; ++t) {
+      stage(t + 1, cur ^ 1);
+      compute_ilv(cur, -1, std::false_type{});
+      X8_WAIT(0);
+      X8_BARRIER();
+      cur ^= 1;
+    }
+    compute_ilv(cur, -1, std::false_type{});
+    X8_BARRIER();
+  } else if constexpr (ILV == 1) {
     prep(0);
 #pragma unroll
     for (int i = 0; i < L; ++i) issue(i, 0);
@@ -410,7 +428,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_x8(ConvParams p) {
 // ---- host side ----
 bool conv_x8_ok(int mode, int bm, int bn, const ConvParams& p) {
   if (mode != 1 && mode != 3) return false;
-  if (!((bm == 256 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 128))) return false;
+  if (!((bm == 256 && (bn == 64 || bn == 128 || bn == 256)) || (bm == 128 && bn == 128))) return false;
   if (p.cdup || p.C % 64 || p.Kg % 64 || p.ldx % 8 || p.ldw % 8) return false;
   if (p.T != 1 || p.KT != 1 || p.ax) return false;
   if (mode == 1 && p.R * p.S > 64) return false;
@@ -421,6 +439,8 @@ template <int MODE, int ILV>
 static void launch_x8(int bm, int bn, dim3 g, hipStream_t s, const ConvParams& p) {
   if (bm == 128)
     hipLaunchKernelGGL((k_conv_x8<128, 128, 2, 2, MODE, ILV>), g, dim3(256), 0, s, p);
+  else if (bn == 256)
+    hipLaunchKernelGGL((k_conv_x8<256, 256, 4, 2, MODE, ILV>), g, dim3(512), 0, s, p);
   else if (bn == 64)
     hipLaunchKernelGGL((k_conv_x8<256, 64, 4, 2, MODE, ILV>), g, dim3(512), 0, s, p);
   else

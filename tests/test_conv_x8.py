@@ -9,7 +9,7 @@ import torch
 pytestmark = pytest.mark.gpu
 dev = "cuda"
 
-X8_TILES = [(128, 1, 128), (64, 1, 256), (128, 1, 256)]
+X8_TILES = [(128, 1, 128), (64, 1, 256), (128, 1, 256), (256, 1, 256)]
 
 CASES = [  # N, C, H, W, K, R, S, stride, pad, dilation
     (2, 64, 14, 14, 128, 3, 3, 1, 1, 1),

@@ -54,6 +54,7 @@ def run():
     bs = int(os.environ.get("BS", "256"))
     tot = {"fwd": 0.0, "fwdstats": 0.0, "dgrad": 0.0, "mm": 0.0, "copy": 0.0}
     tot["wgrad"] = 0.0
+    tot["vendor_fwd"] = 0.0
     only3 = os.environ.get("ONLY3") == "1"
     for C, K, s, H, mult, R in ([] if only3 else [v + (1,) for v in SHAPES]) + [v + (3,) for v in SHAPES3]:
         pd = R // 2
@@ -75,6 +76,11 @@ def run():
             t["mm"] = timeit(lambda: torch.mm(a2, w2.t()))
         else:
             t["mm"] = 0.0
+        if os.environ.get("VENDOR_CONV") == "1":
+            # the vendor library's conv of the same shape (torch → MIOpen, NHWC bf16): forward only
+            t["vendor_fwd"] = timeit(lambda: torch.nn.functional.conv2d(x, w, None, s, pd))
+        else:
+            t["vendor_fwd"] = 0.0
         src = torch.empty(M * K + x.numel(), dtype=torch.bfloat16, device="cuda")
         dst = torch.empty_like(src)
         t["copy"] = timeit(lambda: dst.copy_(src)) / 2  # read+write of (in + out) ≈ 2× the conv's bytes
