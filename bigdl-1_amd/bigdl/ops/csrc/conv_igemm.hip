@@ -749,6 +749,12 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (bnx && (!stats || !bn_mean || relu || bias || p.scatter)) return (int)hipErrorInvalidValue;
   if (bnx && !bn_mask && (!bn_sc || !bn_sh || res)) return (int)hipErrorInvalidValue;
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
+  // the 64 → 64 3×3 stride-1 shape (ResNet-50 stage 1): the persistent halo-patch kernel, whatever
+  // tile the launch carries (it stages each input pixel once instead of once per tap)
+  if (!ax && !c4 && !cdup && groups == 1) {
+    const int e = conv_patch_launch(p, s);
+    if (e != (int)hipErrorNotSupported) return e;
+  }
   // 32x32x16 / LDS-DMA family: pinned by the launch's tile (BK = kX8) or, with no tile given, by
   // BIGDL_CONV_X8=1 (256 × 128 tile; 256 × 64 for K ≤ 64).  Shapes it does not cover (C % 64 != 0,
   // the BN-backward prologue, the C = 4 stem) take the 16x16x32 family with the heuristic tile.

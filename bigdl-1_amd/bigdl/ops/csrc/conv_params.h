@@ -381,17 +381,49 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
     rq[0] = make_float4(q8[0], q8[1], q8[2], q8[3]);
     rq[1] = make_float4(q8[4], q8[5], q8[6], q8[7]);
     __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float a = 0.f, b = 0.f;
+    constexpr int QP = NT >= BN ? NT / BN : 1;  // threads per channel in the fold (RPP / QP = 8 rows each)
+    if constexpr (QP == 1) {
+      for (int c = tid; c < BN; c += NT) {
+        float a = 0.f, b = 0.f;
 #pragma unroll 4
-      for (int g = 0; g < RPP; ++g) {
-        a += red[g * BN + c];
-        b += red[RPP * BN + g * BN + c];
+        for (int g = 0; g < RPP; ++g) {
+          a += red[g * BN + c];
+          b += red[RPP * BN + g * BN + c];
+        }
+        const int g = tm * (BM / SBM) + h;
+        if (n0 + c < p.K && g < p.tiles_m) {
+          put_stat(p, 0, g, n0 + c, a);
+          put_stat(p, 1, g, n0 + c, b);
+        }
       }
-      const int g = tm * (BM / SBM) + h;
-      if (n0 + c < p.K && g < p.tiles_m) {
-        put_stat(p, 0, g, n0 + c, a);
-        put_stat(p, 1, g, n0 + c, b);
+    } else {
+      // every thread folds 8 of a channel's RPP partial rows (16 independent LDS reads in flight
+      // instead of BN threads walking all RPP rows one dependent read at a time — ~5k cycles per
+      // tile at one workgroup per CU), then BN threads add the QP results
+      constexpr int RQ = RPP / QP;
+      const int c = tid % BN, qp = tid / BN;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int g = 0; g < RQ; ++g) {
+        a += red[(qp * RQ + g) * BN + c];
+        b += red[RPP * BN + (qp * RQ + g) * BN + c];
+      }
+      float* red2 = reinterpret_cast<float*>(&et[h * SBM * LDR]);  // this half's staged rows are consumed
+      red2[qp * BN + c] = a;
+      red2[(QP + qp) * BN + c] = b;
+      __syncthreads();
+      if (tid < BN) {
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int q = 0; q < QP; ++q) {
+          sa += red2[q * BN + tid];
+          sb += red2[(QP + q) * BN + tid];
+        }
+        const int g = tm * (BM / SBM) + h;
+        if (n0 + tid < p.K && g < p.tiles_m) {
+          put_stat(p, 0, g, n0 + tid, sa);
+          put_stat(p, 1, g, n0 + tid, sb);
+        }
       }
     }
     if (h + 1 < BM / SBM) __syncthreads();  // the next half rewrites `red`
@@ -403,4 +435,7 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
 // tile; mode 1 = tap-uniform FAST gather, 3 = pointwise.  Returns hipError_t; hipErrorNotSupported
 // when the variant / mode pair is not instantiated.
 int conv_x8_launch(const ConvParams& p, int mode, int bm, int bn, dim3 grid, hipStream_t s);
+// conv_patch.hip: persistent halo-patch 3×3 s1 p1 64 → 64 conv (hipErrorNotSupported: not that shape)
+int conv_patch_launch(ConvParams p, hipStream_t s);
+bool conv_patch_ok(const ConvParams& p);
 bool conv_x8_ok(int mode, int bm, int bn, const ConvParams& p);
