@@ -72,6 +72,60 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const T* __restrict__ x, T*
   }
 }
 
+// 3×3 / stride-2 windows (the ResNet stem pool): all nine 16-B window loads of a thread are issued
+// before the first compare (branch-free: an out-of-image tap reads the window's centre and is masked),
+// where the generic loop above kept one load in flight — 3.8 TB/s on the 112² stem pool.
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const T* __restrict__ x, T* __restrict__ y,
+                                                          int8_t* __restrict__ idx, PoolGeom g) {
+  const int CG = g.C >> 3;
+  const IT total = (IT)g.N * g.P * g.Q * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    IT pix = t / CG;
+    const int q = (int)(pix % g.Q);
+    pix /= g.Q;
+    const int p = (int)(pix % g.P);
+    const int n = (int)(pix / g.P);
+    const int h0 = p * 2 - g.ph, w0 = q * 2 - g.pw;
+    // the window's centre is inside the image for any pad ≤ 1 and P, Q from the usual formulas;
+    // clamp it anyway so a masked tap never addresses outside the tensor
+    const int hc = min(max(h0 + 1, 0), g.H - 1), wc = min(max(w0 + 1, 0), g.W - 1);
+    float v[9][8];
+    bool ok[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int h = h0 + i, w = w0 + j;
+        ok[3 * i + j] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const int hh = ok[3 * i + j] ? h : hc, ww = ok[3 * i + j] ? w : wc;
+        pld8(x + (((size_t)n * g.H + hh) * g.W + ww) * g.C + cg * 8, v[3 * i + j]);
+      }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ok[k] && (v[k][e] > best[e] || v[k][e] != v[k][e])) {  // NaN propagates like torch
+          best[e] = v[k][e];
+          arg[e] = k;
+        }
+    const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + cg * 8;
+    pst8(y + o, best);
+    if (!idx) continue;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo |= (uint32_t)(arg[e] & 0xFF) << (8 * e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hi |= (uint32_t)(arg[4 + e] & 0xFF) << (8 * e);
+    *reinterpret_cast<uint2*>(idx + o) = make_uint2(lo, hi);
+  }
+}
+
 template <typename IT, typename T = bf16_t>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const T* __restrict__ gy, const int8_t* __restrict__ idx,
                                                      T* __restrict__ gx, PoolGeom g) {
@@ -112,6 +166,56 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const T* __restrict__ gy, c
           const int8_t ae = (int8_t)((aw[e >> 2] >> (8 * (e & 3))) & 0xFF);
           if (ae == me) acc[e] += gv[e];
         }
+      }
+    }
+    pst8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+  }
+}
+
+// 3×3 / stride-2 backward: an input pixel lies in at most 2 × 2 windows; all of their argmax and
+// gradient chunks are requested before the first is used (masked, address-clamped when absent).
+template <typename IT, typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_bwd_k3s2(const T* __restrict__ gy, const int8_t* __restrict__ idx,
+                                                          T* __restrict__ gx, PoolGeom g) {
+  const int CG = g.C >> 3;
+  const IT total = (IT)g.N * g.H * g.W * CG;
+  for (IT t = blockIdx.x * (IT)blockDim.x + threadIdx.x; t < total; t += (IT)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    IT pix = t / CG;
+    const int w = (int)(pix % g.W);
+    pix /= g.W;
+    const int h = (int)(pix % g.H);
+    const int n = (int)(pix / g.H);
+    const int hp = h + g.ph, wp = w + g.pw;
+    // windows p with 2p ≤ hp ≤ 2p + 2: p ∈ {hp/2 − 1, hp/2} (clipped to [0, P))
+    const int pa = hp / 2 - 1, qa = wp / 2 - 1;
+    uint2 a[4];
+    float gv[4][8];
+    bool ok[4];
+    int8_t me[4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v2 = 0; v2 < 2; ++v2) {
+        const int p = pa + u, q = qa + v2, k = 2 * u + v2;
+        const int i = hp - 2 * p, j = wp - 2 * q;
+        ok[k] = p >= 0 && p < g.P && q >= 0 && q < g.Q && i <= 2 && j <= 2;
+        me[k] = (int8_t)(i * 3 + j);
+        const int pp = ok[k] ? p : 0, qq = ok[k] ? q : 0;
+        const size_t o = (((size_t)n * g.P + pp) * g.Q + qq) * g.C + cg * 8;
+        a[k] = *reinterpret_cast<const uint2*>(idx + o);
+        pld8(gy + o, gv[k]);
+      }
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t aw[2] = {a[k].x, a[k].y};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int8_t ae = (int8_t)((aw[e >> 2] >> (8 * (e & 3))) & 0xFF);
+        if (ok[k] && ae == me[k]) acc[e] += gv[k][e];
       }
     }
     pst8(gx + (((size_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
@@ -265,10 +369,13 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
   }
   const long long total = (long long)N * P * Q * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
-  if (total < 0x7fffffffLL)
-    hipLaunchKernelGGL(k_maxpool_fwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
-  else
+  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
+  if (total < 0x7fffffffLL) {
+    if (k3s2) hipLaunchKernelGGL(k_maxpool_fwd_k3s2<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
+    else hipLaunchKernelGGL(k_maxpool_fwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
+  } else {
     hipLaunchKernelGGL(k_maxpool_fwd<long long>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
+  }
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -284,7 +391,11 @@ BIGDL_EXPORT int bigdl_maxpool_bwd(const void* gy, const void* idx, void* gx, in
   }
   const long long total = (long long)N * H * W * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
-  if (total < 0x7fffffffLL)
+  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
+  if (total < 0x7fffffffLL && k3s2)
+    hipLaunchKernelGGL(k_maxpool_bwd_k3s2<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx,
+                       (bf16_t*)gx, g);
+  else if (total < 0x7fffffffLL)
     hipLaunchKernelGGL(k_maxpool_bwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)gy, (const int8_t*)idx,
                        (bf16_t*)gx, g);
   else

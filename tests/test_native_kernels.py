@@ -430,13 +430,17 @@ def test_strided_dgrad_subpixel(case):
     torch.testing.assert_close(gi2.float(), xr.grad + res.float(), rtol=3e-2, atol=4e-2)
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 13, 11), (2, 64, 28, 28), (1, 8, 9, 12)])
 @pytest.mark.parametrize("cfg", [((3, 3), (2, 2), (1, 1), False), ((2, 2), (2, 2), (0, 0), True),
-                                 ((3, 3), (2, 2), (0, 0), True), ((3, 3), (1, 1), (1, 1), False)])
-def test_maxpool_native(cfg):
+                                 ((3, 3), (2, 2), (0, 0), True), ((3, 3), (1, 1), (1, 1), False),
+                                 ((3, 3), (2, 2), (1, 1), True)])
+def test_maxpool_native(cfg, shape):
+    """Generic and 3×3 / stride-2 (all window loads in flight) kernels against the reference,
+    forward values and argmax-routed backward, with ceil-mode overhang."""
     N = _native()
     from bigdl.ops import reference as R
     k, s, p, ceil = cfg
-    x = _cl(torch.randn(2, 16, 13, 11, device=dev).bfloat16())
+    x = _cl(torch.randn(*shape, device=dev).bfloat16())
     y, idx = N.maxpool2d_forward(x, k, s, p, ceil)
     yr, idr = R.maxpool2d_forward(x.float(), k, s, p, ceil)
     torch.testing.assert_close(y.float(), yr)
