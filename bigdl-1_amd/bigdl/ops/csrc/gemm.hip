@@ -33,6 +33,12 @@ struct GemmParams {
   int out_f32;  // 0: bf16 C, 1: fp32 C
   float alpha, beta;
   uint32_t a_bytes, b_bytes;
+  // split-K (slab != null): block row blockIdx.y reduces K range [y·kchunk, (y+1)·kchunk) and stores
+  // its raw fp32 partial tile into slab[y][M][N]; k_gemm_splitk_epi sums the slabs and applies the
+  // epilogue.  For the small-M, long-K GEMMs (a classifier head: batch × 25088 · 4096) whose 64×64
+  // tile grid alone fills half the CUs at most, each block walking all of K.
+  float* slab;
+  int kchunk;
 };
 
 template <int BK>
@@ -85,13 +91,15 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmParams p) {
     const int n = n0 + tid / CPK + RPS * i;
     b_row[i] = n < p.N ? (uint32_t)((long long)n * p.ldb * 2) : OOB;
   }
-  const int KT = (p.K + BK - 1) / BK;
+  const int kbeg = p.slab ? (int)blockIdx.y * p.kchunk : 0;
+  const int kend = p.slab ? min(p.K, kbeg + p.kchunk) : p.K;
+  const int KT = (kend - kbeg + BK - 1) / BK;
 
   // every load is issued (dead ones with an out-of-range offset that returns zero) so hipcc's
   // vmcnt accounting stays exact; the K tail inside a row is masked per 16-B chunk (K % 8 == 0)
   auto load_tile = [&](int kt, bool live, uint4 (&ra)[A_CHUNKS], uint4 (&rb)[B_CHUNKS]) {
-    const int k = kt * BK + col8 * 8;
-    const bool kin = live && k < p.K;
+    const int k = kbeg + kt * BK + col8 * 8;
+    const bool kin = live && k < kend;
     const uint32_t kb = (uint32_t)k * 2u;
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
@@ -157,6 +165,22 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmParams p) {
   if (kt < KT) compute(0);
 
   // epilogue straight from the accumulators: lane → (row m, 4 consecutive columns n..n+3)
+  if (p.slab) {  // split-K partial: raw fp32 sums, the epilogue runs after all slices
+    float* sl = p.slab + (size_t)blockIdx.y * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wave_m * (BM / 2) + j * 16 + fr;
+        if (m < p.M)
+          *reinterpret_cast<float4*>(sl + (size_t)m * p.N + n) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int n = n0 + wave_n * (BN / 2) + i * 16 + fq * 4;
@@ -202,11 +226,63 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmParams p) {
 
 static bool al(const void* q, int bytes) { return ((uintptr_t)q & (uintptr_t)(bytes - 1)) == 0; }
 
+// Σ of the S split-K slabs, then alpha, bias, addend, beta·C, activation and the output dtype
+__global__ void __launch_bounds__(256) k_gemm_splitk_epi(GemmParams p, int S) {
+  const long long quads = (long long)p.M * (p.N / 4);
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < quads; t += (long long)gridDim.x * 256) {
+    const int m = (int)(t / (p.N / 4)), n = (int)(t - (long long)m * (p.N / 4)) * 4;
+    float4 a = *reinterpret_cast<const float4*>(p.slab + (size_t)m * p.N + n);
+    for (int y = 1; y < S; ++y) {
+      const float4 b = *reinterpret_cast<const float4*>(p.slab + ((size_t)y * p.M + m) * p.N + n);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {p.alpha * a.x, p.alpha * a.y, p.alpha * a.z, p.alpha * a.w};
+    if (p.bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+    }
+    if (p.d) {
+      const uint2 dd = *reinterpret_cast<const uint2*>(p.d + (long long)m * p.ldd + n);
+      v[0] += __uint_as_float(dd.x << 16);
+      v[1] += __uint_as_float(dd.x & 0xFFFF0000u);
+      v[2] += __uint_as_float(dd.y << 16);
+      v[3] += __uint_as_float(dd.y & 0xFFFF0000u);
+    }
+    if (p.out_f32) {
+      float* cp = reinterpret_cast<float*>(p.c) + (long long)m * p.ldc + n;
+      if (p.beta != 0.f) {
+        const float4 o = *reinterpret_cast<const float4*>(cp);
+        v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
+      bf16_t* cp = reinterpret_cast<bf16_t*>(p.c) + (long long)m * p.ldc + n;
+      *reinterpret_cast<uint2*>(cp) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                 (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    }
+  }
+}
+
 // Requirements (checked): K % 8 == 0, N % 4 == 0, lda / ldb % 8 == 0, ldc / ldd % 4 == 0, a / b 16-B
 // aligned, c 8-B (bf16) or 16-B (fp32) aligned, bias 16-B aligned, operands below 2 GiB.
+BIGDL_EXPORT int bigdl_gemm_splitk(const void* a, long long lda, const void* b, long long ldb, const float* bias,
+                                   const void* d, long long ldd, void* c, long long ldc, int M, int N, int K, int act,
+                                   int out_f32, float alpha, float beta, float* slab, int S, hipStream_t s);
+
 BIGDL_EXPORT int bigdl_gemm(const void* a, long long lda, const void* b, long long ldb, const float* bias,
                             const void* d, long long ldd, void* c, long long ldc, int M, int N, int K, int act,
                             int out_f32, float alpha, float beta, hipStream_t s) {
+  return bigdl_gemm_splitk(a, lda, b, ldb, bias, d, ldd, c, ldc, M, N, K, act, out_f32, alpha, beta, nullptr, 1, s);
+}
+
+// slab: S·M·N fp32 workspace (S > 1 splits K on the 64 × 64 tiles; S ≤ 1 or slab null: no split)
+BIGDL_EXPORT int bigdl_gemm_splitk(const void* a, long long lda, const void* b, long long ldb, const float* bias,
+                                   const void* d, long long ldd, void* c, long long ldc, int M, int N, int K, int act,
+                                   int out_f32, float alpha, float beta, float* slab, int S, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 8 || N % 4) return (int)hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 4) return (int)hipErrorInvalidValue;
   if (d && (ldd < N || ldd % 4 || !al(d, 8))) return (int)hipErrorInvalidValue;
@@ -223,6 +299,21 @@ BIGDL_EXPORT int bigdl_gemm(const void* a, long long lda, const void* b, long lo
   // 128 × 128 tiles while that still gives ≥ 1 block per CU, else 64 × 64 (small-M recurrent /
   // classifier GEMMs are latency-bound: more, smaller blocks)
   const long long big = (long long)((M + 127) / 128) * ((N + 127) / 128);
+  if (slab && S > 1) {
+    if (!al(slab, 16) || S > 64) return (int)hipErrorInvalidValue;
+    constexpr int BK = 64;
+    const int KT = (K + BK - 1) / BK;
+    const int per = (KT + S - 1) / S;  // k-tiles per slice
+    p.kchunk = per * BK;
+    const int Se = (K + p.kchunk - 1) / p.kchunk;  // slices actually used (all non-empty)
+    p.slab = slab;
+    p.tiles_n = (N + 63) / 64;
+    const long long t = (long long)((M + 63) / 64) * p.tiles_n;
+    hipLaunchKernelGGL((k_gemm<64, 64, 64>), dim3((unsigned)t, (unsigned)Se), dim3(256), 0, s, p);
+    const long long quads = (long long)M * (N / 4);
+    hipLaunchKernelGGL(k_gemm_splitk_epi, dim3((unsigned)bigdl_grid(quads, 256, 4096)), dim3(256), 0, s, p, Se);
+    BIGDL_CHECK_LAUNCH();
+  }
   if (big >= 256) {
     p.tiles_n = (N + 127) / 128;
     hipLaunchKernelGGL((k_gemm<128, 128, 64>), dim3((unsigned)big), dim3(256), 0, s, p);

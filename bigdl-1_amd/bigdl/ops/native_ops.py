@@ -2124,11 +2124,25 @@ def gemm(a, b, bias=None, act=0, out=None, d=None, alpha=1.0, beta=0.0):
     if d is not None and (d.dtype != _bf16 or d.dim() != 2 or tuple(d.shape) != (M, N) or d.stride(1) != 1
                           or d.stride(0) % 4 or d.data_ptr() % 8):
         return NotImplemented
-    check(_lib().bigdl_gemm(ptr(a), _ll(a.stride(0)), ptr(b), _ll(b.stride(0)), ptr(bb), ptr(d),
-                            _ll(d.stride(0) if d is not None else 0), ptr(out), _ll(out.stride(0)), C.c_int(M),
-                            C.c_int(N), C.c_int(K), C.c_int(act), C.c_int(1 if out.dtype == _f32 else 0), _f(alpha),
-                            _f(beta), _s()), "gemm")
+    S = _gemm_splits(M, N, K)
+    slab = torch.empty(S * M * N, dtype=_f32, device=a.device) if S > 1 else None
+    check(_lib().bigdl_gemm_splitk(ptr(a), _ll(a.stride(0)), ptr(b), _ll(b.stride(0)), ptr(bb), ptr(d),
+                                   _ll(d.stride(0) if d is not None else 0), ptr(out), _ll(out.stride(0)), C.c_int(M),
+                                   C.c_int(N), C.c_int(K), C.c_int(act), C.c_int(1 if out.dtype == _f32 else 0),
+                                   _f(alpha), _f(beta), ptr(slab), C.c_int(S), _s()), "gemm")
     return out
+
+
+def _gemm_splits(M, N, K):
+    """K slices for gemm(): a GEMM whose 64×64 tile grid cannot fill the chip (under 256 tiles) and
+    whose K is long (≥ 2048: a classifier head, batch × 25088 · 4096) splits K so that ~512 blocks
+    run, each slice ≥ 8 k-tiles; the fp32 partial slabs are summed by the epilogue kernel."""
+    if M * N >= 256 * 128 * 128 or K < 2048:
+        return 1
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    if tiles >= 256:
+        return 1
+    return max(1, min(16, 512 // tiles, K // 512))
 
 
 def transpose_bf16(src):

@@ -59,6 +59,29 @@ def test_gemm_fp32_accumulate_strided_and_addend():
     torch.testing.assert_close(c, ref, rtol=1e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 25088), (128, 1000, 4096), (37, 100, 2056), (3, 12, 8192)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_split_k(M, N, K, act):
+    """Small-M, long-K GEMMs take the split-K path (fp32 partial slabs summed by the epilogue kernel)."""
+    NO = _NO()
+    assert NO._gemm_splits(M, N, K) > 1
+    a = torch.randn(M, K, device=dev).to(bf)
+    b = (torch.randn(N, K, device=dev) * 0.05).to(bf)
+    bias = torch.randn(N, device=dev)
+    y = NO.gemm(a, b, bias, act=act)
+    ref = a.float() @ b.float().t() + bias
+    if act:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()) / 10 + 1e-2)
+    # fp32 output with addend and beta through the split epilogue
+    d = torch.randn(M, N, device=dev).to(bf)
+    c = torch.randn(M, N, device=dev)
+    c0 = c.clone()
+    NO.gemm(a, b, None, out=c, d=d, alpha=0.5, beta=2.0)
+    ref2 = 0.5 * (a.float() @ b.float().t()) + d.float() + 2.0 * c0
+    torch.testing.assert_close(c, ref2, rtol=1e-2, atol=5e-2 * float(ref2.abs().max()) / 10 + 5e-2)
+
+
 def test_transpose_and_colsum():
     NO = _NO()
     x = torch.randn(130, 72, device=dev).to(bf)
