@@ -215,6 +215,13 @@ class SpatialConvolution(_QuantizedBase):
             self._wdeq = wf
         b = self.bias_f.to(x.device).float() if self.bias_f is not None else None
         xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if (self._out_qscale is not None and C <= 4 and self.dilationH == 1 and self.dilationW == 1
+                and ops.native_has("conv2d_forward")):
+            # quantised in the conv's epilogue: no bf16 activation, no separate quantisation pass
+            yq = NO.conv2d_forward_q(xb, wf, b, (self.strideH, self.strideW), (pt, pl), self._relu_fused,
+                                     self._out_qscale, u8=self._out_u8)
+            if yq is not NotImplemented:
+                return yq
         y = NO.conv2d_forward(xb, wf, b, (self.strideH, self.strideW), (pt, pl), (self.dilationH, self.dilationW), 1,
                               relu=self._relu_fused)
         if y is NotImplemented or self._out_qscale is None:

@@ -668,8 +668,12 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
                            int ldx = 0, int groups = 1, const void* ax = nullptr, const float* acoef = nullptr,
                            float* y32 = nullptr, int tile_bn = 0, int tile_bk = 0, int tile_bm = 0,
                            int stats_atomic = 0, const float* res32 = nullptr, int cdup = 0,
-                           const float* bnx32 = nullptr) {
+                           const float* bnx32 = nullptr, int8_t* yq = nullptr, float yq_scale = 0.f,
+                           int yq_u8 = 0) {
   const bool c4 = C == 4;
+  if (yq && (y32 || stats || bnx || res || ldy != K || K % 8 || ((uintptr_t)yq & 7) || !(yq_scale > 0.f) ||
+             osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q || groups != 1))
+    return (int)hipErrorInvalidValue;
   if (cdup && (cdup < 0 || cdup % 8 || 2 * cdup > C || c4 || ax || groups != 1 || !y32)) return (int)hipErrorInvalidValue;
   if (!tile_ok(tile_bn, tile_bk, tile_bm)) return (int)hipErrorInvalidValue;
   if (y32 && (K % 4 || ldy % 4 || ((uintptr_t)y32 & 15) || res || bnx || ax || groups != 1 || osh != 1 ||
@@ -718,6 +722,9 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   p.res = (const bf16_t*)res;
   p.stats = stats;
   p.stats_atomic = stats ? stats_atomic : 0;
+  p.yq = yq;
+  p.yq_inv = yq ? 1.f / yq_scale : 0.f;
+  p.yq_u8 = yq ? yq_u8 : 0;
   p.res_sh = res ? res_sh : 0;
   p.res_sw = res ? res_sw : 0;
   p.res_H = res_H;
@@ -751,7 +758,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
   if (bn_mask && !bnx) return (int)hipErrorInvalidValue;
   // the 64 → 64 3×3 stride-1 shape (ResNet-50 stage 1): the persistent halo-patch kernel, whatever
   // tile the launch carries (it stages each input pixel once instead of once per tap)
-  if (!ax && !c4 && !cdup && groups == 1) {
+  if (!ax && !c4 && !cdup && groups == 1 && !yq) {
     const int e = conv_patch_launch(p, s);
     if (e != (int)hipErrorNotSupported) return e;
   }
@@ -769,7 +776,7 @@ static int conv_fwd_launch(const void* x, const void* w, const float* bias, cons
       xbm = 256;
       xbn = K <= 64 ? 64 : (x8_env == 2 && K >= 256 ? 256 : 128);  // 2: the 256 × 256 tile where K allows
     }
-    if (xbm && !ax && !c4 && !cdup) {
+    if (xbm && !ax && !c4 && !cdup && !yq) {
       const int xmode = (R == 1 && S == 1 && ph == 0 && pw == 0) ? 3 : 1;
       p.tiles_n = (K + xbn - 1) / xbn;
       p.tiles_m = (p.M + SBM - 1) / SBM;
@@ -1078,6 +1085,18 @@ BIGDL_EXPORT int bigdl_conv_fwd_c4(const void* x, const void* w, int ldw, const 
                                    int ph, int pw, int relu, hipStream_t s) {
   return conv_fwd_launch(x, w, bias, res, y, stats, Nb, H, W, 4, K, R, S, P, Q, sh, sw, ph, pw, 1, 1, relu, 1, 1, 0, 0,
                          P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw);
+}
+
+// The C4 stem with an int8 output (bias, ReLU, then static quantisation with q_scale; u8: the unsigned
+// offset code and its 0x80 tail): the calibrated int8 chain's first layer in one pass.
+BIGDL_EXPORT int bigdl_conv_fwd_c4_q(const void* x, const void* w, int ldw, const float* bias, void* yq, float q_scale,
+                                     int u8, int Nb, int H, int W, int K, int R, int S, int P, int Q, int sh, int sw,
+                                     int ph, int pw, int relu, hipStream_t s) {
+  if (!yq) return (int)hipErrorInvalidValue;
+  return conv_fwd_launch(x, w, bias, nullptr, nullptr, nullptr, Nb, H, W, 4, K, R, S, P, Q, sh, sw, ph, pw, 1, 1, relu,
+                         1, 1, 0, 0, P, Q, nullptr, nullptr, nullptr, nullptr, nullptr, K, s, ldw, nullptr, 0, 0, 0, 0,
+                         nullptr, 0, 1, nullptr, nullptr, nullptr, 0, 0, 0, 0, nullptr, 0, nullptr, (int8_t*)yq, q_scale,
+                         u8);
 }
 
 // NHWC channel zero-pad (the RGB stem: 3 → 4 channels, one 8-B store per pixel): dst[p][0:C] = src[p],

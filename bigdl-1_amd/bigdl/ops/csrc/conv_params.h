@@ -84,6 +84,13 @@ struct ConvParams {
   // (the consumer's apply kernel finalises in its prologue and re-zeroes the buffer: no separate
   // reduction launches; not bit-reproducible — bigdl.deterministic keeps mode 0)
   int stats_atomic;
+  // optional int8 output (the calibrated int8 chain's bf16 RGB stem, nn/quantized): the epilogue
+  // writes q = clamp(rint(ReLU?(y) · yq_inv)) as int8 [M][ldy] instead of bf16 — signed [-127, 127],
+  // or (yq_u8) unsigned [0, 255] stored offset by -128 with the 16-byte 0x80 tail after the tensor
+  // (conv_i8.hip's unsigned activation contract).  Plain epilogue only (no residual / statistics).
+  int8_t* yq;
+  float yq_inv;
+  int yq_u8;
 };
 
 // one tile's per-channel partial sum `v` of statistic `which` (0: Σ, 1: Σ²) for channel n, row group g
@@ -141,6 +148,30 @@ __device__ __forceinline__ void conv_store_pass(const ConvParams& p, bf16_t* et,
   constexpr int RPP = NT / CPR;   // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
   const int n = n0 + cc * 8;
+  if (p.yq) {  // int8 output (K % 8 == 0 checked by the launcher)
+    const float qlo = p.yq_u8 ? 0.f : -127.f, qhi = p.yq_u8 ? 255.f : 127.f, qoff = p.yq_u8 ? 128.f : 0.f;
+    const int rmax = p.M - m0;
+    if (n < p.K) {
+#pragma unroll 4
+      for (int r = rr; r < BM; r += RPP) {
+        if (r >= rmax) break;
+        float v[8];
+        unpack8(rd_chunk(r, cc), v);
+        uint32_t w2[2] = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = p.relu ? fmaxf(v[e], 0.f) : v[e];
+          const float q = fminf(fmaxf(rintf(t * p.yq_inv), qlo), qhi) - qoff;
+          w2[e >> 2] |= ((uint32_t)(int)q & 0xFFu) << (8 * (e & 3));
+        }
+        *reinterpret_cast<uint2*>(p.yq + (size_t)(m0 + r) * p.ldy + n) = make_uint2(w2[0], w2[1]);
+      }
+    }
+    if (p.yq_u8 && m0 == 0 && n0 == 0 && tid == 0)
+      *reinterpret_cast<uint4*>(p.yq + (size_t)p.M * p.ldy) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u,
+                                                                         0x80808080u);
+    return;
+  }
   // plain store (no residual / ReLU / BN prologue / scatter, whole channel tile): one LDS read and
   // one 16-B global store per chunk on an incrementally advanced row pointer
   if (!p.res && !p.relu && !p.bnx && !p.scatter && (p.stats == nullptr || rstats) && n0 + BN <= p.K) {

@@ -924,6 +924,37 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
     return y
 
 
+def conv2d_forward_q(x, w4, b, stride, pad, relu, q_scale, u8=False, pad_slot=None):
+    """The RGB (C ≤ 4) stem conv with its output quantised in the epilogue (bias, ReLU, static
+    int8 scale ``q_scale``; ``u8``: the unsigned offset code with its 0x80 tail) — the first layer
+    of a calibrated int8 chain in one pass instead of a bf16 conv plus a quantisation pass.  Returns
+    the tagged int8 NHWC activation, or NotImplemented."""
+    if not (x.is_cuda and x.dtype == _bf16 and x.dim() == 4 and x.shape[1] <= 4 and w4.shape[1] == x.shape[1]):
+        return NotImplemented
+    if not _conv_geom_ok_slot(x, w4, 1, (1, 1), pad_slot):
+        return NotImplemented
+    N_, C_, H, W = x.shape
+    K, _, R, S = w4.shape
+    if K % 8:
+        return NotImplemented
+    wk = _krsc(w4)
+    xp = _pad_channels(x, 4, pad_slot)
+    kg = R * S * 4
+    ldw = (kg + 7) // 8 * 8
+    wp = torch.zeros((K, ldw), dtype=wk.dtype, device=wk.device)
+    wp[:, :kg].view(K, R, S, 4)[..., :C_] = wk
+    P = (H + 2 * pad[0] - R) // stride[0] + 1
+    Q = (W + 2 * pad[1] - S) // stride[1] + 1
+    if P <= 0 or Q <= 0:
+        return NotImplemented
+    y = _i8_act(N_, K, P, Q, x.device, u8)
+    bias = b if (b is None or (b.dtype == _f32 and b.is_contiguous())) else b.float().contiguous()
+    check(_lib().bigdl_conv_fwd_c4_q(ptr(xp), ptr(wp), ldw, ptr(bias), ptr(y), C.c_float(q_scale), C.c_int(int(u8)),
+                                     N_, H, W, K, R, S, P, Q, stride[0], stride[1], pad[0], pad[1], int(relu), _s()),
+          "conv_fwd_c4_q")
+    return _tag(y, q_scale, u8)
+
+
 @register("conv2d_forward")
 def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
     if x.dtype == _f32 and res is None and out is None and F3.enabled(x):

@@ -151,3 +151,28 @@ def test_u8_offset_bias_reproduces_float_conv(stride, pad, k, dil):
     ref = torch.nn.functional.conv2d((q + 128) * sx, wi.double() * sw.double()[:, None, None, None], bias.double(),
                                      stride, pad, dil)
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-4), float((got - ref).abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("u8", [False, True])
+def test_stem_conv_int8_epilogue_matches_two_pass(u8):
+    """The RGB stem's int8 output written by the conv epilogue equals the bf16 conv followed by
+    the static quantisation pass (same bf16-rounded values, same rounding), tail included."""
+    from bigdl.ops import native_ops as NO
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, 30, 34, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 3, 3, device="cuda") * 0.2).bfloat16()
+    b = torch.randn(64, device="cuda")
+    for relu in (True, False):
+        if u8 and not relu:
+            continue
+        y = NO.conv2d_forward(x, w, b, (1, 1), (1, 1), relu=relu)
+        scale = float(y.float().abs().max()) / (255 if u8 else 127)
+        ref = NO.quant_static(y, scale, u8=u8)
+        got = NO.conv2d_forward_q(x, w, b, (1, 1), (1, 1), relu, scale, u8=u8)
+        assert got is not NotImplemented
+        assert got._qscale == ref._qscale and got._qzero == ref._qzero
+        assert torch.equal(got, ref)
+        if u8:
+            tail = torch.empty(0, dtype=torch.int8, device="cuda").set_(got.untyped_storage(), got.numel(), (16,), (1,))
+            assert bool((tail == -128).all())
