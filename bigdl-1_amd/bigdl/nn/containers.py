@@ -269,6 +269,11 @@ class Concat(Container):
         return gi
 
 
+def _deterministic():
+    from ..utils import config
+    return bool(config.get_property("bigdl.deterministic"))
+
+
 class ConcatTable(Container):
     """Apply each member to the same input; output is a Table (``ConcatTable.scala``).
 
@@ -285,7 +290,22 @@ class ConcatTable(Container):
 
     def _fused_forward(self, input):
         br, bn, shortcut, relu = self._residual
-        r = shortcut.forward(input)
+        last = shortcut.modules[-1] if isinstance(shortcut, Sequential) and shortcut.modules else None
+        if last is not None and getattr(last, "_defer_ok", False) and not _deterministic():
+            # shortcut conv → BN: the BN only finalizes its statistics and hands over its input and
+            # coefficients (ops.reference.BNOut); the tail BN applies it inside its own pass, so the
+            # shortcut activation is never written or re-read (one fewer full pass per stage)
+            h2 = input
+            for m in shortcut.modules[:-1]:
+                h2 = m.forward(h2)
+            last._defer_next = True
+            try:
+                r = last.forward(h2)
+            finally:
+                last.__dict__.pop("_defer_next", None)
+            shortcut.output = r
+        else:
+            r = shortcut.forward(input)
         h = input
         for m in br.modules[:-1]:
             h = m.forward(h)

@@ -16,6 +16,9 @@ stay identical); matched modules get execution flags instead:
 * ResNet block tail ``ConcatTable(branch…BN, shortcut) → CAddTable → ReLU`` (``convsum``): the
   shortcut runs first and the branch's last BN computes ReLU(BN(x) + shortcut) in one pass; in
   backward the same kernel emits both the branch gradient and the masked gradient for the shortcut.
+* shortcut BN → block tail (``shortcutbn``): a ``conv → BN`` shortcut's BN only finalizes its
+  statistics in training; the tail computes ReLU(BN(x) + x_s·a_s + b_s) from the shortcut conv's
+  output and the shortcut BN's coefficients in the same pass.
 * block tail → next block (``bnbwd``): the next block's first conv computes, in its dgrad
   epilogue, (dgrad + shortcut gradient) · [block output > 0] and the tail BN's Σg, Σg·(x − mean),
   so the tail BN backward is a single apply pass and the masked gradient IS the shortcut gradient.
@@ -148,6 +151,10 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=Non
                 continue
             relu = mods[i + 2] if i + 2 < len(mods) and _is_relu(mods[i + 2]) else None
             ct._residual = (br, bn, ct.modules[1], relu is not None)
+            sc = ct.modules[1]
+            if (config.get_property("bigdl.fusion.shortcutbn") and isinstance(sc, Sequential) and len(sc.modules) >= 2
+                    and _is_nchw_bn(sc.modules[-1]) and not sc.modules[-1]._fused_relu):
+                sc.modules[-1]._defer_ok = True
             add._passthrough = True
             if relu is not None:
                 relu._passthrough = True
@@ -216,6 +223,7 @@ def unfuse(model):
         if isinstance(m, BatchNormalization):
             m._bias_producer = None
             m._fused_relu = False
+            m._defer_ok = False
             m._pending_stats = None
             m._pending_grad = None
         if isinstance(m, Threshold):

@@ -70,6 +70,7 @@ class BatchNormalization(TensorModule):
         self._init_weight_method = RandomUniform(0, 1)
         self._init_bias_method = Zeros()
         self._fused_relu = False
+        self._defer_ok = False  # nn/fusion.py shortcutbn: the fused block tail applies this BN
         self._sync_group = None
         self._sync = False
         self._sync_force = False
@@ -249,11 +250,17 @@ class BatchNormalization(TensorModule):
         return self._forward_impl(input, None, self._fused_relu)
 
     def _forward_impl(self, input, residual, relu):
+        from ...ops.reference import BNOut
         x = input
         if x.dim() == 1:
             x = x.unsqueeze(0)
         x = to_device_layout(x) if x.dim() == 4 else x
-        if residual is not None and residual.dim() == 4:
+        # a deferred shortcut-BN output: only the native fused tail consumes it as is
+        defer = self.__dict__.pop("_defer_next", False) and residual is None and not relu
+        deferred_res = isinstance(residual, BNOut)
+        if deferred_res and not (self.train and not self._sync_active()):
+            residual, deferred_res = residual.dense(), False
+        if residual is not None and not deferred_res and residual.dim() == 4:
             residual = to_device_layout(residual)
         pdt = torch.float64 if x.dtype == torch.float64 else torch.float32  # statistics dtype
         g = self.cw("weight", pdt) if self.affine else None
@@ -273,20 +280,25 @@ class BatchNormalization(TensorModule):
                 bits = self._tail_bits(x, relu, residual)
                 self._relu_bits = None
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
+                    special = defer or deferred_res
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
                         relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits,
-                        rezero=self._is_rep(ps[2]), zero_next=self._rep_next("fwd", ps[2]),
-                        mean_out=self._shift_next(ps[4]))
+                        rezero=self._is_rep(ps[2]), zero_next=None if special else self._rep_next("fwd", ps[2]),
+                        mean_out=self._shift_next(ps[4]), apply=not defer)
                     if r is not NotImplemented:
                         self._rep_flip("fwd", ps[2])
                 if r is NotImplemented:
+                    if deferred_res:
+                        residual = residual.dense()
                     self._drop_sums(ps, 3)
                     r = ops.batchnorm_forward_train(x, g, b, self.runningMean, self.runningVar,
                                                     self.momentum, self.eps, relu=relu, residual=residual,
                                                     in_bias=ib, coef_out=coef, bits_out=bits)
                 self._relu_bits = bits
                 y, mean, invstd = r
+                if y is None:  # finalize only: the consumer (the fused block tail) applies this BN
+                    y = BNOut(x, coef)
                 self._advance_shift(mean)
                 self._last_input = x
             self.saveMean, self.saveStd = mean, invstd

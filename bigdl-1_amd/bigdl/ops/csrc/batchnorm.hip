@@ -207,7 +207,8 @@ __global__ void k_bn_infer_coef(int C, const float* __restrict__ gamma, const fl
 template <bool RES, bool RELU, bool BITS, int kApplyUnroll>
 __device__ __forceinline__ void bn_apply_rows(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                               bf16_t* __restrict__ y, long long M, int C, const float* scale,
-                                              const float* shift, uint8_t* __restrict__ bits) {
+                                              const float* shift, uint8_t* __restrict__ bits,
+                                              const float* rcoef = nullptr) {
   BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg_local = t % g.tpr;
@@ -215,11 +216,14 @@ __device__ __forceinline__ void bn_apply_rows(const bf16_t* __restrict__ x, cons
   if (r_off >= g.RPI) return;
   const long long rstride = (long long)gridDim.x * g.RPI;
   for (int cg = cg_local; cg < g.CG; cg += g.tpr) {
-    float sc[8], sh[8];
+    float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sc[k] = scale[cg * 8 + k];
       sh[k] = shift[cg * 8 + k];
+      // rcoef: the residual is itself a BN input (a deferred shortcut BN): res · rscale + rshift
+      rsc[k] = (RES && rcoef) ? rcoef[cg * 8 + k] : 1.f;
+      rsh[k] = (RES && rcoef) ? rcoef[C + cg * 8 + k] : 0.f;
     }
     // kApplyUnroll rows per trip: all their loads are issued before the first use, so each thread
     // keeps several 16-B requests in flight (one per trip left the streaming passes latency-bound)
@@ -244,7 +248,7 @@ __device__ __forceinline__ void bn_apply_rows(const bf16_t* __restrict__ x, cons
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float o = fmaf(v[k], sc[k], sh[k]);
-          if (RES) o += rv[k];
+          if (RES) o += fmaf(rv[k], rsc[k], rsh[k]);
           if (RELU) o = fmaxf(o, 0.f);
           v[k] = o;
         }
@@ -266,8 +270,9 @@ template <bool RES, bool RELU, bool BITS = false, int kApplyUnroll = 4>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                   bf16_t* __restrict__ y, long long M, int C,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
-                                                  uint8_t* __restrict__ bits = nullptr) {
-  bn_apply_rows<RES, RELU, BITS, kApplyUnroll>(x, res, y, M, C, scale, shift, bits);
+                                                  uint8_t* __restrict__ bits = nullptr,
+                                                  const float* __restrict__ rcoef = nullptr) {
+  bn_apply_rows<RES, RELU, BITS, kApplyUnroll>(x, res, y, M, C, scale, shift, bits, rcoef);
 }
 
 // A/B knobs (profiles/r3_bn_apply_ab.txt): BIGDL_BN_APPLY_BLOCKS caps the grid (default 1024: 0.87-1.06
@@ -300,7 +305,7 @@ static int apply_grid(long long M, int C) {
 }
 
 static void launch_apply(const void* x, const void* res, void* y, long long M, int C, const float* coef, int relu,
-                         void* bits, hipStream_t s) {
+                         void* bits, hipStream_t s, const float* rcoef = nullptr) {
   int grid = apply_grid(M, C);
   const bf16_t* xr = (const bf16_t*)x;
   const bf16_t* rr = (const bf16_t*)res;
@@ -308,23 +313,23 @@ static void launch_apply(const void* x, const void* res, void* y, long long M, i
   uint8_t* br = (uint8_t*)bits;
   if (apply_unroll1()) {
     if (relu && bits && res)
-      hipLaunchKernelGGL((k_bn_apply<true, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+      hipLaunchKernelGGL((k_bn_apply<true, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
     else if (relu && bits)
-      hipLaunchKernelGGL((k_bn_apply<false, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-    else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-    else if (res) hipLaunchKernelGGL((k_bn_apply<true, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-    else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-    else hipLaunchKernelGGL((k_bn_apply<false, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+      hipLaunchKernelGGL((k_bn_apply<false, true, true, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+    else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+    else if (res) hipLaunchKernelGGL((k_bn_apply<true, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+    else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+    else hipLaunchKernelGGL((k_bn_apply<false, false, false, 1>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
     return;
   }
   if (relu && bits && res)
-    hipLaunchKernelGGL((k_bn_apply<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    hipLaunchKernelGGL((k_bn_apply<true, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
   else if (relu && bits)
-    hipLaunchKernelGGL((k_bn_apply<false, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-  else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
-  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br);
+    hipLaunchKernelGGL((k_bn_apply<false, true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+  else if (res && relu) hipLaunchKernelGGL((k_bn_apply<true, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+  else if (res) hipLaunchKernelGGL((k_bn_apply<true, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+  else if (relu) hipLaunchKernelGGL((k_bn_apply<false, true>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
+  else hipLaunchKernelGGL((k_bn_apply<false, false>), dim3(grid), dim3(256), 0, s, xr, rr, yr, M, C, coef, coef + C, br, rcoef);
 }
 
 // number of partial blocks used by the stats / backward-reduce kernels (mirrored in Python)
@@ -416,12 +421,34 @@ static bool maybe_fold(const float* partial, int& G, int C, float* scratch, hipS
 
 // Training forward from precomputed partials (the producing conv's epilogue wrote Σy, Σy² per row
 // tile, unshifted): finalize + apply only — the stats pass over x is gone.
+BIGDL_EXPORT int bigdl_bn_fwd_train_partials2(const void* x, const void* res, const float* rcoef, void* y, long long M,
+                                              int C, const float* gamma, const float* beta, const float* in_bias,
+                                              float* run_mean, float* run_var, float momentum, float eps,
+                                              float* save_mean, float* save_invstd, const float* partial, int G,
+                                              const float* kshift, float* coef, int relu, float* scratch, void* bits,
+                                              int rezero, hipStream_t s);
+
 BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, void* y, long long M, int C,
                                              const float* gamma, const float* beta, const float* in_bias,
                                              float* run_mean, float* run_var, float momentum, float eps,
                                              float* save_mean, float* save_invstd, const float* partial, int G,
                                              const float* kshift, float* coef, int relu, float* scratch, void* bits,
                                              int rezero, hipStream_t s) {
+  if (!y) return (int)hipErrorInvalidValue;
+  return bigdl_bn_fwd_train_partials2(x, res, nullptr, y, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps,
+                                      save_mean, save_invstd, partial, G, kshift, coef, relu, scratch, bits, rezero, s);
+}
+
+// y == null: finalize only (statistics, running averages, coef) — a shortcut BN whose apply is
+// deferred into the block tail's (rcoef there); rcoef (with res): the residual is res·rcoef[c] +
+// rcoef[C + c], a deferred BN's input and coefficients
+BIGDL_EXPORT int bigdl_bn_fwd_train_partials2(const void* x, const void* res, const float* rcoef, void* y, long long M,
+                                              int C, const float* gamma, const float* beta, const float* in_bias,
+                                              float* run_mean, float* run_var, float momentum, float eps,
+                                              float* save_mean, float* save_invstd, const float* partial, int G,
+                                              const float* kshift, float* coef, int relu, float* scratch, void* bits,
+                                              int rezero, hipStream_t s) {
+  if (rcoef && !res) return (int)hipErrorInvalidValue;
   if (C % 8 || M <= 0 || G <= 0 || (bits && !relu) || (rezero && G > 512)) return (int)hipErrorInvalidValue;
   if (!rezero && maybe_fold(partial, G, C, scratch, s))
     hipLaunchKernelGGL(k_bn_finalize<double>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
@@ -431,7 +458,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_partials(const void* x, const void* res, voi
     hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                        partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd,
                        coef, coef + C, nullptr, rezero ? const_cast<float*>(partial) : nullptr);
-  launch_apply(x, res, y, M, C, coef, relu, bits, s);
+  if (y) launch_apply(x, res, y, M, C, coef, relu, bits, s, rcoef);
   BIGDL_CHECK_LAUNCH();
 }
 

@@ -180,14 +180,44 @@ def _coef_ok(t, C_):
 
 def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, running_var, momentum, eps,
                                     relu=False, residual=None, in_bias=None, coef_out=None, shift=None, bits_out=None,
-                                    rezero=False, zero_next=None, mean_out=None):
+                                    rezero=False, zero_next=None, mean_out=None, apply=True):
     """Training BN whose statistics were produced by the preceding conv's epilogue
     (:func:`conv2d_forward_stats`): finalize + apply only.  ``rezero``: ``partial`` is a replicated
-    atomic-statistics buffer ([2][G][C], G replicas) that the finalize clears after reading."""
+    atomic-statistics buffer ([2][G][C], G replicas) that the finalize clears after reading.
+    ``apply=False``: finalize only (coef_out required) and y = None — the caller defers the apply;
+    ``residual`` may be such a deferred BN output (:class:`~bigdl.ops.reference.BNOut`), applied
+    inside this BN's pass."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
+    deferred = isinstance(residual, R_.BNOut)
+    if deferred or not apply:
+        # the bf16 replicated / partial-rows path only (the fused block tail of the training step)
+        if not (_bn_ok(x, C_) and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias))
+                and G >= 1 and partial is not None and partial.numel() == 2 * G * C_ and partial.dtype == _f32
+                and (not rezero or G <= 512)):
+            return NotImplemented
+        if deferred and not (residual.x.shape == x.shape and residual.x.stride() == x.stride()
+                             and residual.x.dtype == _bf16 and _al16(residual.x) and _f32vec(residual.coef, 2 * C_)):
+            return NotImplemented
+        if not apply and not _coef_ok(coef_out, C_):
+            return NotImplemented
+        coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
+        mean = mean_out if (mean_out is not None and _f32vec(mean_out, C_)) else torch.empty(C_, dtype=_f32,
+                                                                                               device=x.device)
+        invstd = torch.empty(C_, dtype=_f32, device=x.device)
+        y = torch.empty_like(x) if apply else None
+        res_t, rcoef = (residual.x, residual.coef) if deferred else (residual, None)
+        check(_lib().bigdl_bn_fwd_train_partials2(ptr(x), ptr(res_t), ptr(rcoef), ptr(y), _ll(M), C.c_int(C_),
+                                                  ptr(gamma), ptr(beta), ptr(in_bias), ptr(running_mean),
+                                                  ptr(running_var), _f(momentum), _f(eps), ptr(mean), ptr(invstd),
+                                                  ptr(partial), C.c_int(G), ptr(shift if _f32vec(shift, C_) else None),
+                                                  ptr(coef), C.c_int(1 if relu else 0),
+                                                  ptr(_fold_scratch(G, C_, x.device)),
+                                                  ptr(_bits_ok(bits_out, M, C_, relu) if apply else None),
+                                                  C.c_int(1 if rezero else 0), _s()), "bn_fwd_train_partials2")
+        return y, mean, invstd
     if (rezero and 1 <= G <= 512 and _bn32_ok(x, C_, residual) and partial is not None and partial.dtype == _f32
             and partial.numel() == 2 * G * C_ and _f32vec(shift, C_)
             and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias))):

@@ -95,6 +95,35 @@ class StridedGrad:
         return out
 
 
+class BNOut:
+    """Deferred output of a training BatchNorm (no ReLU): y = x·coef[c] + coef[C + c], with ``x`` the
+    BN input and ``coef`` fp32 [scale; shift].  The fused ResNet block tail takes a shortcut BN's
+    output this way and applies it inside its own pass (ops/csrc/batchnorm.hip rcoef), so the
+    shortcut activation is never written; :meth:`dense` builds it for any other consumer."""
+    __slots__ = ("x", "coef", "shape")
+
+    def __init__(self, x, coef):
+        self.x, self.coef, self.shape = x, coef, tuple(x.shape)
+
+    @property
+    def dtype(self):
+        return self.x.dtype
+
+    @property
+    def is_cuda(self):
+        return self.x.is_cuda
+
+    def dim(self):
+        return self.x.dim()
+
+    def dense(self):
+        C = self.shape[1]
+        sc = self.coef[:C].view(1, C, *([1] * (self.x.dim() - 2)))
+        sh = self.coef[C:2 * C].view(1, C, *([1] * (self.x.dim() - 2)))
+        return (self.x.float() * sc + sh).to(self.x.dtype).contiguous(memory_format=torch.channels_last) \
+            if self.x.dim() == 4 else (self.x.float() * sc + sh).to(self.x.dtype)
+
+
 class BNGrad:
     """Deferred input gradient of a training BatchNorm: gx = A·g + B·x + Cc per channel, with ``g``
     the (ReLU-masked) gradient at the BN output, ``x`` the BN input and ``coef`` = fp32 [A; B; Cc]

@@ -517,7 +517,9 @@ class BaseOptimizer:
         if (not getattr(self, "_kernels_selected", False) and self.device.type == "cuda"
                 and not torch.cuda.is_current_stream_capturing()):
             self._kernels_selected = True
-            if config.get_property("bigdl.compile.trainAutotune"):
+            # bigdl.deterministic: no timing-based kernel choice (two runs could pin different tiles
+            # for the same geometry, i.e. different accumulation orders, and lose bit reproducibility)
+            if config.get_property("bigdl.compile.trainAutotune") and not config.get_property("bigdl.deterministic"):
                 from ..nn.compiled import autotune_training_step
                 loss, chosen = autotune_training_step(lambda: self._train_step_run(batch))
                 self.selected_kernels = chosen

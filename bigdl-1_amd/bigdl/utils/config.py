@@ -86,6 +86,7 @@ _REGISTRY = {
     "bigdl.fusion.lstmstack": (bool, True, "run two stacked Recurrent(LSTM) layers on the layer wavefront"),
     "bigdl.fusion.convsum": (bool, True, "fuse residual add"),
     "bigdl.fusion.convstats": (bool, True, "conv epilogue emits the following training BN's statistics"),
+    "bigdl.fusion.shortcutbn": (bool, True, "a ResNet block's conv->BN shortcut hands its BN output to the fused tail deferred (input + coefficients), applied inside the tail's pass"),
     "bigdl.fusion.bnbwd": (bool, True, "dgrad epilogue applies the producing BN's ReLU mask and its backward reductions"),
     "bigdl.fusion.bnprologue": (int, 0, "a BN whose producer is a 1x1 stride-1 conv hands it the input gradient "
                                          "deferred (A*g + B*x + C applied in the conv's dgrad / wgrad operand loads): "

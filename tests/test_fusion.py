@@ -93,3 +93,17 @@ def test_unfuse_restores_flags():
     assert m.modules[2]._passthrough and m.modules[1]._fused_relu
     unfuse(m)
     assert not m.modules[2]._passthrough and not m.modules[1]._fused_relu
+
+
+def test_shortcut_bn_deferred_flag_on_projection_blocks():
+    """fuse() marks the BN of a conv → BN projection shortcut for the deferred apply (the fused tail
+    applies it); identity shortcuts have no such BN; unfuse() clears the flag."""
+    from bigdl.models.resnet import ResNet, DatasetType
+    from bigdl.nn.fusion import fuse, unfuse
+    from bigdl.nn.layers.normalization import BatchNormalization
+    m = ResNet(10, depth=50, dataset=DatasetType.ImageNet)
+    fuse(m)
+    flagged = [b for b in m.flattened_modules() if isinstance(b, BatchNormalization) and b._defer_ok]
+    assert len(flagged) == 4  # one projection shortcut per stage
+    unfuse(m)
+    assert not any(getattr(b, "_defer_ok", False) for b in m.flattened_modules() if isinstance(b, BatchNormalization))
