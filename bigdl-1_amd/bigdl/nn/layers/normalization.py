@@ -256,7 +256,8 @@ class BatchNormalization(TensorModule):
             x = x.unsqueeze(0)
         x = to_device_layout(x) if x.dim() == 4 else x
         # a deferred shortcut-BN output: only the native fused tail consumes it as is
-        defer = self.__dict__.pop("_defer_next", False) and residual is None and not relu
+        defer = (self.__dict__.pop("_defer_next", False) and residual is None and not relu and x.is_cuda
+                 and x.dtype == torch.bfloat16)  # the bf16 native path only (fp32 keeps its own kernels)
         deferred_res = isinstance(residual, BNOut)
         if deferred_res and not (self.train and not self._sync_active()):
             residual, deferred_res = residual.dense(), False
