@@ -107,3 +107,16 @@ def test_shortcut_bn_deferred_flag_on_projection_blocks():
     assert len(flagged) == 4  # one projection shortcut per stage
     unfuse(m)
     assert not any(getattr(b, "_defer_ok", False) for b in m.flattened_modules() if isinstance(b, BatchNormalization))
+
+
+def test_bnout_dense_is_the_affine_map():
+    """A deferred BN output materialises as x·scale + shift per channel (NCHW logical, channels-last)."""
+    from bigdl.ops.reference import BNOut
+    torch.manual_seed(0)
+    x = torch.randn(2, 8, 5, 6).contiguous(memory_format=torch.channels_last)
+    coef = torch.randn(16)
+    y = BNOut(x, coef).dense()
+    ref = x * coef[:8].view(1, 8, 1, 1) + coef[8:].view(1, 8, 1, 1)
+    assert y.shape == x.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y, ref)
+    assert BNOut(x, coef).dim() == 4 and BNOut(x, coef).shape == tuple(x.shape)
