@@ -212,6 +212,9 @@ TILE_CANDIDATES = ((0, 0, 0), (64, 32, 128), (64, 64, 128), (128, 32, 128), (128
 
 #: weight-gradient candidates (target blocks of the pixel split, k-tile pixel depth); 0 = heuristic
 WGRAD_CANDIDATES = ((0, 0), (0, 32), (0, 64), (256, 0), (768, 0), (1024, 0), (256, 32), (768, 64))
+#: a wider split-count grid, on by default (BIGDL_WGRAD_EXTRA=0 drops it): ResNet-50 step 20.77-20.86
+#: vs 20.86-20.90 ms, 3 interleaved repeats (profiles/r5_wgrad_candidates_ab.txt)
+WGRAD_EXTRA = ((512, 32), (512, 64), (1536, 0), (2048, 32), (2048, 0))
 
 
 #: fp32 direct-operand conv (ops/csrc/conv_x3.hip) tiles (BM, BN | wave-layout bits): (0, 0) = the
@@ -226,7 +229,8 @@ WGRAD32_CANDIDATES = ((0,), (-256,), (-1024,), (-2048,), (-4096,))
 
 def _candidates(key):
     if isinstance(key, tuple) and key and key[0] == "wg":
-        return WGRAD_CANDIDATES
+        import os
+        return WGRAD_CANDIDATES + (() if os.environ.get("BIGDL_WGRAD_EXTRA") == "0" else WGRAD_EXTRA)
     if isinstance(key, tuple) and key and key[0] == "wg32":
         return WGRAD32_CANDIDATES
     if isinstance(key, tuple) and key and key[0] == "x3":

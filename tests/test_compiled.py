@@ -111,7 +111,7 @@ def test_training_compile_phase_pins_fwd_dgrad_wgrad_and_keeps_training():
     including the 32x32x16 conv tiles and the wgrad split / depth choices, ends up in use) must leave
     training numerically where the heuristic kernels put it."""
     import copy
-    from bigdl.nn.compiled import autotune_training_step, TILE_CANDIDATES, WGRAD_CANDIDATES
+    from bigdl.nn.compiled import autotune_training_step, TILE_CANDIDATES, WGRAD_CANDIDATES, WGRAD_EXTRA
     from bigdl.ops import native_ops as NO
     from bigdl.utils.engine import Engine
     from bigdl.utils import config
@@ -149,7 +149,7 @@ def test_training_compile_phase_pins_fwd_dgrad_wgrad_and_keeps_training():
     l1, w1, chosen = run(True)
     kinds = {"wg" if k[0] == "wg" else "conv" for k in chosen}
     assert kinds == {"wg", "conv"}, chosen
-    assert all(v in (WGRAD_CANDIDATES if k[0] == "wg" else TILE_CANDIDATES) for k, v in chosen.items())
+    assert all(v in (WGRAD_CANDIDATES + WGRAD_EXTRA if k[0] == "wg" else TILE_CANDIDATES) for k, v in chosen.items())
     rel = float((w1 - w0).norm() / w0.norm())
     assert rel < 2e-2 and abs(l1 - l0) < 0.05 * max(1.0, abs(l0)), (rel, l0, l1)
     NO.conv_tile_table().clear()
