@@ -88,6 +88,7 @@ def test_class_nll_one_based_and_padding():
 
 
 def test_cross_entropy_equals_logsoftmax_nll():
+    torch.manual_seed(0)  # unseeded draws made the absolute tolerance flaky on large losses
     x = torch.randn(6, 10)
     t = torch.randint(1, 11, (6,)).float()
     ce = CrossEntropyCriterion()
@@ -96,7 +97,7 @@ def test_cross_entropy_equals_logsoftmax_nll():
     xr = x.clone().requires_grad_(True)
     lr = torch.nn.functional.cross_entropy(xr, t.long() - 1)
     lr.backward()
-    assert abs(float(l) - float(lr)) < 1e-5
+    assert abs(float(l) - float(lr)) <= 1e-5 * max(1.0, abs(float(lr)))
     torch.testing.assert_close(g, xr.grad, rtol=1e-4, atol=1e-6)
 
 
