@@ -275,14 +275,14 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   bn_apply_rows<RES, RELU, BITS, kApplyUnroll>(x, res, y, M, C, scale, shift, bits, rcoef);
 }
 
-// A/B knobs (profiles/r3_bn_apply_ab.txt): BIGDL_BN_APPLY_BLOCKS caps the grid (default 1024: 0.87-1.06
+// A/B knobs (profiles/r3_bn_apply_ab.txt, r5_bn_apply_blocks_ab.txt): BIGDL_BN_APPLY_BLOCKS caps the grid (default 2048 since round 5; at 1024: 0.87-1.06
 // of the best streaming copy in isolation vs 0.64-0.98 at 2048; neutral inside the ResNet step),
 // BIGDL_BN_UNROLL=1 issues one row per trip instead of 4.
 static int apply_cap() {
   static int cap = [] {
     const char* e = getenv("BIGDL_BN_APPLY_BLOCKS");
     const int v = e ? atoi(e) : 0;
-    return v >= 64 ? v : 1024;
+    return v >= 64 ? v : 2048;  // round 5: 2048 20.64-20.69 vs 1024 20.69-20.73 ms (profiles/r5_bn_apply_blocks_ab.txt)
   }();
   return cap;
 }
