@@ -1309,7 +1309,19 @@ __global__ void __launch_bounds__(256) k_bn32_reduce(const float* __restrict__ x
 }
 
 // forward: y = relu?(x·scale + shift (+ res));  backward (BWD): gx = A·g' + B·x + Cc, g' = gy masked
-// by y > 0 (RELU), g' also stored to gres when given
+// by y > 0 (RELU), g' also stored to gres when given.
+// kU32 rows per trip with every load issued before the first use (as bn_apply_rows): one row per trip
+// left each thread with a single 32-B request in flight and the pass latency-bound (11.4 ms of the
+// fp32 ResNet-50 step at ≈3.6 TB/s, profiles/r5_fp32_profile.txt).  x / aux are read once per pass:
+// non-temporal loads keep them from displacing reusable lines.
+constexpr int kU32 = 4;
+__device__ __forceinline__ void ld8f_nt(const float* __restrict__ p, float (&v)[8]) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
 template <bool BWD, bool RELU>
 __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x, const float* __restrict__ aux,
                                                     const float* __restrict__ y_mask, float* __restrict__ out,
@@ -1330,56 +1342,68 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
       B[k] = coef[C + cg * 8 + k];
       Cc[k] = BWD ? coef[2 * C + cg * 8 + k] : 0.f;
     }
-    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += rstride) {
-      const size_t off = (size_t)r * C + (size_t)cg * 8;
-      float xv[8], o[8];
-      ld8f(x + off, xv);
-      if (BWD) {
-        float gv[8];
-        ld8f(aux + off, gv);
-        if (RELU) {
-          if (mbits) {
-            const unsigned mb = mbits[(size_t)r * (C >> 3) + cg];
+    for (long long r = (long long)blockIdx.x * g.RPI + r_off; r < M; r += kU32 * rstride) {
+      float xv[kU32][8], av[kU32][8];
+      unsigned mbv[kU32];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
+      for (int u = 0; u < kU32; ++u) {
+        const long long ru = r + u * rstride;
+        const size_t off = (size_t)(ru < M ? ru : r) * C + (size_t)cg * 8;
+        ld8f_nt(x + off, xv[u]);
+        if (BWD || aux) ld8f_nt(aux + off, av[u]);
+        if (BWD && RELU) {
+          if (mbits) {
+            mbv[u] = mbits[(size_t)(ru < M ? ru : r) * (C >> 3) + cg];
           } else {
             float yv[8];
             ld8f(y_mask + off, yv);
+            unsigned m = 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+            for (int k = 0; k < 8; ++k) m |= (yv[k] > 0.f ? 1u : 0u) << k;
+            mbv[u] = m;
           }
         }
-        if (gres) st8f(gres + off, gv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[k], Cc[k]));
-      } else {
-        float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (aux) ld8f(aux + off, rv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float v = fmaf(xv[k], A[k], B[k]) + rv[k];
-          o[k] = RELU ? fmaxf(v, 0.f) : v;
-        }
-        if (RELU && mbits) {  // the ReLU mask as bits for the backward (instead of re-reading y)
-          unsigned mb = 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) mb |= (o[k] > 0.f ? 1u : 0u) << k;
-          mbits[(size_t)r * (C >> 3) + cg] = (uint8_t)mb;
-        }
       }
-      if (out) st8f(out + off, o);
-      if (sp) {  // the bf16x3 [hi | lo] split of the output for the consuming conv (fp32x3.py split2)
-        uint32_t hw[4], lw[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bf16_t h0 = f2bf(o[2 * e]), h1 = f2bf(o[2 * e + 1]);
-          const bf16_t l0 = f2bf(o[2 * e] - bf2f(h0)), l1 = f2bf(o[2 * e + 1] - bf2f(h1));
-          hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-          lw[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+      for (int u = 0; u < kU32; ++u) {
+        const long long ru = r + u * rstride;
+        if (ru >= M) break;
+        const size_t off = (size_t)ru * C + (size_t)cg * 8;
+        float o[8];
+        if (BWD) {
+          float gv[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv[k] = (!RELU || ((mbv[u] >> k) & 1u)) ? av[u][k] : 0.f;
+          if (gres) st8f(gres + off, gv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], gv[k], fmaf(B[k], xv[u][k], Cc[k]));
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float v = fmaf(xv[u][k], A[k], B[k]) + (aux ? av[u][k] : 0.f);
+            o[k] = RELU ? fmaxf(v, 0.f) : v;
+          }
+          if (RELU && mbits) {  // the ReLU mask as bits for the backward (instead of re-reading y)
+            unsigned mb = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) mb |= (o[k] > 0.f ? 1u : 0u) << k;
+            mbits[(size_t)ru * (C >> 3) + cg] = (uint8_t)mb;
+          }
         }
-        bf16_t* d = sp + (size_t)r * 2 * C + (size_t)cg * 8;
-        *reinterpret_cast<uint4*>(d) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-        *reinterpret_cast<uint4*>(d + C) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        if (out) st8f(out + off, o);
+        if (sp) {  // the bf16x3 [hi | lo] split of the output for the consuming conv (fp32x3.py split2)
+          uint32_t hw[4], lw[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf16_t h0 = f2bf(o[2 * e]), h1 = f2bf(o[2 * e + 1]);
+            const bf16_t l0 = f2bf(o[2 * e] - bf2f(h0)), l1 = f2bf(o[2 * e + 1] - bf2f(h1));
+            hw[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            lw[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+          }
+          bf16_t* d = sp + (size_t)ru * 2 * C + (size_t)cg * 8;
+          *reinterpret_cast<uint4*>(d) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+          *reinterpret_cast<uint4*>(d + C) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
       }
     }
   }

@@ -90,6 +90,55 @@ BIGDL_EXPORT int bigdl_threshold_bwd_bf16(const void* gy, const void* ref, void*
   BIGDL_CHECK_LAUNCH();
 }
 
+// fp32 variants (the reference's precision, DL/nn/Threshold.scala:46-421): 16 B per lane, a scalar
+// tail for n % 4.  Backward takes the forward's INPUT (in-place forward: its output, which is > th
+// exactly where the input was, since the replacement value v ≤ th is the only other output).
+__global__ void k_threshold_fwd_f32(const float* __restrict__ x, float* __restrict__ y, long long n, float th,
+                                    float val) {
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    v.x = v.x > th ? v.x : val;
+    v.y = v.y > th ? v.y : val;
+    v.z = v.z > th ? v.z : val;
+    v.w = v.w > th ? v.w : val;
+    reinterpret_cast<float4*>(y)[i] = v;
+  }
+  for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = x[i] > th ? x[i] : val;
+}
+
+__global__ void k_threshold_bwd_f32(const float* __restrict__ gy, const float* __restrict__ ref,
+                                    float* __restrict__ gx, long long n, float th) {
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 g = reinterpret_cast<const float4*>(gy)[i];
+    const float4 r = reinterpret_cast<const float4*>(ref)[i];
+    g.x = r.x > th ? g.x : 0.f;
+    g.y = r.y > th ? g.y : 0.f;
+    g.z = r.z > th ? g.z : 0.f;
+    g.w = r.w > th ? g.w : 0.f;
+    reinterpret_cast<float4*>(gx)[i] = g;
+  }
+  for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    gx[i] = ref[i] > th ? gy[i] : 0.f;
+}
+
+BIGDL_EXPORT int bigdl_threshold_fwd_f32(const void* x, void* y, long long n, float th, float val, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_threshold_fwd_f32, dim3(bigdl_grid((n + 3) / 4, 256)), dim3(256), 0, s, (const float*)x,
+                     (float*)y, n, th, val);
+  BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_threshold_bwd_f32(const void* gy, const void* ref, void* gx, long long n, float th,
+                                         hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_threshold_bwd_f32, dim3(bigdl_grid((n + 3) / 4, 256)), dim3(256), 0, s, (const float*)gy,
+                     (const float*)ref, (float*)gx, n, th);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // ------------------------------------------------------------------------------------------------
 // fused SGD (DL/optim/SGD.scala:61-124) over a flat fp32 buffer:
 //   g' = g*scale (+ wd * wds * w) ; v = first ? g' : mom*v + (1-damp)*g' ;

@@ -398,3 +398,45 @@ BIGDL_EXPORT int bigdl_colsum_bf16(const void* x, long long ld, float* out, int 
                      rps, scale);
   BIGDL_CHECK_LAUNCH();
 }
+
+// fp32 rows (the fp32 compute mode's bias gradients, NHWC dY as [N·H·W][K]): 4 columns per lane,
+// 64 column chunks × 4 row groups per block, N % 4 == 0.
+__global__ void __launch_bounds__(256) k_colsum_f32(const float* __restrict__ x, long long ld, float* __restrict__ out,
+                                                    int M, int N, int rows_per_split, float scale) {
+  __shared__ float red[4][256 + 4];
+  const int cc = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 256 + cc * 4;
+  const int mb = blockIdx.y * rows_per_split;
+  const int me = min(M, mb + rows_per_split);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    for (int m = mb + rg; m < me; m += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + (long long)m * ld + n);
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+  }
+  red[rg][cc * 4 + 0] = a.x;
+  red[rg][cc * 4 + 1] = a.y;
+  red[rg][cc * 4 + 2] = a.z;
+  red[rg][cc * 4 + 3] = a.w;
+  __syncthreads();
+  const int c = threadIdx.x;
+  if (blockIdx.x * 256 + c < N) atomicAdd(out + blockIdx.x * 256 + c, scale * (red[0][c] + red[1][c] + red[2][c] + red[3][c]));
+}
+
+BIGDL_EXPORT int bigdl_colsum_f32(const void* x, long long ld, float* out, int M, int N, float scale, hipStream_t s) {
+  if (M <= 0 || N <= 0 || N % 4 || ld < N || ld % 4 || !al(x, 16)) return (int)hipErrorInvalidValue;
+  const int gx = (N + 255) / 256;
+  int splits = (512 + gx - 1) / gx;
+  const int max_splits = (M + 63) / 64;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1 || g_bigdl_deterministic) splits = 1;
+  const int rps = (M + splits - 1) / splits;
+  splits = (M + rps - 1) / rps;
+  hipLaunchKernelGGL(k_colsum_f32, dim3((unsigned)gx, (unsigned)splits), dim3(256), 0, s, (const float*)x, ld, out, M,
+                     N, rps, scale);
+  BIGDL_CHECK_LAUNCH();
+}

@@ -169,6 +169,169 @@ def chunk_split(w_rows: torch.Tensor) -> torch.Tensor:
     return split2(v, 32)
 
 
+# ---- weight operands of a whole step in one launch (csrc/weight_x3.hip k_wx3_multi) ----------------
+# Every filter-derived operand (forward chunks, flipped / transposed dgrad chunks per parity class, the
+# s2d stem filter, Linear [hi | lo | hi] rows) is cached per (weight, form).  An entry is valid while
+# its weight tensor is alive, its version counter unchanged (torch in-place writes) and it is not
+# marked dirty by a native update of the memory it derives from (:func:`mark_dirty`, called by the
+# fused optimizer kernels and the DistriOptimizer's weight gathers).  The first access to a dirty
+# entry refreshes EVERY dirty entry in one launch, so a training step pays one launch after its update
+# instead of ≈120 split / flip / gather launches on the forward and backward critical paths.
+_WP: dict = {}          # key → entry dict
+_WP_TABLES: dict = {}   # tuple(entry ids) → (device table, total blocks, keep-alive)
+_WX_REC = [0]
+
+
+def _wx_rec_size():
+    if not _WX_REC[0]:
+        _WX_REC[0] = int(N.lib().bigdl_wx3_job_size())
+    return _WX_REC[0]
+
+
+def _wx_job(buf, i, e, first):
+    kind, dims, strides, cls = e["job"]
+    K_, C_, R_, S_ = dims
+    ia, la = C.c_int * 32, C.c_longlong * 4
+    ros, sos, rm, sm, offs = [1] * 4, [1] * 4, [0] * 32, [0] * 32, [0] * 4
+    for q, (ro, so, rmap, smap, off) in enumerate(cls):
+        ros[q], sos[q], offs[q] = ro, so, off
+        rm[q * 8:q * 8 + ro] = rmap
+        sm[q * 8:q * 8 + so] = smap
+    nb = C.c_longlong(0)
+    check(N.lib().bigdl_wx3_job(C.byref(buf, i * _wx_rec_size()), C.c_void_p(e["src"]), ptr(e["out"]), kind, K_, C_,
+                                R_, S_,
+                                *(C.c_longlong(v) for v in strides), max(1, len(cls)), ia(*ros), ia(*sos), ia(*rm),
+                                ia(*sm), la(*offs), C.c_longlong(first), C.byref(nb)), "wx3_job")
+    return nb.value
+
+
+def _wx_run_one(e):
+    buf = (C.c_ubyte * _wx_rec_size())()
+    _wx_job(buf, 0, e, 0)
+    check(N.lib().bigdl_wx3_one(buf, _s()), "wx3_one")
+
+
+def _wx_refresh_dirty():
+    ents = [e for e in _WP.values() if e["dirty"] and e["ref"]() is not None]
+    if not ents:
+        return
+    key = tuple(id(e) for e in ents)
+    tab = _WP_TABLES.get(key)
+    if tab is None:
+        rec = _wx_rec_size()
+        buf = (C.c_ubyte * (rec * len(ents)))()
+        first = 0
+        for i, e in enumerate(ents):
+            first += _wx_job(buf, i, e, first)
+        host = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+        dev = torch.empty(host.numel() + 16, dtype=torch.uint8, device=ents[0]["out"].device)
+        off = (-dev.data_ptr()) % 16
+        table = dev[off:off + host.numel()]
+        table.copy_(host)
+        if len(_WP_TABLES) > 64:
+            _WP_TABLES.clear()
+        tab = _WP_TABLES[key] = (table, first, ents, dev)
+    table, total, _e, _keep = tab
+    check(N.lib().bigdl_wx3_multi(ptr(table), C.c_int(len(ents)), C.c_longlong(total), _s()), "wx3_multi")
+    for e in ents:
+        e["dirty"] = False
+        e["ver"] = e["ref"]()._version
+
+
+def mark_dirty(t) -> None:
+    """The memory of ``t`` (an fp32 weight buffer or a slice of one) was rewritten by a kernel torch
+    does not see (fused optimizer update, weight all-gather): derived operands over it go stale."""
+    if not _WP or not isinstance(t, torch.Tensor) or not t.is_cuda:
+        return
+    lo = t.data_ptr()
+    hi = lo + t.numel() * t.element_size()
+    for e in _WP.values():
+        if e["lo"] < hi and lo < e["hi"]:
+            e["dirty"] = True
+
+
+def _wprep(w, form):
+    """The bf16 operand of fp32 weight ``w`` in ``form``:
+    ("fwd",) → conv_x3 chunks of the KRSC rows; ("s2d",) → the stem's s2d filter chunks;
+    ("dg", classes) → [view per class] of the flipped, transposed sub-filters, classes = tuple of
+    (rmap, smap) tap lists; ("rows3", rows, cp, transposed) → [rows][3·cp] = [hi | lo | hi] of w (or wᵀ)."""
+    if not (w.is_cuda and hasattr(N.lib(), "bigdl_wx3_multi")):
+        return NotImplemented
+    wd = w.detach()
+    converted = wd.dtype != _f32
+    if converted:
+        wd = wd.float()
+    root = w._base if w._base is not None else w  # the layer's weight / the parameter arena: stable
+    key = (wd.data_ptr(), tuple(wd.shape), tuple(wd.stride()), form)
+    capturing = torch.cuda.is_current_stream_capturing()
+    e = None if (converted or capturing) else _WP.get(key)
+    if e is not None:
+        if e["ref"]() is root:
+            if e["dirty"] or e["ver"] != w._version:
+                e["dirty"] = True
+                _wx_refresh_dirty()
+            return e["views"]
+        _WP.pop(key, None)
+    kind = form[0]
+    if kind in ("fwd", "s2d", "dg"):
+        k_, c_, r_, s_ = wd.shape
+    if kind == "fwd":
+        if (r_ * s_ * c_) % 32:
+            return NotImplemented
+        out = torch.empty(2 * wd.numel(), dtype=_bf16, device=wd.device)
+        job = (0, (k_, c_, r_, s_), wd.stride(), ())
+        views = out.view(k_, (r_ * s_ * c_) // 32, 64)
+    elif kind == "s2d":
+        r2, s2 = (r_ + 1) // 2, (s_ + 1) // 2
+        if 4 * c_ > 32:
+            return NotImplemented
+        out = torch.empty(k_ * r2 * s2 * 64, dtype=_bf16, device=wd.device)
+        job = (2, (k_, c_, r_, s_), wd.stride(), ())
+        views = out.view(k_, r2 * s2, 64)
+    elif kind == "dg":
+        classes = form[1]
+        if k_ % 32 or not 1 <= len(classes) <= 4 or any(len(a) > 8 or len(b) > 8 for a, b in classes):
+            return NotImplemented
+        cls, off, sizes = [], 0, []
+        for rmap, smap in classes:
+            n = c_ * len(rmap) * len(smap) * k_ * 2
+            cls.append((len(rmap), len(smap), list(rmap), list(smap), off))
+            sizes.append(n)
+            off += n
+        out = torch.empty(off, dtype=_bf16, device=wd.device)
+        views = [out[o:o + n].view(c_, n // (2 * c_) // 32, 64)
+                 for (_a, _b, _c, _d, o), n in zip(cls, sizes)]
+        job = (1, (k_, c_, r_, s_), wd.stride(), tuple(cls))
+    elif kind == "rows3":
+        rows, cp, tr = form[1], form[2], form[3]
+        nr, nc = (wd.shape[1], wd.shape[0]) if tr else (wd.shape[0], wd.shape[1])
+        sr, sc = (wd.stride(1), wd.stride(0)) if tr else (wd.stride(0), wd.stride(1))
+        if rows < nr or cp % 8 or cp < nc:
+            return NotImplemented
+        out = torch.empty((rows, 3 * cp), dtype=_bf16, device=wd.device)
+        job = (3, (nr, nc, rows, cp), (sr, sc, 0, 0), ())
+        views = out
+    else:
+        raise ValueError(form)
+    lo = wd.data_ptr()
+    span = 1 + sum((d - 1) * abs(st) for d, st in zip(wd.shape, wd.stride()))
+    # the entry keeps no reference to the weight memory (a weak reference to its owner instead), so a
+    # freed model releases it; refreshes only ever run over entries whose owner is alive
+    e = {"src": lo, "out": out, "views": views, "job": job, "ref": weakref.ref(root), "ver": w._version,
+         "dirty": True, "lo": lo, "hi": lo + 4 * span}
+    if converted or capturing:
+        _wx_run_one(e)  # a converted copy or a HIP-graph capture: recompute per call, no cache
+        return views
+    dead = [k for k, v in _WP.items() if v["ref"]() is None]
+    for k in dead:
+        _WP.pop(k, None)
+    if dead:
+        _WP_TABLES.clear()
+    _WP[key] = e
+    _wx_refresh_dirty()
+    return views
+
+
 def _x3(x, w2, y, nb, h, w, c, k, r, s, p, q, stride, pad, dil, bias=None, res=None, relu=False, stats=None, rep=0,
         shift=None, bnx=None, mean=None, bits=None, bsc=None, bsh=None, scatter=None, res_strided=None, tile=None,
         persist=0):
@@ -202,9 +365,24 @@ def _x3_geom_ok(c, k, r, s, pad):
 
 
 def _w_fwd(w4):
-    """The forward filter as conv_x3 chunks: KRSC rows of R·S·C."""
+    """The forward filter as conv_x3 chunks: KRSC rows of R·S·C (cached per weight update)."""
+    v = _wprep(w4, ("fwd",))
+    if v is not NotImplemented:
+        return v
     k = w4.shape[0]
     return chunk_split(w4.detach().float().permute(0, 2, 3, 1).reshape(k, -1))
+
+
+def _w_dgrad(w4, classes):
+    """[per class] the flipped, transposed sub-filter chunks of the data gradient: class = (rmap, smap),
+    W'[c][i][j][k] = W[k][c][rmap[i]][smap[j]] as rows of C (cached per weight update)."""
+    form = ("dg", tuple((tuple(a), tuple(b)) for a, b in classes))
+    v = _wprep(w4, form)
+    if v is not NotImplemented:
+        return v
+    wf = w4.detach().float()
+    return [chunk_split(wf[:, :, list(a)][:, :, :, list(b)].permute(1, 2, 3, 0).reshape(wf.shape[1], -1))
+            for a, b in classes]
 
 
 def _stem_ok(c, k, stride, dilation):
@@ -250,7 +428,10 @@ def _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot):
         slot[0] = (("s2d",) + _slot_key(x, 32, True)[1:], xs)
     y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
     bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
-    _x3(xs, chunk_split(_stem_weights(w4).reshape(k, -1)), y, nb, xs.shape[2], xs.shape[3], 32, k, r2, s2, p, q,
+    w2 = _wprep(w4, ("s2d",))
+    if w2 is NotImplemented:
+        w2 = chunk_split(_stem_weights(w4).reshape(k, -1))
+    _x3(xs, w2, y, nb, xs.shape[2], xs.shape[3], 32, k, r2, s2, p, q,
         (1, 1), (0, 0), (1, 1), bias=bias, relu=relu, stats=stats, rep=rep, shift=shift)
     return y
 
@@ -269,11 +450,25 @@ def _stem_wgrad(x, gy, gw_acc, scale, pad, slot):
         slot[0] = None
     else:
         xs = _s2d(x, pad, r, s, p, q)
-    gw2 = torch.zeros((k, r2, s2, 32), dtype=_f32, device=x.device)
+    fold = hasattr(N.lib(), "bigdl_s2d_wgrad_fold") and gw_acc.dtype == _f32
+    bkey = (gw_acc.data_ptr(), k, r2, s2, gw_acc.device)
+    gw2 = _S2D_ACC.get(bkey) if fold else None
+    if gw2 is None:
+        # persistent accumulation buffer (zeroed once; the fold kernel clears what it reads)
+        gw2 = torch.zeros((k, r2, s2, 32), dtype=_f32, device=x.device)
+        if fold:
+            _S2D_ACC[bkey] = gw2
     check(N.lib().bigdl_conv_wgrad_f32(ptr(xs), ptr(gy), ptr(gw2), C.c_float(1.0), nb, xs.shape[2], xs.shape[3], 32, k,
                                        r2, s2, p, q, 1, 1, 0, 0, 1, 1, 0, _s()), "conv_wgrad_f32(s2d)")
+    if fold:
+        check(N.lib().bigdl_s2d_wgrad_fold(ptr(gw2), ptr(gw_acc), k, c, r, s, *(C.c_longlong(v) for v in gw_acc.stride()),
+                                           C.c_float(float(scale)), _s()), "s2d_wgrad_fold")
+        return
     g6 = gw2[..., :4 * c].reshape(k, r2, s2, c, 2, 2).permute(0, 3, 1, 4, 2, 5).reshape(k, c, 2 * r2, 2 * s2)
     gw_acc.add_(g6[:, :, :r, :s], alpha=scale)
+
+
+_S2D_ACC: dict = {}
 
 
 def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None, slot=None):
@@ -477,15 +672,15 @@ def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, laz
         if pd[0] < 0 or pd[1] < 0 or not _x3_geom_ok(k, c, r, s, pd) or (h, w) != (p + 2 * pd[0] - r + 1,
                                                                                  q + 2 * pd[1] - s + 1):
             return NotImplemented
-        wt = w4.detach().float().flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1)  # [C][R][S][K]
+        wt = _w_dgrad(w4, [(tuple(range(r - 1, -1, -1)), tuple(range(s - 1, -1, -1)))])[0]  # [C][R][S][K]
         gi = torch.empty((nb, c, h, w), dtype=_f32, device=gy.device, memory_format=_cl)
         if bnb is not None:
             buf, rep, bx, mean, bits, bsc, bsh = bnb
-            _x3(gy, chunk_split(wt), gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual, stats=buf,
+            _x3(gy, wt, gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual, stats=buf,
                 rep=rep, bnx=bx, mean=mean, bits=bits, bsc=bsc, bsh=bsh, res_strided=res_strided)
             bn_fuse["partial"], bn_fuse["G"] = buf, rep
         else:
-            _x3(gy, chunk_split(wt), gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual,
+            _x3(gy, wt, gi, nb, p, q, k, c, r, s, h, w, (1, 1), pd, (1, 1), res=residual,
                 res_strided=res_strided)
         return gi
     if res_strided is not None:
@@ -498,11 +693,11 @@ def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, laz
     covered = len(live) == len(classes) and sum(cl[4] * cl[5] for cl in live) == h * w
     if bnb is not None and not covered:  # tap-less pixels would miss the BN-backward sums
         return NotImplemented
-    wf = w4.detach().float()
+    subs = _w_dgrad(w4, [(tuple(rs[::-1]), tuple(ss[::-1])) for (a, b, rs, ss, *_r) in live])
     if lazy and residual is None and r == 1 and s == 1 and tuple(pad) == (0, 0) and len(live) == 1:
         (a, b, rs, ss, ho, wo, ea, eb) = live[0]
         tmp = torch.empty((nb, c, ho, wo), dtype=_f32, device=gy.device, memory_format=_cl)
-        _x3(gy, chunk_split(wf.reshape(k, c).t()), tmp, nb, p, q, k, c, 1, 1, ho, wo, (1, 1), (0, 0), (1, 1))
+        _x3(gy, subs[0], tmp, nb, p, q, k, c, 1, 1, ho, wo, (1, 1), (0, 0), (1, 1))
         return StridedGrad(tmp, tuple(stride), (nb, c, h, w))
     gi = torch.empty((nb, c, h, w), dtype=_f32, device=gy.device, memory_format=_cl)
     if not covered:
@@ -515,23 +710,40 @@ def _direct_dgrad(gy, w4, x_shape, stride, pad, dilation, residual, bn_fuse, laz
     if bnb is not None:
         buf, rep, bx, mean, bits, bsc, bsh = bnb
         bn_kw = dict(stats=buf, rep=rep, bnx=bx, mean=mean, bits=bits, bsc=bsc, bsh=bsh)
-    for (a, b, rs, ss, ho, wo, ea, eb) in live:
+    for (a, b, rs, ss, ho, wo, ea, eb), sub in zip(live, subs):
         ra, sb = len(rs), len(ss)
-        sub = wf[:, :, rs[::-1]][:, :, :, ss[::-1]].permute(1, 2, 3, 0).reshape(c, -1)  # [C][Ra][Sb][K]
-        _x3(gy, chunk_split(sub), gi, nb, p, q, k, c, ra, sb, ho, wo, (1, 1), (ra - 1 - ea, sb - 1 - eb), (1, 1),
+        _x3(gy, sub, gi, nb, p, q, k, c, ra, sb, ho, wo, (1, 1), (ra - 1 - ea, sb - 1 - eb), (1, 1),
             res=residual, scatter=(stride[0], stride[1], a, b, h, w), **bn_kw)
     if bnb is not None:
         bn_fuse["partial"], bn_fuse["G"] = bnb[0], bnb[1]
     return gi
 
 
+def _direct_wgrad_ok(x, gy, gw_acc) -> bool:
+    nb, c, h, w = x.shape
+    k = gw_acc.shape[0]
+    p, q = gy.shape[2], gy.shape[3]
+    return (_direct() and _x3_has() and c % 8 == 0 and k % 8 == 0 and _cl_f32(x) and _cl_f32(gy)
+            and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
+            and _fits(nb * h * w * c * 4, nb * p * q * k * 4))
+
+
+def bias_grad_acc(gy, gb_acc, scale):
+    """gb += scale · Σ_{n,h,w} dY (the conv bias gradient) on the fp32 column-sum kernel; torch's
+    reduction only for a layout the kernel does not take."""
+    from .native_ops import colsum_acc
+    k = gy.shape[1]
+    if (gy.dim() == 4 and _cl_f32(gy) and gb_acc.dtype == _f32 and gb_acc.is_contiguous()
+            and colsum_acc(gy.permute(0, 2, 3, 1).reshape(-1, k), gb_acc.view(-1), scale) is not NotImplemented):
+        return
+    gb_acc.add_(gy.sum((0, 2, 3)).reshape(gb_acc.shape), alpha=scale)
+
+
 def _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation):
     nb, c, h, w = x.shape
     k, _, r, s = gw_acc.shape
     p, q = gy.shape[2], gy.shape[3]
-    if not (_direct() and _x3_has() and c % 8 == 0 and k % 8 == 0 and _cl_f32(x) and _cl_f32(gy)
-            and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous()
-            and _fits(nb * h * w * c * 4, nb * p * q * k * 4)):
+    if not _direct_wgrad_ok(x, gy, gw_acc):
         return NotImplemented
     def fn(t):
         # t = (splits,): 0 = the launcher's heuristic (≈512 blocks), < 0 = -target block count
@@ -556,12 +768,37 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     if (not need_input and gw_acc is not None and _stem_ok(x.shape[1], w4.shape[0], stride, dilation)
             and _cl_f32(gy) and x.dtype == _f32 and gw_acc.dtype == _f32):
         if scale != 0:
-            _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
-        if gb_acc is not None and scale != 0:
-            gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+            from .native_ops import _wgrad_side_stream
+            side = _wgrad_side_stream(gy)
+            if side is not None:
+                with torch.cuda.stream(side):
+                    _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
+                    if gb_acc is not None:
+                        bias_grad_acc(gy, gb_acc, scale)
+                for t in (x, gy):
+                    t.record_stream(side)
+            else:
+                _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
+                if gb_acc is not None:
+                    bias_grad_acc(gy, gb_acc, scale)
         return None
     if _direct() and _x3_has() and _cl_f32(gy) and x.dtype == _f32:
-        # each half independently on the direct kernels when its shape allows, else on the split path
+        # each half independently on the direct kernels when its shape allows, else on the split path.
+        # The one-launch fp32 weight gradient is forked onto the wgrad side stream BEFORE the data
+        # gradient (as the bf16 path does, native_ops.conv2d_backward), so it runs beside the
+        # backward-data chain; the optimizer joins the side stream before the update.
+        wg_done = False
+        if gw_acc is not None and scale != 0 and _direct_wgrad_ok(x, gy, gw_acc):
+            from .native_ops import _wgrad_side_stream
+            side = _wgrad_side_stream(gy)
+            if side is not None:
+                with torch.cuda.stream(side):
+                    _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation)
+                    if gb_acc is not None:
+                        bias_grad_acc(gy, gb_acc, scale)
+                for t in (x, gy):
+                    t.record_stream(side)
+                wg_done = True
         gi = None
         if need_input:
             gi = _direct_dgrad(gy, w4, tuple(x.shape), stride, pad, dilation, residual, bn_fuse, lazy_strided)
@@ -569,13 +806,15 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
                 gi = _split_backward(gy, x, w4, stride, pad, dilation, True, None, scale, slot, residual, bn_fuse)
                 if gi is NotImplemented:
                     return NotImplemented
-        if gw_acc is not None and scale != 0:
+        if gw_acc is not None and scale != 0 and not wg_done:
             if _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation) is NotImplemented:
                 r = _split_backward(gy, x, w4, stride, pad, dilation, False, gw_acc, scale, slot)
                 if r is NotImplemented:
                     return NotImplemented
-        if gb_acc is not None and scale != 0:
-            gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+            if gb_acc is not None:
+                bias_grad_acc(gy, gb_acc, scale)
+        elif gb_acc is not None and scale != 0 and not wg_done:
+            bias_grad_acc(gy, gb_acc, scale)
         return gi
     return _split_backward_full(gy, x, w4, stride, pad, dilation, need_input, gw_acc, gb_acc, scale, residual, slot,
                                 bn_fuse)
@@ -687,7 +926,7 @@ def _split_backward_full(gy, x, w4, stride, pad, dilation, need_input, gw_acc, g
         if not direct:
             gw_acc.add_(target[:k, :, :, :c].permute(0, 3, 1, 2), alpha=scale)
     if gb_acc is not None and scale != 0:
-        gb_acc.add_(gy.sum((0, 2, 3)), alpha=scale)
+        bias_grad_acc(gy, gb_acc, scale)
     return gi
 
 
@@ -705,8 +944,10 @@ def linear_forward(x, w, b, act=0):
     n = w.shape[0]
     k8, n4 = _r(k, 8), _r(n, 4)
     a3 = split(x, k8, HHL, False)
-    b3 = split(w.detach().float(), k8, HLH, False,
-               out=torch.zeros((n4, 3 * k8), dtype=_bf16, device=x.device) if n4 != n else None)
+    b3 = _wprep(w, ("rows3", n4, k8, False))
+    if b3 is NotImplemented:
+        b3 = split(w.detach().float(), k8, HLH, False,
+                   out=torch.zeros((n4, 3 * k8), dtype=_bf16, device=x.device) if n4 != n else None)
     bias = None
     if b is not None:
         bias = torch.zeros(n4, dtype=_f32, device=x.device)
@@ -727,8 +968,10 @@ def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1
     two = _two_part()
     if need_input:
         g3 = split(gy, n8, HHL, False)
-        wt3 = split(w.detach().float().t(), n8, HLH, False,
-                    out=torch.zeros((k4, 3 * n8), dtype=_bf16, device=gy.device) if k4 != k else None)
+        wt3 = _wprep(w, ("rows3", k4, n8, True))
+        if wt3 is NotImplemented:
+            wt3 = split(w.detach().float().t(), n8, HLH, False,
+                        out=torch.zeros((k4, 3 * n8), dtype=_bf16, device=gy.device) if k4 != k else None)
         gi = _gemm_f32(g3, wt3, m, k4)
         if gi is NotImplemented:
             return NotImplemented
@@ -745,5 +988,8 @@ def linear_backward(gy, x, w, need_input=True, gw_acc=None, gb_acc=None, scale=1
         if not direct:
             gw_acc.add_(tgt[:n, :k].reshape(gw_acc.shape), alpha=scale)
     if gb_acc is not None and scale != 0:
-        gb_acc.add_(gy.sum(0).reshape(gb_acc.shape), alpha=scale)
+        from .native_ops import colsum_acc
+        if not (gb_acc.dtype == _f32 and gb_acc.is_contiguous()
+                and colsum_acc(gy, gb_acc.view(-1), scale) is not NotImplemented):
+            gb_acc.add_(gy.sum(0).reshape(gb_acc.shape), alpha=scale)
     return gi

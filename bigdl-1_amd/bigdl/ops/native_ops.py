@@ -79,7 +79,14 @@ def cast_copy(dst, src):
 # ------------------------------------------------------------------------------------------------ relu
 @register("relu_forward")
 def relu_forward(x, threshold=0.0, value=0.0, inplace=False):
-    if x.dtype != _bf16 or not _dense(x) or x.numel() % 8 or not _al16(x):
+    if not _dense(x) or not _al16(x):
+        return NotImplemented
+    if x.dtype == _f32:  # the reference's precision (DL/nn/Threshold.scala:46-421)
+        y = x if inplace else torch.empty_like(x)
+        check(_lib().bigdl_threshold_fwd_f32(ptr(x), ptr(y), _ll(x.numel()), _f(threshold), _f(value), _s()),
+              "threshold_fwd_f32")
+        return y
+    if x.dtype != _bf16 or x.numel() % 8:
         return NotImplemented
     y = x if inplace else torch.empty_like(x)
     check(_lib().bigdl_threshold_fwd_bf16(ptr(x), ptr(y), _ll(x.numel()), _f(threshold), _f(value), _s()),
@@ -89,13 +96,19 @@ def relu_forward(x, threshold=0.0, value=0.0, inplace=False):
 
 @register("relu_backward")
 def relu_backward(gy, ref, threshold=0.0):
-    if gy.dtype != _bf16 or ref.dtype != _bf16 or gy.shape != ref.shape:
+    if gy.dtype != ref.dtype or gy.dtype not in (_bf16, _f32) or gy.shape != ref.shape:
         return NotImplemented
-    if not (_dense(gy) and _dense(ref)) or gy.stride() != ref.stride() or gy.numel() % 8:
+    if not (_dense(gy) and _dense(ref)) or gy.stride() != ref.stride():
         return NotImplemented
     if not (_al16(gy) and _al16(ref)):
         return NotImplemented
     gx = torch.empty_like(gy)
+    if gy.dtype == _f32:
+        check(_lib().bigdl_threshold_bwd_f32(ptr(gy), ptr(ref), ptr(gx), _ll(gy.numel()), _f(threshold), _s()),
+              "threshold_bwd_f32")
+        return gx
+    if gy.numel() % 8:
+        return NotImplemented
     check(_lib().bigdl_threshold_bwd_bf16(ptr(gy), ptr(ref), ptr(gx), _ll(gy.numel()), _f(threshold), _s()),
           "threshold_bwd")
     return gx
@@ -1621,6 +1634,7 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
              lrs=None, wds=None, first_dev=None):
     """Fused SGD over a flat fp32 slice; ``g`` is fp32 or bf16 (the bf16-wire reduce-scatter output,
     read directly by the kernel instead of being unpacked into an fp32 shard first)."""
+    F3.mark_dirty(w)
     n = w.numel()
     if w.dtype != _f32 or g.dtype not in (_f32, _bf16) or not _vec_ok(w, buf, lrs, wds, n=n):
         return NotImplemented
@@ -1644,6 +1658,7 @@ def sgd_step(w, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_s
 @register("adam_step")
 def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0, shadow=None):
     import math
+    F3.mark_dirty(w)
     n = w.numel()
     if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n):
         return NotImplemented
@@ -1660,6 +1675,7 @@ def adam_step(w, g, m, v, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_sc
 def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0, shadow=None):
     """Adam whose iteration count ``dev_n`` (fp32 [1], before this step) is read on the device —
     the replay-safe form for HIP-graph capture; the caller advances ``dev_n`` afterwards."""
+    F3.mark_dirty(w)
     n = w.numel()
     if w.dtype != _f32 or g.dtype != _f32 or not _vec_ok(w, g, m, v, n=n) or not (dev_n.is_cuda and
                                                                                   dev_n.dtype == _f32):
@@ -1676,6 +1692,7 @@ def adam_step_dev(w, g, m, v, dev_n, lr, lr_decay, beta1, beta2, eps, weight_dec
 def adagrad_step(w, g, s, lr, lr_decay, n, weight_decay=0.0, grad_scale=1.0, shadow=None, dev_n=None):
     """Fused Adagrad update (bigdl_adagrad); ``dev_n`` (fp32 [1] on the device, the iteration count
     before this step) makes it replay-safe under HIP-graph capture, else ``n`` (host) is used."""
+    F3.mark_dirty(w)
     numel = w.numel()
     if w.dtype != _f32 or g.dtype != _f32 or s.dtype != _f32 or not _vec_ok(w, g, s, n=numel):
         return NotImplemented
@@ -2216,8 +2233,15 @@ def transpose_bf16(src):
 
 
 def colsum_acc(x, out, scale=1.0):
-    """out[n] += scale · Σ_m x[m][n]  (bias gradient, bf16 rows → fp32)."""
+    """out[n] += scale · Σ_m x[m][n]  (bias gradient, bf16 or fp32 rows → fp32)."""
     M, N_ = x.shape
+    if x.dtype == _f32:
+        if not (x.is_cuda and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.stride(0) >= N_ and _al16(x)
+                and N_ % 4 == 0 and out.dtype == _f32 and out.is_contiguous() and out.numel() == N_):
+            return NotImplemented
+        check(_lib().bigdl_colsum_f32(ptr(x), _ll(x.stride(0)), ptr(out), C.c_int(M), C.c_int(N_), _f(scale), _s()),
+              "colsum_f32")
+        return out
     if not (_mat_ok(x) and N_ % 8 == 0 and out.dtype == _f32 and out.is_contiguous() and out.numel() == N_):
         return NotImplemented
     check(_lib().bigdl_colsum_bf16(ptr(x), _ll(x.stride(0)), ptr(out), C.c_int(M), C.c_int(N_), _f(scale), _s()),

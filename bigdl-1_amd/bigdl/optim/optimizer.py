@@ -547,11 +547,24 @@ class BaseOptimizer:
         knobs = getattr(self, "_step_knobs", None)
         if knobs is None:  # read once: config lookups cost microseconds a launch-bound step cannot spare
             knobs = self._step_knobs = (float(config.get_property("bigdl.step.overlapMinMs")),
-                                        bool(config.get_property("bigdl.step.highPriority")))
+                                        bool(config.get_property("bigdl.step.highPriority")),
+                                        int(config.get_property("bigdl.step.maxInflight")))
         big = (getattr(self, "_step_ewma", None) or 0.0) * 1e3 >= knobs[0]
         self._overlap_now = big
-        if self.device.type != "cuda" or not big or not knobs[1] or torch.cuda.is_current_stream_capturing():
+        if self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
             return self._train_step_impl(batch)
+        # bounded run-ahead: at most maxInflight iterations queued on the device (the host waits on
+        # the end event of the oldest one); the reference's iteration ends on the host anyway
+        inflight = getattr(self, "_inflight", None)
+        if inflight is None:
+            import collections
+            inflight = self._inflight = collections.deque()
+        while knobs[2] > 0 and len(inflight) >= knobs[2]:
+            inflight.popleft().synchronize()
+        if not big or not knobs[1]:
+            loss = self._train_step_impl(batch)
+            self._note_inflight(inflight)
+            return loss
         hs = getattr(self, "_hp_stream", None)
         if hs is None:
             hs = self._hp_stream = torch.cuda.Stream(device=self.device, priority=-1)
@@ -565,7 +578,13 @@ class BaseOptimizer:
         cur.wait_stream(hs)
         if isinstance(loss, torch.Tensor) and loss.is_cuda:
             loss.record_stream(cur)
+        self._note_inflight(inflight)
         return loss
+
+    def _note_inflight(self, inflight):
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        inflight.append(ev)
 
     def _train_step_impl(self, batch: MiniBatch) -> torch.Tensor:
         """One synchronous-SGD iteration on ``batch``; returns the (rank-averaged) loss as a

@@ -43,11 +43,14 @@ def broadcast_module(module, src: int = 0):
         return
     p = module.parameters()
     arena = module.flat_parameters()
+    from ..ops import fp32x3
     if arena is not None:
         dist.broadcast(arena.weight, src)
+        fp32x3.mark_dirty(arena.weight)  # a collective writes behind torch's version counters
     elif p is not None:
         for w in p[0]:
             dist.broadcast(w.data, src)
+            fp32x3.mark_dirty(w)
     ex = module.getExtraParameter()
     if ex:
         for b in ex:

@@ -339,6 +339,8 @@ class DistriOptimizer(BaseOptimizer):
         if not b.needs_shadow:
             return
         from .. import ops
+        from ..ops import fp32x3
+        fp32x3.mark_dirty(self.flat.weight[b.lo:b.hi])  # fp32-mode weight operands derived from them
         if self._bf16_gather():
             # fp32 view of the gathered bf16 weights for layers that read fp32 params (BN γ/β);
             # exact fp32 masters stay in this rank's shard
@@ -553,6 +555,8 @@ class DistriOptimizer(BaseOptimizer):
         if self.sharded and self.comm_dtype.startswith("bf16"):
             for b in self.buckets:
                 dist.all_gather_into_tensor(self.flat.weight[b.lo:b.hi], self.shard_w[b.slo:b.shi])
+            from ..ops import fp32x3
+            fp32x3.mark_dirty(self.flat.weight)
             self.flat.mark_shadow_fresh()
 
     def _finish(self):
@@ -567,6 +571,8 @@ class DistriOptimizer(BaseOptimizer):
             for b in self.buckets:
                 per = b.shi - b.slo
                 self.shard_w[b.slo:b.shi].copy_(self.flat.weight[b.lo + r * per:b.lo + (r + 1) * per])
+        from ..ops import fp32x3
+        fp32x3.mark_dirty(self.flat.weight)
         if self.flat.shadow is not None:
             self.flat.refresh_shadow()
 

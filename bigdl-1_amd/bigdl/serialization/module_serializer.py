@@ -469,17 +469,16 @@ def _module_to_pb(ctx: _SerCtx, m) -> pb.BigDLModule:
             sub.preModules.extend([p.element.get_name() for p in n.prev_nodes])
             sub.nextModules.extend([q.element.get_name() for q in n.next_nodes])
             mp.subModules.add().CopyFrom(sub)
-            # the edges' output selections (Graph.scala doSerializeModule "<name>_edges": previous node
-            # name → 1-based output index of its Table, -1 = the whole activity)
+            # the edges' output selections (Graph.scala:672-698 doSerializeModule "<name>_edges", written by
+            # NameListConverter, DataConverter.scala:225-241): ONE NameAttrList named after the node whose
+            # attr maps each previous node's name → INT32 1-based output index of its Table (-1 = the
+            # whole activity)
             name = n.element.get_name()
             ev = mp.attr[f"{name}_edges"]
             ev.dataType = DT["NAME_ATTR_LIST"]
             ev.nameAttrListValue.name = name
-            inner = ev.nameAttrListValue.attr[name]
-            inner.dataType = DT["NAME_ATTR_LIST"]
-            inner.nameAttrListValue.name = name
             for p, idx in zip(n.prev_nodes, n.prev_index):
-                _set_attr(ctx, inner.nameAttrListValue.attr[p.element.get_name()], int(idx) if idx else -1)
+                _set_attr(ctx, ev.nameAttrListValue.attr[p.element.get_name()], int(idx) if idx else -1)
         _set_attr(ctx, mp.attr["inputNames"], [n.element.get_name() for n in m.inputs])
         _set_attr(ctx, mp.attr["outputNames"], [n.element.get_name() for n in m.outputs_nodes])
         if dyn:
@@ -557,8 +556,13 @@ def _module_from_pb(ctx: _DeCtx, mp):
         for sub in mp.subModules:
             nodes[sub.name] = (ModuleNode(_module_from_pb(ctx, sub)), list(sub.preModules))
         for name, (node, pres) in nodes.items():
+            # the decoded NameAttrList is the flat {previous node: index} map (its list name, the node's
+            # own name, is dropped by _get_attr); files of the round-5 writer nested it one level deeper
             edges = attrs.get(f"{name}_edges")
-            edges = edges.get(name, {}) if isinstance(edges, dict) else {}
+            if not isinstance(edges, dict):
+                edges = {}
+            elif isinstance(edges.get(name), dict) and name not in pres:
+                edges = edges[name]
             for p in pres:
                 idx = edges.get(p, -1) if isinstance(edges, dict) else -1
                 node((nodes[p][0], int(idx)) if idx is not None and int(idx) > 0 else nodes[p][0])

@@ -61,6 +61,7 @@ _REGISTRY = {
     "bigdl.native.require": (bool, True, "fail loudly on a GPU if the HIP extension is missing"),
     "bigdl.native.strict": (bool, False, "raise instead of warning when a device-tensor op falls back to the torch reference"),
     "bigdl.step.overlapMinMs": (float, 8.0, "enable the high-priority step stream and async wgrad once the measured step period is at least this long (GPU-bound steps; launch-bound ones lose to the extra host work)"),
+    "bigdl.step.maxInflight": (int, 2, "GPU training iterations the host may queue ahead of the device (0 = unbounded): a host far ahead of a GPU-bound step piles up cross-stream events and fresh allocations (blocks still read by the wgrad side stream cannot be recycled) and was measured to stall for seconds (profiles/r6_fp32_runahead.txt)"),
     "bigdl.step.highPriority": (bool, True, "run each GPU training iteration on a high-priority HIP stream (the critical path outranks side-stream wgrad work)"),
     "bigdl.fp32.native": (bool, True, "fp32 compute on a GPU: convolutions and Linear run the bf16x3 split on the MFMA kernels (ops/fp32x3.py; ≤2^-16 relative per product) instead of torch/MIOpen fp32"),
     "bigdl.fp32.twoPart": (bool, True, "fp32 compute: activation splits stored as [hi | lo] and read by the conv kernels as [hi | hi | lo] (ConvParams::cdup); false = the three-part [hi | hi | lo] buffers"),

@@ -218,3 +218,70 @@ def test_direct_stem_space_to_depth():
     torch.cuda.synchronize()
     ys = out[0].double().cpu()
     assert _rel(buf.reshape(2, rep, 64).sum(1)[0], ys.sum((0, 2, 3))) < 1e-5
+
+
+def test_weight_operand_cache_matches_host_forms():
+    """csrc/weight_x3.hip: every cached fp32-mode weight operand (forward chunks, flipped dgrad chunks,
+    parity sub-filters, the s2d stem filter, Linear [hi | lo | hi] rows) equals the host-side form
+    bit for bit, and goes stale exactly when the weight changes (torch in-place write, or a native
+    update reported by mark_dirty)."""
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn(64, 3, 3, 96, generator=g).to(dev)   # KRSC physical, like the arena
+    w4 = base.permute(0, 3, 1, 2)                             # logical [K][C][R][S]
+    k, c, r, s = w4.shape
+    ref_fwd = F3.chunk_split(w4.float().permute(0, 2, 3, 1).reshape(k, -1).contiguous())
+    got = F3._wprep(w4, ("fwd",))
+    torch.cuda.synchronize()
+    assert torch.equal(got.reshape(-1), ref_fwd.reshape(-1))
+    classes = [((2, 0), (2, 0)), ((1,), (2, 0)), ((2, 0), (1,)), ((1,), (1,))]
+    subs = F3._w_dgrad(w4, classes)
+    for (a, b), sub in zip(classes, subs):
+        ref = F3.chunk_split(w4[:, :, list(a)][:, :, :, list(b)].permute(1, 2, 3, 0).reshape(c, -1).contiguous())
+        assert torch.equal(sub.reshape(-1), ref.reshape(-1)), (a, b)
+    # stem: [64][3][7][7] → s2d [64][4][4][32]
+    ws = torch.randn(64, 7, 7, 3, generator=g).to(dev).permute(0, 3, 1, 2)
+    got = F3._wprep(ws, ("s2d",))
+    ref = F3.chunk_split(F3._stem_weights(ws).reshape(64, -1))
+    assert torch.equal(got.reshape(-1), ref.reshape(-1))
+    # Linear rows, plain and transposed, with padded rows / columns
+    wl = torch.randn(10, 20, generator=g).to(dev)
+    got = F3._wprep(wl, ("rows3", 12, 24, False))
+    ref = F3.split(wl, 24, F3.HLH, False, out=torch.zeros((12, 72), dtype=torch.bfloat16, device=dev))
+    assert torch.equal(got, ref)
+    got = F3._wprep(wl, ("rows3", 20, 16, True))
+    ref = F3.split(wl.t().contiguous(), 16, F3.HLH, False, out=torch.zeros((20, 48), dtype=torch.bfloat16, device=dev))
+    assert torch.equal(got, ref)
+    # staleness: a torch in-place write bumps the version counter
+    before = F3._wprep(w4, ("fwd",)).clone()
+    assert torch.equal(F3._wprep(w4, ("fwd",)), before)      # cached: same contents
+    base.mul_(2.0)
+    assert torch.equal(F3._wprep(w4, ("fwd",)).reshape(-1),
+                       F3.chunk_split(w4.permute(0, 2, 3, 1).reshape(k, -1).contiguous()).reshape(-1))
+    # a write torch does not see (the fused SGD kernel) is reported through mark_dirty
+    from bigdl.ops import native_ops as NO
+    flat = base.view(-1)
+    grad = torch.randn(flat.shape, generator=g).to(dev)
+    assert NO.sgd_step(flat, grad, None, 0.5, 0.0, 0.0, 0.0, False, True) is not NotImplemented
+    torch.cuda.synchronize()
+    assert torch.equal(F3._wprep(w4, ("fwd",)).reshape(-1),
+                       F3.chunk_split(w4.permute(0, 2, 3, 1).reshape(k, -1).contiguous()).reshape(-1))
+
+
+def test_fp32_threshold_and_colsum_kernels():
+    """fp32 ReLU / Threshold (elementwise.hip k_threshold_*_f32) and the fp32 column sum (gemm.hip
+    k_colsum_f32) against torch, including an odd tail."""
+    from bigdl.ops import native_ops as NO
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(1001, generator=g).to(dev)
+    y, names = _kernels(lambda: NO.relu_forward(x, 0.1, -0.5))
+    assert any("k_threshold_fwd_f32" in n for n in names), names
+    assert torch.equal(y, torch.where(x > 0.1, x, torch.full_like(x, -0.5)))
+    gy = torch.randn(1001, generator=g).to(dev)
+    gx = NO.relu_backward(gy, x, 0.1)
+    assert torch.equal(gx, torch.where(x > 0.1, gy, torch.zeros_like(gy)))
+    m = torch.randn(777, 1000, generator=g).to(dev)
+    out = torch.ones(1000, device=dev)
+    NO.colsum_acc(m, out, 0.5)
+    torch.cuda.synchronize()
+    assert _rel(out, 1.0 + 0.5 * m.double().sum(0)) < 1e-6

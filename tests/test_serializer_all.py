@@ -240,3 +240,50 @@ def test_coverage_of_registry():
     names = set(CLASSES)
     covered = names - set(EXEMPT)
     assert len(covered) / len(names) >= 0.9, (len(covered), len(names))
+
+
+def _edge_graph():
+    from bigdl.nn.graph import Graph
+    inp = nn.Input().set_name("in")
+    sp = nn.SplitTable(2)(inp).set_name("split")
+    a = nn.MulConstant(2.0)((sp, 1)).set_name("a")
+    b = nn.MulConstant(-3.0)((sp, 2)).set_name("b")
+    out = nn.CAddTable()(a, b).set_name("sum")
+    return Graph([inp], [out])
+
+
+def test_graph_edges_attribute_is_reference_layout():
+    """Graph.scala:672-698 writes "<node>_edges" through NameListConverter (DataConverter.scala:225-241):
+    ONE NameAttrList named after the node, attr = {previous node name: INT32 output index, -1 = whole}."""
+    g = _edge_graph()
+    mp = ms._module_to_pb(ms._SerCtx(), g)
+    ev = mp.attr["a_edges"]
+    assert ev.nameAttrListValue.name == "a"
+    assert set(ev.nameAttrListValue.attr.keys()) == {"split"}
+    assert ev.nameAttrListValue.attr["split"].int32Value == 1
+    assert mp.attr["b_edges"].nameAttrListValue.attr["split"].int32Value == 2
+    assert mp.attr["sum_edges"].nameAttrListValue.attr["a"].int32Value == -1
+    # a file in that layout loads with the selections intact
+    x = torch.randn(3, 2)
+    g2 = ms.module_from_bytes(ms.module_to_bytes(g))
+    torch.testing.assert_close(g2.forward(x), 2.0 * x[:, 0] - 3.0 * x[:, 1])
+
+
+def test_graph_edges_round5_nested_layout_still_loads():
+    """Files of the round-5 writer nested the map one level deeper ({node: {prev: idx}})."""
+    g = _edge_graph()
+    mp = ms._module_to_pb(ms._SerCtx(), g)
+    for name in ("a", "b"):
+        ev = mp.attr[f"{name}_edges"]
+        flat = {k: v.int32Value for k, v in ev.nameAttrListValue.attr.items()}
+        ev.nameAttrListValue.ClearField("attr")
+        inner = ev.nameAttrListValue.attr[name]
+        inner.dataType = ev.dataType
+        inner.nameAttrListValue.name = name
+        for k, v in flat.items():
+            av = inner.nameAttrListValue.attr[k]
+            av.dataType = mp.attr["sum_edges"].nameAttrListValue.attr["a"].dataType
+            av.int32Value = v
+    g2 = ms._module_from_pb(ms._DeCtx({}), mp)
+    x = torch.randn(3, 2)
+    torch.testing.assert_close(g2.forward(x), 2.0 * x[:, 0] - 3.0 * x[:, 1])
