@@ -33,6 +33,7 @@ from collections import OrderedDict
 from typing import Any, Callable, List, Optional, Tuple
 
 import numpy as np
+
 import torch
 
 from ..utils.engine import Engine
@@ -134,6 +135,11 @@ def to_torch(x, device=None, dtype=None):
 # ----------------------------------------------------------------------------------------------
 # flat parameter arena
 # ----------------------------------------------------------------------------------------------
+
+#: process-wide mutation epoch: bumped by every training-mode forward and every native weight write
+#: (ops.fp32x3.mark_dirty); caches of weight-derived state compare it (AbstractModule._cached_predictor)
+_MUTATION = [0]
+
 
 class FlatParameters:
     """One contiguous fp32 weight storage, one fp32 grad storage, optional bf16 shadow.
@@ -639,6 +645,8 @@ class AbstractModule:
 
     def forward(self, input):
         conv_back = None
+        if self.train:
+            _MUTATION[0] += 1  # a training forward may update buffers (BN running statistics) natively
         if not isinstance(input, (torch.Tensor, Table)):
             conv_back = type(input)
             input = to_torch(input)
@@ -734,6 +742,11 @@ class AbstractModule:
             c.clearState()
         return self
 
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d.pop("_predictor_cache", None)  # compiled forms (HIP graphs) of this module: rebuilt on demand
+        return d
+
     def cloneModule(self):
         import copy
         return copy.deepcopy(self)
@@ -819,13 +832,29 @@ class AbstractModule:
     save_caffe = saveCaffe
 
     # ---- inference helpers ----------------------------------------------------------------------------
-    def predict(self, features, batch_size: int = -1):
+    def _cached_predictor(self, batch_size: int):
+        """One LocalPredictor per (model, batch size), so repeated ``predict`` calls reuse its lowered
+        / compiled forms; refreshed when any weight or buffer may have changed since it compiled: a
+        torch in-place write (version counters), a native optimizer update / weight collective, or a
+        training-mode forward (BN running statistics) anywhere in the process (:data:`_MUTATION`)."""
         from ..optim.predictor import LocalPredictor
-        return LocalPredictor(self, batch_size=batch_size).predict(features)
+        ps = self.parameters()
+        bufs = [getattr(m, n, None) for m in self.flattened_modules() for n in getattr(m, "_buffer_names", ())]
+        sig = (_MUTATION[0], tuple(t._version for t in (list(ps[0]) if ps else []) + bufs
+                                   if isinstance(t, torch.Tensor)))
+        c = self.__dict__.get("_predictor_cache")  # dropped by __getstate__: clones / pickles never carry it
+        if c is None or c[0] != batch_size:
+            c = self.__dict__["_predictor_cache"] = [batch_size, LocalPredictor(self, batch_size=batch_size), sig]
+        elif c[2] != sig:
+            c[1].refresh()
+            c[2] = sig
+        return c[1]
+
+    def predict(self, features, batch_size: int = -1):
+        return self._cached_predictor(batch_size).predict(features)
 
     def predictClass(self, features, batch_size: int = -1):
-        from ..optim.predictor import LocalPredictor
-        return LocalPredictor(self, batch_size=batch_size).predict_class(features)
+        return self._cached_predictor(batch_size).predict_class(features)
 
     predict_class = predictClass
     predict_local = predict

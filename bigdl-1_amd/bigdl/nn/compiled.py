@@ -281,7 +281,11 @@ def select_kernels(records, iters: int = 5, min_gain: float = 0.03) -> Dict[tupl
 
 
 def _select_one(key, fn, iters, min_gain, lib, table, chosen):
-    table.pop(key, None)
+    if key in table:
+        # already pinned by an earlier compile in this process (a predictor per batch shape, a serving
+        # replica, a second optimizer): keep it instead of re-timing (clear the table to re-select)
+        chosen[key] = table[key]
+        return
     times = _time_candidates(key, fn, iters, lib)
     base = times.get(_candidates(key)[0])
     if base is None or not times:
@@ -392,7 +396,7 @@ class CompiledModule:
         self.arena_reserved = 0
         if self.plan.arena_bytes > 0:
             g0 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g0, pool=pool):
+            with torch.cuda.graph(g0, pool=pool, capture_error_mode="thread_local"):
                 slab = torch.empty(int(self.plan.arena_bytes * 1.25) + (1 << 20), dtype=torch.uint8,
                                    device=example.device)
                 slab[:1].zero_()  # (a capture with no kernel at all is reported as an empty graph)
@@ -400,7 +404,7 @@ class CompiledModule:
                 del slab
             del g0
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g, pool=pool):
+        with torch.no_grad(), torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
             self.static_out = m.forward(self.static_in)
         self.graph = g
 
@@ -443,6 +447,7 @@ def _lower(model, lower: Optional[bool]):
     if isinstance(model, IRGraph):
         return model
     was_training = model.isTraining() if hasattr(model, "isTraining") else False
+    was_fused = bool(getattr(model, "_fused", False))
     try:
         model.evaluate()
         ir = ConversionUtils.convert(model)
@@ -456,8 +461,9 @@ def _lower(model, lower: Optional[bool]):
     finally:
         if was_training:
             model.training()
-        if _model_device(model).type == "cuda":
-            from .fusion import fuse
+        if was_fused and _model_device(model).type == "cuda":
+            from .fusion import fuse, unfuse
+            unfuse(model)
             fuse(model)  # the conversion cleared the source's execution-fusion flags: restore them
     return ir
 
@@ -469,7 +475,14 @@ def compile(model, example, phase: str = "inference", graph: Optional[bool] = No
     IR (``lower``; default ``bigdl.compile.lower``): BN folding and conv+sum+ReLU epilogues, then
     kernel selection and a HIP graph of the lowered forward.  The lowered graph holds folded copies
     of the weights taken now: compile again after the weights change."""
-    return CompiledModule(model, example, phase, graph, tune=tune, lower=lower)
+    # one compilation at a time per process: kernel selection swaps the process-wide tile table's
+    # record / retiming state and graph capture must not interleave with another thread's launches
+    # (PredictionService replicas compile lazily inside concurrent request threads)
+    with _COMPILE_LOCK:
+        return CompiledModule(model, example, phase, graph, tune=tune, lower=lower)
+
+
+_COMPILE_LOCK = __import__("threading").RLock()
 
 
 __all__ = ["plan", "autotune", "compile", "CompiledModule", "Plan", "LayerRecord", "Buffer", "TILE_CANDIDATES",

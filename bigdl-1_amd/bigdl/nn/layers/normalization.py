@@ -287,7 +287,9 @@ class BatchNormalization(TensorModule):
                         relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits,
                         rezero=self._is_rep(ps[2]), zero_next=None if special else self._rep_next("fwd", ps[2]),
                         mean_out=self._shift_next(ps[4]), apply=not defer)
-                    if r is not NotImplemented:
+                    if r is not NotImplemented and not special:
+                        # (the special path finalizes without the one-launch fold: it cleared the set
+                        # it read, the other set may still hold a folded step's sums — stay on this one)
                         self._rep_flip("fwd", ps[2])
                 if r is NotImplemented:
                     if deferred_res:

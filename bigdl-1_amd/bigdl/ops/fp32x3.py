@@ -241,6 +241,8 @@ def _wx_refresh_dirty():
 def mark_dirty(t) -> None:
     """The memory of ``t`` (an fp32 weight buffer or a slice of one) was rewritten by a kernel torch
     does not see (fused optimizer update, weight all-gather): derived operands over it go stale."""
+    from ..nn import abstractnn
+    abstractnn._MUTATION[0] += 1
     if not _WP or not isinstance(t, torch.Tensor) or not t.is_cuda:
         return
     lo = t.data_ptr()

@@ -2065,32 +2065,39 @@ def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
 
 # ---------------------------------------------------------------------------------- K18 LRN
 def _lrn_ok(x, size):
-    return (x.dim() == 4 and x.dtype == _bf16 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)
-            and x.shape[1] % 8 == 0 and size % 2 == 1 and x.numel() > 0)
+    return (x.dim() == 4 and x.dtype in (_bf16, _f32) and x.is_contiguous(memory_format=torch.channels_last)
+            and _al16(x) and x.shape[1] % 8 == 0 and size % 2 == 1 and x.numel() > 0)
 
 
 @register("lrn_forward")
 def lrn_forward(x, size, alpha, beta, k):
+    """bf16 or fp32 NHWC (the fp32 kernel: the reference's precision, DL/nn/SpatialCrossMapLRN.scala:96-200)."""
+    if x.dim() == 4 and x.dtype == _f32 and not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
     if not _lrn_ok(x, size) or size > 17:
         return NotImplemented
     y = torch.empty_like(x, memory_format=torch.channels_last)
     n, c, h, w = x.shape
-    check(_lib().bigdl_lrn_fwd(ptr(x), ptr(y), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta),
-                               C.c_float(k), _s()), "lrn_fwd")
+    fn = _lib().bigdl_lrn_fwd_f32 if x.dtype == _f32 else _lib().bigdl_lrn_fwd
+    check(fn(ptr(x), ptr(y), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta), C.c_float(k), _s()),
+          "lrn_fwd")
     return y
 
 
 @register("lrn_backward")
 def lrn_backward(gy, x, size, alpha, beta, k):
+    if x.dim() == 4 and x.dtype == _f32 and not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
     if not _lrn_ok(x, size) or size > 9:
         return NotImplemented
-    gy = gy.to(_bf16).contiguous(memory_format=torch.channels_last)
+    gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
     if gy.shape != x.shape or not _al16(gy):
         return NotImplemented
     gx = torch.empty_like(x, memory_format=torch.channels_last)
     n, c, h, w = x.shape
-    check(_lib().bigdl_lrn_bwd(ptr(x), ptr(gy), ptr(gx), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta),
-                               C.c_float(k), _s()), "lrn_bwd")
+    fn = _lib().bigdl_lrn_bwd_f32 if x.dtype == _f32 else _lib().bigdl_lrn_bwd
+    check(fn(ptr(x), ptr(gy), ptr(gx), _ll(n * h * w), c, size, C.c_float(alpha), C.c_float(beta), C.c_float(k),
+             _s()), "lrn_bwd")
     return gx
 
 

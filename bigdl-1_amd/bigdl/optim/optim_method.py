@@ -507,65 +507,112 @@ class ParallelAdam(Adam):
         super().__init__(learningrate, learningrate_decay, beta1, beta2, epsilon)
 
 
-class Adamax(OptimMethod):
+class _Elementwise(OptimMethod):
+    """An update that is elementwise in (x, g, state): ``begin_iteration`` advances the per-iteration
+    scalars and sizes the state like ``x``; ``apply_update`` runs the update on ``[lo, hi)`` — so the
+    DistriOptimizer can run it on this rank's shard only, bucket by bucket (the reference runs every
+    OptimMethod on its partition ``[paramLocalStart, +paramLocalLen)``,
+    ``DL/optim/DistriOptimizer.scala:378-386``).  ``optimize`` (local) is the same two calls over
+    the whole buffer, so the sharded and local updates are one implementation."""
+
+    supports_slices = True
+
+    def _begin(self, x):  # per-iteration scalars + state tensors shaped like x
+        raise NotImplementedError
+
+    def _update(self, x, g, sl, shadow):  # x, g: the [lo, hi) slices; sl: slice object for state
+        raise NotImplementedError
+
+    def begin_iteration(self, x):
+        self._begin(x)
+        self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
+
+    def apply_update(self, x, g, lo, hi, shadow=None):
+        self._update(x[lo:hi], g[lo:hi], slice(lo, hi), shadow)
+
+    def optimize(self, feval, x):
+        fx, g = feval(x)
+        self.begin_iteration(x)
+        self._update(x, g, slice(0, x.numel()), self.shadow)
+        return x, [fx]
+
+
+def _write_shadow(shadow, x):
+    if shadow is not None:
+        if ops.cast_copy(shadow, x) is NotImplemented:
+            shadow.copy_(x)
+
+
+class Adamax(_Elementwise):
     def __init__(self, learningrate=0.002, beta1=0.9, beta2=0.999, epsilon=1e-38, bigdl_type="float"):
         super().__init__()
         self.learningRate, self.beta1, self.beta2, self.epsilon = learningrate, beta1, beta2, epsilon
 
-    def optimize(self, feval, x):
-        fx, g = feval(x)
+    def _begin(self, x):
+        self._t = self.state.get("evalCounter", 0) + 1
+        self._state_tensor("m", x)
+        self._state_tensor("u", x)
+
+    def _update(self, x, g, sl, shadow):
         g = g * self.grad_scale
-        t = self.state.get("evalCounter", 0) + 1
-        m = self._state_tensor("m", x)
-        u = self._state_tensor("u", x)
+        m, u = self.state["m"][sl], self.state["u"][sl]
         m.mul_(self.beta1).add_(g, alpha=1 - self.beta1)
         torch.maximum(u * self.beta2, g.abs() + self.epsilon, out=u)
-        x.addcdiv_(m, u, value=-self.learningRate / (1 - self.beta1 ** t))
-        self.state["evalCounter"] = t
-        _sync_shadow(self, x)
-        return x, [fx]
+        x.addcdiv_(m, u, value=-self.learningRate / (1 - self.beta1 ** self._t))
+        _write_shadow(shadow, x)
 
 
-class Adagrad(OptimMethod):
+class Adagrad(_Elementwise):
     def __init__(self, learningrate=1e-3, learningrate_decay=0.0, weightdecay=0.0, bigdl_type="float"):
         super().__init__()
         self.learningRate, self.learningRateDecay, self.weightDecay = learningrate, learningrate_decay, weightdecay
 
+    def _begin(self, x):
+        self._n = self.state.get("evalCounter", 0)
+        self._state_tensor("paramVariance", x)
+
+    def _update(self, x, g, sl, shadow):
+        n = self._n
+        s = self.state["paramVariance"][sl]
+        if x.is_cuda and ops.native_has("adagrad_step"):
+            # one fused pass (k_adagrad) over w, g, the accumulator and the bf16 shadow
+            r = ops.native_ops.adagrad_step(x, g, s, self.learningRate, self.learningRateDecay, n, self.weightDecay,
+                                            self.grad_scale, shadow)
+            if r is not NotImplemented:
+                return
+        g = g * self.grad_scale
+        if self.weightDecay != 0:
+            g = g + self.weightDecay * x
+        s.addcmul_(g, g)
+        clr = self.learningRate / (1 + n * self.learningRateDecay)
+        x.addcdiv_(g, s.sqrt().add_(1e-10), value=-clr)
+        _write_shadow(shadow, x)
+
     def optimize(self, feval, x):
+        if not getattr(self, "_graph_mode", False):
+            return super().optimize(feval, x)
         fx, g = feval(x)
         n = self.state.get("evalCounter", 0)
         s = self._state_tensor("paramVariance", x)
+        # replay-safe: the iteration counter lives on the device and the decayed rate is a tensor
+        nt = self.state.get("_dev_n")
+        if not isinstance(nt, torch.Tensor) or nt.device != x.device:
+            nt = torch.full((1,), float(n), device=x.device)
+            self.state["_dev_n"] = nt
         if x.is_cuda and ops.native_has("adagrad_step"):
-            # one fused pass (k_adagrad) over w, g, the accumulator and the bf16 shadow
-            nt = None
-            if getattr(self, "_graph_mode", False):
-                nt = self.state.get("_dev_n")
-                if not isinstance(nt, torch.Tensor) or nt.device != x.device:
-                    nt = torch.full((1,), float(n), device=x.device)
-                    self.state["_dev_n"] = nt
             r = ops.native_ops.adagrad_step(x, g, s, self.learningRate, self.learningRateDecay, n, self.weightDecay,
                                             self.grad_scale, self.shadow, dev_n=nt)
             if r is not NotImplemented:
-                if nt is not None:
-                    nt.add_(1)
+                nt.add_(1)
                 self.state["evalCounter"] = n + 1
                 return x, [fx]
         g = g * self.grad_scale
         if self.weightDecay != 0:
             g = g + self.weightDecay * x
         s.addcmul_(g, g)
-        if getattr(self, "_graph_mode", False):
-            # replay-safe: the iteration counter lives on the device and the decayed rate is a tensor
-            nt = self.state.get("_dev_n")
-            if not isinstance(nt, torch.Tensor) or nt.device != x.device:
-                nt = torch.full((1,), float(n), device=x.device)
-                self.state["_dev_n"] = nt
-            clr_t = (1 + nt * self.learningRateDecay).reciprocal_().mul_(self.learningRate)
-            x.sub_(g / s.sqrt().add_(1e-10) * clr_t)
-            nt.add_(1)
-        else:
-            clr = self.learningRate / (1 + n * self.learningRateDecay)
-            x.addcdiv_(g, s.sqrt().add_(1e-10), value=-clr)
+        clr_t = (1 + nt * self.learningRateDecay).reciprocal_().mul_(self.learningRate)
+        x.sub_(g / s.sqrt().add_(1e-10) * clr_t)
+        nt.add_(1)
         self.state["evalCounter"] = n + 1
         _sync_shadow(self, x)
         return x, [fx]
@@ -575,45 +622,45 @@ class Adagrad(OptimMethod):
         return True
 
 
-class Adadelta(OptimMethod):
+class Adadelta(_Elementwise):
     def __init__(self, decayrate=0.9, epsilon=1e-10, bigdl_type="float"):
         super().__init__()
         self.decayRate, self.epsilon = decayrate, epsilon
 
-    def optimize(self, feval, x):
-        fx, g = feval(x)
+    def _begin(self, x):
+        self._state_tensor("paramVariance", x)
+        self._state_tensor("delta", x)
+
+    def _update(self, x, g, sl, shadow):
         g = g * self.grad_scale
-        v = self._state_tensor("paramVariance", x)
-        d = self._state_tensor("delta", x)
+        v, d = self.state["paramVariance"][sl], self.state["delta"][sl]
         v.mul_(self.decayRate).addcmul_(g, g, value=1 - self.decayRate)
         upd = (d + self.epsilon).sqrt() / (v + self.epsilon).sqrt() * g
         d.mul_(self.decayRate).addcmul_(upd, upd, value=1 - self.decayRate)
         x.sub_(upd)
-        self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
-        _sync_shadow(self, x)
-        return x, [fx]
+        _write_shadow(shadow, x)
 
 
-class RMSprop(OptimMethod):
+class RMSprop(_Elementwise):
     def __init__(self, learningrate=1e-2, learningrate_decay=0.0, decayrate=0.99, epsilon=1e-8, bigdl_type="float"):
         super().__init__()
         self.learningRate, self.learningRateDecay = learningrate, learningrate_decay
         self.decayRate, self.epsilon = decayrate, epsilon
 
-    def optimize(self, feval, x):
-        fx, g = feval(x)
-        g = g * self.grad_scale
+    def _begin(self, x):
         n = self.state.get("evalCounter", 0)
-        clr = self.learningRate / (1 + n * self.learningRateDecay)
-        s = self._state_tensor("sumSquare", x)
+        self._clr = self.learningRate / (1 + n * self.learningRateDecay)
+        self._state_tensor("sumSquare", x)
+
+    def _update(self, x, g, sl, shadow):
+        g = g * self.grad_scale
+        s = self.state["sumSquare"][sl]
         s.mul_(self.decayRate).addcmul_(g, g, value=1 - self.decayRate)
-        x.addcdiv_(g, s.sqrt().add_(self.epsilon), value=-clr)
-        self.state["evalCounter"] = n + 1
-        _sync_shadow(self, x)
-        return x, [fx]
+        x.addcdiv_(g, s.sqrt().add_(self.epsilon), value=-self._clr)
+        _write_shadow(shadow, x)
 
 
-class Ftrl(OptimMethod):
+class Ftrl(_Elementwise):
     """FTRL-proximal (``Ftrl.scala:39``)."""
 
     def __init__(self, learningrate=1e-3, learningrate_power=-0.5, initial_accumulator_value=0.1,
@@ -625,14 +672,15 @@ class Ftrl(OptimMethod):
         self.l1, self.l2, self.l2Shrinkage = (l1_regularization_strength, l2_regularization_strength,
                                               l2_shrinkage_regularization_strength)
 
-    def optimize(self, feval, x):
-        fx, g = feval(x)
-        g = g * self.grad_scale
+    def _begin(self, x):
         acc = self.state.get("accum")
-        if not isinstance(acc, torch.Tensor) or acc.shape != x.shape:
-            acc = torch.full_like(x, self.initialAccumulatorValue)
-            self.state["accum"] = acc
-        lin = self._state_tensor("linear", x)
+        if not isinstance(acc, torch.Tensor) or acc.shape != x.shape or acc.device != x.device:
+            self.state["accum"] = torch.full_like(x, self.initialAccumulatorValue, dtype=torch.float32)
+        self._state_tensor("linear", x)
+
+    def _update(self, x, g, sl, shadow):
+        g = g * self.grad_scale
+        acc, lin = self.state["accum"][sl], self.state["linear"][sl]
         gs = g + 2 * self.l2Shrinkage * x if self.l2Shrinkage > 0 else g
         new_acc = acc + g * g
         p = -self.learningRatePower
@@ -642,9 +690,7 @@ class Ftrl(OptimMethod):
         l1r = torch.clamp(lin.abs() - self.l1, min=0) * torch.sign(lin)
         x.copy_(torch.where(lin.abs() > self.l1, -l1r / quad, torch.zeros_like(x)))
         acc.copy_(new_acc)
-        self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
-        _sync_shadow(self, x)
-        return x, [fx]
+        _write_shadow(shadow, x)
 
 
 class LBFGS(OptimMethod):
@@ -723,8 +769,10 @@ class LBFGS(OptimMethod):
 
 class LarsSGD(SGD):
     """Layer-wise adaptive rate scaling (``LarsSGD.scala:47``): per-layer trust ratio
-    ‖w‖ / (‖g‖ + wd·‖w‖) × trust, computed per parameter slice (X10 all-reduces the norms when
-    the slice is sharded)."""
+    ‖w‖ / (‖g‖ + wd·‖w‖) × trust, computed per parameter slice.  The ratio needs whole-layer norms, so
+    the DistriOptimizer runs it replicated (a rank's shard can split a layer)."""
+
+    supports_slices = False
 
     def __init__(self, lr_schedule=None, learningrate=1e-3, learningrate_decay=0.01, weightdecay=5e-4,
                  momentum=0.5, trust=1.0, bigdl_type="float"):

@@ -230,3 +230,82 @@ def test_vgg_cifar_fp32_step_native():
     finally:
         from bigdl.utils.engine import Engine
         Engine.set_compute_dtype("bf16")
+
+
+def test_lenet_fp32_step_native():
+    """Config 1 at the reference's precision on the GPU: odd channel counts (6 / 12 maps, a 1-channel
+    input) take the split-operand bf16x3 kernels; Tanh, max pooling, Linear, LogSoftMax / NLL native."""
+    from bigdl.models.lenet import LeNet5
+    from bigdl.nn import ClassNLLCriterion
+    from bigdl.optim import SGD
+    _fp32()
+    try:
+        x = torch.randn(16, 1, 28, 28, device=dev)
+        y = (torch.randint(0, 10, (16,)) + 1).float().to(dev)
+        with _NoTorchConv():
+            _train_steps(LeNet5(10), x, y, ClassNLLCriterion(), SGD(learningrate=0.05))
+        _assert_clean()
+    finally:
+        from bigdl.utils.engine import Engine
+        Engine.set_compute_dtype("bf16")
+
+
+def test_ptb_lstm_fp32_step_native():
+    """Config 4 at the reference's precision: fp32 embedding, the bf16x3 LSTM step kernels, fp32
+    TimeDistributed Linear + cross entropy, the fused Adagrad."""
+    from bigdl.models.rnn import PTBModel
+    from bigdl.nn import CrossEntropyCriterion, TimeDistributedCriterion
+    from bigdl.optim import Adagrad
+    _fp32()
+    try:
+        V, B, T = 10000, 20, 20
+        x = (torch.randint(0, V, (B, T)) + 1).float().to(dev)
+        y = (torch.randint(0, V, (B, T)) + 1).float().to(dev)
+        crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=False)
+        _train_steps(PTBModel.lstm(V, 200, V, 2), x, y, crit, Adagrad(learningrate=0.01, learningrate_decay=0.001))
+        _assert_clean()
+    finally:
+        from bigdl.utils.engine import Engine
+        Engine.set_compute_dtype("bf16")
+
+
+def test_inception_v1_fp32_inference_native():
+    """Config 5 at the reference's precision: the s2d stem, bf16x3 convs, native fp32 LRN
+    (SpatialCrossMapLRN.scala:96-200), pooling, concat and the classifier — no torch compute."""
+    from bigdl.models.inception import Inception_v1_NoAuxClassifier
+    from bigdl.nn.fusion import fuse
+    _fp32()
+    try:
+        model = Inception_v1_NoAuxClassifier.graph(1000, has_dropout=True)
+        model.cuda()
+        model.evaluate()
+        fuse(model)
+        x = torch.randn(4, 3, 224, 224, device=dev)
+        with _NoTorchConv(), torch.no_grad():
+            out = model.forward(x)
+        torch.cuda.synchronize()
+        assert out.shape == (4, 1000) and out.dtype == torch.float32
+        assert bool(torch.isfinite(out).all())
+        _assert_clean()
+    finally:
+        from bigdl.utils.engine import Engine
+        Engine.set_compute_dtype("bf16")
+
+
+def test_lrn_fp32_kernel_matches_fp64():
+    """fp32 LRN forward / backward (csrc/lrn.hip, float instantiation) against torch fp64."""
+    import bigdl.nn as nn
+    from bigdl.ops import native_ops as NO
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 64, 7, 9, generator=g)
+    xr = x.double().requires_grad_(True)
+    ref = torch.nn.functional.local_response_norm(xr, 5, 1e-4 * 5 / 5, 0.75, 1.0)
+    gy = torch.randn(ref.shape, generator=g)
+    ref.backward(gy.double())
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    y = NO.lrn_forward(xd, 5, 1e-4, 0.75, 1.0)
+    gi = NO.lrn_backward(gy.to(dev).contiguous(memory_format=torch.channels_last), xd, 5, 1e-4, 0.75, 1.0)
+    torch.cuda.synchronize()
+    assert y is not NotImplemented and gi is not NotImplemented
+    torch.testing.assert_close(y.double().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gi.double().cpu(), xr.grad, rtol=1e-5, atol=1e-6)

@@ -99,7 +99,7 @@ def bench_vgg(args):
     ClassNLLCriterion, SGD(lr 0.01, wd 5e-4, momentum 0.9) as ``vgg/Train.scala``; bf16 compute."""
     import torch
     from bigdl.utils import config
-    config.set_property("bigdl.compute.dtype", "bf16")
+    config.set_property("bigdl.compute.dtype", args.dtype)
     from bigdl.utils.engine import Engine
     Engine.init()
     dev = Engine.device()
@@ -129,7 +129,7 @@ def bench_vgg(args):
     el, loss = _time_steps(lambda: step(batch), dev, args.steps, args.warmup)
     return {"metric": "images/sec VggForCifar10 CIFAR-shape 1 GPU", "value": round(B * args.steps / el, 1),
             "unit": "images/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": args.dtype,
             "data": "synthetic", "config": {"model": "VggForCifar10", "global_batch": B,
                                             "hip_graph": bool(args.graph and getattr(opt, "_graphed", None)),
                                             "tuned_tiles": tiles},
@@ -143,10 +143,19 @@ def bench_ptb(args):
     N>1 ranks run the DistriOptimizer; ``value`` is whole-job tokens/sec."""
     import torch
     from bigdl.utils import config
-    config.set_property("bigdl.compute.dtype", "bf16")
+    config.set_property("bigdl.compute.dtype", args.dtype)
     from bigdl.utils.engine import Engine
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    Engine.init(dist=world > 1)
+    distri = world > 1 or args.force_distri
+    if args.force_distri and "RANK" not in os.environ:
+        # one rank outside torchrun: env:// rendezvous with itself (the DistriOptimizer path at world 1)
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+    Engine.init(dist=distri)
     dev = Engine.device()
     rank = Engine.rank()
     from bigdl.models.rnn import PTBModel
@@ -165,7 +174,7 @@ def bench_ptb(args):
     model = PTBModel.lstm(V, H, V, 2)
     crit = TimeDistributedCriterion(CrossEntropyCriterion(), size_average=False)
     ada = Adagrad(learningrate=0.01, learningrate_decay=0.001)
-    if world > 1:
+    if distri:
         from bigdl.parallel import DistriOptimizer
         opt = DistriOptimizer(model, [batch], crit, ada, batch_size=B)
     else:
@@ -192,11 +201,14 @@ def bench_ptb(args):
     el = comm.allreduce_max(time.perf_counter() - t0)
     res = {"metric": "tokens/sec PTB 2-layer LSTM LM", "value": round(B * T * world * args.steps / el, 1),
            "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": args.dtype,
            "data": "synthetic", "scaling": "weak",
            "config": {"model": "PTBModel.lstm", "vocab": V, "hidden": H, "layers": 2, "seq_len": T,
                       "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
-                      "hip_graph": bool(getattr(opt, "_graphed", None))},
+                      "hip_graph": bool(getattr(opt, "_graphed", None)),
+                      "driver": type(opt).__name__,
+                      "update_mode": ("sharded" if getattr(opt, "sharded", False) else "replicated") if distri
+                      else "local"},
            "final_loss": float(loss)}
     return res if rank == 0 else None
 
@@ -206,7 +218,7 @@ def bench_inception(args):
     written to / loaded from Caffe prototxt+caffemodel and .bigdl, then batch inference, bf16."""
     import torch
     from bigdl.utils import config
-    config.set_property("bigdl.compute.dtype", "bf16")
+    config.set_property("bigdl.compute.dtype", args.dtype)
     from bigdl.utils.engine import Engine
     Engine.init()
     dev = Engine.device()
@@ -263,7 +275,7 @@ def bench_inception(args):
     return {"metric": "images/sec Inception-v1 (Caffe-loaded) batch inference 1 GPU",
             "value": round(B * args.steps / el, 1), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "dtype": "bf16" if dev.type == "cuda" else "fp32", "data": "synthetic",
+            "dtype": args.dtype if dev.type == "cuda" else "fp32", "data": "synthetic",
             "config": {"model": "Inception-v1 (NoAux, Caffe round-trip)", "global_batch": B,
                        "executor": "compiled (autotuned tiles %s, HIP graph)" % tiles if tiles is not None else "eager",
                        "load_roundtrip_s": round(load_s, 2), "roundtrip_max_abs_diff": err}}
@@ -275,7 +287,7 @@ def bench_resnet_infer(args):
     running statistics; checked against the unfolded eval model before timing."""
     import torch
     from bigdl.utils import config
-    config.set_property("bigdl.compute.dtype", "bf16")
+    config.set_property("bigdl.compute.dtype", args.dtype)
     from bigdl.utils.engine import Engine
     Engine.init()
     dev = Engine.device()
@@ -308,7 +320,7 @@ def bench_resnet_infer(args):
     return {"metric": "images/sec ResNet-50 batch inference (IR: BN folded) 1 GPU",
             "value": round(B * args.steps / el, 1), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "dtype": "bf16" if dev.type == "cuda" else "fp32", "data": "synthetic",
+            "dtype": args.dtype if dev.type == "cuda" else "fp32", "data": "synthetic",
             "config": {"model": "ResNet-50 (IRGraph inference lowering)", "global_batch": B,
                        "fold_max_abs_diff": err}}
 
@@ -320,7 +332,7 @@ def bench_transformer(args):
     composed torch LayerNorm for an A/B of the kernel."""
     import torch
     from bigdl.utils import config
-    config.set_property("bigdl.compute.dtype", "bf16")
+    config.set_property("bigdl.compute.dtype", args.dtype)
     from bigdl.utils.engine import Engine
     Engine.init()
     dev = Engine.device()
@@ -349,7 +361,7 @@ def bench_transformer(args):
     el, loss = _time_steps(lambda: step(batch), dev, args.steps, args.warmup)
     return {"metric": "tokens/sec Transformer LM 6x512 1 GPU", "value": round(B * L * args.steps / el, 1),
             "unit": "tokens/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": args.dtype,
             "data": "synthetic", "config": {"model": "Transformer-LM", "layers": 6, "hidden": H, "heads": 8,
                                             "filter": 2048, "vocab": V, "seq_len": L, "global_batch": B,
                                             "native_layernorm": not args.no_native_ln,
@@ -497,6 +509,9 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the training step into a HIP graph (vgg, ptb, transformer)")
     ap.add_argument("--cprofile", type=int, default=0, help="cProfile this many extra steps (host hot spots, stderr)")
     ap.add_argument("--no-native-ln", action="store_true", help="transformer: composed torch LayerNorm")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype of the GPU configs (fp32 = the reference's precision, bf16x3 kernels)")
+    ap.add_argument("--force-distri", action="store_true", help="ptb: the DistriOptimizer even at world 1")
     args = ap.parse_args()
     _CPROFILE["n"] = args.cprofile
     names = list(CONFIGS) if args.config == "all" else [args.config]
