@@ -147,7 +147,11 @@ class SpatialConvolution(_QuantizedBase):
                                m.padH, m.nGroup, getattr(m, "dilationW", 1), getattr(m, "dilationH", 1), m.withBias)
         w = m.weight  # (g, out/g, in/g, kh, kw)
         q._quantize_weight(w.reshape(m.nOutputPlane, -1))
-        if m.withBias:
+        fb = m.__dict__.get("_folded_bias")  # a BatchNorm folded in by the quantizer
+        if fb is not None:
+            q.withBias = True
+            q.qbias = fb.detach().float().clone().cpu()
+        elif m.withBias:
             q.qbias = m.bias.detach().float().clone().cpu()
         q.format = getattr(m, "format", "NCHW")
         q.static_scale = calibrated_scale(m)
@@ -227,6 +231,32 @@ class SpatialConvolution(_QuantizedBase):
         if y is NotImplemented or self._out_qscale is None:
             return y
         return NO.quant_static(y, self._out_qscale, u8=self._out_u8)
+
+    def forward_residual(self, x, res, out_scale=None, out_u8=False):
+        """ReLU(conv(x) + res) with the sum and the ReLU in the int8 kernel's epilogue (a residual block
+        tail), written as int8 for the next quantised layer when ``out_scale`` is given, else bf16;
+        NotImplemented when the calibrated int8 kernel does not apply (the caller sums in torch)."""
+        import torch
+        from ...ops import native_ops as NO
+        if getattr(self, "format", "NCHW") == "NHWC" or x.dim() != 4 or not x.is_cuda:
+            return NotImplemented
+        pt, pb, pl, pr = self._pads(x)
+        C = x.shape[1]
+        if not (self.nGroup == 1 and self.nOutputPlane % 16 == 0 and pt == pb and pl == pr and ops.native_has("gemm_i8")
+                and NO.conv_i8_supported(C, self.kernelH, self.kernelW)):
+            return NotImplemented
+        if x.dtype != torch.int8 and self.static_scale is None:
+            return NotImplemented
+        if res.dtype != torch.int8 or getattr(res, "_qscale", None) is None:
+            res = res.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        prep = self._i8_prep(x, C)
+        xin = x if x.dtype == torch.int8 else x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane, self.kernelH,
+                                           self.kernelW, (self.strideH, self.strideW), (pt, pl),
+                                           (self.dilationH, self.dilationW), self._out_hw(x, (pt, pb, pl, pr)),
+                                           relu=True, in_scale=self.static_scale, out_scale=out_scale,
+                                           out_u8=bool(out_u8 and out_scale is not None),
+                                           u8_bias=self._u8_bias(x, prep, C), residual=res)
 
     def _pads(self, x):
         from ..layers.conv import same_padding

@@ -94,14 +94,248 @@ def _link_int8_chains(model):
                     a._out_qscale = b.static_scale * 127.0 / 255.0
 
 
+def _fold_bn(model):
+    """Fold every evaluation-mode BatchNormalization that directly follows a convolution inside a
+    Sequential into that convolution's weights and bias (the reference's int8 pipeline fuses conv + BN
+    before quantising, DL/nn/mkldnn/Fusion.scala:79-118): w' = w·γ/√(σ²+ε), b' = (b − μ)·γ/√(σ²+ε) + β.
+    The BN becomes an Identity.  Calibrated input scales are unaffected (a conv's input does not change)."""
+    import torch
+    from ..containers import Sequential
+    from ..layers.normalization import BatchNormalization
+    from ..layers.shape import Identity
+    for s in model.flattened_modules():
+        if not isinstance(s, Sequential):
+            continue
+        mods = s.modules
+        for i in range(len(mods) - 1):
+            a, b = mods[i], mods[i + 1]
+            if type(a) not in _REGISTRY or type(a) is L.Linear or not isinstance(b, BatchNormalization):
+                continue
+            if b.runningMean is None or b.runningVar is None or b.runningMean.numel() != a.nOutputPlane:
+                continue
+            with torch.no_grad():
+                inv = (b.runningVar.float() + b.eps).rsqrt()
+                g = b.weight.detach().float().reshape(-1) * inv if getattr(b, "affine", True) and b.weight is not None \
+                    else inv
+                beta = b.bias.detach().float().reshape(-1) if getattr(b, "affine", True) and b.bias is not None \
+                    else torch.zeros_like(inv)
+                w = a.weight
+                shape = [1] * w.dim()
+                if w.dim() == 5:  # (groups, out/groups, in/groups, kh, kw)
+                    gs = g.reshape(w.shape[0], w.shape[1], 1, 1, 1)
+                else:
+                    shape[0] = -1
+                    gs = g.reshape(shape)
+                w.mul_(gs.to(w.dtype))
+                b0 = a.bias.detach().float().reshape(-1) if (a.withBias and a.bias is not None) \
+                    else torch.zeros_like(inv)
+                a._folded_bias = ((b0 - b.runningMean.float()) * g + beta).clone()
+            mods[i + 1] = Identity().set_name(b.get_name())
+    return model
+
+
+from ..containers import Container as _Container  # noqa: E402
+
+
+class Int8ResidualBlock(_Container):
+    """A residual block ``ReLU(branch(x) + shortcut(x))`` of a quantised model whose branch ends in a
+    calibrated int8 convolution: the shortcut runs first, then the branch, and its last convolution sums
+    the shortcut in its epilogue before the ReLU and requantises for the next block (conv + sum,
+    DL/nn/mkldnn/Fusion.scala:120-165) — the sum and the ReLU never exist as separate passes.  An
+    identity shortcut passes the block's int8 input itself (read with its scale); a projection shortcut
+    writes bf16.  ``_out_qscale`` / ``_out_u8`` (set by the linker) make the block's output int8 for the
+    next quantised layer."""
+    SCALA_PACKAGE = "com.intel.analytics.bigdl.nn.quantized"
+    _out_qscale = None
+    _out_u8 = False
+
+    def __init__(self, branch=None, shortcut=None, name=None):
+        super().__init__()
+        self.modules = [branch, shortcut]
+        if name:
+            self.set_name(name)
+
+    @property
+    def branch(self):
+        return self.modules[0]
+
+    @property
+    def shortcut(self):
+        return self.modules[1]
+
+    @property
+    def tail(self):
+        return [m for m in self.branch.modules if not isinstance(m, L.Identity)][-1]
+
+    def head(self):
+        return _first_conv(self.branch)
+
+    def updateOutput(self, input):
+        import torch
+        res = self.shortcut.forward(input)
+        h = input
+        tail = self.tail
+        for m in self.branch.modules:
+            if m is tail:
+                break
+            h = m.forward(h)
+        y = tail.forward_residual(h, res, self._out_qscale, self._out_u8)
+        if y is NotImplemented:  # dynamic-scale tail: sum + ReLU on the dequantised tensors
+            yt = tail.forward(h)
+            yt = Q.dequant(yt) if yt.dtype == torch.int8 else yt
+            r = Q.dequant(res) if res.dtype == torch.int8 else res
+            y = torch.relu(yt.float() + r.float()).to(yt.dtype)
+            if self._out_qscale is not None and y.is_cuda:
+                from ...ops import native_ops as NO
+                yq = NO.quant_static(y.contiguous(memory_format=torch.channels_last), self._out_qscale,
+                                     u8=self._out_u8)
+                if yq is not NotImplemented:
+                    y = yq
+        return y
+
+    def updateGradInput(self, input, gradOutput):
+        raise NotImplementedError("Doesn't updateGradInput for quantized model (Int8ResidualBlock)")
+
+    def parameters(self):
+        return None
+
+    def __repr__(self):
+        return f"quantized.Int8ResidualBlock[{self.get_name()}]"
+
+
+def _first_conv(seq):
+    for m in getattr(seq, "modules", []):
+        if isinstance(m, Q.SpatialConvolution):
+            return m
+        if isinstance(m, L.Identity):
+            continue
+        return None
+    return None
+
+
+def _fuse_residual_blocks(model):
+    """Sequential [ConcatTable(branch, shortcut), CAddTable, ReLU] whose branch ends in a quantised conv
+    → :class:`Int8ResidualBlock`."""
+    from ..containers import Sequential, ConcatTable
+    from ..layers.table_ops import CAddTable
+    from ..layers.activation import Threshold
+    for s in model.flattened_modules():
+        if not isinstance(s, Sequential):
+            continue
+        mods = s.modules
+        if not (len(mods) == 3 and isinstance(mods[0], ConcatTable) and isinstance(mods[1], CAddTable)
+                and isinstance(mods[2], Threshold) and mods[2].threshold == 0.0 and mods[2].value == 0.0
+                and len(mods[0].modules) == 2):
+            continue
+        branch, short = mods[0].modules
+        if not isinstance(branch, Sequential):
+            continue
+        eff = [m for m in branch.modules if not isinstance(m, L.Identity)]
+        if not eff or not isinstance(eff[-1], Q.SpatialConvolution) or eff[-1].nGroup != 1:
+            continue
+        s.modules = [Int8ResidualBlock(branch, short, name=s.get_name() + "_int8")]
+    return model
+
+
+def _exec_units(seq):
+    """The modules of a Sequential in execution order, nested Sequentials flattened (a residual block
+    and any other container stay one unit)."""
+    from ..containers import Sequential
+    out = []
+    for m in seq.modules:
+        if isinstance(m, Sequential):
+            out += _exec_units(m)
+        else:
+            out.append(m)
+    return out
+
+
+def _link_units(units):
+    """Producer → consumer links over one execution sequence: a quantised conv (or a residual block)
+    followed — through ReLU / max pooling / eval dropout / Identity only — by a quantised conv with a
+    static scale or by a residual block whose branch starts with one writes that consumer's int8 input
+    (the ReLU fused into its epilogue, the unsigned code after a ReLU)."""
+    from ..layers.activation import Threshold
+    from ..layers.pooling import SpatialMaxPooling
+    from ..layers.dropout import Dropout
+    from ...ops import native_ops as NO
+    from ...utils import config
+    u8 = bool(config.get_property("bigdl.int8.unsignedActivations"))
+    for i, a in enumerate(units):
+        is_block = isinstance(a, Int8ResidualBlock)
+        if not (is_block or (isinstance(a, Q.SpatialConvolution) and a.nGroup == 1 and a.nOutputPlane % 16 == 0)):
+            continue
+        j, relu = i + 1, None
+        while j < len(units) and isinstance(units[j], (Threshold, SpatialMaxPooling, Dropout, L.Identity)):
+            m = units[j]
+            if isinstance(m, Threshold):
+                if not (m.threshold == 0.0 and m.value == 0.0):
+                    break
+                if relu is None and all(isinstance(units[k], L.Identity) for k in range(i + 1, j)):
+                    relu = m
+            j += 1
+        if j >= len(units):
+            continue
+        b = units[j]
+        head = b.head() if isinstance(b, Int8ResidualBlock) else b
+        if not isinstance(head, Q.SpatialConvolution):
+            continue
+        if head.static_scale is None or head.nGroup != 1 or not NO.conv_i8_supported(
+                a.tail.nOutputPlane if is_block else a.nOutputPlane, head.kernelH, head.kernelW):
+            continue
+        if any(isinstance(m, Threshold) and not (m.threshold == 0.0 and m.value == 0.0) for m in units[i + 1:j]):
+            continue
+        if isinstance(b, Int8ResidualBlock):
+            sc = b.shortcut
+            # the shortcut reads the same tensor: an identity or a quantised conv (any scale tag)
+            if not (isinstance(sc, L.Identity) or isinstance(_first_conv(sc) if hasattr(sc, "modules") else sc,
+                                                              Q.SpatialConvolution)):
+                continue
+        a._out_qscale = head.static_scale
+        if is_block:
+            if u8:  # the block output is ReLU(…) ≥ 0
+                a._out_u8 = True
+                a._out_qscale = head.static_scale * 127.0 / 255.0
+            continue
+        if relu is not None:
+            a._relu_fused = True
+            relu._i8_fused = True
+            if u8:
+                a._out_u8 = True
+                a._out_qscale = head.static_scale * 127.0 / 255.0
+
+
+def _link_all(model):
+    from ..containers import Sequential
+    seqs = [s for s in model.flattened_modules() if isinstance(s, Sequential)]
+    if isinstance(model, Sequential):
+        _link_units(_exec_units(model))
+    for s in seqs:
+        _link_units(list(s.modules))
+    for blk in [m for m in model.flattened_modules() if isinstance(m, Int8ResidualBlock)]:
+        _link_units(_exec_units(blk.branch))
+        if hasattr(blk.shortcut, "modules"):
+            _link_units(_exec_units(blk.shortcut))
+
+
 def quantize(model):
-    """Deep-copy ``model`` and return its int8 version (evaluation mode).  Layers calibrated with
-    ``calcScales`` quantise their input statically and chain int8 activations between quantised
-    convs (:func:`_link_int8_chains`); uncalibrated ones use per-image dynamic scales."""
+    """Deep-copy ``model`` and return its int8 version (evaluation mode).  Evaluation BatchNorms after a
+    convolution are folded into it first; layers calibrated with ``calcScales`` quantise their input
+    statically and chain int8 activations between quantised convs (:func:`_link_int8_chains`), through
+    residual blocks (conv + sum epilogues, :class:`Int8ResidualBlock`); uncalibrated ones use per-image
+    dynamic scales."""
     from ..fusion import unfuse
+    from ...utils import config
     clone = model.cloneModule()
     unfuse(clone)
+    clone.evaluate()
+    if config.get_property("bigdl.int8.foldBN"):
+        _fold_bn(clone)
     q = _convert(clone)
-    _link_int8_chains(q)
+    if config.get_property("bigdl.int8.residual"):
+        _fuse_residual_blocks(q)
+        _link_all(q)
+    else:
+        _link_int8_chains(q)
     q.evaluate()
     return q

@@ -1314,7 +1314,6 @@ __global__ void __launch_bounds__(256) k_bn32_reduce(const float* __restrict__ x
 // left each thread with a single 32-B request in flight and the pass latency-bound (11.4 ms of the
 // fp32 ResNet-50 step at ≈3.6 TB/s, profiles/r5_fp32_profile.txt).  x / aux are read once per pass:
 // non-temporal loads keep them from displacing reusable lines.
-constexpr int kU32 = 4;
 __device__ __forceinline__ void ld8f_nt(const float* __restrict__ p, float (&v)[8]) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
@@ -1322,7 +1321,7 @@ __device__ __forceinline__ void ld8f_nt(const float* __restrict__ p, float (&v)[
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
-template <bool BWD, bool RELU>
+template <bool BWD, bool RELU, int kU32 = 4>
 __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x, const float* __restrict__ aux,
                                                     const float* __restrict__ y_mask, float* __restrict__ out,
                                                     float* __restrict__ gres, long long M, int C,
@@ -1409,6 +1408,40 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
   }
 }
 
+// A/B knobs of the fp32 apply pass: BIGDL_BN32_UNROLL (rows in flight per thread: 1, 2, 4 = default,
+// 8) and BIGDL_BN32_BLOCKS (grid cap, default the bf16 pass's apply_cap)
+static int bn32_unroll() {
+  static int u = [] {
+    const char* e = getenv("BIGDL_BN32_UNROLL");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 8) ? v : 4;
+  }();
+  return u;
+}
+static int bn32_grid(long long M, int C) {
+  static int cap = [] {
+    const char* e = getenv("BIGDL_BN32_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  if (cap < 64) return apply_grid(M, C);
+  int CG = C / 8, tpr = CG < 256 ? CG : 256, rpi = 256 / tpr;
+  long long blocks = (M + rpi - 1) / rpi;
+  if (blocks > cap) blocks = cap;
+  return (int)(blocks < 1 ? 1 : blocks);
+}
+template <bool BWD, bool RELU>
+static void launch_bn32_apply(long long M, int C, hipStream_t s, const float* x, const float* aux, const float* y_mask,
+                              float* out, float* gres, const float* coef, bf16_t* sp = nullptr,
+                              uint8_t* mbits = nullptr) {
+  const dim3 g(bn32_grid(M, C)), b(256);
+  switch (bn32_unroll()) {
+    case 1: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 1>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+    case 2: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 2>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+    case 8: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 8>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+    default: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 4>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+  }
+}
+
 static bool bn32_ok(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y, long long M, int C,
@@ -1426,13 +1459,10 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train(const float* x, const float* res, float* y
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, x,
                      (const float*)ws, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                      save_invstd, coef, coef + C);
-  const int grid = apply_grid(M, C);
   if (relu)
-    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
-                       sp, (uint8_t*)bits);
+    launch_bn32_apply<false, true>(M, C, s, x, res, nullptr, y, nullptr, coef, sp, (uint8_t*)bits);
   else
-    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
-                       sp);
+    launch_bn32_apply<false, false>(M, C, s, x, res, nullptr, y, nullptr, coef, sp);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -1451,14 +1481,11 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train_partials(const float* x, const float* res,
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                      (const float*)partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                      save_invstd, coef, coef + C, nullptr, partial);
-  const int grid = apply_grid(M, C);
   bf16_t* sp = (bf16_t*)split;
   if (relu)
-    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
-                       sp, (uint8_t*)bits);
+    launch_bn32_apply<false, true>(M, C, s, x, res, nullptr, y, nullptr, coef, sp, (uint8_t*)bits);
   else
-    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, res, nullptr, y, nullptr, M, C, coef,
-                       sp);
+    launch_bn32_apply<false, false>(M, C, s, x, res, nullptr, y, nullptr, coef, sp);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -1475,9 +1502,7 @@ BIGDL_EXPORT int bigdl_bn32_bwd_partials(const float* gm, const float* x, float*
   hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)partial, G, M,
                      C, gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef, nullptr, partial);
   if (gx) {
-    const int grid = apply_grid(M, C);
-    hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gm, nullptr, gx, nullptr, M, C, coef,
-                       (bf16_t*)split);
+    launch_bn32_apply<true, false>(M, C, s, x, gm, nullptr, gx, nullptr, coef, (bf16_t*)split);
   }
   BIGDL_CHECK_LAUNCH();
 }
@@ -1488,12 +1513,10 @@ BIGDL_EXPORT int bigdl_bn32_fwd_infer(const float* x, float* y, long long M, int
   if (C % 8 || M <= 0 || !bn32_ok(x) || !bn32_ok(y)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_infer_coef, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, run_mean, run_var,
                      in_bias, eps, coef, coef + C);
-  const int grid = apply_grid(M, C);
   if (relu)
-    hipLaunchKernelGGL((k_bn32_apply<false, true>), dim3(grid), dim3(256), 0, s, x, nullptr, nullptr, y, nullptr, M, C, coef);
+    launch_bn32_apply<false, true>(M, C, s, x, nullptr, nullptr, y, nullptr, coef);
   else
-    hipLaunchKernelGGL((k_bn32_apply<false, false>), dim3(grid), dim3(256), 0, s, x, nullptr, nullptr, y, nullptr, M, C,
-                       coef);
+    launch_bn32_apply<false, false>(M, C, s, x, nullptr, nullptr, y, nullptr, coef);
   BIGDL_CHECK_LAUNCH();
 }
 
@@ -1518,12 +1541,10 @@ BIGDL_EXPORT int bigdl_bn32_bwd(const float* gy, const float* x, const float* y,
   hipLaunchKernelGGL(k_bn_bwd_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const float*)ws, G, M, C,
                      gamma, mean, invstd, ggamma, gbeta, gscale, cbias, cbscale, coef);
   if (gx || gres) {
-    const int grid = apply_grid(M, C);
     if (relu)
-      hipLaunchKernelGGL((k_bn32_apply<true, true>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp,
-                         mb);
+      launch_bn32_apply<true, true>(M, C, s, x, gy, y, gx, gres, coef, sp, mb);
     else
-      hipLaunchKernelGGL((k_bn32_apply<true, false>), dim3(grid), dim3(256), 0, s, x, gy, y, gx, gres, M, C, coef, sp);
+      launch_bn32_apply<true, false>(M, C, s, x, gy, y, gx, gres, coef, sp);
   }
   BIGDL_CHECK_LAUNCH();
 }

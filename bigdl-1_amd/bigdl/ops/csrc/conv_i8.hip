@@ -56,7 +56,27 @@ struct ConvI8Params {
   // 16-byte tail of 0x80 right after its last byte and the loader points padded taps at it.
   // y_u8: write the (ReLU'd) output that way, tail included.
   int x_u8, y_u8;
+  // residual summed before the ReLU (conv + sum, DL/nn/mkldnn/Fusion.scala:120-165): [M][ldr] int8 (the
+  // block input's code: (q + res_zero) · res_scale) or bf16; res_kind 0 = none, 1 = int8, 2 = bf16
+  const void* res;
+  int res_kind, ldr;
+  float res_scale, res_zero;
 };
+
+// the residual of output pixel m, channels n .. n + 3 (m < M, n + 3 < K)
+__device__ __forceinline__ void i8_res4(const ConvI8Params& p, int m, int n, float (&r)[4]) {
+  if (p.res_kind == 1) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>((const int8_t*)p.res + (size_t)m * p.ldr + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = ((float)(int8_t)((u >> (8 * e)) & 0xFFu) + p.res_zero) * p.res_scale;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)p.res + (size_t)m * p.ldr + n);
+    r[0] = __uint_as_float(u.x << 16);
+    r[1] = __uint_as_float(u.x & 0xFFFF0000u);
+    r[2] = __uint_as_float(u.y << 16);
+    r[3] = __uint_as_float(u.y & 0xFFFF0000u);
+  }
+}
 
 template <int BM, int BN, int WM, int WN, int TPT>
 __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
@@ -274,10 +294,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
 #pragma unroll
         for (int j = 0; j < TMI; ++j) {
           const int ml = (b_row0 - BN) + 32 * j + pm;
+          float r4[4] = {0.f, 0.f, 0.f, 0.f};
+          if (p.res_kind && m0 + ml < p.M && n0 + nl < p.K) i8_res4(p, m0 + ml, n0 + nl, r4);
           uint32_t packed = 0;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]) + r4[e];
             if (p.relu) v = fmaxf(v, 0.f);
             const float r = fminf(fmaxf(rintf(v * p.out_inv), qlo), qhi) - qoff;
             packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
@@ -319,10 +341,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
 #pragma unroll
       for (int j = 0; j < TMI; ++j) {
         const int ml = (b_row0 - BN) + 32 * j + pm;
-        float v[4];
+        float v[4], r4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.res_kind && m0 + ml < p.M && n0 + nl < p.K) i8_res4(p, m0 + ml, n0 + nl, r4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]);
+          v[e] = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]) + r4[e];
           if (p.relu) v[e] = fmaxf(v[e], 0.f);
         }
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -558,13 +581,32 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const
                             pw, dh, dw, relu, 0, 0, s);
 }
 
+BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, int x_u8, int y_u8, const void* res, int res_kind,
+                                    int ldr, float res_scale, float res_zero, hipStream_t s);
+
 BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
                                     int dh, int dw, int relu, int x_u8, int y_u8, hipStream_t s) {
+  return bigdl_conv_i8_fwd4(x, w, ldw, sx, sxs, swt, bias, y, yq, out_scale, ldy, Nb, H, W, C, K, R, S, P, Q, sh, sw,
+                            ph, pw, dh, dw, relu, x_u8, y_u8, nullptr, 0, 0, 1.f, 0.f, s);
+}
+
+// res (res_kind 1: int8 [M][ldr], value (q + res_zero)·res_scale; 2: bf16 [M][ldr]): added to the
+// dequantised output before the ReLU (ldr % 4 == 0, 8-B aligned rows for bf16)
+BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
+                                    const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
+                                    int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                    int dh, int dw, int relu, int x_u8, int y_u8, const void* res, int res_kind,
+                                    int ldr, float res_scale, float res_zero, hipStream_t s) {
   // x_u8: x holds 16 bytes of 0x80 after its last byte (and the bias carries the offset term);
   // y_u8: yq is dense (ldy == K) with room for that tail
   if (y_u8 && (!yq || ldy != K)) return (int)hipErrorInvalidValue;
+  if (res_kind < 0 || res_kind > 2 || (res_kind && (!res || ldr < K || ldr % 4 || ((uintptr_t)res & 7))))
+    return (int)hipErrorInvalidValue;
   if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)
     return (int)hipErrorInvalidValue;
   if (yq && (K % 16 || ldy % 16 || ((uintptr_t)yq & 15) || !(out_scale > 0.f))) return (int)hipErrorInvalidValue;
@@ -583,6 +625,7 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const
   p.M = (int)Ml; p.KT = KT; p.ldw = ldw; p.ldy = ldy; p.relu = relu;
   p.sxs = sxs; p.yq = (int8_t*)yq; p.out_inv = yq ? 1.f / out_scale : 1.f;
   p.x_u8 = x_u8; p.y_u8 = y_u8;
+  p.res = res; p.res_kind = res_kind; p.ldr = ldr; p.res_scale = res_scale; p.res_zero = res_zero;
   // 256 × 128 tiles; K ≤ 64 (VGG's 64-channel 224² convs, a quarter of the int8 net's time) takes a
   // 256 × 64 tile instead of leaving half of every 128-wide tile's MFMA work and staging idle
   constexpr int BM = 256;

@@ -1895,13 +1895,15 @@ def conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias):
 
 
 def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation, out_hw, relu=False,
-                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_bias=None):
+                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_bias=None, residual=None):
     """int8 conv with calibrated scales: ``x`` int8 NHWC (tagged ``_qscale``, the producer's
     requantised output) or fp32/bf16 quantised here with ``in_scale`` in one static pass; with
     ``out_scale`` the epilogue writes the int8 NHWC input of the next quantised layer (bias, ReLU
     and requantisation fused), else bf16.  ``in_u8`` (fp32/bf16 input known non-negative) / an int8
     input tagged ``_qzero``: offset −128 u8 input (its bias ``u8_bias``, :func:`conv_i8_u8_bias`);
-    ``out_u8``: write the (ReLU'd) output that way.  NotImplemented when the kernel does not apply."""
+    ``out_u8``: write the (ReLU'd) output that way.  ``residual`` (NHWC [N][K][P][Q], int8 tagged
+    ``_qscale`` / ``_qzero`` or bf16): summed before the ReLU in the epilogue — the conv + sum of a
+    residual block tail.  NotImplemented when the kernel does not apply."""
     if not (x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)):
         return NotImplemented
     N_, C_, H, W = x.shape
@@ -1929,15 +1931,27 @@ def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, di
         y = _i8_act(N_, K, P, Q, x.device, out_u8)
     else:
         y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
+    rkind, rscale, rzero = 0, 1.0, 0.0
+    if residual is not None:
+        if (residual.dim() != 4 or tuple(residual.shape) != (N_, K, P, Q) or not residual.is_cuda
+                or not residual.is_contiguous(memory_format=torch.channels_last) or residual.data_ptr() % 8):
+            return NotImplemented
+        if residual.dtype == torch.int8 and getattr(residual, "_qscale", None) is not None:
+            rkind, rscale, rzero = 1, float(residual._qscale), float(getattr(residual, "_qzero", 0))
+        elif residual.dtype == _bf16:
+            rkind = 2
+        else:
+            return NotImplemented
     b = bias.float().contiguous() if bias is not None else None
     if x_u8:
         b = u8_bias if u8_bias is not None else conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias)
-    check(_lib().bigdl_conv_i8_fwd3(ptr(xq), ptr(wq), C.c_int(ldw), None, C.c_float(sx), ptr(w_scale), ptr(b),
+    check(_lib().bigdl_conv_i8_fwd4(ptr(xq), ptr(wq), C.c_int(ldw), None, C.c_float(sx), ptr(w_scale), ptr(b),
                                     None if out_scale is not None else ptr(y), ptr(y) if out_scale is not None else None,
                                     C.c_float(out_scale if out_scale is not None else 1.0), C.c_int(K), N_, H, W, C_, K,
                                     R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
                                     C.c_int(1 if relu else 0), C.c_int(int(x_u8)),
-                                    C.c_int(int(out_u8)), _s()), "conv_i8_fwd3")
+                                    C.c_int(int(out_u8)), ptr(residual), C.c_int(rkind), C.c_int(K), C.c_float(rscale),
+                                    C.c_float(rzero), _s()), "conv_i8_fwd4")
     if out_scale is not None:
         _tag(y, out_scale, out_u8)
     return y

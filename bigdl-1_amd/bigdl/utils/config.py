@@ -79,6 +79,8 @@ _REGISTRY = {
     # fusion flags (bigdl.mkldnn.fusion.* equivalents, nn/mkldnn/Fusion.scala:34)
     "bigdl.int8.calibration": (str, "p99.999", "static int8 activation scale rule of quantize() after calcScales: max (max|x|, the reference's) or p99.9 / p99.99 / p99.999 (that percentile of |x|)"),
     "bigdl.int8.unsignedActivations": (bool, True, "a quantised conv whose ReLU is fused writes its non-negative int8 output as unsigned 8-bit (offset -128, scale clip/255); the consumer corrects the offset with per-tap weight sums"),
+    "bigdl.int8.foldBN": (bool, True, "quantize() folds evaluation BatchNorms into the preceding convolution before quantising its weights (the reference's int8 conv + BN fusion)"),
+    "bigdl.int8.residual": (bool, True, "quantize() turns ConcatTable(branch, shortcut) + CAddTable + ReLU blocks into int8 residual blocks (conv + sum epilogue, int8 block outputs chained to the next block)"),
     "bigdl.int8.quantizeLinear": (bool, True, "quantize() converts Linear layers too (int8 GEMM, per-row dynamic input scales); False keeps them in the compute dtype"),
     "bigdl.fusion": (bool, True, "enable layer fusion"),
     "bigdl.fusion.convbn": (bool, True, "fold BN into conv for inference"),

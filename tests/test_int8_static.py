@@ -176,3 +176,115 @@ def test_stem_conv_int8_epilogue_matches_two_pass(u8):
         if u8:
             tail = torch.empty(0, dtype=torch.int8, device="cuda").set_(got.untyped_storage(), got.numel(), (16,), (1,))
             assert bool((tail == -128).all())
+
+
+def _resnet50_calibrated(size=64, seed=3):
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.nn import SpatialBatchNormalization
+    from bigdl.utils.random import RNG
+    RNG.setSeed(seed)
+    torch.manual_seed(seed)
+    m = model_init(ResNet(10, depth=50, dataset=DatasetType.ImageNet, image_size=size))
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for bn in m.flattened_modules():
+            if isinstance(bn, SpatialBatchNormalization):
+                bn.weight.uniform_(0.2, 1.0, generator=g)
+                bn.bias.normal_(0.0, 0.1, generator=g)
+        m.training()
+        for _ in range(2):
+            m.forward(torch.randn(4, 3, size, size, generator=g))
+    m.evaluate()
+    xc = torch.randn(4, 3, size, size, generator=g)
+    with torch.no_grad():
+        m.forward(xc)
+    m.calcScales(xc)
+    return m, g
+
+
+def test_resnet50_int8_residual_blocks_link():
+    """quantize() on a calibrated ResNet-50: BN folded into the convs (Fusion.scala conv + BN), every
+    bottleneck becomes an int8 residual block whose last conv sums the shortcut in its epilogue, and
+    every block but the last hands its output to the next block as int8 (MKL-DNN int8 scale
+    propagation through conv + sum, DL/nn/mkldnn/Fusion.scala:120-165)."""
+    from bigdl.nn.quantized import layers as Q
+    from bigdl.nn.quantized.quantizer import Int8ResidualBlock
+    from bigdl.nn import SpatialBatchNormalization
+    m, _g = _resnet50_calibrated()
+    q = m.quantize()
+    assert not any(isinstance(b, SpatialBatchNormalization) for b in q.flattened_modules())
+    blocks = [b for b in q.flattened_modules() if isinstance(b, Int8ResidualBlock)]
+    assert len(blocks) == 16
+    assert [b._out_qscale is not None for b in blocks] == [True] * 15 + [False]
+    assert all(b._out_u8 for b in blocks[:15])
+    # the block output scale is the next block's calibrated input scale (unsigned code: clip / 255)
+    for a, b in zip(blocks, blocks[1:]):
+        assert a._out_qscale == pytest.approx(b.head().static_scale * 127 / 255)
+    # inside every branch conv1 → conv2 → conv3 are chained int8 with the ReLU fused
+    for b in blocks:
+        convs = [c for c in b.branch.modules if isinstance(c, Q.SpatialConvolution)]
+        assert [c._out_qscale is not None for c in convs] == [True, True, False]
+        assert convs[0]._relu_fused and convs[1]._relu_fused
+    # the stem conv (+ folded BN, ReLU, max pooling) writes the first block's int8 input
+    stem = [c for c in q.flattened_modules() if isinstance(c, Q.SpatialConvolution)][0]
+    assert stem._out_qscale is not None and stem._relu_fused
+    # the folded float model and the quantised one agree (CPU: dynamic int8 reference path)
+    x = torch.randn(2, 3, 64, 64)
+    with torch.no_grad():
+        ref = m.forward(x).float()
+        out = q.forward(x).float()
+    cos = float(torch.nn.functional.cosine_similarity(out.reshape(1, -1), ref.reshape(1, -1)))
+    assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+def test_int8_residual_epilogue_matches_reference():
+    """conv2d_i8_forward_static(residual=…): ReLU(conv(x) + res) with the sum in the int8 kernel's
+    epilogue equals the unfused conv (bf16 output) + the dequantised residual, for an int8 (unsigned
+    code) and a bf16 residual, with bf16 and int8 outputs."""
+    from bigdl.nn.quantized import layers as Q
+    from bigdl.ops import native_ops as NO
+    import bigdl.nn as nn
+    torch.manual_seed(1)
+    conv = nn.SpatialConvolution(128, 256, 1, 1).cuda()
+    x = torch.randn(4, 128, 14, 14, device="cuda")
+    conv.forward(x)
+    conv.calcScales(x)
+    q = Q.SpatialConvolution.from_float(conv).cuda()
+    xb = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    plain = q._native_static(xb, (0, 0, 0, 0))  # bf16, no ReLU
+    assert plain is not NotImplemented
+    r = torch.relu(torch.randn(4, 256, 14, 14, device="cuda")).contiguous(memory_format=torch.channels_last)
+    r8 = NO.quant_static(r, float(r.max()) / 255.0, u8=True)
+    for res in (r8, r.bfloat16()):
+        rf = Q.dequant(res).float() if res.dtype == torch.int8 else res.float()
+        ref = torch.relu(plain.float() + rf)
+        y = q.forward_residual(xb, res)
+        torch.cuda.synchronize()
+        assert y is not NotImplemented and y.dtype == torch.bfloat16
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+        sc = float(ref.max()) / 255.0
+        yq = q.forward_residual(xb, res, out_scale=sc, out_u8=True)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(Q.dequant(yq).float(), ref, rtol=0, atol=1.5 * sc + 2e-2 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+def test_resnet50_int8_logits_track_fp32():
+    """Calibrated int8 ResNet-50 (residual blocks, int8 block outputs) on the GPU vs the float model:
+    logit cosine ≥ 0.99 (centred log-probabilities)."""
+    from bigdl.utils.engine import Engine
+    from bigdl.utils import config
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    m, g = _resnet50_calibrated(size=64, seed=4)
+    q = m.quantize().cuda()
+    q.evaluate()
+    x = torch.randn(8, 3, 64, 64, generator=g)
+    with torch.no_grad():
+        ref = m.forward(x).double()
+        out = q.forward(x.cuda().bfloat16().contiguous(memory_format=torch.channels_last)).double().cpu()
+    ref, out = ref - ref.mean(1, keepdim=True), out - out.mean(1, keepdim=True)
+    cos = float(torch.nn.functional.cosine_similarity(out.reshape(1, -1), ref.reshape(1, -1)))
+    print("resnet50 int8 vs fp32 logit cosine", cos)
+    assert cos >= 0.99, cos

@@ -411,21 +411,42 @@ def bench_int8(args):
     from bigdl.utils.engine import Engine
     from bigdl.models.vgg import Vgg_16
     from bigdl.utils.random import RNG
-    B = args.batch or 128
+    B = args.batch or (128 if args.int8_model == "vgg16" else 256)
     res = {}
     RNG.setSeed(11)
     torch.manual_seed(11)
-    base = Vgg_16(1000, has_dropout=False)
-    base.evaluate()
     g = torch.Generator().manual_seed(3)
     x32 = torch.randn(B, 3, 224, 224, generator=g)
-    _lsuv(base, x32[:8])
+    if args.int8_model == "vgg16":
+        base = Vgg_16(1000, has_dropout=False)
+        base.evaluate()
+        _lsuv(base, x32[:8])
+    elif args.int8_model == "resnet50":
+        # residual blocks: BN folded into the convs, conv + sum epilogues, int8 block outputs
+        from bigdl.models.resnet import ResNet, DatasetType, model_init
+        base = model_init(ResNet(1000, depth=50, dataset=DatasetType.ImageNet))
+        from bigdl.nn import SpatialBatchNormalization
+        with torch.no_grad():  # trained-like BN affine parameters (model_init zeroes the block-tail γ)
+            for bn in base.flattened_modules():
+                if isinstance(bn, SpatialBatchNormalization):
+                    bn.weight.uniform_(0.2, 1.0, generator=g)
+                    bn.bias.normal_(0.0, 0.1, generator=g)
+        base.training()
+        with torch.no_grad():  # a few training forwards give the BNs real running statistics
+            for i in range(2):
+                base.forward(torch.randn(8, 3, 224, 224, generator=g))
+        base.evaluate()
+    else:
+        from bigdl.models.inception import Inception_v1_NoAuxClassifier
+        base = Inception_v1_NoAuxClassifier.graph(1000, has_dropout=False)
+        base.evaluate()
     outs = {}
-    for mode in ("fp32", "bf16", "int8"):
+    modes = ("fp32", "bf16", "int8") + (("bf16_compiled", "int8_graph") if args.int8_model != "vgg16" else ())
+    for mode in modes:
         config.set_property("bigdl.compute.dtype", "fp32" if mode == "fp32" else "bf16")
         Engine.init()
         dev = Engine.device()
-        if mode == "int8" and args.calib > 0:
+        if mode.startswith("int8") and args.calib > 0:
             # calibration (MklInt8Convertible.calcScales): a forward of CALIB images that are not the
             # timed batch records every layer's max|input|; quantize() then runs static int8 chains
             cal = base.cloneModule().to(dev)
@@ -446,7 +467,7 @@ def bench_int8(args):
             finally:
                 config.set_property("bigdl.int8.quantizeLinear", old_fc)
             del cal
-        elif mode == "int8":
+        elif mode.startswith("int8"):
             m = base.quantize()
         else:
             m = base.cloneModule()
@@ -458,6 +479,27 @@ def bench_int8(args):
         def step():
             with torch.no_grad():
                 return m.forward(x)
+        if mode == "bf16_compiled":
+            # the compiled inference path the predictors use (IR lowering: BN folded, conv+sum+ReLU
+            # epilogues; kernel selection; HIP graph) — the strongest bf16 baseline
+            from bigdl.nn.compiled import compile as compile_module
+            cm = compile_module(m, x)
+            step = lambda: cm(x)  # noqa: E731
+        elif mode == "int8_graph" and dev.type == "cuda":
+            # the int8 forward captured in one HIP graph (no per-layer host dispatch)
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st), torch.no_grad():
+                for _ in range(2):
+                    m.forward(x)
+            torch.cuda.current_stream().wait_stream(st)
+            gr = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(gr):
+                gout = m.forward(x)
+
+            def step():  # noqa: F811
+                gr.replay()
+                return gout
         el, y = _time_steps(step, dev, args.steps, args.warmup)
         outs[mode] = y.float().cpu()
         res[mode] = {"value": round(B * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3)}
@@ -475,11 +517,18 @@ def bench_int8(args):
     cos = _cos(ci, cf)
     cos_img = _cos(ci - ci.mean(0, keepdim=True), cf - cf.mean(0, keepdim=True))
     top1 = float((qi.argmax(1) == qf.argmax(1)).float().mean())
-    return {"metric": "images/sec VGG16 224x224 batch inference 1 GPU: int8 vs fp32 vs bf16",
+    extra = {}
+    if "int8_graph" in res:
+        extra = {"bf16_compiled": res["bf16_compiled"], "int8_graph": res["int8_graph"],
+                 "int8_graph_over_bf16_compiled": round(res["int8_graph"]["value"] / res["bf16_compiled"]["value"], 3),
+                 "cosine_int8_graph_vs_fp32": round(_cos(outs["int8_graph"].reshape(B, -1) - outs["int8_graph"].reshape(
+                     B, -1).mean(1, keepdim=True), cf), 5)}
+    name = {"vgg16": "VGG16", "resnet50": "ResNet-50", "inception": "Inception-v1"}[args.int8_model]
+    return {"metric": f"images/sec {name} 224x224 batch inference 1 GPU: int8 vs fp32 vs bf16",
             "value": res["int8"]["value"], "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": res["int8"]["ms_per_step"], "higher_is_better": True,
-            "dtype": "int8", "data": "synthetic", "config": {"model": "VGG16", "global_batch": B, "image_size": 224},
-            "fp32": res["fp32"], "bf16": res["bf16"],
+            "dtype": "int8", "data": "synthetic", "config": {"model": name, "global_batch": B, "image_size": 224},
+            "fp32": res["fp32"], "bf16": res["bf16"], **extra,
             "int8_over_fp32": round(res["int8"]["value"] / res["fp32"]["value"], 3),
             "int8_over_bf16": round(res["int8"]["value"] / res["bf16"]["value"], 3),
             "reference_int8_over_fp32": 2.04, "cosine_int8_vs_fp32": round(cos, 5), "calibration_images": args.calib,
@@ -512,6 +561,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype of the GPU configs (fp32 = the reference's precision, bf16x3 kernels)")
     ap.add_argument("--force-distri", action="store_true", help="ptb: the DistriOptimizer even at world 1")
+    ap.add_argument("--int8-model", default="vgg16", choices=["vgg16", "resnet50", "inception"],
+                    help="int8: the network (resnet50: BN folded + int8 residual blocks; inception: concat)")
     args = ap.parse_args()
     _CPROFILE["n"] = args.cprofile
     names = list(CONFIGS) if args.config == "all" else [args.config]

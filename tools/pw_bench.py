@@ -54,7 +54,7 @@ def run():
     bs = int(os.environ.get("BS", "256"))
     tot = {"fwd": 0.0, "fwdstats": 0.0, "dgrad": 0.0, "mm": 0.0, "copy": 0.0}
     tot["wgrad"] = 0.0
-    tot["vendor_fwd"] = 0.0
+    tot["vendor_fwd"] = tot["vendor_dgrad"] = tot["vendor_wgrad"] = 0.0
     only3 = os.environ.get("ONLY3") == "1"
     for C, K, s, H, mult, R in ([] if only3 else [v + (1,) for v in SHAPES]) + [v + (3,) for v in SHAPES3]:
         pd = R // 2
@@ -77,10 +77,17 @@ def run():
         else:
             t["mm"] = 0.0
         if os.environ.get("VENDOR_CONV") == "1":
-            # the vendor library's conv of the same shape (torch → MIOpen, NHWC bf16): forward only
-            t["vendor_fwd"] = timeit(lambda: torch.nn.functional.conv2d(x, w, None, s, pd))
+            # the vendor library's conv of the same shape (torch → MIOpen, NHWC bf16), forward / data
+            # gradient / weight gradient.  For a tuned baseline run with MIOPEN_FIND_MODE=NORMAL (the
+            # find step benchmarks every MIOpen solver on the shape) and VENDOR_BENCH=1
+            # (torch.backends.cudnn.benchmark: the fastest algorithm is chosen per shape, cached)
+            torch.backends.cudnn.benchmark = os.environ.get("VENDOR_BENCH") == "1"
+            wcl = w.contiguous(memory_format=torch.channels_last)
+            t["vendor_fwd"] = timeit(lambda: torch.nn.functional.conv2d(x, wcl, None, s, pd))
+            t["vendor_dgrad"] = timeit(lambda: torch.nn.grad.conv2d_input(x.shape, wcl, gy, s, pd))
+            t["vendor_wgrad"] = timeit(lambda: torch.nn.grad.conv2d_weight(x, w.shape, gy, s, pd))
         else:
-            t["vendor_fwd"] = 0.0
+            t["vendor_fwd"] = t["vendor_dgrad"] = t["vendor_wgrad"] = 0.0
         src = torch.empty(M * K + x.numel(), dtype=torch.bfloat16, device="cuda")
         dst = torch.empty_like(src)
         t["copy"] = timeit(lambda: dst.copy_(src)) / 2  # read+write of (in + out) ≈ 2× the conv's bytes
