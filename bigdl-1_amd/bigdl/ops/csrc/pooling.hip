@@ -224,7 +224,13 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd_k3s2(const T* __restrict__ 
 
 // Channel counts that are not a multiple of 8 (LeNet's 6 / 12 maps): one thread per element, same
 // int8 window-offset argmax and gather backward as the vector kernels above.
-__global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+__device__ __forceinline__ float pld1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float pld1(const float* p) { return *p; }
+__device__ __forceinline__ void pst1(bf16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void pst1(float* p, float v) { *p = v; }
+
+template <typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const T* __restrict__ x, T* __restrict__ y,
                                                         int8_t* __restrict__ idx, PoolGeom g, long long total) {
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(t % g.C);
@@ -242,14 +248,14 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_c1(const bf16_t* __restrict
       for (int j = 0; j < g.kw; ++j) {
         const int w = w0 + j;
         if ((unsigned)w >= (unsigned)g.W) continue;
-        const float v = bf2f(x[(((size_t)n * g.H + h) * g.W + w) * g.C + c]);
+        const float v = pld1(x + (((size_t)n * g.H + h) * g.W + w) * g.C + c);
         if (v > best || v != v) {
           best = v;
           arg = i * g.kw + j;
         }
       }
     }
-    y[t] = f2bf(best);
+    pst1(y + t, best);
     if (idx) idx[t] = (int8_t)arg;
   }
 }
@@ -314,8 +320,9 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_rows(const bf16_t* __restri
   }
 }
 
-__global__ void __launch_bounds__(256) k_maxpool_bwd_c1(const bf16_t* __restrict__ gy, const int8_t* __restrict__ idx,
-                                                        bf16_t* __restrict__ gx, PoolGeom g, long long total) {
+template <typename T = bf16_t>
+__global__ void __launch_bounds__(256) k_maxpool_bwd_c1(const T* __restrict__ gy, const int8_t* __restrict__ idx,
+                                                        T* __restrict__ gx, PoolGeom g, long long total) {
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(t % g.C);
     long long pix = t / g.C;
@@ -334,9 +341,9 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd_c1(const bf16_t* __restrict
     for (int p = p_lo; p <= p_hi; ++p)
       for (int q = q_lo; q <= q_hi; ++q) {
         const size_t o = (((size_t)n * g.P + p) * g.Q + q) * g.C + c;
-        if (idx[o] == (int8_t)((hp - p * g.sh) * g.kw + (wp - q * g.sw))) acc += bf2f(gy[o]);
+        if (idx[o] == (int8_t)((hp - p * g.sh) * g.kw + (wp - q * g.sw))) acc += pld1(gy + o);
       }
-    gx[t] = f2bf(acc);
+    pst1(gx + t, acc);
   }
 }
 
@@ -353,7 +360,7 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
   if (C % 8) {
     const long long te = (long long)N * P * Q * C;
-    hipLaunchKernelGGL(k_maxpool_fwd_c1, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+    hipLaunchKernelGGL(k_maxpool_fwd_c1<bf16_t>, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
                        (int8_t*)idx, g, te);
     BIGDL_CHECK_LAUNCH();
   }
@@ -385,7 +392,7 @@ BIGDL_EXPORT int bigdl_maxpool_bwd(const void* gy, const void* idx, void* gx, in
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
   if (C % 8) {
     const long long te = (long long)N * H * W * C;
-    hipLaunchKernelGGL(k_maxpool_bwd_c1, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)gy,
+    hipLaunchKernelGGL(k_maxpool_bwd_c1<bf16_t>, dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, (const bf16_t*)gy,
                        (const int8_t*)idx, (bf16_t*)gx, g, te);
     BIGDL_CHECK_LAUNCH();
   }
@@ -514,18 +521,28 @@ BIGDL_EXPORT int bigdl_avgpool_bwd(const void* gy, void* gx, int N, int H, int W
   BIGDL_CHECK_LAUNCH();
 }
 
-// ---- fp32 NHWC (bigdl.compute.dtype=fp32): same kernels, fp32 elements; C % 8 == 0, 16-B aligned ----
+// ---- fp32 NHWC (bigdl.compute.dtype=fp32): same kernels, fp32 elements; 16-B aligned when C % 8 == 0,
+// the per-element kernels otherwise (LeNet's 6 / 12 maps) ----
 static bool pool32_ok(const void* a, const void* b, int C) {
   return C % 8 == 0 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
 }
 
 BIGDL_EXPORT int bigdl_maxpool32_fwd(const float* x, float* y, void* idx, int N, int H, int W, int C, int P, int Q,
                                      int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
-  if (kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0 || !pool32_ok(x, y, C)) return (int)hipErrorInvalidValue;
+  if (kh * kw > 127 || N <= 0 || P <= 0 || Q <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (!pool32_ok(x, y, C)) {
+    const long long te = (long long)N * P * Q * C;
+    hipLaunchKernelGGL((k_maxpool_fwd_c1<float>), dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, x, y,
+                       (int8_t*)idx, g, te);
+    BIGDL_CHECK_LAUNCH();
+  }
   const long long total = (long long)N * P * Q * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
-  if (total < 0x7fffffffLL)
+  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
+  if (total < 0x7fffffffLL && k3s2)
+    hipLaunchKernelGGL((k_maxpool_fwd_k3s2<uint32_t, float>), dim3(grid), dim3(256), 0, s, x, y, (int8_t*)idx, g);
+  else if (total < 0x7fffffffLL)
     hipLaunchKernelGGL((k_maxpool_fwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, x, y, (int8_t*)idx, g);
   else
     hipLaunchKernelGGL((k_maxpool_fwd<long long, float>), dim3(grid), dim3(256), 0, s, x, y, (int8_t*)idx, g);
@@ -534,11 +551,20 @@ BIGDL_EXPORT int bigdl_maxpool32_fwd(const float* x, float* y, void* idx, int N,
 
 BIGDL_EXPORT int bigdl_maxpool32_bwd(const float* gy, const void* idx, float* gx, int N, int H, int W, int C, int P,
                                      int Q, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
-  if (kh * kw > 127 || N <= 0 || !idx || !pool32_ok(gy, gx, C)) return (int)hipErrorInvalidValue;
+  if (kh * kw > 127 || N <= 0 || C <= 0 || !idx) return (int)hipErrorInvalidValue;
   PoolGeom g = make_geom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (!pool32_ok(gy, gx, C)) {
+    const long long te = (long long)N * H * W * C;
+    hipLaunchKernelGGL((k_maxpool_bwd_c1<float>), dim3(bigdl_grid(te, 256, 16384)), dim3(256), 0, s, gy,
+                       (const int8_t*)idx, gx, g, te);
+    BIGDL_CHECK_LAUNCH();
+  }
   const long long total = (long long)N * H * W * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
-  if (total < 0x7fffffffLL)
+  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
+  if (total < 0x7fffffffLL && k3s2)
+    hipLaunchKernelGGL((k_maxpool_bwd_k3s2<uint32_t, float>), dim3(grid), dim3(256), 0, s, gy, (const int8_t*)idx, gx, g);
+  else if (total < 0x7fffffffLL)
     hipLaunchKernelGGL((k_maxpool_bwd<uint32_t, float>), dim3(grid), dim3(256), 0, s, gy, (const int8_t*)idx, gx, g);
   else
     hipLaunchKernelGGL((k_maxpool_bwd<long long, float>), dim3(grid), dim3(256), 0, s, gy, (const int8_t*)idx, gx, g);

@@ -2027,9 +2027,10 @@ class _Int8Idx:
 @register("maxpool2d_forward")
 def maxpool2d_forward(x, k, s, p, ceil_mode, need_indices=True):
     """``need_indices=False`` (inference) skips the int8 argmax: 1/3 less traffic.  fp32 NHWC
-    (bigdl.compute.dtype=fp32) runs the fp32 instantiation of the same kernel (C % 8 == 0)."""
-    if (x.dim() == 4 and x.dtype == _f32 and x.is_contiguous(memory_format=torch.channels_last) and _al16(x)
-            and x.shape[1] % 8 == 0 and k[0] * k[1] <= 127 and p[0] * 2 <= k[0] and p[1] * 2 <= k[1]):
+    (bigdl.compute.dtype=fp32) runs the fp32 instantiation of the same kernel (per-element kernels when
+    C % 8 != 0, e.g. LeNet's 6 / 12 maps)."""
+    if (x.dim() == 4 and x.dtype == _f32 and x.is_contiguous(memory_format=torch.channels_last)
+            and k[0] * k[1] <= 127 and p[0] * 2 <= k[0] and p[1] * 2 <= k[1]):
         N_, C_, H, W = x.shape
         P = _pool_out(H, k[0], s[0], p[0], ceil_mode)
         Q = _pool_out(W, k[1], s[1], p[1], ceil_mode)
@@ -2062,8 +2063,6 @@ def maxpool2d_backward(gy, x, idx, k, s, p, ceil_mode):
     P, Q = gy.shape[2], gy.shape[3]
     if x.dtype == _f32:
         gy = gy.float().contiguous(memory_format=torch.channels_last)
-        if C_ % 8 or not _al16(gy):
-            return NotImplemented
         gx = torch.empty((N_, C_, H, W), dtype=_f32, device=x.device, memory_format=torch.channels_last)
         check(_lib().bigdl_maxpool32_bwd(ptr(gy), ptr(idx.t), ptr(gx), N_, H, W, C_, P, Q, k[0], k[1], s[0], s[1],
                                          p[0], p[1], _s()), "maxpool32_bwd")

@@ -11,7 +11,8 @@ cl = torch.channels_last
 
 
 @pytest.mark.parametrize("N,C,H,k,s,p,ceil", [(4, 64, 112, 3, 2, 1, False), (2, 24, 13, 3, 2, 0, True),
-                                               (3, 16, 9, 2, 2, 0, False)])
+                                               (3, 16, 9, 2, 2, 0, False), (16, 6, 24, 2, 2, 0, False),
+                                               (4, 12, 8, 2, 2, 0, False), (2, 3, 11, 3, 2, 1, True)])
 def test_maxpool32_matches_torch(N, C, H, k, s, p, ceil):
     from bigdl.ops import native_ops as NO
     g = torch.Generator().manual_seed(0)
