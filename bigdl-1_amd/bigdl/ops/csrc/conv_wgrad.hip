@@ -88,7 +88,7 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false, bool PW1 = false,
           bool F32 = false>
 __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_conv_wgrad(WgradParams p) {
-  static_assert(!(F32 && (C4 || D3 || AT)), "fp32 operands: 2-D, 8-channel chunks, no BN prologue");
+  static_assert(!(F32 && (D3 || AT)), "fp32 operands: 2-D, 8-channel (or C4) chunks, no BN prologue");
   static_assert(!(PW1 && (C4 || D3)), "pointwise gather: 2-D, 8-channel chunks");
   static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
   static_assert(!(AT && (C4 || D3)), "BN-backward prologue: 2-D, 8-channel chunks");
@@ -210,11 +210,17 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
       if constexpr (C4) {
         const int h1 = (int)pp * p.sh - p.ph + rx1, w1 = (int)q * p.sw - p.pw + sx1;
         const bool ok1 = kx1_ok && m < mend && (unsigned)h1 < (unsigned)p.H && (unsigned)w1 < (unsigned)p.W;
-        const uint32_t off0 = (ok ? (uint32_t)((n * p.H + h) * p.W + w) * 8u : DEAD) | dead;
-        const uint32_t off1 = (ok1 ? (uint32_t)((n * p.H + h1) * p.W + w1) * 8u : DEAD) | dead;
-        const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off0, 0, 0));
-        const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
-        rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        // one pixel of the 4-channel input: 8 B (bf16) or 16 B (fp32, one piece per tap)
+        const uint32_t off0 = (ok ? (uint32_t)((n * p.H + h) * p.W + w) * (4u * ES) : DEAD) | dead;
+        const uint32_t off1 = (ok1 ? (uint32_t)((n * p.H + h1) * p.W + w1) * (4u * ES) : DEAD) | dead;
+        if constexpr (F32) {
+          rx_[2 * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off0, 0, 0));
+          rx_[2 * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off1, 0, 0));
+        } else {
+          const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off0, 0, 0));
+          const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(xr, off1, 0, 0));
+          rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
       } else {
         const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.ldx + (uint32_t)cx) * (uint32_t)ES : DEAD) | dead;
         rx_[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
@@ -597,10 +603,13 @@ BIGDL_EXPORT int bigdl_conv_wgrad_grouped(const void* x, const void* dy, float* 
 // fp32 operands (bf16x3 fp32 compute mode): x [Nb][H][W][C], dy [Nb][P][Q][K] fp32 NHWC (16-B aligned,
 // C % 8 == 0, K % 8 == 0); dw [K][R][S][C] fp32 += scale · Σ dyᵀ·x̂ at bf16x3 accuracy in ONE launch.
 // Pixel depth 32 per k-tile (the hi + lo tiles double the LDS image).  splits <= 0: heuristic.
+// C == 4 (the padded RGB stem, x [Nb][H][W][4]): the C4 gather, an 8-index chunk = two taps × 4 channels.
 BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw, float scale, int Nb, int H, int W,
                                       int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh,
                                       int dwd, int splits, hipStream_t s) {
-  if (C % 8 || K % 8 || Nb <= 0 || !x || !dy || !dw) return (int)hipErrorInvalidValue;
+  const bool c4 = C == 4;
+  if ((C % 8 && !c4) || K % 8 || Nb <= 0 || !x || !dy || !dw) return (int)hipErrorInvalidValue;
+  if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
   if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15)) return (int)hipErrorInvalidValue;
   if ((size_t)Nb * H * W * C * 4 >= 0x80000000ull || (size_t)Nb * P * Q * K * 4 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
@@ -621,9 +630,9 @@ BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw
   p.Kg = R * S * C;
   p.fPQ = make_fastdiv((uint32_t)(P * Q));
   p.fQ = make_fastdiv((uint32_t)Q);
-  p.pw1 = (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && P == H && Q == W) ? 1 : 0;
+  p.pw1 = (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && P == H && Q == W && !c4) ? 1 : 0;
   const int TN = K <= 64 ? 64 : 128;
-  const int TK = p.Kg <= 64 ? 64 : 128;
+  const int TK = (p.Kg <= 64 && !c4) ? 64 : 128;
   p.tiles_n = (K + TN - 1) / TN;
   p.tiles_k = (p.Kg + TK - 1) / TK;
   const int tiles = p.tiles_n * p.tiles_k;
@@ -643,7 +652,10 @@ BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw
   const dim3 grid(tiles, splits, 1);
 #define BIGDL_WF32(TN_, TK_, PW_) \
   hipLaunchKernelGGL((k_conv_wgrad<TN_, TK_, 32, false, false, false, PW_, true>), grid, dim3(256), 0, s, p)
-  if (p.pw1) {
+  if (c4) {
+    if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, true, false, false, false, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32, true, false, false, false, true>), grid, dim3(256), 0, s, p);
+  } else if (p.pw1) {
     if (TN == 64 && TK == 64) BIGDL_WF32(64, 64, true);
     else if (TN == 64) BIGDL_WF32(64, 128, true);
     else if (TK == 64) BIGDL_WF32(128, 64, true);

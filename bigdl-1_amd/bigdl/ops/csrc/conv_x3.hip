@@ -31,7 +31,10 @@
 //   bnbwd  : the data gradient g = acc (+ res) masked by the ReLU of the BN that produced this
 //            conv's input (mask bits, or recomputed as sc·x + sh > 0 from that BN's input x), stored,
 //            and Σg, Σg·(x − mean) of that BN's backward added into its replicated buffer.
-// Modes: 1 = tap-uniform gather (C % 32 == 0, R·S ≤ 64), 3 = pointwise (1×1, no padding).
+// Modes: 1 = tap-uniform gather (C % 32 == 0, R·S ≤ 64), 3 = pointwise (1×1, no padding), 2 = C4: the
+// 4-channel (padded RGB) stem input [Nb][H][W][4] — a k-tile is 8 taps × 4 channels, each lane's 16-B
+// DMA piece one tap of its row (its own padding test), so the 7×7 stem reduces over ⌈49 / 8⌉·32 = 224
+// indices (the s2d image's 16 taps × 32 padded channels were 512).
 #include "common.h"
 #include <type_traits>
 
@@ -124,7 +127,8 @@ __device__ __forceinline__ float x3_row_fold(float v) {
 
 template <int BM, int BN, int WM, int WN, int MODE, int NS>
 __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) k_conv_x3(X3Params p) {
-  static_assert(MODE == 1 || MODE == 3, "tap-uniform / pointwise gathers only");
+  static_assert(MODE == 1 || MODE == 2 || MODE == 3, "tap-uniform / C4 / pointwise gathers only");
+  constexpr bool C4 = MODE == 2;
   static_assert(NS == 2 || NS == 3, "LDS ring depth");
   constexpr bool PW = MODE == 3;
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
@@ -155,7 +159,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
   constexpr uint32_t OOB = 0x80000000u;
 
   const int lrow = lane >> 3, slot = lane & 7;
-  const int KT = p.Kg / BK;  // host-checked: C % 32 == 0
+  const int KT = p.Kg / BK;  // host-checked: C % 32 == 0 (C4: Kg = ⌈R·S / 8⌉·32)
   uint32_t woff[GA];
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
@@ -166,6 +170,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
   }
   int rbase[GB];  // fp32 elements
   uint64_t vmask[GB];
+  int c4h[C4 ? GB : 1], c4w[C4 ? GB : 1], c4t[C4 ? GB : 1];  // C4: the row's window origin, its lane's tap
   const bool pw_direct = PW && p.sh == 1 && p.sw == 1;
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
@@ -173,6 +178,22 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
     const int chunk = slot ^ ((row >> 1) & 7);
     const int m = m0 + row;
     int img = -1, h = 0, w = 0;
+    if constexpr (C4) {
+      if (m < p.M) {
+        const int n = m / (p.P * p.Q);
+        const int pq = m - n * p.P * p.Q;
+        const int pp = pq / p.Q, qq = pq - pp * p.Q;
+        img = n * p.H * p.W;
+        h = pp * p.sh - p.ph;
+        w = qq * p.sw - p.pw;
+      }
+      rbase[j] = img;  // pixel index of the image's (0, 0); -1: a row past M
+      c4h[j] = h;
+      c4w[j] = w;
+      c4t[j] = chunk;  // the tap this lane stages in k-tile 0 (kt·8 + chunk later)
+      vmask[j] = 0;
+      continue;
+    }
     if (m < p.M) {
       if (pw_direct) {
         img = m;
@@ -210,6 +231,17 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
     const uint32_t kb = (uint32_t)kt * 128u;
 #pragma unroll
     for (int i = 0; i < GA; ++i) poff[i] = woff[i] + kb;
+    if constexpr (C4) {
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int t = kt * 8 + c4t[j];
+        const int r = t / p.S, sx = t - r * p.S;
+        const int h = c4h[j] + r * p.dh, w = c4w[j] + sx * p.dw;
+        const bool ok = rbase[j] >= 0 && t < p.R * p.S && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+        poff[GA + j] = ok ? (uint32_t)(rbase[j] + h * p.W + w) * 16u : OOB;
+      }
+      return;
+    }
     const int tap = PW ? 0 : it_tap;
     const int tap_off = PW ? kt * BK : it_off + it_c0;
     if (!PW) {
@@ -522,13 +554,17 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
                                int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
                                int relu, int ldy, int bm, int bn, int osh, int osw, int ooh, int oow, int oH,
                                int oW, int res_sh, int res_sw, int res_H, int res_W, int persist, hipStream_t s) {
-  if (!x || !w2 || !y || Nb <= 0 || C <= 0 || K <= 0 || P <= 0 || Q <= 0 || C % 32 || K % 4 || ldy < K || ldy % 4)
+  const bool c4 = C == 4;  // the padded RGB stem: x [Nb][H][W][4]
+  if (!x || !w2 || !y || Nb <= 0 || C <= 0 || K <= 0 || P <= 0 || Q <= 0 || (C % 32 && !c4) || K % 4 || ldy < K ||
+      ldy % 4)
+    return (int)hipErrorInvalidValue;
+  if (c4 && (R * S > 64 || bnx || osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q || res_sh))
     return (int)hipErrorInvalidValue;
   if (!x3_al(x) || !x3_al(w2) || !x3_al(y) || (res && !x3_al(res)) || (bnx && !x3_al(bnx)))
     return (int)hipErrorInvalidValue;
   if (stats && (R_rep <= 0 || K % 8 || ldy != K || (!bnx && (bias || relu || res)))) return (int)hipErrorInvalidValue;
   if (bnx && (!stats || !mean || relu || bias || (!bits && (!bsc || !bsh)))) return (int)hipErrorInvalidValue;
-  const bool pw1 = R == 1 && S == 1 && ph == 0 && pw == 0;
+  const bool pw1 = R == 1 && S == 1 && ph == 0 && pw == 0 && !c4;
   if (!pw1 && R * S > 64) return (int)hipErrorNotSupported;
   if ((size_t)Nb * H * W * C * 4 >= 0x80000000ull || (size_t)K * R * S * C * 4 >= 0x80000000ull)
     return (int)hipErrorInvalidValue;
@@ -542,7 +578,7 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   p.x = x; p.w = (const bf16_t*)w2; p.bias = bias; p.res = res; p.y = y;
   p.Nb = Nb; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.P = P; p.Q = Q;
   p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
-  p.M = (int)Ml; p.Kg = R * S * C; p.ldx = C; p.ldy = ldy; p.relu = relu;
+  p.M = (int)Ml; p.Kg = c4 ? (R * S + 7) / 8 * 32 : R * S * C; p.ldx = C; p.ldy = ldy; p.relu = relu;
   p.stats = stats; p.R_rep = stats ? R_rep : 1; p.shift = bnx ? nullptr : shift;
   p.bnx = bnx; p.mean = mean; p.bits = (const uint8_t*)bits; p.bsc = bsc; p.bsh = bsh;
   if (osh <= 0 || osw <= 0 || ooh < 0 || oow < 0) return (int)hipErrorInvalidValue;
@@ -562,8 +598,11 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
     // measured per ResNet-50 shape (tools/bench_x3.py, profiles/r5_x3_shapes.txt): 3×3 convs run best as
     // two 128 × 128 blocks per CU (2-deep ring, waves over pixels) except the 64-channel ones (256 × 64,
     // 8 × 1); pointwise convs on 256 × 128 / 256 × 64 (4 × 2), the 7² ones as two 128 × 128 blocks per CU
-    const bool pw1_ = R == 1 && S == 1 && ph == 0 && pw == 0;
-    if (!pw1_) {
+    const bool pw1_ = R == 1 && S == 1 && ph == 0 && pw == 0 && !c4;
+    if (c4) {
+      bm = 256;
+      bn = K <= 64 ? (64 | 0x100) : 128;
+    } else if (!pw1_) {
       bm = K <= 64 ? 256 : 128;
       bn = K <= 64 ? (64 | 0x100) : (128 | 0x300);
     } else if (K <= 64) {
@@ -588,7 +627,8 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   const long long tiles = (Ml + bm - 1) / bm * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   (void)persist;  // (a persistent tile-stream variant measured no gain: removed)
-  if (pw1) launch_x3<3>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
+  if (c4) launch_x3<2>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
+  else if (pw1) launch_x3<3>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   else launch_x3<1>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   BIGDL_CHECK_LAUNCH();
 }

@@ -360,14 +360,29 @@ BIGDL_EXPORT int bigdl_adam_dev(float* w, const float* g, float* m, float* v, bf
 // w -= clr · g' / (sqrt(s) + 1e-10),  clr = lr / (1 + n·lr_decay) — one pass over (w, g, s) plus the
 // optional bf16 shadow, in place of five torch elementwise kernels.  dev_n (nullable): the
 // iteration count n read on the device (replay-safe under HIP-graph capture); else clr is given.
-__global__ void k_adagrad(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ sv,
+// G = bf16: the gradient read straight from the DistriOptimizer's bf16 reduce-scatter wire shard
+// (widened on load, as the SGD kernel does) — no fp32 unpack pass per bucket.
+__device__ __forceinline__ float ag_ld(const float* g, long long e) { return g[e]; }
+__device__ __forceinline__ float ag_ld(const bf16_t* g, long long e) { return bf2f(g[e]); }
+__device__ __forceinline__ void ag_ld4(const float* g, long long i, float (&o)[4]) {
+  const float4 G = reinterpret_cast<const float4*>(g)[i];
+  o[0] = G.x; o[1] = G.y; o[2] = G.z; o[3] = G.w;
+}
+__device__ __forceinline__ void ag_ld4(const bf16_t* g, long long i, float (&o)[4]) {
+  const uint2 u = reinterpret_cast<const uint2*>(g)[i];
+  o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xFFFF0000u);
+  o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xFFFF0000u);
+}
+
+template <typename G>
+__global__ void k_adagrad(float* __restrict__ w, const G* __restrict__ g, float* __restrict__ sv,
                           bf16_t* __restrict__ shadow, long long n4, float clr, float wd, float scale, int tail,
                           const float* __restrict__ dev_n, float lr, float lr_decay) {
   if (dev_n) clr = lr / (1.f + dev_n[0] * lr_decay);
   const long long stride = (long long)gridDim.x * blockDim.x;
   if (blockIdx.x == 0 && threadIdx.x < tail) {
     const long long e = n4 * 4 + threadIdx.x;
-    const float gg = g[e] * scale + wd * w[e];
+    const float gg = ag_ld(g, e) * scale + wd * w[e];
     const float ss = sv[e] + gg * gg;
     sv[e] = ss;
     const float nw = w[e] - clr * gg / (sqrtf(ss) + 1e-10f);
@@ -376,9 +391,9 @@ __global__ void k_adagrad(float* __restrict__ w, const float* __restrict__ g, fl
   }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 W = reinterpret_cast<float4*>(w)[i];
-    const float4 G = reinterpret_cast<const float4*>(g)[i];
     const float4 S = reinterpret_cast<float4*>(sv)[i];
-    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w}, sq[4] = {S.x, S.y, S.z, S.w};
+    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4], sq[4] = {S.x, S.y, S.z, S.w};
+    ag_ld4(g, i, gv);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gg = gv[k] * scale + wd * wv[k];
@@ -399,8 +414,18 @@ BIGDL_EXPORT int bigdl_adagrad(float* w, const float* g, float* sv, bf16_t* shad
                                const float* dev_n, float lr, float lr_decay, float wd, float scale, hipStream_t s) {
   if (n <= 0) return 0;
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(k_adagrad, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, sv, shadow, n4, clr,
-                     wd, scale, (int)(n & 3), dev_n, lr, lr_decay);
+  hipLaunchKernelGGL(k_adagrad<float>, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, sv, shadow, n4,
+                     clr, wd, scale, (int)(n & 3), dev_n, lr, lr_decay);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// the same update with a bf16 gradient (8-B aligned: the host checks)
+BIGDL_EXPORT int bigdl_adagrad_g16(float* w, const bf16_t* g, float* sv, bf16_t* shadow, long long n, float clr,
+                                   const float* dev_n, float lr, float lr_decay, float wd, float scale, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adagrad<bf16_t>, dim3(bigdl_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s, w, g, sv, shadow, n4,
+                     clr, wd, scale, (int)(n & 3), dev_n, lr, lr_decay);
   BIGDL_CHECK_LAUNCH();
 }
 

@@ -119,6 +119,36 @@ __global__ void __launch_bounds__(256) k_s2d_f32(const float* __restrict__ x, lo
   }
 }
 
+// The RGB stem input for the C4 x3 / fp32 wgrad gathers: any-stride fp32 [N][C ≤ 4][H][W] → NHWC
+// [N][H][W][4] fp32 (channels ≥ C zero): one 16-B store per pixel (the 7×7 stem then reduces over 49 taps
+// × 4 channels = 196 → 224 indices instead of the s2d image's 16 taps × 32 padded channels = 512).
+__global__ void __launch_bounds__(256) k_pad4_f32(const float* __restrict__ x, long long sn, long long sc,
+                                                  long long sh, long long sw, int N, int C, int H, int W,
+                                                  float* __restrict__ out) {
+  const long long total = (long long)N * H * W;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int w = (int)(t % W);
+    const long long r = t / W;
+    const int h = (int)(r % H);
+    const int n = (int)(r / H);
+    const float* px = x + n * sn + h * sh + w * sw;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = e < C ? px[e * sc] : 0.f;
+    *reinterpret_cast<float4*>(out + t * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+BIGDL_EXPORT int bigdl_pad4_f32(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C,
+                                int H, int W, float* out, hipStream_t s) {
+  if (!x || !out || N <= 0 || C <= 0 || C > 4 || H <= 0 || W <= 0 || ((uintptr_t)out & 15))
+    return (int)hipErrorInvalidValue;
+  const long long total = (long long)N * H * W;
+  hipLaunchKernelGGL(k_pad4_f32, dim3(bigdl_grid(total, 256, 32768)), dim3(256), 0, s, x, sn, sc, sh, sw, N, C, H, W,
+                     out);
+  BIGDL_CHECK_LAUNCH();
+}
+
 BIGDL_EXPORT int bigdl_s2d_f32(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C,
                                int H, int W, int ph, int pw, int H2, int W2, int Cp, float* out, hipStream_t s) {
   if (!x || !out || N <= 0 || C <= 0 || H2 <= 0 || W2 <= 0 || Cp % 4 || 4 * C > Cp || ((uintptr_t)out & 15))

@@ -17,6 +17,8 @@
 //           W[k][c][2a + bh][2b + bw] (0 outside R×S / C), 32 channels per (a, b)
 //   3 ROWS3 [rows][3·cp] = [hi | lo | hi] of M[row][col] (0 for col ≥ cols or row ≥ nrows); rows = R
 //           (padded row count), cp = S, nrows = K, cols = C; element (row, col) at row·sK + col·sC
+//   4 C4    the 4-channel stem filter (conv_x3.hip MODE 2): row k = ⌈R·S / 8⌉·32 indices, index
+//           tap·4 + c of W[k][c][tap / S][tap % S] (0 for c ≥ C or tap ≥ R·S)
 // Reference: the per-layer weight layouts of DL/nn/SpatialConvolution.scala:435-505 (col2im backward)
 // and DL/nn/Linear.scala:108-158.
 #include "common.h"
@@ -58,14 +60,24 @@ __device__ __forceinline__ bf16_t* chunk_hi(bf16_t* out, long long L) { return o
 
 __device__ void wx_body(const WxJob& jb, long long local) {
   const int tid = threadIdx.x;
-  if (jb.kind == 0 || jb.kind == 2) {
+  if (jb.kind == 0 || jb.kind == 2 || jb.kind == 4) {
     // 8 consecutive output elements per thread
     const long long L = (local * 256 + tid) * 8;
     const int R2 = (jb.R + 1) >> 1, S2 = (jb.S + 1) >> 1;
-    const long long n = jb.kind == 0 ? (long long)jb.K * jb.R * jb.S * jb.C : (long long)jb.K * R2 * S2 * 32;
+    const int KW4 = (jb.R * jb.S + 7) / 8 * 32;  // C4 row length
+    const long long n = jb.kind == 0   ? (long long)jb.K * jb.R * jb.S * jb.C
+                        : jb.kind == 2 ? (long long)jb.K * R2 * S2 * 32
+                                       : (long long)jb.K * KW4;
     if (L >= n) return;
     float v[8];
-    if (jb.kind == 0) {
+    if (jb.kind == 4) {
+      const int k = (int)(L / KW4), i0 = (int)(L - (long long)k * KW4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int idx = i0 + e, tap = idx >> 2, c = idx & 3, r = tap / jb.S, s = tap - (tap / jb.S) * jb.S;
+        v[e] = (c < jb.C && tap < jb.R * jb.S) ? jb.in[k * jb.sK + r * jb.sR + s * jb.sS + c * jb.sC] : 0.f;
+      }
+    } else if (jb.kind == 0) {
       long long q = L;
       int c = (int)(q % jb.C);
       q /= jb.C;
@@ -179,7 +191,7 @@ BIGDL_EXPORT int bigdl_wx3_job(void* rec, const float* in, void* out, int kind, 
                                long long sK, long long sC, long long sR, long long sS, int ncls, const int* ros,
                                const int* sos, const int* rmaps, const int* smaps, const long long* out_offs,
                                long long first_block, long long* nblocks) {
-  if (!in || !out || K <= 0 || C <= 0 || R <= 0 || S <= 0 || ((uintptr_t)out & 15) || kind < 0 || kind > 3)
+  if (!in || !out || K <= 0 || C <= 0 || R <= 0 || S <= 0 || ((uintptr_t)out & 15) || kind < 0 || kind > 4)
     return (int)hipErrorInvalidValue;
   WxJob jb{};
   jb.in = in;
@@ -196,6 +208,10 @@ BIGDL_EXPORT int bigdl_wx3_job(void* rec, const float* in, void* out, int kind, 
   } else if (kind == 2) {
     if (4 * C > 32) return (int)hipErrorInvalidValue;
     const long long n = (long long)K * ((R + 1) / 2) * ((S + 1) / 2) * 32;
+    nb = (n + 2047) / 2048;
+  } else if (kind == 4) {
+    if (C > 4 || R * S > 64) return (int)hipErrorInvalidValue;
+    const long long n = (long long)K * ((R * S + 7) / 8) * 32;
     nb = (n + 2047) / 2048;
   } else if (kind == 3) {
     // R = padded rows (≥ K), S = part width cp (% 8, ≥ C)
@@ -271,6 +287,32 @@ BIGDL_EXPORT int bigdl_s2d_wgrad_fold(float* g2, float* gw, int K, int C, int R,
   if (!g2 || !gw || K <= 0 || C <= 0 || 4 * C > 32 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
   const long long n = (long long)K * ((R + 1) / 2) * ((S + 1) / 2) * 32;
   hipLaunchKernelGGL(k_s2d_wgrad_fold, dim3(bigdl_grid(n, 256)), dim3(256), 0, s, g2, gw, K, C, R, S, sK, sC, sR, sS,
+                     scale);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// The C4 stem's weight gradient onto the KCRS-strided master gradient: gw[k][c][r][s] += scale ·
+// g4[k][r][s][c] (c < C), every g4 entry cleared after it is read (a persistent split-K buffer).
+__global__ void __launch_bounds__(256) k_c4_wgrad_fold(float* __restrict__ g4, float* __restrict__ gw, int K, int C,
+                                                       int R, int S, long long sK, long long sC, long long sR,
+                                                       long long sS, float scale) {
+  const long long n = (long long)K * R * S * 4;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int c = (int)(e & 3);
+    const long long kt = e >> 2;
+    const int tap = (int)(kt % (R * S)), k = (int)(kt / (R * S));
+    const int r = tap / S, s = tap - (tap / S) * S;
+    const float v = g4[e];
+    if (c < C) gw[k * sK + c * sC + r * sR + s * sS] += scale * v;
+    g4[e] = 0.f;
+  }
+}
+
+BIGDL_EXPORT int bigdl_c4_wgrad_fold(float* g4, float* gw, int K, int C, int R, int S, long long sK, long long sC,
+                                     long long sR, long long sS, float scale, hipStream_t s) {
+  if (!g4 || !gw || K <= 0 || C <= 0 || C > 4 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
+  const long long n = (long long)K * R * S * 4;
+  hipLaunchKernelGGL(k_c4_wgrad_fold, dim3(bigdl_grid(n, 256)), dim3(256), 0, s, g4, gw, K, C, R, S, sK, sC, sR, sS,
                      scale);
   BIGDL_CHECK_LAUNCH();
 }

@@ -254,7 +254,8 @@ def mark_dirty(t) -> None:
 
 def _wprep(w, form):
     """The bf16 operand of fp32 weight ``w`` in ``form``:
-    ("fwd",) → conv_x3 chunks of the KRSC rows; ("s2d",) → the stem's s2d filter chunks;
+    ("fwd",) → conv_x3 chunks of the KRSC rows; ("s2d",) → the stem's s2d filter chunks; ("c4",) → the
+    4-channel stem filter chunks (8 taps × 4 channels per 32-index chunk);
     ("dg", classes) → [view per class] of the flipped, transposed sub-filters, classes = tuple of
     (rmap, smap) tap lists; ("rows3", rows, cp, transposed) → [rows][3·cp] = [hi | lo | hi] of w (or wᵀ)."""
     if not (w.is_cuda and hasattr(N.lib(), "bigdl_wx3_multi")):
@@ -275,7 +276,7 @@ def _wprep(w, form):
             return e["views"]
         _WP.pop(key, None)
     kind = form[0]
-    if kind in ("fwd", "s2d", "dg"):
+    if kind in ("fwd", "s2d", "dg", "c4"):
         k_, c_, r_, s_ = wd.shape
     if kind == "fwd":
         if (r_ * s_ * c_) % 32:
@@ -290,6 +291,13 @@ def _wprep(w, form):
         out = torch.empty(k_ * r2 * s2 * 64, dtype=_bf16, device=wd.device)
         job = (2, (k_, c_, r_, s_), wd.stride(), ())
         views = out.view(k_, r2 * s2, 64)
+    elif kind == "c4":
+        if c_ > 4 or r_ * s_ > 64:
+            return NotImplemented
+        kt = (r_ * s_ + 7) // 8
+        out = torch.empty(k_ * kt * 64, dtype=_bf16, device=wd.device)
+        job = (4, (k_, c_, r_, s_), wd.stride(), ())
+        views = out.view(k_, kt, 64)
     elif kind == "dg":
         classes = form[1]
         if k_ % 32 or not 1 <= len(classes) <= 4 or any(len(a) > 8 or len(b) > 8 for a, b in classes):
@@ -387,9 +395,28 @@ def _w_dgrad(w4, classes):
             for a, b in classes]
 
 
-def _stem_ok(c, k, stride, dilation):
+def _c4_ok(c, k, r, s, dilation):
+    """The C4 stem path (conv_x3.hip MODE 2 forward, conv_wgrad.hip C4 F32 weight gradient) applies."""
+    from ..utils import config
+    return (c <= 4 and k % 8 == 0 and r * s <= 64 and tuple(dilation) == (1, 1) and _direct() and _x3_has()
+            and hasattr(N.lib(), "bigdl_pad4_f32") and bool(config.get_property("bigdl.fp32.stemC4")))
+
+
+def _stem_ok(c, k, stride, dilation, r=7, s=7):
+    if _c4_ok(c, k, r, s, dilation):
+        return True
     return (tuple(stride) == (2, 2) and tuple(dilation) == (1, 1) and 4 * c <= 32 and c % 32 != 0 and k % 8 == 0
             and _direct() and _x3_has() and hasattr(N.lib(), "bigdl_s2d_f32"))
+
+
+def _pad4(x):
+    """A ≤ 4-channel fp32 image (any strides) → NHWC [N][H][W][4] fp32, channels ≥ C zero."""
+    nb, c, h, w = x.shape
+    out = torch.empty((nb, 4, h, w), dtype=_f32, device=x.device, memory_format=_cl)
+    xs = x.float()
+    check(N.lib().bigdl_pad4_f32(ptr(xs), *(C.c_longlong(v) for v in xs.stride()), nb, c, h, w, ptr(out), _s()),
+          "pad4_f32")
+    return out
 
 
 def _s2d(x, pad, r, s, p, q):
@@ -418,9 +445,24 @@ def _stem_weights(w4):
     return out
 
 
-def _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot):
+def _stem_forward(x, w4, b, stride, pad, relu, stats, rep, shift, slot):
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
+    if _c4_ok(c, k, r, s, (1, 1)):
+        p, q = _out_hw(h, w, r, s, stride, pad, (1, 1))
+        if p <= 0 or q <= 0:
+            return NotImplemented
+        xs = _pad4(x)
+        if slot is not None:
+            slot[0] = (("c4",) + _slot_key(x, 4, True)[1:], xs)
+        y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
+        bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
+        w2 = _wprep(w4, ("c4",))
+        if w2 is NotImplemented:
+            return NotImplemented
+        _x3(xs, w2, y, nb, h, w, 4, k, r, s, p, q, tuple(stride), tuple(pad), (1, 1), bias=bias, relu=relu,
+            stats=stats, rep=rep, shift=shift)
+        return y
     p, q = _out_hw(h, w, r, s, (2, 2), pad, (1, 1))
     if p <= 0 or q <= 0:
         return NotImplemented
@@ -438,12 +480,31 @@ def _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot):
     return y
 
 
-def _stem_wgrad(x, gy, gw_acc, scale, pad, slot):
-    """Weight gradient of the s2d stem: the fp32 wgrad of the 4×4 stride-1 conv over the s2d image,
-    folded back onto the R×S×C taps."""
+def _stem_wgrad(x, gy, gw_acc, scale, stride, pad, slot):
+    """Weight gradient of the stem.  C4 path: the fp32 C4 wgrad over the 4-channel copy of the input
+    into a persistent [K][R][S][4] buffer, folded onto the master's taps (and cleared) by one launch.
+    s2d path: the fp32 wgrad of the 4×4 stride-1 conv over the s2d image, folded back onto the R×S×C
+    taps."""
     nb, c, h, w = x.shape
     k, _, r, s = gw_acc.shape
     p, q = gy.shape[2], gy.shape[3]
+    if _c4_ok(c, k, r, s, (1, 1)) and hasattr(N.lib(), "bigdl_c4_wgrad_fold") and gw_acc.dtype == _f32:
+        held = slot[0] if slot is not None else None
+        key = ("c4",) + _slot_key(x, 4, True)[1:]
+        if isinstance(held, tuple) and len(held) == 2 and held[0] == key:
+            xs = held[1]
+            slot[0] = None
+        else:
+            xs = _pad4(x)
+        bkey = ("c4", gw_acc.data_ptr(), k, r, s, gw_acc.device)
+        g4 = _S2D_ACC.get(bkey)
+        if g4 is None:
+            g4 = _S2D_ACC[bkey] = torch.zeros((k, r, s, 4), dtype=_f32, device=x.device)
+        check(N.lib().bigdl_conv_wgrad_f32(ptr(xs), ptr(gy), ptr(g4), C.c_float(1.0), nb, h, w, 4, k, r, s, p, q,
+                                           stride[0], stride[1], pad[0], pad[1], 1, 1, 0, _s()), "conv_wgrad_f32(c4)")
+        check(N.lib().bigdl_c4_wgrad_fold(ptr(g4), ptr(gw_acc), k, c, r, s, *(C.c_longlong(v) for v in gw_acc.stride()),
+                                          C.c_float(float(scale)), _s()), "c4_wgrad_fold")
+        return
     r2, s2 = (r + 1) // 2, (s + 1) // 2
     held = slot[0] if slot is not None else None
     key = ("s2d",) + _slot_key(x, 32, True)[1:]
@@ -476,8 +537,8 @@ _S2D_ACC: dict = {}
 def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None, slot=None):
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
-    if _stem_ok(c, k, stride, dilation) and x.dtype == _f32:
-        return _stem_forward(x, w4, b, pad, relu, stats, rep, shift, slot)
+    if _stem_ok(c, k, stride, dilation, r, s) and x.dtype == _f32:
+        return _stem_forward(x, w4, b, stride, pad, relu, stats, rep, shift, slot)
     if not (_direct() and _x3_has() and _x3_geom_ok(c, k, r, s, pad) and _cl_f32(x)):
         return NotImplemented
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
@@ -767,20 +828,21 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     its input gradient as a StridedGrad."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
-    if (not need_input and gw_acc is not None and _stem_ok(x.shape[1], w4.shape[0], stride, dilation)
+    if (not need_input and gw_acc is not None
+            and _stem_ok(x.shape[1], w4.shape[0], stride, dilation, w4.shape[2], w4.shape[3])
             and _cl_f32(gy) and x.dtype == _f32 and gw_acc.dtype == _f32):
         if scale != 0:
             from .native_ops import _wgrad_side_stream
             side = _wgrad_side_stream(gy)
             if side is not None:
                 with torch.cuda.stream(side):
-                    _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
+                    _stem_wgrad(x, gy, gw_acc, scale, stride, pad, slot)
                     if gb_acc is not None:
                         bias_grad_acc(gy, gb_acc, scale)
                 for t in (x, gy):
                     t.record_stream(side)
             else:
-                _stem_wgrad(x, gy, gw_acc, scale, pad, slot)
+                _stem_wgrad(x, gy, gw_acc, scale, stride, pad, slot)
                 if gb_acc is not None:
                     bias_grad_acc(gy, gb_acc, scale)
         return None

@@ -1694,7 +1694,13 @@ def adagrad_step(w, g, s, lr, lr_decay, n, weight_decay=0.0, grad_scale=1.0, sha
     before this step) makes it replay-safe under HIP-graph capture, else ``n`` (host) is used."""
     F3.mark_dirty(w)
     numel = w.numel()
-    if w.dtype != _f32 or g.dtype != _f32 or s.dtype != _f32 or not _vec_ok(w, g, s, n=numel):
+    g16 = g.dtype == _bf16  # the DistriOptimizer's bf16 wire shard, widened on load
+    if w.dtype != _f32 or s.dtype != _f32 or not _vec_ok(w, s, n=numel):
+        return NotImplemented
+    if g16:
+        if not (g.is_cuda and g.is_contiguous() and g.numel() == numel and g.data_ptr() % 8 == 0):
+            return NotImplemented
+    elif g.dtype != _f32 or not _vec_ok(g, n=numel):
         return NotImplemented
     if dev_n is not None and not (dev_n.is_cuda and dev_n.dtype == _f32):
         return NotImplemented
@@ -1702,8 +1708,9 @@ def adagrad_step(w, g, s, lr, lr_decay, n, weight_decay=0.0, grad_scale=1.0, sha
                                    and shadow.data_ptr() % 8 == 0):
         return NotImplemented
     clr = lr / (1 + n * lr_decay)
-    check(_lib().bigdl_adagrad(ptr(w), ptr(g), ptr(s), ptr(shadow), _ll(numel), _f(clr), ptr(dev_n), _f(lr),
-                               _f(lr_decay), _f(weight_decay), _f(grad_scale), _s()), "adagrad")
+    fn = _lib().bigdl_adagrad_g16 if g16 else _lib().bigdl_adagrad
+    check(fn(ptr(w), ptr(g), ptr(s), ptr(shadow), _ll(numel), _f(clr), ptr(dev_n), _f(lr), _f(lr_decay),
+             _f(weight_decay), _f(grad_scale), _s()), "adagrad")
     return w
 
 

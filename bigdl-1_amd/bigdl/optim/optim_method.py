@@ -324,6 +324,8 @@ class EpochDecayWithWarmUp(LearningRateSchedule):
 
 # ----------------------------------------------------------------------------------------- SGD
 class SGD(OptimMethod):
+    reads_bf16_grad = True  # apply_update takes the bf16 wire gradient shard (widened in the kernel)
+
     def prepare_graph(self) -> bool:
         # the fused kernel takes lr by value: replayable only while the schedule is constant
         if type(self.learningRateSchedule) is Default and self.learningRateDecay == 0:
@@ -571,6 +573,8 @@ class Adagrad(_Elementwise):
         self._n = self.state.get("evalCounter", 0)
         self._state_tensor("paramVariance", x)
 
+    reads_bf16_grad = True  # apply_update takes the bf16 wire gradient shard (widened in the kernel)
+
     def _update(self, x, g, sl, shadow):
         n = self._n
         s = self.state["paramVariance"][sl]
@@ -580,7 +584,7 @@ class Adagrad(_Elementwise):
                                             self.grad_scale, shadow)
             if r is not NotImplemented:
                 return
-        g = g * self.grad_scale
+        g = g.float() * self.grad_scale
         if self.weightDecay != 0:
             g = g + self.weightDecay * x
         s.addcmul_(g, g)

@@ -515,12 +515,12 @@ class DistriOptimizer(BaseOptimizer):
             self._drop_after_iteration()
 
     def _grad_for(self, meth, b: _Bucket):
-        """The gradient shard ``meth`` reads for bucket ``b``: the bf16 wire shard itself for SGD
-        (its fused kernel widens on load), else the fp32 shard (unpacked once per bucket)."""
-        from ..optim.optim_method import SGD
+        """The gradient shard ``meth`` reads for bucket ``b``: the bf16 wire shard itself for methods
+        whose fused kernel widens a bf16 gradient on load (SGD, Adagrad), else the fp32 shard
+        (unpacked once per bucket)."""
         if self.grad_wire is None:
             return self.shard_g
-        if type(meth) is SGD and not b.unpacked:
+        if getattr(meth, "reads_bf16_grad", False) and not b.unpacked:
             return self.shard_g_wire
         self._finish_reduce(b, unpack=True)
         return self.shard_g

@@ -186,38 +186,53 @@ def test_direct_off_falls_back_to_split_path():
     assert _rel(y1, y0) < 2e-5
 
 
-def test_direct_stem_space_to_depth():
-    """The fp32 RGB stem (7×7 stride 2 over 3 channels) runs as a 4×4 stride-1 conv over the
-    space-to-depth image on the direct kernels: forward (+ BN statistics epilogue) and weight gradient
-    against fp64."""
+@pytest.mark.parametrize("c4,C,K,H,k,st,pd", [(False, 3, 64, 30, 7, 2, 3), (True, 3, 64, 30, 7, 2, 3),
+                                             (True, 3, 64, 31, 7, 2, 3), (True, 4, 32, 9, 3, 1, 1),
+                                             (True, 1, 16, 12, 5, 1, 0)],
+                         ids=["s2d", "c4", "c4_odd", "c4_3x3", "c4_gray5x5"])
+def test_direct_stem(c4, C, K, H, k, st, pd):
+    """The fp32 RGB stem (≤ 4 input channels) on the direct kernels — either the 4-channel gather
+    (bigdl.fp32.stemC4: conv_x3 MODE 2, 8 taps × 4 channels per k-tile; the C4 fp32 weight gradient
+    folded onto the master's taps) or the space-to-depth image (a 4×4 stride-1 conv): forward (+ BN
+    statistics epilogue) and weight gradient against fp64."""
     from bigdl.ops import fp32x3 as F3, native_ops as NO
-    g = torch.Generator().manual_seed(17)
-    N_, H = 2, 30
-    x = torch.randn(N_, 3, H, H, generator=g)
-    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
-    xr, wr = x.double(), w.double().requires_grad_()
-    yr = F.conv2d(xr, wr, None, 2, 3)
-    gy = torch.randn(yr.shape, generator=g)
-    yr.backward(gy.double())
-    xd = x.to(dev).contiguous(memory_format=cl)
-    slot = [None]
-    y, names = _kernels(lambda: F3.conv_forward(xd, w.to(dev), None, (2, 2), (3, 3), slot=slot))
-    assert any("k_s2d_f32" in n for n in names) and any("k_conv_x3" in n for n in names), names
-    assert _rel(y, yr) < 2e-5, _rel(y, yr)
-    gw = torch.zeros(64, 7, 7, 3, device=dev).permute(0, 3, 1, 2)
-    r, names = _kernels(lambda: F3.conv_backward(gy.to(dev).contiguous(memory_format=cl), xd, w.to(dev), (2, 2),
-                                                 (3, 3), (1, 1), 1, False, gw, None, 1.0, slot=slot))
-    assert r is None and not any("k_s2d_f32" in n for n in names), names  # the forward's s2d image reused
-    assert _rel(gw, wr.grad) < 2e-5, _rel(gw, wr.grad)
-    # the statistics epilogue through the s2d path
-    rep = 8
-    buf = torch.zeros(2 * rep * 64, device=dev)
-    shift = torch.zeros(64, device=dev)
-    out = NO.conv2d_forward_stats(xd, w.to(dev), None, (2, 2), (3, 3), shift=shift, sums=(buf, rep))
-    assert out is not NotImplemented
-    torch.cuda.synchronize()
-    ys = out[0].double().cpu()
-    assert _rel(buf.reshape(2, rep, 64).sum(1)[0], ys.sum((0, 2, 3))) < 1e-5
+    from bigdl.utils import config
+    config.set_property("bigdl.fp32.stemC4", c4)
+    try:
+        g = torch.Generator().manual_seed(17)
+        N_ = 2
+        x = torch.randn(N_, C, H, H, generator=g)
+        w = torch.randn(K, C, k, k, generator=g) * 0.1
+        xr, wr = x.double(), w.double().requires_grad_()
+        yr = F.conv2d(xr, wr, None, st, pd)
+        gy = torch.randn(yr.shape, generator=g)
+        yr.backward(gy.double())
+        xd = x.to(dev).contiguous(memory_format=cl)
+        slot = [None]
+        y, names = _kernels(lambda: F3.conv_forward(xd, w.to(dev), None, (st, st), (pd, pd), slot=slot))
+        prep = "k_pad4_f32" if c4 else "k_s2d_f32"
+        assert any(prep in n for n in names) and any("k_conv_x3" in n for n in names), names
+        assert _rel(y, yr) < 2e-5, _rel(y, yr)
+        gw = torch.zeros(K, k, k, C, device=dev).permute(0, 3, 1, 2)
+        for rep_ in range(2):  # twice: the persistent accumulation buffer is cleared by the fold
+            gw.zero_()
+            r, names = _kernels(lambda: F3.conv_backward(gy.to(dev).contiguous(memory_format=cl), xd, w.to(dev),
+                                                         (st, st), (pd, pd), (1, 1), 1, False, gw, None, 1.0,
+                                                         slot=slot))
+            assert r is None and (rep_ == 1 or not any(prep in n for n in names)), names  # forward's image reused
+            assert _rel(gw, wr.grad) < 2e-5, _rel(gw, wr.grad)
+        # the statistics epilogue through the stem path
+        rep = 8
+        buf = torch.zeros(2 * rep * K, device=dev)
+        shift = torch.zeros(K, device=dev)
+        out = NO.conv2d_forward_stats(xd, w.to(dev), None, (st, st), (pd, pd), shift=shift, sums=(buf, rep))
+        assert out is not NotImplemented
+        torch.cuda.synchronize()
+        ys = out[0].double().cpu()
+        assert _rel(ys, yr) < 2e-5
+        assert _rel(buf.reshape(2, rep, K).sum(1)[0], ys.sum((0, 2, 3))) < 1e-5
+    finally:
+        config.clear_property("bigdl.fp32.stemC4")
 
 
 def test_weight_operand_cache_matches_host_forms():
@@ -243,6 +258,12 @@ def test_weight_operand_cache_matches_host_forms():
     ws = torch.randn(64, 7, 7, 3, generator=g).to(dev).permute(0, 3, 1, 2)
     got = F3._wprep(ws, ("s2d",))
     ref = F3.chunk_split(F3._stem_weights(ws).reshape(64, -1))
+    assert torch.equal(got.reshape(-1), ref.reshape(-1))
+    # stem: [64][3][7][7] → C4 [64][7][64] (8 taps × 4 channels per chunk, zero past 49 taps / 3 channels)
+    got = F3._wprep(ws, ("c4",))
+    w4p = torch.zeros(64, 56, 4, device=dev)
+    w4p[:, :49, :3] = ws.permute(0, 2, 3, 1).reshape(64, 49, 3)
+    ref = F3.chunk_split(w4p.reshape(64, -1))
     assert torch.equal(got.reshape(-1), ref.reshape(-1))
     # Linear rows, plain and transposed, with padded rows / columns
     wl = torch.randn(10, 20, generator=g).to(dev)

@@ -199,6 +199,19 @@ def bench_ptb(args):
     _sync(dev)
     comm.barrier()
     el = comm.allreduce_max(time.perf_counter() - t0)
+    if _CPROFILE["n"] and rank == 0:  # host-side hot spots of the step (stderr), after the timed run
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(_CPROFILE["n"]):
+            step(batch)
+        _sync(dev)
+        pr.disable()
+        out = io.StringIO()
+        pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(40)
+        print(out.getvalue()[:12000], file=sys.stderr, flush=True)
     res = {"metric": "tokens/sec PTB 2-layer LSTM LM", "value": round(B * T * world * args.steps / el, 1),
            "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": args.dtype,
