@@ -137,6 +137,8 @@ def fuse(model, convbn=None, bnrelu=None, convsum=None, bnbwd=None, convrelu=Non
                 c = mods[i + 2] if i + 2 < len(mods) else None
                 if bnbwd and isinstance(c, SpatialConvolution) and c.format == "NCHW" and c.nGroup == 1:
                     c._bn_bwd_target = a
+                    if type(c) in _PLAIN_CONVS:
+                        a._pro_consumer = c  # fp32: its output may reach c deferred (bigdl.fp32.bnPrologue)
         if not convsum:
             continue
         for i in range(len(mods) - 1):
@@ -224,6 +226,7 @@ def unfuse(model):
             m._bias_producer = None
             m._fused_relu = False
             m._defer_ok = False
+            m._pro_consumer = None
             m._pending_stats = None
             m._pending_grad = None
         if isinstance(m, Threshold):

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import ops
-from ...ops.reference import BNGrad, StridedGrad, as_dense
+from ...ops.reference import BNGrad, BNOut, StridedGrad, as_dense
 from ...utils.engine import Engine
 from ...utils import config
 from ..abstractnn import AbstractModule, TensorModule, AutogradModule
@@ -196,7 +196,22 @@ class SpatialConvolution(TensorModule):
             return None
         return bn
 
+    def _pro_input(self, input):
+        """A deferred BN + ReLU output (fp32 bigdl.fp32.bnPrologue) this conv can take as is: (BN input,
+        [scale | shift]) or None (the caller materialises it)."""
+        if not (isinstance(input, BNOut) and input.relu and self.format == "NCHW" and self.nGroup == 1
+                and input.dim() == 4 and input.is_cuda and self.padW >= 0 and self.padH >= 0):
+            return None
+        return input.x, input.coef
+
     def updateOutput(self, input):
+        pro = self._pro_input(input)
+        if pro is not None:
+            y = self._pro_forward(pro[0], pro[1])
+            if y is not NotImplemented:
+                return y
+        if isinstance(input, BNOut):
+            input = input.dense()
         x, pad, batched, _ = self._prep(input)
         w4 = self._w4(self.cw("weight"))
         # fp32 master bias: the HIP epilogue adds fp32 (no per-call cast), the reference casts
@@ -223,7 +238,40 @@ class SpatialConvolution(TensorModule):
             y = y.permute(0, 2, 3, 1)
         return y if batched else y.squeeze(0)
 
+    def _pro_forward(self, xb, coef):
+        """Forward of a deferred BN + ReLU output (BN input ``xb``, ``coef`` = [scale | shift]) on the
+        fp32 direct kernels' B-operand prologue (+ this conv's own BN statistics epilogue)."""
+        if not ops.native_has("conv2d_forward"):
+            return NotImplemented
+        pt, pb, pl, pr = self._pads(xb)
+        if pt != pb or pl != pr:
+            return NotImplemented
+        pad = (pt, pl)
+        w4 = self._w4(self.cw("weight"))
+        b = self.bias if (self.withBias and self._bias_folded_into is None) else None
+        st, dl = (self.strideH, self.strideW), (self.dilationH, self.dilationW)
+        bn = self._stats_consumer(xb)
+        if bn is not None:
+            shift = bn._stat_shift() if config.get_property("bigdl.bn.shiftedStats") else None
+            sums = bn._atomic_sums("fwd", self.nOutputPlane, xb.device) if shift is not None else None
+            r = ops.native_ops.conv2d_forward_stats(xb, w4, b, st, pad, dl, self.nGroup, shift=shift, sums=sums,
+                                                    pro=coef) if sums is not None else NotImplemented
+            if r is not NotImplemented:
+                y, part, G = r
+                bn._pending_stats = (y.data_ptr(), tuple(y.shape), part, G, shift)
+                return y
+            if sums is not None:
+                bn._drop_sums((None, None, sums[0], sums[1]), 3)
+        return ops.native_ops.conv2d_forward(xb, w4, b, st, pad, dl, self.nGroup, relu=self._fused_relu, pro=coef)
+
     def _backward(self, input, gradOutput, need_input, acc):
+        pro = self._pro_input(input)
+        if pro is not None:
+            r = self._pro_backward(pro[0], pro[1], gradOutput, need_input, acc)
+            if r is not NotImplemented:
+                return r
+        if isinstance(input, BNOut):
+            input = input.dense()
         x, pad, batched, pads = self._prep(input)
         if isinstance(gradOutput, BNGrad):
             # a deferred BN input gradient: consumed in the backward prologues when this conv can
@@ -292,6 +340,47 @@ class SpatialConvolution(TensorModule):
                 gi = gi.squeeze(0)
             if res is not None and not fuse_res:
                 gi = gi + as_dense(res)
+        return gi
+
+    def _pro_backward(self, xb, coef, gradOutput, need_input, acc):
+        """Backward of a conv whose input is a deferred BN + ReLU output: the weight gradient reads
+        relu(xb·scale + shift) through the fp32 wgrad prologue; the data gradient's epilogue applies
+        that BN's ReLU mask (recomputed from xb) and adds its backward statistics (bn_fuse)."""
+        if not isinstance(gradOutput, torch.Tensor) or gradOutput.dim() != 4 or not gradOutput.is_cuda:
+            return NotImplemented
+        pt, pb, pl, pr = self._pads(xb)
+        if pt != pb or pl != pr:
+            return NotImplemented
+        pad = (pt, pl)
+        gy = to_device_layout(gradOutput)
+        w4 = self._w4(self.cw("weight"))
+        gw = self._w4(self.gradWeight) if acc else None
+        own_bias = self.withBias and self._bias_folded_into is None
+        same_scale = self.scale_b == self.scale_w
+        gb = self.gradBias if (acc and own_bias and same_scale) else None
+        if self._grad_residual is not None and need_input:
+            return NotImplemented  # (a block head never consumes a deferred BN output)
+        bn = self._bn_bwd_target
+        bn_fuse = None
+        if (need_input and bn is not None and bn.train and bn._coef is coef and bn._last_input is xb
+                and config.get_property("bigdl.fusion.bnbwd")):
+            C_ = coef.numel() // 2
+            bn_fuse = {"x": xb, "scale": coef[:C_], "shift": coef[C_:], "mean": bn.saveMean,
+                       "sums": bn._atomic_sums("bwd", C_, bn.saveMean.device)}
+        elif need_input:
+            return NotImplemented
+        gi = ops.native_ops.conv2d_backward(gy, xb, w4, (self.strideH, self.strideW), pad,
+                                            (self.dilationH, self.dilationW), self.nGroup, need_input, gw, gb,
+                                            self.scale_w if acc else 0.0, bn_fuse=bn_fuse, pro=coef)
+        if gi is NotImplemented:
+            if bn_fuse is not None:
+                bn._drop_sums((None, bn_fuse["sums"][0], bn_fuse["sums"][1]), 2)
+            return NotImplemented
+        if bn_fuse is not None and "partial" in bn_fuse and gi is not None:
+            bn._pending_grad = (gi.data_ptr(), bn_fuse["partial"], bn_fuse["G"])
+        # (otherwise gi is unmasked and the BN's own backward applies its ReLU mask from BNOut.dense())
+        if acc and own_bias and not same_scale and self.scale_b != 0:
+            self.gradBias.add_(acc_float(gy).sum((0, 2, 3)), alpha=self.scale_b)
         return gi
 
     #: False when this conv consumes the model input of a training run (set by

@@ -71,6 +71,9 @@ class BatchNormalization(TensorModule):
         self._init_bias_method = Zeros()
         self._fused_relu = False
         self._defer_ok = False  # nn/fusion.py shortcutbn: the fused block tail applies this BN
+        #: the conv consuming this BN + ReLU's output (nn/fusion.py, bnbwd): in fp32 compute the output
+        #: may be handed over deferred (BNOut) and applied in that conv's operand prologues
+        self._pro_consumer = None
         self._sync_group = None
         self._sync = False
         self._sync_force = False
@@ -236,6 +239,17 @@ class BatchNormalization(TensorModule):
             return None
         return p.cw("bias", torch.float32)
 
+    def _pro_deferrable(self, x, relu, residual, coef):
+        """fp32 compute: hand this BN + ReLU's output to its consumer conv deferred (bigdl.fp32.bnPrologue)."""
+        c = self._pro_consumer
+        if (c is None or not relu or residual is not None or not x.is_cuda or x.dtype != torch.float32
+                or c._bn_bwd_target is not self or not c.train):
+            return False
+        if not config.get_property("bigdl.fp32.bnPrologue") or not config.get_property("bigdl.fusion.bnbwd"):
+            return False
+        from ...ops import fp32x3 as F3
+        return F3.pro_ok(x, coef)
+
     def forward_residual(self, x, residual, relu):
         """y = [relu](BN(x) + residual) — the fused ResNet block tail (K9)."""
         self._residual_mode = True
@@ -282,11 +296,14 @@ class BatchNormalization(TensorModule):
                 self._relu_bits = None
                 if ps is not None and ps[0] == x.data_ptr() and ps[1] == tuple(x.shape):
                     special = defer or deferred_res
+                    # fp32: a mid-block BN + ReLU whose consumer conv applies it on load
+                    pdefer = not special and self._pro_deferrable(x, relu, residual, coef)
                     r = ops.native_ops.batchnorm_forward_train_partials(
                         x, ps[2], ps[3], g, b, self.runningMean, self.runningVar, self.momentum, self.eps,
-                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4], bits_out=bits,
+                        relu=relu, residual=residual, in_bias=ib, coef_out=coef, shift=ps[4],
+                        bits_out=None if pdefer else bits,
                         rezero=self._is_rep(ps[2]), zero_next=None if special else self._rep_next("fwd", ps[2]),
-                        mean_out=self._shift_next(ps[4]), apply=not defer)
+                        mean_out=self._shift_next(ps[4]), apply=not (defer or pdefer))
                     if r is not NotImplemented and not special:
                         # (the special path finalizes without the one-launch fold: it cleared the set
                         # it read, the other set may still hold a folded step's sums — stay on this one)
@@ -300,8 +317,8 @@ class BatchNormalization(TensorModule):
                                                     in_bias=ib, coef_out=coef, bits_out=bits)
                 self._relu_bits = bits
                 y, mean, invstd = r
-                if y is None:  # finalize only: the consumer (the fused block tail) applies this BN
-                    y = BNOut(x, coef)
+                if y is None:  # finalize only: the consumer (fused block tail / conv prologue) applies it
+                    y = BNOut(x, coef, relu=bool(relu))
                 self._advance_shift(mean)
                 self._last_input = x
             self.saveMean, self.saveStd = mean, invstd
@@ -425,6 +442,9 @@ class BatchNormalization(TensorModule):
             gy = to_device_layout(gy)
         relu = getattr(self, "_last_relu", self._fused_relu)
         y = self.output if relu else None
+        from ...ops.reference import BNOut
+        if isinstance(y, BNOut):
+            y = None if (self._pending_grad is not None and self._pending_grad[0] == gy.data_ptr()) else y.dense()
         if y is not None and y.dim() == 1:
             y = y.unsqueeze(0)
         g = self.cw("weight", torch.float64 if x.dtype == torch.float64 else torch.float32) if self.affine else None

@@ -1475,12 +1475,14 @@ BIGDL_EXPORT int bigdl_bn32_fwd_train_partials(const float* x, const float* res,
                                                float* save_mean, float* save_invstd, float* partial, int G,
                                                const float* kshift, float* coef, int relu, void* split, void* bits,
                                                hipStream_t s) {
-  if (C % 8 || M <= 0 || G <= 0 || G > 512 || !partial || !bn32_ok(x) || !bn32_ok(y) || (res && !bn32_ok(res)) ||
-      (split && !bn32_ok(split)))
+  // y == null: finalize only (the consumer conv applies the BN + ReLU in its operand prologue)
+  if (C % 8 || M <= 0 || G <= 0 || G > 512 || !partial || !bn32_ok(x) || (y && !bn32_ok(y)) || (res && !bn32_ok(res)) ||
+      (split && !bn32_ok(split)) || (!y && (res || split || bits || !coef)))
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift,
                      (const float*)partial, G, M, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean,
                      save_invstd, coef, coef + C, nullptr, partial);
+  if (!y) BIGDL_CHECK_LAUNCH();
   bf16_t* sp = (bf16_t*)split;
   if (relu)
     launch_bn32_apply<false, true>(M, C, s, x, res, nullptr, y, nullptr, coef, sp, (uint8_t*)bits);

@@ -59,6 +59,8 @@ struct WgradParams {
   int skip_epi;
   // 1×1, stride 1, no padding (2-D): X̂ row m is input pixel m — the gather needs no index math
   int pw1;
+  // PRO instantiations: [scale | shift] of the BN + ReLU applied to x on load ([2][C])
+  const float* pro;
   // 1: the split-K partial tile is staged in LDS (fp32) and added with wave-instructions covering
   // 256 contiguous bytes of a dW row (the fast atomic shape, MI355X_MICROARCH.md 'Global float
   // atomics'); 0: straight from the accumulators (four 64-B row segments per instruction)
@@ -85,9 +87,12 @@ __device__ __forceinline__ int tr_swz_dword(int row, int dword) {
 // two 16-B fp32 pieces, split in registers into bf16 hi = rne(v) and lo = rne(v − hi) tiles (LDS holds
 // both), and every fragment pair feeds three MFMAs (dY_hi·X_hi + dY_lo·X_hi + dY_hi·X_lo) — one launch
 // reading 4 B per element instead of three over a materialised [hi | lo] split.
+// PRO (F32 only): x is the INPUT of a training BN + ReLU whose (never written) output the conv consumed:
+// X̂ = relu(x·pro[c] + pro[C + c]) per loaded chunk, padded taps 0 (ops/fp32x3.py deferred BN).
 template <int TILE_N, int TILE_K, int BPT, bool C4 = false, bool D3 = false, bool AT = false, bool PW1 = false,
-          bool F32 = false>
+          bool F32 = false, bool PRO = false>
 __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_conv_wgrad(WgradParams p) {
+  static_assert(!PRO || (F32 && !C4 && !D3 && !AT), "BN prologue on X: fp32 8-channel chunks only");
   static_assert(!(F32 && (D3 || AT)), "fp32 operands: 2-D, 8-channel (or C4) chunks, no BN prologue");
   static_assert(!(PW1 && (C4 || D3)), "pointwise gather: 2-D, 8-channel chunks");
   static_assert(!(C4 && D3), "3-D wgrad gathers 8-channel chunks");
@@ -145,6 +150,14 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
   if (sx1 == p.S) { sx1 = 0; ++rx1; }
   const int ndy = n0 + dy_col * 8;
   const bool ndy_ok = ndy < p.K;
+  float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];  // PRO: this thread's X̂ column channels cx .. cx + 7
+  if constexpr (PRO) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      psc[e] = kx_ok ? p.pro[cx + e] : 0.f;
+      psh[e] = kx_ok ? p.pro[p.C + cx + e] : 0.f;
+    }
+  }
 
   // Raw buffer loads (OOB offsets → zeros, no branches) into two register sets; tile t+2 is
   // requested while tile t is multiplied (loads always issued — beyond the range with a dead
@@ -167,8 +180,10 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
     }
   }
 
-  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH * PC], uint4 (&rx_)[X_CH * PC], uint4 (&r2)[AT ? DY_CH : 1]) {
+  auto load = [&](int mt, bool live, uint4 (&rdy)[DY_CH * PC], uint4 (&rx_)[X_CH * PC], uint4 (&r2)[AT ? DY_CH : 1],
+                  uint32_t& okm) {
     const uint32_t dead = live ? 0u : DEAD;
+    okm = 0;
 #pragma unroll
     for (int i = 0; i < DY_CH; ++i) {
       const int m = mt + dy_row0 + i * DY_RSTEP;
@@ -183,6 +198,7 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
       for (int i = 0; i < X_CH; ++i) {
         const int m = mt + x_row0 + i * X_RSTEP;
         const bool ok = kx_ok && m < mend;
+        if (PRO && ok) okm |= 1u << i;
         const uint32_t off = (ok ? ((uint32_t)m * (uint32_t)p.ldx + (uint32_t)cx) * (uint32_t)ES : DEAD) | dead;
         rx_[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
         if constexpr (F32) rx_[PC * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, 0, 0));
@@ -222,6 +238,7 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
           rx_[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
         }
       } else {
+        if (PRO && ok) okm |= 1u << i;
         const uint32_t off = (ok ? ((uint32_t)((n * p.H + h) * p.W + w) * (uint32_t)p.ldx + (uint32_t)cx) * (uint32_t)ES : DEAD) | dead;
         rx_[PC * i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
         if constexpr (F32) rx_[PC * i + 1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, 0, 0));
@@ -242,8 +259,17 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
     h = make_uint4(hw[0], hw[1], hw[2], hw[3]);
     l = make_uint4(lw[0], lw[1], lw[2], lw[3]);
   };
+  // PRO: relu(x·sc + sh) of a loaded 8-channel chunk (two 16-B pieces), 0 for a padded / dead row
+  auto pro8 = [&](uint4& a, uint4& b, bool ok) {
+    uint32_t u[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      u[e] = ok ? __float_as_uint(fmaxf(fmaf(__uint_as_float(u[e]), psc[e], psh[e]), 0.f)) : 0u;
+    a = make_uint4(u[0], u[1], u[2], u[3]);
+    b = make_uint4(u[4], u[5], u[6], u[7]);
+  };
   auto store = [&](int buf, int mt, const uint4 (&rdy)[DY_CH * PC], const uint4 (&rx_)[X_CH * PC],
-                   const uint4 (&r2)[AT ? DY_CH : 1]) {
+                   const uint4 (&r2)[AT ? DY_CH : 1], uint32_t okm) {
     if constexpr (F32) {
 #pragma unroll
       for (int i = 0; i < DY_CH; ++i) {
@@ -257,7 +283,13 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
       for (int i = 0; i < X_CH; ++i) {
         const int row = x_row0 + i * X_RSTEP;
         uint4 h, l;
-        split8(rx_[2 * i], rx_[2 * i + 1], h, l);
+        if constexpr (PRO) {
+          uint4 a = rx_[2 * i], b = rx_[2 * i + 1];
+          pro8(a, b, (okm >> i) & 1u);
+          split8(a, b, h, l);
+        } else {
+          split8(rx_[2 * i], rx_[2 * i + 1], h, l);
+        }
         *reinterpret_cast<uint4*>(&lds[buf][DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = h;
         *reinterpret_cast<uint4*>(&lds[buf][LO + DY_WORDS + tr_swz_dword<TILE_K>(row, x_col * 4)]) = l;
       }
@@ -350,20 +382,21 @@ __global__ void __launch_bounds__(256, BPT == 32 && !AT ? (F32 ? 2 : 3) : 2) k_c
 
   uint4 dy0[DY_CH * PC], x0[X_CH * PC], dy1[DY_CH * PC], x1[X_CH * PC];
   uint4 z0[AT ? DY_CH : 1], z1[AT ? DY_CH : 1];
+  uint32_t ok0 = 0, ok1 = 0;
   const int NT = (mend - mbeg + BPT - 1) / BPT;
-  load(mbeg, true, dy0, x0, z0);
-  load(mbeg + BPT, NT > 1, dy1, x1, z1);
-  store(0, mbeg, dy0, x0, z0);
+  load(mbeg, true, dy0, x0, z0, ok0);
+  load(mbeg + BPT, NT > 1, dy1, x1, z1, ok1);
+  store(0, mbeg, dy0, x0, z0, ok0);
   __syncthreads();
   int it = 0;
   for (; it + 2 <= NT; it += 2) {
-    load(mbeg + (it + 2) * BPT, it + 2 < NT, dy0, x0, z0);
+    load(mbeg + (it + 2) * BPT, it + 2 < NT, dy0, x0, z0, ok0);
     compute(0);
-    store(1, mbeg + (it + 1) * BPT, dy1, x1, z1);
+    store(1, mbeg + (it + 1) * BPT, dy1, x1, z1, ok1);
     __syncthreads();
-    load(mbeg + (it + 3) * BPT, it + 3 < NT, dy1, x1, z1);
+    load(mbeg + (it + 3) * BPT, it + 3 < NT, dy1, x1, z1, ok1);
     compute(1);
-    if (it + 2 < NT) store(0, mbeg + (it + 2) * BPT, dy0, x0, z0);
+    if (it + 2 < NT) store(0, mbeg + (it + 2) * BPT, dy0, x0, z0, ok0);
     __syncthreads();
   }
   if (it < NT) {
@@ -604,10 +637,11 @@ BIGDL_EXPORT int bigdl_conv_wgrad_grouped(const void* x, const void* dy, float* 
 // C % 8 == 0, K % 8 == 0); dw [K][R][S][C] fp32 += scale · Σ dyᵀ·x̂ at bf16x3 accuracy in ONE launch.
 // Pixel depth 32 per k-tile (the hi + lo tiles double the LDS image).  splits <= 0: heuristic.
 // C == 4 (the padded RGB stem, x [Nb][H][W][4]): the C4 gather, an 8-index chunk = two taps × 4 channels.
-BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw, float scale, int Nb, int H, int W,
-                                      int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh,
-                                      int dwd, int splits, hipStream_t s) {
+static int wgrad_f32_impl(const float* x, const float* dy, float* dw, float scale, int Nb, int H, int W, int C, int K,
+                          int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dwd, int splits,
+                          hipStream_t s, const float* pro) {
   const bool c4 = C == 4;
+  if (pro && (c4 || C % 8 || ((uintptr_t)pro & 15))) return (int)hipErrorInvalidValue;
   if ((C % 8 && !c4) || K % 8 || Nb <= 0 || !x || !dy || !dw) return (int)hipErrorInvalidValue;
   if (c4 && (dh != 1 || dwd != 1)) return (int)hipErrorInvalidValue;
   if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15)) return (int)hipErrorInvalidValue;
@@ -631,6 +665,7 @@ BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw
   p.fPQ = make_fastdiv((uint32_t)(P * Q));
   p.fQ = make_fastdiv((uint32_t)Q);
   p.pw1 = (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && P == H && Q == W && !c4) ? 1 : 0;
+  p.pro = pro;
   const int TN = K <= 64 ? 64 : 128;
   const int TK = (p.Kg <= 64 && !c4) ? 64 : 128;
   p.tiles_n = (K + TN - 1) / TN;
@@ -652,7 +687,21 @@ BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw
   const dim3 grid(tiles, splits, 1);
 #define BIGDL_WF32(TN_, TK_, PW_) \
   hipLaunchKernelGGL((k_conv_wgrad<TN_, TK_, 32, false, false, false, PW_, true>), grid, dim3(256), 0, s, p)
-  if (c4) {
+#define BIGDL_WF32P(TN_, TK_, PW_) \
+  hipLaunchKernelGGL((k_conv_wgrad<TN_, TK_, 32, false, false, false, PW_, true, true>), grid, dim3(256), 0, s, p)
+  if (pro) {
+    if (p.pw1) {
+      if (TN == 64 && TK == 64) BIGDL_WF32P(64, 64, true);
+      else if (TN == 64) BIGDL_WF32P(64, 128, true);
+      else if (TK == 64) BIGDL_WF32P(128, 64, true);
+      else BIGDL_WF32P(128, 128, true);
+    } else {
+      if (TN == 64 && TK == 64) BIGDL_WF32P(64, 64, false);
+      else if (TN == 64) BIGDL_WF32P(64, 128, false);
+      else if (TK == 64) BIGDL_WF32P(128, 64, false);
+      else BIGDL_WF32P(128, 128, false);
+    }
+  } else if (c4) {
     if (TN == 64) hipLaunchKernelGGL((k_conv_wgrad<64, 128, 32, true, false, false, false, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((k_conv_wgrad<128, 128, 32, true, false, false, false, true>), grid, dim3(256), 0, s, p);
   } else if (p.pw1) {
@@ -667,5 +716,21 @@ BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw
     else BIGDL_WF32(128, 128, false);
   }
 #undef BIGDL_WF32
+#undef BIGDL_WF32P
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_wgrad_f32(const float* x, const float* dy, float* dw, float scale, int Nb, int H, int W,
+                                      int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh,
+                                      int dwd, int splits, hipStream_t s) {
+  return wgrad_f32_impl(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, nullptr);
+}
+
+// bigdl_conv_wgrad_f32 whose x is the INPUT of a training BN + ReLU (its output deferred): X̂ =
+// relu(x·pro[c] + pro[C + c]) on load, pro = [scale | shift] [2][C].
+BIGDL_EXPORT int bigdl_conv_wgrad_f32_pro(const float* x, const float* pro, const float* dy, float* dw, float scale,
+                                          int Nb, int H, int W, int C, int K, int R, int S, int P, int Q, int sh,
+                                          int sw, int ph, int pw, int dh, int dwd, int splits, hipStream_t s) {
+  if (!pro) return (int)hipErrorInvalidValue;
+  return wgrad_f32_impl(x, dy, dw, scale, Nb, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dwd, splits, s, pro);
 }

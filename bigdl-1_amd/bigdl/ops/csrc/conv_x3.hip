@@ -84,7 +84,24 @@ struct X3Params {
   int res_sh, res_sw, res_H, res_W;
   // measurement knob (BIGDL_X3_DEBUG, read per launch): bit 0 = skip the output stores (leaves y WRONG)
   int dbg;
+  // B-operand prologue (PRO instantiations): x is the INPUT of a training BN + ReLU whose output this
+  // conv consumes; the conv reads relu(x·pro[c] + pro[C + c]) (padded taps stay 0), so the BN output is
+  // never written (C ≤ X3_PRO_MAXC)
+  const float* pro;
 };
+
+constexpr int X3_PRO_MAXC = 512;
+
+// y = relu(x·sc + sh) of 8 consecutive channels (or 0 for a padded tap)
+__device__ __forceinline__ void x3_pro8(v4f& a, v4f& b, const float* sc, const float* sh, bool valid) {
+  const v4f s0 = *reinterpret_cast<const v4f*>(sc), s1 = *reinterpret_cast<const v4f*>(sc + 4);
+  const v4f h0 = *reinterpret_cast<const v4f*>(sh), h1 = *reinterpret_cast<const v4f*>(sh + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = valid ? fmaxf(fmaf(a[e], s0[e], h0[e]), 0.f) : 0.f;
+    b[e] = valid ? fmaxf(fmaf(b[e], s1[e], h1[e]), 0.f) : 0.f;
+  }
+}
 
 // One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds): lane l's 16 bytes land at lds + 16·l.
 // (A non-template function: inside the kernel template the builtin fails host-side substitution.)
@@ -125,8 +142,9 @@ __device__ __forceinline__ float x3_row_fold(float v) {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int NS>
+template <int BM, int BN, int WM, int WN, int MODE, int NS, bool PRO = false>
 __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) k_conv_x3(X3Params p) {
+  static_assert(!PRO || MODE != 2, "the BN prologue reads a BN output: never the RGB stem");
   static_assert(MODE == 1 || MODE == 2 || MODE == 3, "tap-uniform / C4 / pointwise gathers only");
   constexpr bool C4 = MODE == 2;
   static_assert(NS == 2 || NS == 3, "LDS ring depth");
@@ -144,6 +162,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
   constexpr int EPI = BM * BN * 4 + 2 * RPP * BN * 4;
   constexpr int LDS_BYTES = NS * STAGE > EPI ? NS * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 2 * X3_PRO_MAXC : 4];  // [scale | shift]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -151,6 +170,12 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
   const int tile = x3_xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  if constexpr (PRO) {  // visible after the main loop's first barrier
+    for (int i = tid; i < p.C; i += NT) {
+      pro_s[i] = p.pro[i];
+      pro_s[X3_PRO_MAXC + i] = p.pro[p.C + i];
+    }
+  }
 
   const uint32_t x_bytes = (uint32_t)((size_t)p.Nb * p.H * p.W * p.ldx * 4);
   const uint32_t w_bytes = (uint32_t)((size_t)p.K * p.Kg * 4);  // 2 bf16 parts per index
@@ -292,6 +317,32 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
     fb1[kk] = frow * 128 + (((4 * kk + 2 * fh + 1) ^ swz) << 4);
   }
   const int a_row0 = wave_n * (BN / WN), b_row0 = BN + wave_m * (BM / WM);
+  // PRO, tap-uniform mode: which taps of this lane's B-fragment rows (pixels) are inside the image
+  uint64_t fmask[PRO ? TMI : 1];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < TMI; ++j) {
+      uint64_t msk = ~0ull;
+      const int m = m0 + (b_row0 - BN) + 32 * j + frow;
+      if (!PW && m < p.M) {
+        msk = 0;
+        const int n = m / (p.P * p.Q);
+        const int pq = m - n * p.P * p.Q;
+        const int pp = pq / p.Q, qq = pq - pp * p.Q;
+        const int h = pp * p.sh - p.ph, w = qq * p.sw - p.pw;
+        for (int r = 0; r < p.R; ++r) {
+          const int hh = h + r * p.dh;
+          if ((unsigned)hh >= (unsigned)p.H) continue;
+          for (int sx = 0; sx < p.S; ++sx) {
+            const int ww = w + sx * p.dw;
+            if ((unsigned)ww < (unsigned)p.W) msk |= 1ull << (r * p.S + sx);
+          }
+        }
+      }
+      fmask[j] = msk;
+    }
+  }
+  int pc_c0 = 0, pc_tap = 0;  // PRO: channel offset / tap of the k-tile compute() multiplies next
 
   constexpr int PPK = (L + 1) / 2;  // DMA pieces of the next stage per slice
   auto compute = [&](int slotbuf, int nslot, auto issue_on) {
@@ -309,6 +360,19 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
       for (int j = 0; j < TMI; ++j) {
         b0[kk][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb0[kk]);
         b1[kk][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[kk]);
+      }
+    }
+    if constexpr (PRO) {  // the deferred BN + ReLU of the input, before the split
+      const float* scp = pro_s + pc_c0 + 8 * fh;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < TMI; ++j)
+          x3_pro8(b0[kk][j], b1[kk][j], scp + 16 * kk, scp + X3_PRO_MAXC + 16 * kk, (fmask[j] >> pc_tap) & 1ull);
+      pc_c0 += BK;
+      if (pc_c0 == p.C) {
+        pc_c0 = 0;
+        ++pc_tap;
       }
     }
     // slice 0's B split is exposed; slice 1's is issued right after slice 0's MFMAs so it overlaps
@@ -516,22 +580,22 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
 // wave layout `wl`: 0 = the 2-D split (WM × WN = 4 × 2 / 2 × 2), 1 = waves over pixels only (8 × 1 /
 // 4 × 1): each wave's split B fragment then feeds all BN / 32 channel blocks (half the split VALU per MFMA).
 // ns2: the 2-deep ring (two 128 × 128 or three 128 × 64 blocks share a CU).
-template <int MODE>
+template <int MODE, bool PRO = false>
 static void launch_x3(int bm, int bn, int wl, int ns2, dim3 g, hipStream_t s, const X3Params& p) {
   if (bm == 128 && bn == 64) {
-    hipLaunchKernelGGL((k_conv_x3<128, 64, 4, 1, MODE, 2>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((k_conv_x3<128, 64, 4, 1, MODE, 2, PRO>), g, dim3(256), 0, s, p);
   } else if (bm == 128 && ns2) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 2>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 2>), g, dim3(256), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 2, PRO>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 2, PRO>), g, dim3(256), 0, s, p);
   } else if (bm == 128) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 3>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 3>), g, dim3(256), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<128, 128, 4, 1, MODE, 3, PRO>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<128, 128, 2, 2, MODE, 3, PRO>), g, dim3(256), 0, s, p);
   } else if (bn == 64) {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 64, 8, 1, MODE, 3>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, 3>), g, dim3(512), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 64, 8, 1, MODE, 3, PRO>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 64, 4, 2, MODE, 3, PRO>), g, dim3(512), 0, s, p);
   } else {
-    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 128, 8, 1, MODE, 3>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, 3>), g, dim3(512), 0, s, p);
+    if (wl) hipLaunchKernelGGL((k_conv_x3<256, 128, 8, 1, MODE, 3, PRO>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_x3<256, 128, 4, 2, MODE, 3, PRO>), g, dim3(512), 0, s, p);
   }
 }
 
@@ -548,13 +612,15 @@ static int x3_env_tile() {
 // [K·R·S·C / 32][32] view), K % 8 == 0 for statistics / bnbwd (else K % 4).  bm / bn: the tile
 // (256 × 128, 256 × 64 or 128 × 128; 0 = heuristic).  osh … oW: the output scatter (1, 1, 0, 0, P, Q =
 // none); res_sh … res_W: the strided residual (0 = dense); persist: unused (ABI).  Returns hipError_t.
-BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias, const float* res, float* y,
-                               float* stats, int R_rep, const float* shift, const float* bnx, const float* mean,
-                               const void* bits, const float* bsc, const float* bsh, int Nb, int H, int W, int C,
-                               int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
-                               int relu, int ldy, int bm, int bn, int osh, int osw, int ooh, int oow, int oH,
-                               int oW, int res_sh, int res_sw, int res_H, int res_W, int persist, hipStream_t s) {
+static int conv_x3_impl(const float* x, const void* w2, const float* bias, const float* res, float* y,
+                        float* stats, int R_rep, const float* shift, const float* bnx, const float* mean,
+                        const void* bits, const float* bsc, const float* bsh, int Nb, int H, int W, int C,
+                        int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                        int relu, int ldy, int bm, int bn, int osh, int osw, int ooh, int oow, int oH,
+                        int oW, int res_sh, int res_sw, int res_H, int res_W, int persist, hipStream_t s,
+                        const float* pro) {
   const bool c4 = C == 4;  // the padded RGB stem: x [Nb][H][W][4]
+  if (pro && (c4 || C > X3_PRO_MAXC || ((uintptr_t)pro & 15) || C % 32)) return (int)hipErrorInvalidValue;
   if (!x || !w2 || !y || Nb <= 0 || C <= 0 || K <= 0 || P <= 0 || Q <= 0 || (C % 32 && !c4) || K % 4 || ldy < K ||
       ldy % 4)
     return (int)hipErrorInvalidValue;
@@ -581,6 +647,7 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   p.M = (int)Ml; p.Kg = c4 ? (R * S + 7) / 8 * 32 : R * S * C; p.ldx = C; p.ldy = ldy; p.relu = relu;
   p.stats = stats; p.R_rep = stats ? R_rep : 1; p.shift = bnx ? nullptr : shift;
   p.bnx = bnx; p.mean = mean; p.bits = (const uint8_t*)bits; p.bsc = bsc; p.bsh = bsh;
+  p.pro = pro;
   if (osh <= 0 || osw <= 0 || ooh < 0 || oow < 0) return (int)hipErrorInvalidValue;
   p.scatter = (osh != 1 || osw != 1 || ooh != 0 || oow != 0 || oH != P || oW != Q) ? 1 : 0;
   p.osh = osh; p.osw = osw; p.ooh = ooh; p.oow = oow; p.oH = oH; p.oW = oW;
@@ -628,7 +695,33 @@ BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   (void)persist;  // (a persistent tile-stream variant measured no gain: removed)
   if (c4) launch_x3<2>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
+  else if (pro && pw1) launch_x3<3, true>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
+  else if (pro) launch_x3<1, true>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   else if (pw1) launch_x3<3>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   else launch_x3<1>(bm, bn, wl, ns2, dim3((unsigned)tiles), s, p);
   BIGDL_CHECK_LAUNCH();
+}
+
+BIGDL_EXPORT int bigdl_conv_x3(const float* x, const void* w2, const float* bias, const float* res, float* y,
+                               float* stats, int R_rep, const float* shift, const float* bnx, const float* mean,
+                               const void* bits, const float* bsc, const float* bsh, int Nb, int H, int W, int C,
+                               int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw,
+                               int relu, int ldy, int bm, int bn, int osh, int osw, int ooh, int oow, int oH,
+                               int oW, int res_sh, int res_sw, int res_H, int res_W, int persist, hipStream_t s) {
+  return conv_x3_impl(x, w2, bias, res, y, stats, R_rep, shift, bnx, mean, bits, bsc, bsh, Nb, H, W, C, K, R, S, P, Q,
+                      sh, sw, ph, pw, dh, dw, relu, ldy, bm, bn, osh, osw, ooh, oow, oH, oW, res_sh, res_sw, res_H,
+                      res_W, persist, s, nullptr);
+}
+
+// bigdl_conv_x3 whose input x is the INPUT of a training BN + ReLU (the deferred BN output): the conv
+// reads relu(x·pro[c] + pro[C + c]), pro = the BN's [scale | shift] (C % 32 == 0, C ≤ 512).
+BIGDL_EXPORT int bigdl_conv_x3_pro(const float* x, const void* w2, const float* pro, const float* bias,
+                                   const float* res, float* y, float* stats, int R_rep, const float* shift,
+                                   const float* bnx, const float* mean, const void* bits, const float* bsc,
+                                   const float* bsh, int Nb, int H, int W, int C, int K, int R, int S, int P, int Q,
+                                   int sh, int sw, int ph, int pw, int dh, int dw, int relu, int ldy, int bm, int bn,
+                                   int osh, int osw, int ooh, int oow, int oH, int oW, hipStream_t s) {
+  if (!pro) return (int)hipErrorInvalidValue;
+  return conv_x3_impl(x, w2, bias, res, y, stats, R_rep, shift, bnx, mean, bits, bsc, bsh, Nb, H, W, C, K, R, S, P, Q,
+                      sh, sw, ph, pw, dh, dw, relu, ldy, bm, bn, osh, osw, ooh, oow, oH, oW, 0, 0, 0, 0, 0, s, pro);
 }

@@ -344,13 +344,22 @@ def _wprep(w, form):
 
 def _x3(x, w2, y, nb, h, w, c, k, r, s, p, q, stride, pad, dil, bias=None, res=None, relu=False, stats=None, rep=0,
         shift=None, bnx=None, mean=None, bits=None, bsc=None, bsh=None, scatter=None, res_strided=None, tile=None,
-        persist=0):
+        persist=0, pro=None):
     """One conv_x3 launch (csrc/conv_x3.hip); ``scatter`` = (osh, osw, ooh, oow, oH, oW) of a
-    sub-pixel dgrad, ``res_strided`` = (res_sh, res_sw, res_H, res_W) of a compact residual."""
+    sub-pixel dgrad, ``res_strided`` = (res_sh, res_sw, res_H, res_W) of a compact residual; ``pro``
+    (fp32 [2·C] scale | shift): ``x`` is the input of a training BN + ReLU and the conv reads
+    relu(x·scale + shift) — the deferred BN output (bigdl.fp32.bnPrologue)."""
     osh, osw, ooh, oow, oh_, ow_ = scatter if scatter is not None else (1, 1, 0, 0, p, q)
     rsh, rsw, rh, rw = res_strided if res_strided is not None else (0, 0, 0, 0)
 
     def launch(t, st):
+        if pro is not None:
+            check(N.lib().bigdl_conv_x3_pro(ptr(x), ptr(w2), ptr(pro), ptr(bias), ptr(res), ptr(y), ptr(st), rep,
+                                            ptr(shift), ptr(bnx), ptr(mean), ptr(bits), ptr(bsc), ptr(bsh), nb, h, w,
+                                            c, k, r, s, p, q, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1],
+                                            int(bool(relu)), k, t[0], t[1], osh, osw, ooh, oow, oh_, ow_, _s()),
+                  "conv_x3_pro")
+            return
         check(N.lib().bigdl_conv_x3(ptr(x), ptr(w2), ptr(bias), ptr(res), ptr(y), ptr(st), rep, ptr(shift), ptr(bnx),
                                     ptr(mean), ptr(bits), ptr(bsc), ptr(bsh), nb, h, w, c, k, r, s, p, q, stride[0],
                                     stride[1], pad[0], pad[1], dil[0], dil[1], int(bool(relu)), k, t[0], t[1], osh,
@@ -361,7 +370,7 @@ def _x3(x, w2, y, nb, h, w, c, k, r, s, p, q, stride, pad, dil, bias=None, res=N
     # the kernel-selection table (training / inference compile phase): candidates per launch geometry
     from .native_ops import _tiled_launch, _stat_target
     key = ("x3", nb, h, w, c, k, r, s, p, q, tuple(stride), tuple(pad), scatter is not None, stats is not None,
-           bnx is not None)
+           bnx is not None) + (("pro",) if pro is not None else ())
 
     def fn(t):
         t = (0, 0) if len(t) != 2 else t  # (0, 0, 0): no entry → the launcher's heuristic
@@ -534,12 +543,24 @@ def _stem_wgrad(x, gy, gw_acc, scale, stride, pad, slot):
 _S2D_ACC: dict = {}
 
 
-def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None, slot=None):
+def pro_ok(x, coef) -> bool:
+    """A deferred BN + ReLU output (input ``x``, fp32 [scale | shift] ``coef``) can be consumed by the
+    direct kernels' operand prologues (conv_x3 PRO, conv_wgrad F32 PRO)."""
+    c = x.shape[1] if x.dim() == 4 else 0
+    return (x.dim() == 4 and _cl_f32(x) and c % 32 == 0 and c <= 512 and isinstance(coef, torch.Tensor)
+            and coef.dtype == _f32 and coef.numel() == 2 * c and coef.is_contiguous() and coef.data_ptr() % 16 == 0
+            and _direct() and _x3_has() and hasattr(N.lib(), "bigdl_conv_x3_pro")
+            and hasattr(N.lib(), "bigdl_conv_wgrad_f32_pro"))
+
+
+def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, shift=None, slot=None, pro=None):
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
-    if _stem_ok(c, k, stride, dilation, r, s) and x.dtype == _f32:
+    if pro is None and _stem_ok(c, k, stride, dilation, r, s) and x.dtype == _f32:
         return _stem_forward(x, w4, b, stride, pad, relu, stats, rep, shift, slot)
     if not (_direct() and _x3_has() and _x3_geom_ok(c, k, r, s, pad) and _cl_f32(x)):
+        return NotImplemented
+    if pro is not None and (not pro_ok(x, pro) or tuple(dilation) != (1, 1)):
         return NotImplemented
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
     if p <= 0 or q <= 0 or not _fits(nb * h * w * c * 4, k * r * s * c * 4):
@@ -547,7 +568,7 @@ def _direct_forward(x, w4, b, stride, pad, dilation, relu, stats=None, rep=0, sh
     y = torch.empty((nb, k, p, q), dtype=_f32, device=x.device, memory_format=_cl)
     bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
     _x3(x, _w_fwd(w4), y, nb, h, w, c, k, r, s, p, q, stride, pad, dilation, bias=bias, relu=relu, stats=stats,
-        rep=rep, shift=shift)
+        rep=rep, shift=shift, pro=pro)
     return y
 
 
@@ -599,14 +620,15 @@ def _slot_key(x, cp, two):
     return ("bf16x3", x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), cp, two)
 
 
-def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, slot=None):
+def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, slot=None, pro=None):
     """fp32 NCHW-logical conv (any memory format in, channels-last fp32 out).  ``slot`` (the layer's
     one-entry holder, passed while training): keeps the input split for the weight gradient of the
-    same input, which then skips its own split of x."""
+    same input, which then skips its own split of x.  ``pro``: x is a deferred BN + ReLU output's
+    input (see :func:`_x3`); NotImplemented when the direct kernels cannot take it."""
     if groups != 1 or x.dim() != 4 or w4.dim() != 4 or w4.shape[1] != x.shape[1]:
         return NotImplemented
-    y = _direct_forward(x, w4, b, stride, pad, dilation, relu, slot=slot)
-    if y is not NotImplemented:
+    y = _direct_forward(x, w4, b, stride, pad, dilation, relu, slot=slot, pro=pro)
+    if y is not NotImplemented or pro is not None:
         return y
     nb, c, h, w = x.shape
     k, _, r, s = w4.shape
@@ -635,7 +657,7 @@ def conv_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, s
     return y
 
 
-def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
+def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None, pro=None):
     """fp32 conv (no bias / ReLU) whose epilogue also ADDS the following BN's statistics
     Σ(y − shift), Σ(y − shift)² into the BN's replicated buffer ``sums = (buf [2][R][K], R)``: returns
     ``(y, buf, R)`` for ``batchnorm_forward_train_partials`` (which finalizes from the R rows and clears
@@ -649,9 +671,12 @@ def conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=None):
     if (k % 8 or shift is None or shift.dtype != _f32 or shift.numel() != k or not shift.is_contiguous()
             or buf.dtype != _f32 or buf.numel() != 2 * rep * k or not 1 <= rep <= 512):
         return NotImplemented
-    y = _direct_forward(x, w4, None, stride, pad, dilation, False, stats=buf, rep=rep, shift=shift, slot=slot)
+    y = _direct_forward(x, w4, None, stride, pad, dilation, False, stats=buf, rep=rep, shift=shift, slot=slot,
+                        pro=pro)
     if y is not NotImplemented:
         return y, buf, rep
+    if pro is not None:
+        return NotImplemented
     p, q = _out_hw(h, w, r, s, stride, pad, dilation)
     cp = _r(c, 8)
     if p <= 0 or q <= 0 or not _fits(nb * h * w * 2 * cp * 2, k * r * s * 3 * cp * 2):
@@ -802,24 +827,31 @@ def bias_grad_acc(gy, gb_acc, scale):
     gb_acc.add_(gy.sum((0, 2, 3)).reshape(gb_acc.shape), alpha=scale)
 
 
-def _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation):
+def _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation, pro=None):
     nb, c, h, w = x.shape
     k, _, r, s = gw_acc.shape
     p, q = gy.shape[2], gy.shape[3]
-    if not _direct_wgrad_ok(x, gy, gw_acc):
+    if not _direct_wgrad_ok(x, gy, gw_acc) or (pro is not None and not pro_ok(x, pro)):
         return NotImplemented
     def fn(t):
         # t = (splits,): 0 = the launcher's heuristic (≈512 blocks), < 0 = -target block count
+        sp = t[0] if len(t) == 1 else 0
+        if pro is not None:
+            check(N.lib().bigdl_conv_wgrad_f32_pro(ptr(x), ptr(pro), ptr(gy), ptr(gw_acc), C.c_float(float(scale)), nb,
+                                                   h, w, c, k, r, s, p, q, stride[0], stride[1], pad[0], pad[1],
+                                                   dilation[0], dilation[1], sp, _s()), "conv_wgrad_f32_pro")
+            return
         check(N.lib().bigdl_conv_wgrad_f32(ptr(x), ptr(gy), ptr(gw_acc), C.c_float(float(scale)), nb, h, w, c, k, r,
                                            s, p, q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
-                                           t[0] if len(t) == 1 else 0, _s()), "conv_wgrad_f32")
+                                           sp, _s()), "conv_wgrad_f32")
     from .native_ops import _tiled_launch
-    _tiled_launch(("wg32", nb, h, w, c, k, r, s, p, q, tuple(stride), tuple(pad)), fn)
+    _tiled_launch(("wg32", nb, h, w, c, k, r, s, p, q, tuple(stride), tuple(pad))
+                  + (("pro",) if pro is not None else ()), fn)
     return None
 
 
 def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                  scale=1.0, residual=None, slot=None, bn_fuse=None, lazy_strided=False):
+                  scale=1.0, residual=None, slot=None, bn_fuse=None, lazy_strided=False, pro=None):
     """Data gradient (fp32, channels-last) and fp32 weight / bias gradient accumulation.  ``bn_fuse``
     (conv.py: the BN + ReLU whose output this conv consumed): the data gradient's epilogue stores the
     ReLU-masked gradient and adds that BN's backward statistics into its replicated buffer, reported
@@ -828,7 +860,14 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
     its input gradient as a StridedGrad."""
     if groups != 1 or x.dim() != 4 or gy.dim() != 4 or gy.dtype != _f32:
         return NotImplemented
-    if (not need_input and gw_acc is not None
+    if pro is not None:
+        # x is a deferred BN + ReLU output's input: only the weight gradient reads x (through the F32
+        # prologue); the data gradient never does
+        if not (_direct() and _x3_has() and _cl_f32(gy) and pro_ok(x, pro)):
+            return NotImplemented
+        if gw_acc is not None and scale != 0 and not _direct_wgrad_ok(x, gy, gw_acc):
+            return NotImplemented
+    if (pro is None and not need_input and gw_acc is not None
             and _stem_ok(x.shape[1], w4.shape[0], stride, dilation, w4.shape[2], w4.shape[3])
             and _cl_f32(gy) and x.dtype == _f32 and gw_acc.dtype == _f32):
         if scale != 0:
@@ -857,21 +896,28 @@ def conv_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=
             side = _wgrad_side_stream(gy)
             if side is not None:
                 with torch.cuda.stream(side):
-                    _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation)
+                    _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation, pro=pro)
                     if gb_acc is not None:
                         bias_grad_acc(gy, gb_acc, scale)
-                for t in (x, gy):
+                for t in (x, gy) + ((pro,) if pro is not None else ()):
                     t.record_stream(side)
                 wg_done = True
         gi = None
         if need_input:
             gi = _direct_dgrad(gy, w4, tuple(x.shape), stride, pad, dilation, residual, bn_fuse, lazy_strided)
             if gi is NotImplemented:
-                gi = _split_backward(gy, x, w4, stride, pad, dilation, True, None, scale, slot, residual, bn_fuse)
+                if pro is not None:
+                    # (the split path's dgrad never reads x: it only needs x's shape)
+                    gi = _split_backward(gy, x, w4, stride, pad, dilation, True, None, scale, None, residual,
+                                         bn_fuse)
+                else:
+                    gi = _split_backward(gy, x, w4, stride, pad, dilation, True, None, scale, slot, residual, bn_fuse)
                 if gi is NotImplemented:
                     return NotImplemented
         if gw_acc is not None and scale != 0 and not wg_done:
-            if _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation) is NotImplemented:
+            if _direct_wgrad(x, gy, gw_acc, scale, stride, pad, dilation, pro=pro) is NotImplemented:
+                if pro is not None:
+                    raise RuntimeError("fp32 BN prologue: the weight gradient lost its direct kernel mid-call")
                 r = _split_backward(gy, x, w4, stride, pad, dilation, False, gw_acc, scale, slot)
                 if r is NotImplemented:
                     return NotImplemented

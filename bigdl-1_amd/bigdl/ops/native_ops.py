@@ -205,6 +205,20 @@ def batchnorm_forward_train_partials(x, partial, G, gamma, beta, running_mean, r
         return NotImplemented
     M, C_ = rc
     deferred = isinstance(residual, R_.BNOut)
+    if (not apply and not deferred and residual is None and rezero and 1 <= G <= 512 and _bn32_ok(x, C_, None)
+            and partial is not None and partial.dtype == _f32 and partial.numel() == 2 * G * C_
+            and _f32vec(shift, C_) and _coef_ok(coef_out, C_)
+            and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias))):
+        # fp32 compute, finalize only: the consuming conv applies BN + ReLU in its operand prologues
+        # (bigdl.fp32.bnPrologue), so the BN output is never written
+        mean = torch.empty(C_, dtype=_f32, device=x.device)
+        invstd = torch.empty(C_, dtype=_f32, device=x.device)
+        check(_lib().bigdl_bn32_fwd_train_partials(ptr(x), None, None, _ll(M), C.c_int(C_), ptr(gamma), ptr(beta),
+                                                   ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum),
+                                                   _f(eps), ptr(mean), ptr(invstd), ptr(partial), C.c_int(G),
+                                                   ptr(shift), ptr(coef_out), C.c_int(1 if relu else 0), None, None,
+                                                   _s()), "bn32_fwd_train_partials(finalize)")
+        return None, mean, invstd
     if deferred or not apply:
         # the bf16 replicated / partial-rows path only (the fused block tail of the training step)
         if not (_bn_ok(x, C_) and all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias))
@@ -999,7 +1013,15 @@ def conv2d_forward_q(x, w4, b, stride, pad, relu, q_scale, u8=False, pad_slot=No
 
 
 @register("conv2d_forward")
-def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None):
+def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False, out=None, res=None, pad_slot=None,
+                   pro=None):
+    """``pro`` (fp32 compute): ``x`` is the INPUT of a training BN + ReLU whose deferred output this conv
+    consumes, ``pro`` that BN's [scale | shift] — the direct fp32 kernels apply it on load
+    (NotImplemented when they cannot: the caller then materialises the BN output)."""
+    if pro is not None:
+        if x.dtype != _f32 or res is not None or out is not None or not F3.enabled(x):
+            return NotImplemented
+        return F3.conv_forward(x, w4, b, stride, pad, dilation, groups, relu, slot=pad_slot, pro=pro)
     if x.dtype == _f32 and res is None and out is None and F3.enabled(x):
         r = F3.conv_forward(x, w4, b, stride, pad, dilation, groups, relu, slot=pad_slot)
         if r is not NotImplemented:
@@ -1009,7 +1031,8 @@ def conv2d_forward(x, w4, b, stride, pad, dilation=(1, 1), groups=1, relu=False,
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, res=res, relu=relu, out=out, pad_slot=pad_slot)
 
 
-def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None, shift=None, sums=None):
+def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_slot=None, shift=None, sums=None,
+                         pro=None):
     """Forward conv whose epilogue also emits per-row-tile Σ(y−K)/Σ(y−K)² partials for a following
     BN (128-row tiles; the BN finalize combines them in fp64).  ``shift`` (fp32 [K], e.g. the BN's
     running mean) is K; the same array must reach the finalize.  ``sums`` (fp32 [2K + 1], zero): the
@@ -1018,7 +1041,9 @@ def conv2d_forward_stats(x, w4, b, stride, pad, dilation=(1, 1), groups=1, pad_s
     if x.dtype == _f32 and F3.enabled(x):  # fp32 compute: the bf16x3 conv's fp32 epilogue (replicas only)
         if groups != 1 or b is not None:
             return NotImplemented
-        return F3.conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=pad_slot)
+        return F3.conv_forward_stats(x, w4, stride, pad, dilation, sums, shift, slot=pad_slot, pro=pro)
+    if pro is not None:
+        return NotImplemented
     return _conv_fwd_impl(x, w4, b, stride, pad, dilation, groups, stats=True, pad_slot=pad_slot, shift=shift,
                           sums=sums)
 
@@ -1485,7 +1510,7 @@ def bngrad_consumable(g, x, w4, stride, pad, groups=1):
 
 @register("conv2d_backward")
 def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_input=True, gw_acc=None, gb_acc=None,
-                    scale=1.0, residual=None, bn_fuse=None, pad_slot=None, lazy_strided=False):
+                    scale=1.0, residual=None, bn_fuse=None, pad_slot=None, lazy_strided=False, pro=None):
     """``lazy_strided``: a 1×1 stride-s unpadded conv may return its input gradient as a
     :class:`~bigdl.ops.reference.StridedGrad` (the caller sums it as a strided residual).  ``gy`` may
     be a deferred :class:`~bigdl.ops.reference.BNGrad` (consumed in the operand prologues of a 1×1
@@ -1494,9 +1519,11 @@ def conv2d_backward(gy, x, w4, stride, pad, dilation=(1, 1), groups=1, need_inpu
         # fp32 (bf16x3): the bf16 epilogue fusions are optional — bn_fuse is left unconsumed (the BN
         # runs its own backward), a lazy strided gradient is returned dense
         r = F3.conv_backward(gy, x, w4, stride, pad, dilation, groups, need_input, gw_acc, gb_acc, scale, residual,
-                             slot=pad_slot, bn_fuse=bn_fuse, lazy_strided=lazy_strided)
-        if r is not NotImplemented:
+                             slot=pad_slot, bn_fuse=bn_fuse, lazy_strided=lazy_strided, pro=pro)
+        if r is not NotImplemented or pro is not None:
             return r
+    if pro is not None:
+        return NotImplemented
     if isinstance(gy, R_.BNGrad) and not (bngrad_consumable(gy, x, w4, stride, pad, groups) and gb_acc is None):
         gy = gy.dense()
     if isinstance(gy, R_.BNGrad):

@@ -96,14 +96,16 @@ class StridedGrad:
 
 
 class BNOut:
-    """Deferred output of a training BatchNorm (no ReLU): y = x·coef[c] + coef[C + c], with ``x`` the
+    """Deferred output of a training BatchNorm: y = [relu](x·coef[c] + coef[C + c]), with ``x`` the
     BN input and ``coef`` fp32 [scale; shift].  The fused ResNet block tail takes a shortcut BN's
-    output this way and applies it inside its own pass (ops/csrc/batchnorm.hip rcoef), so the
-    shortcut activation is never written; :meth:`dense` builds it for any other consumer."""
-    __slots__ = ("x", "coef", "shape")
+    output this way (no ReLU) and applies it inside its own pass (ops/csrc/batchnorm.hip rcoef); in
+    fp32 compute a mid-block BN + ReLU hands its output to the next conv this way (``relu``), which
+    applies it in its operand prologues (bigdl.fp32.bnPrologue) — either way the activation is never
+    written; :meth:`dense` builds it for any other consumer."""
+    __slots__ = ("x", "coef", "shape", "relu")
 
-    def __init__(self, x, coef):
-        self.x, self.coef, self.shape = x, coef, tuple(x.shape)
+    def __init__(self, x, coef, relu=False):
+        self.x, self.coef, self.shape, self.relu = x, coef, tuple(x.shape), relu
 
     @property
     def dtype(self):
@@ -113,6 +115,10 @@ class BNOut:
     def is_cuda(self):
         return self.x.is_cuda
 
+    @property
+    def device(self):
+        return self.x.device
+
     def dim(self):
         return self.x.dim()
 
@@ -120,8 +126,11 @@ class BNOut:
         C = self.shape[1]
         sc = self.coef[:C].view(1, C, *([1] * (self.x.dim() - 2)))
         sh = self.coef[C:2 * C].view(1, C, *([1] * (self.x.dim() - 2)))
-        return (self.x.float() * sc + sh).to(self.x.dtype).contiguous(memory_format=torch.channels_last) \
-            if self.x.dim() == 4 else (self.x.float() * sc + sh).to(self.x.dtype)
+        y = torch.addcmul(sh, self.x.float(), sc)  # one rounding, like the kernels' fma
+        if self.relu:
+            y = torch.relu(y)
+        return y.to(self.x.dtype).contiguous(memory_format=torch.channels_last) if self.x.dim() == 4 \
+            else y.to(self.x.dtype)
 
 
 class BNGrad:

@@ -66,6 +66,7 @@ _REGISTRY = {
     "bigdl.fp32.native": (bool, True, "fp32 compute on a GPU: convolutions and Linear run the bf16x3 split on the MFMA kernels (ops/fp32x3.py; ≤2^-16 relative per product) instead of torch/MIOpen fp32"),
     "bigdl.fp32.twoPart": (bool, True, "fp32 compute: activation splits stored as [hi | lo] and read by the conv kernels as [hi | hi | lo] (ConvParams::cdup); false = the three-part [hi | hi | lo] buffers"),
     "bigdl.fp32.producerSplit": (bool, True, "fp32 compute: the BN apply passes also write the [hi | lo] split of their output for the consuming conv (forward input, backward dY), so the conv skips its own split pass"),
+    "bigdl.fp32.bnPrologue": (bool, True, "fp32 compute: a training BN + ReLU whose only consumer is a conv hands its output over deferred (ops.reference.BNOut); the conv applies relu(x·scale + shift) in its forward B-operand and weight-gradient X-operand prologues (conv_x3 / conv_wgrad PRO) and its dgrad epilogue recomputes the ReLU mask — the BN output is never written or read"),
     "bigdl.fp32.stemC4": (bool, True, "fp32 compute: a conv with ≤ 4 input channels (the RGB stem) reads a 4-channel NHWC copy of its input and gathers 8 taps × 4 channels per k-tile (conv_x3.hip MODE 2, conv_wgrad.hip C4 F32): 224 reduction indices for the 7×7 stem instead of the space-to-depth image's 512"),
     "bigdl.fp32.direct": (bool, True, "fp32 compute: convolutions with C % 32 == 0 read the fp32 activations and gradients directly (csrc/conv_x3.hip: hi / lo split while reading the MFMA fragments; conv_wgrad.hip F32: split between load and LDS store) — no [hi | lo] split is materialised and the BN passes write fp32 only"),
     "bigdl.fp32.convStats": (bool, True, "fp32 compute: a conv followed by a training BN adds the BN statistics into the BN's replicated buffer from its fp32 epilogue (the BN skips its statistics pass)"),

@@ -1,0 +1,133 @@
+"""fp32 compute, deferred mid-block BN + ReLU (bigdl.fp32.bnPrologue): the BN only finalizes its
+statistics and the consuming conv reads relu(x·scale + shift) through the operand prologues of the
+direct kernels (csrc/conv_x3.hip PRO: forward B operand, padded taps stay 0; csrc/conv_wgrad.hip F32
+PRO: weight-gradient X operand), while its data-gradient epilogue recomputes the ReLU mask from the BN
+input.  Checked against the materialised BN output (the same kernels without the prologue) and, for
+the whole ResNet-50 step, against the step with the prologue off (reference: the BN + ReLU → conv
+chain of SpatialBatchNormalization / ReLU / SpatialConvolution in fp32, DL/nn/mkldnn/Fusion.scala:79)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+cl = torch.channels_last
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _kernels(fn):
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        out = fn()
+        torch.cuda.synchronize()
+    return out, [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+
+
+@pytest.mark.parametrize("N,C,K,H,k,s,p", [(2, 64, 96, 13, 3, 1, 1), (3, 128, 64, 9, 1, 1, 0),
+                                           (2, 64, 64, 15, 3, 2, 1), (2, 96, 128, 7, 3, 1, 1)])
+def test_prologue_conv_matches_materialised_bn_output(N, C, K, H, k, s, p):
+    from bigdl.ops import fp32x3 as F3
+    g = torch.Generator().manual_seed(4)
+    xb = (torch.randn(N, C, H, H, generator=g) * 2 + 0.3).to(dev).contiguous(memory_format=cl)
+    coef = torch.cat([torch.rand(C, generator=g) * 1.5 - 0.25, torch.randn(C, generator=g) * 0.5]).to(dev)
+    ymat = torch.relu(torch.addcmul(coef[C:].view(1, C, 1, 1), xb, coef[:C].view(1, C, 1, 1))).contiguous(
+        memory_format=cl)
+    w = (torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5).to(dev)
+    y1, names = _kernels(lambda: F3.conv_forward(xb, w, None, (s, s), (p, p), pro=coef))
+    assert y1 is not NotImplemented
+    assert any("k_conv_x3" in n and ", true>" in n for n in names), names
+    y0 = F3.conv_forward(ymat, w, None, (s, s), (p, p))
+    torch.cuda.synchronize()
+    assert _rel(y1, y0) < 1e-6, _rel(y1, y0)
+    gy = torch.randn(y0.shape, generator=g).to(dev).contiguous(memory_format=cl)
+    gw1 = torch.zeros(K, k, k, C, device=dev).permute(0, 3, 1, 2)
+    gw0 = torch.zeros_like(gw1)
+    _, names = _kernels(lambda: F3.conv_backward(gy, xb, w, (s, s), (p, p), (1, 1), 1, False, gw1, None, 1.0,
+                                                 pro=coef))
+    assert any("k_conv_wgrad" in n and n.split("(")[0].rstrip(">").endswith("true, true") for n in names), names
+    F3.conv_backward(gy, ymat, w, (s, s), (p, p), (1, 1), 1, False, gw0, None, 1.0)
+    torch.cuda.synchronize()
+    assert _rel(gw1, gw0) < 1e-6, _rel(gw1, gw0)
+
+
+def _resnet_grads(prologue):
+    """One fp32-mode training forward + backward of fused ResNet-50 (batch 4) from fixed weights:
+    (loss, [(name, gradient)], kernel names of the step)."""
+    from bigdl.models.resnet import ResNet, DatasetType, model_init
+    from bigdl.utils.random import RNG
+    from bigdl.nn import CrossEntropyCriterion
+    from bigdl.nn.fusion import fuse, mark_input_no_grad
+    from bigdl.utils import config
+    from bigdl.utils.engine import Engine
+    from bigdl.ops import native_ops as NO
+    config.set_property("bigdl.compute.dtype", "fp32")
+    config.set_property("bigdl.fp32.bnPrologue", prologue)
+    Engine.init(device="cuda:0")
+    Engine.set_compute_dtype("fp32")
+    try:
+        RNG.setSeed(7)
+        torch.manual_seed(7)
+        m = model_init(ResNet(10, depth=50, dataset=DatasetType.ImageNet))
+        from bigdl.nn import SpatialBatchNormalization
+        with torch.no_grad():  # well-conditioned (block-tail γ = 0.1, as tests/test_train_parity.py)
+            for bn in m.flattened_modules():
+                if isinstance(bn, SpatialBatchNormalization) and float(bn.weight.abs().max()) == 0.0:
+                    bn.weight.fill_(0.1)
+        m.cuda()
+        m.training()
+        fuse(m)
+        mark_input_no_grad(m)
+        m.getParameters()
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(4, 3, 224, 224, generator=g).to(dev)
+        y = (torch.randint(0, 10, (4,), generator=g) + 1).float().to(dev)
+        crit = CrossEntropyCriterion()
+        names = []
+        for it in range(2):  # the second pass (kernel selection settled) is the one compared
+            m.zeroGradParameters()
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+                out = m.forward(x)
+                loss = float(crit.forward(out, y))
+                m.backward(x, crit.backward(out, y))
+                NO.join_wgrad()
+                torch.cuda.synchronize()
+            names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+        pn = [f"{type(mm).__name__}.{n}" for (mm, n, _g) in m._param_entries()]
+        grads = [(nm, gr.detach().float().cpu().clone()) for nm, gr in zip(pn, m.parameters()[1])]
+        return loss, grads, names
+    finally:
+        Engine.set_compute_dtype("bf16")
+        config.set_property("bigdl.compute.dtype", "bf16")
+        config.clear_property("bigdl.fp32.bnPrologue")
+
+
+def _cosines(ga, gb):
+    cs = []
+    for (nm, a), (_nm, b) in zip(ga, gb):
+        if (nm.endswith(".bias") and "Convolution" in nm) or float(b.norm()) == 0:
+            continue  # conv biases feeding a BN: true gradient 0 (rounding noise)
+        a, b = a.double().reshape(-1), b.double().reshape(-1)
+        cs.append(float(a @ b / (a.norm() * b.norm()).clamp_min(1e-30)))
+    return sorted(cs)
+
+
+def test_resnet50_fp32_step_with_bn_prologue_matches_materialised():
+    """Same weights, same batch: the step with the deferred BN outputs against the materialised one
+    (and, as the noise floor, against a second materialised run — the split-K weight gradients add
+    with float atomics, so two runs already differ in the last bits)."""
+    l1, g1, n1 = _resnet_grads(True)
+    l0, g0, n0 = _resnet_grads(False)
+    l2, g2, _n2 = _resnet_grads(False)
+    pro = sum("k_conv_x3" in n and ", true>" in n for n in n1)
+    fwd_apply = lambda ns: sum("k_bn32_apply<false" in n for n in ns)  # noqa: E731  (forward applies)
+    c_pro, c_ctl = _cosines(g1, g0), _cosines(g2, g0)
+    print("loss", l1, l0, l2, "prologue conv launches", pro, "forward BN applies", fwd_apply(n1), fwd_apply(n0),
+          "cos min/p10 pro", c_pro[0], c_pro[len(c_pro) // 10], "control", c_ctl[0], c_ctl[len(c_ctl) // 10])
+    assert pro >= 32, pro  # 16 bottlenecks × 2 mid-block BN + ReLU consumed by their next conv
+    assert fwd_apply(n1) <= fwd_apply(n0) - 32, (fwd_apply(n1), fwd_apply(n0))
+    assert abs(l1 - l0) <= 1e-5 * abs(l0) and abs(l2 - l0) <= 1e-5 * abs(l0), (l1, l0, l2)
+    assert c_pro[0] >= 0.9999 or c_pro[0] >= c_ctl[0] - 1e-4, (c_pro[:5], c_ctl[:5])
