@@ -92,16 +92,22 @@ struct X3Params {
 
 constexpr int X3_PRO_MAXC = 512;
 
-// y = relu(x·sc + sh) of 8 consecutive channels (or 0 for a padded tap)
-__device__ __forceinline__ void x3_pro8(v4f& a, v4f& b, const float* sc, const float* sh, bool valid) {
+
+// the prologue of one slice: y = relu(x·sc + sh) of a lane's 8 channels for its TMI fragment rows
+// (0 for a padded tap); sc = this slice's scales in the [scale | shift] LDS copy
+template <int TMI>
+__device__ __forceinline__ void x3_pro_slice(v4f (&a)[TMI], v4f (&b)[TMI], const float* sc, const bool (&valid)[TMI]) {
   const v4f s0 = *reinterpret_cast<const v4f*>(sc), s1 = *reinterpret_cast<const v4f*>(sc + 4);
-  const v4f h0 = *reinterpret_cast<const v4f*>(sh), h1 = *reinterpret_cast<const v4f*>(sh + 4);
+  const v4f h0 = *reinterpret_cast<const v4f*>(sc + X3_PRO_MAXC), h1 = *reinterpret_cast<const v4f*>(sc + X3_PRO_MAXC + 4);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    a[e] = valid ? fmaxf(fmaf(a[e], s0[e], h0[e]), 0.f) : 0.f;
-    b[e] = valid ? fmaxf(fmaf(b[e], s1[e], h1[e]), 0.f) : 0.f;
-  }
+  for (int j = 0; j < TMI; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[j][e] = valid[j] ? fmaxf(fmaf(a[j][e], s0[e], h0[e]), 0.f) : 0.f;
+      b[j][e] = valid[j] ? fmaxf(fmaf(b[j][e], s1[e], h1[e]), 0.f) : 0.f;
+    }
 }
+
 
 // One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds): lane l's 16 bytes land at lds + 16·l.
 // (A non-template function: inside the kernel template the builtin fails host-side substitution.)
@@ -362,13 +368,14 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
         b1[kk][j] = *reinterpret_cast<const v4f*>(base + (b_row0 + 32 * j) * 128 + fb1[kk]);
       }
     }
-    if constexpr (PRO) {  // the deferred BN + ReLU of the input, before the split
-      const float* scp = pro_s + pc_c0 + 8 * fh;
+    // PRO: the deferred BN + ReLU of the input, applied to each slice right before its split (slice 1's
+    // with slice 1's split, under slice 0's MFMAs); a padded tap of a row reads 0 (pointwise: none)
+    const float* scp = pro_s + pc_c0 + 8 * fh;
+    bool pvalid[TMI];
+    if constexpr (PRO) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < TMI; ++j)
-          x3_pro8(b0[kk][j], b1[kk][j], scp + 16 * kk, scp + X3_PRO_MAXC + 16 * kk, (fmask[j] >> pc_tap) & 1ull);
+      for (int j = 0; j < TMI; ++j) pvalid[j] = PW || ((fmask[j] >> pc_tap) & 1ull);
+      x3_pro_slice<TMI>(b0[0], b1[0], scp, pvalid);
       pc_c0 += BK;
       if (pc_c0 == p.C) {
         pc_c0 = 0;
@@ -401,6 +408,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
         if (decltype(issue_on)::value && kk * PPK + q < L) issue(kk * PPK + q, nslot);
       __builtin_amdgcn_sched_barrier(0);
       if (kk == 0) {
+        if constexpr (PRO) x3_pro_slice<TMI>(b0[1], b1[1], scp + 16, pvalid);
 #pragma unroll
         for (int j = 0; j < TMI; ++j) x3_split8(b0[1][j], b1[1][j], bh[1][j], bl[1][j]);
         __builtin_amdgcn_sched_barrier(0);

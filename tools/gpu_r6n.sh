@@ -20,3 +20,8 @@ python tools/rocpd_dispatches.py "$db" 700 > $O/fp32_dispatches.txt
 ms=$(python -c "import json; print([json.loads(l) for l in open('$O/pf32.log') if l.startswith('{\"metric')][-1]['ms_per_step']*3)")
 LAST_MS=$ms python tools/rocpd_summary.py "$db" 3 40 > $O/fp32_serial_summary.txt; rm -rf $O/pf32
 head -24 $O/fp32_serial_summary.txt
+# bf16 headline (default bench) and PTB world-1 distri host profile
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | tail -1 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("bench bf16", d["ms_per_step"], "fp32", d["fp32"]["ms_per_step"])'
+timeout -k 10 200 python tools/bench_configs.py --config ptb --steps 50 --warmup 10 --cprofile 100 --force-distri > $O/ptb_cp.log 2>&1 || { tail -20 $O/ptb_cp.log; exit 1; }
+grep -A45 "function calls" $O/ptb_cp.log | head -60
