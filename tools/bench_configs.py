@@ -211,7 +211,8 @@ def bench_ptb(args):
         pr.disable()
         out = io.StringIO()
         pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(40)
-        print(out.getvalue()[:12000], file=sys.stderr, flush=True)
+        pstats.Stats(pr, stream=out).sort_stats("cumulative").print_stats(45)
+        print(out.getvalue()[:24000], file=sys.stderr, flush=True)
     res = {"metric": "tokens/sec PTB 2-layer LSTM LM", "value": round(B * T * world * args.steps / el, 1),
            "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "dtype": args.dtype,
