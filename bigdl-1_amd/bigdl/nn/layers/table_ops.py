@@ -137,10 +137,43 @@ class JoinTable(TensorModule):
     #: concat, planned by :func:`bigdl.nn.containers.plan_concat`); consumed once
     _planned = None
 
+    #: set by the int8 quantizer (nn/quantized/quantizer.py _link_graph): the inputs arrive as int8 codes
+    #: of one common scale
+    _i8_join = False
+
+    def _int8_cat(self, ts, d):
+        """Concat of int8 activations sharing one scale / code (a quantised Inception block): the
+        codes are concatenated as they are and the result keeps the tag (+ the 0x80 tail an unsigned
+        code carries for padded consumer taps)."""
+        from ...ops import native_ops as NO
+        t0 = ts[0]
+        sc, z = getattr(t0, "_qscale", None), getattr(t0, "_qzero", 0)
+        if (sc is None or d != 1 or t0.dim() != 4 or not t0.is_cuda
+                or any(t.dtype != torch.int8 or getattr(t, "_qscale", None) != sc or getattr(t, "_qzero", 0) != z
+                       or t.shape[0] != t0.shape[0] or t.shape[2:] != t0.shape[2:] for t in ts)):
+            return None
+        u8 = bool(z)
+        N_, H, W = t0.shape[0], t0.shape[2], t0.shape[3]
+        y = NO._i8_act(N_, sum(t.shape[1] for t in ts), H, W, t0.device, u8)
+        c0 = 0
+        for t in ts:
+            y[:, c0:c0 + t.shape[1]].copy_(t)
+            c0 += t.shape[1]
+        if u8:
+            n = y.numel()
+            y._base.view(-1)[n:n + 16].fill_(-128)
+        return NO._tag(y, sc, u8)
+
     def updateOutput(self, input):
         ts = list(input)
         d = self._d(ts[0])
         self._sizes = [t.shape[d] for t in ts]
+        if ts[0].dtype == torch.int8:
+            y = self._int8_cat(ts, d)
+            if y is not None:
+                return y
+            from ..quantized.layers import dequant
+            ts = [dequant(t) if getattr(t, "_qscale", None) is not None else t for t in ts]
         big, self._planned = self._planned, None
         if big is not None and d == 1 and _tiles_channels(big, ts):
             return big

@@ -318,6 +318,117 @@ def _link_all(model):
             _link_units(_exec_units(blk.shortcut))
 
 
+def _graph_pass(e):
+    """Single-tensor layers an int8 activation of a quantised chain passes through unchanged in
+    scale (ReLU(0, 0), max pooling, evaluation dropout, Identity)."""
+    from ..layers.activation import Threshold
+    from ..layers.pooling import SpatialMaxPooling
+    from ..layers.dropout import Dropout
+    if isinstance(e, Threshold):
+        return e.threshold == 0.0 and e.value == 0.0
+    return isinstance(e, (SpatialMaxPooling, Dropout, L.Identity))
+
+
+def _graph_consumers(node):
+    """The quantised convs that read ``node``'s output through pass-through layers only (fan-out
+    allowed): list of conv elements, or None when any path reaches something else."""
+    out, todo, seen = [], list(node.next_nodes), set()
+    while todo:
+        n = todo.pop()
+        if n._id in seen:
+            continue
+        seen.add(n._id)
+        e = n.element
+        if len(n.prev_nodes) != 1:
+            return None
+        if isinstance(e, Q.SpatialConvolution):
+            out.append(e)
+        elif _graph_pass(e) and n.next_nodes:
+            todo.extend(n.next_nodes)
+        else:
+            return None
+    return out or None
+
+
+def _graph_producer(p):
+    """(quantised conv, its ReLU or None) whose output reaches node ``p``'s output through at most one
+    ReLU (a single-consumer chain), else None."""
+    from ..layers.activation import Threshold
+    relu = None
+    if isinstance(p.element, Threshold) and _graph_pass(p.element) and len(p.prev_nodes) == 1:
+        relu = p.element
+        if len(p.prev_nodes[0].next_nodes) != 1:
+            return None
+        p = p.prev_nodes[0]
+    e = p.element
+    if isinstance(e, Q.SpatialConvolution) and e.nGroup == 1 and e.nOutputPlane % 16 == 0:
+        return e, relu
+    return None
+
+
+def _link_graph(g):
+    """int8 chains of a Graph model (node topology instead of Sequential order):
+
+    * a calibrated int8 conv (optionally through its ReLU) whose consumers — through ReLU / max pooling
+      / eval dropout / Identity, fan-out allowed — are all calibrated int8 convs writes their int8
+      input directly, at ONE scale (the largest of the consumers' calibrated input scales; they read
+      the same tensor, so they agree);
+    * a channel JoinTable whose every input is such a producer and whose consumers are all int8 convs:
+      every producer writes at the common scale and the concat runs on the int8 codes — the
+      reference's input-scale unification ahead of a JoinTable (``setScalesPrevousJoinTable``,
+      DL/nn/mkldnn/Fusion.scala:240-290)."""
+    from ..layers.table_ops import JoinTable
+    from ...ops import native_ops as NO
+    from ...utils import config
+    u8ok = bool(config.get_property("bigdl.int8.unsignedActivations"))
+
+    def link(producers, consumers, in_channels):
+        scales = [c.static_scale for c in consumers]
+        if any(s is None for s in scales) or any(c.nGroup != 1 or not NO.conv_i8_supported(
+                in_channels, c.kernelH, c.kernelW) for c in consumers):
+            return False
+        sc = max(scales)
+        all_relu = all(r is not None for _c, r in producers)
+        for conv, relu in producers:
+            conv._out_qscale = sc
+            if relu is not None:
+                conv._relu_fused = True
+                relu._i8_fused = True
+            if u8ok and all_relu:  # every input of the tensor is ReLU'd: the unsigned code
+                conv._out_u8 = True
+                conv._out_qscale = sc * 127.0 / 255.0
+        return True
+
+    for n in g.forward_order:
+        e = n.element
+        if isinstance(e, JoinTable):
+            if e.dimension != 2 or len(n.prev_nodes) < 2:
+                continue
+            prods = [_graph_producer(p) for p in n.prev_nodes]
+            if any(x is None for x in prods) or len({id(c) for c, _r in prods}) != len(prods):
+                continue
+            if any(len(p.next_nodes) != 1 for p in n.prev_nodes):
+                continue
+            cons = _graph_consumers(n)
+            if cons and link(prods, cons, sum(c.nOutputPlane for c, _r in prods)):
+                e._i8_join = True
+            continue
+        if not (isinstance(e, Q.SpatialConvolution) and e.nGroup == 1 and e.nOutputPlane % 16 == 0
+                and len(n.next_nodes) == 1):
+            continue
+        nxt = n.next_nodes[0]
+        from ..layers.activation import Threshold
+        relu = nxt.element if (isinstance(nxt.element, Threshold) and _graph_pass(nxt.element)) else None
+        src = nxt if relu is not None else n
+        if relu is not None and len(nxt.prev_nodes) != 1:
+            continue
+        if any(isinstance(m.element, JoinTable) for m in src.next_nodes):
+            continue  # (the join's pass decides)
+        cons = _graph_consumers(src)
+        if cons:
+            link([(e, relu)], cons, e.nOutputPlane)
+
+
 def quantize(model):
     """Deep-copy ``model`` and return its int8 version (evaluation mode).  Evaluation BatchNorms after a
     convolution are folded into it first; layers calibrated with ``calcScales`` quantise their input
@@ -337,5 +448,8 @@ def quantize(model):
         _link_all(q)
     else:
         _link_int8_chains(q)
+    from ..graph import Graph
+    for g in [m for m in ([q] + list(q.flattened_modules())) if isinstance(m, Graph)]:
+        _link_graph(g)
     q.evaluate()
     return q

@@ -15,7 +15,8 @@
 // weights per output channel (sw[k], symmetric); the epilogue dequantises acc·sx[img]·sw[k] + bias,
 // applies ReLU and stores bf16 through the shared row-major store pass.
 //
-// Channel counts: C % 128 == 0 (a k-tile lies inside one tap: the tap is wave-uniform) or C == 64
+// Channel counts: C % 16 == 0 (a k-tile lies inside one tap: the tap is wave-uniform; C % 128 != 0 leaves
+// the tap's last k-tile partial, its chunks past C read the pad code against zero weights) or C == 64
 // (a k-tile holds two taps: chunks 0–3 tap 2t, chunks 4–7 tap 2t + 1, per-lane source offsets; an
 // odd R·S leaves a zero half tile).  Weight rows are [K][ldw] int8, (r, s, c) order, zero-padded to
 // ldw = KT·128.
@@ -120,6 +121,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
   // four chunks belong to the tile's first tap, the high four to its second)
   int rbase[GB];
   uint64_t vmask[GB];
+  int cinj[GB];  // TPT == 1: this lane's channel offset inside the k-tile (C % 128 != 0: the last k-tile
+                 // of a tap is partial, its chunks past C read the pad code)
   int hi_half = 0;
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
@@ -137,6 +140,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
       w = qq * p.sw - p.pw;
     }
     const int cin = TPT == 2 ? (chunk & 3) * 16 : chunk * 16;
+    cinj[j] = cin;
     rbase[j] = ((img * p.H + h) * p.W + w) * p.C + cin;
     uint64_t msk = 0;
     if (img >= 0) {
@@ -182,7 +186,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
       off_a = it_off;
       c0 = it_c0;
       it_c0 += 128;
-      if (it_c0 == p.C) {
+      if (it_c0 >= p.C) {  // (C % 128 != 0: ⌈C / 128⌉ k-tiles per tap)
         it_c0 = 0;
         next_tap();
       }
@@ -199,7 +203,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
         const bool ok = tap < RS && ((vmask[j] >> tap) & 1ull);
         off = ok ? (uint32_t)(rbase[j] + (hi ? off_b : off_a)) : XPAD;
       } else {
-        const bool ok = (vmask[j] >> tap_a) & 1ull;
+        const bool ok = ((vmask[j] >> tap_a) & 1ull) && c0 + cinj[j] < p.C;
         off = ok ? (uint32_t)(rbase[j] + off_a + c0) : XPAD;
       }
       i8_glds16(xr, dst, off);
@@ -550,8 +554,9 @@ BIGDL_EXPORT int bigdl_quant_img(const void* x, int Nb, long long per_img, float
 }
 
 // y[m][n] (bf16, row stride ldy) = [ReLU](Σ_k w[n][k]·x̂[m][k] · sx[img(m)] · sw[n] + bias[n]).
-// x: int8 NHWC [Nb][H][W][C] (C % 128 == 0 or C == 64); w: int8 [K][ldw], (r, s, c) order zero-padded
-// to ldw = KT·128 (KT = R·S·C / 128, or ⌈R·S / 2⌉ for C == 64); R·S ≤ 64; K % 8 == 0.
+// x: int8 NHWC [Nb][H][W][C] (C % 16 == 0 or C == 64); w: int8 [K][ldw], (r, s, c) order, each tap's
+// C channels zero-padded to ⌈C / 128⌉·128, ldw = KT·128 (KT = R·S·⌈C / 128⌉, or ⌈R·S / 2⌉ for C == 64);
+// R·S ≤ 64; K % 8 == 0.
 // sx null: one static activation scale sxs for every image (calibrated, nn/quantized); yq non-null:
 // int8 output requantised by 1 / out_scale (K % 16, ldy % 16, 16-B aligned) instead of bf16 y.
 BIGDL_EXPORT int bigdl_conv_i8_fwd2(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
@@ -610,9 +615,11 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
   if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)
     return (int)hipErrorInvalidValue;
   if (yq && (K % 16 || ldy % 16 || ((uintptr_t)yq & 15) || !(out_scale > 0.f))) return (int)hipErrorInvalidValue;
-  const int tpt = C == 64 ? 2 : (C % 128 == 0 ? 1 : 0);
+  // C % 128 != 0 (C % 16 == 0, e.g. Inception's 480 / 528 / 832-channel concats): every tap takes
+  // ⌈C / 128⌉ k-tiles and the weight rows are zero-padded per tap to that many 128-byte tiles
+  const int tpt = C == 64 ? 2 : (C % 16 == 0 ? 1 : 0);
   if (!tpt || R * S > 64 || R <= 0 || S <= 0) return (int)hipErrorInvalidValue;
-  const int KT = tpt == 2 ? (R * S + 1) / 2 : R * S * C / 128;
+  const int KT = tpt == 2 ? (R * S + 1) / 2 : R * S * ((C + 127) / 128);
   if (ldw != KT * 128 || ldy < K || ldy % 8 || ((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15))
     return (int)hipErrorInvalidValue;
   if ((size_t)Nb * H * W * C >= 0x80000000ull || (size_t)K * ldw >= 0x80000000ull) return (int)hipErrorInvalidValue;

@@ -1822,7 +1822,7 @@ def quant_rows(x2d, kp=None):
 
 # ---- int8 implicit-GEMM convolution (conv_i8.hip) ----------------------------------------------
 def conv_i8_supported(C_, R, S, groups=1) -> bool:
-    return groups == 1 and (C_ == 64 or C_ % 128 == 0) and R * S <= 64
+    return groups == 1 and (C_ == 64 or C_ % 16 == 0) and R * S <= 64
 
 
 def conv_i8_weight(qweight, K, C_, R, S):
@@ -1830,11 +1830,17 @@ def conv_i8_weight(qweight, K, C_, R, S):
     [K][ldw] rows in (r, s, c) order, zero-padded to whole 128-byte k-tiles.  Returns (w, ldw)."""
     kg = C_ * R * S
     w = qweight[:, :kg].reshape(K, C_, R, S).permute(0, 2, 3, 1).reshape(K, R * S, C_)
-    KT = (R * S + 1) // 2 if C_ == 64 else kg // 128
-    ldw = KT * 128
-    out = torch.zeros((K, ldw), dtype=torch.int8, device=qweight.device)
-    out[:, :kg] = w.reshape(K, kg)
-    return out, ldw
+    if C_ == 64:
+        KT = (R * S + 1) // 2
+        ldw = KT * 128
+        out = torch.zeros((K, ldw), dtype=torch.int8, device=qweight.device)
+        out[:, :kg] = w.reshape(K, kg)
+        return out, ldw
+    cp = (C_ + 127) // 128 * 128  # each tap's channels padded to whole 128-byte k-tiles
+    ldw = R * S * cp
+    out = torch.zeros((K, R * S, cp), dtype=torch.int8, device=qweight.device)
+    out[:, :, :C_] = w
+    return out.reshape(K, ldw), ldw
 
 
 def quant_images(x):
@@ -1923,7 +1929,7 @@ def conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias):
     """The bias of the int8 conv for an unsigned (offset −128) input of scale ``sx``: the offset's
     share of the dot product, 128·Σ_(taps, c) w · sx · sw, is a per-channel constant (padded taps
     read the code of 0 from the input's tail) folded in here."""
-    w = wq.view(torch.int8).reshape(K, ldw)[:, :R * S * C_].to(torch.int32).sum(-1).double()
+    w = wq.view(torch.int8).reshape(K, ldw).to(torch.int32).sum(-1).double()  # (padding entries are 0)
     b = bias.double() if bias is not None else torch.zeros(K, dtype=torch.float64, device=wq.device)
     return (b + 128.0 * w * float(sx) * w_scale.double()).float().contiguous()
 

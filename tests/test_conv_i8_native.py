@@ -26,6 +26,11 @@ SHAPES = [  # N, C, H, K, R, stride, pad, dilation
     (2, 512, 14, 1024, 1, 2, 0, 1),
     (3, 64, 17, 72, 3, 1, 2, 2),      # dilated, M and K tails
     (2, 64, 9, 64, 5, 1, 2, 1),       # R·S = 25: odd tap count → half-empty last k-tile
+    (2, 480, 14, 192, 1, 1, 0, 1),    # C % 128 != 0 (Inception concats): partial last k-tile per tap
+    (2, 528, 14, 160, 1, 1, 0, 1),
+    (2, 832, 7, 384, 1, 1, 0, 1),
+    (2, 96, 15, 128, 3, 1, 1, 1),     # … and with padded taps
+    (2, 16, 12, 32, 5, 1, 2, 1),
 ]
 
 

@@ -288,3 +288,71 @@ def test_resnet50_int8_logits_track_fp32():
     cos = float(torch.nn.functional.cosine_similarity(out.reshape(1, -1), ref.reshape(1, -1)))
     print("resnet50 int8 vs fp32 logit cosine", cos)
     assert cos >= 0.99, cos
+
+
+def _inception_calibrated(size=224, seed=5):
+    from bigdl.models.inception import Inception_v1_NoAuxClassifier
+    from bigdl.utils.random import RNG
+    RNG.setSeed(seed)
+    torch.manual_seed(seed)
+    m = Inception_v1_NoAuxClassifier.graph(10, has_dropout=False)
+    m.evaluate()
+    g = torch.Generator().manual_seed(seed)
+    xc = torch.randn(2, 3, size, size, generator=g)
+    with torch.no_grad():
+        m.forward(xc)
+    m.calcScales(xc)
+    return m, g
+
+
+def test_inception_int8_graph_links_and_unified_join_scales():
+    """quantize() on a calibrated Inception-v1 graph: inside every branch the 1×1 reduce conv writes the
+    3×3 / 5×5 conv's int8 input (ReLU fused), and every inception JoinTable whose consumers are int8
+    convs gets its four producers at ONE common scale (the reference's input-scale unification ahead of
+    a JoinTable, DL/nn/mkldnn/Fusion.scala:240-290) — the concat then runs on int8 codes."""
+    from bigdl.nn.quantized import layers as Q
+    from bigdl.nn.layers.table_ops import JoinTable
+    m, _g = _inception_calibrated()
+    q = m.quantize()
+    joins = [n for n in q.forward_order if isinstance(n.element, JoinTable)]
+    linked = [n for n in joins if n.element._i8_join]
+    # 9 inception blocks; the last one feeds the average pooling (not a conv): stays float
+    assert len(joins) == 9 and len(linked) == 8, (len(joins), len(linked))
+    for n in linked:
+        prods = []
+        for p in n.prev_nodes:
+            e = p.element if isinstance(p.element, Q.SpatialConvolution) else p.prev_nodes[0].element
+            prods.append(e)
+        assert len({c._out_qscale for c in prods}) == 1 and all(c._relu_fused for c in prods)
+    # every 1×1 reduce conv feeding a 3×3 / 5×5 conv of its branch is linked
+    reduces = [n.element for n in q.forward_order if isinstance(n.element, Q.SpatialConvolution)
+               and n.element.get_name().startswith("inception_")
+               and n.element.get_name().endswith(("3x3_reduce", "5x5_reduce"))]
+    assert len(reduces) == 18
+    # (the int8 kernel tiles channel counts % 16: the two 24-channel 5×5 reduces stay bf16-out)
+    assert all(c._out_qscale is not None and c._relu_fused for c in reduces if c.nOutputPlane % 16 == 0)
+    assert sum(c.nOutputPlane % 16 == 0 for c in reduces) == 16
+
+
+@pytest.mark.gpu
+def test_inception_int8_logits_track_fp32():
+    """Calibrated int8 Inception-v1 on the GPU (int8 branch chains, int8 concats at unified scales) vs
+    the float model: logit cosine ≥ 0.99 and the linked JoinTables really produce int8."""
+    from bigdl.utils.engine import Engine
+    from bigdl.utils import config
+    from bigdl.nn.layers.table_ops import JoinTable
+    config.set_property("bigdl.compute.dtype", "bf16")
+    Engine.init(device="cuda:0")
+    m, g = _inception_calibrated(seed=6)
+    q = m.quantize().cuda()
+    q.evaluate()
+    x = torch.randn(8, 3, 224, 224, generator=g)
+    with torch.no_grad():
+        ref = m.forward(x).double()
+        out = q.forward(x.cuda().bfloat16().contiguous(memory_format=torch.channels_last)).double().cpu()
+    joins = [n.element for n in q.forward_order if isinstance(n.element, JoinTable) and n.element._i8_join]
+    assert joins and all(j.output.dtype == torch.int8 for j in joins), [j.output.dtype for j in joins]
+    ref, out = ref - ref.mean(1, keepdim=True), out - out.mean(1, keepdim=True)
+    cos = float(torch.nn.functional.cosine_similarity(out.reshape(1, -1), ref.reshape(1, -1)))
+    print("inception int8 vs fp32 logit cosine", cos)
+    assert cos >= 0.99, cos
