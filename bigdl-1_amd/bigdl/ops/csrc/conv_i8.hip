@@ -79,16 +79,19 @@ __device__ __forceinline__ void i8_res4(const ConvI8Params& p, int m, int n, flo
   }
 }
 
-template <int BM, int BN, int WM, int WN, int TPT>
-__global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
+// NS: LDS ring depth — 3 (the k-loop pipeline), or 2 for the short reductions (KT ≤ 2: the 1×1 convs
+// over ≤ 256 channels) on 128-row tiles, where the launch is load → one or two MFMA tiles → store and
+// two blocks per CU overlap one block's epilogue with the other's loads (one 147 KB block per CU did not)
+template <int BM, int BN, int WM, int WN, int TPT, int NS = 3>
+__global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? 2 : 1) k_conv_i8(ConvI8Params p) {
+  static_assert(NS == 2 || NS == 3, "LDS ring depth");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
-  constexpr int NS = 3;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;
   static_assert(GA * NW * 8 == BN && GB * NW * 8 == BM, "tile rows must split evenly over the waves");
   constexpr int L = GA + GB;
   constexpr int TMI = BM / WM / 32, TNI = BN / WN / 32;
-  constexpr int EPI = BM * BN * 2;
+  constexpr int EPI = BM * BN * 4;  // (the fp32 conv + sum tile; the bf16 tile needs half)
   constexpr int LDS_BYTES = NS * STAGE > EPI ? NS * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
@@ -241,7 +244,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
     }
   };
 
-  const int KT = p.KT;
+  const int KT = p.KT;  // (NS == 2: the host launches KT ≤ 2 only)
   stage(0, 0);
   if (KT > 1) {
     stage(1, 1);
@@ -279,6 +282,75 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) k_conv_i8(ConvI8Params p) {
     sxm[j] = m < p.M ? (p.sx ? p.sx[m / (p.P * p.Q)] : p.sxs) : 0.f;
   }
   const float qlo = p.y_u8 ? 0.f : -127.f, qhi = p.y_u8 ? 255.f : 127.f, qoff = p.y_u8 ? 128.f : 0.f;
+  if (p.yq && p.res_kind) {
+    // conv + sum with an int8 output: park the dequantised tile as fp32 [BM][BN] (16-B chunk c of row r
+    // at c ^ (r & (BN/4 − 1))), then a row-major pass adds the residual with whole-row reads (16
+    // consecutive channels per thread), applies the ReLU, requantises and stores 16 B — the residual
+    // is never read in the accumulator layout (32 rows × 4 B per wave-instruction)
+    constexpr int CPRF = BN / 4;
+    float* ef = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < TNI; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
+        float s4[4], b4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + nl + e;
+          s4[e] = n < p.K ? p.swt[n] : 0.f;
+          b4[e] = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < TMI; ++j) {
+          const int ml = (b_row0 - BN) + 32 * j + pm;
+          float4 v;
+          v.x = fmaf((float)acc[i][j][4 * g + 0] * sxm[j], s4[0], b4[0]);
+          v.y = fmaf((float)acc[i][j][4 * g + 1] * sxm[j], s4[1], b4[1]);
+          v.z = fmaf((float)acc[i][j][4 * g + 2] * sxm[j], s4[2], b4[2]);
+          v.w = fmaf((float)acc[i][j][4 * g + 3] * sxm[j], s4[3], b4[3]);
+          *reinterpret_cast<float4*>(ef + ml * BN + (((nl >> 2) ^ (ml & (CPRF - 1))) << 2)) = v;
+        }
+      }
+    __syncthreads();
+    constexpr int G16 = BN / 16;  // 16-channel groups per tile row
+    for (int idx = tid; idx < BM * G16; idx += NT) {
+      const int row = idx / G16, g16 = idx - row * G16;
+      const int m = m0 + row, n = n0 + g16 * 16;
+      if (m >= p.M || n >= p.K) continue;
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 f = *reinterpret_cast<const float4*>(ef + row * BN + (((g16 * 4 + c) ^ (row & (CPRF - 1))) << 2));
+        v[4 * c] = f.x; v[4 * c + 1] = f.y; v[4 * c + 2] = f.z; v[4 * c + 3] = f.w;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float r4[4];
+        i8_res4(p, m, n + 4 * c, r4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * c + e] += r4[e];
+      }
+      uint32_t w4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = v[4 * c + e];
+          if (p.relu) x = fmaxf(x, 0.f);
+          const float r = fminf(fmaxf(rintf(x * p.out_inv), qlo), qhi) - qoff;
+          packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+        }
+        w4[c] = packed;
+      }
+      *reinterpret_cast<uint4*>(p.yq + (size_t)m * p.ldy + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    if (p.y_u8 && blockIdx.x == 0 && tid == 0)
+      *reinterpret_cast<uint4*>(p.yq + (size_t)p.M * p.ldy) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u,
+                                                                         0x80808080u);
+    return;
+  }
   if (p.yq) {
     // int8 output: requantise with the consumer's static scale and park the tile as bytes
     // ([BM][BN], 16-B chunk c of row r at chunk c ^ (r & 7)), then one 16-B store per chunk
@@ -635,18 +707,24 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
   p.res = res; p.res_kind = res_kind; p.ldr = ldr; p.res_scale = res_scale; p.res_zero = res_zero;
   // 256 × 128 tiles; K ≤ 64 (VGG's 64-channel 224² convs, a quarter of the int8 net's time) takes a
   // 256 × 64 tile instead of leaving half of every 128-wide tile's MFMA work and staging idle
-  constexpr int BM = 256;
   const int BN = K <= 64 ? 64 : 128;
+  const bool short_k = KT <= 2 && BN == 128;  // 128 × 128 tiles, 2-deep ring, two blocks per CU
+  const int BM = short_k ? 128 : 256;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles);
+  if (short_k) {
+    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 2, 2>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 1, 2>), g, dim3(256), 0, s, p);
+    BIGDL_CHECK_LAUNCH();
+  }
   if (BN == 64) {
-    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<BM, 64, 4, 2, 2>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_i8<BM, 64, 4, 2, 1>), g, dim3(512), 0, s, p);
+    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<256, 64, 4, 2, 2>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_i8<256, 64, 4, 2, 1>), g, dim3(512), 0, s, p);
   } else {
-    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<BM, 128, 4, 2, 2>), g, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_i8<BM, 128, 4, 2, 1>), g, dim3(512), 0, s, p);
+    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<256, 128, 4, 2, 2>), g, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((k_conv_i8<256, 128, 4, 2, 1>), g, dim3(512), 0, s, p);
   }
   BIGDL_CHECK_LAUNCH();
 }

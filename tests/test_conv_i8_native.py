@@ -31,6 +31,9 @@ SHAPES = [  # N, C, H, K, R, stride, pad, dilation
     (2, 832, 7, 384, 1, 1, 0, 1),
     (2, 96, 15, 128, 3, 1, 1, 1),     # … and with padded taps
     (2, 16, 12, 32, 5, 1, 2, 1),
+    (2, 64, 28, 256, 1, 1, 0, 1),     # short reductions (≤ 2 k-tiles): 128 × 128 tiles, 2-deep ring
+    (2, 128, 14, 512, 1, 1, 0, 1),
+    (3, 256, 14, 520, 1, 2, 0, 1),    # … strided, K tail
 ]
 
 
