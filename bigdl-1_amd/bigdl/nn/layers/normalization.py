@@ -106,13 +106,24 @@ class BatchNormalization(TensorModule):
         return self
 
     def _sync_active(self):
-        if not (self._sync and _dist_ready(self._sync_force)):
+        if not self._sync:
             return False
-        if config.get_property("bigdl.bn.syncOneRankLocal") and self._sync_world() == 1:
+        # asked ~7 times per BN call: cached against the process group, the sync settings and the
+        # property version (the uncached checks cost ~37 µs of host time per BN call, enough to make
+        # the ResNet-50 step host-bound under SyncBN)
+        import torch.distributed as dist
+        pg = dist.distributed_c10d.GroupMember.WORLD if dist.is_available() else None
+        token = (id(pg), id(self._sync_group), self._sync_force, config.version())
+        c = self.__dict__.get("_sa_cache")
+        if c is not None and c[0] == token:
+            return c[1]
+        on = _dist_ready(self._sync_force)
+        if on and config.get_property("bigdl.bn.syncOneRankLocal") and self._sync_world() == 1:
             # a one-rank group: the all-reduce is the identity and the global statistics ARE the
             # local ones, so the local finalize+apply kernels run (the launch count of local BN)
-            return False
-        return True
+            on = False
+        self.__dict__["_sa_cache"] = (token, on)
+        return on
 
     def _sync_world(self):
         import torch.distributed as dist
@@ -273,7 +284,7 @@ class BatchNormalization(TensorModule):
         defer = (self.__dict__.pop("_defer_next", False) and residual is None and not relu and x.is_cuda
                  and x.dtype == torch.bfloat16)  # the bf16 native path only (fp32 keeps its own kernels)
         deferred_res = isinstance(residual, BNOut)
-        if deferred_res and not (self.train and not self._sync_active()):
+        if deferred_res and not self.train:
             residual, deferred_res = residual.dense(), False
         if residual is not None and not deferred_res and residual.dim() == 4:
             residual = to_device_layout(residual)
@@ -284,7 +295,7 @@ class BatchNormalization(TensorModule):
         self._last_relu = relu
         if self.train:
             if self._sync_active():
-                y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib)
+                y, mean, invstd = self._sync_forward(x, g, b, relu, residual, ib, defer=defer)
             else:
                 r = NotImplemented
                 C_ = x.shape[1]
@@ -383,12 +394,14 @@ class BatchNormalization(TensorModule):
             return NO
         return R
 
-    def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None):
+    def _sync_forward(self, x, g, b, relu=False, residual=None, in_bias=None, defer=False):
         """SyncBN forward (``SpatialBatchNormalization.scala:1114-1151``): this rank's shifted sums
         [Σ(x−K), Σ(x−K)², rows] (from the producing conv's epilogue partials when it left them) →
         ONE all-reduce of 2·C + 1 floats → finalize over the global row count (read on the device:
         no host sync, and ranks with uneven batches still issue identical collectives) → apply
-        (+residual, ReLU).  K is the running mean, identical on every rank."""
+        (+residual, ReLU).  K is the running mean, identical on every rank.  As in the local path, a
+        projection-shortcut BN (``defer``) only finalizes and returns its output deferred
+        (:class:`~bigdl.ops.reference.BNOut`), and the block tail applies it inside its own pass."""
         from ...ops import reference as R
         impl = self._sync_ops(x)
         C_ = x.shape[1]
@@ -416,13 +429,15 @@ class BatchNormalization(TensorModule):
             kw = dict(mean_out=nxt) if (m is not R and nxt is not None) else {}
             r = m.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar, self.momentum,
                                        self.eps, relu=relu, residual=residual, in_bias=in_bias, coef_out=coef,
-                                       bits_out=bits if m is not R else None, **kw)
+                                       bits_out=bits if (m is not R and not defer) else None, apply=not defer, **kw)
             if r is NotImplemented and m is not R:
                 m = R
                 r = R.bn_forward_from_sums(x, sums, 0, shift, g, b, self.runningMean, self.runningVar,
                                            self.momentum, self.eps, relu=relu, residual=residual, in_bias=in_bias,
-                                           coef_out=coef)
+                                           coef_out=coef, apply=not defer)
             if r is not NotImplemented:
+                if r[0] is None:  # finalize only: the fused block tail applies it
+                    r = (R.BNOut(x, coef, relu=bool(relu)),) + tuple(r[1:])
                 self._relu_bits = bits if m is not R else None
                 self._sync_path = "native" if m is not R else "reference"
                 self._last_input = x

@@ -72,11 +72,21 @@ class Reshape(TensorModule):
 
     def updateOutput(self, input):
         if (self.batchMode is False) or (self.batchMode is None and input.numel() == self.nElement):
-            return input.reshape(self.size)
-        return input.reshape([input.shape[0]] + self.size)
+            return _keep_qtags(input.reshape(self.size), input)
+        return _keep_qtags(input.reshape([input.shape[0]] + self.size), input)
 
     def updateGradInput(self, input, gradOutput):
         return gradOutput.reshape(input.shape)
+
+
+def _keep_qtags(y, x):
+    """A reshaped int8 activation of a quantised chain keeps its scale tags (the 0x80 padding tail
+    only when the reshape is a view of the same memory)."""
+    if x.dtype == torch.int8 and getattr(x, "_qscale", None) is not None:
+        y._qscale = x._qscale
+        y._qzero = getattr(x, "_qzero", 0)
+        y._qtail = bool(getattr(x, "_qtail", False)) and y.data_ptr() == x.data_ptr()
+    return y
 
 
 class View(TensorModule):
@@ -92,10 +102,10 @@ class View(TensorModule):
     def updateOutput(self, input):
         n = int(np.prod([s for s in self.sizes if s != -1]))
         if self.numInputDims > 0 and input.dim() > self.numInputDims:
-            return input.reshape([input.shape[0]] + self.sizes)
+            return _keep_qtags(input.reshape([input.shape[0]] + self.sizes), input)
         if -1 not in self.sizes and input.numel() != n:
-            return input.reshape([input.shape[0]] + self.sizes)
-        return input.reshape(self.sizes)
+            return _keep_qtags(input.reshape([input.shape[0]] + self.sizes), input)
+        return _keep_qtags(input.reshape(self.sizes), input)
 
     def updateGradInput(self, input, gradOutput):
         return gradOutput.reshape(input.shape)
@@ -114,7 +124,7 @@ class InferReshape(TensorModule):
         out = [src[i] if s == 0 else s for i, s in enumerate(self.size)]
         if self.batchMode:
             out = [input.shape[0]] + out
-        return input.reshape(out)
+        return _keep_qtags(input.reshape(out), input)
 
     def updateGradInput(self, input, gradOutput):
         return gradOutput.reshape(input.shape)

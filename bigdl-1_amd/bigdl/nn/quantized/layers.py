@@ -111,10 +111,59 @@ class Linear(_QuantizedBase):
         q._quantize_weight(m.weight)
         if m.bias is not None:
             q.qbias = m.bias.detach().float().clone().cpu()
+        q.static_scale = calibrated_scale(m)
         q.set_name(m.get_name())
         return q.to(m.weight.device)
 
+    def _u8_bias(self, sx, dev):
+        """The bias with the offset term of an unsigned (offset −128) int8 input of scale ``sx``:
+        128·sx·sw[n]·Σ_k w[n][k] (padding columns are 0), cached per (device, scale)."""
+        key = (dev, sx)
+        t = getattr(self, "_lin_u8", None)
+        if t is None or t[0] != key:
+            w = self.qweight.to(dev).to(torch.int32).sum(-1).double()
+            b = self.bias_f.to(dev).double() if self.bias_f is not None else torch.zeros_like(w)
+            t = self._lin_u8 = (key, (b + 128.0 * w * float(sx) * self.weight_scale.to(dev).double()).float())
+        return t[1]
+
+    def _native_static(self, x):
+        """Calibrated int8 path (the reference's int8 FC, quantized/Linear.scala, with MKL-DNN's static
+        scales): an int8 input from the chain (tagged ``_qscale``) is used as is, an fp32 / bf16 input is
+        quantised with the calibrated scale in one pass; split-K int8 GEMM with bias, ReLU and — when
+        the next layer is a quantised Linear — the requantised int8 output in its epilogue."""
+        from ...ops import native_ops as NO
+        if not (x.is_cuda and x.dim() == 2 and ops.native_has("gemm_i8")):
+            return NotImplemented
+        M, K = x.shape
+        kp = self.qweight.shape[1]
+        dev = x.device
+        if x.dtype == torch.int8:
+            sx = getattr(x, "_qscale", None)
+            if sx is None:
+                return NotImplemented
+            z = getattr(x, "_qzero", 0)
+            qa = x.contiguous()
+        elif self.static_scale is not None and x.dtype in (torch.float32, torch.bfloat16):
+            sx, z = self.static_scale, 0
+            qa = NO.quant_static(x.contiguous(), sx)
+            if qa is NotImplemented:
+                return NotImplemented
+        else:
+            return NotImplemented
+        if kp != K:
+            qa = torch.nn.functional.pad(qa, (0, kp - K))  # weight padding columns are 0
+        qw = self.qweight if self.qweight.device == dev else self.qweight.to(dev)
+        bias = self._u8_bias(sx, dev) if z else (self.bias_f.to(dev) if self.bias_f is not None else None)
+        return NO.gemm_i8_static(qa, sx, qw, self.weight_scale.to(dev), bias, out_dtype=torch.bfloat16,
+                                 relu=self._relu_fused, out_scale=self._out_qscale, out_u8=self._out_u8)
+
     def updateOutput(self, input):
+        x2 = input if input.dim() == 2 else input.reshape(1, -1)
+        if x2.dtype == torch.int8 and x2 is not input:
+            _retag(x2, input)
+        y = self._native_static(x2)
+        if y is not NotImplemented:
+            return y if input.dim() == 2 else _retag(y.reshape(-1), y)
         if input.dtype == torch.int8:
             input = dequant(input)
         x = input if input.dim() == 2 else input.reshape(1, -1)

@@ -260,13 +260,17 @@ def _link_units(units):
     from ..layers.dropout import Dropout
     from ...ops import native_ops as NO
     from ...utils import config
+    from ..layers.shape import View, Reshape, InferReshape
     u8 = bool(config.get_property("bigdl.int8.unsignedActivations"))
+    flat = (View, Reshape, InferReshape)
     for i, a in enumerate(units):
         is_block = isinstance(a, Int8ResidualBlock)
-        if not (is_block or (isinstance(a, Q.SpatialConvolution) and a.nGroup == 1 and a.nOutputPlane % 16 == 0)):
+        is_fc = isinstance(a, Q.Linear)
+        if not (is_block or is_fc or (isinstance(a, Q.SpatialConvolution) and a.nGroup == 1
+                                      and a.nOutputPlane % 16 == 0)):
             continue
         j, relu = i + 1, None
-        while j < len(units) and isinstance(units[j], (Threshold, SpatialMaxPooling, Dropout, L.Identity)):
+        while j < len(units) and isinstance(units[j], (Threshold, SpatialMaxPooling, Dropout, L.Identity) + flat):
             m = units[j]
             if isinstance(m, Threshold):
                 if not (m.threshold == 0.0 and m.value == 0.0):
@@ -278,9 +282,13 @@ def _link_units(units):
             continue
         b = units[j]
         head = b.head() if isinstance(b, Int8ResidualBlock) else b
-        if not isinstance(head, Q.SpatialConvolution):
+        if isinstance(head, Q.Linear):
+            # the classifier head: conv / pool → flatten → FC, FC → ReLU → dropout → FC (int8 FC head)
+            if head.static_scale is None or (is_fc and any(isinstance(m, SpatialMaxPooling) for m in units[i + 1:j])):
+                continue
+        elif not isinstance(head, Q.SpatialConvolution) or is_fc or any(isinstance(m, flat) for m in units[i + 1:j]):
             continue
-        if head.static_scale is None or head.nGroup != 1 or not NO.conv_i8_supported(
+        elif head.static_scale is None or head.nGroup != 1 or not NO.conv_i8_supported(
                 a.tail.nOutputPlane if is_block else a.nOutputPlane, head.kernelH, head.kernelW):
             continue
         if any(isinstance(m, Threshold) and not (m.threshold == 0.0 and m.value == 0.0) for m in units[i + 1:j]):

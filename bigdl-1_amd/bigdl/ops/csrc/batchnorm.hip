@@ -1114,15 +1114,19 @@ BIGDL_EXPORT int bigdl_bn_partials_sums2(const float* partial, int G, int C, flo
 }
 
 // Forward from GLOBAL sums (2C, shifted by kshift): finalize over `count` rows (all ranks; 0 = the
-// all-reduced count stored at sums[2C]), apply to this rank's M rows.
-BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y, long long M, long long count, int C,
-                                         const float* gamma, const float* beta, const float* in_bias,
-                                         float* run_mean, float* run_var, float momentum, float eps,
-                                         float* save_mean, float* save_invstd, const float* sums,
+// all-reduced count stored at sums[2C]), apply to this rank's M rows.  y == null: finalize only (a
+// SyncBN shortcut BN whose apply is deferred into the block tail's); rcoef (with res): the residual is
+// a deferred BN output res·rcoef[c] + rcoef[C + c], applied inside this pass (as
+// bigdl_bn_fwd_train_partials2).
+BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, const float* rcoef, void* y, long long M,
+                                         long long count, int C, const float* gamma, const float* beta,
+                                         const float* in_bias, float* run_mean, float* run_var, float momentum,
+                                         float eps, float* save_mean, float* save_invstd, const float* sums,
                                          const float* kshift, float* coef, int relu, void* bits, unsigned* ticket,
                                          hipStream_t s) {
-  if (C % 8 || M <= 0 || count < 0 || (bits && !relu)) return (int)hipErrorInvalidValue;
-  if (ticket && C <= 8192) {
+  if (C % 8 || M <= 0 || count < 0 || (bits && !relu) || (rcoef && !res) || (!y && (res || bits)))
+    return (int)hipErrorInvalidValue;
+  if (ticket && C <= 8192 && y && !rcoef) {
     // ONE launch: every block derives its channels' coefficients from the global sums, the last
     // arriver writes the saved statistics / coefficients / running statistics (k_bn_apply_fin)
     BnFwdFin f{const_cast<float*>(sums), kshift, gamma, beta, in_bias, run_mean, run_var, save_mean, save_invstd, coef,
@@ -1144,7 +1148,7 @@ BIGDL_EXPORT int bigdl_bn_fwd_train_sums(const void* x, const void* res, void* y
   hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 31) / 32), dim3(32 * kFinRG), 0, s, (const bf16_t*)nullptr, kshift, sums,
                      1, count, C, gamma, beta, in_bias, run_mean, run_var, momentum, eps, save_mean, save_invstd, coef,
                      coef + C, count == 0 ? sums + 2 * C : nullptr);
-  launch_apply(x, res, y, M, C, coef, relu, bits, s);
+  if (y) launch_apply(x, res, y, M, C, coef, relu, bits, s, rcoef);
   BIGDL_CHECK_LAUNCH();
 }
 

@@ -82,9 +82,11 @@ __device__ __forceinline__ void i8_res4(const ConvI8Params& p, int m, int n, flo
 // NS: LDS ring depth — 3 (the k-loop pipeline), or 2 for the short reductions (KT ≤ 2: the 1×1 convs
 // over ≤ 256 channels) on 128-row tiles, where the launch is load → one or two MFMA tiles → store and
 // two blocks per CU overlap one block's epilogue with the other's loads (one 147 KB block per CU did not)
-template <int BM, int BN, int WM, int WN, int TPT, int NS = 3>
-__global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? 2 : 1) k_conv_i8(ConvI8Params p) {
-  static_assert(NS == 2 || NS == 3, "LDS ring depth");
+// NS == 1 (KT == 1 launches only: the 1×1 convs over ≤ 128 channels, or C = 64): no ring at all.
+// MINB: blocks per CU the register budget is sized for.
+template <int BM, int BN, int WM, int WN, int TPT, int NS = 3, int MINB = (NS == 2 ? 2 : 1)>
+__global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) {
+  static_assert(NS >= 1 && NS <= 3, "LDS ring depth");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int GA = BN / 8 / NW, GB = BM / 8 / NW;
@@ -664,6 +666,21 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
                                     int dh, int dw, int relu, int x_u8, int y_u8, const void* res, int res_kind,
                                     int ldr, float res_scale, float res_zero, hipStream_t s);
 
+// default 0.  Alone (tools/i8_shortk_bench.py, batch 256) variant 2 is faster on every single-k-tile
+// shape (64→256 at 56² with the residual 326 → 285 µs, 128→512 at 28² 137.5 → 118), but inside the
+// int8 ResNet-50 forward it is slower: 5.33 vs 4.96 ms per batch (gpurun_out r6ab, profiles/r6_int8.txt)
+static int g_i8_shortk = [] {
+  const char* e = getenv("BIGDL_I8_SHORTK");
+  return e ? atoi(e) : 0;
+}();
+
+// the short-K tile variant (measurement hook: tools/i8_shortk_bench.py); returns the previous one
+BIGDL_EXPORT int bigdl_conv_i8_set_shortk(int v) {
+  const int old = g_i8_shortk;
+  if (v >= 0 && v <= 2) g_i8_shortk = v;
+  return old;
+}
+
 BIGDL_EXPORT int bigdl_conv_i8_fwd3(const void* x, const void* w, int ldw, const float* sx, float sxs, const float* swt,
                                     const float* bias, void* y, void* yq, float out_scale, int ldy, int Nb, int H,
                                     int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
@@ -708,15 +725,26 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
   // 256 × 128 tiles; K ≤ 64 (VGG's 64-channel 224² convs, a quarter of the int8 net's time) takes a
   // 256 × 64 tile instead of leaving half of every 128-wide tile's MFMA work and staging idle
   const int BN = K <= 64 ? 64 : 128;
-  const bool short_k = KT <= 2 && BN == 128;  // 128 × 128 tiles, 2-deep ring, two blocks per CU
-  const int BM = short_k ? 128 : 256;
+  const bool short_k = KT <= 2 && BN == 128;  // short reductions: small tiles, several blocks per CU
+  // short-K tile (g_i8_shortk): 0 = 128 × 128, 2-deep ring, 2 blocks/CU; 1 = 64 × 128, 2-deep ring,
+  // 3 blocks/CU; 2 = as 1, and for a single k-tile no ring (32 KB of LDS, 5 blocks/CU)
+  const int sk = short_k ? g_i8_shortk : 0;
+  const int BM = short_k ? (sk ? 64 : 128) : 256;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles);
   if (short_k) {
-    if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 2, 2>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 1, 2>), g, dim3(256), 0, s, p);
+    if (sk == 2 && KT == 1) {
+      if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 2, 1, 5>), g, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 1, 1, 5>), g, dim3(256), 0, s, p);
+    } else if (sk == 1) {
+      if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 2, 2, 3>), g, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 1, 2, 3>), g, dim3(256), 0, s, p);
+    } else {
+      if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 2, 2>), g, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((k_conv_i8<128, 128, 2, 2, 1, 2>), g, dim3(256), 0, s, p);
+    }
     BIGDL_CHECK_LAUNCH();
   }
   if (BN == 64) {

@@ -413,24 +413,34 @@ def _ticket(dev):
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
-                         residual=None, in_bias=None, coef_out=None, bits_out=None, mean_out=None):
+                         residual=None, in_bias=None, coef_out=None, bits_out=None, mean_out=None, apply=True):
     """Training BN from GLOBAL shifted sums over ``count`` rows (0: the all-reduced count at
     ``sums[2C]``): (y, save_mean, save_invstd).  ``bits_out`` (uint8 [M·C/8], with ``relu``): the
-    output's ReLU mask as bits for a block-tail consumer's dgrad epilogue."""
+    output's ReLU mask as bits for a block-tail consumer's dgrad epilogue.  ``apply=False``: finalize
+    only (``coef_out`` required, y = None: a deferred shortcut BN); ``residual`` may be such a deferred
+    BN output (:class:`~bigdl.ops.reference.BNOut`), applied inside this pass."""
     rc = _rows_c(x)
     if rc is None:
         return NotImplemented
     M, C_ = rc
     if not _bn_ok(x, C_) or not all(_f32vec(t, C_) for t in (gamma, beta, running_mean, running_var, in_bias, shift)):
         return NotImplemented
+    rcoef = None
+    if isinstance(residual, R_.BNOut):
+        if residual.relu or not (residual.x.shape == x.shape and residual.x.stride() == x.stride()
+                                 and residual.x.dtype == _bf16 and _al16(residual.x) and _f32vec(residual.coef, 2 * C_)):
+            return NotImplemented
+        residual, rcoef = residual.x, residual.coef
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride() or
                                  residual.dtype != _bf16 or not _al16(residual)):
+        return NotImplemented
+    if not apply and (residual is not None or bits_out is not None or not _coef_ok(coef_out, C_)):
         return NotImplemented
     coef = coef_out if _coef_ok(coef_out, C_) else torch.empty(2 * C_, dtype=_f32, device=x.device)
     mean = mean_out if _f32vec(mean_out, C_) and mean_out is not None else torch.empty(C_, dtype=_f32, device=x.device)
     invstd = torch.empty(C_, dtype=_f32, device=x.device)
-    y = torch.empty_like(x)
-    check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
+    y = torch.empty_like(x) if apply else None
+    check(_lib().bigdl_bn_fwd_train_sums(ptr(x), ptr(residual), ptr(rcoef), ptr(y), _ll(M), _ll(count), C.c_int(C_), ptr(gamma),
                                          ptr(beta), ptr(in_bias), ptr(running_mean), ptr(running_var), _f(momentum),
                                          _f(eps), ptr(mean), ptr(invstd), ptr(sums), ptr(shift), ptr(coef),
                                          C.c_int(1 if relu else 0), ptr(bits_out if relu else None),
@@ -2014,6 +2024,47 @@ def gemm_i8(qa, sa, qb, sb, bias=None, out_dtype=torch.float32, relu=False):
     check(_lib().bigdl_gemm_i8(ptr(qa), ptr(qb), C.c_int(M), C.c_int(N), C.c_int(Kp), ptr(sa), ptr(sb), ptr(b),
                                ptr(out), C.c_int(1 if out_dtype == _bf16 else 0), C.c_int(1 if relu else 0), _s()),
           "gemm_i8")
+    return out
+
+
+def _i8_splits(M, N, Kp):
+    """Split-K factor of an int8 GEMM: whole-K 128×128 tiles fill ≥ 2 waves of the 256 CUs already,
+    else split the reduction (≥ 4 k-tiles per split) until they do."""
+    tiles = -(-M // 128) * -(-N // 128)
+    kt = -(-Kp // 128)
+    if tiles >= 512 or kt < 8:
+        return 1
+    return max(1, min(kt // 4, -(-512 // tiles)))
+
+
+def gemm_i8_static(qa, sa0, qb, sb, bias=None, out_dtype=torch.bfloat16, relu=False, out_scale=None, out_u8=False):
+    """int8 GEMM of a statically quantised activation ``qa`` [M][Kp] (one scale ``sa0``) with per-row
+    int8 weights ``qb`` [N][Kp] (scales ``sb``): bias, ReLU, then ``out_dtype`` or — ``out_scale`` — the
+    next quantised layer's int8 input (tagged; ``out_u8``: the offset unsigned code of a ReLU'd
+    output).  Split-K for small-M, long-K products (classifier heads)."""
+    if qa.dtype != torch.int8 or qb.dtype != torch.int8 or qa.dim() != 2 or qa.shape[1] != qb.shape[1] \
+            or qa.shape[1] % 16 or not (sa0 and sa0 > 0):
+        return NotImplemented
+    if not (qa.is_contiguous() and qb.is_contiguous() and _al16(qa) and _al16(qb)) or out_dtype not in (_f32, _bf16):
+        return NotImplemented
+    M, Kp = qa.shape
+    N = qb.shape[0]
+    sb = sb.float().contiguous()
+    b = bias.float().contiguous() if bias is not None else None
+    if out_scale is not None:
+        out = torch.empty((M, N), dtype=torch.int8, device=qa.device)
+    else:
+        out = torch.empty((M, N), dtype=out_dtype, device=qa.device)
+    splits = _i8_splits(M, N, Kp)
+    work = torch.empty(splits * M * N, dtype=torch.int32, device=qa.device) if splits > 1 else None
+    check(_lib().bigdl_gemm_i8_ex(ptr(qa), ptr(qb), C.c_int(M), C.c_int(N), C.c_int(Kp), None, C.c_float(sa0), ptr(sb),
+                                  ptr(b), ptr(out), C.c_int(1 if out_dtype == _bf16 else 0), C.c_int(1 if relu else 0),
+                                  C.c_float(out_scale if out_scale is not None else 0.0),
+                                  C.c_int(1 if (out_scale is not None and out_u8) else 0), C.c_int(splits), ptr(work),
+                                  _s()), "gemm_i8_ex")
+    if out_scale is not None:
+        _tag(out, out_scale, out_u8)
+        out._qtail = False
     return out
 
 

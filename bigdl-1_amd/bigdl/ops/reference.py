@@ -309,8 +309,9 @@ def bn_local_sums(x, shift, partial=None, G=0, rezero=False):
 
 
 def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, running_var, momentum, eps, relu=False,
-                         residual=None, in_bias=None, coef_out=None, bits_out=None):
-    """Training BN from GLOBAL shifted sums over ``count`` rows (0: ``sums[2C]``)."""
+                         residual=None, in_bias=None, coef_out=None, bits_out=None, apply=True):
+    """Training BN from GLOBAL shifted sums over ``count`` rows (0: ``sums[2C]``); ``apply=False``:
+    finalize only (y = None, ``coef_out`` filled); ``residual`` may be a deferred :class:`BNOut`."""
     C = x.shape[1]
     dims, shape = _bn_dims(x)
     n = sums[2 * C].double() if count == 0 else torch.tensor(float(count), dtype=torch.float64, device=x.device)
@@ -331,7 +332,11 @@ def bn_forward_from_sums(x, sums, count, shift, gamma, beta, running_mean, runni
     if coef_out is not None:
         coef_out[:C].copy_(sc)
         coef_out[C:2 * C].copy_(sh)
+    if not apply:
+        return None, mean, invstd
     y = acc_float(x) * sc.view(shape) + sh.view(shape)
+    if isinstance(residual, BNOut):
+        residual = residual.dense()
     if residual is not None:
         y = y + acc_float(residual)
     if relu:

@@ -382,6 +382,8 @@ class DistriOptimizer(BaseOptimizer):
 
     def _reduce_scalar(self, t):
         if not self._drop_mode():
+            if self.world == 1:  # a one-rank all-reduce is the identity: no collective per step
+                return t
             return comm.allreduce_scalar(t, average=True)
         return self._drop_decide(t)
 

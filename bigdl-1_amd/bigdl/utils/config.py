@@ -139,10 +139,20 @@ def get_property(key: str, default=None):
     return dflt if default is None else default
 
 
+_VERSION = [0]
+
+
+def version() -> int:
+    """A counter bumped by every ``set_property`` / ``clear_property``: per-call decisions derived
+    from properties can be cached against it (environment overrides are read at first use)."""
+    return _VERSION[0]
+
+
 def set_property(key: str, value):
     typ = _REGISTRY.get(key, (type(value), None, ""))[0]
     with _lock:
         _overrides[key] = _coerce(typ, value)
+        _VERSION[0] += 1
     for fn in _listeners.get(key, ()):
         fn(get_property(key))
 
@@ -150,6 +160,7 @@ def set_property(key: str, value):
 def clear_property(key: str):
     with _lock:
         _overrides.pop(key, None)
+        _VERSION[0] += 1
     for fn in _listeners.get(key, ()):
         fn(get_property(key))
 
