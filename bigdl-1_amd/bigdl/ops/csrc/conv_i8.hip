@@ -129,12 +129,21 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
   int cinj[GB];  // TPT == 1: this lane's channel offset inside the k-tile (C % 128 != 0: the last k-tile
                  // of a tap is partial, its chunks past C read the pad code)
   int hi_half = 0;
+  const bool pointwise = p.R == 1 && p.S == 1 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 &&
+                         p.P == p.H && p.Q == p.W;
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = 8 * (wid + NW * j) + lrow;
     const int chunk = slot ^ ((row >> 1) & 7);
     hi_half = chunk >> 2;  // the same for every j (rows 8 apart share (row >> 1) & 7 … per group)
     const int m = m0 + row;
+    const int cin = TPT == 2 ? (chunk & 3) * 16 : chunk * 16;
+    cinj[j] = cin;
+    if (pointwise) {  // output pixel m reads input pixel m: no index divisions, one tap
+      rbase[j] = m * p.C + cin;
+      vmask[j] = m < p.M ? 1ull : 0ull;
+      continue;
+    }
     int img = -1, h = 0, w = 0;
     if (m < p.M) {
       const int n = m / (p.P * p.Q);
@@ -144,8 +153,6 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
       h = pp * p.sh - p.ph;
       w = qq * p.sw - p.pw;
     }
-    const int cin = TPT == 2 ? (chunk & 3) * 16 : chunk * 16;
-    cinj[j] = cin;
     rbase[j] = ((img * p.H + h) * p.W + w) * p.C + cin;
     uint64_t msk = 0;
     if (img >= 0) {
@@ -283,34 +290,41 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
     const int m = m0 + (b_row0 - BN) + 32 * j + pm;
     sxm[j] = m < p.M ? (p.sx ? p.sx[m / (p.P * p.Q)] : p.sxs) : 0.f;
   }
-  const float qlo = p.y_u8 ? 0.f : -127.f, qhi = p.y_u8 ? 255.f : 127.f, qoff = p.y_u8 ? 128.f : 0.f;
   if (p.yq && p.res_kind) {
     // conv + sum with an int8 output: park the dequantised tile as fp32 [BM][BN] (16-B chunk c of row r
     // at c ^ (r & (BN/4 − 1))), then a row-major pass adds the residual with whole-row reads (16
     // consecutive channels per thread), applies the ReLU, requantises and stores 16 B — the residual
     // is never read in the accumulator layout (32 rows × 4 B per wave-instruction)
+    // The tile holds the pre-rounding code t = v/out_scale + cadd (+ the residual's constant term
+    // for an int8 residual), so the row pass is one fma per element before the rounding.
     constexpr int CPRF = BN / 4;
     float* ef = reinterpret_cast<float*>(lds);
+    const float cadd = (p.y_u8 ? 0.f : 128.f) +
+                       (p.res_kind == 1 ? (p.res_zero - 128.f) * p.res_scale * p.out_inv : 0.f);
+    const bool stat = p.sx == nullptr;
 #pragma unroll
     for (int i = 0; i < TNI; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
-        float s4[4], b4[4];
+        float a4[4], c4[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int n = n0 + nl + e;
-          s4[e] = n < p.K ? p.swt[n] : 0.f;
-          b4[e] = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+          const float sw = n < p.K ? p.swt[n] : 0.f;
+          const float b = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+          a4[e] = sw * p.out_inv * (stat ? p.sxs : 1.f);
+          c4[e] = fmaf(b, p.out_inv, cadd);
         }
 #pragma unroll
         for (int j = 0; j < TMI; ++j) {
           const int ml = (b_row0 - BN) + 32 * j + pm;
+          const float sj = stat ? 1.f : sxm[j];
           float4 v;
-          v.x = fmaf((float)acc[i][j][4 * g + 0] * sxm[j], s4[0], b4[0]);
-          v.y = fmaf((float)acc[i][j][4 * g + 1] * sxm[j], s4[1], b4[1]);
-          v.z = fmaf((float)acc[i][j][4 * g + 2] * sxm[j], s4[2], b4[2]);
-          v.w = fmaf((float)acc[i][j][4 * g + 3] * sxm[j], s4[3], b4[3]);
+          v.x = fmaf((float)acc[i][j][4 * g + 0] * sj, a4[0], c4[0]);
+          v.y = fmaf((float)acc[i][j][4 * g + 1] * sj, a4[1], c4[1]);
+          v.z = fmaf((float)acc[i][j][4 * g + 2] * sj, a4[2], c4[2]);
+          v.w = fmaf((float)acc[i][j][4 * g + 3] * sj, a4[3], c4[3]);
           *reinterpret_cast<float4*>(ef + ml * BN + (((nl >> 2) ^ (ml & (CPRF - 1))) << 2)) = v;
         }
       }
@@ -326,25 +340,39 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
         const float4 f = *reinterpret_cast<const float4*>(ef + row * BN + (((g16 * 4 + c) ^ (row & (CPRF - 1))) << 2));
         v[4 * c] = f.x; v[4 * c + 1] = f.y; v[4 * c + 2] = f.z; v[4 * c + 3] = f.w;
       }
+      if (p.res_kind == 1) {
+        // the int8 residual's 16 codes in one load; code q → q + 128 = byte ^ 0x80 as an unsigned
+        // byte (v_cvt_f32_ubyteN): value (q + res_zero)·s = ub·s + (res_zero − 128)·s, the constant
+        // already in the tile
+        const uint4 rq = *reinterpret_cast<const uint4*>((const int8_t*)p.res + (size_t)m * p.ldr + n);
+        const uint32_t rw[4] = {rq.x ^ 0x80808080u, rq.y ^ 0x80808080u, rq.z ^ 0x80808080u, rq.w ^ 0x80808080u};
+        const float rs = p.res_scale * p.out_inv;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float r4[4];
-        i8_res4(p, m, n + 4 * c, r4);
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * c + e] += r4[e];
+          for (int e = 0; e < 4; ++e)
+            v[4 * c + e] = fmaf((float)((rw[c] >> (8 * e)) & 0xFFu), rs, v[4 * c + e]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float r4[4];
+          i8_res4(p, m, n + 4 * c, r4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * c + e] = fmaf(r4[e], p.out_inv, v[4 * c + e]);
+        }
       }
+      const float ulo = p.y_u8 ? 0.f : (p.relu ? 128.f : 1.f);
       uint32_t w4[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         uint32_t packed = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float x = v[4 * c + e];
-          if (p.relu) x = fmaxf(x, 0.f);
-          const float r = fminf(fmaxf(rintf(x * p.out_inv), qlo), qhi) - qoff;
-          packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+          // an exact integer in [0, 255]: the byte convert-and-insert needs no rounding of its own
+          const float u = __builtin_amdgcn_fmed3f(rintf(v[4 * c + e]), ulo, 255.f);
+          packed = __builtin_amdgcn_cvt_pk_u8_f32(u, e, packed);
         }
-        w4[c] = packed;
+        w4[c] = packed ^ 0x80808080u;
       }
       *reinterpret_cast<uint4*>(p.yq + (size_t)m * p.ldy + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
@@ -355,35 +383,52 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
   }
   if (p.yq) {
     // int8 output: requantise with the consumer's static scale and park the tile as bytes
-    // ([BM][BN], 16-B chunk c of row r at chunk c ^ (r & 7)), then one 16-B store per chunk
+    // ([BM][BN], 16-B chunk c of row r at chunk c ^ (r & 7)), then one 16-B store per chunk.
+    // The code is formed unsigned — u = med3(rint(acc·a + c), lo, 255), a = sx·sw·(1/out_scale),
+    // c = bias/out_scale (+128 for the signed code) — and stored as u ^ 0x80 (the offset u8 code, or
+    // the signed code's two's complement): one fma, one rounding, one clamp per element (the separate
+    // dequantise / ReLU / requantise / clamp / offset / mask sequence made this epilogue VALU-bound on
+    // the short-reduction 1x1 convs: ~1700 VALU per wave for 16 MFMAs)
     int8_t* eq = reinterpret_cast<int8_t*>(lds);
+    const float cadd = p.y_u8 ? 0.f : 128.f;
+    const float ulo = p.y_u8 ? 0.f : (p.relu ? 128.f : 1.f);
+    const bool stat = p.sx == nullptr && !p.res_kind;
 #pragma unroll
     for (int i = 0; i < TNI; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int nl = a_row0 + 32 * i + 8 * g + 4 * fh;
-        float s4[4], b4[4];
+        float a4[4], c4[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int n = n0 + nl + e;
-          s4[e] = n < p.K ? p.swt[n] : 0.f;
-          b4[e] = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+          const float sw = n < p.K ? p.swt[n] : 0.f;
+          const float b = (p.bias && n < p.K) ? p.bias[n] : 0.f;
+          a4[e] = sw * p.out_inv * (stat ? p.sxs : 1.f);
+          c4[e] = fmaf(b, p.out_inv, cadd);
         }
 #pragma unroll
         for (int j = 0; j < TMI; ++j) {
           const int ml = (b_row0 - BN) + 32 * j + pm;
-          float r4[4] = {0.f, 0.f, 0.f, 0.f};
-          if (p.res_kind && m0 + ml < p.M && n0 + nl < p.K) i8_res4(p, m0 + ml, n0 + nl, r4);
           uint32_t packed = 0;
+          if (stat) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], s4[e], b4[e]) + r4[e];
-            if (p.relu) v = fmaxf(v, 0.f);
-            const float r = fminf(fmaxf(rintf(v * p.out_inv), qlo), qhi) - qoff;
-            packed |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+            for (int e = 0; e < 4; ++e) {
+              const float u = __builtin_amdgcn_fmed3f(rintf(fmaf((float)acc[i][j][4 * g + e], a4[e], c4[e])), ulo, 255.f);
+              packed = __builtin_amdgcn_cvt_pk_u8_f32(u, e, packed);
+            }
+          } else {
+            float r4[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p.res_kind && m0 + ml < p.M && n0 + nl < p.K) i8_res4(p, m0 + ml, n0 + nl, r4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaf((float)acc[i][j][4 * g + e] * sxm[j], a4[e], fmaf(r4[e], p.out_inv, c4[e]));
+              const float u = __builtin_amdgcn_fmed3f(rintf(v), ulo, 255.f);
+              packed = __builtin_amdgcn_cvt_pk_u8_f32(u, e, packed);
+            }
           }
           const int off = ml * BN + ((((nl >> 4) ^ (ml & 7)) & (BN / 16 - 1)) << 4) + (nl & 15);
-          *reinterpret_cast<uint32_t*>(eq + off) = packed;
+          *reinterpret_cast<uint32_t*>(eq + off) = packed ^ 0x80808080u;
         }
       }
     __syncthreads();
@@ -666,12 +711,12 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
                                     int dh, int dw, int relu, int x_u8, int y_u8, const void* res, int res_kind,
                                     int ldr, float res_scale, float res_zero, hipStream_t s);
 
-// default 0.  Alone (tools/i8_shortk_bench.py, batch 256) variant 2 is faster on every single-k-tile
-// shape (64→256 at 56² with the residual 326 → 285 µs, 128→512 at 28² 137.5 → 118), but inside the
-// int8 ResNet-50 forward it is slower: 5.33 vs 4.96 ms per batch (gpurun_out r6ab, profiles/r6_int8.txt)
+// default 2 (tools/i8_shortk_bench.py, batch 256: 64→256 at 56² with the residual 266 → 230 µs,
+// 128→512 at 28² 103 → 92.5; the int8 ResNet-50 forward 4.37-4.39 → 4.23 ms per batch in 3 interleaved
+// repeats, VGG16 unchanged — profiles/r6_int8.txt)
 static int g_i8_shortk = [] {
   const char* e = getenv("BIGDL_I8_SHORTK");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 2;
 }();
 
 // the short-K tile variant (measurement hook: tools/i8_shortk_bench.py); returns the previous one
@@ -728,14 +773,15 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
   const bool short_k = KT <= 2 && BN == 128;  // short reductions: small tiles, several blocks per CU
   // short-K tile (g_i8_shortk): 0 = 128 × 128, 2-deep ring, 2 blocks/CU; 1 = 64 × 128, 2-deep ring,
   // 3 blocks/CU; 2 = as 1, and for a single k-tile no ring (32 KB of LDS, 5 blocks/CU)
-  const int sk = short_k ? g_i8_shortk : 0;
+  int sk = short_k ? g_i8_shortk : 0;
+  if (sk == 2 && KT != 1) sk = 0;  // variant 2 differs from 0 on single-k-tile launches only
   const int BM = short_k ? (sk ? 64 : 128) : 256;
   p.tiles_n = (K + BN - 1) / BN;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * p.tiles_n;
   if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)tiles);
   if (short_k) {
-    if (sk == 2 && KT == 1) {
+    if (sk == 2) {
       if (tpt == 2) hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 2, 1, 5>), g, dim3(256), 0, s, p);
       else hipLaunchKernelGGL((k_conv_i8<64, 128, 2, 2, 1, 1, 5>), g, dim3(256), 0, s, p);
     } else if (sk == 1) {

@@ -30,7 +30,11 @@ def main():
     torch.manual_seed(0)
     lib = NO._lib()
     N = 256
-    for (C, K, H, res) in SHAPES:
+    shapes, variants = SHAPES, (0, 1, 2)
+    if len(sys.argv) > 1:  # one shape / variant (PMC passes): C,K,H,res variant
+        c, k, h, r = (int(v) for v in sys.argv[1].split(","))
+        shapes, variants = [(c, k, h, bool(r))], (int(sys.argv[2]) if len(sys.argv) > 2 else 0,)
+    for (C, K, H, res) in shapes:
         w = torch.randn(K, C, 1, 1)
         q, ws = R.quant_rows(w.reshape(K, -1))
         wq, ldw = NO.conv_i8_weight(q.cuda(), K, C, 1, 1)
@@ -43,7 +47,7 @@ def main():
                                                 relu=True, out_scale=0.04, out_u8=True, u8_bias=ub, residual=r)
         byt = N * H * H * (C + K + (K if res else 0))
         outs, line = [], []
-        for v in (0, 1, 2):
+        for v in variants:
             lib.bigdl_conv_i8_set_shortk(v)
             y = f()
             torch.cuda.synchronize()
