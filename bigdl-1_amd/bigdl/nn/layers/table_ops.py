@@ -141,6 +141,20 @@ class JoinTable(TensorModule):
     #: of one common scale
     _i8_join = False
 
+    def _i8_cat_buffer(self, N_, C_, H, W, dev, u8):
+        """This forward's concat output, shared by the producing int8 convs (each writes its channel
+        slice: quantizer._link_graph ``_cat_join``); the 0x80 tail of an unsigned code written once."""
+        from ...ops import native_ops as NO
+        b = self.__dict__.get("_i8buf")
+        if b is None or tuple(b.shape) != (N_, C_, H, W) or b.device != dev or bool(b._qtail) != bool(u8):
+            b = NO._i8_act(N_, C_, H, W, dev, u8)
+            if u8:
+                n = b.numel()
+                b._base.view(-1)[n:n + 16].fill_(-128)
+            b._qtail = bool(u8)
+            self.__dict__["_i8buf"] = b
+        return b
+
     def _int8_cat(self, ts, d):
         """Concat of int8 activations sharing one scale / code (a quantised Inception block): the
         codes are concatenated as they are and the result keeps the tag (+ the 0x80 tail an unsigned
@@ -169,6 +183,19 @@ class JoinTable(TensorModule):
         d = self._d(ts[0])
         self._sizes = [t.shape[d] for t in ts]
         if ts[0].dtype == torch.int8:
+            buf = self.__dict__.pop("_i8buf", None)
+            if buf is not None and d == 1:
+                off, ok = 0, True
+                for t in ts:  # every input is the producer's slice of the shared output, in order
+                    ok = ok and (t.dtype == torch.int8 and t.data_ptr() == buf.data_ptr() + off
+                                 and t.shape[0] == buf.shape[0] and t.shape[2:] == buf.shape[2:]
+                                 and getattr(t, "_qscale", None) == getattr(ts[0], "_qscale", None))
+                    off += t.shape[1]
+                if ok and off == buf.shape[1]:
+                    from ...ops import native_ops as NO
+                    y = NO._tag(buf, ts[0]._qscale, bool(getattr(ts[0], "_qzero", 0)))
+                    y._qtail = bool(getattr(ts[0], "_qzero", 0))
+                    return y
             y = self._int8_cat(ts, d)
             if y is not None:
                 return y

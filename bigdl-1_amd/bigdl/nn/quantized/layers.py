@@ -250,12 +250,28 @@ class SpatialConvolution(_QuantizedBase):
         if NO.conv_i8_supported(C, self.kernelH, self.kernelW):
             prep = self._i8_prep(x, C)
             xin = x if x.dtype == torch.int8 else x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            return NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane,
-                                               self.kernelH, self.kernelW, (self.strideH, self.strideW), (pt, pl),
-                                               (self.dilationH, self.dilationW), self._out_hw(x, pads),
-                                               relu=self._relu_fused, in_scale=self.static_scale,
-                                               out_scale=self._out_qscale, out_u8=self._out_u8,
-                                               u8_bias=self._u8_bias(x, prep, C))
+            out = None
+            cj = self.__dict__.get("_cat_join")
+            if cj is not None and self._out_qscale is not None:
+                # zero-copy concat: write this conv's channel slice of the join's output
+                join, off, ctot = cj
+                P, Q = self._out_hw(x, pads)
+                buf = join._i8_cat_buffer(x.shape[0], ctot, P, Q, x.device, self._out_u8)
+                out = buf[:, off:off + self.nOutputPlane]
+            y = NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane,
+                                            self.kernelH, self.kernelW, (self.strideH, self.strideW), (pt, pl),
+                                            (self.dilationH, self.dilationW), self._out_hw(x, pads),
+                                            relu=self._relu_fused, in_scale=self.static_scale,
+                                            out_scale=self._out_qscale, out_u8=self._out_u8,
+                                            u8_bias=self._u8_bias(x, prep, C), out=out)
+            if y is NotImplemented and out is not None:
+                y = NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane,
+                                                self.kernelH, self.kernelW, (self.strideH, self.strideW), (pt, pl),
+                                                (self.dilationH, self.dilationW), self._out_hw(x, pads),
+                                                relu=self._relu_fused, in_scale=self.static_scale,
+                                                out_scale=self._out_qscale, out_u8=self._out_u8,
+                                                u8_bias=self._u8_bias(x, prep, C))
+            return y
         if x.dtype == torch.int8:
             return NotImplemented
         # a shape the int8 kernel does not tile (the C = 3 RGB stem): bf16 conv with the dequantised

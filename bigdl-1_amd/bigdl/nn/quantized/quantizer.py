@@ -420,6 +420,11 @@ def _link_graph(g):
             cons = _graph_consumers(n)
             if cons and link(prods, cons, sum(c.nOutputPlane for c, _r in prods)):
                 e._i8_join = True
+                # zero-copy concat: each producer writes its channel slice of the join's output
+                ctot, off = sum(c.nOutputPlane for c, _r in prods), 0
+                for c, _r in prods:
+                    c._cat_join = (e, off, ctot)
+                    off += c.nOutputPlane
             continue
         if not (isinstance(e, Q.SpatialConvolution) and e.nGroup == 1 and e.nOutputPlane % 16 == 0
                 and len(n.next_nodes) == 1):
@@ -435,6 +440,18 @@ def _link_graph(g):
         cons = _graph_consumers(src)
         if cons:
             link([(e, relu)], cons, e.nOutputPlane)
+    # a conv whose only consumer is a ReLU but whose output does not chain on in int8 (an LRN, a
+    # float layer follows): the ReLU still runs in the conv's epilogue, the ReLU node passes through
+    from ..layers.activation import Threshold
+    for n in g.forward_order:
+        e = n.element
+        if not (isinstance(e, Q.SpatialConvolution) and len(n.next_nodes) == 1) or e._relu_fused:
+            continue
+        nxt = n.next_nodes[0]
+        if (isinstance(nxt.element, Threshold) and _graph_pass(nxt.element) and len(nxt.prev_nodes) == 1
+                and not getattr(nxt.element, "_i8_fused", False)):
+            e._relu_fused = True
+            nxt.element._passthrough = True
 
 
 def quantize(model):

@@ -376,7 +376,7 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
       }
       *reinterpret_cast<uint4*>(p.yq + (size_t)m * p.ldy + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
-    if (p.y_u8 && blockIdx.x == 0 && tid == 0)
+    if (p.y_u8 && p.ldy == p.K && blockIdx.x == 0 && tid == 0)
       *reinterpret_cast<uint4*>(p.yq + (size_t)p.M * p.ldy) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u,
                                                                          0x80808080u);
     return;
@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
       }
     }
     // the unsigned code's padding tail (the code of 0) for the consumer's padded taps
-    if (p.y_u8 && blockIdx.x == 0 && tid == 0)
+    if (p.y_u8 && p.ldy == p.K && blockIdx.x == 0 && tid == 0)
       *reinterpret_cast<uint4*>(p.yq + (size_t)p.M * p.ldy) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u,
                                                                          0x80808080u);
     return;
@@ -635,6 +635,62 @@ __global__ void __launch_bounds__(256) k_maxpool_i8(const int8_t* __restrict__ x
   }
 }
 
+// Fixed-window form (3x3 and 2x2, the Inception / VGG / ResNet pools): all KH·KW 16-B window loads of
+// a thread issued before the first compare (an out-of-image tap reads the clamped window centre, which
+// is inside the window for pad ≤ 1), 32-bit index math, and the byte max done two bytes per lane of
+// v_pk_max_u16 on the codes flipped to unsigned order (q ^ 0x80 orders the signed and the offset code
+// alike): ~5 VALU per 4 bytes per tap where byte-wise extract / compare / insert took ~11.
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  u16x2_t x = __builtin_bit_cast(u16x2_t, a), y = __builtin_bit_cast(u16x2_t, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+
+template <int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool_i8_k(const int8_t* __restrict__ x, int8_t* __restrict__ y, int Nb,
+                                                      int H, int W, int C, int P, int Q, int sh, int sw, int ph,
+                                                      int pw, int tail) {
+  const uint32_t CG = (uint32_t)C >> 4;
+  const uint32_t total = (uint32_t)Nb * P * Q * CG;
+  if (tail && blockIdx.x == 0 && threadIdx.x == 0)
+    *reinterpret_cast<uint4*>(y + (size_t)total * 16) = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+  for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+    const uint32_t cg = t % CG, pix = t / CG;
+    const uint32_t q = pix % (uint32_t)Q, r = pix / (uint32_t)Q;
+    const uint32_t pp = r % (uint32_t)P, n = r / (uint32_t)P;
+    const int h0 = (int)pp * sh - ph, w0 = (int)q * sw - pw;
+    const int hc = min(max(h0 + KH / 2, 0), H - 1), wc = min(max(w0 + KW / 2, 0), W - 1);
+    // one 64-bit base (the clamped centre), 32-bit tap offsets from it
+    const int8_t* base = x + ((size_t)(n * (uint32_t)H + (uint32_t)hc) * (uint32_t)W + (uint32_t)wc) * C + cg * 16;
+    uint4 v[KH * KW];
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+#pragma unroll
+      for (int j = 0; j < KW; ++j) {
+        const int h = h0 + i, w = w0 + j;
+        const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const int off = in ? ((h - hc) * W + (w - wc)) * C : 0;
+        v[i * KW + j] = *reinterpret_cast<const uint4*>(base + off);
+      }
+    uint32_t ev[4] = {0, 0, 0, 0}, od[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < KH * KW; ++k) {
+      const uint32_t a[4] = {v[k].x ^ 0x80808080u, v[k].y ^ 0x80808080u, v[k].z ^ 0x80808080u, v[k].w ^ 0x80808080u};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        ev[d] = pk_max_u16(ev[d], a[d] & 0x00FF00FFu);
+        od[d] = pk_max_u16(od[d], (a[d] >> 8) & 0x00FF00FFu);
+      }
+    }
+    uint4 o;
+    o.x = (ev[0] | (od[0] << 8)) ^ 0x80808080u;
+    o.y = (ev[1] | (od[1] << 8)) ^ 0x80808080u;
+    o.z = (ev[2] | (od[2] << 8)) ^ 0x80808080u;
+    o.w = (ev[3] | (od[3] << 8)) ^ 0x80808080u;
+    *reinterpret_cast<uint4*>(y + (size_t)pix * C + cg * 16) = o;
+  }
+}
+
 BIGDL_EXPORT int bigdl_maxpool_i8_t(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
                                     int sh, int sw, int ph, int pw, int tail, hipStream_t s);
 BIGDL_EXPORT int bigdl_maxpool_i8(const void* x, void* y, int Nb, int H, int W, int C, int P, int Q, int kh, int kw,
@@ -649,6 +705,17 @@ BIGDL_EXPORT int bigdl_maxpool_i8_t(const void* x, void* y, int Nb, int H, int W
       ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
     return (int)hipErrorInvalidValue;
   const long long total = (long long)Nb * P * Q * (C / 16);
+  const bool small = total < 0x7fffffffLL - 65536LL * 256 && (long long)Nb * H * W < 0x7fffffffLL;
+  if (small && ph <= 1 && pw <= 1 && ((kh == 3 && kw == 3) || (kh == 2 && kw == 2))) {
+    const dim3 g((unsigned)bigdl_grid(total, 256, 65536));
+    if (kh == 3)
+      hipLaunchKernelGGL((k_maxpool_i8_k<3, 3>), g, dim3(256), 0, s, (const int8_t*)x, (int8_t*)y, Nb, H, W, C, P, Q, sh,
+                         sw, ph, pw, tail);
+    else
+      hipLaunchKernelGGL((k_maxpool_i8_k<2, 2>), g, dim3(256), 0, s, (const int8_t*)x, (int8_t*)y, Nb, H, W, C, P, Q, sh,
+                         sw, ph, pw, tail);
+    BIGDL_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(k_maxpool_i8, dim3((unsigned)bigdl_grid(total, 256, 65536)), dim3(256), 0, s, (const int8_t*)x,
                      (int8_t*)y, Nb, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, tail);
   BIGDL_CHECK_LAUNCH();
@@ -742,8 +809,9 @@ BIGDL_EXPORT int bigdl_conv_i8_fwd4(const void* x, const void* w, int ldw, const
                                     int dh, int dw, int relu, int x_u8, int y_u8, const void* res, int res_kind,
                                     int ldr, float res_scale, float res_zero, hipStream_t s) {
   // x_u8: x holds 16 bytes of 0x80 after its last byte (and the bias carries the offset term);
-  // y_u8: yq is dense (ldy == K) with room for that tail
-  if (y_u8 && (!yq || ldy != K)) return (int)hipErrorInvalidValue;
+  // y_u8: yq is dense (ldy == K) with room for that tail, or a channel slice of a wider tensor
+  // (ldy > K: a zero-copy concat whose owner writes the tail)
+  if (y_u8 && !yq) return (int)hipErrorInvalidValue;
   if (res_kind < 0 || res_kind > 2 || (res_kind && (!res || ldr < K || ldr % 4 || ((uintptr_t)res & 7))))
     return (int)hipErrorInvalidValue;
   if (!x || !w || (!sx && !(sxs > 0.f)) || !swt || (!y && !yq) || Nb <= 0 || K <= 0 || K % 8 || P <= 0 || Q <= 0)

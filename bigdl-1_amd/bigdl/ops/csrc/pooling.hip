@@ -364,6 +364,15 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
                        (int8_t*)idx, g, te);
     BIGDL_CHECK_LAUNCH();
   }
+  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
+  if (!idx && k3s2 && (long long)N * P * Q * (C / 8) < 0x7fffffffLL) {
+    // inference 3x3 / stride-2 pools (the Inception / ResNet stems): every window load in flight
+    // (the row-sharing kernel below streamed the 112² Inception pool at ~2 TB/s)
+    const long long total = (long long)N * P * Q * (C / 8);
+    hipLaunchKernelGGL(k_maxpool_fwd_k3s2<uint32_t>, dim3(bigdl_grid(total, 256, 16384)), dim3(256), 0, s,
+                       (const bf16_t*)x, (bf16_t*)y, (int8_t*)nullptr, g);
+    BIGDL_CHECK_LAUNCH();
+  }
   if (!idx) {
     const long long rows = (long long)N * ((P + MP_ROWS - 1) / MP_ROWS) * Q * (C / 8);
     if (rows < 0x7fffffffLL - 65536LL * 256)
@@ -376,7 +385,6 @@ BIGDL_EXPORT int bigdl_maxpool_fwd(const void* x, void* y, void* idx, int N, int
   }
   const long long total = (long long)N * P * Q * (C / 8);
   const int grid = bigdl_grid(total, 256, 16384);
-  const bool k3s2 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph <= 1 && pw <= 1;
   if (total < 0x7fffffffLL) {
     if (k3s2) hipLaunchKernelGGL(k_maxpool_fwd_k3s2<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);
     else hipLaunchKernelGGL(k_maxpool_fwd<uint32_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, (int8_t*)idx, g);

@@ -1945,7 +1945,8 @@ def conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias):
 
 
 def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, dilation, out_hw, relu=False,
-                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_bias=None, residual=None):
+                             in_scale=None, out_scale=None, in_u8=False, out_u8=False, u8_bias=None, residual=None,
+                             out=None):
     """int8 conv with calibrated scales: ``x`` int8 NHWC (tagged ``_qscale``, the producer's
     requantised output) or fp32/bf16 quantised here with ``in_scale`` in one static pass; with
     ``out_scale`` the epilogue writes the int8 NHWC input of the next quantised layer (bias, ReLU
@@ -1977,7 +1978,15 @@ def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, di
     if out_u8 and not (relu and out_scale is not None):
         raise ValueError("conv2d_i8_forward_static: out_u8 needs a fused ReLU and an int8 output")
     P, Q = out_hw
-    if out_scale is not None:
+    ldy = K
+    if out is not None and out_scale is not None:
+        # a channel slice [N][K][P][Q] of a wider channels-last int8 tensor (zero-copy concat)
+        if not (out.dtype == torch.int8 and tuple(out.shape) == (N_, K, P, Q) and out.stride(1) == 1
+                and out.stride(2) == Q * out.stride(3) and out.stride(0) == P * Q * out.stride(3)
+                and out.stride(3) % 16 == 0 and out.data_ptr() % 16 == 0):
+            return NotImplemented
+        y, ldy = out, out.stride(3)
+    elif out_scale is not None:
         y = _i8_act(N_, K, P, Q, x.device, out_u8)
     else:
         y = torch.empty((N_, K, P, Q), dtype=_bf16, device=x.device, memory_format=torch.channels_last)
@@ -1997,7 +2006,7 @@ def conv2d_i8_forward_static(x, wq, ldw, w_scale, bias, K, R, S, stride, pad, di
         b = u8_bias if u8_bias is not None else conv_i8_u8_bias(wq, ldw, K, R, S, C_, sx, w_scale, bias)
     check(_lib().bigdl_conv_i8_fwd4(ptr(xq), ptr(wq), C.c_int(ldw), None, C.c_float(sx), ptr(w_scale), ptr(b),
                                     None if out_scale is not None else ptr(y), ptr(y) if out_scale is not None else None,
-                                    C.c_float(out_scale if out_scale is not None else 1.0), C.c_int(K), N_, H, W, C_, K,
+                                    C.c_float(out_scale if out_scale is not None else 1.0), C.c_int(ldy), N_, H, W, C_, K,
                                     R, S, P, Q, stride[0], stride[1], pad[0], pad[1], dilation[0], dilation[1],
                                     C.c_int(1 if relu else 0), C.c_int(int(x_u8)),
                                     C.c_int(int(out_u8)), ptr(residual), C.c_int(rkind), C.c_int(K), C.c_float(rscale),

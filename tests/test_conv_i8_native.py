@@ -130,3 +130,33 @@ def test_quantized_vgg16_forward_vs_fp32():
     # logits as much as int8 does, so both comparisons carry the same tolerance
     assert _cos(r(yq), r(host)) > 0.95
     assert _cos(r(yq), r(ref)) > 0.95
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,s,p,H,u8", [(3, 2, 0, 15, False), (3, 2, 1, 14, True), (2, 2, 0, 16, False),
+                                        (3, 1, 1, 9, True), (3, 2, 0, 112, True)])
+def test_maxpool_i8_matches_torch(k, s, p, H, u8):
+    """int8 max pooling (fixed-window kernels for 3x3 / 2x2, ceil-mode output sizes as Caffe's) against
+    torch's max pool of the same codes; the unsigned (offset) code keeps its padding tail."""
+    import math
+    from bigdl.ops import native_ops as NO
+    torch.manual_seed(3)
+    N, C = 2, 48
+    P = int(math.ceil((H + 2 * p - k) / s)) + 1
+    if p > 0 and (P - 1) * s >= H + p:
+        P -= 1
+    codes = torch.randint(-128, 128, (N, C, H, H), dtype=torch.int8, device="cuda")
+    if u8:
+        x = NO._i8_act(N, C, H, H, "cuda", True)
+        x.copy_(codes)
+        x.untyped_storage()[x.numel():].fill_(0x80)
+        x = NO._tag(x, 0.1, True)
+    else:
+        x = NO._tag(codes.contiguous(memory_format=torch.channels_last), 0.1, False)
+    y = NO.maxpool_i8(x, k, k, s, s, p, p, P, P)
+    assert y is not NotImplemented
+    ref = torch.nn.functional.max_pool2d(codes.float(), k, s, p, ceil_mode=True)[:, :, :P, :P]
+    assert torch.equal(y.float(), ref)
+    if u8:
+        raw = torch.empty(0, dtype=torch.uint8, device="cuda").set_(y.untyped_storage())
+        assert bool((raw[y.numel():y.numel() + 16] == 0x80).all())
