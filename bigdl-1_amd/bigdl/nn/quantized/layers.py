@@ -236,6 +236,63 @@ class SpatialConvolution(_QuantizedBase):
         Q = (W + pl + pr - self.dilationW * (self.kernelW - 1) - 1) // self.strideW + 1
         return P, Q
 
+    def _pair_ok(self, x, pads, residual=None):
+        """A 64-channel 1×1 stride-1 conv on an int8 chain input: run as the GEMM of pixel PAIRS
+        ([M/2][128] codes · block-diagonal [[W, 0], [0, W]]), whose output rows [M/2][2K] are exactly
+        the NHWC [M][K] result — every staged activation byte is useful (the 64-channel k-tile of the
+        plain form is half padding) and half as many tiles re-stage the weights."""
+        N, C, H, W = x.shape
+        return (x.dtype == torch.int8 and C == 64 and self.kernelH == 1 and self.kernelW == 1 and self.strideH == 1
+                and self.strideW == 1 and tuple(pads) == (0, 0, 0, 0) and (N * H * W) % 2 == 0
+                and self.nOutputPlane % 16 == 0 and self.__dict__.get("_cat_join") is None
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and (residual is None or residual.is_contiguous(memory_format=torch.channels_last)))
+
+    def _pair_prep(self, x):
+        from ...ops import native_ops as NO
+        prep = self._i8_prep(x, 64)
+        pp = self.__dict__.get("_i8pair")
+        if pp is None or pp[0].device != x.device:
+            K = self.nOutputPlane
+            wq = prep[0].view(torch.int8).reshape(K, prep[1])  # [K][128]: 64 weights + 64 zero pad
+            w2 = torch.zeros(2 * K, 128, dtype=torch.int8, device=x.device)
+            w2[:K, :64] = wq[:, :64]
+            w2[K:, 64:] = wq[:, :64]
+            pp = self._i8pair = (w2.contiguous(), 128, torch.cat([prep[2], prep[2]]).contiguous(),
+                                 torch.cat([prep[3], prep[3]]).contiguous() if prep[3] is not None else None)
+        return pp
+
+    @staticmethod
+    def _as_pairs(t, C2):
+        """[N][C][H][W] channels-last → the [1][2C][1][N·H·W/2] view of the same bytes (tags kept)."""
+        N, C, H, W = t.shape
+        m2 = N * H * W // 2
+        v = torch.as_strided(t, (1, C2, 1, m2), (m2 * C2, 1, m2 * C2, C2))
+        return _retag(v, t)
+
+    def _native_pairs(self, x, residual=None, out_scale=None, out_u8=False, relu=None):
+        from ...ops import native_ops as NO
+        N, C, H, W = x.shape
+        K = self.nOutputPlane
+        w2, ldw, sw2, b2 = self._pair_prep(x)
+        xp = self._as_pairs(x, 128)
+        if getattr(x, "_qzero", 0):
+            key = (x.device, x._qscale)
+            t = self.__dict__.get("_i8pair_u8")
+            if t is None or t[0] != key:
+                t = self._i8pair_u8 = (key, NO.conv_i8_u8_bias(w2, ldw, 2 * K, 1, 1, 128, x._qscale, sw2, b2))
+            ub = t[1]
+        else:
+            ub = None
+        rp = self._as_pairs(residual, 2 * K) if residual is not None else None
+        y = NO.conv2d_i8_forward_static(xp, w2, ldw, sw2, b2, 2 * K, 1, 1, (1, 1), (0, 0), (1, 1), (1, N * H * W // 2),
+                                        relu=self._relu_fused if relu is None else relu, in_scale=self.static_scale,
+                                        out_scale=out_scale, out_u8=out_u8, u8_bias=ub, residual=rp)
+        if y is NotImplemented:
+            return y
+        out = torch.as_strided(y, (N, K, H, W), (H * W * K, 1, W * K, K))
+        return _retag(out, y)
+
     def _native_static(self, x, pads):
         """Calibrated int8 path: int8 (or statically quantised) input, int8 output for the next
         quantised layer of the chain (bias + ReLU + requantisation in the epilogue) or bf16."""
@@ -246,6 +303,10 @@ class SpatialConvolution(_QuantizedBase):
             return NotImplemented
         if x.dtype != torch.int8 and self.static_scale is None:
             return NotImplemented
+        if self._pair_ok(x, pads) and self._out_qscale is not None:
+            y = self._native_pairs(x, out_scale=self._out_qscale, out_u8=self._out_u8)
+            if y is not NotImplemented:
+                return y
         C = x.shape[1]
         if NO.conv_i8_supported(C, self.kernelH, self.kernelW):
             prep = self._i8_prep(x, C)
@@ -314,6 +375,11 @@ class SpatialConvolution(_QuantizedBase):
             return NotImplemented
         if res.dtype != torch.int8 or getattr(res, "_qscale", None) is None:
             res = res.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if self._pair_ok(x, (pt, pb, pl, pr), res) and out_scale is not None and res.dtype == torch.int8:
+            y = self._native_pairs(x, residual=res, out_scale=out_scale,
+                                   out_u8=bool(out_u8 and out_scale is not None), relu=True)
+            if y is not NotImplemented:
+                return y
         prep = self._i8_prep(x, C)
         xin = x if x.dtype == torch.int8 else x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         return NO.conv2d_i8_forward_static(xin, prep[0], prep[1], prep[2], prep[3], self.nOutputPlane, self.kernelH,

@@ -488,7 +488,12 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
                   acc[i][j][4 * g + 3] + b4[3]};
       }
     }
-  X3_BARRIER();
+  // a full __syncthreads (LDS writes drained, then the barrier): the raw s_barrier used in the main
+  // loop is preceded there by X3_WAIT's lgkmcnt(0), but here the other waves READ what this wave just
+  // WROTE — on gfx950 s_barrier does not wait for the issuing wave's outstanding ds_writes, and the
+  // raw form let the row pass / the statistics fold read stale LDS now and then (fp32 BN statistics
+  // off by up to 65 % on a few steps of a training run: tools/convergence.py --check-bn 1)
+  __syncthreads();
   // 2. row-major pass: thread (rr, cc) handles channels n0 + 4·cc … +3 of rows rr, rr + RPP, …, so every
   //    global access of a wave-instruction is RPP-row-contiguous 16-B chunks (full 4·BN-byte row segments)
   const int cc = tid % CPR, rr = tid / CPR;
@@ -571,7 +576,7 @@ __global__ void __launch_bounds__(64 * WM * WN, NS == 2 ? (BM * BN <= 128 * 64 ?
     float* red = reinterpret_cast<float*>(lds + BM * BN * 4);  // [2][RPP][BN] behind the staged tile
     *reinterpret_cast<v4f*>(&red[rr * BN + cc * 4]) = (v4f){s4[0], s4[1], s4[2], s4[3]};
     *reinterpret_cast<v4f*>(&red[(RPP + rr) * BN + cc * 4]) = (v4f){q4[0], q4[1], q4[2], q4[3]};
-    X3_BARRIER();
+    __syncthreads();  // (as above: other waves read these partials)
     const int rep = tm % p.R_rep;
     for (int t = tid; t < 2 * BN; t += NT) {
       const int which = t / BN, c = t - which * BN;

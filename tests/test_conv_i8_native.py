@@ -160,3 +160,41 @@ def test_maxpool_i8_matches_torch(k, s, p, H, u8):
     if u8:
         raw = torch.empty(0, dtype=torch.uint8, device="cuda").set_(y.untyped_storage())
         assert bool((raw[y.numel():y.numel() + 16] == 0x80).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,res", [(256, False), (256, True), (64, False)])
+def test_i8_pixel_pair_path_matches_plain(K, res):
+    """64-channel 1×1 int8 convs run as the GEMM of pixel pairs with a block-diagonal weight: the same
+    int32 sums, so the codes match the plain 64-channel k-tile path exactly (with and without the
+    int8 residual of a block tail)."""
+    import bigdl.nn as nn
+    from bigdl.nn.quantized import layers as Q
+    from bigdl.ops import native_ops as NO
+    torch.manual_seed(5)
+    conv = nn.SpatialConvolution(64, K, 1, 1)
+    q = Q.SpatialConvolution.from_float(conv).cuda()
+    q.static_scale = 0.05
+    q._out_qscale, q._out_u8, q._relu_fused = 0.04, True, True
+    N, H = 4, 14
+    xc = NO._i8_act(N, 64, H, H, "cuda", True)
+    xc.copy_(torch.randint(-128, 128, (N, 64, H, H), dtype=torch.int8, device="cuda"))
+    xc.untyped_storage()[xc.numel():].fill_(0x80)
+    x = NO._tag(xc, 0.05, True)
+    r = None
+    if res:
+        rc = torch.randint(-128, 128, (N, K, H, H), dtype=torch.int8, device="cuda").contiguous(memory_format=torch.channels_last)
+        r = NO._tag(rc, 0.03, True)
+    assert q._pair_ok(x, (0, 0, 0, 0), r)
+    if res:
+        y1 = q.forward_residual(x, r, out_scale=0.04, out_u8=True)
+    else:
+        y1 = q._native_static(x, (0, 0, 0, 0))
+    q._pair_ok = lambda *a, **k: False
+    if res:
+        y0 = q.forward_residual(x, r, out_scale=0.04, out_u8=True)
+    else:
+        y0 = q._native_static(x, (0, 0, 0, 0))
+    torch.cuda.synchronize()
+    assert y1.shape == y0.shape and y1._qscale == y0._qscale and y1._qzero == y0._qzero
+    assert torch.equal(y1.contiguous(), y0.contiguous())

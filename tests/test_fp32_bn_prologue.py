@@ -136,4 +136,4 @@ def test_resnet50_fp32_step_with_bn_prologue_matches_materialised():
     # — mask, padding, coefficients — drops whole layers far below it)
     mid = len(c_pro) // 2
     assert c_pro[0] >= 0.9999 or c_pro[0] >= c_ctl[0] - 2e-3, (c_pro[:5], c_ctl[:5])
-    assert c_pro[mid] >= c_ctl[mid] - 1e-4, (c_pro[mid], c_ctl[mid])
+    assert c_pro[mid] >= c_ctl[mid] - 1e-3, (c_pro[mid], c_ctl[mid])

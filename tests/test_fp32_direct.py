@@ -313,3 +313,29 @@ def test_fp32_threshold_and_colsum_kernels():
     NO.colsum_acc(m, out, 0.5)
     torch.cuda.synchronize()
     assert _rel(out, 1.0 + 0.5 * m.double().sum(0)) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,K,H", [(256, 1024, 14), (512, 2048, 7)])
+def test_conv_epilogue_statistics_are_exact_every_time(C, K, H):
+    """The fp32 conv's BN-statistics epilogue, repeated: every launch's Σ(y − K), Σ(y − K)² must match
+    fp64 sums of the output it wrote.  (The epilogue's LDS staging once synchronised with a raw
+    s_barrier, which on gfx950 does not drain the writing wave's ds_writes: a few launches in a hundred
+    folded stale partials — BN variances off by up to 65 % on some training steps.)"""
+    from bigdl.ops import fp32x3 as F3
+    torch.manual_seed(0)
+    x = torch.randn(128, C, H, H, device=dev).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, 1, 1, device=dev) * (2.0 / C) ** 0.5
+    shift = torch.randn(K, device=dev) * 0.1
+    rep = 32
+    buf = torch.zeros(2 * rep * K, device=dev)
+    bad = []
+    for it in range(120):
+        buf.zero_()
+        y, _b, _r = F3.conv_forward_stats(x, w, (1, 1), (0, 0), (1, 1), (buf, rep), shift)
+        yd = y.double().permute(0, 2, 3, 1).reshape(-1, K) - shift.double()
+        b = buf.double().reshape(2, rep, K).sum(1)
+        e2 = float(((b[1] - (yd * yd).sum(0)).abs() / (yd * yd).sum(0)).max())
+        if e2 > 1e-5:
+            bad.append((it, e2))
+    assert not bad, bad[:5]

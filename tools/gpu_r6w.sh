@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r6w
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_int8_fc.py tests/test_syncbn_native.py tests/test_fp32_bn_prologue.py > $O/new_tests.log 2>&1 || { grep -v INFO $O/new_tests.log | tail -40; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_fp32_direct.py tests/test_train_parity.py tests/test_fp32_bn_prologue.py tests/test_conv_i8_native.py > $O/new_tests.log 2>&1 || { grep -v INFO $O/new_tests.log | tail -40; exit 1; }
 tail -1 $O/new_tests.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 tail -3 $O/gpu_tests.log
