@@ -204,6 +204,8 @@ class SpatialConvolution(_QuantizedBase):
             q.qbias = m.bias.detach().float().clone().cpu()
         q.format = getattr(m, "format", "NCHW")
         q.static_scale = calibrated_scale(m)
+        oa = m.__dict__.get("_folded_out_amax")
+        q.static_out_scale = oa / 127.0 if oa else None
         q.set_name(m.get_name())
         return q.to(w.device)
 

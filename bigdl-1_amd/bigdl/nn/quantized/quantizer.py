@@ -130,6 +130,11 @@ def _fold_bn(model):
                 b0 = a.bias.detach().float().reshape(-1) if (a.withBias and a.bias is not None) \
                     else torch.zeros_like(inv)
                 a._folded_bias = ((b0 - b.runningMean.float()) * g + beta).clone()
+            bst = b.__dict__.get("_int8_state")
+            if bst and bst.get("out") and bst.get("outMask", 0) == 0:
+                # the calibrated output range of the folded pair (the BN's output): a projection
+                # shortcut writes its int8 residual with it
+                a.__dict__["_folded_out_amax"] = max(float(v[0]) for v in bst["out"] if v)
             mods[i + 1] = Identity().set_name(b.get_name())
     return model
 
@@ -324,6 +329,15 @@ def _link_all(model):
         _link_units(_exec_units(blk.branch))
         if hasattr(blk.shortcut, "modules"):
             _link_units(_exec_units(blk.shortcut))
+            # a projection shortcut (conv + folded BN) with a calibrated output range writes the tail's
+            # residual as int8 (signed, clip = the calibrated max) instead of bf16: half the bytes the
+            # conv + sum epilogue reads
+            eff = [m for m in _exec_units(blk.shortcut) if not isinstance(m, L.Identity)]
+            if (len(eff) == 1 and isinstance(eff[0], Q.SpatialConvolution) and eff[0]._out_qscale is None
+                    and getattr(eff[0], "static_out_scale", None) and eff[0].nOutputPlane % 16 == 0
+                    and isinstance(blk.tail, Q.SpatialConvolution) and blk.tail.static_scale is not None):
+                eff[0]._out_qscale = eff[0].static_out_scale
+                eff[0]._out_u8 = False
 
 
 def _graph_pass(e):

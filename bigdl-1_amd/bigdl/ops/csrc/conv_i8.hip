@@ -253,6 +253,24 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
     }
   };
 
+  // conv + sum with an int8 residual and int8 output: the row pass's residual codes (16 per item,
+  // BM·BN/16/NT items per thread) are requested now, so their latency hides under the operand loads
+  // and the MFMAs instead of following them (the short-reduction convs are one load → one k-tile →
+  // epilogue per block: the residual round trip was a second exposed HBM latency)
+  constexpr int RPI = (BM * (BN / 16) + NT - 1) / NT;
+  uint4 rpre[RPI];
+  const bool res_pre = p.yq && p.res_kind == 1;
+  if (res_pre) {
+#pragma unroll
+    for (int it = 0; it < RPI; ++it) {
+      const int idx = tid + NT * it;
+      const int row = idx / (BN / 16), g16 = idx - row * (BN / 16);
+      const int m = m0 + row, n = n0 + g16 * 16;
+      rpre[it] = (idx < BM * (BN / 16) && m < p.M && n < p.K)
+                     ? *reinterpret_cast<const uint4*>((const int8_t*)p.res + (size_t)m * p.ldr + n)
+                     : make_uint4(0, 0, 0, 0);
+    }
+  }
   const int KT = p.KT;  // (NS == 2: the host launches KT ≤ 2 only)
   stage(0, 0);
   if (KT > 1) {
@@ -330,7 +348,10 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
       }
     __syncthreads();
     constexpr int G16 = BN / 16;  // 16-channel groups per tile row
-    for (int idx = tid; idx < BM * G16; idx += NT) {
+#pragma unroll
+    for (int it = 0; it < RPI; ++it) {
+      const int idx = tid + NT * it;
+      if (idx >= BM * G16) break;
       const int row = idx / G16, g16 = idx - row * G16;
       const int m = m0 + row, n = n0 + g16 * 16;
       if (m >= p.M || n >= p.K) continue;
@@ -344,7 +365,7 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) k_conv_i8(ConvI8Params p) 
         // the int8 residual's 16 codes in one load; code q → q + 128 = byte ^ 0x80 as an unsigned
         // byte (v_cvt_f32_ubyteN): value (q + res_zero)·s = ub·s + (res_zero − 128)·s, the constant
         // already in the tile
-        const uint4 rq = *reinterpret_cast<const uint4*>((const int8_t*)p.res + (size_t)m * p.ldr + n);
+        const uint4 rq = rpre[it];
         const uint32_t rw[4] = {rq.x ^ 0x80808080u, rq.y ^ 0x80808080u, rq.z ^ 0x80808080u, rq.w ^ 0x80808080u};
         const float rs = p.res_scale * p.out_inv;
 #pragma unroll
