@@ -1412,13 +1412,15 @@ __global__ void __launch_bounds__(256) k_bn32_apply(const float* __restrict__ x,
   }
 }
 
-// A/B knobs of the fp32 apply pass: BIGDL_BN32_UNROLL (rows in flight per thread: 1, 2, 4 = default,
-// 8) and BIGDL_BN32_BLOCKS (grid cap, default the bf16 pass's apply_cap)
+// A/B knobs of the fp32 apply pass: BIGDL_BN32_UNROLL (rows in flight per thread: 1, 2 = default, 4,
+// 8) and BIGDL_BN32_BLOCKS (grid cap, default the bf16 pass's apply_cap).  Round 6, whole fp32 step, 3
+// interleaved repeats on two boxes: 2 rows 45.06-45.23 / 44.41-44.83 ms vs 4 rows 45.50-45.65 /
+// 44.64-44.99 (8 rows and a 4096-block cap slower; profiles/r6_fp32_bn_unroll_ab.txt)
 static int bn32_unroll() {
   static int u = [] {
     const char* e = getenv("BIGDL_BN32_UNROLL");
-    const int v = e ? atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 8) ? v : 4;
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4 || v == 8) ? v : 2;
   }();
   return u;
 }
@@ -1440,9 +1442,9 @@ static void launch_bn32_apply(long long M, int C, hipStream_t s, const float* x,
   const dim3 g(bn32_grid(M, C)), b(256);
   switch (bn32_unroll()) {
     case 1: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 1>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
-    case 2: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 2>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+    case 4: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 4>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
     case 8: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 8>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
-    default: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 4>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
+    default: hipLaunchKernelGGL((k_bn32_apply<BWD, RELU, 2>), g, b, 0, s, x, aux, y_mask, out, gres, M, C, coef, sp, mbits); break;
   }
 }
 
