@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--log-every", type=int, default=20)
+    ap.add_argument("--model", default="resnet50", help="resnet50 (224²) | vgg_cifar (VggForCifar10, 32²)")
     ap.add_argument("--check-bn", type=int, default=0,
                     help="after every step compare each BN's saved batch statistics with fp64 statistics of its input")
     args = ap.parse_args()
@@ -44,18 +45,24 @@ def main():
     dev = torch.device("cuda")
     dt = Engine.compute_dtype()
     RNG.setSeed(42)
-    model = model_init(ResNet(args.classes, depth=50, dataset=DatasetType.ImageNet))
+    S = 224
+    if args.model == "vgg_cifar":
+        from bigdl.models.vgg import VggForCifar10
+        model = VggForCifar10(args.classes)
+        S = 32
+    else:
+        model = model_init(ResNet(args.classes, depth=50, dataset=DatasetType.ImageNet))
     crit = CrossEntropyCriterion()
     sgd = SGD(learningrate=args.lr, learningrate_decay=0.0, weightdecay=1e-4, momentum=0.9, dampening=0.0,
               nesterov=True)
     g0 = torch.Generator(device="cpu").manual_seed(7)
-    templates = torch.nn.functional.interpolate(torch.randn(args.classes, 3, 7, 7, generator=g0), size=(224, 224),
+    templates = torch.nn.functional.interpolate(torch.randn(args.classes, 3, 7, 7, generator=g0), size=(S, S),
                                                 mode="nearest").to(dev)
 
     def batch(step, salt=0):
         g = torch.Generator(device=dev).manual_seed(1000003 * salt + step)
         lab = torch.randint(0, args.classes, (args.batch,), generator=g, device=dev)
-        x = templates[lab] + args.noise * torch.randn(args.batch, 3, 224, 224, generator=g, device=dev)
+        x = templates[lab] + args.noise * torch.randn(args.batch, 3, S, S, generator=g, device=dev)
         return MiniBatch(x.to(dt).contiguous(memory_format=torch.channels_last), (lab + 1).float())
 
     first = batch(0)
