@@ -101,6 +101,8 @@ class _Bucket:
 
 
 class DistriOptimizer(BaseOptimizer):
+    _alias = False
+
     def __init__(self, model, training_set, criterion, optim_method=None, end_trigger=None, batch_size=32,
                  bigdl_type="float"):
         super().__init__(model, training_set, criterion, batch_size)
@@ -152,7 +154,17 @@ class DistriOptimizer(BaseOptimizer):
             self.buckets.append(_Bucket(i, lo, hi, soff, soff + per))
             soff += per
         dev = self.flat.weight.device
-        if self.sharded:
+        # one rank: its shard is the whole arena (slo == lo for every bucket), so the shard tensors
+        # ALIAS the arena and the reduce-scatter / all-gather — identity copies on a one-rank group —
+        # are not issued; hooks, buckets, side-stream early updates and the shard update path run as at
+        # any world size (the fused update writes the fp32 masters and the bf16 compute shadow itself)
+        self._alias = self.sharded and W == 1 and bool(config.get_property("bigdl.comm.aliasWorld1"))
+        if self._alias:
+            self.shard_w = self.flat.weight[:soff]
+            self.shard_g = self.flat.grad[:soff]
+            self.shard_shadow = self.flat.shadow[:soff] if self.flat.shadow is not None else None
+            self.grad_wire = None
+        elif self.sharded:
             self.shard_w = torch.empty(soff, dtype=torch.float32, device=dev)
             self.shard_g = torch.zeros(soff, dtype=torch.float32, device=dev)
             for b in self.buckets:
@@ -287,6 +299,8 @@ class DistriOptimizer(BaseOptimizer):
         side.wait_stream(_cur_stream(self.flat.grad.device))
         if isinstance(side, torch.cuda.Stream):
             NO.join_wgrad(side)
+        if self._alias:
+            return  # the gradient shard IS the arena gradient
         with _on(side):
             g = self.flat.grad[b.lo:b.hi]
             if self.sharded:
@@ -324,7 +338,7 @@ class DistriOptimizer(BaseOptimizer):
         return self.comm_dtype.startswith("bf16") and self.flat.shadow is not None
 
     def _launch_gather(self, b: _Bucket):
-        if not self.sharded:
+        if not self.sharded or self._alias:
             return
         if self._bf16_gather():
             # reference wire format: replicas compute with the bf16 copy of the weights
@@ -532,8 +546,8 @@ class DistriOptimizer(BaseOptimizer):
             for name, meth in self.optim_methods.items():
                 for (bb, lo, hi) in self._method_shard_ranges[name]:
                     if bb is b:
-                        sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and
-                                                          self.comm_dtype.startswith("bf16")) else None
+                        sh = self.shard_shadow[lo:hi] if (self.shard_shadow is not None and (
+                            self._alias or self.comm_dtype.startswith("bf16"))) else None
                         meth.apply_update(self.shard_w, self._grad_for(meth, b), lo, hi, shadow=sh)
 
     def _update_order(self):
@@ -554,7 +568,7 @@ class DistriOptimizer(BaseOptimizer):
         """Bring every rank's fp32 arena up to date (needed before validation/checkpoint when
         the bf16 wire format gathered only the compute shadow)."""
         self._wait_all_gathers()
-        if self.sharded and self.comm_dtype.startswith("bf16"):
+        if self.sharded and self.comm_dtype.startswith("bf16") and not self._alias:
             for b in self.buckets:
                 dist.all_gather_into_tensor(self.flat.weight[b.lo:b.hi], self.shard_w[b.slo:b.shi])
             from ..ops import fp32x3
@@ -568,7 +582,7 @@ class DistriOptimizer(BaseOptimizer):
 
     def _on_restore(self):
         comm.broadcast_module(self.model, 0)
-        if self.sharded:
+        if self.sharded and not self._alias:
             W, r = self.world, self.rank
             for b in self.buckets:
                 per = b.shi - b.slo

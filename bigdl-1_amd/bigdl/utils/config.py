@@ -44,6 +44,7 @@ _REGISTRY = {
     "bigdl.comm.sharded": (bool, True, "reduce-scatter + sharded update + all-gather (ZeRO-1)"),
     "bigdl.comm.channels": (int, 0, "RCCL channel cap (NCCL_MIN/MAX_NCHANNELS, set by the launcher before any GPU call; 0 = RCCL default): bounds the CUs collectives take from compute"),
     "bigdl.comm.streamPriority": (int, -1, "priority of the comm-side stream that runs the shard update + all-gather (-1 = high, 0 = normal)"),
+    "bigdl.comm.aliasWorld1": (bool, True, "sharded mode with one rank: the shard tensors alias the parameter arena and the identity reduce-scatter / all-gather are skipped"),
     "bigdl.comm.earlyUpdate": (bool, True, "sharded mode on a GPU: issue each bucket's shard update + all-gather on the comm-side stream as soon as its reduce-scatter is launched (overlaps the rest of backward)"),
     # observability
     "bigdl.metrics.jsonPath": (str, "", "per-rank JSON metrics stream: one line per iteration to <path>.rank<r>.jsonl ('' = off)"),

@@ -34,7 +34,7 @@ def _data(n=64):
     return x, y
 
 
-def _worker(rank, world, port, mode, comm_dtype, out_q):
+def _worker(rank, world, port, mode, comm_dtype, out_q, alias=True):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bigdl-1_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -42,6 +42,7 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     config.set_property("bigdl.comm.sharded", mode in ("sharded", "parallel"))
     config.set_property("bigdl.comm.dtype", comm_dtype)
     config.set_property("bigdl.comm.bucketMB", 0.0005)  # several buckets even for a tiny model
+    config.set_property("bigdl.comm.aliasWorld1", alias)
     from bigdl.utils.engine import Engine
     Engine.init(device="cpu", dist=True, backend="gloo")
     from bigdl.nn import ClassNLLCriterion
@@ -60,6 +61,13 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     else:
         opt = DistriOptimizer(model, [MiniBatch(x[:per], y[:per])], ClassNLLCriterion(), sgd)
     opt.prepare()
+    issued = []
+    if world == 1:  # count the collectives the step issues
+        import torch.distributed as dist
+        from bigdl.parallel import distri_optimizer as D
+        for nm in ("reduce_scatter_tensor", "all_gather_into_tensor", "all_reduce"):
+            real = getattr(dist, nm)
+            setattr(D.dist, nm, (lambda real, nm: lambda *a, **k: (issued.append(nm), real(*a, **k))[1])(real, nm))
     for step in range(4):
         xs = x[rank * per:(rank + 1) * per]
         ys = y[rank * per:(rank + 1) * per]
@@ -68,7 +76,7 @@ def _worker(rank, world, port, mode, comm_dtype, out_q):
     w = opt.flat.weight.clone()
     if rank == 0:
         ws = torch.cat([p.reshape(-1) for p in model.parameters()[0]])
-        out_q.put(ws.numpy())
+        out_q.put((ws.numpy(), len(issued), bool(opt._alias)))
     Engine.shutdown()
 
 
@@ -99,12 +107,35 @@ def test_distri_matches_serial(mode, comm_dtype):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, comm_dtype, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = torch.from_numpy(q.get(timeout=240))
+    got = torch.from_numpy(q.get(timeout=240)[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     tol = 1e-5 if comm_dtype == "fp32" else 3e-2
     torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("mode,comm_dtype,alias", [("sharded", "fp32", True), ("sharded", "bf16", True),
+                                                   ("parallel", "fp32", True), ("sharded", "fp32", False)])
+def test_distri_world1_matches_serial(mode, comm_dtype, alias):
+    """One rank: the sharded DistriOptimizer (hooks, buckets, shard update path) must give the serial
+    optimizer's weights; with ``bigdl.comm.aliasWorld1`` the shard tensors alias the arena and no
+    gradient / weight collective is issued (a bf16 wire is then never used, so the match is fp32-exact)."""
+    ref = _reference_weights()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), mode, comm_dtype, q, alias))
+    p.start()
+    w, n_coll, aliased = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert aliased == alias
+    if alias:
+        assert n_coll == 0, n_coll
+    else:
+        assert n_coll > 0
+    tol = 1e-5 if (comm_dtype == "fp32" or alias) else 3e-2
+    torch.testing.assert_close(torch.from_numpy(w), ref, rtol=tol, atol=tol)
 
 
 def test_bf16_truncate_golden():
