@@ -85,7 +85,8 @@ class Container(AbstractModule):
 
     def zeroGradParameters(self):
         if self._arena is not None and self._arena.grad is not None and self._owns_arena():
-            self._arena.grad.zero_()
+            from .. import ops
+            ops.zero_fill(self._arena.grad)
             return
         for m in self.modules:
             m.zeroGradParameters()

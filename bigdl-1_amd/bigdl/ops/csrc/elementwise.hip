@@ -32,6 +32,47 @@ __global__ void k_bf16_to_f32(const bf16_t* __restrict__ src, float* __restrict_
     dst[i] = bf2f(src[i]);
 }
 
+// 32-bit fill (the per-step gradient-arena clear): 16-B vector stores, grid-stride, scalar tail
+__global__ void k_fill32(uint32_t* __restrict__ dst, long long n, uint32_t v) {
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const uint4 q = make_uint4(v, v, v, v);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<uint4*>(dst)[i] = q;
+  for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = v;
+}
+
+// n 32-bit words of dst (16-B aligned, checked on the host) set to the bit pattern v
+BIGDL_EXPORT int bigdl_fill32(void* dst, long long n, uint32_t v, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int grid = bigdl_grid((n + 3) / 4, 256);
+  hipLaunchKernelGGL(k_fill32, dim3(grid), dim3(256), 0, s, (uint32_t*)dst, n, v);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// conv weight rows [K][taps][C] (bf16, KRSC) → [K][ldw] with every tap's channels zero-padded to cp
+// and the row zero-padded to ldw (the narrow-channel conv operand: the RGB stem's C4 gather, C % 8
+// inputs); one pass, every destination element written once
+__global__ void k_pad_taps_bf16(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int K, int taps, int C,
+                                int cp, int ldw) {
+  const long long n = (long long)K * ldw;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int k = (int)(i / ldw), j = (int)(i - (long long)k * ldw);
+    const int t = j / cp, c = j - t * cp;
+    dst[i] = (t < taps && c < C) ? src[((long long)k * taps + t) * C + c] : (bf16_t)0;
+  }
+}
+
+BIGDL_EXPORT int bigdl_pad_taps_bf16(const void* src, void* dst, int K, int taps, int C, int cp, int ldw,
+                                     hipStream_t s) {
+  if (K <= 0 || taps <= 0 || C <= 0 || cp < C || ldw < taps * cp) return (int)hipErrorInvalidValue;
+  const int grid = bigdl_grid((long long)K * ldw, 256);
+  hipLaunchKernelGGL(k_pad_taps_bf16, dim3(grid), dim3(256), 0, s, (const bf16_t*)src, (bf16_t*)dst, K, taps, C, cp,
+                     ldw);
+  BIGDL_CHECK_LAUNCH();
+}
+
 // mode 0: f32->bf16, 1: bf16->f32.  Pointers must be 16-B aligned (checked on the host).
 BIGDL_EXPORT int bigdl_cast(const void* src, void* dst, long long n, int mode, hipStream_t s) {
   if (n <= 0) return 0;

@@ -32,8 +32,10 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
 }
 
 // per row: lse, row loss (weighted), row weight
-template <typename T>
-__global__ void __launch_bounds__(256) k_ce_rows(const T* __restrict__ x, const int* __restrict__ tgt,
+// TT: the target type — int32, or float (BigDL's 1-based labels as the data loader hands them over,
+// read directly instead of a per-step cast)
+template <typename T, typename TT = int>
+__global__ void __launch_bounds__(256) k_ce_rows(const T* __restrict__ x, const TT* __restrict__ tgt,
                                                  const float* __restrict__ cw, int K, int padding,
                                                  float* __restrict__ lse, float* __restrict__ rloss,
                                                  float* __restrict__ rw) {
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(256) k_ce_rows(const T* __restrict__ x, const 
   if (threadIdx.x == 0) {
     float l = m + __logf(s);
     lse[row] = l;
-    int t = tgt[row];
+    int t = (int)tgt[row];
     bool valid = t != padding && t >= 1 && t <= K;
     float w = valid ? (cw ? cw[t - 1] : 1.f) : 0.f;
     rw[row] = w;
@@ -75,8 +77,8 @@ __global__ void k_ce_total(const float* __restrict__ rloss, const float* __restr
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) k_ce_grad(const T* __restrict__ x, const int* __restrict__ tgt,
+template <typename T, typename TT = int>
+__global__ void __launch_bounds__(256) k_ce_grad(const T* __restrict__ x, const TT* __restrict__ tgt,
                                                  const float* __restrict__ lse, const float* __restrict__ rw,
                                                  const float* __restrict__ tot, int K, T* __restrict__ gx) {
   const long long row = blockIdx.x;
@@ -84,10 +86,30 @@ __global__ void __launch_bounds__(256) k_ce_grad(const T* __restrict__ x, const 
   T* gr = gx + row * K;
   const float scale = rw[row] / tot[1];
   const float l = lse[row];
-  const int t = tgt[row] - 1;
+  const int t = (int)tgt[row] - 1;
   for (int i = threadIdx.x; i < K; i += blockDim.x) {
     float p = __expf(ld(xr, i) - l);
     st(gr, i, scale * (p - (i == t ? 1.f : 0.f)));
+  }
+}
+
+template <typename TT>
+static void launch_ce(const void* x, const TT* tgt, const float* cw, void* gx, long long B, int K, int padding,
+                      int size_avg, int dtype, float* ws, float* out, hipStream_t s) {
+  float *lse = ws, *rl = ws + B, *rw = ws + 2 * B;
+  if (dtype == 1) {
+    hipLaunchKernelGGL((k_ce_rows<bf16_t, TT>), dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, cw, K, padding, lse, rl, rw);
+  } else {
+    hipLaunchKernelGGL((k_ce_rows<float, TT>), dim3(B), dim3(256), 0, s, (const float*)x, tgt, cw, K, padding, lse, rl, rw);
+  }
+  hipLaunchKernelGGL(k_ce_total, dim3(1), dim3(256), 0, s, rl, rw, B, size_avg, out);
+  if (gx) {
+    if (dtype == 1)
+      hipLaunchKernelGGL((k_ce_grad<bf16_t, TT>), dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, lse, rw, out, K,
+                         (bf16_t*)gx);
+    else
+      hipLaunchKernelGGL((k_ce_grad<float, TT>), dim3(B), dim3(256), 0, s, (const float*)x, tgt, lse, rw, out, K,
+                         (float*)gx);
   }
 }
 
@@ -95,21 +117,15 @@ __global__ void __launch_bounds__(256) k_ce_grad(const T* __restrict__ x, const 
 BIGDL_EXPORT int bigdl_cross_entropy(const void* x, const int* tgt, const float* cw, void* gx, long long B, int K,
                                      int padding, int size_avg, int dtype, float* ws, float* out, hipStream_t s) {
   if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  float *lse = ws, *rl = ws + B, *rw = ws + 2 * B;
-  if (dtype == 1) {
-    hipLaunchKernelGGL(k_ce_rows<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, cw, K, padding, lse, rl, rw);
-  } else {
-    hipLaunchKernelGGL(k_ce_rows<float>, dim3(B), dim3(256), 0, s, (const float*)x, tgt, cw, K, padding, lse, rl, rw);
-  }
-  hipLaunchKernelGGL(k_ce_total, dim3(1), dim3(256), 0, s, rl, rw, B, size_avg, out);
-  if (gx) {
-    if (dtype == 1)
-      hipLaunchKernelGGL(k_ce_grad<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)x, tgt, lse, rw, out, K,
-                         (bf16_t*)gx);
-    else
-      hipLaunchKernelGGL(k_ce_grad<float>, dim3(B), dim3(256), 0, s, (const float*)x, tgt, lse, rw, out, K,
-                         (float*)gx);
-  }
+  launch_ce<int>(x, tgt, cw, gx, B, K, padding, size_avg, dtype, ws, out, s);
+  BIGDL_CHECK_LAUNCH();
+}
+
+// the same with fp32 targets (1-based class indices stored as floats)
+BIGDL_EXPORT int bigdl_cross_entropy_ft(const void* x, const float* tgt, const float* cw, void* gx, long long B, int K,
+                                        int padding, int size_avg, int dtype, float* ws, float* out, hipStream_t s) {
+  if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  launch_ce<float>(x, tgt, cw, gx, B, K, padding, size_avg, dtype, ws, out, s);
   BIGDL_CHECK_LAUNCH();
 }
 

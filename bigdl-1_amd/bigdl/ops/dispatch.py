@@ -7,7 +7,7 @@ from . import reference as R
 from . import native as N
 
 __all__ = [
-    "cast_copy", "relu_forward", "relu_backward",
+    "cast_copy", "zero_fill", "relu_forward", "relu_backward",
     "conv2d_forward", "conv2d_backward", "conv_transpose2d_forward",
     "batchnorm_forward_train", "batchnorm_forward_infer", "batchnorm_backward",
     "maxpool2d_forward", "maxpool2d_backward", "avgpool2d_forward", "avgpool2d_backward",

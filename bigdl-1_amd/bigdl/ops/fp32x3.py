@@ -1060,8 +1060,10 @@ def linear_forward(x, w, b, act=0):
                    out=torch.zeros((n4, 3 * k8), dtype=_bf16, device=x.device) if n4 != n else None)
     bias = None
     if b is not None:
-        bias = torch.zeros(n4, dtype=_f32, device=x.device)
-        bias[:n] = b.detach().float().reshape(-1)
+        bias = b.detach().reshape(-1)
+        if n4 != n or bias.dtype != _f32 or not bias.is_contiguous() or bias.data_ptr() % 16:  # float4 epilogue reads
+            bias = torch.zeros(n4, dtype=_f32, device=x.device)
+            bias[:n] = b.detach().float().reshape(-1)
     y = _gemm_f32(a3, b3, m, n4, bias, act)
     if y is NotImplemented:
         return NotImplemented

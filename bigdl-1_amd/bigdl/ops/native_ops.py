@@ -60,6 +60,16 @@ def _ll(x):
 
 
 # ------------------------------------------------------------------------------------------------ casts
+@register("zero_fill")
+def zero_fill(t):
+    """t[:] = 0 for a contiguous 32-bit device tensor (the per-step gradient-arena clear) with the
+    native 16-B store kernel, so no torch fill kernel runs in the training step."""
+    if not (t.is_cuda and t.is_contiguous() and t.element_size() == 4 and _al16(t)) or not hasattr(_lib(), "bigdl_fill32"):
+        return NotImplemented
+    check(_lib().bigdl_fill32(ptr(t), _ll(t.numel()), C.c_uint32(0), _s()), "fill32")
+    return t
+
+
 @register("cast_copy")
 def cast_copy(dst, src):
     if not (dst.is_cuda and src.is_cuda and dst.numel() == src.numel()):
@@ -583,8 +593,12 @@ def cross_entropy_fused(x, target_1b, weights=None, size_average=True, padding_v
     if x.dim() != 2 or not x.is_contiguous() or x.dtype not in (_bf16, _f32):
         return NotImplemented
     B, K = x.shape
-    t = _targets_i32(target_1b.to(x.device), B)
-    if t is None:
+    # float labels already on the device are read by the kernel as they are (no per-step int cast)
+    tf = target_1b.reshape(-1) if target_1b.dtype == _f32 and target_1b.device == x.device else None
+    if tf is not None and (tf.numel() != B or not tf.is_contiguous() or not hasattr(_lib(), "bigdl_cross_entropy_ft")):
+        tf = None
+    t = None if tf is not None else _targets_i32(target_1b.to(x.device), B)
+    if tf is None and t is None:
         return NotImplemented
     w = None
     if weights is not None:
@@ -594,9 +608,10 @@ def cross_entropy_fused(x, target_1b, weights=None, size_average=True, padding_v
     ws = torch.empty(3 * B, dtype=_f32, device=x.device)
     out = torch.empty(2, dtype=_f32, device=x.device)
     gx = torch.empty_like(x)
-    check(_lib().bigdl_cross_entropy(ptr(x), ptr(t), ptr(w), ptr(gx), _ll(B), C.c_int(K), C.c_int(int(padding_value)),
-                                     C.c_int(1 if size_average else 0), C.c_int(1 if x.dtype == _bf16 else 0),
-                                     ptr(ws), ptr(out), _s()), "cross_entropy")
+    fn = _lib().bigdl_cross_entropy_ft if tf is not None else _lib().bigdl_cross_entropy
+    check(fn(ptr(x), ptr(tf if tf is not None else t), ptr(w), ptr(gx), _ll(B), C.c_int(K), C.c_int(int(padding_value)),
+             C.c_int(1 if size_average else 0), C.c_int(1 if x.dtype == _bf16 else 0),
+             ptr(ws), ptr(out), _s()), "cross_entropy")
     return out[0], gx
 
 
@@ -630,6 +645,19 @@ def _krsc(w4):
     """(O, I, kH, kW) view → contiguous (O, kH, kW, I) tensor (a view when already KRSC)."""
     k = w4.permute(0, 2, 3, 1)
     return k if k.is_contiguous() else k.contiguous()
+
+
+def _pad_taps(wk, K, taps, C_, cp, ldw):
+    """KRSC bf16 weights → [K][ldw] rows, each tap's channels zero-padded to ``cp`` and the row to
+    ``ldw`` (one native pass; the weights change every step, so nothing is cached)."""
+    wp = torch.empty((K, ldw), dtype=wk.dtype, device=wk.device)
+    if wk.is_cuda and wk.dtype == _bf16 and wk.is_contiguous() and hasattr(_lib(), "bigdl_pad_taps_bf16"):
+        check(_lib().bigdl_pad_taps_bf16(ptr(wk), ptr(wp), C.c_int(K), C.c_int(taps), C.c_int(C_), C.c_int(cp),
+                                         C.c_int(ldw), _s()), "pad_taps_bf16")
+        return wp
+    wp.zero_()
+    wp[:, :taps * cp].view(K, taps, cp)[..., :C_] = wk.reshape(K, taps, C_)
+    return wp
 
 
 def _pad_channels(x_nhwc_4d, c_to, slot=None, reuse=False):
@@ -920,14 +948,12 @@ def _conv_fwd_impl(x, w4, b, stride, pad, dilation=(1, 1), groups=1, res=None, s
         x = _pad_channels(x, 4, pad_slot)
         kg = R * S * 4
         ldw = (kg + 7) // 8 * 8
-        wp = torch.zeros((K, ldw), dtype=wk.dtype, device=wk.device)
-        wp[:, :kg].view(K, R, S, 4)[..., :C_] = wk
+        wp = _pad_taps(wk, K, R * S, C_, 4, ldw)
         wk, C_ = wp, 4
     elif C_ % 8:
         cp = (C_ + 7) // 8 * 8
         x = _pad_channels(x, cp, pad_slot)
-        wp = torch.zeros((K, R, S, cp), dtype=wk.dtype, device=wk.device)
-        wp[..., :C_] = wk
+        wp = _pad_taps(wk, K, R * S, C_, cp, R * S * cp).view(K, R, S, cp)
         wk, C_ = wp, cp
     P = (H + 2 * pad[0] - dilation[0] * (R - 1) - 1) // stride[0] + 1
     Q = (W + 2 * pad[1] - dilation[1] * (S - 1) - 1) // stride[1] + 1
@@ -1485,7 +1511,12 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
         cc = 4 if (C_ <= 4 and tuple(dilation) == (1, 1)) else (C_ + 7) // 8 * 8
         xx = _pad_channels(x, cc, pad_slot, reuse=True)
     direct = (cc == C_ and gw_acc.dtype == _f32 and gw_acc.permute(0, 2, 3, 1).is_contiguous())
-    target = gw_acc.permute(0, 2, 3, 1) if direct else torch.zeros((K, R, S, cc), dtype=_f32, device=x.device)
+    if direct:
+        target = gw_acc.permute(0, 2, 3, 1)
+    else:
+        target = torch.empty((K, R, S, cc), dtype=_f32, device=x.device)
+        if zero_fill(target) is NotImplemented:
+            target.zero_()
     P, Q = gy.shape[2], gy.shape[3]
     if isinstance(gy, R_.BNGrad):  # dY = the BN input gradient, applied while loading dY
         check(_lib().bigdl_conv_wgrad_bnbwd(ptr(xx), ptr(gy.g), ptr(gy.x), ptr(gy.coef), ptr(target),

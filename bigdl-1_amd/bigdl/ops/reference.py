@@ -18,6 +18,10 @@ aten = torch.ops.aten
 
 
 # ------------------------------------------------------------------------- casts / elementwise
+def zero_fill(t: torch.Tensor):
+    return t.zero_()
+
+
 def cast_copy(dst: torch.Tensor, src: torch.Tensor):
     dst.copy_(src.reshape(dst.shape) if src.shape != dst.shape else src)
     return dst

@@ -109,18 +109,34 @@ def test_bn_infer():
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("n", [1, 7, 4096, 25557032])
+def test_zero_fill(n):
+    """The gradient-arena clear: native 16-B store kernel, tail and all (no torch fill kernel)."""
+    N = _native()
+    from bigdl import ops
+    t = torch.randn(n + 1, device=dev)[:n] if n % 4 == 0 else torch.randn(n, device=dev)
+    assert N.zero_fill(t) is not NotImplemented
+    assert int(torch.count_nonzero(t)) == 0
+    g = torch.randn(n + 3, device=dev)
+    ops.zero_fill(g)
+    assert int(torch.count_nonzero(g)) == 0
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("weights", [False, True])
-def test_cross_entropy(dtype, weights):
+@pytest.mark.parametrize("tdtype", [torch.float32, torch.int64])
+def test_cross_entropy(dtype, weights, tdtype):
+    """float labels on the device go to the float-target kernel (no per-step int cast), others to
+    the int32 one; both against the fp32 reference."""
     N = _native()
     from bigdl.ops import reference as R
     B, K = 37, 1000
     x = (torch.randn(B, K, device=dev) * 4).to(dtype)
-    t = torch.randint(1, K + 1, (B,), device=dev).float()
+    t = torch.randint(1, K + 1, (B,), device=dev).to(tdtype)
     t[3] = -1  # padding value -> skipped
     w = torch.rand(K, device=dev) if weights else None
     loss, g = N.cross_entropy_fused(x, t, w, True, -1)
-    lr, gr = R.cross_entropy_fused(x.float(), t, w, True, -1)
+    lr, gr = R.cross_entropy_fused(x.float(), t.float(), w, True, -1)
     torch.testing.assert_close(loss, lr, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(g.float(), gr.float(), rtol=2e-2, atol=2e-4 if dtype == torch.float32 else 2e-3)
 
@@ -637,3 +653,16 @@ def test_transposed_conv_native(Cin, Cout, R, st, pd, adj):
     torch.testing.assert_close(w.grad, wr.grad, rtol=3e-2, atol=3e-2 * float(wr.grad.abs().max()))
     # the output is bf16, so the incoming gradient is bf16-rounded before the bias sum
     torch.testing.assert_close(b.grad, gy.bfloat16().float().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("K,taps,C,cp,ldw", [(64, 49, 3, 4, 200), (16, 9, 5, 8, 72), (32, 1, 3, 8, 8)])
+def test_pad_taps(K, taps, C, cp, ldw):
+    """Narrow-channel conv weights padded per tap and per row in one native pass (the stem's C4
+    operand) == the zero-fill + strided-copy construction."""
+    _native()
+    from bigdl.ops import native_ops as NO
+    wk = torch.randn(K, taps, C, device=dev).bfloat16()
+    got = NO._pad_taps(wk, K, taps, C, cp, ldw)
+    ref = torch.zeros(K, ldw, dtype=torch.bfloat16, device=dev)
+    ref[:, :taps * cp].view(K, taps, cp)[..., :C] = wk
+    assert torch.equal(got, ref)
