@@ -1531,7 +1531,13 @@ def _wgrad_launch(x, gy, w4, gw_acc, scale, stride, pad, dilation, pad_slot):
             stride[1], pad[0], pad[1], dilation[0], dilation[1], -(t[0] or _wgrad_blocks(N_ * P * Q, cc, K)), t[1],
             _s()), "conv_wgrad"))
     if not direct:
-        gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
+        if cc == 4 and C_ <= 4 and gw_acc.dtype == _f32 and gw_acc.dim() == 4:
+            # the RGB stem's C4 gradient folded onto the KCRS master gradient natively (weight_x3.hip)
+            check(_lib().bigdl_c4_wgrad_fold(ptr(target), ptr(gw_acc), K, C_, R, S,
+                                             *(C.c_longlong(v) for v in gw_acc.stride()), _f(scale), _s()),
+                  "c4_wgrad_fold")
+        else:
+            gw_acc.add_(target[..., :C_].permute(0, 3, 1, 2), alpha=scale)
     return xx
 
 
