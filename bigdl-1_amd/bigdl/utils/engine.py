@@ -77,7 +77,9 @@ class Engine:
             if want_dist:
                 import torch.distributed as tdist
                 if not tdist.is_initialized():
-                    be = backend or ("nccl" if _S.device.type == "cuda" else "gloo")
+                    # BIGDL_DIST_BACKEND=gloo rehearses the multi-rank device path with several ranks
+                    # on one card (RCCL refuses two ranks on the same GPU)
+                    be = backend or os.environ.get("BIGDL_DIST_BACKEND") or ("nccl" if _S.device.type == "cuda" else "gloo")
                     import datetime
                     # collective watchdog: a hung collective becomes an error after
                     # this many seconds, which the optimizer's retry loop / the launcher can handle
